@@ -1,0 +1,632 @@
+// Canary-scoring kernels (K4 pairwise rank tests, K1+K7 fused history-stats +
+// anomaly decision, service reduce, anomaly compaction, K11 synthetic fleet).
+//
+// Reference behaviour being rebuilt (foremast-brain is external; see
+// docs/BRAIN_SPEC.md): per (service, metric) the brain fits a historical model
+// (ML_ALGORITHM=moving_average_all, deploy/foremast/3_brain/foremast-brain.yaml:24-25),
+// compares canary vs baseline with pairwise tests (foremast-brain/README.md:32-38,
+// docs/guides/design.md:35) and flags current points outside the bounds
+// (design.md:43, fail fast).
+//
+// Layout: rows = services x metrics, row r -> metric r % M.  history [R, ld_h]
+// fp32 (NaN = missing sample), current [R, ld_c], baseline [R, ld_b].
+#include "fm_common.h"
+
+using namespace fm;
+
+// ---------------------------------------------------------------------------
+// K4: pairwise tests. One wave per (service, metric) row, 4 rows per 256-thread
+// workgroup.  The pooled sample (n1 + n2 <= 64*K) is sorted in registers with a
+// bitonic network (in-register swaps for strides >= 64, __shfl_xor below),
+// average ranks with ties come from a max-scan / suffix-min-scan over tie runs.
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr float kPad = INFINITY;
+
+template <int K>
+__device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int size = 2; size <= 64 * K; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= 64) {
+        const int ks = stride / 64;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int p = k ^ ks;
+          if (p > k) {
+            const int i = k * 64 + lane;
+            const bool asc = (i & size) == 0;
+            const bool sw = asc ? (v[k] > v[p]) : (v[k] < v[p]);
+            if (sw) {
+              float tv = v[k]; v[k] = v[p]; v[p] = tv;
+              int tt = tag[k]; tag[k] = tag[p]; tag[p] = tt;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int i = k * 64 + lane;
+          const float ov = __shfl_xor(v[k], stride);
+          const int ot = __shfl_xor(tag[k], stride);
+          const bool asc = (i & size) == 0;
+          const bool lower = (lane & stride) == 0;
+          const bool take = lower ? (asc ? ov < v[k] : ov > v[k]) : (asc ? ov > v[k] : ov < v[k]);
+          if (take) { v[k] = ov; tag[k] = ot; }
+        }
+      }
+    }
+  }
+}
+
+// Average (1-based) ranks for a sorted register array whose first n entries are
+// real.  tie_term accumulates sum(t^3 - t) over tie runs; is_end marks the last
+// element of each run (where empirical CDFs are evaluated).
+template <int K>
+__device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&rank)[K], bool (&is_end)[K],
+                                          double& tie_term) {
+  const int lane = lane_id();
+  int start_idx[K];
+  int carry = 0;
+  float last_prev = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = k * 64 + lane;
+    float prev = __shfl_up(v[k], 1);
+    if (lane == 0) prev = last_prev;
+    const bool st = (i == 0) || (v[k] != prev);
+    int s = st ? i : 0;
+    s = wave_incl_max(s);
+    s = s > carry ? s : carry;
+    start_idx[k] = s;
+    carry = __shfl(s, 63);
+    last_prev = __shfl(v[k], 63);
+  }
+  int carry_e = 0x7fffffff;
+  float next_first = 0.f;
+  double tl = 0.0;
+#pragma unroll
+  for (int k = K - 1; k >= 0; --k) {
+    const int i = k * 64 + lane;
+    float next = __shfl_down(v[k], 1);
+    if (lane == 63) next = next_first;
+    const bool en = (i < n) && ((i == n - 1) || (v[k] != next));
+    int e = en ? i : 0x7fffffff;
+    e = wave_incl_suffix_min(e);
+    e = e < carry_e ? e : carry_e;
+    carry_e = __shfl(e, 0);
+    next_first = __shfl(v[k], 0);
+    is_end[k] = en;
+    rank[k] = 0.5f * (float)(start_idx[k] + e) + 1.0f;
+    if (i < n && i == start_idx[k]) {
+      const double t = (double)(e - start_idx[k] + 1);
+      tl += t * t * t - t;
+    }
+  }
+  tie_term = wave_sum(tl);
+}
+
+}  // namespace
+
+enum { T_MW = 0, T_WIL = 1, T_KRU = 2, T_KS = 3, T_T = 4, N_TESTS = 5 };
+constexpr int kSuff = 12;
+
+template <int K>
+__global__ __launch_bounds__(256) void pairwise_kernel(
+    const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
+    int n_base, int64_t R, double* __restrict__ suff) {
+  const int lane = lane_id();
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
+  if (row >= R) return;  // wave-uniform exit
+  const float* c = cur + row * ld_c;
+  const float* b = base + row * ld_b;
+
+  float v[K];
+  int tag[K];
+  double s1 = 0, s2 = 0;
+  int c1 = 0, c2 = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = k * 64 + lane;
+    float x = kPad;
+    int t = -1;
+    if (i < n_cur) { x = c[i]; t = 0; }
+    else if (i < n_cur + n_base) { x = b[i - n_cur]; t = 1; }
+    if (!isfinite(x)) { x = kPad; t = -1; }
+    v[k] = x; tag[k] = t;
+    if (t == 0) { s1 += x; ++c1; }
+    if (t == 1) { s2 += x; ++c2; }
+  }
+  const int n1 = wave_sum(c1), n2 = wave_sum(c2);
+  const int n = n1 + n2;
+  const double m1 = wave_sum(s1) / (n1 > 0 ? n1 : 1), m2 = wave_sum(s2) / (n2 > 0 ? n2 : 1);
+  double q1 = 0, q2 = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (tag[k] == 0) { double d = v[k] - m1; q1 += d * d; }
+    if (tag[k] == 1) { double d = v[k] - m2; q2 += d * d; }
+  }
+  q1 = wave_sum(q1); q2 = wave_sum(q2);
+
+  // ---- Wilcoxon signed-rank on position-paired differences (zero_method='wilcox')
+  constexpr int KW = (K + 1) / 2;
+  float dv[KW];
+  int dt[KW];
+  const int npair = n_cur < n_base ? n_cur : n_base;
+  int cw = 0;
+#pragma unroll
+  for (int k = 0; k < KW; ++k) {
+    const int j = k * 64 + lane;
+    float d = kPad;
+    int t = -1;
+    if (j < npair) {
+      const float xc = c[j], xb = b[j];
+      if (isfinite(xc) && isfinite(xb)) {
+        const float dd = xc - xb;
+        if (dd != 0.f) { d = fabsf(dd); t = dd > 0.f ? 1 : 0; ++cw; }
+      }
+    }
+    dv[k] = d; dt[k] = t;
+  }
+  const int nw = wave_sum(cw);
+
+  bitonic_sort<K>(v, tag);
+  float rk[K];
+  bool en[K];
+  double tie = 0.0;
+  avg_ranks<K>(v, n, rk, en, tie);
+
+  double r1 = 0.0;
+  double dmax = 0.0;
+  int base1 = 0, base2 = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (tag[k] == 0) r1 += rk[k];
+    // KS: inclusive prefix counts of each sample along the sorted order
+    const int a1 = wave_incl_sum(tag[k] == 0 ? 1 : 0) + base1;
+    const int a2 = wave_incl_sum(tag[k] == 1 ? 1 : 0) + base2;
+    base1 = __shfl(a1, 63);
+    base2 = __shfl(a2, 63);
+    if (en[k] && n1 > 0 && n2 > 0) {
+      const double dd = fabs((double)a1 / n1 - (double)a2 / n2);
+      dmax = dd > dmax ? dd : dmax;
+    }
+  }
+  r1 = wave_sum(r1);
+  dmax = wave_max(dmax);
+
+  bitonic_sort<KW>(dv, dt);
+  float rw[KW];
+  bool ew[KW];
+  double tiew = 0.0;
+  avg_ranks<KW>(dv, nw, rw, ew, tiew);
+  double rplus = 0.0;
+#pragma unroll
+  for (int k = 0; k < KW; ++k)
+    if (dt[k] == 1) rplus += rw[k];
+  rplus = wave_sum(rplus);
+
+  // Per-row sufficient statistics; p-values are evaluated one row per THREAD
+  // by pvalue_kernel (the double-precision special functions would otherwise
+  // run on lane 0 with 63 lanes idle).
+  if (lane == 0) {
+    double* o = suff + row * kSuff;
+    o[0] = n1; o[1] = n2; o[2] = nw; o[3] = r1; o[4] = tie; o[5] = dmax;
+    o[6] = rplus; o[7] = tiew; o[8] = m1; o[9] = m2; o[10] = q1; o[11] = q2;
+  }
+}
+
+__global__ __launch_bounds__(256) void pvalue_kernel(const double* __restrict__ suff, int64_t R, int test_mask,
+                                                     int combine_any, float p_thr, int min_mw, int min_wil,
+                                                     int min_kru, float* __restrict__ pvals,
+                                                     float* __restrict__ stats, int8_t* __restrict__ diff) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= R) return;
+  const double* o = suff + row * kSuff;
+  const int n1 = (int)o[0], n2 = (int)o[1], nw = (int)o[2];
+  const double r1 = o[3], tie = o[4], dmax = o[5], rplus = o[6], tiew = o[7];
+  const double m1 = o[8], m2 = o[9], q1 = o[10], q2 = o[11];
+  const int n = n1 + n2;
+  const double NaN = __builtin_nan("");
+  double p[N_TESTS], st[N_TESTS];
+  for (int t = 0; t < N_TESTS; ++t) { p[t] = NaN; st[t] = NaN; }
+  const double dn1 = n1, dn2 = n2, dn = n;
+  // Mann-Whitney U (two-sided, continuity-corrected normal approximation)
+  if (n1 >= min_mw && n2 >= min_mw && n1 > 0 && n2 > 0) {
+    const double u1 = r1 - dn1 * (dn1 + 1.0) / 2.0;
+    const double u2 = dn1 * dn2 - u1;
+    const double u = u1 > u2 ? u1 : u2;
+    const double mu = dn1 * dn2 / 2.0;
+    const double var = dn1 * dn2 / 12.0 * ((dn + 1.0) - tie / (dn * (dn - 1.0)));
+    st[T_MW] = u1;
+    if (var > 0) {
+      const double z = (u - mu - 0.5) / sqrt(var);
+      double pp = 2.0 * norm_sf(z);
+      p[T_MW] = pp > 1.0 ? 1.0 : pp;
+    } else {
+      p[T_MW] = 1.0;
+    }
+  }
+  // Kruskal-Wallis H with two groups (tie-corrected), chi2 with 1 dof
+  if (n1 >= min_kru && n2 >= min_kru && n1 > 0 && n2 > 0) {
+    const double r2 = dn * (dn + 1.0) / 2.0 - r1;
+    double h = 12.0 / (dn * (dn + 1.0)) * (r1 * r1 / dn1 + r2 * r2 / dn2) - 3.0 * (dn + 1.0);
+    const double corr = 1.0 - tie / (dn * dn * dn - dn);
+    if (corr > 0) {
+      st[T_KRU] = h / corr;
+      // chi2(1) survival = erfc(sqrt(x/2))
+      p[T_KRU] = h / corr > 0 ? erfc(sqrt(0.5 * h / corr)) : 1.0;
+    }
+  }
+  // Two-sample Kolmogorov-Smirnov (asymptotic Kolmogorov distribution)
+  if (n1 >= min_mw && n2 >= min_mw && n1 > 0 && n2 > 0) {
+    const double en_ = dn1 * dn2 / (dn1 + dn2);
+    st[T_KS] = dmax;
+    p[T_KS] = kolmogorov_sf(sqrt(en_) * dmax);
+  }
+  // Welch t-test
+  if (n1 >= 2 && n2 >= 2 && n1 >= min_kru && n2 >= min_kru) {
+    const double v1 = q1 / (dn1 - 1.0), v2 = q2 / (dn2 - 1.0);
+    const double se2 = v1 / dn1 + v2 / dn2;
+    if (se2 > 0) {
+      const double t = (m1 - m2) / sqrt(se2);
+      const double a = v1 / dn1, bb = v2 / dn2;
+      const double df = se2 * se2 / (a * a / (dn1 - 1.0) + bb * bb / (dn2 - 1.0));
+      st[T_T] = t;
+      p[T_T] = student_t_2sided(t, df);
+    }
+  }
+  // Wilcoxon signed-rank (normal approximation, no continuity correction)
+  if (nw >= min_wil && nw > 0) {
+    const double dnw = nw;
+    const double tot = dnw * (dnw + 1.0) / 2.0;
+    const double rminus = tot - rplus;
+    const double T = rplus < rminus ? rplus : rminus;
+    const double mn = dnw * (dnw + 1.0) / 4.0;
+    const double se = sqrt(dnw * (dnw + 1.0) * (2.0 * dnw + 1.0) / 24.0 - tiew / 48.0);
+    st[T_WIL] = T;
+    if (se > 0) {
+      double pp = 2.0 * norm_sf(fabs((T - mn) / se));
+      p[T_WIL] = pp > 1.0 ? 1.0 : pp;
+    }
+  }
+  int applicable = 0, significant = 0;
+  for (int t = 0; t < N_TESTS; ++t) {
+    pvals[row * N_TESTS + t] = (float)p[t];
+    stats[row * N_TESTS + t] = (float)st[t];
+    if ((test_mask >> t) & 1) {
+      if (!isnan(p[t])) {
+        ++applicable;
+        if (p[t] < p_thr) ++significant;
+      }
+    }
+  }
+  int8_t d = 0;
+  if (applicable > 0) d = combine_any ? (significant > 0) : (significant == applicable);
+  diff[row] = d;
+}
+
+FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const float* base, int64_t ld_b, int n_base,
+                             int64_t R, int test_mask, int combine_any, float p_thr, int min_mw, int min_wil,
+                             int min_kru, float* pvals, float* stats, int8_t* diff, double* suff,
+                             hipStream_t stream) {
+  if (R <= 0) return 0;
+  const int n = n_cur + n_base;
+  const dim3 grid((unsigned)((R + 3) / 4)), block(256);
+#define FM_PW(KK) hipLaunchKernelGGL(pairwise_kernel<KK>, grid, block, 0, stream, cur, ld_c, n_cur, base, ld_b, \
+                                     n_base, R, suff)
+  if (n <= 64) FM_PW(1);
+  else if (n <= 128) FM_PW(2);
+  else if (n <= 256) FM_PW(4);
+  else if (n <= 512) FM_PW(8);
+  else return (int)hipErrorInvalidValue;
+#undef FM_PW
+  FM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, suff, R, test_mask,
+                     combine_any, p_thr, min_mw, min_wil, min_kru, pvals, stats, diff);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// K1 + K7 fused: moving_average_all bounds over the whole history row and the
+// anomaly decision on the current window, one 256-thread workgroup per row.
+// The row is read once from HBM with 16-B loads and kept in registers
+// (NV float4 per thread) so the two-pass mean / variance costs no re-read.
+// ---------------------------------------------------------------------------
+template <int NV>
+__global__ __launch_bounds__(256) void stats_decide_kernel(
+    const float* __restrict__ hist, int64_t ld_h, int T, const float* __restrict__ cur, int64_t ld_c, int n_cur,
+    int64_t R, int M, const float* __restrict__ thr, const int* __restrict__ bound, const float* __restrict__ minlb,
+    float pair_factor, const int8_t* __restrict__ diff, int min_hist, float* __restrict__ out_stats,
+    unsigned long long* __restrict__ out_flags, int NW, int* __restrict__ out_count, float* __restrict__ out_score,
+    int* __restrict__ out_valid) {
+  __shared__ double red[4];
+  __shared__ int redi[4];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* h = hist + row * ld_h;
+  const int nq = (T + 3) >> 2;
+  float4 q[NV];
+  double s = 0.0;
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int qi = tid + j * 256;
+    float4 x = make_float4(NAN, NAN, NAN, NAN);
+    if (qi < nq) {
+      x = reinterpret_cast<const float4*>(h)[qi];
+      const int e0 = qi * 4;
+      if (e0 + 1 >= T) x.y = NAN;
+      if (e0 + 2 >= T) x.z = NAN;
+      if (e0 + 3 >= T) x.w = NAN;
+    }
+    q[j] = x;
+    float ls = 0.f;
+    if (isfinite(x.x)) { ls += x.x; ++cnt; }
+    if (isfinite(x.y)) { ls += x.y; ++cnt; }
+    if (isfinite(x.z)) { ls += x.z; ++cnt; }
+    if (isfinite(x.w)) { ls += x.w; ++cnt; }
+    s += ls;
+  }
+  const double tot = block_sum<256>(s, red);
+  const int n = block_sum<256>(cnt, redi);
+  const double mean = n > 0 ? tot / n : 0.0;
+  const float mf = (float)mean;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float4 x = q[j];
+    if (isfinite(x.x)) { float d = x.x - mf; ss += d * d; }
+    if (isfinite(x.y)) { float d = x.y - mf; ss += d * d; }
+    if (isfinite(x.z)) { float d = x.z - mf; ss += d * d; }
+    if (isfinite(x.w)) { float d = x.w - mf; ss += d * d; }
+  }
+  const double sst = block_sum<256>((double)ss, red);
+  const double var = n > 0 ? sst / n : 0.0;
+  const float sd = (float)sqrt(var);
+  const int m = (int)(row % M);
+  float th = thr[m];
+  if (diff != nullptr && diff[row]) th *= pair_factor;
+  const int bd = bound[m];
+  const float up = mf + th * sd;
+  float lo = mf - th * sd;
+  const float mlb = minlb[m];
+  if (lo < mlb) lo = mlb;
+  const bool has_hist = n >= min_hist && n > 0;
+
+  const float* cr = cur + row * ld_c;
+  int acnt = 0, ccnt = 0;
+  float best = 0.f;
+  const float inv = sd > 0.f ? 1.0f / sd : 0.f;
+  for (int i0 = 0; i0 < n_cur; i0 += 256) {
+    const int i = i0 + tid;
+    bool f = false;
+    if (i < n_cur) {
+      const float x = cr[i];
+      if (isfinite(x)) {
+        ++ccnt;
+        if (has_hist) {
+          const bool hi = (bd & 1) && x > up;
+          const bool lw = (bd & 2) && x < lo;
+          f = hi || lw;
+          if (f) {
+            ++acnt;
+            const float e = hi ? (x - up) : (lo - x);
+            const float z = sd > 0.f ? e * inv : 1e30f;
+            best = z > best ? z : best;
+          }
+        }
+      }
+    }
+    const unsigned long long bal = __ballot(f);
+    const int w = i0 / 64 + wave_id();
+    if (lane_id() == 0 && w < NW) out_flags[row * NW + w] = bal;
+  }
+  acnt = block_sum<256>(acnt, redi);
+  ccnt = block_sum<256>(ccnt, redi);
+  best = block_max<256>(best, (float*)red);
+  if (tid == 0) {
+    out_stats[row * 4 + 0] = mf;
+    out_stats[row * 4 + 1] = sd;
+    out_stats[row * 4 + 2] = up;
+    out_stats[row * 4 + 3] = lo;
+    out_count[row] = acnt;
+    out_score[row] = best;
+    out_valid[row] = (has_hist ? 1 : 0) | (ccnt > 0 ? 2 : 0);
+  }
+}
+
+FM_API int fm_stats_decide(const float* hist, int64_t ld_h, int T, const float* cur, int64_t ld_c, int n_cur, int64_t R,
+                           int M, const float* thr, const int* bound, const float* minlb, float pair_factor,
+                           const int8_t* diff, int min_hist, float* out_stats, unsigned long long* out_flags, int NW,
+                           int* out_count, float* out_score, int* out_valid, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
+  if (NW * 64 < n_cur) return (int)hipErrorInvalidValue;
+  const int nq = (T + 3) / 4;
+  const dim3 grid((unsigned)R), block(256);
+#define FM_SD(NVV)                                                                                                    \
+  hipLaunchKernelGGL(stats_decide_kernel<NVV>, grid, block, 0, stream, hist, ld_h, T, cur, ld_c, n_cur, R, M, thr,     \
+                     bound, minlb, pair_factor, diff, min_hist, out_stats, out_flags, NW, out_count, out_score,        \
+                     out_valid)
+  if (nq <= 256 * 2) FM_SD(2);
+  else if (nq <= 256 * 4) FM_SD(4);
+  else if (nq <= 256 * 8) FM_SD(8);
+  else if (nq <= 256 * 10) FM_SD(10);
+  else if (nq <= 256 * 12) FM_SD(12);
+  else if (nq <= 256 * 16) FM_SD(16);
+  else return (int)hipErrorInvalidValue;
+#undef FM_SD
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Service reduce: per service, fold its M metric rows into the packed result
+// row [status, score, anomalous-metric mask, anomalous point count] that is
+// all-gathered across ranks.  status: 0 = no anomaly, 1 = anomaly, 2 = unknown
+// (missing current data or not enough history).
+// ---------------------------------------------------------------------------
+__global__ void service_reduce_kernel(const int* __restrict__ count, const float* __restrict__ score,
+                                      const int* __restrict__ valid, int64_t S, int M, float* __restrict__ packed) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  int tot = 0, mask = 0;
+  bool unknown = false;
+  float best = 0.f;
+  for (int m = 0; m < M; ++m) {
+    const int64_t r = s * M + m;
+    const int c = count[r];
+    tot += c;
+    if (c > 0) mask |= 1 << m;
+    if ((valid[r] & 3) != 3) unknown = true;
+    best = score[r] > best ? score[r] : best;
+  }
+  const int status = tot > 0 ? 1 : (unknown ? 2 : 0);
+  packed[s * 4 + 0] = (float)status;
+  packed[s * 4 + 1] = best;
+  packed[s * 4 + 2] = (float)mask;
+  packed[s * 4 + 3] = (float)tot;
+}
+
+FM_API int fm_service_reduce(const int* count, const float* score, const int* valid, int64_t S, int M, float* packed,
+                             hipStream_t stream) {
+  if (S <= 0) return 0;
+  if (M > 24) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(service_reduce_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, count, score,
+                     valid, S, M, packed);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Stream compaction of anomalous points: one wave per row, entries
+// (row, index, value) appended through one atomic per row with anomalies.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void compact_kernel(const unsigned long long* __restrict__ flags, int NW,
+                                                      const float* __restrict__ cur, int64_t ld_c, int n_cur,
+                                                      const int* __restrict__ count, int64_t R, int cap,
+                                                      int* __restrict__ counter, int* __restrict__ out_idx,
+                                                      float* __restrict__ out_val) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
+  if (row >= R) return;
+  const int c = count[row];
+  if (c == 0) return;
+  const int lane = lane_id();
+  int base = 0;
+  if (lane == 0) base = atomicAdd(counter, c);
+  base = __shfl(base, 0);
+  int written = 0;
+  for (int w = 0; w < NW; ++w) {
+    const unsigned long long word = flags[row * NW + w];
+    if (!word) continue;
+    const bool mine = (word >> lane) & 1ull;
+    const unsigned long long below = lane == 0 ? 0ull : (word & ((1ull << lane) - 1ull));
+    const int pos = written + __popcll(below);
+    if (mine) {
+      const int slot = base + pos;
+      const int i = w * 64 + lane;
+      if (slot < cap) {
+        out_idx[2 * slot + 0] = (int)row;
+        out_idx[2 * slot + 1] = i;
+        out_val[slot] = cur[row * ld_c + i];
+      }
+    }
+    written += __popcll(word);
+  }
+}
+
+FM_API int fm_compact_anomalies(const unsigned long long* flags, int NW, const float* cur, int64_t ld_c, int n_cur,
+                                const int* count, int64_t R, int cap, int* counter, int* out_idx, float* out_val,
+                                hipStream_t stream) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(compact_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, stream, flags, NW, cur, ld_c, n_cur,
+                     count, R, cap, counter, out_idx, out_val);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// K11: synthetic Prometheus-shaped fleet.  Deterministic in the GLOBAL service
+// id so every world size sees the same fleet (docs/BRAIN_SPEC.md, "synthetic
+// fleet"); mirrors the daily/weekly seasonality + noise + injected faults of
+// examples/spring-boot-demo/src/main/resources/load.txt.
+// ---------------------------------------------------------------------------
+struct SynthParams {
+  float level, amp_d, amp_w, phase, noise;
+};
+
+__host__ __device__ __forceinline__ SynthParams synth_params(uint32_t gs, uint32_t m, uint32_t seed) {
+  const uint32_t key = gs * 64u + m;
+  SynthParams p;
+  p.level = 1.0f + 99.0f * u01(hash3(key, 0u, seed));
+  p.amp_d = 0.1f + 0.3f * u01(hash3(key, 1u, seed));
+  p.amp_w = 0.01f + 0.04f * u01(hash3(key, 2u, seed));
+  p.phase = 6.2831853f * u01(hash3(key, 3u, seed));
+  p.noise = 0.005f + 0.015f * u01(hash3(key, 4u, seed));
+  return p;
+}
+
+__device__ __forceinline__ float synth_value(const SynthParams& p, uint32_t key, int64_t t, uint32_t stream_id,
+                                             uint32_t seed) {
+  const float tf = (float)t;
+  const float season = 1.0f + p.amp_d * sinf(6.2831853f * tf / 1440.0f + p.phase) +
+                       p.amp_w * sinf(6.2831853f * tf / 10080.0f + p.phase);
+  const uint32_t h1 = hash3(key, (uint32_t)t * 2654435761u + stream_id, seed ^ 0xA5A5A5A5u);
+  const uint32_t h2 = hash_u32(h1 ^ 0x68E31DA4u);
+  const float g = sqrtf(-2.0f * logf(u01(h1))) * cosf(6.2831853f * u01(h2));
+  float v = p.level * season * (1.0f + p.noise * g);
+  return v > 0.f ? v : 0.f;
+}
+
+// kind: 0 = history [R, ld] for t in [0, T); 1 = baseline (P pods x W points,
+// t in [T-W, T)); 2 = current (P pods x W points, t in [T, T+W)) with faults
+// injected into services whose hash falls under fault_rate.
+__global__ void synth_kernel(float* __restrict__ out, int64_t ld, int64_t n_per_row, int64_t S, int M,
+                             int64_t svc0, int T, int P, int W, int kind, float fault_rate, float fault_mag,
+                             uint32_t seed) {
+  const int64_t total = S * M * n_per_row;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = e / n_per_row;
+    const int64_t j = e - row * n_per_row;
+    const uint32_t gs = (uint32_t)(svc0 + row / M);
+    const uint32_t m = (uint32_t)(row % M);
+    const SynthParams p = synth_params(gs, m, seed);
+    const uint32_t key = gs * 64u + m;
+    float v;
+    if (kind == 0) {
+      v = synth_value(p, key, j, 0u, seed);
+    } else {
+      const int64_t pod = j / W, w = j - pod * W;
+      const int64_t t = (kind == 1) ? (T - W + w) : (T + w);
+      v = synth_value(p, key, t, 1000u + (uint32_t)pod + (kind == 2 ? 500u : 0u), seed);
+      if (kind == 2) {
+        const bool faulty = u01(hash3(gs, 7u, seed)) < fault_rate;
+        if (faulty && (m % 4u) == 0u) v = v + p.level * fault_mag * (1.0f + p.amp_d + p.amp_w);
+      }
+    }
+    out[row * ld + j] = v;
+  }
+  // padding columns of the history are NaN (missing samples)
+  if (kind == 0 && ld > n_per_row) {
+    const int64_t pad = ld - n_per_row;
+    const int64_t tp = S * M * pad;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tp; e += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t row = e / pad;
+      out[row * ld + n_per_row + (e - row * pad)] = NAN;
+    }
+  }
+}
+
+FM_API int fm_synth_fleet(float* out, int64_t ld, int64_t n_per_row, int64_t S, int M, int64_t svc0, int T, int P,
+                          int W, int kind, float fault_rate, float fault_mag, uint32_t seed, hipStream_t stream) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(synth_kernel, dim3(2048), dim3(256), 0, stream, out, ld, n_per_row, S, M, svc0, T, P, W, kind,
+                     fault_rate, fault_mag, seed);
+  FM_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,156 @@
+"""Typed configuration loaded from the SAME environment variable names the
+reference components use, so existing manifests keep working.
+
+* brain:     deploy/foremast/3_brain/foremast-brain.yaml:21-81, foremast-brain/README.md:16-38
+* service:   foremast-service/cmd/manager/main.go:301-309 (ELASTIC_URL, QUERY_SERVICE_ENDPOINT)
+* barrelman: foremast-barrelman/cmd/manager/main.go:69-76 (MODE, HPA_STRATEGY), Barrelman.go:402 (NAMESPACE)
+* trigger:   foremast-trigger/README.md:14-22
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Mapping
+
+# Metric-type overrides shipped in foremast-brain.yaml:32-73 (threshold, bound, min_lower_bound).
+DEFAULT_METRIC_TYPES: dict[str, tuple[float, int, float]] = {
+    "error5xx": (2.0, 1, 0.0),
+    "error4xx": (3.0, 1, 0.0),
+    "latency": (10.0, 3, 0.0),
+    "cpu": (5.0, 1, 0.0),
+    "memory": (5.0, 1, 0.0),
+}
+
+# bound codes ([inferred], docs/BRAIN_SPEC.md §3): 1 upper only, 2 lower only, 3 both
+BOUND_UPPER, BOUND_LOWER, BOUND_BOTH = 1, 2, 3
+
+
+def _f(env: Mapping[str, str], k: str, d: float) -> float:
+    v = env.get(k)
+    try:
+        return float(v) if v not in (None, "") else d
+    except ValueError:
+        return d
+
+
+def _i(env: Mapping[str, str], k: str, d: int) -> int:
+    v = env.get(k)
+    try:
+        return int(float(v)) if v not in (None, "") else d
+    except ValueError:
+        return d
+
+
+@dataclass
+class MetricRule:
+    threshold: float
+    bound: int
+    min_lower_bound: float
+
+
+@dataclass
+class BrainConfig:
+    ml_algorithm: str = "moving_average_all"
+    threshold: float = 2.0
+    bound: int = BOUND_UPPER
+    min_lower_bound: float = 0.0
+    metric_rules: dict[str, MetricRule] = field(
+        default_factory=lambda: {k: MetricRule(*v) for k, v in DEFAULT_METRIC_TYPES.items()})
+    min_historical_points: int = 10          # MIN_HISTORICAL_DATA_POINT_TO_MEASURE
+    pairwise_algorithm: str = "ALL"          # ML_PAIRWISE_ALGORITHM
+    pairwise_threshold: float = 0.05         # ML_PAIRWISE_THRESHOLD
+    min_mann_white: int = 20                 # MIN_MANN_WHITE_DATA_POINTS
+    min_wilcoxon: int = 20                   # MIN_WILCOXON_DATA_POINTS
+    min_kruskal: int = 5                     # MIN_KRUSKAL_DATA_POINTS
+    pairwise_threshold_factor: float = 0.8   # [inferred] "lower threshold" factor (design.md:35)
+    max_stuck_seconds: float = 90.0          # MAX_STUCK_IN_SECONDS
+    max_cache_size: int = 10000              # MAX_CACHE_SIZE
+    es_endpoint: str = "http://elasticsearch-discovery.foremast.svc.cluster.local:9200"  # ES_ENDPOINT
+    metrics_port: int = 8000
+    poll_interval: float = 5.0
+    hpa_breath_up: float = 60.0              # docs/dynamic_autoscaling.md:117-125
+    hpa_breath_down: float = 300.0
+    hpa_max_flips: int = 4                   # docs/dynamic_autoscaling.md:127-130 (flip feedback)
+    hpa_flip_window: float = 1800.0
+
+    def rule_for(self, alias: str) -> MetricRule:
+        """Per-metric override: exact alias match first, then substring match
+        (aliases like 'error5xx_rate' pick up the error5xx rule)."""
+        if alias in self.metric_rules:
+            return self.metric_rules[alias]
+        for k, r in self.metric_rules.items():
+            if k and k in alias:
+                return r
+        return MetricRule(self.threshold, self.bound, self.min_lower_bound)
+
+    @classmethod
+    def from_env(cls, env: Mapping[str, str] | None = None) -> "BrainConfig":
+        env = os.environ if env is None else env
+        c = cls()
+        c.ml_algorithm = env.get("ML_ALGORITHM", c.ml_algorithm) or c.ml_algorithm
+        c.threshold = _f(env, "ML_THRESHOLD", _f(env, "threshold", c.threshold))
+        c.bound = _i(env, "ML_BOUND", _i(env, "bound", c.bound))
+        c.min_lower_bound = _f(env, "min_lower_bound", c.min_lower_bound)
+        n = _i(env, "metric_type_threshold_count", -1)
+        if n >= 0:
+            rules = {}
+            for i in range(n):
+                name = env.get(f"metric_type{i}")
+                if not name:
+                    continue
+                rules[name] = MetricRule(_f(env, f"threshold{i}", c.threshold), _i(env, f"bound{i}", c.bound),
+                                         _f(env, f"min_lower_bound{i}", c.min_lower_bound))
+            c.metric_rules = rules
+        c.min_historical_points = _i(env, "MIN_HISTORICAL_DATA_POINT_TO_MEASURE", c.min_historical_points)
+        c.pairwise_algorithm = env.get("ML_PAIRWISE_ALGORITHM", c.pairwise_algorithm) or c.pairwise_algorithm
+        c.pairwise_threshold = _f(env, "ML_PAIRWISE_THRESHOLD", c.pairwise_threshold)
+        c.min_mann_white = _i(env, "MIN_MANN_WHITE_DATA_POINTS", c.min_mann_white)
+        c.min_wilcoxon = _i(env, "MIN_WILCOXON_DATA_POINTS", c.min_wilcoxon)
+        c.min_kruskal = _i(env, "MIN_KRUSKAL_DATA_POINTS", c.min_kruskal)
+        c.pairwise_threshold_factor = _f(env, "ML_PAIRWISE_THRESHOLD_FACTOR", c.pairwise_threshold_factor)
+        c.max_stuck_seconds = _f(env, "MAX_STUCK_IN_SECONDS", c.max_stuck_seconds)
+        c.max_cache_size = _i(env, "MAX_CACHE_SIZE", c.max_cache_size)
+        c.es_endpoint = env.get("ES_ENDPOINT", c.es_endpoint) or c.es_endpoint
+        c.metrics_port = _i(env, "METRICS_PORT", c.metrics_port)
+        c.poll_interval = _f(env, "POLL_INTERVAL", c.poll_interval)
+        c.hpa_breath_up = _f(env, "HPA_BREATH_UP_SECONDS", c.hpa_breath_up)
+        c.hpa_breath_down = _f(env, "HPA_BREATH_DOWN_SECONDS", c.hpa_breath_down)
+        return c
+
+
+@dataclass
+class ServiceConfig:
+    elastic_url: str = "http://localhost:9200/"
+    query_endpoint: str = "http://prometheus-k8s.monitoring.svc.cluster.local:9090/"
+    store: str = "memory"          # memory | sqlite:<path> | elasticsearch
+    port: int = 8099
+
+    @classmethod
+    def from_env(cls, env: Mapping[str, str] | None = None) -> "ServiceConfig":
+        env = os.environ if env is None else env
+        c = cls()
+        c.elastic_url = env.get("ELASTIC_URL") or c.elastic_url
+        c.query_endpoint = env.get("QUERY_SERVICE_ENDPOINT") or c.query_endpoint
+        c.store = env.get("FOREMAST_STORE") or c.store
+        c.port = _i(env, "PORT", c.port)
+        return c
+
+
+@dataclass
+class BarrelmanConfig:
+    mode: str = "hpa_and_healthy_monitoring"   # MODE
+    hpa_strategy: str = "hpa_exists"           # HPA_STRATEGY
+    namespace: str = ""                        # NAMESPACE (controller's own namespace)
+    poll_seconds: float = 10.0                 # Barrelman.go:64
+    watch_time_minutes: int = 10               # DeploymentController.go:48
+    wait_until_max_minutes: int = 30           # DeploymentController.go:50
+    workers: int = 2                           # cmd/manager/main.go:108
+
+    @classmethod
+    def from_env(cls, env: Mapping[str, str] | None = None) -> "BarrelmanConfig":
+        env = os.environ if env is None else env
+        c = cls()
+        c.mode = env.get("MODE") or c.mode
+        c.hpa_strategy = env.get("HPA_STRATEGY") or c.hpa_strategy
+        c.namespace = env.get("NAMESPACE", c.namespace)
+        return c

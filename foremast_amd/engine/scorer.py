@@ -1,0 +1,118 @@
+"""Batched canary scorer: the brain's per-cycle judgement for a whole shard of
+services in three kernel launches.
+
+Pipeline per tick (docs/BRAIN_SPEC.md §4-5; reference intent
+docs/guides/design.md:31-43, sequence diagram
+.gitbook/assets/foremastjudgementsequencediagram.png):
+
+1. K4 pairwise tests current-vs-baseline -> ``diff`` (distribution changed)
+2. K1+K7 moving_average_all bounds over the 7-day history fused with the
+   decision on the current window; rows whose distribution changed get the
+   lowered threshold (``threshold * pairwise_threshold_factor``)
+3. service reduce -> packed [S, 4] verdict (status, score, metric mask, count)
+
+All buffers are pre-allocated per shape so the chain can be captured into a
+HIP graph (``capture``) and replayed with zero host work per tick.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from ..config import BrainConfig
+from ..ops import canary as C
+
+
+@dataclass
+class CanaryOutputs:
+    pvals: torch.Tensor
+    pstats: torch.Tensor
+    diff: torch.Tensor
+    suff: torch.Tensor
+    decide: C.DecideResult
+    packed: torch.Tensor        # [S, 4]
+
+
+class CanaryScorer:
+    def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu"):
+        self.cfg = cfg or BrainConfig()
+        self.aliases = list(aliases)
+        self.M = len(aliases)
+        self.device = torch.device(device)
+        rules = [self.cfg.rule_for(a) for a in aliases]
+        self.thr = torch.tensor([r.threshold for r in rules], dtype=torch.float32, device=self.device)
+        self.bound = torch.tensor([r.bound for r in rules], dtype=torch.int32, device=self.device)
+        self.minlb = torch.tensor([r.min_lower_bound for r in rules], dtype=torch.float32, device=self.device)
+        self.pcfg = C.PairwiseConfig(self.cfg.pairwise_algorithm, self.cfg.pairwise_threshold,
+                                     self.cfg.min_mann_white, self.cfg.min_wilcoxon, self.cfg.min_kruskal)
+        self._out: dict[tuple, CanaryOutputs] = {}
+        self._graph = None
+        self._graph_key = None
+
+    def _alloc(self, R: int, n_cur: int) -> CanaryOutputs:
+        key = (R, n_cur)
+        if key not in self._out:
+            d = self.device
+            self._out[key] = CanaryOutputs(
+                pvals=torch.empty((R, C.N_TESTS), dtype=torch.float32, device=d),
+                pstats=torch.empty((R, C.N_TESTS), dtype=torch.float32, device=d),
+                diff=torch.empty((R,), dtype=torch.int8, device=d),
+                suff=torch.empty((R, C.SUFF), dtype=torch.float64, device=d),
+                decide=C.alloc_decide(R, n_cur, d),
+                packed=torch.empty((R // self.M, 4), dtype=torch.float32, device=d),
+            )
+        return self._out[key]
+
+    def score(self, hist: torch.Tensor, base: torch.Tensor | None, cur: torch.Tensor,
+              n_hist: int | None = None) -> CanaryOutputs:
+        R = cur.shape[0]
+        if not cur.is_cuda:
+            if base is not None and base.shape[1] > 0:
+                pv, ps, df = C.pairwise_tests(cur, base, self.pcfg)
+            else:
+                pv = torch.full((R, C.N_TESTS), float("nan"))
+                ps = pv.clone()
+                df = torch.zeros((R,), dtype=torch.int8)
+            dec = C.stats_decide(hist, cur, n_hist, self.M, self.thr, self.bound, self.minlb, df,
+                                 self.cfg.pairwise_threshold_factor, self.cfg.min_historical_points)
+            packed = C.service_reduce(dec.count, dec.score, dec.valid, self.M)
+            return CanaryOutputs(pv, ps, df, None, dec, packed)
+        o = self._alloc(R, cur.shape[1])
+        has_base = base is not None and base.shape[1] > 0
+        if has_base:
+            self._pairwise_into(cur, base, o)
+        C.stats_decide(hist, cur, n_hist, self.M, self.thr, self.bound, self.minlb, o.diff if has_base else None,
+                       self.cfg.pairwise_threshold_factor, self.cfg.min_historical_points, out=o.decide)
+        C.service_reduce(o.decide.count, o.decide.score, o.decide.valid, self.M, out=o.packed)
+        return o
+
+    def _pairwise_into(self, cur, base, o: CanaryOutputs) -> None:
+        from ..ops._lib import LIB, ptr, stream_of
+        R = cur.shape[0]
+        mask, anyc = self.pcfg.mask_and_combine()
+        LIB.call("fm_pairwise_tests", ptr(cur), cur.stride(0), cur.shape[1], ptr(base), base.stride(0),
+                 base.shape[1], R, mask, anyc, float(self.pcfg.p_threshold), self.pcfg.min_mann_white,
+                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(o.diff),
+                 ptr(o.suff), stream_of(cur))
+
+    # -- HIP graph capture of the whole tick ---------------------------------
+    def capture(self, hist, base, cur, n_hist=None):
+        """Capture the 3-kernel tick into a graph over static buffers; returns
+        a replay callable producing outputs in ``self._out``."""
+        assert cur.is_cuda
+        o = self.score(hist, base, cur, n_hist)  # warm / allocate
+        torch.cuda.synchronize(cur.device)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(cur.device)
+        s.wait_stream(torch.cuda.current_stream(cur.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self.score(hist, base, cur, n_hist)
+        torch.cuda.current_stream(cur.device).wait_stream(s)
+        self._graph = g
+
+        def replay() -> CanaryOutputs:
+            g.replay()
+            return o
+        return replay

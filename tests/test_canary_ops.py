@@ -1,0 +1,190 @@
+"""Numerics of the canary slice: CPU reference vs scipy (CPU), HIP kernels vs
+the fp64 numpy reference / scipy (GPU)."""
+import numpy as np
+import pytest
+import scipy.stats as ss
+import torch
+
+from foremast_amd.ops import canary as C
+from foremast_amd.ops import reference as ref
+
+
+def _data(R, n1, n2, seed=0, ties=True, nan_frac=0.0, shift=0.3):
+    rng = np.random.default_rng(seed)
+    cur = rng.normal(0, 1, (R, n1))
+    base = rng.normal(shift, 1.2, (R, n2))
+    if ties:
+        cur = np.round(cur, 1)
+        base = np.round(base, 1)
+    if nan_frac:
+        cur[rng.random(cur.shape) < nan_frac] = np.nan
+        base[rng.random(base.shape) < nan_frac] = np.nan
+    return cur.astype(np.float32), base.astype(np.float32)
+
+
+def _scipy_row(c, b):
+    cf, bf = c[np.isfinite(c)].astype(np.float64), b[np.isfinite(b)].astype(np.float64)
+    out = {}
+    out["mw"] = ss.mannwhitneyu(cf, bf, method="asymptotic")
+    out["kru"] = ss.kruskal(cf, bf)
+    D = ss.ks_2samp(cf, bf).statistic
+    en = len(cf) * len(bf) / (len(cf) + len(bf))
+    out["ks"] = (D, ss.kstwobign.sf(D * np.sqrt(en)))
+    out["t"] = ss.ttest_ind(cf, bf, equal_var=False)
+    npair = min(len(c), len(b))
+    # differences formed in fp32 (device semantics), ranked in fp64
+    d = (c[:npair].astype(np.float32) - b[:npair].astype(np.float32)).astype(np.float64)
+    ok = np.isfinite(d)
+    out["wil"] = ss.wilcoxon(d[ok], method="approx") if (d[ok] != 0).sum() > 0 else None
+    return out
+
+
+@pytest.mark.parametrize("n1,n2,nan_frac", [(50, 50, 0.0), (30, 41, 0.05), (200, 150, 0.0)])
+def test_reference_pairwise_matches_scipy(n1, n2, nan_frac):
+    cur, base = _data(8, n1, n2, nan_frac=nan_frac)
+    P, S, _ = ref.pairwise_tests(cur, base, 31, 0, 0.05, 20, 20, 5)
+    for r in range(8):
+        o = _scipy_row(cur[r], base[r])
+        np.testing.assert_allclose(P[r, 0], o["mw"].pvalue, rtol=1e-5)
+        np.testing.assert_allclose(S[r, 0], o["mw"].statistic, rtol=1e-6)
+        np.testing.assert_allclose(P[r, 2], o["kru"].pvalue, rtol=1e-5)
+        np.testing.assert_allclose(S[r, 3], o["ks"][0], rtol=1e-6)
+        np.testing.assert_allclose(P[r, 3], o["ks"][1], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(P[r, 4], o["t"].pvalue, rtol=1e-4)
+        if o["wil"] is not None:
+            np.testing.assert_allclose(P[r, 1], o["wil"].pvalue, rtol=1e-4)
+
+
+def test_reference_gates_and_combination():
+    cur, base = _data(4, 10, 10)
+    P, _, d = ref.pairwise_tests(cur, base, 31, 0, 0.05, 20, 20, 5)
+    assert np.isnan(P[:, 0]).all() and np.isnan(P[:, 1]).all()  # below MW/Wilcoxon gates
+    assert not np.isnan(P[:, 2]).any()                          # Kruskal gate is 5
+    # ALL over a big shift -> different; identical -> not different
+    c = np.tile(np.linspace(0, 1, 40, dtype=np.float32), (2, 1))
+    b = c.copy()
+    b[0] += 5
+    _, _, d = ref.pairwise_tests(c, b, 31, 0, 0.05, 20, 20, 5)
+    assert d.tolist() == [1, 0]
+
+
+def test_reference_stats_decide_and_reduce():
+    rng = np.random.default_rng(1)
+    M = 4
+    hist = rng.normal(10, 2, (8, 1000)).astype(np.float32)
+    hist[0, :10] = np.nan
+    cur = rng.normal(10, 2, (8, 30)).astype(np.float32)
+    cur[1, 5] = 100.0   # upper violation on metric 1 (bound both)
+    cur[2, 7] = -50.0   # lower violation on metric 2 (bound upper only -> ignored)
+    thr = np.array([2, 3, 2, 5], np.float32)
+    bound = np.array([1, 3, 1, 1], np.int32)
+    minlb = np.zeros(4, np.float32)
+    stats, words, count, score, valid = ref.stats_decide(hist, cur, M, thr, bound, minlb, None, 0.8, 10)
+    h = hist[0][np.isfinite(hist[0])].astype(np.float64)
+    np.testing.assert_allclose(stats[0, 0], h.mean(), rtol=1e-6)
+    np.testing.assert_allclose(stats[0, 1], h.std(), rtol=1e-5)
+    assert count[1] >= 1 and (words[1].view(np.uint64)[0] >> np.uint64(5)) & np.uint64(1)
+    assert count[2] == ((cur[2] > stats[2, 2])).sum()
+    packed = ref.service_reduce(count, score, valid, M)
+    assert packed.shape == (2, 4)
+    assert packed[0, 0] == 1 and int(packed[0, 2]) & 2
+
+
+def test_synth_reference_deterministic_across_shards():
+    h1, b1, c1 = ref.synth_fleet(6, 4, 200, 3, 5, 0, 7, 0.5, 1.0, 200)
+    h2, b2, c2 = ref.synth_fleet(3, 4, 200, 3, 5, 3, 7, 0.5, 1.0, 200)
+    np.testing.assert_array_equal(h1[12:], h2)
+    np.testing.assert_array_equal(c1[12:], c2)
+
+
+# --------------------------------------------------------------------------- GPU
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1,n2,nan_frac", [(20, 25, 0.0), (50, 50, 0.0), (60, 60, 0.03), (100, 120, 0.0),
+                                            (256, 200, 0.02)])
+def test_gpu_pairwise_matches_reference(cuda, n1, n2, nan_frac):
+    R = 257
+    cur, base = _data(R, n1, n2, seed=n1 + n2, nan_frac=nan_frac)
+    P0, S0, d0 = ref.pairwise_tests(cur, base, 31, 0, 0.05, 20, 20, 5)
+    pv, st, d = C.pairwise_tests(torch.from_numpy(cur).to(cuda), torch.from_numpy(base).to(cuda))
+    pv, st, d = pv.cpu().numpy(), st.cpu().numpy(), d.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(pv), np.isnan(P0))
+    np.testing.assert_allclose(np.nan_to_num(st[:, [0, 1, 3]]), np.nan_to_num(S0[:, [0, 1, 3]]), rtol=1e-5,
+                               atol=1e-5)
+    np.testing.assert_allclose(np.nan_to_num(pv), np.nan_to_num(P0), rtol=2e-4, atol=2e-6)
+    assert (d == d0).mean() > 0.995
+
+
+@pytest.mark.gpu
+def test_gpu_pairwise_scipy_spot(cuda):
+    cur, base = _data(16, 50, 50, seed=3)
+    pv, _, _ = C.pairwise_tests(torch.from_numpy(cur).to(cuda), torch.from_numpy(base).to(cuda))
+    pv = pv.cpu().numpy()
+    for r in range(16):
+        o = _scipy_row(cur[r], base[r])
+        np.testing.assert_allclose(pv[r, 0], o["mw"].pvalue, rtol=2e-4)
+        np.testing.assert_allclose(pv[r, 2], o["kru"].pvalue, rtol=2e-4)
+        np.testing.assert_allclose(pv[r, 4], o["t"].pvalue, rtol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1000, 10080, 4097])
+def test_gpu_stats_decide_matches_reference(cuda, T):
+    M, S = 8, 37
+    R = S * M
+    rng = np.random.default_rng(T)
+    ld = (T + 3) // 4 * 4
+    hist = np.full((R, ld), np.nan, np.float32)
+    hist[:, :T] = rng.gamma(3.0, 2.0, (R, T)).astype(np.float32)
+    hist[3, 100:200] = np.nan
+    cur = rng.gamma(3.0, 2.0, (R, 50)).astype(np.float32)
+    cur[5, :] = 200.0
+    cur[9, 3] = np.nan
+    thr = np.array([2, 10, 2, 3, 5, 5, 2, 2], np.float32)
+    bound = np.array([1, 3, 1, 1, 1, 1, 2, 3], np.int32)
+    minlb = np.zeros(M, np.float32)
+    diff = (rng.random(R) < 0.3).astype(np.int8)
+    r0 = ref.stats_decide(hist[:, :T], cur, M, thr, bound, minlb, diff, 0.8, 10)
+    t = lambda a: torch.from_numpy(a).to(cuda)
+    o = C.stats_decide(t(hist), t(cur), T, M, t(thr), t(bound), t(minlb), t(diff), 0.8, 10)
+    np.testing.assert_allclose(o.stats.cpu().numpy(), r0[0], rtol=2e-5, atol=1e-5)
+    fl = C.unpack_flags(o.flags, 50)
+    fr = C.unpack_flags(torch.from_numpy(r0[1]), 50)
+    assert (fl != fr).sum() <= 2  # boundary points may flip at fp32 rounding
+    assert np.abs(o.count.cpu().numpy() - r0[2]).sum() <= 2
+    np.testing.assert_array_equal(o.valid.cpu().numpy(), r0[4])
+    packed = C.service_reduce(o.count, o.score, o.valid, M).cpu().numpy()
+    p0 = ref.service_reduce(r0[2], r0[3], r0[4], M)
+    assert (packed[:, 0] == p0[:, 0]).mean() > 0.97
+    idx, val = C.compact_anomalies(o, t(cur))
+    assert idx.shape[0] == int(o.count.sum())
+    ii = idx.cpu().numpy()
+    np.testing.assert_array_equal(val.cpu().numpy(), cur[ii[:, 0], ii[:, 1]])
+
+
+@pytest.mark.gpu
+def test_gpu_synth_matches_reference(cuda):
+    S, M, T, P, W = 7, 8, 3000, 3, 10
+    h, b, c = C.synth_fleet(S, M, T, P, W, 11, device=cuda, fault_rate=0.5)
+    h0, b0, c0 = C.synth_fleet(S, M, T, P, W, 11, device="cpu", fault_rate=0.5)
+    np.testing.assert_allclose(h.cpu().numpy()[:, :T], h0.numpy()[:, :T], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(c.cpu().numpy(), c0.numpy(), rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(b.cpu().numpy(), b0.numpy(), rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_gpu_scorer_graph_equals_eager_and_cpu(cuda):
+    from foremast_amd.engine.scorer import CanaryScorer
+    aliases = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
+    S, T = 64, 2000
+    h, b, c = C.synth_fleet(S, 8, T, 5, 10, 0, device=cuda, fault_rate=0.2)
+    sc = CanaryScorer(aliases, device=cuda)
+    eager = sc.score(h, b, c, T).packed.clone()
+    replay = sc.capture(h, b, c, T)
+    g = replay().packed.clone()
+    torch.testing.assert_close(g, eager)
+    hc, bc, cc = (x.cpu() for x in (h, b, c))
+    cpu = CanaryScorer(aliases, device="cpu").score(hc, bc, cc, T).packed
+    assert (cpu[:, 0] == eager.cpu()[:, 0]).float().mean() > 0.95
+    assert int((eager[:, 0] == 1).sum()) > 0
