@@ -1,0 +1,117 @@
+// K8: HPA score and K9: downstream-impact propagation.
+//
+// K8 (docs/dynamic_autoscaling.md:30-130, examples/hpa/images/HPA_Score.png,
+// examples/hpa/README.MD:26-64): per service the template metrics are placed
+// against their learned [lower, upper] band; load metrics above the band AND an
+// SLA metric violated -> score > 50 (scale up); load below the band with the SLA
+// met -> score < 50 (scale down); otherwise 50.  Breath-up < breath-down
+// hysteresis and a flip counter suppress oscillation.  Exact rules:
+// docs/BRAIN_SPEC.md §7.  One thread per service; state is updated in place.
+//
+// K9 (README.md:24,27; CallerWebMvcTagsProvider.java:22-28): the caller->callee
+// graph built from the `caller` tag; downstream impact of u after k hops is
+// max over paths of (edge weight product) * anomaly score of the reached callee.
+// CSR max-times SpMV, one wave per row, k launches ping-ponging two buffers.
+#include "fm_common.h"
+
+using namespace fm;
+
+__global__ __launch_bounds__(256) void hpa_score_kernel(
+    const float* __restrict__ cur, const float* __restrict__ upper, const float* __restrict__ lower, int64_t S, int Mt,
+    const float* __restrict__ weight, const int8_t* __restrict__ is_increase, const int8_t* __restrict__ is_absolute,
+    const int8_t* __restrict__ role, double now, float breath_up, float breath_down, int max_flips,
+    float flip_window, int8_t* __restrict__ last_dir, double* __restrict__ last_time, int* __restrict__ flips,
+    double* __restrict__ flip_t0, int* __restrict__ score_out, int8_t* __restrict__ reason_out,
+    float* __restrict__ raw_out) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  float up = 0.f, down = 0.f;
+  bool has_sla = false, sla_violated = false;
+  for (int j = 0; j < Mt; ++j) {
+    const float c = cur[s * Mt + j], u = upper[s * Mt + j], l = lower[s * Mt + j];
+    if (role[j] == 1) has_sla = true;
+    if (!isfinite(c) || !isfinite(u) || !isfinite(l)) continue;
+    float scale = is_absolute[j] ? fmaxf(fabsf(u), 1e-12f) : fmaxf(u - l, 1e-12f);
+    float dev = 0.f;
+    if (c > u) dev = (c - u) / scale;
+    else if (c < l) dev = (c - l) / scale;
+    if (!is_increase[j]) dev = -dev;
+    if (role[j] == 1) {
+      if (dev > 0.f) sla_violated = true;
+    } else {
+      const float w = weight[j];
+      if (dev > 0.f) up = fmaxf(up, w * dev);
+      if (dev < 0.f) down = fmaxf(down, -w * dev);
+    }
+  }
+  if (!has_sla) sla_violated = up > 0.f;
+  int raw = 50;
+  if (up > 0.f && sla_violated) raw = 50 + (int)lrintf(50.f * fminf(1.f, up));
+  else if (down > 0.f && up == 0.f && !sla_violated) raw = 50 - (int)lrintf(50.f * fminf(1.f, down));
+  raw_out[s] = (float)raw;
+  int dir = raw > 50 ? 1 : (raw < 50 ? -1 : 0);
+  int8_t reason = dir > 0 ? 1 : (dir < 0 ? 2 : 0);
+  int score = raw;
+  if (now - flip_t0[s] > flip_window) { flips[s] = 0; flip_t0[s] = now; }
+  if (dir != 0) {
+    const int ld = last_dir[s];
+    const float wait = dir > 0 ? breath_up : breath_down;
+    if (ld != 0 && now - last_time[s] < wait) {
+      score = 50; reason = 3;
+    } else if (ld != 0 && dir != ld && flips[s] >= max_flips) {
+      score = 50; reason = 4;
+    } else {
+      if (ld != 0 && dir != ld) flips[s] += 1;
+      last_dir[s] = (int8_t)dir;
+      last_time[s] = now;
+    }
+  }
+  score_out[s] = score;
+  reason_out[s] = reason;
+}
+
+FM_API int fm_hpa_score(const float* cur, const float* upper, const float* lower, int64_t S, int Mt, const float* weight,
+                        const int8_t* is_increase, const int8_t* is_absolute, const int8_t* role, double now,
+                        float breath_up, float breath_down, int max_flips, float flip_window, int8_t* last_dir,
+                        double* last_time, int* flips, double* flip_t0, int* score, int8_t* reason, float* raw,
+                        hipStream_t stream) {
+  if (S <= 0) return 0;
+  hipLaunchKernelGGL(hpa_score_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, cur, upper, lower, S,
+                     Mt, weight, is_increase, is_absolute, role, now, breath_up, breath_down, max_flips, flip_window,
+                     last_dir, last_time, flips, flip_t0, score, reason, raw);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void impact_hop_kernel(const int64_t* __restrict__ rowptr,
+                                                         const int* __restrict__ col, const float* __restrict__ w,
+                                                         const float* __restrict__ a, const float* __restrict__ prev,
+                                                         int64_t S, float* __restrict__ out) {
+  const int64_t u = (int64_t)blockIdx.x * 4 + wave_id();
+  if (u >= S) return;
+  const int lane = lane_id();
+  const int64_t b = rowptr[u], e = rowptr[u + 1];
+  float best = 0.f;
+  for (int64_t k = b + lane; k < e; k += 64) {
+    const int v = col[k];
+    const float val = fmaxf(a[v], prev != nullptr ? prev[v] : 0.f) * w[k];
+    best = fmaxf(best, val);
+  }
+  best = wave_max(best);
+  if (lane == 0) out[u] = best;
+}
+
+FM_API int fm_downstream_impact(const int64_t* rowptr, const int* col, const float* w, const float* a, int64_t S,
+                                int hops, float* buf0, float* buf1, hipStream_t stream) {
+  if (S <= 0 || hops <= 0) return 0;
+  const dim3 grid((unsigned)((S + 3) / 4)), block(256);
+  const float* prev = nullptr;
+  float* bufs[2] = {buf0, buf1};
+  for (int h = 0; h < hops; ++h) {
+    float* out = bufs[h & 1];
+    hipLaunchKernelGGL(impact_hop_kernel, grid, block, 0, stream, rowptr, col, w, a, prev, S, out);
+    FM_LAUNCH_CHECK();
+    prev = out;
+  }
+  return 0;
+}

@@ -1,0 +1,94 @@
+"""Minimal Go-encoding/json-compatible dataclass (de)serialisation.
+
+* field names come from ``jf("name", omitempty=...)`` metadata, like Go struct tags;
+* ``omitempty`` drops "", 0, False, None, empty list/dict — but NOT nested
+  structs (Go never treats a struct value as empty);
+* decoding matches keys case-insensitively, as Go's encoding/json does (this is
+  how the service's ``hpalogs`` key fills barrelman's ``HpaLogs`` field,
+  foremast-barrelman/pkg/client/analyst/analystclient.go:64 vs
+  foremast-service/pkg/models/models.go:90).
+"""
+from __future__ import annotations
+
+import dataclasses
+import typing
+from typing import Any
+
+
+def jf(name: str, omitempty: bool = False, default=dataclasses.MISSING, default_factory=dataclasses.MISSING):
+    md = {"json": name, "omitempty": omitempty}
+    if default_factory is not dataclasses.MISSING:
+        return dataclasses.field(default_factory=default_factory, metadata=md)
+    if default is not dataclasses.MISSING:
+        return dataclasses.field(default=default, metadata=md)
+    return dataclasses.field(metadata=md)
+
+
+def _empty(v: Any) -> bool:
+    if dataclasses.is_dataclass(v):
+        return False
+    return v is None or v == "" or v is False or (isinstance(v, (int, float)) and not isinstance(v, bool) and v == 0) \
+        or (isinstance(v, (list, dict, tuple)) and len(v) == 0)
+
+
+def to_json(obj: Any) -> Any:
+    if dataclasses.is_dataclass(obj):
+        out = {}
+        for f in dataclasses.fields(obj):
+            name = f.metadata.get("json", f.name)
+            if name == "-":
+                continue
+            v = getattr(obj, f.name)
+            if f.metadata.get("omitempty") and _empty(v):
+                continue
+            out[name] = to_json(v)
+        return out
+    if isinstance(obj, dict):
+        return {k: to_json(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return [to_json(v) for v in obj]
+    return obj
+
+
+def _ci_get(d: dict, key: str):
+    if key in d:
+        return True, d[key]
+    lk = key.lower()
+    for k, v in d.items():
+        if isinstance(k, str) and k.lower() == lk:
+            return True, v
+    return False, None
+
+
+def _convert(tp, v):
+    if v is None:
+        return None
+    origin = typing.get_origin(tp)
+    args = typing.get_args(tp)
+    if origin is typing.Union:
+        non_none = [a for a in args if a is not type(None)]
+        return _convert(non_none[0], v) if non_none else v
+    if dataclasses.is_dataclass(tp):
+        return from_json(tp, v) if isinstance(v, dict) else tp()
+    if origin in (list, typing.List):
+        return [_convert(args[0], x) for x in v] if isinstance(v, list) else []
+    if origin in (dict, typing.Dict):
+        return {k: _convert(args[1], x) for k, x in v.items()} if isinstance(v, dict) else {}
+    if tp is float and isinstance(v, (int, float)) and not isinstance(v, bool):
+        return float(v)
+    if tp is int and isinstance(v, (int, float)) and not isinstance(v, bool):
+        return int(v)
+    return v
+
+
+def from_json(cls, data: dict):
+    if data is None:
+        return cls()
+    hints = typing.get_type_hints(cls)
+    kw = {}
+    for f in dataclasses.fields(cls):
+        name = f.metadata.get("json", f.name)
+        ok, v = _ci_get(data, name)
+        if ok:
+            kw[f.name] = _convert(hints[f.name], v)
+    return cls(**kw)

@@ -38,6 +38,24 @@ _SIGS: dict[str, list] = {
                              c_void_p, c_void_p],
     "fm_synth_fleet": [c_void_p, c_i64, c_i64, c_i64, c_int, c_i64, c_int, c_int, c_int, c_int, c_float, c_float,
                        c_u32, c_void_p],
+    "fm_es_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                  c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fm_band_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p, c_i64, c_int, c_void_p, c_void_p,
+                       c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                       c_void_p],
+    "fm_fft_seasonal": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                        c_i64, c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fm_phase_profile": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fm_bivariate": [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p,
+                     c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "fm_hpa_score": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                     ctypes.c_double, c_float, c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_void_p, c_void_p, c_void_p],
+    "fm_downstream_impact": [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p],
+    "fm_lsq_project": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_void_p],
+    "fm_lstm_forward": [c_void_p, c_i64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_void_p, c_void_p],
 }
 
 

@@ -1,0 +1,90 @@
+"""K6 LSTM forward on bf16 MFMA (csrc/kernels/lstm.hip).
+
+Weights use torch.nn.LSTM conventions (gate order i, f, g, o; W_ih [4H, I],
+W_hh [4H, H], b = b_ih + b_hh).  ``pack_lstm`` swizzles them into the
+per-wave register-fragment layout the kernel loads with one 16-B load per
+fragment, folding the input projection and bias into an extra K step."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._lib import LIB, check, ptr, require_native, stream_of
+
+SUPPORTED_H = (32, 64, 128)
+
+
+def _bf16_bits(a: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return u.astype(np.uint16)
+
+
+def bf16_round(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def pack_lstm(w_ih: torch.Tensor, w_hh: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """-> uint8 tensor [H/16, 2, KS, 64, 16 bytes] (bf16 fragments)."""
+    w_ih = w_ih.detach().float().cpu().numpy()
+    w_hh = w_hh.detach().float().cpu().numpy()
+    b = bias.detach().float().cpu().numpy()
+    H4, I = w_ih.shape
+    H = H4 // 4
+    check(H in SUPPORTED_H, f"hidden size must be one of {SUPPORTED_H}")
+    check(I <= 15, "input features must be <= 15 (folded into one K step with the bias)")
+    KS = H // 16 + 1
+    nw = H // 16
+    out = np.zeros((nw, 2, KS, 64, 8), np.float32)
+    lane = np.arange(64)
+    r, hh = lane & 31, lane >> 5
+    for w in range(nw):
+        for rt in range(2):
+            gate, unit = r >> 3, 16 * w + 8 * rt + (r & 7)
+            trow = gate * H + unit
+            for ks in range(KS):
+                for j in range(8):
+                    if ks < KS - 1:
+                        out[w, rt, ks, :, j] = w_hh[trow, 16 * ks + 8 * hh + j]
+                    else:
+                        kk = 8 * hh + j
+                        v = np.where(kk < I, w_ih[trow, np.minimum(kk, I - 1)] if I > 0 else 0.0,
+                                     np.where(kk == I, b[trow], 0.0))
+                        out[w, rt, ks, :, j] = v
+    return torch.from_numpy(_bf16_bits(out).view(np.uint8).copy())
+
+
+def lstm_forward(x: torch.Tensor, packed: torch.Tensor, H: int, h0=None, c0=None, return_seq: bool = False):
+    """x [B, L, I] float32 -> (h_L [B,H], c_L [B,H], seq [B,L,H] bf16 or None)."""
+    check(x.dim() == 3 and x.dtype == torch.float32 and x.is_contiguous(), "x must be contiguous [B, L, I] float32")
+    B, L, I = x.shape
+    require_native(x)
+    check(x.is_cuda, "lstm_forward runs on the GPU; use ref_lstm_forward on CPU")
+    d = x.device
+    hT = torch.empty((B, H), dtype=torch.float32, device=d)
+    cT = torch.empty((B, H), dtype=torch.float32, device=d)
+    seq = torch.empty((B, L, H), dtype=torch.bfloat16, device=d) if return_seq else None
+    pk = packed.to(d)
+    LIB.call("fm_lstm_forward", ptr(x), B, L, I, H, ptr(pk), ptr(h0), ptr(c0), ptr(hT), ptr(cT), ptr(seq),
+             stream_of(x))
+    return hT, cT, seq
+
+
+def ref_lstm_forward(x: torch.Tensor, w_ih, w_hh, bias, h0=None, c0=None, emulate_bf16: bool = True):
+    """fp32 reference; with emulate_bf16 the weights, inputs and the recurrent h
+    are rounded to bf16 exactly where the kernel rounds them."""
+    B, L, I = x.shape
+    H = w_hh.shape[1]
+    rd = bf16_round if emulate_bf16 else (lambda t: t)
+    Wi, Wh, b = rd(w_ih.float()), rd(w_hh.float()), rd(bias.float())
+    h = torch.zeros(B, H) if h0 is None else h0.float().clone()
+    c = torch.zeros(B, H) if c0 is None else c0.float().clone()
+    hr = rd(h)
+    xs = rd(x.float())
+    for t in range(L):
+        g = hr @ Wh.T + xs[:, t] @ Wi.T + b
+        i, f, gg, o = g.chunk(4, dim=1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        hr = rd(h)
+    return h, c

@@ -1,0 +1,255 @@
+"""Numerics of the model kernels (K2 smoothing, K3 FFT, K5 bivariate, K6 LSTM,
+K8 HPA score, K9 downstream impact, K10 least squares): references on CPU,
+HIP kernels vs the references on GPU."""
+import numpy as np
+import pytest
+import torch
+
+from foremast_amd.ops import fft as FF
+from foremast_amd.ops import lsq as LQ
+from foremast_amd.ops import lstm as LS
+from foremast_amd.ops import misc as MI
+from foremast_amd.ops import smoothing as SM
+
+
+def _seasonal(R, T, period=1440, seed=0, noise=0.05):
+    rng = np.random.default_rng(seed)
+    t = np.arange(T)
+    amp = rng.uniform(0.5, 2.0, (R, 1))
+    ph = rng.uniform(0, 2 * np.pi, (R, 1))
+    x = 10 + amp * np.sin(2 * np.pi * t / period + ph) + 0.0005 * t + rng.normal(0, noise, (R, T))
+    return x.astype(np.float32)
+
+
+# ----------------------------------------------------------------- CPU references
+def test_ref_es_matches_scalar_loop():
+    x = _seasonal(3, 300, period=24, seed=1)
+    grid = SM.default_grid(2)[:4]
+    fc, sig, best, sse = SM.ref_es_fit(x, 2, 5, 24, grid)
+    for r in range(3):
+        for g in range(4):
+            a, b, gm = grid[g]
+            y = x[r].astype(np.float32)
+            m = 24
+            s1, s2 = y[:m].mean(), y[m:2 * m].mean()
+            lvl, tr = s1, (s2 - s1) / m
+            season = list(y[:m] - s1)
+            e2 = 0.0
+            for t in range(m, len(y)):
+                so = season[t % m]
+                e2 += float(y[t] - (lvl + tr + so)) ** 2
+                lp = lvl
+                lvl = a * (y[t] - so) + (1 - a) * (lvl + tr)
+                tr = b * (lvl - lp) + (1 - b) * tr
+                season[t % m] = gm * (y[t] - lvl) + (1 - gm) * so
+            np.testing.assert_allclose(sse[r, g], e2, rtol=1e-3)
+
+
+def test_ref_fft_detects_daily_period():
+    assert FF.plan_radices(5040) == [4, 4, 9, 5, 7]
+    assert FF.supported_length(10080) and not FF.supported_length(10082)
+    x = _seasonal(4, 10080, period=1440)
+    s = FF.fft_seasonal(torch.from_numpy(x))
+    assert s.period_bin.tolist() == [7, 7, 7, 7]
+    np.testing.assert_allclose(s.period.numpy(), 1440.0)
+    prof = FF.phase_profile(torch.from_numpy(x), 10080, torch.full((4,), 1440, dtype=torch.int32), s.mean, 1440, s.slope)
+    assert prof.shape == (4, 1440) and float(prof.abs().max()) > 0.4
+
+
+def test_ref_prophet_recovers_signal():
+    T, H = 4032, 30
+    X = LQ.design_matrix(T, H)
+    rng = np.random.default_rng(0)
+    beta = rng.normal(0, 1, (5, 32))
+    beta[:, 0] += 50
+    y = (beta @ X.T).astype(np.float32)
+    y[:, :T] += rng.normal(0, 0.01, (5, T)).astype(np.float32)
+    ld = (T + 3) // 4 * 4
+    Y = np.zeros((5, ld), np.float32)
+    Y[:, :T] = y[:, :T]
+    fit = LQ.prophet_fit(torch.from_numpy(Y), T, H)
+    np.testing.assert_allclose(fit.forecast.numpy(), y[:, T:], rtol=0, atol=0.05)
+    assert float(fit.sigma.max()) < 0.02
+
+
+def test_ref_bivariate_matches_numpy_cov():
+    rng = np.random.default_rng(2)
+    a = rng.normal(0, 1, (3, 500))
+    b = 0.7 * a + rng.normal(0, 0.5, (3, 500))
+    ca = np.array([[0.0, 4.0, 0.5]] * 3)
+    cb = np.array([[0.0, -3.0, 0.4]] * 3)
+    params, dist, flags, cnt = MI.ref_bivariate(a, b, ca, cb, 3.0)
+    C = np.cov(a[0], b[0])
+    np.testing.assert_allclose(params[0, 2:], [C[0, 0], C[0, 1], C[1, 1]], rtol=1e-5)
+    d = np.array([ca[0, 1] - a[0].mean(), cb[0, 1] - b[0].mean()])
+    np.testing.assert_allclose(dist[0, 1], np.sqrt(d @ np.linalg.inv(C) @ d), rtol=1e-4)
+    assert cnt.tolist() == [1, 1, 1]
+
+
+def test_ref_hpa_score_rules():
+    # columns of examples/hpa/images/HPA_Score.png: (tps, latency)
+    tmpl = MI.HpaTemplate.from_aliases(["traffic", "latency"])
+    up = np.array([[10, 1.0]] * 5, np.float32)
+    lo = np.array([[5, 0.5]] * 5, np.float32)
+    cur = np.array([[15, 1.5],    # tps up, latency up  -> scale up
+                    [15, 0.7],    # tps up, latency ok  -> hold
+                    [2, 1.5],     # tps down, latency bad -> hold
+                    [2, 0.7],     # tps down, latency ok -> scale down
+                    [7, 0.7]], np.float32)  # within band -> hold
+    st = MI.HpaState.zeros(5)
+    sc, rs, raw = MI.hpa_score(torch.from_numpy(cur), torch.from_numpy(up), torch.from_numpy(lo), tmpl, st, 1000.0)
+    sc = sc.numpy()
+    assert sc[0] > 50 and sc[1] == 50 and sc[2] == 50 and sc[3] < 50 and sc[4] == 50
+    assert MI.REASONS[int(rs[0])] == "hpa is scaling up"
+    # breath-up: a second up decision 10 s later is held
+    sc2, rs2, _ = MI.hpa_score(torch.from_numpy(cur), torch.from_numpy(up), torch.from_numpy(lo), tmpl, st, 1010.0)
+    assert sc2[0] == 50 and rs2[0] == 3
+    sc3, _, _ = MI.hpa_score(torch.from_numpy(cur), torch.from_numpy(up), torch.from_numpy(lo), tmpl, st, 1100.0)
+    assert sc3[0] > 50
+
+
+def test_ref_downstream_impact():
+    g = MI.CallGraph.from_edges(4, [0, 1, 1], [1, 2, 3], [1.0, 0.5, 1.0])
+    a = np.array([0.0, 0.0, 2.0, 0.0], np.float32)
+    imp1 = MI.downstream_impact(g, torch.from_numpy(a), hops=1).numpy()
+    imp2 = MI.downstream_impact(g, torch.from_numpy(a), hops=2).numpy()
+    np.testing.assert_allclose(imp1, [0, 1.0, 0, 0])
+    np.testing.assert_allclose(imp2, [1.0, 1.0, 0, 0])
+
+
+def test_ref_lstm_matches_torch_lstm():
+    torch.manual_seed(0)
+    m = torch.nn.LSTM(3, 32, batch_first=True)
+    x = torch.randn(5, 7, 3)
+    out, (h, c) = m(x)
+    h2, c2 = LS.ref_lstm_forward(x, m.weight_ih_l0, m.weight_hh_l0, m.bias_ih_l0 + m.bias_hh_l0, emulate_bf16=False)
+    torch.testing.assert_close(h2, h[0], atol=1e-5, rtol=1e-5)
+    pk = LS.pack_lstm(m.weight_ih_l0, m.weight_hh_l0, m.bias_ih_l0 + m.bias_hh_l0)
+    assert pk.numel() == (32 // 16) * 2 * 3 * 64 * 16
+
+
+# ----------------------------------------------------------------- GPU kernels
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,m", [(0, 1), (1, 1), (2, 24), (2, 1440)])
+def test_gpu_es_fit(cuda, kind, m):
+    T = 3000 if m < 1440 else 10080
+    x = _seasonal(37, T, period=max(m, 24), seed=kind)
+    x[3, 500] = np.nan
+    fc0, sig0, best0, sse0 = SM.ref_es_fit(x, kind, 10, m, SM.default_grid(kind))
+    r = SM.es_fit(torch.from_numpy(x).to(cuda), T, kind, 10, m)
+    np.testing.assert_allclose(r.sse.cpu().numpy(), sse0, rtol=5e-3)
+    same = r.best.cpu().numpy() == best0
+    assert same.mean() > 0.9
+    np.testing.assert_allclose(r.forecast.cpu().numpy()[same], fc0[same], rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_gpu_band_decide(cuda):
+    rng = np.random.default_rng(5)
+    R, n, M = 64, 70, 4
+    cur = rng.normal(0, 1, (R, n)).astype(np.float32)
+    ctr = rng.normal(0, 0.2, (R, n)).astype(np.float32)
+    sig = rng.uniform(0.3, 1, R).astype(np.float32)
+    thr = np.array([2, 1, 3, 1.5], np.float32)
+    bound = np.array([1, 3, 2, 3], np.int32)
+    mlb = np.array([0, -10, -10, -0.5], np.float32)
+    t = lambda a: torch.from_numpy(a).to(cuda)
+    g = SM.band_decide(t(cur), t(ctr), t(sig), M, t(thr), t(bound), t(mlb))
+    c = SM.band_decide(*(torch.from_numpy(a) for a in (cur, ctr, sig)), M, *(torch.from_numpy(a) for a in
+                                                                           (thr, bound, mlb)))
+    for a, b in zip(g, c):
+        np.testing.assert_allclose(a.cpu().numpy(), b.numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nr,period", [(10080, 1440), (2016, 288), (1440, 60), (4096, 128)])
+def test_gpu_fft_seasonal(cuda, nr, period):
+    x = _seasonal(50, nr, period=period, seed=nr)
+    x[2, 10:20] = np.nan
+    g = FF.fft_seasonal(torch.from_numpy(x).to(cuda), return_power=True)
+    c = FF.fft_seasonal(torch.from_numpy(x), return_power=True)
+    np.testing.assert_array_equal(g.period_bin.cpu().numpy(), c.period_bin.numpy())
+    pg, pc = g.power.cpu().numpy(), c.power.numpy()
+    scale = pc.max(1, keepdims=True)
+    np.testing.assert_allclose(pg / scale, pc / scale, atol=2e-5)
+    np.testing.assert_allclose(g.strength.cpu().numpy(), c.strength.numpy(), rtol=1e-3, atol=1e-5)
+    per = torch.full((50,), period, dtype=torch.int32)
+    pp = FF.phase_profile(torch.from_numpy(x).to(cuda), nr, per.to(cuda), g.mean, period, g.slope)
+    pr = FF.phase_profile(torch.from_numpy(x), nr, per, c.mean, period, c.slope)
+    np.testing.assert_allclose(pp.cpu().numpy(), pr.numpy(), atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_gpu_lsq_prophet(cuda):
+    T, H, R = 10080, 50, 100
+    x = _seasonal(R, T, period=1440, seed=9)
+    ld = (T + 3) // 4 * 4
+    Y = np.full((R, ld), 0, np.float32)
+    Y[:, :T] = x
+    g = LQ.prophet_fit(torch.from_numpy(Y).to(cuda), T, H)
+    c = LQ.prophet_fit(torch.from_numpy(Y), T, H)
+    np.testing.assert_allclose(g.forecast.cpu().numpy(), c.forecast.numpy(), rtol=1e-3, atol=2e-3)
+    np.testing.assert_allclose(g.sigma.cpu().numpy(), c.sigma.numpy(), rtol=0.05)
+    Zg = LQ.lsq_project(torch.from_numpy(Y).to(cuda), T, LQ._XT_CACHE[(T, H, 60.0, str(torch.device(cuda)))])
+    Zc = LQ.lsq_project(torch.from_numpy(Y), T, LQ._XT_CACHE[(T, H, 60.0, "cpu")])
+    np.testing.assert_allclose(Zg[0].cpu().numpy(), Zc[0].numpy(), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_bivariate(cuda):
+    rng = np.random.default_rng(3)
+    P, T, n = 40, 2000, 30
+    a = rng.normal(5, 1, (P, T)).astype(np.float32)
+    b = (0.5 * a + rng.normal(0, 0.3, (P, T))).astype(np.float32)
+    ca = rng.normal(5, 2, (P, n)).astype(np.float32)
+    cb = rng.normal(2.5, 1, (P, n)).astype(np.float32)
+    t = lambda v: torch.from_numpy(v).to(cuda)
+    g = MI.bivariate(t(a), t(b), T, t(ca), t(cb), 3.0)
+    c = MI.bivariate(*(torch.from_numpy(v) for v in (a, b)), T, *(torch.from_numpy(v) for v in (ca, cb)), 3.0)
+    np.testing.assert_allclose(g[0].cpu().numpy(), c[0].numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(g[1].cpu().numpy(), c[1].numpy(), rtol=1e-3, atol=1e-3)
+    assert np.abs(g[3].cpu().numpy() - c[3].numpy()).sum() <= 1
+
+
+@pytest.mark.gpu
+def test_gpu_hpa_and_impact(cuda):
+    rng = np.random.default_rng(4)
+    S = 1000
+    tmpl = MI.HpaTemplate.from_aliases(["traffic", "cpu", "latency"])
+    up = rng.uniform(1, 2, (S, 3)).astype(np.float32)
+    lo = (up - rng.uniform(0.2, 1, (S, 3))).astype(np.float32)
+    cur = rng.uniform(0, 3, (S, 3)).astype(np.float32)
+    sg, sc_ = MI.HpaState.zeros(S, cuda), MI.HpaState.zeros(S)
+    for now in (100.0, 130.0, 500.0):
+        g = MI.hpa_score(*(torch.from_numpy(v).to(cuda) for v in (cur, up, lo)), tmpl, sg, now)
+        c = MI.hpa_score(*(torch.from_numpy(v) for v in (cur, up, lo)), tmpl, sc_, now)
+        np.testing.assert_array_equal(g[0].cpu().numpy(), c[0].numpy())
+        np.testing.assert_array_equal(g[1].cpu().numpy(), c[1].numpy())
+        cur = rng.uniform(0, 3, (S, 3)).astype(np.float32)
+    src = rng.integers(0, S, 5000)
+    dst = rng.integers(0, S, 5000)
+    gr = MI.CallGraph.from_edges(S, src, dst, rng.uniform(0.3, 1, 5000))
+    a = rng.uniform(0, 1, S).astype(np.float32)
+    for hops in (1, 2, 3):
+        ig = MI.downstream_impact(gr, torch.from_numpy(a).to(cuda), hops)
+        ic = MI.downstream_impact(gr, torch.from_numpy(a), hops)
+        np.testing.assert_allclose(ig.cpu().numpy(), ic.numpy(), rtol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,I", [(128, 1), (64, 4), (32, 15), (128, 0)])
+def test_gpu_lstm_matches_reference(cuda, H, I):
+    torch.manual_seed(H + I)
+    B, L = 130, 24
+    w_ih = torch.randn(4 * H, max(I, 1))[:, :I] * 0.3
+    w_hh = torch.randn(4 * H, H) * (1.0 / H ** 0.5)
+    b = torch.randn(4 * H) * 0.1
+    x = torch.randn(B, L, I)
+    h0 = torch.randn(B, H) * 0.1
+    c0 = torch.randn(B, H) * 0.1
+    pk = LS.pack_lstm(w_ih, w_hh, b)
+    hg, cg, seq = LS.lstm_forward(x.to(cuda).contiguous(), pk, H, h0.to(cuda), c0.to(cuda), return_seq=True)
+    hr, cr = LS.ref_lstm_forward(x, w_ih, w_hh, b, h0, c0, emulate_bf16=True)
+    torch.testing.assert_close(hg.cpu(), hr, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(cg.cpu(), cr, atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(seq[:, -1].float().cpu(), hr, atol=3e-2, rtol=3e-2)
