@@ -1,0 +1,408 @@
+"""The brain: the analysis engine the reference keeps in the external
+foremast-brain repo, rebuilt as a batched GPU engine (docs/BRAIN_SPEC.md).
+
+One ``run_once`` cycle (sequence diagram
+.gitbook/assets/foremastjudgementsequencediagram.png):
+
+1. lease-claim up to ``batch_size`` jobs this worker owns (``MAX_STUCK_IN_SECONDS``
+   takeover, foremast-brain/README.md:29);
+2. fetch historical / baseline / current series for every (job, metric)
+   (placeholders ``START_TIME``/``END_TIME`` filled with sliding windows for
+   continuous and HPA jobs);
+3. pack ALL rows of ALL claimed jobs into one [R, T] history tensor + [R, n]
+   current/baseline tensors (right-aligned to "now") on the device;
+4. pairwise canary tests (K4) -> lowered thresholds, the configured
+   ``ML_ALGORITHM`` (model zoo) -> per-point bands and anomaly flags;
+5. per job: fail-fast ``completed_unhealth`` with reason + anomaly map;
+   ``completed_health`` / ``completed_unknown`` once the end time is reached;
+   otherwise back to ``preprocess_completed`` (re-examined next cycle);
+   HPA jobs write an ``hpalogs`` entry and stay alive;
+6. exporter gauges; distributed: rank-0 view via all-gather of job summaries.
+"""
+from __future__ import annotations
+
+import html
+import json
+import logging
+import math
+import os
+import socket
+import time
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from datetime import datetime, timezone
+
+import numpy as np
+import torch
+
+from ..api import status as ST
+from ..api.jobs import parse_rfc3339, rfc3339
+from ..api.models import Document, HPALog, HPALogBody, HPALogDetail
+from ..api.urls import parse_config, prometheus_query_of, promql_metric_name
+from ..config import BrainConfig
+from ..models import zoo
+from ..ops import canary as C
+from ..ops import misc as MI
+from ..parallel import dist as D
+from . import native_rt
+from .exporter import BrainExporter
+from .sources import Series, SourceError, SourceRouter, substitute_window
+
+log = logging.getLogger("foremast.brain")
+
+MAX_T = 16384
+
+
+@dataclass
+class Row:
+    job: int
+    alias: str
+    base_metric: str
+    hist: np.ndarray
+    hist_t_last: float
+    cur: np.ndarray
+    cur_t: np.ndarray
+    base: np.ndarray
+    tags: str = ""
+
+
+@dataclass
+class Work:
+    doc: Document
+    rows: list[Row] = field(default_factory=list)
+    errors: list[str] = field(default_factory=list)
+    end_ts: float = 0.0
+    missing: list[str] = field(default_factory=list)
+    namespace: str = ""
+
+    @property
+    def hpa(self) -> bool:
+        return self.doc.strategy == "hpa"
+
+
+def _series_values(ss: list[Series]) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate pod series of a window (pods side by side, time order kept)."""
+    if not ss:
+        return np.zeros(0, np.float32), np.zeros(0)
+    return (np.concatenate([s.values for s in ss]).astype(np.float32), np.concatenate([s.times for s in ss]))
+
+
+def _app_level(ss: list[Series]) -> tuple[np.ndarray, float]:
+    """History is app-level; if several series come back, average them per timestamp."""
+    if not ss:
+        return np.zeros(0, np.float32), 0.0
+    if len(ss) == 1:
+        s = ss[0]
+        return s.values.astype(np.float32), float(s.times[-1]) if len(s.times) else 0.0
+    t = np.unique(np.concatenate([s.times for s in ss]))
+    acc = np.zeros(len(t))
+    cnt = np.zeros(len(t))
+    for s in ss:
+        idx = np.searchsorted(t, s.times)
+        ok = np.isfinite(s.values)
+        np.add.at(acc, idx[ok], s.values[ok])
+        np.add.at(cnt, idx[ok], 1)
+    v = np.where(cnt > 0, acc / np.maximum(cnt, 1), np.nan).astype(np.float32)
+    return v, float(t[-1])
+
+
+class Brain:
+    def __init__(self, store, cfg: BrainConfig | None = None, device="cpu", sources: SourceRouter | None = None,
+                 worker_id: str | None = None, batch_size: int = 512, exporter: BrainExporter | None = None,
+                 clock=time.time, step: float = 60.0, watch_minutes: float = 10.0, fetch_threads: int = 16,
+                 lstm_model=None):
+        self.store = store
+        self.cfg = cfg or BrainConfig()
+        self.device = torch.device(device)
+        self.sources = sources or SourceRouter()
+        self.worker = worker_id or f"{socket.gethostname()}-{os.getpid()}"
+        self.batch_size = batch_size
+        self.exporter = exporter
+        self.clock = clock
+        self.step = step
+        self.watch_s = watch_minutes * 60.0
+        self.fetch_threads = fetch_threads
+        self.lstm_model = lstm_model
+        self.hpa_state: dict[str, MI.HpaState] = {}
+        self.info = D.env_info() if D.is_dist() else D.DistInfo()
+        zoo.canonical(self.cfg.ml_algorithm)   # validate early
+
+    # ------------------------------------------------------------------ claim
+    def _owner(self, doc: Document) -> bool:
+        if self.info.world <= 1:
+            return True
+        return D.service_owner(doc.namespace, doc.app_name, self.info.world) == self.info.rank
+
+    # ------------------------------------------------------------------ fetch
+    def _windows(self, doc: Document, now: float) -> dict[str, tuple[float, float]]:
+        w = self.watch_s
+        if doc.strategy == "hpa":
+            return {"current": (now - 5 * self.step, now), "baseline": (now - 2 * w, now - w),
+                    "historical": (now - 7 * 86400.0, now)}
+        return {"current": (now - w, now), "baseline": (now - 2 * w, now - w),
+                "historical": (now - 7 * 86400.0, now - w)}
+
+    def _fetch_job(self, doc: Document, now: float) -> Work:
+        wk = Work(doc, namespace=doc.namespace)
+        try:
+            wk.end_ts = parse_rfc3339(doc.end_time).timestamp() if doc.end_time else now
+        except ValueError:
+            wk.end_ts = now
+        wins = self._windows(doc, now)
+        cats = {}
+        for cat, cfg_s, store_s in (("current", doc.current_config, doc.current_metric_store),
+                                    ("baseline", doc.baseline_config, doc.baseline_metric_store),
+                                    ("historical", doc.historical_config, doc.historical_metric_store)):
+            urls = parse_config(cfg_s)
+            stores = parse_config(store_s)
+            got = {}
+            for alias, url in urls.items():
+                u = substitute_window(url, *wins[cat])
+                try:
+                    got[alias] = self.sources.fetch(stores.get(alias, "prometheus"), u)
+                except (SourceError, OSError, ValueError) as e:
+                    wk.errors.append(f"{cat}/{alias}: {e}")
+                    got[alias] = []
+            cats[cat] = (urls, got)
+        cur_urls, cur = cats["current"]
+        _, base = cats["baseline"]
+        hist_urls, hist = cats["historical"]
+        aliases = list(cur_urls) if doc.strategy != "hpa" else list(hist_urls) or list(cur_urls)
+        for alias in aliases:
+            hv, ht = _app_level(hist.get(alias, []))
+            cv, ct = _series_values(cur.get(alias, []))
+            bv, _ = _series_values(base.get(alias, []))
+            url = cur_urls.get(alias) or hist_urls.get(alias, "")
+            q = prometheus_query_of(url).get("query", "") if "query_range?" in url else url
+            if len(hv) == 0 or not np.isfinite(cv).any():
+                wk.missing.append(alias)
+            # exported under the app-level name the dashboard charts (metrics.js:12-101)
+            base_metric = (promql_metric_name(q) or alias).replace("namespace_pod_", "namespace_app_pod_", 1)
+            if not wk.namespace:
+                wk.namespace = _label(q, "namespace")
+            wk.rows.append(Row(-1, alias, base_metric, hv, ht, cv, ct, bv))
+        return wk
+
+    # ------------------------------------------------------------------ score
+    def _pack(self, rows: list[Row]):
+        R = len(rows)
+        T = max([len(r.hist) for r in rows] + [2])
+        T = min(T, MAX_T)
+        ld = (T + 3) // 4 * 4
+        hist = native_rt.pack_right([r.hist for r in rows], T, ld)
+        n = max([len(r.cur) for r in rows] + [1])
+        nb = max([len(r.base) for r in rows] + [1])
+        cur = np.full((R, n), np.nan, np.float32)
+        base = np.full((R, nb), np.nan, np.float32)
+        hor = np.ones((R, n), np.int64)
+        for i, r in enumerate(rows):
+            cur[i, :len(r.cur)] = r.cur
+            base[i, :len(r.base)] = r.base
+            if len(r.cur_t) and r.hist_t_last:
+                hor[i, :len(r.cur_t)] = np.maximum(1, np.rint((r.cur_t - r.hist_t_last) / self.step)).astype(np.int64)
+        dev = self.device
+        t = lambda a: torch.from_numpy(a).to(dev)
+        return t(hist), T, t(cur), t(base), t(hor)
+
+    def score_rows(self, rows: list[Row]):
+        hist, T, cur, base, hor = self._pack(rows)
+        tables = zoo.make_tables([r.alias for r in rows], self.cfg, self.device)
+        R = len(rows)
+        diff = None
+        if any(len(r.base) for r in rows):
+            pcfg = C.PairwiseConfig(self.cfg.pairwise_algorithm, self.cfg.pairwise_threshold,
+                                    self.cfg.min_mann_white, self.cfg.min_wilcoxon, self.cfg.min_kruskal)
+            _, _, diff = C.pairwise_tests(cur, base, pcfg)
+        pairs = None
+        if zoo.canonical(self.cfg.ml_algorithm) == "bivariate_normal":
+            pairs = self._pairs(rows)
+        dec = zoo.decide(self.cfg.ml_algorithm, hist, T, cur, hor, R, tables, diff, lstm_model=self.lstm_model,
+                         pairs=pairs)
+        out = {k: getattr(dec, k).detach().cpu().numpy() for k in ("upper", "lower", "count", "score", "valid")}
+        out["flags"] = C.unpack_flags(dec.flags, cur.shape[1])
+        out["diff"] = None if diff is None else diff.cpu().numpy()
+        return out
+
+    @staticmethod
+    def _pairs(rows: list[Row]):
+        ia, ib, singles = [], [], []
+        by_job: dict[int, list[int]] = {}
+        for i, r in enumerate(rows):
+            by_job.setdefault(r.job, []).append(i)
+        for idx in by_job.values():
+            for k in range(0, len(idx) - 1, 2):
+                ia.append(idx[k])
+                ib.append(idx[k + 1])
+            if len(idx) % 2:
+                singles.append(idx[-1])
+        f = lambda v: torch.tensor(v, dtype=torch.int64)
+        return f(ia), f(ib), f(singles)
+
+    # ------------------------------------------------------------------ cycle
+    def run_once(self) -> dict:
+        t0 = time.perf_counter()
+        now = self.clock()
+        docs = self.store.claim(self.worker, self.batch_size, self.cfg.max_stuck_seconds, now=now, owner=self._owner)
+        if not docs:
+            return {"claimed": 0}
+        with ThreadPoolExecutor(max_workers=max(1, min(self.fetch_threads, len(docs)))) as ex:
+            works = list(ex.map(lambda d: self._fetch_job(d, now), docs))
+        rows: list[Row] = []
+        for j, wk in enumerate(works):
+            for r in wk.rows:
+                r.job = j
+                rows.append(r)
+        res = self.score_rows(rows) if rows else None
+        outcome = {}
+        summaries = []
+        offs = 0
+        for j, wk in enumerate(works):
+            k = len(wk.rows)
+            sl = slice(offs, offs + k)
+            offs += k
+            st = self._finish(wk, rows[sl], res, sl, now)
+            outcome[st] = outcome.get(st, 0) + 1
+            summaries.append((wk.doc.id, wk.doc.namespace, wk.doc.app_name, st))
+        if self.exporter is not None:
+            self.exporter.tick_seconds.observe(time.perf_counter() - t0)
+            self.exporter.windows.inc(len(rows))
+            for s, c in outcome.items():
+                self.exporter.jobs.labels(s).inc(c)
+        fleet = self._gather(summaries)
+        return {"claimed": len(docs), "rows": len(rows), "outcome": outcome, "fleet": len(fleet),
+                "seconds": time.perf_counter() - t0}
+
+    def _gather(self, summaries):
+        if not D.is_dist():
+            return summaries
+        out = [None] * torch.distributed.get_world_size()
+        torch.distributed.all_gather_object(out, summaries)
+        return [s for part in out for s in part]
+
+    def run_forever(self, stop=None, poll: float | None = None) -> None:  # pragma: no cover - service loop
+        poll = self.cfg.poll_interval if poll is None else poll
+        while stop is None or not stop.is_set():
+            try:
+                r = self.run_once()
+                if r.get("claimed", 0) == 0:
+                    time.sleep(poll)
+            except Exception:
+                log.exception("brain cycle failed")
+                time.sleep(poll)
+
+    # ------------------------------------------------------------------ verdicts
+    def _finish(self, wk: Work, rows: list[Row], res, sl: slice, now: float) -> str:
+        doc = wk.doc
+        anomalies = {}
+        reasons = []
+        ns, app = wk.namespace, doc.app_name
+        for i, r in enumerate(rows):
+            gi = sl.start + i
+            n = len(r.cur)
+            flags = res["flags"][gi][:n] if n else np.zeros(0, bool)
+            up = res["upper"][gi][:max(n, 1)]
+            lo = res["lower"][gi][:max(n, 1)]
+            if self.exporter is not None and n:
+                last = int(np.nonzero(np.isfinite(r.cur))[0][-1]) if np.isfinite(r.cur).any() else n - 1
+                anom_v = float(r.cur[last]) if flags[last] else float("nan")
+                self.exporter.set_bounds(r.base_metric, ns, app, float(up[last]), float(lo[last]), anom_v)
+            if flags.any():
+                idx = np.nonzero(flags)[0]
+                ts = [float(r.cur_t[k]) for k in idx]
+                vals = [float(r.cur[k]) for k in idx]
+                flat = []
+                for a, b in zip(ts, vals):
+                    flat += [a, b]
+                anomalies[r.alias] = {"tags": r.tags, "values": flat}
+                reasons.append({"name": r.alias, "ts": ts, "values": vals,
+                                "upper": float(up[idx[0]]), "lower": float(lo[idx[0]])})
+        if wk.hpa:
+            return self._finish_hpa(wk, rows, res, sl, now)
+        if anomalies:
+            reason = html.escape(json.dumps(reasons))
+            self.store.update(doc.id, status=ST.COMPLETED_UNHEALTH, reason=reason,
+                              anomaly_info=json.dumps(anomalies))
+            return ST.COMPLETED_UNHEALTH
+        if now >= wk.end_ts:
+            if wk.missing or not rows:
+                msg = "no current metric or missing historical data: " + ", ".join(wk.missing or ["all"])
+                self.store.update(doc.id, status=ST.COMPLETED_UNKNOWN, reason=msg)
+                return ST.COMPLETED_UNKNOWN
+            self.store.update(doc.id, status=ST.COMPLETED_HEALTH, reason="")
+            return ST.COMPLETED_HEALTH
+        self.store.update(doc.id, status=ST.PREPROCESS_COMPLETED)
+        return ST.PREPROCESS_COMPLETED
+
+    def _finish_hpa(self, wk: Work, rows: list[Row], res, sl: slice, now: float) -> str:
+        doc = wk.doc
+        cfgs = {k: {"priority": v.priority, "isIncrease": v.is_increase, "isAbsolute": v.is_absolute}
+                for k, v in doc.hpa_metrics.items()}
+        order = sorted(range(len(rows)), key=lambda i: cfgs.get(rows[i].alias, {}).get("priority", i + 1))
+        aliases = [rows[i].alias for i in order]
+        tmpl = MI.HpaTemplate.from_aliases(aliases, cfgs)
+        cur = np.full((1, len(order)), np.nan, np.float32)
+        up = np.full_like(cur, np.nan)
+        lo = np.full_like(cur, np.nan)
+        for c, i in enumerate(order):
+            r = rows[i]
+            ok = np.nonzero(np.isfinite(r.cur))[0]
+            if len(ok):
+                k = ok[-1]
+                cur[0, c] = r.cur[k]
+                up[0, c] = res["upper"][sl.start + i][k]
+                lo[0, c] = res["lower"][sl.start + i][k]
+        state = self.hpa_state.setdefault(doc.id, MI.HpaState.zeros(1))
+        sc, rs, _ = MI.hpa_score(torch.from_numpy(cur), torch.from_numpy(up), torch.from_numpy(lo), tmpl, state, now,
+                                 self.cfg.hpa_breath_up, self.cfg.hpa_breath_down, self.cfg.hpa_max_flips,
+                                 self.cfg.hpa_flip_window)
+        score = int(sc[0])
+        details = [HPALogDetail(a, _f(cur[0, c]), _f(up[0, c]), _f(lo[0, c])) for c, a in enumerate(aliases)]
+        self.store.add_hpalog(HPALog(job_id=doc.id, timestamp=float(now), created_at=rfc3339(
+            datetime.fromtimestamp(now, timezone.utc)), log=HPALogBody(score, MI.REASONS[int(rs[0])], details)))
+        if self.exporter is not None:
+            self.exporter.set_hpa_score(doc.namespace, doc.app_name, score)
+        self.store.update(doc.id, status=ST.PREPROCESS_COMPLETED)
+        return "hpa_scored"
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_tensors(self) -> tuple[dict[str, torch.Tensor], dict]:
+        ids = sorted(self.hpa_state)
+        t = {}
+        if ids:
+            t["hpa.last_dir"] = torch.cat([self.hpa_state[i].last_dir for i in ids])
+            t["hpa.last_time"] = torch.cat([self.hpa_state[i].last_time for i in ids])
+            t["hpa.flips"] = torch.cat([self.hpa_state[i].flips for i in ids])
+            t["hpa.flip_t0"] = torch.cat([self.hpa_state[i].flip_t0 for i in ids])
+        if self.lstm_model is not None:
+            t.update({"lstm." + k: v for k, v in self.lstm_model.state_dict().items()})
+        return t, {"hpa_jobs": ids, "worker": self.worker, "algorithm": self.cfg.ml_algorithm}
+
+    def save_checkpoint(self, dirpath: str):
+        from . import checkpoint
+        t, meta = self.state_tensors()
+        return checkpoint.save(dirpath, t, meta)
+
+    def load_checkpoint(self, dirpath: str) -> bool:
+        from . import checkpoint
+        got = checkpoint.load_latest(dirpath)
+        if got is None:
+            return False
+        t, meta = got
+        for i, jid in enumerate(meta.get("hpa_jobs", [])):
+            self.hpa_state[jid] = MI.HpaState(t["hpa.last_dir"][i:i + 1].clone(), t["hpa.last_time"][i:i + 1].clone(),
+                                              t["hpa.flips"][i:i + 1].clone(), t["hpa.flip_t0"][i:i + 1].clone())
+        lstm = {k[5:]: v for k, v in t.items() if k.startswith("lstm.")}
+        if lstm and self.lstm_model is not None:
+            self.lstm_model.load_state_dict(lstm)
+        return True
+
+
+def _label(q: str, name: str) -> str:
+    import re
+    m = re.search(name + r'\s*=\s*"([^"]*)"', q or "")
+    return m.group(1) if m else ""
+
+
+def _f(x) -> float:
+    v = float(x)
+    return v if math.isfinite(v) else 0.0

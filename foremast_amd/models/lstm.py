@@ -1,0 +1,137 @@
+"""LSTM forecaster for HPA / ClusterAutoScaler prediction (BASELINE config 4;
+docs/guides/design.md:81-85 "Deep Learning (LSTM)", README.md:58-59).
+
+Inference runs the hand-written bf16 MFMA LSTM kernel (``ops.lstm``) over the
+last ``window`` samples of every series (z-scored per row, plus daily phase
+features), then a linear head maps h_T to ``horizon`` future points.  Training
+(``fit``) uses torch autograd on an ``nn.LSTM`` with identical parameters —
+the reference trained Keras models offline too (foremast-brain/faq.md:10);
+the trained weights are what the HIP forward consumes.  Weights persist via
+``engine.checkpoint`` (safetensors).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..ops import lstm as LS
+
+
+class LSTMForecaster:
+    def __init__(self, hidden: int = 128, window: int = 240, horizon: int = 60, n_features: int = 3,
+                 seed: int = 0, device="cpu", period: float = 1440.0):
+        assert hidden in LS.SUPPORTED_H
+        self.H, self.L, self.horizon, self.I = hidden, window, horizon, n_features
+        self.period = period
+        self.device = torch.device(device)
+        g = torch.Generator().manual_seed(seed)
+        self.lstm = torch.nn.LSTM(n_features, hidden, batch_first=True)
+        self.head = torch.nn.Linear(hidden, horizon)
+        k = 1.0 / math.sqrt(hidden)
+        with torch.no_grad():
+            for p in list(self.lstm.parameters()) + list(self.head.parameters()):
+                p.copy_(torch.empty_like(p).uniform_(-k, k, generator=g))
+        self._packed = None
+
+    @classmethod
+    def default(cls, device="cpu") -> "LSTMForecaster":
+        return cls(device=device)
+
+    # ------------------------------------------------------------------ params
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        sd = {f"lstm.{k}": v.detach().cpu() for k, v in self.lstm.state_dict().items()}
+        sd.update({f"head.{k}": v.detach().cpu() for k, v in self.head.state_dict().items()})
+        return sd
+
+    def load_state_dict(self, sd: dict[str, torch.Tensor]) -> None:
+        self.lstm.load_state_dict({k[5:]: v for k, v in sd.items() if k.startswith("lstm.")})
+        self.head.load_state_dict({k[5:]: v for k, v in sd.items() if k.startswith("head.")})
+        self._packed = None
+
+    def packed(self) -> torch.Tensor:
+        if self._packed is None:
+            l = self.lstm
+            self._packed = LS.pack_lstm(l.weight_ih_l0, l.weight_hh_l0, l.bias_ih_l0 + l.bias_hh_l0).to(self.device)
+        return self._packed
+
+    # ------------------------------------------------------------------ features
+    def features(self, hist: torch.Tensor, T: int):
+        """[R, L, I] float32: z-scored value, sin/cos of the daily phase."""
+        L = min(self.L, T)
+        win = hist[:, T - L:T].float()
+        ok = torch.isfinite(win)
+        n = ok.sum(1).clamp(min=1)
+        mu = torch.where(ok, win, torch.zeros_like(win)).sum(1) / n
+        var = torch.where(ok, (win - mu[:, None]) ** 2, torch.zeros_like(win)).sum(1) / n
+        sd = var.sqrt().clamp(min=1e-6)
+        z = torch.where(ok, (win - mu[:, None]) / sd[:, None], torch.zeros_like(win))
+        t = torch.arange(T - L, T, device=hist.device, dtype=torch.float32)
+        ph = 2 * math.pi * t / self.period
+        feats = [z, torch.sin(ph).expand_as(z), torch.cos(ph).expand_as(z)][: self.I]
+        return torch.stack(feats, -1).contiguous(), mu, sd
+
+    @torch.no_grad()
+    def forecast(self, hist: torch.Tensor, T: int, H: int):
+        """-> (forecast [R, H] in data units, sigma [R]) with sigma = window std."""
+        x, mu, sd = self.features(hist, T)
+        if x.is_cuda:
+            hT, _, _ = LS.lstm_forward(x, self.packed(), self.H)
+        else:
+            with torch.no_grad():
+                _, (h, _) = self.lstm(x)
+                hT = h[0]
+        W = self.head.weight.to(hT.device)
+        b = self.head.bias.to(hT.device)
+        z = hT @ W.T + b                                    # [R, horizon]
+        if H > self.horizon:
+            z = torch.cat([z, z[:, -1:].expand(-1, H - self.horizon)], 1)
+        fc = mu[:, None] + sd[:, None] * z[:, :H]
+        return fc.contiguous(), sd.contiguous()
+
+    # ------------------------------------------------------------------ training
+    def fit(self, hist: torch.Tensor, T: int, epochs: int = 2, batch: int = 256, lr: float = 1e-3,
+            max_windows: int = 4096, seed: int = 0) -> list[float]:
+        """Train on sliding windows of the history (next-``horizon`` targets)."""
+        dev = hist.device
+        lstm = self.lstm.to(dev)
+        head = self.head.to(dev)
+        rng = np.random.default_rng(seed)
+        L, Hz = min(self.L, T - self.horizon - 1), self.horizon
+        R = hist.shape[0]
+        ends = rng.integers(L, T - Hz, size=max_windows)
+        rows = rng.integers(0, R, size=max_windows)
+        opt = torch.optim.Adam(list(lstm.parameters()) + list(head.parameters()), lr=lr)
+        losses = []
+        for _ in range(epochs):
+            for s in range(0, max_windows, batch):
+                e, r = ends[s:s + batch], rows[s:s + batch]
+                idx = torch.as_tensor(e[:, None] + np.arange(-L, Hz)[None, :], device=dev)
+                seg = hist[torch.as_tensor(r, device=dev)[:, None], idx].float()
+                seg = torch.nan_to_num(seg, nan=0.0)
+                win, tgt = seg[:, :L], seg[:, L:]
+                mu, sd = win.mean(1, keepdim=True), win.std(1, keepdim=True).clamp(min=1e-6)
+                t = torch.as_tensor(e[:, None] + np.arange(-L, 0)[None, :], device=dev, dtype=torch.float32)
+                ph = 2 * math.pi * t / self.period
+                x = torch.stack([(win - mu) / sd, torch.sin(ph), torch.cos(ph)][: self.I], -1)
+                _, (h, _) = lstm(x)
+                pred = head(h[0])
+                loss = torch.nn.functional.mse_loss(pred, (tgt - mu) / sd)
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+                losses.append(float(loss.item()))
+        self.lstm, self.head = lstm.cpu(), head.cpu()
+        self._packed = None
+        return losses
+
+
+def smoke_forward(device) -> None:
+    """Tiny LSTM forecast through the HIP kernel (used by __graft_entry__.smoke)."""
+    m = LSTMForecaster(hidden=64, window=48, horizon=8, device=device)
+    hist = torch.randn(70, 96, device=device).cumsum(1).contiguous()
+    fc, sd = m.forecast(hist, 96, 8)
+    torch.cuda.synchronize(device)
+    assert torch.isfinite(fc).all()
+    print("smoke: lstm forecast", tuple(fc.shape))

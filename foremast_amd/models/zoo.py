@@ -1,0 +1,212 @@
+"""Model zoo: every ``ML_ALGORITHM`` of the brain as one batched call over a
+packed shard ``hist [R, ld]`` (rows = jobs x metrics) that returns per-point
+decisions for the current window.
+
+Algorithms (docs/guides/design.md:53-85; default moving_average_all,
+deploy/foremast/3_brain/foremast-brain.yaml:24-25):
+
+==============================  ======================================  ==================
+name                            model                                   kernels
+==============================  ======================================  ==================
+moving_average_all              mean/std over the whole history         K1+K7 fused
+moving_average                  mean/std over the last ``window`` pts   K1+K7 fused (view)
+exponential_smoothing           SES, alpha grid                         K2 + band decide
+double_exponential_smoothing    Holt, (alpha, beta) grid                K2 + band decide
+holt_winters                    additive HW, period from the FFT        K3 + K2 + band
+prophet                         trend+hinges+daily/weekly Fourier LSQ   K10 (f32 MFMA)
+lstm                            LSTM forecaster (bf16 MFMA)             K6 + band decide
+bivariate_normal                Mahalanobis over metric pairs           K5
+==============================  ======================================  ==================
+
+Thresholds are in sigma units per metric (``BrainConfig.rule_for``), lowered
+by ``pairwise_threshold_factor`` on rows whose canary distribution differs.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..ops import canary as C
+from ..ops import fft as FF
+from ..ops import lsq as LQ
+from ..ops import smoothing as SM
+
+ALGORITHMS = ("moving_average_all", "moving_average", "exponential_smoothing", "double_exponential_smoothing",
+              "holt_winters", "prophet", "lstm", "bivariate_normal")
+
+ALIASES = {"moving_average_all": "moving_average_all", "ma_all": "moving_average_all",
+           "moving_average": "moving_average", "ma": "moving_average",
+           "exponential_smoothing": "exponential_smoothing", "ses": "exponential_smoothing",
+           "double_exponential_smoothing": "double_exponential_smoothing", "holt": "double_exponential_smoothing",
+           "holt_winters": "holt_winters", "hw": "holt_winters", "triple_exponential_smoothing": "holt_winters",
+           "prophet": "prophet", "lstm": "lstm", "bivariate_normal": "bivariate_normal", "bivariate": "bivariate_normal"}
+
+
+def canonical(name: str) -> str:
+    k = (name or "moving_average_all").strip().lower()
+    if k not in ALIASES:
+        raise ValueError(f"unknown ML_ALGORITHM {name!r}; supported: {', '.join(ALGORITHMS)}")
+    return ALIASES[k]
+
+
+@dataclass
+class RowDecision:
+    upper: torch.Tensor      # [R, n] per-point upper bound
+    lower: torch.Tensor      # [R, n]
+    flags: torch.Tensor      # [R, NW] int64 bit-packed
+    count: torch.Tensor      # [R] int32
+    score: torch.Tensor      # [R] f32
+    valid: torch.Tensor      # [R] int32 bit0 history ok, bit1 current present
+    center: torch.Tensor | None = None
+
+
+@dataclass
+class Tables:
+    thr: torch.Tensor
+    bound: torch.Tensor
+    minlb: torch.Tensor
+    pair_factor: float
+    min_hist: int
+
+
+def _expand_stats(dec: C.DecideResult, n: int) -> RowDecision:
+    up = dec.stats[:, 2:3].expand(-1, n)
+    lo = dec.stats[:, 3:4].expand(-1, n)
+    return RowDecision(up, lo, dec.flags, dec.count, dec.score, dec.valid, dec.stats[:, 0:1].expand(-1, n))
+
+
+def _valid(hist: torch.Tensor, T: int, cur: torch.Tensor, min_hist: int) -> torch.Tensor:
+    nh = torch.isfinite(hist[:, :T]).sum(1)
+    has_cur = torch.isfinite(cur).any(1)
+    return ((nh >= max(min_hist, 1)).to(torch.int32) | (has_cur.to(torch.int32) << 1))
+
+
+def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizon: torch.Tensor, M: int,
+           tables: Tables, diff: torch.Tensor | None = None, window: int = 60, period: int | None = None,
+           lstm_model=None, pairs=None) -> RowDecision:
+    """Score current points of every row.
+
+    ``horizon`` [R, n] int64: steps past the end of the history of each current
+    point (1 = the next sample), used by forecasting models."""
+    algo = canonical(algorithm)
+    n = cur.shape[1]
+    if algo == "moving_average_all":
+        dec = C.stats_decide(hist, cur, T, M, tables.thr, tables.bound, tables.minlb, diff, tables.pair_factor,
+                             tables.min_hist)
+        return _expand_stats(dec, n)
+    if algo == "moving_average":
+        w = min(T, max(4, (window + 3) // 4 * 4))
+        start = (T - w) // 4 * 4        # keep the view 16-B aligned for the vector loads
+        view = hist[:, start:T]
+        dec = C.stats_decide(view, cur, T - start, M, tables.thr, tables.bound, tables.minlb, diff,
+                             tables.pair_factor, tables.min_hist)
+        return _expand_stats(dec, n)
+    if algo == "bivariate_normal":
+        return _bivariate(hist, T, cur, M, tables, pairs)
+    H = int(horizon.max().item()) if horizon.numel() else 1
+    H = max(H, 1)
+    if algo in ("exponential_smoothing", "double_exponential_smoothing", "holt_winters"):
+        kind = {"exponential_smoothing": 0, "double_exponential_smoothing": 1, "holt_winters": 2}[algo]
+        m = 1
+        if kind == 2:
+            m = period or _detect_period(hist, T)
+            if 2 * m > T:
+                kind, m = 1, 1
+        fit = SM.es_fit(hist, T, kind, H, m)
+        fc, sigma = fit.forecast, fit.sigma
+    elif algo == "prophet":
+        fit = LQ.prophet_fit(hist, T, H)
+        fc, sigma = fit.forecast, fit.sigma
+    elif algo == "lstm":
+        if lstm_model is None:
+            from .lstm import LSTMForecaster
+            lstm_model = LSTMForecaster.default(device=hist.device)
+        fc, sigma = lstm_model.forecast(hist, T, H)
+    else:  # pragma: no cover
+        raise AssertionError(algo)
+    idx = (horizon.clamp(1, H) - 1).to(fc.device)
+    center = torch.gather(fc, 1, idx).contiguous()
+    up, lo, flags, cnt, sc = SM.band_decide(cur, center, sigma.contiguous(), M, tables.thr, tables.bound,
+                                            tables.minlb, diff, tables.pair_factor)
+    valid = _valid(hist, T, cur, tables.min_hist)
+    has = (valid & 1).bool()
+    cnt = torch.where(has, cnt, torch.zeros_like(cnt))
+    return RowDecision(up, lo, flags, cnt, sc, valid, center)
+
+
+def _detect_period(hist: torch.Tensor, T: int, default: int = 1440) -> int:
+    """Fleet period for Holt-Winters: the median of per-row FFT peaks with
+    strong seasonality, else ``default`` (daily at 60 s)."""
+    nr = T - (T % 2)
+    while nr > 64 and not FF.supported_length(nr):
+        nr -= 2
+    if nr <= 64:
+        return min(default, max(2, T // 2))
+    off = T - nr
+    off -= off % 2
+    view = hist[:, off:off + nr] if off % 4 == 0 else hist[:, :nr]
+    s = FF.fft_seasonal(view.contiguous() if off % 2 else view, nr, min_period=12, max_period=nr / 2)
+    strong = s.strength > 0.1
+    if int(strong.sum()) == 0:
+        return min(default, T // 2)
+    p = int(torch.median(s.period[strong]).item())
+    return max(2, min(p, T // 2))
+
+
+def _bivariate(hist, T, cur, M, tables, pairs=None) -> RowDecision:
+    """Metric pairs scored jointly; both rows of a pair get the pair's decision
+    (bounds reported in Mahalanobis units: upper = threshold, lower = 0).
+    ``pairs`` = (ia, ib, singles) row-index tensors; default: (0,1), (2,3), ...
+    of each service with M metrics, an odd last metric -> moving_average_all."""
+    from ..ops import misc as MI
+    R, n = cur.shape
+    device = hist.device
+    if pairs is None:
+        S = R // M
+        base = torch.arange(S, device=device) * M
+        ia = torch.cat([base + a for a in range(0, M - 1, 2)]) if M > 1 else base[:0]
+        ib = ia + 1
+        singles = base + (M - 1) if M % 2 == 1 else base[:0]
+    else:
+        ia, ib, singles = (p.to(device) for p in pairs)
+    flags_all = torch.zeros((R, max(1, (n + 63) // 64)), dtype=torch.int64, device=device)
+    count_all = torch.zeros((R,), dtype=torch.int32, device=device)
+    score_all = torch.zeros((R,), dtype=torch.float32, device=device)
+    up_all = torch.full((R, n), float("nan"), device=device)
+    lo_all = torch.full((R, n), float("nan"), device=device)
+    if ia.numel():
+        ha, hb = hist[ia].contiguous(), hist[ib].contiguous()
+        ca, cb = cur[ia].contiguous(), cur[ib].contiguous()
+        thr = float(tables.thr[0].item()) if tables.thr.numel() == 1 else float(tables.thr.max().item())
+        params, dist, flags, cnt = MI.bivariate(ha, hb, T, ca, cb, thr)
+        sc = torch.nan_to_num(dist, nan=0.0).amax(1)
+        for i in (ia, ib):
+            flags_all[i] = flags
+            count_all[i] = cnt
+            score_all[i] = sc
+            up_all[i] = thr
+            lo_all[i] = 0.0
+    if singles.numel():
+        sub = C.stats_decide(hist[singles].contiguous(), cur[singles].contiguous(), T, 1,
+                             tables.thr[:1].contiguous(), tables.bound[:1].contiguous(), tables.minlb[:1].contiguous(),
+                             None, tables.pair_factor, tables.min_hist)
+        flags_all[singles], count_all[singles], score_all[singles] = sub.flags, sub.count, sub.score
+        up_all[singles] = sub.stats[:, 2:3].expand(-1, n)
+        lo_all[singles] = sub.stats[:, 3:4].expand(-1, n)
+    valid = _valid(hist, T, cur, tables.min_hist)
+    return RowDecision(up_all, lo_all, flags_all, count_all, score_all, valid)
+
+
+def make_tables(aliases_per_row: list[str], cfg, device) -> Tables:
+    """Per-row metric tables when rows of one batch carry different aliases:
+    M = 1 logical metric per row (row r -> table entry r)."""
+    rules = [cfg.rule_for(a) for a in aliases_per_row]
+    return Tables(torch.tensor([r.threshold for r in rules], dtype=torch.float32, device=device),
+                  torch.tensor([r.bound for r in rules], dtype=torch.int32, device=device),
+                  torch.tensor([r.min_lower_bound for r in rules], dtype=torch.float32, device=device),
+                  cfg.pairwise_threshold_factor, cfg.min_historical_points)
+
+
+_ = np

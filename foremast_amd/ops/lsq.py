@@ -65,29 +65,40 @@ def lsq_project(Y: torch.Tensor, T: int, XT: torch.Tensor):
 _XT_CACHE: dict = {}
 
 
-def prophet_fit(Y: torch.Tensor, T: int, H: int, step_s: float = 60.0, ridge: float = 1e-6) -> LsqFit:
+@lru_cache(maxsize=8)
+def _basis(T: int, H: int, step_s: float):
+    """Orthonormal basis of the history design (thin SVD X_h = U S V^T, rank-
+    truncated) so the kernel projects onto orthonormal columns: G = I, no
+    normal-equation conditioning blow-up of the fp32 MFMA sums.  Returns
+    (U^T padded [F, ld] f32, forecast map X_f V S^-1 [H, F], coef map V S^-1 [F, F])."""
     X = design_matrix(T, H, step_s)
     Xh, Xf = X[:T], X[T:]
-    G = Xh.T @ Xh
-    G = G + ridge * np.trace(G) / F * np.eye(F)
-    Ginv = np.linalg.inv(G)
+    U, S, Vt = np.linalg.svd(Xh, full_matrices=False)
+    keep = S > S[0] * 1e-10
+    Sinv = np.where(keep, 1.0 / np.where(keep, S, 1.0), 0.0)
+    U = U * keep[None, :]
+    ld = (T + 3) // 4 * 4
+    ut = np.zeros((F, ld), np.float32)
+    ut[:, :T] = U.T
+    vs = Vt.T * Sinv[None, :]
+    return ut, Xf @ vs, vs, int(keep.sum())
+
+
+def prophet_fit(Y: torch.Tensor, T: int, H: int, step_s: float = 60.0) -> LsqFit:
+    """Least-squares fit of the shared design to every row; residual sigma
+    from SSE = |y - c|^2 - |U^T (y - c)|^2 (orthonormal U)."""
+    ut, fmap, vs, rank = _basis(T, H, step_s)
     d = Y.device
     key = (T, H, step_s, str(d))
     if key not in _XT_CACHE:
-        ld = (T + 3) // 4 * 4
-        xt = np.zeros((F, ld), np.float32)
-        xt[:, :T] = Xh.T
-        _XT_CACHE[key] = torch.from_numpy(xt).to(d)
+        _XT_CACHE[key] = torch.from_numpy(ut).to(d)
     XT = _XT_CACHE[key]
     Z, yy, sh, nv = lsq_project(Y, T, XT)
     Zd = Z.to(torch.float64)
-    Gi = torch.from_numpy(Ginv).to(d)
-    Gd = torch.from_numpy(G).to(d)
-    beta = Zd @ Gi
-    sse = yy.to(torch.float64) - 2 * (beta * Zd).sum(1) + ((beta @ Gd) * beta).sum(1)
-    sse = sse.clamp(min=0)
+    sse = (yy.to(torch.float64) - (Zd * Zd).sum(1)).clamp(min=0)
+    fc = Zd @ torch.from_numpy(fmap.T.copy()).to(d) + sh.to(torch.float64)[:, None]
+    beta = Zd @ torch.from_numpy(vs.T.copy()).to(d)
     beta[:, 0] += sh.to(torch.float64)
-    fc = beta @ torch.from_numpy(Xf.T.copy()).to(d)
-    dof = (nv.to(torch.float64) - F).clamp(min=1)
+    dof = (nv.to(torch.float64) - rank).clamp(min=1)
     sigma = torch.sqrt(sse / dof)
     return LsqFit(beta.to(torch.float32), fc.to(torch.float32), sigma.to(torch.float32), sse.to(torch.float32))

@@ -123,7 +123,7 @@ def ref_es_fit(x: np.ndarray, kind: int, H: int, m: int, grid: np.ndarray):
     nb = n[pid]
     sig = np.sqrt(sse[np.arange(R), best] / np.maximum(nb - 1, 1)).astype(np.float32)
     h = np.arange(1, H + 1)[None, :]
-    fc = lvl[pid][:, None] + (h * tr[pid][:, None] if kind >= 1 else 0)
+    fc = lvl[pid][:, None] + (h * tr[pid][:, None] if kind >= 1 else np.zeros((1, H), np.float32))
     if kind == 2:
         tph = T % m
         idx = (tph + h - 1) % m

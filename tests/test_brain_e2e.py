@@ -1,0 +1,151 @@
+"""End-to-end: barrelman-style request -> REST service -> brain (batched
+scoring, synthetic Prometheus) -> status/anomaly/hpalogs back through REST."""
+import html
+import json
+
+import numpy as np
+import pytest
+
+from foremast_amd.api import crd
+from foremast_amd.config import BrainConfig
+from foremast_amd.controller.analyst import AnalystClient
+from foremast_amd.engine.brain import Brain
+from foremast_amd.engine.exporter import BrainExporter
+from foremast_amd.engine.sources import SourceRouter
+from foremast_amd.service.app import create_app
+from foremast_amd.service.store import MemoryStore
+
+T0 = 1_760_000_000.0
+
+
+class Clock:
+    def __init__(self, t=T0):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+def _metrics():
+    return crd.Metrics("prometheus", "http://prom/api/v1/", [
+        crd.Monitoring("http_server_requests_errors_5xx", "counter", "error5xx"),
+        crd.Monitoring("http_server_requests_latency", "gauge", "latency"),
+        crd.Monitoring("cpu_usage_seconds_total", "gauge", "cpu"),
+    ])
+
+
+def _setup(faults=None, algorithm="moving_average_all", device="cpu"):
+    clock = Clock()
+    store = MemoryStore()
+    app = create_app(store)
+    client = AnalystClient.for_app(app, clock=clock)
+    cfg = BrainConfig()
+    cfg.ml_algorithm = algorithm
+    exp = BrainExporter()
+    brain = Brain(store, cfg, device=device, sources=SourceRouter.synthetic_only(faults=faults or {}), clock=clock,
+                  exporter=exp, worker_id="w0")
+    return clock, store, client, brain, exp
+
+
+PODS = [["demo-7687b9f4d7-aaaa1", "demo-7687b9f4d7-aaaa2"], ["demo-5db89899b5-bbbb1", "demo-5db89899b5-bbbb2"]]
+
+
+def test_canary_with_injected_fault_goes_unhealthy():
+    clock, store, client, brain, exp = _setup(faults={"7687b9f4d7-aaaa1": 6.0})
+    jid = client.start_analyzing("default", "demo", PODS, _metrics(), 10, "canary")
+    r = brain.run_once()
+    assert r["claimed"] == 1 and r["rows"] == 3
+    st = client.get_status(jid)
+    assert st.status == crd.PHASE_UNHEALTHY
+    assert "error5xx" in st.anomaly or "latency" in st.anomaly or "cpu" in st.anomaly
+    name = next(iter(st.anomaly))
+    vals = st.anomaly[name]["values"]
+    assert len(vals) % 2 == 0 and len(vals) >= 2
+    # reason: HTML-escaped JSON with "name"/"ts" the trigger's regexes parse (trigger.go:295-312)
+    import re
+    assert re.search(r'&quot;name&quot;\s*:\s*&quot;([\w\.]*)', st.reason)
+    assert re.search(r'&quot;ts&quot;\s*:\s*\[(\d*).\d', st.reason)
+    parsed = json.loads(html.unescape(st.reason))
+    assert parsed[0]["name"] in st.anomaly
+    # exporter series names of the reference dashboard
+    assert exp.sample("foremastbrain:namespace_app_pod_http_server_requests_errors_5xx_upper", "default",
+                      "demo") is not None
+
+
+def test_healthy_rolling_update_completes_at_end_time():
+    clock, store, client, brain, exp = _setup()
+    jid = client.start_analyzing("default", "demo", PODS[:1], _metrics(), 10, "rollingUpdate")
+    brain.run_once()
+    st = client.get_status(jid)
+    assert st.status == crd.PHASE_RUNNING, st.reason      # healthy so far, end time not reached
+    clock.t += 11 * 60
+    brain.run_once()
+    assert client.get_status(jid).status == crd.PHASE_HEALTHY
+
+
+def test_missing_data_is_unknown():
+    clock, store, client, brain, exp = _setup()
+    m = _metrics()
+    m.monitoring = [crd.Monitoring("nope", "gauge", "error5xx")]
+    jid = client.start_analyzing("default", "demo", PODS[:1], m, 10, "rollingUpdate")
+    # break the current query so no samples come back
+    d = store.get(jid)
+    d.current_config = d.current_config.replace("start=", "start=9").replace("end=", "end=0")
+    store.put(d)
+    clock.t += 11 * 60
+    brain.run_once()
+    # completed_unknown -> service "abort" (converter.go:20-21) -> barrelman Abort
+    assert store.get(jid).status == "completed_unknown"
+    assert client.get_status(jid).status == crd.PHASE_ABORT
+
+
+def test_hpa_job_writes_logs_and_score():
+    clock, store, client, brain, exp = _setup()
+    jid = client.start_analyzing("default", "demo", None, _metrics(), 10, "hpa", ["cpu", "latency"])
+    assert jid == "demo:default:hpa"
+    for k in range(3):
+        r = brain.run_once()
+        assert r["outcome"] == {"hpa_scored": 1}
+        clock.t += 30
+    st = client.get_status(jid)
+    assert st.status == crd.PHASE_RUNNING and len(st.hpa_logs) == 3
+    e = st.hpa_logs[0]
+    assert 0 <= e.hpa_log.hpa_score <= 100 and e.hpa_log.reason.startswith("hpa is")
+    assert [d.metric_alias for d in e.hpa_log.details] == ["cpu", "latency"]
+    assert exp.sample("namespace_app_pod_hpa_score", "default", "demo") is not None
+
+
+@pytest.mark.parametrize("algo", ["moving_average", "exponential_smoothing", "double_exponential_smoothing",
+                                  "holt_winters", "prophet", "lstm", "bivariate_normal"])
+def test_every_algorithm_runs_end_to_end(algo):
+    clock, store, client, brain, exp = _setup(faults={"7687b9f4d7-aaaa1": 8.0}, algorithm=algo)
+    jid = client.start_analyzing("default", "demo", PODS, _metrics(), 10, "canary")
+    brain.run_once()
+    assert client.get_status(jid).status in (crd.PHASE_UNHEALTHY, crd.PHASE_RUNNING)
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    clock, store, client, brain, exp = _setup()
+    client.start_analyzing("default", "demo", None, _metrics(), 10, "hpa", ["cpu"])
+    brain.run_once()
+    p = brain.save_checkpoint(str(tmp_path))
+    assert p.exists()
+    b2 = Brain(store, BrainConfig(), sources=brain.sources, clock=clock)
+    assert b2.load_checkpoint(str(tmp_path))
+    assert set(b2.hpa_state) == set(brain.hpa_state)
+    np.testing.assert_array_equal(b2.hpa_state["demo:default:hpa"].last_time.numpy(),
+                                  brain.hpa_state["demo:default:hpa"].last_time.numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["moving_average_all", "moving_average", "exponential_smoothing",
+                                  "double_exponential_smoothing", "holt_winters", "prophet", "lstm",
+                                  "bivariate_normal"])
+def test_gpu_brain_every_algorithm(cuda, algo):
+    clock, store, client, brain, exp = _setup(faults={"7687b9f4d7-aaaa1": 8.0}, algorithm=algo, device=cuda)
+    jid = client.start_analyzing("default", "demo", PODS, _metrics(), 10, "canary")
+    brain.run_once()
+    st = client.get_status(jid)
+    assert st.status in (crd.PHASE_UNHEALTHY, crd.PHASE_RUNNING)
+    if algo in ("moving_average_all", "moving_average", "prophet"):
+        assert st.status == crd.PHASE_UNHEALTHY
