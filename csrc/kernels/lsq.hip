@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void lsq_project_kernel(const float* __restric
 #pragma unroll
       for (int q = 0; q < 32; ++q) {
         const int t = tb + q;
-        yv[q] = (live && t < T) ? yr[t] : 0.f;
+        yv[q] = (live && t < T) ? yr[t] : NAN;   // past the end = missing (not a zero sample)
         xv[q] = t < T ? xr[t] : 0.f;
       }
     }
