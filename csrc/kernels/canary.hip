@@ -466,6 +466,156 @@ FM_API int fm_stats_decide(const float* hist, int64_t ld_h, int T, const float* 
 }
 
 // ---------------------------------------------------------------------------
+// Split form of the same computation for the two-stream tick: hist_stats is
+// the HBM-bound pass (mean, std, count per row) and runs concurrently with the
+// compute-bound pairwise kernel on another stream; window_decide (one wave per
+// row, reads only the small current window) applies the diff-dependent
+// thresholds once both are done.
+// ---------------------------------------------------------------------------
+template <int NV>
+__global__ __launch_bounds__(256) void hist_stats_kernel(const float* __restrict__ hist, int64_t ld_h, int T,
+                                                         int64_t R, float* __restrict__ out /*[R,3]*/) {
+  __shared__ double red[4];
+  __shared__ int redi[4];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* h = hist + row * ld_h;
+  const int nq = (T + 3) >> 2;
+  float4 q[NV];
+  double s = 0.0;
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int qi = tid + j * 256;
+    float4 x = make_float4(NAN, NAN, NAN, NAN);
+    if (qi < nq) {
+      typedef float nt4 __attribute__((ext_vector_type(4)));
+      const nt4 v = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(h) + qi);   // streamed once
+      x = make_float4(v.x, v.y, v.z, v.w);
+      const int e0 = qi * 4;
+      if (e0 + 1 >= T) x.y = NAN;
+      if (e0 + 2 >= T) x.z = NAN;
+      if (e0 + 3 >= T) x.w = NAN;
+    }
+    q[j] = x;
+    float ls = 0.f;
+    if (isfinite(x.x)) { ls += x.x; ++cnt; }
+    if (isfinite(x.y)) { ls += x.y; ++cnt; }
+    if (isfinite(x.z)) { ls += x.z; ++cnt; }
+    if (isfinite(x.w)) { ls += x.w; ++cnt; }
+    s += ls;
+  }
+  const double tot = block_sum<256>(s, red);
+  const int n = block_sum<256>(cnt, redi);
+  const float mf = n > 0 ? (float)(tot / n) : 0.f;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float4 x = q[j];
+    if (isfinite(x.x)) { float d = x.x - mf; ss += d * d; }
+    if (isfinite(x.y)) { float d = x.y - mf; ss += d * d; }
+    if (isfinite(x.z)) { float d = x.z - mf; ss += d * d; }
+    if (isfinite(x.w)) { float d = x.w - mf; ss += d * d; }
+  }
+  const double sst = block_sum<256>((double)ss, red);
+  if (tid == 0) {
+    out[row * 3 + 0] = mf;
+    out[row * 3 + 1] = n > 0 ? (float)sqrt(sst / n) : 0.f;
+    out[row * 3 + 2] = (float)n;
+  }
+}
+
+FM_API int fm_hist_stats(const float* hist, int64_t ld_h, int T, int64_t R, float* out, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
+  const int nq = (T + 3) / 4;
+  const dim3 grid((unsigned)R), block(256);
+#define FM_HS(NVV) hipLaunchKernelGGL(hist_stats_kernel<NVV>, grid, block, 0, stream, hist, ld_h, T, R, out)
+  if (nq <= 256 * 2) FM_HS(2);
+  else if (nq <= 256 * 4) FM_HS(4);
+  else if (nq <= 256 * 8) FM_HS(8);
+  else if (nq <= 256 * 10) FM_HS(10);
+  else if (nq <= 256 * 12) FM_HS(12);
+  else if (nq <= 256 * 16) FM_HS(16);
+  else return (int)hipErrorInvalidValue;
+#undef FM_HS
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void window_decide_kernel(
+    const float* __restrict__ hs, const float* __restrict__ cur, int64_t ld_c, int n_cur, int64_t R, int M,
+    const float* __restrict__ thr, const int* __restrict__ bound, const float* __restrict__ minlb, float pair_factor,
+    const int8_t* __restrict__ diff, int min_hist, float* __restrict__ out_stats,
+    unsigned long long* __restrict__ out_flags, int NW, int* __restrict__ out_count, float* __restrict__ out_score,
+    int* __restrict__ out_valid) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
+  if (row >= R) return;
+  const int lane = lane_id();
+  const float mf = hs[row * 3 + 0], sd = hs[row * 3 + 1];
+  const int n = (int)hs[row * 3 + 2];
+  const int m = (int)(row % M);
+  float th = thr[m];
+  if (diff != nullptr && diff[row]) th *= pair_factor;
+  const int bd = bound[m];
+  const float up = mf + th * sd;
+  float lo = mf - th * sd;
+  if (lo < minlb[m]) lo = minlb[m];
+  const bool has_hist = n >= min_hist && n > 0;
+  const float inv = sd > 0.f ? 1.0f / sd : 0.f;
+  const float* cr = cur + row * ld_c;
+  int acnt = 0, ccnt = 0;
+  float best = 0.f;
+  for (int i0 = 0; i0 < n_cur; i0 += 64) {
+    const int i = i0 + lane;
+    bool f = false;
+    if (i < n_cur) {
+      const float x = cr[i];
+      if (isfinite(x)) {
+        ++ccnt;
+        if (has_hist) {
+          const bool hi = (bd & 1) && x > up;
+          const bool lw = (bd & 2) && x < lo;
+          f = hi || lw;
+          if (f) {
+            ++acnt;
+            const float z = sd > 0.f ? (hi ? x - up : lo - x) * inv : 1e30f;
+            best = z > best ? z : best;
+          }
+        }
+      }
+    }
+    const unsigned long long bal = __ballot(f);
+    if (lane == 0 && i0 / 64 < NW) out_flags[row * NW + i0 / 64] = bal;
+  }
+  acnt = wave_sum(acnt);
+  ccnt = wave_sum(ccnt);
+  best = wave_max(best);
+  if (lane == 0) {
+    out_stats[row * 4 + 0] = mf;
+    out_stats[row * 4 + 1] = sd;
+    out_stats[row * 4 + 2] = up;
+    out_stats[row * 4 + 3] = lo;
+    out_count[row] = acnt;
+    out_score[row] = best;
+    out_valid[row] = (has_hist ? 1 : 0) | (ccnt > 0 ? 2 : 0);
+  }
+}
+
+FM_API int fm_window_decide(const float* hs, const float* cur, int64_t ld_c, int n_cur, int64_t R, int M,
+                            const float* thr, const int* bound, const float* minlb, float pair_factor,
+                            const int8_t* diff, int min_hist, float* out_stats, unsigned long long* out_flags, int NW,
+                            int* out_count, float* out_score, int* out_valid, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if (NW * 64 < n_cur) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(window_decide_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, stream, hs, cur, ld_c, n_cur,
+                     R, M, thr, bound, minlb, pair_factor, diff, min_hist, out_stats, out_flags, NW, out_count,
+                     out_score, out_valid);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // Service reduce: per service, fold its M metric rows into the packed result
 // row [status, score, anomalous-metric mask, anomalous point count] that is
 // all-gathered across ranks.  status: 0 = no anomaly, 1 = anomaly, 2 = unknown

@@ -32,10 +32,13 @@ class CanaryOutputs:
     suff: torch.Tensor
     decide: C.DecideResult
     packed: torch.Tensor        # [S, 4]
+    hs: torch.Tensor | None = None   # [R, 3] history mean, std, count (two-stream path)
 
 
 class CanaryScorer:
-    def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu"):
+    def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu", overlap: bool = True):
+        self.overlap = overlap
+        self._side = None
         self.cfg = cfg or BrainConfig()
         self.aliases = list(aliases)
         self.M = len(aliases)
@@ -59,6 +62,7 @@ class CanaryScorer:
                 pstats=torch.empty((R, C.N_TESTS), dtype=torch.float32, device=d),
                 diff=torch.empty((R,), dtype=torch.int8, device=d),
                 suff=torch.empty((R, C.SUFF), dtype=torch.float64, device=d),
+                hs=torch.empty((R, 3), dtype=torch.float32, device=d),
                 decide=C.alloc_decide(R, n_cur, d),
                 packed=torch.empty((R // self.M, 4), dtype=torch.float32, device=d),
             )
@@ -80,12 +84,40 @@ class CanaryScorer:
             return CanaryOutputs(pv, ps, df, None, dec, packed)
         o = self._alloc(R, cur.shape[1])
         has_base = base is not None and base.shape[1] > 0
-        if has_base:
-            self._pairwise_into(cur, base, o)
-        C.stats_decide(hist, cur, n_hist, self.M, self.thr, self.bound, self.minlb, o.diff if has_base else None,
-                       self.cfg.pairwise_threshold_factor, self.cfg.min_historical_points, out=o.decide)
+        if not self.overlap:
+            if has_base:
+                self._pairwise_into(cur, base, o)
+            C.stats_decide(hist, cur, n_hist, self.M, self.thr, self.bound, self.minlb,
+                           o.diff if has_base else None, self.cfg.pairwise_threshold_factor,
+                           self.cfg.min_historical_points, out=o.decide)
+        else:
+            # fork: pairwise (compute-bound) on a side stream || history stats
+            # (HBM-bound) on the main stream; join; tiny threshold/decide pass
+            from ..ops._lib import LIB, ptr, stream_of
+            dev = cur.device
+            main = torch.cuda.current_stream(dev)
+            if has_base:
+                side = self._side_stream(dev)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._pairwise_into(cur, base, o)
+            T = hist.shape[1] if n_hist is None else int(n_hist)
+            C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
+            LIB.call("fm_hist_stats", ptr(hist), hist.stride(0), T, R, ptr(o.hs), stream_of(hist))
+            if has_base:
+                main.wait_stream(side)
+            d = o.decide
+            LIB.call("fm_window_decide", ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1], R, self.M, ptr(self.thr),
+                     ptr(self.bound), ptr(self.minlb), float(self.cfg.pairwise_threshold_factor),
+                     ptr(o.diff) if has_base else None, int(self.cfg.min_historical_points), ptr(d.stats),
+                     ptr(d.flags), d.flags.shape[1], ptr(d.count), ptr(d.score), ptr(d.valid), stream_of(cur))
         C.service_reduce(o.decide.count, o.decide.score, o.decide.valid, self.M, out=o.packed)
         return o
+
+    def _side_stream(self, dev):
+        if self._side is None:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
 
     def _pairwise_into(self, cur, base, o: CanaryOutputs) -> None:
         from ..ops._lib import LIB, ptr, stream_of

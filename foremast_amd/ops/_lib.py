@@ -34,6 +34,9 @@ _SIGS: dict[str, list] = {
     "fm_stats_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p, c_void_p, c_void_p,
                         c_float, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_service_reduce": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p],
+    "fm_hist_stats": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p],
+    "fm_window_decide": [c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                         c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_compact_anomalies": [c_void_p, c_int, c_void_p, c_i64, c_int, c_void_p, c_i64, c_int, c_void_p, c_void_p,
                              c_void_p, c_void_p],
     "fm_synth_fleet": [c_void_p, c_i64, c_i64, c_i64, c_int, c_i64, c_int, c_int, c_int, c_int, c_float, c_float,

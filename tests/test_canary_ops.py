@@ -188,3 +188,18 @@ def test_gpu_scorer_graph_equals_eager_and_cpu(cuda):
     cpu = CanaryScorer(aliases, device="cpu").score(hc, bc, cc, T).packed
     assert (cpu[:, 0] == eager.cpu()[:, 0]).float().mean() > 0.95
     assert int((eager[:, 0] == 1).sum()) > 0
+
+
+@pytest.mark.gpu
+def test_gpu_two_stream_tick_equals_single_stream(cuda):
+    from foremast_amd.engine.scorer import CanaryScorer
+    aliases = ["error5xx", "latency", "traffic", "error4xx"]
+    h, b, c = C.synth_fleet(300, 4, 10080, 5, 10, 0, device=cuda, fault_rate=0.1)
+    a = CanaryScorer(aliases, device=cuda, overlap=False).score(h, b, c, 10080)
+    s2 = CanaryScorer(aliases, device=cuda, overlap=True)
+    o = s2.score(h, b, c, 10080)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(o.packed, a.packed)
+    torch.testing.assert_close(o.decide.stats, a.decide.stats)
+    g = s2.capture(h, b, c, 10080)().packed.clone()
+    torch.testing.assert_close(g, a.packed)
