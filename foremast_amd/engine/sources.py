@@ -154,8 +154,10 @@ class SyntheticSource:
             parts = url.split("&&")
             q = urllib.parse.unquote_plus(parts[0])
             start, end = float(parts[1]), float(parts[3])
-            if start > 1e11:   # wavefront trigger passes milliseconds
-                start, end = start / 1000, end / 1000
+            # the trigger passes milliseconds, except the historical end in
+            # seconds (trigger.go:250-258): normalise each bound separately
+            start = start / 1000 if start > 1e11 else start
+            end = end / 1000 if end > 1e11 else end
         pods = _pod_selector(q)
         metric = q.split("{")[0].replace("namespace_pod_", "").replace("namespace_app_pod_", "")
         if not pods:
