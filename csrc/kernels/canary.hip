@@ -111,8 +111,8 @@ __device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&ra
 
 }  // namespace
 
-enum { T_MW = 0, T_WIL = 1, T_KRU = 2, T_KS = 3, T_T = 4, N_TESTS = 5 };
-constexpr int kSuff = 12;
+enum { T_MW = 0, T_WIL = 1, T_KRU = 2, T_KS = 3, T_T = 4, T_FRI = 5, N_TESTS = 6 };
+constexpr int kSuff = 14;
 
 template <int K>
 __global__ __launch_bounds__(256) void pairwise_kernel(
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void pairwise_kernel(
   float dv[KW];
   int dt[KW];
   const int npair = n_cur < n_base ? n_cur : n_base;
-  int cw = 0;
+  int cw = 0, cpos = 0, cz = 0;
 #pragma unroll
   for (int k = 0; k < KW; ++k) {
     const int j = k * 64 + lane;
@@ -166,12 +166,14 @@ __global__ __launch_bounds__(256) void pairwise_kernel(
       const float xc = c[j], xb = b[j];
       if (isfinite(xc) && isfinite(xb)) {
         const float dd = xc - xb;
-        if (dd != 0.f) { d = fabsf(dd); t = dd > 0.f ? 1 : 0; ++cw; }
+        if (dd != 0.f) { d = fabsf(dd); t = dd > 0.f ? 1 : 0; ++cw; cpos += t; }
+        else ++cz;
       }
     }
     dv[k] = d; dt[k] = t;
   }
   const int nw = wave_sum(cw);
+  const int npos = wave_sum(cpos), nzero = wave_sum(cz);
 
   bitonic_sort<K>(v, tag);
   float rk[K];
@@ -216,6 +218,7 @@ __global__ __launch_bounds__(256) void pairwise_kernel(
     double* o = suff + row * kSuff;
     o[0] = n1; o[1] = n2; o[2] = nw; o[3] = r1; o[4] = tie; o[5] = dmax;
     o[6] = rplus; o[7] = tiew; o[8] = m1; o[9] = m2; o[10] = q1; o[11] = q2;
+    o[12] = npos; o[13] = nzero;
   }
 }
 
@@ -291,6 +294,19 @@ __global__ __launch_bounds__(256) void pvalue_kernel(const double* __restrict__ 
     if (se > 0) {
       double pp = 2.0 * norm_sf(fabs((T - mn) / se));
       p[T_WIL] = pp > 1.0 ? 1.0 : pp;
+    }
+  }
+  // Friedman chi-square over position-paired blocks with k = 2 treatments
+  // (current, baseline).  Within a block the ranks are {1,2} or {1.5,1.5};
+  // after the tie correction 1 - nzero/b the statistic reduces exactly to
+  // (npos - nneg)^2 / (npos + nneg) with 1 dof.
+  {
+    const int npos = (int)o[12], nzero = (int)o[13];
+    const int nneg = nw - npos, b = nw + nzero;
+    if (b >= min_wil && b > 0) {
+      const double q = nw > 0 ? (double)(npos - nneg) * (npos - nneg) / nw : 0.0;
+      st[T_FRI] = q;
+      p[T_FRI] = q > 0 ? erfc(sqrt(0.5 * q)) : 1.0;
     }
   }
   int applicable = 0, significant = 0;

@@ -17,9 +17,9 @@ import torch
 from . import reference as ref
 from ._lib import LIB, check, ptr, require_native, stream_of
 
-TEST_NAMES = ("MANN_WHITE", "WILCOXON", "KRUSKAL", "KS", "TTEST")
+TEST_NAMES = ("MANN_WHITE", "WILCOXON", "KRUSKAL", "KS", "TTEST", "FRIEDMAN")
 N_TESTS = len(TEST_NAMES)
-SUFF = 12  # per-row sufficient statistics written by the wave kernel, read by the p-value kernel
+SUFF = 14  # per-row sufficient statistics written by the wave kernel, read by the p-value kernel
 
 
 @dataclass(frozen=True)
@@ -27,7 +27,7 @@ class PairwiseConfig:
     """Pairwise canary test settings (foremast-brain/README.md:32-38,
     deploy/foremast/3_brain/foremast-brain.yaml:74-79)."""
 
-    algorithm: str = "ALL"          # ML_PAIRWISE_ALGORITHM: ALL | ANY | MANN_WHITE | WILCOXON | KRUSKAL | KS | TTEST
+    algorithm: str = "ALL"          # ML_PAIRWISE_ALGORITHM: ALL | ANY | MANN_WHITE | WILCOXON | KRUSKAL | KS | TTEST | FRIEDMAN
     p_threshold: float = 0.05       # ML_PAIRWISE_THRESHOLD
     min_mann_white: int = 20        # MIN_MANN_WHITE_DATA_POINTS
     min_wilcoxon: int = 20          # MIN_WILCOXON_DATA_POINTS
@@ -39,7 +39,8 @@ class PairwiseConfig:
             return (1 << N_TESTS) - 1, 0
         if a == "ANY":
             return (1 << N_TESTS) - 1, 1
-        alias = {"MANN_WHITNEY": "MANN_WHITE", "MANNWHITNEY": "MANN_WHITE", "T_TEST": "TTEST", "KS_2SAMP": "KS"}
+        alias = {"MANN_WHITNEY": "MANN_WHITE", "MANNWHITNEY": "MANN_WHITE", "T_TEST": "TTEST", "KS_2SAMP": "KS",
+                 "FRIEDMANCHISQUARE": "FRIEDMAN", "FRIEDMAN_CHI_SQUARE": "FRIEDMAN"}
         a = alias.get(a, a)
         if a not in TEST_NAMES:
             raise ValueError(f"unknown pairwise algorithm {self.algorithm!r}")
@@ -54,7 +55,7 @@ def _rows(x: torch.Tensor) -> tuple[int, int]:
 
 
 def pairwise_tests(cur: torch.Tensor, base: torch.Tensor, cfg: PairwiseConfig = PairwiseConfig()):
-    """Returns (pvals [R,5] f32, stats [R,5] f32, diff [R] int8) in TEST_NAMES order.
+    """Returns (pvals [R,6] f32, stats [R,6] f32, diff [R] int8) in TEST_NAMES order.
 
     NaN / inf samples are treated as missing.  A test whose min-points gate is
     not met yields NaN and is excluded from the ALL/ANY combination.

@@ -53,7 +53,15 @@ def kolmogorov_sf(lam):
     return special.kolmogorov(lam)
 
 
-TEST_NAMES = ("MANN_WHITE", "WILCOXON", "KRUSKAL", "KS", "TTEST")
+TEST_NAMES = ("MANN_WHITE", "WILCOXON", "KRUSKAL", "KS", "TTEST", "FRIEDMAN")
+
+
+def special_rank2(cb):
+    """Within-block average ranks of a [R, b, 2] array (1/2, or 1.5/1.5 on a tie)."""
+    lt = (cb[..., 0] < cb[..., 1]).astype(np.float64)
+    eq = (cb[..., 0] == cb[..., 1]).astype(np.float64)
+    r0 = np.where(eq > 0, 1.5, np.where(lt > 0, 1.0, 2.0))
+    return np.stack([r0, 3.0 - r0], axis=-1)
 
 
 def pairwise_tests(cur, base, mask, combine_any, p_thr, min_mw, min_wil, min_kru):
@@ -70,8 +78,8 @@ def pairwise_tests(cur, base, mask, combine_any, p_thr, min_mw, min_wil, min_kru
     n = n1 + n2
     ranks, _, tie, order, is_end = avg_ranks(pooled)
     r1 = np.where(tags == 0, ranks, 0.0).sum(1)
-    P = np.full((R, 5), np.nan)
-    S = np.full((R, 5), np.nan)
+    P = np.full((R, 6), np.nan)
+    S = np.full((R, 6), np.nan)
     with np.errstate(divide="ignore", invalid="ignore"):
         # Mann-Whitney
         u1 = r1 - n1 * (n1 + 1) / 2
@@ -138,7 +146,24 @@ def pairwise_tests(cur, base, mask, combine_any, p_thr, min_mw, min_wil, min_kru
         g = (nw >= min_wil) & (nw > 0)
         P[:, 1] = np.where(g, pw, np.nan)
         S[:, 1] = np.where(g, T, np.nan)
-    sel = np.array([(mask >> i) & 1 for i in range(5)], dtype=bool)
+        # Friedman chi-square, k = 2 treatments over the paired blocks, in
+        # its general form (per-block ranks, sum of rank sums, tie correction)
+        if npair > 0:
+            cb = np.stack([cur[:, :npair].astype(np.float32), base[:, :npair].astype(np.float32)], axis=2)
+            okb = np.isfinite(cb).all(axis=2)
+            rk = special_rank2(cb)
+            b = okb.sum(1).astype(np.float64)
+            Rj = np.where(okb[:, :, None], rk, 0.0).sum(1)                 # [R, 2]
+            k = 2.0
+            q = 12.0 / (b * k * (k + 1)) * (Rj ** 2).sum(1) - 3.0 * b * (k + 1)
+            ties = np.where(okb & (cb[:, :, 0] == cb[:, :, 1]), 6.0, 0.0).sum(1)
+            c = 1.0 - ties / (b * (k ** 3 - k))
+            qf = np.where(c > 0, q / c, 0.0)
+            pf = np.where(qf > 0, special.chdtrc(1.0, qf), 1.0)
+            g = (b >= min_wil) & (b > 0)
+            P[:, 5] = np.where(g, pf, np.nan)
+            S[:, 5] = np.where(g, qf, np.nan)
+    sel = np.array([(mask >> i) & 1 for i in range(6)], dtype=bool)
     app = ~np.isnan(P[:, sel])
     sig = app & (np.nan_to_num(P[:, sel], nan=1.0) < p_thr)
     na = app.sum(1)

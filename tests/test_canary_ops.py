@@ -55,6 +55,21 @@ def test_reference_pairwise_matches_scipy(n1, n2, nan_frac):
             np.testing.assert_allclose(P[r, 1], o["wil"].pvalue, rtol=1e-4)
 
 
+def test_reference_friedman_two_treatments():
+    """k=2 Friedman (general rank-sum form with tie correction) equals the
+    sign-test chi-square (npos-nneg)^2/(npos+nneg); p from scipy chi2(1)."""
+    cur, base = _data(6, 40, 40, seed=5)
+    P, S, _ = ref.pairwise_tests(cur, base, 63, 0, 0.05, 20, 20, 5)
+    for r in range(6):
+        d = cur[r].astype(np.float32) - base[r].astype(np.float32)
+        npos, nneg = (d > 0).sum(), (d < 0).sum()
+        q = (npos - nneg) ** 2 / (npos + nneg)
+        np.testing.assert_allclose(S[r, 5], q, rtol=1e-6)
+        np.testing.assert_allclose(P[r, 5], ss.chi2.sf(q, 1), rtol=1e-6)
+    P2, _, _ = ref.pairwise_tests(cur[:, :10], base[:, :10], 63, 0, 0.05, 20, 20, 5)
+    assert np.isnan(P2[:, 5]).all()
+
+
 def test_reference_gates_and_combination():
     cur, base = _data(4, 10, 10)
     P, _, d = ref.pairwise_tests(cur, base, 31, 0, 0.05, 20, 20, 5)
@@ -106,11 +121,11 @@ def test_synth_reference_deterministic_across_shards():
 def test_gpu_pairwise_matches_reference(cuda, n1, n2, nan_frac):
     R = 257
     cur, base = _data(R, n1, n2, seed=n1 + n2, nan_frac=nan_frac)
-    P0, S0, d0 = ref.pairwise_tests(cur, base, 31, 0, 0.05, 20, 20, 5)
+    P0, S0, d0 = ref.pairwise_tests(cur, base, 63, 0, 0.05, 20, 20, 5)
     pv, st, d = C.pairwise_tests(torch.from_numpy(cur).to(cuda), torch.from_numpy(base).to(cuda))
     pv, st, d = pv.cpu().numpy(), st.cpu().numpy(), d.cpu().numpy()
     np.testing.assert_array_equal(np.isnan(pv), np.isnan(P0))
-    np.testing.assert_allclose(np.nan_to_num(st[:, [0, 1, 3]]), np.nan_to_num(S0[:, [0, 1, 3]]), rtol=1e-5,
+    np.testing.assert_allclose(np.nan_to_num(st[:, [0, 1, 3, 5]]), np.nan_to_num(S0[:, [0, 1, 3, 5]]), rtol=1e-5,
                                atol=1e-5)
     np.testing.assert_allclose(np.nan_to_num(pv), np.nan_to_num(P0), rtol=2e-4, atol=2e-6)
     assert (d == d0).mean() > 0.995
