@@ -3,7 +3,7 @@
 (BASELINE.json config 3), data-parallel over the GPUs of one node.
 
 One step = one full brain judgement cycle for the whole fleet:
-  pairwise canary tests (Mann-Whitney, Wilcoxon, Kruskal, KS, Welch-t; ALL)
+  pairwise canary tests (Mann-Whitney, Wilcoxon, Kruskal, KS, Welch-t, Friedman; ALL)
   -> moving_average_all bounds over the 7-day history (10,080 points @ 60 s)
   -> anomaly decision on the current window (fail-fast flags, per-service verdict)
   -> all-gather of the packed per-service verdicts to every rank (RCCL over xGMI)
@@ -122,7 +122,7 @@ def main() -> None:
             "dtype": "fp32",
             "data": "synthetic (on-device Prometheus-shaped fleet, K11; 2% injected faults)",
             "config": {
-                "model": "foremast-brain canary: moving_average_all + pairwise ALL(MW,Wilcoxon,Kruskal,KS,Welch-t)",
+                "model": "foremast-brain canary: moving_average_all + pairwise ALL(MW,Wilcoxon,Kruskal,KS,Welch-t,Friedman)",
                 "global_batch": windows,
                 "seq_len": args.hist,
                 "services": S,

@@ -244,7 +244,9 @@ class Brain:
         now = self.clock()
         docs = self.store.claim(self.worker, self.batch_size, self.cfg.max_stuck_seconds, now=now, owner=self._owner)
         if not docs:
-            return {"claimed": 0}
+            # ranks without work still join the tick's collective
+            fleet = self._gather([])
+            return {"claimed": 0, "fleet": len(fleet)}
         with ThreadPoolExecutor(max_workers=max(1, min(self.fetch_threads, len(docs)))) as ex:
             works = list(ex.map(lambda d: self._fetch_job(d, now), docs))
         rows: list[Row] = []

@@ -1,0 +1,184 @@
+"""Multi-process data-parallel paths on CPU (gloo, world 2) — the same code the
+RCCL ranks run on GPU (distributed tests without 8 GPUs)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from foremast_amd.parallel import dist as D
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    return D.init_distributed(backend="gloo")
+
+
+def _run(fn, world, *args):
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in procs:
+        r, res = q.get(timeout=240)
+        out[r] = res
+    for p in procs:
+        p.join(60)
+    for r, res in out.items():
+        if isinstance(res, BaseException) or (isinstance(res, str) and res.startswith("ERR")):
+            raise AssertionError(f"rank {r}: {res}")
+    return out
+
+
+def _entry(fn, rank, world, port, q, *args):
+    try:
+        _init(rank, world, port)
+        res = fn(rank, world, *args)
+        q.put((rank, res))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, "ERR " + traceback.format_exc()))
+    finally:
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- workers
+def _w_collectives(rank, world):
+    x = torch.full((3, 2), float(rank))
+    g = D.all_gather_rows(x)
+    assert g.shape == (3 * world, 2) and g[3:, 0].eq(1).all() and g[:3].eq(0).all()
+    parts = D.all_gather_varlen(torch.arange(rank + 1, dtype=torch.float32).reshape(-1, 1))
+    assert [p.shape[0] for p in parts] == [1, 2]
+    assert D.all_reduce_max(float(rank) + 0.5, torch.device("cpu")) == world - 0.5
+    assert D.broadcast_object({"r": rank} if rank == 0 else None) == {"r": 0}
+    mine, grp = D.cluster_groups(2)
+    assert mine == [rank] and grp is not None
+    t = torch.tensor([rank + 1.0])
+    torch.distributed.all_reduce(t, group=grp)
+    assert t.item() == rank + 1.0              # group of one rank
+    mine4, grp4 = D.cluster_groups(4)
+    assert mine4 == [c for c in range(4) if c % world == rank] and grp4 is None
+    return "ok"
+
+
+def _w_sharded_scoring(rank, world, S, M):
+    from foremast_amd.config import BrainConfig
+    from foremast_amd.engine.scorer import CanaryScorer
+    from foremast_amd.ops import canary as C
+    svc0, here, pad = D.shard_range(S, rank, world)
+    h, b, c = C.synth_fleet(pad, M, 600, 3, 10, svc0)
+    cfg = BrainConfig()
+    cfg.min_historical_points = 10
+    sc = CanaryScorer(["error5xx", "latency", "cpu", "memory"][:M], cfg)
+    o = sc.score(h, b, c, 600)
+    g = D.all_gather_rows(o.packed.float())
+    return g[:S].numpy()
+
+
+def _w_impact(rank, world, S_total, n_clusters):
+    from foremast_amd.engine.impact import FleetImpact, synth_call_graph
+    g, cl = synth_call_graph(S_total, n_clusters, seed=3)
+    _, _, pad = D.shard_range(S_total, rank, world)
+    rng = np.random.default_rng(9)
+    scores = rng.random(S_total).astype(np.float32) * (rng.random(S_total) < 0.1)
+    scores = np.concatenate([scores, np.zeros(world * pad - S_total, np.float32)])
+    fi = FleetImpact(g, cl, n_clusters, pad)
+    _, imp, agg = fi.step(torch.from_numpy(scores[rank * pad:(rank + 1) * pad].copy()))
+    return imp.numpy(), agg.numpy()
+
+
+# --------------------------------------------------------------------------- tests
+def test_gloo_collectives_world2():
+    assert set(_run(_w_collectives, 2).values()) == {"ok"}
+
+
+def test_sharded_scoring_equals_single_process():
+    S, M = 7, 4
+    out = _run(_w_sharded_scoring, 2, S, M)
+    np.testing.assert_array_equal(out[0], out[1])
+    single = _w_sharded_scoring(0, 1, S, M)
+    np.testing.assert_array_equal(out[0], single)
+
+
+def test_cross_cluster_impact_equals_single_process():
+    from foremast_amd.engine.impact import FleetImpact, synth_call_graph
+    from foremast_amd.ops.misc import ref_downstream_impact
+    S, K = 403, 4
+    out = _run(_w_impact, 2, S, K)
+    g, cl = synth_call_graph(S, K, seed=3)
+    rng = np.random.default_rng(9)
+    scores = rng.random(S).astype(np.float32) * (rng.random(S) < 0.1)
+    imp = ref_downstream_impact(g, scores, 2)
+    np.testing.assert_allclose(out[0][0], imp)
+    np.testing.assert_allclose(out[1][0], imp)
+    eff = np.maximum(scores, imp)
+    np.testing.assert_allclose(out[0][1], [eff[cl == c].max() for c in range(K)])
+    fi = FleetImpact(g, cl, K, S)
+    np.testing.assert_allclose(fi.step(torch.from_numpy(scores))[1].numpy(), imp)
+
+
+def test_caller_series_graph():
+    from foremast_amd.engine.impact import graph_from_caller_series
+    from foremast_amd.ops.misc import ref_downstream_impact
+    svcs = ["web", "cart", "db", "auth"]
+    g = graph_from_caller_series([("cart", "web", 30.0), ("auth", "web", 10.0), ("db", "cart", 5.0),
+                                  ("web", "", 100.0), ("db", "unknown", 1.0)], svcs)
+    assert g.rowptr.tolist() == [0, 2, 3, 3, 3]
+    a = np.array([0, 0, 1.0, 0], np.float32)        # db anomalous
+    imp = ref_downstream_impact(g, a, 2)
+    assert imp[1] == pytest.approx(1.0) and imp[0] == pytest.approx(0.75) and imp[3] == 0
+
+
+def _w_brain(rank, world, db, n_apps):
+    from foremast_amd.config import BrainConfig
+    from foremast_amd.engine.brain import Brain
+    from foremast_amd.engine.sources import SourceRouter
+    from foremast_amd.service.store import SQLiteStore
+    store = SQLiteStore(db)
+    clock = lambda: 1_760_000_000.0
+    brain = Brain(store, BrainConfig(), sources=SourceRouter.synthetic_only(faults={"app3": 8.0}, fault_after=1_760_000_000.0 - 600),
+                  clock=clock,
+                  worker_id=f"rank{rank}")
+    r1 = brain.run_once()
+    r2 = brain.run_once()                  # a rank with no claim still joins the gather
+    return r1.get("claimed", 0), r1.get("fleet", 0), r2.get("fleet", 0)
+
+
+def test_brain_ranks_claim_disjoint_owned_jobs(tmp_path):
+    from foremast_amd.api import crd
+    from foremast_amd.controller.analyst import AnalystClient
+    from foremast_amd.service.app import create_app
+    from foremast_amd.service.store import SQLiteStore
+    db = str(tmp_path / "jobs.db")
+    store = SQLiteStore(db)
+    client = AnalystClient.for_app(create_app(store), clock=lambda: 1_760_000_000.0)
+    m = crd.Metrics("prometheus", "http://prom/api/v1/", [crd.Monitoring("cpu_usage", "gauge", "cpu")])
+    n = 8
+    ids = [client.start_analyzing("default", f"app{i}", [[f"app{i}-5db89899b5-p1"]], m, 10, "rollingUpdate")
+           for i in range(n)]
+    out = _run(_w_brain, 2, db, n)
+    claimed = [out[r][0] for r in range(2)]
+    assert sum(claimed) == n
+    # owner = stable hash of the document's namespace:app (namespace is only
+    # filled for HPA documents, models.go:102-124)
+    owners = [D.service_owner(store.get(i).namespace, store.get(i).app_name, 2) for i in ids]
+    assert claimed == [owners.count(0), owners.count(1)]
+    assert out[0][1] == out[1][1] == n and out[0][2] == out[1][2]
+    docs = [store.get(i) for i in ids]
+    assert all(d.status != "initial" for d in docs)
+    assert store.get(ids[3]).status == "completed_unhealth"
