@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmarks for the BASELINE.json configs other than the headline (config 3
+is the root ``bench.py``).
+
+  --config 1  single-metric (latency_p99) pairwise canary Welch t-test, the
+              whole plumbing on the CPU reference path: REST create ->
+              brain cycle (claim, fetch synthetic Prometheus, score, verdict)
+              -> REST status, for ``--jobs`` canary jobs per step
+  --config 2  4-metric (error%, TPS, p99, 4xx) Holt-Winters baseline anomaly
+              (FFT period detection K3 + grid-searched HW fit K2 + band
+              decision) over the 7-day history, 1 MI355X
+  --config 4  LSTM forecaster for HPA / ClusterAutoScaler prediction, bf16
+              MFMA recurrence (K6) + head + band decision, data-parallel
+  --config 5  downstream-impact aggregation across 4 synthetic clusters:
+              canary tick per rank (HIP graph) -> cross-cluster all-gather of
+              per-service scores (C5) -> 2-hop impact over the global call
+              graph (K9) -> per-cluster aggregate
+
+All on synthetic Prometheus-shaped series / random-init weights (no network).
+Reference publishes no numbers for any config: vs_baseline null.
+Launch like ``bench.py`` (``torch.distributed.run`` for N>1).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from benchmarks.harness import emit, setup, time_steps  # noqa: E402
+from foremast_amd.config import BrainConfig  # noqa: E402
+from foremast_amd.ops import canary as C  # noqa: E402
+from foremast_amd.parallel import dist as D  # noqa: E402
+
+T_HIST = 10080
+
+
+def _common(args, info, ms, p50, metric, value, unit, model, global_batch, seq_len, scaling, dtype, data, extra=None):
+    out = {"metric": metric, "value": value, "unit": unit, "n_gpus": info.world if args.device != "cpu" else 0,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "p50_decision_latency_ms": p50,
+           "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": dtype, "data": data,
+           "config": {"id": args.config, "model": model, "global_batch": global_batch, "seq_len": seq_len,
+                      "parallelism": f"dp{info.world}"}}
+    if extra:
+        out["config"].update(extra)
+    emit(info, **out)
+
+
+# --------------------------------------------------------------------------- config 1
+def config1(args):
+    from foremast_amd.api import crd
+    from foremast_amd.controller.analyst import AnalystClient
+    from foremast_amd.engine.brain import Brain
+    from foremast_amd.engine.sources import SourceRouter
+    from foremast_amd.service.app import create_app
+    from foremast_amd.service.store import MemoryStore
+
+    info, dev = setup(gpus_required=args.device != "cpu")
+    dev = torch.device("cpu") if args.device == "cpu" else dev
+    t = {"now": 1_760_000_000.0}
+    clock = lambda: t["now"]
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    cfg = BrainConfig()
+    cfg.pairwise_algorithm = "TTEST"
+    cfg.ml_algorithm = "moving_average_all"
+    src = SourceRouter.synthetic_only(faults={"-p-0": 3.0}, fault_after=t["now"] - 900)
+    brain = Brain(store, cfg, device=dev, sources=src, clock=clock, batch_size=args.jobs, worker_id="bench")
+    m = crd.Metrics("prometheus", "http://prom/api/v1/", [crd.Monitoring("latency_p99", "gauge", "latency")])
+    pods = 5
+
+    def step():
+        t["now"] += 60.0
+        ids = [client.start_analyzing("default", f"svc{j}", [[f"svc{j}-5db89899b5-p-{k}" for k in range(pods)],
+                                                              [f"svc{j}-7687b9f4d7-q-{k}" for k in range(pods)]],
+                                      m, 10, "canary") for j in range(args.jobs)]
+        brain.run_once()
+        for i in ids:
+            client.get_status(i)
+
+    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    _common(args, info, ms, p50, "canary jobs judged/sec end-to-end (REST create -> brain -> REST status)",
+            args.jobs / (ms / 1e3), "jobs/s", "pairwise Welch t-test (ML_PAIRWISE_ALGORITHM=TTEST) + "
+            "moving_average_all, 1 metric latency_p99", args.jobs, T_HIST, "weak", "fp32",
+            "synthetic Prometheus query_range source (in-process), 5+5 pods x 10 points per side",
+            {"device": str(dev), "jobs_per_step": args.jobs})
+
+
+# --------------------------------------------------------------------------- config 2
+def config2(args):
+    from foremast_amd.models import zoo
+    info, dev = setup()
+    S, M = args.services, 4
+    svc0, _, pad = D.shard_range(S, info.rank, info.world)
+    hist, _, cur = C.synth_fleet(pad, M, T_HIST, 1, args.window, svc0, device=dev)
+    cur = cur.contiguous()
+    cfg = BrainConfig()
+    aliases = ["error5xx", "traffic", "latency", "error4xx"] * pad
+    tables = zoo.make_tables(aliases, cfg, dev)
+    hor = torch.arange(1, args.window + 1, device=dev).expand(pad * M, -1).contiguous()
+    period = None if args.detect_period else 1440
+
+    def step():
+        d = zoo.decide("holt_winters", hist, T_HIST, cur, hor, M, tables, period=period)
+        C.service_reduce(d.count, d.score, d.valid, M)
+
+    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    _common(args, info, ms, p50, "metric windows scored/sec (node), Holt-Winters baseline",
+            S * M / (ms / 1e3), "windows/s", "additive Holt-Winters, 27-candidate (alpha,beta,gamma) grid, period "
+            + ("from FFT (K3)" if args.detect_period else "1440") + ", band decision", S * M, T_HIST, "strong", "fp32",
+            "synthetic on-device Prometheus-shaped fleet (K11)", {"services": S, "metrics": M,
+                                                                  "current_points": args.window})
+
+
+# --------------------------------------------------------------------------- config 4
+def config4(args):
+    from foremast_amd.models.lstm import LSTMForecaster
+    from foremast_amd.ops import smoothing as SM
+    info, dev = setup()
+    S, M = args.services, args.metrics
+    svc0, _, pad = D.shard_range(S, info.rank, info.world)
+    hist, _, cur = C.synth_fleet(pad, M, T_HIST, 1, args.window, svc0, device=dev)
+    model = LSTMForecaster(hidden=args.hidden, window=args.lookback, horizon=args.window, device=dev)
+    # random-init weights broadcast from rank 0 (C6) so every rank runs the same model
+    sd = D.broadcast_object(model.state_dict() if info.is_main else None)
+    model.load_state_dict(sd)
+    cfg = BrainConfig()
+    rules = [cfg.rule_for(a) for a in (["cpu", "memory", "latency", "traffic"] * 4)[:M]]
+    thr = torch.tensor([r.threshold for r in rules], dtype=torch.float32, device=dev)
+    bound = torch.tensor([r.bound for r in rules], dtype=torch.int32, device=dev)
+    minlb = torch.tensor([r.min_lower_bound for r in rules], dtype=torch.float32, device=dev)
+    gathered = torch.empty((info.world * pad, 4), dtype=torch.float32, device=dev)
+
+    def step():
+        fc, sig = model.forecast(hist, T_HIST, args.window)
+        up, lo, flags, cnt, sc = SM.band_decide(cur, fc, sig, M, thr, bound, minlb, None, 1.0)
+        valid = torch.full_like(cnt, 3)
+        packed = C.service_reduce(cnt, sc, valid, M)
+        D.all_gather_rows(packed, gathered)
+
+    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    _common(args, info, ms, p50, "series forecast+judged/sec (node), LSTM HPA forecaster",
+            S * M / (ms / 1e3), "series/s", f"LSTM H={args.hidden}, lookback {args.lookback}, horizon {args.window},"
+            " bf16 MFMA recurrence, fp32 cell/accumulate", S * M, args.lookback, "strong", "bf16",
+            "synthetic on-device fleet (K11), random-init weights", {"services": S, "metrics": M})
+
+
+# --------------------------------------------------------------------------- config 5
+def config5(args):
+    from foremast_amd.engine.impact import FleetImpact, synth_call_graph
+    from foremast_amd.engine.scorer import CanaryScorer
+    info, dev = setup()
+    K = args.clusters
+    S = args.services * K
+    M = args.metrics
+    svc0, _, pad = D.shard_range(S, info.rank, info.world)
+    hist, base, cur = C.synth_fleet(pad, M, T_HIST, args.pods, args.window, svc0, device=dev)
+    cfg = BrainConfig()
+    cfg.min_historical_points = 10
+    aliases = (["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"] * 2)[:M]
+    scorer = CanaryScorer(aliases, cfg, device=dev)
+    tick = scorer.capture(hist, base, cur, T_HIST)
+    graph, cluster_of = synth_call_graph(S, K, avg_deg=args.degree, seed=5)
+    fi = FleetImpact(graph, cluster_of, K, pad, device=dev, hops=args.hops)
+    host = torch.empty((K,), dtype=torch.float32, pin_memory=True)
+    res = {}
+
+    def step():
+        o = tick()
+        _, imp, agg = fi.step(o.packed[:, 1].contiguous())
+        if info.is_main:
+            host.copy_(agg, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        res["agg"] = host
+
+    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    _common(args, info, ms, p50, "metric windows scored/sec (node) incl. cross-cluster downstream impact",
+            S * M / (ms / 1e3), "windows/s", f"canary tick + {args.hops}-hop max-times impact over a "
+            f"{K}-cluster call graph ({graph.col.size} edges)", S * M, T_HIST, "strong", "fp32",
+            "synthetic on-device fleet (K11) + synthetic heavy-tailed call graph, 5% cross-cluster edges",
+            {"clusters": K, "services": S, "metrics": M, "edges": int(graph.col.size)})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--device", default="cuda", help="config 1 only: cpu (reference path) or cuda")
+    ap.add_argument("--jobs", type=int, default=200)
+    ap.add_argument("--services", type=int, default=10000)
+    ap.add_argument("--metrics", type=int, default=8)
+    ap.add_argument("--window", type=int, default=10)
+    ap.add_argument("--pods", type=int, default=5)
+    ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--lookback", type=int, default=240)
+    ap.add_argument("--clusters", type=int, default=4)
+    ap.add_argument("--degree", type=int, default=6)
+    ap.add_argument("--hops", type=int, default=2)
+    ap.add_argument("--detect-period", action="store_true")
+    args = ap.parse_args()
+    {1: config1, 2: config2, 4: config4, 5: config5}[args.config](args)
+
+
+if __name__ == "__main__":
+    main()

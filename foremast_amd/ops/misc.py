@@ -211,11 +211,14 @@ def downstream_impact(g: CallGraph, score: torch.Tensor, hops: int = 2) -> torch
         return torch.from_numpy(ref_downstream_impact(g, score.numpy(), hops))
     require_native(score)
     d = score.device
-    rp = torch.from_numpy(g.rowptr).to(d)
-    col = torch.from_numpy(g.col).to(d)
-    w = torch.from_numpy(g.weight).to(d)
-    b0 = torch.empty((S,), dtype=torch.float32, device=d)
-    b1 = torch.empty_like(b0)
+    # the CSR and the ping-pong buffers are uploaded/allocated once per device
+    # (the tick replays with no host->device traffic and can be graph-captured)
+    cache = g.__dict__.setdefault("_dev", {})
+    if d not in cache:
+        cache[d] = (torch.from_numpy(g.rowptr).to(d), torch.from_numpy(g.col).to(d),
+                    torch.from_numpy(g.weight).to(d), torch.empty((S,), dtype=torch.float32, device=d),
+                    torch.empty((S,), dtype=torch.float32, device=d))
+    rp, col, w, b0, b1 = cache[d]
     LIB.call("fm_downstream_impact", ptr(rp), ptr(col), ptr(w), ptr(score), S, hops, ptr(b0), ptr(b1),
              stream_of(score))
     return b0 if (hops - 1) % 2 == 0 else b1
