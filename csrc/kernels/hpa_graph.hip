@@ -115,3 +115,38 @@ FM_API int fm_downstream_impact(const int64_t* rowptr, const int* col, const flo
   }
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Per-cluster maximum of non-negative scores (the cross-cluster aggregate of
+// the downstream-impact step).  Each block folds a grid-stride slice into an
+// LDS array of K partial maxima, then merges with K global atomics; a float
+// >= 0 orders like its bit pattern, so atomicMax on the int view is exact.
+// (A scatter with amax over 4 targets serialises 40k atomics on 4 words.)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void segment_max_kernel(const float* __restrict__ v, const int64_t* __restrict__ seg,
+                                                          int64_t S, int K, int* __restrict__ out) {
+  extern __shared__ int smax[];
+  for (int k = threadIdx.x; k < K; k += blockDim.x) smax[k] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (int64_t)gridDim.x * blockDim.x) {
+    const float x = v[i];
+    const int64_t c = seg[i];
+    if (x > 0.f && c >= 0 && c < K) atomicMax(&smax[c], __float_as_int(x));
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += blockDim.x)
+    if (smax[k] > 0) atomicMax(&out[k], smax[k]);
+}
+
+FM_API int fm_segment_max(const float* v, const int64_t* seg, int64_t S, int K, float* out, hipStream_t stream) {
+  if (K <= 0 || K > 16384) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)K, stream);
+  if (e != hipSuccess) return (int)e;
+  if (S <= 0) return 0;
+  int64_t blocks = (S + 2047) / 2048;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(segment_max_kernel, dim3((unsigned)blocks), dim3(256), sizeof(int) * K, stream, v, seg, S, K,
+                     reinterpret_cast<int*>(out));
+  FM_LAUNCH_CHECK();
+  return 0;
+}

@@ -18,6 +18,7 @@
 using namespace fm;
 
 struct Cand { float a, b, g; };
+constexpr int kPrefetch = 16;  // season/sample loads issued ahead per chunk (HW fit)
 
 // kind: 0 = SES, 1 = Holt (double), 2 = Holt-Winters additive
 template <int KIND>
@@ -56,7 +57,49 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
   float acc = 0.f;
   int n = 0, chunk = 0;
   int ph = 0;  // t % m, advanced incrementally (no per-step integer modulo)
-  for (int t = t0; t < T; ++t) {
+  int t = t0;
+  if (KIND == 2 && m > kPrefetch) {
+    // The season slot read at step t was written at step t - m, so the U
+    // reads of a chunk never alias the chunk's own writes (U < m): issue all
+    // U season + sample loads up front, then run the U dependent steps from
+    // registers.  The per-step memory latency of the naive loop (load ->
+    // dependent update -> store -> next load) is paid once per chunk.
+    for (; t + kPrefetch <= T; t += kPrefetch) {
+      float sv[kPrefetch], xv[kPrefetch];
+      int64_t si[kPrefetch];
+#pragma unroll
+      for (int u = 0; u < kPrefetch; ++u) {
+        int pu = ph + u;
+        if (pu >= m) pu -= m;
+        si[u] = (int64_t)pu * P + pid;
+        sv[u] = season[si[u]];
+        xv[u] = xr[t + u];
+      }
+      ph += kPrefetch;
+      if (ph >= m) ph -= m;
+#pragma unroll
+      for (int u = 0; u < kPrefetch; ++u) {
+        const float xt = xv[u], s_old = sv[u];
+        const float pred = lvl + tr + s_old;
+        if (isfinite(xt)) {
+          const float e = xt - pred;
+          acc += e * e;
+          ++n;
+          const float lprev = lvl;
+          lvl = al * (xt - s_old) + (1.f - al) * (lvl + tr);
+          tr = be * (lvl - lprev) + (1.f - be) * tr;
+          sv[u] = ga * (xt - lvl) + (1.f - ga) * s_old;
+        } else {
+          lvl = lvl + tr;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kPrefetch; ++u) season[si[u]] = sv[u];
+      chunk += kPrefetch;
+      if (chunk >= 64) { err2 += acc; acc = 0.f; chunk = 0; }
+    }
+  }
+  for (; t < T; ++t) {
     const float xt = xr[t];
     float s_old = 0.f;
     int64_t sidx = 0;

@@ -23,7 +23,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ..ops.misc import CallGraph, downstream_impact
+from ..ops.misc import CallGraph, downstream_impact, segment_max
 from ..parallel import dist as D
 
 
@@ -100,6 +100,4 @@ class FleetImpact:
         g = g.contiguous()
         imp = downstream_impact(self.graph, g, self.hops)
         eff = torch.maximum(g, imp)
-        agg = torch.zeros((self.n_clusters,), dtype=torch.float32, device=self.device)
-        agg = agg.scatter_reduce(0, self.cluster, eff, reduce="amax", include_self=True)
-        return g, imp, agg
+        return g, imp, segment_max(eff, self.cluster, self.n_clusters)

@@ -234,3 +234,16 @@ def ref_downstream_impact(g: CallGraph, a: np.ndarray, hops: int) -> np.ndarray:
         np.maximum.at(out, src, val.astype(np.float32))
         prev = out
     return prev
+
+
+def segment_max(v: torch.Tensor, seg: torch.Tensor, K: int) -> torch.Tensor:
+    """out[k] = max(0, max of v[i] with seg[i] == k) for non-negative scores
+    (per-cluster aggregate of the impact step)."""
+    check(v.dtype == torch.float32 and seg.dtype == torch.int64 and v.numel() == seg.numel(), "bad segment_max args")
+    if not v.is_cuda:
+        out = torch.zeros((K,), dtype=torch.float32)
+        return out.scatter_reduce(0, seg, v.clamp(min=0), reduce="amax", include_self=True)
+    require_native(v)
+    out = torch.empty((K,), dtype=torch.float32, device=v.device)
+    LIB.call("fm_segment_max", ptr(v.contiguous()), ptr(seg.contiguous()), v.numel(), K, ptr(out), stream_of(v))
+    return out

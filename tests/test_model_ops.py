@@ -130,9 +130,10 @@ def test_ref_lstm_matches_torch_lstm():
 
 # ----------------------------------------------------------------- GPU kernels
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,m", [(0, 1), (1, 1), (2, 24), (2, 1440)])
+@pytest.mark.parametrize("kind,m", [(0, 1), (1, 1), (2, 12), (2, 24), (2, 1440)])
 def test_gpu_es_fit(cuda, kind, m):
-    T = 3000 if m < 1440 else 10080
+    # m=12: plain loop (m <= prefetch depth); 24/1440: prefetched chunks + tail
+    T = 3001 if m < 1440 else 10080
     x = _seasonal(37, T, period=max(m, 24), seed=kind)
     x[3, 500] = np.nan
     fc0, sig0, best0, sse0 = SM.ref_es_fit(x, kind, 10, m, SM.default_grid(kind))
@@ -234,6 +235,11 @@ def test_gpu_hpa_and_impact(cuda):
         ig = MI.downstream_impact(gr, torch.from_numpy(a).to(cuda), hops)
         ic = MI.downstream_impact(gr, torch.from_numpy(a), hops)
         np.testing.assert_allclose(ig.cpu().numpy(), ic.numpy(), rtol=1e-6)
+    seg = torch.from_numpy(rng.integers(0, 7, S).astype(np.int64))
+    mg = MI.segment_max(torch.from_numpy(a).to(cuda), seg.to(cuda), 9).cpu().numpy()
+    mc = MI.segment_max(torch.from_numpy(a), seg, 9).numpy()
+    np.testing.assert_array_equal(mg, mc)
+    assert mg[7] == 0 and mg[8] == 0
 
 
 @pytest.mark.gpu
