@@ -21,16 +21,28 @@ using namespace fm;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// RNE float -> bf16 on the hardware converter (v_cvt_pk_bf16_f32 on gfx950)
 __device__ __forceinline__ unsigned short f2bf(float f) {
-  unsigned u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+  const __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
 }
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, v);
+}
+// Gate nonlinearities on the transcendental unit, 2 transcendentals each:
+//   sigm(x) = 1 / (1 + 2^(-x log2 e))          v_mul, v_exp, v_add, v_rcp
+//   tanh(x) = 2 sigm(2x) - 1                    (+1 fma; saturates correctly
+//                                                 through exp -> inf/0)
+// A correctly rounded '/' would expand to a ~10-instruction
+// div_scale/div_fmas/div_fixup sequence; the cell update does 5 per unit per step.
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ float sigm(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -kLog2e));
+}
 __device__ __forceinline__ float tanh_f(float x) {
-  const float e = __expf(-2.f * fabsf(x));
-  const float t = (1.f - e) / (1.f + e);
-  return copysignf(t, x);
+  return 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * (-2.f * kLog2e))) - 1.f;
 }
 
 union Frag {
@@ -79,22 +91,31 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const float* __restrict
       }
   __syncthreads();
 
-  int cur = 0;
-  for (int t = 0; t < L; ++t) {
-    // augmented operand: x_t features (h == 0 lanes: k = 0..7; h == 1: k = 8..15), bias "1" at k = I
-    Frag xb[2];
+  // x_t of this lane's features (h == 0 lanes: k = 0..7; h == 1: k = 8..15) is
+  // loaded one step ahead so the global-memory latency hides behind the
+  // previous step's MFMAs instead of stalling the head of every step.
+  float xn[2][8];
+  auto load_x = [&](int tt) {
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       const int64_t bb = b0 + 32 * ct + col;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 8 * h + j;
-        float v = 0.f;
-        if (k < I && bb < B) v = x[(bb * L + t) * I + k];
-        else if (k == I) v = 1.f;
-        xb[ct].s[j] = f2bf(v);
+        xn[ct][j] = (k < I && bb < B && tt < L) ? x[(bb * L + tt) * I + k] : 0.f;
       }
     }
+  };
+  load_x(0);
+  int cur = 0;
+  for (int t = 0; t < L; ++t) {
+    // augmented operand: x_t features, bias "1" at k = I
+    Frag xb[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xb[ct].s[j] = f2bf(8 * h + j == I ? 1.f : xn[ct][j]);
+    load_x(t + 1);
     f32x16 acc[2][2];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
@@ -124,7 +145,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const float* __restrict
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        unsigned short hv[4];
+        float hv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float ig = sigm(acc[rt][ct][j]);
@@ -134,7 +155,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const float* __restrict
           const float cc = fg * c[rt][ct][j] + ig * gg;
           c[rt][ct][j] = cc;
           const float hh = og * tanh_f(cc);
-          hv[j] = f2bf(hh);
+          hv[j] = hh;
           if (t == L - 1) {
             const int64_t bb = b0 + 32 * ct + col;
             const int u = 16 * w + 8 * rt + 4 * h + j;
@@ -143,8 +164,8 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const float* __restrict
         }
         const int u0 = 16 * w + 8 * rt + 4 * h;
         uint2 pk;
-        pk.x = (unsigned)hv[0] | ((unsigned)hv[1] << 16);
-        pk.y = (unsigned)hv[2] | ((unsigned)hv[3] << 16);
+        pk.x = pack_bf2(hv[0], hv[1]);
+        pk.y = pack_bf2(hv[2], hv[3]);
         *reinterpret_cast<uint2*>(&hbuf[nxt][(32 * ct + col) * HP + u0]) = pk;
         if (hseq != nullptr) {
           const int64_t bb = b0 + 32 * ct + col;
