@@ -216,7 +216,7 @@ def recording_rules() -> dict:
 
 # --------------------------------------------------------------------------- workloads
 def _env(d: dict) -> list[dict]:
-    return [{"name": k, "value": str(v)} for k, v in d.items()]
+    return [{"name": k, "value": f"{v:g}" if isinstance(v, float) else str(v)} for k, v in d.items()]
 
 
 def _deployment(name: str, containers: list[dict], sa: str | None = None, volumes=None, node_selector=None) -> dict:

@@ -1,0 +1,149 @@
+"""Deploy bundle (generated CRDs/RBAC/rules), CLI watch/unwatch/status/validate
+against the fake API server, and the fault-injection demo workload."""
+import asyncio
+import os
+import random
+import subprocess
+
+import pytest
+import yaml
+from fastapi.testclient import TestClient
+
+from foremast_amd import cli
+from foremast_amd.api import crd
+from foremast_amd.controller import kube as K
+from foremast_amd.deploy import manifests as MF
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_committed_bundle_is_up_to_date(tmp_path):
+    MF.write(str(tmp_path))
+    for name in MF.bundle():
+        assert open(tmp_path / name).read() == open(os.path.join(ROOT, "deploy/foremast", name)).read(), name
+
+
+def test_crd_schema_covers_wire_types():
+    docs = MF.bundle()["10-crds.yaml"]
+    mon = next(d for d in docs if d["spec"]["names"]["kind"] == "DeploymentMonitor")
+    s = mon["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]
+    assert set(s["spec"]["properties"]) == set(crd.field_list(crd.DeploymentMonitorSpec()))
+    assert set(s["status"]["properties"]) == set(crd.field_list(crd.DeploymentMonitorStatus()))
+    assert s["status"]["properties"]["hpaLogs"]["nullable"] is True
+    anomaly = s["status"]["properties"]["anomaly"]["properties"]["anomalousMetrics"]["items"]
+    assert anomaly["properties"]["values"]["items"]["properties"]["time"]["type"] == "integer"
+    m = crd.monitor_new("demo", "default")
+    m.spec.continuous = True
+    m.status.phase = crd.PHASE_UNHEALTHY
+    m.status.anomaly.anomalous_metrics = [crd.AnomalousMetric("error5xx", "", [crd.AnomalousMetricValue(1, 2.5)])]
+    assert cli.validate_docs([m.to_dict()]) == []
+    bad = m.to_dict()
+    bad["spec"]["continuous"] = "yes"
+    bad["status"]["bogus"] = 1
+    errs = cli.validate_docs([bad])
+    assert any("continuous" in e for e in errs) and any("bogus" in e for e in errs)
+
+
+def test_default_metadata_and_rules():
+    md = crd.DeploymentMetadata.from_dict(MF.default_metadata())
+    assert md.name == "spring-boot" and md.spec.metrics.monitoring[0].metric_alias == "error5xx"
+    assert cli.validate_docs([MF.default_metadata()]) == []
+    rules = [r["record"] for g in MF.recording_rules()["spec"]["groups"] for r in g["rules"]]
+    for must in ("namespace_app_pod_http_server_requests_errors_5xx", "namespace_app_pod_http_server_requests_latency",
+                 "namespace_app_pod_cpu_utilization", "namespace_pod_cpu_usage_seconds_total",
+                 "namespace_app_pod_count", "namespace_app_caller_http_server_requests_rate"):
+        assert must in rules
+    env = {e["name"]: e["value"] for e in MF.brain()[0]["spec"]["template"]["spec"]["containers"][1]["env"]}
+    assert env["ML_ALGORITHM"] == "moving_average_all" and env["metric_type2"] == "latency"
+    assert env["threshold2"] == "10" and env["MIN_KRUSKAL_DATA_POINTS"] == "5"
+    # the brain env round-trips through BrainConfig.from_env
+    from foremast_amd.config import BrainConfig
+    c = BrainConfig.from_env(env)
+    assert c.rule_for("latency").threshold == 10 and c.rule_for("latency").bound == 3
+
+
+def test_cli_watch_unwatch_status():
+    kube = K.FakeKube()
+    m = crd.monitor_new("demo", "default")
+    m.status.phase = crd.PHASE_RUNNING
+    kube.create(K.MONITORS, "default", m.to_dict())
+    cli.set_continuous(kube, "default", "demo", True)
+    assert kube.get(K.MONITORS, "default", "demo")["spec"]["continuous"] is True
+    st = cli.monitor_status(kube, "default", "demo")
+    assert st["phase"] == "Running" and st["continuous"] is True
+    cli.set_continuous(kube, "default", "demo", False)
+    assert not kube.get(K.MONITORS, "default", "demo")["spec"].get("continuous")
+
+
+def test_kubectl_plugins_patch_continuous(tmp_path):
+    fake = tmp_path / "kubectl"
+    fake.write_text('#!/bin/bash\necho "$@" > "$(dirname "$0")/args"\n')
+    fake.chmod(0o755)
+    env = dict(os.environ, PATH=f"{tmp_path}:{os.environ['PATH']}")
+    out = subprocess.run([os.path.join(ROOT, "bin/kubectl-watch"), "demo", "-n", "prod"], env=env,
+                         capture_output=True, text=True, check=True).stdout
+    assert "starts watching application demo" in out
+    args = (tmp_path / "args").read_text()
+    assert args.startswith("patch deploymentmonitor demo --type=merge") and '"continuous":true' in args
+    assert args.strip().endswith("-n prod")
+    subprocess.run([os.path.join(ROOT, "bin/kubectl-unwatch"), "demo"], env=env, check=True, capture_output=True)
+    assert '"continuous":false' in (tmp_path / "args").read_text()
+
+
+# --------------------------------------------------------------------------- demo
+def test_demo_app_endpoints_and_metrics():
+    from foremast_amd.demo.app import create_demo_app
+    from foremast_amd.emitter.metrics import K8sMetrics, K8sMetricsProperties
+
+    async def no_sleep(_):
+        return None
+    app = create_demo_app(K8sMetrics(K8sMetricsProperties(), env={"APP_NAME": "demo"}), random.Random(1), no_sleep)
+    c = TestClient(app)
+    assert c.get("/load", params={"latency": 5, "errorRate": 0}).text == "OK"
+    codes = [c.get("/load", params={"latency": 5, "errorRate": 0.5}).status_code for _ in range(200)]
+    assert 60 < codes.count(501) < 140
+    assert c.get("/error5xx").status_code == 501
+    assert c.get("/pushSome").text.startswith("Done:")
+    n = len(app.queue.items)
+    app.queue.drain_quarter()
+    assert len(app.queue.items) == n - n // 4
+    text = c.get("/actuator/prometheus").text
+    assert 'http_server_requests_seconds_count{app="demo",caller="",method="GET",status="501",uri="/load"}' in text
+    assert "k8s_metrics_demo_queue_size" in text
+
+
+def test_demo_generators():
+    from foremast_amd.demo.app import (DEFAULT_PROFILE, ErrorGenerator, FileErrorGenerator, LoadGenerator,
+                                       parse_profile)
+    urls = []
+
+    async def req(u):
+        urls.append(u)
+        return 200
+
+    async def no_sleep(_):
+        return None
+    prof = parse_profile(DEFAULT_PROFILE)
+    assert prof[3].traffic == 40 and prof[0].error == pytest.approx(0.0166)
+    lg = LoadGenerator(req, prof[:2], segment_seconds=3, sleep=no_sleep)
+    asyncio.run(lg.run(cycles=1))
+    assert lg.sent == (10 + 10) * 3 and urls[0].startswith("http://localhost:8080/load?latency=166.0&errorRate=")
+    urls.clear()
+    eg = ErrorGenerator(req, 5, "4xx", sleep=no_sleep)
+    asyncio.run(eg.run(7))
+    assert eg.sent == 7 and urls[0].endswith("/not_existed?t=")
+    urls.clear()
+    fg = FileErrorGenerator(req, "2014-02-15 03:00:00,0.5\n2014-02-15 03:05:00,0.0\n2014-02-15 03:10:00,2.5\n",
+                            sleep=no_sleep)
+    asyncio.run(fg.run())
+    assert fg.sent == 1 + 15 * 3 and all(u.endswith("/error5xx?t=") for u in urls)
+
+
+def test_cli_help_and_manifests(tmp_path, capsys):
+    assert cli.main([]) == 0
+    assert cli.main(["manifests", str(tmp_path)]) == 0
+    assert (tmp_path / "10-crds.yaml").exists()
+    docs = list(yaml.safe_load_all(open(tmp_path / "21-deployment-metadata-default.yaml")))
+    p = tmp_path / "md.yaml"
+    p.write_text(yaml.safe_dump_all(docs))
+    assert cli.main(["validate", str(p)]) == 0
