@@ -306,8 +306,12 @@ class Brain:
             lo = res["lower"][gi][:max(n, 1)]
             if self.exporter is not None and n:
                 last = int(np.nonzero(np.isfinite(r.cur))[0][-1]) if np.isfinite(r.cur).any() else n - 1
-                anom_v = float(r.cur[last]) if flags[last] else float("nan")
-                self.exporter.set_bounds(r.base_metric, ns, app, float(up[last]), float(lo[last]), anom_v)
+                # the _anomaly gauge carries the unix time of the newest anomalous
+                # point (the dashboard reads anomaly VALUES as timestamps and marks
+                # the base series there: foremast-dashboard/src/reducers/metricReducer.js:77-102)
+                fl = np.nonzero(flags[:n])[0] if flags.any() else []
+                anom_ts = float(r.cur_t[fl[-1]]) if len(fl) and len(r.cur_t) > fl[-1] else float("nan")
+                self.exporter.set_bounds(r.base_metric, ns, app, float(up[last]), float(lo[last]), anom_ts)
             if flags.any():
                 idx = np.nonzero(flags)[0]
                 ts = [float(r.cur_t[k]) for k in idx]

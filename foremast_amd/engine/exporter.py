@@ -5,6 +5,9 @@
   ``namespace``, ``app`` (Prometheus re-labels ``namespace`` to
   ``exported_namespace`` on scrape, which is what the dashboard queries:
   foremast-dashboard/src/config/metrics.js:12-101);
+* ``_anomaly`` holds the unix time of the newest anomalous point (the
+  reference dashboard reads anomaly values as timestamps:
+  foremast-dashboard/src/reducers/metricReducer.js:77-102);
 * the HPA score gauge ``namespace_app_pod_hpa_score`` (HpaController.go:98;
   exposed to the HPA through deploy/custom-metrics/custom-metrics-config-map.yaml:27-35);
 * engine self-metrics: per-tick latency histogram, jobs processed, windows scored.
@@ -52,7 +55,8 @@ class BrainExporter:
         b = "foremastbrain:" + sanitize(base_metric)
         self._gauge(b + "_upper", "upper bound").labels(namespace, app).set(upper)
         self._gauge(b + "_lower", "lower bound").labels(namespace, app).set(lower)
-        self._gauge(b + "_anomaly", "anomalous value (NaN when none)").labels(namespace, app).set(anomaly)
+        self._gauge(b + "_anomaly", "unix time of the newest anomalous point (NaN when none)").labels(
+            namespace, app).set(anomaly)
 
     def set_hpa_score(self, namespace: str, app: str, score: float) -> None:
         self._gauge(self.HPA_SCORE, "foremast HPA score [0,100], 50 = hold").labels(namespace, app).set(score)

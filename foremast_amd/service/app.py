@@ -120,6 +120,31 @@ def create_app(store: JobStore | None = None, cfg: ServiceConfig | None = None, 
                for d in store.all_docs() if status is None or d.status == status]
         return JSONResponse(out)
 
+    # ------------------------------------------------------------ dashboard (R19)
+    async def _prom_range(q: str, start: int, end: int, step: int) -> dict:
+        import urllib.parse
+        url = cfg.query_endpoint + "api/v1/query_range?" + urllib.parse.urlencode(
+            {"query": q, "start": start, "end": end, "step": step})
+        try:
+            client = http_client or httpx.AsyncClient(timeout=30.0)
+            r = await client.get(url)
+            if http_client is None:
+                await client.aclose()
+            return r.json()
+        except Exception:
+            return {}
+
+    @app.get("/dashboard/api/{namespace}/{app_name}")
+    async def dashboard_api(namespace: str, app_name: str, minutes: int = 15):
+        from ..dashboard.data import dashboard_data_async
+        return JSONResponse(await dashboard_data_async(_prom_range, namespace, app_name, minutes=minutes))
+
+    @app.get("/dashboard/{namespace}/{app_name}")
+    async def dashboard_page(namespace: str, app_name: str):
+        from fastapi.responses import HTMLResponse
+        from ..dashboard.page import render
+        return HTMLResponse(render(namespace, app_name))
+
     @app.get("/healthz")
     async def healthz():
         return PlainTextResponse("ok")
