@@ -21,32 +21,135 @@ namespace fm {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (FM_WAVE - 1); }
 __device__ __forceinline__ int wave_id() { return threadIdx.x / FM_WAVE; }
 
+// ---------------------------------------------------------------------------
+// Cross-lane primitives without the LDS crossbar.  __shfl_xor lowers to
+// ds_bpermute_b32 (an LDS-pipe round trip per exchange); inside a 16-lane row
+// DPP does the same exchange as a VALU operand modifier, and the gfx950
+// v_permlane16_swap / v_permlane32_swap move whole rows / half-waves:
+//   xor 1, 2  quad_perm [1,0,3,2] / [2,3,0,1]
+//   xor 4     row_shl:4 for lanes with bit 2 clear, row_shr:4 otherwise
+//   xor 8     row_ror:8 (a rotate by half a row IS the xor)
+//   xor 16    permlane16_swap(v, v): rows {r0,r0,r2,r2} / {r1,r1,r3,r3}
+//   xor 32    permlane32_swap(v, v): halves {lo,lo} / {hi,hi}
+// ---------------------------------------------------------------------------
+template <int S>
+__device__ __forceinline__ unsigned xor_lane_u32(unsigned v) {
+  if constexpr (S == 1) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  } else if constexpr (S == 2) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  } else if constexpr (S == 4) {
+    const unsigned up = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, false);
+    const unsigned dn = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    return (lane_id() & 4) ? dn : up;
+  } else if constexpr (S == 8) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+  } else if constexpr (S == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane_id() & 16) ? r[0] : r[1];
+  } else {
+    static_assert(S == 32, "xor stride must be a power of two < 64");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane_id() & 32) ? r[0] : r[1];
+  }
+}
+
+// DPP move with compile-time control; lanes whose source is invalid get `old`.
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_mov(T old, T x) {
+  static_assert(sizeof(T) == 4, "32-bit");
+  return __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_update_dpp(
+      (int)__builtin_bit_cast(unsigned, old), (int)__builtin_bit_cast(unsigned, x), CTRL, 0xF, 0xF, false));
+}
+
+template <int S, typename T>
+__device__ __forceinline__ T xor_lane(T v) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit lanes only");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, xor_lane_u32<S>(__builtin_bit_cast(unsigned, v)));
+  } else {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = xor_lane_u32<S>((unsigned)u), hi = xor_lane_u32<S>((unsigned)(u >> 32));
+    return __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
+  }
+}
+
+// Runtime-stride form for unrolled loops (the switch folds to one case).
+template <typename T>
+__device__ __forceinline__ T xor_lane_any(T v, int s) {
+  switch (s) {
+    case 1: return xor_lane<1>(v);
+    case 2: return xor_lane<2>(v);
+    case 4: return xor_lane<4>(v);
+    case 8: return xor_lane<8>(v);
+    case 16: return xor_lane<16>(v);
+    default: return xor_lane<32>(v);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v += xor_lane<1>(v); v += xor_lane<2>(v); v += xor_lane<4>(v);
+  v += xor_lane<8>(v); v += xor_lane<16>(v); v += xor_lane<32>(v);
   return v;
 }
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o); v = v > w ? v : w; }
+  T w;
+  w = xor_lane<1>(v); v = v > w ? v : w;
+  w = xor_lane<2>(v); v = v > w ? v : w;
+  w = xor_lane<4>(v); v = v > w ? v : w;
+  w = xor_lane<8>(v); v = v > w ? v : w;
+  w = xor_lane<16>(v); v = v > w ? v : w;
+  w = xor_lane<32>(v); v = v > w ? v : w;
   return v;
 }
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { T w = __shfl_xor(v, o); v = v < w ? v : w; }
+  T w;
+  w = xor_lane<1>(v); v = v < w ? v : w;
+  w = xor_lane<2>(v); v = v < w ? v : w;
+  w = xor_lane<4>(v); v = v < w ? v : w;
+  w = xor_lane<8>(v); v = v < w ? v : w;
+  w = xor_lane<16>(v); v = v < w ? v : w;
+  w = xor_lane<32>(v); v = v < w ? v : w;
   return v;
 }
 
-// Inclusive prefix sum over the 64 lanes of a wave.
+// Inclusive prefix scans over the 64 lanes (Hillis-Steele: row_shr 1,2,4,8
+// inside each 16-lane row, then the row totals carried by permlane swaps).
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan_dpp(T v, T ident, Op op) {
+  static_assert(sizeof(T) == 4, "32-bit scans");
+  const int l = lane_id();
+  v = op(v, dpp_mov<0x111>(ident, v));  // row_shr:1 (lanes with l%16 < 1 read the identity)
+  v = op(v, dpp_mov<0x112>(ident, v));
+  v = op(v, dpp_mov<0x114>(ident, v));
+  v = op(v, dpp_mov<0x118>(ident, v));
+  // row r's total sits in lane 16r+15; carry row 0 -> 1 and row 2 -> 3
+  const T t15 = __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned, v), 15));
+  const T t47 = __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned, v), 47));
+  if ((l >> 4) == 1) v = op(v, t15);
+  if ((l >> 4) == 3) v = op(v, t47);
+  const T t31 = __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned, v), 31));
+  if (l >= 32) v = op(v, t31);
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_incl_sum(T v) {
-  const int l = lane_id();
+  if constexpr (sizeof(T) == 4) {
+    return wave_incl_scan_dpp(v, (T)0, [](T a, T b) { return a + b; });
+  } else {
+    const int l = lane_id();
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) { T w = __shfl_up(v, o); if (l >= o) v += w; }
-  return v;
+    for (int o = 1; o < 64; o <<= 1) { T w = __shfl_up(v, o); if (l >= o) v += w; }
+    return v;
+  }
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_max(T v, T ident) {
+  return wave_incl_scan_dpp(v, ident, [](T a, T b) { return a > b ? a : b; });
 }
 template <typename T>
 __device__ __forceinline__ T wave_incl_max(T v) {
@@ -55,6 +158,41 @@ __device__ __forceinline__ T wave_incl_max(T v) {
   for (int o = 1; o < 64; o <<= 1) { T w = __shfl_up(v, o); if (l >= o) v = v > w ? v : w; }
   return v;
 }
+// Inclusive suffix scan, 32-bit (row_shl 1,2,4,8 inside rows, then row totals
+// carried downward through readlane of each row's first lane).
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_suffix_scan_dpp(T v, T ident, Op op) {
+  static_assert(sizeof(T) == 4, "32-bit scans");
+  const int l = lane_id();
+  v = op(v, dpp_mov<0x101>(ident, v));  // row_shl:1 (lane i reads i+1 inside the row)
+  v = op(v, dpp_mov<0x102>(ident, v));
+  v = op(v, dpp_mov<0x104>(ident, v));
+  v = op(v, dpp_mov<0x108>(ident, v));
+  const T t16 = __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned, v), 16));
+  const T t48 = __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned, v), 48));
+  if ((l >> 4) == 0) v = op(v, t16);
+  if ((l >> 4) == 2) v = op(v, t48);
+  const T t32 = __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned, v), 32));
+  if (l < 32) v = op(v, t32);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_suffix_min(T v, T ident) {
+  return wave_incl_suffix_scan_dpp(v, ident, [](T a, T b) { return a < b ? a : b; });
+}
+
+// Neighbour lanes across the whole wave (gfx9 DPP wave_shr:1 / wave_shl:1);
+// lane 0 (resp. 63) receives `edge`.
+template <typename T>
+__device__ __forceinline__ T lane_prev(T v, T edge) { return dpp_mov<0x138>(edge, v); }
+template <typename T>
+__device__ __forceinline__ T lane_next(T v, T edge) { return dpp_mov<0x130>(edge, v); }
+template <typename T>
+__device__ __forceinline__ T lane_bcast(T v, int lane) {
+  static_assert(sizeof(T) == 4, "32-bit");
+  return __builtin_bit_cast(T, (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(unsigned, v), lane));
+}
+
 // Inclusive suffix min (lane l sees min over lanes l..63).
 template <typename T>
 __device__ __forceinline__ T wave_incl_suffix_min(T v) {

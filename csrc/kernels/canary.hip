@@ -50,8 +50,8 @@ __device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const int i = k * 64 + lane;
-          const float ov = __shfl_xor(v[k], stride);
-          const int ot = __shfl_xor(tag[k], stride);
+          const float ov = xor_lane_any(v[k], stride);
+          const int ot = xor_lane_any(tag[k], stride);
           const bool asc = (i & size) == 0;
           const bool lower = (lane & stride) == 0;
           const bool take = lower ? (asc ? ov < v[k] : ov > v[k]) : (asc ? ov > v[k] : ov < v[k]);
@@ -75,15 +75,14 @@ __device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&ra
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int i = k * 64 + lane;
-    float prev = __shfl_up(v[k], 1);
-    if (lane == 0) prev = last_prev;
+    const float prev = lane_prev(v[k], last_prev);
     const bool st = (i == 0) || (v[k] != prev);
     int s = st ? i : 0;
-    s = wave_incl_max(s);
+    s = wave_incl_max(s, 0);
     s = s > carry ? s : carry;
     start_idx[k] = s;
-    carry = __shfl(s, 63);
-    last_prev = __shfl(v[k], 63);
+    carry = lane_bcast(s, 63);
+    last_prev = lane_bcast(v[k], 63);
   }
   int carry_e = 0x7fffffff;
   float next_first = 0.f;
@@ -91,14 +90,13 @@ __device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&ra
 #pragma unroll
   for (int k = K - 1; k >= 0; --k) {
     const int i = k * 64 + lane;
-    float next = __shfl_down(v[k], 1);
-    if (lane == 63) next = next_first;
+    const float next = lane_next(v[k], next_first);
     const bool en = (i < n) && ((i == n - 1) || (v[k] != next));
     int e = en ? i : 0x7fffffff;
-    e = wave_incl_suffix_min(e);
+    e = wave_incl_suffix_min(e, 0x7fffffff);
     e = e < carry_e ? e : carry_e;
-    carry_e = __shfl(e, 0);
-    next_first = __shfl(v[k], 0);
+    carry_e = lane_bcast(e, 0);
+    next_first = lane_bcast(v[k], 0);
     is_end[k] = en;
     rank[k] = 0.5f * (float)(start_idx[k] + e) + 1.0f;
     if (i < n && i == start_idx[k]) {
@@ -190,8 +188,8 @@ __global__ __launch_bounds__(256) void pairwise_kernel(
     // KS: inclusive prefix counts of each sample along the sorted order
     const int a1 = wave_incl_sum(tag[k] == 0 ? 1 : 0) + base1;
     const int a2 = wave_incl_sum(tag[k] == 1 ? 1 : 0) + base2;
-    base1 = __shfl(a1, 63);
-    base2 = __shfl(a2, 63);
+    base1 = lane_bcast(a1, 63);
+    base2 = lane_bcast(a2, 63);
     if (en[k] && n1 > 0 && n2 > 0) {
       const double dd = fabs((double)a1 / n1 - (double)a2 / n2);
       dmax = dd > dmax ? dd : dmax;
@@ -793,6 +791,35 @@ FM_API int fm_synth_fleet(float* out, int64_t ld, int64_t n_per_row, int64_t S, 
   if (S <= 0) return 0;
   hipLaunchKernelGGL(synth_kernel, dim3(2048), dim3(256), 0, stream, out, ld, n_per_row, S, M, svc0, T, P, W, kind,
                      fault_rate, fault_mag, seed);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Self-test of the cross-lane primitives (one wave): the DPP / permlane-swap
+// encodings are checked against their definitions by tests/test_canary_ops.py.
+// out [12][64]: xor 1,2,4,8,16,32 | incl sum | incl max | suffix min | prev |
+// next | wave sum
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void selftest_lanes_kernel(const int* __restrict__ in, int* __restrict__ out) {
+  const int l = lane_id();
+  const int v = in[l];
+  out[0 * 64 + l] = xor_lane<1>(v);
+  out[1 * 64 + l] = xor_lane<2>(v);
+  out[2 * 64 + l] = xor_lane<4>(v);
+  out[3 * 64 + l] = xor_lane<8>(v);
+  out[4 * 64 + l] = xor_lane<16>(v);
+  out[5 * 64 + l] = xor_lane<32>(v);
+  out[6 * 64 + l] = wave_incl_sum(v);
+  out[7 * 64 + l] = wave_incl_max(v, (int)0x80000000);
+  out[8 * 64 + l] = wave_incl_suffix_min(v, 0x7fffffff);
+  out[9 * 64 + l] = lane_prev(v, -1);
+  out[10 * 64 + l] = lane_next(v, -2);
+  out[11 * 64 + l] = wave_sum(v);
+}
+
+FM_API int fm_selftest_lanes(const int* in, int* out, hipStream_t stream) {
+  hipLaunchKernelGGL(selftest_lanes_kernel, dim3(1), dim3(64), 0, stream, in, out);
   FM_LAUNCH_CHECK();
   return 0;
 }

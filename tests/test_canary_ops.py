@@ -218,3 +218,24 @@ def test_gpu_two_stream_tick_equals_single_stream(cuda):
     torch.testing.assert_close(o.decide.stats, a.decide.stats)
     g = s2.capture(h, b, c, 10080)().packed.clone()
     torch.testing.assert_close(g, a.packed)
+
+
+@pytest.mark.gpu
+def test_gpu_cross_lane_primitives(cuda):
+    """DPP / permlane-swap exchanges and scans against their definitions."""
+    from foremast_amd.ops._lib import LIB, ptr, stream_of
+    rng = np.random.default_rng(0)
+    v = rng.integers(-1000, 1000, 64).astype(np.int32)
+    x = torch.from_numpy(v).to(cuda)
+    out = torch.empty((12, 64), dtype=torch.int32, device=cuda)
+    LIB.call("fm_selftest_lanes", ptr(x), ptr(out), stream_of(x))
+    o = out.cpu().numpy()
+    lanes = np.arange(64)
+    for k, s in enumerate((1, 2, 4, 8, 16, 32)):
+        np.testing.assert_array_equal(o[k], v[lanes ^ s], err_msg=f"xor {s}")
+    np.testing.assert_array_equal(o[6], np.cumsum(v))
+    np.testing.assert_array_equal(o[7], np.maximum.accumulate(v))
+    np.testing.assert_array_equal(o[8], np.minimum.accumulate(v[::-1])[::-1])
+    np.testing.assert_array_equal(o[9], np.concatenate([[-1], v[:-1]]))
+    np.testing.assert_array_equal(o[10], np.concatenate([v[1:], [-2]]))
+    np.testing.assert_array_equal(o[11], np.full(64, v.sum()))
