@@ -50,7 +50,9 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=5)
     ap.add_argument("--window", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true", help="single-stream tick (A/B of the two-stream fork/join)")
+    ap.add_argument("--mode", choices=["fused", "overlap", "serial"], default="fused",
+                    help="tick structure: fused row kernel (default), two-stream fork/join, or serial")
+    ap.add_argument("--no-overlap", action="store_true", help="alias of --mode serial")
     args = ap.parse_args()
 
     info = D.env_info()
@@ -70,7 +72,8 @@ def main() -> None:
     hist, base, cur = C.synth_fleet(s_pad, M, args.hist, args.pods, args.window, svc0, device=dev)
     cfg = BrainConfig()
     cfg.min_historical_points = 10
-    scorer = CanaryScorer(aliases, cfg, device=dev, overlap=not args.no_overlap)
+    mode = "serial" if args.no_overlap else args.mode
+    scorer = CanaryScorer(aliases, cfg, device=dev, mode=mode)
     gathered = torch.empty((world * s_pad, 4), dtype=torch.float32, device=dev)
     host = torch.empty((world * s_pad, 4), dtype=torch.float32, pin_memory=True)
 
@@ -130,7 +133,7 @@ def main() -> None:
                 "current_points_per_window": args.pods * args.window,
                 "parallelism": f"dp{world}",
                 "hip_graph": not args.no_graph,
-                "two_stream_overlap": not args.no_overlap,
+                "tick_mode": mode,
             },
             "services_flagged": n_anom,
         }

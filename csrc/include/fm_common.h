@@ -34,16 +34,18 @@ __device__ __forceinline__ int wave_id() { return threadIdx.x / FM_WAVE; }
 // ---------------------------------------------------------------------------
 template <int S>
 __device__ __forceinline__ unsigned xor_lane_u32(unsigned v) {
+  // mov_dpp (no "old" operand): every lane we keep has a valid source, so
+  // no v_mov to pre-initialise the destination is needed
   if constexpr (S == 1) {
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
   } else if constexpr (S == 2) {
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);
   } else if constexpr (S == 4) {
-    const unsigned up = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, false);
-    const unsigned dn = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    const unsigned up = (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xF, 0xF, true);
+    const unsigned dn = (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true);
     return (lane_id() & 4) ? dn : up;
   } else if constexpr (S == 8) {
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+    return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true);
   } else if constexpr (S == 16) {
     const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
     return (lane_id() & 16) ? r[0] : r[1];

@@ -26,6 +26,9 @@ constexpr float kPad = INFINITY;
 
 template <int K>
 __device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
+  // Branch-free compare-exchange (selects, no exec-mask branches): strides
+  // >= 64 swap registers inside the lane, smaller strides exchange with the
+  // partner lane through DPP / permlane (xor_lane_any).
   const int lane = lane_id();
 #pragma unroll
   for (int size = 2; size <= 64 * K; size <<= 1) {
@@ -39,23 +42,34 @@ __device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
           if (p > k) {
             const int i = k * 64 + lane;
             const bool asc = (i & size) == 0;
-            const bool sw = asc ? (v[k] > v[p]) : (v[k] < v[p]);
-            if (sw) {
-              float tv = v[k]; v[k] = v[p]; v[p] = tv;
-              int tt = tag[k]; tag[k] = tag[p]; tag[p] = tt;
-            }
+            const float a = v[k], b = v[p];
+            const int ta = tag[k], tb = tag[p];
+            const bool alt = a < b;
+            const float mn = alt ? a : b, mx = alt ? b : a;
+            const int tmn = alt ? ta : tb, tmx = alt ? tb : ta;
+            v[k] = asc ? mn : mx; v[p] = asc ? mx : mn;
+            tag[k] = asc ? tmn : tmx; tag[p] = asc ? tmx : tmn;
           }
         }
       } else {
+        float ov[K];
+        int ot[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) { ov[k] = xor_lane_any(v[k], stride); ot[k] = xor_lane_any(tag[k], stride); }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const int i = k * 64 + lane;
-          const float ov = xor_lane_any(v[k], stride);
-          const int ot = xor_lane_any(tag[k], stride);
           const bool asc = (i & size) == 0;
           const bool lower = (lane & stride) == 0;
-          const bool take = lower ? (asc ? ov < v[k] : ov > v[k]) : (asc ? ov > v[k] : ov < v[k]);
-          if (take) { v[k] = ov; tag[k] = ot; }
+          // keep the smaller value in the lower lane of an ascending pair
+          const bool keep_min = lower == asc;
+          // select min or max of the pair; the tag follows only when the value
+          // actually moved (equal values keep their own tags on both lanes)
+          const bool vlt = v[k] < ov[k];
+          const float mn = vlt ? v[k] : ov[k], mx = vlt ? ov[k] : v[k];
+          const float nv = keep_min ? mn : mx;
+          tag[k] = nv != v[k] ? ot[k] : tag[k];
+          v[k] = nv;
         }
       }
     }
@@ -66,8 +80,10 @@ __device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
 // real.  tie_term accumulates sum(t^3 - t) over tie runs; is_end marks the last
 // element of each run (where empirical CDFs are evaluated).
 template <int K>
-__device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&rank)[K], bool (&is_end)[K],
-                                          double& tie_term) {
+__device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, int (&rank2)[K], bool (&is_end)[K],
+                                          int& tie_term) {
+  // rank2 = 2 x (1-based average rank) = start + end + 2: exact integers, so
+  // rank sums and the tie term sum(t^3 - t) (<= 512^3) need no doubles.
   const int lane = lane_id();
   int start_idx[K];
   int carry = 0;
@@ -86,7 +102,7 @@ __device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&ra
   }
   int carry_e = 0x7fffffff;
   float next_first = 0.f;
-  double tl = 0.0;
+  int tl = 0;
 #pragma unroll
   for (int k = K - 1; k >= 0; --k) {
     const int i = k * 64 + lane;
@@ -98,9 +114,9 @@ __device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&ra
     carry_e = lane_bcast(e, 0);
     next_first = lane_bcast(v[k], 0);
     is_end[k] = en;
-    rank[k] = 0.5f * (float)(start_idx[k] + e) + 1.0f;
+    rank2[k] = start_idx[k] + e + 2;
     if (i < n && i == start_idx[k]) {
-      const double t = (double)(e - start_idx[k] + 1);
+      const int t = e - start_idx[k] + 1;
       tl += t * t * t - t;
     }
   }
@@ -112,112 +128,246 @@ __device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, float (&ra
 enum { T_MW = 0, T_WIL = 1, T_KRU = 2, T_KS = 3, T_T = 4, T_FRI = 5, N_TESTS = 6 };
 constexpr int kSuff = 14;
 
+// Per-row pairwise inputs, split into a LOAD half (raw samples into
+// registers, no arithmetic that would wait on them) and a COMPUTE half, so a
+// fused kernel can put other loads in flight between the two.
 template <int K>
-__global__ __launch_bounds__(256) void pairwise_kernel(
-    const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
-    int n_base, int64_t R, double* __restrict__ suff) {
-  const int lane = lane_id();
-  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
-  if (row >= R) return;  // wave-uniform exit
-  const float* c = cur + row * ld_c;
-  const float* b = base + row * ld_b;
+struct PwIn {
+  static constexpr int KW = (K + 1) / 2;
+  float v[K];     // pooled sample slot i = k*64 + lane: cur[i] (i < n_cur) or base[i - n_cur]
+  float pc[KW];   // position-paired cur[j], base[j] (Wilcoxon / Friedman)
+  float pb[KW];
+};
 
-  float v[K];
-  int tag[K];
-  double s1 = 0, s2 = 0;
-  int c1 = 0, c2 = 0;
+template <int K>
+__device__ __forceinline__ void pw_load(const float* __restrict__ c, const float* __restrict__ b, int n_cur,
+                                        int n_base, PwIn<K>& in) {
+  const int lane = lane_id();
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int i = k * 64 + lane;
-    float x = kPad;
-    int t = -1;
-    if (i < n_cur) { x = c[i]; t = 0; }
-    else if (i < n_cur + n_base) { x = b[i - n_cur]; t = 1; }
-    if (!isfinite(x)) { x = kPad; t = -1; }
-    v[k] = x; tag[k] = t;
-    if (t == 0) { s1 += x; ++c1; }
-    if (t == 1) { s2 += x; ++c2; }
+    in.v[k] = i < n_cur ? c[i] : (i < n_cur + n_base ? b[i - n_cur] : kPad);
   }
-  const int n1 = wave_sum(c1), n2 = wave_sum(c2);
-  const int n = n1 + n2;
-  const double m1 = wave_sum(s1) / (n1 > 0 ? n1 : 1), m2 = wave_sum(s2) / (n2 > 0 ? n2 : 1);
-  double q1 = 0, q2 = 0;
+  const int npair = n_cur < n_base ? n_cur : n_base;
+#pragma unroll
+  for (int k = 0; k < PwIn<K>::KW; ++k) {
+    const int j = k * 64 + lane;
+    in.pc[k] = j < npair ? c[j] : 0.f;
+    in.pb[k] = j < npair ? b[j] : 0.f;
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void pw_compute(PwIn<K>& in, int n_cur, int n_base, double* __restrict__ o) {
+  // Everything exact is carried in integers (counts, doubled rank sums, tie
+  // terms, the KS numerator); only the Welch moments are floating point.
+  const int lane = lane_id();
+  float (&v)[K] = in.v;
+  int tag[K];
+  float s1 = 0.f, s2 = 0.f;
+  int c12 = 0;  // n1 | n2 << 16
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    if (tag[k] == 0) { double d = v[k] - m1; q1 += d * d; }
-    if (tag[k] == 1) { double d = v[k] - m2; q2 += d * d; }
+    const int i = k * 64 + lane;
+    int t = i < n_cur ? 0 : (i < n_cur + n_base ? 1 : -1);
+    float x = v[k];
+    if (!isfinite(x)) { x = kPad; t = -1; }
+    v[k] = x; tag[k] = t;
+    if (t == 0) { s1 += x; c12 += 1; }
+    if (t == 1) { s2 += x; c12 += 1 << 16; }
+  }
+  c12 = wave_sum(c12);
+  const int n1 = c12 & 0xFFFF, n2 = c12 >> 16;
+  const int n = n1 + n2;
+  const float m1 = wave_sum(s1) / (float)(n1 > 0 ? n1 : 1), m2 = wave_sum(s2) / (float)(n2 > 0 ? n2 : 1);
+  float q1 = 0.f, q2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (tag[k] == 0) { const float d = v[k] - m1; q1 += d * d; }
+    if (tag[k] == 1) { const float d = v[k] - m2; q2 += d * d; }
   }
   q1 = wave_sum(q1); q2 = wave_sum(q2);
 
   // ---- Wilcoxon signed-rank on position-paired differences (zero_method='wilcox')
-  constexpr int KW = (K + 1) / 2;
+  constexpr int KW = PwIn<K>::KW;
   float dv[KW];
   int dt[KW];
   const int npair = n_cur < n_base ? n_cur : n_base;
-  int cw = 0, cpos = 0, cz = 0;
+  int cwz = 0;  // nonzero | positive << 10 | zero << 20 (each <= 512)
 #pragma unroll
   for (int k = 0; k < KW; ++k) {
     const int j = k * 64 + lane;
     float d = kPad;
     int t = -1;
     if (j < npair) {
-      const float xc = c[j], xb = b[j];
+      const float xc = in.pc[k], xb = in.pb[k];
       if (isfinite(xc) && isfinite(xb)) {
         const float dd = xc - xb;
-        if (dd != 0.f) { d = fabsf(dd); t = dd > 0.f ? 1 : 0; ++cw; cpos += t; }
-        else ++cz;
+        if (dd != 0.f) { d = fabsf(dd); t = dd > 0.f ? 1 : 0; cwz += 1 + (t << 10); }
+        else cwz += 1 << 20;
       }
     }
     dv[k] = d; dt[k] = t;
   }
-  const int nw = wave_sum(cw);
-  const int npos = wave_sum(cpos), nzero = wave_sum(cz);
+  cwz = wave_sum(cwz);
+  const int nw = cwz & 0x3FF, npos = (cwz >> 10) & 0x3FF, nzero = cwz >> 20;
 
   bitonic_sort<K>(v, tag);
-  float rk[K];
+  int rk2[K];
   bool en[K];
-  double tie = 0.0;
-  avg_ranks<K>(v, n, rk, en, tie);
+  int tie = 0;
+  avg_ranks<K>(v, n, rk2, en, tie);
 
-  double r1 = 0.0;
-  double dmax = 0.0;
-  int base1 = 0, base2 = 0;
+  int r1x2 = 0;
+  int dnum = 0;   // max |a1 n2 - a2 n1| over tie-run ends = D n1 n2
+  int base12 = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    if (tag[k] == 0) r1 += rk[k];
-    // KS: inclusive prefix counts of each sample along the sorted order
-    const int a1 = wave_incl_sum(tag[k] == 0 ? 1 : 0) + base1;
-    const int a2 = wave_incl_sum(tag[k] == 1 ? 1 : 0) + base2;
-    base1 = lane_bcast(a1, 63);
-    base2 = lane_bcast(a2, 63);
+    if (tag[k] == 0) r1x2 += rk2[k];
+    // KS: inclusive prefix counts of both samples along the sorted order, one packed scan
+    const int a12 = wave_incl_sum(tag[k] == 0 ? 1 : (tag[k] == 1 ? (1 << 16) : 0)) + base12;
+    base12 = lane_bcast(a12, 63);
     if (en[k] && n1 > 0 && n2 > 0) {
-      const double dd = fabs((double)a1 / n1 - (double)a2 / n2);
-      dmax = dd > dmax ? dd : dmax;
+      const int a1 = a12 & 0xFFFF, a2 = a12 >> 16;
+      const int dd = abs(a1 * n2 - a2 * n1);
+      dnum = dd > dnum ? dd : dnum;
     }
   }
-  r1 = wave_sum(r1);
-  dmax = wave_max(dmax);
+  r1x2 = wave_sum(r1x2);
+  dnum = wave_max(dnum);
 
   bitonic_sort<KW>(dv, dt);
-  float rw[KW];
+  int rw2[KW];
   bool ew[KW];
-  double tiew = 0.0;
-  avg_ranks<KW>(dv, nw, rw, ew, tiew);
-  double rplus = 0.0;
+  int tiew = 0;
+  avg_ranks<KW>(dv, nw, rw2, ew, tiew);
+  int rplus2 = 0;
 #pragma unroll
   for (int k = 0; k < KW; ++k)
-    if (dt[k] == 1) rplus += rw[k];
-  rplus = wave_sum(rplus);
+    if (dt[k] == 1) rplus2 += rw2[k];
+  rplus2 = wave_sum(rplus2);
 
   // Per-row sufficient statistics; p-values are evaluated one row per THREAD
   // by pvalue_kernel (the double-precision special functions would otherwise
   // run on lane 0 with 63 lanes idle).
   if (lane == 0) {
-    double* o = suff + row * kSuff;
-    o[0] = n1; o[1] = n2; o[2] = nw; o[3] = r1; o[4] = tie; o[5] = dmax;
-    o[6] = rplus; o[7] = tiew; o[8] = m1; o[9] = m2; o[10] = q1; o[11] = q2;
+    o[0] = n1; o[1] = n2; o[2] = nw; o[3] = 0.5 * r1x2; o[4] = tie;
+    o[5] = (n1 > 0 && n2 > 0) ? (double)dnum / ((double)n1 * n2) : 0.0;
+    o[6] = 0.5 * rplus2; o[7] = tiew; o[8] = m1; o[9] = m2; o[10] = q1; o[11] = q2;
     o[12] = npos; o[13] = nzero;
   }
+}
+
+// Grid-stride over rows: launched with one wave per row, or capped to a few
+// workgroups per CU so a concurrently running HBM-bound kernel keeps most of
+// the wave slots (two-stream tick).
+template <int K>
+__global__ __launch_bounds__(256) void pairwise_kernel(
+    const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
+    int n_base, int64_t R, double* __restrict__ suff) {
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave_id(); row < R; row += (int64_t)gridDim.x * 4) {
+    PwIn<K> in;
+    pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
+    pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused canary row kernel: ONE wave per (service, metric) row does both the
+// HBM-bound history statistics (mean / std / count over the 7-day row) and the
+// compute-bound pairwise rank tests.  Order inside the wave: the small
+// cur/base loads, then the whole history row (NQ float4 per lane, streamed,
+// non-temporal), then the pairwise compute runs while the history is still in
+// flight (vmcnt waits only for the first, small loads: in-order completion),
+// then the history is reduced from registers.  The separate two-stream form
+// (pairwise on a side stream || hist_stats) shares the CUs between two kernels
+// whose waves compete for slots; here each wave carries both.
+// ---------------------------------------------------------------------------
+template <int NQ, int K>
+__global__ __launch_bounds__(256) void canary_row_kernel(
+    const float* __restrict__ hist, int64_t ld_h, int T, const float* __restrict__ cur, int64_t ld_c, int n_cur,
+    const float* __restrict__ base, int64_t ld_b, int n_base, int64_t R, float* __restrict__ hs /*[R,3]*/,
+    double* __restrict__ suff) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
+  if (row >= R) return;
+  const int lane = lane_id();
+  const bool do_pw = n_base > 0;
+  PwIn<K> in;
+  if (do_pw) pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
+
+  typedef float nt4 __attribute__((ext_vector_type(4)));
+  const nt4* h = reinterpret_cast<const nt4*>(hist + row * ld_h);
+  const int nq = (T + 3) >> 2;
+  nt4 q[NQ];
+  // Unpredicated loads (index clamped into the row, surplus masked by e0 < T
+  // in the reduction): with exec-masked branches around them the waitcnt pass
+  // could not prove how many loads are outstanding and waited for all of them
+  // before the pairwise compute.
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    const int qi = lane + j * 64;
+    q[j] = __builtin_nontemporal_load(h + (qi < nq ? qi : nq - 1));
+  }
+
+  if (do_pw) pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+
+  float ls = 0.f;
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    const int e0 = (lane + j * 64) * 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = q[j][c];
+      if (e0 + c < T && isfinite(x)) { ls += x; ++cnt; }
+    }
+  }
+  const double tot = wave_sum((double)ls);
+  const int n = wave_sum(cnt);
+  const float mf = n > 0 ? (float)(tot / n) : 0.f;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    const int e0 = (lane + j * 64) * 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = q[j][c];
+      if (e0 + c < T && isfinite(x)) { const float d = x - mf; ss += d * d; }
+    }
+  }
+  const double sst = wave_sum((double)ss);
+  if (lane == 0) {
+    hs[row * 3 + 0] = mf;
+    hs[row * 3 + 1] = n > 0 ? (float)sqrt(sst / n) : 0.f;
+    hs[row * 3 + 2] = (float)n;
+  }
+}
+
+FM_API int fm_canary_rows(const float* hist, int64_t ld_h, int T, const float* cur, int64_t ld_c, int n_cur,
+                          const float* base, int64_t ld_b, int n_base, int64_t R, float* hs, double* suff,
+                          hipStream_t stream) {
+  if (R <= 0) return 0;
+  if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
+  const int nq = (T + 3) / 4;
+  const int n = n_cur + (n_base > 0 ? n_base : 0);
+  const dim3 grid((unsigned)((R + 3) / 4)), block(256);
+#define FM_CR(NQQ, KK) hipLaunchKernelGGL((canary_row_kernel<NQQ, KK>), grid, block, 0, stream, hist, ld_h, T, cur, \
+                                          ld_c, n_cur, base, ld_b, n_base, R, hs, suff)
+#define FM_CR_K(NQQ)              \
+  if (n <= 64) FM_CR(NQQ, 1);     \
+  else if (n <= 128) FM_CR(NQQ, 2); \
+  else if (n <= 256) FM_CR(NQQ, 4); \
+  else return (int)hipErrorInvalidValue;
+  if (nq <= 64 * 8) { FM_CR_K(8) }
+  else if (nq <= 64 * 16) { FM_CR_K(16) }
+  else if (nq <= 64 * 24) { FM_CR_K(24) }
+  else if (nq <= 64 * 32) { FM_CR_K(32) }
+  else if (nq <= 64 * 40) { FM_CR_K(40) }
+  else return (int)hipErrorInvalidValue;
+#undef FM_CR_K
+#undef FM_CR
+  FM_LAUNCH_CHECK();
+  return 0;
 }
 
 __global__ __launch_bounds__(256) void pvalue_kernel(const double* __restrict__ suff, int64_t R, int test_mask,
@@ -323,6 +473,34 @@ __global__ __launch_bounds__(256) void pvalue_kernel(const double* __restrict__ 
   diff[row] = d;
 }
 
+FM_API int fm_pairwise_suff(const float* cur, int64_t ld_c, int n_cur, const float* base, int64_t ld_b, int n_base,
+                            int64_t R, double* suff, int max_blocks, hipStream_t stream) {
+  if (R <= 0) return 0;
+  const int n = n_cur + n_base;
+  int64_t blocks = (R + 3) / 4;
+  if (max_blocks > 0 && blocks > max_blocks) blocks = max_blocks;
+  const dim3 grid((unsigned)blocks), block(256);
+#define FM_PW(KK) hipLaunchKernelGGL(pairwise_kernel<KK>, grid, block, 0, stream, cur, ld_c, n_cur, base, ld_b, \
+                                     n_base, R, suff)
+  if (n <= 64) FM_PW(1);
+  else if (n <= 128) FM_PW(2);
+  else if (n <= 256) FM_PW(4);
+  else if (n <= 512) FM_PW(8);
+  else return (int)hipErrorInvalidValue;
+#undef FM_PW
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+FM_API int fm_pvalues(const double* suff, int64_t R, int test_mask, int combine_any, float p_thr, int min_mw,
+                      int min_wil, int min_kru, float* pvals, float* stats, int8_t* diff, hipStream_t stream) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, suff, R, test_mask,
+                     combine_any, p_thr, min_mw, min_wil, min_kru, pvals, stats, diff);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
 FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const float* base, int64_t ld_b, int n_base,
                              int64_t R, int test_mask, int combine_any, float p_thr, int min_mw, int min_wil,
                              int min_kru, float* pvals, float* stats, int8_t* diff, double* suff,
@@ -360,8 +538,8 @@ __global__ __launch_bounds__(256) void stats_decide_kernel(
     int* __restrict__ out_valid) {
   __shared__ double red[4];
   __shared__ int redi[4];
-  const int64_t row = blockIdx.x;
   const int tid = threadIdx.x;
+  const int64_t row = blockIdx.x;
   const float* h = hist + row * ld_h;
   const int nq = (T + 3) >> 2;
   float4 q[NV];
@@ -491,8 +669,8 @@ __global__ __launch_bounds__(256) void hist_stats_kernel(const float* __restrict
                                                          int64_t R, float* __restrict__ out /*[R,3]*/) {
   __shared__ double red[4];
   __shared__ int redi[4];
-  const int64_t row = blockIdx.x;
   const int tid = threadIdx.x;
+  for (int64_t row = blockIdx.x; row < R; row += gridDim.x) {
   const float* h = hist + row * ld_h;
   const int nq = (T + 3) >> 2;
   float4 q[NV];
@@ -537,13 +715,15 @@ __global__ __launch_bounds__(256) void hist_stats_kernel(const float* __restrict
     out[row * 3 + 1] = n > 0 ? (float)sqrt(sst / n) : 0.f;
     out[row * 3 + 2] = (float)n;
   }
+  }
 }
 
-FM_API int fm_hist_stats(const float* hist, int64_t ld_h, int T, int64_t R, float* out, hipStream_t stream) {
+FM_API int fm_hist_stats_capped(const float* hist, int64_t ld_h, int T, int64_t R, float* out, int max_blocks,
+                                hipStream_t stream) {
   if (R <= 0) return 0;
   if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
   const int nq = (T + 3) / 4;
-  const dim3 grid((unsigned)R), block(256);
+  const dim3 grid((unsigned)(max_blocks > 0 && R > max_blocks ? max_blocks : R)), block(256);
 #define FM_HS(NVV) hipLaunchKernelGGL(hist_stats_kernel<NVV>, grid, block, 0, stream, hist, ld_h, T, R, out)
   if (nq <= 256 * 2) FM_HS(2);
   else if (nq <= 256 * 4) FM_HS(4);
@@ -555,6 +735,10 @@ FM_API int fm_hist_stats(const float* hist, int64_t ld_h, int T, int64_t R, floa
 #undef FM_HS
   FM_LAUNCH_CHECK();
   return 0;
+}
+
+FM_API int fm_hist_stats(const float* hist, int64_t ld_h, int T, int64_t R, float* out, hipStream_t stream) {
+  return fm_hist_stats_capped(hist, ld_h, T, R, out, 0, stream);
 }
 
 __global__ __launch_bounds__(256) void window_decide_kernel(

@@ -35,9 +35,29 @@ class CanaryOutputs:
     hs: torch.Tensor | None = None   # [R, 3] history mean, std, count (two-stream path)
 
 
+MODES = ("fused", "overlap", "serial")
+
+
 class CanaryScorer:
-    def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu", overlap: bool = True):
-        self.overlap = overlap
+    """``mode`` (GPU only):
+
+    * ``fused`` (default) — one wave per row streams the 7-day history and runs
+      the pairwise rank tests while it is in flight (fm_canary_rows), then
+      p-values, window decision, service reduce: 4 launches, 1 stream;
+    * ``overlap`` — pairwise on a side stream || history stats on the main
+      stream, joined before the decision (fork/join captured in the graph);
+    * ``serial`` — pairwise, then the fused stats+decide kernel.
+    """
+
+    def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu", overlap: bool = True,
+                 mode: str | None = None, hist_blocks: int = 0, pw_blocks: int = 0):
+        self.mode = mode or ("fused" if overlap else "serial")
+        if self.mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}")
+        self.overlap = self.mode == "overlap"
+        # workgroup caps of the two concurrent kernels of the overlap tick
+        # (0 = one workgroup per row / per 4 rows); see tools/tick_breakdown.py
+        self.hist_blocks, self.pw_blocks = hist_blocks, pw_blocks
         self._side = None
         self.cfg = cfg or BrainConfig()
         self.aliases = list(aliases)
@@ -84,7 +104,9 @@ class CanaryScorer:
             return CanaryOutputs(pv, ps, df, None, dec, packed)
         o = self._alloc(R, cur.shape[1])
         has_base = base is not None and base.shape[1] > 0
-        if not self.overlap:
+        if self.mode == "fused":
+            self._fused(hist, base if has_base else None, cur, n_hist, o)
+        elif not self.overlap:
             if has_base:
                 self._pairwise_into(cur, base, o)
             C.stats_decide(hist, cur, n_hist, self.M, self.thr, self.bound, self.minlb,
@@ -100,10 +122,11 @@ class CanaryScorer:
                 side = self._side_stream(dev)
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    self._pairwise_into(cur, base, o)
+                    self._pairwise_into(cur, base, o, self.pw_blocks)
             T = hist.shape[1] if n_hist is None else int(n_hist)
             C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
-            LIB.call("fm_hist_stats", ptr(hist), hist.stride(0), T, R, ptr(o.hs), stream_of(hist))
+            LIB.call("fm_hist_stats_capped", ptr(hist), hist.stride(0), T, R, ptr(o.hs), self.hist_blocks,
+                     stream_of(hist))
             if has_base:
                 main.wait_stream(side)
             d = o.decide
@@ -114,19 +137,40 @@ class CanaryScorer:
         C.service_reduce(o.decide.count, o.decide.score, o.decide.valid, self.M, out=o.packed)
         return o
 
+    def _fused(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:
+        from ..ops._lib import LIB, ptr, stream_of
+        R = cur.shape[0]
+        T = hist.shape[1] if n_hist is None else int(n_hist)
+        C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
+        st = stream_of(cur)
+        has_base = base is not None
+        LIB.call("fm_canary_rows", ptr(hist), hist.stride(0), T, ptr(cur), cur.stride(0), cur.shape[1],
+                 ptr(base) if has_base else None, base.stride(0) if has_base else 0,
+                 base.shape[1] if has_base else 0, R, ptr(o.hs), ptr(o.suff), st)
+        if has_base:
+            mask, anyc = self.pcfg.mask_and_combine()
+            LIB.call("fm_pvalues", ptr(o.suff), R, mask, anyc, float(self.pcfg.p_threshold), self.pcfg.min_mann_white,
+                     self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(o.diff), st)
+        d = o.decide
+        LIB.call("fm_window_decide", ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1], R, self.M, ptr(self.thr),
+                 ptr(self.bound), ptr(self.minlb), float(self.cfg.pairwise_threshold_factor),
+                 ptr(o.diff) if has_base else None, int(self.cfg.min_historical_points), ptr(d.stats),
+                 ptr(d.flags), d.flags.shape[1], ptr(d.count), ptr(d.score), ptr(d.valid), st)
+
     def _side_stream(self, dev):
         if self._side is None:
             self._side = torch.cuda.Stream(dev)
         return self._side
 
-    def _pairwise_into(self, cur, base, o: CanaryOutputs) -> None:
+    def _pairwise_into(self, cur, base, o: CanaryOutputs, max_blocks: int = 0) -> None:
         from ..ops._lib import LIB, ptr, stream_of
         R = cur.shape[0]
         mask, anyc = self.pcfg.mask_and_combine()
-        LIB.call("fm_pairwise_tests", ptr(cur), cur.stride(0), cur.shape[1], ptr(base), base.stride(0),
-                 base.shape[1], R, mask, anyc, float(self.pcfg.p_threshold), self.pcfg.min_mann_white,
-                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(o.diff),
-                 ptr(o.suff), stream_of(cur))
+        st = stream_of(cur)
+        LIB.call("fm_pairwise_suff", ptr(cur), cur.stride(0), cur.shape[1], ptr(base), base.stride(0),
+                 base.shape[1], R, ptr(o.suff), int(max_blocks), st)
+        LIB.call("fm_pvalues", ptr(o.suff), R, mask, anyc, float(self.pcfg.p_threshold), self.pcfg.min_mann_white,
+                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(o.diff), st)
 
     # -- HIP graph capture of the whole tick ---------------------------------
     def capture(self, hist, base, cur, n_hist=None):

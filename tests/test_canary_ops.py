@@ -206,18 +206,25 @@ def test_gpu_scorer_graph_equals_eager_and_cpu(cuda):
 
 
 @pytest.mark.gpu
-def test_gpu_two_stream_tick_equals_single_stream(cuda):
+@pytest.mark.parametrize("T,base", [(10080, True), (9001, True), (10080, False)])
+def test_gpu_tick_modes_agree(cuda, T, base):
+    """fused row kernel == two-stream fork/join == serial, eager and graph-captured."""
     from foremast_amd.engine.scorer import CanaryScorer
     aliases = ["error5xx", "latency", "traffic", "error4xx"]
-    h, b, c = C.synth_fleet(300, 4, 10080, 5, 10, 0, device=cuda, fault_rate=0.1)
-    a = CanaryScorer(aliases, device=cuda, overlap=False).score(h, b, c, 10080)
-    s2 = CanaryScorer(aliases, device=cuda, overlap=True)
-    o = s2.score(h, b, c, 10080)
-    torch.cuda.synchronize()
-    torch.testing.assert_close(o.packed, a.packed)
-    torch.testing.assert_close(o.decide.stats, a.decide.stats)
-    g = s2.capture(h, b, c, 10080)().packed.clone()
-    torch.testing.assert_close(g, a.packed)
+    h, b, c = C.synth_fleet(300, 4, T, 5, 10, 0, device=cuda, fault_rate=0.1)
+    b = b if base else None
+    ref = CanaryScorer(aliases, device=cuda, mode="serial").score(h, b, c, T)
+    for mode in ("overlap", "fused"):
+        sc = CanaryScorer(aliases, device=cuda, mode=mode)
+        o = sc.score(h, b, c, T)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(o.packed, ref.packed, msg=mode)
+        torch.testing.assert_close(o.decide.stats, ref.decide.stats, rtol=2e-5, atol=1e-5, msg=mode)
+        torch.testing.assert_close(o.decide.count, ref.decide.count, msg=mode)
+        if base:
+            torch.testing.assert_close(o.pvals, ref.pvals, equal_nan=True, msg=mode)
+        g = sc.capture(h, b, c, T)().packed.clone()
+        torch.testing.assert_close(g, ref.packed, msg=mode)
 
 
 @pytest.mark.gpu
