@@ -50,8 +50,8 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=5)
     ap.add_argument("--window", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--mode", choices=["fused", "overlap", "serial"], default="fused",
-                    help="tick structure: fused row kernel (default), two-stream fork/join, or serial")
+    ap.add_argument("--mode", choices=["fused", "overlap", "serial"], default="overlap",
+                    help="tick structure: two-stream fork/join (default), fused row kernel, or serial")
     ap.add_argument("--no-overlap", action="store_true", help="alias of --mode serial")
     args = ap.parse_args()
 

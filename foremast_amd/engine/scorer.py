@@ -41,17 +41,19 @@ MODES = ("fused", "overlap", "serial")
 class CanaryScorer:
     """``mode`` (GPU only):
 
-    * ``fused`` (default) — one wave per row streams the 7-day history and runs
-      the pairwise rank tests while it is in flight (fm_canary_rows), then
-      p-values, window decision, service reduce: 4 launches, 1 stream;
-    * ``overlap`` — pairwise on a side stream || history stats on the main
-      stream, joined before the decision (fork/join captured in the graph);
+    * ``overlap`` (default) — pairwise on a side stream || history stats on
+      the main stream, joined before the decision (fork/join captured in the
+      graph);
+    * ``fused`` — one wave per row streams the 7-day history and runs the
+      pairwise rank tests while it is in flight (fm_canary_rows).  Measured
+      slower on MI355X (profiles/tick_breakdown_1gpu.json: the 160-VGPR row
+      image leaves 2 waves/SIMD, too few to keep HBM busy), kept for A/B;
     * ``serial`` — pairwise, then the fused stats+decide kernel.
     """
 
     def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu", overlap: bool = True,
                  mode: str | None = None, hist_blocks: int = 0, pw_blocks: int = 0):
-        self.mode = mode or ("fused" if overlap else "serial")
+        self.mode = mode or ("overlap" if overlap else "serial")
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         self.overlap = self.mode == "overlap"
