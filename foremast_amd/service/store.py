@@ -225,6 +225,37 @@ class ElasticsearchStore(JobStore):
         r.raise_for_status()
         return [Document.from_dict(h["_source"]) for h in r.json().get("hits", {}).get("hits", [])]
 
+    def _claim_candidates(self) -> list[Document]:
+        states = sorted(ST.CLAIMABLE | ST.IN_PROGRESS)
+        q = {"query": {"terms": {"status.keyword": states}}, "size": 10000}
+        r = self.http.post(f"{self.url}/documents/_search", json=q)
+        if r.status_code == 404:
+            return []
+        r.raise_for_status()
+        return [Document.from_dict(h["_source"]) for h in r.json().get("hits", {}).get("hits", [])]
+
+    def _cas_claim(self, d: Document, worker: str, now: float) -> bool:
+        """Optimistic concurrency: re-read the document with its sequence
+        number, re-check that it is still claimable, write conditionally
+        (``if_seq_no``/``if_primary_term``); a 409 means another brain won."""
+        r = self.http.get(f"{self.url}/documents/document/{d.id}")
+        if r.status_code != 200:
+            return False
+        body = r.json()
+        cur = Document.from_dict(body.get("_source", {}))
+        stuck = cur.status in ST.IN_PROGRESS
+        if cur.status not in ST.CLAIMABLE and not (stuck and cur.modified_at == d.modified_at):
+            return False
+        cur.status = ST.PREPROCESS_INPROGRESS
+        cur.processing_content = worker
+        cur.modified_at = rfc3339(datetime.fromtimestamp(now, timezone.utc))
+        w = self.http.put(f"{self.url}/documents/document/{d.id}?refresh=true&if_seq_no={body.get('_seq_no', 0)}"
+                          f"&if_primary_term={body.get('_primary_term', 1)}", json=cur.to_dict())
+        if w.status_code == 409:
+            return False
+        w.raise_for_status()
+        return True
+
     def add_hpalog(self, log: HPALog) -> None:
         r = self.http.post(f"{self.url}/hpalogs/hpalog?refresh=true", json=log.to_dict())
         r.raise_for_status()
