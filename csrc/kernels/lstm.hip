@@ -16,6 +16,8 @@
 // ds_read_b128 from a [batch][H + 8] image (row pad -> conflict-free).
 #include "fm_common.h"
 
+#include <type_traits>
+
 using namespace fm;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -53,9 +55,14 @@ union Frag {
 
 // Wpack: [H/16 waves][2 rt][KS k-steps][64 lanes] x 8 bf16, pre-swizzled on the
 // host so each lane loads its A fragment with one 16-B load.
+//
+// Input xa: [B, L, 16] bf16, the augmented K step already laid out
+// (features at k < I, 1.0 at k = I for the bias, zeros above): lane half h
+// reads its 8 values of step t with ONE 16-B load, no conversion and no
+// per-feature branches (fm_lstm_features writes it straight from the history).
 template <int H>
-__global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const float* __restrict__ x /*[B, L, I]*/, int64_t B, int L,
-                                                         int I, const uint4* __restrict__ Wpack,
+__global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict__ xa /*[B, L, 2] x 16 B*/,
+                                                         int64_t B, int L, const uint4* __restrict__ Wpack,
                                                          const float* __restrict__ h0, const float* __restrict__ c0,
                                                          float* __restrict__ h_out /*[B,H]*/,
                                                          float* __restrict__ c_out /*[B,H]*/,
@@ -91,38 +98,41 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const float* __restrict
       }
   __syncthreads();
 
-  // x_t of this lane's features (h == 0 lanes: k = 0..7; h == 1: k = 8..15) is
-  // loaded one step ahead so the global-memory latency hides behind the
-  // previous step's MFMAs instead of stalling the head of every step.
-  float xn[2][8];
-  auto load_x = [&](int tt) {
+  // per-lane input streams (rows past B clamp to B-1: loaded, never stored)
+  const uint4* xp[2];
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      const int64_t bb = b0 + 32 * ct + col;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * h + j;
-        xn[ct][j] = (k < I && bb < B && tt < L) ? x[(bb * L + tt) * I + k] : 0.f;
-      }
-    }
-  };
-  load_x(0);
+  for (int ct = 0; ct < 2; ++ct) {
+    int64_t bb = b0 + 32 * ct + col;
+    bb = bb < B ? bb : B - 1;
+    xp[ct] = xa + (bb * L) * 2 + h;
+  }
+  // x_{t+1} is loaded while step t computes
+  uint4 xn[2] = {xp[0][0], xp[1][0]};
   int cur = 0;
-  for (int t = 0; t < L; ++t) {
-    // augmented operand: x_t features, bias "1" at k = I
+
+  auto step = [&](int t, auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
     Frag xb[2];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xb[ct].s[j] = f2bf(8 * h + j == I ? 1.f : xn[ct][j]);
-    load_x(t + 1);
+    xb[0].u = xn[0];
+    xb[1].u = xn[1];
+    if (!LAST) {
+      xn[0] = xp[0][(t + 1) * 2];
+      xn[1] = xp[1][(t + 1) * 2];
+    }
     f32x16 acc[2][2];
+    {
+      Frag bfr[2];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+      for (int ct = 0; ct < 2; ++ct)
+        bfr[ct].u = *reinterpret_cast<const uint4*>(&hbuf[cur][(32 * ct + col) * HP + 8 * h]);
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) acc[rt][ct] = (f32x16){};
+      for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-    for (int ks = 0; ks < KS - 1; ++ks) {
+        for (int ct = 0; ct < 2; ++ct)
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][0].v, bfr[ct].v, (f32x16){}, 0, 0, 0);
+    }
+#pragma unroll
+    for (int ks = 1; ks < KS - 1; ++ks) {
       Frag bfr[2];
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
@@ -154,42 +164,110 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const float* __restrict
           const float og = sigm(acc[rt][ct][12 + j]);
           const float cc = fg * c[rt][ct][j] + ig * gg;
           c[rt][ct][j] = cc;
-          const float hh = og * tanh_f(cc);
-          hv[j] = hh;
-          if (t == L - 1) {
-            const int64_t bb = b0 + 32 * ct + col;
-            const int u = 16 * w + 8 * rt + 4 * h + j;
-            if (bb < B) { h_out[bb * H + u] = hh; c_out[bb * H + u] = cc; }
-          }
+          hv[j] = og * tanh_f(cc);
         }
         const int u0 = 16 * w + 8 * rt + 4 * h;
+        const int64_t bb = b0 + 32 * ct + col;
         uint2 pk;
         pk.x = pack_bf2(hv[0], hv[1]);
         pk.y = pack_bf2(hv[2], hv[3]);
-        *reinterpret_cast<uint2*>(&hbuf[nxt][(32 * ct + col) * HP + u0]) = pk;
-        if (hseq != nullptr) {
-          const int64_t bb = b0 + 32 * ct + col;
-          if (bb < B) *reinterpret_cast<uint2*>(&hseq[(bb * L + t) * H + u0]) = pk;
+        if (LAST) {
+          if (bb < B) {
+            *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+            *reinterpret_cast<float4*>(&c_out[bb * H + u0]) =
+                make_float4(c[rt][ct][0], c[rt][ct][1], c[rt][ct][2], c[rt][ct][3]);
+          }
+        } else {
+          *reinterpret_cast<uint2*>(&hbuf[nxt][(32 * ct + col) * HP + u0]) = pk;
         }
+        if (hseq != nullptr && bb < B) *reinterpret_cast<uint2*>(&hseq[(bb * L + t) * H + u0]) = pk;
       }
-    __syncthreads();
-    cur = nxt;
-  }
+    if (!LAST) {
+      __syncthreads();
+      cur = nxt;
+    }
+  };
+  for (int t = 0; t < L - 1; ++t) step(t, std::false_type{});
+  step(L - 1, std::true_type{});
 }
 
-FM_API int fm_lstm_forward(const float* x, int64_t B, int L, int I, int H, const void* Wpack, const float* h0,
+// ---------------------------------------------------------------------------
+// Forecaster features straight from the packed history: per row the last L
+// samples are z-scored (finite mean / population std, missing -> 0) and laid
+// out as the kernel's augmented input [z, sin(2 pi t/P), cos(2 pi t/P)][:I],
+// 1.0 at k = I, zeros above, in bf16.  One wave per row.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lstm_features_kernel(const float* __restrict__ hist, int64_t ld, int T,
+                                                            int64_t R, int L, float period, int I,
+                                                            uint4* __restrict__ xa, float* __restrict__ mu_out,
+                                                            float* __restrict__ sd_out) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave_id();
+  if (row >= R) return;
+  const int lane = lane_id();
+  const float* hr = hist + row * ld + (T - L);
+  float s = 0.f;
+  int n = 0;
+  for (int i = lane; i < L; i += 64) {
+    const float v = hr[i];
+    if (isfinite(v)) { s += v; ++n; }
+  }
+  s = wave_sum(s);
+  n = wave_sum(n);
+  const float mu = s / (float)(n > 0 ? n : 1);
+  float q = 0.f;
+  for (int i = lane; i < L; i += 64) {
+    const float v = hr[i];
+    if (isfinite(v)) { const float d = v - mu; q += d * d; }
+  }
+  q = wave_sum(q);
+  float sd = sqrtf(q / (float)(n > 0 ? n : 1));
+  sd = sd > 1e-6f ? sd : 1e-6f;
+  const float inv = 1.f / sd;
+  const float w0 = 6.283185307179586f / period;
+  for (int i = lane; i < L; i += 64) {
+    const float v = hr[i];
+    const float z = isfinite(v) ? (v - mu) * inv : 0.f;
+    const float ph = w0 * (float)(T - L + i);
+    float f[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) f[k] = 0.f;
+    if (I > 0) f[0] = z;
+    if (I > 1) f[1] = sinf(ph);
+    if (I > 2) f[2] = cosf(ph);
+    f[I < 15 ? I : 15] = 1.f;
+    uint4 lo, hi;
+    lo.x = pack_bf2(f[0], f[1]); lo.y = pack_bf2(f[2], f[3]); lo.z = pack_bf2(f[4], f[5]); lo.w = pack_bf2(f[6], f[7]);
+    hi.x = pack_bf2(f[8], f[9]); hi.y = pack_bf2(f[10], f[11]); hi.z = pack_bf2(f[12], f[13]);
+    hi.w = pack_bf2(f[14], f[15]);
+    xa[(row * L + i) * 2 + 0] = lo;
+    xa[(row * L + i) * 2 + 1] = hi;
+  }
+  if (lane == 0) { mu_out[row] = mu; sd_out[row] = sd; }
+}
+
+FM_API int fm_lstm_features(const float* hist, int64_t ld, int T, int64_t R, int L, float period, int I, void* xa,
+                            float* mu, float* sd, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if (L <= 0 || L > T || I < 0 || I > 3) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(lstm_features_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, stream, hist, ld, T, R, L,
+                     period, I, (uint4*)xa, mu, sd);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+FM_API int fm_lstm_forward(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
                            const float* c0, float* h_out, float* c_out, unsigned short* hseq, hipStream_t stream) {
   if (B <= 0 || L <= 0) return 0;
-  if (I < 0 || I > 15) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)((B + 63) / 64));
+  const uint4* x = (const uint4*)xa;
   if (H == 128)
-    hipLaunchKernelGGL(lstm_fwd_kernel<128>, grid, dim3(512), 0, stream, x, B, L, I, (const uint4*)Wpack, h0, c0,
+    hipLaunchKernelGGL(lstm_fwd_kernel<128>, grid, dim3(512), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0,
                        h_out, c_out, hseq);
   else if (H == 64)
-    hipLaunchKernelGGL(lstm_fwd_kernel<64>, grid, dim3(256), 0, stream, x, B, L, I, (const uint4*)Wpack, h0, c0,
+    hipLaunchKernelGGL(lstm_fwd_kernel<64>, grid, dim3(256), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0,
                        h_out, c_out, hseq);
   else if (H == 32)
-    hipLaunchKernelGGL(lstm_fwd_kernel<32>, grid, dim3(128), 0, stream, x, B, L, I, (const uint4*)Wpack, h0, c0,
+    hipLaunchKernelGGL(lstm_fwd_kernel<32>, grid, dim3(128), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0,
                        h_out, c_out, hseq);
   else
     return (int)hipErrorInvalidValue;

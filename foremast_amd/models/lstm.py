@@ -75,10 +75,12 @@ class LSTMForecaster:
     @torch.no_grad()
     def forecast(self, hist: torch.Tensor, T: int, H: int):
         """-> (forecast [R, H] in data units, sigma [R]) with sigma = window std."""
-        x, mu, sd = self.features(hist, T)
-        if x.is_cuda:
-            hT, _, _ = LS.lstm_forward(x, self.packed(), self.H)
+        if hist.is_cuda:
+            # features written by a HIP kernel straight into the bf16 augmented layout
+            xa, mu, sd = LS.lstm_features(hist, T, min(self.L, T), self.period, self.I)
+            hT, _, _ = LS.lstm_forward_packed(xa, self.packed(), self.H)
         else:
+            x, mu, sd = self.features(hist, T)
             with torch.no_grad():
                 _, (h, _) = self.lstm(x)
                 hT = h[0]

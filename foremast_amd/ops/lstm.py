@@ -54,20 +54,61 @@ def pack_lstm(w_ih: torch.Tensor, w_hh: torch.Tensor, bias: torch.Tensor) -> tor
     return torch.from_numpy(_bf16_bits(out).view(np.uint8).copy())
 
 
+def augment(x: torch.Tensor) -> torch.Tensor:
+    """[B, L, I] float -> the kernel's augmented input [B, L, 16] bf16
+    (features at k < I, 1.0 at k = I for the bias, zeros above)."""
+    B, L, I = x.shape
+    check(I <= 15, "input features must be <= 15 (folded into one K step with the bias)")
+    xa = torch.zeros((B, L, 16), dtype=torch.bfloat16, device=x.device)
+    if I:
+        xa[..., :I] = x.to(torch.bfloat16)
+    xa[..., I] = 1.0
+    return xa
+
+
 def lstm_forward(x: torch.Tensor, packed: torch.Tensor, H: int, h0=None, c0=None, return_seq: bool = False):
     """x [B, L, I] float32 -> (h_L [B,H], c_L [B,H], seq [B,L,H] bf16 or None)."""
     check(x.dim() == 3 and x.dtype == torch.float32 and x.is_contiguous(), "x must be contiguous [B, L, I] float32")
-    B, L, I = x.shape
     require_native(x)
     check(x.is_cuda, "lstm_forward runs on the GPU; use ref_lstm_forward on CPU")
-    d = x.device
+    return lstm_forward_packed(augment(x), packed, H, h0, c0, return_seq)
+
+
+def lstm_forward_packed(xa: torch.Tensor, packed: torch.Tensor, H: int, h0=None, c0=None, return_seq: bool = False):
+    """xa [B, L, 16] bf16 augmented input (``augment`` / ``lstm_features``)."""
+    check(xa.dim() == 3 and xa.shape[2] == 16 and xa.dtype == torch.bfloat16 and xa.is_contiguous(),
+          "xa must be contiguous [B, L, 16] bfloat16")
+    check(H in SUPPORTED_H, f"hidden size must be one of {SUPPORTED_H}")
+    require_native(xa)
+    B, L, _ = xa.shape
+    d = xa.device
     hT = torch.empty((B, H), dtype=torch.float32, device=d)
     cT = torch.empty((B, H), dtype=torch.float32, device=d)
     seq = torch.empty((B, L, H), dtype=torch.bfloat16, device=d) if return_seq else None
     pk = packed.to(d)
-    LIB.call("fm_lstm_forward", ptr(x), B, L, I, H, ptr(pk), ptr(h0), ptr(c0), ptr(hT), ptr(cT), ptr(seq),
-             stream_of(x))
+    for t in (h0, c0):
+        check(t is None or (t.is_contiguous() and t.dtype == torch.float32 and tuple(t.shape) == (B, H)),
+              "h0/c0 must be contiguous [B, H] float32")
+    LIB.call("fm_lstm_forward", ptr(xa), B, L, H, ptr(pk), ptr(h0), ptr(c0), ptr(hT), ptr(cT), ptr(seq),
+             stream_of(xa))
     return hT, cT, seq
+
+
+def lstm_features(hist: torch.Tensor, T: int, L: int, period: float, I: int = 3):
+    """Augmented forecaster input straight from the packed history (GPU):
+    -> (xa [R, L, 16] bf16, mu [R], sd [R]).  Features [z, sin, cos][:I] of the
+    last L samples (z-score over the window's finite samples, missing -> 0)."""
+    check(hist.dim() == 2 and hist.dtype == torch.float32 and hist.stride(1) == 1, "hist must be [R, T] float32")
+    check(0 < L <= T <= hist.shape[1] and 0 <= I <= 3, "bad window / feature count")
+    require_native(hist)
+    R = hist.shape[0]
+    d = hist.device
+    xa = torch.empty((R, L, 16), dtype=torch.bfloat16, device=d)
+    mu = torch.empty((R,), dtype=torch.float32, device=d)
+    sd = torch.empty((R,), dtype=torch.float32, device=d)
+    LIB.call("fm_lstm_features", ptr(hist), hist.stride(0), T, R, L, float(period), I, ptr(xa), ptr(mu), ptr(sd),
+             stream_of(hist))
+    return xa, mu, sd
 
 
 def ref_lstm_forward(x: torch.Tensor, w_ih, w_hh, bias, h0=None, c0=None, emulate_bf16: bool = True):

@@ -259,3 +259,25 @@ def test_gpu_lstm_matches_reference(cuda, H, I):
     torch.testing.assert_close(hg.cpu(), hr, atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(cg.cpu(), cr, atol=5e-2, rtol=5e-2)
     torch.testing.assert_close(seq[:, -1].float().cpu(), hr, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_lstm_features_and_forecast(cuda):
+    """fm_lstm_features == the CPU feature path (bf16-rounded), and the GPU
+    forecaster agrees with the CPU nn.LSTM forecaster."""
+    from foremast_amd.models.lstm import LSTMForecaster
+    T = 600
+    x = _seasonal(37, T, period=144, seed=3)
+    x[5, T - 10] = np.nan
+    h = torch.from_numpy(np.ascontiguousarray(np.pad(x, ((0, 0), (0, 4)), constant_values=np.nan)))
+    m = LSTMForecaster(hidden=64, window=120, horizon=10, period=144.0)
+    xa, mu, sd = LS.lstm_features(h.to(cuda), T, 120, 144.0, 3)
+    f, mu0, sd0 = m.features(h, T)
+    torch.testing.assert_close(mu.cpu(), mu0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(sd.cpu(), sd0, rtol=1e-5, atol=1e-5)
+    xa = xa.float().cpu()
+    torch.testing.assert_close(xa[..., :3], f.to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
+    assert (xa[..., 3] == 1).all() and (xa[..., 4:] == 0).all()
+    fc_g, sg = m.forecast(h.to(cuda), T, 10)
+    fc_c, sc = m.forecast(h, T, 10)
+    torch.testing.assert_close(fc_g.cpu(), fc_c, rtol=5e-2, atol=5e-2 * float(sc.max()))
