@@ -60,7 +60,7 @@ union Frag {
 // (features at k < I, 1.0 at k = I for the bias, zeros above): lane half h
 // reads its 8 values of step t with ONE 16-B load, no conversion and no
 // per-feature branches (fm_lstm_features writes it straight from the history).
-template <int H>
+template <int H, int NCT>
 __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict__ xa /*[B, L, 2] x 16 B*/,
                                                          int64_t B, int L, const uint4* __restrict__ Wpack,
                                                          const float* __restrict__ h0, const float* __restrict__ c0,
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
                                                          unsigned short* __restrict__ hseq /*[B,L,H] bf16 or null*/) {
   constexpr int KS = H / 16 + 1;  // k-steps: H/16 recurrent + 1 augmented (x, 1)
   constexpr int HP = H + 8;       // padded LDS row (bf16)
-  constexpr int BT = 64;
+  constexpr int BT = 32 * NCT;     // batch columns per workgroup (NCT 32-wide MFMA column tiles)
   __shared__ __attribute__((aligned(16))) unsigned short hbuf[2][BT * HP];
   const int lane = lane_id(), w = wave_id();
   const int h = lane >> 5, col = lane & 31;
@@ -83,11 +83,11 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
     for (int ks = 0; ks < KS; ++ks) A[rt][ks].u = Wpack[(((int64_t)w * 2 + rt) * KS + ks) * 64 + lane];
 
   // initial state: this lane's units u = 16w + 8rt + 4h + j, batch = b0 + 32ct + col
-  float c[2][2][4];
+  float c[2][NCT][4];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
+    for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int u = 16 * w + 8 * rt + 4 * h + j;
@@ -99,54 +99,55 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
   __syncthreads();
 
   // per-lane input streams (rows past B clamp to B-1: loaded, never stored)
-  const uint4* xp[2];
+  const uint4* xp[NCT];
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
+  for (int ct = 0; ct < NCT; ++ct) {
     int64_t bb = b0 + 32 * ct + col;
     bb = bb < B ? bb : B - 1;
     xp[ct] = xa + (bb * L) * 2 + h;
   }
   // x_{t+1} is loaded while step t computes
-  uint4 xn[2] = {xp[0][0], xp[1][0]};
+  uint4 xn[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) xn[ct] = xp[ct][0];
   int cur = 0;
 
   auto step = [&](int t, auto last_tag) {
     constexpr bool LAST = decltype(last_tag)::value;
-    Frag xb[2];
-    xb[0].u = xn[0];
-    xb[1].u = xn[1];
-    if (!LAST) {
-      xn[0] = xp[0][(t + 1) * 2];
-      xn[1] = xp[1][(t + 1) * 2];
-    }
-    f32x16 acc[2][2];
-    {
-      Frag bfr[2];
+    Frag xb[NCT];
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
+    for (int ct = 0; ct < NCT; ++ct) {
+      xb[ct].u = xn[ct];
+      if (!LAST) xn[ct] = xp[ct][(t + 1) * 2];
+    }
+    f32x16 acc[2][NCT];
+    {
+      Frag bfr[NCT];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
         bfr[ct].u = *reinterpret_cast<const uint4*>(&hbuf[cur][(32 * ct + col) * HP + 8 * h]);
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
+        for (int ct = 0; ct < NCT; ++ct)
           acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][0].v, bfr[ct].v, (f32x16){}, 0, 0, 0);
     }
 #pragma unroll
     for (int ks = 1; ks < KS - 1; ++ks) {
-      Frag bfr[2];
+      Frag bfr[NCT];
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
         bfr[ct].u = *reinterpret_cast<const uint4*>(&hbuf[cur][(32 * ct + col) * HP + 16 * ks + 8 * h]);
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
+        for (int ct = 0; ct < NCT; ++ct)
           acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][ks].v, bfr[ct].v, acc[rt][ct], 0, 0, 0);
     }
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
         acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][KS - 1].v, xb[ct].v, acc[rt][ct], 0, 0, 0);
 
     // lane-local cell update; regs j, 4+j, 8+j, 12+j = i, f, g, o of unit 16w+8rt+4h+j
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
+      for (int ct = 0; ct < NCT; ++ct) {
         float hv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -255,22 +256,30 @@ FM_API int fm_lstm_features(const float* hist, int64_t ld, int T, int64_t R, int
   return 0;
 }
 
-FM_API int fm_lstm_forward(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
-                           const float* c0, float* h_out, float* c_out, unsigned short* hseq, hipStream_t stream) {
+// nct: batch column tiles per workgroup (1 or 2); 0 = tuned default.
+FM_API int fm_lstm_forward_nct(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
+                               const float* c0, float* h_out, float* c_out, unsigned short* hseq, int nct,
+                               hipStream_t stream) {
   if (B <= 0 || L <= 0) return 0;
-  const dim3 grid((unsigned)((B + 63) / 64));
   const uint4* x = (const uint4*)xa;
-  if (H == 128)
-    hipLaunchKernelGGL(lstm_fwd_kernel<128>, grid, dim3(512), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0,
-                       h_out, c_out, hseq);
-  else if (H == 64)
-    hipLaunchKernelGGL(lstm_fwd_kernel<64>, grid, dim3(256), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0,
-                       h_out, c_out, hseq);
-  else if (H == 32)
-    hipLaunchKernelGGL(lstm_fwd_kernel<32>, grid, dim3(128), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0,
-                       h_out, c_out, hseq);
-  else
-    return (int)hipErrorInvalidValue;
+  // Default 64 columns (2 tiles).  For H=128 one tile gives 162 VGPRs and 3
+  // waves/SIMD instead of 2 but measured 1.5 % slower (tools/lstm_ab.py:
+  // 3.66 vs 3.61 ms at 80k x 240): the cell update is transcendental-bound
+  // (10 v_exp/v_rcp per unit per step), not latency-bound.
+  if (nct == 0) nct = 2;
+#define FM_LSTM(HH, NC)                                                                                          \
+  hipLaunchKernelGGL((lstm_fwd_kernel<HH, NC>), dim3((unsigned)((B + 32 * NC - 1) / (32 * NC))), dim3(HH * 4), 0, \
+                     stream, x, B, L, (const uint4*)Wpack, h0, c0, h_out, c_out, hseq)
+  if (H == 128) { if (nct == 1) FM_LSTM(128, 1); else FM_LSTM(128, 2); }
+  else if (H == 64) { if (nct == 1) FM_LSTM(64, 1); else FM_LSTM(64, 2); }
+  else if (H == 32) { if (nct == 1) FM_LSTM(32, 1); else FM_LSTM(32, 2); }
+  else return (int)hipErrorInvalidValue;
+#undef FM_LSTM
   FM_LAUNCH_CHECK();
   return 0;
+}
+
+FM_API int fm_lstm_forward(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
+                           const float* c0, float* h_out, float* c_out, unsigned short* hseq, hipStream_t stream) {
+  return fm_lstm_forward_nct(xa, B, L, H, Wpack, h0, c0, h_out, c_out, hseq, 0, stream);
 }

@@ -67,6 +67,8 @@ _SIGS: dict[str, list] = {
                        c_void_p],
     "fm_lstm_forward": [c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p],
+    "fm_lstm_forward_nct": [c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_int, c_void_p],
     "fm_lstm_features": [c_void_p, c_i64, c_int, c_i64, c_int, c_float, c_int, c_void_p, c_void_p, c_void_p,
                          c_void_p],
 }
