@@ -78,7 +78,15 @@ def _expand_stats(dec: C.DecideResult, n: int) -> RowDecision:
 
 
 def _valid(hist: torch.Tensor, T: int, cur: torch.Tensor, min_hist: int) -> torch.Tensor:
-    nh = torch.isfinite(hist[:, :T]).sum(1)
+    if hist.is_cuda and hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0:
+        # finite-sample count from the streaming history-stats kernel (one HBM
+        # pass) instead of isfinite -> bool [R, T] -> sum
+        from ..ops._lib import LIB, ptr, stream_of
+        hs = torch.empty((hist.shape[0], 3), dtype=torch.float32, device=hist.device)
+        LIB.call("fm_hist_stats", ptr(hist), hist.stride(0), T, hist.shape[0], ptr(hs), stream_of(hist))
+        nh = hs[:, 2]
+    else:
+        nh = torch.isfinite(hist[:, :T]).sum(1)
     has_cur = torch.isfinite(cur).any(1)
     return ((nh >= max(min_hist, 1)).to(torch.int32) | (has_cur.to(torch.int32) << 1))
 
