@@ -53,6 +53,7 @@ def main() -> None:
     ap.add_argument("--mode", choices=["fused", "overlap", "serial"], default="overlap",
                     help="tick structure: two-stream fork/join (default), fused row kernel, or serial")
     ap.add_argument("--no-overlap", action="store_true", help="alias of --mode serial")
+    ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace of 5 extra steps (rank 0)")
     args = ap.parse_args()
 
     info = D.env_info()
@@ -138,6 +139,13 @@ def main() -> None:
             "services_flagged": n_anom,
         }
         print(json.dumps(out))
+    if args.trace and info.is_main:
+        # outside the timed region: a HIP-activity trace of a few ticks
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(5):
+                step()
+        prof.export_chrome_trace(args.trace)
     if D.is_dist():
         torch.distributed.destroy_process_group()
 

@@ -95,7 +95,13 @@ class LSTMForecaster:
     # ------------------------------------------------------------------ training
     def fit(self, hist: torch.Tensor, T: int, epochs: int = 2, batch: int = 256, lr: float = 1e-3,
             max_windows: int = 4096, seed: int = 0) -> list[float]:
-        """Train on sliding windows of the history (next-``horizon`` targets)."""
+        """Train on sliding windows of the history (next-``horizon`` targets).
+
+        Data-parallel when torch.distributed is initialised: every rank samples
+        windows from its own shard of rows and the gradients are averaged with
+        ONE all-reduce of a flat buffer per step (C4, SURVEY §2.5: the whole
+        model is ~70k parameters, so one bucket; ring all-reduce over xGMI is
+        per-link bound and a single message amortises its latency)."""
         dev = hist.device
         lstm = self.lstm.to(dev)
         head = self.head.to(dev)
@@ -122,11 +128,29 @@ class LSTMForecaster:
                 loss = torch.nn.functional.mse_loss(pred, (tgt - mu) / sd)
                 opt.zero_grad()
                 loss.backward()
+                _allreduce_grads(list(lstm.parameters()) + list(head.parameters()))
                 opt.step()
                 losses.append(float(loss.item()))
         self.lstm, self.head = lstm.cpu(), head.cpu()
         self._packed = None
         return losses
+
+
+def _allreduce_grads(params: list[torch.nn.Parameter]) -> None:
+    from ..parallel import dist as D
+    if not D.is_dist():
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    torch.distributed.all_reduce(flat)
+    flat /= torch.distributed.get_world_size()
+    off = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n
 
 
 def smoke_forward(device) -> None:

@@ -46,7 +46,12 @@ def init_distributed(backend: str | None = None, device: torch.device | None = N
         kw = {}
         if backend == "nccl" and device is not None and device.type == "cuda":
             kw["device_id"] = device
-        dist.init_process_group(backend=backend, rank=info.rank, world_size=info.world, **kw)
+            # rank-failure detection: a collective that a dead/hung rank never
+            # joins raises after the timeout instead of hanging the node
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        from datetime import timedelta
+        timeout = timedelta(seconds=float(os.environ.get("FOREMAST_COLLECTIVE_TIMEOUT_S", "300")))
+        dist.init_process_group(backend=backend, rank=info.rank, world_size=info.world, timeout=timeout, **kw)
     return info
 
 

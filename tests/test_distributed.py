@@ -182,3 +182,25 @@ def test_brain_ranks_claim_disjoint_owned_jobs(tmp_path):
     docs = [store.get(i) for i in ids]
     assert all(d.status != "initial" for d in docs)
     assert store.get(ids[3]).status == "completed_unhealth"
+
+
+def _w_lstm_fit(rank, world):
+    import torch
+    from foremast_amd.models.lstm import LSTMForecaster
+    torch.manual_seed(0)
+    m = LSTMForecaster(hidden=32, window=24, horizon=4, seed=1)
+    g = torch.Generator().manual_seed(100 + rank)        # every rank has different data
+    hist = torch.randn(8, 120, generator=g).cumsum(1)
+    m.fit(hist, 120, epochs=1, batch=16, max_windows=32, seed=rank)
+    return {k: v.numpy().copy() for k, v in m.state_dict().items()}
+
+
+def test_data_parallel_lstm_fit_keeps_ranks_in_sync():
+    out = _run(_w_lstm_fit, 2)
+    for k in out[0]:
+        np.testing.assert_allclose(out[0][k], out[1][k], rtol=1e-6, atol=1e-7, err_msg=k)
+    # and it differs from training on rank 0's data alone (gradients were averaged)
+    import foremast_amd.parallel.dist as DD
+    assert not DD.is_dist()
+    solo = _w_lstm_fit(0, 1)
+    assert any(not np.allclose(solo[k], out[0][k]) for k in solo)
