@@ -139,13 +139,18 @@ def main() -> None:
             "services_flagged": n_anom,
         }
         print(json.dumps(out))
-    if args.trace and info.is_main:
-        # outside the timed region: a HIP-activity trace of a few ticks
+    if args.trace:
+        # outside the timed region: a HIP-activity trace of a few ticks; every
+        # rank steps (the tick has a collective), rank 0 records
+        import contextlib
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        ctx = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) if info.is_main \
+            else contextlib.nullcontext()
+        with ctx as prof:
             for _ in range(5):
                 step()
-        prof.export_chrome_trace(args.trace)
+        if info.is_main:
+            prof.export_chrome_trace(args.trace)
     if D.is_dist():
         torch.distributed.destroy_process_group()
 
