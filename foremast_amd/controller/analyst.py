@@ -8,8 +8,8 @@ from __future__ import annotations
 import json
 import time
 import urllib.parse
-from dataclasses import dataclass, field
-from datetime import datetime, timedelta, timezone
+from dataclasses import dataclass
+from datetime import datetime, timezone
 from typing import Callable
 
 from ..api import crd
@@ -103,6 +103,3 @@ class AnalystClient:
         st = from_json(AnalyzeStatus, d)
         st.status = to_monitor_phase(st.status)
         return st
-
-
-_ = (field, timedelta)

@@ -15,7 +15,7 @@ import copy
 import logging
 import time
 from concurrent.futures import ThreadPoolExecutor
-from datetime import datetime, timedelta, timezone
+from datetime import datetime, timezone
 from typing import Callable
 
 from ..api import crd
@@ -381,6 +381,3 @@ def convert_to_anomaly(anomaly: dict) -> crd.Anomaly:
             m.values.append(crd.AnomalousMetricValue(time=int(vals[i]), value=float(vals[i + 1])))
         out.anomalous_metrics.append(m)
     return out
-
-
-_ = timedelta

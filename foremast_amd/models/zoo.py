@@ -25,7 +25,6 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
-import numpy as np
 import torch
 
 from ..ops import canary as C
@@ -215,6 +214,3 @@ def make_tables(aliases_per_row: list[str], cfg, device) -> Tables:
                   torch.tensor([r.bound for r in rules], dtype=torch.int32, device=device),
                   torch.tensor([r.min_lower_bound for r in rules], dtype=torch.float32, device=device),
                   cfg.pairwise_threshold_factor, cfg.min_historical_points)
-
-
-_ = np

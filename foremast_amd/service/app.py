@@ -12,7 +12,6 @@ Extra (not in the reference):
 """
 from __future__ import annotations
 
-import json
 import logging
 
 import httpx
@@ -177,6 +176,3 @@ def main() -> None:  # pragma: no cover - entry point
 
 if __name__ == "__main__":  # pragma: no cover
     main()
-
-
-_ = json

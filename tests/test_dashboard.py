@@ -1,6 +1,5 @@
 """Dashboard (R19): query set, anomaly placement, scatter, annotations, and
 the service routes over a fake Prometheus."""
-import json
 import urllib.parse
 
 import httpx
@@ -56,4 +55,3 @@ def test_service_dashboard_routes():
     assert len(d["charts"]) == 4 and d["annotations"][1]["version"] == "v2"
     page = c.get('/dashboard/prod/de"mo').text
     assert 'de&quot;mo' in page and "/dashboard/api/" in page
-    _ = json

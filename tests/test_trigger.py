@@ -1,6 +1,5 @@
 """foremast-trigger against the in-process service + brain (Wavefront-shaped
 synthetic source)."""
-import json
 import os
 
 from foremast_amd.config import BrainConfig
@@ -64,4 +63,3 @@ def test_trigger_cycle(tmp_path):
     assert rep[0].startswith("Timestamp\tlatency\terrors")
     assert any(l.endswith("\t3\t3") for l in rep) and any(l.endswith("\t-1") for l in rep)
     assert os.path.basename(path).startswith("anomalyreport")
-    _ = json
