@@ -58,6 +58,7 @@ _SIGS: dict[str, list] = {
     "fm_segment_max": [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p],
     "fm_selftest_lanes": [c_void_p, c_void_p, c_void_p],
     "fm_pairwise_suff": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_void_p],
+    "fm_pairwise_suff_v": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_void_p],
     "fm_hist_stats_capped": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_void_p],
     "fm_pvalues": [c_void_p, c_i64, c_int, c_int, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                    c_void_p],

@@ -246,3 +246,22 @@ def test_gpu_cross_lane_primitives(cuda):
     np.testing.assert_array_equal(o[9], np.concatenate([[-1], v[:-1]]))
     np.testing.assert_array_equal(o[10], np.concatenate([v[1:], [-2]]))
     np.testing.assert_array_equal(o[11], np.full(64, v.sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1,n2,nan_frac", [(50, 50, 0.0), (37, 61, 0.05), (120, 100, 0.02), (7, 9, 0.0)])
+def test_gpu_pairwise_count_equals_sort(cuda, n1, n2, nan_frac):
+    """The bitonic-sort (0) and counting (1) forms produce identical sufficient statistics."""
+    from foremast_amd.ops._lib import LIB, ptr, stream_of
+    R = 301
+    cur, base = _data(R, n1, n2, seed=n1 * 7 + n2, nan_frac=nan_frac)
+    c, b = torch.from_numpy(cur).to(cuda), torch.from_numpy(base).to(cuda)
+    out = []
+    for variant in (0, 1):
+        suff = torch.full((R, C.SUFF), -1.0, dtype=torch.float64, device=cuda)
+        LIB.call("fm_pairwise_suff_v", ptr(c), c.stride(0), n1, ptr(b), b.stride(0), n2, R, ptr(suff), 0, variant,
+                 stream_of(c))
+        out.append(suff.cpu().numpy())
+    exact = [0, 1, 2, 3, 4, 5, 6, 7, 12, 13]      # counts, rank sums, tie terms, KS D
+    np.testing.assert_array_equal(out[0][:, exact], out[1][:, exact])
+    np.testing.assert_allclose(out[0][:, 8:12], out[1][:, 8:12], rtol=1e-6, atol=1e-6)

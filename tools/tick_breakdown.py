@@ -53,6 +53,12 @@ def main():
     res["pairwise_us"] = timed(lambda: LIB.call(
         "fm_pairwise_tests", ptr(c), c.stride(0), c.shape[1], ptr(b), b.stride(0), b.shape[1], R, 63, 0, 0.05, 20, 20,
         5, ptr(pv), ptr(ps), ptr(df), ptr(suff), stream_of(c)))
+    res["pairwise_sortform_us"] = timed(lambda: LIB.call(
+        "fm_pairwise_suff_v", ptr(c), c.stride(0), c.shape[1], ptr(b), b.stride(0), b.shape[1], R, ptr(suff), 0, 0,
+        stream_of(c)))
+    res["pairwise_countform_us"] = timed(lambda: LIB.call(
+        "fm_pairwise_suff_v", ptr(c), c.stride(0), c.shape[1], ptr(b), b.stride(0), b.shape[1], R, ptr(suff), 0, 1,
+        stream_of(c)))
     res["canary_rows_us"] = timed(lambda: LIB.call(
         "fm_canary_rows", ptr(h), h.stride(0), T, ptr(c), c.stride(0), c.shape[1], ptr(b), b.stride(0), b.shape[1],
         R, ptr(hs), ptr(suff), stream_of(h)))
@@ -72,8 +78,8 @@ def main():
         res[f"pairwise_capped_{pb}_us"] = timed(lambda: LIB.call(
             "fm_pairwise_suff", ptr(c), c.stride(0), c.shape[1], ptr(b), b.stride(0), b.shape[1], R, ptr(suff),
             pb * cu, stream_of(c)))
-    for hb in (0, 4, 8):
-        for pb in (0, 1, 2, 4):
+    for hb in (0,):
+        for pb in (0, 2):
             sc = CanaryScorer(aliases, cfg, device=dev, mode="overlap", hist_blocks=hb * cu, pw_blocks=pb * cu)
             g = sc.capture(h, b, c, T)
             res[f"tick_overlap_h{hb}_p{pb}_us"] = timed(g)
