@@ -538,107 +538,135 @@ FM_API int fm_canary_rows(const float* hist, int64_t ld_h, int T, const float* c
   return 0;
 }
 
-__global__ __launch_bounds__(256) void pvalue_kernel(const double* __restrict__ suff, int64_t R, int test_mask,
-                                                     int combine_any, float p_thr, int min_mw, int min_wil,
-                                                     int min_kru, float* __restrict__ pvals,
-                                                     float* __restrict__ stats, int8_t* __restrict__ diff) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= R) return;
-  const double* o = suff + row * kSuff;
+// p-value of ONE test for one row from its sufficient statistics (NaN when the
+// test is gated out).  t is uniform per workgroup (grid y), so the fp64
+// special-function code paths never diverge inside a wave.
+__device__ __forceinline__ void eval_test(int t, const double* __restrict__ o, int min_mw, int min_wil, int min_kru,
+                                          double& pv, double& sv) {
   const int n1 = (int)o[0], n2 = (int)o[1], nw = (int)o[2];
   const double r1 = o[3], tie = o[4], dmax = o[5], rplus = o[6], tiew = o[7];
   const double m1 = o[8], m2 = o[9], q1 = o[10], q2 = o[11];
   const int n = n1 + n2;
   const double NaN = __builtin_nan("");
   double p[N_TESTS], st[N_TESTS];
-  for (int t = 0; t < N_TESTS; ++t) { p[t] = NaN; st[t] = NaN; }
+  p[t] = NaN; st[t] = NaN;
   const double dn1 = n1, dn2 = n2, dn = n;
-  // Mann-Whitney U (two-sided, continuity-corrected normal approximation)
-  if (n1 >= min_mw && n2 >= min_mw && n1 > 0 && n2 > 0) {
-    const double u1 = r1 - dn1 * (dn1 + 1.0) / 2.0;
-    const double u2 = dn1 * dn2 - u1;
-    const double u = u1 > u2 ? u1 : u2;
-    const double mu = dn1 * dn2 / 2.0;
-    const double var = dn1 * dn2 / 12.0 * ((dn + 1.0) - tie / (dn * (dn - 1.0)));
-    st[T_MW] = u1;
-    if (var > 0) {
-      const double z = (u - mu - 0.5) / sqrt(var);
-      double pp = 2.0 * norm_sf(z);
-      p[T_MW] = pp > 1.0 ? 1.0 : pp;
-    } else {
-      p[T_MW] = 1.0;
-    }
-  }
-  // Kruskal-Wallis H with two groups (tie-corrected), chi2 with 1 dof
-  if (n1 >= min_kru && n2 >= min_kru && n1 > 0 && n2 > 0) {
-    const double r2 = dn * (dn + 1.0) / 2.0 - r1;
-    double h = 12.0 / (dn * (dn + 1.0)) * (r1 * r1 / dn1 + r2 * r2 / dn2) - 3.0 * (dn + 1.0);
-    const double corr = 1.0 - tie / (dn * dn * dn - dn);
-    if (corr > 0) {
-      st[T_KRU] = h / corr;
-      // chi2(1) survival = erfc(sqrt(x/2))
-      p[T_KRU] = h / corr > 0 ? erfc(sqrt(0.5 * h / corr)) : 1.0;
-    }
-  }
-  // Two-sample Kolmogorov-Smirnov (asymptotic Kolmogorov distribution)
-  if (n1 >= min_mw && n2 >= min_mw && n1 > 0 && n2 > 0) {
-    const double en_ = dn1 * dn2 / (dn1 + dn2);
-    st[T_KS] = dmax;
-    p[T_KS] = kolmogorov_sf(sqrt(en_) * dmax);
-  }
-  // Welch t-test
-  if (n1 >= 2 && n2 >= 2 && n1 >= min_kru && n2 >= min_kru) {
-    const double v1 = q1 / (dn1 - 1.0), v2 = q2 / (dn2 - 1.0);
-    const double se2 = v1 / dn1 + v2 / dn2;
-    if (se2 > 0) {
-      const double t = (m1 - m2) / sqrt(se2);
-      const double a = v1 / dn1, bb = v2 / dn2;
-      const double df = se2 * se2 / (a * a / (dn1 - 1.0) + bb * bb / (dn2 - 1.0));
-      st[T_T] = t;
-      p[T_T] = student_t_2sided(t, df);
-    }
-  }
-  // Wilcoxon signed-rank (normal approximation, no continuity correction)
-  if (nw >= min_wil && nw > 0) {
-    const double dnw = nw;
-    const double tot = dnw * (dnw + 1.0) / 2.0;
-    const double rminus = tot - rplus;
-    const double T = rplus < rminus ? rplus : rminus;
-    const double mn = dnw * (dnw + 1.0) / 4.0;
-    const double se = sqrt(dnw * (dnw + 1.0) * (2.0 * dnw + 1.0) / 24.0 - tiew / 48.0);
-    st[T_WIL] = T;
-    if (se > 0) {
-      double pp = 2.0 * norm_sf(fabs((T - mn) / se));
-      p[T_WIL] = pp > 1.0 ? 1.0 : pp;
-    }
-  }
-  // Friedman chi-square over position-paired blocks with k = 2 treatments
-  // (current, baseline).  Within a block the ranks are {1,2} or {1.5,1.5};
-  // after the tie correction 1 - nzero/b the statistic reduces exactly to
-  // (npos - nneg)^2 / (npos + nneg) with 1 dof.
-  {
-    const int npos = (int)o[12], nzero = (int)o[13];
-    const int nneg = nw - npos, b = nw + nzero;
-    if (b >= min_wil && b > 0) {
-      const double q = nw > 0 ? (double)(npos - nneg) * (npos - nneg) / nw : 0.0;
-      st[T_FRI] = q;
-      p[T_FRI] = q > 0 ? erfc(sqrt(0.5 * q)) : 1.0;
-    }
-  }
-  int applicable = 0, significant = 0;
-  for (int t = 0; t < N_TESTS; ++t) {
-    pvals[row * N_TESTS + t] = (float)p[t];
-    stats[row * N_TESTS + t] = (float)st[t];
-    if ((test_mask >> t) & 1) {
-      if (!isnan(p[t])) {
-        ++applicable;
-        if (p[t] < p_thr) ++significant;
+  switch (t) {
+    case T_MW:
+      if (n1 >= min_mw && n2 >= min_mw && n1 > 0 && n2 > 0) {
+        const double u1 = r1 - dn1 * (dn1 + 1.0) / 2.0;
+        const double u2 = dn1 * dn2 - u1;
+        const double u = u1 > u2 ? u1 : u2;
+        const double mu = dn1 * dn2 / 2.0;
+        const double var = dn1 * dn2 / 12.0 * ((dn + 1.0) - tie / (dn * (dn - 1.0)));
+        st[T_MW] = u1;
+        if (var > 0) {
+          const double z = (u - mu - 0.5) / sqrt(var);
+          double pp = 2.0 * norm_sf(z);
+          p[T_MW] = pp > 1.0 ? 1.0 : pp;
+        } else {
+          p[T_MW] = 1.0;
+        }
+      }
+      break;
+    case T_KRU:
+      if (n1 >= min_kru && n2 >= min_kru && n1 > 0 && n2 > 0) {
+        const double r2 = dn * (dn + 1.0) / 2.0 - r1;
+        double h = 12.0 / (dn * (dn + 1.0)) * (r1 * r1 / dn1 + r2 * r2 / dn2) - 3.0 * (dn + 1.0);
+        const double corr = 1.0 - tie / (dn * dn * dn - dn);
+        if (corr > 0) {
+          st[T_KRU] = h / corr;
+          p[T_KRU] = h / corr > 0 ? erfc(sqrt(0.5 * h / corr)) : 1.0;   // chi2(1) survival
+        }
+      }
+      break;
+    case T_KS:
+      if (n1 >= min_mw && n2 >= min_mw && n1 > 0 && n2 > 0) {
+        const double en_ = dn1 * dn2 / (dn1 + dn2);
+        st[T_KS] = dmax;
+        p[T_KS] = kolmogorov_sf(sqrt(en_) * dmax);
+      }
+      break;
+    case T_T:
+      if (n1 >= 2 && n2 >= 2 && n1 >= min_kru && n2 >= min_kru) {
+        const double v1 = q1 / (dn1 - 1.0), v2 = q2 / (dn2 - 1.0);
+        const double se2 = v1 / dn1 + v2 / dn2;
+        if (se2 > 0) {
+          const double tt = (m1 - m2) / sqrt(se2);
+          const double a = v1 / dn1, bb = v2 / dn2;
+          const double df = se2 * se2 / (a * a / (dn1 - 1.0) + bb * bb / (dn2 - 1.0));
+          st[T_T] = tt;
+          p[T_T] = student_t_2sided(tt, df);
+        }
+      }
+      break;
+    case T_WIL:
+      if (nw >= min_wil && nw > 0) {
+        const double dnw = nw;
+        const double tot = dnw * (dnw + 1.0) / 2.0;
+        const double rminus = tot - rplus;
+        const double T = rplus < rminus ? rplus : rminus;
+        const double mn = dnw * (dnw + 1.0) / 4.0;
+        const double se = sqrt(dnw * (dnw + 1.0) * (2.0 * dnw + 1.0) / 24.0 - tiew / 48.0);
+        st[T_WIL] = T;
+        if (se > 0) {
+          double pp = 2.0 * norm_sf(fabs((T - mn) / se));
+          p[T_WIL] = pp > 1.0 ? 1.0 : pp;
+        }
+      }
+      break;
+    default: {  // T_FRI: k = 2 treatments over paired blocks, (n+ - n-)^2 / (n+ + n-), chi2(1)
+      const int npos = (int)o[12], nzero = (int)o[13];
+      const int nneg = nw - npos, b = nw + nzero;
+      if (b >= min_wil && b > 0) {
+        const double q = nw > 0 ? (double)(npos - nneg) * (npos - nneg) / nw : 0.0;
+        st[T_FRI] = q;
+        p[T_FRI] = q > 0 ? erfc(sqrt(0.5 * q)) : 1.0;
       }
     }
   }
-  int8_t d = 0;
-  if (applicable > 0) d = combine_any ? (significant > 0) : (significant == applicable);
-  diff[row] = d;
+  pv = p[t];
+  sv = st[t];
+}
+
+__global__ __launch_bounds__(256) void pvalue_kernel(const double* __restrict__ suff, int64_t R, int min_mw,
+                                                     int min_wil, int min_kru, float* __restrict__ pvals,
+                                                     float* __restrict__ stats) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.y;
+  if (row >= R) return;
+  double pv, sv;
+  eval_test(t, suff + row * kSuff, min_mw, min_wil, min_kru, pv, sv);
+  pvals[row * N_TESTS + t] = (float)pv;
+  stats[row * N_TESTS + t] = (float)sv;
+}
+
+// ALL / ANY over the selected, applicable tests -> "distribution differs".
+__global__ __launch_bounds__(256) void pcombine_kernel(const float* __restrict__ pvals, int64_t R, int test_mask,
+                                                       int combine_any, float p_thr, int8_t* __restrict__ diff) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= R) return;
+  int applicable = 0, significant = 0;
+#pragma unroll
+  for (int t = 0; t < N_TESTS; ++t) {
+    const float p = pvals[row * N_TESTS + t];
+    if (((test_mask >> t) & 1) && !isnan(p)) {
+      ++applicable;
+      if (p < p_thr) ++significant;
+    }
+  }
+  diff[row] = applicable > 0 ? (int8_t)(combine_any ? (significant > 0) : (significant == applicable)) : (int8_t)0;
+}
+
+static int launch_pvalues(const double* suff, int64_t R, int test_mask, int combine_any, float p_thr, int min_mw,
+                          int min_wil, int min_kru, float* pvals, float* stats, int8_t* diff, hipStream_t stream) {
+  const unsigned nb = (unsigned)((R + 255) / 256);
+  hipLaunchKernelGGL(pvalue_kernel, dim3(nb, N_TESTS), dim3(256), 0, stream, suff, R, min_mw, min_wil, min_kru, pvals,
+                     stats);
+  FM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(pcombine_kernel, dim3(nb), dim3(256), 0, stream, pvals, R, test_mask, combine_any, p_thr, diff);
+  FM_LAUNCH_CHECK();
+  return 0;
 }
 
 // variant: 0 = bitonic-sort form (default), 1 = counting form.  Measured at
@@ -679,10 +707,8 @@ FM_API int fm_pairwise_suff(const float* cur, int64_t ld_c, int n_cur, const flo
 FM_API int fm_pvalues(const double* suff, int64_t R, int test_mask, int combine_any, float p_thr, int min_mw,
                       int min_wil, int min_kru, float* pvals, float* stats, int8_t* diff, hipStream_t stream) {
   if (R <= 0) return 0;
-  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, suff, R, test_mask,
-                     combine_any, p_thr, min_mw, min_wil, min_kru, pvals, stats, diff);
-  FM_LAUNCH_CHECK();
-  return 0;
+  return launch_pvalues(suff, R, test_mask, combine_any, p_thr, min_mw, min_wil, min_kru, pvals, stats, diff,
+                        stream);
 }
 
 FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const float* base, int64_t ld_b, int n_base,
@@ -701,10 +727,8 @@ FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const fl
   else return (int)hipErrorInvalidValue;
 #undef FM_PW
   FM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, suff, R, test_mask,
-                     combine_any, p_thr, min_mw, min_wil, min_kru, pvals, stats, diff);
-  FM_LAUNCH_CHECK();
-  return 0;
+  return launch_pvalues(suff, R, test_mask, combine_any, p_thr, min_mw, min_wil, min_kru, pvals, stats, diff,
+                        stream);
 }
 
 // ---------------------------------------------------------------------------

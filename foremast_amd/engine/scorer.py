@@ -60,6 +60,11 @@ class CanaryScorer:
         # workgroup caps of the two concurrent kernels of the overlap tick
         # (0 = one workgroup per row / per 4 rows); see tools/tick_breakdown.py
         self.hist_blocks, self.pw_blocks = hist_blocks, pw_blocks
+        if self.mode == "overlap" and pw_blocks == 0 and self.device.type == "cuda":
+            # pairwise capped at 2 workgroups per CU so the concurrent HBM-bound
+            # history kernel keeps most wave slots (tick_breakdown sweeps:
+            # 716-759 us vs 729-782 us uncapped)
+            self.pw_blocks = 2 * torch.cuda.get_device_properties(self.device).multi_processor_count
         self._side = None
         self.cfg = cfg or BrainConfig()
         self.aliases = list(aliases)
