@@ -69,8 +69,7 @@ def add_rs(kube, depl, h, rev, image, pods=2):
     return rs
 
 
-@pytest.fixture
-def env():
+def _env(device="cpu"):
     clock = Clock()
     kube = K.FakeKube()
     for ns, ann in (("default", {}), ("foremast", {}), ("optout", {"foremast.ai/monitoring": "false"}),
@@ -79,12 +78,18 @@ def env():
     kube.create(K.METADATAS, "foremast", metadata_obj())
     store = MemoryStore()
     app = create_app(store)
-    brain = Brain(store, BrainConfig(), sources=SourceRouter.synthetic_only(faults={"-h2-": 8.0}), clock=clock)
+    brain = Brain(store, BrainConfig(), sources=SourceRouter.synthetic_only(faults={"-h2-": 8.0}), clock=clock,
+                  device=device)
     cfg = BarrelmanConfig(namespace="foremast")
     mgr = Manager(kube, cfg, analyst_factory=lambda ep: AnalystClient.for_app(app, ep, clock), clock=clock,
                   sleep=lambda s: None, inline=True)
     mgr.register_watches()
     return clock, kube, store, brain, mgr
+
+
+@pytest.fixture
+def env():
+    return _env()
 
 
 def monitor(kube, name="demo"):
@@ -135,6 +140,13 @@ def test_rolling_update_unhealthy_triggers_auto_rollback(env):
     assert any(e["reason"] == "Rollback" for e in kube.list(K.EVENTS, "default"))
     # the rollback itself is not monitored again (revision == rollbackRevision guard)
     assert monitor(kube).status.job_id == m.status.job_id
+
+
+@pytest.mark.gpu
+def test_gpu_rolling_update_rollback_full_loop(cuda):
+    """Deployment update -> monitor + job -> brain on the GPU (HIP kernels) ->
+    poller -> Unhealthy -> AutoRollback, all through the real contracts."""
+    test_rolling_update_unhealthy_triggers_auto_rollback(_env(cuda))
 
 
 def test_auto_pause(env):

@@ -1,0 +1,132 @@
+"""HttpKube (the real-cluster client) against an in-process API server: the
+REST paths of every resource kind, 404/409 mapping, merge-patch, rollback and
+the list+watch informer loop (httpx MockTransport over a FakeKube tracker)."""
+import json
+import threading
+import time
+
+import httpx
+import pytest
+
+from foremast_amd.controller import kube as K
+
+
+class FakeAPIServer:
+    def __init__(self):
+        self.kube = K.FakeKube()
+        self.watch_events: dict[str, list] = {}
+        self.requests = []
+
+    def _route(self, path):
+        parts = path.strip("/").split("/")
+        for res, (prefix, namespaced) in K.API_PATHS.items():
+            pp = prefix.strip("/").split("/")
+            if parts[:len(pp)] != pp:
+                continue
+            rest = parts[len(pp):]
+            ns = ""
+            if namespaced and len(rest) >= 2 and rest[0] == "namespaces":
+                ns, rest = rest[1], rest[2:]
+            if rest and rest[0] == res:
+                return res, ns, (rest[1] if len(rest) > 1 else "")
+        return None, "", ""
+
+    def handler(self, req: httpx.Request) -> httpx.Response:
+        res, ns, name = self._route(req.url.path)
+        self.requests.append((req.method, req.url.path, dict(req.url.params)))
+        if res is None:
+            return httpx.Response(404, json={"kind": "Status", "code": 404})
+        try:
+            if req.method == "GET" and req.url.params.get("watch") == "1":
+                evs = self.watch_events.pop(res, [])
+                body = "".join(json.dumps(e) + "\n" for e in evs)
+                return httpx.Response(200, content=body.encode())
+            if req.method == "GET" and name:
+                return httpx.Response(200, json=self.kube.get(res, ns, name))
+            if req.method == "GET":
+                return httpx.Response(200, json={"metadata": {"resourceVersion": "7"},
+                                                 "items": self.kube.list(res, ns)})
+            if req.method == "POST":
+                return httpx.Response(201, json=self.kube.create(res, ns, json.loads(req.content)))
+            if req.method == "PUT":
+                return httpx.Response(200, json=self.kube.update(res, ns, json.loads(req.content)))
+            if req.method == "DELETE":
+                self.kube.delete(res, ns, name)
+                return httpx.Response(200, json={"kind": "Status", "status": "Success"})
+        except K.NotFound:
+            return httpx.Response(404, json={"kind": "Status", "code": 404})
+        except K.Conflict:
+            return httpx.Response(409, json={"kind": "Status", "code": 409})
+        return httpx.Response(405)
+
+
+@pytest.fixture
+def api():
+    srv = FakeAPIServer()
+    client = httpx.Client(transport=httpx.MockTransport(srv.handler), base_url="https://k8s")
+    hk = K.HttpKube("https://k8s", token="t", client=client)
+    yield srv, hk
+    hk.stop()
+
+
+def test_crud_paths_and_errors(api):
+    srv, hk = api
+    hk.create(K.NAMESPACES, "", {"metadata": {"name": "default"}})
+    m = hk.create(K.MONITORS, "default", {"apiVersion": "deployment.foremast.ai/v1alpha1", "kind": "DeploymentMonitor",
+                                          "metadata": {"name": "demo", "namespace": "default"}, "spec": {}})
+    assert m["metadata"]["name"] == "demo"
+    assert ("POST", "/apis/deployment.foremast.ai/v1alpha1/namespaces/default/deploymentmonitors", {}) in srv.requests
+    hk.patch_merge(K.MONITORS, "default", "demo", {"spec": {"continuous": True}})
+    assert hk.get(K.MONITORS, "default", "demo")["spec"]["continuous"] is True
+    with pytest.raises(K.NotFound):
+        hk.get(K.MONITORS, "default", "nope")
+    with pytest.raises(K.Conflict):
+        hk.create(K.MONITORS, "default", {"metadata": {"name": "demo", "namespace": "default"}})
+    hk.create(K.PODS, "default", {"metadata": {"name": "p1", "namespace": "default", "labels": {"app": "a"}}})
+    hk.create(K.PODS, "default", {"metadata": {"name": "p2", "namespace": "default", "labels": {"app": "b"}}})
+    assert [p["metadata"]["name"] for p in hk.list(K.PODS, "default", {"app": "a"})] == ["p1"]
+    hk.delete(K.PODS, "default", "p2")
+    assert len(hk.list(K.PODS, "default")) == 1
+    assert any(p == "/api/v1/namespaces" for _, p, _ in srv.requests)
+
+
+def test_rollback_copies_revision_template(api):
+    srv, hk = api
+    d = hk.create(K.DEPLOYMENTS, "default", {
+        "metadata": {"name": "demo", "namespace": "default", "annotations": {K.REVISION_ANNOTATION: "2"}},
+        "spec": {"template": {"metadata": {"labels": {"app": "demo"}},
+                              "spec": {"containers": [{"name": "c", "image": "demo:v2"}]}}}})
+    hk.create(K.REPLICASETS, "default", {
+        "metadata": {"name": "demo-h1", "namespace": "default", "annotations": {K.REVISION_ANNOTATION: "1"},
+                     "ownerReferences": [{"uid": d["metadata"]["uid"]}]},
+        "spec": {"template": {"metadata": {"labels": {"app": "demo", "pod-template-hash": "h1"}},
+                              "spec": {"containers": [{"name": "c", "image": "demo:v1"}]}}}})
+    hk.rollback("default", "demo", 1)
+    got = hk.get(K.DEPLOYMENTS, "default", "demo")
+    assert got["spec"]["template"]["spec"]["containers"][0]["image"] == "demo:v1"
+    assert "pod-template-hash" not in got["spec"]["template"]["metadata"]["labels"]
+    with pytest.raises(K.NotFound):
+        hk.rollback("default", "demo", 9)
+
+
+def test_informer_list_then_watch(api):
+    srv, hk = api
+    srv.kube.create(K.HPAS, "default", {"metadata": {"name": "h1", "namespace": "default"}})
+    srv.watch_events[K.HPAS] = [
+        {"type": "ADDED", "object": {"metadata": {"name": "h2", "namespace": "default"}}},
+        {"type": "MODIFIED", "object": {"metadata": {"name": "h1", "namespace": "default"}, "spec": {"x": 1}}},
+        {"type": "DELETED", "object": {"metadata": {"name": "h2", "namespace": "default"}}},
+    ]
+    seen = []
+    done = threading.Event()
+
+    def handler(etype, old, new):
+        seen.append((etype, new["metadata"]["name"], old is not None))
+        if len(seen) >= 4:
+            done.set()
+    hk.watch(K.HPAS, handler, resync=0.5)
+    assert done.wait(10)
+    hk.stop()
+    assert seen[:4] == [("ADDED", "h1", False), ("ADDED", "h2", False), ("MODIFIED", "h1", True),
+                        ("DELETED", "h2", True)]
+    time.sleep(0.05)
