@@ -60,16 +60,16 @@ class CanaryScorer:
         # workgroup caps of the two concurrent kernels of the overlap tick
         # (0 = one workgroup per row / per 4 rows); see tools/tick_breakdown.py
         self.hist_blocks, self.pw_blocks = hist_blocks, pw_blocks
-        if self.mode == "overlap" and pw_blocks == 0 and self.device.type == "cuda":
-            # pairwise capped at 2 workgroups per CU so the concurrent HBM-bound
-            # history kernel keeps most wave slots (tick_breakdown sweeps:
-            # 716-759 us vs 729-782 us uncapped)
-            self.pw_blocks = 2 * torch.cuda.get_device_properties(self.device).multi_processor_count
         self._side = None
         self.cfg = cfg or BrainConfig()
         self.aliases = list(aliases)
         self.M = len(aliases)
         self.device = torch.device(device)
+        if self.mode == "overlap" and pw_blocks == 0 and self.device.type == "cuda":
+            # pairwise capped at 2 workgroups per CU so the concurrent HBM-bound
+            # history kernel keeps most wave slots (tick_breakdown sweeps:
+            # 716-759 us vs 729-782 us uncapped)
+            self.pw_blocks = 2 * torch.cuda.get_device_properties(self.device).multi_processor_count
         rules = [self.cfg.rule_for(a) for a in aliases]
         self.thr = torch.tensor([r.threshold for r in rules], dtype=torch.float32, device=self.device)
         self.bound = torch.tensor([r.bound for r in rules], dtype=torch.int32, device=self.device)
