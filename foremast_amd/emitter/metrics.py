@@ -3,14 +3,22 @@ Spring Boot starters (foremast-metrics/*; the reference ships Java only).
 
 What a service gets by wrapping its ASGI/WSGI app:
 
-* ``http_server_requests_seconds`` (count/sum/buckets) labelled ``app``,
-  ``status``, ``uri``, ``method`` and ``caller`` — the ``caller`` label comes
-  from the ``X-CALLER`` header (CallerWebMvcTagsProvider.java:22-36) and is
-  what the brain's downstream-impact graph is built from;
+* ``http_server_requests_seconds`` — a Micrometer-shaped timer exposed as a
+  Prometheus summary (``_count``, ``_sum``, client-side ``quantile`` samples
+  over a sliding window, plus ``_max``) labelled ``exception``, ``method``,
+  ``status``, ``uri``, ``caller`` and the common tags — the ``caller`` label
+  comes from the ``X-CALLER`` header (CallerWebMvcTagsProvider.java:22-36; an
+  empty header name drops the tag) and is what the brain's downstream-impact
+  graph is built from; default percentiles 0.95 / 0.98
+  (``management.metrics.distribution.percentiles.http.server.requests``,
+  starter ``config/application.properties:11``);
 * common tags resolved from ``app:ENV.APP_NAME|info.app.name``
   (K8sMetricsProperties.java ``commonTagNameValuePairs``);
-* zero-initialised series for ``initializeForStatuses`` (403,404,501,502) so
-  error-rate recording rules exist before the first error;
+* zero-initialised timers for ``initialize-for-statuses`` (403,404,500,503,
+  the starter's shipped ``application.properties:7``) with tags
+  ``exception=None, method=GET, uri=/**, caller=*``
+  (K8sMetricsAutoConfiguration.java:117-128) so error-rate recording rules
+  exist before the first error;
 * the common metrics filter (CommonMetricsFilter.java:38-196): per-metric
   enable map with dotted-prefix lookup and ``all`` fallback, whitelist,
   blacklist, prefixes, tag rules, runtime enable/disable;
@@ -19,12 +27,17 @@ What a service gets by wrapping its ASGI/WSGI app:
 """
 from __future__ import annotations
 
+import math
 import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable
 
-from prometheus_client import CollectorRegistry, Histogram, generate_latest
+import threading
+from collections import deque
+
+from prometheus_client import CollectorRegistry, generate_latest
+from prometheus_client.core import GaugeMetricFamily, Metric
 
 NEUTRAL, ACCEPT, DENY = "NEUTRAL", "ACCEPT", "DENY"
 
@@ -32,7 +45,7 @@ NEUTRAL, ACCEPT, DENY = "NEUTRAL", "ACCEPT", "DENY"
 @dataclass
 class K8sMetricsProperties:
     common_tag_name_value_pairs: str = "app:ENV.APP_NAME|info.app.name"
-    initialize_for_statuses: str = "403,404,501,502"
+    initialize_for_statuses: str = "403,404,500,503"
     caller_header: str = "X-CALLER"
     enable_common_metrics_filter: bool = False
     enable_common_metrics_filter_action: bool = False
@@ -41,6 +54,10 @@ class K8sMetricsProperties:
     common_metrics_prefix: str | None = None
     common_metrics_tag_rules: str | None = None
     enable: dict[str, bool] = field(default_factory=dict)    # management.metrics.enable.*
+    # management.metrics.distribution.percentiles.* (dotted name or "all")
+    percentiles: dict[str, list[float]] = field(
+        default_factory=lambda: {"http.server.requests": [0.95, 0.98]})
+    percentile_window: int = 1024          # observations kept per series for the quantiles
     info: dict[str, str] = field(default_factory=dict)       # info.app.name, ...
 
     @classmethod
@@ -82,7 +99,9 @@ class CommonMetricsFilter:
 
     @staticmethod
     def normalize(name: str) -> str:
-        return name.replace("_", ".")
+        """'_' -> '.' (CommonMetricsFilter.java) and a Prometheus unit suffix
+        dropped, so 'http_server_requests_seconds' names the meter too."""
+        return _meter_name(name)
 
     def _lookup_enable(self, name: str):
         vals = self.props.enable
@@ -151,8 +170,71 @@ def resolve_common_tags(spec: str, env=None, info: dict | None = None) -> dict[s
     return out
 
 
+_UNIT_SUFFIXES = ("_seconds_max", "_seconds", "_bytes", "_total", "_max")
+
+
+def _meter_name(family: str) -> str:
+    """Prometheus family name -> Micrometer meter name (dotted, unit suffix
+    stripped): http_server_requests_seconds -> http.server.requests."""
+    for suf in _UNIT_SUFFIXES:
+        if family.endswith(suf):
+            family = family[: -len(suf)]
+            break
+    return family.replace("_", ".")
+
+
+def _lookup_dotted(table: dict, name: str, default=None):
+    n = name
+    while n:
+        if n in table:
+            return table[n]
+        n = n[: n.rfind(".")] if "." in n else ""
+    return table.get("all", default)
+
+
+class Timer:
+    """Micrometer-style timer: count, total, and a sliding window of the last
+    ``window`` observations per label set for quantiles and max."""
+
+    def __init__(self, name: str, doc: str, labelnames: list[str], quantiles: list[float], window: int):
+        self.name, self.doc, self.labelnames = name, doc, labelnames
+        self.quantiles = sorted(quantiles)
+        self.window = window
+        self._series: dict[tuple, list] = {}
+        self._lock = threading.Lock()
+
+    def init(self, labels: tuple) -> None:
+        with self._lock:
+            self._series.setdefault(labels, [0, 0.0, deque(maxlen=self.window)])
+
+    def observe(self, labels: tuple, seconds: float) -> None:
+        with self._lock:
+            s = self._series.setdefault(labels, [0, 0.0, deque(maxlen=self.window)])
+            s[0] += 1
+            s[1] += seconds
+            s[2].append(seconds)
+
+    def collect(self):
+        summ = Metric(self.name, self.doc, "summary")
+        mx = GaugeMetricFamily(self.name + "_max", self.doc + " (window max)", labels=self.labelnames)
+        with self._lock:
+            items = [(k, v[0], v[1], sorted(v[2])) for k, v in self._series.items()]
+        for key, cnt, tot, win in items:
+            lab = dict(zip(self.labelnames, key))
+            for q in self.quantiles:
+                val = win[min(len(win) - 1, int(math.ceil(q * len(win))) - 1)] if win else 0.0
+                summ.add_sample(self.name, dict(lab, quantile=f"{q:g}"), val)
+            summ.add_sample(self.name + "_count", lab, float(cnt))
+            summ.add_sample(self.name + "_sum", lab, tot)
+            mx.add_metric(list(key), win[-1] if win else 0.0)
+        yield summ
+        yield mx
+
+
 class K8sMetrics:
     """Request metrics + filtered exposition for one application."""
+
+    METRIC = "http.server.requests"
 
     def __init__(self, props: K8sMetricsProperties | None = None, registry: CollectorRegistry | None = None,
                  env=None, clock: Callable[[], float] = time.perf_counter):
@@ -161,15 +243,25 @@ class K8sMetrics:
         self.filter = CommonMetricsFilter(self.props)
         self.common = resolve_common_tags(self.props.common_tag_name_value_pairs, env, self.props.info)
         self.clock = clock
-        self.labels = ["app", "method", "uri", "status", "caller"]
-        self.requests = Histogram("http_server_requests_seconds", "HTTP server request latency", self.labels,
-                                  registry=self.registry)
-        app = self.common.get("app", "")
+        self.with_caller = bool(self.props.caller_header)
+        self.labels = sorted(set(self.common) | {"exception", "method", "status", "uri"} |
+                             ({"caller"} if self.with_caller else set()))
+        q = _lookup_dotted(self.props.percentiles, self.METRIC, []) or []
+        self.requests = Timer("http_server_requests_seconds", "HTTP server request latency", self.labels, q,
+                              self.props.percentile_window)
+        self.registry.register(self.requests)
         for st in _tokens(self.props.initialize_for_statuses):
-            self.requests.labels(app, "GET", "UNKNOWN", st, "")
+            self.requests.init(self._key("GET", "/**", st, "*", "None"))
 
-    def record(self, method: str, uri: str, status: int | str, seconds: float, caller: str = "") -> None:
-        self.requests.labels(self.common.get("app", ""), method, uri, str(status), caller or "").observe(seconds)
+    def _key(self, method: str, uri: str, status, caller: str, exception: str) -> tuple:
+        vals = dict(self.common, exception=exception, method=method, status=str(status), uri=uri)
+        if self.with_caller:
+            vals["caller"] = caller or ""
+        return tuple(vals[k] for k in self.labels)
+
+    def record(self, method: str, uri: str, status: int | str, seconds: float, caller: str = "",
+               exception: str = "None") -> None:
+        self.requests.observe(self._key(method, uri, status, caller, exception), seconds)
 
     def exposition(self) -> bytes:
         """Prometheus text of the families the filter lets through."""
@@ -178,7 +270,7 @@ class K8sMetrics:
         class Filtered:
             def collect(self_inner):
                 for fam in self.registry.collect():
-                    dotted = fam.name.replace("_", ".")
+                    dotted = _meter_name(fam.name)
                     tags = fam.samples[0].labels if fam.samples else {}
                     if flt.accept(dotted, tags) != DENY:
                         yield fam
@@ -221,12 +313,17 @@ class K8sMetrics:
                 if msg["type"] == "http.response.start":
                     status["code"] = msg["status"]
                 await send(msg)
+            exc_name = "None"
             try:
                 await app(scope, receive, send_wrapper)
+            except Exception as e:
+                exc_name = type(e).__name__
+                raise
             finally:
                 route = scope.get("route")
                 uri = getattr(route, "path", None) or path
-                metrics.record(scope.get("method", "GET"), uri, status["code"], metrics.clock() - t0, caller)
+                metrics.record(scope.get("method", "GET"), uri, status["code"], metrics.clock() - t0, caller,
+                               exc_name)
         return wrapped
 
     # ------------------------------------------------------------------ WSGI

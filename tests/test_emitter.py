@@ -78,8 +78,37 @@ def test_asgi_middleware_records_caller_and_serves_endpoints():
     c = TestClient(m.asgi(api))
     assert c.get("/hello", headers={"X-CALLER": "checkout"}).status_code == 200
     text = c.get("/actuator/prometheus").text
-    assert 'http_server_requests_seconds_count{app="demo",caller="checkout",method="GET",status="200",uri="/hello"}' \
-        in text
-    assert 'status="404"' in text                 # initializeForStatuses
+    assert ('http_server_requests_seconds_count{app="demo",caller="checkout",exception="None",method="GET",'
+            'status="200",uri="/hello"} 1.0') in text
+    assert 'quantile="0.95"' in text and 'quantile="0.98"' in text and "http_server_requests_seconds_max" in text
+    # initialize-for-statuses: zero timers with the starter's tags
+    assert ('http_server_requests_seconds_count{app="demo",caller="*",exception="None",method="GET",status="404",'
+            'uri="/**"} 0.0') in text
     assert c.get("/k8s-metrics/disable/http_server_requests_seconds").status_code == 200
     assert "http_server_requests_seconds" not in c.get("/actuator/prometheus").text
+
+
+def test_timer_quantiles_window_and_no_caller_tag():
+    from foremast_amd.emitter.metrics import K8sMetrics
+    m = K8sMetrics(K8sMetricsProperties(caller_header="", initialize_for_statuses="",
+                                        percentiles={"all": [0.5, 0.9]}, percentile_window=100), env={})
+    for i in range(1, 201):                 # the window keeps the last 100: 101..200 ms
+        m.record("GET", "/x", 200, i / 1000.0)
+    text = m.exposition().decode()
+    assert "caller" not in text
+    assert 'http_server_requests_seconds{exception="None",method="GET",quantile="0.5",status="200",uri="/x"} 0.15' \
+        in text
+    assert 'quantile="0.9",status="200",uri="/x"} 0.19' in text
+    assert 'http_server_requests_seconds_sum{exception="None",method="GET",status="200",uri="/x"} 20.1' in text
+    assert 'http_server_requests_seconds_max{exception="None",method="GET",status="200",uri="/x"} 0.2' in text
+
+
+def test_filter_uses_meter_names():
+    from foremast_amd.emitter.metrics import K8sMetrics
+    m = K8sMetrics(K8sMetricsProperties(enable_common_metrics_filter=True, common_metrics_whitelist="http_server_requests"),
+                   env={})
+    m.record("GET", "/x", 200, 0.01)
+    assert "http_server_requests_seconds_count" in m.exposition().decode()
+    m2 = K8sMetrics(K8sMetricsProperties(enable_common_metrics_filter=True, enable={"http.server": False}), env={})
+    m2.record("GET", "/x", 200, 0.01)
+    assert "http_server_requests" not in m2.exposition().decode()
