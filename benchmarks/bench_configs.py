@@ -25,6 +25,7 @@ from __future__ import annotations
 import argparse
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -56,15 +57,41 @@ def config1(args):
     from foremast_amd.controller.analyst import AnalystClient
     from foremast_amd.engine.brain import Brain
     from foremast_amd.engine.sources import SourceRouter
-    from foremast_amd.service.app import create_app
-    from foremast_amd.service.store import MemoryStore
+    from foremast_amd.service.store import SQLiteStore
 
     info, dev = setup(gpus_required=args.device != "cpu")
     dev = torch.device("cpu") if args.device == "cpu" else dev
     t = {"now": 1_760_000_000.0}
     clock = lambda: t["now"]
-    store = MemoryStore()
-    client = AnalystClient.for_app(create_app(store), clock=clock)
+    # deployment shape (deploy/foremast/31-brain.yaml): the REST service is its
+    # own process (uvicorn on 127.0.0.1) sharing a WAL SQLite job store with the
+    # brain; the client side (barrelman / trigger role) talks HTTP with a pooled
+    # keep-alive connection
+    import socket
+    import subprocess
+    import tempfile
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    db = os.path.join(tempfile.mkdtemp(prefix="fm_c1_"), "jobs.db")
+    store = SQLiteStore(db)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    server = subprocess.Popen([sys.executable, "-m", "foremast_amd.cli", "service", "--port", str(port), "--store",
+                               f"sqlite:{db}"], cwd=root, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    client = AnalystClient(f"http://127.0.0.1:{port}/v1/healthcheck/", clock=clock)
+    deadline = time.time() + 120
+    while True:
+        try:
+            import httpx
+            if httpx.get(f"http://127.0.0.1:{port}/healthz", timeout=1).status_code == 200:
+                break
+        except Exception:
+            pass
+        if time.time() > deadline or server.poll() is not None:
+            raise SystemExit("REST service did not start")
+        time.sleep(0.2)
     cfg = BrainConfig()
     cfg.pairwise_algorithm = "TTEST"
     cfg.ml_algorithm = "moving_average_all"
@@ -82,11 +109,16 @@ def config1(args):
         for i in ids:
             client.get_status(i)
 
-    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    try:
+        ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    finally:
+        server.terminate()
+        server.wait(30)
     _common(args, info, ms, p50, "canary jobs judged/sec end-to-end (REST create -> brain -> REST status)",
             args.jobs / (ms / 1e3), "jobs/s", "pairwise Welch t-test (ML_PAIRWISE_ALGORITHM=TTEST) + "
             "moving_average_all, 1 metric latency_p99", args.jobs, T_HIST, "weak", "fp32",
-            "synthetic Prometheus query_range source (in-process), 5+5 pods x 10 points per side",
+            "synthetic Prometheus query_range source (in-process), 5+5 pods x 10 points per side; REST service "
+            "in its own process (uvicorn, 127.0.0.1) sharing a WAL SQLite job store with the brain",
             {"device": str(dev), "jobs_per_step": args.jobs})
 
 

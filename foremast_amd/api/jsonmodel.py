@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import dataclasses
+import functools
 import typing
 from typing import Any
 
@@ -81,14 +82,29 @@ def _convert(tp, v):
     return v
 
 
+@functools.lru_cache(maxsize=None)
+def _plan(cls) -> tuple:
+    """(attribute, json key, lower-cased key, type) per field — resolved once
+    per class (type-hint evaluation dominated decoding otherwise)."""
+    hints = typing.get_type_hints(cls)
+    out = []
+    for f in dataclasses.fields(cls):
+        name = f.metadata.get("json", f.name)
+        out.append((f.name, name, name.lower(), hints[f.name]))
+    return tuple(out)
+
+
 def from_json(cls, data: dict):
     if data is None:
         return cls()
-    hints = typing.get_type_hints(cls)
     kw = {}
-    for f in dataclasses.fields(cls):
-        name = f.metadata.get("json", f.name)
-        ok, v = _ci_get(data, name)
-        if ok:
-            kw[f.name] = _convert(hints[f.name], v)
+    lower = None
+    for attr, name, lname, tp in _plan(cls):
+        if name in data:
+            kw[attr] = _convert(tp, data[name])
+            continue
+        if lower is None:   # case-insensitive fallback, built once per object
+            lower = {k.lower(): v for k, v in data.items() if isinstance(k, str)}
+        if lname in lower:
+            kw[attr] = _convert(tp, lower[lname])
     return cls(**kw)

@@ -51,11 +51,16 @@ class AnalystClient:
         self.base_url = base_url if base_url.endswith("/") else base_url + "/"
         self.do = do or self._http_do
         self.clock = clock
+        self._http = None
 
-    @staticmethod
-    def _http_do(method: str, url: str, body: bytes | None) -> Response:
-        import httpx
-        r = httpx.request(method, url, content=body, headers={"Accept": "application/json"}, timeout=30)
+    def _http_do(self, method: str, url: str, body: bytes | None) -> Response:
+        # one pooled keep-alive client per analyst client (the 10 s poller and
+        # the trigger issue one request per monitored service per cycle)
+        if self._http is None:
+            import httpx
+            self._http = httpx.Client(timeout=30, headers={"Accept": "application/json",
+                                                          "Content-Type": "application/json"})
+        r = self._http.request(method, url, content=body)
         return Response(r.status_code, r.content)
 
     @classmethod

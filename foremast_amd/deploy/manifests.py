@@ -312,7 +312,7 @@ def brain(gpus: int = 8) -> list[dict]:
     mount = [{"name": "jobs", "mountPath": "/data"}]
     svc_c = {"name": "foremast-service", "image": IMAGE, "command": ["python", "-m", "foremast_amd.cli", "service"],
              "ports": [{"containerPort": 8099, "name": "api"}], "volumeMounts": mount,
-             "env": _env({"FOREMAST_STORE": "sqlite:/data/jobs.db",
+             "env": _env({"FOREMAST_STORE": "sqlite:/data/jobs.db", "SERVICE_WORKERS": 4,
                           "QUERY_SERVICE_ENDPOINT": "http://prometheus-k8s.monitoring.svc.cluster.local:9090/"}),
              "readinessProbe": {"httpGet": {"path": "/healthz", "port": 8099}},
              "resources": {"requests": {"cpu": "1", "memory": "1Gi"}}}

@@ -127,6 +127,13 @@ class Brain:
         self.info = D.env_info() if D.is_dist() else D.DistInfo()
         zoo.canonical(self.cfg.ml_algorithm)   # validate early
 
+    def _executor(self) -> ThreadPoolExecutor:
+        # one long-lived fetch pool (I/O-bound metric queries); spawning a pool
+        # per cycle cost more than small cycles' scoring
+        if getattr(self, "_pool", None) is None:
+            self._pool = ThreadPoolExecutor(max_workers=max(1, self.fetch_threads), thread_name_prefix="brain-fetch")
+        return self._pool
+
     # ------------------------------------------------------------------ claim
     def _owner(self, doc: Document) -> bool:
         if self.info.world <= 1:
@@ -247,8 +254,7 @@ class Brain:
             # ranks without work still join the tick's collective
             fleet = self._gather([])
             return {"claimed": 0, "fleet": len(fleet)}
-        with ThreadPoolExecutor(max_workers=max(1, min(self.fetch_threads, len(docs)))) as ex:
-            works = list(ex.map(lambda d: self._fetch_job(d, now), docs))
+        works = list(self._executor().map(lambda d: self._fetch_job(d, now), docs))
         rows: list[Row] = []
         for j, wk in enumerate(works):
             for r in wk.rows:

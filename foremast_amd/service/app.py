@@ -158,20 +158,37 @@ def create_app(store: JobStore | None = None, cfg: ServiceConfig | None = None, 
     return app
 
 
+def app_from_env() -> FastAPI:
+    """Factory for multi-worker uvicorn (each worker opens the store itself)."""
+    from .store import open_store
+    cfg = ServiceConfig.from_env()
+    return create_app(open_store(cfg.store, cfg.elastic_url), cfg)
+
+
 def main() -> None:  # pragma: no cover - entry point
     import argparse
+    import os
+
     import uvicorn
-    from .store import open_store
 
     ap = argparse.ArgumentParser(description="foremast-service (MI355X framework)")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--store", default=None, help="memory | sqlite:<path> | elasticsearch")
+    ap.add_argument("--workers", type=int, default=int(os.environ.get("SERVICE_WORKERS", "1")),
+                    help="uvicorn worker processes (sqlite/elasticsearch stores only: memory is per process)")
     a = ap.parse_args()
     cfg = ServiceConfig.from_env()
     if a.store:
         cfg.store = a.store
-    store = open_store(cfg.store, cfg.elastic_url)
-    uvicorn.run(create_app(store, cfg), host="0.0.0.0", port=a.port or cfg.port)
+        os.environ["FOREMAST_STORE"] = a.store
+    port = a.port or cfg.port
+    if a.workers > 1 and cfg.store != "memory":
+        uvicorn.run("foremast_amd.service.app:app_from_env", factory=True, host="0.0.0.0", port=port,
+                    workers=a.workers, log_level="warning", access_log=False)
+        return
+    from .store import open_store
+    uvicorn.run(create_app(open_store(cfg.store, cfg.elastic_url), cfg), host="0.0.0.0", port=port,
+                log_level="warning", access_log=False)
 
 
 if __name__ == "__main__":  # pragma: no cover

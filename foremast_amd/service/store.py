@@ -128,6 +128,12 @@ class MemoryStore(JobStore):
         rows.sort(key=lambda l: l.get("timestamp", 0.0), reverse=True)
         return [HPALog.from_dict(r) for r in rows[:size]]
 
+    def _claim_candidates(self) -> list[Document]:
+        # filter on the stored dicts before decoding (completed documents
+        # accumulate; only live ones are worth deserialising)
+        live = ST.CLAIMABLE | ST.IN_PROGRESS
+        return [Document.from_dict(d) for d in self._docs.values() if d.get("status") in live]
+
     def claim(self, worker, limit, max_stuck_s, now=None, owner=None):
         with self._lock:
             return super().claim(worker, limit, max_stuck_s, now, owner)
@@ -148,6 +154,10 @@ class SQLiteStore(JobStore):
         if c is None:
             c = sqlite3.connect(self.path, timeout=30, isolation_level=None)
             c.execute("pragma journal_mode=wal")
+            # WAL + NORMAL: no fsync per autocommit statement; the database stays
+            # consistent on a crash (a power loss may drop the last commits, which
+            # the brain re-derives: job ids are deterministic and claims lease out)
+            c.execute("pragma synchronous=normal")
             self._local.c = c
         return c
 
