@@ -1022,6 +1022,131 @@ FM_API int fm_window_decide(const float* hs, const float* cur, int64_t ld_c, int
 }
 
 // ---------------------------------------------------------------------------
+// Decision + pairwise combine + service reduce in ONE launch: a workgroup per
+// service, one wave per metric row (M <= 16).  Each wave folds its row's
+// p-values into "distribution differs" (lanes 0..N_TESTS-1 + two ballots),
+// lowers the threshold accordingly, flags the current window against the
+// history band, and the M waves reduce to the packed service verdict through
+// LDS.  Replaces pcombine + window_decide + service_reduce (two kernel
+// boundaries fewer per tick, which is what a small per-GPU shard pays for).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void decide_service_kernel(
+    const float* __restrict__ hs, const float* __restrict__ cur, int64_t ld_c, int n_cur, int64_t S, int M,
+    const float* __restrict__ thr, const int* __restrict__ bound, const float* __restrict__ minlb, float pair_factor,
+    const float* __restrict__ pvals, int test_mask, int combine_any, float p_thr, int min_hist,
+    float* __restrict__ out_stats, unsigned long long* __restrict__ out_flags, int NW, int* __restrict__ out_count,
+    float* __restrict__ out_score, int* __restrict__ out_valid, int8_t* __restrict__ out_diff,
+    float* __restrict__ packed) {
+  __shared__ int s_cnt[16], s_valid[16];
+  __shared__ float s_best[16];
+  const int64_t svc = blockIdx.x;
+  const int m = wave_id();
+  const int lane = lane_id();
+  const int64_t row = svc * M + m;
+  // pairwise combine
+  bool differs = false;
+  if (pvals != nullptr) {
+    const float p = lane < N_TESTS ? pvals[row * N_TESTS + lane] : NAN;
+    const bool sel = lane < N_TESTS && ((test_mask >> lane) & 1) && !isnan(p);
+    const unsigned long long app = __ballot(sel), sig = __ballot(sel && p < p_thr);
+    differs = app != 0ull && (combine_any ? sig != 0ull : sig == app);
+    if (lane == 0 && out_diff != nullptr) out_diff[row] = (int8_t)differs;
+  }
+  const float mf = hs[row * 3 + 0], sd = hs[row * 3 + 1];
+  const int n = (int)hs[row * 3 + 2];
+  float th = thr[m];
+  if (differs) th *= pair_factor;
+  const int bd = bound[m];
+  const float up = mf + th * sd;
+  float lo = mf - th * sd;
+  if (lo < minlb[m]) lo = minlb[m];
+  const bool has_hist = n >= min_hist && n > 0;
+  const float inv = sd > 0.f ? 1.0f / sd : 0.f;
+  const float* cr = cur + row * ld_c;
+  int acnt = 0, ccnt = 0;
+  float best = 0.f;
+  for (int i0 = 0; i0 < n_cur; i0 += 64) {
+    const int i = i0 + lane;
+    bool f = false;
+    if (i < n_cur) {
+      const float x = cr[i];
+      if (isfinite(x)) {
+        ++ccnt;
+        if (has_hist) {
+          const bool hi = (bd & 1) && x > up;
+          const bool lw = (bd & 2) && x < lo;
+          f = hi || lw;
+          if (f) {
+            ++acnt;
+            const float z = sd > 0.f ? (hi ? x - up : lo - x) * inv : 1e30f;
+            best = z > best ? z : best;
+          }
+        }
+      }
+    }
+    const unsigned long long bal = __ballot(f);
+    if (lane == 0 && i0 / 64 < NW) out_flags[row * NW + i0 / 64] = bal;
+  }
+  acnt = wave_sum(acnt);
+  ccnt = wave_sum(ccnt);
+  best = wave_max(best);
+  const int valid = (has_hist ? 1 : 0) | (ccnt > 0 ? 2 : 0);
+  if (lane == 0) {
+    out_stats[row * 4 + 0] = mf;
+    out_stats[row * 4 + 1] = sd;
+    out_stats[row * 4 + 2] = up;
+    out_stats[row * 4 + 3] = lo;
+    out_count[row] = acnt;
+    out_score[row] = best;
+    out_valid[row] = valid;
+    s_cnt[m] = acnt;
+    s_valid[m] = valid;
+    s_best[m] = best;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0, mask = 0;
+    bool unknown = false;
+    float b = 0.f;
+    for (int k = 0; k < M; ++k) {
+      tot += s_cnt[k];
+      if (s_cnt[k] > 0) mask |= 1 << k;
+      if ((s_valid[k] & 3) != 3) unknown = true;
+      b = s_best[k] > b ? s_best[k] : b;
+    }
+    packed[svc * 4 + 0] = (float)(tot > 0 ? 1 : (unknown ? 2 : 0));
+    packed[svc * 4 + 1] = b;
+    packed[svc * 4 + 2] = (float)mask;
+    packed[svc * 4 + 3] = (float)tot;
+  }
+}
+
+FM_API int fm_decide_services(const float* hs, const float* cur, int64_t ld_c, int n_cur, int64_t S, int M,
+                              const float* thr, const int* bound, const float* minlb, float pair_factor,
+                              const float* pvals, int test_mask, int combine_any, float p_thr, int min_hist,
+                              float* out_stats, unsigned long long* out_flags, int NW, int* out_count,
+                              float* out_score, int* out_valid, int8_t* out_diff, float* packed,
+                              hipStream_t stream) {
+  if (S <= 0) return 0;
+  if (M < 1 || M > 16 || NW * 64 < n_cur) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(decide_service_kernel, dim3((unsigned)S), dim3(64 * M), 0, stream, hs, cur, ld_c, n_cur, S, M,
+                     thr, bound, minlb, pair_factor, pvals, test_mask, combine_any, p_thr, min_hist, out_stats,
+                     out_flags, NW, out_count, out_score, out_valid, out_diff, packed);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// p-values only (the combine happens in fm_decide_services)
+FM_API int fm_pvalues_only(const double* suff, int64_t R, int min_mw, int min_wil, int min_kru, float* pvals,
+                           float* stats, hipStream_t stream) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)((R + 255) / 256), N_TESTS), dim3(256), 0, stream, suff, R,
+                     min_mw, min_wil, min_kru, pvals, stats);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // Service reduce: per service, fold its M metric rows into the packed result
 // row [status, score, anomalous-metric mask, anomalous point count] that is
 // all-gathered across ranks.  status: 0 = no anomaly, 1 = anomaly, 2 = unknown

@@ -113,6 +113,7 @@ class CanaryScorer:
         has_base = base is not None and base.shape[1] > 0
         if self.mode == "fused":
             self._fused(hist, base if has_base else None, cur, n_hist, o)
+            return o
         elif not self.overlap:
             if has_base:
                 self._pairwise_into(cur, base, o)
@@ -128,21 +129,35 @@ class CanaryScorer:
             if has_base:
                 side = self._side_stream(dev)
                 side.wait_stream(main)
+                # the cap only pays when each capped wave still loops over many
+                # rows; a small shard (per-GPU slice of a multi-GPU fleet) runs
+                # one row per wave
+                cap = self.pw_blocks if R > 32 * self.pw_blocks else 0
                 with torch.cuda.stream(side):
-                    self._pairwise_into(cur, base, o, self.pw_blocks)
+                    self._pairwise_into(cur, base, o, cap, combine=False)
             T = hist.shape[1] if n_hist is None else int(n_hist)
             C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
             LIB.call("fm_hist_stats_capped", ptr(hist), hist.stride(0), T, R, ptr(o.hs), self.hist_blocks,
                      stream_of(hist))
             if has_base:
                 main.wait_stream(side)
-            d = o.decide
-            LIB.call("fm_window_decide", ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1], R, self.M, ptr(self.thr),
-                     ptr(self.bound), ptr(self.minlb), float(self.cfg.pairwise_threshold_factor),
-                     ptr(o.diff) if has_base else None, int(self.cfg.min_historical_points), ptr(d.stats),
-                     ptr(d.flags), d.flags.shape[1], ptr(d.count), ptr(d.score), ptr(d.valid), stream_of(cur))
+            self._decide_services(cur, o, has_base)
+            return o
         C.service_reduce(o.decide.count, o.decide.score, o.decide.valid, self.M, out=o.packed)
         return o
+
+    def _decide_services(self, cur, o: CanaryOutputs, has_base: bool) -> None:
+        """p-value combine + window decision + service reduce, one launch
+        (a workgroup per service, a wave per metric row)."""
+        from ..ops._lib import LIB, ptr, stream_of
+        C.check(self.M <= 16, "overlap/fused ticks support up to 16 metrics per service (use mode='serial')")
+        mask, anyc = self.pcfg.mask_and_combine()
+        d = o.decide
+        LIB.call("fm_decide_services", ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1], cur.shape[0] // self.M,
+                 self.M, ptr(self.thr), ptr(self.bound), ptr(self.minlb), float(self.cfg.pairwise_threshold_factor),
+                 ptr(o.pvals) if has_base else None, mask, anyc, float(self.pcfg.p_threshold),
+                 int(self.cfg.min_historical_points), ptr(d.stats), ptr(d.flags), d.flags.shape[1], ptr(d.count),
+                 ptr(d.score), ptr(d.valid), ptr(o.diff) if has_base else None, ptr(o.packed), stream_of(cur))
 
     def _fused(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:
         from ..ops._lib import LIB, ptr, stream_of
@@ -155,29 +170,29 @@ class CanaryScorer:
                  ptr(base) if has_base else None, base.stride(0) if has_base else 0,
                  base.shape[1] if has_base else 0, R, ptr(o.hs), ptr(o.suff), st)
         if has_base:
-            mask, anyc = self.pcfg.mask_and_combine()
-            LIB.call("fm_pvalues", ptr(o.suff), R, mask, anyc, float(self.pcfg.p_threshold), self.pcfg.min_mann_white,
-                     self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(o.diff), st)
-        d = o.decide
-        LIB.call("fm_window_decide", ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1], R, self.M, ptr(self.thr),
-                 ptr(self.bound), ptr(self.minlb), float(self.cfg.pairwise_threshold_factor),
-                 ptr(o.diff) if has_base else None, int(self.cfg.min_historical_points), ptr(d.stats),
-                 ptr(d.flags), d.flags.shape[1], ptr(d.count), ptr(d.score), ptr(d.valid), st)
+            LIB.call("fm_pvalues_only", ptr(o.suff), R, self.pcfg.min_mann_white, self.pcfg.min_wilcoxon,
+                     self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), st)
+        self._decide_services(cur, o, has_base)
 
     def _side_stream(self, dev):
         if self._side is None:
             self._side = torch.cuda.Stream(dev)
         return self._side
 
-    def _pairwise_into(self, cur, base, o: CanaryOutputs, max_blocks: int = 0) -> None:
+    def _pairwise_into(self, cur, base, o: CanaryOutputs, max_blocks: int = 0, combine: bool = True) -> None:
         from ..ops._lib import LIB, ptr, stream_of
         R = cur.shape[0]
-        mask, anyc = self.pcfg.mask_and_combine()
         st = stream_of(cur)
         LIB.call("fm_pairwise_suff", ptr(cur), cur.stride(0), cur.shape[1], ptr(base), base.stride(0),
                  base.shape[1], R, ptr(o.suff), int(max_blocks), st)
-        LIB.call("fm_pvalues", ptr(o.suff), R, mask, anyc, float(self.pcfg.p_threshold), self.pcfg.min_mann_white,
-                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(o.diff), st)
+        if combine:
+            mask, anyc = self.pcfg.mask_and_combine()
+            LIB.call("fm_pvalues", ptr(o.suff), R, mask, anyc, float(self.pcfg.p_threshold),
+                     self.pcfg.min_mann_white, self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals),
+                     ptr(o.pstats), ptr(o.diff), st)
+        else:
+            LIB.call("fm_pvalues_only", ptr(o.suff), R, self.pcfg.min_mann_white, self.pcfg.min_wilcoxon,
+                     self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), st)
 
     # -- HIP graph capture of the whole tick ---------------------------------
     def capture(self, hist, base, cur, n_hist=None):

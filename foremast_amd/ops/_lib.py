@@ -57,6 +57,10 @@ _SIGS: dict[str, list] = {
     "fm_downstream_impact": [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p],
     "fm_segment_max": [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p],
     "fm_selftest_lanes": [c_void_p, c_void_p, c_void_p],
+    "fm_decide_services": [c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                           c_void_p, c_int, c_int, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p],
+    "fm_pvalues_only": [c_void_p, c_i64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fm_pairwise_suff": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_void_p],
     "fm_pairwise_suff_v": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_void_p],
     "fm_hist_stats_capped": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_void_p],
