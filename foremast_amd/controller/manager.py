@@ -44,7 +44,8 @@ def main() -> None:  # pragma: no cover - entry point
     ap.add_argument("--apiserver", default=None, help="API server URL (default: in-cluster)")
     ap.add_argument("--token", default=None)
     a = ap.parse_args()
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    from ..utils import logs
+    logs.setup(component="barrelman")
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())

@@ -125,6 +125,8 @@ class Brain:
         self.lstm_model = lstm_model
         self.hpa_state: dict[str, MI.HpaState] = {}
         self.info = D.env_info() if D.is_dist() else D.DistInfo()
+        from ..utils.spans import Spans
+        self.spans = Spans(exporter.registry if exporter is not None else None)
         zoo.canonical(self.cfg.ml_algorithm)   # validate early
 
     def _executor(self) -> ThreadPoolExecutor:
@@ -254,23 +256,26 @@ class Brain:
             # ranks without work still join the tick's collective
             fleet = self._gather([])
             return {"claimed": 0, "fleet": len(fleet)}
-        works = list(self._executor().map(lambda d: self._fetch_job(d, now), docs))
+        with self.spans.span("fetch"):
+            works = list(self._executor().map(lambda d: self._fetch_job(d, now), docs))
         rows: list[Row] = []
         for j, wk in enumerate(works):
             for r in wk.rows:
                 r.job = j
                 rows.append(r)
-        res = self.score_rows(rows) if rows else None
+        with self.spans.span("score"):
+            res = self.score_rows(rows) if rows else None
         outcome = {}
         summaries = []
         offs = 0
-        for j, wk in enumerate(works):
-            k = len(wk.rows)
-            sl = slice(offs, offs + k)
-            offs += k
-            st = self._finish(wk, rows[sl], res, sl, now)
-            outcome[st] = outcome.get(st, 0) + 1
-            summaries.append((wk.doc.id, wk.doc.namespace, wk.doc.app_name, st))
+        with self.spans.span("finish"):
+            for j, wk in enumerate(works):
+                k = len(wk.rows)
+                sl = slice(offs, offs + k)
+                offs += k
+                st = self._finish(wk, rows[sl], res, sl, now)
+                outcome[st] = outcome.get(st, 0) + 1
+                summaries.append((wk.doc.id, wk.doc.namespace, wk.doc.app_name, st))
         if self.exporter is not None:
             self.exporter.tick_seconds.observe(time.perf_counter() - t0)
             self.exporter.windows.inc(len(rows))

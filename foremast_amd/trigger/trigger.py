@@ -203,7 +203,8 @@ class Trigger:
 
 
 def main() -> None:  # pragma: no cover - entry point
-    logging.basicConfig(level=logging.INFO)
+    from ..utils import logs
+    logs.setup(component="trigger")
     services = parse_requests(open(os.environ["REQUESTS_FILE"]).read())
     client = AnalystClient(os.environ.get("FOREMAST_SERVICE_ENDPOINT", "http://localhost:8099") + "/v1/healthcheck/")
     t = Trigger(client, os.environ.get("WAVEFRONT_ENDPOINT", ""), os.environ.get("WAVEFRONT_TOKEN", ""),

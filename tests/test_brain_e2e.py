@@ -149,3 +149,20 @@ def test_gpu_brain_every_algorithm(cuda, algo):
     assert st.status in (crd.PHASE_UNHEALTHY, crd.PHASE_RUNNING)
     if algo in ("moving_average_all", "moving_average", "prophet"):
         assert st.status == crd.PHASE_UNHEALTHY
+
+
+def test_stage_spans_and_json_logs(capsys):
+    import json as _json
+    import logging
+    from foremast_amd.utils import logs
+    clock, store, client, brain, exp = _setup()
+    client.start_analyzing("default", "demo", PODS[:1], _metrics(), 10, "rollingUpdate")
+    brain.run_once()
+    for stage in ("fetch", "score", "finish"):
+        assert exp.registry.get_sample_value("foremast_stage_seconds_count", {"stage": stage}) == 1.0
+    logs.setup(component="brain", fmt="json")
+    logs.log_fields(logging.getLogger("foremast.test"), logging.INFO, "tick", rows=3)
+    line = capsys.readouterr().err.strip().splitlines()[-1]
+    rec = _json.loads(line)
+    assert rec["msg"] == "tick" and rec["rows"] == 3 and rec["component"] == "brain" and rec["level"] == "info"
+    logging.getLogger().handlers[:] = []
