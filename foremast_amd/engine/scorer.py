@@ -65,11 +65,17 @@ class CanaryScorer:
         self.aliases = list(aliases)
         self.M = len(aliases)
         self.device = torch.device(device)
-        if self.mode == "overlap" and pw_blocks == 0 and self.device.type == "cuda":
-            # pairwise capped at 2 workgroups per CU so the concurrent HBM-bound
-            # history kernel keeps most wave slots (tick_breakdown sweeps:
-            # 716-759 us vs 729-782 us uncapped)
-            self.pw_blocks = 2 * torch.cuda.get_device_properties(self.device).multi_processor_count
+        if self.mode == "overlap" and self.device.type == "cuda":
+            # Concurrent kernels of the tick, capped in workgroups per CU
+            # (tools/tick_breakdown.py sweeps, 80k rows): pairwise at 1 WG/CU
+            # (one wave per SIMD) and the persistent history stream at 8 WG/CU
+            # give 597-613 us vs 668-700 us uncapped; fewer pairwise workgroups
+            # make the side stream the critical path (0.5 WG/CU: ~800 us).
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            if pw_blocks == 0:
+                self.pw_blocks = cus
+            if hist_blocks == 0:
+                self.hist_blocks = 8 * cus
         rules = [self.cfg.rule_for(a) for a in aliases]
         self.thr = torch.tensor([r.threshold for r in rules], dtype=torch.float32, device=self.device)
         self.bound = torch.tensor([r.bound for r in rules], dtype=torch.int32, device=self.device)

@@ -78,11 +78,15 @@ def main():
         res[f"pairwise_capped_{pb}_us"] = timed(lambda: LIB.call(
             "fm_pairwise_suff", ptr(c), c.stride(0), c.shape[1], ptr(b), b.stride(0), b.shape[1], R, ptr(suff),
             pb * cu, stream_of(c)))
-    for hb in (0,):
-        for pb in (0, 2):
-            sc = CanaryScorer(aliases, cfg, device=dev, mode="overlap", hist_blocks=hb * cu, pw_blocks=pb * cu)
+    # caps in workgroups per CU (fractions allowed), override with env SWEEP_H / SWEEP_P
+    hs_ = [float(x) for x in os.environ.get("SWEEP_H", "0,4").split(",")]
+    ps_ = [float(x) for x in os.environ.get("SWEEP_P", "1,2").split(",")]
+    for hb in hs_:
+        for pb in ps_:
+            sc = CanaryScorer(aliases, cfg, device=dev, mode="overlap", hist_blocks=max(1, int(hb * cu)) if hb else -1,
+                              pw_blocks=max(1, int(pb * cu)) if pb else -1)
             g = sc.capture(h, b, c, T)
-            res[f"tick_overlap_h{hb}_p{pb}_us"] = timed(g)
+            res[f"tick_overlap_h{hb:g}_p{pb:g}_us"] = timed(g)
     res["hist_bytes_GB"] = R * T * 4 / 1e9
     res["hist_TBps"] = res["hist_bytes_GB"] / (res["hist_stats_us"] * 1e-6) / 1e3
     print(json.dumps(res))
