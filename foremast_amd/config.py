@@ -72,6 +72,9 @@ class BrainConfig:
     hpa_breath_down: float = 300.0
     hpa_max_flips: int = 4                   # docs/dynamic_autoscaling.md:127-130 (flip feedback)
     hpa_flip_window: float = 1800.0
+    # load forecast published for HPA jobs (cluster-autoscaler prediction)
+    hpa_forecast_algorithm: str = "double_exponential_smoothing"   # HPA_FORECAST_ALGORITHM ("" disables)
+    hpa_forecast_steps: int = 15                                    # HPA_FORECAST_STEPS (60 s samples)
 
     def rule_for(self, alias: str) -> MetricRule:
         """Per-metric override: exact alias match first, then substring match
@@ -115,6 +118,8 @@ class BrainConfig:
         c.poll_interval = _f(env, "POLL_INTERVAL", c.poll_interval)
         c.hpa_breath_up = _f(env, "HPA_BREATH_UP_SECONDS", c.hpa_breath_up)
         c.hpa_breath_down = _f(env, "HPA_BREATH_DOWN_SECONDS", c.hpa_breath_down)
+        c.hpa_forecast_algorithm = env.get("HPA_FORECAST_ALGORITHM", c.hpa_forecast_algorithm)
+        c.hpa_forecast_steps = _i(env, "HPA_FORECAST_STEPS", c.hpa_forecast_steps)
         return c
 
 

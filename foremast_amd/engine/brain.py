@@ -228,6 +228,7 @@ class Brain:
         dec = zoo.decide(self.cfg.ml_algorithm, hist, T, cur, hor, R, tables, diff, lstm_model=self.lstm_model,
                          pairs=pairs)
         out = {k: getattr(dec, k).detach().cpu().numpy() for k in ("upper", "lower", "count", "score", "valid")}
+        out["_hist"], out["_T"] = hist, T
         out["flags"] = C.unpack_flags(dec.flags, cur.shape[1])
         out["diff"] = None if diff is None else diff.cpu().numpy()
         return out
@@ -268,6 +269,9 @@ class Brain:
         outcome = {}
         summaries = []
         offs = 0
+        if res is not None and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
+            with self.spans.span("forecast"):
+                self._hpa_forecasts(works, rows, res)
         with self.spans.span("finish"):
             for j, wk in enumerate(works):
                 k = len(wk.rows)
@@ -349,6 +353,30 @@ class Brain:
             return ST.COMPLETED_HEALTH
         self.store.update(doc.id, status=ST.PREPROCESS_COMPLETED)
         return ST.PREPROCESS_COMPLETED
+
+    def _hpa_forecasts(self, works: list[Work], rows: list[Row], res) -> None:
+        """Batched H-step load forecast for every row of this cycle's HPA jobs,
+        published as ``foremastbrain:<metric>_forecast_max`` (max over the next
+        ``hpa_forecast_steps`` samples) so a cluster autoscaler can provision
+        ahead of the HPA."""
+        idx = [i for i, r in enumerate(rows) if works[r.job].hpa]
+        if not idx:
+            return
+        hist, T = res["_hist"], res["_T"]
+        sel = torch.as_tensor(idx, dtype=torch.int64, device=hist.device)
+        h = hist.index_select(0, sel).contiguous()
+        try:
+            fc, _ = zoo.forecast(self.cfg.hpa_forecast_algorithm, h, T, max(1, self.cfg.hpa_forecast_steps),
+                                 lstm_model=self.lstm_model)
+        except (ValueError, RuntimeError) as e:
+            log.warning("HPA forecast skipped: %s", e)
+            return
+        peak = torch.nan_to_num(fc, nan=float("-inf")).amax(1).cpu().numpy()
+        for k, i in enumerate(idx):
+            r = rows[i]
+            wk = works[r.job]
+            if np.isfinite(peak[k]):
+                self.exporter.set_forecast(r.base_metric, wk.namespace, wk.doc.app_name, float(peak[k]))
 
     def _finish_hpa(self, wk: Work, rows: list[Row], res, sl: slice, now: float) -> str:
         doc = wk.doc

@@ -58,6 +58,13 @@ class BrainExporter:
         self._gauge(b + "_anomaly", "unix time of the newest anomalous point (NaN when none)").labels(
             namespace, app).set(anomaly)
 
+    def set_forecast(self, base_metric: str, namespace: str, app: str, value: float) -> None:
+        """Peak of the H-step load forecast (HPA jobs): the cluster-autoscaler
+        prediction signal of BASELINE config 4."""
+        b = "foremastbrain:" + sanitize(base_metric)
+        self._gauge(b + "_forecast_max", "max of the load forecast over the prediction horizon").labels(
+            namespace, app).set(value)
+
     def set_hpa_score(self, namespace: str, app: str, score: float) -> None:
         self._gauge(self.HPA_SCORE, "foremast HPA score [0,100], 50 = hold").labels(namespace, app).set(score)
         self._gauge("foremastbrain:namespace_app_per_pod:hpa_score",

@@ -114,25 +114,7 @@ def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizo
         return _bivariate(hist, T, cur, M, tables, pairs)
     H = int(horizon.max().item()) if horizon.numel() else 1
     H = max(H, 1)
-    if algo in ("exponential_smoothing", "double_exponential_smoothing", "holt_winters"):
-        kind = {"exponential_smoothing": 0, "double_exponential_smoothing": 1, "holt_winters": 2}[algo]
-        m = 1
-        if kind == 2:
-            m = period or _detect_period(hist, T)
-            if 2 * m > T:
-                kind, m = 1, 1
-        fit = SM.es_fit(hist, T, kind, H, m)
-        fc, sigma = fit.forecast, fit.sigma
-    elif algo == "prophet":
-        fit = LQ.prophet_fit(hist, T, H)
-        fc, sigma = fit.forecast, fit.sigma
-    elif algo == "lstm":
-        if lstm_model is None:
-            from .lstm import LSTMForecaster
-            lstm_model = LSTMForecaster.default(device=hist.device)
-        fc, sigma = lstm_model.forecast(hist, T, H)
-    else:  # pragma: no cover
-        raise AssertionError(algo)
+    fc, sigma = forecast(algo, hist, T, H, period=period, lstm_model=lstm_model)
     idx = (horizon.clamp(1, H) - 1).to(fc.device)
     center = torch.gather(fc, 1, idx).contiguous()
     up, lo, flags, cnt, sc = SM.band_decide(cur, center, sigma.contiguous(), M, tables.thr, tables.bound,
@@ -141,6 +123,37 @@ def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizo
     has = (valid & 1).bool()
     cnt = torch.where(has, cnt, torch.zeros_like(cnt))
     return RowDecision(up, lo, flags, cnt, sc, valid, center)
+
+
+FORECASTERS = ("exponential_smoothing", "double_exponential_smoothing", "holt_winters", "prophet", "lstm")
+
+
+def forecast(algorithm: str, hist: torch.Tensor, T: int, H: int, period: int | None = None,
+             lstm_model=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """H-step forecast past the end of the history for every row with a
+    forecasting model -> (forecast [R, H], residual sigma [R]).  Used by the
+    band decision and, for HPA jobs, to publish the load forecast a cluster
+    autoscaler can act on ahead of time (README.md:58-59 "ClusterAutoScaler
+    prediction"; BASELINE config 4)."""
+    algo = canonical(algorithm)
+    if algo in ("exponential_smoothing", "double_exponential_smoothing", "holt_winters"):
+        kind = {"exponential_smoothing": 0, "double_exponential_smoothing": 1, "holt_winters": 2}[algo]
+        m = 1
+        if kind == 2:
+            m = period or _detect_period(hist, T)
+            if 2 * m > T:
+                kind, m = 1, 1
+        fit = SM.es_fit(hist, T, kind, H, m)
+        return fit.forecast, fit.sigma
+    if algo == "prophet":
+        fit = LQ.prophet_fit(hist, T, H)
+        return fit.forecast, fit.sigma
+    if algo == "lstm":
+        if lstm_model is None:
+            from .lstm import LSTMForecaster
+            lstm_model = LSTMForecaster.default(device=hist.device)
+        return lstm_model.forecast(hist, T, H)
+    raise ValueError(f"{algorithm!r} is not a forecasting model ({', '.join(FORECASTERS)})")
 
 
 def _detect_period(hist: torch.Tensor, T: int, default: int = 1440) -> int:

@@ -113,6 +113,19 @@ def test_hpa_job_writes_logs_and_score():
     assert 0 <= e.hpa_log.hpa_score <= 100 and e.hpa_log.reason.startswith("hpa is")
     assert [d.metric_alias for d in e.hpa_log.details] == ["cpu", "latency"]
     assert exp.sample("namespace_app_pod_hpa_score", "default", "demo") is not None
+    # load forecast for cluster-autoscaler prediction, one gauge per template metric
+    fc = exp.sample("foremastbrain:namespace_app_pod_cpu_usage_seconds_total_forecast_max", "default", "demo")
+    assert fc is not None and fc > 0
+
+
+@pytest.mark.parametrize("algo", ["lstm", "holt_winters", "prophet"])
+def test_hpa_forecast_algorithms(algo):
+    clock, store, client, brain, exp = _setup()
+    brain.cfg.hpa_forecast_algorithm = algo
+    client.start_analyzing("default", "demo", None, _metrics(), 10, "hpa", ["cpu", "latency"])
+    brain.run_once()
+    v = exp.sample("foremastbrain:namespace_app_pod_http_server_requests_latency_forecast_max", "default", "demo")
+    assert v is not None and np.isfinite(v)
 
 
 @pytest.mark.parametrize("algo", ["moving_average", "exponential_smoothing", "double_exponential_smoothing",
