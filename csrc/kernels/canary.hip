@@ -731,6 +731,95 @@ FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const fl
                         stream);
 }
 
+// Mean / population std / finite count of one history row, computed by a
+// 256-thread block with the row held in registers (NV float4 per thread).
+// Fast path for rows without missing samples (the common case): the plain
+// sum is computed with packed f32 adds (v_pk_add_f32, 2 elements per
+// instruction) and is finite iff every sample is; only a non-finite sum sends
+// the block to the masked per-element path.  Per element that is ~0.75 VALU
+// instructions instead of ~8, which leaves the CU's issue slots to the
+// pairwise kernel running concurrently on the side stream.
+template <int NV>
+__device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, int T, double* red, int* redi,
+                                                float& mf, float& sd, int& n) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef float nt4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int nq = (T + 3) >> 2;
+  const nt4* h = reinterpret_cast<const nt4*>(hrow);
+  nt4 q[NV];
+  f2 acc = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int qi = tid + j * 256;
+    nt4 v = __builtin_nontemporal_load(h + (qi < nq ? qi : nq - 1));   // streamed once, unpredicated
+    if (qi >= nq) {
+      v = (nt4){0.f, 0.f, 0.f, 0.f};
+    } else if (qi == nq - 1) {
+      const int e0 = qi * 4;
+      if (e0 + 1 >= T) v.y = 0.f;
+      if (e0 + 2 >= T) v.z = 0.f;
+      if (e0 + 3 >= T) v.w = 0.f;
+    }
+    q[j] = v;
+    acc += v.xy;
+    acc += v.zw;
+  }
+  const double tot = block_sum<256>((double)acc.x + (double)acc.y, red);
+  if (isfinite(tot)) {                       // block-uniform
+    n = T;
+    mf = (float)(tot / T);
+    const f2 mm = {mf, mf};
+    f2 a2 = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int qi = tid + j * 256;
+      if (qi < nq - 1) {
+        const f2 d0 = q[j].xy - mm, d1 = q[j].zw - mm;
+        a2 += d0 * d0;
+        a2 += d1 * d1;
+      } else if (qi == nq - 1) {
+        const int e0 = qi * 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (e0 + c < T) { const float d = q[j][c] - mf; a2.x += d * d; }
+      }
+    }
+    const double sst = block_sum<256>((double)a2.x + (double)a2.y, red);
+    sd = (float)sqrt(sst / n);
+    return;
+  }
+  // masked path: exclude non-finite samples (and the zero padding past T)
+  double s = 0.0;
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int e0 = (tid + j * 256) * 4;
+    float ls = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = q[j][c];
+      if (e0 + c < T && isfinite(x)) { ls += x; ++cnt; }
+    }
+    s += ls;
+  }
+  const double t2 = block_sum<256>(s, red);
+  n = block_sum<256>(cnt, redi);
+  mf = n > 0 ? (float)(t2 / n) : 0.f;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int e0 = (tid + j * 256) * 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = q[j][c];
+      if (e0 + c < T && isfinite(x)) { const float d = x - mf; ss += d * d; }
+    }
+  }
+  const double sst = block_sum<256>((double)ss, red);
+  sd = n > 0 ? (float)sqrt(sst / n) : 0.f;
+}
+
 // ---------------------------------------------------------------------------
 // K1 + K7 fused: moving_average_all bounds over the whole history row and the
 // anomaly decision on the current window, one 256-thread workgroup per row.
@@ -748,46 +837,9 @@ __global__ __launch_bounds__(256) void stats_decide_kernel(
   __shared__ int redi[4];
   const int tid = threadIdx.x;
   const int64_t row = blockIdx.x;
-  const float* h = hist + row * ld_h;
-  const int nq = (T + 3) >> 2;
-  float4 q[NV];
-  double s = 0.0;
-  int cnt = 0;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const int qi = tid + j * 256;
-    float4 x = make_float4(NAN, NAN, NAN, NAN);
-    if (qi < nq) {
-      x = reinterpret_cast<const float4*>(h)[qi];
-      const int e0 = qi * 4;
-      if (e0 + 1 >= T) x.y = NAN;
-      if (e0 + 2 >= T) x.z = NAN;
-      if (e0 + 3 >= T) x.w = NAN;
-    }
-    q[j] = x;
-    float ls = 0.f;
-    if (isfinite(x.x)) { ls += x.x; ++cnt; }
-    if (isfinite(x.y)) { ls += x.y; ++cnt; }
-    if (isfinite(x.z)) { ls += x.z; ++cnt; }
-    if (isfinite(x.w)) { ls += x.w; ++cnt; }
-    s += ls;
-  }
-  const double tot = block_sum<256>(s, red);
-  const int n = block_sum<256>(cnt, redi);
-  const double mean = n > 0 ? tot / n : 0.0;
-  const float mf = (float)mean;
-  float ss = 0.f;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const float4 x = q[j];
-    if (isfinite(x.x)) { float d = x.x - mf; ss += d * d; }
-    if (isfinite(x.y)) { float d = x.y - mf; ss += d * d; }
-    if (isfinite(x.z)) { float d = x.z - mf; ss += d * d; }
-    if (isfinite(x.w)) { float d = x.w - mf; ss += d * d; }
-  }
-  const double sst = block_sum<256>((double)ss, red);
-  const double var = n > 0 ? sst / n : 0.0;
-  const float sd = (float)sqrt(var);
+  float mf, sd;
+  int n;
+  block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
   const int m = (int)(row % M);
   float th = thr[m];
   if (diff != nullptr && diff[row]) th *= pair_factor;
@@ -875,94 +927,13 @@ FM_API int fm_stats_decide(const float* hist, int64_t ld_h, int T, const float* 
 template <int NV>
 __global__ __launch_bounds__(256) void hist_stats_kernel(const float* __restrict__ hist, int64_t ld_h, int T,
                                                          int64_t R, float* __restrict__ out /*[R,3]*/) {
-  // Fast path for rows without missing samples (the common case): the plain
-  // sum is computed with packed f32 adds (v_pk_add_f32, 2 elements per
-  // instruction) and is finite iff every sample is; only a non-finite sum
-  // sends the block to the masked per-element path.  Per element that is
-  // ~0.75 VALU instructions instead of ~8, which leaves the CU's issue slots
-  // to the pairwise kernel running concurrently on the side stream.
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef float nt4 __attribute__((ext_vector_type(4)));
   __shared__ double red[4];
   __shared__ int redi[4];
-  const int tid = threadIdx.x;
-  const int nq = (T + 3) >> 2;
   for (int64_t row = blockIdx.x; row < R; row += gridDim.x) {
-    const nt4* h = reinterpret_cast<const nt4*>(hist + row * ld_h);
-    nt4 q[NV];
-    f2 acc = {0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int qi = tid + j * 256;
-      nt4 v = __builtin_nontemporal_load(h + (qi < nq ? qi : nq - 1));   // streamed once, unpredicated
-      if (qi >= nq) {
-        v = (nt4){0.f, 0.f, 0.f, 0.f};
-      } else if (qi == nq - 1) {
-        const int e0 = qi * 4;
-        if (e0 + 1 >= T) v.y = 0.f;
-        if (e0 + 2 >= T) v.z = 0.f;
-        if (e0 + 3 >= T) v.w = 0.f;
-      }
-      q[j] = v;
-      acc += v.xy;
-      acc += v.zw;
-    }
-    const double tot = block_sum<256>((double)acc.x + (double)acc.y, red);
     float mf, sd;
     int n;
-    if (isfinite(tot)) {                       // block-uniform
-      n = T;
-      mf = (float)(tot / T);
-      const f2 mm = {mf, mf};
-      f2 a2 = {0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int qi = tid + j * 256;
-        if (qi < nq - 1) {
-          const f2 d0 = q[j].xy - mm, d1 = q[j].zw - mm;
-          a2 += d0 * d0;
-          a2 += d1 * d1;
-        } else if (qi == nq - 1) {
-          const int e0 = qi * 4;
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (e0 + c < T) { const float d = q[j][c] - mf; a2.x += d * d; }
-        }
-      }
-      const double sst = block_sum<256>((double)a2.x + (double)a2.y, red);
-      sd = (float)sqrt(sst / n);
-    } else {
-      // masked path: exclude non-finite samples (and the zero padding past T)
-      double s = 0.0;
-      int cnt = 0;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int e0 = (tid + j * 256) * 4;
-        float ls = 0.f;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float x = q[j][c];
-          if (e0 + c < T && isfinite(x)) { ls += x; ++cnt; }
-        }
-        s += ls;
-      }
-      const double t2 = block_sum<256>(s, red);
-      n = block_sum<256>(cnt, redi);
-      mf = n > 0 ? (float)(t2 / n) : 0.f;
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int e0 = (tid + j * 256) * 4;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float x = q[j][c];
-          if (e0 + c < T && isfinite(x)) { const float d = x - mf; ss += d * d; }
-        }
-      }
-      const double sst = block_sum<256>((double)ss, red);
-      sd = n > 0 ? (float)sqrt(sst / n) : 0.f;
-    }
-    if (tid == 0) {
+    block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
+    if (threadIdx.x == 0) {
       out[row * 3 + 0] = mf;
       out[row * 3 + 1] = sd;
       out[row * 3 + 2] = (float)n;

@@ -27,7 +27,8 @@ def rows_from_csv(p: Path):
 def main() -> None:
     agg = defaultdict(list)
     for arg in sys.argv[1:]:
-        for p in Path(arg).rglob("*"):
+        root = Path(arg)
+        for p in ([root] if root.is_file() else root.rglob("*")):
             if p.suffix == ".db":
                 it = rows_from_db(p)
             elif p.name.endswith("kernel_trace.csv"):
