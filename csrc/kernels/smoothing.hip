@@ -1,9 +1,12 @@
 // K2: exponential smoothing family (single / double (Holt) / Holt-Winters
-// additive) with a batched parameter-grid fit.
+// additive and multiplicative) with a batched parameter-grid fit, plus an
+// incremental update that advances a cached fitted model over new samples.
 //
 // Reference: the brain's model zoo lists Exponential Smoothing, Double
-// Exponential Smoothing and Holt-Winters (docs/guides/design.md:62-72); the
-// statistics follow the textbook additive recursions (docs/BRAIN_SPEC.md §3.2).
+// Exponential Smoothing and Holt-Winters (docs/guides/design.md:62-72) and
+// caches fitted models between cycles (MAX_CACHE_SIZE, foremast-brain/
+// README.md:30); the statistics follow the textbook recursions
+// (docs/BRAIN_SPEC.md §3.2).
 //
 // Mapping: one THREAD per (row, candidate) pair, candidates fastest, so the
 // lanes that share a row read the same history sample (one coalesced request).
@@ -13,52 +16,70 @@
 // BASELINE config-2 shape (40k series x 27 candidates x m=1440) that is 6 GB of
 // scratch, deliberately spent from the 288 GB of HBM instead of serialising the
 // grid.
+//
+// Rows are right-aligned with NaN padding on the left (ragged histories), so
+// every fit starts at the row's first finite sample and the seasonal
+// initialisation averages only finite samples.
 #include "fm_common.h"
 
 using namespace fm;
 
-struct Cand { float a, b, g; };
 constexpr int kPrefetch = 16;  // season/sample loads issued ahead per chunk (HW fit)
+constexpr float kDivEps = 1e-6f;
 
-// kind: 0 = SES, 1 = Holt (double), 2 = Holt-Winters additive
+// kind: 0 = SES, 1 = Holt (double), 2 = Holt-Winters additive, 3 = multiplicative
 template <int KIND>
-__global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x, int64_t ld, int T, int64_t R,
-                                                    const float* __restrict__ cand, int G, int m,
-                                                    float* __restrict__ season /*[m][R*G]*/, float* __restrict__ sse,
-                                                    float* __restrict__ state /*[R*G,3]*/, int* __restrict__ nobs) {
-  const int64_t pid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t P = R * G;
-  if (pid >= P) return;
-  const int64_t row = pid / G;
-  const int g = (int)(pid - row * G);
-  const float al = cand[3 * g + 0], be = cand[3 * g + 1], ga = cand[3 * g + 2];
-  const float* xr = x + row * ld;
-  float lvl, tr = 0.f;
-  int t0;
-  if (KIND == 2) {
-    // initial level = mean of season 1, trend = (mean season 2 - mean season 1)/m,
-    // seasonal indices = x_i - level over season 1
-    float s1 = 0.f, s2 = 0.f;
-    for (int i = 0; i < m; ++i) { s1 += xr[i]; s2 += xr[m + i]; }
-    s1 /= m; s2 /= m;
-    lvl = s1;
-    tr = (s2 - s1) / m;
-    for (int i = 0; i < m; ++i) season[(int64_t)i * P + pid] = xr[i] - s1;
-    t0 = m;
-  } else if (KIND == 1) {
-    lvl = xr[0];
-    tr = xr[1] - xr[0];
-    t0 = 1;
-  } else {
-    lvl = xr[0];
-    t0 = 1;
+struct EsModel {
+  float al, be, ga;
+  float lvl, tr;
+  // One step on sample xt with seasonal index s (in/out); an observed sample
+  // adds its squared one-step error to acc and counts in n.  (Accumulating
+  // inside the observed branch keeps the compiler from deferring 16 error
+  // terms to the end of a prefetch chunk, which cost ~15 % in VGPRs/VALU.)
+  __device__ __forceinline__ void step(float xt, float& s, float& acc, int& n) {
+    const float pred = KIND == 3 ? (lvl + tr) * s : lvl + tr + s;
+    if (isfinite(xt)) {
+      const float e = xt - pred;
+      acc += e * e;
+      ++n;
+      const float lprev = lvl;
+      if (KIND == 0) {
+        lvl = al * xt + (1.f - al) * lvl;
+      } else if (KIND == 1) {
+        lvl = al * xt + (1.f - al) * (lvl + tr);
+        tr = be * (lvl - lprev) + (1.f - be) * tr;
+      } else if (KIND == 2) {
+        lvl = al * (xt - s) + (1.f - al) * (lvl + tr);
+        tr = be * (lvl - lprev) + (1.f - be) * tr;
+        s = ga * (xt - lvl) + (1.f - ga) * s;
+      } else {
+        const float ds = fabsf(s) > kDivEps ? xt / s : xt;
+        lvl = al * ds + (1.f - al) * (lvl + tr);
+        tr = be * (lvl - lprev) + (1.f - be) * tr;
+        const float dl = fabsf(lvl) > kDivEps ? xt / lvl : 1.f;
+        s = ga * dl + (1.f - ga) * s;
+      }
+    } else {
+      lvl = lvl + tr;  // missing sample: propagate the forecast
+    }
   }
-  double err2 = 0.0;
+};
+
+// Run the recursion over samples [t, T) of row xr.  Seasonal state of this
+// (row, candidate) pair is column `col` of season[m][P]; ph = t % m on entry
+// and on exit.  `t` and `ph` must be wave-uniform so the season addressing
+// stays scalar (SGPR phase, one VGPR column offset); lanes whose own series
+// starts later (ragged rows) pass GATED = true and their first sample t_act,
+// and skip the steps before it.  err2/n carry the SSE (fp32 partials flushed
+// to fp64 every 64 steps) and the observation count.
+template <int KIND, bool GATED>
+__device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restrict__ xr, int t, int T, int t_act,
+                                       int m, float* __restrict__ season, int64_t P, int64_t col, int& ph,
+                                       double& err2, int& n) {
+  constexpr bool kSeason = KIND >= 2;
   float acc = 0.f;
-  int n = 0, chunk = 0;
-  int ph = 0;  // t % m, advanced incrementally (no per-step integer modulo)
-  int t = t0;
-  if (KIND == 2 && m > kPrefetch) {
+  int chunk = 0;
+  if (kSeason && m > kPrefetch) {
     // The season slot read at step t was written at step t - m, so the U
     // reads of a chunk never alias the chunk's own writes (U < m): issue all
     // U season + sample loads up front, then run the U dependent steps from
@@ -71,7 +92,7 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
       for (int u = 0; u < kPrefetch; ++u) {
         int pu = ph + u;
         if (pu >= m) pu -= m;
-        si[u] = (int64_t)pu * P + pid;
+        si[u] = (int64_t)pu * P + col;
         sv[u] = season[si[u]];
         xv[u] = xr[t + u];
       }
@@ -79,19 +100,8 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
       if (ph >= m) ph -= m;
 #pragma unroll
       for (int u = 0; u < kPrefetch; ++u) {
-        const float xt = xv[u], s_old = sv[u];
-        const float pred = lvl + tr + s_old;
-        if (isfinite(xt)) {
-          const float e = xt - pred;
-          acc += e * e;
-          ++n;
-          const float lprev = lvl;
-          lvl = al * (xt - s_old) + (1.f - al) * (lvl + tr);
-          tr = be * (lvl - lprev) + (1.f - be) * tr;
-          sv[u] = ga * (xt - lvl) + (1.f - ga) * s_old;
-        } else {
-          lvl = lvl + tr;
-        }
+        if (GATED && t + u < t_act) continue;
+        md.step(xv[u], sv[u], acc, n);
       }
 #pragma unroll
       for (int u = 0; u < kPrefetch; ++u) season[si[u]] = sv[u];
@@ -100,42 +110,134 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     }
   }
   for (; t < T; ++t) {
-    const float xt = xr[t];
-    float s_old = 0.f;
+    float s = 0.f;
     int64_t sidx = 0;
-    if (KIND == 2) { sidx = (int64_t)ph * P + pid; s_old = season[sidx]; if (++ph == m) ph = 0; }
-    const float pred = lvl + tr + s_old;
-    if (isfinite(xt)) {
-      const float e = xt - pred;
-      acc += e * e;
-      ++n;
-      if (++chunk == 64) { err2 += acc; acc = 0.f; chunk = 0; }
-      const float lprev = lvl;
-      if (KIND == 0) {
-        lvl = al * xt + (1.f - al) * lvl;
-      } else if (KIND == 1) {
-        lvl = al * xt + (1.f - al) * (lvl + tr);
-        tr = be * (lvl - lprev) + (1.f - be) * tr;
-      } else {
-        lvl = al * (xt - s_old) + (1.f - al) * (lvl + tr);
-        tr = be * (lvl - lprev) + (1.f - be) * tr;
-        season[sidx] = ga * (xt - lvl) + (1.f - ga) * s_old;
-      }
-    } else {
-      // missing sample: propagate the forecast
-      lvl = lvl + tr;
-    }
+    if (kSeason) { sidx = (int64_t)ph * P + col; s = season[sidx]; if (++ph == m) ph = 0; }
+    if (GATED && t < t_act) continue;
+    md.step(xr[t], s, acc, n);
+    if (kSeason) season[sidx] = s;
+    if (++chunk == 64) { err2 += acc; acc = 0.f; chunk = 0; }
   }
   err2 += acc;
+}
+
+// Wave-uniform entry into es_run: all lanes start at the wave's earliest
+// first step; the gated variant only runs when the lanes' starts differ.
+template <int KIND>
+__device__ __forceinline__ void es_run_wave(EsModel<KIND>& md, const float* __restrict__ xr, int t0, int T, int m,
+                                            float* __restrict__ season, int64_t P, int64_t col, double& err2,
+                                            int& n, int& ph_out) {
+  const int lo = __builtin_amdgcn_readfirstlane(wave_min(t0));
+  const int hi = __builtin_amdgcn_readfirstlane(wave_max(t0));
+  int ph = KIND >= 2 ? lo % m : 0;
+  if (lo == hi) es_run<KIND, false>(md, xr, lo, T, lo, m, season, P, col, ph, err2, n);
+  else es_run<KIND, true>(md, xr, lo, T, t0, m, season, P, col, ph, err2, n);
+  ph_out = ph;
+}
+
+__device__ __forceinline__ int first_finite(const float* __restrict__ xr, int T) {
+  int b = 0;
+  while (b < T && !isfinite(xr[b])) ++b;
+  return b;
+}
+
+// Finite-sample mean of xr[lo, hi); sets cnt.
+__device__ __forceinline__ float nan_mean(const float* __restrict__ xr, int lo, int hi, int& cnt) {
+  float s = 0.f;
+  cnt = 0;
+  for (int i = lo; i < hi; ++i)
+    if (isfinite(xr[i])) { s += xr[i]; ++cnt; }
+  return cnt > 0 ? s / cnt : 0.f;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x, int64_t ld, int T, int64_t R,
+                                                    const float* __restrict__ cand, int G, int m,
+                                                    float* __restrict__ season /*[m][R*G]*/, float* __restrict__ sse,
+                                                    float* __restrict__ state /*[R*G,3]*/, int* __restrict__ nobs) {
+  const int64_t P = R * G;
+  const int64_t pid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((pid_raw & ~(int64_t)63) >= P) return;      // whole wave past the end
+  // tail lanes of the last wave shadow the last pair (the wave-uniform start
+  // below needs every lane) and store nothing
+  const bool live = pid_raw < P;
+  const int64_t pid = live ? pid_raw : P - 1;
+  const int64_t row = pid / G;
+  const int g = (int)(pid - row * G);
+  EsModel<KIND> md{cand[3 * g + 0], cand[3 * g + 1], cand[3 * g + 2], 0.f, 0.f};
+  const float* xr = x + row * ld;
+  const int base = first_finite(xr, T);
+  int t0;
+  if (base >= T) {
+    md.lvl = __builtin_nanf("");
+    t0 = T;
+  } else if (KIND >= 2) {
+    // level = mean of the first season, trend = (mean of the second - mean of
+    // the first) / m, seasonal indices from the first season (finite samples)
+    int c1, c2;
+    const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
+    const float s1 = nan_mean(xr, base, e1, c1);
+    const float s2 = nan_mean(xr, e1, e2, c2);
+    md.lvl = s1;
+    md.tr = c2 > 0 ? (s2 - s1) / m : 0.f;
+    const bool mul_ok = fabsf(s1) > kDivEps;
+    const float inv1 = mul_ok ? 1.f / s1 : 0.f;
+    int ph = base % m;                    // absolute phase, advanced without a modulo per sample
+    for (int i = 0; i < m; ++i) {
+      const int t = base + i;
+      const float v = xr[t < T ? t : T - 1];
+      float si = KIND == 3 ? 1.f : 0.f;
+      if (t < T && isfinite(v)) si = KIND == 3 ? (mul_ok ? v * inv1 : 1.f) : v - s1;
+      if (live) season[(int64_t)ph * P + pid] = si;
+      if (++ph == m) ph = 0;
+    }
+    t0 = base + m;
+  } else {
+    md.lvl = xr[base];
+    if (KIND == 1 && base + 1 < T && isfinite(xr[base + 1])) md.tr = xr[base + 1] - xr[base];
+    t0 = base + 1;
+  }
+  double err2 = 0.0;
+  int n = 0, ph;
+  // shadow lanes recompute their twin's pair in lockstep (same values, same
+  // addresses) and then store nothing of their own
+  es_run_wave<KIND>(md, xr, t0, T, m, season, P, pid, err2, n, ph);
+  if (!live) return;
   sse[pid] = (float)err2;
-  state[pid * 3 + 0] = lvl;
-  state[pid * 3 + 1] = tr;
-  state[pid * 3 + 2] = (float)(T % (m > 0 ? m : 1));
+  state[pid * 3 + 0] = md.lvl;
+  state[pid * 3 + 1] = md.tr;
+  state[pid * 3 + 2] = (float)(KIND >= 2 ? T % m : 0);
   nobs[pid] = n;
 }
 
+// Incremental update of one cached model per row over its new samples
+// x[row, t_new[row] .. T): state [R,3] (level, trend, phase of the next
+// sample), season [m][R], params [R,3], sse/nobs accumulate.
+template <int KIND>
+__global__ __launch_bounds__(256) void es_update_kernel(const float* __restrict__ x, int64_t ld, int T, int64_t R,
+                                                       const int* __restrict__ t_new, const float* __restrict__ params,
+                                                       int m, float* __restrict__ season, float* __restrict__ sse,
+                                                       float* __restrict__ state, int* __restrict__ nobs) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= R) return;
+  EsModel<KIND> md{params[row * 3 + 0], params[row * 3 + 1], params[row * 3 + 2], state[row * 3 + 0],
+                   state[row * 3 + 1]};
+  // phases differ per cached series: per-lane (VGPR) phase, gated-free loop
+  int ph = KIND >= 2 ? (int)state[row * 3 + 2] : 0;
+  int t0 = t_new[row];
+  t0 = t0 < 0 ? 0 : (t0 > T ? T : t0);
+  double err2 = sse[row];
+  int n = nobs[row];
+  es_run<KIND, false>(md, x + row * ld, t0, T, t0, m, season, R, row, ph, err2, n);
+  sse[row] = (float)err2;
+  state[row * 3 + 0] = md.lvl;
+  state[row * 3 + 1] = md.tr;
+  state[row * 3 + 2] = (float)ph;
+  nobs[row] = n;
+}
+
 // Per row: pick the candidate with the smallest SSE and write the H-step
-// forecast + residual sigma.
+// forecast + residual sigma (G = 1 for an updated cached model).
 __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restrict__ sse, const float* __restrict__ state,
                                                           const int* __restrict__ nobs, const float* __restrict__ season,
                                                           int64_t R, int G, int m, int kind, int H,
@@ -158,31 +260,55 @@ __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restric
   best[row] = bg;
   for (int h = 1; h <= H; ++h) {
     float f = lvl + (kind >= 1 ? h * tr : 0.f);
-    if (kind == 2) f += season[(int64_t)((tph + h - 1) % m) * P + pid];
+    if (kind >= 2) {
+      const float s = season[(int64_t)((tph + h - 1) % m) * P + pid];
+      f = kind == 3 ? f * s : f + s;
+    }
     fc[row * H + (h - 1)] = f;
   }
 }
+
+#define FM_ES_DISPATCH(KERNEL, GRID, ...)                                                           \
+  do {                                                                                              \
+    if (kind == 0) hipLaunchKernelGGL(KERNEL<0>, GRID, dim3(256), 0, stream, __VA_ARGS__);          \
+    else if (kind == 1) hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, stream, __VA_ARGS__);     \
+    else if (kind == 2) hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, stream, __VA_ARGS__);     \
+    else hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, stream, __VA_ARGS__);                    \
+  } while (0)
 
 FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int kind,
                      float* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma, int* best,
                      hipStream_t stream) {
   if (R <= 0) return 0;
-  if (kind == 2 && (m < 2 || 2 * m > T)) return (int)hipErrorInvalidValue;
+  if (kind < 0 || kind > 3) return (int)hipErrorInvalidValue;
+  if (kind >= 2 && (m < 2 || 2 * m > T)) return (int)hipErrorInvalidValue;
   if (kind < 2 && T < 2) return (int)hipErrorInvalidValue;
+  if (kind < 2) m = 1;
   const int64_t P = R * G;
-  const dim3 grid((unsigned)((P + 255) / 256)), block(256);
-  if (kind == 0)
-    hipLaunchKernelGGL(es_fit_kernel<0>, grid, block, 0, stream, x, ld, T, R, cand, G, m, season, sse, state, nobs);
-  else if (kind == 1)
-    hipLaunchKernelGGL(es_fit_kernel<1>, grid, block, 0, stream, x, ld, T, R, cand, G, m, season, sse, state, nobs);
-  else
-    hipLaunchKernelGGL(es_fit_kernel<2>, grid, block, 0, stream, x, ld, T, R, cand, G, m, season, sse, state, nobs);
+  FM_ES_DISPATCH(es_fit_kernel, dim3((unsigned)((P + 255) / 256)), x, ld, T, R, cand, G, m, season, sse, state, nobs);
   FM_LAUNCH_CHECK();
   hipLaunchKernelGGL(es_forecast_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, sse, state, nobs,
                      season, R, G, m, kind, H, fc, sigma, best);
   FM_LAUNCH_CHECK();
   return 0;
 }
+
+FM_API int fm_es_update(const float* x, int64_t ld, int T, int64_t R, const int* t_new, const float* params, int m,
+                        int kind, float* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma,
+                        int* best, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if (kind < 0 || kind > 3) return (int)hipErrorInvalidValue;
+  if (kind >= 2 && m < 2) return (int)hipErrorInvalidValue;
+  if (kind < 2) m = 1;
+  const dim3 grid((unsigned)((R + 255) / 256));
+  FM_ES_DISPATCH(es_update_kernel, grid, x, ld, T, R, t_new, params, m, season, sse, state, nobs);
+  FM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(es_forecast_kernel, grid, dim3(256), 0, stream, sse, state, nobs, season, R, 1, m, kind, H, fc,
+                     sigma, best);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+#undef FM_ES_DISPATCH
 
 // ---------------------------------------------------------------------------
 // Model-agnostic band decision: compare current points against per-point

@@ -64,7 +64,8 @@ class BrainConfig:
     min_kruskal: int = 5                     # MIN_KRUSKAL_DATA_POINTS
     pairwise_threshold_factor: float = 0.8   # [inferred] "lower threshold" factor (design.md:35)
     max_stuck_seconds: float = 90.0          # MAX_STUCK_IN_SECONDS
-    max_cache_size: int = 10000              # MAX_CACHE_SIZE
+    max_cache_size: int = 100000             # MAX_CACHE_SIZE (fitted models kept between cycles, models/cache.py)
+    model_refit_seconds: float = 6 * 3600.0  # MODEL_REFIT_SECONDS: re-run the grid fit of a cached model after this
     es_endpoint: str = "http://elasticsearch-discovery.foremast.svc.cluster.local:9200"  # ES_ENDPOINT
     metrics_port: int = 8000
     poll_interval: float = 5.0
@@ -113,6 +114,7 @@ class BrainConfig:
         c.pairwise_threshold_factor = _f(env, "ML_PAIRWISE_THRESHOLD_FACTOR", c.pairwise_threshold_factor)
         c.max_stuck_seconds = _f(env, "MAX_STUCK_IN_SECONDS", c.max_stuck_seconds)
         c.max_cache_size = _i(env, "MAX_CACHE_SIZE", c.max_cache_size)
+        c.model_refit_seconds = _f(env, "MODEL_REFIT_SECONDS", c.model_refit_seconds)
         c.es_endpoint = env.get("ES_ENDPOINT", c.es_endpoint) or c.es_endpoint
         c.metrics_port = _i(env, "METRICS_PORT", c.metrics_port)
         c.poll_interval = _f(env, "POLL_INTERVAL", c.poll_interval)

@@ -64,6 +64,7 @@ class Row:
     cur_t: np.ndarray
     base: np.ndarray
     tags: str = ""
+    series: str = ""        # "<namespace>/<app>": identity of the history across jobs (model cache key)
 
 
 @dataclass
@@ -124,6 +125,8 @@ class Brain:
         self.fetch_threads = fetch_threads
         self.lstm_model = lstm_model
         self.hpa_state: dict[str, MI.HpaState] = {}
+        from ..models.cache import ModelCache
+        self.model_cache = ModelCache(self.cfg.max_cache_size, self.cfg.model_refit_seconds)
         self.info = D.env_info() if D.is_dist() else D.DistInfo()
         from ..utils.spans import Spans
         self.spans = Spans(exporter.registry if exporter is not None else None)
@@ -226,12 +229,19 @@ class Brain:
         if zoo.canonical(self.cfg.ml_algorithm) == "bivariate_normal":
             pairs = self._pairs(rows)
         dec = zoo.decide(self.cfg.ml_algorithm, hist, T, cur, hor, R, tables, diff, lstm_model=self.lstm_model,
-                         pairs=pairs)
+                         pairs=pairs, cache=self._cache_ctx(rows, self.cfg.ml_algorithm))
         out = {k: getattr(dec, k).detach().cpu().numpy() for k in ("upper", "lower", "count", "score", "valid")}
         out["_hist"], out["_T"] = hist, T
         out["flags"] = C.unpack_flags(dec.flags, cur.shape[1])
         out["diff"] = None if diff is None else diff.cpu().numpy()
         return out
+
+    def _cache_ctx(self, rows: list[Row], algorithm: str) -> "zoo.CacheContext | None":
+        if self.model_cache.capacity <= 0 or zoo.canonical(algorithm) not in zoo.ES_KINDS:
+            return None
+        algo = zoo.canonical(algorithm)
+        return zoo.CacheContext(self.model_cache, [(r.series, r.alias, r.base_metric, algo) for r in rows],
+                                np.array([r.hist_t_last for r in rows], np.float64), self.step, self.clock())
 
     @staticmethod
     def _pairs(rows: list[Row]):
@@ -263,6 +273,7 @@ class Brain:
         for j, wk in enumerate(works):
             for r in wk.rows:
                 r.job = j
+                r.series = f"{wk.namespace or wk.doc.namespace}/{wk.doc.app_name}"
                 rows.append(r)
         with self.spans.span("score"):
             res = self.score_rows(rows) if rows else None
@@ -367,7 +378,8 @@ class Brain:
         h = hist.index_select(0, sel).contiguous()
         try:
             fc, _ = zoo.forecast(self.cfg.hpa_forecast_algorithm, h, T, max(1, self.cfg.hpa_forecast_steps),
-                                 lstm_model=self.lstm_model)
+                                 lstm_model=self.lstm_model,
+                                 cache=self._cache_ctx([rows[i] for i in idx], self.cfg.hpa_forecast_algorithm))
         except (ValueError, RuntimeError) as e:
             log.warning("HPA forecast skipped: %s", e)
             return
@@ -420,7 +432,9 @@ class Brain:
             t["hpa.flip_t0"] = torch.cat([self.hpa_state[i].flip_t0 for i in ids])
         if self.lstm_model is not None:
             t.update({"lstm." + k: v for k, v in self.lstm_model.state_dict().items()})
-        return t, {"hpa_jobs": ids, "worker": self.worker, "algorithm": self.cfg.ml_algorithm}
+        ct, cmeta = self.model_cache.state_tensors()
+        t.update(ct)
+        return t, {"hpa_jobs": ids, "worker": self.worker, "algorithm": self.cfg.ml_algorithm, "model_cache": cmeta}
 
     def save_checkpoint(self, dirpath: str):
         from . import checkpoint
@@ -439,6 +453,7 @@ class Brain:
         lstm = {k[5:]: v for k, v in t.items() if k.startswith("lstm.")}
         if lstm and self.lstm_model is not None:
             self.lstm_model.load_state_dict(lstm)
+        self.model_cache.load_state(t, meta.get("model_cache", []), self.device)
         return True
 
 

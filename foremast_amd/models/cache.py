@@ -1,0 +1,256 @@
+"""Fitted-model cache of the brain (``MAX_CACHE_SIZE``, foremast-brain/
+README.md:30 "Max cached model size").
+
+Continuous-monitoring and HPA jobs are re-scored every cycle over a history
+window that has only slid by a few samples.  Re-running the exponential-
+smoothing grid fit over the whole 7-day window each time costs O(T x G) per
+series; instead the cache keeps, per (series, metric, algorithm), the best
+candidate's fitted state (parameters, level, trend, seasonal indices, SSE) and
+the timestamp of the last sample folded in.  On the next cycle the k new
+samples are pushed through the same recursion (``fm_es_update``: one thread
+per series, O(k)), and the grid is re-run only for rows that miss, whose
+history jumped backwards or by a whole window, or whose fit is older than
+``refit_seconds``.
+
+Storage is a device-resident slab per (kind, period): ``params [C, 3]``,
+``state [C, 3]``, ``season [C, m]``, ``sse [C]``, ``nobs [C]`` plus host
+timestamps and use stamps, so a cycle costs one gather and one scatter per
+tensor whatever the number of series; the per-row host work is one dict
+lookup.  Eviction is least-recently-used by stamp (vectorised), bounded by
+``capacity`` entries: at m = 1440 an entry is ~5.8 KB of HBM, so the default
+of 100k entries (a full 10k-service x 8-metric shard plus headroom) is
+~0.6 GB of the 288 GB.  The cache is saved in the brain checkpoint
+(``state_tensors`` / ``load_state``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import smoothing as SM
+
+_SLOT_BITS = 40
+
+
+class _Slab:
+    def __init__(self, sid: int, kind: int, m: int, device):
+        self.sid, self.kind, self.m, self.device = sid, kind, m, torch.device(device)
+        self.cap = 0
+        self.hw = 0                      # high-water mark of allocated slots
+        self.free: list[int] = []
+        f = lambda *s, dt=torch.float32: torch.empty(s, dtype=dt, device=self.device)
+        self.params, self.state, self.sse = f(0, 3), f(0, 3), f(0)
+        self.nobs = f(0, dt=torch.int32)
+        self.season = f(0, m) if kind >= 2 else None
+        self.t_last = np.zeros(0)
+        self.fitted_at = np.zeros(0)
+        self.stamp = np.zeros(0, np.int64)
+        self.keys: list = []             # slot -> key (None when free)
+
+    def _grow(self, need: int) -> None:
+        cap = max(need, 2 * self.cap, 64)
+
+        def g(t):
+            n = torch.empty((cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            n[:self.cap] = t
+            return n
+        self.params, self.state, self.sse, self.nobs = g(self.params), g(self.state), g(self.sse), g(self.nobs)
+        if self.season is not None:
+            self.season = g(self.season)
+        pad = cap - self.cap
+        self.t_last = np.concatenate([self.t_last, np.zeros(pad)])
+        self.fitted_at = np.concatenate([self.fitted_at, np.zeros(pad)])
+        self.stamp = np.concatenate([self.stamp, np.zeros(pad, np.int64)])
+        self.keys += [None] * pad
+        self.cap = cap
+
+    def alloc(self, n: int) -> list[int]:
+        out = [self.free.pop() for _ in range(min(n, len(self.free)))]
+        rest = n - len(out)
+        if rest:
+            if self.hw + rest > self.cap:
+                self._grow(self.hw + rest)
+            out += range(self.hw, self.hw + rest)
+            self.hw += rest
+        return out
+
+    def write(self, slots, md: "SM.ESState", t_last, fitted_at) -> None:
+        s = torch.as_tensor(np.asarray(slots, np.int64), device=self.device)
+        self.params[s] = md.params.to(self.device)
+        self.state[s] = md.state.to(self.device)
+        self.sse[s] = md.sse.to(self.device, torch.float32)
+        self.nobs[s] = md.nobs.to(self.device, torch.int32)
+        if self.season is not None:
+            self.season[s] = md.season.to(self.device).t()
+        self.t_last[slots] = t_last
+        self.fitted_at[slots] = fitted_at
+
+    def read(self, slots) -> "SM.ESState":
+        s = torch.as_tensor(np.asarray(slots, np.int64), device=self.device)
+        return SM.ESState(self.kind, self.m, self.params[s], self.state[s],
+                          None if self.season is None else self.season[s].t().contiguous(), self.sse[s],
+                          self.nobs[s])
+
+    def live_slots(self) -> np.ndarray:
+        return np.array([i for i in range(self.hw) if self.keys[i] is not None], np.int64)
+
+
+class ModelCache:
+    def __init__(self, capacity: int = 100000, refit_seconds: float = 6 * 3600.0):
+        self.capacity = max(0, int(capacity))
+        self.refit_seconds = float(refit_seconds)
+        self.entries: dict = {}                    # key -> slab id << _SLOT_BITS | slot
+        self.slabs: list[_Slab] = []
+        self._by_kind_m: dict[tuple[int, int], _Slab] = {}
+        self.clock = 0                              # use stamp (one tick per forecast call)
+        self.hits = 0
+        self.misses = 0
+
+    def __len__(self) -> int:
+        return len(self.entries)
+
+    def locate(self, key) -> tuple[_Slab, int] | None:
+        g = self.entries.get(key)
+        return None if g is None else (self.slabs[g >> _SLOT_BITS], g & ((1 << _SLOT_BITS) - 1))
+
+    def _drop_slot(self, slab: _Slab, slot: int) -> None:
+        del self.entries[slab.keys[slot]]
+        slab.keys[slot] = None
+        slab.free.append(slot)
+
+    def _evict(self, n: int) -> None:
+        """Drop the n least recently used entries."""
+        cand = [(slab, slab.live_slots()) for slab in self.slabs]
+        stamps = np.concatenate([slab.stamp[s] for slab, s in cand] + [np.zeros(0, np.int64)])
+        owner = np.concatenate([np.full(len(s), i) for i, (_, s) in enumerate(cand)] + [np.zeros(0, np.int64)])
+        slots = np.concatenate([s for _, s in cand] + [np.zeros(0, np.int64)])
+        n = min(n, len(stamps))
+        if n <= 0:
+            return
+        for j in np.argpartition(stamps, n - 1)[:n]:
+            self._drop_slot(cand[owner[j]][0], int(slots[j]))
+
+    def _store(self, keys: list, kind: int, m: int, md: "SM.ESState", t_last, fitted_at, device) -> None:
+        if self.capacity <= 0 or not keys:
+            return
+        last = {k: j for j, k in enumerate(keys)}       # one slot per key (last occurrence wins)
+        ok = torch.isfinite(md.state[:, :2]).all(1).cpu().numpy()   # never cache a model without data
+        for k in last:
+            loc = self.locate(k)
+            if loc is not None:
+                self._drop_slot(*loc)
+        keep = [j for j in sorted(last.values()) if ok[j]][-self.capacity:]
+        if not keep:
+            return
+        over = len(self.entries) + len(keep) - self.capacity
+        if over > 0:
+            self._evict(over)
+        slab = self._by_kind_m.get((kind, m))
+        if slab is None:
+            slab = _Slab(len(self.slabs), kind, m, device)
+            self.slabs.append(slab)
+            self._by_kind_m[(kind, m)] = slab
+        slots = slab.alloc(len(keep))
+        sel = torch.as_tensor(np.asarray(keep, np.int64), device=md.params.device)
+        sub = SM.ESState(kind, m, md.params[sel], md.state[sel], None if md.season is None else md.season[:, sel],
+                         md.sse[sel], md.nobs[sel])
+        slab.write(slots, sub, np.asarray(t_last, np.float64)[keep], np.asarray(fitted_at, np.float64)[keep])
+        slab.stamp[slots] = self.clock
+        base = slab.sid << _SLOT_BITS
+        for j, slot in zip(keep, slots):
+            slab.keys[slot] = keys[j]
+            self.entries[keys[j]] = base | slot
+
+    # ------------------------------------------------------------------ forecast
+    def es_forecast(self, keys: list, t_last: np.ndarray, step: float, now: float, hist: torch.Tensor, T: int,
+                    kind: int, H: int, period_for) -> tuple[torch.Tensor, torch.Tensor]:
+        """Forecast [R, H] + sigma [R] for every row of ``hist`` through the
+        cache.  ``period_for(rows)`` returns the seasonal period used to
+        grid-fit the rows that miss (kind >= 2)."""
+        self.clock += 1
+        R = hist.shape[0]
+        dev = hist.device
+        t_last = np.asarray(t_last, np.float64)
+        fc = torch.empty((R, H), dtype=torch.float32, device=dev)
+        sig = torch.empty((R,), dtype=torch.float32, device=dev)
+        g = np.fromiter((-1 if v is None else v for v in map(self.entries.get, keys)), np.int64, R)
+        if len(set(keys)) != R:                    # a key seen twice in one batch is fitted, not advanced twice
+            seen: set = set()
+            for i, key in enumerate(keys):
+                if key in seen:
+                    g[i] = -1
+                seen.add(key)
+        sid = np.where(g >= 0, g >> _SLOT_BITS, -1)
+        slot = g & ((1 << _SLOT_BITS) - 1)
+        usable = np.zeros(R, bool)
+        knew = np.zeros(R, np.int64)
+        for slab in self.slabs:
+            if slab.kind != kind:
+                continue
+            rows = np.nonzero(sid == slab.sid)[0]
+            if not len(rows):
+                continue
+            sl = slot[rows]
+            k = np.rint((t_last[rows] - slab.t_last[sl]) / step).astype(np.int64)
+            ok = (now - slab.fitted_at[sl] <= self.refit_seconds) & (k >= 0) & (k < T)
+            usable[rows[ok]] = True
+            knew[rows] = k
+        hit = np.nonzero(usable)[0]
+        miss = np.nonzero(~usable)[0]
+        self.hits += len(hit)
+        self.misses += len(miss)
+        for slab in self.slabs:
+            rows = hit[sid[hit] == slab.sid]
+            if not len(rows):
+                continue
+            sl = slot[rows]
+            idx = torch.as_tensor(rows, device=dev)
+            t_new = torch.as_tensor((T - knew[rows]).astype(np.int32))
+            f, s, new = SM.es_update(hist.index_select(0, idx).contiguous(), T, t_new, slab.read(sl), H)
+            fc[idx], sig[idx] = f, s
+            slab.write(sl, new, t_last[rows], slab.fitted_at[sl])
+            slab.stamp[sl] = self.clock
+            dead = ~torch.isfinite(new.state[:, :2]).all(1).cpu().numpy()
+            for j in np.nonzero(dead)[0]:
+                self._drop_slot(slab, int(sl[j]))
+        if len(miss):
+            idx = torch.as_tensor(miss, device=dev)
+            sub = hist.index_select(0, idx).contiguous()
+            k_eff, m = kind, 1
+            if kind >= 2:
+                m = int(period_for(sub))
+                if 2 * m > T:
+                    k_eff, m = 1, 1
+            fit = SM.es_fit(sub, T, k_eff, H, m, keep_state=True)
+            fc[idx], sig[idx] = fit.forecast, fit.sigma
+            if k_eff == kind:
+                self._store([keys[i] for i in miss], kind, m, fit.model, t_last[miss], np.full(len(miss), now), dev)
+        return fc, sig
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_tensors(self, prefix: str = "cache.") -> tuple[dict[str, torch.Tensor], list]:
+        """Flatten for the safetensors checkpoint: one tensor group per slab."""
+        t: dict[str, torch.Tensor] = {}
+        meta = []
+        for gi, slab in enumerate(s for s in self.slabs if len(s.live_slots())):
+            sl = slab.live_slots()
+            md = slab.read(sl)
+            p = f"{prefix}{gi}."
+            t[p + "params"], t[p + "state"] = md.params.cpu(), md.state.cpu()
+            t[p + "sse"], t[p + "nobs"] = md.sse.cpu(), md.nobs.cpu()
+            if md.season is not None:
+                t[p + "season"] = md.season.cpu().contiguous()
+            meta.append({"kind": slab.kind, "m": slab.m, "keys": [list(slab.keys[i]) for i in sl],
+                         "t_last": slab.t_last[sl].tolist(), "fitted_at": slab.fitted_at[sl].tolist()})
+        return t, meta
+
+    def load_state(self, t: dict[str, torch.Tensor], meta: list, device, prefix: str = "cache.") -> None:
+        self.entries.clear()
+        self.slabs.clear()
+        self._by_kind_m.clear()
+        for gi, g in enumerate(meta):
+            p = f"{prefix}{gi}."
+            kind, m = int(g["kind"]), int(g["m"])
+            md = SM.ESState(kind, m, t[p + "params"], t[p + "state"], t.get(p + "season") if kind >= 2 else None,
+                            t[p + "sse"], t[p + "nobs"])
+            self._store([tuple(k) for k in g["keys"]], kind, m, md, g["t_last"], g["fitted_at"], device)

@@ -13,10 +13,15 @@ moving_average                  mean/std over the last ``window`` pts   K1+K7 fu
 exponential_smoothing           SES, alpha grid                         K2 + band decide
 double_exponential_smoothing    Holt, (alpha, beta) grid                K2 + band decide
 holt_winters                    additive HW, period from the FFT        K3 + K2 + band
+holt_winters_multiplicative     multiplicative HW (seasonal ratio)      K3 + K2 + band
 prophet                         trend+hinges+daily/weekly Fourier LSQ   K10 (f32 MFMA)
 lstm                            LSTM forecaster (bf16 MFMA)             K6 + band decide
 bivariate_normal                Mahalanobis over metric pairs           K5
 ==============================  ======================================  ==================
+
+The exponential-smoothing family goes through the brain's fitted-model cache
+when one is given (``models/cache.py``, ``MAX_CACHE_SIZE``): cached series are
+advanced over their new samples instead of re-fitting the grid.
 
 Thresholds are in sigma units per metric (``BrainConfig.rule_for``), lowered
 by ``pairwise_threshold_factor`` on rows whose canary distribution differs.
@@ -25,6 +30,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from ..ops import canary as C
@@ -33,13 +39,14 @@ from ..ops import lsq as LQ
 from ..ops import smoothing as SM
 
 ALGORITHMS = ("moving_average_all", "moving_average", "exponential_smoothing", "double_exponential_smoothing",
-              "holt_winters", "prophet", "lstm", "bivariate_normal")
+              "holt_winters", "holt_winters_multiplicative", "prophet", "lstm", "bivariate_normal")
 
 ALIASES = {"moving_average_all": "moving_average_all", "ma_all": "moving_average_all",
            "moving_average": "moving_average", "ma": "moving_average",
            "exponential_smoothing": "exponential_smoothing", "ses": "exponential_smoothing",
            "double_exponential_smoothing": "double_exponential_smoothing", "holt": "double_exponential_smoothing",
            "holt_winters": "holt_winters", "hw": "holt_winters", "triple_exponential_smoothing": "holt_winters",
+           "holt_winters_multiplicative": "holt_winters_multiplicative", "hw_mul": "holt_winters_multiplicative",
            "prophet": "prophet", "lstm": "lstm", "bivariate_normal": "bivariate_normal", "bivariate": "bivariate_normal"}
 
 
@@ -59,6 +66,16 @@ class RowDecision:
     score: torch.Tensor      # [R] f32
     valid: torch.Tensor      # [R] int32 bit0 history ok, bit1 current present
     center: torch.Tensor | None = None
+
+
+@dataclass
+class CacheContext:
+    """Which cached model each row maps to (see ``models/cache.py``)."""
+    cache: "ModelCache"
+    keys: list              # one hashable key per row, e.g. (job id, alias, algorithm)
+    t_last: np.ndarray      # [R] timestamp of each row's last history sample
+    step: float             # sample spacing, seconds
+    now: float              # wall clock (refit age)
 
 
 @dataclass
@@ -92,7 +109,7 @@ def _valid(hist: torch.Tensor, T: int, cur: torch.Tensor, min_hist: int) -> torc
 
 def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizon: torch.Tensor, M: int,
            tables: Tables, diff: torch.Tensor | None = None, window: int = 60, period: int | None = None,
-           lstm_model=None, pairs=None) -> RowDecision:
+           lstm_model=None, pairs=None, cache: CacheContext | None = None) -> RowDecision:
     """Score current points of every row.
 
     ``horizon`` [R, n] int64: steps past the end of the history of each current
@@ -114,7 +131,7 @@ def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizo
         return _bivariate(hist, T, cur, M, tables, pairs)
     H = int(horizon.max().item()) if horizon.numel() else 1
     H = max(H, 1)
-    fc, sigma = forecast(algo, hist, T, H, period=period, lstm_model=lstm_model)
+    fc, sigma = forecast(algo, hist, T, H, period=period, lstm_model=lstm_model, cache=cache)
     idx = (horizon.clamp(1, H) - 1).to(fc.device)
     center = torch.gather(fc, 1, idx).contiguous()
     up, lo, flags, cnt, sc = SM.band_decide(cur, center, sigma.contiguous(), M, tables.thr, tables.bound,
@@ -125,21 +142,26 @@ def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizo
     return RowDecision(up, lo, flags, cnt, sc, valid, center)
 
 
-FORECASTERS = ("exponential_smoothing", "double_exponential_smoothing", "holt_winters", "prophet", "lstm")
+ES_KINDS = {"exponential_smoothing": 0, "double_exponential_smoothing": 1, "holt_winters": 2,
+            "holt_winters_multiplicative": 3}
+FORECASTERS = tuple(ES_KINDS) + ("prophet", "lstm")
 
 
 def forecast(algorithm: str, hist: torch.Tensor, T: int, H: int, period: int | None = None,
-             lstm_model=None) -> tuple[torch.Tensor, torch.Tensor]:
+             lstm_model=None, cache: CacheContext | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """H-step forecast past the end of the history for every row with a
     forecasting model -> (forecast [R, H], residual sigma [R]).  Used by the
     band decision and, for HPA jobs, to publish the load forecast a cluster
     autoscaler can act on ahead of time (README.md:58-59 "ClusterAutoScaler
     prediction"; BASELINE config 4)."""
     algo = canonical(algorithm)
-    if algo in ("exponential_smoothing", "double_exponential_smoothing", "holt_winters"):
-        kind = {"exponential_smoothing": 0, "double_exponential_smoothing": 1, "holt_winters": 2}[algo]
+    if algo in ES_KINDS:
+        kind = ES_KINDS[algo]
+        if cache is not None:
+            return cache.cache.es_forecast(cache.keys, cache.t_last, cache.step, cache.now, hist, T, kind, H,
+                                           lambda sub: period or _detect_period(sub, T))
         m = 1
-        if kind == 2:
+        if kind >= 2:
             m = period or _detect_period(hist, T)
             if 2 * m > T:
                 kind, m = 1, 1

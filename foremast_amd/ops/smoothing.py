@@ -11,11 +11,12 @@ import torch
 from ._lib import LIB, check, ptr, require_native, stream_of
 
 KINDS = {"exponential_smoothing": 0, "ses": 0, "double_exponential_smoothing": 1, "holt": 1,
-         "holt_winters": 2, "hw": 2}
+         "holt_winters": 2, "hw": 2, "holt_winters_multiplicative": 3, "hw_mul": 3}
+DIV_EPS = np.float32(1e-6)
 
 
 def default_grid(kind: int) -> np.ndarray:
-    """(alpha, beta, gamma) candidates.  SES: 9 alphas; Holt: 5x4; HW: 3x3x3."""
+    """(alpha, beta, gamma) candidates.  SES: 9 alphas; Holt: 5x4; HW (both forms): 3x3x3."""
     if kind == 0:
         g = [(a, 0.0, 0.0) for a in (0.05, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.8, 0.95)]
     elif kind == 1:
@@ -26,31 +27,61 @@ def default_grid(kind: int) -> np.ndarray:
 
 
 @dataclass
+class ESState:
+    """One fitted model per row: what the brain's model cache keeps between
+    cycles and ``es_update`` advances over new samples."""
+    kind: int
+    m: int
+    params: torch.Tensor            # [R, 3] alpha, beta, gamma
+    state: torch.Tensor             # [R, 3] level, trend, phase of the next sample
+    season: torch.Tensor | None     # [m, R] seasonal indices (kind >= 2)
+    sse: torch.Tensor               # [R] one-step SSE so far
+    nobs: torch.Tensor              # [R] int32 observations so far
+
+    def rows(self, idx: torch.Tensor) -> "ESState":
+        idx = idx.to(self.params.device)
+        return ESState(self.kind, self.m, self.params[idx], self.state[idx],
+                       None if self.season is None else self.season[:, idx].contiguous(), self.sse[idx],
+                       self.nobs[idx])
+
+
+@dataclass
 class ESFit:
     forecast: torch.Tensor   # [R, H]
     sigma: torch.Tensor      # [R]
     best: torch.Tensor       # [R] candidate index
     sse: torch.Tensor        # [R, G]
+    model: ESState | None = None
 
 
-def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, grid: np.ndarray | None = None) -> ESFit:
-    """Fit SES / Holt / additive Holt-Winters by grid search on one-step SSE
-    and forecast H steps past the end of the history."""
+def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, grid: np.ndarray | None = None,
+           keep_state: bool = False) -> ESFit:
+    """Fit SES / Holt / Holt-Winters (additive, multiplicative) by grid search
+    on one-step SSE and forecast H steps past the end of the history.  With
+    ``keep_state`` the best candidate's fitted state is returned as an
+    :class:`ESState` (for the model cache)."""
     check(x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1, "x must be [R, T] float32")
+    check(0 <= kind <= 3, f"kind must be 0..3, got {kind}")
     R = x.shape[0]
     T = x.shape[1] if T is None else int(T)
     grid = default_grid(kind) if grid is None else np.asarray(grid, np.float32)
     G = grid.shape[0]
-    if kind != 2:
+    if kind < 2:
         m = 1
     if not x.is_cuda:
-        fc, sig, best, sse = ref_es_fit(x.numpy()[:, :T], kind, H, m, grid)
-        return ESFit(torch.from_numpy(fc), torch.from_numpy(sig), torch.from_numpy(best), torch.from_numpy(sse))
+        fc, sig, best, sse, st = ref_es_fit(x.numpy()[:, :T], kind, H, m, grid, return_state=True)
+        model = None
+        if keep_state:
+            model = ESState(kind, m, *(torch.from_numpy(np.ascontiguousarray(v)) for v in (
+                grid[best], st["state"], st["season"].T if kind >= 2 else np.zeros((0,)), st["sse"], st["nobs"])))
+            if kind < 2:
+                model.season = None
+        return ESFit(torch.from_numpy(fc), torch.from_numpy(sig), torch.from_numpy(best), torch.from_numpy(sse), model)
     require_native(x)
     d = x.device
     cand = torch.from_numpy(grid).to(d)
     P = R * G
-    season = torch.empty((max(m, 1) if kind == 2 else 1, P), dtype=torch.float32, device=d)
+    season = torch.empty((m if kind >= 2 else 1, P), dtype=torch.float32, device=d)
     sse = torch.empty((R, G), dtype=torch.float32, device=d)
     state = torch.empty((P, 3), dtype=torch.float32, device=d)
     nobs = torch.empty((P,), dtype=torch.int32, device=d)
@@ -59,11 +90,110 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     best = torch.empty((R,), dtype=torch.int32, device=d)
     LIB.call("fm_es_fit", ptr(x), x.stride(0), T, R, ptr(cand), G, m, kind, ptr(season), ptr(sse), ptr(state),
              ptr(nobs), H, ptr(fc), ptr(sig), ptr(best), stream_of(x))
-    return ESFit(fc, sig, best, sse)
+    model = None
+    if keep_state:
+        b = best.long()
+        pid = torch.arange(R, device=d) * G + b
+        model = ESState(kind, m, cand[b].contiguous(), state[pid].contiguous(),
+                        season[:, pid].contiguous() if kind >= 2 else None,
+                        sse.gather(1, b[:, None])[:, 0].contiguous(), nobs[pid].contiguous())
+    return ESFit(fc, sig, best, sse, model)
 
 
-def ref_es_fit(x: np.ndarray, kind: int, H: int, m: int, grid: np.ndarray):
-    """fp32 recursion mirrored in numpy (vectorised over rows x candidates)."""
+def es_update(x: torch.Tensor, T: int, t_new: torch.Tensor, model: ESState, H: int) -> tuple:
+    """Advance cached fitted models over their new samples ``x[r, t_new[r]:T]``
+    (same recursion as the fit, parameters kept) and forecast H steps.
+    Returns (forecast [R, H], sigma [R], updated ESState)."""
+    check(x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1, "x must be [R, T] float32")
+    R = x.shape[0]
+    check(model.params.shape[0] == R and t_new.shape[0] == R, "one cached model and one t_new per row")
+    kind, m = model.kind, model.m
+    if not x.is_cuda:
+        st = {"state": model.state.numpy().copy(), "season": None if model.season is None else
+              model.season.numpy().T.copy(), "sse": model.sse.numpy().astype(np.float64), "nobs":
+              model.nobs.numpy().astype(np.int64)}
+        fc, sig = ref_es_update(x.numpy()[:, :T], t_new.numpy(), kind, m, model.params.numpy(), st, H)
+        new = ESState(kind, m, model.params, torch.from_numpy(st["state"]),
+                      None if st["season"] is None else torch.from_numpy(np.ascontiguousarray(st["season"].T)),
+                      torch.from_numpy(st["sse"].astype(np.float32)), torch.from_numpy(st["nobs"].astype(np.int32)))
+        return torch.from_numpy(fc), torch.from_numpy(sig), new
+    require_native(x)
+    d = x.device
+    new = ESState(kind, m, model.params.to(d).contiguous(), model.state.to(d).clone(),
+                  None if model.season is None else model.season.to(d).clone(), model.sse.to(d).clone(),
+                  model.nobs.to(d).clone())
+    tn = t_new.to(device=d, dtype=torch.int32).contiguous()
+    fc = torch.empty((R, H), dtype=torch.float32, device=d)
+    sig = torch.empty((R,), dtype=torch.float32, device=d)
+    best = torch.empty((R,), dtype=torch.int32, device=d)
+    season = new.season if new.season is not None else torch.empty((1,), dtype=torch.float32, device=d)
+    LIB.call("fm_es_update", ptr(x), x.stride(0), T, R, ptr(tn), ptr(new.params), m, kind, ptr(season),
+             ptr(new.sse), ptr(new.state), ptr(new.nobs), H, ptr(fc), ptr(sig), ptr(best), stream_of(x))
+    return fc, sig, new
+
+
+# ----------------------------------------------------------------- fp32 numpy mirror of the kernels
+def _step(kind, xt, act, lvl, tr, s_old, al, be, ga):
+    """One recursion step on every pair; ``act`` masks pairs that have
+    started.  Returns (ok, e, lvl, tr, s_new)."""
+    f1 = np.float32(1)
+    ok = act & np.isfinite(xt)
+    x0 = np.where(ok, xt, 0).astype(np.float32)
+    if kind == 3:
+        pred = (lvl + tr) * s_old
+    else:
+        pred = lvl + tr + s_old
+    e = np.where(ok, x0 - pred, 0).astype(np.float32)
+    lprev = lvl
+    s_new = s_old
+    nt = tr
+    if kind == 0:
+        nl = al * x0 + (f1 - al) * lvl
+    elif kind == 1:
+        nl = al * x0 + (f1 - al) * (lvl + tr)
+        nt = be * (nl - lprev) + (f1 - be) * tr
+    elif kind == 2:
+        nl = al * (x0 - s_old) + (f1 - al) * (lvl + tr)
+        nt = be * (nl - lprev) + (f1 - be) * tr
+        s_new = ga * (x0 - nl) + (f1 - ga) * s_old
+    else:
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ds = np.where(np.abs(s_old) > DIV_EPS, x0 / np.where(s_old == 0, 1, s_old), x0)
+            nl = (al * ds + (f1 - al) * (lvl + tr)).astype(np.float32)
+            nt = be * (nl - lprev) + (f1 - be) * tr
+            dl = np.where(np.abs(nl) > DIV_EPS, x0 / np.where(nl == 0, 1, nl), f1)
+        s_new = ga * dl + (f1 - ga) * s_old
+    miss = act & ~ok
+    lvl = np.where(ok, nl, np.where(miss, lvl + tr, lvl)).astype(np.float32)
+    tr = np.where(ok, nt, tr).astype(np.float32)
+    s_new = np.where(ok, s_new, s_old).astype(np.float32)
+    return ok, e, lvl, tr, s_new
+
+
+def _run(kind, xr, t0, T, m, al, be, ga, lvl, tr, season, sse, n):
+    P = xr.shape[0]
+    rows = np.arange(P)
+    for t in range(int(t0.min()) if P else T, T):
+        act = t >= t0
+        xt = xr[:, t]
+        if kind >= 2:
+            ph = t % m
+            s_old = season[:, ph]
+        else:
+            s_old = np.float32(0)
+        ok, e, lvl, tr, s_new = _step(kind, xt, act, lvl, tr, s_old, al, be, ga)
+        sse += e.astype(np.float64) ** 2
+        n += ok
+        if kind >= 2:
+            season[rows, ph] = s_new
+    return lvl, tr
+
+
+def ref_es_fit(x: np.ndarray, kind: int, H: int, m: int, grid: np.ndarray, return_state: bool = False):
+    """fp32 recursion mirrored in numpy (vectorised over rows x candidates),
+    including the kernel's ragged-row handling: each row starts at its first
+    finite sample and the seasonal initialisation averages finite samples.
+    Seasonal phases are absolute (t % m) in both."""
     x = np.asarray(x, dtype=np.float32)
     R, T = x.shape
     G = grid.shape[0]
@@ -72,64 +202,99 @@ def ref_es_fit(x: np.ndarray, kind: int, H: int, m: int, grid: np.ndarray):
     ga = np.tile(grid[:, 2], R)
     xr = np.repeat(x, G, axis=0)  # [R*G, T]
     P = R * G
-    f = np.float32
-    if kind == 2:
-        s1 = xr[:, :m].mean(1, dtype=np.float32)
-        s2 = xr[:, m:2 * m].mean(1, dtype=np.float32)
+    fin = np.isfinite(xr)
+    base = np.where(fin.any(1), fin.argmax(1), T)
+    none = base >= T
+    bcl = np.minimum(base, T - 1)
+    lvl = np.zeros(P, np.float32)
+    tr = np.zeros(P, np.float32)
+    season = None
+    if kind >= 2:
+        def nanmean(lo, hi):
+            idx = lo[:, None] + np.arange(m)[None, :]
+            valid = idx < hi[:, None]
+            v = np.take_along_axis(xr, np.minimum(idx, T - 1), 1)
+            ok = valid & np.isfinite(v)
+            c = ok.sum(1)
+            s = np.where(ok, v, 0).sum(1, dtype=np.float32)
+            return (s / np.maximum(c, 1)).astype(np.float32), c, v, ok
+        e1 = np.minimum(base + m, T)
+        e2 = np.minimum(base + 2 * m, T)
+        s1, _, v1, ok1 = nanmean(bcl, e1)
+        s2, c2, _, _ = nanmean(np.minimum(e1, T - 1), e2)
+        c2 = np.where(e1 >= T, 0, c2)
         lvl = s1.copy()
-        tr = ((s2 - s1) / f(m)).astype(np.float32)
-        season = (xr[:, :m] - s1[:, None]).astype(np.float32)  # [P, m]
-        t0 = m
-    elif kind == 1:
-        lvl = xr[:, 0].copy()
-        tr = (xr[:, 1] - xr[:, 0]).astype(np.float32)
-        season = None
-        t0 = 1
+        tr = np.where(c2 > 0, (s2 - s1) / np.float32(m), 0).astype(np.float32)
+        if kind == 3:
+            mul_ok = np.abs(s1) > DIV_EPS
+            with np.errstate(divide="ignore", invalid="ignore"):
+                sv = np.where(ok1 & mul_ok[:, None], v1 / np.where(s1 == 0, 1, s1)[:, None], 1)
+        else:
+            sv = np.where(ok1, v1 - s1[:, None], 0)
+        season = np.zeros((P, m), np.float32)
+        ph0 = (base[:, None] + np.arange(m)[None, :]) % m
+        np.put_along_axis(season, ph0, sv.astype(np.float32), 1)
+        t0 = base + m
     else:
-        lvl = xr[:, 0].copy()
-        tr = np.zeros(P, np.float32)
-        season = None
-        t0 = 1
+        lvl = xr[np.arange(P), bcl].copy()
+        if kind == 1:
+            nxt = xr[np.arange(P), np.minimum(bcl + 1, T - 1)]
+            tr = np.where((bcl + 1 < T) & np.isfinite(nxt), nxt - lvl, 0).astype(np.float32)
+        t0 = base + 1
+    lvl = np.where(none, np.float32(np.nan), lvl).astype(np.float32)
     sse = np.zeros(P, np.float64)
     n = np.zeros(P, np.int64)
-    for t in range(t0, T):
-        xt = xr[:, t]
-        ph = (t - t0) % m if kind == 2 else 0
-        s_old = season[:, ph] if kind == 2 else np.float32(0)
-        pred = lvl + tr + s_old
-        ok = np.isfinite(xt)
-        e = np.where(ok, xt - pred, 0).astype(np.float32)
-        sse += e.astype(np.float64) ** 2
-        n += ok
-        lprev = lvl
-        if kind == 0:
-            nl = al * xt + (f(1) - al) * lvl
-            lvl = np.where(ok, nl, lvl + tr).astype(np.float32)
-        elif kind == 1:
-            nl = al * xt + (f(1) - al) * (lvl + tr)
-            nt = be * (nl - lprev) + (f(1) - be) * tr
-            lvl = np.where(ok, nl, lvl + tr).astype(np.float32)
-            tr = np.where(ok, nt, tr).astype(np.float32)
-        else:
-            nl = al * (xt - s_old) + (f(1) - al) * (lvl + tr)
-            nt = be * (nl - lprev) + (f(1) - be) * tr
-            ns = ga * (xt - nl) + (f(1) - ga) * s_old
-            lvl = np.where(ok, nl, lvl + tr).astype(np.float32)
-            tr = np.where(ok, nt, tr).astype(np.float32)
-            season[:, ph] = np.where(ok, ns, s_old)
+    lvl, tr = _run(kind, xr, t0, T, max(m, 1), al, be, ga, lvl, tr, season, sse, n)
     sse = sse.reshape(R, G)
-    best = np.argmin(sse, axis=1)
+    best = np.argmin(np.where(np.isfinite(sse), sse, np.inf), axis=1)
     pid = np.arange(R) * G + best
-    nb = n[pid]
-    sig = np.sqrt(sse[np.arange(R), best] / np.maximum(nb - 1, 1)).astype(np.float32)
+    fc, sig = _forecast(kind, m, lvl[pid], tr[pid], None if season is None else season[pid], T % max(m, 1),
+                        sse[np.arange(R), best], n[pid], H)
+    out = (fc, sig, best.astype(np.int32), sse.astype(np.float32))
+    if return_state:
+        st = {"state": np.stack([lvl[pid], tr[pid], np.full(R, T % m if kind >= 2 else 0, np.float32)], 1)
+              .astype(np.float32), "season": None if season is None else season[pid],
+              "sse": sse[np.arange(R), best].astype(np.float32), "nobs": n[pid].astype(np.int32)}
+        out = out + (st,)
+    return out
+
+
+def _forecast(kind, m, lvl, tr, season, tph, sse, n, H):
     h = np.arange(1, H + 1)[None, :]
-    fc = lvl[pid][:, None] + (h * tr[pid][:, None] if kind >= 1 else np.zeros((1, H), np.float32))
-    if kind == 2:
-        tph = T % m
-        idx = (tph + h - 1) % m
-        # phases in `season` are relative to t0 = m, i.e. absolute phase t % m
-        fc = fc + season[pid][:, idx[0]]
-    return fc.astype(np.float32), sig, best.astype(np.int32), sse.astype(np.float32)
+    fc = lvl[:, None] + (h * tr[:, None] if kind >= 1 else np.zeros((1, H), np.float32))
+    if kind >= 2:
+        tph = np.broadcast_to(np.asarray(tph), lvl.shape)
+        idx = (tph[:, None] + h - 1) % m
+        s = np.take_along_axis(season, idx.astype(np.int64), 1)
+        fc = fc * s if kind == 3 else fc + s
+    sig = np.where(n > 1, np.sqrt(sse / np.maximum(n - 1, 1)), 0).astype(np.float32)
+    return fc.astype(np.float32), sig
+
+
+def ref_es_update(x: np.ndarray, t_new: np.ndarray, kind: int, m: int, params: np.ndarray, st: dict, H: int):
+    """numpy mirror of ``fm_es_update``; updates ``st`` in place (season [R, m]).
+    Phases stay relative to the cached model: the first new sample has phase
+    ``state[:, 2]``."""
+    x = np.asarray(x, np.float32)
+    R, T = x.shape
+    lvl = st["state"][:, 0].astype(np.float32)
+    tr = st["state"][:, 1].astype(np.float32)
+    ph = st["state"][:, 2].astype(np.int64) if kind >= 2 else np.zeros(R, np.int64)
+    t0 = np.clip(t_new.astype(np.int64), 0, T)
+    al, be, ga = (params[:, i].astype(np.float32) for i in range(3))
+    season = st["season"]
+    rows = np.arange(R)
+    for t in range(int(t0.min()) if R else T, T):
+        act = t >= t0
+        s_old = season[rows, ph] if kind >= 2 else np.float32(0)
+        ok, e, lvl, tr, s_new = _step(kind, x[:, t], act, lvl, tr, s_old, al, be, ga)
+        st["sse"] += e.astype(np.float64) ** 2
+        st["nobs"] += ok
+        if kind >= 2:
+            season[rows, ph] = s_new
+            ph = np.where(act, (ph + 1) % m, ph)
+    st["state"] = np.stack([lvl, tr, ph.astype(np.float32)], 1).astype(np.float32)
+    return _forecast(kind, m, lvl, tr, season, ph, st["sse"], st["nobs"], H)
 
 
 def band_decide(cur: torch.Tensor, center: torch.Tensor, sigma: torch.Tensor, M: int, thr, bound, minlb,

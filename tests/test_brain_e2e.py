@@ -129,12 +129,38 @@ def test_hpa_forecast_algorithms(algo):
 
 
 @pytest.mark.parametrize("algo", ["moving_average", "exponential_smoothing", "double_exponential_smoothing",
-                                  "holt_winters", "prophet", "lstm", "bivariate_normal"])
+                                  "holt_winters", "holt_winters_multiplicative", "prophet", "lstm",
+                                  "bivariate_normal"])
 def test_every_algorithm_runs_end_to_end(algo):
     clock, store, client, brain, exp = _setup(faults={"7687b9f4d7-aaaa1": 8.0}, algorithm=algo)
     jid = client.start_analyzing("default", "demo", PODS, _metrics(), 10, "canary")
     brain.run_once()
     assert client.get_status(jid).status in (crd.PHASE_UNHEALTHY, crd.PHASE_RUNNING)
+
+
+def test_hpa_cycles_reuse_cached_models(tmp_path):
+    # HPA jobs are re-scored every cycle: the second cycle advances the cached
+    # fits over the new samples instead of re-running the grid
+    clock, store, client, brain, exp = _setup(algorithm="double_exponential_smoothing")
+    brain.cfg.hpa_forecast_algorithm = "double_exponential_smoothing"
+    client.start_analyzing("default", "demo", None, _metrics(), 10, "hpa", ["cpu", "latency"])
+    brain.run_once()
+    c = brain.model_cache
+    assert len(c) == 2 and c.misses == 2 and c.hits == 2     # scoring fits, HPA forecast reuses (k = 0)
+    clock.t += 120
+    brain.run_once()
+    assert c.hits == 6 and c.misses == 2
+    # refit after MODEL_REFIT_SECONDS
+    clock.t += brain.cfg.model_refit_seconds + 60
+    brain.run_once()
+    assert c.misses == 4
+    # the cache survives a checkpoint round trip
+    brain.save_checkpoint(str(tmp_path))
+    b2 = Brain(store, brain.cfg, sources=brain.sources, clock=clock)
+    assert b2.load_checkpoint(str(tmp_path)) and len(b2.model_cache) == 2
+    k = next(iter(c.entries))
+    (s1, i1), (s2, i2) = c.locate(k), b2.model_cache.locate(k)
+    np.testing.assert_array_equal(s1.read([i1]).state.numpy(), s2.read([i2]).state.numpy())
 
 
 def test_checkpoint_roundtrip(tmp_path):
@@ -152,8 +178,8 @@ def test_checkpoint_roundtrip(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("algo", ["moving_average_all", "moving_average", "exponential_smoothing",
-                                  "double_exponential_smoothing", "holt_winters", "prophet", "lstm",
-                                  "bivariate_normal"])
+                                  "double_exponential_smoothing", "holt_winters", "holt_winters_multiplicative",
+                                  "prophet", "lstm", "bivariate_normal"])
 def test_gpu_brain_every_algorithm(cuda, algo):
     clock, store, client, brain, exp = _setup(faults={"7687b9f4d7-aaaa1": 8.0}, algorithm=algo, device=cuda)
     jid = client.start_analyzing("default", "demo", PODS, _metrics(), 10, "canary")

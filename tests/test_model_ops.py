@@ -45,6 +45,103 @@ def test_ref_es_matches_scalar_loop():
             np.testing.assert_allclose(sse[r, g], e2, rtol=1e-3)
 
 
+def test_ref_multiplicative_hw_matches_scalar_loop():
+    x = _seasonal(2, 240, period=12, seed=3)
+    grid = SM.default_grid(3)[:3]
+    fc, sig, best, sse = SM.ref_es_fit(x, 3, 4, 12, grid)
+    m = 12
+    for r in range(2):
+        for g in range(3):
+            a, b, gm = (np.float32(v) for v in grid[g])
+            y = x[r].astype(np.float32)
+            s1, s2 = y[:m].mean(), y[m:2 * m].mean()
+            lvl, tr = s1, (s2 - s1) / m
+            season = list(y[:m] / s1)
+            e2 = 0.0
+            for t in range(m, len(y)):
+                so = season[t % m]
+                e2 += float(y[t] - (lvl + tr) * so) ** 2
+                lp = lvl
+                lvl = a * (y[t] / so) + (1 - a) * (lvl + tr)
+                tr = b * (lvl - lp) + (1 - b) * tr
+                season[t % m] = gm * (y[t] / lvl) + (1 - gm) * so
+            np.testing.assert_allclose(sse[r, g], e2, rtol=1e-3)
+            if g == best[r]:
+                h = np.arange(1, 5)
+                want = (lvl + h * tr) * np.array([season[(len(y) + k - 1) % m] for k in h])
+                np.testing.assert_allclose(fc[r], want, rtol=1e-4)
+
+
+@pytest.mark.parametrize("kind,m", [(0, 1), (1, 1), (2, 12), (3, 12)])
+def test_ref_es_left_padding_is_a_relabelling(kind, m):
+    # ragged batches are right-aligned with NaN on the left: the fit must start
+    # at the first finite sample and give the unpadded row's answer
+    x = _seasonal(3, 300, period=12, seed=kind)
+    pad = np.full((3, 37), np.nan, np.float32)
+    xp = np.concatenate([pad, x], 1)
+    grid = SM.default_grid(kind)
+    a = SM.ref_es_fit(x, kind, 6, m, grid)
+    b = SM.ref_es_fit(xp, kind, 6, m, grid)
+    np.testing.assert_allclose(b[3], a[3], rtol=1e-5)
+    np.testing.assert_allclose(b[0], a[0], rtol=1e-5)
+    allnan = np.full((1, 300), np.nan, np.float32)
+    fc, sig, _, _ = SM.ref_es_fit(allnan, kind, 3, m, grid)
+    assert np.isnan(fc).all() and sig[0] == 0
+
+
+@pytest.mark.parametrize("kind,m", [(0, 1), (1, 1), (2, 12), (3, 12)])
+def test_ref_es_update_equals_longer_fit(kind, m):
+    # cache semantics: fit on the first T samples, then slide the window by k
+    # and advance the cached model over the k new samples == one fit over T+k
+    T, k, H = 240, 17, 5
+    y = _seasonal(4, T + k, period=12, seed=7 + kind)
+    y[1, T + 3] = np.nan
+    grid = SM.default_grid(kind)[[4]]
+    f0 = SM.es_fit(torch.from_numpy(y[:, :T].copy()), T, kind, H, m, grid=grid, keep_state=True)
+    win = torch.from_numpy(y[:, k:].copy())
+    fc, sig, st = SM.es_update(win, T, torch.full((4,), T - k, dtype=torch.int32), f0.model, H)
+    full = SM.es_fit(torch.from_numpy(y), T + k, kind, H, m, grid=grid)
+    np.testing.assert_allclose(fc.numpy(), full.forecast.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(sig.numpy(), full.sigma.numpy(), rtol=1e-5)
+    assert st.nobs.tolist() == [int(v) for v in np.isfinite(y[:, 1 if kind < 2 else m:]).sum(1)]
+
+
+def test_model_cache_advances_lru_and_refit():
+    from foremast_amd.models.cache import ModelCache
+    T, k, H, m = 240, 7, 4, 12
+    y = _seasonal(3, T + 2 * k, period=12, seed=21)
+    c = ModelCache(capacity=3, refit_seconds=1000.0)
+    keys = [("ns/a", "cpu"), ("ns/b", "cpu"), ("ns/c", "cpu")]
+    t_last = np.array([1000.0] * 3)
+    per = lambda sub: m
+    x0 = torch.from_numpy(y[:, :T].copy())
+    f0, s0 = c.es_forecast(keys, t_last, 60.0, 0.0, x0, T, 2, H, per)
+    ref = SM.es_fit(x0, T, 2, H, m, keep_state=True)
+    np.testing.assert_allclose(f0.numpy(), ref.forecast.numpy(), rtol=1e-6)
+    assert (c.hits, c.misses, len(c)) == (0, 3, 3)
+    # next cycle: window slid by k samples -> advanced, equal to es_update
+    x1 = torch.from_numpy(y[:, k:T + k].copy())
+    f1, s1 = c.es_forecast(keys, t_last + 60 * k, 60.0, 10.0, x1, T, 2, H, per)
+    u, us, _ = SM.es_update(x1, T, torch.full((3,), T - k, dtype=torch.int32), ref.model, H)
+    np.testing.assert_allclose(f1.numpy(), u.numpy(), rtol=1e-6)
+    np.testing.assert_allclose(s1.numpy(), us.numpy(), rtol=1e-6)
+    assert c.hits == 3
+    c.es_forecast(keys[1:], t_last[1:] + 60 * k, 60.0, 10.0, x1[1:].contiguous(), T, 2, H, per)
+    assert c.hits == 5
+    # a new key evicts the least recently used one; history going backwards re-fits
+    c.es_forecast([("ns/d", "cpu")], np.array([2000.0]), 60.0, 10.0, x1[:1].contiguous(), T, 2, H, per)
+    assert len(c) == 3 and ("ns/a", "cpu") not in c.entries
+    c.es_forecast([("ns/b", "cpu")], np.array([500.0]), 60.0, 10.0, x1[1:2].contiguous(), T, 2, H, per)
+    assert c.misses == 5
+    # stale fits are re-run
+    c.es_forecast([("ns/c", "cpu")], t_last[:1] + 60 * (k + 1), 60.0, 5000.0, x1[2:3].contiguous(), T, 2, H, per)
+    assert c.misses == 6
+    # rows without any data are never cached
+    c2 = ModelCache(4)
+    c2.es_forecast([("e", "x")], np.array([0.0]), 60.0, 0.0, torch.full((1, T), float("nan")), T, 1, H, per)
+    assert len(c2) == 0
+
+
 def test_ref_fft_detects_daily_period():
     assert FF.plan_radices(5040) == [4, 4, 9, 5, 7]
     assert FF.supported_length(10080) and not FF.supported_length(10082)
@@ -130,18 +227,44 @@ def test_ref_lstm_matches_torch_lstm():
 
 # ----------------------------------------------------------------- GPU kernels
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,m", [(0, 1), (1, 1), (2, 12), (2, 24), (2, 1440)])
+@pytest.mark.parametrize("kind,m", [(0, 1), (1, 1), (2, 12), (2, 24), (2, 1440), (3, 24), (3, 1440)])
 def test_gpu_es_fit(cuda, kind, m):
     # m=12: plain loop (m <= prefetch depth); 24/1440: prefetched chunks + tail
     T = 3001 if m < 1440 else 10080
     x = _seasonal(37, T, period=max(m, 24), seed=kind)
     x[3, 500] = np.nan
+    x[5, :77] = np.nan           # ragged row (left padding)
+    x[6, :] = np.nan             # no data at all
     fc0, sig0, best0, sse0 = SM.ref_es_fit(x, kind, 10, m, SM.default_grid(kind))
     r = SM.es_fit(torch.from_numpy(x).to(cuda), T, kind, 10, m)
-    np.testing.assert_allclose(r.sse.cpu().numpy(), sse0, rtol=5e-3)
+    # candidates whose recursion diverges (some multiplicative (alpha, beta,
+    # gamma) corners) amplify fp32 rounding chaotically: compare stable fits
+    stable = sse0 < 1e3 * np.median(sse0)
+    assert stable.mean() > 0.9
+    np.testing.assert_allclose(r.sse.cpu().numpy()[stable], sse0[stable], rtol=5e-3)
     same = r.best.cpu().numpy() == best0
     assert same.mean() > 0.9
     np.testing.assert_allclose(r.forecast.cpu().numpy()[same], fc0[same], rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,m", [(1, 1), (2, 24), (3, 1440)])
+def test_gpu_es_update_matches_reference(cuda, kind, m):
+    T = 3001 if m < 1440 else 10080
+    k, H = 45, 12
+    y = _seasonal(33, T + k, period=max(m, 24), seed=11 + kind)
+    y[2, T + 5] = np.nan
+    f0 = SM.es_fit(torch.from_numpy(y[:, :T].copy()).to(cuda), T, kind, H, m, keep_state=True)
+    c0 = SM.es_fit(torch.from_numpy(y[:, :T].copy()), T, kind, H, m, keep_state=True)
+    tn = torch.full((33,), T - k, dtype=torch.int32)
+    win = y[:, k:].copy()
+    fg, sg, stg = SM.es_update(torch.from_numpy(win).to(cuda), T, tn, f0.model, H)
+    same = (f0.best.cpu() == c0.best).numpy()
+    assert same.mean() > 0.9
+    fc, sc, stc = SM.es_update(torch.from_numpy(win), T, tn, c0.model, H)
+    np.testing.assert_allclose(fg.cpu().numpy()[same], fc.numpy()[same], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(sg.cpu().numpy()[same], sc.numpy()[same], rtol=5e-3)
+    np.testing.assert_array_equal(stg.nobs.cpu().numpy(), stc.nobs.numpy())
 
 
 @pytest.mark.gpu
