@@ -65,6 +65,18 @@ struct EsModel {
   }
 };
 
+// Initial seasonal index of a sample one season before (additive: x - s1,
+// multiplicative: x / s1; missing -> 0 / 1).
+template <int KIND>
+struct SeasonInit {
+  float s1, inv1;
+  bool mul_ok;
+  __device__ __forceinline__ float operator()(float v) const {
+    const bool ok = isfinite(v);
+    return KIND == 3 ? (ok && mul_ok ? v * inv1 : 1.f) : (ok ? v - s1 : 0.f);
+  }
+};
+
 // Run the recursion over samples [t, T) of row xr.  Seasonal state of this
 // (row, candidate) pair is column `col` of season[m][P]; ph = t % m on entry
 // and on exit.  `t` and `ph` must be wave-uniform so the season addressing
@@ -72,10 +84,19 @@ struct EsModel {
 // starts later (ragged rows) pass GATED = true and their first sample t_act,
 // and skip the steps before it.  err2/n carry the SSE (fp32 partials flushed
 // to fp64 every 64 steps) and the observation count.
-template <int KIND, bool GATED>
+// LAP1: the first season after the initialisation window, whose seasonal
+// indices are computed from the sample one period earlier (x[t - m], shared
+// by the row's candidates and L2-resident) instead of being materialised per
+// candidate and read back: saves a full write + read pass over the
+// [m][R*G] scratch.
+// NOSTORE: the tail of the last season, whose updated indices no forecast
+// reads (the H-step forecast needs phases T..T+H-1, last written in the
+// first H steps of the final season) -- when the caller does not keep the
+// fitted state, those stores are skipped.
+template <int KIND, bool GATED, bool LAP1 = false, bool NOSTORE = false>
 __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restrict__ xr, int t, int T, int t_act,
                                        int m, float* __restrict__ season, int64_t P, int64_t col, int& ph,
-                                       double& err2, int& n) {
+                                       double& err2, int& n, SeasonInit<KIND> init = {}) {
   constexpr bool kSeason = KIND >= 2;
   float acc = 0.f;
   int chunk = 0;
@@ -93,18 +114,24 @@ __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restric
         int pu = ph + u;
         if (pu >= m) pu -= m;
         si[u] = (int64_t)pu * P + col;
-        sv[u] = season[si[u]];
+        sv[u] = LAP1 ? xr[t + u - m] : season[si[u]];
         xv[u] = xr[t + u];
       }
       ph += kPrefetch;
       if (ph >= m) ph -= m;
+      if (LAP1) {
+#pragma unroll
+        for (int u = 0; u < kPrefetch; ++u) sv[u] = init(sv[u]);
+      }
 #pragma unroll
       for (int u = 0; u < kPrefetch; ++u) {
         if (GATED && t + u < t_act) continue;
         md.step(xv[u], sv[u], acc, n);
       }
+      if (!NOSTORE) {
 #pragma unroll
-      for (int u = 0; u < kPrefetch; ++u) season[si[u]] = sv[u];
+        for (int u = 0; u < kPrefetch; ++u) season[si[u]] = sv[u];
+      }
       chunk += kPrefetch;
       if (chunk >= 64) { err2 += acc; acc = 0.f; chunk = 0; }
     }
@@ -112,27 +139,17 @@ __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restric
   for (; t < T; ++t) {
     float s = 0.f;
     int64_t sidx = 0;
-    if (kSeason) { sidx = (int64_t)ph * P + col; s = season[sidx]; if (++ph == m) ph = 0; }
+    if (kSeason) {
+      sidx = (int64_t)ph * P + col;
+      s = LAP1 ? init(xr[t - m]) : season[sidx];
+      if (++ph == m) ph = 0;
+    }
     if (GATED && t < t_act) continue;
     md.step(xr[t], s, acc, n);
-    if (kSeason) season[sidx] = s;
+    if (kSeason && !NOSTORE) season[sidx] = s;
     if (++chunk == 64) { err2 += acc; acc = 0.f; chunk = 0; }
   }
   err2 += acc;
-}
-
-// Wave-uniform entry into es_run: all lanes start at the wave's earliest
-// first step; the gated variant only runs when the lanes' starts differ.
-template <int KIND>
-__device__ __forceinline__ void es_run_wave(EsModel<KIND>& md, const float* __restrict__ xr, int t0, int T, int m,
-                                            float* __restrict__ season, int64_t P, int64_t col, double& err2,
-                                            int& n, int& ph_out) {
-  const int lo = __builtin_amdgcn_readfirstlane(wave_min(t0));
-  const int hi = __builtin_amdgcn_readfirstlane(wave_max(t0));
-  int ph = KIND >= 2 ? lo % m : 0;
-  if (lo == hi) es_run<KIND, false>(md, xr, lo, T, lo, m, season, P, col, ph, err2, n);
-  else es_run<KIND, true>(md, xr, lo, T, t0, m, season, P, col, ph, err2, n);
-  ph_out = ph;
 }
 
 __device__ __forceinline__ int first_finite(const float* __restrict__ xr, int T) {
@@ -141,25 +158,46 @@ __device__ __forceinline__ int first_finite(const float* __restrict__ xr, int T)
   return b;
 }
 
-// Finite-sample mean of xr[lo, hi); sets cnt.
+// Finite-sample mean of xr[lo, hi); sets cnt.  Branch-free body so the
+// loads of consecutive iterations are issued back to back.
 __device__ __forceinline__ float nan_mean(const float* __restrict__ xr, int lo, int hi, int& cnt) {
   float s = 0.f;
-  cnt = 0;
-  for (int i = lo; i < hi; ++i)
-    if (isfinite(xr[i])) { s += xr[i]; ++cnt; }
-  return cnt > 0 ? s / cnt : 0.f;
+  int c = 0;
+#pragma unroll 8
+  for (int i = lo; i < hi; ++i) {
+    const float v = xr[i];
+    const bool f = isfinite(v);
+    s += f ? v : 0.f;
+    c += f;
+  }
+  cnt = c;
+  return c > 0 ? s / c : 0.f;
+}
+
+// Seasonal indices of samples xs[i0, i1) written to consecutive phases from
+// sp on (stride P); samples at or past navail are missing.
+template <int KIND>
+__device__ __forceinline__ void season_init(const float* __restrict__ xs, int i0, int i1, int navail,
+                                            SeasonInit<KIND> init, float* __restrict__ sp, int64_t P) {
+  const int last = navail > 0 ? navail - 1 : 0;
+#pragma unroll 8
+  for (int i = i0; i < i1; ++i) {
+    const float v = xs[i < last ? i : last];   // unpredicated load, masked below
+    sp[(int64_t)(i - i0) * P] = i < navail ? init(v) : init(__builtin_nanf(""));
+  }
 }
 
 template <int KIND>
 __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x, int64_t ld, int T, int64_t R,
                                                     const float* __restrict__ cand, int G, int m,
                                                     float* __restrict__ season /*[m][R*G]*/, float* __restrict__ sse,
-                                                    float* __restrict__ state /*[R*G,3]*/, int* __restrict__ nobs) {
+                                                    float* __restrict__ state /*[R*G,3]*/, int* __restrict__ nobs,
+                                                    int t_store_end) {
   const int64_t P = R * G;
   const int64_t pid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if ((pid_raw & ~(int64_t)63) >= P) return;      // whole wave past the end
   // tail lanes of the last wave shadow the last pair (the wave-uniform start
-  // below needs every lane) and store nothing
+  // below needs every lane) and store no results of their own
   const bool live = pid_raw < P;
   const int64_t pid = live ? pid_raw : P - 1;
   const int64_t row = pid / G;
@@ -168,6 +206,7 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
   const float* xr = x + row * ld;
   const int base = first_finite(xr, T);
   int t0;
+  SeasonInit<KIND> sinit{0.f, 0.f, false};
   if (base >= T) {
     md.lvl = __builtin_nanf("");
     t0 = T;
@@ -181,16 +220,7 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     md.lvl = s1;
     md.tr = c2 > 0 ? (s2 - s1) / m : 0.f;
     const bool mul_ok = fabsf(s1) > kDivEps;
-    const float inv1 = mul_ok ? 1.f / s1 : 0.f;
-    int ph = base % m;                    // absolute phase, advanced without a modulo per sample
-    for (int i = 0; i < m; ++i) {
-      const int t = base + i;
-      const float v = xr[t < T ? t : T - 1];
-      float si = KIND == 3 ? 1.f : 0.f;
-      if (t < T && isfinite(v)) si = KIND == 3 ? (mul_ok ? v * inv1 : 1.f) : v - s1;
-      if (live) season[(int64_t)ph * P + pid] = si;
-      if (++ph == m) ph = 0;
-    }
+    sinit = SeasonInit<KIND>{s1, mul_ok ? 1.f / s1 : 0.f, mul_ok};
     t0 = base + m;
   } else {
     md.lvl = xr[base];
@@ -198,10 +228,35 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     t0 = base + 1;
   }
   double err2 = 0.0;
-  int n = 0, ph;
+  int n = 0;
+  // wave-uniform start: all lanes run from the wave's earliest first step
+  const int lo = __builtin_amdgcn_readfirstlane(wave_min(t0));
+  const int hi = __builtin_amdgcn_readfirstlane(wave_max(t0));
+  int ph = KIND >= 2 ? lo % m : 0;
+  if (lo == hi && (KIND < 2 || lo + m <= T)) {
+    if (KIND >= 2) {
+      // seasons written up to t_store_end (T when the fitted state is kept)
+      const int ts = max(lo + m, min(t_store_end, T));
+      es_run<KIND, false, true>(md, xr, lo, lo + m, lo, m, season, P, pid, ph, err2, n, sinit);
+      es_run<KIND, false>(md, xr, lo + m, ts, lo, m, season, P, pid, ph, err2, n);
+      es_run<KIND, false, false, true>(md, xr, ts, T, lo, m, season, P, pid, ph, err2, n);
+    } else {
+      es_run<KIND, false>(md, xr, lo, T, lo, m, season, P, pid, ph, err2, n);
+    }
+  } else {
+    // ragged rows in this wave: materialise the initial seasons (sample
+    // base + i has absolute phase (base + i) % m: phases ph0 .. m-1, then
+    // 0 .. ph0-1), then run with per-lane start gating
+    if (KIND >= 2 && base < T) {
+      const int ph0 = base % m;
+      const int navail = min(m, T - base);
+      season_init<KIND>(xr + base, 0, m - ph0, navail, sinit, season + (int64_t)ph0 * P + pid, P);
+      season_init<KIND>(xr + base, m - ph0, m, navail, sinit, season + pid, P);
+    }
+    es_run<KIND, true>(md, xr, lo, T, t0, m, season, P, pid, ph, err2, n);
+  }
   // shadow lanes recompute their twin's pair in lockstep (same values, same
-  // addresses) and then store nothing of their own
-  es_run_wave<KIND>(md, xr, t0, T, m, season, P, pid, err2, n, ph);
+  // addresses) and then store no results of their own
   if (!live) return;
   sse[pid] = (float)err2;
   state[pid * 3 + 0] = md.lvl;
@@ -210,34 +265,52 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
   nobs[pid] = n;
 }
 
-// Incremental update of one cached model per row over its new samples
-// x[row, t_new[row] .. T): state [R,3] (level, trend, phase of the next
-// sample), season [m][R], params [R,3], sse/nobs accumulate.
+// Incremental update of cached models, in place in the cache's slab: row r
+// of x (its new samples x[r, t_new[r] .. T)) advances slot s = slots[r] (or
+// r when slots is null) of params/state [C,3] (level, trend, phase of the
+// next sample), season [C, m] (row-major per slot), sse/nobs [C], then
+// writes the H-step forecast and residual sigma of row r.  One thread per
+// row; k is a handful of samples, so the scattered slot accesses are noise.
 template <int KIND>
 __global__ __launch_bounds__(256) void es_update_kernel(const float* __restrict__ x, int64_t ld, int T, int64_t R,
-                                                       const int* __restrict__ t_new, const float* __restrict__ params,
-                                                       int m, float* __restrict__ season, float* __restrict__ sse,
-                                                       float* __restrict__ state, int* __restrict__ nobs) {
+                                                       const int* __restrict__ t_new,
+                                                       const int64_t* __restrict__ slots,
+                                                       const float* __restrict__ params, int m,
+                                                       float* __restrict__ season, float* __restrict__ sse,
+                                                       float* __restrict__ state, int* __restrict__ nobs, int H,
+                                                       float* __restrict__ fc, float* __restrict__ sigma) {
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= R) return;
-  EsModel<KIND> md{params[row * 3 + 0], params[row * 3 + 1], params[row * 3 + 2], state[row * 3 + 0],
-                   state[row * 3 + 1]};
-  // phases differ per cached series: per-lane (VGPR) phase, gated-free loop
-  int ph = KIND >= 2 ? (int)state[row * 3 + 2] : 0;
+  const int64_t sl = slots != nullptr ? slots[row] : row;
+  EsModel<KIND> md{params[sl * 3 + 0], params[sl * 3 + 1], params[sl * 3 + 2], state[sl * 3 + 0],
+                   state[sl * 3 + 1]};
+  int ph = KIND >= 2 ? (int)state[sl * 3 + 2] : 0;
   int t0 = t_new[row];
   t0 = t0 < 0 ? 0 : (t0 > T ? T : t0);
-  double err2 = sse[row];
-  int n = nobs[row];
-  es_run<KIND, false>(md, x + row * ld, t0, T, t0, m, season, R, row, ph, err2, n);
-  sse[row] = (float)err2;
-  state[row * 3 + 0] = md.lvl;
-  state[row * 3 + 1] = md.tr;
-  state[row * 3 + 2] = (float)ph;
-  nobs[row] = n;
+  double err2 = sse[sl];
+  int n = nobs[sl];
+  float* srow = KIND >= 2 ? season + sl * m : season;
+  es_run<KIND, false>(md, x + row * ld, t0, T, t0, m, srow, 1, 0, ph, err2, n);
+  sse[sl] = (float)err2;
+  state[sl * 3 + 0] = md.lvl;
+  state[sl * 3 + 1] = md.tr;
+  state[sl * 3 + 2] = (float)ph;
+  nobs[sl] = n;
+  sigma[row] = n > 1 ? sqrtf((float)err2 / (float)(n - 1)) : 0.f;
+  int p = ph;
+  for (int h = 1; h <= H; ++h) {
+    float f = md.lvl + (KIND >= 1 ? h * md.tr : 0.f);
+    if (KIND >= 2) {
+      const float sv = srow[p];
+      f = KIND == 3 ? f * sv : f + sv;
+      if (++p == m) p = 0;
+    }
+    fc[row * H + (h - 1)] = f;
+  }
 }
 
 // Per row: pick the candidate with the smallest SSE and write the H-step
-// forecast + residual sigma (G = 1 for an updated cached model).
+// forecast + residual sigma.
 __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restrict__ sse, const float* __restrict__ state,
                                                           const int* __restrict__ nobs, const float* __restrict__ season,
                                                           int64_t R, int G, int m, int kind, int H,
@@ -276,16 +349,21 @@ __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restric
     else hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, stream, __VA_ARGS__);                    \
   } while (0)
 
+// keep_season = 0: only the seasonal indices the H-step forecast reads are
+// guaranteed in `season` afterwards (saves one store pass); 1: all of them
+// (the caller extracts the fitted state, e.g. for the model cache).
 FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int kind,
                      float* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma, int* best,
-                     hipStream_t stream) {
+                     int keep_season, hipStream_t stream) {
   if (R <= 0) return 0;
   if (kind < 0 || kind > 3) return (int)hipErrorInvalidValue;
   if (kind >= 2 && (m < 2 || 2 * m > T)) return (int)hipErrorInvalidValue;
   if (kind < 2 && T < 2) return (int)hipErrorInvalidValue;
   if (kind < 2) m = 1;
   const int64_t P = R * G;
-  FM_ES_DISPATCH(es_fit_kernel, dim3((unsigned)((P + 255) / 256)), x, ld, T, R, cand, G, m, season, sse, state, nobs);
+  const int t_store_end = keep_season || kind < 2 || H >= m ? T : T - m + H;
+  FM_ES_DISPATCH(es_fit_kernel, dim3((unsigned)((P + 255) / 256)), x, ld, T, R, cand, G, m, season, sse, state, nobs,
+                 t_store_end);
   FM_LAUNCH_CHECK();
   hipLaunchKernelGGL(es_forecast_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, sse, state, nobs,
                      season, R, G, m, kind, H, fc, sigma, best);
@@ -293,18 +371,15 @@ FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* 
   return 0;
 }
 
-FM_API int fm_es_update(const float* x, int64_t ld, int T, int64_t R, const int* t_new, const float* params, int m,
-                        int kind, float* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma,
-                        int* best, hipStream_t stream) {
+FM_API int fm_es_update(const float* x, int64_t ld, int T, int64_t R, const int* t_new, const int64_t* slots,
+                        const float* params, int m, int kind, float* season, float* sse, float* state, int* nobs,
+                        int H, float* fc, float* sigma, hipStream_t stream) {
   if (R <= 0) return 0;
   if (kind < 0 || kind > 3) return (int)hipErrorInvalidValue;
   if (kind >= 2 && m < 2) return (int)hipErrorInvalidValue;
   if (kind < 2) m = 1;
-  const dim3 grid((unsigned)((R + 255) / 256));
-  FM_ES_DISPATCH(es_update_kernel, grid, x, ld, T, R, t_new, params, m, season, sse, state, nobs);
-  FM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(es_forecast_kernel, grid, dim3(256), 0, stream, sse, state, nobs, season, R, 1, m, kind, H, fc,
-                     sigma, best);
+  FM_ES_DISPATCH(es_update_kernel, dim3((unsigned)((R + 255) / 256)), x, ld, T, R, t_new, slots, params, m, season,
+                 sse, state, nobs, H, fc, sigma);
   FM_LAUNCH_CHECK();
   return 0;
 }

@@ -14,9 +14,10 @@ history jumped backwards or by a whole window, or whose fit is older than
 
 Storage is a device-resident slab per (kind, period): ``params [C, 3]``,
 ``state [C, 3]``, ``season [C, m]``, ``sse [C]``, ``nobs [C]`` plus host
-timestamps and use stamps, so a cycle costs one gather and one scatter per
-tensor whatever the number of series; the per-row host work is one dict
-lookup.  Eviction is least-recently-used by stamp (vectorised), bounded by
+timestamps and use stamps.  The update kernel advances the slab in place
+through a row -> slot index and reads only the last k columns of the
+history, so a cycle moves O(rows x k) bytes whatever the period; the per-row
+host work is one dict lookup.  Eviction is least-recently-used by stamp (vectorised), bounded by
 ``capacity`` entries: at m = 1440 an entry is ~5.8 KB of HBM, so the default
 of 100k entries (a full 10k-service x 8-metric shard plus headroom) is
 ~0.6 GB of the 288 GB.  The cache is saved in the brain checkpoint
@@ -81,15 +82,18 @@ class _Slab:
         self.sse[s] = md.sse.to(self.device, torch.float32)
         self.nobs[s] = md.nobs.to(self.device, torch.int32)
         if self.season is not None:
-            self.season[s] = md.season.to(self.device).t()
+            self.season[s] = md.season.to(self.device)
         self.t_last[slots] = t_last
         self.fitted_at[slots] = fitted_at
 
     def read(self, slots) -> "SM.ESState":
         s = torch.as_tensor(np.asarray(slots, np.int64), device=self.device)
         return SM.ESState(self.kind, self.m, self.params[s], self.state[s],
-                          None if self.season is None else self.season[s].t().contiguous(), self.sse[s],
-                          self.nobs[s])
+                          None if self.season is None else self.season[s], self.sse[s], self.nobs[s])
+
+    def as_state(self) -> "SM.ESState":
+        """The whole slab as one ESState (for in-place slot updates)."""
+        return SM.ESState(self.kind, self.m, self.params, self.state, self.season, self.sse, self.nobs)
 
     def live_slots(self) -> np.ndarray:
         return np.array([i for i in range(self.hw) if self.keys[i] is not None], np.int64)
@@ -105,6 +109,8 @@ class ModelCache:
         self.clock = 0                              # use stamp (one tick per forecast call)
         self.hits = 0
         self.misses = 0
+        self._gen = 0            # bumped on every key -> slot change
+        self._memo = None        # (keys list object, gen, resolved slots); keys lists are never mutated
 
     def __len__(self) -> int:
         return len(self.entries)
@@ -114,6 +120,7 @@ class ModelCache:
         return None if g is None else (self.slabs[g >> _SLOT_BITS], g & ((1 << _SLOT_BITS) - 1))
 
     def _drop_slot(self, slab: _Slab, slot: int) -> None:
+        self._gen += 1
         del self.entries[slab.keys[slot]]
         slab.keys[slot] = None
         slab.free.append(slot)
@@ -152,11 +159,11 @@ class ModelCache:
             self._by_kind_m[(kind, m)] = slab
         slots = slab.alloc(len(keep))
         sel = torch.as_tensor(np.asarray(keep, np.int64), device=md.params.device)
-        sub = SM.ESState(kind, m, md.params[sel], md.state[sel], None if md.season is None else md.season[:, sel],
-                         md.sse[sel], md.nobs[sel])
+        sub = md.rows(sel)
         slab.write(slots, sub, np.asarray(t_last, np.float64)[keep], np.asarray(fitted_at, np.float64)[keep])
         slab.stamp[slots] = self.clock
         base = slab.sid << _SLOT_BITS
+        self._gen += 1
         for j, slot in zip(keep, slots):
             slab.keys[slot] = keys[j]
             self.entries[keys[j]] = base | slot
@@ -173,13 +180,20 @@ class ModelCache:
         t_last = np.asarray(t_last, np.float64)
         fc = torch.empty((R, H), dtype=torch.float32, device=dev)
         sig = torch.empty((R,), dtype=torch.float32, device=dev)
-        g = np.fromiter((-1 if v is None else v for v in map(self.entries.get, keys)), np.int64, R)
-        if len(set(keys)) != R:                    # a key seen twice in one batch is fitted, not advanced twice
-            seen: set = set()
-            for i, key in enumerate(keys):
-                if key in seen:
-                    g[i] = -1
-                seen.add(key)
+        memo = self._memo
+        if memo is not None and memo[0] is keys and memo[1] == self._gen:
+            # same batch object and no key -> slot change since: a steady-state
+            # shard re-scoring its series skips the per-row lookups
+            g = memo[2].copy()
+        else:
+            g = np.fromiter((-1 if v is None else v for v in map(self.entries.get, keys)), np.int64, R)
+            if len(set(keys)) != R:                # a key seen twice in one batch is fitted, not advanced twice
+                seen: set = set()
+                for i, key in enumerate(keys):
+                    if key in seen:
+                        g[i] = -1
+                    seen.add(key)
+            self._memo = (keys, self._gen, g.copy())
         sid = np.where(g >= 0, g >> _SLOT_BITS, -1)
         slot = g & ((1 << _SLOT_BITS) - 1)
         usable = np.zeros(R, bool)
@@ -204,13 +218,22 @@ class ModelCache:
             if not len(rows):
                 continue
             sl = slot[rows]
-            idx = torch.as_tensor(rows, device=dev)
-            t_new = torch.as_tensor((T - knew[rows]).astype(np.int32))
-            f, s, new = SM.es_update(hist.index_select(0, idx).contiguous(), T, t_new, slab.read(sl), H)
-            fc[idx], sig[idx] = f, s
-            slab.write(sl, new, t_last[rows], slab.fitted_at[sl])
+            # only the last kmax columns are read: select rows of that view
+            kmax = max(int(knew[rows].max()), 1)
+            tail = hist[:, T - kmax:T]
+            full = len(rows) == R
+            x = tail if full else tail.index_select(0, torch.as_tensor(rows, device=dev))
+            t_new = torch.as_tensor((kmax - knew[rows]).astype(np.int32))
+            slots_t = torch.as_tensor(sl, device=slab.device)
+            f, s, _ = SM.es_update(x, kmax, t_new, slab.as_state(), H, slots=slots_t)
+            if full:
+                fc, sig = f, s
+            else:
+                idx = torch.as_tensor(rows, device=dev)
+                fc[idx], sig[idx] = f, s
+            slab.t_last[sl] = t_last[rows]
             slab.stamp[sl] = self.clock
-            dead = ~torch.isfinite(new.state[:, :2]).all(1).cpu().numpy()
+            dead = ~torch.isfinite(slab.state[slots_t, :2]).all(1).cpu().numpy()
             for j in np.nonzero(dead)[0]:
                 self._drop_slot(slab, int(sl[j]))
         if len(miss):
@@ -248,6 +271,7 @@ class ModelCache:
         self.entries.clear()
         self.slabs.clear()
         self._by_kind_m.clear()
+        self._gen += 1
         for gi, g in enumerate(meta):
             p = f"{prefix}{gi}."
             kind, m = int(g["kind"]), int(g["m"])

@@ -34,15 +34,18 @@ class ESState:
     m: int
     params: torch.Tensor            # [R, 3] alpha, beta, gamma
     state: torch.Tensor             # [R, 3] level, trend, phase of the next sample
-    season: torch.Tensor | None     # [m, R] seasonal indices (kind >= 2)
+    season: torch.Tensor | None     # [R, m] seasonal indices by absolute phase (kind >= 2)
     sse: torch.Tensor               # [R] one-step SSE so far
     nobs: torch.Tensor              # [R] int32 observations so far
 
     def rows(self, idx: torch.Tensor) -> "ESState":
         idx = idx.to(self.params.device)
         return ESState(self.kind, self.m, self.params[idx], self.state[idx],
-                       None if self.season is None else self.season[:, idx].contiguous(), self.sse[idx],
-                       self.nobs[idx])
+                       None if self.season is None else self.season[idx], self.sse[idx], self.nobs[idx])
+
+    def clone(self) -> "ESState":
+        c = lambda t: None if t is None else t.clone()
+        return ESState(self.kind, self.m, c(self.params), c(self.state), c(self.season), c(self.sse), c(self.nobs))
 
 
 @dataclass
@@ -73,7 +76,7 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
         model = None
         if keep_state:
             model = ESState(kind, m, *(torch.from_numpy(np.ascontiguousarray(v)) for v in (
-                grid[best], st["state"], st["season"].T if kind >= 2 else np.zeros((0,)), st["sse"], st["nobs"])))
+                grid[best], st["state"], st["season"] if kind >= 2 else np.zeros((0,)), st["sse"], st["nobs"])))
             if kind < 2:
                 model.season = None
         return ESFit(torch.from_numpy(fc), torch.from_numpy(sig), torch.from_numpy(best), torch.from_numpy(sse), model)
@@ -89,46 +92,55 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     sig = torch.empty((R,), dtype=torch.float32, device=d)
     best = torch.empty((R,), dtype=torch.int32, device=d)
     LIB.call("fm_es_fit", ptr(x), x.stride(0), T, R, ptr(cand), G, m, kind, ptr(season), ptr(sse), ptr(state),
-             ptr(nobs), H, ptr(fc), ptr(sig), ptr(best), stream_of(x))
+             ptr(nobs), H, ptr(fc), ptr(sig), ptr(best), int(keep_state), stream_of(x))
     model = None
     if keep_state:
         b = best.long()
         pid = torch.arange(R, device=d) * G + b
         model = ESState(kind, m, cand[b].contiguous(), state[pid].contiguous(),
-                        season[:, pid].contiguous() if kind >= 2 else None,
+                        season[:, pid].t().contiguous() if kind >= 2 else None,
                         sse.gather(1, b[:, None])[:, 0].contiguous(), nobs[pid].contiguous())
     return ESFit(fc, sig, best, sse, model)
 
 
-def es_update(x: torch.Tensor, T: int, t_new: torch.Tensor, model: ESState, H: int) -> tuple:
-    """Advance cached fitted models over their new samples ``x[r, t_new[r]:T]``
+def es_update(x: torch.Tensor, T: int, t_new: torch.Tensor, model: ESState, H: int,
+              slots: torch.Tensor | None = None) -> tuple:
+    """Advance fitted models over their new samples ``x[r, t_new[r]:T]``
     (same recursion as the fit, parameters kept) and forecast H steps.
-    Returns (forecast [R, H], sigma [R], updated ESState)."""
+
+    Without ``slots`` row r of ``x`` advances row r of a copy of ``model``.
+    With ``slots`` (int64 [R]) ``model`` is a slab of C >= R models updated
+    IN PLACE: row r advances slot ``slots[r]`` (the model cache's layout).
+    Returns (forecast [R, H], sigma [R], the updated ESState)."""
     check(x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1, "x must be [R, T] float32")
     R = x.shape[0]
-    check(model.params.shape[0] == R and t_new.shape[0] == R, "one cached model and one t_new per row")
+    check(t_new.shape[0] == R, "one t_new per row")
+    check(slots is not None or model.params.shape[0] == R, "one cached model per row")
     kind, m = model.kind, model.m
+    new = model if slots is not None else model.clone()
     if not x.is_cuda:
-        st = {"state": model.state.numpy().copy(), "season": None if model.season is None else
-              model.season.numpy().T.copy(), "sse": model.sse.numpy().astype(np.float64), "nobs":
-              model.nobs.numpy().astype(np.int64)}
-        fc, sig = ref_es_update(x.numpy()[:, :T], t_new.numpy(), kind, m, model.params.numpy(), st, H)
-        new = ESState(kind, m, model.params, torch.from_numpy(st["state"]),
-                      None if st["season"] is None else torch.from_numpy(np.ascontiguousarray(st["season"].T)),
-                      torch.from_numpy(st["sse"].astype(np.float32)), torch.from_numpy(st["nobs"].astype(np.int32)))
+        sl = np.arange(R) if slots is None else slots.cpu().numpy()
+        st = {"state": new.state.numpy()[sl].copy(), "season": None if new.season is None else
+              new.season.numpy()[sl].copy(), "sse": new.sse.numpy()[sl].astype(np.float64),
+              "nobs": new.nobs.numpy()[sl].astype(np.int64)}
+        fc, sig = ref_es_update(x.numpy()[:, :T], t_new.numpy(), kind, m, new.params.numpy()[sl], st, H)
+        new.state[sl] = torch.from_numpy(st["state"])
+        if new.season is not None:
+            new.season[sl] = torch.from_numpy(st["season"])
+        new.sse[sl] = torch.from_numpy(st["sse"].astype(np.float32))
+        new.nobs[sl] = torch.from_numpy(st["nobs"].astype(np.int32))
         return torch.from_numpy(fc), torch.from_numpy(sig), new
     require_native(x)
     d = x.device
-    new = ESState(kind, m, model.params.to(d).contiguous(), model.state.to(d).clone(),
-                  None if model.season is None else model.season.to(d).clone(), model.sse.to(d).clone(),
-                  model.nobs.to(d).clone())
+    for t in (new.params, new.state, new.sse, new.nobs) + ((new.season,) if new.season is not None else ()):
+        check(t.device == d and t.is_contiguous(), "model tensors must be contiguous on the device of x")
     tn = t_new.to(device=d, dtype=torch.int32).contiguous()
+    sl = None if slots is None else slots.to(device=d, dtype=torch.int64).contiguous()
     fc = torch.empty((R, H), dtype=torch.float32, device=d)
     sig = torch.empty((R,), dtype=torch.float32, device=d)
-    best = torch.empty((R,), dtype=torch.int32, device=d)
     season = new.season if new.season is not None else torch.empty((1,), dtype=torch.float32, device=d)
-    LIB.call("fm_es_update", ptr(x), x.stride(0), T, R, ptr(tn), ptr(new.params), m, kind, ptr(season),
-             ptr(new.sse), ptr(new.state), ptr(new.nobs), H, ptr(fc), ptr(sig), ptr(best), stream_of(x))
+    LIB.call("fm_es_update", ptr(x), x.stride(0), T, R, ptr(tn), 0 if sl is None else ptr(sl), ptr(new.params), m,
+             kind, ptr(season), ptr(new.sse), ptr(new.state), ptr(new.nobs), H, ptr(fc), ptr(sig), stream_of(x))
     return fc, sig, new
 
 

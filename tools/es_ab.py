@@ -25,6 +25,7 @@ sig = torch.empty((R,), device=dev)
 best = torch.empty((R,), dtype=torch.int32, device=dev)
 args = [ptr(hist), hist.stride(0), T, R, ptr(grid), G, m, 2, ptr(season), ptr(sse), ptr(state), ptr(nobs), H,
         ptr(fc), ptr(sig), ptr(best), stream_of(hist)]
+args_tree = args[:-1] + [0, args[-1]]      # in-tree API has keep_season before the stream
 def load(path):
     lib = ctypes.CDLL(path)
     lib.fm_es_fit.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
@@ -33,7 +34,7 @@ def load(path):
     return lambda: lib.fm_es_fit(*args)
 
 
-runs = [("tree", lambda: LIB.call("fm_es_fit", *args))] + [(p.rsplit("/", 1)[-1], load(p)) for p in sys.argv[1:]]
+runs = [("tree", lambda: LIB.call("fm_es_fit", *args_tree))] + [(p.rsplit("/", 1)[-1], load(p)) for p in sys.argv[1:]]
 out = {}
 for rep in range(2):
     for name, fn in runs:
