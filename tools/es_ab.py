@@ -27,11 +27,14 @@ args = [ptr(hist), hist.stride(0), T, R, ptr(grid), G, m, 2, ptr(season), ptr(ss
         ptr(fc), ptr(sig), ptr(best), stream_of(hist)]
 args_tree = args[:-1] + [0, args[-1]]      # in-tree API has keep_season before the stream
 def load(path):
+    """Libraries named *old* have the pre-keep_season signature."""
     lib = ctypes.CDLL(path)
+    legacy = "old" in path.rsplit("/", 1)[-1]
     lib.fm_es_fit.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
                               ctypes.c_int, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + \
-                             [ctypes.c_void_p] * 4
-    return lambda: lib.fm_es_fit(*args)
+                             [ctypes.c_void_p] * 3 + ([] if legacy else [ctypes.c_int]) + [ctypes.c_void_p]
+    a = args if legacy else args_tree
+    return lambda: lib.fm_es_fit(*a)
 
 
 runs = [("tree", lambda: LIB.call("fm_es_fit", *args_tree))] + [(p.rsplit("/", 1)[-1], load(p)) for p in sys.argv[1:]]
