@@ -9,6 +9,10 @@ is the root ``bench.py``).
   --config 2  4-metric (error%, TPS, p99, 4xx) Holt-Winters baseline anomaly
               (FFT period detection K3 + grid-searched HW fit K2 + band
               decision) over the 7-day history, 1 MI355X
+  --config 3  the headline tick (``bench.py``) on the CPU reference path
+              (``--device cpu``: numpy/fp64 oracles of every kernel, the
+              comparison point BASELINE.md promises); ``--device cuda``
+              runs the same single-rank tick through the GPU scorer
   --config 4  LSTM forecaster for HPA / ClusterAutoScaler prediction, bf16
               MFMA recurrence (K6) + head + band decision, data-parallel
   --config 5  downstream-impact aggregation across 4 synthetic clusters:
@@ -173,6 +177,34 @@ def config2(args):
             "synthetic on-device Prometheus-shaped fleet (K11)", extra)
 
 
+# --------------------------------------------------------------------------- config 3
+def config3(args):
+    from foremast_amd.engine.scorer import CanaryScorer
+    info, dev = setup(gpus_required=args.device != "cpu")
+    dev = torch.device("cpu") if args.device == "cpu" else dev
+    S, M = args.services, args.metrics
+    svc0, _, pad = D.shard_range(S, info.rank, info.world)
+    hist, base, cur = C.synth_fleet(pad, M, T_HIST, args.pods, args.window, svc0, device=dev)
+    cfg = BrainConfig()
+    cfg.min_historical_points = 10
+    aliases = (["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"] * 4)[:M]
+    scorer = CanaryScorer(aliases, cfg, device=dev)
+    tick = (lambda: scorer.score(hist, base, cur, T_HIST)) if dev.type == "cpu" else scorer.capture(hist, base, cur,
+                                                                                                    T_HIST)
+
+    def step():
+        o = tick()
+        o.packed.cpu()
+
+    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    _common(args, info, ms, p50, "metric windows scored/sec (node) + p50 decision latency, 10k-service canary"
+            + (" [CPU reference path]" if dev.type == "cpu" else ""), S * M / (ms / 1e3), "windows/s",
+            "foremast-brain canary: moving_average_all + pairwise ALL(MW,Wilcoxon,Kruskal,KS,Welch-t,Friedman)",
+            S * M, T_HIST, "strong", "fp32" if dev.type != "cpu" else "fp32 data / fp64 statistics",
+            "synthetic (Prometheus-shaped fleet, K11; 2% injected faults)",
+            {"services": S, "metrics": M, "device": str(dev), "torch_threads": torch.get_num_threads()})
+
+
 # --------------------------------------------------------------------------- config 4
 def config4(args):
     from foremast_amd.models.lstm import LSTMForecaster
@@ -244,11 +276,11 @@ def config5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5])
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--device", default="cuda", help="config 1 only: cpu (reference path) or cuda")
+    ap.add_argument("--device", default="cuda", help="configs 1 and 3: cpu (reference path) or cuda")
     ap.add_argument("--jobs", type=int, default=200)
     ap.add_argument("--services", type=int, default=10000)
     ap.add_argument("--metrics", type=int, default=8)
@@ -263,7 +295,7 @@ def main():
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "
                     "the fitted-model cache")
     args = ap.parse_args()
-    {1: config1, 2: config2, 4: config4, 5: config5}[args.config](args)
+    {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}[args.config](args)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,8 @@ run c1 300 python3 "$R/benchmarks/bench_configs.py" --config 1 --device cuda --j
 run c1cpu 300 python3 "$R/benchmarks/bench_configs.py" --config 1 --device cpu --jobs 200 --steps 5 --warmup 1 &&
 run c2 200 python3 "$R/benchmarks/bench_configs.py" --config 2 &&
 run c2fft 200 python3 "$R/benchmarks/bench_configs.py" --config 2 --detect-period &&
+run c2cached 200 python3 "$R/benchmarks/bench_configs.py" --config 2 --cached &&
+run c3cpu 600 python3 "$R/benchmarks/bench_configs.py" --config 3 --device cpu --steps 2 --warmup 1 &&
 run c4 200 python3 "$R/benchmarks/bench_configs.py" --config 4 &&
 run c5 200 python3 "$R/benchmarks/bench_configs.py" --config 5 &&
 cd /tmp && export TMPDIR=/tmp &&
