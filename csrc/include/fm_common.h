@@ -19,7 +19,10 @@
 namespace fm {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (FM_WAVE - 1); }
-__device__ __forceinline__ int wave_id() { return threadIdx.x / FM_WAVE; }
+// Wave index within the workgroup, as a wave-uniform (SGPR) value: rows and
+// addresses derived from it stay scalar instead of being recomputed per lane
+// in 64-bit VALU arithmetic.  Block x-dimensions are multiples of 64.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x / FM_WAVE); }
 
 // ---------------------------------------------------------------------------
 // Cross-lane primitives without the LDS crossbar.  __shfl_xor lowers to

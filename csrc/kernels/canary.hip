@@ -853,7 +853,7 @@ __global__ __launch_bounds__(256) void stats_decide_kernel(
   const float* cr = cur + row * ld_c;
   int acnt = 0, ccnt = 0;
   float best = 0.f;
-  const float inv = sd > 0.f ? 1.0f / sd : 0.f;
+  const float inv = sd > 0.f ? __builtin_amdgcn_rcpf(sd) : 0.f;   // z-score scale, 1-ulp rcp
   for (int i0 = 0; i0 < n_cur; i0 += 256) {
     const int i = i0 + tid;
     bool f = false;
@@ -983,7 +983,7 @@ __global__ __launch_bounds__(256) void window_decide_kernel(
   float lo = mf - th * sd;
   if (lo < minlb[m]) lo = minlb[m];
   const bool has_hist = n >= min_hist && n > 0;
-  const float inv = sd > 0.f ? 1.0f / sd : 0.f;
+  const float inv = sd > 0.f ? __builtin_amdgcn_rcpf(sd) : 0.f;   // z-score scale, 1-ulp rcp
   const float* cr = cur + row * ld_c;
   int acnt = 0, ccnt = 0;
   float best = 0.f;
@@ -1037,100 +1037,113 @@ FM_API int fm_window_decide(const float* hs, const float* cur, int64_t ld_c, int
 }
 
 // ---------------------------------------------------------------------------
-// Decision + pairwise combine + service reduce in ONE launch: a workgroup per
-// service, one wave per metric row (M <= 16).  Each wave folds its row's
-// p-values into "distribution differs" (lanes 0..N_TESTS-1 + two ballots),
-// lowers the threshold accordingly, flags the current window against the
-// history band, and the M waves reduce to the packed service verdict through
-// LDS.  Replaces pcombine + window_decide + service_reduce (two kernel
-// boundaries fewer per tick, which is what a small per-GPU shard pays for).
+// Decision + pairwise combine + service reduce in ONE launch: one WAVE per
+// service, looping over its M <= 16 metric rows.  All global loads of the
+// service (current window, p-values) are issued before any arithmetic, so a
+// wave pays one memory latency; with 4 services per workgroup a CU keeps up to
+// 32 services in flight (a workgroup-per-service layout with a wave per metric
+// kept only 4, and the kernel was latency-bound at ~30 us for 10k services).
+// Per row: p-values fold into "distribution differs" (lanes 0..N_TESTS-1 +
+// two ballots), the threshold is lowered accordingly, the current window is
+// flagged against the history band (anomalous / observed counts from ballot
+// popcounts), and the service verdict is reduced in registers.  Replaces
+// pcombine + window_decide + service_reduce.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void decide_service_kernel(
+template <int MAXM>
+__global__ __launch_bounds__(256) void decide_service_kernel(
     const float* __restrict__ hs, const float* __restrict__ cur, int64_t ld_c, int n_cur, int64_t S, int M,
     const float* __restrict__ thr, const int* __restrict__ bound, const float* __restrict__ minlb, float pair_factor,
     const float* __restrict__ pvals, int test_mask, int combine_any, float p_thr, int min_hist,
     float* __restrict__ out_stats, unsigned long long* __restrict__ out_flags, int NW, int* __restrict__ out_count,
     float* __restrict__ out_score, int* __restrict__ out_valid, int8_t* __restrict__ out_diff,
     float* __restrict__ packed) {
-  __shared__ int s_cnt[16], s_valid[16];
-  __shared__ float s_best[16];
-  const int64_t svc = blockIdx.x;
-  const int m = wave_id();
+  const int64_t svc = (int64_t)blockIdx.x * 4 + wave_id();
+  if (svc >= S) return;
   const int lane = lane_id();
-  const int64_t row = svc * M + m;
-  // pairwise combine
-  bool differs = false;
-  if (pvals != nullptr) {
-    const float p = lane < N_TESTS ? pvals[row * N_TESTS + lane] : NAN;
-    const bool sel = lane < N_TESTS && ((test_mask >> lane) & 1) && !isnan(p);
-    const unsigned long long app = __ballot(sel), sig = __ballot(sel && p < p_thr);
-    differs = app != 0ull && (combine_any ? sig != 0ull : sig == app);
-    if (lane == 0 && out_diff != nullptr) out_diff[row] = (int8_t)differs;
+  const float NaNf = __builtin_nanf("");
+  // phase 1: every load of the service up front (clamped, unpredicated)
+  const int li = lane < n_cur ? lane : n_cur - 1;
+  const int lp = lane < N_TESTS ? lane : N_TESTS - 1;
+  float xs[MAXM], pv[MAXM];
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m) {
+    const int64_t row = svc * M + (m < M ? m : M - 1);
+    xs[m] = cur[row * ld_c + li];
+    pv[m] = pvals != nullptr ? pvals[row * N_TESTS + lp] : NaNf;
   }
-  const float mf = hs[row * 3 + 0], sd = hs[row * 3 + 1];
-  const int n = (int)hs[row * 3 + 2];
-  float th = thr[m];
-  if (differs) th *= pair_factor;
-  const int bd = bound[m];
-  const float up = mf + th * sd;
-  float lo = mf - th * sd;
-  if (lo < minlb[m]) lo = minlb[m];
-  const bool has_hist = n >= min_hist && n > 0;
-  const float inv = sd > 0.f ? 1.0f / sd : 0.f;
-  const float* cr = cur + row * ld_c;
-  int acnt = 0, ccnt = 0;
-  float best = 0.f;
-  for (int i0 = 0; i0 < n_cur; i0 += 64) {
-    const int i = i0 + lane;
-    bool f = false;
-    if (i < n_cur) {
-      const float x = cr[i];
-      if (isfinite(x)) {
-        ++ccnt;
-        if (has_hist) {
-          const bool hi = (bd & 1) && x > up;
-          const bool lw = (bd & 2) && x < lo;
-          f = hi || lw;
-          if (f) {
-            ++acnt;
-            const float z = sd > 0.f ? (hi ? x - up : lo - x) * inv : 1e30f;
-            best = z > best ? z : best;
-          }
-        }
-      }
+  // the service's [M, 3] history stats (3M <= 48 floats) as one vector
+  // load, lane j holding element j, broadcast per metric with readlane
+  const int nh = 3 * M;
+  const float hsv = hs[svc * nh + (lane < nh ? lane : nh - 1)];
+  int tot = 0, mask = 0;
+  bool unknown = false;
+  float bestm[MAXM];
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m) {
+    bestm[m] = 0.f;
+    if (m >= M) continue;
+    const int64_t row = svc * M + m;
+    bool differs = false;
+    if (pvals != nullptr) {
+      const bool sel = lane < N_TESTS && ((test_mask >> lane) & 1) && !isnan(pv[m]);
+      const unsigned long long app = __ballot(sel), sig = __ballot(sel && pv[m] < p_thr);
+      differs = app != 0ull && (combine_any ? sig != 0ull : sig == app);
     }
-    const unsigned long long bal = __ballot(f);
-    if (lane == 0 && i0 / 64 < NW) out_flags[row * NW + i0 / 64] = bal;
+    const float mf = lane_bcast(hsv, 3 * m);
+    const float sd = lane_bcast(hsv, 3 * m + 1);
+    const int n = (int)lane_bcast(hsv, 3 * m + 2);
+    float th = thr[m];
+    if (differs) th *= pair_factor;
+    const int bd = bound[m];
+    const float up = mf + th * sd;
+    float lo = mf - th * sd;
+    if (lo < minlb[m]) lo = minlb[m];
+    const bool has_hist = n >= min_hist && n > 0;
+    const float inv = sd > 0.f ? __builtin_amdgcn_rcpf(sd) : 0.f;   // z-score scale, 1-ulp rcp
+    int acnt = 0, ccnt = 0;
+    float best = 0.f;
+    for (int i0 = 0; i0 < n_cur; i0 += 64) {
+      const int i = i0 + lane;
+      const float x = i0 == 0 ? xs[m] : cur[row * ld_c + (i < n_cur ? i : n_cur - 1)];
+      const bool obs = i < n_cur && isfinite(x);
+      const bool hi = has_hist && obs && (bd & 1) && x > up;
+      const bool lw = has_hist && obs && (bd & 2) && x < lo;
+      const bool f = hi || lw;
+      const float z = sd > 0.f ? (hi ? x - up : lo - x) * inv : 1e30f;
+      best = f && z > best ? z : best;
+      const unsigned long long bal = __ballot(f);
+      acnt += __popcll(bal);
+      ccnt += __popcll(__ballot(obs));
+      if (lane == 0 && i0 / 64 < NW) out_flags[row * NW + i0 / 64] = bal;
+    }
+    bestm[m] = best;
+    const int valid = (has_hist ? 1 : 0) | (ccnt > 0 ? 2 : 0);
+    if (lane == 0) {
+      if (out_diff != nullptr && pvals != nullptr) out_diff[row] = (int8_t)differs;
+      out_stats[row * 4 + 0] = mf;
+      out_stats[row * 4 + 1] = sd;
+      out_stats[row * 4 + 2] = up;
+      out_stats[row * 4 + 3] = lo;
+      out_count[row] = acnt;
+      out_valid[row] = valid;
+    }
+    tot += acnt;
+    if (acnt > 0) mask |= 1 << m;
+    if ((valid & 3) != 3) unknown = true;
   }
-  acnt = wave_sum(acnt);
-  ccnt = wave_sum(ccnt);
-  best = wave_max(best);
-  const int valid = (has_hist ? 1 : 0) | (ccnt > 0 ? 2 : 0);
+  // the M max-reductions are independent: issued together they overlap
+  float sbest = 0.f;
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m) bestm[m] = wave_max(bestm[m]);
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m) {
+    if (m >= M) break;
+    if (lane == 0) out_score[svc * M + m] = bestm[m];
+    sbest = bestm[m] > sbest ? bestm[m] : sbest;
+  }
   if (lane == 0) {
-    out_stats[row * 4 + 0] = mf;
-    out_stats[row * 4 + 1] = sd;
-    out_stats[row * 4 + 2] = up;
-    out_stats[row * 4 + 3] = lo;
-    out_count[row] = acnt;
-    out_score[row] = best;
-    out_valid[row] = valid;
-    s_cnt[m] = acnt;
-    s_valid[m] = valid;
-    s_best[m] = best;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int tot = 0, mask = 0;
-    bool unknown = false;
-    float b = 0.f;
-    for (int k = 0; k < M; ++k) {
-      tot += s_cnt[k];
-      if (s_cnt[k] > 0) mask |= 1 << k;
-      if ((s_valid[k] & 3) != 3) unknown = true;
-      b = s_best[k] > b ? s_best[k] : b;
-    }
     packed[svc * 4 + 0] = (float)(tot > 0 ? 1 : (unknown ? 2 : 0));
-    packed[svc * 4 + 1] = b;
+    packed[svc * 4 + 1] = sbest;
     packed[svc * 4 + 2] = (float)mask;
     packed[svc * 4 + 3] = (float)tot;
   }
@@ -1143,10 +1156,15 @@ FM_API int fm_decide_services(const float* hs, const float* cur, int64_t ld_c, i
                               float* out_score, int* out_valid, int8_t* out_diff, float* packed,
                               hipStream_t stream) {
   if (S <= 0) return 0;
-  if (M < 1 || M > 16 || NW * 64 < n_cur) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(decide_service_kernel, dim3((unsigned)S), dim3(64 * M), 0, stream, hs, cur, ld_c, n_cur, S, M,
-                     thr, bound, minlb, pair_factor, pvals, test_mask, combine_any, p_thr, min_hist, out_stats,
-                     out_flags, NW, out_count, out_score, out_valid, out_diff, packed);
+  if (M < 1 || M > 16 || n_cur < 1 || NW * 64 < n_cur) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((S + 3) / 4)), block(256);
+#define FM_DS(MM)                                                                                                     \
+  hipLaunchKernelGGL(decide_service_kernel<MM>, grid, block, 0, stream, hs, cur, ld_c, n_cur, S, M, thr, bound,       \
+                     minlb, pair_factor, pvals, test_mask, combine_any, p_thr, min_hist, out_stats, out_flags, NW,     \
+                     out_count, out_score, out_valid, out_diff, packed)
+  if (M <= 8) FM_DS(8);
+  else FM_DS(16);
+#undef FM_DS
   FM_LAUNCH_CHECK();
   return 0;
 }
