@@ -11,7 +11,10 @@ One step = one full brain judgement cycle for the whole fleet:
 
 Metric: metric windows scored per second for the whole node (services x metrics
 / step time; strong scaling: the 10k-service fleet is fixed and sharded over
-ranks) and the p50 decision latency (median step time).
+ranks) and the p50 decision latency (GPU time from the start of a tick to the
+fleet verdict in rank 0's host memory).  Ticks are issued up to --pipeline
+steps ahead on one stream (default 2) so the GPU does not idle through the
+host's wake-up and graph launch; every step completes inside the timed region.
 
 Data: synthetic Prometheus-shaped series generated on device (K11), the model
 is the deployed default (no learned weights).  Reference publishes no number
@@ -34,6 +37,7 @@ import torch
 from foremast_amd.config import BrainConfig
 from foremast_amd.engine.scorer import CanaryScorer
 from foremast_amd.ops import canary as C
+from foremast_amd.ops._lib import LIB, stream_of
 from foremast_amd.parallel import dist as D
 
 ALIASES = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
@@ -50,8 +54,13 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=5)
     ap.add_argument("--window", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--mode", choices=["fused", "overlap", "serial"], default="overlap",
-                    help="tick structure: two-stream fork/join (default), fused row kernel, or serial")
+    ap.add_argument("--graph-scope", choices=["step", "tick"], default="step",
+                    help="capture the whole step (tick + all-gather + host copy) or only the tick kernels")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="steps in flight (1 = host waits for each verdict before launching the next tick)")
+    ap.add_argument("--mode", choices=["front", "fused", "overlap", "serial"], default="front",
+                    help="tick structure: role-split front kernel (default), fused row kernel, two-stream "
+                         "fork/join, or serial")
     ap.add_argument("--no-overlap", action="store_true", help="alias of --mode serial")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace of 5 extra steps (rank 0)")
     args = ap.parse_args()
@@ -75,40 +84,80 @@ def main() -> None:
     cfg.min_historical_points = 10
     mode = "serial" if args.no_overlap else args.mode
     scorer = CanaryScorer(aliases, cfg, device=dev, mode=mode)
+    depth = max(1, args.pipeline)
     gathered = torch.empty((world * s_pad, 4), dtype=torch.float32, device=dev)
-    host = torch.empty((world * s_pad, 4), dtype=torch.float32, pin_memory=True)
+    # one pinned host verdict buffer per in-flight step (the host reads step
+    # k's verdict while step k+1 may already be copying its own)
+    hosts = [torch.empty((world * s_pad, 4), dtype=torch.float32, pin_memory=True) for _ in range(depth)]
 
+    def publisher(host):
+        def publish(o):
+            """all-gather of the packed verdicts (RCCL over xGMI) + rank 0's
+            copy of the fleet verdict to pinned host memory, on the current
+            stream."""
+            g = D.all_gather_rows(o.packed, gathered)
+            if info.is_main:
+                LIB.call("fm_copy_d2h_async", host.data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
+        return publish
+
+    whole = "tick"
+    launches = []
     if args.no_graph:
-        def tick():
-            return scorer.score(hist, base, cur, args.hist)
+        launches = [lambda h=h: publisher(h)(scorer.score(hist, base, cur, args.hist)) for h in hosts]
     else:
-        tick = scorer.capture(hist, base, cur, args.hist)
+        if args.graph_scope == "step":
+            # the whole step (tick kernels, all-gather, host copy) is ONE graph
+            # launch; RCCL collectives are graph-capturable after a warm-up
+            try:
+                launches = [scorer.capture(hist, base, cur, args.hist, epilogue=publisher(h)) for h in hosts]
+                whole = "step"
+            except Exception as e:  # noqa: BLE001 - fall back to an eager collective
+                if info.is_main:
+                    print(f"bench: step capture failed ({e!r}); collective outside the graph", file=sys.stderr)
+                torch.cuda.synchronize(dev)
+                D.barrier()
+                launches = []
+        if not launches:
+            tick = scorer.capture(hist, base, cur, args.hist)
+            launches = [lambda h=h: publisher(h)(tick()) for h in hosts]
 
-    def step():
-        o = tick()
-        g = D.all_gather_rows(o.packed, gathered)
-        if info.is_main:
-            host.copy_(g, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
+    # Steps are issued up to `depth` ahead: step k+1 is queued behind step k
+    # on the same stream (shared intermediates are safe: one stream), so the
+    # GPU runs ticks back to back instead of idling through the host's
+    # wake-up + graph launch.  Every step is complete (verdict in pinned host
+    # memory, event observed) before the timed region closes.
+    stream = torch.cuda.current_stream(dev)
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(depth)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(depth)]
+    lat: list[float] = []
 
-    for _ in range(args.warmup):
-        step()
+    def run(n: int, record: bool) -> None:
+        for k in range(n + depth):
+            slot = k % depth
+            if k >= depth:                       # retire step k - depth
+                ev1[slot].synchronize()
+                if record:
+                    lat.append(ev0[slot].elapsed_time(ev1[slot]))
+            if k < n:
+                ev0[slot].record(stream)
+                launches[slot]()
+                ev1[slot].record(stream)
+
+    run(args.warmup, False)
     D.barrier()
     torch.cuda.synchronize(dev)
-    lat = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ts = time.perf_counter()
-        step()
-        lat.append(time.perf_counter() - ts)
+    run(args.steps, True)
     torch.cuda.synchronize(dev)
     D.barrier()
     t1 = time.perf_counter()
     elapsed = D.all_reduce_max(t1 - t0, dev)
-    p50 = D.all_reduce_max(statistics.median(lat), dev)
+    # decision latency: GPU time from the start of a tick to its fleet verdict
+    # in host memory (event-timed, excludes queueing behind the previous step)
+    p50 = D.all_reduce_max(statistics.median(lat) / 1e3, dev)
     ms = elapsed / args.steps * 1e3
     windows = S * M
-    verdict = host[:S].numpy() if info.is_main else None
+    verdict = hosts[(args.steps - 1) % depth][:S].numpy() if info.is_main else None
     if info.is_main:
         n_anom = int((verdict[:, 0] == 1).sum())
         out = {
@@ -135,6 +184,8 @@ def main() -> None:
                 "parallelism": f"dp{world}",
                 "hip_graph": not args.no_graph,
                 "tick_mode": mode,
+                "graph_scope": whole if not args.no_graph else "none",
+                "pipeline_depth": depth,
             },
             "services_flagged": n_anom,
         }
@@ -148,7 +199,7 @@ def main() -> None:
             else contextlib.nullcontext()
         with ctx as prof:
             for _ in range(5):
-                step()
+                run(1, False)
         if info.is_main:
             prof.export_chrome_trace(args.trace)
     if D.is_dist():

@@ -548,8 +548,8 @@ __device__ __forceinline__ void eval_test(int t, const double* __restrict__ o, i
   const double m1 = o[8], m2 = o[9], q1 = o[10], q2 = o[11];
   const int n = n1 + n2;
   const double NaN = __builtin_nan("");
-  double p[N_TESTS], st[N_TESTS];
-  p[t] = NaN; st[t] = NaN;
+  pv = NaN;
+  sv = NaN;
   const double dn1 = n1, dn2 = n2, dn = n;
   switch (t) {
     case T_MW:
@@ -559,13 +559,13 @@ __device__ __forceinline__ void eval_test(int t, const double* __restrict__ o, i
         const double u = u1 > u2 ? u1 : u2;
         const double mu = dn1 * dn2 / 2.0;
         const double var = dn1 * dn2 / 12.0 * ((dn + 1.0) - tie / (dn * (dn - 1.0)));
-        st[T_MW] = u1;
+        sv = u1;
         if (var > 0) {
           const double z = (u - mu - 0.5) / sqrt(var);
           double pp = 2.0 * norm_sf(z);
-          p[T_MW] = pp > 1.0 ? 1.0 : pp;
+          pv = pp > 1.0 ? 1.0 : pp;
         } else {
-          p[T_MW] = 1.0;
+          pv = 1.0;
         }
       }
       break;
@@ -575,16 +575,16 @@ __device__ __forceinline__ void eval_test(int t, const double* __restrict__ o, i
         double h = 12.0 / (dn * (dn + 1.0)) * (r1 * r1 / dn1 + r2 * r2 / dn2) - 3.0 * (dn + 1.0);
         const double corr = 1.0 - tie / (dn * dn * dn - dn);
         if (corr > 0) {
-          st[T_KRU] = h / corr;
-          p[T_KRU] = h / corr > 0 ? erfc(sqrt(0.5 * h / corr)) : 1.0;   // chi2(1) survival
+          sv = h / corr;
+          pv = h / corr > 0 ? erfc(sqrt(0.5 * h / corr)) : 1.0;   // chi2(1) survival
         }
       }
       break;
     case T_KS:
       if (n1 >= min_mw && n2 >= min_mw && n1 > 0 && n2 > 0) {
         const double en_ = dn1 * dn2 / (dn1 + dn2);
-        st[T_KS] = dmax;
-        p[T_KS] = kolmogorov_sf(sqrt(en_) * dmax);
+        sv = dmax;
+        pv = kolmogorov_sf(sqrt(en_) * dmax);
       }
       break;
     case T_T:
@@ -595,8 +595,8 @@ __device__ __forceinline__ void eval_test(int t, const double* __restrict__ o, i
           const double tt = (m1 - m2) / sqrt(se2);
           const double a = v1 / dn1, bb = v2 / dn2;
           const double df = se2 * se2 / (a * a / (dn1 - 1.0) + bb * bb / (dn2 - 1.0));
-          st[T_T] = tt;
-          p[T_T] = student_t_2sided(tt, df);
+          sv = tt;
+          pv = student_t_2sided(tt, df);
         }
       }
       break;
@@ -608,10 +608,10 @@ __device__ __forceinline__ void eval_test(int t, const double* __restrict__ o, i
         const double T = rplus < rminus ? rplus : rminus;
         const double mn = dnw * (dnw + 1.0) / 4.0;
         const double se = sqrt(dnw * (dnw + 1.0) * (2.0 * dnw + 1.0) / 24.0 - tiew / 48.0);
-        st[T_WIL] = T;
+        sv = T;
         if (se > 0) {
           double pp = 2.0 * norm_sf(fabs((T - mn) / se));
-          p[T_WIL] = pp > 1.0 ? 1.0 : pp;
+          pv = pp > 1.0 ? 1.0 : pp;
         }
       }
       break;
@@ -620,20 +620,18 @@ __device__ __forceinline__ void eval_test(int t, const double* __restrict__ o, i
       const int nneg = nw - npos, b = nw + nzero;
       if (b >= min_wil && b > 0) {
         const double q = nw > 0 ? (double)(npos - nneg) * (npos - nneg) / nw : 0.0;
-        st[T_FRI] = q;
-        p[T_FRI] = q > 0 ? erfc(sqrt(0.5 * q)) : 1.0;
+        sv = q;
+        pv = q > 0 ? erfc(sqrt(0.5 * q)) : 1.0;
       }
     }
   }
-  pv = p[t];
-  sv = st[t];
 }
 
 __global__ __launch_bounds__(256) void pvalue_kernel(const double* __restrict__ suff, int64_t R, int min_mw,
                                                      int min_wil, int min_kru, float* __restrict__ pvals,
-                                                     float* __restrict__ stats) {
+                                                     float* __restrict__ stats, int t0 = 0) {
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int t = blockIdx.y;
+  const int t = blockIdx.y + t0;
   if (row >= R) return;
   double pv, sv;
   eval_test(t, suff + row * kSuff, min_mw, min_wil, min_kru, pv, sv);
@@ -662,7 +660,7 @@ static int launch_pvalues(const double* suff, int64_t R, int test_mask, int comb
                           int min_wil, int min_kru, float* pvals, float* stats, int8_t* diff, hipStream_t stream) {
   const unsigned nb = (unsigned)((R + 255) / 256);
   hipLaunchKernelGGL(pvalue_kernel, dim3(nb, N_TESTS), dim3(256), 0, stream, suff, R, min_mw, min_wil, min_kru, pvals,
-                     stats);
+                     stats, 0);
   FM_LAUNCH_CHECK();
   hipLaunchKernelGGL(pcombine_kernel, dim3(nb), dim3(256), 0, stream, pvals, R, test_mask, combine_any, p_thr, diff);
   FM_LAUNCH_CHECK();
@@ -964,6 +962,115 @@ FM_API int fm_hist_stats(const float* hist, int64_t ld_h, int T, int64_t R, floa
   return fm_hist_stats_capped(hist, ld_h, T, R, out, 0, stream);
 }
 
+// ---------------------------------------------------------------------------
+// Horizontally fused front half of the canary tick: ONE launch whose
+// workgroups take one of two roles by blockIdx.
+//   * blockIdx <  nP: pairwise role — grid-stride over rows, one wave per row
+//     (sorted-rank sufficient statistics), then the workgroup evaluates the
+//     six p-values of its own rows, one (test, row) pair per thread,
+//     test-major so a wave mostly runs one special function;
+//   * blockIdx >= nP: history role — mean / std / count of a 7-day row per
+//     workgroup (HBM-bound, grid-stride over rows).
+// The compute-bound and the HBM-bound halves share every CU without a
+// second stream: no fork/join in the graph (the side branch of a two-stream
+// graph starts ~11-13 us late, and whether the branches land on different
+// hardware queues varied run to run: profiles/tick_timeline_*.txt).  The
+// pairwise workgroups have the lowest ids, so the dispatcher places them
+// first and the history workgroups fill the remaining slots.
+// ---------------------------------------------------------------------------
+// Out-of-line p-value evaluation for the fused kernel: inlined into the
+// role-split kernel the special functions pushed it to 256 VGPRs (one wave
+// per SIMD); as a call the kernel keeps the history role's 96.
+__device__ __attribute__((noinline)) void eval_test_call(int t, const double* __restrict__ o, int min_mw, int min_wil,
+                                                         int min_kru, double& pv, double& sv) {
+  eval_test(t, o, min_mw, min_wil, min_kru, pv, sv);
+}
+
+template <int NV, int K>
+__global__ __launch_bounds__(256) void tick_front_kernel(
+    const float* __restrict__ hist, int64_t ld_h, int T, int64_t R, float* __restrict__ hs /*[R,3]*/,
+    const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
+    int n_base, double* __restrict__ suff, int nP, int min_mw, int min_wil, int min_kru,
+    float* __restrict__ pvals, float* __restrict__ pstats) {
+  __shared__ double red[4];
+  __shared__ int redi[4];
+  if ((int)blockIdx.x < nP) {
+    const int64_t first = (int64_t)blockIdx.x * 4, stride = (int64_t)nP * 4;
+    for (int64_t row = first + wave_id(); row < R; row += stride) {
+      PwIn<K> in;
+      pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
+      pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+    }
+    __syncthreads();   // this workgroup's suff rows are visible to all its waves
+    // local row j -> global row first + (j & 3) + (j >> 2) * stride
+    const int64_t span = R > first ? R - first : 0;
+    const int nr = (int)(((span + stride - 1) / stride) * 4);
+    // wave-sized chunks of (test, 64 rows); the test is wave-uniform so the
+    // special-function switch stays a scalar branch (a per-lane test index
+    // made the compiler keep every path live: 256 VGPRs)
+    const int cpt = (nr + 63) >> 6;
+    for (int ci = wave_id(); ci < N_TESTS * cpt; ci += 4) {
+      const int t = __builtin_amdgcn_readfirstlane(ci / cpt);
+      const int j = (ci - t * cpt) * 64 + lane_id();
+      const int64_t row = first + (j & 3) + (int64_t)(j >> 2) * stride;
+      if (j < nr && row < R) {
+        double pv, sv;
+        eval_test_call(t, suff + row * kSuff, min_mw, min_wil, min_kru, pv, sv);
+        pvals[row * N_TESTS + t] = (float)pv;
+        pstats[row * N_TESTS + t] = (float)sv;
+      }
+    }
+    return;
+  }
+  const int nH = (int)gridDim.x - nP;
+  for (int64_t row = (int64_t)blockIdx.x - nP; row < R; row += nH) {
+    float mf, sd;
+    int n;
+    block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
+    if (threadIdx.x == 0) {
+      hs[row * 3 + 0] = mf;
+      hs[row * 3 + 1] = sd;
+      hs[row * 3 + 2] = (float)n;
+    }
+  }
+}
+
+// nP / nH: workgroups of each role (0 = defaults: one pairwise workgroup per
+// 4 rows capped at pw_cap, one history workgroup per row capped at h_cap).
+FM_API int fm_tick_front(const float* hist, int64_t ld_h, int T, int64_t R, float* hs, const float* cur, int64_t ld_c,
+                         int n_cur, const float* base, int64_t ld_b, int n_base, double* suff, int nP, int nH,
+                         int min_mw, int min_wil, int min_kru, float* pvals, float* pstats, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
+  const int n = n_cur + n_base;
+  if (base == nullptr || n_base <= 0 || n > 256) return (int)hipErrorInvalidValue;
+  const int64_t pmax = (R + 3) / 4;
+  if (nP <= 0 || nP > pmax) nP = (int)pmax;
+  if (nH <= 0 || nH > R) nH = (int)R;
+  const int nq = (T + 3) / 4;
+  const dim3 grid((unsigned)(nP + nH)), block(256);
+#define FM_TF(NVV, KK)                                                                                             \
+  hipLaunchKernelGGL((tick_front_kernel<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c, n_cur, \
+                     base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats)
+#define FM_TF_K(NVV)           \
+  do {                         \
+    if (n <= 64) FM_TF(NVV, 1);  \
+    else if (n <= 128) FM_TF(NVV, 2); \
+    else FM_TF(NVV, 4);        \
+  } while (0)
+  if (nq <= 256 * 2) FM_TF_K(2);
+  else if (nq <= 256 * 4) FM_TF_K(4);
+  else if (nq <= 256 * 8) FM_TF_K(8);
+  else if (nq <= 256 * 10) FM_TF_K(10);
+  else if (nq <= 256 * 12) FM_TF_K(12);
+  else if (nq <= 256 * 16) FM_TF_K(16);
+  else return (int)hipErrorInvalidValue;
+#undef FM_TF_K
+#undef FM_TF
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
 __global__ __launch_bounds__(256) void window_decide_kernel(
     const float* __restrict__ hs, const float* __restrict__ cur, int64_t ld_c, int n_cur, int64_t R, int M,
     const float* __restrict__ thr, const int* __restrict__ bound, const float* __restrict__ minlb, float pair_factor,
@@ -1078,6 +1185,12 @@ __global__ __launch_bounds__(256) void decide_service_kernel(
   int tot = 0, mask = 0;
   bool unknown = false;
   float bestm[MAXM];
+  // per-row outputs are collected in lane m (values are wave-uniform per
+  // metric) and stored once by lanes 0..M-1: 7 store instructions per
+  // service instead of 7 per metric from lane 0
+  float4 o_st = make_float4(0.f, 0.f, 0.f, 0.f);
+  int o_cnt = 0, o_valid = 0, o_diff = 0;
+  unsigned long long o_flag = 0ull;
 #pragma unroll
   for (int m = 0; m < MAXM; ++m) {
     bestm[m] = 0.f;
@@ -1114,32 +1227,42 @@ __global__ __launch_bounds__(256) void decide_service_kernel(
       const unsigned long long bal = __ballot(f);
       acnt += __popcll(bal);
       ccnt += __popcll(__ballot(obs));
-      if (lane == 0 && i0 / 64 < NW) out_flags[row * NW + i0 / 64] = bal;
+      if (i0 == 0) {
+        if (lane == m) o_flag = bal;
+      } else if (lane == 0 && i0 / 64 < NW) {
+        out_flags[row * NW + i0 / 64] = bal;
+      }
     }
     bestm[m] = best;
     const int valid = (has_hist ? 1 : 0) | (ccnt > 0 ? 2 : 0);
-    if (lane == 0) {
-      if (out_diff != nullptr && pvals != nullptr) out_diff[row] = (int8_t)differs;
-      out_stats[row * 4 + 0] = mf;
-      out_stats[row * 4 + 1] = sd;
-      out_stats[row * 4 + 2] = up;
-      out_stats[row * 4 + 3] = lo;
-      out_count[row] = acnt;
-      out_valid[row] = valid;
+    if (lane == m) {
+      o_st = make_float4(mf, sd, up, lo);
+      o_cnt = acnt;
+      o_valid = valid;
+      o_diff = differs ? 1 : 0;
     }
     tot += acnt;
     if (acnt > 0) mask |= 1 << m;
     if ((valid & 3) != 3) unknown = true;
   }
   // the M max-reductions are independent: issued together they overlap
-  float sbest = 0.f;
+  float sbest = 0.f, o_score = 0.f;
 #pragma unroll
   for (int m = 0; m < MAXM; ++m) bestm[m] = wave_max(bestm[m]);
 #pragma unroll
   for (int m = 0; m < MAXM; ++m) {
     if (m >= M) break;
-    if (lane == 0) out_score[svc * M + m] = bestm[m];
+    if (lane == m) o_score = bestm[m];
     sbest = bestm[m] > sbest ? bestm[m] : sbest;
+  }
+  if (lane < M) {
+    const int64_t row = svc * M + lane;
+    reinterpret_cast<float4*>(out_stats)[row] = o_st;
+    out_count[row] = o_cnt;
+    out_valid[row] = o_valid;
+    out_score[row] = o_score;
+    out_flags[row * NW] = o_flag;
+    if (out_diff != nullptr && pvals != nullptr) out_diff[row] = (int8_t)o_diff;
   }
   if (lane == 0) {
     packed[svc * 4 + 0] = (float)(tot > 0 ? 1 : (unknown ? 2 : 0));
@@ -1157,6 +1280,7 @@ FM_API int fm_decide_services(const float* hs, const float* cur, int64_t ld_c, i
                               hipStream_t stream) {
   if (S <= 0) return 0;
   if (M < 1 || M > 16 || n_cur < 1 || NW * 64 < n_cur) return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)out_stats) & 15) != 0) return (int)hipErrorInvalidValue;   // float4 row stores
   const dim3 grid((unsigned)((S + 3) / 4)), block(256);
 #define FM_DS(MM)                                                                                                     \
   hipLaunchKernelGGL(decide_service_kernel<MM>, grid, block, 0, stream, hs, cur, ld_c, n_cur, S, M, thr, bound,       \
@@ -1174,7 +1298,17 @@ FM_API int fm_pvalues_only(const double* suff, int64_t R, int min_mw, int min_wi
                            float* stats, hipStream_t stream) {
   if (R <= 0) return 0;
   hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)((R + 255) / 256), N_TESTS), dim3(256), 0, stream, suff, R,
-                     min_mw, min_wil, min_kru, pvals, stats);
+                     min_mw, min_wil, min_kru, pvals, stats, 0);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Tests [t0, t1) only (per-test timing in tools/tick_breakdown.py).
+FM_API int fm_pvalues_range(const double* suff, int64_t R, int t0, int t1, int min_mw, int min_wil, int min_kru,
+                            float* pvals, float* stats, hipStream_t stream) {
+  if (R <= 0 || t0 < 0 || t1 > N_TESTS || t1 <= t0) return 0;
+  hipLaunchKernelGGL(pvalue_kernel, dim3((unsigned)((R + 255) / 256), t1 - t0), dim3(256), 0, stream, suff, R,
+                     min_mw, min_wil, min_kru, pvals, stats, t0);
   FM_LAUNCH_CHECK();
   return 0;
 }
@@ -1372,4 +1506,12 @@ FM_API int fm_selftest_lanes(const int* in, int* out, hipStream_t stream) {
   hipLaunchKernelGGL(selftest_lanes_kernel, dim3(1), dim3(64), 0, stream, in, out);
   FM_LAUNCH_CHECK();
   return 0;
+}
+
+// Async device -> pinned-host copy of the fleet verdict, issued on the
+// caller's stream so it is captured into the tick's HIP graph as a memcpy
+// node (the whole step — tick, all-gather, host copy — is one graph launch).
+FM_API int fm_copy_d2h_async(void* dst, const void* src, int64_t bytes, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  return (int)hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, stream);
 }

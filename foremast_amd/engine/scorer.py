@@ -35,13 +35,17 @@ class CanaryOutputs:
     hs: torch.Tensor | None = None   # [R, 3] history mean, std, count (two-stream path)
 
 
-MODES = ("fused", "overlap", "serial")
+MODES = ("front", "fused", "overlap", "serial")
 
 
 class CanaryScorer:
     """``mode`` (GPU only):
 
-    * ``overlap`` (default) — pairwise on a side stream || history stats on
+    * ``front`` (default) — ONE role-split launch (fm_tick_front): pairwise workgroups
+      (sorted-rank statistics, then the p-values of their own rows) and
+      history-stats workgroups share the CUs without a second stream, then
+      the decide kernel.  No fork/join in the graph;
+    * ``overlap`` — pairwise on a side stream || history stats on
       the main stream, joined before the decision (fork/join captured in the
       graph);
     * ``fused`` — one wave per row streams the 7-day history and runs the
@@ -52,14 +56,18 @@ class CanaryScorer:
     """
 
     def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu", overlap: bool = True,
-                 mode: str | None = None, hist_blocks: int = 0, pw_blocks: int = 0):
-        self.mode = mode or ("overlap" if overlap else "serial")
+                 mode: str | None = None, hist_blocks: int = 0, pw_blocks: int = 0, pw_cap_rows: int = 32,
+                 front_wgs: tuple[float, float] | None = None):
+        self.mode = mode or ("front" if overlap else "serial")
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         self.overlap = self.mode == "overlap"
         # workgroup caps of the two concurrent kernels of the overlap tick
         # (0 = one workgroup per row / per 4 rows); see tools/tick_breakdown.py
         self.hist_blocks, self.pw_blocks = hist_blocks, pw_blocks
+        # cap the pairwise grid only when each capped workgroup still loops
+        # over more than this many rows (per workgroup of 4 waves)
+        self.pw_cap_rows = pw_cap_rows
         self._side = None
         self.cfg = cfg or BrainConfig()
         self.aliases = list(aliases)
@@ -76,6 +84,11 @@ class CanaryScorer:
                 self.pw_blocks = cus
             if hist_blocks == 0:
                 self.hist_blocks = 8 * cus
+        # front mode: (pairwise, history) workgroups per CU, 0 = one per 4 rows /
+        # one per row (tools/tick_breakdown.py SWEEP_FRONT)
+        self.front_wgs = front_wgs or (1.0, 4.0)
+        self._cus = (torch.cuda.get_device_properties(self.device).multi_processor_count
+                     if self.device.type == "cuda" else 0)
         rules = [self.cfg.rule_for(a) for a in aliases]
         self.thr = torch.tensor([r.threshold for r in rules], dtype=torch.float32, device=self.device)
         self.bound = torch.tensor([r.bound for r in rules], dtype=torch.int32, device=self.device)
@@ -117,10 +130,13 @@ class CanaryScorer:
             return CanaryOutputs(pv, ps, df, None, dec, packed)
         o = self._alloc(R, cur.shape[1])
         has_base = base is not None and base.shape[1] > 0
+        if self.mode == "front" and has_base and cur.shape[1] + base.shape[1] <= 256:
+            self._front(hist, base, cur, n_hist, o)
+            return o
         if self.mode == "fused":
             self._fused(hist, base if has_base else None, cur, n_hist, o)
             return o
-        elif not self.overlap:
+        elif self.mode == "serial":
             if has_base:
                 self._pairwise_into(cur, base, o)
             C.stats_decide(hist, cur, n_hist, self.M, self.thr, self.bound, self.minlb,
@@ -132,17 +148,20 @@ class CanaryScorer:
             from ..ops._lib import LIB, ptr, stream_of
             dev = cur.device
             main = torch.cuda.current_stream(dev)
+            T = hist.shape[1] if n_hist is None else int(n_hist)
+            C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
             if has_base:
+                # the capped pairwise grid is issued first so its workgroups
+                # are resident before the persistent history grid fills the
+                # CUs (history first serialises the two: 0.60 -> 0.87 ms)
                 side = self._side_stream(dev)
                 side.wait_stream(main)
                 # the cap only pays when each capped wave still loops over many
                 # rows; a small shard (per-GPU slice of a multi-GPU fleet) runs
                 # one row per wave
-                cap = self.pw_blocks if R > 32 * self.pw_blocks else 0
+                cap = self.pw_blocks if R > self.pw_cap_rows * self.pw_blocks else 0
                 with torch.cuda.stream(side):
                     self._pairwise_into(cur, base, o, cap, combine=False)
-            T = hist.shape[1] if n_hist is None else int(n_hist)
-            C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
             LIB.call("fm_hist_stats_capped", ptr(hist), hist.stride(0), T, R, ptr(o.hs), self.hist_blocks,
                      stream_of(hist))
             if has_base:
@@ -164,6 +183,19 @@ class CanaryScorer:
                  ptr(o.pvals) if has_base else None, mask, anyc, float(self.pcfg.p_threshold),
                  int(self.cfg.min_historical_points), ptr(d.stats), ptr(d.flags), d.flags.shape[1], ptr(d.count),
                  ptr(d.score), ptr(d.valid), ptr(o.diff) if has_base else None, ptr(o.packed), stream_of(cur))
+
+    def _front(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:
+        from ..ops._lib import LIB, ptr, stream_of
+        R = cur.shape[0]
+        T = hist.shape[1] if n_hist is None else int(n_hist)
+        C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
+        fp, fh = self.front_wgs
+        n_p = int(fp * self._cus) if fp > 0 else 0
+        n_h = int(fh * self._cus) if fh > 0 else 0
+        LIB.call("fm_tick_front", ptr(hist), hist.stride(0), T, R, ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1],
+                 ptr(base), base.stride(0), base.shape[1], ptr(o.suff), n_p, n_h, self.pcfg.min_mann_white,
+                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), stream_of(cur))
+        self._decide_services(cur, o, True)
 
     def _fused(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:
         from ..ops._lib import LIB, ptr, stream_of
@@ -201,11 +233,15 @@ class CanaryScorer:
                      self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), st)
 
     # -- HIP graph capture of the whole tick ---------------------------------
-    def capture(self, hist, base, cur, n_hist=None):
-        """Capture the 3-kernel tick into a graph over static buffers; returns
-        a replay callable producing outputs in ``self._out``."""
+    def capture(self, hist, base, cur, n_hist=None, epilogue=None):
+        """Capture the tick into a graph over static buffers; returns a replay
+        callable producing outputs in ``self._out``.  ``epilogue(outputs)`` is
+        captured after the tick (e.g. the verdict all-gather and the host
+        copy), so a whole brain step is a single graph launch."""
         assert cur.is_cuda
         o = self.score(hist, base, cur, n_hist)  # warm / allocate
+        if epilogue is not None:
+            epilogue(o)                           # warm the collective outside the capture
         torch.cuda.synchronize(cur.device)
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(cur.device)
@@ -213,6 +249,8 @@ class CanaryScorer:
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
                 self.score(hist, base, cur, n_hist)
+                if epilogue is not None:
+                    epilogue(o)
         torch.cuda.current_stream(cur.device).wait_stream(s)
         self._graph = g
 

@@ -208,14 +208,16 @@ def test_gpu_scorer_graph_equals_eager_and_cpu(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,base", [(10080, True), (9001, True), (10080, False)])
 def test_gpu_tick_modes_agree(cuda, T, base):
-    """fused row kernel == two-stream fork/join == serial, eager and graph-captured."""
+    """role-split front kernel == fused row kernel == two-stream fork/join ==
+    serial, eager and graph-captured."""
     from foremast_amd.engine.scorer import CanaryScorer
     aliases = ["error5xx", "latency", "traffic", "error4xx"]
     h, b, c = C.synth_fleet(300, 4, T, 5, 10, 0, device=cuda, fault_rate=0.1)
     b = b if base else None
     ref = CanaryScorer(aliases, device=cuda, mode="serial").score(h, b, c, T)
-    for mode in ("overlap", "fused"):
-        sc = CanaryScorer(aliases, device=cuda, mode=mode)
+    for mode, kw in (("front", {}), ("front", {"front_wgs": (0.05, 0.1)}), ("front", {"front_wgs": (0, 0)}),
+                     ("overlap", {}), ("fused", {})):
+        sc = CanaryScorer(aliases, device=cuda, mode=mode, **kw)
         o = sc.score(h, b, c, T)
         torch.cuda.synchronize()
         torch.testing.assert_close(o.packed, ref.packed, msg=mode)

@@ -65,7 +65,7 @@ def main():
     res["canary_rows_nobase_us"] = timed(lambda: LIB.call(
         "fm_canary_rows", ptr(h), h.stride(0), T, ptr(c), c.stride(0), c.shape[1], None, 0, 0, R, ptr(hs),
         ptr(suff), stream_of(h)))
-    for mode in ("fused", "overlap", "serial"):
+    for mode in ("front", "fused", "overlap", "serial"):
         sc = CanaryScorer(aliases, cfg, device=dev, mode=mode)
         g = sc.capture(h, b, c, T)
         res[f"tick_{mode}_us"] = timed(g)
@@ -87,6 +87,19 @@ def main():
                               pw_blocks=max(1, int(pb * cu)) if pb else -1)
             g = sc.capture(h, b, c, T)
             res[f"tick_overlap_h{hb:g}_p{pb:g}_us"] = timed(g)
+    # minimum rows per capped pairwise workgroup before the cap applies
+    for cr in [int(x) for x in os.environ.get("SWEEP_CAPROWS", "").split(",") if x]:
+        sc = CanaryScorer(aliases, cfg, device=dev, mode="overlap", pw_cap_rows=cr)
+        g = sc.capture(h, b, c, T)
+        res[f"tick_overlap_caprows{cr}_us"] = timed(g)
+    # role-split front kernel: "p:h" workgroups per CU (0 = uncapped)
+    for spec in [x for x in os.environ.get("SWEEP_FRONT", "1:4").split(",") if x]:
+        fp, fh = (float(v) for v in spec.split(":"))
+        sc = CanaryScorer(aliases, cfg, device=dev, mode="front", front_wgs=(fp, fh))
+        g = sc.capture(h, b, c, T)
+        res[f"tick_front_p{fp:g}_h{fh:g}_us"] = timed(g)
+    res["pvalues_us"] = timed(lambda: LIB.call("fm_pvalues_only", ptr(suff), R, 20, 20, 5, ptr(pv), ptr(ps),
+                                               stream_of(pv)))
     res["hist_bytes_GB"] = R * T * 4 / 1e9
     res["hist_TBps"] = res["hist_bytes_GB"] / (res["hist_stats_us"] * 1e-6) / 1e3
     print(json.dumps(res))
