@@ -54,8 +54,9 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=5)
     ap.add_argument("--window", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--graph-scope", choices=["step", "tick"], default="step",
-                    help="capture the whole step (tick + all-gather + host copy) or only the tick kernels")
+    ap.add_argument("--graph-scope", choices=["auto", "step", "tick"], default="auto",
+                    help="capture the whole step (tick + all-gather + host copy) or only the tick kernels; auto = "
+                         "step on one GPU, tick (eager RCCL all-gather, hidden by the pipeline) on several")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="steps in flight (1 = host waits for each verdict before launching the next tick)")
     ap.add_argument("--mode", choices=["front", "fused", "overlap", "serial"], default="front",
@@ -69,7 +70,9 @@ def main() -> None:
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)
         sys.exit(2)
-    dev = torch.device("cuda", info.local_rank)
+    # FOREMAST_DEVICE_INDEX pins every rank to one GPU (multi-rank rehearsal
+    # on a 1-GPU box together with FOREMAST_DIST_BACKEND=gloo)
+    dev = torch.device("cuda", int(os.environ.get("FOREMAST_DEVICE_INDEX", info.local_rank)))
     torch.cuda.set_device(dev)
     info = D.init_distributed(device=dev)
     world = info.world
@@ -105,7 +108,12 @@ def main() -> None:
     if args.no_graph:
         launches = [lambda h=h: publisher(h)(scorer.score(hist, base, cur, args.hist)) for h in hosts]
     else:
-        if args.graph_scope == "step":
+        scope = args.graph_scope
+        if scope == "auto":
+            scope = "step" if world == 1 else "tick"
+        if scope == "step" and world > 1 and torch.distributed.get_backend() != "nccl":
+            scope = "tick"     # only RCCL collectives are graph-capturable
+        if scope == "step":
             # the whole step (tick kernels, all-gather, host copy) is ONE graph
             # launch; RCCL collectives are graph-capturable after a warm-up
             try:

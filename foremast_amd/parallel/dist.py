@@ -40,7 +40,9 @@ def init_distributed(backend: str | None = None, device: torch.device | None = N
     info = env_info()
     if info.world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # FOREMAST_DIST_BACKEND=gloo rehearses several ranks on one GPU
+            # (RCCL refuses two ranks on the same device)
+            backend = os.environ.get("FOREMAST_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         kw = {}
