@@ -8,13 +8,15 @@ One step = one full brain judgement cycle for the whole fleet:
   -> anomaly decision on the current window (fail-fast flags, per-service verdict)
   -> all-gather of the packed per-service verdicts to every rank (RCCL over xGMI)
   -> rank 0 copies the fleet verdict to the host (decision available to the control plane).
+The tick is one HIP graph on the compute stream; the all-gather and the host
+copy of tick k run on a comm stream, overlapped with tick k+1.
 
 Metric: metric windows scored per second for the whole node (services x metrics
 / step time; strong scaling: the 10k-service fleet is fixed and sharded over
 ranks) and the p50 decision latency (GPU time from the start of a tick to the
-fleet verdict in rank 0's host memory).  Ticks are issued up to --pipeline
-steps ahead on one stream (default 2) so the GPU does not idle through the
-host's wake-up and graph launch; every step completes inside the timed region.
+fleet verdict in rank 0's host memory).  Steps are issued up to --pipeline
+ahead (default 2) so the GPU does not idle through the host's wake-up and
+graph launch; every step completes inside the timed region.
 
 Data: synthetic Prometheus-shaped series generated on device (K11), the model
 is the deployed default (no learned weights).  Reference publishes no number
@@ -54,9 +56,6 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=5)
     ap.add_argument("--window", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--graph-scope", choices=["auto", "step", "tick"], default="auto",
-                    help="capture the whole step (tick + all-gather + host copy) or only the tick kernels; auto = "
-                         "step on one GPU, tick (eager RCCL all-gather, hidden by the pipeline) on several")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="steps in flight (1 = host waits for each verdict before launching the next tick)")
     ap.add_argument("--mode", choices=["front", "fused", "overlap", "serial"], default="front",
@@ -88,84 +87,73 @@ def main() -> None:
     mode = "serial" if args.no_overlap else args.mode
     scorer = CanaryScorer(aliases, cfg, device=dev, mode=mode)
     depth = max(1, args.pipeline)
-    gathered = torch.empty((world * s_pad, 4), dtype=torch.float32, device=dev)
-    # one pinned host verdict buffer per in-flight step (the host reads step
-    # k's verdict while step k+1 may already be copying its own)
+    # Per in-flight step ("slot"): the tick's packed verdicts and rank 0's
+    # pinned host copy of the gathered fleet verdict.  Tick k+1 (compute
+    # stream) never waits for the all-gather + host copy of tick k (comm
+    # stream): the collective and the copy overlap the next tick's kernels.
+    packed = [torch.empty((s_pad, 4), dtype=torch.float32, device=dev) for _ in range(depth)]
     hosts = [torch.empty((world * s_pad, 4), dtype=torch.float32, pin_memory=True) for _ in range(depth)]
-
-    def publisher(host):
-        def publish(o):
-            """all-gather of the packed verdicts (RCCL over xGMI) + rank 0's
-            copy of the fleet verdict to pinned host memory, on the current
-            stream."""
-            g = D.all_gather_rows(o.packed, gathered)
-            if info.is_main:
-                LIB.call("fm_copy_d2h_async", host.data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
-        return publish
-
-    whole = "tick"
-    launches = []
+    gathered = torch.empty((world * s_pad, 4), dtype=torch.float32, device=dev)
     if args.no_graph:
-        launches = [lambda h=h: publisher(h)(scorer.score(hist, base, cur, args.hist)) for h in hosts]
+        ticks = [lambda p=p: scorer.score(hist, base, cur, args.hist, packed_out=p) for p in packed]
     else:
-        scope = args.graph_scope
-        if scope == "auto":
-            scope = "step" if world == 1 else "tick"
-        if scope == "step" and world > 1 and torch.distributed.get_backend() != "nccl":
-            scope = "tick"     # only RCCL collectives are graph-capturable
-        if scope == "step":
-            # the whole step (tick kernels, all-gather, host copy) is ONE graph
-            # launch; RCCL collectives are graph-capturable after a warm-up
-            try:
-                launches = [scorer.capture(hist, base, cur, args.hist, epilogue=publisher(h)) for h in hosts]
-                whole = "step"
-            except Exception as e:  # noqa: BLE001 - fall back to an eager collective
-                if info.is_main:
-                    print(f"bench: step capture failed ({e!r}); collective outside the graph", file=sys.stderr)
-                torch.cuda.synchronize(dev)
-                D.barrier()
-                launches = []
-        if not launches:
-            tick = scorer.capture(hist, base, cur, args.hist)
-            launches = [lambda h=h: publisher(h)(tick()) for h in hosts]
+        ticks = [scorer.capture(hist, base, cur, args.hist, packed_out=p) for p in packed]
 
-    # Steps are issued up to `depth` ahead: step k+1 is queued behind step k
-    # on the same stream (shared intermediates are safe: one stream), so the
-    # GPU runs ticks back to back instead of idling through the host's
-    # wake-up + graph launch.  Every step is complete (verdict in pinned host
-    # memory, event observed) before the timed region closes.
-    stream = torch.cuda.current_stream(dev)
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(depth)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(depth)]
-    lat: list[float] = []
+    compute = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(dev)
+    ev_tick = [torch.cuda.Event() for _ in range(depth)]
+    ev1 = [torch.cuda.Event() for _ in range(depth)]
 
-    def run(n: int, record: bool) -> None:
+    def publish(slot: int, done) -> None:
+        """comm stream: all-gather of the slot's verdicts (RCCL over xGMI) and
+        rank 0's copy of the fleet verdict to pinned host memory."""
+        comm.wait_event(ev_tick[slot])
+        with torch.cuda.stream(comm):
+            g = D.all_gather_rows(packed[slot], gathered)
+            if info.is_main:
+                LIB.call("fm_copy_d2h_async", hosts[slot].data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
+        done.record(comm)
+
+    # Steps are issued up to `depth` ahead, so the GPU runs ticks back to back
+    # instead of idling through the host's wake-up and launch; a slot is
+    # reused only after its previous step retired (verdict in host memory,
+    # event observed), and every step retires inside the timed region.
+    def run(n: int) -> None:
         for k in range(n + depth):
             slot = k % depth
             if k >= depth:                       # retire step k - depth
                 ev1[slot].synchronize()
-                if record:
-                    lat.append(ev0[slot].elapsed_time(ev1[slot]))
             if k < n:
-                ev0[slot].record(stream)
-                launches[slot]()
-                ev1[slot].record(stream)
+                ticks[slot]()
+                ev_tick[slot].record(compute)
+                publish(slot, ev1[slot])
 
-    run(args.warmup, False)
+    run(args.warmup)
     D.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    run(args.steps, True)
+    run(args.steps)
     torch.cuda.synchronize(dev)
     D.barrier()
     t1 = time.perf_counter()
     elapsed = D.all_reduce_max(t1 - t0, dev)
-    # decision latency: GPU time from the start of a tick to its fleet verdict
-    # in host memory (event-timed, excludes queueing behind the previous step)
+
+    # decision latency, measured after the throughput run on unpipelined
+    # steps: GPU time from the start of a tick to the fleet verdict in rank
+    # 0's host memory (timing events stay out of the timed loop)
+    t_a, t_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    lat: list[float] = []
+    for _ in range(max(5, min(args.steps, 50))):
+        t_a.record(compute)
+        ticks[0]()
+        ev_tick[0].record(compute)
+        publish(0, t_b)
+        t_b.synchronize()
+        lat.append(t_a.elapsed_time(t_b))
     p50 = D.all_reduce_max(statistics.median(lat) / 1e3, dev)
     ms = elapsed / args.steps * 1e3
     windows = S * M
-    verdict = hosts[(args.steps - 1) % depth][:S].numpy() if info.is_main else None
+    verdict = hosts[0][:S].numpy() if info.is_main else None
     if info.is_main:
         n_anom = int((verdict[:, 0] == 1).sum())
         out = {
@@ -192,7 +180,7 @@ def main() -> None:
                 "parallelism": f"dp{world}",
                 "hip_graph": not args.no_graph,
                 "tick_mode": mode,
-                "graph_scope": whole if not args.no_graph else "none",
+                "comm_overlap": "all-gather + host copy of tick k on a comm stream || tick k+1",
                 "pipeline_depth": depth,
             },
             "services_flagged": n_anom,
@@ -207,7 +195,7 @@ def main() -> None:
             else contextlib.nullcontext()
         with ctx as prof:
             for _ in range(5):
-                run(1, False)
+                run(1)
         if info.is_main:
             prof.export_chrome_trace(args.trace)
     if D.is_dist():

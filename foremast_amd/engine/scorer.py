@@ -16,6 +16,7 @@ HIP graph (``capture``) and replayed with zero host work per tick.
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass
 
 import torch
@@ -115,7 +116,10 @@ class CanaryScorer:
         return self._out[key]
 
     def score(self, hist: torch.Tensor, base: torch.Tensor | None, cur: torch.Tensor,
-              n_hist: int | None = None) -> CanaryOutputs:
+              n_hist: int | None = None, packed_out: torch.Tensor | None = None) -> CanaryOutputs:
+        """``packed_out`` ([S, 4] fp32, optional): where the service verdicts
+        go instead of the scorer's own buffer (one per in-flight tick when
+        the consumer of tick k overlaps tick k+1)."""
         R = cur.shape[0]
         if not cur.is_cuda:
             if base is not None and base.shape[1] > 0:
@@ -129,6 +133,10 @@ class CanaryScorer:
             packed = C.service_reduce(dec.count, dec.score, dec.valid, self.M)
             return CanaryOutputs(pv, ps, df, None, dec, packed)
         o = self._alloc(R, cur.shape[1])
+        if packed_out is not None:
+            C.check(packed_out.shape == o.packed.shape and packed_out.is_contiguous()
+                    and packed_out.dtype == torch.float32, "packed_out must be a contiguous fp32 [S, 4] tensor")
+            o = dataclasses.replace(o, packed=packed_out)
         has_base = base is not None and base.shape[1] > 0
         if self.mode == "front" and has_base and cur.shape[1] + base.shape[1] <= 256:
             self._front(hist, base, cur, n_hist, o)
@@ -233,13 +241,13 @@ class CanaryScorer:
                      self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), st)
 
     # -- HIP graph capture of the whole tick ---------------------------------
-    def capture(self, hist, base, cur, n_hist=None, epilogue=None):
+    def capture(self, hist, base, cur, n_hist=None, epilogue=None, packed_out=None):
         """Capture the tick into a graph over static buffers; returns a replay
         callable producing outputs in ``self._out``.  ``epilogue(outputs)`` is
         captured after the tick (e.g. the verdict all-gather and the host
         copy), so a whole brain step is a single graph launch."""
         assert cur.is_cuda
-        o = self.score(hist, base, cur, n_hist)  # warm / allocate
+        o = self.score(hist, base, cur, n_hist, packed_out)  # warm / allocate
         if epilogue is not None:
             epilogue(o)                           # warm the collective outside the capture
         torch.cuda.synchronize(cur.device)
@@ -248,7 +256,7 @@ class CanaryScorer:
         s.wait_stream(torch.cuda.current_stream(cur.device))
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
-                self.score(hist, base, cur, n_hist)
+                self.score(hist, base, cur, n_hist, packed_out)
                 if epilogue is not None:
                     epilogue(o)
         torch.cuda.current_stream(cur.device).wait_stream(s)
