@@ -991,7 +991,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
     const float* __restrict__ hist, int64_t ld_h, int T, int64_t R, float* __restrict__ hs /*[R,3]*/,
     const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
     int n_base, double* __restrict__ suff, int nP, int min_mw, int min_wil, int min_kru,
-    float* __restrict__ pvals, float* __restrict__ pstats) {
+    float* __restrict__ pvals, float* __restrict__ pstats, unsigned* __restrict__ queue) {
   __shared__ double red[4];
   __shared__ int redi[4];
   if ((int)blockIdx.x < nP) {
@@ -1023,23 +1023,72 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
     return;
   }
   const int nH = (int)gridDim.x - nP;
-  for (int64_t row = (int64_t)blockIdx.x - nP; row < R; row += nH) {
-    float mf, sd;
-    int n;
-    block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
-    if (threadIdx.x == 0) {
-      hs[row * 3 + 0] = mf;
-      hs[row * 3 + 1] = sd;
-      hs[row * 3 + 2] = (float)n;
+  if (queue == nullptr) {
+    for (int64_t row = (int64_t)blockIdx.x - nP; row < R; row += nH) {
+      float mf, sd;
+      int n;
+      block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
+      if (threadIdx.x == 0) {
+        hs[row * 3 + 0] = mf;
+        hs[row * 3 + 1] = sd;
+        hs[row * 3 + 2] = (float)n;
+      }
+    }
+    return;
+  }
+  // Dynamic history queue: the rows are split into 8 contiguous ranges, one
+  // per XCD (workgroup ids are dealt round-robin over the XCDs), and the
+  // history workgroups of a range grab chunks of kHistChunk rows from its
+  // counter (one 128-B line per counter).  A slot freed by a finished
+  // pairwise workgroup is then filled by a history workgroup that starts late
+  // and simply takes what is left, instead of idling (static grid-stride).
+  // The next chunk index is requested while the current chunk streams.  The
+  // last workgroup of a range to find it empty resets the counters for the
+  // next tick (every other workgroup of the range has already exited).
+  constexpr int kHistChunk = 2;
+  __shared__ unsigned s_next;
+  const int hb = (int)blockIdx.x - nP;
+  const int xcd = hb & 7;
+  const int nwg = (nH >> 3) + ((nH & 7) > xcd ? 1 : 0);   // workgroups sharing this range
+  const int64_t lo = R * xcd / 8, hi = R * (xcd + 1) / 8;
+  unsigned* ctr = queue + xcd * 32;
+  if (threadIdx.x == 0) s_next = atomicAdd(ctr, (unsigned)kHistChunk);
+  __syncthreads();
+  int64_t r0 = lo + (int64_t)s_next;
+  while (r0 < hi) {
+    unsigned nxt = 0;
+    if (threadIdx.x == 0) nxt = atomicAdd(ctr, (unsigned)kHistChunk);
+    const int64_t r1 = r0 + kHistChunk < hi ? r0 + kHistChunk : hi;
+    for (int64_t row = r0; row < r1; ++row) {
+      float mf, sd;
+      int n;
+      block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
+      if (threadIdx.x == 0) {
+        hs[row * 3 + 0] = mf;
+        hs[row * 3 + 1] = sd;
+        hs[row * 3 + 2] = (float)n;
+      }
+    }
+    __syncthreads();               // everyone is done reading s_next
+    if (threadIdx.x == 0) s_next = nxt;
+    __syncthreads();
+    r0 = lo + (int64_t)s_next;
+  }
+  if (threadIdx.x == 0) {
+    const unsigned d = atomicAdd(ctr + 1, 1u);
+    if (d == (unsigned)nwg - 1) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
-// nP / nH: workgroups of each role (0 = defaults: one pairwise workgroup per
-// 4 rows capped at pw_cap, one history workgroup per row capped at h_cap).
+// nP / nH: workgroups of each role (0 = one pairwise workgroup per 4 rows /
+// one history workgroup per row); queue: dynamic history rows (or nullptr).
 FM_API int fm_tick_front(const float* hist, int64_t ld_h, int T, int64_t R, float* hs, const float* cur, int64_t ld_c,
                          int n_cur, const float* base, int64_t ld_b, int n_base, double* suff, int nP, int nH,
-                         int min_mw, int min_wil, int min_kru, float* pvals, float* pstats, hipStream_t stream) {
+                         int min_mw, int min_wil, int min_kru, float* pvals, float* pstats, unsigned* queue,
+                         hipStream_t stream) {
   if (R <= 0) return 0;
   if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
   const int n = n_cur + n_base;
@@ -1047,11 +1096,14 @@ FM_API int fm_tick_front(const float* hist, int64_t ld_h, int T, int64_t R, floa
   const int64_t pmax = (R + 3) / 4;
   if (nP <= 0 || nP > pmax) nP = (int)pmax;
   if (nH <= 0 || nH > R) nH = (int)R;
+  // queue: 8 x 32 zero-initialised uints (kept zero between launches by the
+  // kernel itself); needs at least one history workgroup per XCD range
+  if (queue != nullptr && nH < 8) nH = 8;
   const int nq = (T + 3) / 4;
   const dim3 grid((unsigned)(nP + nH)), block(256);
 #define FM_TF(NVV, KK)                                                                                             \
   hipLaunchKernelGGL((tick_front_kernel<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c, n_cur, \
-                     base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats)
+                     base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue)
 #define FM_TF_K(NVV)           \
   do {                         \
     if (n <= 64) FM_TF(NVV, 1);  \
@@ -1156,7 +1208,10 @@ FM_API int fm_window_decide(const float* hs, const float* cur, int64_t ld_c, int
 // popcounts), and the service verdict is reduced in registers.  Replaces
 // pcombine + window_decide + service_reduce.
 // ---------------------------------------------------------------------------
-template <int MAXM>
+// MAXM: metric slots in registers; EXACT: M == MAXM (no per-metric guards);
+// ONE: n_cur <= 64 (the current window is one wave-wide chunk).  The
+// specialised forms roughly halve the instruction count of the generic one.
+template <int MAXM, bool EXACT, bool ONE>
 __global__ __launch_bounds__(256) void decide_service_kernel(
     const float* __restrict__ hs, const float* __restrict__ cur, int64_t ld_c, int n_cur, int64_t S, int M,
     const float* __restrict__ thr, const int* __restrict__ bound, const float* __restrict__ minlb, float pair_factor,
@@ -1164,6 +1219,7 @@ __global__ __launch_bounds__(256) void decide_service_kernel(
     float* __restrict__ out_stats, unsigned long long* __restrict__ out_flags, int NW, int* __restrict__ out_count,
     float* __restrict__ out_score, int* __restrict__ out_valid, int8_t* __restrict__ out_diff,
     float* __restrict__ packed) {
+  if (EXACT) M = MAXM;
   const int64_t svc = (int64_t)blockIdx.x * 4 + wave_id();
   if (svc >= S) return;
   const int lane = lane_id();
@@ -1174,7 +1230,7 @@ __global__ __launch_bounds__(256) void decide_service_kernel(
   float xs[MAXM], pv[MAXM];
 #pragma unroll
   for (int m = 0; m < MAXM; ++m) {
-    const int64_t row = svc * M + (m < M ? m : M - 1);
+    const int64_t row = svc * M + ((EXACT || m < M) ? m : M - 1);
     xs[m] = cur[row * ld_c + li];
     pv[m] = pvals != nullptr ? pvals[row * N_TESTS + lp] : NaNf;
   }
@@ -1194,7 +1250,7 @@ __global__ __launch_bounds__(256) void decide_service_kernel(
 #pragma unroll
   for (int m = 0; m < MAXM; ++m) {
     bestm[m] = 0.f;
-    if (m >= M) continue;
+    if (!EXACT && m >= M) continue;
     const int64_t row = svc * M + m;
     bool differs = false;
     if (pvals != nullptr) {
@@ -1215,9 +1271,9 @@ __global__ __launch_bounds__(256) void decide_service_kernel(
     const float inv = sd > 0.f ? __builtin_amdgcn_rcpf(sd) : 0.f;   // z-score scale, 1-ulp rcp
     int acnt = 0, ccnt = 0;
     float best = 0.f;
-    for (int i0 = 0; i0 < n_cur; i0 += 64) {
+    for (int i0 = 0; i0 < (ONE ? 64 : n_cur); i0 += 64) {
       const int i = i0 + lane;
-      const float x = i0 == 0 ? xs[m] : cur[row * ld_c + (i < n_cur ? i : n_cur - 1)];
+      const float x = (ONE || i0 == 0) ? xs[m] : cur[row * ld_c + (i < n_cur ? i : n_cur - 1)];
       const bool obs = i < n_cur && isfinite(x);
       const bool hi = has_hist && obs && (bd & 1) && x > up;
       const bool lw = has_hist && obs && (bd & 2) && x < lo;
@@ -1251,7 +1307,7 @@ __global__ __launch_bounds__(256) void decide_service_kernel(
   for (int m = 0; m < MAXM; ++m) bestm[m] = wave_max(bestm[m]);
 #pragma unroll
   for (int m = 0; m < MAXM; ++m) {
-    if (m >= M) break;
+    if (!EXACT && m >= M) break;
     if (lane == m) o_score = bestm[m];
     sbest = bestm[m] > sbest ? bestm[m] : sbest;
   }
@@ -1282,12 +1338,14 @@ FM_API int fm_decide_services(const float* hs, const float* cur, int64_t ld_c, i
   if (M < 1 || M > 16 || n_cur < 1 || NW * 64 < n_cur) return (int)hipErrorInvalidValue;
   if ((((uintptr_t)out_stats) & 15) != 0) return (int)hipErrorInvalidValue;   // float4 row stores
   const dim3 grid((unsigned)((S + 3) / 4)), block(256);
-#define FM_DS(MM)                                                                                                     \
-  hipLaunchKernelGGL(decide_service_kernel<MM>, grid, block, 0, stream, hs, cur, ld_c, n_cur, S, M, thr, bound,       \
-                     minlb, pair_factor, pvals, test_mask, combine_any, p_thr, min_hist, out_stats, out_flags, NW,     \
-                     out_count, out_score, out_valid, out_diff, packed)
-  if (M <= 8) FM_DS(8);
-  else FM_DS(16);
+#define FM_DS(MM, EX, ONE)                                                                                            \
+  hipLaunchKernelGGL((decide_service_kernel<MM, EX, ONE>), grid, block, 0, stream, hs, cur, ld_c, n_cur, S, M, thr,    \
+                     bound, minlb, pair_factor, pvals, test_mask, combine_any, p_thr, min_hist, out_stats, out_flags,  \
+                     NW, out_count, out_score, out_valid, out_diff, packed)
+  if (M == 8 && n_cur <= 64) FM_DS(8, true, true);
+  else if (M == 4 && n_cur <= 64) FM_DS(4, true, true);
+  else if (M <= 8) FM_DS(8, false, false);
+  else FM_DS(16, false, false);
 #undef FM_DS
   FM_LAUNCH_CHECK();
   return 0;

@@ -58,7 +58,7 @@ class CanaryScorer:
 
     def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu", overlap: bool = True,
                  mode: str | None = None, hist_blocks: int = 0, pw_blocks: int = 0, pw_cap_rows: int = 32,
-                 front_wgs: tuple[float, float] | None = None):
+                 front_wgs: tuple[float, float] | None = None, front_queue: bool = True):
         self.mode = mode or ("front" if overlap else "serial")
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
@@ -88,6 +88,10 @@ class CanaryScorer:
         # front mode: (pairwise, history) workgroups per CU, 0 = one per 4 rows /
         # one per row (tools/tick_breakdown.py SWEEP_FRONT)
         self.front_wgs = front_wgs or (1.0, 4.0)
+        # dynamic history-row queue (8 per-XCD counters, kept zero between
+        # launches by the kernel itself)
+        self._queue = (torch.zeros(8 * 32, dtype=torch.int32, device=self.device)
+                       if front_queue and self.device.type == "cuda" else None)
         self._cus = (torch.cuda.get_device_properties(self.device).multi_processor_count
                      if self.device.type == "cuda" else 0)
         rules = [self.cfg.rule_for(a) for a in aliases]
@@ -202,7 +206,8 @@ class CanaryScorer:
         n_h = int(fh * self._cus) if fh > 0 else 0
         LIB.call("fm_tick_front", ptr(hist), hist.stride(0), T, R, ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1],
                  ptr(base), base.stride(0), base.shape[1], ptr(o.suff), n_p, n_h, self.pcfg.min_mann_white,
-                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), stream_of(cur))
+                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(self._queue),
+                 stream_of(cur))
         self._decide_services(cur, o, True)
 
     def _fused(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:

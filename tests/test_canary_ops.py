@@ -216,6 +216,7 @@ def test_gpu_tick_modes_agree(cuda, T, base):
     b = b if base else None
     ref = CanaryScorer(aliases, device=cuda, mode="serial").score(h, b, c, T)
     for mode, kw in (("front", {}), ("front", {"front_wgs": (0.05, 0.1)}), ("front", {"front_wgs": (0, 0)}),
+                     ("front", {"front_queue": False}), ("front", {"front_wgs": (0.05, 0.02)}),
                      ("overlap", {}), ("fused", {})):
         sc = CanaryScorer(aliases, device=cuda, mode=mode, **kw)
         o = sc.score(h, b, c, T)

@@ -93,11 +93,14 @@ def main():
         g = sc.capture(h, b, c, T)
         res[f"tick_overlap_caprows{cr}_us"] = timed(g)
     # role-split front kernel: "p:h" workgroups per CU (0 = uncapped)
+    # ("p:h" dynamic history queue, "p:h:s" static grid-stride)
     for spec in [x for x in os.environ.get("SWEEP_FRONT", "1:4").split(",") if x]:
-        fp, fh = (float(v) for v in spec.split(":"))
-        sc = CanaryScorer(aliases, cfg, device=dev, mode="front", front_wgs=(fp, fh))
+        parts = spec.split(":")
+        fp, fh = float(parts[0]), float(parts[1])
+        q = len(parts) <= 2 or parts[2] == "q"     # "p:h:s" = static grid-stride history
+        sc = CanaryScorer(aliases, cfg, device=dev, mode="front", front_wgs=(fp, fh), front_queue=q)
         g = sc.capture(h, b, c, T)
-        res[f"tick_front_p{fp:g}_h{fh:g}_us"] = timed(g)
+        res[f"tick_front_p{fp:g}_h{fh:g}{'_q' if q else ''}_us"] = timed(g)
     res["pvalues_us"] = timed(lambda: LIB.call("fm_pvalues_only", ptr(suff), R, 20, 20, 5, ptr(pv), ptr(ps),
                                                stream_of(pv)))
     res["hist_bytes_GB"] = R * T * 4 / 1e9
