@@ -47,6 +47,30 @@ __device__ __forceinline__ float tanh_f(float x) {
   return 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * (-2.f * kLog2e))) - 1.f;
 }
 
+// Fused-fraction cell (CELL = 1): with E = e^{-x} terms,
+//   sigm(a) = 1/(1+E_a),  tanh(b) = (1-E_2b)/(1+E_2b)
+//   c' = f c + i g = [c (1+E_i)(1+E_g) + (1-E_g)(1+E_f)] / [(1+E_f)(1+E_i)(1+E_g)]
+//   h  = o tanh(c') = (1-E_c) / ((1+E_o)(1+E_c))
+// = 5 v_exp + 2 v_rcp per unit per step instead of 5 + 5.  The exp2
+// arguments are clamped (v_med3) to |.| <= 29 so the triple product stays
+// finite (<= 2^87); sigm / tanh are saturated to fp32 1 well inside that.
+constexpr float kExpClamp = 29.f;
+__device__ __forceinline__ float exp2_clamped(float x) {
+  return __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(x, -kExpClamp, kExpClamp));
+}
+__device__ __forceinline__ void cell_fused(float ai, float af, float ag, float ao, float& c, float& h) {
+  const float pi = 1.f + exp2_clamped(ai * -kLog2e);
+  const float pf = 1.f + exp2_clamped(af * -kLog2e);
+  const float eg = exp2_clamped(ag * (-2.f * kLog2e));
+  const float pg = 1.f + eg;
+  const float pig = pi * pg;
+  const float cn = (c * pig + (1.f - eg) * pf) * __builtin_amdgcn_rcpf(pf * pig);
+  c = cn;
+  const float po = 1.f + exp2_clamped(ao * -kLog2e);
+  const float ec = exp2_clamped(cn * (-2.f * kLog2e));
+  h = (1.f - ec) * __builtin_amdgcn_rcpf(po * (1.f + ec));
+}
+
 union Frag {
   bf16x8 v;
   unsigned short s[8];
@@ -60,7 +84,7 @@ union Frag {
 // (features at k < I, 1.0 at k = I for the bias, zeros above): lane half h
 // reads its 8 values of step t with ONE 16-B load, no conversion and no
 // per-feature branches (fm_lstm_features writes it straight from the history).
-template <int H, int NCT>
+template <int H, int NCT, int CELL>
 __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict__ xa /*[B, L, 2] x 16 B*/,
                                                          int64_t B, int L, const uint4* __restrict__ Wpack,
                                                          const float* __restrict__ h0, const float* __restrict__ c0,
@@ -159,13 +183,18 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
         float hv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float ig = sigm(acc[rt][ct][j]);
-          const float fg = sigm(acc[rt][ct][4 + j]);
-          const float gg = tanh_f(acc[rt][ct][8 + j]);
-          const float og = sigm(acc[rt][ct][12 + j]);
-          const float cc = fg * c[rt][ct][j] + ig * gg;
-          c[rt][ct][j] = cc;
-          hv[j] = og * tanh_f(cc);
+          if (CELL == 1) {
+            cell_fused(acc[rt][ct][j], acc[rt][ct][4 + j], acc[rt][ct][8 + j], acc[rt][ct][12 + j], c[rt][ct][j],
+                       hv[j]);
+          } else {
+            const float ig = sigm(acc[rt][ct][j]);
+            const float fg = sigm(acc[rt][ct][4 + j]);
+            const float gg = tanh_f(acc[rt][ct][8 + j]);
+            const float og = sigm(acc[rt][ct][12 + j]);
+            const float cc = fg * c[rt][ct][j] + ig * gg;
+            c[rt][ct][j] = cc;
+            hv[j] = og * tanh_f(cc);
+          }
         }
         const int u0 = 16 * w + 8 * rt + 4 * h;
         const int64_t bb = b0 + 32 * ct + col;
@@ -257,26 +286,36 @@ FM_API int fm_lstm_features(const float* hist, int64_t ld, int T, int64_t R, int
 }
 
 // nct: batch column tiles per workgroup (1 or 2); 0 = tuned default.
-FM_API int fm_lstm_forward_nct(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
-                               const float* c0, float* h_out, float* c_out, unsigned short* hseq, int nct,
-                               hipStream_t stream) {
+// cell: 0 = separate sigm/tanh (10 transcendentals per unit-step), 1 = fused
+// fractions (7); -1 = default.
+FM_API int fm_lstm_forward_v(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
+                             const float* c0, float* h_out, float* c_out, unsigned short* hseq, int nct, int cell,
+                             hipStream_t stream) {
   if (B <= 0 || L <= 0) return 0;
   const uint4* x = (const uint4*)xa;
   // Default 64 columns (2 tiles).  For H=128 one tile gives 162 VGPRs and 3
   // waves/SIMD instead of 2 but measured 1.5 % slower (tools/lstm_ab.py:
-  // 3.66 vs 3.61 ms at 80k x 240): the cell update is transcendental-bound
-  // (10 v_exp/v_rcp per unit per step), not latency-bound.
+  // 3.66 vs 3.61 ms at 80k x 240).
   if (nct == 0) nct = 2;
-#define FM_LSTM(HH, NC)                                                                                          \
-  hipLaunchKernelGGL((lstm_fwd_kernel<HH, NC>), dim3((unsigned)((B + 32 * NC - 1) / (32 * NC))), dim3(HH * 4), 0, \
-                     stream, x, B, L, (const uint4*)Wpack, h0, c0, h_out, c_out, hseq)
-  if (H == 128) { if (nct == 1) FM_LSTM(128, 1); else FM_LSTM(128, 2); }
-  else if (H == 64) { if (nct == 1) FM_LSTM(64, 1); else FM_LSTM(64, 2); }
-  else if (H == 32) { if (nct == 1) FM_LSTM(32, 1); else FM_LSTM(32, 2); }
+  if (cell < 0) cell = 1;
+#define FM_LSTM(HH, NC, CC)                                                                                     \
+  hipLaunchKernelGGL((lstm_fwd_kernel<HH, NC, CC>), dim3((unsigned)((B + 32 * NC - 1) / (32 * NC))),           \
+                     dim3(HH * 4), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0, h_out, c_out, hseq)
+#define FM_LSTM_C(HH, NC) do { if (cell == 1) FM_LSTM(HH, NC, 1); else FM_LSTM(HH, NC, 0); } while (0)
+  if (H == 128) { if (nct == 1) FM_LSTM_C(128, 1); else FM_LSTM_C(128, 2); }
+  else if (H == 64) { if (nct == 1) FM_LSTM_C(64, 1); else FM_LSTM_C(64, 2); }
+  else if (H == 32) { if (nct == 1) FM_LSTM_C(32, 1); else FM_LSTM_C(32, 2); }
   else return (int)hipErrorInvalidValue;
+#undef FM_LSTM_C
 #undef FM_LSTM
   FM_LAUNCH_CHECK();
   return 0;
+}
+
+FM_API int fm_lstm_forward_nct(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
+                               const float* c0, float* h_out, float* c_out, unsigned short* hseq, int nct,
+                               hipStream_t stream) {
+  return fm_lstm_forward_v(xa, B, L, H, Wpack, h0, c0, h_out, c_out, hseq, nct, -1, stream);
 }
 
 FM_API int fm_lstm_forward(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,

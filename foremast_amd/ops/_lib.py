@@ -76,6 +76,8 @@ _SIGS: dict[str, list] = {
                         c_void_p],
     "fm_lstm_forward_nct": [c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_int, c_void_p],
+    "fm_lstm_forward_v": [c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p, c_int, c_int, c_void_p],
     "fm_tick_front": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_i64, c_int,
                       c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_copy_d2h_async": [c_void_p, c_void_p, c_i64, c_void_p],
