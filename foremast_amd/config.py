@@ -46,6 +46,7 @@ class MetricRule:
     threshold: float
     bound: int
     min_lower_bound: float
+    algorithm: str | None = None     # per-metric-type ML_ALGORITHM override (ml_algorithmN); None = global
 
 
 @dataclass
@@ -87,6 +88,12 @@ class BrainConfig:
                 return r
         return MetricRule(self.threshold, self.bound, self.min_lower_bound)
 
+    def algorithm_for(self, alias: str) -> str:
+        """Model of a metric: its metric type's ``ml_algorithmN`` override, else
+        the global ``ML_ALGORITHM``.  The brain groups the rows of a cycle by
+        this (one batched zoo call per algorithm)."""
+        return self.rule_for(alias).algorithm or self.ml_algorithm
+
     @classmethod
     def from_env(cls, env: Mapping[str, str] | None = None) -> "BrainConfig":
         env = os.environ if env is None else env
@@ -103,7 +110,8 @@ class BrainConfig:
                 if not name:
                     continue
                 rules[name] = MetricRule(_f(env, f"threshold{i}", c.threshold), _i(env, f"bound{i}", c.bound),
-                                         _f(env, f"min_lower_bound{i}", c.min_lower_bound))
+                                         _f(env, f"min_lower_bound{i}", c.min_lower_bound),
+                                         env.get(f"ml_algorithm{i}") or None)
             c.metric_rules = rules
         c.min_historical_points = _i(env, "MIN_HISTORICAL_DATA_POINT_TO_MEASURE", c.min_historical_points)
         c.pairwise_algorithm = env.get("ML_PAIRWISE_ALGORITHM", c.pairwise_algorithm) or c.pairwise_algorithm

@@ -225,14 +225,46 @@ class Brain:
             pcfg = C.PairwiseConfig(self.cfg.pairwise_algorithm, self.cfg.pairwise_threshold,
                                     self.cfg.min_mann_white, self.cfg.min_wilcoxon, self.cfg.min_kruskal)
             _, _, diff = C.pairwise_tests(cur, base, pcfg)
-        pairs = None
-        if zoo.canonical(self.cfg.ml_algorithm) == "bivariate_normal":
-            pairs = self._pairs(rows)
-        dec = zoo.decide(self.cfg.ml_algorithm, hist, T, cur, hor, R, tables, diff, lstm_model=self.lstm_model,
-                         pairs=pairs, cache=self._cache_ctx(rows, self.cfg.ml_algorithm))
-        out = {k: getattr(dec, k).detach().cpu().numpy() for k in ("upper", "lower", "count", "score", "valid")}
+        # Model dispatch: rows are grouped by their metric type's algorithm
+        # (ml_algorithmN, else ML_ALGORITHM) and each group is ONE batched zoo
+        # call over its rows (per-series model selection as a
+        # sort by algorithm id, not one launch per series).
+        algos = [zoo.canonical(self.cfg.algorithm_for(r.alias)) for r in rows]
+        groups: dict[str, list[int]] = {}
+        for i, a in enumerate(algos):
+            groups.setdefault(a, []).append(i)
+        keys = ("upper", "lower", "count", "score", "valid")
+        if len(groups) == 1:
+            algo = algos[0]
+            pairs = self._pairs(rows) if algo == "bivariate_normal" else None
+            dec = zoo.decide(algo, hist, T, cur, hor, R, tables, diff, lstm_model=self.lstm_model,
+                             pairs=pairs, cache=self._cache_ctx(rows, algo))
+            out = {k: getattr(dec, k).detach().cpu().numpy() for k in keys}
+            flags = dec.flags
+        else:
+            out, flags = {}, None
+            for algo, idx in sorted(groups.items()):
+                sub = [rows[i] for i in idx]
+                it = torch.tensor(idx, dtype=torch.int64, device=hist.device)
+                pairs = self._pairs(sub) if algo == "bivariate_normal" else None
+                dec = zoo.decide(algo, hist.index_select(0, it).contiguous(), T, cur.index_select(0, it).contiguous(),
+                                 hor.index_select(0, it), len(idx),
+                                 zoo.make_tables([r.alias for r in sub], self.cfg, self.device),
+                                 None if diff is None else diff.index_select(0, it), lstm_model=self.lstm_model,
+                                 pairs=pairs, cache=self._cache_ctx(sub, algo))
+                for k in keys:
+                    v = getattr(dec, k).detach()
+                    if k not in out:
+                        out[k] = torch.zeros((R,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+                    out[k][it] = v
+                if flags is None:
+                    flags = torch.zeros((R,) + tuple(dec.flags.shape[1:]), dtype=dec.flags.dtype,
+                                        device=dec.flags.device)
+                flags[it] = dec.flags
+            out = {k: v.cpu().numpy() for k, v in out.items()}
+        out["algorithms"] = algos
         out["_hist"], out["_T"] = hist, T
-        out["flags"] = C.unpack_flags(dec.flags, cur.shape[1])
+        out["flags"] = C.unpack_flags(flags, cur.shape[1])
         out["diff"] = None if diff is None else diff.cpu().numpy()
         return out
 

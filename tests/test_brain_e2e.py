@@ -138,6 +138,35 @@ def test_every_algorithm_runs_end_to_end(algo):
     assert client.get_status(jid).status in (crd.PHASE_UNHEALTHY, crd.PHASE_RUNNING)
 
 
+def test_per_metric_type_algorithm_groups_equal_single_algorithm_runs():
+    """ml_algorithmN overrides: rows are grouped by algorithm, one batched zoo
+    call per group; each row's result equals a brain running that algorithm
+    for every row."""
+    env = {"ML_ALGORITHM": "moving_average_all", "metric_type_threshold_count": "3",
+           "metric_type0": "error5xx", "threshold0": "2", "bound0": "1",
+           "metric_type1": "latency", "threshold1": "10", "bound1": "3", "ml_algorithm1": "double_exponential_smoothing",
+           "metric_type2": "cpu", "threshold2": "5", "bound2": "1", "ml_algorithm2": "prophet"}
+    cfg = BrainConfig.from_env(env)
+    assert cfg.algorithm_for("latency") == "double_exponential_smoothing"
+    assert cfg.algorithm_for("error5xx") == "moving_average_all"
+    faults = {"7687b9f4d7-aaaa1": 6.0}
+    clock, store, client, brain, exp = _setup(faults=faults)
+    brain.cfg = cfg
+    client.start_analyzing("default", "demo", PODS, _metrics(), 10, "canary")
+    wk = brain._fetch_job(store.claim("w0", 1, 90, now=clock())[0], clock())
+    rows = wk.rows
+    mixed = brain.score_rows(rows)
+    assert mixed["algorithms"] == ["moving_average_all", "double_exponential_smoothing", "prophet"]
+    for i, algo in enumerate(mixed["algorithms"]):
+        single_cfg = BrainConfig.from_env({**env, "ML_ALGORITHM": algo, "ml_algorithm1": algo, "ml_algorithm2": algo})
+        brain.cfg = single_cfg
+        ref = brain.score_rows(rows)
+        for k in ("upper", "lower", "count", "valid"):
+            np.testing.assert_allclose(mixed[k][i], ref[k][i], rtol=1e-5, atol=1e-6, err_msg=f"{algo} {k}")
+        np.testing.assert_array_equal(mixed["flags"][i], ref["flags"][i])
+    brain.cfg = cfg
+
+
 def test_hpa_cycles_reuse_cached_models(tmp_path):
     # HPA jobs are re-scored every cycle: the second cycle advances the cached
     # fits over the new samples instead of re-running the grid
