@@ -204,3 +204,42 @@ def test_data_parallel_lstm_fit_keeps_ranks_in_sync():
     assert not DD.is_dist()
     solo = _w_lstm_fit(0, 1)
     assert any(not np.allclose(solo[k], out[0][k]) for k in solo)
+
+
+# ------------------------------------------------------------------ context parallel (time axis)
+def _cp_series(kind, R=6, T=960, m=24):
+    rng = np.random.default_rng(7 + kind)
+    t = np.arange(T)
+    x = (50 + 0.02 * t[None, :] * rng.uniform(0.5, 1.5, (R, 1))
+         + (8 * np.sin(2 * np.pi * t / m)[None, :] if kind >= 2 else 0)
+         + rng.normal(0, 1.5, (R, T))).astype(np.float32)
+    x[1, 100:110] = np.nan          # missing samples propagate the forecast inside a later chunk
+    x[2, 700] = np.nan
+    return x
+
+
+def _w_cp_es(rank, world, kind, m):
+    from foremast_amd.parallel.seqpar import cp_es_fit
+    x = _cp_series(kind, m=m)
+    T = x.shape[1]
+    bounds = np.linspace(0, T, world + 1).astype(int)
+    chunk = torch.from_numpy(np.ascontiguousarray(x[:, bounds[rank]:bounds[rank + 1]]))
+    f = cp_es_fit(chunk, kind, H=12, m=m)
+    return (f.forecast.numpy(), f.sigma.numpy(), f.best.numpy(), f.sse.numpy())
+
+
+@pytest.mark.parametrize("kind,world", [(0, 2), (1, 3), (2, 2), (3, 3)])
+def test_context_parallel_es_fit_equals_single_rank(kind, world):
+    """Time-sharded grid fit (affine carries for SES / Holt, relay pipeline
+    for Holt-Winters) == es_fit on the whole series, on every rank."""
+    from foremast_amd.ops import smoothing as SM
+    m = 24
+    x = _cp_series(kind, m=m)
+    ref = SM.es_fit(torch.from_numpy(x), None, kind, 12, m)
+    out = _run(_w_cp_es, world, kind, m)
+    for r in range(world):
+        fc, sig, best, sse = out[r]
+        np.testing.assert_allclose(sse, ref.sse.numpy(), rtol=2e-4, atol=1e-3)
+        np.testing.assert_array_equal(best, ref.best.numpy())
+        np.testing.assert_allclose(fc, ref.forecast.numpy(), rtol=1e-4, atol=1e-3)
+        np.testing.assert_allclose(sig, ref.sigma.numpy(), rtol=1e-4, atol=1e-4)
