@@ -222,6 +222,137 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// Column-tile pipelined form (2 tiles of 32 sequences per workgroup).  The
+// kernel above does, per step, all MFMAs (both tiles) and then the cell
+// update that consumes them, so the matrix pipe and the VALU/transcendental
+// pipes take turns (PMC: MFMA busy 32 %, co-exec cycles ~30 % of MFMA
+// cycles).  Here a step is two half-steps, each pairing the MFMAs of one tile
+// with the cell update of the OTHER tile, whose accumulators were produced in
+// the previous half-step:
+//     A(t): MFMA tile1(t)   ||  cell tile0(t) -> h tile0(t)   ; barrier
+//     B(t): MFMA tile0(t+1) ||  cell tile1(t) -> h tile1(t)   ; barrier
+// The two instruction streams of a half-step are independent, so a wave
+// issues VALU while its own MFMAs occupy the matrix pipe.  Each tile's h is
+// single-buffered in LDS: it is rewritten one half-step after its last
+// reader, with a barrier in between.
+// ---------------------------------------------------------------------------
+template <int H, bool HSEQ>
+__global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __restrict__ xa /*[B, L, 2] x 16 B*/,
+                                                              int64_t B, int L, const uint4* __restrict__ Wpack,
+                                                              const float* __restrict__ h0,
+                                                              const float* __restrict__ c0,
+                                                              float* __restrict__ h_out, float* __restrict__ c_out,
+                                                              unsigned short* __restrict__ hseq) {
+  constexpr int KS = H / 16 + 1;
+  constexpr int HP = H + 8;
+  constexpr int BT = 64;
+  __shared__ __attribute__((aligned(16))) unsigned short hbuf[BT * HP];
+  const int lane = lane_id(), w = wave_id();
+  const int h = lane >> 5, col = lane & 31;
+  const int64_t b0 = (int64_t)blockIdx.x * BT;
+
+  Frag A[2][KS];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) A[rt][ks].u = Wpack[(((int64_t)w * 2 + rt) * KS + ks) * 64 + lane];
+
+  float c[2][2][4];   // [tile][rt][j]
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = 16 * w + 8 * rt + 4 * h + j;
+        const int64_t bb = b0 + 32 * ct + col;
+        c[ct][rt][j] = (c0 != nullptr && bb < B) ? c0[bb * H + u] : 0.f;
+        const float hv = (h0 != nullptr && bb < B) ? h0[bb * H + u] : 0.f;
+        hbuf[(32 * ct + col) * HP + u] = f2bf(hv);
+      }
+  __syncthreads();
+
+  const uint4* xp[2];
+  bool inb[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    int64_t bb = b0 + 32 * ct + col;
+    inb[ct] = bb < B;
+    bb = bb < B ? bb : B - 1;
+    xp[ct] = xa + (bb * L) * 2 + h;
+  }
+
+  // MFMAs of one tile for one step: h_{t-1} of the tile from LDS, x_t from xv
+  auto gates = [&](int ct, const uint4& xv, f32x16 (&acc)[2]) {
+    const unsigned short* hb = &hbuf[(32 * ct + col) * HP + 8 * h];
+    Frag bfr[KS - 1];
+#pragma unroll
+    for (int ks = 0; ks < KS - 1; ++ks) bfr[ks].u = *reinterpret_cast<const uint4*>(hb + 16 * ks);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][0].v, bfr[0].v,
+                                                                                    (f32x16){}, 0, 0, 0);
+#pragma unroll
+    for (int ks = 1; ks < KS - 1; ++ks)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+        acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][ks].v, bfr[ks].v, acc[rt], 0, 0, 0);
+    Frag xb;
+    xb.u = xv;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+      acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[rt][KS - 1].v, xb.v, acc[rt], 0, 0, 0);
+  };
+  // cell update of one tile; writes h_t to LDS (or the final state)
+  auto cell = [&](int ct, int t, const f32x16 (&acc)[2], bool last) {
+    const int64_t bb = b0 + 32 * ct + col;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      float hv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cell_fused(acc[rt][j], acc[rt][4 + j], acc[rt][8 + j], acc[rt][12 + j], c[ct][rt][j],
+                                             hv[j]);
+      const int u0 = 16 * w + 8 * rt + 4 * h;
+      uint2 pk;
+      pk.x = pack_bf2(hv[0], hv[1]);
+      pk.y = pack_bf2(hv[2], hv[3]);
+      if (last) {
+        if (inb[ct]) {
+          *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+          *reinterpret_cast<float4*>(&c_out[bb * H + u0]) =
+              make_float4(c[ct][rt][0], c[ct][rt][1], c[ct][rt][2], c[ct][rt][3]);
+        }
+      } else {
+        *reinterpret_cast<uint2*>(&hbuf[(32 * ct + col) * HP + u0]) = pk;
+      }
+      if (HSEQ && inb[ct]) *reinterpret_cast<uint2*>(&hseq[(bb * L + t) * H + u0]) = pk;
+    }
+  };
+
+  f32x16 acc0[2], acc1[2];
+  uint4 x0n = xp[0][0], x1n = xp[1][0];
+  gates(0, x0n, acc0);                               // tile 0, step 0
+  if (L > 1) x0n = xp[0][2];                         // x_1 of tile 0
+  __syncthreads();                                   // tile-0 h_{-1} read by all before A(0) rewrites it
+  for (int t = 0; t < L; ++t) {
+    const bool last = t == L - 1;
+    // A(t): tile-1 MFMAs for step t || tile-0 cell of step t
+    const uint4 x1 = x1n;
+    if (!last) x1n = xp[1][(t + 1) * 2];
+    gates(1, x1, acc1);
+    cell(0, t, acc0, last);
+    __syncthreads();
+    // B(t): tile-0 MFMAs for step t+1 || tile-1 cell of step t
+    if (!last) {
+      const uint4 x0 = x0n;
+      if (t + 2 < L) x0n = xp[0][(t + 2) * 2];
+      gates(0, x0, acc0);
+    }
+    cell(1, t, acc1, last);
+    if (!last) __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Forecaster features straight from the packed history: per row the last L
 // samples are z-scored (finite mean / population std, missing -> 0) and laid
 // out as the kernel's augmented input [z, sin(2 pi t/P), cos(2 pi t/P)][:I],
@@ -287,7 +418,8 @@ FM_API int fm_lstm_features(const float* hist, int64_t ld, int T, int64_t R, int
 
 // nct: batch column tiles per workgroup (1 or 2); 0 = tuned default.
 // cell: 0 = separate sigm/tanh (10 transcendentals per unit-step), 1 = fused
-// fractions (7); -1 = default.
+// fractions (7), 2 = fused fractions in the column-tile pipelined kernel
+// (nct ignored); -1 = default.
 FM_API int fm_lstm_forward_v(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
                              const float* c0, float* h_out, float* c_out, unsigned short* hseq, int nct, int cell,
                              hipStream_t stream) {
@@ -297,7 +429,26 @@ FM_API int fm_lstm_forward_v(const void* xa, int64_t B, int L, int H, const void
   // waves/SIMD instead of 2 but measured 1.5 % slower (tools/lstm_ab.py:
   // 3.66 vs 3.61 ms at 80k x 240).
   if (nct == 0) nct = 2;
-  if (cell < 0) cell = 1;
+  if (cell < 0) cell = 2;   // tools/lstm_ab.py: 3.21-3.29 ms vs 3.34-3.36 (cell 1) at 80k x 240 x H128
+  if (cell == 2) {   // column-tile pipelined kernel (2 tiles, fused cell)
+    const dim3 grid((unsigned)((B + 63) / 64));
+#define FM_LSTMP(HH)                                                                                              \
+    do {                                                                                                         \
+      if (hseq != nullptr)                                                                                       \
+        hipLaunchKernelGGL((lstm_fwd_pipe_kernel<HH, true>), grid, dim3(HH * 4), 0, stream, x, B, L,            \
+                           (const uint4*)Wpack, h0, c0, h_out, c_out, hseq);                                     \
+      else                                                                                                       \
+        hipLaunchKernelGGL((lstm_fwd_pipe_kernel<HH, false>), grid, dim3(HH * 4), 0, stream, x, B, L,           \
+                           (const uint4*)Wpack, h0, c0, h_out, c_out, hseq);                                     \
+    } while (0)
+    if (H == 128) FM_LSTMP(128);
+    else if (H == 64) FM_LSTMP(64);
+    else if (H == 32) FM_LSTMP(32);
+    else return (int)hipErrorInvalidValue;
+#undef FM_LSTMP
+    FM_LAUNCH_CHECK();
+    return 0;
+  }
 #define FM_LSTM(HH, NC, CC)                                                                                     \
   hipLaunchKernelGGL((lstm_fwd_kernel<HH, NC, CC>), dim3((unsigned)((B + 32 * NC - 1) / (32 * NC))),           \
                      dim3(HH * 4), 0, stream, x, B, L, (const uint4*)Wpack, h0, c0, h_out, c_out, hseq)

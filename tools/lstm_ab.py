@@ -23,7 +23,7 @@ def main():
     hT = torch.empty((B, H), device=dev)
     cT = torch.empty_like(hT)
     out = {}
-    for nct, cell in ((1, 0), (2, 0), (1, 1), (2, 1)):
+    for nct, cell in ((1, 0), (2, 0), (1, 1), (2, 1), (2, 2)):
         f = lambda: LIB.call("fm_lstm_forward_v", ptr(xa), B, L, H, ptr(pk), None, None, ptr(hT), ptr(cT), None,
                              nct, cell, stream_of(xa))
         for _ in range(2):
