@@ -1,6 +1,6 @@
 #!/bin/bash
 # Hardware-counter passes (kernel-trace + PMC only) for the headline tick and
-# configs 2 / 4.  Results: gpurun_out/pmc_<target>_<pass>/; summarise with
+# configs 2 / 4 (or the targets given as arguments).  Results: gpurun_out/pmc_<target>_<pass>/; summarise with
 # tools/pmc_summary.py.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
@@ -12,7 +12,7 @@ PASS[write]="WRITE_SIZE"
 PASS[inst]="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVES"
 PASS[busy]="SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"
 PASS[lds]="SQ_LDS_BANK_CONFLICT"
-for target in bench c2 c4; do
+for target in ${@:-bench c2 c4}; do
   case $target in
     bench) cmd=("$R/bench.py" --steps 3 --warmup 1) ;;
     c2) cmd=("$R/benchmarks/bench_configs.py" --config 2 --steps 1 --warmup 1) ;;
