@@ -72,22 +72,43 @@ __device__ __forceinline__ void dft(float2 (&v)[R]) {
 constexpr int kMaxN = 8192;
 constexpr int kThreads = 256;
 
+// j / Ns and j % Ns by a multiply-high with a per-pass magic number (exact
+// for j, Ns < 2^13: the 32-bit reciprocal's error times j stays below one
+// part in 2^19, less than the smallest fractional part 1/Ns).
+__device__ __forceinline__ int div_magic(int j, unsigned magic) { return (int)__umulhi((unsigned)j, magic); }
+
+// Twiddle w^q, q = 1..R-1, for w = exp(-2 pi i m / N): w from the hardware
+// sine / cosine (v_sin_f32 / v_cos_f32 take revolutions, so the argument is
+// the exact fraction m / N), the powers by complex products (R <= 9: a few
+// ulps) instead of R-1 gathers from a global table.
 template <int R>
-__device__ __forceinline__ void stockham_pass(float2* buf, int N, int Ns, const float2* __restrict__ tw) {
-  constexpr int MAXB = (kMaxN / R + kThreads - 1) / kThreads;
+__device__ __forceinline__ void twiddles(int m, float invN, float2 (&w)[R]) {
+  const float r = -(float)m * invN;
+  w[0] = make_float2(1.f, 0.f);
+  w[1] = make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
+#pragma unroll
+  for (int q = 2; q < R; ++q) w[q] = cmul(w[q - 1], w[1]);
+}
+
+template <int R, int MAXN>
+__device__ __forceinline__ void stockham_pass(float2* buf, int N, int Ns, float invN) {
+  constexpr int MAXB = (MAXN / R + kThreads - 1) / kThreads;
   const int nb = N / R;
   const int step = N / (Ns * R);
+  const unsigned magic = 0xFFFFFFFFu / (unsigned)Ns + 1u;   // scalar
   float2 v[MAXB][R];
 #pragma unroll
   for (int b = 0; b < MAXB; ++b) {
     const int j = threadIdx.x + b * kThreads;
     if (j < nb) {
-      const int k = j % Ns;
+      const int k = Ns == 1 ? 0 : j - div_magic(j, magic) * Ns;
 #pragma unroll
-      for (int q = 0; q < R; ++q) {
-        float2 a = buf[j + q * nb];
-        if (q > 0 && k > 0) a = cmul(a, tw[k * q * step]);
-        v[b][q] = a;
+      for (int q = 0; q < R; ++q) v[b][q] = buf[j + q * nb];
+      if (k > 0) {
+        float2 w[R];
+        twiddles<R>(k * step, invN, w);
+#pragma unroll
+        for (int q = 1; q < R; ++q) v[b][q] = cmul(v[b][q], w[q]);
       }
       dft<R>(v[b]);
     }
@@ -97,8 +118,9 @@ __device__ __forceinline__ void stockham_pass(float2* buf, int N, int Ns, const 
   for (int b = 0; b < MAXB; ++b) {
     const int j = threadIdx.x + b * kThreads;
     if (j < nb) {
-      const int k = j % Ns;
-      const int base = (j / Ns) * Ns * R + k;
+      const int g = Ns == 1 ? j : div_magic(j, magic);
+      const int k = j - g * Ns;
+      const int base = g * Ns * R + k;
 #pragma unroll
       for (int p = 0; p < R; ++p) buf[base + p * Ns] = v[b][p];
     }
@@ -113,55 +135,81 @@ struct FftPlan {
   int radix[16];
 };
 
+// MAXN: compile-time bound on N (register arrays are sized by it; the
+// 7-day series has N = 5040 and runs the 5120 variant at 4 workgroups/CU).
+template <int MAXN>
 __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
     const float* __restrict__ x, int64_t ld, int Nr, int64_t R, const float2* __restrict__ tw,
     const float2* __restrict__ tw2, FftPlan plan, int kmin, int kmax, float* __restrict__ power, int64_t ld_p,
     float2* __restrict__ spec, int64_t ld_s, int* __restrict__ period_bin, float* __restrict__ strength,
     float* __restrict__ mean_out, float* __restrict__ slope_out) {
   extern __shared__ __attribute__((aligned(16))) float2 buf[];
-  __shared__ double red[4];
+  (void)tw;   // twiddles are computed in-kernel (kept in the C ABI)
   __shared__ float redf[8];
   __shared__ int redi[8];
   const int64_t row = blockIdx.x;
   const int N = Nr >> 1;
   const float* xr = x + row * ld;
   const int tid = threadIdx.x;
-  // least-squares linear detrend over finite samples (NaN -> trend line), so a
-  // slow trend does not leak into the low-frequency bins
-  double s = 0.0, st = 0.0, stt = 0.0, sx = 0.0;
-  int c = 0;
-  for (int i = tid; i < Nr; i += kThreads) {
-    const float v = xr[i];
-    if (isfinite(v)) { s += v; st += i; stt += (double)i * i; sx += (double)i * v; ++c; }
+  // The row is read ONCE: its complex pairs z_j = (x_2j, x_2j+1) go to
+  // registers (all loads issued up front), the least-squares linear detrend
+  // sums over finite samples are taken from there, and the detrended values
+  // are written to LDS.  (NaN -> trend line, so a slow trend does not leak
+  // into the low-frequency bins.)
+  constexpr int NPT = MAXN / kThreads;        // complex values per thread
+  float2 z[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int j = tid + i * kThreads;
+    z[i] = j < N ? reinterpret_cast<const float2*>(xr)[j] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
   }
-  s = block_sum<kThreads>(s, red);
-  st = block_sum<kThreads>(st, red);
-  stt = block_sum<kThreads>(stt, red);
-  sx = block_sum<kThreads>(sx, red);
-  c = block_sum<kThreads>(c, redi);
-  const double dc = c > 0 ? (double)c : 1.0;
+  double s = 0.0, st = 0.0, stt = 0.0, sx = 0.0, c = 0.0;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const double t0 = 2.0 * (tid + i * kThreads);
+    if (isfinite(z[i].x)) { s += z[i].x; st += t0; stt += t0 * t0; sx += t0 * z[i].x; c += 1.0; }
+    if (isfinite(z[i].y)) { const double t1 = t0 + 1.0; s += z[i].y; st += t1; stt += t1 * t1; sx += t1 * z[i].y; c += 1.0; }
+  }
+  // the five block sums in one LDS round trip
+  __shared__ double red5[5][kThreads / 64];
+  s = wave_sum(s); st = wave_sum(st); stt = wave_sum(stt); sx = wave_sum(sx); c = wave_sum(c);
+  if (lane_id() == 0) {
+    red5[0][wave_id()] = s; red5[1][wave_id()] = st; red5[2][wave_id()] = stt; red5[3][wave_id()] = sx;
+    red5[4][wave_id()] = c;
+  }
+  __syncthreads();
+  s = st = stt = sx = c = 0.0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    s += red5[0][w]; st += red5[1][w]; stt += red5[2][w]; sx += red5[3][w]; c += red5[4][w];
+  }
+  const double dc = c > 0 ? c : 1.0;
   const double tbar = st / dc, xbar = s / dc;
   const double vt = stt / dc - tbar * tbar;
   const double slope_d = vt > 0 ? (sx / dc - tbar * xbar) / vt : 0.0;
   const float mu = c > 0 ? (float)xbar : 0.f;
   const float slope = (float)slope_d, tb = (float)tbar;
-  for (int j = tid; j < N; j += kThreads) {
-    const float2 p = reinterpret_cast<const float2*>(xr)[j];
-    const float t0 = (float)(2 * j) - tb;
-    buf[j] = make_float2(isfinite(p.x) ? p.x - mu - slope * t0 : 0.f,
-                         isfinite(p.y) ? p.y - mu - slope * (t0 + 1.f) : 0.f);
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int j = tid + i * kThreads;
+    if (j < N) {
+      const float t0 = (float)(2 * j) - tb;
+      buf[j] = make_float2(isfinite(z[i].x) ? z[i].x - mu - slope * t0 : 0.f,
+                           isfinite(z[i].y) ? z[i].y - mu - slope * (t0 + 1.f) : 0.f);
+    }
   }
   __syncthreads();
+  const float invN = 1.f / (float)N;
   int Ns = 1;
   for (int ps = 0; ps < plan.n_pass; ++ps) {
     const int r = plan.radix[ps];
     switch (r) {
-      case 2: stockham_pass<2>(buf, N, Ns, tw); break;
-      case 3: stockham_pass<3>(buf, N, Ns, tw); break;
-      case 4: stockham_pass<4>(buf, N, Ns, tw); break;
-      case 5: stockham_pass<5>(buf, N, Ns, tw); break;
-      case 7: stockham_pass<7>(buf, N, Ns, tw); break;
-      case 9: stockham_pass<9>(buf, N, Ns, tw); break;
+      case 2: stockham_pass<2, MAXN>(buf, N, Ns, invN); break;
+      case 3: stockham_pass<3, MAXN>(buf, N, Ns, invN); break;
+      case 4: stockham_pass<4, MAXN>(buf, N, Ns, invN); break;
+      case 5: stockham_pass<5, MAXN>(buf, N, Ns, invN); break;
+      case 7: stockham_pass<7, MAXN>(buf, N, Ns, invN); break;
+      case 9: stockham_pass<9, MAXN>(buf, N, Ns, invN); break;
       default: break;
     }
     Ns *= r;
@@ -218,8 +266,13 @@ FM_API int fm_fft_seasonal(const float* x, int64_t ld, int Nr, int64_t R, const 
   for (int i = 0; i < n_pass; ++i) { plan.radix[i] = radices[i]; prod *= radices[i]; }
   if (prod != Nr / 2) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)(Nr / 2) * sizeof(float2);
-  hipLaunchKernelGGL(fft_seasonal_kernel, dim3((unsigned)R), dim3(kThreads), lds, stream, x, ld, Nr, R, tw, tw2, plan,
-                     kmin, kmax, power, ld_p, spec, ld_s, period_bin, strength, mean_out, slope_out);
+#define FM_FFT(MN)                                                                                            \
+  hipLaunchKernelGGL(fft_seasonal_kernel<MN>, dim3((unsigned)R), dim3(kThreads), lds, stream, x, ld, Nr, R, tw, tw2, \
+                     plan, kmin, kmax, power, ld_p, spec, ld_s, period_bin, strength, mean_out, slope_out)
+  if (Nr / 2 <= 2048) FM_FFT(2048);
+  else if (Nr / 2 <= 5120) FM_FFT(5120);
+  else FM_FFT(kMaxN);
+#undef FM_FFT
   FM_LAUNCH_CHECK();
   return 0;
 }
