@@ -1059,7 +1059,13 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
   // The next chunk index is requested while the current chunk streams.  The
   // last workgroup of a range to find it empty resets the counters for the
   // next tick (every other workgroup of the range has already exited).
-  constexpr int kHistChunk = 2;
+  // One row per grab: at the 1,250-service shard (~10 rows per workgroup) the
+  // tail waits on at most one row instead of two (0.0951/0.0919 -> 0.0937/
+  // 0.0904 ms per step, interleaved runs); neutral at 10k services.
+#ifndef FM_HIST_CHUNK
+#define FM_HIST_CHUNK 1
+#endif
+  constexpr int kHistChunk = FM_HIST_CHUNK;
   __shared__ unsigned s_next;
   const int hb = (int)blockIdx.x - nP;
   const int xcd = hb & 7;
