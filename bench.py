@@ -8,8 +8,10 @@ One step = one full brain judgement cycle for the whole fleet:
   -> anomaly decision on the current window (fail-fast flags, per-service verdict)
   -> all-gather of the packed per-service verdicts to every rank (RCCL over xGMI)
   -> rank 0 copies the fleet verdict to the host (decision available to the control plane).
-The tick is one HIP graph on the compute stream; the all-gather and the host
-copy of tick k run on a comm stream, overlapped with tick k+1.
+The front kernel of a tick (pairwise tests + p-values + history stats, one
+launch) is a HIP graph on the compute stream; tick k's decision kernel, the
+all-gather and the host copy run on a comm stream, overlapped with tick k+1's
+front kernel (one output buffer set per in-flight step).
 
 Metric: metric windows scored per second for the whole node (services x metrics
 / step time; strong scaling: the 10k-service fleet is fixed and sharded over
@@ -48,8 +50,8 @@ ALIASES = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomca
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--services", type=int, default=10000)
     ap.add_argument("--metrics", type=int, default=8)
     ap.add_argument("--hist", type=int, default=10080)
@@ -62,6 +64,13 @@ def main() -> None:
                     help="tick structure: role-split front kernel (default), fused row kernel, two-stream "
                          "fork/join, or serial")
     ap.add_argument("--no-overlap", action="store_true", help="alias of --mode serial")
+    ap.add_argument("--decide-on", choices=["comm", "compute"], default="comm",
+                    help="front mode: run tick k's decision kernel on the comm stream (overlapping tick k+1's "
+                         "front kernel; one buffer set per in-flight step) or on the compute stream")
+    ap.add_argument("--front-wgs", default="auto",
+                    help="front kernel workgroups per CU, pairwise:history; auto = 1:4 on one GPU, 1:3 on several "
+                         "(leaves a workgroup slot per CU for the previous tick's decision, RCCL all-gather and "
+                         "copy kernels; 1:3 and 1:4 measure within 1%% of each other on one GPU)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace of 5 extra steps (rank 0)")
     args = ap.parse_args()
 
@@ -85,8 +94,12 @@ def main() -> None:
     cfg = BrainConfig()
     cfg.min_historical_points = 10
     mode = "serial" if args.no_overlap else args.mode
-    scorer = CanaryScorer(aliases, cfg, device=dev, mode=mode)
+    if args.front_wgs == "auto":
+        args.front_wgs = "1:4" if world == 1 else "1:3"
+    fp, fh = (float(x) for x in args.front_wgs.split(":"))
+    scorer = CanaryScorer(aliases, cfg, device=dev, mode=mode, front_wgs=(fp, fh))
     depth = max(1, args.pipeline)
+    split = mode == "front" and args.decide_on == "comm"
     # Per in-flight step ("slot"): the tick's packed verdicts and rank 0's
     # pinned host copy of the gathered fleet verdict.  Tick k+1 (compute
     # stream) never waits for the all-gather + host copy of tick k (comm
@@ -94,7 +107,23 @@ def main() -> None:
     packed = [torch.empty((s_pad, 4), dtype=torch.float32, device=dev) for _ in range(depth)]
     hosts = [torch.empty((world * s_pad, 4), dtype=torch.float32, pin_memory=True) for _ in range(depth)]
     gathered = torch.empty((world * s_pad, 4), dtype=torch.float32, device=dev)
-    if args.no_graph:
+    outs = [None] * depth
+    if split:
+        # tick = front kernel on the compute stream; its decision runs in
+        # publish() on the comm stream, so tick k's decision + all-gather +
+        # host copy overlap tick k+1's front kernel (buffer set per slot)
+        if args.no_graph:
+            def _front(i):
+                return lambda: scorer.front_only(hist, base, cur, args.hist, packed_out=packed[i], slot=i)
+            ticks = [_front(i) for i in range(depth)]
+            for i in range(depth):
+                outs[i] = scorer.front_only(hist, base, cur, args.hist, packed_out=packed[i], slot=i)
+        else:
+            ticks = []
+            for i in range(depth):
+                rep, outs[i] = scorer.capture_front(hist, base, cur, args.hist, packed_out=packed[i], slot=i)
+                ticks.append(rep)
+    elif args.no_graph:
         ticks = [lambda p=p: scorer.score(hist, base, cur, args.hist, packed_out=p) for p in packed]
     else:
         ticks = [scorer.capture(hist, base, cur, args.hist, packed_out=p) for p in packed]
@@ -109,6 +138,8 @@ def main() -> None:
         rank 0's copy of the fleet verdict to pinned host memory."""
         comm.wait_event(ev_tick[slot])
         with torch.cuda.stream(comm):
+            if split:
+                scorer.decide_only(cur, outs[slot])
             g = D.all_gather_rows(packed[slot], gathered)
             if info.is_main:
                 LIB.call("fm_copy_d2h_async", hosts[slot].data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
@@ -180,7 +211,10 @@ def main() -> None:
                 "parallelism": f"dp{world}",
                 "hip_graph": not args.no_graph,
                 "tick_mode": mode,
-                "comm_overlap": "all-gather + host copy of tick k on a comm stream || tick k+1",
+                "decision_stream": "comm (overlaps next front kernel)" if split else "compute",
+                "front_wgs_per_cu": args.front_wgs,
+                "comm_overlap": "decision + all-gather + host copy of tick k on a comm stream || tick k+1"
+                                if split else "all-gather + host copy of tick k on a comm stream || tick k+1",
                 "pipeline_depth": depth,
             },
             "services_flagged": n_anom,

@@ -104,8 +104,8 @@ class CanaryScorer:
         self._graph = None
         self._graph_key = None
 
-    def _alloc(self, R: int, n_cur: int) -> CanaryOutputs:
-        key = (R, n_cur)
+    def _alloc(self, R: int, n_cur: int, slot: int = 0) -> CanaryOutputs:
+        key = (R, n_cur, slot)
         if key not in self._out:
             d = self.device
             self._out[key] = CanaryOutputs(
@@ -183,6 +183,42 @@ class CanaryScorer:
         C.service_reduce(o.decide.count, o.decide.score, o.decide.valid, self.M, out=o.packed)
         return o
 
+    # -- split tick: front kernel and decision on different streams ----------
+    def front_only(self, hist, base, cur, n_hist=None, packed_out=None, slot: int = 0) -> CanaryOutputs:
+        """First half of a front-mode tick (pairwise tests, p-values, history
+        stats: one launch) into the buffers of ``slot``.  ``decide_only`` on
+        the returned outputs finishes the tick; with one buffer set per
+        in-flight step, the decision of tick k can run on another stream
+        while tick k+1's front kernel runs."""
+        C.check(cur.is_cuda and self.mode == "front" and base is not None and base.shape[1] > 0
+                and cur.shape[1] + base.shape[1] <= 256, "front_only needs a GPU front-mode tick with a baseline")
+        o = self._alloc(cur.shape[0], cur.shape[1], slot)
+        if packed_out is not None:
+            C.check(packed_out.shape == o.packed.shape and packed_out.is_contiguous()
+                    and packed_out.dtype == torch.float32, "packed_out must be a contiguous fp32 [S, 4] tensor")
+            o = dataclasses.replace(o, packed=packed_out)
+        self._front(hist, base, cur, n_hist, o, decide=False)
+        return o
+
+    def decide_only(self, cur, o: CanaryOutputs) -> CanaryOutputs:
+        """Second half of a split tick (p-value combine, window decision,
+        service reduce: one launch) on the current stream."""
+        self._decide_services(cur, o, True)
+        return o
+
+    def capture_front(self, hist, base, cur, n_hist=None, packed_out=None, slot: int = 0):
+        """Graph of ``front_only`` for one buffer slot; returns (replay, outputs)."""
+        o = self.front_only(hist, base, cur, n_hist, packed_out, slot)   # warm / allocate
+        torch.cuda.synchronize(cur.device)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(cur.device)
+        s.wait_stream(torch.cuda.current_stream(cur.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self.front_only(hist, base, cur, n_hist, packed_out, slot)
+        torch.cuda.current_stream(cur.device).wait_stream(s)
+        return g.replay, o
+
     def _decide_services(self, cur, o: CanaryOutputs, has_base: bool) -> None:
         """p-value combine + window decision + service reduce, one launch
         (a workgroup per service, a wave per metric row)."""
@@ -196,7 +232,7 @@ class CanaryScorer:
                  int(self.cfg.min_historical_points), ptr(d.stats), ptr(d.flags), d.flags.shape[1], ptr(d.count),
                  ptr(d.score), ptr(d.valid), ptr(o.diff) if has_base else None, ptr(o.packed), stream_of(cur))
 
-    def _front(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:
+    def _front(self, hist, base, cur, n_hist, o: CanaryOutputs, decide: bool = True) -> None:
         from ..ops._lib import LIB, ptr, stream_of
         R = cur.shape[0]
         T = hist.shape[1] if n_hist is None else int(n_hist)
@@ -208,7 +244,8 @@ class CanaryScorer:
                  ptr(base), base.stride(0), base.shape[1], ptr(o.suff), n_p, n_h, self.pcfg.min_mann_white,
                  self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(self._queue),
                  stream_of(cur))
-        self._decide_services(cur, o, True)
+        if decide:
+            self._decide_services(cur, o, True)
 
     def _fused(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:
         from ..ops._lib import LIB, ptr, stream_of

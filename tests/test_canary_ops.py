@@ -287,3 +287,39 @@ def test_gpu_front_tick_generic_shapes(cuda, M, P, T):
     torch.testing.assert_close(o.pvals, ref.pvals, equal_nan=True)
     g = sc.capture(h, b, c, T)().packed.clone()
     torch.testing.assert_close(g, ref.packed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,M", [(1250, 8), (77, 4)])
+def test_gpu_split_tick_equals_score(cuda, S, M):
+    """front_only (graph, per-slot buffers) + decide_only on another stream ==
+    score(), for two slots in flight (bench.py --decide-on comm)."""
+    from foremast_amd.engine.scorer import CanaryScorer
+    aliases = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"][:M]
+    T = 10080
+    h, b, c = C.synth_fleet(S, M, T, 5, 10, 1, device=cuda, fault_rate=0.2)
+    ref = CanaryScorer(aliases, device=cuda).score(h, b, c, T)
+    torch.cuda.synchronize()
+    sc = CanaryScorer(aliases, device=cuda, front_wgs=(1.0, 3.0))
+    packed = [torch.full((S, 4), -1.0, device=cuda) for _ in range(2)]
+    fronts = [sc.capture_front(h, b, c, T, packed_out=packed[i], slot=i) for i in range(2)]
+    assert fronts[0][1].hs.data_ptr() != fronts[1][1].hs.data_ptr()
+    side = torch.cuda.Stream()
+    ev = [torch.cuda.Event() for _ in range(2)]
+    done = [torch.cuda.Event() for _ in range(2)]
+    for k in range(6):
+        i = k % 2
+        if k >= 2:                     # slot i is reused once its decision has run
+            torch.cuda.current_stream().wait_event(done[i])
+        packed[i].fill_(-1.0)
+        fronts[i][0]()
+        ev[i].record()
+        side.wait_event(ev[i])
+        with torch.cuda.stream(side):  # overlaps the next tick's front kernel
+            sc.decide_only(c, fronts[i][1])
+        done[i].record(side)
+    torch.cuda.synchronize()
+    for i in range(2):
+        torch.testing.assert_close(packed[i], ref.packed, rtol=0, atol=0)
+        torch.testing.assert_close(fronts[i][1].decide.count, ref.decide.count, rtol=0, atol=0)
+
