@@ -224,28 +224,65 @@ class CanaryScorer:
         (a workgroup per service, a wave per metric row)."""
         from ..ops._lib import LIB, ptr, stream_of
         C.check(self.M <= 16, "overlap/fused ticks support up to 16 metrics per service (use mode='serial')")
+        LIB.call("fm_decide_services", *self._decide_call_args(cur, o, has_base), stream_of(cur))
+
+    def _decide_call_args(self, cur, o: CanaryOutputs, has_base: bool) -> tuple:
+        from ..ops._lib import ptr
         mask, anyc = self.pcfg.mask_and_combine()
         d = o.decide
-        LIB.call("fm_decide_services", ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1], cur.shape[0] // self.M,
-                 self.M, ptr(self.thr), ptr(self.bound), ptr(self.minlb), float(self.cfg.pairwise_threshold_factor),
-                 ptr(o.pvals) if has_base else None, mask, anyc, float(self.pcfg.p_threshold),
-                 int(self.cfg.min_historical_points), ptr(d.stats), ptr(d.flags), d.flags.shape[1], ptr(d.count),
-                 ptr(d.score), ptr(d.valid), ptr(o.diff) if has_base else None, ptr(o.packed), stream_of(cur))
+        return (ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1], cur.shape[0] // self.M,
+                self.M, ptr(self.thr), ptr(self.bound), ptr(self.minlb), float(self.cfg.pairwise_threshold_factor),
+                ptr(o.pvals) if has_base else None, mask, anyc, float(self.pcfg.p_threshold),
+                int(self.cfg.min_historical_points), ptr(d.stats), ptr(d.flags), d.flags.shape[1], ptr(d.count),
+                ptr(d.score), ptr(d.valid), ptr(o.diff) if has_base else None, ptr(o.packed))
 
     def _front(self, hist, base, cur, n_hist, o: CanaryOutputs, decide: bool = True) -> None:
-        from ..ops._lib import LIB, ptr, stream_of
-        R = cur.shape[0]
+        from ..ops._lib import LIB, stream_of
         T = hist.shape[1] if n_hist is None else int(n_hist)
         C.check(hist.stride(0) % 4 == 0 and hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
+        LIB.call("fm_tick_front", *self._front_call_args(hist, base, cur, T, o), stream_of(cur))
+        if decide:
+            self._decide_services(cur, o, True)
+
+    def _front_call_args(self, hist, base, cur, T: int, o: CanaryOutputs) -> tuple:
+        from ..ops._lib import ptr
         fp, fh = self.front_wgs
         n_p = int(fp * self._cus) if fp > 0 else 0
         n_h = int(fh * self._cus) if fh > 0 else 0
-        LIB.call("fm_tick_front", ptr(hist), hist.stride(0), T, R, ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1],
-                 ptr(base), base.stride(0), base.shape[1], ptr(o.suff), n_p, n_h, self.pcfg.min_mann_white,
-                 self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(self._queue),
-                 stream_of(cur))
-        if decide:
-            self._decide_services(cur, o, True)
+        return (ptr(hist), hist.stride(0), T, cur.shape[0], ptr(o.hs), ptr(cur), cur.stride(0), cur.shape[1],
+                ptr(base), base.stride(0), base.shape[1], ptr(o.suff), n_p, n_h, self.pcfg.min_mann_white,
+                self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals), ptr(o.pstats), ptr(self._queue))
+
+    def split_launchers(self, hist, base, cur, n_hist=None, packed_out=None, slot: int = 0,
+                        front_stream=None, decide_stream=None):
+        """Pre-bound launchers of a split tick for one buffer slot: returns
+        (front, decide, outputs).  Each launcher is one foreign call with
+        every argument resolved up front (no tensor inspection per tick), on
+        the stream given here (default: the current stream at creation).  A
+        single-kernel HIP graph buys nothing here: at the 1,250-service shard
+        the graph launch cost 6 % of the step."""
+        from ..ops._lib import LIB
+        o = self.front_only(hist, base, cur, n_hist, packed_out, slot)    # validate / allocate / warm
+        torch.cuda.synchronize(cur.device)
+        T = hist.shape[1] if n_hist is None else int(n_hist)
+        dev = cur.device
+        fs = (front_stream or torch.cuda.current_stream(dev)).cuda_stream
+        ds = (decide_stream or torch.cuda.current_stream(dev)).cuda_stream
+        lib = LIB.load()
+        f_fn, d_fn = lib.fm_tick_front, lib.fm_decide_services
+        f_args = self._front_call_args(hist, base, cur, T, o) + (fs,)
+        d_args = self._decide_call_args(cur, o, True) + (ds,)
+
+        def front() -> None:
+            rc = f_fn(*f_args)
+            if rc:
+                raise RuntimeError(f"fm_tick_front failed with hipError {rc}")
+
+        def decide() -> None:
+            rc = d_fn(*d_args)
+            if rc:
+                raise RuntimeError(f"fm_decide_services failed with hipError {rc}")
+        return front, decide, o
 
     def _fused(self, hist, base, cur, n_hist, o: CanaryOutputs) -> None:
         from ..ops._lib import LIB, ptr, stream_of

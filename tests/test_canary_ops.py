@@ -322,4 +322,22 @@ def test_gpu_split_tick_equals_score(cuda, S, M):
     for i in range(2):
         torch.testing.assert_close(packed[i], ref.packed, rtol=0, atol=0)
         torch.testing.assert_close(fronts[i][1].decide.count, ref.decide.count, rtol=0, atol=0)
+    # pre-bound direct launchers (bench.py default): front on the current
+    # stream, decision on the side stream, slots 2 and 3
+    main = torch.cuda.current_stream()
+    ls = [sc.split_launchers(h, b, c, T, packed_out=packed[i], slot=2 + i, front_stream=main, decide_stream=side)
+          for i in range(2)]
+    for k in range(6):
+        i = k % 2
+        if k >= 2:
+            main.wait_event(done[i])
+        packed[i].fill_(-1.0)
+        ls[i][0]()
+        ev[i].record(main)
+        side.wait_event(ev[i])
+        ls[i][1]()
+        done[i].record(side)
+    torch.cuda.synchronize()
+    for i in range(2):
+        torch.testing.assert_close(packed[i], ref.packed, rtol=0, atol=0)
 
