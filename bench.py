@@ -72,8 +72,9 @@ def main() -> None:
                          "one-kernel HIP graph (measured 6%% slower per step at the 1,250-service shard)")
     ap.add_argument("--front-wgs", default="auto",
                     help="front kernel workgroups per CU, pairwise:history; auto = 1:4 on one GPU, 1:3 on several "
-                         "(leaves a workgroup slot per CU for the previous tick's decision, RCCL all-gather and "
-                         "copy kernels; 1:3 and 1:4 measure within 1%% of each other on one GPU)")
+                         "(1:3 is exactly one resident grid at 4 workgroups per CU, so no front workgroups queue "
+                         "ahead of the previous tick's decision / RCCL all-gather / copy kernels; 1:3 and 1:4 "
+                         "measure within 1%% of each other on one GPU)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace of 5 extra steps (rank 0)")
     args = ap.parse_args()
 
