@@ -1000,6 +1000,17 @@ __device__ __attribute__((noinline)) void eval_test_call(int t, const double* __
   eval_test(t, o, min_mw, min_wil, min_kru, pv, sv);
 }
 
+// FM_FRONT_TIMING builds (tools/front_timing.py): every workgroup of the
+// front kernel records its start / end on the 100 MHz real-time counter, so
+// the critical role (pairwise or history) of a shape can be read off.
+#ifdef FM_FRONT_TIMING
+__device__ unsigned long long g_front_t[2 * 8192];
+#define FM_FT_MARK(k) \
+  do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_front_t[2 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define FM_FT_MARK(k) do {} while (0)
+#endif
+
 template <int NV, int K>
 __global__ __launch_bounds__(256) void tick_front_kernel(
     const float* __restrict__ hist, int64_t ld_h, int T, int64_t R, float* __restrict__ hs /*[R,3]*/,
@@ -1008,6 +1019,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
     float* __restrict__ pvals, float* __restrict__ pstats, unsigned* __restrict__ queue) {
   __shared__ double red[4];
   __shared__ int redi[4];
+  FM_FT_MARK(0);
   if ((int)blockIdx.x < nP) {
     const int64_t first = (int64_t)blockIdx.x * 4, stride = (int64_t)nP * 4;
     for (int64_t row = first + wave_id(); row < R; row += stride) {
@@ -1034,6 +1046,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
         pstats[row * N_TESTS + t] = (float)sv;
       }
     }
+    FM_FT_MARK(1);
     return;
   }
   const int nH = (int)gridDim.x - nP;
@@ -1048,6 +1061,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
         hs[row * 3 + 2] = (float)n;
       }
     }
+    FM_FT_MARK(1);
     return;
   }
   // Dynamic history queue: the rows are split into 8 contiguous ranges, one
@@ -1101,6 +1115,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
       __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  FM_FT_MARK(1);
 }
 
 // nP / nH: workgroups of each role (0 = one pairwise workgroup per 4 rows /
@@ -1589,6 +1604,16 @@ FM_API int fm_selftest_lanes(const int* in, int* out, hipStream_t stream) {
 // Async device -> pinned-host copy of the fleet verdict, issued on the
 // caller's stream so it is captured into the tick's HIP graph as a memcpy
 // node (the whole step — tick, all-gather, host copy — is one graph launch).
+FM_API int fm_front_timing_read(unsigned long long* host, int n) {
+#ifdef FM_FRONT_TIMING
+  if (n > 2 * 8192) n = 2 * 8192;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_front_t), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+#else
+  (void)host; (void)n;
+  return (int)hipErrorNotSupported;
+#endif
+}
+
 FM_API int fm_copy_d2h_async(void* dst, const void* src, int64_t bytes, hipStream_t stream) {
   if (bytes <= 0) return 0;
   return (int)hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, stream);
