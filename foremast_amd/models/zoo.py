@@ -249,3 +249,26 @@ def make_tables(aliases_per_row: list[str], cfg, device) -> Tables:
                   torch.tensor([r.bound for r in rules], dtype=torch.int32, device=device),
                   torch.tensor([r.min_lower_bound for r in rules], dtype=torch.float32, device=device),
                   cfg.pairwise_threshold_factor, cfg.min_historical_points)
+
+
+def rolling_bands(hist: torch.Tensor, T: int, M: int, tables: Tables, window: int = 60,
+                  min_count: int | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """moving_average bands at every time point of the history (the
+    dashboard's metric bands, foremast-dashboard/src/config/metrics.js:21-29):
+    center = trailing-window mean, upper = center + thr * std, lower =
+    max(center - thr * std, min_lower_bound), with the metric's bound code
+    masking the side it does not judge (NaN).  Row r uses table entry r % M.
+    Returns (center, upper, lower) [R, T] fp32 (K1 rolling kernel on GPU)."""
+    from ..ops import misc as MI
+    mc = tables.min_hist if min_count is None else min_count
+    w = max(1, min(int(window), MI.ROLLING_MAX_WINDOW, T))
+    mean, sd = MI.rolling_stats(hist, T, w, max(1, min(mc, w)))
+    R = hist.shape[0]
+    idx = torch.arange(R, device=mean.device) % M
+    thr = tables.thr.to(mean.device)[idx].unsqueeze(1)
+    bd = tables.bound.to(mean.device)[idx].unsqueeze(1)
+    mlb = tables.minlb.to(mean.device)[idx].unsqueeze(1)
+    nan = torch.full_like(mean, float("nan"))
+    up = torch.where((bd & 1) != 0, mean + thr * sd, nan)
+    lo = torch.where((bd & 2) != 0, torch.maximum(mean - thr * sd, mlb.expand_as(mean)), nan)
+    return mean, up, lo

@@ -247,3 +247,51 @@ def segment_max(v: torch.Tensor, seg: torch.Tensor, K: int) -> torch.Tensor:
     out = torch.empty((K,), dtype=torch.float32, device=v.device)
     LIB.call("fm_segment_max", ptr(v.contiguous()), ptr(seg.contiguous()), v.numel(), K, ptr(out), stream_of(v))
     return out
+
+
+# ---------------------------------------------------------------------------
+# K1 rolling bands (csrc/kernels/rolling.hip)
+# ---------------------------------------------------------------------------
+ROLLING_MAX_WINDOW = 2048
+
+
+def rolling_stats(x: torch.Tensor, T: int, w: int, min_count: int = 1) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-time-point mean and population std of the finite samples in the
+    trailing window [t - w + 1, t] of every row of ``x[:, :T]`` (NaN where
+    the window holds fewer than ``min_count`` finite samples).  Returns
+    (mean [R, T], std [R, T]) fp32."""
+    check(1 <= w <= ROLLING_MAX_WINDOW, f"rolling window must be in [1, {ROLLING_MAX_WINDOW}]")
+    check(0 < T <= x.shape[1], "T must be within the row length")
+    if not x.is_cuda:
+        m, s = ref_rolling_stats(x.numpy()[:, :T], w, min_count)
+        return torch.from_numpy(m), torch.from_numpy(s)
+    require_native(x)
+    check(x.dtype == torch.float32 and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0,
+          "rows must be fp32, contiguous and 16-B aligned")
+    R = x.shape[0]
+    mean = torch.empty((R, T), dtype=torch.float32, device=x.device)
+    sd = torch.empty((R, T), dtype=torch.float32, device=x.device)
+    LIB.call("fm_rolling_stats", ptr(x), x.stride(0), T, R, w, int(min_count), ptr(mean), ptr(sd), T, stream_of(x))
+    return mean, sd
+
+
+def ref_rolling_stats(x: np.ndarray, w: int, min_count: int = 1) -> tuple[np.ndarray, np.ndarray]:
+    """fp64 oracle: windowed sums from prefix sums of the finite-sample mask,
+    the values and their squares about the row mean."""
+    x = np.asarray(x, dtype=np.float64)
+    f = np.isfinite(x)
+    cnt_all = f.sum(1, keepdims=True)
+    c = np.where(cnt_all > 0, np.where(f, x, 0.0).sum(1, keepdims=True) / np.maximum(cnt_all, 1), 0.0)
+    d = np.where(f, x - c, 0.0)
+
+    def win(a):
+        p = np.cumsum(a, axis=1)
+        out = p.copy()
+        out[:, w:] -= p[:, :-w]
+        return out
+    n, s, q = win(f.astype(np.float64)), win(d), win(d * d)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        m = s / n
+        var = np.maximum(q / n - m * m, 0.0)
+    ok = (n >= min_count) & (n > 0)
+    return (np.where(ok, c + m, np.nan).astype(np.float32), np.where(ok, np.sqrt(var), np.nan).astype(np.float32))
