@@ -5,21 +5,24 @@
 // over the brain's moving_average window; deploy/foremast/3_brain/
 // foremast-brain.yaml:24-25 names the algorithm).
 //
-// One 256-thread workgroup per row walks it in tiles of 2048 samples (8
-// contiguous samples per thread, two 16-B loads).  Per tile: thread-local
-// prefix sums of (count, d, d^2) with d = x - c (c = mean of the row's first
-// tile, so the squares do not swamp the variance), a wave scan on DPP and a
-// 4-entry cross-wave pass, and the tile-local prefixes go to an LDS ring of
-// two tiles (counts uint16, sums fp64: 72 KB, two workgroups per CU).  The
-// next tile's samples are loaded while this tile's outputs are written.  A window
-// sum is then P[t] - P[t - w]: both ends sit in this tile or the previous one
-// (w <= 2048), so only the previous tile's totals bridge the two and every
-// prefix stays tile-local (no row-long running sum).  The sums are fp64 because
-// a fp32 prefix difference over a 2048-sample tile loses ~2048 ulps of the
-// tile's sum of squares: for a 1-point window that is a std of 1 % of the
-// row's instead of 0.  Outputs are written one sample per thread per
-// 256-wide stripe: coalesced.  HBM traffic: the row read once, the two bands
-// written once.
+// One 256-thread workgroup per row walks it in tiles of 2048 samples; thread
+// i owns the 8 contiguous samples / outputs [8i, 8i + 8) of a tile (two 16-B
+// loads, two 16-B stores per band).  Per tile: the shifted samples d = x - c
+// (c = mean of the row's first tile, so squares do not swamp the variance;
+// NaN kept for missing samples) go to an LDS ring of two tiles, a block scan
+// gives each thread the tile-local exclusive prefix of (count, sum d, sum d^2)
+// (sums fp64), and those 256 prefixes go to a second small ring.  A thread's
+// first window sum is P(t0) - P(t0 - w): P(t0) is its own prefix, P(t0 - w)
+// the owner segment's prefix plus up to 8 ring samples.  Its next 7 windows
+// slide in registers (+ own sample, - the sample leaving the window).
+// Because t0 is a multiple of 8, the offset (t0 - w) mod 8 = (-w) mod 8 is the
+// same for every thread, so the leaving samples are a fixed rotation of two
+// ring segments (a switch on a uniform value).  w <= 2048 keeps every window
+// inside this tile and the previous one, bridged by the previous tile's
+// totals, so prefixes stay tile-local.  LDS 26 KB: several workgroups per CU
+// keep enough rows in flight (a first version held full fp64 prefix rings,
+// 72 KB, two workgroups per CU: 2.45 TB/s).  HBM traffic: the row read once,
+// the two bands written once.
 #include "fm_common.h"
 
 using namespace fm;
@@ -27,7 +30,7 @@ using namespace fm;
 namespace {
 
 constexpr int kTile = 2048;           // samples per tile = 256 threads x 8
-constexpr int kRing = 2 * kTile;      // LDS ring: this tile + the previous one
+constexpr int kRing = 2 * kTile;      // sample ring: this tile + the previous one
 
 struct Tri {
   float n;
@@ -50,11 +53,20 @@ __device__ __forceinline__ Tri block_incl_scan(Tri v, Tri* scratch, Tri& total) 
   return tri_add(w, off);
 }
 
-__global__ __launch_bounds__(256) void rolling_stats_kernel(const float* __restrict__ x, int64_t ld_x, int T,
+// contributions of one (shifted) sample: finite count, d, d^2
+__device__ __forceinline__ void contrib(float d, float& n, float& s, float& q) {
+  const bool f = isfinite(d);
+  n = f ? 1.f : 0.f;
+  s = f ? d : 0.f;
+  q = s * s;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void rolling_stats_kernel(const float* __restrict__ x, int64_t ld_x, int T,
                                                             int w, int min_count, float* __restrict__ mean,
                                                             float* __restrict__ sd, int64_t ld_o) {
-  __shared__ unsigned short pn[kRing];
-  __shared__ double ps[kRing], pq[kRing];
+  __shared__ float4 ring4[kRing / 4];              // shifted samples (NaN = missing)
+  __shared__ float exn[2 * 256];                    // per-thread exclusive prefixes, two tiles
+  __shared__ double exs[2 * 256], exq[2 * 256];
   __shared__ Tri scratch[4];
   __shared__ double red[4];
   const int64_t row = blockIdx.x;
@@ -63,9 +75,7 @@ __global__ __launch_bounds__(256) void rolling_stats_kernel(const float* __restr
   float* __restrict__ sr = sd + row * ld_o;
   const int tid = threadIdx.x;
   const float NaNf = __builtin_nanf("");
-  float c = 0.f;
-  Tri prev_total{0.f, 0.0, 0.0};
-  // 8 contiguous samples per thread
+  const float* ring = reinterpret_cast<const float*>(ring4);
   auto load8 = [&](int tb, float (&v)[8]) {
     const int e0 = tb + 8 * tid;
     if (e0 + 8 <= T) {
@@ -77,80 +87,127 @@ __global__ __launch_bounds__(256) void rolling_stats_kernel(const float* __restr
       for (int k = 0; k < 8; ++k) v[k] = e0 + k < T ? xr[e0 + k] : NaNf;
     }
   };
+  const int r = (-w) & 7;                     // (t0 - w) mod 8, the same for every thread
+  const int segback = (w + r) >> 3;           // owner segment of t0 - w is (own segment) - segback
+  float c = 0.f;
+  Tri prev_total{0.f, 0.0, 0.0};
   float nx[8];
   load8(0, nx);
   for (int tb = 0, tile = 0; tb < T; tb += kTile, ++tile) {
-    float v[8];
+    float d[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = nx[k];
+    for (int k = 0; k < 8; ++k) d[k] = nx[k];
     if (tb + kTile < T) load8(tb + kTile, nx);   // in flight while this tile is scanned and written
     if (tile == 0) {
-      // shift: mean of the first tile's finite samples
       float ls = 0.f, lc = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (isfinite(v[k])) { ls += v[k]; lc += 1.f; }
+        if (isfinite(d[k])) { ls += d[k]; lc += 1.f; }
       const double s = block_sum<256>((double)ls, red);
       const double n = block_sum<256>((double)lc, red);
       c = n > 0 ? (float)(s / n) : 0.f;
     }
-    // thread-local inclusive prefixes (8 terms: fp32 is exact enough)
-    float ln[8], ls[8], lq[8];
     float an = 0.f, as = 0.f, aq = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const bool f = isfinite(v[k]);
-      const float d = f ? v[k] - c : 0.f;
-      an += f ? 1.f : 0.f;
-      as += d;
-      aq = fmaf(d, d, aq);
-      ln[k] = an; ls[k] = as; lq[k] = aq;
+      d[k] = d[k] - c;                        // NaN stays NaN
+      float n, s, q;
+      contrib(d[k], n, s, q);
+      an += n; as += s; aq = fmaf(s, s, aq);
     }
+    const int half = tile & 1;
+    ring4[half * (kTile / 4) + 2 * tid] = make_float4(d[0], d[1], d[2], d[3]);
+    ring4[half * (kTile / 4) + 2 * tid + 1] = make_float4(d[4], d[5], d[6], d[7]);
     Tri total;
     const Tri incl = block_incl_scan(Tri{an, (double)as, (double)aq}, scratch, total);
     const float en = incl.n - an;
     const double es = incl.s - (double)as, eq = incl.q - (double)aq;
-    const int rb = (tile & 1) * kTile;
+    exn[half * 256 + tid] = en;
+    exs[half * 256 + tid] = es;
+    exq[half * 256 + tid] = eq;
+    __syncthreads();
+    // P(t0 - w), relative to this tile's carry, and the 8 samples leaving
+    // the 8 windows: positions g0 .. g0 + 7 (g0 = t0 - w)
+    const int seg = (tb >> 3) + tid - segback;        // global owner segment of g0 (may be < 0)
+    float lv[16];
+    double pn = 0.0, ps = 0.0, pq = 0.0;
+    if (seg + 1 >= 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int sg = seg + h;
+        float4 a = make_float4(NaNf, NaNf, NaNf, NaNf), b = a;
+        if (sg >= 0) {
+          const int rbase = ((sg >> 8) & 1) * (kTile / 4) + (sg & 255) * 2;
+          a = ring4[rbase];
+          b = ring4[rbase + 1];
+        }
+        lv[8 * h + 0] = a.x; lv[8 * h + 1] = a.y; lv[8 * h + 2] = a.z; lv[8 * h + 3] = a.w;
+        lv[8 * h + 4] = b.x; lv[8 * h + 5] = b.y; lv[8 * h + 6] = b.z; lv[8 * h + 7] = b.w;
+      }
+      if (seg >= 0) {
+        const int eh = ((seg >> 8) & 1) * 256 + (seg & 255);
+        pn = exn[eh]; ps = exs[eh]; pq = exq[eh];
+        float sn = 0.f, ss = 0.f, sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float n, s, q;
+          contrib(lv[i], n, s, q);
+          if (i <= r) { sn += n; ss += s; sq = fmaf(s, s, sq); }
+        }
+        pn += sn; ps += ss; pq += sq;
+        if ((seg >> 8) != tile) { pn -= prev_total.n; ps -= prev_total.s; pq -= prev_total.q; }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) lv[i] = NaNf;
+    }
+    // leaving sample of window k is lv[r + 1 + k] (k < 7 slides); rotate by the uniform r
+    float out[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = lv[k + 8];
+    switch (r) {
+#define FM_ROT(RR) case RR: _Pragma("unroll") for (int k = 0; k < 8; ++k) out[k] = lv[RR + 1 + k < 16 ? RR + 1 + k : 15]; break;
+      FM_ROT(0) FM_ROT(1) FM_ROT(2) FM_ROT(3) FM_ROT(4) FM_ROT(5) FM_ROT(6) FM_ROT(7)
+#undef FM_ROT
+    }
+    // window 0 = P(t0) - P(g0); window k = window k-1 + own d[k] - leaving out[k-1]
+    double wn = (double)en - pn, ws = es - ps, wq = eq - pq;
+    float om[8], os[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int i = rb + 8 * tid + k;
-      pn[i] = (unsigned short)(en + ln[k]);
-      ps[i] = es + (double)ls[k];
-      pq[i] = eq + (double)lq[k];
-    }
-    __syncthreads();
-    // outputs of this tile: one per thread per 256-wide stripe
-    const int pb = ((tile + 1) & 1) * kTile;   // ring base of the previous tile
-#pragma unroll 2
-    for (int j = tid; j < kTile; j += 256) {
-      const int t = tb + j;
-      if (t >= T) break;
-      float n = (float)pn[rb + j];
-      double s = ps[rb + j], q = pq[rb + j];
-      const int u = j - w;     // t - w, relative to this tile
-      if (u >= 0) {
-        n -= (float)pn[rb + u]; s -= ps[rb + u]; q -= pq[rb + u];
-      } else if (t - w >= 0) {
-        // the window starts in the previous tile: its prefix there is
-        // P_prev[u + kTile], and the previous tile's total bridges the two
-        n += prev_total.n - (float)pn[pb + u + kTile];
-        s += prev_total.s - ps[pb + u + kTile];
-        q += prev_total.q - pq[pb + u + kTile];
-      }   // else t < w: the window is [0, t], whose prefix is already tile 0's
-      if (n >= (float)min_count && n > 0.f) {
-        const double inv = 1.0 / (double)n;
-        const double m = s * inv;
-        const double var = fmax(q * inv - m * m, 0.0);
-        mr[t] = c + (float)m;
-        sr[t] = (float)sqrt(var);
+      float n, s, q;
+      contrib(d[k], n, s, q);
+      wn += n; ws += s; wq += q;
+      if (k > 0) {
+        contrib(out[k - 1], n, s, q);
+        wn -= n; ws -= s; wq -= q;
+      }
+      if (wn >= (double)min_count && wn > 0.5) {
+        // wn is an integer <= 2048: a 1-ulp fp32 reciprocal is exact enough,
+        // and the moments stay fp64 until the variance is formed (no fp64
+        // divide / sqrt sequences per output)
+        const double inv = (double)__builtin_amdgcn_rcpf((float)wn);
+        const double m = ws * inv;
+        om[k] = c + (float)m;
+        os[k] = sqrtf((float)fmax(fma(-m, m, wq * inv), 0.0));
       } else {
-        mr[t] = NaNf;
-        sr[t] = NaNf;
+        om[k] = NaNf;
+        os[k] = NaNf;
       }
     }
+    const int t0 = tb + 8 * tid;
+    if (t0 + 8 <= T && (ld_o & 3) == 0) {
+      *reinterpret_cast<float4*>(mr + t0) = make_float4(om[0], om[1], om[2], om[3]);
+      *reinterpret_cast<float4*>(mr + t0 + 4) = make_float4(om[4], om[5], om[6], om[7]);
+      *reinterpret_cast<float4*>(sr + t0) = make_float4(os[0], os[1], os[2], os[3]);
+      *reinterpret_cast<float4*>(sr + t0 + 4) = make_float4(os[4], os[5], os[6], os[7]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (t0 + k < T) { mr[t0 + k] = om[k]; sr[t0 + k] = os[k]; }
+    }
     prev_total = total;
-    // the next tile overwrites the ring half this tile's outputs read as
-    // "previous": wait for every output of this tile first
+    // the next tile overwrites the ring half this tile read as "previous"
     __syncthreads();
   }
 }
