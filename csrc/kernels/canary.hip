@@ -24,14 +24,26 @@ namespace {
 
 constexpr float kPad = INFINITY;
 
-template <int K>
+// SPLIT (K == 2 only): register 0 holds sample 1 and register 1 sample 2
+// (each <= 64 values).  Every stage up to size 64 then stays inside one
+// register, so a value's sample is its register index and the tags need no
+// exchange; they are rebuilt (k, or -1 for pads) before the final 128-merge.
+// That drops the tag exchange and select from 21 of the 27 lane-exchange
+// steps.
+template <int K, bool SPLIT = false>
 __device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
   // Branch-free compare-exchange (selects, no exec-mask branches): strides
   // >= 64 swap registers inside the lane, smaller strides exchange with the
   // partner lane through DPP / permlane (xor_lane_any).
+  static_assert(!SPLIT || K == 2, "split layout is two 64-lane registers");
   const int lane = lane_id();
 #pragma unroll
   for (int size = 2; size <= 64 * K; size <<= 1) {
+    const bool tags = !SPLIT || size > 64;
+    if (SPLIT && size == 128) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) tag[k] = v[k] == kPad ? -1 : k;
+    }
 #pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       if (stride >= 64) {
@@ -55,7 +67,10 @@ __device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
         float ov[K];
         int ot[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) { ov[k] = xor_lane_any(v[k], stride); ot[k] = xor_lane_any(tag[k], stride); }
+        for (int k = 0; k < K; ++k) {
+          ov[k] = xor_lane_any(v[k], stride);
+          ot[k] = tags ? xor_lane_any(tag[k], stride) : 0;
+        }
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const int i = k * 64 + lane;
@@ -68,7 +83,7 @@ __device__ __forceinline__ void bitonic_sort(float (&v)[K], int (&tag)[K]) {
           const bool vlt = v[k] < ov[k];
           const float mn = vlt ? v[k] : ov[k], mx = vlt ? ov[k] : v[k];
           const float nv = keep_min ? mn : mx;
-          tag[k] = nv != v[k] ? ot[k] : tag[k];
+          if (tags) tag[k] = nv != v[k] ? ot[k] : tag[k];
           v[k] = nv;
         }
       }
@@ -139,14 +154,21 @@ struct PwIn {
   float pb[KW];
 };
 
-template <int K>
+// SPLIT (K == 2, n_cur <= 64, n_base <= 64): v[0] = current, v[1] = baseline
+// instead of the pooled order (see bitonic_sort).
+template <int K, bool SPLIT = false>
 __device__ __forceinline__ void pw_load(const float* __restrict__ c, const float* __restrict__ b, int n_cur,
                                         int n_base, PwIn<K>& in) {
   const int lane = lane_id();
+  if constexpr (SPLIT) {
+    in.v[0] = lane < n_cur ? c[lane] : kPad;
+    in.v[1] = lane < n_base ? b[lane] : kPad;
+  } else {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int i = k * 64 + lane;
-    in.v[k] = i < n_cur ? c[i] : (i < n_cur + n_base ? b[i - n_cur] : kPad);
+    for (int k = 0; k < K; ++k) {
+      const int i = k * 64 + lane;
+      in.v[k] = i < n_cur ? c[i] : (i < n_cur + n_base ? b[i - n_cur] : kPad);
+    }
   }
   const int npair = n_cur < n_base ? n_cur : n_base;
 #pragma unroll
@@ -157,7 +179,7 @@ __device__ __forceinline__ void pw_load(const float* __restrict__ c, const float
   }
 }
 
-template <int K>
+template <int K, bool SPLIT = false>
 __device__ __forceinline__ void pw_compute(PwIn<K>& in, int n_cur, int n_base, double* __restrict__ o) {
   // Everything exact is carried in integers (counts, doubled rank sums, tie
   // terms, the KS numerator); only the Welch moments are floating point.
@@ -169,7 +191,7 @@ __device__ __forceinline__ void pw_compute(PwIn<K>& in, int n_cur, int n_base, d
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int i = k * 64 + lane;
-    int t = i < n_cur ? 0 : (i < n_cur + n_base ? 1 : -1);
+    int t = SPLIT ? (lane < (k == 0 ? n_cur : n_base) ? k : -1) : (i < n_cur ? 0 : (i < n_cur + n_base ? 1 : -1));
     float x = v[k];
     if (!isfinite(x)) { x = kPad; t = -1; }
     v[k] = x; tag[k] = t;
@@ -212,7 +234,7 @@ __device__ __forceinline__ void pw_compute(PwIn<K>& in, int n_cur, int n_base, d
   cwz = wave_sum(cwz);
   const int nw = cwz & 0x3FF, npos = (cwz >> 10) & 0x3FF, nzero = cwz >> 20;
 
-  bitonic_sort<K>(v, tag);
+  bitonic_sort<K, SPLIT>(v, tag);
   int rk2[K];
   bool en[K];
   int tie = 0;
@@ -411,6 +433,23 @@ __device__ __forceinline__ void pw_compute_count(PwIn<K>& in, int n_cur, int n_b
   }
 }
 
+// One row's sufficient statistics (sort form): the split layout when both
+// samples fit one register each (the usual 5 pods x 10 points per side).
+template <int K>
+__device__ __forceinline__ void pw_row(const float* __restrict__ c, const float* __restrict__ b, int n_cur,
+                                       int n_base, double* __restrict__ o) {
+  PwIn<K> in;
+  if constexpr (K == 2) {
+    if (n_cur <= 64 && n_base <= 64) {
+      pw_load<K, true>(c, b, n_cur, n_base, in);
+      pw_compute<K, true>(in, n_cur, n_base, o);
+      return;
+    }
+  }
+  pw_load<K>(c, b, n_cur, n_base, in);
+  pw_compute<K>(in, n_cur, n_base, o);
+}
+
 template <int K>
 __global__ __launch_bounds__(256) void pairwise_count_kernel(
     const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
@@ -434,9 +473,7 @@ __global__ __launch_bounds__(256) void pairwise_kernel(
     const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
     int n_base, int64_t R, double* __restrict__ suff) {
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave_id(); row < R; row += (int64_t)gridDim.x * 4) {
-    PwIn<K> in;
-    pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
-    pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+    pw_row<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, suff + row * kSuff);
   }
 }
 
@@ -461,7 +498,17 @@ __global__ __launch_bounds__(256) void canary_row_kernel(
   const int lane = lane_id();
   const bool do_pw = n_base > 0;
   PwIn<K> in;
-  if (do_pw) pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
+  // same layout choice as pw_row, so every tick mode sums the Welch moments
+  // in the same order (bit-identical p-values across modes)
+  const bool split = K == 2 && n_cur <= 64 && n_base <= 64;
+  if (do_pw) {
+    if constexpr (K == 2) {
+      if (split) pw_load<K, true>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
+      else pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
+    } else {
+      pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
+    }
+  }
 
   typedef float nt4 __attribute__((ext_vector_type(4)));
   const nt4* h = reinterpret_cast<const nt4*>(hist + row * ld_h);
@@ -477,7 +524,14 @@ __global__ __launch_bounds__(256) void canary_row_kernel(
     q[j] = __builtin_nontemporal_load(h + (qi < nq ? qi : nq - 1));
   }
 
-  if (do_pw) pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+  if (do_pw) {
+    if constexpr (K == 2) {
+      if (split) pw_compute<K, true>(in, n_cur, n_base, suff + row * kSuff);
+      else pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+    } else {
+      pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+    }
+  }
 
   float ls = 0.f;
   int cnt = 0;
@@ -1023,9 +1077,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
   if ((int)blockIdx.x < nP) {
     const int64_t first = (int64_t)blockIdx.x * 4, stride = (int64_t)nP * 4;
     for (int64_t row = first + wave_id(); row < R; row += stride) {
-      PwIn<K> in;
-      pw_load<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, in);
-      pw_compute<K>(in, n_cur, n_base, suff + row * kSuff);
+      pw_row<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, suff + row * kSuff);
     }
     __syncthreads();   // this workgroup's suff rows are visible to all its waves
     // local row j -> global row first + (j & 3) + (j >> 2) * stride
