@@ -990,15 +990,23 @@ FM_API int fm_stats_decide(const float* hist, int64_t ld_h, int T, const float* 
 // row, reads only the small current window) applies the diff-dependent
 // thresholds once both are done.
 // ---------------------------------------------------------------------------
+// History row of logical row `row`: identity, or a slot of the brain's
+// device-resident history store (engine/resident.py) when a row map is given.
+// The row index is wave-uniform, so the map read is one scalar load.
+__device__ __forceinline__ int64_t hist_row(const int* __restrict__ rowmap, int64_t row) {
+  return rowmap != nullptr ? (int64_t)rowmap[row] : row;
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void hist_stats_kernel(const float* __restrict__ hist, int64_t ld_h, int T,
-                                                         int64_t R, float* __restrict__ out /*[R,3]*/) {
+                                                         int64_t R, float* __restrict__ out /*[R,3]*/,
+                                                         const int* __restrict__ rowmap) {
   __shared__ double red[4];
   __shared__ int redi[4];
   for (int64_t row = blockIdx.x; row < R; row += gridDim.x) {
     float mf, sd;
     int n;
-    block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
+    block_row_stats<NV>(hist + hist_row(rowmap, row) * ld_h, T, red, redi, mf, sd, n);
     if (threadIdx.x == 0) {
       out[row * 3 + 0] = mf;
       out[row * 3 + 1] = sd;
@@ -1007,13 +1015,13 @@ __global__ __launch_bounds__(256) void hist_stats_kernel(const float* __restrict
   }
 }
 
-FM_API int fm_hist_stats_capped(const float* hist, int64_t ld_h, int T, int64_t R, float* out, int max_blocks,
-                                hipStream_t stream) {
+FM_API int fm_hist_stats_rm(const float* hist, int64_t ld_h, int T, int64_t R, float* out, int max_blocks,
+                            const int* rowmap, hipStream_t stream) {
   if (R <= 0) return 0;
   if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
   const int nq = (T + 3) / 4;
   const dim3 grid((unsigned)(max_blocks > 0 && R > max_blocks ? max_blocks : R)), block(256);
-#define FM_HS(NVV) hipLaunchKernelGGL(hist_stats_kernel<NVV>, grid, block, 0, stream, hist, ld_h, T, R, out)
+#define FM_HS(NVV) hipLaunchKernelGGL(hist_stats_kernel<NVV>, grid, block, 0, stream, hist, ld_h, T, R, out, rowmap)
   if (nq <= 256 * 2) FM_HS(2);
   else if (nq <= 256 * 4) FM_HS(4);
   else if (nq <= 256 * 8) FM_HS(8);
@@ -1026,8 +1034,13 @@ FM_API int fm_hist_stats_capped(const float* hist, int64_t ld_h, int T, int64_t 
   return 0;
 }
 
+FM_API int fm_hist_stats_capped(const float* hist, int64_t ld_h, int T, int64_t R, float* out, int max_blocks,
+                                hipStream_t stream) {
+  return fm_hist_stats_rm(hist, ld_h, T, R, out, max_blocks, nullptr, stream);
+}
+
 FM_API int fm_hist_stats(const float* hist, int64_t ld_h, int T, int64_t R, float* out, hipStream_t stream) {
-  return fm_hist_stats_capped(hist, ld_h, T, R, out, 0, stream);
+  return fm_hist_stats_rm(hist, ld_h, T, R, out, 0, nullptr, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -1070,7 +1083,8 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
     const float* __restrict__ hist, int64_t ld_h, int T, int64_t R, float* __restrict__ hs /*[R,3]*/,
     const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
     int n_base, double* __restrict__ suff, int nP, int min_mw, int min_wil, int min_kru,
-    float* __restrict__ pvals, float* __restrict__ pstats, unsigned* __restrict__ queue) {
+    float* __restrict__ pvals, float* __restrict__ pstats, unsigned* __restrict__ queue,
+    const int* __restrict__ rowmap) {
   __shared__ double red[4];
   __shared__ int redi[4];
   FM_FT_MARK(0);
@@ -1106,7 +1120,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
     for (int64_t row = (int64_t)blockIdx.x - nP; row < R; row += nH) {
       float mf, sd;
       int n;
-      block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
+      block_row_stats<NV>(hist + hist_row(rowmap, row) * ld_h, T, red, redi, mf, sd, n);
       if (threadIdx.x == 0) {
         hs[row * 3 + 0] = mf;
         hs[row * 3 + 1] = sd;
@@ -1148,7 +1162,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
     for (int64_t row = r0; row < r1; ++row) {
       float mf, sd;
       int n;
-      block_row_stats<NV>(hist + row * ld_h, T, red, redi, mf, sd, n);
+      block_row_stats<NV>(hist + hist_row(rowmap, row) * ld_h, T, red, redi, mf, sd, n);
       if (threadIdx.x == 0) {
         hs[row * 3 + 0] = mf;
         hs[row * 3 + 1] = sd;
@@ -1172,10 +1186,10 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
 
 // nP / nH: workgroups of each role (0 = one pairwise workgroup per 4 rows /
 // one history workgroup per row); queue: dynamic history rows (or nullptr).
-FM_API int fm_tick_front(const float* hist, int64_t ld_h, int T, int64_t R, float* hs, const float* cur, int64_t ld_c,
-                         int n_cur, const float* base, int64_t ld_b, int n_base, double* suff, int nP, int nH,
-                         int min_mw, int min_wil, int min_kru, float* pvals, float* pstats, unsigned* queue,
-                         hipStream_t stream) {
+FM_API int fm_tick_front_rm(const float* hist, int64_t ld_h, int T, int64_t R, float* hs, const float* cur,
+                            int64_t ld_c, int n_cur, const float* base, int64_t ld_b, int n_base, double* suff, int nP,
+                            int nH, int min_mw, int min_wil, int min_kru, float* pvals, float* pstats,
+                            unsigned* queue, const int* rowmap, hipStream_t stream) {
   if (R <= 0) return 0;
   if ((ld_h & 3) != 0 || (((uintptr_t)hist) & 15) != 0) return (int)hipErrorInvalidValue;
   const int n = n_cur + n_base;
@@ -1190,7 +1204,7 @@ FM_API int fm_tick_front(const float* hist, int64_t ld_h, int T, int64_t R, floa
   const dim3 grid((unsigned)(nP + nH)), block(256);
 #define FM_TF(NVV, KK)                                                                                             \
   hipLaunchKernelGGL((tick_front_kernel<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c, n_cur, \
-                     base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue)
+                     base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap)
 #define FM_TF_K(NVV)           \
   do {                         \
     if (n <= 64) FM_TF(NVV, 1);  \
@@ -1208,6 +1222,14 @@ FM_API int fm_tick_front(const float* hist, int64_t ld_h, int T, int64_t R, floa
 #undef FM_TF
   FM_LAUNCH_CHECK();
   return 0;
+}
+
+FM_API int fm_tick_front(const float* hist, int64_t ld_h, int T, int64_t R, float* hs, const float* cur, int64_t ld_c,
+                         int n_cur, const float* base, int64_t ld_b, int n_base, double* suff, int nP, int nH,
+                         int min_mw, int min_wil, int min_kru, float* pvals, float* pstats, unsigned* queue,
+                         hipStream_t stream) {
+  return fm_tick_front_rm(hist, ld_h, T, R, hs, cur, ld_c, n_cur, base, ld_b, n_base, suff, nP, nH, min_mw, min_wil,
+                          min_kru, pvals, pstats, queue, nullptr, stream);
 }
 
 __global__ __launch_bounds__(256) void window_decide_kernel(

@@ -111,9 +111,11 @@ class Brain:
     def __init__(self, store, cfg: BrainConfig | None = None, device="cpu", sources: SourceRouter | None = None,
                  worker_id: str | None = None, batch_size: int = 512, exporter: BrainExporter | None = None,
                  clock=time.time, step: float = 60.0, watch_minutes: float = 10.0, fetch_threads: int = 16,
-                 lstm_model=None):
+                 lstm_model=None, resident_history: bool | None = None):
         self.store = store
         self.cfg = cfg or BrainConfig()
+        if resident_history is None:
+            resident_history = os.environ.get("RESIDENT_HISTORY", "1") not in ("0", "false", "False")
         self.device = torch.device(device)
         self.sources = sources or SourceRouter()
         self.worker = worker_id or f"{socket.gethostname()}-{os.getpid()}"
@@ -124,13 +126,19 @@ class Brain:
         self.watch_s = watch_minutes * 60.0
         self.fetch_threads = fetch_threads
         self.lstm_model = lstm_model
-        self.hpa_state: dict[str, MI.HpaState] = {}
         from ..models.cache import ModelCache
         self.model_cache = ModelCache(self.cfg.max_cache_size, self.cfg.model_refit_seconds)
         self.info = D.env_info() if D.is_dist() else D.DistInfo()
         from ..utils.spans import Spans
         self.spans = Spans(exporter.registry if exporter is not None else None)
         zoo.canonical(self.cfg.ml_algorithm)   # validate early
+        from .fastpath import FastPath, HpaTable
+        # moving_average_all jobs: device-resident history + the benchmarked
+        # tick (engine/fastpath.py); RESIDENT_HISTORY=0 sends every job
+        # through the general model-zoo path
+        self.fast = FastPath(self) if resident_history else None
+        self.hpa = self.fast.hpa if self.fast is not None else HpaTable(self.device)
+        self.cycles = 0
 
     def _executor(self) -> ThreadPoolExecutor:
         # one long-lived fetch pool (I/O-bound metric queries); spawning a pool
@@ -144,6 +152,9 @@ class Brain:
         if self.info.world <= 1:
             return True
         return D.service_owner(doc.namespace, doc.app_name, self.info.world) == self.info.rank
+
+    def _shard(self) -> tuple[int, int] | None:
+        return (self.info.rank, self.info.world) if self.info.world > 1 else None
 
     # ------------------------------------------------------------------ fetch
     def _windows(self, doc: Document, now: float) -> dict[str, tuple[float, float]]:
@@ -292,52 +303,136 @@ class Brain:
 
     # ------------------------------------------------------------------ cycle
     def run_once(self) -> dict:
+        """One brain cycle.  Collective discipline under DP: every rank calls
+        the export sync exactly once per cycle, from ``finally`` (a cycle that
+        raises still joins it, so the ranks' collective sequences never
+        diverge); there is no other per-cycle collective."""
         t0 = time.perf_counter()
+        self.cycles += 1
+        try:
+            return self._cycle(t0)
+        finally:
+            if self.exporter is not None and D.is_dist():
+                with self.spans.span("export_sync"):
+                    self.exporter.sync()
+
+    def _cycle(self, t0: float) -> dict:
         now = self.clock()
-        docs = self.store.claim(self.worker, self.batch_size, self.cfg.max_stuck_seconds, now=now, owner=self._owner)
+        with self.spans.span("claim"):
+            docs = self.store.claim(self.worker, self.batch_size, self.cfg.max_stuck_seconds, now=now,
+                                    shard=self._shard())
         if not docs:
-            # ranks without work still join the tick's collective
-            fleet = self._gather([])
-            return {"claimed": 0, "fleet": len(fleet)}
+            return {"claimed": 0}
+        fast, rest = (self.fast.prepare(docs, now) if self.fast is not None else ([], docs))
         with self.spans.span("fetch"):
-            works = list(self._executor().map(lambda d: self._fetch_job(d, now), docs))
+            ex = self._executor()
+            ff = [ex.submit(self.fast.fetch, fw, now) for fw in fast]
+            works = list(ex.map(lambda d: self._fetch_job(d, now), rest))
+            fast = [f.result() for f in ff]
+        updates: list = []
+        hpalogs: list = []
+        outcome: dict = {}
+        n_rows = 0
+        if fast:
+            n_rows += self._run_fast(fast, now, updates, hpalogs, outcome)
+        if works:
+            n_rows += self._run_general(works, now, updates, hpalogs, outcome)
+        with self.spans.span("persist"):
+            if hpalogs:
+                self.store.add_hpalogs(hpalogs)
+            self.store.update_many(updates)
+        if self.exporter is not None:
+            self.exporter.tick_seconds.observe(time.perf_counter() - t0)
+            self.exporter.windows.inc(n_rows)
+            for s_, c in outcome.items():
+                self.exporter.jobs.labels(s_).inc(c)
+        if self.fast is not None:
+            self.fast.housekeeping()
+        return {"claimed": len(docs), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast),
+                "seconds": time.perf_counter() - t0}
+
+    def _run_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict) -> int:
+        fp = self.fast
+        with self.spans.span("stage"):
+            fp.stage_history(fast)
+        n_rows = 0
+        for key, grp in fp.groups(fast).items():
+            M = len(key[0])
+            try:
+                with self.spans.span("score"):
+                    g = fp.score_group(grp, now)
+                with self.spans.span("finish"):
+                    fp.finish_group(g, now, updates, hpalogs, outcome)
+                    if grp[0].plan.hpa and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
+                        self._fast_hpa_forecasts(g)
+                n_rows += len(grp) * M
+            except Exception:                       # contain: re-score job by job
+                log.exception("fast-path group of %d jobs failed; re-scoring per job", len(grp))
+                for fw in grp:
+                    try:
+                        g = fp.score_group([fw], now)
+                        fp.finish_group(g, now, updates, hpalogs, outcome)
+                        n_rows += M
+                    except Exception as e:   # noqa: BLE001 - a failure closes the job, not the cycle
+                        fp.fail_job(fw, f"{type(e).__name__}: {e}", updates, outcome)
+        return n_rows
+
+    def _fast_hpa_forecasts(self, g: dict) -> None:
+        works, M = g["works"], g["M"]
+        store = g["store"]
+        view = store.view()
+        rows = torch.as_tensor(g["hist_rows"].astype(np.int64), device=view.hist.device)
+        h = view.hist.index_select(0, rows).contiguous()
+        algo = self.cfg.hpa_forecast_algorithm
+        keys = [(f"{w.plan.namespace}/{w.doc.app_name}", a, bm, zoo.canonical(algo))
+                for w in works for a, bm in zip(w.plan.aliases, w.plan.base_metrics)]
+        ctx = None
+        if self.model_cache.capacity > 0 and zoo.canonical(algo) in zoo.ES_KINDS:
+            ctx = zoo.CacheContext(self.model_cache, keys, store.last_t[g["hist_rows"]].astype(np.float64),
+                                   self.step, self.clock())
+        try:
+            fc, _ = zoo.forecast(algo, h, view.T, max(1, self.cfg.hpa_forecast_steps), lstm_model=self.lstm_model,
+                                 cache=ctx)
+        except (ValueError, RuntimeError) as e:
+            log.warning("HPA forecast skipped: %s", e)
+            return
+        peak = torch.nan_to_num(fc, nan=float("-inf")).amax(1).cpu().numpy()
+        for j, w in enumerate(works):
+            for m in range(M):
+                v = peak[j * M + m]
+                if np.isfinite(v):
+                    self.exporter.set_forecast(w.plan.base_metrics[m], w.plan.namespace, w.doc.app_name, float(v))
+
+    def _run_general(self, works: list[Work], now: float, updates: list, hpalogs: list, outcome: dict) -> int:
         rows: list[Row] = []
         for j, wk in enumerate(works):
             for r in wk.rows:
                 r.job = j
                 r.series = f"{wk.namespace or wk.doc.namespace}/{wk.doc.app_name}"
                 rows.append(r)
-        with self.spans.span("score"):
-            res = self.score_rows(rows) if rows else None
-        outcome = {}
-        summaries = []
-        offs = 0
+        try:
+            with self.spans.span("score"):
+                res = self.score_rows(rows) if rows else None
+        except Exception as e:                       # contain: score job by job
+            if len(works) == 1:
+                updates.append((works[0].doc.id, {"status": ST.COMPLETED_UNKNOWN,
+                                                  "reason": f"scoring failed: {type(e).__name__}: {e}"[:2000]}))
+                outcome[ST.COMPLETED_UNKNOWN] = outcome.get(ST.COMPLETED_UNKNOWN, 0) + 1
+                return 0
+            log.exception("general-path batch failed; scoring per job")
+            return sum(self._run_general([wk], now, updates, hpalogs, outcome) for wk in works)
         if res is not None and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
             with self.spans.span("forecast"):
                 self._hpa_forecasts(works, rows, res)
+        offs = 0
         with self.spans.span("finish"):
             for j, wk in enumerate(works):
                 k = len(wk.rows)
                 sl = slice(offs, offs + k)
                 offs += k
-                st = self._finish(wk, rows[sl], res, sl, now)
+                st = self._finish(wk, rows[sl], res, sl, now, updates, hpalogs)
                 outcome[st] = outcome.get(st, 0) + 1
-                summaries.append((wk.doc.id, wk.doc.namespace, wk.doc.app_name, st))
-        if self.exporter is not None:
-            self.exporter.tick_seconds.observe(time.perf_counter() - t0)
-            self.exporter.windows.inc(len(rows))
-            for s, c in outcome.items():
-                self.exporter.jobs.labels(s).inc(c)
-        fleet = self._gather(summaries)
-        return {"claimed": len(docs), "rows": len(rows), "outcome": outcome, "fleet": len(fleet),
-                "seconds": time.perf_counter() - t0}
-
-    def _gather(self, summaries):
-        if not D.is_dist():
-            return summaries
-        out = [None] * torch.distributed.get_world_size()
-        torch.distributed.all_gather_object(out, summaries)
-        return [s for part in out for s in part]
+        return len(rows)
 
     def run_forever(self, stop=None, poll: float | None = None) -> None:  # pragma: no cover - service loop
         poll = self.cfg.poll_interval if poll is None else poll
@@ -351,7 +446,7 @@ class Brain:
                 time.sleep(poll)
 
     # ------------------------------------------------------------------ verdicts
-    def _finish(self, wk: Work, rows: list[Row], res, sl: slice, now: float) -> str:
+    def _finish(self, wk: Work, rows: list[Row], res, sl: slice, now: float, updates: list, hpalogs: list) -> str:
         doc = wk.doc
         anomalies = {}
         reasons = []
@@ -381,20 +476,20 @@ class Brain:
                 reasons.append({"name": r.alias, "ts": ts, "values": vals,
                                 "upper": float(up[idx[0]]), "lower": float(lo[idx[0]])})
         if wk.hpa:
-            return self._finish_hpa(wk, rows, res, sl, now)
+            return self._finish_hpa(wk, rows, res, sl, now, updates, hpalogs)
         if anomalies:
             reason = html.escape(json.dumps(reasons))
-            self.store.update(doc.id, status=ST.COMPLETED_UNHEALTH, reason=reason,
-                              anomaly_info=json.dumps(anomalies))
+            updates.append((doc.id, {"status": ST.COMPLETED_UNHEALTH, "reason": reason,
+                                     "anomaly_info": json.dumps(anomalies)}))
             return ST.COMPLETED_UNHEALTH
         if now >= wk.end_ts:
             if wk.missing or not rows:
                 msg = "no current metric or missing historical data: " + ", ".join(wk.missing or ["all"])
-                self.store.update(doc.id, status=ST.COMPLETED_UNKNOWN, reason=msg)
+                updates.append((doc.id, {"status": ST.COMPLETED_UNKNOWN, "reason": msg}))
                 return ST.COMPLETED_UNKNOWN
-            self.store.update(doc.id, status=ST.COMPLETED_HEALTH, reason="")
+            updates.append((doc.id, {"status": ST.COMPLETED_HEALTH, "reason": ""}))
             return ST.COMPLETED_HEALTH
-        self.store.update(doc.id, status=ST.PREPROCESS_COMPLETED)
+        updates.append((doc.id, {"status": ST.PREPROCESS_COMPLETED}))
         return ST.PREPROCESS_COMPLETED
 
     def _hpa_forecasts(self, works: list[Work], rows: list[Row], res) -> None:
@@ -422,7 +517,8 @@ class Brain:
             if np.isfinite(peak[k]):
                 self.exporter.set_forecast(r.base_metric, wk.namespace, wk.doc.app_name, float(peak[k]))
 
-    def _finish_hpa(self, wk: Work, rows: list[Row], res, sl: slice, now: float) -> str:
+    def _finish_hpa(self, wk: Work, rows: list[Row], res, sl: slice, now: float, updates: list,
+                    hpalogs: list) -> str:
         doc = wk.doc
         cfgs = {k: {"priority": v.priority, "isIncrease": v.is_increase, "isAbsolute": v.is_absolute}
                 for k, v in doc.hpa_metrics.items()}
@@ -440,28 +536,35 @@ class Brain:
                 cur[0, c] = r.cur[k]
                 up[0, c] = res["upper"][sl.start + i][k]
                 lo[0, c] = res["lower"][sl.start + i][k]
-        state = self.hpa_state.setdefault(doc.id, MI.HpaState.zeros(1))
-        sc, rs, _ = MI.hpa_score(torch.from_numpy(cur), torch.from_numpy(up), torch.from_numpy(lo), tmpl, state, now,
-                                 self.cfg.hpa_breath_up, self.cfg.hpa_breath_down, self.cfg.hpa_max_flips,
-                                 self.cfg.hpa_flip_window)
+        sl_ = self.hpa.slots([doc.id])
+        state = self.hpa.gather(sl_)
+        dv = lambda a: torch.from_numpy(a).to(self.device)
+        sc, rs, _ = MI.hpa_score(dv(cur), dv(up), dv(lo), tmpl, state, now, self.cfg.hpa_breath_up,
+                                 self.cfg.hpa_breath_down, self.cfg.hpa_max_flips, self.cfg.hpa_flip_window)
+        self.hpa.scatter(sl_, state)
         score = int(sc[0])
         details = [HPALogDetail(a, _f(cur[0, c]), _f(up[0, c]), _f(lo[0, c])) for c, a in enumerate(aliases)]
-        self.store.add_hpalog(HPALog(job_id=doc.id, timestamp=float(now), created_at=rfc3339(
+        hpalogs.append(HPALog(job_id=doc.id, timestamp=float(now), created_at=rfc3339(
             datetime.fromtimestamp(now, timezone.utc)), log=HPALogBody(score, MI.REASONS[int(rs[0])], details)))
         if self.exporter is not None:
             self.exporter.set_hpa_score(doc.namespace, doc.app_name, score)
-        self.store.update(doc.id, status=ST.PREPROCESS_COMPLETED)
+        updates.append((doc.id, {"status": ST.PREPROCESS_COMPLETED}))
         return "hpa_scored"
+
+    @property
+    def hpa_state(self) -> dict[str, MI.HpaState]:
+        """Per-job views of the device-resident HPA hysteresis table."""
+        return {j: self.hpa.view(j) for j in self.hpa.slot}
 
     # ------------------------------------------------------------------ checkpoint
     def state_tensors(self) -> tuple[dict[str, torch.Tensor], dict]:
-        ids = sorted(self.hpa_state)
+        ids = sorted(self.hpa.slot, key=self.hpa.slot.get)
         t = {}
         if ids:
-            t["hpa.last_dir"] = torch.cat([self.hpa_state[i].last_dir for i in ids])
-            t["hpa.last_time"] = torch.cat([self.hpa_state[i].last_time for i in ids])
-            t["hpa.flips"] = torch.cat([self.hpa_state[i].flips for i in ids])
-            t["hpa.flip_t0"] = torch.cat([self.hpa_state[i].flip_t0 for i in ids])
+            idx = torch.as_tensor([self.hpa.slot[i] for i in ids], dtype=torch.int64, device=self.hpa.device)
+            st = self.hpa.gather(idx)
+            t["hpa.last_dir"], t["hpa.last_time"], t["hpa.flips"], t["hpa.flip_t0"] = (
+                st.last_dir, st.last_time, st.flips, st.flip_t0)
         if self.lstm_model is not None:
             t.update({"lstm." + k: v for k, v in self.lstm_model.state_dict().items()})
         ct, cmeta = self.model_cache.state_tensors()
@@ -479,9 +582,12 @@ class Brain:
         if got is None:
             return False
         t, meta = got
-        for i, jid in enumerate(meta.get("hpa_jobs", [])):
-            self.hpa_state[jid] = MI.HpaState(t["hpa.last_dir"][i:i + 1].clone(), t["hpa.last_time"][i:i + 1].clone(),
-                                              t["hpa.flips"][i:i + 1].clone(), t["hpa.flip_t0"][i:i + 1].clone())
+        jobs = meta.get("hpa_jobs", [])
+        if jobs:
+            idx = self.hpa.slots(jobs)
+            d = self.hpa.device
+            self.hpa.scatter(idx, MI.HpaState(t["hpa.last_dir"].to(d), t["hpa.last_time"].to(d), t["hpa.flips"].to(d),
+                                              t["hpa.flip_t0"].to(d)))
         lstm = {k[5:]: v for k, v in t.items() if k.startswith("lstm.")}
         if lstm and self.lstm_model is not None:
             self.lstm_model.load_state_dict(lstm)

@@ -1,0 +1,236 @@
+"""Device-resident history rows of the brain (HBM as the series cache).
+
+The reference brain re-queries the whole 7-day history of every metric of
+every job on every cycle (foremast-barrelman/pkg/client/metrics/metricsquery.go:93-99
+builds a now-7d..now ``historical`` query; the brain re-reads it per cycle,
+docs/guides/design.md:31-43).  At fleet scale that is 80k x 10,080 samples =
+3.2 GB per cycle, i.e. ~60 ms of host->device copy before any scoring.  Here
+each history row is fetched ONCE and stays in device memory (288 GB of HBM3E
+holds ~90x the 10k x 8 fleet); a cycle only appends the samples that arrived
+since the row's newest one, and the scoring kernels read the rows in place
+through a row map (``fm_tick_front_rm`` / ``fm_hist_stats_rm``).
+
+Two layouts:
+
+* ``static`` — a row is a right-aligned fixed window (NaN padded on the left)
+  written once: the absolute-time ``historical`` query of a canary / rolling
+  update job never changes while the job is re-examined.
+* ``sliding`` — every row lives on one global time grid (column c = time
+  t0 + c*step) and the window is the last ``T`` columns before "now".  When
+  time advances the window start moves right (a view offset, no data moved);
+  the columns that fall out of the window are overwritten with NaN, and the
+  buffer is compacted back to column 0 only when its right-hand slack runs
+  out (once every ``slack`` steps).  Continuous / HPA jobs, whose queries use
+  the ``START_TIME``/``END_TIME`` placeholders, live here; each cycle fetches
+  only ``(last_t, now]``.
+
+moving_average_all (the deployed default, foremast-brain.yaml:24-25) skips
+non-finite samples, so a row's statistics depend only on which samples sit in
+its window, not on their column: both layouts reproduce the per-cycle
+re-fetch exactly.  Rows whose model depends on sample position (forecasters)
+keep the per-cycle packed path.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import native_rt
+
+
+def _ceil4(x: int) -> int:
+    return (x + 3) // 4 * 4
+
+
+@dataclass
+class HistView:
+    """What a scoring launch needs: the buffer view (16-B aligned rows), its
+    leading dimension, the logical history length and the row map."""
+    hist: torch.Tensor        # [rows, >= T] view into the resident buffer
+    ld: int
+    T: int
+
+
+class ResidentHistory:
+    def __init__(self, T: int, device, step: float = 60.0, sliding: bool = False, slack: int = 1024,
+                 capacity: int = 0):
+        self.T = int(T)
+        self.step = float(step)
+        self.sliding = sliding
+        self.device = torch.device(device)
+        # static rows: T rounded up to a multiple of 4 columns (NaN on the left);
+        # sliding rows: the window may start up to 3 columns early (aligned view)
+        self.width = _ceil4(self.T) if not sliding else _ceil4(self.T + 3) + _ceil4(max(4, slack))
+        self.buf = torch.empty((0, self.width), dtype=torch.float32, device=self.device)
+        self.slot: dict = {}
+        self.free: list[int] = []
+        self.last_t = np.zeros(0, np.float64)       # time of each row's newest sample (-inf: none)
+        self.used = np.zeros(0, np.int64)           # cycle of last use (eviction)
+        self.keys: list = []
+        self.t0: float | None = None                # sliding: time of column 0
+        self.e = 0                                  # sliding: exclusive end column of the window
+        self.ws = 0                                 # sliding: first column inside the window
+        if capacity:
+            self._grow(capacity)
+        self.compactions = 0
+        self.bytes_in = 0
+
+    # ------------------------------------------------------------------ rows
+    def __len__(self) -> int:
+        return len(self.slot)
+
+    def _grow(self, need: int) -> None:
+        cap = self.buf.shape[0]
+        if need <= cap:
+            return
+        new_cap = max(need, int(cap * 1.5) + 256)
+        nb = torch.full((new_cap, self.width), float("nan"), dtype=torch.float32, device=self.device)
+        if cap:
+            nb[:cap].copy_(self.buf)
+        self.buf = nb
+        self.free.extend(range(new_cap - 1, cap - 1, -1))
+        self.last_t = np.concatenate([self.last_t, np.full(new_cap - cap, -np.inf)])
+        self.used = np.concatenate([self.used, np.zeros(new_cap - cap, np.int64)])
+        self.keys.extend([None] * (new_cap - cap))
+
+    def rows_for(self, keys: list, cycle: int = 0) -> tuple[np.ndarray, np.ndarray]:
+        """Row index of every key (allocating missing ones) and a mask of the
+        rows that were just allocated (need a full history fetch)."""
+        out = np.empty(len(keys), np.int32)
+        new = np.zeros(len(keys), bool)
+        missing = [i for i, k in enumerate(keys) if k not in self.slot]
+        if missing:
+            self._grow(len(self.slot) + len(missing))
+            for i in missing:
+                k = keys[i]
+                if k in self.slot:          # duplicate key within this call
+                    continue
+                r = self.free.pop()
+                self.slot[k] = r
+                self.keys[r] = k
+                self.last_t[r] = -np.inf
+                new[i] = True
+        for i, k in enumerate(keys):
+            out[i] = self.slot[k]
+        self.used[out] = cycle
+        return out, new
+
+    def get(self, key):
+        return self.slot.get(key)
+
+    def release(self, keys) -> int:
+        rows = [self.slot.pop(k) for k in keys if k in self.slot]
+        if rows:
+            idx = torch.as_tensor(rows, dtype=torch.int64, device=self.device)
+            self.buf.index_fill_(0, idx, float("nan"))
+            for r in rows:
+                self.keys[r] = None
+                self.last_t[r] = -np.inf
+            self.free.extend(rows)
+        return len(rows)
+
+    def evict_idle(self, cycle: int, max_idle: int) -> int:
+        """Drop rows not used for more than ``max_idle`` cycles."""
+        old = [k for k, r in self.slot.items() if cycle - self.used[r] > max_idle]
+        return self.release(old)
+
+    # ------------------------------------------------------------------ writes
+    def write_static(self, rows: np.ndarray, values: list[np.ndarray], t_last: np.ndarray) -> None:
+        """Static rows: right-align each series into its row (one packed
+        host->device copy, one scatter of whole rows)."""
+        assert not self.sliding
+        if len(rows) == 0:
+            return
+        packed = native_rt.pack_right(values, self.width, self.width)
+        src = torch.from_numpy(packed)
+        if self.device.type == "cuda":
+            src = src.pin_memory().to(self.device, non_blocking=True)
+        self.buf.index_copy_(0, torch.as_tensor(rows, dtype=torch.int64).to(self.device), src)
+        self.last_t[rows] = t_last
+        self.bytes_in += packed.nbytes
+
+    def view(self) -> HistView:
+        if not self.sliding:
+            return HistView(self.buf, self.width, self.width)
+        vs = max(0, self.ws // 4 * 4)
+        return HistView(self.buf[:, vs:], self.width, self.e - vs)
+
+    # ------------------------------------------------------------------ sliding grid
+    def col(self, t) -> np.ndarray:
+        return np.rint((np.asarray(t, np.float64) - self.t0) / self.step).astype(np.int64)
+
+    def advance(self, t_end: float, t_start: float | None = None) -> None:
+        """Move the window to the samples in ``[t_start, t_end]`` (grid
+        points; at most ``T`` columns ending at the last grid point <= t_end)."""
+        assert self.sliding
+        t_last = math.floor(t_end / self.step) * self.step
+        t_first = None if t_start is None else math.ceil(t_start / self.step) * self.step
+        if self.t0 is None:
+            self.t0 = t_last - (self.T - 1) * self.step
+            self.e = self.ws = 0
+
+        def target() -> tuple[int, int]:
+            e = int(self.col(t_last)) + 1
+            ws = e - self.T if t_first is None else max(e - self.T, int(self.col(t_first)))
+            return e, ws
+        e_new, ws_new = target()
+        if e_new < self.e or (e_new == self.e and ws_new <= self.ws):
+            return
+        if e_new > self.width:
+            self._compact(ws_new)
+            e_new, ws_new = target()
+        # columns that leave the window (those before the aligned view start
+        # included) must read as missing
+        lo, hi = max(0, self.ws), max(0, ws_new)
+        if hi > lo and self.buf.shape[0]:
+            self.buf[:, lo:min(hi, self.width)] = float("nan")
+        self.e, self.ws = e_new, max(ws_new, 0)
+
+    def _compact(self, ws_new: int) -> None:
+        """Shift the live columns back to column 0 (rows in chunks, so the
+        temporary stays small) and NaN the freed tail."""
+        vs = max(0, ws_new // 4 * 4)
+        keep = self.e - vs                       # live columns after the shift
+        if self.buf.shape[0] and keep > 0:
+            for r0 in range(0, self.buf.shape[0], 4096):
+                blk = self.buf[r0:r0 + 4096]
+                tmp = blk[:, vs:self.e].clone()
+                blk[:, :keep] = tmp
+                blk[:, keep:] = float("nan")
+        elif self.buf.shape[0]:
+            self.buf.fill_(float("nan"))
+        self.t0 += vs * self.step
+        self.e -= vs
+        self.ws = max(0, self.ws - vs)
+        self.compactions += 1
+
+    def window_start_t(self) -> float:
+        return self.t0 + self.ws * self.step
+
+    def write_sliding(self, rows: np.ndarray, times: list[np.ndarray], values: list[np.ndarray]) -> None:
+        """Scatter the samples of each row onto the grid (samples outside the
+        current window are dropped); rows' ``last_t`` advance."""
+        assert self.sliding and self.t0 is not None
+        if len(rows) == 0:
+            return
+        lens = np.fromiter((len(t) for t in times), np.int64, len(times))
+        if lens.sum() == 0:
+            return
+        t = np.concatenate(times)
+        v = np.concatenate(values).astype(np.float32, copy=False)
+        r = np.repeat(np.asarray(rows, np.int64), lens)
+        c = self.col(t)
+        ok = (c >= self.ws) & (c < self.e) & np.isfinite(v)
+        r, c, v, t = r[ok], c[ok], v[ok], t[ok]
+        if len(r):
+            np.maximum.at(self.last_t, r, t)
+            flat = torch.from_numpy(r * self.width + c)
+            vals = torch.from_numpy(np.ascontiguousarray(v))
+            if self.device.type == "cuda":
+                flat = flat.pin_memory().to(self.device, non_blocking=True)
+                vals = vals.pin_memory().to(self.device, non_blocking=True)
+            self.buf.view(-1).index_copy_(0, flat, vals)
+            self.bytes_in += v.nbytes + 8 * len(r)

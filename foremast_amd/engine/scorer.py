@@ -183,6 +183,52 @@ class CanaryScorer:
         C.service_reduce(o.decide.count, o.decide.score, o.decide.valid, self.M, out=o.packed)
         return o
 
+    # -- resident history (the brain's production path) ----------------------
+    def score_resident(self, hview, rowmap: torch.Tensor, cur: torch.Tensor, base: torch.Tensor | None,
+                       slot: int = 0) -> CanaryOutputs:
+        """The tick over rows of the device-resident history store
+        (engine/resident.py): logical row r reads history row ``rowmap[r]`` of
+        ``hview.hist`` in place.  GPU: one role-split front launch when the
+        pairwise windows fit a wave-sorted 256 (n_cur + n_base <= 256),
+        otherwise history stats || pairwise (<= 512 on the GPU, wider on the
+        CPU oracle) — then the decision kernel.  Rows are services x M."""
+        R = cur.shape[0]
+        has_base = base is not None and base.shape[1] > 0
+        if not cur.is_cuda:
+            hist = hview.hist.index_select(0, rowmap.to(torch.int64))
+            return self.score(hist, base if has_base else None, cur, hview.T)
+        from ..ops._lib import LIB, ptr, stream_of
+        C.check(rowmap.dtype == torch.int32 and rowmap.numel() == R and rowmap.is_cuda, "rowmap must be int32 [R]")
+        C.check(hview.ld % 4 == 0 and hview.hist.data_ptr() % 16 == 0, "history rows must be 16-B aligned")
+        C.check(self.M <= 16, "resident tick supports up to 16 metrics per service")
+        o = self._alloc(R, cur.shape[1], slot)
+        st = stream_of(cur)
+        n = cur.shape[1] + (base.shape[1] if has_base else 0)
+        if has_base and n <= 256:
+            fp, fh = self.front_wgs
+            n_p = int(fp * self._cus) if fp > 0 else 0
+            n_h = int(fh * self._cus) if fh > 0 else 0
+            LIB.call("fm_tick_front_rm", ptr(hview.hist), hview.ld, hview.T, R, ptr(o.hs), ptr(cur), cur.stride(0),
+                     cur.shape[1], ptr(base), base.stride(0), base.shape[1], ptr(o.suff), n_p, n_h,
+                     self.pcfg.min_mann_white, self.pcfg.min_wilcoxon, self.pcfg.min_kruskal, ptr(o.pvals),
+                     ptr(o.pstats), ptr(self._queue), ptr(rowmap), st)
+        else:
+            LIB.call("fm_hist_stats_rm", ptr(hview.hist), hview.ld, hview.T, R, ptr(o.hs), 0, ptr(rowmap), st)
+            if has_base and n <= 512:
+                self._pairwise_into(cur, base, o, combine=False)
+            elif has_base:
+                # wider than the register sort: the fp64 CPU oracle for these
+                # rows (rare: > 512 points per side pair), p-values uploaded
+                mask, anyc = self.pcfg.mask_and_combine()
+                from ..ops import reference as ref
+                p, s_, _ = ref.pairwise_tests(cur.cpu().numpy(), base.cpu().numpy(), mask, anyc,
+                                              self.pcfg.p_threshold, self.pcfg.min_mann_white,
+                                              self.pcfg.min_wilcoxon, self.pcfg.min_kruskal)
+                o.pvals.copy_(torch.from_numpy(p))
+                o.pstats.copy_(torch.from_numpy(s_))
+        self._decide_services(cur, o, has_base)
+        return o
+
     # -- split tick: front kernel and decision on different streams ----------
     def front_only(self, hist, base, cur, n_hist=None, packed_out=None, slot: int = 0) -> CanaryOutputs:
         """First half of a front-mode tick (pairwise tests, p-values, history

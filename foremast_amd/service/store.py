@@ -16,23 +16,40 @@ taken over.
 """
 from __future__ import annotations
 
+import dataclasses
 import json
 import sqlite3
 import threading
 import time
 from abc import ABC, abstractmethod
+
+import numpy as np
 from datetime import datetime, timezone
 
 from ..api import status as ST
 from ..api.jobs import parse_rfc3339, rfc3339
+from ..api.jsonmodel import to_json
 from ..api.models import Document, HPALog
 
 
 def _ts(doc: Document) -> float:
+    return _ts_str(doc.modified_at)
+
+
+def _ts_str(s: str) -> float:
     try:
-        return parse_rfc3339(doc.modified_at).timestamp()
+        return parse_rfc3339(s).timestamp()
     except ValueError:
         return 0.0
+
+
+def _shard_filter(rank: int, world: int):
+    from ..parallel.dist import service_owner
+    return lambda d: service_owner(d.namespace, d.app_name, world) == rank
+
+
+def _stamp(now: float) -> str:
+    return rfc3339(datetime.fromtimestamp(now, timezone.utc))
 
 
 class JobStore(ABC):
@@ -71,11 +88,25 @@ class JobStore(ABC):
         self.put(d)
         return d
 
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
+        """Apply ``(job id, fields)`` updates in one batch (one transaction /
+        one ``_bulk`` request on the persistent backends)."""
+        for jid, fields in updates:
+            self.update(jid, **fields)
+
+    def add_hpalogs(self, logs: list[HPALog]) -> None:
+        for lg in logs:
+            self.add_hpalog(lg)
+
     def claim(self, worker: str, limit: int, max_stuck_s: float, now: float | None = None,
-              owner=None) -> list[Document]:
+              owner=None, shard: tuple[int, int] | None = None) -> list[Document]:
         """Reserve up to ``limit`` jobs for ``worker``; ``owner(doc) -> bool``
-        restricts claims to this worker's shard."""
+        or ``shard=(rank, world)`` (owner hash of ``namespace:app``,
+        parallel/dist.py:service_owner) restricts claims to this worker's
+        shard."""
         now = time.time() if now is None else now
+        if shard is not None and owner is None:
+            owner = _shard_filter(*shard)
         out = []
         for d in self._claim_candidates():
             if len(out) >= limit:
@@ -100,43 +131,157 @@ class JobStore(ABC):
 
 
 class MemoryStore(JobStore):
+    """In-process store.  The claim / status hot path is columnar: status
+    codes, lease times and (per world size) owner ranks are numpy arrays, so
+    claiming or updating a 10k-job batch is a few vectorised operations plus
+    one attribute store per job, not a decode of every live document."""
+
     def __init__(self) -> None:
-        self._docs: dict[str, dict] = {}
+        self._objs: list[Document] = []
+        self._index: dict[str, int] = {}
+        self._codes: dict[str, int] = {}
+        self._names: list[str] = []
+        self._st = np.zeros(0, np.int16)
+        self._mod = np.zeros(0, np.float64)
+        self._owners: dict[int, np.ndarray] = {}
         self._logs: list[dict] = []
         self._lock = threading.RLock()
+        self._claimable = np.zeros(0, bool)
+        self._inprog = np.zeros(0, bool)
+
+    def _code(self, status: str) -> int:
+        c = self._codes.get(status)
+        if c is None:
+            c = self._codes[status] = len(self._names)
+            self._names.append(status)
+            self._claimable = np.array([n in ST.CLAIMABLE for n in self._names])
+            self._inprog = np.array([n in ST.IN_PROGRESS for n in self._names])
+        return c
 
     def put(self, doc: Document) -> None:
+        d = Document.from_dict(doc.to_dict())
         with self._lock:
-            self._docs[doc.id] = doc.to_dict()
+            i = self._index.get(d.id)
+            if i is None:
+                i = self._index[d.id] = len(self._objs)
+                self._objs.append(d)
+                if i >= len(self._st):
+                    n = max(1024, 2 * len(self._st))
+                    self._st = np.concatenate([self._st, np.zeros(n - len(self._st), np.int16)])
+                    self._mod = np.concatenate([self._mod, np.zeros(n - len(self._mod))])
+                for w, o in self._owners.items():
+                    if len(o) <= i:
+                        self._owners[w] = np.concatenate([o, np.full(len(self._st) - len(o), -1, np.int32)])
+                    self._owners[w][i] = -1
+            else:
+                self._objs[i] = d
+                for o in self._owners.values():
+                    o[i] = -1
+            self._st[i] = self._code(d.status)
+            self._mod[i] = _ts(d)
 
     def get(self, job_id: str) -> Document | None:
         with self._lock:
-            d = self._docs.get(job_id)
-            return Document.from_dict(d) if d is not None else None
+            i = self._index.get(job_id)
+            return Document.from_dict(self._objs[i].to_dict()) if i is not None else None
 
     def all_docs(self) -> list[Document]:
         with self._lock:
-            return [Document.from_dict(d) for d in self._docs.values()]
+            return [Document.from_dict(d.to_dict()) for d in self._objs]
+
+    def update(self, job_id: str, **fields) -> Document | None:
+        with self._lock:
+            i = self._index.get(job_id)
+            if i is None:
+                return None
+            d = self._objs[i]
+            for k, v in fields.items():
+                setattr(d, k, v)
+            now = time.time()
+            d.modified_at = _stamp(now)
+            self._st[i] = self._code(d.status)
+            self._mod[i] = _ts(d)
+            return Document.from_dict(d.to_dict())
+
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
+        now = time.time() if now is None else now
+        stamp = _stamp(now)
+        with self._lock:
+            idx = np.fromiter((self._index.get(j, -1) for j, _ in updates), np.int64, len(updates))
+            codes = np.empty(len(updates), np.int16)
+            for k, (i, (_, fields)) in enumerate(zip(idx, updates)):
+                if i < 0:
+                    codes[k] = -1
+                    continue
+                d = self._objs[i]
+                for f, v in fields.items():
+                    setattr(d, f, v)
+                d.modified_at = stamp
+                codes[k] = self._code(d.status)
+            ok = idx >= 0
+            self._st[idx[ok]] = codes[ok]
+            self._mod[idx[ok]] = _ts_str(stamp)
+
+    def _owner_of(self, world: int) -> np.ndarray:
+        from ..parallel.dist import service_owner
+        n = len(self._objs)
+        o = self._owners.get(world)
+        if o is None or len(o) < len(self._st):
+            o2 = np.full(len(self._st), -1, np.int32)
+            if o is not None:
+                o2[:len(o)] = o
+            o = self._owners[world] = o2
+        todo = np.flatnonzero(o[:n] < 0)
+        for i in todo:
+            d = self._objs[i]
+            o[i] = service_owner(d.namespace, d.app_name, world)
+        return o
+
+    def claim(self, worker, limit, max_stuck_s, now=None, owner=None, shard=None):
+        now = time.time() if now is None else now
+        with self._lock:
+            n = len(self._objs)
+            if n == 0 or not self._names:
+                return []
+            st = self._st[:n]
+            mask = self._claimable[st] | (self._inprog[st] & (now - self._mod[:n] > max_stuck_s))
+            if shard is not None:
+                rank, world = shard
+                mask &= self._owner_of(world)[:n] == rank
+            idx = np.flatnonzero(mask)
+            if owner is not None:
+                idx = np.array([i for i in idx if owner(self._objs[i])], np.int64)
+            # oldest lease first (fair across cycles), stable in insertion order
+            idx = idx[np.argsort(self._mod[idx], kind="stable")][:limit]
+            if len(idx) == 0:
+                return []
+            stamp = _stamp(now)
+            code = self._code(ST.PREPROCESS_INPROGRESS)
+            out = []
+            for i in idx:
+                d = self._objs[i]
+                d.status = ST.PREPROCESS_INPROGRESS
+                d.processing_content = worker
+                d.modified_at = stamp
+                out.append(d)
+            self._st[idx] = code
+            self._mod[idx] = _ts_str(stamp)
+            return out
 
     def add_hpalog(self, log: HPALog) -> None:
         with self._lock:
             self._logs.append(log.to_dict())
+
+    def add_hpalogs(self, logs: list[HPALog]) -> None:
+        rows = [lg.to_dict() for lg in logs]
+        with self._lock:
+            self._logs.extend(rows)
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
         with self._lock:
             rows = [l for l in self._logs if l.get("job_id") == job_id]
         rows.sort(key=lambda l: l.get("timestamp", 0.0), reverse=True)
         return [HPALog.from_dict(r) for r in rows[:size]]
-
-    def _claim_candidates(self) -> list[Document]:
-        # filter on the stored dicts before decoding (completed documents
-        # accumulate; only live ones are worth deserialising)
-        live = ST.CLAIMABLE | ST.IN_PROGRESS
-        return [Document.from_dict(d) for d in self._docs.values() if d.get("status") in live]
-
-    def claim(self, worker, limit, max_stuck_s, now=None, owner=None):
-        with self._lock:
-            return super().claim(worker, limit, max_stuck_s, now, owner)
 
 
 class SQLiteStore(JobStore):
@@ -200,6 +345,81 @@ class SQLiteStore(JobStore):
     def add_hpalog(self, log: HPALog) -> None:
         self._conn().execute("insert into hpalogs values (?,?,?)", (log.job_id, log.timestamp,
                                                                     json.dumps(log.to_dict())))
+
+    def add_hpalogs(self, logs: list[HPALog]) -> None:
+        c = self._conn()
+        c.execute("begin")
+        try:
+            c.executemany("insert into hpalogs values (?,?,?)",
+                          [(lg.job_id, lg.timestamp, json.dumps(lg.to_dict())) for lg in logs])
+            c.execute("commit")
+        except Exception:
+            c.execute("rollback")
+            raise
+
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
+        """One IMMEDIATE transaction: read the bodies, apply, ``executemany``."""
+        if not updates:
+            return
+        stamp = _stamp(time.time() if now is None else now)
+        c = self._conn()
+        c.execute("begin immediate")
+        try:
+            bodies = {}
+            ids = [j for j, _ in updates]
+            for k in range(0, len(ids), 500):
+                chunk = ids[k:k + 500]
+                q = f"select id, body from documents where id in ({','.join('?' * len(chunk))})"
+                bodies.update({r[0]: r[1] for r in c.execute(q, chunk)})
+            rows = []
+            for jid, fields in updates:
+                b = bodies.get(jid)
+                if b is None:
+                    continue
+                d = Document.from_dict(json.loads(b))
+                for f, v in fields.items():
+                    setattr(d, f, v)
+                d.modified_at = stamp
+                rows.append((d.id, d.status, _ts(d), json.dumps(d.to_dict())))
+            c.executemany("insert or replace into documents values (?,?,?,?)", rows)
+            c.execute("commit")
+        except Exception:
+            c.execute("rollback")
+            raise
+
+    def claim(self, worker, limit, max_stuck_s, now=None, owner=None, shard=None):
+        """The whole batch in one IMMEDIATE transaction (the write lock makes
+        it atomic against other brain processes sharing the file)."""
+        now = time.time() if now is None else now
+        if shard is not None and owner is None:
+            owner = _shard_filter(*shard)
+        st = tuple(ST.CLAIMABLE | ST.IN_PROGRESS)
+        stamp = _stamp(now)
+        c = self._conn()
+        c.execute("begin immediate")
+        try:
+            q = f"select body from documents where status in ({','.join('?' * len(st))}) order by modified"
+            out = []
+            for (b,) in c.execute(q, st).fetchall():
+                if len(out) >= limit:
+                    break
+                d = Document.from_dict(json.loads(b))
+                stuck = d.status in ST.IN_PROGRESS and now - _ts(d) > max_stuck_s
+                if not (d.status in ST.CLAIMABLE or stuck):
+                    continue
+                if owner is not None and not owner(d):
+                    continue
+                d.status = ST.PREPROCESS_INPROGRESS
+                d.processing_content = worker
+                d.modified_at = stamp
+                out.append(d)
+            c.executemany("insert or replace into documents values (?,?,?,?)",
+                          [(d.id, d.status, _ts(d), json.dumps(d.to_dict())) for d in out])
+            c.execute("commit")
+            return out
+        except Exception:
+            c.execute("rollback")
+            raise
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
         rows = self._conn().execute("select body from hpalogs where job_id=? order by ts desc limit ?",
@@ -269,6 +489,37 @@ class ElasticsearchStore(JobStore):
     def add_hpalog(self, log: HPALog) -> None:
         r = self.http.post(f"{self.url}/hpalogs/hpalog?refresh=true", json=log.to_dict())
         r.raise_for_status()
+
+    def _bulk(self, lines: list[dict]) -> dict:
+        body = "".join(json.dumps(x) + "\n" for x in lines)
+        r = self.http.post(f"{self.url}/_bulk?refresh=true", content=body.encode(),
+                           headers={"Content-Type": "application/x-ndjson"})
+        r.raise_for_status()
+        out = r.json()
+        if out.get("errors"):
+            bad = [it for it in out.get("items", []) for v in it.values() if v.get("status", 200) >= 300]
+            raise RuntimeError(f"ES _bulk: {len(bad)} failed actions, first {bad[:1]}")
+        return out
+
+    def add_hpalogs(self, logs: list[HPALog]) -> None:
+        """One ``_bulk`` request of index actions."""
+        lines = []
+        for lg in logs:
+            lines += [{"index": {"_index": "hpalogs", "_type": "hpalog"}}, lg.to_dict()]
+        if lines:
+            self._bulk(lines)
+
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
+        """One ``_bulk`` request of partial-document ``update`` actions."""
+        stamp = _stamp(time.time() if now is None else now)
+        names = {f.name: f.metadata.get("json", f.name) for f in dataclasses.fields(Document)}
+        lines = []
+        for jid, fields in updates:
+            doc = {names[k]: to_json(v) for k, v in fields.items()}
+            doc["modified_at"] = stamp
+            lines += [{"update": {"_index": "documents", "_type": "document", "_id": jid}}, {"doc": doc}]
+        if lines:
+            self._bulk(lines)
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
         q = {"query": {"bool": {"must": [{"match": {"job_id.keyword": job_id}}]}},

@@ -147,16 +147,18 @@ def test_caller_series_graph():
 def _w_brain(rank, world, db, n_apps):
     from foremast_amd.config import BrainConfig
     from foremast_amd.engine.brain import Brain
+    from foremast_amd.engine.exporter import BrainExporter
     from foremast_amd.engine.sources import SourceRouter
     from foremast_amd.service.store import SQLiteStore
     store = SQLiteStore(db)
     clock = lambda: 1_760_000_000.0
+    exp = BrainExporter()
     brain = Brain(store, BrainConfig(), sources=SourceRouter.synthetic_only(faults={"app3": 8.0}, fault_after=1_760_000_000.0 - 600),
-                  clock=clock,
-                  worker_id=f"rank{rank}")
+                  clock=clock, worker_id=f"rank{rank}", exporter=exp)
     r1 = brain.run_once()
-    r2 = brain.run_once()                  # a rank with no claim still joins the gather
-    return r1.get("claimed", 0), r1.get("fleet", 0), r2.get("fleet", 0)
+    r2 = brain.run_once()                  # a rank with no claim still joins the export sync
+    ups = {k[2]: v for k in exp.table.keys if k[0].endswith("_upper") for v in [exp.table.get(k)]}
+    return r1.get("claimed", 0), r2.get("claimed", 0), ups
 
 
 def test_brain_ranks_claim_disjoint_owned_jobs(tmp_path):
@@ -178,10 +180,17 @@ def test_brain_ranks_claim_disjoint_owned_jobs(tmp_path):
     # filled for HPA documents, models.go:102-124)
     owners = [D.service_owner(store.get(i).namespace, store.get(i).app_name, 2) for i in ids]
     assert claimed == [owners.count(0), owners.count(1)]
-    assert out[0][1] == out[1][1] == n and out[0][2] == out[1][2]
     docs = [store.get(i) for i in ids]
     assert all(d.status != "initial" for d in docs)
     assert store.get(ids[3]).status == "completed_unhealth"
+    # C2: rank 0's exporter (the one scrape target) holds the bounds of EVERY
+    # app, including the ones rank 1 scored, with rank 1's values
+    apps = {f"app{i}" for i in range(n)}
+    assert set(out[0][2]) == apps
+    r1_apps = {f"app{i}" for i in range(n) if owners[i] == 1}
+    assert r1_apps and set(out[1][2]) == r1_apps
+    for a in r1_apps:
+        assert out[0][2][a] == out[1][2][a]
 
 
 def _w_lstm_fit(rank, world):

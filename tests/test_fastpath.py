@@ -1,0 +1,204 @@
+"""The brain's resident-history fast path (engine/fastpath.py) against the
+general model-zoo path on the same job stream: identical statuses, reasons,
+anomaly maps, HPA logs and exporter gauges, cycle after cycle; plus the
+resident store's sliding window and the wide-window / failure containment
+rules (a > 512-point pairwise batch must not abort the cycle)."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from foremast_amd.api import crd
+from foremast_amd.api import status as ST
+from foremast_amd.config import BrainConfig
+from foremast_amd.controller.analyst import AnalystClient
+from foremast_amd.engine.brain import Brain
+from foremast_amd.engine.exporter import BrainExporter
+from foremast_amd.engine.resident import ResidentHistory
+from foremast_amd.engine.sources import SourceRouter
+from foremast_amd.service.app import create_app
+from foremast_amd.service.store import MemoryStore
+
+T0 = 1_760_000_000.0
+
+
+class Clock:
+    def __init__(self, t=T0):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+def _metrics(n=3):
+    ms = [crd.Monitoring("http_server_requests_errors_5xx", "counter", "error5xx"),
+          crd.Monitoring("http_server_requests_latency", "gauge", "latency"),
+          crd.Monitoring("cpu_usage_seconds_total", "gauge", "cpu"),
+          crd.Monitoring("memory_usage_bytes", "gauge", "memory")]
+    return crd.Metrics("prometheus", "http://prom/api/v1/", ms[:n])
+
+
+def _pods(app, n, tag):
+    return [f"{app}-{tag}{'a' * 9}-p{k:04d}" for k in range(n)]
+
+
+def _submit(client):
+    ids = []
+    for j in range(6):
+        app = f"canary{j}"
+        ids.append(client.start_analyzing("default", app, [_pods(app, 2, "7687b9f4d"), _pods(app, 2, "5db89899b")],
+                                          _metrics(), 10, "canary"))
+    for j in range(3):
+        ids.append(client.start_analyzing("default", f"roll{j}", [_pods(f"roll{j}", 2, "7687b9f4d")], _metrics(2), 10,
+                                          "rollingUpdate"))
+    for j in range(2):
+        ids.append(client.start_analyzing("prod", f"cont{j}", None, _metrics(), 10, "continuous"))
+    for j in range(2):
+        ids.append(client.start_analyzing("prod", f"hpa{j}", None, _metrics(), 10, "hpa", ["cpu", "latency"]))
+    # wide canaries: 14 + 14 pods x 11 points = 308 (> 256), 30 + 30 = 660 (> 512)
+    for j, npods in ((0, 14), (1, 30)):
+        app = f"wide{j}"
+        ids.append(client.start_analyzing("default", app, [_pods(app, npods, "7687b9f4d"), _pods(app, npods, "5db8989")],
+                                          _metrics(2), 10, "canary"))
+    return ids
+
+
+def _brain(resident, faults, device="cpu"):
+    clock = Clock()
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    exp = BrainExporter()
+    brain = Brain(store, BrainConfig(), device=device,
+                  sources=SourceRouter.synthetic_only(faults=faults, fault_after=T0 + 120), clock=clock, exporter=exp,
+                  worker_id="w0", resident_history=resident)
+    return clock, store, client, brain, exp
+
+
+FAULTS = {"canary1-7687b9f4daaaaaaaaa-p0000": 5.0, "canary4-7687b9f4daaaaaaaaa-p0001": 0.2,
+          "cont1": 4.0, "wide1-7687b9f4daaaaaaaaa-p0003": 6.0}
+
+
+def _run_pair(device="cpu"):
+    a = _brain(True, FAULTS, device)
+    b = _brain(False, FAULTS, device)
+    ids_a, ids_b = _submit(a[2]), _submit(b[2])
+    assert ids_a == ids_b
+    history = []
+    for cyc in range(5):
+        ra, rb = a[3].run_once(), b[3].run_once()
+        assert ra["claimed"] == rb["claimed"]
+        history.append((ra, rb))
+        for jid in ids_a:
+            da, db = a[1].get(jid), b[1].get(jid)
+            assert da.status == db.status, (cyc, jid, da.status, db.status, da.reason, db.reason)
+            assert da.reason == db.reason, (cyc, jid)
+            assert (json.loads(da.anomaly_info) if da.anomaly_info else {}) == \
+                   (json.loads(db.anomaly_info) if db.anomaly_info else {}), (cyc, jid)
+        for jid in ids_a:
+            la = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current, d.upper, d.lower) for d in l.log.details])
+                  for l in a[1].hpalogs(jid)]
+            lb = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current, d.upper, d.lower) for d in l.log.details])
+                  for l in b[1].hpalogs(jid)]
+            assert la == lb, (cyc, jid)
+        ta, tb = a[4].table, b[4].table
+        assert set(ta.index) == set(tb.index)
+        for k in ta.index:
+            va, vb = ta.get(k), tb.get(k)
+            if "forecast" in k[0]:
+                continue
+            assert (np.isnan(va) and np.isnan(vb)) or va == pytest.approx(vb, rel=1e-6, abs=1e-9), (cyc, k, va, vb)
+        a[0].t += 240
+        b[0].t += 240
+    return a, b, ids_a, history
+
+
+def test_fast_path_equals_general_path_over_cycles():
+    a, b, ids, hist = _run_pair()
+    # the fast path actually carried the jobs (all metrics are moving_average_all)
+    assert hist[0][0]["fast_jobs"] == len(ids)
+    statuses = {a[1].get(j).status for j in ids}
+    assert ST.COMPLETED_UNHEALTH in statuses and ST.COMPLETED_HEALTH in statuses
+    # unhealthy canary verdict names the faulty metric
+    d = a[1].get(ids[1])
+    assert d.status == ST.COMPLETED_UNHEALTH and json.loads(d.anomaly_info)
+    # static history rows of finished jobs were released, sliding ones kept
+    assert len(a[3].fast.static) == 0
+    assert len(a[3].fast.sliding) > 0
+
+
+def test_wide_pairwise_window_does_not_abort_cycle():
+    a, b, ids, hist = _run_pair()
+    wide = ids[-1]
+    assert a[1].get(wide).status in (ST.COMPLETED_UNHEALTH, ST.COMPLETED_HEALTH)
+
+
+def test_failing_group_is_contained_per_job(monkeypatch):
+    clock, store, client, brain, exp = _brain(True, {})
+    ids = _submit(client)
+    orig = brain.fast.score_group
+
+    def boom(works, now):
+        if any(w.doc.app_name == "canary2" for w in works):
+            raise RuntimeError("injected kernel failure")
+        return orig(works, now)
+    monkeypatch.setattr(brain.fast, "score_group", boom)
+    r = brain.run_once()
+    assert r["claimed"] == len(ids)
+    bad = [j for j in ids if store.get(j).app_name == "canary2"][0]
+    assert store.get(bad).status == ST.COMPLETED_UNKNOWN and "injected kernel failure" in store.get(bad).reason
+    others = [store.get(j).status for j in ids if j != bad]
+    assert ST.COMPLETED_UNKNOWN not in others
+
+
+def test_sliding_history_window_moves_and_compacts():
+    h = ResidentHistory(10, "cpu", step=60.0, sliding=True, slack=4)
+    h.advance(T0)
+    rows, new = h.rows_for(["a", "b"])
+    assert new.all()
+    t = T0 - 60.0 * np.arange(9, -1, -1)
+    h.write_sliding(rows, [t, t[5:]], [np.arange(10, dtype=np.float32), np.arange(5, dtype=np.float32)])
+    v = h.view()
+    win = v.hist[:, :v.T].numpy()
+    assert np.nansum(win[rows[0]]) == 45 and np.isfinite(win[rows[1]]).sum() == 5
+    # advance 7 steps: 7 oldest samples leave the window, new ones land at the end
+    for k in range(1, 8):
+        h.advance(T0 + 60.0 * k)
+        h.write_sliding(rows[:1], [np.array([T0 + 60.0 * k])], [np.array([100.0 + k], np.float32)])
+    v = h.view()
+    win = v.hist[:, :v.T].numpy()
+    got = win[rows[0]][np.isfinite(win[rows[0]])]
+    np.testing.assert_array_equal(got, np.concatenate([np.arange(7, 10), 100.0 + np.arange(1, 8)]))
+    assert h.last_t[rows[0]] == T0 + 420.0
+    # 5 more: the right-hand slack runs out and the buffer compacts to column 0
+    for k in range(8, 13):
+        h.advance(T0 + 60.0 * k)
+        h.write_sliding(rows[:1], [np.array([T0 + 60.0 * k])], [np.array([100.0 + k], np.float32)])
+    assert h.compactions >= 1
+    v = h.view()
+    win = v.hist[:, :v.T].numpy()
+    np.testing.assert_array_equal(win[rows[0]][np.isfinite(win[rows[0]])], 100.0 + np.arange(3, 13))
+    assert not np.isfinite(win[rows[1]]).any()
+    # a window start given in time trims the oldest grid point
+    h.advance(T0 + 60.0 * 12 + 30.0, T0 + 60.0 * 12 + 30.0 - 60.0 * 9)
+    v = h.view()
+    win = v.hist[:, :v.T].numpy()
+    np.testing.assert_array_equal(win[rows[0]][np.isfinite(win[rows[0]])], 100.0 + np.arange(4, 13))
+
+
+def test_static_rows_are_written_once_and_released():
+    h = ResidentHistory(16, "cpu", step=60.0)
+    rows, new = h.rows_for([("j", "a"), ("j", "b")])
+    h.write_static(rows, [np.arange(20, dtype=np.float32), np.arange(3, dtype=np.float32)], np.array([1.0, 2.0]))
+    v = h.view()
+    np.testing.assert_array_equal(v.hist[rows[0]].numpy(), np.arange(4, 20, dtype=np.float32))
+    assert np.isnan(v.hist[rows[1], :13]).all() and (v.hist[rows[1], 13:].numpy() == [0, 1, 2]).all()
+    rows2, new2 = h.rows_for([("j", "a")])
+    assert not new2.any() and rows2[0] == rows[0]
+    assert h.release([("j", "a"), ("j", "b")]) == 2 and len(h) == 0
+    assert torch.isnan(h.buf[rows]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_fast_path_equals_general_path(cuda):
+    _run_pair(device=cuda)
