@@ -24,15 +24,20 @@ Data: synthetic Prometheus-shaped series generated on device (K11), the model
 is the deployed default (no learned weights).  Reference publishes no number
 (BASELINE.md), so vs_baseline is null.
 
-Launch: ``python bench.py`` (1 GPU) or
+Launch: ``python bench.py`` (1 GPU), ``python bench.py --gpus N`` (spawns N
+rank processes itself, one per GPU, before anything touches the GPU) or
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
+``--device cpu`` rehearses the same multi-rank path on the CPU (gloo, the
+fp64 reference scorer), which is how the CPU test-suite covers it.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -47,9 +52,64 @@ from foremast_amd.parallel import dist as D
 ALIASES = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, rendezvous on 127.0.0.1) and
+    return the first failing exit code.  The parent never initialises the GPU
+    and never execs; if one rank dies the others are terminated instead of
+    waiting out the collective timeout."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def _device_census(info, dev) -> tuple[int, str]:
+    """(distinct devices across ranks, backend).  Ranks sharing one GPU
+    (FOREMAST_DEVICE_INDEX rehearsal over gloo) count once."""
+    import torch.distributed as tdist
+    backend = tdist.get_backend() if D.is_dist() else "none"
+    if dev.type != "cuda":
+        return 0, backend
+    props = torch.cuda.get_device_properties(dev)
+    ident = f"{socket.gethostname()}:{getattr(props, 'uuid', '')}:{getattr(props, 'pci_bus_id', dev.index)}"
+    if not D.is_dist():
+        return 1, backend
+    ids = [None] * info.world
+    tdist.all_gather_object(ids, ident)
+    return len(set(ids)), backend
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks, one per GPU); without a launcher's WORLD_SIZE the script spawns them")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: multi-rank rehearsal on the CPU (gloo, fp64 reference scorer)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--services", type=int, default=10000)
@@ -78,9 +138,16 @@ def main() -> None:
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace of 5 extra steps (rank 0)")
     args = ap.parse_args()
 
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     info = D.env_info()
+    if args.gpus is not None and args.gpus != info.world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={info.world}", file=sys.stderr)
+        sys.exit(2)
+    if args.device == "cpu":
+        return run_cpu(args, info)
     if not torch.cuda.is_available():
-        print("bench.py needs a GPU", file=sys.stderr)
+        print("bench.py needs a GPU (or --device cpu for the CPU rehearsal)", file=sys.stderr)
         sys.exit(2)
     # FOREMAST_DEVICE_INDEX pins every rank to one GPU (multi-rank rehearsal
     # on a 1-GPU box together with FOREMAST_DIST_BACKEND=gloo)
@@ -186,6 +253,7 @@ def main() -> None:
         t_b.synchronize()
         lat.append(t_a.elapsed_time(t_b))
     p50 = D.all_reduce_max(statistics.median(lat) / 1e3, dev)
+    n_dev, backend = _device_census(info, dev)
     ms = elapsed / args.steps * 1e3
     windows = S * M
     verdict = hosts[0][:S].numpy() if info.is_main else None
@@ -195,7 +263,9 @@ def main() -> None:
             "metric": "metric windows scored/sec (node) + p50 decision latency, 10k-service canary",
             "value": windows / (ms / 1e3),
             "unit": "windows/s",
-            "n_gpus": world,
+            "n_gpus": n_dev,
+            "n_ranks": world,
+            "backend": backend,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms,
@@ -236,6 +306,58 @@ def main() -> None:
                 run(1)
         if info.is_main:
             prof.export_chrome_trace(args.trace)
+    if D.is_dist():
+        torch.distributed.destroy_process_group()
+
+
+def run_cpu(args, info) -> None:
+    """The bench step on the CPU: same sharding, same verdict all-gather (gloo)
+    and the same JSON line, scored by the fp64 reference path.  Exists so the
+    multi-rank launch + gather + reporting path is exercised without a GPU;
+    its numbers are not a performance claim (n_gpus 0)."""
+    dev = torch.device("cpu")
+    info = D.init_distributed(backend="gloo" if info.world > 1 else None, device=dev)
+    world = info.world
+    S, M = args.services, args.metrics
+    aliases = (ALIASES * ((M + len(ALIASES) - 1) // len(ALIASES)))[:M]
+    svc0, _, s_pad = D.shard_range(S, info.rank, world)
+    hist, base, cur = C.synth_fleet(s_pad, M, args.hist, args.pods, args.window, svc0, device=dev)
+    cfg = BrainConfig()
+    cfg.min_historical_points = 10
+    scorer = CanaryScorer(aliases, cfg, device=dev, mode="serial")
+    gathered = torch.empty((world * s_pad, 4), dtype=torch.float32)
+    lat: list[float] = []
+
+    def step() -> torch.Tensor:
+        o = scorer.score(hist, base, cur, args.hist)
+        return D.all_gather_rows(o.packed.contiguous(), gathered)
+
+    for _ in range(args.warmup):
+        step()
+    D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        g = step()
+        lat.append(time.perf_counter() - ts)
+    D.barrier()
+    elapsed = D.all_reduce_max(time.perf_counter() - t0, dev)
+    p50 = D.all_reduce_max(statistics.median(lat), dev)
+    _, backend = _device_census(info, dev)
+    ms = elapsed / args.steps * 1e3
+    if info.is_main:
+        verdict = g[:S].numpy()
+        print(json.dumps({
+            "metric": "metric windows scored/sec (node) + p50 decision latency, 10k-service canary [CPU rehearsal]",
+            "value": S * M / (ms / 1e3), "unit": "windows/s", "n_gpus": 0, "n_ranks": world, "backend": backend,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "p50_decision_latency_ms": p50 * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32 data / fp64 statistics",
+            "data": "synthetic (Prometheus-shaped fleet, K11; 2% injected faults)",
+            "config": {"model": "foremast-brain canary: moving_average_all + pairwise ALL", "global_batch": S * M,
+                       "seq_len": args.hist, "services": S, "metrics": M, "parallelism": f"dp{world}",
+                       "device": "cpu"},
+            "services_flagged": int((verdict[:, 0] == 1).sum()),
+        }))
     if D.is_dist():
         torch.distributed.destroy_process_group()
 

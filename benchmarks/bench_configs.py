@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import argparse
 import os
+import statistics
 import sys
 import time
 
@@ -205,6 +206,88 @@ def config3(args):
             {"services": S, "metrics": M, "device": str(dev), "torch_threads": torch.get_num_threads()})
 
 
+# --------------------------------------------------------------------------- config 3e2e
+def config3e2e(args):
+    """The production brain (``Brain.run_once``) on the config-3 fleet: 10k
+    canary jobs x 8 metrics (5 + 5 pods x 10 points, 7-day history) in the job
+    store, one cycle = claim -> fetch current/baseline -> stage -> resident
+    tick (pairwise + moving_average_all + decision, GPU) -> compaction ->
+    verdicts -> exporter gauges -> bulk store update (+ the C2 exporter
+    gather on several ranks).  Series are pre-staged in memory (the first,
+    untimed cycle fetches and stages them, history into the device-resident
+    store); the fetch span is reported separately."""
+    from foremast_amd.api import crd
+    from foremast_amd.api import jobs as J
+    from foremast_amd.api.models import ApplicationHealthAnalyzeRequest
+    from foremast_amd.controller.analyst import AnalystClient, Response
+    from foremast_amd.engine.brain import Brain
+    from foremast_amd.engine.exporter import BrainExporter
+    from foremast_amd.engine.sources import SourceRouter, StagedSource, SyntheticSource
+    from foremast_amd.service.store import MemoryStore
+    import json as _json
+
+    info, dev = setup(gpus_required=args.device != "cpu")
+    dev = torch.device("cpu") if args.device == "cpu" else dev
+    S, M, P = args.services, args.metrics, args.pods
+    t = {"now": 1_760_000_000.0}
+    clock = lambda: t["now"]
+    store = MemoryStore()
+
+    def do(method, url, body):                 # the service's create handler, in-process
+        req = ApplicationHealthAnalyzeRequest.from_dict(_json.loads(body))
+        jid, _ = store.create(J.build_document(req))
+        return Response(200, _json.dumps(J.new_response(jid, 0, "new")).encode())
+    client = AnalystClient("http://foremast-service/v1/healthcheck/", do, clock)
+    names = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
+    mons = [crd.Monitoring(f"http_server_requests_{a}", "gauge", a) for a in (names * 2)[:M]]
+    metrics = crd.Metrics("prometheus", "http://prom/api/v1/", mons)
+    faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, S, 50)}    # 2% of services regress
+    staged = StagedSource(SyntheticSource(faults=faults, fault_after=t["now"] - 3600))
+    cfg = BrainConfig()
+    exp = BrainExporter()
+    brain = Brain(store, cfg, device=dev, sources=SourceRouter(synthetic=staged, force="synthetic"), clock=clock,
+                  batch_size=S + 1, worker_id=f"bench-{info.rank}", exporter=exp, history_days=args.history_days)
+    t_sub = time.perf_counter()
+    for j in range(S):
+        client.start_analyzing("default", f"svc{j}", [[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
+                                                      [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]],
+                               metrics, args.window, "canary")
+    t_sub = time.perf_counter() - t_sub
+    print(f"[3e2e] submitted {S} jobs in {t_sub:.1f}s", file=sys.stderr, flush=True)
+    t["now"] += args.poll_seconds
+    t_first = time.perf_counter()
+    first = brain.run_once()                    # fetch + stage history (untimed)
+    t_first = time.perf_counter() - t_first
+    print(f"[3e2e] first cycle (fetch + stage history) {t_first:.1f}s: {first}", file=sys.stderr, flush=True)
+    rows, spans = [], {}
+
+    def step():
+        # cycles every poll interval inside the jobs' watch window (the
+        # synthetic source serves the whole window: pre-staged series)
+        t["now"] += args.poll_seconds
+        r = brain.run_once()
+        rows.append(r.get("rows", 0))
+        for k, v in brain.spans.last.items():
+            spans.setdefault(k, []).append(v * 1e3)
+
+    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    timed = rows[args.warmup:]
+    per_cycle = sum(timed) / max(1, len(timed))
+    windows = D.all_reduce_max(float(per_cycle), torch.device("cpu") if dev.type == "cpu" else dev)
+    total_rows = per_cycle * info.world if D.is_dist() else per_cycle
+    span_ms = {k: round(statistics.median(v[args.warmup:] or v), 3) for k, v in spans.items()}
+    _common(args, info, ms, p50, "metric windows scored/sec (node), production brain cycle (Brain.run_once) "
+            "on the 10k-service canary fleet", total_rows / (ms / 1e3), "windows/s",
+            "Brain.run_once: claim + fetch (pre-staged) + resident tick (moving_average_all + pairwise ALL) + "
+            "compaction + verdicts + exporter + bulk store update", S * M, int(args.history_days * 1440) + 1,
+            "strong", "fp32" if dev.type != "cpu" else "fp32 data / fp64 statistics",
+            "synthetic Prometheus-shaped series (pre-staged in memory; 2% of services regress)",
+            {"services": S, "metrics": M, "pods_per_side": P, "rows_per_cycle_rank0": per_cycle,
+             "rows_per_cycle_max_rank": windows, "span_ms_median_rank0": span_ms,
+             "first_cycle_s (fetch+stage history)": round(t_first, 3), "submit_s": round(t_sub, 3),
+             "fast_jobs_first_cycle": first.get("fast_jobs"), "device": str(dev)})
+
+
 # --------------------------------------------------------------------------- config 4
 def config4(args):
     from foremast_amd.models.lstm import LSTMForecaster
@@ -276,7 +359,7 @@ def config5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--config", required=True, choices=["1", "2", "3", "3e2e", "4", "5"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -292,10 +375,13 @@ def main():
     ap.add_argument("--degree", type=int, default=6)
     ap.add_argument("--hops", type=int, default=2)
     ap.add_argument("--detect-period", action="store_true")
+    ap.add_argument("--history-days", type=float, default=7.0, help="config 3e2e: history window")
+    ap.add_argument("--poll-seconds", type=float, default=1.0, help="config 3e2e: clock advance per cycle (the "
+                    "jobs' 10-minute watch window must outlive warmup + steps)")
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "
                     "the fitted-model cache")
     args = ap.parse_args()
-    {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}[args.config](args)
+    {"1": config1, "2": config2, "3": config3, "3e2e": config3e2e, "4": config4, "5": config5}[args.config](args)
 
 
 if __name__ == "__main__":

@@ -111,7 +111,7 @@ class Brain:
     def __init__(self, store, cfg: BrainConfig | None = None, device="cpu", sources: SourceRouter | None = None,
                  worker_id: str | None = None, batch_size: int = 512, exporter: BrainExporter | None = None,
                  clock=time.time, step: float = 60.0, watch_minutes: float = 10.0, fetch_threads: int = 16,
-                 lstm_model=None, resident_history: bool | None = None):
+                 lstm_model=None, resident_history: bool | None = None, history_days: float = 7.0):
         self.store = store
         self.cfg = cfg or BrainConfig()
         if resident_history is None:
@@ -124,6 +124,7 @@ class Brain:
         self.clock = clock
         self.step = step
         self.watch_s = watch_minutes * 60.0
+        self.history_s = history_days * 86400.0
         self.fetch_threads = fetch_threads
         self.lstm_model = lstm_model
         from ..models.cache import ModelCache
@@ -136,7 +137,7 @@ class Brain:
         # moving_average_all jobs: device-resident history + the benchmarked
         # tick (engine/fastpath.py); RESIDENT_HISTORY=0 sends every job
         # through the general model-zoo path
-        self.fast = FastPath(self) if resident_history else None
+        self.fast = FastPath(self, history_days) if resident_history else None
         self.hpa = self.fast.hpa if self.fast is not None else HpaTable(self.device)
         self.cycles = 0
 
@@ -161,9 +162,9 @@ class Brain:
         w = self.watch_s
         if doc.strategy == "hpa":
             return {"current": (now - 5 * self.step, now), "baseline": (now - 2 * w, now - w),
-                    "historical": (now - 7 * 86400.0, now)}
+                    "historical": (now - self.history_s, now)}
         return {"current": (now - w, now), "baseline": (now - 2 * w, now - w),
-                "historical": (now - 7 * 86400.0, now - w)}
+                "historical": (now - self.history_s, now - w)}
 
     def _fetch_job(self, doc: Document, now: float) -> Work:
         wk = Work(doc, namespace=doc.namespace)
@@ -319,27 +320,38 @@ class Brain:
     def _cycle(self, t0: float) -> dict:
         now = self.clock()
         with self.spans.span("claim"):
-            docs = self.store.claim(self.worker, self.batch_size, self.cfg.max_stuck_seconds, now=now,
-                                    shard=self._shard())
-        if not docs:
+            batch = self.store.claim_batch(self.worker, self.batch_size, self.cfg.max_stuck_seconds, now=now,
+                                           shard=self._shard())
+        if not len(batch):
             return {"claimed": 0}
-        fast, rest = (self.fast.prepare(docs, now) if self.fast is not None else ([], docs))
+        with self.spans.span("prepare"):
+            fast, rest = self.fast.prepare(batch, now) if self.fast is not None else ([], batch.docs())
         with self.spans.span("fetch"):
-            ex = self._executor()
-            ff = [ex.submit(self.fast.fetch, fw, now) for fw in fast]
-            works = list(ex.map(lambda d: self._fetch_job(d, now), rest))
-            fast = [f.result() for f in ff]
+            if self.sources.local:
+                # in-memory sources: no I/O to overlap, a pool only adds overhead
+                if fast:
+                    self.fast.fetch_all(fast, now)
+                works = [self._fetch_job(d, now) for d in rest]
+            else:
+                ex = self._executor()
+                gf = [ex.submit(self._fetch_job, d, now) for d in rest]
+                if fast:
+                    self.fast.fetch_all(fast, now, ex)
+                works = [f.result() for f in gf]
         updates: list = []
+        bulk: list = []          # uniform (ids, fields) updates of the fast path
         hpalogs: list = []
         outcome: dict = {}
         n_rows = 0
         if fast:
-            n_rows += self._run_fast(fast, now, updates, hpalogs, outcome)
+            n_rows += self._run_fast(fast, now, updates, hpalogs, outcome, bulk)
         if works:
             n_rows += self._run_general(works, now, updates, hpalogs, outcome)
         with self.spans.span("persist"):
             if hpalogs:
                 self.store.add_hpalogs(hpalogs)
+            for ids, fields in bulk:
+                self.store.update_uniform(ids, fields, now=now)
             self.store.update_many(updates)
         if self.exporter is not None:
             self.exporter.tick_seconds.observe(time.perf_counter() - t0)
@@ -348,10 +360,10 @@ class Brain:
                 self.exporter.jobs.labels(s_).inc(c)
         if self.fast is not None:
             self.fast.housekeeping()
-        return {"claimed": len(docs), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast),
+        return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast),
                 "seconds": time.perf_counter() - t0}
 
-    def _run_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict) -> int:
+    def _run_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict, bulk: list) -> int:
         fp = self.fast
         with self.spans.span("stage"):
             fp.stage_history(fast)
@@ -360,9 +372,11 @@ class Brain:
             M = len(key[0])
             try:
                 with self.spans.span("score"):
-                    g = fp.score_group(grp, now)
+                    g = fp.score_group(grp, now, key)
                 with self.spans.span("finish"):
-                    fp.finish_group(g, now, updates, hpalogs, outcome)
+                    gb: list = []
+                    fp.finish_group(g, now, updates, hpalogs, outcome, gb)
+                    bulk.extend(gb)
                     if grp[0].plan.hpa and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
                         self._fast_hpa_forecasts(g)
                 n_rows += len(grp) * M

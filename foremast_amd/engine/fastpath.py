@@ -81,12 +81,19 @@ class JobPlan:
 
 @dataclass
 class FastWork:
+    """A job's fast-path state.  It persists across the cycles the job is
+    re-examined (keyed by job id), so the steady state costs no per-job
+    planning, no re-fetch of immutable windows and no per-job numpy calls."""
     doc: Document
     plan: JobPlan
     rows: np.ndarray                           # resident history row per metric
-    need_hist: np.ndarray                      # bool per metric: fetch + write history this cycle
-    hist_since: np.ndarray                     # per metric: fetch history after this time (sliding)
     end_ts: float = 0.0
+    hist_complete: bool = False                # static rows: every metric's history is resident
+    has_window: bool = False                   # current / baseline fetched at least once
+    dirty: bool = True                         # data changed since the group arrays were built
+    wclass: int = 0                            # pairwise width class (groups)
+    version: object = None                     # store version of the document this plan is for
+    gkey: tuple | None = None                  # group key (plan group + width class)
     cur: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))    # metrics concatenated
     cur_t: np.ndarray = field(default_factory=lambda: np.zeros(0))
     cur_len: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
@@ -95,6 +102,24 @@ class FastWork:
     hist: list = field(default_factory=list)   # (metric index, times, values) to write
     errors: list = field(default_factory=list)
     failed: str = ""
+
+
+@dataclass
+class GroupArrays:
+    """Host/device arrays of one group, reused while the group's job list
+    and data are unchanged (the steady state of a re-examined fleet)."""
+    ident: tuple
+    ids: np.ndarray                            # object array of job ids
+    cur: np.ndarray
+    cur_t: np.ndarray
+    cur_len: np.ndarray
+    rowmap: np.ndarray
+    cur_d: torch.Tensor
+    base_d: torch.Tensor | None
+    rm_d: torch.Tensor
+    end: np.ndarray
+    missing: np.ndarray                        # [S, M] no history or no current data
+    export_slots: np.ndarray | None = None
 
 
 def _label(q: str, name: str) -> str:
@@ -130,7 +155,7 @@ class HpaTable:
     def slots(self, ids: list[str]) -> torch.Tensor:
         new = [i for i in ids if i not in self.slot]
         if new:
-            n0 = len(self.slot)
+            n0 = int(self.state.last_dir.shape[0])      # never reuse a live slot after drop()
             for k, i in enumerate(new):
                 self.slot[i] = n0 + k
             add = MI.HpaState.zeros(len(new), self.device)
@@ -170,7 +195,8 @@ class FastPath:
         self.T_static = (n + 3) // 4 * 4
         self.static = ResidentHistory(self.T_static, brain.device, step, sliding=False)
         self.sliding = ResidentHistory(n, brain.device, step, sliding=True)
-        self.plans: dict[str, JobPlan] = {}
+        self.works: dict[str, FastWork] = {}
+        self._garr: dict[tuple, GroupArrays] = {}
         self.scorers: dict[tuple, CanaryScorer] = {}
         self.hpa = HpaTable(brain.device)
         self.cycle = 0
@@ -178,16 +204,6 @@ class FastPath:
         self._cmp = {}            # device compaction buffers per capacity
 
     # ------------------------------------------------------------------ planning
-    def plan(self, doc: Document) -> JobPlan | None:
-        fp = (doc.created_at, doc.strategy, len(doc.current_config), len(doc.historical_config))
-        p = self.plans.get(doc.id)
-        if p is not None and p.fp == fp:
-            return p
-        p = self._make_plan(doc, fp)
-        if p is not None:
-            self.plans[doc.id] = p
-        return p
-
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
         cfg = self.b.cfg
         cur = parse_config(doc.current_config)
@@ -234,37 +250,75 @@ class FastPath:
         return zoo.canonical(a)
 
     # ------------------------------------------------------------------ prepare / fetch
-    def prepare(self, docs: list[Document], now: float) -> tuple[list[FastWork], list[Document]]:
-        """Split claimed jobs into fast-path work (history rows resolved) and
-        the rest (general model-zoo path)."""
+    def prepare(self, batch, now: float) -> tuple[list[FastWork], list[Document]]:
+        """Split a claim batch (service/store.py:ClaimBatch) into fast-path
+        work and the documents for the general model-zoo path.  A job seen
+        before at the same version reuses its FastWork: no document decode,
+        no planning, no row lookups; only new / resubmitted jobs are
+        materialised and planned."""
         self.cycle += 1
-        fast, rest = [], []
         self.sliding.advance(now, now - self.history_s)
-        for d in docs:
-            p = self.plan(d)
-            if p is None:
-                rest.append(d)
-                continue
-            store = self.sliding if p.sliding else self.static
-            rows, new = store.rows_for(p.keys, self.cycle)
-            if p.sliding:
-                since = store.last_t[rows].copy()
-                need = np.ones(len(rows), bool)
+        works = self.works
+        fast, unknown = [], []
+        for k, (jid, ver) in enumerate(zip(batch.ids, batch.versions)):
+            fw = works.get(jid)
+            if fw is not None and fw.version == ver:
+                fast.append(fw)
             else:
-                since = np.full(len(rows), -np.inf)
-                # new rows, and rows whose history never arrived (fetch error / no data yet)
-                need = new | ~np.isfinite(store.last_t[rows])
-            try:
-                end_ts = parse_rfc3339(d.end_time).timestamp() if d.end_time else now
-            except ValueError:
-                end_ts = now
-            fast.append(FastWork(d, p, rows, need, since, end_ts))
+                unknown.append(k)
+        rest = []
+        if unknown:
+            for k, d in zip(unknown, batch.docs(unknown)):
+                old = works.pop(d.id, None)
+                if old is not None:              # resubmitted under the same id
+                    self._release([old])
+                p = self._make_plan(d, batch.versions[k])
+                if p is None:
+                    rest.append(d)
+                    continue
+                store = self.sliding if p.sliding else self.static
+                rows, _ = store.rows_for(p.keys, self.cycle)
+                try:
+                    end_ts = parse_rfc3339(d.end_time).timestamp() if d.end_time else now
+                except ValueError:
+                    end_ts = now
+                fw = works[d.id] = FastWork(d, p, rows, end_ts, version=batch.versions[k])
+                fast.append(fw)
         return fast, rest
+
+    def fetch_all(self, works: list[FastWork], now: float, pool=None) -> list[FastWork]:
+        """Fetch what each job needs this cycle.  From an immutable source a
+        static job whose windows and history are resident needs nothing."""
+        if self._immutable:
+            todo = [fw for fw in works if not (fw.has_window and fw.hist_complete and not fw.plan.sliding)]
+        else:
+            todo = works
+        if pool is None:
+            for fw in todo:
+                self.fetch(fw, now)
+        else:
+            list(pool.map(lambda fw: self.fetch(fw, now), todo))
+        return works
 
     def fetch(self, fw: FastWork, now: float) -> FastWork:
         b = self.b
-        wins = b._windows(fw.doc, now)
         p = fw.plan
+        if p.sliding:
+            need = np.ones(len(fw.rows), bool)
+            since = self.sliding.last_t[fw.rows]
+        elif fw.hist_complete:
+            need = None
+        else:
+            # new rows, and rows whose history never arrived (fetch error / no data yet)
+            need = ~np.isfinite(self.static.last_t[fw.rows])
+            since = None
+        fw.hist = []
+        if fw.has_window and need is None and self._immutable:
+            # absolute-time windows from a pre-staged / immutable source: the
+            # previous answer is still the answer, nothing to fetch
+            return fw
+        fw.errors = []
+        wins = b._windows(fw.doc, now)
         cv, ct, cl, bv, bl = [], [], [], [], []
         for i, a in enumerate(p.aliases):
             for cat, urls, stores, vals, lens, times in (("current", p.cur_urls, p.cur_stores, cv, cl, ct),
@@ -283,10 +337,10 @@ class FastPath:
                         times.append(np.asarray(s.times, np.float64))
                     n += len(s.values)
                 lens.append(n)
-            if fw.need_hist[i] and p.hist_urls[i]:
+            if need is not None and need[i] and p.hist_urls[i]:
                 lo, hi = wins["historical"]
-                if p.sliding and np.isfinite(fw.hist_since[i]):
-                    lo = max(lo, fw.hist_since[i] + b.step)
+                if p.sliding and np.isfinite(since[i]):
+                    lo = max(lo, since[i] + b.step)
                 if hi >= lo or not p.sliding:
                     url = substitute_window(p.hist_urls[i], lo, hi)
                     try:
@@ -303,13 +357,23 @@ class FastPath:
         cat = lambda xs, dt: np.concatenate(xs).astype(dt, copy=False) if xs else np.zeros(0, dt)
         fw.cur, fw.cur_t, fw.base = cat(cv, np.float32), cat(ct, np.float64), cat(bv, np.float32)
         fw.cur_len, fw.base_len = np.asarray(cl, np.int64), np.asarray(bl, np.int64)
+        c = int(fw.cur_len.max()) if len(cl) else 0
+        bb = int(fw.base_len.max()) if len(bl) else 0
+        fw.wclass = 0 if max(c, bb) <= 128 else (1 if max(c, bb) <= 256 else 2)
+        fw.has_window = True
+        fw.dirty = True
         return fw
+
+    @property
+    def _immutable(self) -> bool:
+        return bool(getattr(self.b.sources, "immutable", False))
 
     # ------------------------------------------------------------------ stage + score
     def stage_history(self, works: list[FastWork]) -> None:
         srows, svals, stl = [], [], []
         drows, dts, dvs = [], [], []
-        for fw in works:
+        got = [fw for fw in works if fw.hist]
+        for fw in got:
             for i, t, v in fw.hist:
                 if fw.plan.sliding:
                     drows.append(fw.rows[i])
@@ -323,11 +387,23 @@ class FastPath:
             self.static.write_static(np.asarray(srows, np.int64), svals, np.asarray(stl, np.float64))
         if drows:
             self.sliding.write_sliding(np.asarray(drows, np.int64), dts, dvs)
+        for fw in got:
+            fw.dirty = True
+            if not fw.plan.sliding:
+                fw.hist_complete = bool(np.isfinite(self.static.last_t[fw.rows]).all())
+            fw.hist = []
 
     def groups(self, works: list[FastWork]) -> dict[tuple, list[FastWork]]:
+        """Jobs of one plan group split by pairwise width class, so a group's
+        padded window stays on the role-split kernel (<= 128 points per side:
+        <= 256 together) or the separate pairwise kernel (<= 256 per side)
+        and one wide canary never widens the whole fleet's batch."""
         g: dict[tuple, list[FastWork]] = {}
         for fw in works:
-            g.setdefault(fw.plan.group, []).append(fw)
+            k = fw.gkey
+            if k is None or k[-1] != fw.wclass:
+                k = fw.gkey = fw.plan.group + (fw.wclass,)
+            g.setdefault(k, []).append(fw)
         return g
 
     def _scorer(self, aliases: tuple) -> CanaryScorer:
@@ -338,15 +414,21 @@ class FastPath:
             sc._out.clear()
         return sc
 
-    def score_group(self, works: list[FastWork], now: float) -> dict:
+    def _arrays(self, works: list[FastWork], key: tuple) -> GroupArrays:
+        """The group's packed arrays: rebuilt only when its job list or any
+        job's data changed since the last cycle."""
+        ident = tuple(map(id, works))
+        ga = self._garr.get(key)
+        if ga is not None and ga.ident == ident and not any(fw.dirty for fw in works):
+            return ga
         p0 = works[0].plan
         M = len(p0.aliases)
         S = len(works)
-        R = S * M
         dev = self.b.device
         store = self.sliding if p0.sliding else self.static
         cur_len = np.concatenate([w.cur_len for w in works])
         base_len = np.concatenate([w.base_len for w in works])
+        R = S * M
         n = max(1, int(cur_len.max()) if R else 1)
         nb = int(base_len.max()) if R else 0
         cur = pack_left(np.concatenate([w.cur for w in works]), cur_len, n)
@@ -355,29 +437,58 @@ class FastPath:
         rowmap = np.concatenate([w.rows for w in works]).astype(np.int32)
         up = lambda a: (torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"
                         else torch.from_numpy(a))
-        cur_d, rm_d = up(cur), up(rowmap)
-        base_d = up(base) if base is not None else None
-        o = self._scorer(p0.aliases).score_resident(store.view(), rm_d, cur_d, base_d)
+        has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
+        has_cur = np.isfinite(cur).any(1).reshape(S, M)
+        ids = np.empty(S, object)
+        ids[:] = [w.doc.id for w in works]
+        ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
+                         up(rowmap), np.fromiter((w.end_ts for w in works), np.float64, S), ~(has_hist & has_cur))
+        exp = self.b.exporter
+        if exp is not None:
+            slots = []
+            for w in works:
+                p = w.plan
+                if p.export_slots is None:
+                    p.export_slots = exp.bound_slots(p.base_metrics, [p.namespace] * M, [p.app] * M)
+                slots.append(p.export_slots)
+            ga.export_slots = np.concatenate(slots)
+        for w in works:
+            w.dirty = False
+        self._garr[key] = ga
+        return ga
+
+    def score_group(self, works: list[FastWork], now: float, key: tuple | None = None) -> dict:
+        p0 = works[0].plan
+        M = len(p0.aliases)
+        S = len(works)
+        R = S * M
+        dev = self.b.device
+        store = self.sliding if p0.sliding else self.static
+        ga = self._arrays(works, key if key is not None else ("adhoc",) + p0.group)
+        store.used[ga.rowmap] = self.cycle
+        n = ga.cur.shape[1]
+        o = self._scorer(p0.aliases).score_resident(store.view(), ga.rm_d, ga.cur_d, ga.base_d)
         dec = o.decide
         if dev.type == "cuda":
             cap = max(1024, min(R * n, 1 << 16))
-            idx_d, val_d, ctr = self._compact(dec, cur_d, R, n, cap)
+            idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, cap)
             host = [t.to("cpu", non_blocking=True) for t in (o.packed, dec.stats, dec.count, ctr)]
             torch.cuda.current_stream(dev).synchronize()
             packed, stats, count, total = (t.numpy() for t in host)
             total = int(total[0])
             if total > cap:
-                idx_d, val_d, ctr = self._compact(dec, cur_d, R, n, total)
-            idx = idx_d[:total].cpu().numpy()
+                idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, total)
+            idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
         else:
             packed, stats, count = o.packed.numpy(), dec.stats.numpy(), dec.count.numpy()
-            ix, _ = C.compact_anomalies(dec, cur_d)
+            ix, _ = C.compact_anomalies(dec, ga.cur_d)
             idx = ix.numpy()
         # (row, point) sorted: the order of atomically appended rows is arbitrary
         if len(idx):
             idx = idx[np.lexsort((idx[:, 1], idx[:, 0]))]
-        return {"works": works, "M": M, "cur": cur, "cur_t": cur_t, "cur_len": cur_len, "packed": packed,
-                "stats": stats, "count": count, "anom": idx, "hist_rows": rowmap, "store": store}
+        return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
+                "packed": packed, "stats": stats, "count": count, "anom": idx, "hist_rows": ga.rowmap,
+                "store": store}
 
     def _compact(self, dec, cur_d, R: int, n: int, cap: int):
         dev = cur_d.device
@@ -394,65 +505,70 @@ class FastPath:
         return idx, val, ctr
 
     # ------------------------------------------------------------------ finish
-    def finish_group(self, g: dict, now: float, updates: list, hpalogs: list, outcome: dict) -> None:
+    def finish_group(self, g: dict, now: float, updates: list, hpalogs: list, outcome: dict,
+                     bulk: list | None = None) -> None:
+        """Verdicts of a group as array operations.  Jobs that stay alive
+        (``preprocess_completed``) and healthy closes go out as uniform bulk
+        updates ``(ids, fields)``; only unhealthy / unknown verdicts build
+        per-job reasons."""
         works, M = g["works"], g["M"]
+        ga: GroupArrays = g["ga"]
         S = len(works)
         R = S * M
-        stats, count, packed = g["stats"], g["count"], g["packed"]
+        stats, packed = g["stats"], g["packed"]
         cur, cur_t = g["cur"], g["cur_t"]
         anom = g["anom"]
-        store = g["store"]
-        rows_hist = g["hist_rows"]
-        # newest anomalous timestamp per row (dashboard reads it as a time)
-        anom_ts = np.full(R, np.nan)
-        if len(anom):
-            np.fmax.at(anom_ts, anom[:, 0], cur_t[anom[:, 0], anom[:, 1]])
         exp = self.b.exporter
         if exp is not None:
-            slots = []
-            for w in works:
-                p = w.plan
-                if p.export_slots is None:
-                    p.export_slots = exp.bound_slots(p.base_metrics, [p.namespace] * M, [p.app] * M)
-                slots.append(p.export_slots)
-            up_, lo_ = stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64)
-            exp.set_bounds_many(np.concatenate(slots), up_, lo_, anom_ts)
-        has_hist = np.isfinite(store.last_t[rows_hist]).reshape(S, M)
-        has_cur = np.isfinite(cur).any(1).reshape(S, M)
-        missing = ~(has_hist & has_cur)
+            # newest anomalous timestamp per row (dashboard reads it as a time)
+            anom_ts = np.full(R, np.nan)
+            if len(anom):
+                np.fmax.at(anom_ts, anom[:, 0], cur_t[anom[:, 0], anom[:, 1]])
+            exp.set_bounds_many(ga.export_slots, stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64),
+                                anom_ts)
         if works[0].plan.hpa:
             self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome)
             return
         status = packed[:, 0]
-        end = np.fromiter((w.end_ts for w in works), np.float64, S)
-        done = now >= end
-        row_start = np.searchsorted(anom[:, 0], np.arange(S) * M) if len(anom) else None
-        release = []
-        for j in range(S):
+        unh = status == 1
+        done = (now >= ga.end) & ~unh
+        miss = ga.missing.any(1)
+        alive = ~unh & ~done
+        healthy = done & ~miss
+        unknown = done & miss
+        if bulk is None:
+            bulk = []
+            flush = True
+        else:
+            flush = False
+        if alive.any():
+            bulk.append((ga.ids[alive].tolist(), {"status": ST.PREPROCESS_COMPLETED}))
+            outcome[ST.PREPROCESS_COMPLETED] = outcome.get(ST.PREPROCESS_COMPLETED, 0) + int(alive.sum())
+        if healthy.any():
+            bulk.append((ga.ids[healthy].tolist(), {"status": ST.COMPLETED_HEALTH, "reason": ""}))
+            outcome[ST.COMPLETED_HEALTH] = outcome.get(ST.COMPLETED_HEALTH, 0) + int(healthy.sum())
+        for j in np.flatnonzero(unknown):
             w = works[j]
-            if status[j] == 1:
-                st, fields = self._unhealthy(w, j, M, anom, row_start, cur, cur_t, stats)
-                release.append(w)
-            elif done[j]:
-                if missing[j].any():
-                    miss = [w.plan.aliases[m] for m in np.flatnonzero(missing[j])]
-                    st = ST.COMPLETED_UNKNOWN
-                    fields = {"status": st, "reason": "no current metric or missing historical data: "
-                              + ", ".join(miss)}
-                else:
-                    st = ST.COMPLETED_HEALTH
-                    fields = {"status": st, "reason": ""}
-                release.append(w)
-            else:
-                st = ST.PREPROCESS_COMPLETED
-                fields = {"status": st}
-            updates.append((w.doc.id, fields))
-            outcome[st] = outcome.get(st, 0) + 1
-        self._release(release)
+            miss_al = [w.plan.aliases[m] for m in np.flatnonzero(ga.missing[j])]
+            updates.append((w.doc.id, {"status": ST.COMPLETED_UNKNOWN,
+                                       "reason": "no current metric or missing historical data: " + ", ".join(miss_al)}))
+        if unknown.any():
+            outcome[ST.COMPLETED_UNKNOWN] = outcome.get(ST.COMPLETED_UNKNOWN, 0) + int(unknown.sum())
+        if unh.any():
+            row_start = np.searchsorted(anom[:, 0], np.arange(S) * M) if len(anom) else None
+            for j in np.flatnonzero(unh):
+                st, fields = self._unhealthy(works[j], j, M, anom, row_start, cur, cur_t, stats)
+                updates.append((works[j].doc.id, fields))
+            outcome[ST.COMPLETED_UNHEALTH] = outcome.get(ST.COMPLETED_UNHEALTH, 0) + int(unh.sum())
+        if flush:
+            updates.extend((i, f) for ids, f in bulk for i in ids)
+        closed = ~alive
+        if closed.any():
+            self._release([works[j] for j in np.flatnonzero(closed)])
 
     def _unhealthy(self, w: FastWork, j: int, M: int, anom, row_start, cur, cur_t, stats):
         r0 = j * M
-        a0 = row_start[j]
+        a0 = row_start[j] if row_start is not None else 0
         a1 = np.searchsorted(anom[:, 0], r0 + M) if len(anom) else 0
         ent = anom[a0:a1]
         anomalies, reasons = {}, []
@@ -514,7 +630,8 @@ class FastPath:
         if keys:
             self.static.release(keys)
         for w in works:
-            self.plans.pop(w.doc.id, None)
+            if self.works.get(w.doc.id) is w:
+                del self.works[w.doc.id]
 
     def fail_job(self, fw: FastWork, err: str, updates: list, outcome: dict) -> None:
         st = ST.COMPLETED_UNKNOWN
@@ -523,10 +640,14 @@ class FastPath:
         self._release([fw])
 
     def housekeeping(self) -> None:
-        self.sliding.evict_idle(self.cycle, self.max_idle_cycles)
-        self.static.evict_idle(self.cycle, self.max_idle_cycles)
-        if len(self.plans) > 4 * max(1, len(self.static) + len(self.sliding)) + 1024:
-            self.plans.clear()
+        gone = self.sliding.evict_idle(self.cycle, self.max_idle_cycles) + \
+            self.static.evict_idle(self.cycle, self.max_idle_cycles)
+        if gone:
+            # jobs whose rows were evicted re-plan (and re-fetch) if they come back
+            stale = [k for k, w in self.works.items()
+                     if (self.sliding if w.plan.sliding else self.static).keys[int(w.rows[0])] != w.plan.keys[0]]
+            for k in stale:
+                del self.works[k]
 
 
 def _merge_series(ss) -> tuple[np.ndarray, np.ndarray]:

@@ -69,6 +69,7 @@ class ResidentHistory:
         self.free: list[int] = []
         self.last_t = np.zeros(0, np.float64)       # time of each row's newest sample (-inf: none)
         self.used = np.zeros(0, np.int64)           # cycle of last use (eviction)
+        self.occ = np.zeros(0, bool)                # row holds a key
         self.keys: list = []
         self.t0: float | None = None                # sliding: time of column 0
         self.e = 0                                  # sliding: exclusive end column of the window
@@ -94,6 +95,7 @@ class ResidentHistory:
         self.free.extend(range(new_cap - 1, cap - 1, -1))
         self.last_t = np.concatenate([self.last_t, np.full(new_cap - cap, -np.inf)])
         self.used = np.concatenate([self.used, np.zeros(new_cap - cap, np.int64)])
+        self.occ = np.concatenate([self.occ, np.zeros(new_cap - cap, bool)])
         self.keys.extend([None] * (new_cap - cap))
 
     def rows_for(self, keys: list, cycle: int = 0) -> tuple[np.ndarray, np.ndarray]:
@@ -111,6 +113,7 @@ class ResidentHistory:
                 r = self.free.pop()
                 self.slot[k] = r
                 self.keys[r] = k
+                self.occ[r] = True
                 self.last_t[r] = -np.inf
                 new[i] = True
         for i, k in enumerate(keys):
@@ -129,13 +132,16 @@ class ResidentHistory:
             for r in rows:
                 self.keys[r] = None
                 self.last_t[r] = -np.inf
+            self.occ[rows] = False
             self.free.extend(rows)
         return len(rows)
 
     def evict_idle(self, cycle: int, max_idle: int) -> int:
         """Drop rows not used for more than ``max_idle`` cycles."""
-        old = [k for k, r in self.slot.items() if cycle - self.used[r] > max_idle]
-        return self.release(old)
+        idle = np.flatnonzero(self.occ & (cycle - self.used > max_idle))
+        if len(idle) == 0:
+            return 0
+        return self.release([self.keys[r] for r in idle])
 
     # ------------------------------------------------------------------ writes
     def write_static(self, rows: np.ndarray, values: list[np.ndarray], t_last: np.ndarray) -> None:

@@ -217,15 +217,12 @@ class CanaryScorer:
             if has_base and n <= 512:
                 self._pairwise_into(cur, base, o, combine=False)
             elif has_base:
-                # wider than the register sort: the fp64 CPU oracle for these
-                # rows (rare: > 512 points per side pair), p-values uploaded
-                mask, anyc = self.pcfg.mask_and_combine()
-                from ..ops import reference as ref
-                p, s_, _ = ref.pairwise_tests(cur.cpu().numpy(), base.cpu().numpy(), mask, anyc,
-                                              self.pcfg.p_threshold, self.pcfg.min_mann_white,
-                                              self.pcfg.min_wilcoxon, self.pcfg.min_kruskal)
-                o.pvals.copy_(torch.from_numpy(p))
-                o.pstats.copy_(torch.from_numpy(s_))
+                # padded wider than the register sort: rows bucketed by their
+                # own widths, only really wide rows (> 512 points per side
+                # pair, rare) on the fp64 CPU oracle
+                p, s_, _ = C.pairwise_tests(cur, base, self.pcfg)
+                o.pvals.copy_(p)
+                o.pstats.copy_(s_)
         self._decide_services(cur, o, has_base)
         return o
 

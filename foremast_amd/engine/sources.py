@@ -168,6 +168,31 @@ class SyntheticSource:
                                      fault_key=q + "|" + p), "pod", p) for i, p in enumerate(pods)]
 
 
+class StagedSource:
+    """Pre-staged series: every distinct query is answered once by ``inner``
+    and served from memory afterwards (a Prometheus response cache / the
+    bench's "series pre-staged" mode).  ``local`` tells the brain there is no
+    I/O to overlap, so it fetches inline instead of through its thread pool."""
+
+    local = True
+    immutable = True        # a query's answer never changes (absolute-time windows need no re-fetch)
+
+    def __init__(self, inner, cache_history: bool = False):
+        self.inner = inner
+        self.cache: dict[str, list[Series]] = {}
+        self.cache_history = cache_history
+        self.misses = 0
+
+    def fetch(self, url: str) -> list[Series]:
+        got = self.cache.get(url)
+        if got is None:
+            self.misses += 1
+            got = self.inner.fetch(url)
+            if self.cache_history or sum(len(s.values) for s in got) <= 4096:
+                self.cache[url] = got
+        return got
+
+
 def dict_set(s: Series, k: str, v: str) -> Series:
     s.labels[k] = v
     return s
@@ -201,6 +226,17 @@ class SourceRouter:
     def synthetic_only(cls, **kw) -> "SourceRouter":
         s = SyntheticSource(**kw)
         return cls(synthetic=s, force="synthetic")
+
+    @property
+    def local(self) -> bool:
+        """Every configured source answers from memory (no network)."""
+        srcs = [self.sources.get(self.force)] if self.force else [v for v in self.sources.values() if v is not None]
+        return bool(srcs) and all(getattr(s, "local", False) for s in srcs)
+
+    @property
+    def immutable(self) -> bool:
+        srcs = [self.sources.get(self.force)] if self.force else [v for v in self.sources.values() if v is not None]
+        return bool(srcs) and all(getattr(s, "immutable", False) for s in srcs)
 
     def fetch(self, store_type: str, url: str) -> list[Series]:
         kind = self.force or store_type or "prometheus"

@@ -70,7 +70,8 @@ def pairwise_tests(cur: torch.Tensor, base: torch.Tensor, cfg: PairwiseConfig = 
         return torch.from_numpy(p), torch.from_numpy(s), torch.from_numpy(d)
     require_native(cur)
     n_cur, n_base = cur.shape[1], base.shape[1]
-    check(n_cur + n_base <= 512, "pairwise kernel supports n_cur + n_base <= 512")
+    if n_cur + n_base > 512:
+        return _pairwise_bucketed(cur, base, cfg)
     pv = torch.empty((R, N_TESTS), dtype=torch.float32, device=cur.device)
     st = torch.empty_like(pv)
     df = torch.empty((R,), dtype=torch.int8, device=cur.device)
@@ -78,6 +79,52 @@ def pairwise_tests(cur: torch.Tensor, base: torch.Tensor, cfg: PairwiseConfig = 
     LIB.call("fm_pairwise_tests", ptr(cur), ldc, n_cur, ptr(base), ldb, n_base, R, mask, anyc,
              float(cfg.p_threshold), cfg.min_mann_white, cfg.min_wilcoxon, cfg.min_kruskal, ptr(pv), ptr(st),
              ptr(df), ptr(suff), stream_of(cur))
+    return pv, st, df
+
+
+def used_width(x: torch.Tensor) -> torch.Tensor:
+    """[R, n] -> [R] int64: 1 + column of the last finite sample (0 if none).
+    Columns past it are padding, so slicing them off leaves every test exact."""
+    idx = torch.arange(1, x.shape[1] + 1, device=x.device, dtype=torch.int64)
+    return (torch.isfinite(x).to(torch.int64) * idx).amax(1) if x.shape[1] else \
+        torch.zeros(x.shape[0], dtype=torch.int64, device=x.device)
+
+
+def _pairwise_bucketed(cur: torch.Tensor, base: torch.Tensor, cfg: PairwiseConfig):
+    """A batch padded wider than the register sort (n_cur + n_base > 512):
+    rows are bucketed by their own used widths.  Rows whose samples fit
+    (<= 256 per side, or <= 512 together when the whole bucket does) run the
+    GPU kernel on a narrowed copy; only rows that are really wider take the
+    fp64 CPU oracle.  One wide job never moves the whole batch off the GPU
+    and never fails it."""
+    R = cur.shape[0]
+    lc, lb = used_width(cur).cpu(), used_width(base).cpu()
+    fit = (lc + lb) <= 512
+    if fit.any() and int(lc[fit].max()) + int(lb[fit].max()) > 512:
+        fit &= (lc <= 256) & (lb <= 256)
+    pv = torch.full((R, N_TESTS), float("nan"), dtype=torch.float32, device=cur.device)
+    st = torch.full_like(pv, float("nan"))
+    df = torch.zeros((R,), dtype=torch.int8, device=cur.device)
+    k = torch.nonzero(fit).flatten()
+    if len(k):
+        a, b = max(1, int(lc[k].max())), max(1, int(lb[k].max()))
+        kd = k.to(cur.device)
+        p1, s1, d1 = pairwise_tests(cur.index_select(0, kd)[:, :a].contiguous(),
+                                    base.index_select(0, kd)[:, :b].contiguous(), cfg)
+        pv.index_copy_(0, kd, p1)
+        st.index_copy_(0, kd, s1)
+        df.index_copy_(0, kd, d1)
+    w = torch.nonzero(~fit).flatten()
+    if len(w):
+        a, b = max(1, int(lc[w].max())), max(1, int(lb[w].max()))
+        wd = w.to(cur.device)
+        mask, anyc = cfg.mask_and_combine()
+        p2, s2, d2 = ref.pairwise_tests(cur.index_select(0, wd)[:, :a].cpu().numpy(),
+                                        base.index_select(0, wd)[:, :b].cpu().numpy(), mask, anyc, cfg.p_threshold,
+                                        cfg.min_mann_white, cfg.min_wilcoxon, cfg.min_kruskal)
+        pv.index_copy_(0, wd, torch.from_numpy(np.asarray(p2, np.float32)).to(cur.device))
+        st.index_copy_(0, wd, torch.from_numpy(np.asarray(s2, np.float32)).to(cur.device))
+        df.index_copy_(0, wd, torch.from_numpy(np.asarray(d2).astype(np.int8)).to(cur.device))
     return pv, st, df
 
 

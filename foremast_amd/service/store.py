@@ -52,6 +52,29 @@ def _stamp(now: float) -> str:
     return rfc3339(datetime.fromtimestamp(now, timezone.utc))
 
 
+def doc_version(d: Document) -> tuple:
+    """What identifies one submission of a job (a resubmission under the same
+    id changes it): the brain re-plans a job when this changes."""
+    return (d.created_at, d.strategy, len(d.current_config), len(d.historical_config))
+
+
+class ClaimBatch:
+    """Result of :meth:`JobStore.claim_batch`: the claimed job ids with an
+    opaque version per job; documents are materialised only for the
+    positions the caller asks for (jobs it has not planned yet)."""
+
+    def __init__(self, ids: list[str], versions: list, resolve):
+        self.ids = ids
+        self.versions = versions
+        self._resolve = resolve
+
+    def __len__(self) -> int:
+        return len(self.ids)
+
+    def docs(self, positions=None) -> list[Document]:
+        return self._resolve(range(len(self.ids)) if positions is None else positions)
+
+
 class JobStore(ABC):
     @abstractmethod
     def put(self, doc: Document) -> None: ...
@@ -94,6 +117,11 @@ class JobStore(ABC):
         for jid, fields in updates:
             self.update(jid, **fields)
 
+    def update_uniform(self, ids: list[str], fields: dict, now: float | None = None) -> None:
+        """The same ``fields`` for many jobs (the brain's per-cycle "still in
+        progress" / "healthy" verdicts): one batch."""
+        self.update_many([(i, fields) for i in ids], now=now)
+
     def add_hpalogs(self, logs: list[HPALog]) -> None:
         for lg in logs:
             self.add_hpalog(lg)
@@ -118,6 +146,13 @@ class JobStore(ABC):
                 if self._cas_claim(d, worker, now):
                     out.append(self.get(d.id))
         return out
+
+    def claim_batch(self, worker: str, limit: int, max_stuck_s: float, now: float | None = None,
+                    shard: tuple[int, int] | None = None) -> ClaimBatch:
+        """:meth:`claim` for a caller that keeps per-job state across cycles:
+        ids + versions, documents on demand."""
+        docs = self.claim(worker, limit, max_stuck_s, now=now, shard=shard)
+        return ClaimBatch([d.id for d in docs], [doc_version(d) for d in docs], lambda pos: [docs[i] for i in pos])
 
     def _claim_candidates(self) -> list[Document]:
         return [d for d in self.all_docs() if d.status in ST.CLAIMABLE or d.status in ST.IN_PROGRESS]
@@ -148,6 +183,13 @@ class MemoryStore(JobStore):
         self._lock = threading.RLock()
         self._claimable = np.zeros(0, bool)
         self._inprog = np.zeros(0, bool)
+        # uniform bulk updates are recorded per job as an index into
+        # ``_pending`` and applied to the document object when it is read
+        self._pend = np.zeros(0, np.int32)
+        self._pending: list[tuple[dict, str]] = []
+        self._ver = np.zeros(0, np.int64)          # bumped by every put (create / replace)
+        self._ids = np.zeros(0, object)
+        self._puts = 0
 
     def _code(self, status: str) -> int:
         c = self._codes.get(status)
@@ -169,6 +211,10 @@ class MemoryStore(JobStore):
                     n = max(1024, 2 * len(self._st))
                     self._st = np.concatenate([self._st, np.zeros(n - len(self._st), np.int16)])
                     self._mod = np.concatenate([self._mod, np.zeros(n - len(self._mod))])
+                    self._pend = np.concatenate([self._pend, np.full(n - len(self._pend), -1, np.int32)])
+                    self._ver = np.concatenate([self._ver, np.zeros(n - len(self._ver), np.int64)])
+                    self._ids = np.concatenate([self._ids, np.empty(n - len(self._ids), object)])
+                self._ids[i] = d.id
                 for w, o in self._owners.items():
                     if len(o) <= i:
                         self._owners[w] = np.concatenate([o, np.full(len(self._st) - len(o), -1, np.int32)])
@@ -177,24 +223,62 @@ class MemoryStore(JobStore):
                 self._objs[i] = d
                 for o in self._owners.values():
                     o[i] = -1
+            self._pend[i] = -1
+            self._puts += 1
+            self._ver[i] = self._puts
             self._st[i] = self._code(d.status)
             self._mod[i] = _ts(d)
+
+    def _pend_merge(self, idx: np.ndarray, fields: dict, stamp: str) -> None:
+        """Record ``fields`` as pending for the jobs ``idx``.  Jobs that still
+        carry an older pending update get one merged entry per distinct older
+        update (a handful per cycle), so no document object is touched."""
+        old = self._pend[idx]
+        base = len(self._pending)
+        self._pending.append((dict(fields), stamp))
+        self._pend[idx] = base
+        if (old >= 0).any():
+            ks, inv = np.unique(old, return_inverse=True)
+            for j, k in enumerate(ks):
+                if k < 0:
+                    continue
+                merged = dict(self._pending[k][0])
+                merged.update(fields)
+                self._pending.append((merged, stamp))
+                self._pend[idx[inv == j]] = len(self._pending) - 1
+        if len(self._pending) > 65536:           # re-index the live entries
+            live = np.flatnonzero(self._pend >= 0)
+            ks, inv = np.unique(self._pend[live], return_inverse=True)
+            self._pending = [self._pending[k] for k in ks]
+            self._pend[live] = inv.astype(np.int32)
+
+    def _obj(self, i: int) -> Document:
+        """The live document with any pending uniform update applied."""
+        d = self._objs[i]
+        k = self._pend[i]
+        if k >= 0:
+            fields, stamp = self._pending[k]
+            for f, v in fields.items():
+                setattr(d, f, v)
+            d.modified_at = stamp
+            self._pend[i] = -1
+        return d
 
     def get(self, job_id: str) -> Document | None:
         with self._lock:
             i = self._index.get(job_id)
-            return Document.from_dict(self._objs[i].to_dict()) if i is not None else None
+            return Document.from_dict(self._obj(i).to_dict()) if i is not None else None
 
     def all_docs(self) -> list[Document]:
         with self._lock:
-            return [Document.from_dict(d.to_dict()) for d in self._objs]
+            return [Document.from_dict(self._obj(i).to_dict()) for i in range(len(self._objs))]
 
     def update(self, job_id: str, **fields) -> Document | None:
         with self._lock:
             i = self._index.get(job_id)
             if i is None:
                 return None
-            d = self._objs[i]
+            d = self._obj(i)
             for k, v in fields.items():
                 setattr(d, k, v)
             now = time.time()
@@ -213,7 +297,7 @@ class MemoryStore(JobStore):
                 if i < 0:
                     codes[k] = -1
                     continue
-                d = self._objs[i]
+                d = self._obj(i)
                 for f, v in fields.items():
                     setattr(d, f, v)
                 d.modified_at = stamp
@@ -221,6 +305,22 @@ class MemoryStore(JobStore):
             ok = idx >= 0
             self._st[idx[ok]] = codes[ok]
             self._mod[idx[ok]] = _ts_str(stamp)
+
+    def update_uniform(self, ids: list[str], fields: dict, now: float | None = None) -> None:
+        """Vectorised: status codes and lease times are array stores; the
+        document objects pick the fields up lazily when next read."""
+        if not ids:
+            return
+        now = time.time() if now is None else now
+        stamp = _stamp(now)
+        with self._lock:
+            get = self._index.get
+            idx = np.fromiter((get(j, -1) for j in ids), np.int64, len(ids))
+            idx = idx[idx >= 0]
+            self._pend_merge(idx, fields, stamp)
+            if "status" in fields:
+                self._st[idx] = self._code(fields["status"])
+            self._mod[idx] = _ts_str(stamp)
 
     def _owner_of(self, world: int) -> np.ndarray:
         from ..parallel.dist import service_owner
@@ -237,29 +337,32 @@ class MemoryStore(JobStore):
             o[i] = service_owner(d.namespace, d.app_name, world)
         return o
 
+    def _claim_idx(self, limit, max_stuck_s, now, owner=None, shard=None) -> np.ndarray:
+        n = len(self._objs)
+        if n == 0 or not self._names:
+            return np.zeros(0, np.int64)
+        st = self._st[:n]
+        mask = self._claimable[st] | (self._inprog[st] & (now - self._mod[:n] > max_stuck_s))
+        if shard is not None:
+            rank, world = shard
+            mask &= self._owner_of(world)[:n] == rank
+        idx = np.flatnonzero(mask)
+        if owner is not None:
+            idx = np.array([i for i in idx if owner(self._objs[i])], np.int64)
+        # oldest lease first (fair across cycles), stable in insertion order
+        return idx[np.argsort(self._mod[idx], kind="stable")][:limit]
+
     def claim(self, worker, limit, max_stuck_s, now=None, owner=None, shard=None):
         now = time.time() if now is None else now
         with self._lock:
-            n = len(self._objs)
-            if n == 0 or not self._names:
-                return []
-            st = self._st[:n]
-            mask = self._claimable[st] | (self._inprog[st] & (now - self._mod[:n] > max_stuck_s))
-            if shard is not None:
-                rank, world = shard
-                mask &= self._owner_of(world)[:n] == rank
-            idx = np.flatnonzero(mask)
-            if owner is not None:
-                idx = np.array([i for i in idx if owner(self._objs[i])], np.int64)
-            # oldest lease first (fair across cycles), stable in insertion order
-            idx = idx[np.argsort(self._mod[idx], kind="stable")][:limit]
+            idx = self._claim_idx(limit, max_stuck_s, now, owner, shard)
             if len(idx) == 0:
                 return []
             stamp = _stamp(now)
             code = self._code(ST.PREPROCESS_INPROGRESS)
             out = []
             for i in idx:
-                d = self._objs[i]
+                d = self._obj(i)
                 d.status = ST.PREPROCESS_INPROGRESS
                 d.processing_content = worker
                 d.modified_at = stamp
@@ -267,6 +370,27 @@ class MemoryStore(JobStore):
             self._st[idx] = code
             self._mod[idx] = _ts_str(stamp)
             return out
+
+    def claim_batch(self, worker, limit, max_stuck_s, now=None, shard=None) -> ClaimBatch:
+        """Columnar lease claim: status codes, lease times and the lease
+        fields are array stores (the fields reach the document objects lazily,
+        like :meth:`update_uniform`); per-job Python work is only the id list."""
+        now = time.time() if now is None else now
+        with self._lock:
+            idx = self._claim_idx(limit, max_stuck_s, now, None, shard)
+            if len(idx) == 0:
+                return ClaimBatch([], [], lambda pos: [])
+            stamp = _stamp(now)
+            self._pend_merge(idx, {"status": ST.PREPROCESS_INPROGRESS, "processing_content": worker}, stamp)
+            self._st[idx] = self._code(ST.PREPROCESS_INPROGRESS)
+            self._mod[idx] = _ts_str(stamp)
+            ids = self._ids[idx].tolist()
+            vers = self._ver[idx].tolist()
+
+        def resolve(pos):
+            with self._lock:
+                return [self._obj(int(idx[p])) for p in pos]
+        return ClaimBatch(ids, vers, resolve)
 
     def add_hpalog(self, log: HPALog) -> None:
         with self._lock:

@@ -131,6 +131,46 @@ def test_gpu_pairwise_matches_reference(cuda, n1, n2, nan_frac):
     assert (d == d0).mean() > 0.995
 
 
+def _mixed_width_batch():
+    """Left-packed rows padded to 700 + 700 columns: most rows narrow, a few
+    wide on one side (fit the kernel only in the <= 256 / side bucket) and two
+    wider than 512 together (CPU oracle)."""
+    rng = np.random.default_rng(7)
+    R = 40
+    cur = np.full((R, 700), np.nan, np.float32)
+    base = np.full((R, 700), np.nan, np.float32)
+    widths = [(50, 50)] * 30 + [(300, 40)] * 4 + [(40, 300)] * 4 + [(400, 300), (700, 700)]
+    for r, (a, b) in enumerate(widths):
+        cur[r, :a] = np.round(rng.normal(0, 1, a), 1)
+        base[r, :b] = np.round(rng.normal(0.2, 1.1, b), 1)
+    cur[3, 10] = np.nan                      # a gap inside a row stays a gap
+    return cur, base
+
+
+def test_pairwise_bucketed_equals_reference_cpu():
+    cur, base = _mixed_width_batch()
+    cfg = C.PairwiseConfig("ALL")
+    P0, S0, d0 = ref.pairwise_tests(cur, base, *cfg.mask_and_combine(), cfg.p_threshold, 20, 20, 5)
+    pv, st, d = C._pairwise_bucketed(torch.from_numpy(cur), torch.from_numpy(base), cfg)
+    np.testing.assert_allclose(pv.numpy(), P0.astype(np.float32), rtol=1e-6, equal_nan=True)
+    np.testing.assert_allclose(st.numpy(), S0.astype(np.float32), rtol=1e-6, equal_nan=True)
+    np.testing.assert_array_equal(d.numpy(), d0)
+
+
+@pytest.mark.gpu
+def test_gpu_pairwise_wide_batch_buckets_rows(cuda):
+    """a batch padded past 512 columns no longer raises; rows
+    that fit run on the GPU, the rest on the oracle."""
+    cur, base = _mixed_width_batch()
+    cfg = C.PairwiseConfig("ALL")
+    P0, S0, d0 = ref.pairwise_tests(cur, base, *cfg.mask_and_combine(), cfg.p_threshold, 20, 20, 5)
+    pv, st, d = C.pairwise_tests(torch.from_numpy(cur).to(cuda), torch.from_numpy(base).to(cuda), cfg)
+    pv, d = pv.cpu().numpy(), d.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(pv), np.isnan(P0))
+    np.testing.assert_allclose(np.nan_to_num(pv), np.nan_to_num(P0), rtol=2e-4, atol=2e-6)
+    np.testing.assert_array_equal(d[-2:], d0[-2:])
+
+
 @pytest.mark.gpu
 def test_gpu_pairwise_scipy_spot(cuda):
     cur, base = _data(16, 50, 50, seed=3)

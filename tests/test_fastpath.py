@@ -202,3 +202,60 @@ def test_static_rows_are_written_once_and_released():
 @pytest.mark.gpu
 def test_gpu_fast_path_equals_general_path(cuda):
     _run_pair(device=cuda)
+
+
+def test_fast_path_with_staged_source_equals_general_path():
+    """Pre-staged (immutable) series: re-examined canary jobs skip the
+    re-fetch and reuse their group arrays; verdicts must not change."""
+    from foremast_amd.engine.sources import StagedSource, SyntheticSource
+
+    def mk(resident):
+        clock = Clock()
+        store = MemoryStore()
+        client = AnalystClient.for_app(create_app(store), clock=clock)
+        exp = BrainExporter()
+        src = SourceRouter(synthetic=StagedSource(SyntheticSource(faults=FAULTS, fault_after=T0 + 120)),
+                           force="synthetic")
+        brain = Brain(store, BrainConfig(), sources=src, clock=clock, exporter=exp, worker_id="w0",
+                      resident_history=resident)
+        return clock, store, client, brain, exp
+    a, b = mk(True), mk(False)
+    ids = _submit(a[2])
+    assert ids == _submit(b[2])
+    for cyc in range(4):
+        ra, rb = a[3].run_once(), b[3].run_once()
+        assert ra["claimed"] == rb["claimed"]
+        for jid in ids:
+            da, db = a[1].get(jid), b[1].get(jid)
+            assert (da.status, da.reason, da.anomaly_info) == (db.status, db.reason, db.anomaly_info), (cyc, jid)
+        a[0].t += 60
+        b[0].t += 60
+    assert a[3].sources.immutable and a[3].fast._garr
+
+
+def test_memory_store_claim_batch_and_uniform_updates():
+    from foremast_amd.api import jobs as J
+    from foremast_amd.api.models import ApplicationHealthAnalyzeRequest
+    from foremast_amd.service.store import doc_version
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=Clock())
+    ids = _submit(client)[:4]
+    b = store.claim_batch("w1", 100, 90.0, now=T0)
+    assert set(ids) <= set(b.ids) and len(b.versions) == len(b.ids)
+    assert store.get(ids[0]).status == ST.PREPROCESS_INPROGRESS and store.get(ids[0]).processing_content == "w1"
+    assert store.claim_batch("w2", 100, 90.0, now=T0 + 1).ids == []          # leased
+    store.update_uniform(ids[:2], {"status": ST.PREPROCESS_COMPLETED}, now=T0 + 2)
+    b2 = store.claim_batch("w2", 100, 90.0, now=T0 + 3)
+    assert b2.ids == ids[:2] and b2.versions == [b.versions[b.ids.index(i)] for i in ids[:2]]
+    d = b2.docs([0])[0]
+    assert d.id == ids[0] and d.processing_content == "w2"
+    # a resubmission under the same id changes the version
+    old = store.get(ids[1])
+    old.status = ST.INITIAL
+    store.put(old)
+    b3 = store.claim_batch("w3", 100, 90.0, now=T0 + 4)
+    assert b3.ids == [ids[1]] and b3.versions[0] != b2.versions[1]
+    assert isinstance(doc_version(old), tuple)
+    store.update_uniform(ids, {"status": ST.COMPLETED_HEALTH, "reason": ""}, now=T0 + 5)
+    assert {store.get(i).status for i in ids} == {ST.COMPLETED_HEALTH}
+    assert store.claim_batch("w4", 100, 1e9, now=T0 + 6).ids == []
