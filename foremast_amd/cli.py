@@ -86,7 +86,15 @@ def brain_main(argv=None) -> None:  # pragma: no cover - process entry
     ckpt = os.environ.get("BRAIN_CHECKPOINT_DIR")
     if ckpt:
         brain.load_checkpoint(ckpt)
-    brain.run_forever()
+    # SIGTERM (pod shutdown; torchrun forwards it to every rank) ends the
+    # loop after the current cycle and writes a final checkpoint
+    import signal
+    import threading
+    stop = threading.Event()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda *_: stop.set())
+    brain.run_forever(stop=stop, checkpoint_dir=ckpt or None,
+                      checkpoint_every=int(os.environ.get("BRAIN_CHECKPOINT_EVERY", "30")))
 
 
 def main(argv=None) -> int:

@@ -448,16 +448,32 @@ class Brain:
                 outcome[st] = outcome.get(st, 0) + 1
         return len(rows)
 
-    def run_forever(self, stop=None, poll: float | None = None) -> None:  # pragma: no cover - service loop
+    def run_forever(self, stop=None, poll: float | None = None, checkpoint_dir: str | None = None,
+                    checkpoint_every: int = 30) -> None:
+        """Service loop.  With ``checkpoint_dir`` the state is saved every
+        ``checkpoint_every`` cycles and once more when ``stop`` is set (the
+        CLI sets it on SIGTERM), so a restarted brain resumes HPA hysteresis
+        and its fitted-model cache."""
         poll = self.cfg.poll_interval if poll is None else poll
-        while stop is None or not stop.is_set():
-            try:
-                r = self.run_once()
-                if r.get("claimed", 0) == 0:
-                    time.sleep(poll)
-            except Exception:
-                log.exception("brain cycle failed")
-                time.sleep(poll)
+        n = 0
+        try:
+            while stop is None or not stop.is_set():
+                try:
+                    r = self.run_once()
+                    n += 1
+                    if checkpoint_dir and checkpoint_every > 0 and n % checkpoint_every == 0:
+                        self.save_checkpoint(checkpoint_dir)
+                    if r.get("claimed", 0) == 0:
+                        (stop.wait(poll) if stop is not None else time.sleep(poll))
+                except Exception:
+                    log.exception("brain cycle failed")
+                    (stop.wait(poll) if stop is not None else time.sleep(poll))
+        finally:
+            if checkpoint_dir:
+                try:
+                    self.save_checkpoint(checkpoint_dir)
+                except Exception:  # noqa: BLE001 - shutting down
+                    log.exception("final checkpoint failed")
 
     # ------------------------------------------------------------------ verdicts
     def _finish(self, wk: Work, rows: list[Row], res, sl: slice, now: float, updates: list, hpalogs: list) -> str:
@@ -583,30 +599,62 @@ class Brain:
             t.update({"lstm." + k: v for k, v in self.lstm_model.state_dict().items()})
         ct, cmeta = self.model_cache.state_tensors()
         t.update(ct)
-        return t, {"hpa_jobs": ids, "worker": self.worker, "algorithm": self.cfg.ml_algorithm, "model_cache": cmeta}
+        owners = [list(self.hpa.owner.get(i, ("", ""))) for i in ids]
+        return t, {"hpa_jobs": ids, "hpa_owner_keys": owners, "worker": self.worker,
+                   "algorithm": self.cfg.ml_algorithm, "model_cache": cmeta, "rank": self.info.rank,
+                   "world": self.info.world, "cycles": self.cycles}
 
     def save_checkpoint(self, dirpath: str):
+        """This rank's state (``engine-r<rank>of<world>-<ms>.safetensors``)."""
         from . import checkpoint
         t, meta = self.state_tensors()
-        return checkpoint.save(dirpath, t, meta)
+        return checkpoint.save(dirpath, t, meta, tag=checkpoint.rank_tag(self.info.rank, self.info.world))
+
+    def _owns_key(self, namespace: str, app: str) -> bool:
+        if self.info.world <= 1:
+            return True
+        return D.service_owner(namespace, app, self.info.world) == self.info.rank
 
     def load_checkpoint(self, dirpath: str) -> bool:
+        """Resume from this rank's latest checkpoint, or — after a world-size
+        change — from every rank's checkpoint of the previous world, keeping
+        only the HPA hysteresis and fitted models of services this rank owns
+        now (``service_owner`` of ``namespace:app``)."""
         from . import checkpoint
-        got = checkpoint.load_latest(dirpath)
-        if got is None:
+        own = checkpoint.load_latest(dirpath, checkpoint.rank_tag(self.info.rank, self.info.world))
+        sets = [own] if own is not None else checkpoint.load_any_world(dirpath)
+        if not sets:
             return False
-        t, meta = got
-        jobs = meta.get("hpa_jobs", [])
-        if jobs:
-            idx = self.hpa.slots(jobs)
-            d = self.hpa.device
-            self.hpa.scatter(idx, MI.HpaState(t["hpa.last_dir"].to(d), t["hpa.last_time"].to(d), t["hpa.flips"].to(d),
-                                              t["hpa.flip_t0"].to(d)))
-        lstm = {k[5:]: v for k, v in t.items() if k.startswith("lstm.")}
-        if lstm and self.lstm_model is not None:
-            self.lstm_model.load_state_dict(lstm)
-        self.model_cache.load_state(t, meta.get("model_cache", []), self.device)
+        first = True
+        for t, meta in sets:
+            jobs = meta.get("hpa_jobs", [])
+            keys = meta.get("hpa_owner_keys") or [_hpa_owner_of(j) for j in jobs]
+            sel = [k for k, (ns, app) in enumerate(keys) if self._owns_key(ns, app)]
+            if sel:
+                ix = torch.as_tensor(sel, dtype=torch.int64)
+                mine = [jobs[k] for k in sel]
+                idx = self.hpa.slots(mine)
+                for j, (ns, app) in zip(mine, [keys[k] for k in sel]):
+                    self.hpa.owner[j] = (ns, app)
+                d = self.hpa.device
+                self.hpa.scatter(idx, MI.HpaState(*(t[f"hpa.{n}"].index_select(0, ix).to(d)
+                                                   for n in ("last_dir", "last_time", "flips", "flip_t0"))))
+            lstm = {k[5:]: v for k, v in t.items() if k.startswith("lstm.")}
+            if lstm and self.lstm_model is not None and first:
+                self.lstm_model.load_state_dict(lstm)
+
+            def keep(key):
+                ns, _, app = str(key[0]).partition("/")
+                return self._owns_key(ns, app)
+            self.model_cache.load_state(t, meta.get("model_cache", []), self.device, keep=keep, clear=first)
+            first = False
         return True
+
+
+def _hpa_owner_of(job_id: str) -> tuple[str, str]:
+    """HPA job ids are ``<app>:<namespace>:hpa`` (elasticsearchstore.go:31-33)."""
+    parts = job_id.split(":")
+    return (parts[1], parts[0]) if len(parts) == 3 else ("", job_id)
 
 
 def _label(q: str, name: str) -> str:

@@ -19,27 +19,34 @@ from safetensors.torch import load_file, save_file
 FORMAT_VERSION = "foremast-amd/engine-checkpoint/1"
 
 
-def save(dirpath: str, tensors: dict[str, torch.Tensor], meta: dict, step: int | None = None) -> Path:
+def rank_tag(rank: int, world: int) -> str:
+    return f"-r{rank}of{world}" if world > 1 else ""
+
+
+def save(dirpath: str, tensors: dict[str, torch.Tensor], meta: dict, step: int | None = None, tag: str = "",
+         keep: int = 3) -> Path:
+    """``tag`` separates the ranks of a data-parallel brain
+    (``-r<rank>of<world>``): each rank writes its own file and LATEST pointer.
+    The ``keep`` newest files of the tag are retained."""
     d = Path(dirpath)
     d.mkdir(parents=True, exist_ok=True)
-    step = int(time.time()) if step is None else step
-    path = d / f"engine-{step}.safetensors"
-    tmp = d / f".engine-{step}.tmp"
+    step = int(time.time() * 1000) if step is None else step
+    path = d / f"engine{tag}-{step}.safetensors"
+    tmp = d / f".engine{tag}-{step}.tmp"
     md = {"format": FORMAT_VERSION, "meta": json.dumps(meta), "saved_at": str(time.time())}
     save_file({k: v.detach().contiguous().cpu() for k, v in tensors.items()}, str(tmp), metadata=md)
     os.replace(tmp, path)
-    latest_tmp = d / ".LATEST.tmp"
+    latest_tmp = d / f".LATEST{tag}.tmp"
     latest_tmp.write_text(path.name)
-    os.replace(latest_tmp, d / "LATEST")
+    os.replace(latest_tmp, d / f"LATEST{tag}")
+    old = sorted(d.glob(f"engine{tag}-*.safetensors"), key=lambda p: p.stat().st_mtime)
+    for p in old[:-keep] if keep > 0 else []:
+        if p != path:
+            p.unlink(missing_ok=True)
     return path
 
 
-def load_latest(dirpath: str) -> tuple[dict[str, torch.Tensor], dict] | None:
-    d = Path(dirpath)
-    lf = d / "LATEST"
-    if not lf.exists():
-        return None
-    path = d / lf.read_text().strip()
+def _read(path: Path) -> tuple[dict[str, torch.Tensor], dict, float] | None:
     if not path.exists():
         return None
     from safetensors import safe_open
@@ -47,4 +54,42 @@ def load_latest(dirpath: str) -> tuple[dict[str, torch.Tensor], dict] | None:
         md = f.metadata() or {}
     if md.get("format") != FORMAT_VERSION:
         raise ValueError(f"unsupported checkpoint format {md.get('format')!r}")
-    return load_file(str(path)), json.loads(md.get("meta", "{}"))
+    return load_file(str(path)), json.loads(md.get("meta", "{}")), float(md.get("saved_at", "0"))
+
+
+def load_latest(dirpath: str, tag: str = "") -> tuple[dict[str, torch.Tensor], dict] | None:
+    d = Path(dirpath)
+    lf = d / f"LATEST{tag}"
+    if not lf.exists():
+        return None
+    got = _read(d / lf.read_text().strip())
+    return None if got is None else got[:2]
+
+
+def load_any_world(dirpath: str) -> list[tuple[dict[str, torch.Tensor], dict]]:
+    """Every rank's latest checkpoint of the most recently saved world size
+    (a restart with a different world re-shards from all of them)."""
+    d = Path(dirpath)
+    sets: dict[int, list[tuple[float, Path]]] = {}
+    for lf in d.glob("LATEST*"):
+        name = lf.name[len("LATEST"):]
+        world = 1
+        if name.startswith("-r") and "of" in name:
+            try:
+                world = int(name.split("of", 1)[1])
+            except ValueError:
+                continue
+        elif name:
+            continue
+        p = d / lf.read_text().strip()
+        if p.exists():
+            sets.setdefault(world, []).append((p.stat().st_mtime, p))
+    if not sets:
+        return []
+    world = max(sets, key=lambda w: max(t for t, _ in sets[w]))
+    out = []
+    for _, p in sets[world]:
+        got = _read(p)
+        if got is not None:
+            out.append(got[:2])
+    return out

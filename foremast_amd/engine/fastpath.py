@@ -150,6 +150,7 @@ class HpaTable:
     def __init__(self, device):
         self.device = torch.device(device)
         self.slot: dict[str, int] = {}
+        self.owner: dict[str, tuple[str, str]] = {}     # job id -> (namespace, app): checkpoint re-sharding
         self.state = MI.HpaState.zeros(0, self.device)
 
     def slots(self, ids: list[str]) -> torch.Tensor:
@@ -600,6 +601,8 @@ class FastPath:
         dev = self.b.device
         ids = [w.doc.id for w in works]
         sl = self.hpa.slots(ids)
+        for w in works:
+            self.hpa.owner[w.doc.id] = (w.plan.namespace, w.doc.app_name)
         sub = self.hpa.gather(sl)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         cfg = self.b.cfg

@@ -267,14 +267,26 @@ class ModelCache:
                          "t_last": slab.t_last[sl].tolist(), "fitted_at": slab.fitted_at[sl].tolist()})
         return t, meta
 
-    def load_state(self, t: dict[str, torch.Tensor], meta: list, device, prefix: str = "cache.") -> None:
-        self.entries.clear()
-        self.slabs.clear()
-        self._by_kind_m.clear()
-        self._gen += 1
+    def load_state(self, t: dict[str, torch.Tensor], meta: list, device, prefix: str = "cache.",
+                   keep=None, clear: bool = True) -> None:
+        """Restore the slabs of :meth:`state_tensors`.  ``keep(key) -> bool``
+        selects entries (re-sharding after a world-size change keeps the
+        series this rank owns); ``clear=False`` merges several checkpoints."""
+        if clear:
+            self.entries.clear()
+            self.slabs.clear()
+            self._by_kind_m.clear()
+            self._gen += 1
         for gi, g in enumerate(meta):
             p = f"{prefix}{gi}."
             kind, m = int(g["kind"]), int(g["m"])
-            md = SM.ESState(kind, m, t[p + "params"], t[p + "state"], t.get(p + "season") if kind >= 2 else None,
-                            t[p + "sse"], t[p + "nobs"])
-            self._store([tuple(k) for k in g["keys"]], kind, m, md, g["t_last"], g["fitted_at"], device)
+            keys = [tuple(k) for k in g["keys"]]
+            sel = [i for i, k in enumerate(keys) if keep is None or keep(k)]
+            if not sel:
+                continue
+            ix = torch.as_tensor(sel, dtype=torch.int64)
+            pick = lambda x: None if x is None else x.index_select(0, ix)
+            md = SM.ESState(kind, m, pick(t[p + "params"]), pick(t[p + "state"]),
+                            pick(t.get(p + "season")) if kind >= 2 else None, pick(t[p + "sse"]), pick(t[p + "nobs"]))
+            self._store([keys[i] for i in sel], kind, m, md, np.asarray(g["t_last"])[sel],
+                        np.asarray(g["fitted_at"])[sel], device)

@@ -234,3 +234,77 @@ def test_stage_spans_and_json_logs(capsys):
     rec = _json.loads(line)
     assert rec["msg"] == "tick" and rec["rows"] == 3 and rec["component"] == "brain" and rec["level"] == "info"
     logging.getLogger().handlers[:] = []
+
+
+def test_service_loop_checkpoints_and_resumes_hysteresis(tmp_path):
+    """the running loop saves every N cycles and on stop
+    (SIGTERM in the CLI); a restarted brain continues the HPA hysteresis and
+    keeps its fitted-model cache."""
+    import threading
+    clock, store, client, brain, exp = _setup(algorithm="double_exponential_smoothing")
+    brain.cfg.hpa_forecast_algorithm = "double_exponential_smoothing"
+    for app in ("demo", "other"):
+        client.start_analyzing("default", app, None, _metrics(), 10, "hpa", ["cpu", "latency"])
+    stop = threading.Event()
+    cycles = {"n": 0}
+    orig = brain.run_once
+
+    def counted():
+        cycles["n"] += 1
+        clock.t += 60
+        if cycles["n"] >= 5:
+            stop.set()
+        return orig()
+    brain.run_once = counted
+    brain.run_forever(stop=stop, poll=0.0, checkpoint_dir=str(tmp_path), checkpoint_every=2)
+    files = sorted(p.name for p in tmp_path.glob("engine-*.safetensors"))
+    assert len(files) >= 2 and (tmp_path / "LATEST").exists()      # periodic + final
+    # "kill" and restart: a fresh brain on the same store resumes
+    b2 = Brain(store, brain.cfg, sources=brain.sources, clock=clock, worker_id="w1")
+    assert b2.load_checkpoint(str(tmp_path))
+    for j, st in brain.hpa_state.items():
+        for f in ("last_dir", "last_time", "flips", "flip_t0"):
+            np.testing.assert_array_equal(getattr(b2.hpa_state[j], f).numpy(), getattr(st, f).numpy())
+    assert len(b2.model_cache) == len(brain.model_cache) > 0
+    h0 = b2.model_cache.hits
+    clock.t += 60
+    store.update_uniform([d.id for d in store.all_docs()], {"status": "preprocess_completed"}, now=clock.t)
+    b2.run_once()
+    assert b2.model_cache.hits > h0                                  # cached fits reused after restart
+
+
+def test_checkpoint_reshards_after_world_size_change(tmp_path):
+    """Two ranks save (world 2); a single-rank restart loads both files and a
+    rank of a new world 3 keeps only the services it owns now."""
+    from foremast_amd.engine.fastpath import HpaTable
+    from foremast_amd.ops import misc as MI
+    from foremast_amd.parallel import dist as D
+    import torch
+    apps = [f"app{i}" for i in range(12)]
+    for rank in range(2):
+        b = Brain(MemoryStore(), BrainConfig(), worker_id=f"r{rank}")
+        b.info = D.DistInfo(rank, 2, rank)
+        mine = [a for a in apps if D.service_owner("ns", a, 2) == rank]
+        ids = [f"{a}:ns:hpa" for a in mine]
+        sl = b.hpa.slots(ids)
+        for a, j in zip(mine, ids):
+            b.hpa.owner[j] = ("ns", a)
+        n = len(ids)
+        b.hpa.scatter(sl, MI.HpaState(torch.ones(n, dtype=b.hpa.state.last_dir.dtype),
+                                      torch.arange(n, dtype=b.hpa.state.last_time.dtype) + 100 * rank,
+                                      torch.zeros(n, dtype=b.hpa.state.flips.dtype),
+                                      torch.zeros(n, dtype=b.hpa.state.flip_t0.dtype)))
+        b.save_checkpoint(str(tmp_path))
+    assert {p.name for p in tmp_path.glob("LATEST*")} == {"LATEST-r0of2", "LATEST-r1of2"}
+    one = Brain(MemoryStore(), BrainConfig(), worker_id="solo")
+    assert one.load_checkpoint(str(tmp_path))
+    assert set(one.hpa_state) == {f"{a}:ns:hpa" for a in apps}
+    got = {}
+    for rank in range(3):
+        b = Brain(MemoryStore(), BrainConfig(), worker_id=f"n{rank}")
+        b.info = D.DistInfo(rank, 3, rank)
+        assert b.load_checkpoint(str(tmp_path))
+        for j in b.hpa_state:
+            assert D.service_owner("ns", j.split(":")[0], 3) == rank
+            got[j] = rank
+    assert set(got) == {f"{a}:ns:hpa" for a in apps}

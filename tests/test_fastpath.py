@@ -107,7 +107,10 @@ def _run_pair(device="cpu"):
             va, vb = ta.get(k), tb.get(k)
             if "forecast" in k[0]:
                 continue
-            assert (np.isnan(va) and np.isnan(vb)) or va == pytest.approx(vb, rel=1e-6, abs=1e-9), (cyc, k, va, vb)
+            # GPU: the resident front kernel and the general path's stats kernel
+            # reduce in different orders (fp32 bounds agree to ~10 ulp)
+            rel = 1e-6 if str(device) == "cpu" else 2e-5
+            assert (np.isnan(va) and np.isnan(vb)) or va == pytest.approx(vb, rel=rel, abs=1e-9), (cyc, k, va, vb)
         a[0].t += 240
         b[0].t += 240
     return a, b, ids_a, history
