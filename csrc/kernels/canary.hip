@@ -791,46 +791,6 @@ FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const fl
 // the block to the masked per-element path.  Per element that is ~0.75 VALU
 // instructions instead of ~8, which leaves the CU's issue slots to the
 // pairwise kernel running concurrently on the side stream.
-// Mean / population std / finite count over the finite samples of a row
-// (the masked path of block_row_stats, for rows with missing samples).  It
-// re-reads the row one float4 at a time instead of reusing the fast path's
-// register image, so the masked path adds no register pressure.
-__device__ __forceinline__ void block_row_stats_masked(const float* __restrict__ hrow, int T, double* red, int* redi,
-                                                       float& mf, float& sd, int& n) {
-  typedef float nt4 __attribute__((ext_vector_type(4)));
-  const int tid = threadIdx.x;
-  const int nq = (T + 3) >> 2;
-  const nt4* h = reinterpret_cast<const nt4*>(hrow);
-  double s = 0.0;
-  int cnt = 0;
-#pragma unroll 2
-  for (int qi = tid; qi < nq; qi += 256) {
-    const nt4 v = h[qi];
-    float ls = 0.f;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float x = v[c];
-      if (qi * 4 + c < T && isfinite(x)) { ls += x; ++cnt; }
-    }
-    s += ls;
-  }
-  const double t2 = block_sum<256>(s, red);
-  n = block_sum<256>(cnt, redi);
-  mf = n > 0 ? (float)(t2 / n) : 0.f;
-  float ss = 0.f;
-#pragma unroll 2
-  for (int qi = tid; qi < nq; qi += 256) {
-    const nt4 v = h[qi];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float x = v[c];
-      if (qi * 4 + c < T && isfinite(x)) { const float d = x - mf; ss += d * d; }
-    }
-  }
-  const double sst = block_sum<256>((double)ss, red);
-  sd = n > 0 ? (float)sqrt(sst / n) : 0.f;
-}
-
 template <int NV>
 __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, int T, double* red, int* redi,
                                                 float& mf, float& sd, int& n) {
@@ -881,9 +841,40 @@ __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, 
     sd = (float)sqrt(sst / n);
     return;
   }
-  // rows with missing samples: re-read the row in the out-of-line masked
-  // path, so the fast path's registers are all the kernel needs
-  block_row_stats_masked(hrow, T, red, redi, mf, sd, n);
+  // Rows with missing samples (Prometheus gaps; the resident store's NaN
+  // padding in front of a right-aligned window): masked mean / variance over
+  // the register image already loaded -- no second or third pass over HBM.
+  // Only this block-uniform branch pays the per-element finite tests.
+  f2 ms = {0.f, 0.f};
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int qi = tid + j * 256;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = q[j][c];
+      const bool ok = qi < nq && qi * 4 + c < T && isfinite(x);
+      ms[c & 1] += ok ? x : 0.f;
+      cnt += ok ? 1 : 0;
+    }
+  }
+  const double t2 = block_sum<256>((double)ms.x + (double)ms.y, red);
+  n = block_sum<256>(cnt, redi);
+  mf = n > 0 ? (float)(t2 / n) : 0.f;
+  f2 a2 = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int qi = tid + j * 256;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float x = q[j][c];
+      const bool ok = qi < nq && qi * 4 + c < T && isfinite(x);
+      const float d = ok ? x - mf : 0.f;
+      a2[c & 1] += d * d;
+    }
+  }
+  const double sst = block_sum<256>((double)a2.x + (double)a2.y, red);
+  sd = n > 0 ? (float)sqrt(sst / n) : 0.f;
 }
 
 // ---------------------------------------------------------------------------

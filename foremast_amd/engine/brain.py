@@ -350,8 +350,8 @@ class Brain:
         with self.spans.span("persist"):
             if hpalogs:
                 self.store.add_hpalogs(hpalogs)
-            for ids, fields in bulk:
-                self.store.update_uniform(ids, fields, now=now)
+            for ids, fields, handles in bulk:
+                self.store.update_uniform(ids, fields, now=now, handles=handles)
             self.store.update_many(updates)
         if self.exporter is not None:
             self.exporter.tick_seconds.observe(time.perf_counter() - t0)
@@ -359,16 +359,19 @@ class Brain:
             for s_, c in outcome.items():
                 self.exporter.jobs.labels(s_).inc(c)
         if self.fast is not None:
-            self.fast.housekeeping()
+            with self.spans.span("housekeeping"):
+                self.fast.housekeeping()
         return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast),
                 "seconds": time.perf_counter() - t0}
 
     def _run_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict, bulk: list) -> int:
         fp = self.fast
         with self.spans.span("stage"):
-            fp.stage_history(fast)
+            fp.stage_history()
         n_rows = 0
-        for key, grp in fp.groups(fast).items():
+        with self.spans.span("group"):
+            groups = fp.groups(fast)
+        for key, grp in groups.items():
             M = len(key[0])
             try:
                 with self.spans.span("score"):

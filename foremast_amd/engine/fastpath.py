@@ -93,6 +93,8 @@ class FastWork:
     dirty: bool = True                         # data changed since the group arrays were built
     wclass: int = 0                            # pairwise width class (groups)
     version: object = None                     # store version of the document this plan is for
+    handle: int | None = None                  # store-side row of the job (bulk updates without id lookups)
+    settled: bool = False                      # static, windows fetched, history resident
     gkey: tuple | None = None                  # group key (plan group + width class)
     cur: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))    # metrics concatenated
     cur_t: np.ndarray = field(default_factory=lambda: np.zeros(0))
@@ -120,6 +122,8 @@ class GroupArrays:
     end: np.ndarray
     missing: np.ndarray                        # [S, M] no history or no current data
     export_slots: np.ndarray | None = None
+    handles: np.ndarray | None = None          # store rows of the jobs (ClaimBatch.handles)
+    works: list | None = None                  # the job list object these arrays were built for
 
 
 def _label(q: str, name: str) -> str:
@@ -198,6 +202,10 @@ class FastPath:
         self.sliding = ResidentHistory(n, brain.device, step, sliding=True)
         self.works: dict[str, FastWork] = {}
         self._garr: dict[tuple, GroupArrays] = {}
+        self.todo: list[FastWork] = []
+        self._last = None                 # (ids, versions, fast, todo) of the previous claim batch
+        self._last_groups = None
+        self._reused = False
         self.scorers: dict[tuple, CanaryScorer] = {}
         self.hpa = HpaTable(brain.device)
         self.cycle = 0
@@ -256,15 +264,28 @@ class FastPath:
         work and the documents for the general model-zoo path.  A job seen
         before at the same version reuses its FastWork: no document decode,
         no planning, no row lookups; only new / resubmitted jobs are
-        materialised and planned."""
+        materialised and planned.  ``self.todo`` lists the jobs that need a
+        fetch this cycle; a batch identical to the previous cycle's (the
+        steady state of a re-examined fleet) reuses the previous lists."""
         self.cycle += 1
         self.sliding.advance(now, now - self.history_s)
+        immutable = self._immutable
+        last = self._last
+        if last is not None and batch.ids == last[0] and batch.versions == last[1]:
+            fast = last[2]
+            self.todo = [fw for fw in last[3] if not (immutable and fw.settled)] if immutable else fast
+            self._reused = True
+            return fast, []
+        self._reused = False
         works = self.works
-        fast, unknown = [], []
+        fast, unknown, todo = [], [], []
+        handles = getattr(batch, "handles", None)
         for k, (jid, ver) in enumerate(zip(batch.ids, batch.versions)):
             fw = works.get(jid)
             if fw is not None and fw.version == ver:
                 fast.append(fw)
+                if not (immutable and fw.settled):
+                    todo.append(fw)
             else:
                 unknown.append(k)
         rest = []
@@ -283,17 +304,19 @@ class FastPath:
                     end_ts = parse_rfc3339(d.end_time).timestamp() if d.end_time else now
                 except ValueError:
                     end_ts = now
-                fw = works[d.id] = FastWork(d, p, rows, end_ts, version=batch.versions[k])
+                fw = works[d.id] = FastWork(d, p, rows, end_ts, version=batch.versions[k],
+                                            handle=None if handles is None else int(handles[k]))
                 fast.append(fw)
+                todo.append(fw)
+        self.todo = todo
+        self._last = (batch.ids, batch.versions, fast, todo) if not rest else None
         return fast, rest
 
     def fetch_all(self, works: list[FastWork], now: float, pool=None) -> list[FastWork]:
-        """Fetch what each job needs this cycle.  From an immutable source a
-        static job whose windows and history are resident needs nothing."""
-        if self._immutable:
-            todo = [fw for fw in works if not (fw.has_window and fw.hist_complete and not fw.plan.sliding)]
-        else:
-            todo = works
+        """Fetch what the jobs in ``self.todo`` need this cycle (from an
+        immutable source a static job whose windows and history are resident
+        needs nothing and is not in it)."""
+        todo = self.todo
         if pool is None:
             for fw in todo:
                 self.fetch(fw, now)
@@ -363,6 +386,7 @@ class FastPath:
         fw.wclass = 0 if max(c, bb) <= 128 else (1 if max(c, bb) <= 256 else 2)
         fw.has_window = True
         fw.dirty = True
+        fw.settled = fw.hist_complete and not p.sliding
         return fw
 
     @property
@@ -370,10 +394,12 @@ class FastPath:
         return bool(getattr(self.b.sources, "immutable", False))
 
     # ------------------------------------------------------------------ stage + score
-    def stage_history(self, works: list[FastWork]) -> None:
+    def stage_history(self, works: list[FastWork] | None = None) -> None:
+        """Scatter the history fetched this cycle (jobs in ``self.todo``)
+        into the resident stores."""
         srows, svals, stl = [], [], []
         drows, dts, dvs = [], [], []
-        got = [fw for fw in works if fw.hist]
+        got = [fw for fw in (self.todo if works is None else works) if fw.hist]
         for fw in got:
             for i, t, v in fw.hist:
                 if fw.plan.sliding:
@@ -392,6 +418,7 @@ class FastPath:
             fw.dirty = True
             if not fw.plan.sliding:
                 fw.hist_complete = bool(np.isfinite(self.static.last_t[fw.rows]).all())
+                fw.settled = fw.hist_complete and fw.has_window
             fw.hist = []
 
     def groups(self, works: list[FastWork]) -> dict[tuple, list[FastWork]]:
@@ -399,12 +426,15 @@ class FastPath:
         padded window stays on the role-split kernel (<= 128 points per side:
         <= 256 together) or the separate pairwise kernel (<= 256 per side)
         and one wide canary never widens the whole fleet's batch."""
+        if self._reused and not self.todo and self._last_groups is not None:
+            return self._last_groups
         g: dict[tuple, list[FastWork]] = {}
         for fw in works:
             k = fw.gkey
             if k is None or k[-1] != fw.wclass:
                 k = fw.gkey = fw.plan.group + (fw.wclass,)
             g.setdefault(k, []).append(fw)
+        self._last_groups = g
         return g
 
     def _scorer(self, aliases: tuple) -> CanaryScorer:
@@ -418,9 +448,12 @@ class FastPath:
     def _arrays(self, works: list[FastWork], key: tuple) -> GroupArrays:
         """The group's packed arrays: rebuilt only when its job list or any
         job's data changed since the last cycle."""
-        ident = tuple(map(id, works))
         ga = self._garr.get(key)
+        if ga is not None and ga.works is works and self._reused and not self.todo:
+            return ga                     # same job list object, nothing fetched: nothing changed
+        ident = tuple(map(id, works))
         if ga is not None and ga.ident == ident and not any(fw.dirty for fw in works):
+            ga.works = works
             return ga
         p0 = works[0].plan
         M = len(p0.aliases)
@@ -442,8 +475,11 @@ class FastPath:
         has_cur = np.isfinite(cur).any(1).reshape(S, M)
         ids = np.empty(S, object)
         ids[:] = [w.doc.id for w in works]
+        hd = [w.handle for w in works]
+        handles = None if any(h is None for h in hd) else np.asarray(hd, np.int64)
         ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
-                         up(rowmap), np.fromiter((w.end_ts for w in works), np.float64, S), ~(has_hist & has_cur))
+                         up(rowmap), np.fromiter((w.end_ts for w in works), np.float64, S), ~(has_hist & has_cur),
+                         handles=handles, works=works)
         exp = self.b.exporter
         if exp is not None:
             slots = []
@@ -542,11 +578,17 @@ class FastPath:
             flush = True
         else:
             flush = False
+        hd = ga.handles
         if alive.any():
-            bulk.append((ga.ids[alive].tolist(), {"status": ST.PREPROCESS_COMPLETED}))
-            outcome[ST.PREPROCESS_COMPLETED] = outcome.get(ST.PREPROCESS_COMPLETED, 0) + int(alive.sum())
+            n_alive = int(alive.sum())
+            if n_alive == S:
+                bulk.append((ga.ids, {"status": ST.PREPROCESS_COMPLETED}, hd))
+            else:
+                bulk.append((ga.ids[alive], {"status": ST.PREPROCESS_COMPLETED}, None if hd is None else hd[alive]))
+            outcome[ST.PREPROCESS_COMPLETED] = outcome.get(ST.PREPROCESS_COMPLETED, 0) + n_alive
         if healthy.any():
-            bulk.append((ga.ids[healthy].tolist(), {"status": ST.COMPLETED_HEALTH, "reason": ""}))
+            bulk.append((ga.ids[healthy], {"status": ST.COMPLETED_HEALTH, "reason": ""},
+                         None if hd is None else hd[healthy]))
             outcome[ST.COMPLETED_HEALTH] = outcome.get(ST.COMPLETED_HEALTH, 0) + int(healthy.sum())
         for j in np.flatnonzero(unknown):
             w = works[j]
@@ -562,7 +604,7 @@ class FastPath:
                 updates.append((works[j].doc.id, fields))
             outcome[ST.COMPLETED_UNHEALTH] = outcome.get(ST.COMPLETED_UNHEALTH, 0) + int(unh.sum())
         if flush:
-            updates.extend((i, f) for ids, f in bulk for i in ids)
+            updates.extend((i, f) for ids, f, _ in bulk for i in ids)
         closed = ~alive
         if closed.any():
             self._release([works[j] for j in np.flatnonzero(closed)])

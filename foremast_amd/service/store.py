@@ -63,10 +63,11 @@ class ClaimBatch:
     opaque version per job; documents are materialised only for the
     positions the caller asks for (jobs it has not planned yet)."""
 
-    def __init__(self, ids: list[str], versions: list, resolve):
+    def __init__(self, ids: list[str], versions: list, resolve, handles=None):
         self.ids = ids
         self.versions = versions
         self._resolve = resolve
+        self.handles = handles        # store-side rows (MemoryStore), else None
 
     def __len__(self) -> int:
         return len(self.ids)
@@ -117,9 +118,10 @@ class JobStore(ABC):
         for jid, fields in updates:
             self.update(jid, **fields)
 
-    def update_uniform(self, ids: list[str], fields: dict, now: float | None = None) -> None:
+    def update_uniform(self, ids, fields: dict, now: float | None = None, handles=None) -> None:
         """The same ``fields`` for many jobs (the brain's per-cycle "still in
-        progress" / "healthy" verdicts): one batch."""
+        progress" / "healthy" verdicts): one batch.  ``handles`` are the
+        store rows a :class:`ClaimBatch` of this store handed out (optional)."""
         self.update_many([(i, fields) for i in ids], now=now)
 
     def add_hpalogs(self, logs: list[HPALog]) -> None:
@@ -306,17 +308,21 @@ class MemoryStore(JobStore):
             self._st[idx[ok]] = codes[ok]
             self._mod[idx[ok]] = _ts_str(stamp)
 
-    def update_uniform(self, ids: list[str], fields: dict, now: float | None = None) -> None:
+    def update_uniform(self, ids, fields: dict, now: float | None = None, handles=None) -> None:
         """Vectorised: status codes and lease times are array stores; the
         document objects pick the fields up lazily when next read."""
-        if not ids:
+        if len(ids) == 0:
             return
         now = time.time() if now is None else now
         stamp = _stamp(now)
         with self._lock:
-            get = self._index.get
-            idx = np.fromiter((get(j, -1) for j in ids), np.int64, len(ids))
-            idx = idx[idx >= 0]
+            if handles is not None and len(handles) == len(ids) and \
+                    self._ids[handles[0]] == ids[0] and self._ids[handles[-1]] == ids[-1]:
+                idx = np.asarray(handles, np.int64)
+            else:
+                get = self._index.get
+                idx = np.fromiter((get(j, -1) for j in ids), np.int64, len(ids))
+                idx = idx[idx >= 0]
             self._pend_merge(idx, fields, stamp)
             if "status" in fields:
                 self._st[idx] = self._code(fields["status"])
@@ -390,7 +396,7 @@ class MemoryStore(JobStore):
         def resolve(pos):
             with self._lock:
                 return [self._obj(int(idx[p])) for p in pos]
-        return ClaimBatch(ids, vers, resolve)
+        return ClaimBatch(ids, vers, resolve, handles=idx)
 
     def add_hpalog(self, log: HPALog) -> None:
         with self._lock:
