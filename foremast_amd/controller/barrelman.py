@@ -265,8 +265,8 @@ class Barrelman:
                 self.kube.create(K.MONITORS, ns, m.to_dict())
             else:
                 d = m.to_dict()
-                d["metadata"].pop("resourceVersion", None)
-                self.kube.update(K.MONITORS, ns, d)
+                self.kube.update_retry(K.MONITORS, ns, name,
+                                       lambda o: dict(o, spec=d["spec"], status=d.get("status", {})))
         except Exception as e:
             log.info("upsert DeploymentMonitor %s/%s failed: %s", ns, name, e)
 
@@ -332,8 +332,12 @@ class Barrelman:
                             pass
                     if changed:
                         st.remediation_taken = False
+                        sd = item.to_dict().get("status", {})
                         try:
-                            self.kube.update(K.MONITORS, ns, item.to_dict())
+                            # the poller owns the status: written onto the freshest
+                            # object (a concurrent spec edit, e.g. ``kubectl watch``,
+                            # survives; a 409 re-reads and re-applies)
+                            self.kube.update_retry(K.MONITORS, ns, item.name, lambda o, sd=sd: dict(o, status=sd))
                             updated += 1
                         except Exception as e:
                             log.info("update monitor %s/%s failed: %s", ns, item.name, e)

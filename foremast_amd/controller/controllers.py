@@ -151,7 +151,11 @@ class DeploymentController:
             if create:
                 self.kube.create(K.MONITORS, ns, mon.to_dict())
             else:
-                self.kube.update(K.MONITORS, ns, mon.to_dict())
+                d = mon.to_dict()
+                # spec + status replaced on the freshest object; a 409 from a
+                # concurrent writer (the 10 s poller) re-reads and re-applies
+                self.kube.update_retry(K.MONITORS, ns, name,
+                                       lambda o: dict(o, spec=d["spec"], status=d.get("status", {})))
         except Exception as e:
             log.info("upsert monitor %s/%s failed: %s", ns, name, e)
         if strategy == MQ.STRATEGY_CANARY:
@@ -272,12 +276,25 @@ class MonitorController:
         if healthy_mon and new_phase == crd.PHASE_UNHEALTHY and not new.status.remediation_taken:
             action = self.actions.get(new.spec.remediation.option)
             if action is not None:
-                new.status.remediation_taken = True
+                took = {"ok": False}
+
+                def mark(o):
+                    st = o.setdefault("status", {})
+                    if st.get("remediationTaken") or st.get("phase") != crd.PHASE_UNHEALTHY:
+                        return None          # already taken by a concurrent handler / no longer unhealthy
+                    st["remediationTaken"] = True
+                    took["ok"] = True
+                    return o
                 try:
-                    self.kube.update(K.MONITORS, new.namespace, new.to_dict())
+                    self.kube.update_retry(K.MONITORS, new.namespace, new.name, mark)
                 except Exception as e:
+                    # the write failed for good: act anyway (MonitorController.go:122-141
+                    # ignores the update error), the revision guard stops a loop
                     log.info("mark remediationTaken failed: %s", e)
-                self.b.go(action, new)
+                    took["ok"] = True
+                if took["ok"]:
+                    new.status.remediation_taken = True
+                    self.b.go(action, new)
                 return
         if healthy_mon and new.spec.continuous and new_phase != crd.PHASE_RUNNING:
             if new_phase == crd.PHASE_UNHEALTHY:
@@ -308,9 +325,13 @@ class MonitorController:
             log.info("rolled back already to %d", rev)
             return False
         msg = f"Foremast detected unhealthy, so roll it back automatically to revision:{rev}"
-        depl.setdefault("status", {}).setdefault("conditions", []).append(self._condition("RollbackProgressing", msg))
+        cond = self._condition("RollbackProgressing", msg)
+
+        def add_cond(o):
+            o.setdefault("status", {}).setdefault("conditions", []).append(cond)
+            return o
         try:
-            depl = self.kube.update(K.DEPLOYMENTS, m.namespace, depl)
+            depl = self.kube.update_retry(K.DEPLOYMENTS, m.namespace, name, add_cond)
         except Exception as e:
             log.info("updating deployment conditions failed: %s", e)
         if depl.get("spec", {}).get("paused"):
@@ -321,11 +342,13 @@ class MonitorController:
         return True
 
     def pause(self, m: crd.DeploymentMonitor) -> bool:
-        depl = self.kube.get(K.DEPLOYMENTS, m.namespace, self._depl_name(m))
-        depl.setdefault("spec", {})["paused"] = True
-        depl.setdefault("status", {}).setdefault("conditions", []).append(
-            self._condition("ForemastPaused", "Foremast detected unhealthy, so paused this deployment"))
-        self.kube.update(K.DEPLOYMENTS, m.namespace, depl)
+        cond = self._condition("ForemastPaused", "Foremast detected unhealthy, so paused this deployment")
+
+        def mut(depl):
+            depl.setdefault("spec", {})["paused"] = True
+            depl.setdefault("status", {}).setdefault("conditions", []).append(cond)
+            return depl
+        self.kube.update_retry(K.DEPLOYMENTS, m.namespace, self._depl_name(m), mut)
         return True
 
     def auto(self, m: crd.DeploymentMonitor) -> bool:
@@ -428,7 +451,11 @@ class HpaController:
         m = self.get_deployment_monitor(hpa)
         if m is not None:
             m.spec.hpa_score_template = ""
+
+            def clear(o):
+                o.setdefault("spec", {}).pop("hpaScoreTemplate", None)
+                return o
             try:
-                self.kube.update(K.MONITORS, m.namespace, m.to_dict())
+                self.kube.update_retry(K.MONITORS, m.namespace, m.name, clear)
             except Exception as e:
                 log.info("clearing hpa template failed: %s", e)

@@ -167,9 +167,33 @@ class KubeAPI(ABC):
     def watch(self, resource: str, handler: Handler, resync: float = 0.0) -> None: ...
 
     def patch_merge(self, resource: str, namespace: str, name: str, patch: dict) -> dict:
-        obj = self.get(resource, namespace, name)
-        _merge(obj, patch)
-        return self.update(resource, namespace, obj)
+        """RFC 7386 merge patch (``kubectl patch --type merge``).  Generic
+        form: read-modify-write retried on conflicts; HttpKube sends a real
+        PATCH, which the API server applies atomically."""
+        def mut(obj):
+            _merge(obj, patch)
+            return obj
+        return self.update_retry(resource, namespace, name, mut)
+
+    def update_retry(self, resource: str, namespace: str, name: str, mutate: Callable[[dict], dict | None],
+                     attempts: int = 5, backoff: float = 0.05) -> dict:
+        """Optimistic-concurrency write (client-go ``retry.RetryOnConflict``):
+        GET the object, apply ``mutate`` (returns the object to write, or None
+        when no write is needed any more), PUT with the fresh
+        resourceVersion; on 409 re-GET and re-apply."""
+        for k in range(attempts):
+            obj = self.get(resource, namespace, name)
+            new = mutate(copy.deepcopy(obj))
+            if new is None:
+                return obj
+            new.setdefault("metadata", {})["resourceVersion"] = obj.get("metadata", {}).get("resourceVersion")
+            try:
+                return self.update(resource, namespace, new)
+            except Conflict:
+                if k == attempts - 1:
+                    raise
+                time.sleep(backoff * (2 ** k))
+        raise AssertionError("unreachable")
 
     def rollback(self, namespace: str, name: str, to_revision: int, annotations: dict | None = None) -> dict:
         """Roll a Deployment back to ``to_revision``: what the extensions/v1beta1
@@ -376,48 +400,80 @@ class HttpKube(KubeAPI):
     def update(self, resource, namespace, obj):
         return self._check(self.http.put(self._path(resource, namespace, obj["metadata"]["name"]), json=obj))
 
+    def patch_merge(self, resource, namespace, name, patch):
+        return self._check(self.http.patch(self._path(resource, namespace, name), content=json.dumps(patch),
+                                           headers={"Content-Type": "application/merge-patch+json"}))
+
     def delete(self, resource, namespace, name):
         self._check(self.http.delete(self._path(resource, namespace, name)))
 
     def watch(self, resource, handler, resync=30.0):
-        """Informer: list, then stream ``?watch=1``; relist every ``resync`` s."""
+        """Informer: list, then stream ``?watch=1`` from the list's
+        resourceVersion, resuming from the last seen version when a stream
+        times out.  An ``ERROR`` event (410 Gone: the version is too old) or a
+        failed stream forces a fresh list, whose diff against the known
+        objects is delivered as ADDED / MODIFIED / DELETED."""
+        def relist(known):
+            lst = self._check(self.http.get(self._path(resource, "")))
+            seen = set()
+            for o in lst.get("items", []):
+                k = o["metadata"].get("namespace", "") + "/" + o["metadata"]["name"]
+                seen.add(k)
+                old = known.get(k)
+                handler("MODIFIED" if old else "ADDED", old, o)
+                known[k] = o
+            for k in set(known) - seen:
+                handler("DELETED", known[k], known.pop(k))
+            return lst.get("metadata", {}).get("resourceVersion", "")
+
         def loop():
             known: dict[str, dict] = {}
+            rv = None
             while not self._stop.is_set():
                 try:
-                    lst = self._check(self.http.get(self._path(resource, "")))
-                    rv = lst.get("metadata", {}).get("resourceVersion", "")
-                    seen = set()
-                    for o in lst.get("items", []):
-                        k = o["metadata"].get("namespace", "") + "/" + o["metadata"]["name"]
-                        seen.add(k)
-                        old = known.get(k)
-                        handler("MODIFIED" if old else "ADDED", old, o)
-                        known[k] = o
-                    for k in set(known) - seen:
-                        handler("DELETED", known[k], known.pop(k))
-                    with self.http.stream("GET", self._path(resource, ""),
-                                          params={"watch": "1", "resourceVersion": rv,
-                                                  "timeoutSeconds": str(int(resync))}, timeout=resync + 10) as s:
-                        for line in s.iter_lines():
-                            if not line:
-                                continue
-                            ev = json.loads(line)
-                            o = ev.get("object", {})
-                            k = o.get("metadata", {}).get("namespace", "") + "/" + o.get("metadata", {}).get("name", "")
-                            old = known.get(k)
-                            if ev.get("type") == "DELETED":
-                                known.pop(k, None)
-                                handler("DELETED", old, o)
-                            elif ev.get("type") in ("ADDED", "MODIFIED"):
-                                known[k] = o
-                                handler(ev["type"] if old is None else "MODIFIED", old, o)
+                    if rv is None:
+                        rv = relist(known)
+                    rv = self._watch_once(resource, rv, resync, known, handler)
                 except Exception:
-                    log.warning("watch %s failed; retrying", resource, exc_info=True)
+                    log.warning("watch %s failed; relisting", resource, exc_info=True)
+                    rv = None
                     self._stop.wait(3.0)
         t = threading.Thread(target=loop, name=f"watch-{resource}", daemon=True)
         t.start()
         self._threads.append(t)
+
+    def _watch_once(self, resource, rv, resync, known, handler):
+        """One watch stream; returns the resourceVersion to resume from, or
+        None when the caller must relist."""
+        with self.http.stream("GET", self._path(resource, ""),
+                              params={"watch": "1", "resourceVersion": rv, "allowWatchBookmarks": "true",
+                                      "timeoutSeconds": str(int(resync))}, timeout=resync + 10) as s:
+            if s.status_code == 410:
+                return None
+            if s.status_code >= 400:
+                raise RuntimeError(f"watch {resource}: HTTP {s.status_code}")
+            for line in s.iter_lines():
+                if not line:
+                    continue
+                ev = json.loads(line)
+                et = ev.get("type")
+                o = ev.get("object", {}) or {}
+                if et == "ERROR":
+                    log.info("watch %s: %s; relisting", resource, o.get("message", o.get("reason", "")))
+                    return None
+                md = o.get("metadata", {})
+                rv = md.get("resourceVersion", rv)
+                if et == "BOOKMARK":
+                    continue
+                k = md.get("namespace", "") + "/" + md.get("name", "")
+                old = known.get(k)
+                if et == "DELETED":
+                    known.pop(k, None)
+                    handler("DELETED", old, o)
+                elif et in ("ADDED", "MODIFIED"):
+                    known[k] = o
+                    handler(et if old is None else "MODIFIED", old, o)
+        return rv
 
     def stop(self):
         self._stop.set()

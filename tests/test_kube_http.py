@@ -15,6 +15,7 @@ class FakeAPIServer:
     def __init__(self):
         self.kube = K.FakeKube()
         self.watch_events: dict[str, list] = {}
+        self.watch_gone: dict[str, bool] = {}
         self.requests = []
 
     def _route(self, path):
@@ -38,6 +39,8 @@ class FakeAPIServer:
             return httpx.Response(404, json={"kind": "Status", "code": 404})
         try:
             if req.method == "GET" and req.url.params.get("watch") == "1":
+                if self.watch_gone.pop(res, False):
+                    return httpx.Response(410, json={"kind": "Status", "code": 410, "reason": "Expired"})
                 evs = self.watch_events.pop(res, [])
                 body = "".join(json.dumps(e) + "\n" for e in evs)
                 return httpx.Response(200, content=body.encode())
@@ -50,6 +53,9 @@ class FakeAPIServer:
                 return httpx.Response(201, json=self.kube.create(res, ns, json.loads(req.content)))
             if req.method == "PUT":
                 return httpx.Response(200, json=self.kube.update(res, ns, json.loads(req.content)))
+            if req.method == "PATCH":
+                assert req.headers["content-type"] == "application/merge-patch+json"
+                return httpx.Response(200, json=self.kube.patch_merge(res, ns, name, json.loads(req.content)))
             if req.method == "DELETE":
                 self.kube.delete(res, ns, name)
                 return httpx.Response(200, json={"kind": "Status", "status": "Success"})
@@ -130,3 +136,70 @@ def test_informer_list_then_watch(api):
     assert seen[:4] == [("ADDED", "h1", False), ("ADDED", "h2", False), ("MODIFIED", "h1", True),
                         ("DELETED", "h2", True)]
     time.sleep(0.05)
+
+
+def test_merge_patch_is_a_real_patch(api):
+    srv, hk = api
+    hk.create(K.MONITORS, "default", {"metadata": {"name": "demo", "namespace": "default"},
+                                      "spec": {"continuous": False, "remediation": {"option": "AutoRollback"}}})
+    hk.patch_merge(K.MONITORS, "default", "demo", {"spec": {"continuous": True}})
+    got = hk.get(K.MONITORS, "default", "demo")
+    assert got["spec"] == {"continuous": True, "remediation": {"option": "AutoRollback"}}
+    assert [m for m, p, _ in srv.requests if p.endswith("/deploymentmonitors/demo")].count("PATCH") == 1
+
+
+def test_watch_error_event_relists_and_bookmark_resumes(api):
+    """A 410 / ERROR event forces a fresh list (its diff is delivered), a
+    BOOKMARK only advances the resume version (client-go informer semantics)."""
+    srv, hk = api
+    srv.kube.create(K.HPAS, "default", {"metadata": {"name": "h1", "namespace": "default"}})
+    srv.watch_events[K.HPAS] = [
+        {"type": "BOOKMARK", "object": {"metadata": {"resourceVersion": "42"}}},
+        {"type": "ERROR", "object": {"kind": "Status", "code": 410, "message": "too old resource version"}},
+    ]
+    seen = []
+    done = threading.Event()
+
+    def handler(etype, old, new):
+        seen.append((etype, new["metadata"]["name"]))
+        if ("DELETED", "h1") in seen:
+            done.set()
+    hk.watch(K.HPAS, handler, resync=0.5)
+    deadline = time.time() + 10
+    while not any(p.get("resourceVersion") == "42" for m, _, p in srv.requests if p.get("watch") == "1") \
+            and time.time() < deadline:
+        time.sleep(0.02)
+    # while the informer relists, h1 disappears and h3 appears: delivered as a diff
+    srv.kube.delete(K.HPAS, "default", "h1")
+    srv.kube.create(K.HPAS, "default", {"metadata": {"name": "h3", "namespace": "default"}})
+    srv.watch_gone[K.HPAS] = True
+    assert done.wait(10), seen
+    hk.stop()
+    assert seen[0] == ("ADDED", "h1") and ("ADDED", "h3") in seen and ("DELETED", "h1") in seen
+    lists = [p for m, path, p in srv.requests if m == "GET" and path.endswith("/horizontalpodautoscalers")
+             and p.get("watch") != "1"]
+    assert len(lists) >= 2
+
+
+def test_update_retry_rereads_on_conflict():
+    class Racy(K.FakeKube):
+        def __init__(self, n):
+            super().__init__()
+            self.n = n
+
+        def update(self, resource, namespace, obj):
+            if self.n > 0 and resource == K.MONITORS:
+                self.n -= 1
+                # a concurrent writer bumps the object between our GET and PUT
+                cur = K.FakeKube.get(self, resource, namespace, obj["metadata"]["name"])
+                cur.setdefault("status", {})["phase"] = "Running"
+                K.FakeKube.update(self, resource, namespace, cur)
+            return K.FakeKube.update(self, resource, namespace, obj)
+    kube = Racy(2)
+    kube.create(K.MONITORS, "default", {"metadata": {"name": "demo", "namespace": "default"}, "spec": {}})
+    out = kube.update_retry(K.MONITORS, "default", "demo", lambda o: dict(o, spec={"continuous": True}))
+    assert out["spec"] == {"continuous": True} and out["status"]["phase"] == "Running"
+    kube2 = Racy(10)
+    kube2.create(K.MONITORS, "default", {"metadata": {"name": "demo", "namespace": "default"}, "spec": {}})
+    with pytest.raises(K.Conflict):
+        kube2.update_retry(K.MONITORS, "default", "demo", lambda o: o, attempts=3, backoff=0.0)
