@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# Local cluster for the Foremast bundle (reference: deploy/minikube.sh).
+# The custom-metrics adapter (40-custom-metrics.yaml) needs webhook token
+# authentication on the kubelet; the brain itself needs MI355X nodes
+# (amd.com/gpu), so on a laptop run it with --nproc-per-node=1 on the CPU
+# (gloo) or point FOREMAST_STORE at a brain running elsewhere.
+set -euo pipefail
+minikube start \
+  --kubernetes-version="${K8S_VERSION:-v1.30.0}" \
+  --cpus="${CPUS:-4}" \
+  --memory="${MEMORY:-8192}" \
+  --extra-config=kubelet.authentication-token-webhook=true \
+  --extra-config=kubelet.authorization-mode=Webhook
+python -m foremast_amd.cli manifests deploy/foremast
+kubectl apply -f deploy/foremast/00-namespace.yaml -f deploy/foremast/10-crds.yaml
+kubectl apply -f deploy/foremast/

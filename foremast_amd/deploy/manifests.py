@@ -17,8 +17,18 @@ defaults (the reference ships hand-written YAML: deploy/foremast/*, R3/R21-R24/R
 * ``31-brain.yaml`` — one pod on an 8-GPU MI355X node: the REST service
   container and the brain (``torchrun``, one rank per GPU, RCCL over xGMI)
   sharing the SQLite job store; exporter :8000 + ServiceMonitor; env of R24
-* ``40-custom-metrics.yaml`` — prometheus-adapter rules exposing
-  ``namespace_app*`` and ``foremastbrain*`` to the HPA (R23)
+* ``40-custom-metrics.yaml`` — the custom-metrics API adapter (R23): the
+  prometheus-adapter rules exposing ``namespace_app*`` and ``foremastbrain*``
+  (incl. the HPA score) plus everything that serves them to the HPA
+  controller: ServiceAccount, auth-delegator / auth-reader bindings, resource
+  reader role, the adapter Deployment + Service, the
+  ``v1beta1.custom.metrics.k8s.io`` APIService and the HPA controller's read
+  access (reference: deploy/custom-metrics/*.yaml)
+* ``50-elasticsearch.yaml`` — optional ES 6 StatefulSet + Service for
+  ``FOREMAST_STORE=elasticsearch`` (reference: deploy/foremast/3_brain/es.yaml)
+
+``deploy/minikube.sh`` (hand-written) starts a local cluster with the kubelet
+flags the adapter needs (reference: deploy/minikube.sh).
 """
 from __future__ import annotations
 
@@ -304,6 +314,8 @@ def brain_env(cfg: BrainConfig | None = None) -> dict:
                 "MIN_KRUSKAL_DATA_POINTS": cfg.min_kruskal, "MAX_STUCK_IN_SECONDS": int(cfg.max_stuck_seconds),
                 "MIN_HISTORICAL_DATA_POINT_TO_MEASURE": cfg.min_historical_points,
                 "FOREMAST_STORE": "sqlite:/data/jobs.db",
+                # rank-tagged engine checkpoints every 30 cycles and on SIGTERM
+                "BRAIN_CHECKPOINT_DIR": "/data/checkpoints", "BRAIN_CHECKPOINT_EVERY": 30,
                 "HSA_ENABLE_IPC_MODE_LEGACY": 0})
     return env
 
@@ -324,6 +336,8 @@ def brain(gpus: int = 8) -> list[dict]:
     dep = _deployment("foremast-brain", [svc_c, brain_c],
                       volumes=[{"name": "jobs", "persistentVolumeClaim": {"claimName": "foremast-jobs"}}])
     dep["spec"]["strategy"] = {"type": "Recreate"}     # one writer set per PVC
+    # SIGTERM -> the brain finishes its cycle and writes a final checkpoint
+    dep["spec"]["template"]["spec"]["terminationGracePeriodSeconds"] = 60
     metrics = _service("foremast-brain", 8000)
     sm = {"apiVersion": "monitoring.coreos.com/v1", "kind": "ServiceMonitor",
           "metadata": {"name": "foremast-brain", "namespace": NS, "labels": {"k8s-app": "foremast-brain"}},
@@ -332,15 +346,100 @@ def brain(gpus: int = 8) -> list[dict]:
     return [dep, metrics, sm]
 
 
-def custom_metrics() -> dict:
+def custom_metrics_rules() -> dict:
     def rule(series: str, ns_label: str) -> dict:
         return {"seriesQuery": f'{{__name__=~"{series}",{ns_label}!="",app!=""}}', "seriesFilters": [],
                 "resources": {"overrides": {ns_label: {"resource": "namespace"},
                                             "app": {"group": "apps", "resource": "deployment"}}},
                 "metricsQuery": "sum(<<.Series>>{<<.LabelMatchers>>}) by (<<.GroupBy>>)"}
     cfg = {"rules": [rule("^namespace_app.*", "namespace"), rule("^foremastbrain.*", "exported_namespace")]}
-    return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "adapter-config", "namespace": "monitoring"},
+    return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "adapter-config", "namespace": CM_NS},
             "data": {"config.yaml": yaml.safe_dump(cfg, sort_keys=False)}}
+
+
+CM_NS = "monitoring"
+CM_SA = "custom-metrics-apiserver"
+ADAPTER_IMAGE = "registry.k8s.io/prometheus-adapter/prometheus-adapter:v0.12.0"
+RBAC = "rbac.authorization.k8s.io/v1"
+
+
+def _crb(name: str, role: str, sa: str = CM_SA, ns: str = CM_NS, kind: str = "ClusterRoleBinding",
+         role_kind: str = "ClusterRole", meta_ns: str | None = None) -> dict:
+    md = {"name": name}
+    if meta_ns:
+        md["namespace"] = meta_ns
+    return {"apiVersion": RBAC, "kind": kind, "metadata": md,
+            "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": role_kind, "name": role},
+            "subjects": [{"kind": "ServiceAccount", "name": sa, "namespace": ns}]}
+
+
+def custom_metrics(prometheus_url: str = "http://prometheus-k8s.monitoring.svc:9090/") -> list[dict]:
+    """The custom-metrics API adapter: how an HPA reads
+    ``namespace_app_pod_hpa_score`` (HpaController.go:98) from Prometheus."""
+    sa = {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": CM_SA, "namespace": CM_NS}}
+    c = {"name": CM_SA, "image": ADAPTER_IMAGE,
+         "args": ["--secure-port=6443", "--cert-dir=/var/run/serving-cert", "--logtostderr=true",
+                  f"--prometheus-url={prometheus_url}", "--metrics-relist-interval=30s", "--v=2",
+                  "--config=/etc/adapter/config.yaml"],
+         "ports": [{"containerPort": 6443, "name": "https"}],
+         "volumeMounts": [{"name": "config", "mountPath": "/etc/adapter", "readOnly": True},
+                          {"name": "serving-cert", "mountPath": "/var/run/serving-cert"}],
+         "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}
+    dep = {"apiVersion": "apps/v1", "kind": "Deployment",
+           "metadata": {"name": CM_SA, "namespace": CM_NS, "labels": {"app": CM_SA}},
+           "spec": {"replicas": 1, "selector": {"matchLabels": {"app": CM_SA}},
+                    "template": {"metadata": {"labels": {"app": CM_SA}, "name": CM_SA},
+                                 "spec": {"serviceAccountName": CM_SA, "containers": [c],
+                                          "volumes": [{"name": "config", "configMap": {"name": "adapter-config"}},
+                                                      {"name": "serving-cert", "emptyDir": {}}]}}}}
+    svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": CM_SA, "namespace": CM_NS},
+           "spec": {"selector": {"app": CM_SA}, "ports": [{"port": 443, "targetPort": 6443}]}}
+    apisvc = {"apiVersion": "apiregistration.k8s.io/v1", "kind": "APIService",
+              "metadata": {"name": "v1beta1.custom.metrics.k8s.io"},
+              "spec": {"service": {"name": CM_SA, "namespace": CM_NS}, "group": "custom.metrics.k8s.io",
+                       "version": "v1beta1", "insecureSkipTLSVerify": True, "groupPriorityMinimum": 100,
+                       "versionPriority": 100}}
+    server_res = {"apiVersion": RBAC, "kind": "ClusterRole", "metadata": {"name": "custom-metrics-server-resources"},
+                  "rules": [{"apiGroups": ["custom.metrics.k8s.io"], "resources": ["*"], "verbs": ["*"]}]}
+    reader = {"apiVersion": RBAC, "kind": "ClusterRole", "metadata": {"name": "custom-metrics-resource-reader"},
+              "rules": [{"apiGroups": [""], "resources": ["namespaces", "pods", "services"], "verbs": ["get", "list"]},
+                        {"apiGroups": ["apps"], "resources": ["deployments"], "verbs": ["get", "list"]}]}
+    return [
+        custom_metrics_rules(), sa,
+        _crb("custom-metrics:system:auth-delegator", "system:auth-delegator"),
+        _crb("custom-metrics-auth-reader", "extension-apiserver-authentication-reader", kind="RoleBinding",
+             role_kind="Role", meta_ns="kube-system"),
+        reader, _crb("custom-metrics-resource-reader", "custom-metrics-resource-reader"),
+        server_res,
+        _crb("hpa-controller-custom-metrics", "custom-metrics-server-resources", sa="horizontal-pod-autoscaler",
+             ns="kube-system"),
+        dep, svc, apisvc,
+    ]
+
+
+def elasticsearch(replicas: int = 1) -> list[dict]:
+    """ES 6 for ``FOREMAST_STORE=elasticsearch`` (indexes ``documents`` and
+    ``hpalogs``, foremast-service/pkg/search/elasticsearchstore.go:17-21)."""
+    c = {"name": "elasticsearch", "image": "docker.elastic.co/elasticsearch/elasticsearch-oss:6.8.23",
+         "env": _env({"discovery.type": "single-node", "ES_JAVA_OPTS": "-Xms2g -Xmx2g",
+                      "cluster.name": "foremast"}),
+         "ports": [{"containerPort": 9200, "name": "http"}, {"containerPort": 9300, "name": "transport"}],
+         "volumeMounts": [{"name": "data", "mountPath": "/usr/share/elasticsearch/data"}],
+         "readinessProbe": {"httpGet": {"path": "/_cluster/health", "port": 9200}, "initialDelaySeconds": 10},
+         "resources": {"requests": {"cpu": "1", "memory": "4Gi"}}}
+    init = {"name": "sysctl", "image": "busybox:1.36", "command": ["sysctl", "-w", "vm.max_map_count=262144"],
+            "securityContext": {"privileged": True}}
+    sts = {"apiVersion": "apps/v1", "kind": "StatefulSet",
+           "metadata": {"name": "elasticsearch", "namespace": NS, "labels": {"app": "elasticsearch"}},
+           "spec": {"serviceName": "elasticsearch", "replicas": replicas,
+                    "selector": {"matchLabels": {"app": "elasticsearch"}},
+                    "template": {"metadata": {"labels": {"app": "elasticsearch"}},
+                                 "spec": {"initContainers": [init], "containers": [c]}},
+                    "volumeClaimTemplates": [{"metadata": {"name": "data"},
+                                              "spec": {"accessModes": ["ReadWriteOnce"],
+                                                       "resources": {"requests": {"storage": "20Gi"}}}}]}}
+    svc = _service("elasticsearch", 9200)
+    return [svc, sts]
 
 
 def bundle() -> dict[str, list[dict]]:
@@ -353,7 +452,8 @@ def bundle() -> dict[str, list[dict]]:
         "22-recording-rules.yaml": [recording_rules()],
         "30-service.yaml": service(),
         "31-brain.yaml": brain(),
-        "40-custom-metrics.yaml": [custom_metrics()],
+        "40-custom-metrics.yaml": custom_metrics(),
+        "50-elasticsearch.yaml": elasticsearch(),
     }
 
 

