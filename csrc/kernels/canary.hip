@@ -841,21 +841,32 @@ __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, 
     sd = (float)sqrt(sst / n);
     return;
   }
-  // Rows with missing samples (Prometheus gaps; the resident store's NaN
-  // padding in front of a right-aligned window): masked mean / variance over
-  // the register image already loaded -- no second or third pass over HBM.
-  // Only this block-uniform branch pays the per-element finite tests.
+  // Rows with missing samples (Prometheus gaps, a young service's short
+  // history, the sliding store's aligned window start): masked mean /
+  // variance over the register image already loaded -- no second pass over
+  // HBM.  Only this block-uniform branch pays for the masking (per element a
+  // class test, a select and a carry-in count add).
+  if (threadIdx.x == (nq - 1) % 256) {            // the tail quad: lanes past T are padding, not zeros
+    const int j = (nq - 1) / 256, e0 = (nq - 1) * 4;
+#pragma unroll
+    for (int jj = 0; jj < NV; ++jj)
+      if (jj == j) {
+        if (e0 + 1 >= T) q[jj].y = __builtin_nanf("");
+        if (e0 + 2 >= T) q[jj].z = __builtin_nanf("");
+        if (e0 + 3 >= T) q[jj].w = __builtin_nanf("");
+      }
+  }
   f2 ms = {0.f, 0.f};
   int cnt = 0;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const int qi = tid + j * 256;
+    const bool inq = tid + j * 256 < nq;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float x = q[j][c];
-      const bool ok = qi < nq && qi * 4 + c < T && isfinite(x);
-      ms[c & 1] += ok ? x : 0.f;
+      const bool ok = inq && isfinite(x);
       cnt += ok ? 1 : 0;
+      ms[c & 1] += ok ? x : 0.f;
     }
   }
   const double t2 = block_sum<256>((double)ms.x + (double)ms.y, red);
@@ -864,12 +875,11 @@ __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, 
   f2 a2 = {0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const int qi = tid + j * 256;
+    const bool inq = tid + j * 256 < nq;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float x = q[j][c];
-      const bool ok = qi < nq && qi * 4 + c < T && isfinite(x);
-      const float d = ok ? x - mf : 0.f;
+      const float d = (inq && isfinite(x)) ? x - mf : 0.f;
       a2[c & 1] += d * d;
     }
   }

@@ -241,6 +241,28 @@ FM_API void fm_prom_count_many(const char* const* bufs, const int64_t* lens, int
   for (auto& th : pool) th.join();
 }
 
+// Left-align variable-length rows into a padded [nrows, ld] matrix: the newest
+// min(len, ncols) samples of every row start at column 0, NaN after.  The
+// resident history store keeps static rows this way so a full row has no
+// missing sample inside the scored view (the row-stats fast path).
+FM_API void fm_pack_left(const float* const* srcs, const int64_t* lens, int64_t nrows, float* dst, int64_t ld,
+                         int64_t ncols, int threads) {
+  std::atomic<int64_t> next{0};
+  auto work = [&]() {
+    for (int64_t r = next++; r < nrows; r = next++) {
+      float* d = dst + r * ld;
+      const int64_t n = lens[r] < ncols ? lens[r] : ncols;
+      if (n > 0) std::memcpy(d, srcs[r] + (lens[r] - n), n * sizeof(float));
+      for (int64_t i = n; i < ld; ++i) d[i] = NAN;
+    }
+  };
+  int nt = threads > 0 ? threads : 1;
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+}
+
 // Right-align variable-length rows into a padded [nrows, ld] matrix: the last
 // sample of every source row lands in column ncols-1 (the "now" edge), missing
 // leading samples are NaN.  Rows longer than ncols keep their newest ncols.

@@ -77,6 +77,16 @@ class BrainConfig:
     # load forecast published for HPA jobs (cluster-autoscaler prediction)
     hpa_forecast_algorithm: str = "double_exponential_smoothing"   # HPA_FORECAST_ALGORITHM ("" disables)
     hpa_forecast_steps: int = 15                                    # HPA_FORECAST_STEPS (60 s samples)
+    # downstream impact (README.md:24,27; the judgement diagram's "app or app
+    # downstream" branch): caller -> callee edges from the ``caller``-tagged
+    # request series (recording rule namespace_app_caller[_uri]_http_server_requests_rate)
+    downstream_edges_url: str = ""         # DOWNSTREAM_EDGES_URL (Prometheus /api/v1/query URL); "" disables
+    downstream_edges_store: str = "prometheus"   # DOWNSTREAM_EDGES_STORE
+    downstream_mode: str = "judge"         # DOWNSTREAM_IMPACT_MODE: judge | annotate | off
+    downstream_threshold: float = 0.2      # DOWNSTREAM_IMPACT_THRESHOLD: traffic share reaching an anomalous callee
+    downstream_hops: int = 2               # DOWNSTREAM_IMPACT_HOPS
+    downstream_refresh_cycles: int = 30    # DOWNSTREAM_REFRESH_CYCLES: re-read the call graph every N cycles
+    downstream_ttl_s: float = 600.0        # DOWNSTREAM_SCORE_TTL_SECONDS: a callee verdict counts this long
 
     def rule_for(self, alias: str) -> MetricRule:
         """Per-metric override: exact alias match first, then substring match
@@ -130,6 +140,13 @@ class BrainConfig:
         c.hpa_breath_down = _f(env, "HPA_BREATH_DOWN_SECONDS", c.hpa_breath_down)
         c.hpa_forecast_algorithm = env.get("HPA_FORECAST_ALGORITHM", c.hpa_forecast_algorithm)
         c.hpa_forecast_steps = _i(env, "HPA_FORECAST_STEPS", c.hpa_forecast_steps)
+        c.downstream_edges_url = env.get("DOWNSTREAM_EDGES_URL", c.downstream_edges_url)
+        c.downstream_edges_store = env.get("DOWNSTREAM_EDGES_STORE", c.downstream_edges_store) or "prometheus"
+        c.downstream_mode = env.get("DOWNSTREAM_IMPACT_MODE", c.downstream_mode) or c.downstream_mode
+        c.downstream_threshold = _f(env, "DOWNSTREAM_IMPACT_THRESHOLD", c.downstream_threshold)
+        c.downstream_hops = _i(env, "DOWNSTREAM_IMPACT_HOPS", c.downstream_hops)
+        c.downstream_refresh_cycles = _i(env, "DOWNSTREAM_REFRESH_CYCLES", c.downstream_refresh_cycles)
+        c.downstream_ttl_s = _f(env, "DOWNSTREAM_SCORE_TTL_SECONDS", c.downstream_ttl_s)
         return c
 
 

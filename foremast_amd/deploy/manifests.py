@@ -204,6 +204,10 @@ def recording_rules() -> dict:
     # caller -> app edge rates for the downstream-impact graph (engine/impact.py)
     http.append(("namespace_app_caller_http_server_requests_rate",
                  'sum by (namespace, app, caller) (rate(http_server_requests_seconds_count{caller!=""}[5m]))'))
+    # per-API (uri) split of the same edges: the downstream reason names the
+    # callee APIs a caller depends on
+    http.append(("namespace_app_caller_uri_http_server_requests_rate",
+                 'sum by (namespace, app, caller, uri) (rate(http_server_requests_seconds_count{caller!=""}[5m]))'))
     jvm = [
         ("namespace_app_pod_jvm_memory_heap_utilization",
          _by_app('sum by (namespace, app) (jvm_memory_used_bytes{area="heap"}) * 100 / '
@@ -316,6 +320,11 @@ def brain_env(cfg: BrainConfig | None = None) -> dict:
                 "FOREMAST_STORE": "sqlite:/data/jobs.db",
                 # rank-tagged engine checkpoints every 30 cycles and on SIGTERM
                 "BRAIN_CHECKPOINT_DIR": "/data/checkpoints", "BRAIN_CHECKPOINT_EVERY": 30,
+                # downstream impact over the caller graph (per-API edges)
+                "DOWNSTREAM_EDGES_URL": "http://prometheus-k8s.monitoring.svc.cluster.local:9090/api/v1/query?"
+                                        "query=namespace_app_caller_uri_http_server_requests_rate",
+                "DOWNSTREAM_IMPACT_MODE": cfg.downstream_mode,
+                "DOWNSTREAM_IMPACT_THRESHOLD": cfg.downstream_threshold,
                 "HSA_ENABLE_IPC_MODE_LEGACY": 0})
     return env
 

@@ -139,6 +139,9 @@ class Brain:
         # through the general model-zoo path
         self.fast = FastPath(self, history_days) if resident_history else None
         self.hpa = self.fast.hpa if self.fast is not None else HpaTable(self.device)
+        from .impact import DownstreamImpact
+        self.impact = DownstreamImpact(self.cfg, self.sources, self.device, clock, self.info)
+        self._impact_done = True
         self.cycles = 0
 
     def _executor(self) -> ThreadPoolExecutor:
@@ -310,12 +313,34 @@ class Brain:
         diverge); there is no other per-cycle collective."""
         t0 = time.perf_counter()
         self.cycles += 1
+        imp = self.impact
+        if imp.enabled:
+            # collectives in a fixed order on every rank: graph refresh
+            # (broadcast) every N cycles, the verdict all-reduce once per cycle
+            # (mid-cycle when the cycle scores jobs, else here in ``finally``)
+            self._impact_done = False
+            if (self.cycles - 1) % max(1, self.cfg.downstream_refresh_cycles) == 0:
+                with self.spans.span("impact_graph"):
+                    imp.refresh()
         try:
             return self._cycle(t0)
         finally:
+            if imp.enabled and not self._impact_done:
+                self._impact_step(self.clock())
             if self.exporter is not None and D.is_dist():
                 with self.spans.span("export_sync"):
                     self.exporter.sync()
+
+    def _impact_step(self, now: float) -> None:
+        """Global verdict vector + K9 impact (collective, once per cycle)."""
+        if not self.impact.enabled or self._impact_done:
+            return
+        self._impact_done = True
+        with self.spans.span("impact"):
+            self.impact.step(now)
+            if self.exporter is not None and self.info.rank == 0:
+                for c, v in self.impact.cluster_health().items():
+                    self.exporter.cluster_impact.labels(c or "local").set(v)
 
     def _cycle(self, t0: float) -> dict:
         now = self.clock()
@@ -343,10 +368,16 @@ class Brain:
         hpalogs: list = []
         outcome: dict = {}
         n_rows = 0
-        if fast:
-            n_rows += self._run_fast(fast, now, updates, hpalogs, outcome, bulk)
-        if works:
-            n_rows += self._run_general(works, now, updates, hpalogs, outcome)
+        # score everything first, then the downstream-impact step (its
+        # collective), then the verdicts: a caller judged this cycle sees its
+        # callees' verdicts of this cycle, on any rank
+        scored = self._score_fast(fast, now, updates, hpalogs, outcome) if fast else []
+        batches = self._score_general(works, updates, outcome) if works else []
+        self._impact_step(now)
+        if scored:
+            n_rows += self._finish_fast(scored, now, updates, hpalogs, outcome, bulk)
+        if batches:
+            n_rows += self._finish_general(batches, now, updates, hpalogs, outcome)
         with self.spans.span("persist"):
             if hpalogs:
                 self.store.add_hpalogs(hpalogs)
@@ -364,35 +395,62 @@ class Brain:
         return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast),
                 "seconds": time.perf_counter() - t0}
 
-    def _run_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict, bulk: list) -> int:
+    def _score_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict) -> list:
+        """Stage, group and score the fast-path jobs; their verdicts are
+        recorded for the downstream-impact step.  A group whose scoring
+        raises is re-scored (and finished) job by job right away."""
         fp = self.fast
         with self.spans.span("stage"):
             fp.stage_history()
-        n_rows = 0
         with self.spans.span("group"):
             groups = fp.groups(fast)
+        scored = []
+        self._n_contained = 0
         for key, grp in groups.items():
             M = len(key[0])
             try:
                 with self.spans.span("score"):
                     g = fp.score_group(grp, now, key)
+                scored.append((key, grp, g))
+                if self.impact.enabled:
+                    fp.observe_impact(g, self.impact, now)
+            except Exception:                       # contain: re-score job by job
+                log.exception("fast-path group of %d jobs failed; re-scoring per job", len(grp))
+                self._n_contained += self._fast_per_job(grp, M, now, updates, hpalogs, outcome)
+        return scored
+
+    def _finish_fast(self, scored: list, now: float, updates: list, hpalogs: list, outcome: dict,
+                     bulk: list) -> int:
+        fp = self.fast
+        n_rows = self._n_contained
+        for key, grp, g in scored:
+            M = len(key[0])
+            try:
                 with self.spans.span("finish"):
                     gb: list = []
-                    fp.finish_group(g, now, updates, hpalogs, outcome, gb)
+                    fp.finish_group(g, now, updates, hpalogs, outcome, gb,
+                                    impact=self.impact if self.impact.enabled else None)
                     bulk.extend(gb)
                     if grp[0].plan.hpa and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
                         self._fast_hpa_forecasts(g)
                 n_rows += len(grp) * M
-            except Exception:                       # contain: re-score job by job
-                log.exception("fast-path group of %d jobs failed; re-scoring per job", len(grp))
-                for fw in grp:
-                    try:
-                        g = fp.score_group([fw], now)
-                        fp.finish_group(g, now, updates, hpalogs, outcome)
-                        n_rows += M
-                    except Exception as e:   # noqa: BLE001 - a failure closes the job, not the cycle
-                        fp.fail_job(fw, f"{type(e).__name__}: {e}", updates, outcome)
+            except Exception:
+                log.exception("fast-path finish of %d jobs failed; re-scoring per job", len(grp))
+                n_rows += self._fast_per_job(grp, M, now, updates, hpalogs, outcome)
         return n_rows
+
+    def _fast_per_job(self, grp, M: int, now: float, updates: list, hpalogs: list, outcome: dict) -> int:
+        n = 0
+        fp = self.fast
+        for fw in grp:
+            try:
+                g = fp.score_group([fw], now)
+                fp.finish_group(g, now, updates, hpalogs, outcome,
+                                impact=self.impact if self.impact.enabled else None)
+                n += M
+            except Exception as e:   # noqa: BLE001 - a failure closes the job, not the cycle
+                fp.fail_job(fw, f"{type(e).__name__}: {e}", updates, outcome)
+        return n
 
     def _fast_hpa_forecasts(self, g: dict) -> None:
         works, M = g["works"], g["M"]
@@ -420,7 +478,10 @@ class Brain:
                 if np.isfinite(v):
                     self.exporter.set_forecast(w.plan.base_metrics[m], w.plan.namespace, w.doc.app_name, float(v))
 
-    def _run_general(self, works: list[Work], now: float, updates: list, hpalogs: list, outcome: dict) -> int:
+    def _score_general(self, works: list[Work], updates: list, outcome: dict) -> list:
+        """Score the general-path jobs: one batch, or job by job when the
+        batch raises (a job that still fails is closed completed_unknown).
+        Returns [(works, rows, result)] batches to finish."""
         rows: list[Row] = []
         for j, wk in enumerate(works):
             for r in wk.rows:
@@ -435,21 +496,38 @@ class Brain:
                 updates.append((works[0].doc.id, {"status": ST.COMPLETED_UNKNOWN,
                                                   "reason": f"scoring failed: {type(e).__name__}: {e}"[:2000]}))
                 outcome[ST.COMPLETED_UNKNOWN] = outcome.get(ST.COMPLETED_UNKNOWN, 0) + 1
-                return 0
+                return []
             log.exception("general-path batch failed; scoring per job")
-            return sum(self._run_general([wk], now, updates, hpalogs, outcome) for wk in works)
-        if res is not None and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
-            with self.spans.span("forecast"):
-                self._hpa_forecasts(works, rows, res)
-        offs = 0
-        with self.spans.span("finish"):
-            for j, wk in enumerate(works):
+            return [b for wk in works for b in self._score_general([wk], updates, outcome)]
+        if res is not None and self.impact.enabled:
+            offs = 0
+            nss, apps, bad = [], [], []
+            for wk in works:
                 k = len(wk.rows)
-                sl = slice(offs, offs + k)
+                if not wk.hpa:
+                    nss.append(wk.namespace or wk.doc.namespace)
+                    apps.append(wk.doc.app_name)
+                    bad.append(bool(res["flags"][offs:offs + k].any()))
                 offs += k
-                st = self._finish(wk, rows[sl], res, sl, now, updates, hpalogs)
-                outcome[st] = outcome.get(st, 0) + 1
-        return len(rows)
+            self.impact.observe(self.impact.ids(nss, apps), np.asarray(bad, bool), self.clock())
+        return [(works, rows, res)]
+
+    def _finish_general(self, batches: list, now: float, updates: list, hpalogs: list, outcome: dict) -> int:
+        n = 0
+        for works, rows, res in batches:
+            if res is not None and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
+                with self.spans.span("forecast"):
+                    self._hpa_forecasts(works, rows, res)
+            offs = 0
+            with self.spans.span("finish"):
+                for j, wk in enumerate(works):
+                    k = len(wk.rows)
+                    sl = slice(offs, offs + k)
+                    offs += k
+                    st = self._finish(wk, rows[sl], res, sl, now, updates, hpalogs)
+                    outcome[st] = outcome.get(st, 0) + 1
+            n += len(rows)
+        return n
 
     def run_forever(self, stop=None, poll: float | None = None, checkpoint_dir: str | None = None,
                     checkpoint_every: int = 30) -> None:
@@ -510,6 +588,10 @@ class Brain:
                                 "upper": float(up[idx[0]]), "lower": float(lo[idx[0]])})
         if wk.hpa:
             return self._finish_hpa(wk, rows, res, sl, now, updates, hpalogs)
+        down = self._downstream(ns, app, bool(anomalies))
+        if down:
+            reasons.append(down)
+            anomalies["downstream"] = {"tags": "", "values": []}
         if anomalies:
             reason = html.escape(json.dumps(reasons))
             updates.append((doc.id, {"status": ST.COMPLETED_UNHEALTH, "reason": reason,
@@ -524,6 +606,18 @@ class Brain:
             return ST.COMPLETED_HEALTH
         updates.append((doc.id, {"status": ST.PREPROCESS_COMPLETED}))
         return ST.PREPROCESS_COMPLETED
+
+    def _downstream(self, namespace: str, app: str, unhealthy: bool) -> dict | None:
+        """The ``downstream`` reason entry of a job whose service sends at
+        least ``DOWNSTREAM_IMPACT_THRESHOLD`` of its traffic (over <= hops
+        hops) to an anomalous service (None if not, or mode forbids)."""
+        imp = self.impact
+        if not imp.enabled or (imp.cfg.downstream_mode == "annotate" and not unhealthy):
+            return None
+        u = imp.node.get(("", namespace, app), -1)
+        if u < 0 or u >= len(imp.impact) or imp.impact[u] < self.cfg.downstream_threshold:
+            return None
+        return {"name": "downstream", "impact": round(float(imp.impact[u]), 4), "callees": imp.explain(u)}
 
     def _hpa_forecasts(self, works: list[Work], rows: list[Row], res) -> None:
         """Batched H-step load forecast for every row of this cycle's HPA jobs,

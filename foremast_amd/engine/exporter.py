@@ -31,7 +31,7 @@ import re
 import threading
 
 import numpy as np
-from prometheus_client import CollectorRegistry, Counter, Histogram, start_http_server
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, start_http_server
 from prometheus_client.core import GaugeMetricFamily
 
 _NAME_OK = re.compile(r"[^a-zA-Z0-9_:]")
@@ -128,6 +128,15 @@ class BrainExporter:
         self.windows = Counter("foremast_brain_windows_scored_total", "metric windows scored",
                                registry=self.registry)
         self._remote: dict[int, np.ndarray] = {}      # rank 0: remote slot -> local slot, per rank
+        # multi-cluster aggregate of the downstream-impact step (engine/impact.py)
+        self.cluster_impact = Gauge("foremastbrain:cluster_impact_max",
+                                    "max over a cluster's services of max(anomaly, downstream impact)", ["cluster"],
+                                    registry=self.registry)
+
+    IMPACT = "foremastbrain:namespace_app_pod_downstream_impact"
+
+    def impact_slots(self, namespaces, apps) -> np.ndarray:
+        return self.table.slots([(self.IMPACT, ns, a) for ns, a in zip(namespaces, apps)])
 
     # ---------------------------------------------------------------- writes
     @staticmethod

@@ -124,6 +124,9 @@ class GroupArrays:
     export_slots: np.ndarray | None = None
     handles: np.ndarray | None = None          # store rows of the jobs (ClaimBatch.handles)
     works: list | None = None                  # the job list object these arrays were built for
+    impact_ids: np.ndarray | None = None       # call-graph node per job (-1: none)
+    impact_version: int = -1
+    impact_slots: np.ndarray | None = None     # exporter slots of the downstream-impact gauge
 
 
 def _label(q: str, name: str) -> str:
@@ -542,8 +545,21 @@ class FastPath:
         return idx, val, ctr
 
     # ------------------------------------------------------------------ finish
+    def _impact_ids(self, ga: GroupArrays, works: list[FastWork], impact) -> np.ndarray:
+        if ga.impact_version != impact.version:
+            ga.impact_ids = impact.ids([w.plan.namespace for w in works], [w.doc.app_name for w in works])
+            ga.impact_version = impact.version
+        return ga.impact_ids
+
+    def observe_impact(self, g: dict, impact, now: float) -> None:
+        """Record this group's service verdicts for the downstream step."""
+        if g["works"][0].plan.hpa:
+            return
+        ids = self._impact_ids(g["ga"], g["works"], impact)
+        impact.observe(ids, g["packed"][:, 0] == 1, now)
+
     def finish_group(self, g: dict, now: float, updates: list, hpalogs: list, outcome: dict,
-                     bulk: list | None = None) -> None:
+                     bulk: list | None = None, impact=None) -> None:
         """Verdicts of a group as array operations.  Jobs that stay alive
         (``preprocess_completed``) and healthy closes go out as uniform bulk
         updates ``(ids, fields)``; only unhealthy / unknown verdicts build
@@ -568,6 +584,22 @@ class FastPath:
             return
         status = packed[:, 0]
         unh = status == 1
+        down = None
+        if impact is not None and len(impact.impact):
+            ids = self._impact_ids(ga, works, impact)
+            val = np.where(ids >= 0, impact.impact[np.maximum(ids, 0)], 0.0)
+            if exp is not None:
+                if ga.impact_slots is None:
+                    ga.impact_slots = exp.impact_slots([w.plan.namespace for w in works],
+                                                       [w.doc.app_name for w in works])
+                exp.table.set(ga.impact_slots, val.astype(np.float64))
+            down = val >= self.b.cfg.downstream_threshold
+            if impact.cfg.downstream_mode == "judge":
+                unh = unh | down
+            else:
+                down &= unh
+            if not down.any():
+                down = None
         done = (now >= ga.end) & ~unh
         miss = ga.missing.any(1)
         alive = ~unh & ~done
@@ -600,7 +632,12 @@ class FastPath:
         if unh.any():
             row_start = np.searchsorted(anom[:, 0], np.arange(S) * M) if len(anom) else None
             for j in np.flatnonzero(unh):
-                st, fields = self._unhealthy(works[j], j, M, anom, row_start, cur, cur_t, stats)
+                extra = None
+                if down is not None and down[j]:
+                    u = int(ga.impact_ids[j])
+                    extra = {"name": "downstream", "impact": round(float(impact.impact[u]), 4),
+                             "callees": impact.explain(u)}
+                st, fields = self._unhealthy(works[j], j, M, anom, row_start, cur, cur_t, stats, extra)
                 updates.append((works[j].doc.id, fields))
             outcome[ST.COMPLETED_UNHEALTH] = outcome.get(ST.COMPLETED_UNHEALTH, 0) + int(unh.sum())
         if flush:
@@ -609,7 +646,7 @@ class FastPath:
         if closed.any():
             self._release([works[j] for j in np.flatnonzero(closed)])
 
-    def _unhealthy(self, w: FastWork, j: int, M: int, anom, row_start, cur, cur_t, stats):
+    def _unhealthy(self, w: FastWork, j: int, M: int, anom, row_start, cur, cur_t, stats, extra=None):
         r0 = j * M
         a0 = row_start[j] if row_start is not None else 0
         a1 = np.searchsorted(anom[:, 0], r0 + M) if len(anom) else 0
@@ -627,6 +664,9 @@ class FastPath:
             anomalies[alias] = {"tags": "", "values": flat}
             reasons.append({"name": alias, "ts": ts, "values": vals, "upper": float(stats[r, 2]),
                             "lower": float(stats[r, 3])})
+        if extra is not None:
+            reasons.append(extra)
+            anomalies["downstream"] = {"tags": "", "values": []}
         return ST.COMPLETED_UNHEALTH, {"status": ST.COMPLETED_UNHEALTH, "reason": html.escape(json.dumps(reasons)),
                                        "anomaly_info": json.dumps(anomalies)}
 

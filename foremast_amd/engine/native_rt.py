@@ -31,6 +31,8 @@ def _load():
     lib.fm_prom_fill.restype = ctypes.c_int
     lib.fm_pack_right.argtypes = [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, ctypes.c_int]
     lib.fm_pack_right.restype = None
+    lib.fm_pack_left.argtypes = [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, ctypes.c_int]
+    lib.fm_pack_left.restype = None
     _lib = lib
     return lib
 
@@ -59,6 +61,25 @@ def parse_prometheus(body: bytes):
         a, b = spans[i]
         labels = json.loads(body[a:b]) if a >= 0 else {}
         out.append(Series(labels, t[off[i]:off[i + 1]], v[off[i]:off[i + 1]]))
+    return out
+
+
+def pack_left(rows: list[np.ndarray], ncols: int, ld: int, threads: int = 4) -> np.ndarray:
+    """Left-align float32 rows into [len(rows), ld] (newest ``ncols`` samples
+    of each row from column 0, NaN after)."""
+    out = np.empty((len(rows), ld), np.float32)
+    rows = [np.ascontiguousarray(r, dtype=np.float32) for r in rows]
+    lib = _load()
+    if lib is None or not rows:
+        out.fill(np.nan)
+        for i, r in enumerate(rows):
+            n = min(len(r), ncols)
+            if n:
+                out[i, :n] = r[len(r) - n:]
+        return out
+    ptrs = (ctypes.c_void_p * len(rows))(*[r.ctypes.data for r in rows])
+    lens = np.array([len(r) for r in rows], np.int64)
+    lib.fm_pack_left(ptrs, lens.ctypes.data, len(rows), out.ctypes.data, ld, ncols, threads)
     return out
 
 

@@ -12,9 +12,13 @@ through a row map (``fm_tick_front_rm`` / ``fm_hist_stats_rm``).
 
 Two layouts:
 
-* ``static`` — a row is a right-aligned fixed window (NaN padded on the left)
-  written once: the absolute-time ``historical`` query of a canary / rolling
-  update job never changes while the job is re-examined.
+* ``static`` — a row is a fixed window written once, LEFT-aligned (samples
+  from column 0, NaN after): the absolute-time ``historical`` query of a
+  canary / rolling update job never changes while the job is re-examined.
+  The scored view is ``[0, longest row)``, so a complete row holds no missing
+  sample inside the view and the row-stats kernel keeps its unmasked fast
+  path (right-aligned rows carried up to 3 NaN of alignment padding in front
+  of every 7-day window, which sent every row down the masked path).
 * ``sliding`` — every row lives on one global time grid (column c = time
   t0 + c*step) and the window is the last ``T`` columns before "now".  When
   time advances the window start moves right (a view offset, no data moved);
@@ -78,6 +82,7 @@ class ResidentHistory:
             self._grow(capacity)
         self.compactions = 0
         self.bytes_in = 0
+        self.max_len = 0                            # static: longest row written (view length)
 
     # ------------------------------------------------------------------ rows
     def __len__(self) -> int:
@@ -145,12 +150,13 @@ class ResidentHistory:
 
     # ------------------------------------------------------------------ writes
     def write_static(self, rows: np.ndarray, values: list[np.ndarray], t_last: np.ndarray) -> None:
-        """Static rows: right-align each series into its row (one packed
+        """Static rows: left-align each series into its row (one packed
         host->device copy, one scatter of whole rows)."""
         assert not self.sliding
         if len(rows) == 0:
             return
-        packed = native_rt.pack_right(values, self.width, self.width)
+        packed = native_rt.pack_left(values, self.width, self.width)
+        self.max_len = max(self.max_len, min(self.width, max((len(v) for v in values), default=0)))
         src = torch.from_numpy(packed)
         if self.device.type == "cuda":
             src = src.pin_memory().to(self.device, non_blocking=True)
@@ -160,7 +166,7 @@ class ResidentHistory:
 
     def view(self) -> HistView:
         if not self.sliding:
-            return HistView(self.buf, self.width, self.width)
+            return HistView(self.buf, self.width, max(1, self.max_len))
         vs = max(0, self.ws // 4 * 4)
         return HistView(self.buf[:, vs:], self.width, self.e - vs)
 

@@ -193,6 +193,29 @@ class StagedSource:
         return got
 
 
+class StaticSource:
+    """Fixed answers by URL substring (tests, demos, and operator-provided
+    series such as a static call graph)."""
+
+    local = True
+    immutable = True
+
+    def __init__(self, answers: dict[str, list[Series]], fallback=None):
+        self.answers = answers
+        self.fallback = fallback
+        if fallback is not None:
+            self.local = getattr(fallback, "local", False)
+            self.immutable = getattr(fallback, "immutable", False)
+
+    def fetch(self, url: str) -> list[Series]:
+        for k, v in self.answers.items():
+            if k in url:
+                return v
+        if self.fallback is None:
+            raise SourceError(f"no static answer for {url}")
+        return self.fallback.fetch(url)
+
+
 def dict_set(s: Series, k: str, v: str) -> Series:
     s.labels[k] = v
     return s

@@ -308,3 +308,63 @@ def test_checkpoint_reshards_after_world_size_change(tmp_path):
             assert D.service_owner("ns", j.split(":")[0], 3) == rank
             got[j] = rank
     assert set(got) == {f"{a}:ns:hpa" for a in apps}
+
+
+def _impact_brain(algorithm="moving_average_all", mode="judge", faults=None):
+    from foremast_amd.engine.sources import Series, StaticSource, SyntheticSource
+    clock = Clock()
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    cfg = BrainConfig()
+    cfg.ml_algorithm = algorithm
+    cfg.downstream_edges_url = "http://prom/api/v1/query?query=namespace_app_caller_uri_http_server_requests_rate"
+    cfg.downstream_mode = mode
+    e = lambda app, caller, uri, r: Series({"namespace": "default", "app": app, "caller": caller, "uri": uri},
+                                           np.array([T0]), np.array([r], np.float32))
+    # frontend sends 80% of its calls to payments (/pay 60, /refund 20), 20% to search;
+    # payments calls ledger
+    edges = [e("payments", "frontend", "/pay", 60.0), e("payments", "frontend", "/refund", 20.0),
+             e("search", "frontend", "/q", 20.0), e("ledger", "payments", "/post", 5.0)]
+    src = SourceRouter(synthetic=StaticSource({"caller_uri": edges}, fallback=SyntheticSource(
+        faults=faults or {}, fault_after=T0 - 900)),
+                       force="synthetic")
+    exp = BrainExporter()
+    brain = Brain(store, cfg, sources=src, clock=clock, exporter=exp, worker_id="w0")
+    return clock, store, client, brain, exp
+
+
+@pytest.mark.parametrize("algorithm", ["moving_average_all", "moving_average"])
+def test_callee_fault_marks_caller_job_downstream(algorithm):
+    """an injected fault in a callee (ledger, 2 hops down)
+    marks the caller's job unhealthy with a ``downstream`` reason naming the
+    path, the traffic share and the caller's APIs on the first edge; a
+    service with no anomalous callee stays healthy."""
+    clock, store, client, brain, exp = _impact_brain(algorithm, faults={"ledger": 6.0})
+    ids = {app: client.start_analyzing("default", app, None, _metrics(), 10, "continuous")
+           for app in ("frontend", "payments", "search", "ledger")}
+    brain.run_once()
+    st = {a: store.get(j) for a, j in ids.items()}
+    assert st["ledger"].status == "completed_unhealth"
+    for caller in ("payments", "frontend"):
+        d = st[caller]
+        assert d.status == "completed_unhealth", (caller, d.status, d.reason)
+        rs = json.loads(html.unescape(d.reason))
+        down = [r for r in rs if r["name"] == "downstream"][0]
+        assert down["callees"][0]["callee"] == "default/ledger"
+        assert "downstream" in json.loads(d.anomaly_info)
+    fr = [r for r in json.loads(html.unescape(st["frontend"].reason)) if r["name"] == "downstream"][0]
+    assert fr["callees"][0]["path"] == ["default/payments", "default/ledger"]
+    assert fr["callees"][0]["share"] == pytest.approx(0.8) and fr["callees"][0]["apis"] == ["/pay", "/refund"]
+    assert st["search"].status != "completed_unhealth"
+    assert exp.sample("foremastbrain:namespace_app_pod_downstream_impact", "default", "frontend") == \
+        pytest.approx(0.8) or algorithm != "moving_average_all"
+    assert exp.registry.get_sample_value("foremastbrain:cluster_impact_max", {"cluster": "local"}) == 1.0
+
+
+def test_downstream_annotate_mode_keeps_healthy_callers():
+    clock, store, client, brain, exp = _impact_brain(mode="annotate", faults={"ledger": 6.0})
+    ids = {app: client.start_analyzing("default", app, None, _metrics(), 10, "continuous")
+           for app in ("frontend", "payments", "search", "ledger")}
+    brain.run_once()
+    assert store.get(ids["ledger"]).status == "completed_unhealth"
+    assert store.get(ids["frontend"]).status != "completed_unhealth"

@@ -194,8 +194,10 @@ def test_static_rows_are_written_once_and_released():
     rows, new = h.rows_for([("j", "a"), ("j", "b")])
     h.write_static(rows, [np.arange(20, dtype=np.float32), np.arange(3, dtype=np.float32)], np.array([1.0, 2.0]))
     v = h.view()
+    # left-aligned: the newest 16 samples from column 0; the view is the longest row
     np.testing.assert_array_equal(v.hist[rows[0]].numpy(), np.arange(4, 20, dtype=np.float32))
-    assert np.isnan(v.hist[rows[1], :13]).all() and (v.hist[rows[1], 13:].numpy() == [0, 1, 2]).all()
+    assert (v.hist[rows[1], :3].numpy() == [0, 1, 2]).all() and np.isnan(v.hist[rows[1], 3:]).all()
+    assert v.T == 16
     rows2, new2 = h.rows_for([("j", "a")])
     assert not new2.any() and rows2[0] == rows[0]
     assert h.release([("j", "a"), ("j", "b")]) == 2 and len(h) == 0
@@ -262,3 +264,31 @@ def test_memory_store_claim_batch_and_uniform_updates():
     store.update_uniform(ids, {"status": ST.COMPLETED_HEALTH, "reason": ""}, now=T0 + 5)
     assert {store.get(i).status for i in ids} == {ST.COMPLETED_HEALTH}
     assert store.claim_batch("w4", 100, 1e9, now=T0 + 6).ids == []
+
+
+@pytest.mark.gpu
+def test_gpu_resident_tick_masked_rows_match_cpu(cuda):
+    """The row-stats kernel's masked path (gaps, short rows, NaN tails) in the
+    resident front tick against the CPU scorer on the same rows."""
+    from foremast_amd.engine.resident import HistView
+    from foremast_amd.engine.scorer import CanaryScorer
+    from foremast_amd.ops import canary as C
+    aliases = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
+    S, T = 96, 10081
+    h, b, c = C.synth_fleet(S, 8, T, 5, 10, 0, device="cpu", fault_rate=0.2)
+    h = h.numpy().copy()
+    rng = np.random.default_rng(3)
+    h[rng.random(h.shape) < 0.01] = np.nan          # Prometheus gaps everywhere
+    h[5, :9000] = np.nan                             # a young service
+    h[7, :] = np.nan                                 # no history at all
+    W = 10084
+    buf = np.full((S * 8 + 16, W), np.nan, np.float32)
+    perm = rng.permutation(S * 8)
+    buf[perm, :T] = h[:, :T]
+    rm = torch.from_numpy(perm.astype(np.int32)).to(cuda)
+    sc = CanaryScorer(aliases, device=cuda)
+    o = sc.score_resident(HistView(torch.from_numpy(buf).to(cuda), W, T), rm, c.to(cuda), b.to(cuda))
+    ref = CanaryScorer(aliases, device="cpu").score(torch.from_numpy(np.ascontiguousarray(h[:, :T])), b, c, T)
+    np.testing.assert_allclose(o.decide.stats.cpu().numpy(), ref.decide.stats.numpy(), rtol=3e-5, atol=1e-4)
+    np.testing.assert_array_equal(o.decide.valid.cpu().numpy(), ref.decide.valid.numpy())
+    assert (o.packed[:, 0].cpu() == ref.packed[:, 0]).float().mean() >= 0.99
