@@ -72,6 +72,8 @@ _SIGS: dict[str, list] = {
                        c_void_p, c_void_p],
     "fm_lsq_project": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p],
+    "fm_lsq_residual": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fm_stream_read": [c_void_p, c_i64, c_void_p, c_int, c_void_p],
     "fm_lstm_forward": [c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p],
     "fm_lstm_forward_nct": [c_void_p, c_i64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -84,9 +84,27 @@ def _basis(T: int, H: int, step_s: float):
     return ut, Xf @ vs, vs, int(keep.sum())
 
 
+def lsq_residual(Y: torch.Tensor, T: int, XT: torch.Tensor, Z: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
+    """SSE of every row's fit from a direct residual pass: sum over finite
+    samples of (y - c - U z)^2, fp32 residuals accumulated in fp64 (not the
+    cancellation-prone |y - c|^2 - |z|^2)."""
+    R = Y.shape[0]
+    if not Y.is_cuda:
+        y = Y.numpy()[:, :T].astype(np.float64)
+        fit = Z.numpy().astype(np.float64) @ XT.numpy()[:, :T].astype(np.float64)
+        r = y - shift.numpy().astype(np.float64)[:, None] - fit
+        return torch.from_numpy(np.where(np.isfinite(y), r * r, 0.0).sum(1))
+    require_native(Y)
+    check(Z.is_contiguous() and Z.shape == (R, F) and Z.dtype == torch.float32, "Z must be a contiguous [R, 32] f32")
+    sse = torch.empty((R,), dtype=torch.float64, device=Y.device)
+    LIB.call("fm_lsq_residual", ptr(Y), Y.stride(0), T, R, ptr(XT), XT.stride(0), ptr(Z), ptr(shift), ptr(sse),
+             stream_of(Y))
+    return sse
+
+
 def prophet_fit(Y: torch.Tensor, T: int, H: int, step_s: float = 60.0) -> LsqFit:
-    """Least-squares fit of the shared design to every row; residual sigma
-    from SSE = |y - c|^2 - |U^T (y - c)|^2 (orthonormal U)."""
+    """Least-squares fit of the shared design to every row (projection pass),
+    residual sigma from a second, direct residual pass (lsq_residual)."""
     ut, fmap, vs, rank = _basis(T, H, step_s)
     d = Y.device
     key = (T, H, step_s, str(d))
@@ -95,7 +113,7 @@ def prophet_fit(Y: torch.Tensor, T: int, H: int, step_s: float = 60.0) -> LsqFit
     XT = _XT_CACHE[key]
     Z, yy, sh, nv = lsq_project(Y, T, XT)
     Zd = Z.to(torch.float64)
-    sse = (yy.to(torch.float64) - (Zd * Zd).sum(1)).clamp(min=0)
+    sse = lsq_residual(Y, T, XT, Z, sh).to(d)
     fc = Zd @ torch.from_numpy(fmap.T.copy()).to(d) + sh.to(torch.float64)[:, None]
     beta = Zd @ torch.from_numpy(vs.T.copy()).to(d)
     beta[:, 0] += sh.to(torch.float64)

@@ -313,7 +313,20 @@ def test_gpu_lsq_prophet(cuda):
     g = LQ.prophet_fit(torch.from_numpy(Y).to(cuda), T, H)
     c = LQ.prophet_fit(torch.from_numpy(Y), T, H)
     np.testing.assert_allclose(g.forecast.cpu().numpy(), c.forecast.numpy(), rtol=1e-3, atol=2e-3)
-    np.testing.assert_allclose(g.sigma.cpu().numpy(), c.sigma.numpy(), rtol=0.05)
+    # sigma from the direct residual pass, not yy - |z|^2
+    np.testing.assert_allclose(g.sigma.cpu().numpy(), c.sigma.numpy(), rtol=1e-3)
+    # a near-perfect fit (residual 1e-4 of the level): the old difference of
+    # sums lost every digit here
+    rng = np.random.default_rng(5)
+    Xd = LQ.design_matrix(T, H)[:T]
+    beta = rng.normal(0, 1, (R, LQ.F))
+    beta[:, 0] += 100.0
+    Y2 = np.full((R, ld), 0, np.float32)
+    Y2[:, :T] = (beta @ Xd.T + rng.normal(0, 0.01, (R, T))).astype(np.float32)
+    g2 = LQ.prophet_fit(torch.from_numpy(Y2).to(cuda), T, H)
+    c2 = LQ.prophet_fit(torch.from_numpy(Y2), T, H)
+    np.testing.assert_allclose(g2.sigma.cpu().numpy(), c2.sigma.numpy(), rtol=1e-3)
+    np.testing.assert_allclose(c2.sigma.numpy(), 0.01, rtol=0.1)
     Zg = LQ.lsq_project(torch.from_numpy(Y).to(cuda), T, LQ._XT_CACHE[(T, H, 60.0, str(torch.device(cuda)))])
     Zc = LQ.lsq_project(torch.from_numpy(Y), T, LQ._XT_CACHE[(T, H, 60.0, "cpu")])
     np.testing.assert_allclose(Zg[0].cpu().numpy(), Zc[0].numpy(), rtol=1e-4, atol=1e-2)
