@@ -296,7 +296,8 @@ def config4(args):
     S, M = args.services, args.metrics
     svc0, _, pad = D.shard_range(S, info.rank, info.world)
     hist, _, cur = C.synth_fleet(pad, M, T_HIST, 1, args.window, svc0, device=dev)
-    model = LSTMForecaster(hidden=args.hidden, window=args.lookback, horizon=args.window, device=dev)
+    model = LSTMForecaster(hidden=args.hidden, window=args.lookback, horizon=args.window, device=dev,
+                           layers=args.layers, n_metrics=M if args.multivariate else None)
     # random-init weights broadcast from rank 0 (C6) so every rank runs the same model
     sd = D.broadcast_object(model.state_dict() if info.is_main else None)
     model.load_state_dict(sd)
@@ -315,10 +316,14 @@ def config4(args):
         D.all_gather_rows(packed, gathered)
 
     ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    mode = (f"multivariate (one sequence per service, {M} metrics + daily phase as features)" if args.multivariate
+            else "univariate (one sequence per series)")
+    kern = "streamed-weight stacked kernel" if model.stacked else "register-resident kernel"
     _common(args, info, ms, p50, "series forecast+judged/sec (node), LSTM HPA forecaster",
-            S * M / (ms / 1e3), "series/s", f"LSTM H={args.hidden}, lookback {args.lookback}, horizon {args.window},"
-            " bf16 MFMA recurrence, fp32 cell/accumulate", S * M, args.lookback, "strong", "bf16",
-            "synthetic on-device fleet (K11), random-init weights", {"services": S, "metrics": M})
+            S * M / (ms / 1e3), "series/s", f"LSTM H={args.hidden} x {args.layers} layer(s), {mode}, lookback "
+            f"{args.lookback}, horizon {args.window}, bf16 MFMA recurrence ({kern}), fp32 cell/accumulate", S * M,
+            args.lookback, "strong", "bf16", "synthetic on-device fleet (K11), random-init weights",
+            {"services": S, "metrics": M, "layers": args.layers, "multivariate": bool(args.multivariate)})
 
 
 # --------------------------------------------------------------------------- config 5
@@ -371,6 +376,9 @@ def main():
     ap.add_argument("--pods", type=int, default=5)
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--lookback", type=int, default=240)
+    ap.add_argument("--layers", type=int, default=1, help="config 4: stacked LSTM layers (1 or 2)")
+    ap.add_argument("--multivariate", action="store_true", help="config 4: one sequence per service, all metrics "
+                    "as input features")
     ap.add_argument("--clusters", type=int, default=4)
     ap.add_argument("--degree", type=int, default=6)
     ap.add_argument("--hops", type=int, default=2)

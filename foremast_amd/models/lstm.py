@@ -1,9 +1,19 @@
 """LSTM forecaster for HPA / ClusterAutoScaler prediction (BASELINE config 4;
 docs/guides/design.md:81-85 "Deep Learning (LSTM)", README.md:58-59).
 
-Inference runs the hand-written bf16 MFMA LSTM kernel (``ops.lstm``) over the
-last ``window`` samples of every series (z-scored per row, plus daily phase
-features), then a linear head maps h_T to ``horizon`` future points.  Training
+Inference runs the hand-written bf16 MFMA LSTM kernels (``ops.lstm``) over the
+last ``window`` samples, then a linear head maps h_T to ``horizon`` future
+points.  Two input modes:
+
+* univariate (``n_metrics=None``): one sequence per series, features
+  [z, sin, cos] of the daily phase;
+* multivariate (``n_metrics=M``, the reference's "LSTM for 3+ metrics",
+  docs/guides/design.md:81-85): one sequence per SERVICE whose features are
+  the z-scores of all M metrics plus the phase; the head forecasts all M.
+
+H in {32, 64, 128} with one layer runs the register-resident kernel
+(lstm.hip); H = 256 and/or two stacked layers run the streamed-weight kernel
+(lstm_stack.hip), which keeps layer 0's h on chip for layer 1.  Training
 (``fit``) uses torch autograd on an ``nn.LSTM`` with identical parameters —
 the reference trained Keras models offline too (foremast-brain/faq.md:10);
 the trained weights are what the HIP forward consumes.  Weights persist via
@@ -21,14 +31,19 @@ from ..ops import lstm as LS
 
 class LSTMForecaster:
     def __init__(self, hidden: int = 128, window: int = 240, horizon: int = 60, n_features: int = 3,
-                 seed: int = 0, device="cpu", period: float = 1440.0):
-        assert hidden in LS.SUPPORTED_H
+                 seed: int = 0, device="cpu", period: float = 1440.0, layers: int = 1, n_metrics: int | None = None):
+        assert hidden in LS.STACK_H and layers in (1, 2)
+        self.M = n_metrics
+        if n_metrics is not None:
+            assert 1 <= n_metrics <= 13, "multivariate input: M z-scores + sin + cos + bias in one 16-wide K step"
+            n_features = n_metrics + 2
         self.H, self.L, self.horizon, self.I = hidden, window, horizon, n_features
+        self.layers = layers
         self.period = period
         self.device = torch.device(device)
         g = torch.Generator().manual_seed(seed)
-        self.lstm = torch.nn.LSTM(n_features, hidden, batch_first=True)
-        self.head = torch.nn.Linear(hidden, horizon)
+        self.lstm = torch.nn.LSTM(n_features, hidden, num_layers=layers, batch_first=True)
+        self.head = torch.nn.Linear(hidden, horizon * (n_metrics or 1))
         k = 1.0 / math.sqrt(hidden)
         with torch.no_grad():
             for p in list(self.lstm.parameters()) + list(self.head.parameters()):
@@ -50,11 +65,27 @@ class LSTMForecaster:
         self.head.load_state_dict({k[5:]: v for k, v in sd.items() if k.startswith("head.")})
         self._packed = None
 
-    def packed(self) -> torch.Tensor:
+    @property
+    def stacked(self) -> bool:
+        """Streamed-weight kernel (H = 256 or two layers)."""
+        return self.layers > 1 or self.H not in LS.SUPPORTED_H
+
+    def packed(self):
         if self._packed is None:
             l = self.lstm
-            self._packed = LS.pack_lstm(l.weight_ih_l0, l.weight_hh_l0, l.bias_ih_l0 + l.bias_hh_l0).to(self.device)
+            if self.stacked:
+                ws = [(getattr(l, f"weight_ih_l{k}"), getattr(l, f"weight_hh_l{k}"),
+                       getattr(l, f"bias_ih_l{k}") + getattr(l, f"bias_hh_l{k}")) for k in range(self.layers)]
+                self._packed = [p.to(self.device) for p in LS.pack_stack(ws, self.H)]
+            else:
+                self._packed = LS.pack_lstm(l.weight_ih_l0, l.weight_hh_l0,
+                                            l.bias_ih_l0 + l.bias_hh_l0).to(self.device)
         return self._packed
+
+    def _run(self, xa: torch.Tensor) -> torch.Tensor:
+        if self.stacked:
+            return LS.lstm_stack_forward(xa, self.packed(), self.H)[0]
+        return LS.lstm_forward_packed(xa, self.packed(), self.H)[0]
 
     # ------------------------------------------------------------------ features
     def features(self, hist: torch.Tensor, T: int):
@@ -72,21 +103,47 @@ class LSTMForecaster:
         feats = [z, torch.sin(ph).expand_as(z), torch.cos(ph).expand_as(z)][: self.I]
         return torch.stack(feats, -1).contiguous(), mu, sd
 
+    def features_mv(self, hist: torch.Tensor, T: int):
+        """Multivariate features [S, L, M + 2] (rows of ``hist`` are services x M)."""
+        M = self.M
+        R = hist.shape[0]
+        x, mu, sd = self.features_uni(hist, T)            # [R, L, 3]: z, sin, cos
+        S = R // M
+        z = x[..., 0].reshape(S, M, -1).permute(0, 2, 1)   # [S, L, M]
+        return torch.cat([z, x[: S * M: M, :, 1:3]], -1).contiguous(), mu, sd
+
+    def features_uni(self, hist, T):
+        I, self.I = self.I, 3
+        try:
+            return self.features(hist, T)
+        finally:
+            self.I = I
+
     @torch.no_grad()
     def forecast(self, hist: torch.Tensor, T: int, H: int):
-        """-> (forecast [R, H] in data units, sigma [R]) with sigma = window std."""
+        """-> (forecast [R, H] in data units, sigma [R]) with sigma = window std.
+        Multivariate models take rows as services x M (R % M == 0)."""
+        R = hist.shape[0]
+        if self.M is not None:
+            assert R % self.M == 0, "multivariate forecaster: rows must be services x n_metrics"
+        L = min(self.L, T)
         if hist.is_cuda:
             # features written by a HIP kernel straight into the bf16 augmented layout
-            xa, mu, sd = LS.lstm_features(hist, T, min(self.L, T), self.period, self.I)
-            hT, _, _ = LS.lstm_forward_packed(xa, self.packed(), self.H)
+            if self.M is not None:
+                xa, mu, sd = LS.lstm_features_mv(hist, T, R // self.M, self.M, L, self.period)
+            else:
+                xa, mu, sd = LS.lstm_features(hist, T, L, self.period, self.I)
+            hT = self._run(xa)
         else:
-            x, mu, sd = self.features(hist, T)
+            x, mu, sd = self.features_mv(hist, T) if self.M is not None else self.features(hist, T)
             with torch.no_grad():
                 _, (h, _) = self.lstm(x)
-                hT = h[0]
+                hT = h[-1]
         W = self.head.weight.to(hT.device)
         b = self.head.bias.to(hT.device)
-        z = hT @ W.T + b                                    # [R, horizon]
+        z = hT @ W.T + b                                    # [rows, horizon (x M)]
+        if self.M is not None:
+            z = z.reshape(-1, self.M, self.horizon).reshape(R, self.horizon)
         if H > self.horizon:
             z = torch.cat([z, z[:, -1:].expand(-1, H - self.horizon)], 1)
         fc = mu[:, None] + sd[:, None] * z[:, :H]
@@ -118,14 +175,26 @@ class LSTMForecaster:
                 idx = torch.as_tensor(e[:, None] + np.arange(-L, Hz)[None, :], device=dev)
                 seg = hist[torch.as_tensor(r, device=dev)[:, None], idx].float()
                 seg = torch.nan_to_num(seg, nan=0.0)
-                win, tgt = seg[:, :L], seg[:, L:]
-                mu, sd = win.mean(1, keepdim=True), win.std(1, keepdim=True).clamp(min=1e-6)
                 t = torch.as_tensor(e[:, None] + np.arange(-L, 0)[None, :], device=dev, dtype=torch.float32)
                 ph = 2 * math.pi * t / self.period
-                x = torch.stack([(win - mu) / sd, torch.sin(ph), torch.cos(ph)][: self.I], -1)
+                if self.M is None:
+                    win, tgt = seg[:, :L], seg[:, L:]
+                    mu, sd = win.mean(1, keepdim=True), win.std(1, keepdim=True).clamp(min=1e-6)
+                    x = torch.stack([(win - mu) / sd, torch.sin(ph), torch.cos(ph)][: self.I], -1)
+                    target = (tgt - mu) / sd
+                else:
+                    # rows are services: all M metric rows of service r // M
+                    M = self.M
+                    svc = torch.as_tensor((r // M) * M, device=dev)[:, None] + torch.arange(M, device=dev)[None, :]
+                    seg = torch.nan_to_num(hist[svc[:, :, None], idx[:, None, :]].float(), nan=0.0)  # [b, M, L+Hz]
+                    win, tgt = seg[..., :L], seg[..., L:]
+                    mu, sd = win.mean(2, keepdim=True), win.std(2, keepdim=True).clamp(min=1e-6)
+                    x = torch.cat([((win - mu) / sd).permute(0, 2, 1), torch.sin(ph)[..., None],
+                                   torch.cos(ph)[..., None]], -1)
+                    target = ((tgt - mu) / sd).reshape(len(r), -1)
                 _, (h, _) = lstm(x)
-                pred = head(h[0])
-                loss = torch.nn.functional.mse_loss(pred, (tgt - mu) / sd)
+                pred = head(h[-1])
+                loss = torch.nn.functional.mse_loss(pred, target)
                 opt.zero_grad()
                 loss.backward()
                 _allreduce_grads(list(lstm.parameters()) + list(head.parameters()))

@@ -11,7 +11,9 @@ import torch
 
 from ._lib import LIB, check, ptr, require_native, stream_of
 
-SUPPORTED_H = (32, 64, 128)
+SUPPORTED_H = (32, 64, 128)              # register-resident single-layer kernel (lstm.hip)
+STACK_H = (32, 64, 128, 256)             # streamed-weight 1-2 layer kernel (lstm_stack.hip)
+STACK_TILING = {256: (4, 1), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row tiles / wave, column tiles)
 
 
 def _bf16_bits(a: np.ndarray) -> np.ndarray:
@@ -52,6 +54,83 @@ def pack_lstm(w_ih: torch.Tensor, w_hh: torch.Tensor, bias: torch.Tensor) -> tor
                                      np.where(kk == I, b[trow], 0.0))
                         out[w, rt, ks, :, j] = v
     return torch.from_numpy(_bf16_bits(out).view(np.uint8).copy())
+
+
+def pack_aug(aug: np.ndarray, H: int, RT: int) -> np.ndarray:
+    """Augmented gate matrix [4H, K] (columns in the B operand's k order,
+    K a multiple of 16) -> bf16 A fragments [H/(8 RT) waves, RT, K/16, 64 lanes, 8]
+    as uint16: wave w, row tile rt holds the gate rows [i f g o] x 8 units of
+    units 8 RT w + 8 rt + (0..7) (lane l: row l & 31, k half l >> 5)."""
+    K = aug.shape[1]
+    KS = K // 16
+    nw = H // (8 * RT)
+    lane = np.arange(64)
+    r, hh = lane & 31, lane >> 5
+    out = np.zeros((nw, RT, KS, 64, 8), np.float32)
+    for w in range(nw):
+        for rt in range(RT):
+            trow = (r >> 3) * H + 8 * RT * w + 8 * rt + (r & 7)
+            for ks in range(KS):
+                cols = 16 * ks + 8 * hh[:, None] + np.arange(8)[None, :]
+                out[w, rt, ks] = aug[trow[:, None], cols]
+    return _bf16_bits(out)
+
+
+def pack_stack(layers: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]], H: int) -> list[torch.Tensor]:
+    """[(W_ih, W_hh, b_ih + b_hh)] per layer (torch.nn.LSTM conventions) ->
+    the stacked kernel's per-layer fragment buffers (uint8)."""
+    RT = STACK_TILING[H][0]
+    out = []
+    for li, (w_ih, w_hh, b) in enumerate(layers):
+        w_ih, w_hh, b = (t.detach().float().cpu().numpy() for t in (w_ih, w_hh, b))
+        I = w_ih.shape[1]
+        if li == 0:
+            check(I <= 15, "layer-0 input features must be <= 15 (x, then the bias, in one K step)")
+            aug = np.zeros((4 * H, H + 16), np.float32)
+            aug[:, :H] = w_hh
+            aug[:, H:H + I] = w_ih
+            aug[:, H + I] = b
+        else:
+            check(I == H, "stacked layers take the previous layer's h")
+            aug = np.zeros((4 * H, 2 * H + 16), np.float32)
+            aug[:, :H] = w_hh
+            aug[:, H:2 * H] = w_ih
+            aug[:, 2 * H] = b
+        out.append(torch.from_numpy(pack_aug(aug, H, RT).view(np.uint8).copy()))
+    return out
+
+
+def lstm_stack_forward(xa: torch.Tensor, packed: list[torch.Tensor], H: int):
+    """xa [B, L, 16] bf16 augmented input -> (h_L, c_L) [B, H] f32 of the TOP
+    layer; 1 or 2 layers (``pack_stack``), H in STACK_H."""
+    check(xa.dim() == 3 and xa.shape[2] == 16 and xa.dtype == torch.bfloat16 and xa.is_contiguous(),
+          "xa must be contiguous [B, L, 16] bfloat16")
+    check(H in STACK_H and len(packed) in (1, 2), f"H must be one of {STACK_H}, 1 or 2 layers")
+    require_native(xa)
+    B, L, _ = xa.shape
+    d = xa.device
+    hT = torch.empty((B, H), dtype=torch.float32, device=d)
+    cT = torch.empty((B, H), dtype=torch.float32, device=d)
+    w0 = packed[0].to(d)
+    w1 = packed[1].to(d) if len(packed) > 1 else None
+    LIB.call("fm_lstm_stack", ptr(xa), B, L, H, len(packed), ptr(w0), ptr(w1), ptr(hT), ptr(cT), stream_of(xa))
+    return hT, cT
+
+
+def lstm_features_mv(hist: torch.Tensor, T: int, S: int, M: int, L: int, period: float):
+    """Multivariate input, one row per service: [z(metric 0..M-1), sin, cos, 1]
+    of the last L samples -> (xa [S, L, 16] bf16, mu [S*M], sd [S*M])."""
+    check(hist.dim() == 2 and hist.dtype == torch.float32 and hist.stride(1) == 1 and hist.shape[0] >= S * M,
+          "hist must be [S*M, T] float32")
+    check(0 < L <= T <= hist.shape[1] and 0 < M <= 13, "bad window / metric count (M + 3 <= 16)")
+    require_native(hist)
+    d = hist.device
+    xa = torch.empty((S, L, 16), dtype=torch.bfloat16, device=d)
+    mu = torch.empty((S * M,), dtype=torch.float32, device=d)
+    sd = torch.empty((S * M,), dtype=torch.float32, device=d)
+    LIB.call("fm_lstm_features_mv", ptr(hist), hist.stride(0), T, S, M, L, float(period), ptr(xa), ptr(mu), ptr(sd),
+             stream_of(hist))
+    return xa, mu, sd
 
 
 def augment(x: torch.Tensor) -> torch.Tensor:
@@ -128,4 +207,31 @@ def ref_lstm_forward(x: torch.Tensor, w_ih, w_hh, bias, h0=None, c0=None, emulat
         c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
         h = torch.sigmoid(o) * torch.tanh(c)
         hr = rd(h)
+    return h, c
+
+
+def ref_lstm_stack(x: torch.Tensor, layers: list, emulate_bf16: bool = True):
+    """fp32 reference of the stacked kernel: [(W_ih, W_hh, b)] per layer; with
+    emulate_bf16 weights, inputs and every h that feeds a GEMM (the recurrent
+    h and layer 0's h into layer 1) are rounded to bf16 as in the kernel.
+    -> (h_L, c_L) of the top layer."""
+    rd = bf16_round if emulate_bf16 else (lambda t: t)
+    B, L, _ = x.shape
+    seq = rd(x.float())
+    h = c = None
+    for w_ih, w_hh, b in layers:
+        H = w_hh.shape[1]
+        Wi, Wh, bb = rd(w_ih.float()), rd(w_hh.float()), rd(b.float())
+        h = torch.zeros(B, H)
+        c = torch.zeros(B, H)
+        hr = rd(h)
+        out = []
+        for t in range(L):
+            g = hr @ Wh.T + seq[:, t] @ Wi.T + bb
+            i, f, gg, o = g.chunk(4, dim=1)
+            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+            h = torch.sigmoid(o) * torch.tanh(c)
+            hr = rd(h)
+            out.append(hr)
+        seq = torch.stack(out, 1)
     return h, c

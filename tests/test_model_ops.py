@@ -417,3 +417,68 @@ def test_gpu_lstm_features_and_forecast(cuda):
     fc_g, sg = m.forecast(h.to(cuda), T, 10)
     fc_c, sc = m.forecast(h, T, 10)
     torch.testing.assert_close(fc_g.cpu(), fc_c, rtol=5e-2, atol=5e-2 * float(sc.max()))
+
+
+def test_ref_lstm_stack_matches_torch_two_layers():
+    torch.manual_seed(0)
+    m = torch.nn.LSTM(5, 32, num_layers=2, batch_first=True)
+    x = torch.randn(4, 30, 5)
+    _, (h, c) = m(x)
+    ws = [(getattr(m, f"weight_ih_l{k}"), getattr(m, f"weight_hh_l{k}"),
+           getattr(m, f"bias_ih_l{k}") + getattr(m, f"bias_hh_l{k}")) for k in range(2)]
+    hr, cr = LS.ref_lstm_stack(x, ws, emulate_bf16=False)
+    torch.testing.assert_close(hr, h[-1].detach(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(cr, c[-1].detach(), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("layers,M", [(2, None), (1, 4), (2, 8)])
+def test_lstm_forecaster_layers_and_multivariate_cpu(layers, M):
+    from foremast_amd.models.lstm import LSTMForecaster
+    m = LSTMForecaster(hidden=32, window=48, horizon=6, layers=layers, n_metrics=M, period=144.0)
+    R = 24 if M is None else 3 * M
+    hist = torch.from_numpy(_seasonal(R, 400, period=144, seed=layers))
+    fc, sd = m.forecast(hist, 400, 6)
+    assert fc.shape == (R, 6) and torch.isfinite(fc).all()
+    losses = m.fit(hist, 400, epochs=1, batch=8, max_windows=16)
+    assert np.isfinite(losses).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,layers,I", [(256, 2, 10), (128, 2, 3), (256, 1, 5), (64, 2, 15)])
+def test_gpu_lstm_stack_matches_fp32_lstm(cuda, H, layers, I):
+    """the streamed-weight kernel (H up to 256, 2 stacked
+    layers, multivariate input) against fp32 torch.nn.LSTM over 240 steps
+    (bf16 drift pinned) and against the bf16-emulating reference (tight)."""
+    torch.manual_seed(H + layers + I)
+    B, L = 200, 240
+    m = torch.nn.LSTM(I, H, num_layers=layers, batch_first=True)
+    x = torch.randn(B, L, I)
+    with torch.no_grad():
+        _, (h32, c32) = m(x)
+    ws = [(getattr(m, f"weight_ih_l{k}"), getattr(m, f"weight_hh_l{k}"),
+           getattr(m, f"bias_ih_l{k}") + getattr(m, f"bias_hh_l{k}")) for k in range(layers)]
+    pk = LS.pack_stack(ws, H)
+    hg, cg = LS.lstm_stack_forward(LS.augment(x.to(cuda).contiguous()), pk, H)
+    hr, cr = LS.ref_lstm_stack(x, ws, emulate_bf16=True)
+    torch.testing.assert_close(hg.cpu(), hr, atol=2e-2, rtol=2e-2)
+    err = (hg.cpu() - h32[-1]).abs()
+    assert float(err.max()) < 0.08 and float(err.mean()) < 0.01, (float(err.max()), float(err.mean()))
+
+
+@pytest.mark.gpu
+def test_gpu_lstm_multivariate_forecaster(cuda):
+    from foremast_amd.models.lstm import LSTMForecaster
+    S, M, T = 40, 8, 600
+    x = _seasonal(S * M, T, period=144, seed=11)
+    x[3, T - 7] = np.nan
+    h = torch.from_numpy(np.ascontiguousarray(np.pad(x, ((0, 0), (0, 4)), constant_values=np.nan)))
+    m = LSTMForecaster(hidden=256, window=120, horizon=12, layers=2, n_metrics=M, period=144.0)
+    xa, mu, sd = LS.lstm_features_mv(h.to(cuda), T, S, M, 120, 144.0)
+    f, mu0, sd0 = m.features_mv(h, T)
+    torch.testing.assert_close(mu.cpu(), mu0, rtol=1e-5, atol=1e-5)
+    xa = xa.float().cpu()
+    torch.testing.assert_close(xa[..., :M + 2], f.to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
+    assert (xa[..., M + 2] == 1).all() and (xa[..., M + 3:] == 0).all()
+    fc_g, _ = m.forecast(h.to(cuda), T, 12)
+    fc_c, sc = m.forecast(h, T, 12)
+    torch.testing.assert_close(fc_g.cpu(), fc_c, rtol=5e-2, atol=5e-2 * float(sc.max()))
