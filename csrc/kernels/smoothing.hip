@@ -10,12 +10,18 @@
 //
 // Mapping: one THREAD per (row, candidate) pair, candidates fastest, so the
 // lanes that share a row read the same history sample (one coalesced request).
-// The Holt-Winters seasonal state (m floats per pair) lives in a global
+// The Holt-Winters seasonal state (m values per pair) lives in a global
 // scratch laid out [m][pairs]: at step t every lane touches phase t % m of its
-// own column, i.e. one coalesced 256-B load + store per wave per step.  At the
-// BASELINE config-2 shape (40k series x 27 candidates x m=1440) that is 6 GB of
-// scratch, deliberately spent from the 288 GB of HBM instead of serialising the
-// grid.
+// own column, i.e. one coalesced load + store per wave per step.  At the
+// BASELINE config-2 shape (40k series x 27 candidates x m=1440) that scratch
+// traffic IS the fit's cost (2 x 8,640 steps x 1.08M pairs per fit), so the
+// additive grid fit can store it in fp16, scaled per row (indices / mean |x|
+// of the first season, saturated to the fp16 range): half the bytes of fp32
+// scratch (ops/smoothing.py picks it for the additive model with m >= 1000;
+// multiplicative indices, which multiply the level, stay fp32).  The recursion itself runs in
+// fp32 registers; only the parked seasonal indices are rounded (relative
+// 2^-11 per lap, damped by (1 - gamma) on every later lap).  The incremental
+// update of cached models keeps fp32 seasons (es_update_kernel).
 //
 // Rows are right-aligned with NaN padding on the left (ragged histories), so
 // every fit starts at the row's first finite sample and the seasonal
@@ -65,6 +71,21 @@ struct EsModel {
   }
 };
 
+// Seasonal-state storage: fp32 as is, or fp16 scaled by 1/sc (sc = 1 for the
+// multiplicative model).
+template <typename ST>
+struct SeasonIO {
+  float sc, isc;
+  __device__ __forceinline__ float ld(const ST* p, int64_t i) const {
+    if constexpr (sizeof(ST) == 4) return p[i];
+    else return (float)p[i] * sc;
+  }
+  __device__ __forceinline__ void st(ST* p, int64_t i, float v) const {
+    if constexpr (sizeof(ST) == 4) p[i] = v;
+    else p[i] = (ST)__builtin_amdgcn_fmed3f(v * isc, -65504.f, 65504.f);
+  }
+};
+
 // Initial seasonal index of a sample one season before (additive: x - s1,
 // multiplicative: x / s1; missing -> 0 / 1).
 template <int KIND>
@@ -93,10 +114,11 @@ struct SeasonInit {
 // reads (the H-step forecast needs phases T..T+H-1, last written in the
 // first H steps of the final season) -- when the caller does not keep the
 // fitted state, those stores are skipped.
-template <int KIND, bool GATED, bool LAP1 = false, bool NOSTORE = false>
+template <int KIND, bool GATED, bool LAP1 = false, bool NOSTORE = false, typename ST = float>
 __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restrict__ xr, int t, int T, int t_act,
-                                       int m, float* __restrict__ season, int64_t P, int64_t col, int& ph,
-                                       double& err2, int& n, SeasonInit<KIND> init = {}) {
+                                       int m, ST* __restrict__ season, int64_t P, int64_t col, int& ph,
+                                       double& err2, int& n, SeasonInit<KIND> init = {},
+                                       SeasonIO<ST> io = {1.f, 1.f}) {
   constexpr bool kSeason = KIND >= 2;
   float acc = 0.f;
   int chunk = 0;
@@ -114,7 +136,7 @@ __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restric
         int pu = ph + u;
         if (pu >= m) pu -= m;
         si[u] = (int64_t)pu * P + col;
-        sv[u] = LAP1 ? xr[t + u - m] : season[si[u]];
+        sv[u] = LAP1 ? xr[t + u - m] : io.ld(season, si[u]);
         xv[u] = xr[t + u];
       }
       ph += kPrefetch;
@@ -130,7 +152,7 @@ __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restric
       }
       if (!NOSTORE) {
 #pragma unroll
-        for (int u = 0; u < kPrefetch; ++u) season[si[u]] = sv[u];
+        for (int u = 0; u < kPrefetch; ++u) io.st(season, si[u], sv[u]);
       }
       chunk += kPrefetch;
       if (chunk >= 64) { err2 += acc; acc = 0.f; chunk = 0; }
@@ -141,12 +163,12 @@ __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restric
     int64_t sidx = 0;
     if (kSeason) {
       sidx = (int64_t)ph * P + col;
-      s = LAP1 ? init(xr[t - m]) : season[sidx];
+      s = LAP1 ? init(xr[t - m]) : io.ld(season, sidx);
       if (++ph == m) ph = 0;
     }
     if (GATED && t < t_act) continue;
     md.step(xr[t], s, acc, n);
-    if (kSeason && !NOSTORE) season[sidx] = s;
+    if (kSeason && !NOSTORE) io.st(season, sidx, s);
     if (++chunk == 64) { err2 += acc; acc = 0.f; chunk = 0; }
   }
   err2 += acc;
@@ -158,41 +180,45 @@ __device__ __forceinline__ int first_finite(const float* __restrict__ xr, int T)
   return b;
 }
 
-// Finite-sample mean of xr[lo, hi); sets cnt.  Branch-free body so the
-// loads of consecutive iterations are issued back to back.
-__device__ __forceinline__ float nan_mean(const float* __restrict__ xr, int lo, int hi, int& cnt) {
-  float s = 0.f;
+// Finite-sample mean of xr[lo, hi); sets cnt (and the mean |x| in *mabs).
+// Branch-free body so the loads of consecutive iterations are issued back to
+// back.
+__device__ __forceinline__ float nan_mean(const float* __restrict__ xr, int lo, int hi, int& cnt,
+                                          float* mabs = nullptr) {
+  float s = 0.f, a = 0.f;
   int c = 0;
 #pragma unroll 8
   for (int i = lo; i < hi; ++i) {
     const float v = xr[i];
     const bool f = isfinite(v);
     s += f ? v : 0.f;
+    a += f ? fabsf(v) : 0.f;
     c += f;
   }
   cnt = c;
+  if (mabs != nullptr) *mabs = c > 0 ? a / c : 0.f;
   return c > 0 ? s / c : 0.f;
 }
 
 // Seasonal indices of samples xs[i0, i1) written to consecutive phases from
 // sp on (stride P); samples at or past navail are missing.
-template <int KIND>
+template <int KIND, typename ST>
 __device__ __forceinline__ void season_init(const float* __restrict__ xs, int i0, int i1, int navail,
-                                            SeasonInit<KIND> init, float* __restrict__ sp, int64_t P) {
+                                            SeasonInit<KIND> init, ST* __restrict__ sp, int64_t P, SeasonIO<ST> io) {
   const int last = navail > 0 ? navail - 1 : 0;
 #pragma unroll 8
   for (int i = i0; i < i1; ++i) {
     const float v = xs[i < last ? i : last];   // unpredicated load, masked below
-    sp[(int64_t)(i - i0) * P] = i < navail ? init(v) : init(__builtin_nanf(""));
+    io.st(sp, (int64_t)(i - i0) * P, i < navail ? init(v) : init(__builtin_nanf("")));
   }
 }
 
-template <int KIND>
+template <int KIND, typename ST>
 __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x, int64_t ld, int T, int64_t R,
                                                     const float* __restrict__ cand, int G, int m,
-                                                    float* __restrict__ season /*[m][R*G]*/, float* __restrict__ sse,
+                                                    ST* __restrict__ season /*[m][R*G]*/, float* __restrict__ sse,
                                                     float* __restrict__ state /*[R*G,3]*/, int* __restrict__ nobs,
-                                                    int t_store_end) {
+                                                    int t_store_end, float* __restrict__ sscale /*[R]*/) {
   const int64_t P = R * G;
   const int64_t pid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if ((pid_raw & ~(int64_t)63) >= P) return;      // whole wave past the end
@@ -207,6 +233,7 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
   const int base = first_finite(xr, T);
   int t0;
   SeasonInit<KIND> sinit{0.f, 0.f, false};
+  SeasonIO<ST> io{1.f, 1.f};
   if (base >= T) {
     md.lvl = __builtin_nanf("");
     t0 = T;
@@ -215,7 +242,12 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     // the first) / m, seasonal indices from the first season (finite samples)
     int c1, c2;
     const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
-    const float s1 = nan_mean(xr, base, e1, c1);
+    float a1;
+    const float s1 = nan_mean(xr, base, e1, c1, &a1);
+    if (sizeof(ST) == 2 && KIND == 2) {
+      const float sc = a1 > 1e-20f ? a1 : 1.f;
+      io = SeasonIO<ST>{sc, 1.f / sc};
+    }
     const float s2 = nan_mean(xr, e1, e2, c2);
     md.lvl = s1;
     md.tr = c2 > 0 ? (s2 - s1) / m : 0.f;
@@ -237,11 +269,11 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     if (KIND >= 2) {
       // seasons written up to t_store_end (T when the fitted state is kept)
       const int ts = max(lo + m, min(t_store_end, T));
-      es_run<KIND, false, true>(md, xr, lo, lo + m, lo, m, season, P, pid, ph, err2, n, sinit);
-      es_run<KIND, false>(md, xr, lo + m, ts, lo, m, season, P, pid, ph, err2, n);
-      es_run<KIND, false, false, true>(md, xr, ts, T, lo, m, season, P, pid, ph, err2, n);
+      es_run<KIND, false, true, false, ST>(md, xr, lo, lo + m, lo, m, season, P, pid, ph, err2, n, sinit, io);
+      es_run<KIND, false, false, false, ST>(md, xr, lo + m, ts, lo, m, season, P, pid, ph, err2, n, {}, io);
+      es_run<KIND, false, false, true, ST>(md, xr, ts, T, lo, m, season, P, pid, ph, err2, n, {}, io);
     } else {
-      es_run<KIND, false>(md, xr, lo, T, lo, m, season, P, pid, ph, err2, n);
+      es_run<KIND, false, false, false, ST>(md, xr, lo, T, lo, m, season, P, pid, ph, err2, n, {}, io);
     }
   } else {
     // ragged rows in this wave: materialise the initial seasons (sample
@@ -250,14 +282,15 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     if (KIND >= 2 && base < T) {
       const int ph0 = base % m;
       const int navail = min(m, T - base);
-      season_init<KIND>(xr + base, 0, m - ph0, navail, sinit, season + (int64_t)ph0 * P + pid, P);
-      season_init<KIND>(xr + base, m - ph0, m, navail, sinit, season + pid, P);
+      season_init<KIND, ST>(xr + base, 0, m - ph0, navail, sinit, season + (int64_t)ph0 * P + pid, P, io);
+      season_init<KIND, ST>(xr + base, m - ph0, m, navail, sinit, season + pid, P, io);
     }
-    es_run<KIND, true>(md, xr, lo, T, t0, m, season, P, pid, ph, err2, n);
+    es_run<KIND, true, false, false, ST>(md, xr, lo, T, t0, m, season, P, pid, ph, err2, n, {}, io);
   }
   // shadow lanes recompute their twin's pair in lockstep (same values, same
   // addresses) and then store no results of their own
   if (!live) return;
+  if (g == 0) sscale[row] = io.sc;
   sse[pid] = (float)err2;
   state[pid * 3 + 0] = md.lvl;
   state[pid * 3 + 1] = md.tr;
@@ -311,11 +344,12 @@ __global__ __launch_bounds__(256) void es_update_kernel(const float* __restrict_
 
 // Per row: pick the candidate with the smallest SSE and write the H-step
 // forecast + residual sigma.
+template <typename ST>
 __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restrict__ sse, const float* __restrict__ state,
-                                                          const int* __restrict__ nobs, const float* __restrict__ season,
-                                                          int64_t R, int G, int m, int kind, int H,
-                                                          float* __restrict__ fc /*[R,H]*/, float* __restrict__ sigma,
-                                                          int* __restrict__ best) {
+                                                          const int* __restrict__ nobs, const ST* __restrict__ season,
+                                                          const float* __restrict__ sscale, int64_t R, int G, int m,
+                                                          int kind, int H, float* __restrict__ fc /*[R,H]*/,
+                                                          float* __restrict__ sigma, int* __restrict__ best) {
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= R) return;
   const int64_t P = R * G;
@@ -334,7 +368,7 @@ __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restric
   for (int h = 1; h <= H; ++h) {
     float f = lvl + (kind >= 1 ? h * tr : 0.f);
     if (kind >= 2) {
-      const float s = season[(int64_t)((tph + h - 1) % m) * P + pid];
+      const float s = (float)season[(int64_t)((tph + h - 1) % m) * P + pid] * sscale[row];
       f = kind == 3 ? f * s : f + s;
     }
     fc[row * H + (h - 1)] = f;
@@ -348,13 +382,22 @@ __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restric
     else if (kind == 2) hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, stream, __VA_ARGS__);     \
     else hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, stream, __VA_ARGS__);                    \
   } while (0)
+#define FM_ES_DISPATCH_T(KERNEL, ST, GRID, ...)                                                      \
+  do {                                                                                              \
+    if (kind == 0) hipLaunchKernelGGL((KERNEL<0, ST>), GRID, dim3(256), 0, stream, __VA_ARGS__);    \
+    else if (kind == 1) hipLaunchKernelGGL((KERNEL<1, ST>), GRID, dim3(256), 0, stream, __VA_ARGS__); \
+    else if (kind == 2) hipLaunchKernelGGL((KERNEL<2, ST>), GRID, dim3(256), 0, stream, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<3, ST>), GRID, dim3(256), 0, stream, __VA_ARGS__);              \
+  } while (0)
 
 // keep_season = 0: only the seasonal indices the H-step forecast reads are
 // guaranteed in `season` afterwards (saves one store pass); 1: all of them
 // (the caller extracts the fitted state, e.g. for the model cache).
+// season_half = 1: the season scratch is fp16 [m][R*G] (scaled per row, the
+// scale written to sscale[R]); 0: fp32 (sscale[R] = 1).
 FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int kind,
-                     float* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma, int* best,
-                     int keep_season, hipStream_t stream) {
+                     void* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma, int* best,
+                     int keep_season, int season_half, float* sscale, hipStream_t stream) {
   if (R <= 0) return 0;
   if (kind < 0 || kind > 3) return (int)hipErrorInvalidValue;
   if (kind >= 2 && (m < 2 || 2 * m > T)) return (int)hipErrorInvalidValue;
@@ -362,11 +405,20 @@ FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* 
   if (kind < 2) m = 1;
   const int64_t P = R * G;
   const int t_store_end = keep_season || kind < 2 || H >= m ? T : T - m + H;
-  FM_ES_DISPATCH(es_fit_kernel, dim3((unsigned)((P + 255) / 256)), x, ld, T, R, cand, G, m, season, sse, state, nobs,
-                 t_store_end);
-  FM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(es_forecast_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, sse, state, nobs,
-                     season, R, G, m, kind, H, fc, sigma, best);
+  const dim3 gf((unsigned)((P + 255) / 256)), gr((unsigned)((R + 255) / 256));
+  if (season_half) {
+    FM_ES_DISPATCH_T(es_fit_kernel, _Float16, gf, x, ld, T, R, cand, G, m, (_Float16*)season, sse, state, nobs,
+                     t_store_end, sscale);
+    FM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(es_forecast_kernel<_Float16>, gr, dim3(256), 0, stream, sse, state, nobs,
+                       (const _Float16*)season, sscale, R, G, m, kind, H, fc, sigma, best);
+  } else {
+    FM_ES_DISPATCH_T(es_fit_kernel, float, gf, x, ld, T, R, cand, G, m, (float*)season, sse, state, nobs, t_store_end,
+                     sscale);
+    FM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(es_forecast_kernel<float>, gr, dim3(256), 0, stream, sse, state, nobs, (const float*)season,
+                       sscale, R, G, m, kind, H, fc, sigma, best);
+  }
   FM_LAUNCH_CHECK();
   return 0;
 }
@@ -384,6 +436,7 @@ FM_API int fm_es_update(const float* x, int64_t ld, int T, int64_t R, const int*
   return 0;
 }
 #undef FM_ES_DISPATCH
+#undef FM_ES_DISPATCH_T
 
 // ---------------------------------------------------------------------------
 // Model-agnostic band decision: compare current points against per-point

@@ -57,12 +57,17 @@ class ESFit:
     model: ESState | None = None
 
 
+HALF_SEASON_MIN_M = 1000     # <= ~10 laps of a 7-day history: measured within 2e-3 of fp32 (tests)
+
+
 def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, grid: np.ndarray | None = None,
-           keep_state: bool = False) -> ESFit:
+           keep_state: bool = False, half_season: bool = True) -> ESFit:
     """Fit SES / Holt / Holt-Winters (additive, multiplicative) by grid search
     on one-step SSE and forecast H steps past the end of the history.  With
     ``keep_state`` the best candidate's fitted state is returned as an
-    :class:`ESState` (for the model cache)."""
+    :class:`ESState` (for the model cache).  ``half_season``: the GPU grid
+    keeps its [m][R*G] seasonal scratch in fp16 scaled per row (half the HBM
+    traffic that bounds the fit; csrc/kernels/smoothing.hip)."""
     check(x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1, "x must be [R, T] float32")
     check(0 <= kind <= 3, f"kind must be 0..3, got {kind}")
     R = x.shape[0]
@@ -84,7 +89,15 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     d = x.device
     cand = torch.from_numpy(grid).to(d)
     P = R * G
-    season = torch.empty((m if kind >= 2 else 1, P), dtype=torch.float32, device=d)
+    # fp16 only where the scratch is big enough to be HBM traffic (daily /
+    # longer seasons: a handful of laps, little rounding to accumulate; at
+    # m = 288 (35 laps) SSEs moved by up to 1.2 %); short seasons stay fp32
+    # (their scratch is L2-resident anyway)
+    # multiplicative indices (~1, multiplying the level) keep fp32: fp16's 2^-11
+    # relative step moved their SSEs by up to 5 % on the oracle set
+    half = bool(half_season) and kind == 2 and m >= HALF_SEASON_MIN_M
+    season = torch.empty((m if kind >= 2 else 1, P), dtype=torch.float16 if half else torch.float32, device=d)
+    sscale = torch.empty((R,), dtype=torch.float32, device=d)
     sse = torch.empty((R, G), dtype=torch.float32, device=d)
     state = torch.empty((P, 3), dtype=torch.float32, device=d)
     nobs = torch.empty((P,), dtype=torch.int32, device=d)
@@ -92,13 +105,13 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     sig = torch.empty((R,), dtype=torch.float32, device=d)
     best = torch.empty((R,), dtype=torch.int32, device=d)
     LIB.call("fm_es_fit", ptr(x), x.stride(0), T, R, ptr(cand), G, m, kind, ptr(season), ptr(sse), ptr(state),
-             ptr(nobs), H, ptr(fc), ptr(sig), ptr(best), int(keep_state), stream_of(x))
+             ptr(nobs), H, ptr(fc), ptr(sig), ptr(best), int(keep_state), int(half), ptr(sscale), stream_of(x))
     model = None
     if keep_state:
         b = best.long()
         pid = torch.arange(R, device=d) * G + b
         model = ESState(kind, m, cand[b].contiguous(), state[pid].contiguous(),
-                        season[:, pid].t().contiguous() if kind >= 2 else None,
+                        (season[:, pid].t().float() * sscale[:, None]).contiguous() if kind >= 2 else None,
                         sse.gather(1, b[:, None])[:, 0].contiguous(), nobs[pid].contiguous())
     return ESFit(fc, sig, best, sse, model)
 

@@ -482,3 +482,31 @@ def test_gpu_lstm_multivariate_forecaster(cuda):
     fc_g, _ = m.forecast(h.to(cuda), T, 12)
     fc_c, sc = m.forecast(h, T, 12)
     torch.testing.assert_close(fc_g.cpu(), fc_c, rtol=5e-2, atol=5e-2 * float(sc.max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,m", [(2, 1440), (2, 1008)])
+def test_gpu_es_fit_half_season_matches_fp32(cuda, kind, m):
+    """the fp16 (row-scaled) seasonal scratch against the fp32
+    scratch on the same GPU grid: same SSEs to 2e-3, the same winner except
+    near-ties (both winners' SSEs within 1e-3), same forecast."""
+    T = 10080
+    x = _seasonal(64, T, period=m, seed=20 + kind)
+    x[:, :] *= np.geomspace(1e-3, 1e5, 64)[:, None].astype(np.float32)     # wide dynamic range across rows
+    x[5, :300] = np.nan
+    xt = torch.from_numpy(x).to(cuda)
+    h = SM.es_fit(xt, T, kind, 10, m, half_season=True)
+    f = SM.es_fit(xt, T, kind, 10, m, half_season=False)
+    s_h, s_f = h.sse.cpu().numpy(), f.sse.cpu().numpy()
+    stable = s_f < 1e3 * np.median(s_f, axis=1, keepdims=True)
+    np.testing.assert_allclose(s_h[stable], s_f[stable], rtol=2e-3)
+    bh, bf = h.best.cpu().numpy(), f.best.cpu().numpy()
+    flip = np.flatnonzero(bh != bf)
+    for r in flip:
+        a, b = s_f[r, bh[r]], s_f[r, bf[r]]
+        assert abs(a - b) <= 1e-3 * max(a, b), (r, a, b)
+    same = bh == bf
+    assert same.mean() >= 0.95
+    amp = np.abs(x[same]).mean(1, keepdims=True)
+    np.testing.assert_allclose(h.forecast.cpu().numpy()[same] / amp, f.forecast.cpu().numpy()[same] / amp,
+                               atol=2e-3)
