@@ -174,6 +174,95 @@ __device__ __forceinline__ void es_run(EsModel<KIND>& md, const float* __restric
   err2 += acc;
 }
 
+// fp16 seasonal scratch, blocked [m/8][P][8]: the 8 phases of a block are
+// one 16-B vector per pair, so a 16-step chunk of the recursion is 2 vector
+// loads + 2 vector stores per lane (1 KB fully coalesced per wave each)
+// instead of 16 + 16 two-byte accesses.  Requires m % 8 == 0.
+__device__ __forceinline__ int64_t blk_idx(int ph, int64_t P, int64_t col) {
+  return ((int64_t)(ph >> 3) * P + col) * 8 + (ph & 7);
+}
+
+template <int KIND, bool GATED, bool LAP1 = false, bool NOSTORE = false>
+__device__ __forceinline__ void es_run_blk(EsModel<KIND>& md, const float* __restrict__ xr, int t, int T, int t_act,
+                                           int m, _Float16* __restrict__ season, int64_t P, int64_t col, int& ph,
+                                           double& err2, int& n, SeasonInit<KIND> init, SeasonIO<_Float16> io) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  float acc = 0.f;
+  int chunk = 0;
+  auto one = [&](int tt) {
+    const int64_t si = blk_idx(ph, P, col);
+    float s = LAP1 ? init(xr[tt - m]) : io.ld(season, si);
+    if (++ph == m) ph = 0;
+    if (!(GATED && tt < t_act)) {
+      md.step(xr[tt], s, acc, n);
+      if (!NOSTORE) io.st(season, si, s);
+    }
+    if (++chunk >= 64) { err2 += acc; acc = 0.f; chunk = 0; }
+  };
+  for (; t < T && (ph & 7) != 0; ++t) one(t);            // align the phase to a block
+  h8* sv8 = reinterpret_cast<h8*>(season);
+  // Software-pipelined: chunk k+1's two season vectors and 16 samples are
+  // loaded before chunk k's 16 dependent steps run (the slots read by chunk
+  // k+1 were written m >> 32 steps earlier, never by chunk k), so the HBM
+  // latency overlaps the recursion instead of preceding it.
+  if (t + 16 <= T) {
+    h8 na = {}, nb = {};
+    float nx[16];
+    int64_t nb0, nb1;
+    auto issue = [&](int tt, int p0) {
+      int p1 = p0 + 8;
+      if (p1 >= m) p1 -= m;
+      nb0 = (int64_t)(p0 >> 3) * P + col;
+      nb1 = (int64_t)(p1 >> 3) * P + col;
+      if (!LAP1) {
+        na = sv8[nb0];
+        nb = sv8[nb1];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) nx[u] = xr[tt + u];
+    };
+    issue(t, ph);
+    for (; t + 16 <= T; t += 16) {
+      const int64_t b0 = nb0, b1 = nb1;
+      float sv[16], xv[16];
+      if (LAP1) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sv[u] = init(xr[t + u - m]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          sv[u] = (float)na[u] * io.sc;
+          sv[8 + u] = (float)nb[u] * io.sc;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) xv[u] = nx[u];
+      ph += 16;
+      if (ph >= m) ph -= m;
+      if (t + 32 <= T) issue(t + 16, ph);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if (GATED && t + u < t_act) continue;
+        md.step(xv[u], sv[u], acc, n);
+      }
+      if (!NOSTORE) {
+        h8 a, b;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          a[u] = (_Float16)__builtin_amdgcn_fmed3f(sv[u] * io.isc, -65504.f, 65504.f);
+          b[u] = (_Float16)__builtin_amdgcn_fmed3f(sv[8 + u] * io.isc, -65504.f, 65504.f);
+        }
+        sv8[b0] = a;
+        sv8[b1] = b;
+      }
+      chunk += 16;
+      if (chunk >= 64) { err2 += acc; acc = 0.f; chunk = 0; }
+    }
+  }
+  for (; t < T; ++t) one(t);
+  err2 += acc;
+}
+
 __device__ __forceinline__ int first_finite(const float* __restrict__ xr, int T) {
   int b = 0;
   while (b < T && !isfinite(xr[b])) ++b;
@@ -210,6 +299,19 @@ __device__ __forceinline__ void season_init(const float* __restrict__ xs, int i0
   for (int i = i0; i < i1; ++i) {
     const float v = xs[i < last ? i : last];   // unpredicated load, masked below
     io.st(sp, (int64_t)(i - i0) * P, i < navail ? init(v) : init(__builtin_nanf("")));
+  }
+}
+
+template <int KIND>
+__device__ __forceinline__ void season_init_blk(const float* __restrict__ xs, int ph0, int m, int navail,
+                                                SeasonInit<KIND> init, _Float16* __restrict__ season, int64_t P,
+                                                int64_t col, SeasonIO<_Float16> io) {
+  const int last = navail > 0 ? navail - 1 : 0;
+  for (int i = 0; i < m; ++i) {
+    const float v = xs[i < last ? i : last];
+    int ph = ph0 + i;
+    if (ph >= m) ph -= m;
+    io.st(season, blk_idx(ph, P, col), i < navail ? init(v) : init(__builtin_nanf("")));
   }
 }
 
@@ -269,11 +371,17 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     if (KIND >= 2) {
       // seasons written up to t_store_end (T when the fitted state is kept)
       const int ts = max(lo + m, min(t_store_end, T));
-      es_run<KIND, false, true, false, ST>(md, xr, lo, lo + m, lo, m, season, P, pid, ph, err2, n, sinit, io);
-      es_run<KIND, false, false, false, ST>(md, xr, lo + m, ts, lo, m, season, P, pid, ph, err2, n, {}, io);
-      es_run<KIND, false, false, true, ST>(md, xr, ts, T, lo, m, season, P, pid, ph, err2, n, {}, io);
+      if constexpr (sizeof(ST) == 2) {
+        es_run_blk<KIND, false, true, false>(md, xr, lo, lo + m, lo, m, season, P, pid, ph, err2, n, sinit, io);
+        es_run_blk<KIND, false, false, false>(md, xr, lo + m, ts, lo, m, season, P, pid, ph, err2, n, {}, io);
+        es_run_blk<KIND, false, false, true>(md, xr, ts, T, lo, m, season, P, pid, ph, err2, n, {}, io);
+      } else {
+        es_run<KIND, false, true, false, ST>(md, xr, lo, lo + m, lo, m, season, P, pid, ph, err2, n, sinit, io);
+        es_run<KIND, false, false, false, ST>(md, xr, lo + m, ts, lo, m, season, P, pid, ph, err2, n, {}, io);
+        es_run<KIND, false, false, true, ST>(md, xr, ts, T, lo, m, season, P, pid, ph, err2, n, {}, io);
+      }
     } else {
-      es_run<KIND, false, false, false, ST>(md, xr, lo, T, lo, m, season, P, pid, ph, err2, n, {}, io);
+      es_run<KIND, false, false, false, float>(md, xr, lo, T, lo, m, (float*)season, P, pid, ph, err2, n);
     }
   } else {
     // ragged rows in this wave: materialise the initial seasons (sample
@@ -282,10 +390,17 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     if (KIND >= 2 && base < T) {
       const int ph0 = base % m;
       const int navail = min(m, T - base);
-      season_init<KIND, ST>(xr + base, 0, m - ph0, navail, sinit, season + (int64_t)ph0 * P + pid, P, io);
-      season_init<KIND, ST>(xr + base, m - ph0, m, navail, sinit, season + pid, P, io);
+      if constexpr (sizeof(ST) == 2) {
+        season_init_blk<KIND>(xr + base, ph0, m, navail, sinit, season, P, pid, io);
+      } else {
+        season_init<KIND, ST>(xr + base, 0, m - ph0, navail, sinit, season + (int64_t)ph0 * P + pid, P, io);
+        season_init<KIND, ST>(xr + base, m - ph0, m, navail, sinit, season + pid, P, io);
+      }
     }
-    es_run<KIND, true, false, false, ST>(md, xr, lo, T, t0, m, season, P, pid, ph, err2, n, {}, io);
+    if constexpr (sizeof(ST) == 2)
+      es_run_blk<KIND, true>(md, xr, lo, T, t0, m, season, P, pid, ph, err2, n, {}, io);
+    else
+      es_run<KIND, true, false, false, ST>(md, xr, lo, T, t0, m, season, P, pid, ph, err2, n, {}, io);
   }
   // shadow lanes recompute their twin's pair in lockstep (same values, same
   // addresses) and then store no results of their own
@@ -296,6 +411,229 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
   state[pid * 3 + 1] = md.tr;
   state[pid * 3 + 2] = (float)(KIND >= 2 ? T % m : 0);
   nobs[pid] = n;
+}
+
+// ---------------------------------------------------------------------------
+// Additive Holt-Winters grid fit, packed: each THREAD runs TWO candidates of
+// one row (g = 2j, 2j+1) as float2 with v_pk_{add,mul,fma}_f32, so the
+// recursion costs ~half the VALU instructions per candidate, and the shared
+// sample is loaded, scaled and tested once.  The fit runs in row-scaled units
+// (x / sc, sc = mean |x| of the first season), so the fp16 seasonal scratch
+// is stored without per-access rescaling.  Missing samples are branch-free:
+// the sample is replaced by the prediction, which leaves level + trend
+// advancing, trend and season unchanged and adds no error (the recursion's
+// own missing-sample rule).  Scratch: blocked [m/8][R*GP][2][8] fp16.
+// ---------------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ h8v to_h8(const float* v) {
+  h8v o;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) o[u] = (_Float16)__builtin_amdgcn_fmed3f(v[u], -65504.f, 65504.f);
+  return o;
+}
+
+template <bool GATED, bool LAP1, bool NOSTORE>
+__device__ __forceinline__ void hw2_run(f2v& l, f2v& tr, const f2v al, const f2v be, const f2v ga,
+                                        const float* __restrict__ xr, float isc, float s1, int t, int T, int t_act,
+                                        int m, h8v* __restrict__ sv8, int64_t NT, int64_t tid, int& ph, f2v& acc,
+                                        double& ea, double& eb, int& n, int& chunk) {
+  auto step = [&](float xv_raw, f2v& s, bool act) {
+    const float xv = xv_raw * isc;
+    const bool fin = isfinite(xv);
+    const f2v lt = l + tr;
+    const f2v pred = lt + s;
+    const f2v xe = fin ? (f2v){xv, xv} : pred;
+    const f2v e = xe - pred;
+    const f2v ln = __builtin_elementwise_fma(al, (xe - s) - lt, lt);
+    const f2v tn = __builtin_elementwise_fma(be, (ln - l) - tr, tr);
+    const f2v sn = __builtin_elementwise_fma(ga, (xe - ln) - s, s);
+    if (!GATED || act) {
+      acc = __builtin_elementwise_fma(e, e, acc);
+      n += fin ? 1 : 0;
+      l = ln;
+      tr = tn;
+      s = sn;
+    }
+  };
+  auto flush = [&](int k) {
+    chunk += k;
+    if (chunk >= 64) { ea += acc.x; eb += acc.y; acc = (f2v){0.f, 0.f}; chunk = 0; }
+  };
+  auto one = [&](int tt) {            // single step, scalar phase access
+    const int64_t bi = ((int64_t)(ph >> 3) * NT + tid) * 16 + (ph & 7);
+    _Float16* sh = reinterpret_cast<_Float16*>(sv8);
+    f2v s;
+    if (LAP1) {
+      const float v = xr[tt - m] * isc;
+      s = (f2v){isfinite(v) ? v - s1 : 0.f, isfinite(v) ? v - s1 : 0.f};
+    } else {
+      s = (f2v){(float)sh[bi], (float)sh[bi + 8]};
+    }
+    if (++ph == m) ph = 0;
+    step(xr[tt], s, !GATED || tt >= t_act);
+    if (!NOSTORE && (!GATED || tt >= t_act)) {
+      sh[bi] = (_Float16)__builtin_amdgcn_fmed3f(s.x, -65504.f, 65504.f);
+      sh[bi + 8] = (_Float16)__builtin_amdgcn_fmed3f(s.y, -65504.f, 65504.f);
+    }
+    flush(1);
+  };
+  for (; t < T && (ph & 7) != 0; ++t) one(t);
+  for (; t + 8 <= T; t += 8) {
+    const int64_t b = ((int64_t)(ph >> 3) * NT + tid) * 2;
+    float sa[8], sb[8];
+    if (LAP1) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float v = xr[t + u - m] * isc;
+        sa[u] = sb[u] = isfinite(v) ? v - s1 : 0.f;
+      }
+    } else {
+      const h8v a = sv8[b], c = sv8[b + 1];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { sa[u] = (float)a[u]; sb[u] = (float)c[u]; }
+    }
+    float xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = xr[t + u];
+    ph += 8;
+    if (ph >= m) ph -= m;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      f2v s = {sa[u], sb[u]};
+      step(xv[u], s, !GATED || t + u >= t_act);
+      sa[u] = s.x;
+      sb[u] = s.y;
+    }
+    if (!NOSTORE) {
+      sv8[b] = to_h8(sa);
+      sv8[b + 1] = to_h8(sb);
+    }
+    flush(8);
+  }
+  for (; t < T; ++t) one(t);
+}
+
+__global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ x, int64_t ld, int T, int64_t R,
+                                                      const float* __restrict__ cand, int G, int m,
+                                                      h8v* __restrict__ season, float* __restrict__ sse,
+                                                      float* __restrict__ state, int* __restrict__ nobs,
+                                                      int t_store_end, float* __restrict__ sscale) {
+  const int GP = (G + 1) >> 1;
+  const int64_t NT = R * GP;
+  const int64_t tid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((tid_raw & ~(int64_t)63) >= NT) return;
+  const bool live = tid_raw < NT;
+  const int64_t tid = live ? tid_raw : NT - 1;
+  const int64_t row = tid / GP;
+  const int j = (int)(tid - row * GP);
+  const int ga_i = 2 * j, gb_i = 2 * j + 1 < G ? 2 * j + 1 : 2 * j;
+  const f2v al = {cand[3 * ga_i], cand[3 * gb_i]}, be = {cand[3 * ga_i + 1], cand[3 * gb_i + 1]},
+            gm = {cand[3 * ga_i + 2], cand[3 * gb_i + 2]};
+  const float* xr = x + row * ld;
+  const int base = first_finite(xr, T);
+  f2v l = {0.f, 0.f}, tr = {0.f, 0.f};
+  float sc = 1.f, s1 = 0.f;
+  int t0;
+  if (base >= T) {
+    l = (f2v){__builtin_nanf(""), __builtin_nanf("")};
+    t0 = T;
+  } else {
+    int c1, c2;
+    const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
+    float a1;
+    const float m1 = nan_mean(xr, base, e1, c1, &a1);
+    const float m2 = nan_mean(xr, e1, e2, c2);
+    sc = a1 > 1e-20f ? a1 : 1.f;
+    s1 = m1 / sc;
+    const float trend = c2 > 0 ? (m2 - m1) / sc / m : 0.f;
+    l = (f2v){s1, s1};
+    tr = (f2v){trend, trend};
+    t0 = base + m;
+  }
+  const float isc = 1.f / sc;
+  f2v acc = {0.f, 0.f};
+  double ea = 0.0, eb = 0.0;
+  int n = 0, chunk = 0;
+  const int lo = __builtin_amdgcn_readfirstlane(wave_min(t0));
+  const int hi = __builtin_amdgcn_readfirstlane(wave_max(t0));
+  int ph = lo % m;
+  if (lo == hi && lo + m <= T) {
+    const int ts = max(lo + m, min(t_store_end, T));
+    hw2_run<false, true, false>(l, tr, al, be, gm, xr, isc, s1, lo, lo + m, lo, m, season, NT, tid, ph, acc, ea, eb, n,
+                                chunk);
+    hw2_run<false, false, false>(l, tr, al, be, gm, xr, isc, s1, lo + m, ts, lo, m, season, NT, tid, ph, acc, ea, eb,
+                                 n, chunk);
+    hw2_run<false, false, true>(l, tr, al, be, gm, xr, isc, s1, ts, T, lo, m, season, NT, tid, ph, acc, ea, eb, n,
+                                chunk);
+  } else {
+    // ragged rows in this wave: materialise each row's initial seasons, then
+    // run with per-lane start gating
+    if (base < T) {
+      _Float16* sh = reinterpret_cast<_Float16*>(season);
+      const int navail = min(m, T - base);
+      for (int i = 0; i < m; ++i) {
+        const float v = i < navail ? xr[base + i] * isc : __builtin_nanf("");
+        const float si = isfinite(v) ? v - s1 : 0.f;
+        const int p = (base + i) % m;
+        const int64_t bi = ((int64_t)(p >> 3) * NT + tid) * 16 + (p & 7);
+        sh[bi] = sh[bi + 8] = (_Float16)__builtin_amdgcn_fmed3f(si, -65504.f, 65504.f);
+      }
+    }
+    hw2_run<true, false, false>(l, tr, al, be, gm, xr, isc, s1, lo, T, t0, m, season, NT, tid, ph, acc, ea, eb, n,
+                                chunk);
+  }
+  ea += acc.x;
+  eb += acc.y;
+  if (!live) return;
+  const float s2 = sc * sc;
+  const int64_t pa = row * G + ga_i;
+  sse[pa] = (float)(ea * s2);
+  state[pa * 3 + 0] = l.x * sc;
+  state[pa * 3 + 1] = tr.x * sc;
+  state[pa * 3 + 2] = (float)(T % m);
+  nobs[pa] = n;
+  if (2 * j + 1 < G) {
+    const int64_t pb = pa + 1;
+    sse[pb] = (float)(eb * s2);
+    state[pb * 3 + 0] = l.y * sc;
+    state[pb * 3 + 1] = tr.y * sc;
+    state[pb * 3 + 2] = (float)(T % m);
+    nobs[pb] = n;
+  }
+  if (j == 0) sscale[row] = sc;
+}
+
+__global__ __launch_bounds__(256) void hw2_forecast_kernel(const float* __restrict__ sse,
+                                                           const float* __restrict__ state,
+                                                           const int* __restrict__ nobs,
+                                                           const _Float16* __restrict__ season,
+                                                           const float* __restrict__ sscale, int64_t R, int G, int m,
+                                                           int H, float* __restrict__ fc, float* __restrict__ sigma,
+                                                           int* __restrict__ best) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= R) return;
+  const int GP = (G + 1) >> 1;
+  const int64_t NT = R * GP;
+  int bg = 0;
+  float bs = sse[row * G];
+  for (int g = 1; g < G; ++g) {
+    const float v = sse[row * G + g];
+    if (v < bs || !isfinite(bs)) { bs = v; bg = g; }
+  }
+  const int64_t pid = row * G + bg;
+  const int64_t tid = row * GP + (bg >> 1);
+  const float lvl = state[pid * 3 + 0], tr = state[pid * 3 + 1], sc = sscale[row];
+  const int tph = (int)state[pid * 3 + 2];
+  const int n = nobs[pid];
+  sigma[row] = n > 1 ? sqrtf(bs / (float)(n - 1)) : 0.f;
+  best[row] = bg;
+  for (int h = 1; h <= H; ++h) {
+    const int p = (tph + h - 1) % m;
+    const float sv = (float)season[((int64_t)(p >> 3) * NT + tid) * 16 + (bg & 1) * 8 + (p & 7)] * sc;
+    fc[row * H + (h - 1)] = lvl + h * tr + sv;
+  }
 }
 
 // Incremental update of cached models, in place in the cache's slab: row r
@@ -368,7 +706,8 @@ __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restric
   for (int h = 1; h <= H; ++h) {
     float f = lvl + (kind >= 1 ? h * tr : 0.f);
     if (kind >= 2) {
-      const float s = (float)season[(int64_t)((tph + h - 1) % m) * P + pid] * sscale[row];
+      const int sp = (tph + h - 1) % m;
+      const float s = (float)season[sizeof(ST) == 2 ? blk_idx(sp, P, pid) : (int64_t)sp * P + pid] * sscale[row];
       f = kind == 3 ? f * s : f + s;
     }
     fc[row * H + (h - 1)] = f;
@@ -393,8 +732,9 @@ __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restric
 // keep_season = 0: only the seasonal indices the H-step forecast reads are
 // guaranteed in `season` afterwards (saves one store pass); 1: all of them
 // (the caller extracts the fitted state, e.g. for the model cache).
-// season_half = 1: the season scratch is fp16 [m][R*G] (scaled per row, the
-// scale written to sscale[R]); 0: fp32 (sscale[R] = 1).
+// season_half = 1 (additive, m % 8 == 0): packed two-candidate kernel with
+// an fp16 season scratch blocked [m/8][R*ceil(G/2)][2][8] in row-scaled units
+// (the scale written to sscale[R]); 0: fp32 [m][R*G] (sscale[R] = 1).
 FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int kind,
                      void* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma, int* best,
                      int keep_season, int season_half, float* sscale, hipStream_t stream) {
@@ -402,16 +742,19 @@ FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* 
   if (kind < 0 || kind > 3) return (int)hipErrorInvalidValue;
   if (kind >= 2 && (m < 2 || 2 * m > T)) return (int)hipErrorInvalidValue;
   if (kind < 2 && T < 2) return (int)hipErrorInvalidValue;
+  if (season_half && (kind != 2 || m % 8 != 0)) return (int)hipErrorInvalidValue;   // blocked fp16 layout
   if (kind < 2) m = 1;
   const int64_t P = R * G;
   const int t_store_end = keep_season || kind < 2 || H >= m ? T : T - m + H;
   const dim3 gf((unsigned)((P + 255) / 256)), gr((unsigned)((R + 255) / 256));
   if (season_half) {
-    FM_ES_DISPATCH_T(es_fit_kernel, _Float16, gf, x, ld, T, R, cand, G, m, (_Float16*)season, sse, state, nobs,
-                     t_store_end, sscale);
+    // packed two-candidates-per-thread additive fit (hw2_fit_kernel)
+    const int64_t NT = R * ((G + 1) / 2);
+    hipLaunchKernelGGL(hw2_fit_kernel, dim3((unsigned)((NT + 255) / 256)), dim3(256), 0, stream, x, ld, T, R, cand, G,
+                       m, (h8v*)season, sse, state, nobs, t_store_end, sscale);
     FM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(es_forecast_kernel<_Float16>, gr, dim3(256), 0, stream, sse, state, nobs,
-                       (const _Float16*)season, sscale, R, G, m, kind, H, fc, sigma, best);
+    hipLaunchKernelGGL(hw2_forecast_kernel, gr, dim3(256), 0, stream, sse, state, nobs, (const _Float16*)season,
+                       sscale, R, G, m, H, fc, sigma, best);
   } else {
     FM_ES_DISPATCH_T(es_fit_kernel, float, gf, x, ld, T, R, cand, G, m, (float*)season, sse, state, nobs, t_store_end,
                      sscale);

@@ -95,8 +95,11 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     # (their scratch is L2-resident anyway)
     # multiplicative indices (~1, multiplying the level) keep fp32: fp16's 2^-11
     # relative step moved their SSEs by up to 5 % on the oracle set
-    half = bool(half_season) and kind == 2 and m >= HALF_SEASON_MIN_M
-    season = torch.empty((m if kind >= 2 else 1, P), dtype=torch.float16 if half else torch.float32, device=d)
+    half = bool(half_season) and kind == 2 and m >= HALF_SEASON_MIN_M and m % 8 == 0
+    # fp16 scratch (packed 2-candidate kernel): [m/8][R * ceil(G/2)][2 candidates][8 phases]
+    GP = (G + 1) // 2
+    season = (torch.empty((m // 8, R * GP, 16), dtype=torch.float16, device=d) if half else
+              torch.empty((m if kind >= 2 else 1, P), dtype=torch.float32, device=d))
     sscale = torch.empty((R,), dtype=torch.float32, device=d)
     sse = torch.empty((R, G), dtype=torch.float32, device=d)
     state = torch.empty((P, 3), dtype=torch.float32, device=d)
@@ -111,9 +114,21 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
         b = best.long()
         pid = torch.arange(R, device=d) * G + b
         model = ESState(kind, m, cand[b].contiguous(), state[pid].contiguous(),
-                        (season[:, pid].t().float() * sscale[:, None]).contiguous() if kind >= 2 else None,
+                        _half_season_of(season, b, R, GP, m, sscale) if half else
+                        (season[:, pid].t().contiguous() if kind >= 2 else None),
                         sse.gather(1, b[:, None])[:, 0].contiguous(), nobs[pid].contiguous())
     return ESFit(fc, sig, best, sse, model)
+
+
+def _half_season_of(season: torch.Tensor, best: torch.Tensor, R: int, GP: int, m: int,
+                    sscale: torch.Tensor) -> torch.Tensor:
+    """The best candidate's seasonal indices [R, m] (data units) out of the
+    packed fp16 scratch [m/8][R*GP][2][8]."""
+    tid = torch.arange(R, device=season.device) * GP + best // 2
+    half = (best % 2)[None, :, None] * 8 + torch.arange(8, device=season.device)[None, None, :]
+    blk = season[:, tid, :]                                          # [m/8, R, 16]
+    sel = blk.gather(2, half.expand(blk.shape[0], -1, -1))           # [m/8, R, 8]
+    return (sel.permute(1, 0, 2).reshape(R, m).float() * sscale[:, None]).contiguous()
 
 
 def es_update(x: torch.Tensor, T: int, t_new: torch.Tensor, model: ESState, H: int,
