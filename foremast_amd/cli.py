@@ -11,6 +11,7 @@ process of the framework plus the operator-facing commands.
   manifests   write the deploy bundle
   validate F  check DeploymentMonitor/DeploymentMetadata YAML against the CRD schema
   demo        fault-injection demo workload (examples/spring-boot-demo analogue)
+  sidecar     metrics reverse-proxy sidecar: foremast-metrics series for any app (JVM included)
 """
 from __future__ import annotations
 
@@ -121,6 +122,10 @@ def main(argv=None) -> int:
     if cmd == "trigger":
         from .trigger import trigger
         trigger.main()
+        return 0
+    if cmd == "sidecar":
+        from .emitter import sidecar
+        sidecar.main(rest)
         return 0
     if cmd == "demo":
         from .demo import app as demo
