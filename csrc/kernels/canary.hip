@@ -1079,7 +1079,7 @@ __device__ unsigned long long g_front_t[2 * 8192];
 #define FM_FT_MARK(k) do {} while (0)
 #endif
 
-template <int NV, int K>
+template <int NV, int K, bool PRIO = false>
 __global__ __launch_bounds__(256) void tick_front_kernel(
     const float* __restrict__ hist, int64_t ld_h, int T, int64_t R, float* __restrict__ hs /*[R,3]*/,
     const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
@@ -1090,6 +1090,7 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
   __shared__ int redi[4];
   FM_FT_MARK(0);
   if ((int)blockIdx.x < nP) {
+    if (PRIO) __builtin_amdgcn_s_setprio(2);
     const int64_t first = (int64_t)blockIdx.x * 4, stride = (int64_t)nP * 4;
     for (int64_t row = first + wave_id(); row < R; row += stride) {
       pw_row<K>(cur + row * ld_c, base + row * ld_b, n_cur, n_base, suff + row * kSuff);
@@ -1117,6 +1118,9 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
     return;
   }
   const int nH = (int)gridDim.x - nP;
+  // PRIO: the co-resident pairwise waves issue ahead of the history waves
+  // (history first measured 0.64-0.66 vs 0.53-0.56 ms per step: worse)
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
   if (queue == nullptr) {
     for (int64_t row = (int64_t)blockIdx.x - nP; row < R; row += nH) {
       float mf, sd;
@@ -1185,6 +1189,16 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
   FM_FT_MARK(1);
 }
 
+// FM_FRONT_PRIO=1 (environment, read once): A/B of wave priorities in the
+// front kernel (tools: bench.py with and without it on one box).
+static bool front_prio() {
+  static const bool on = [] {
+    const char* e = getenv("FM_FRONT_PRIO");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 // nP / nH: workgroups of each role (0 = one pairwise workgroup per 4 rows /
 // one history workgroup per row); queue: dynamic history rows (or nullptr).
 FM_API int fm_tick_front_rm(const float* hist, int64_t ld_h, int T, int64_t R, float* hs, const float* cur,
@@ -1204,6 +1218,10 @@ FM_API int fm_tick_front_rm(const float* hist, int64_t ld_h, int T, int64_t R, f
   const int nq = (T + 3) / 4;
   const dim3 grid((unsigned)(nP + nH)), block(256);
 #define FM_TF(NVV, KK)                                                                                             \
+  if (front_prio())                                                                                                 \
+    hipLaunchKernelGGL((tick_front_kernel<NVV, KK, true>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c,  \
+                       n_cur, base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap); \
+  else                                                                                                               \
   hipLaunchKernelGGL((tick_front_kernel<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c, n_cur, \
                      base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap)
 #define FM_TF_K(NVV)           \
