@@ -77,6 +77,11 @@ class BrainConfig:
     # load forecast published for HPA jobs (cluster-autoscaler prediction)
     hpa_forecast_algorithm: str = "double_exponential_smoothing"   # HPA_FORECAST_ALGORITHM ("" disables)
     hpa_forecast_steps: int = 15                                    # HPA_FORECAST_STEPS (60 s samples)
+    # LSTM model (ML_ALGORITHM=lstm, docs/guides/design.md:81-85)
+    lstm_hidden: int = 128                 # LSTM_HIDDEN: 32 | 64 | 128 | 256
+    lstm_layers: int = 1                   # LSTM_LAYERS: 1 | 2
+    lstm_multivariate: int = 0             # LSTM_MULTIVARIATE: M > 0 = one sequence per job over its M metrics
+    lstm_window: int = 240                 # LSTM_WINDOW (lookback samples)
     # downstream impact (README.md:24,27; the judgement diagram's "app or app
     # downstream" branch): caller -> callee edges from the ``caller``-tagged
     # request series (recording rule namespace_app_caller[_uri]_http_server_requests_rate)
@@ -140,6 +145,10 @@ class BrainConfig:
         c.hpa_breath_down = _f(env, "HPA_BREATH_DOWN_SECONDS", c.hpa_breath_down)
         c.hpa_forecast_algorithm = env.get("HPA_FORECAST_ALGORITHM", c.hpa_forecast_algorithm)
         c.hpa_forecast_steps = _i(env, "HPA_FORECAST_STEPS", c.hpa_forecast_steps)
+        c.lstm_hidden = _i(env, "LSTM_HIDDEN", c.lstm_hidden)
+        c.lstm_layers = _i(env, "LSTM_LAYERS", c.lstm_layers)
+        c.lstm_multivariate = _i(env, "LSTM_MULTIVARIATE", c.lstm_multivariate)
+        c.lstm_window = _i(env, "LSTM_WINDOW", c.lstm_window)
         c.downstream_edges_url = env.get("DOWNSTREAM_EDGES_URL", c.downstream_edges_url)
         c.downstream_edges_store = env.get("DOWNSTREAM_EDGES_STORE", c.downstream_edges_store) or "prometheus"
         c.downstream_mode = env.get("DOWNSTREAM_IMPACT_MODE", c.downstream_mode) or c.downstream_mode

@@ -127,6 +127,7 @@ class Brain:
         self.history_s = history_days * 86400.0
         self.fetch_threads = fetch_threads
         self.lstm_model = lstm_model
+        self._lstm_uni = None         # univariate fallback next to a multivariate model
         from ..models.cache import ModelCache
         self.model_cache = ModelCache(self.cfg.max_cache_size, self.cfg.model_refit_seconds)
         self.info = D.env_info() if D.is_dist() else D.DistInfo()
@@ -252,7 +253,8 @@ class Brain:
         if len(groups) == 1:
             algo = algos[0]
             pairs = self._pairs(rows) if algo == "bivariate_normal" else None
-            dec = zoo.decide(algo, hist, T, cur, hor, R, tables, diff, lstm_model=self.lstm_model,
+            dec = zoo.decide(algo, hist, T, cur, hor, R, tables, diff,
+                             lstm_model=self._lstm_for(rows) if algo == "lstm" else self.lstm_model,
                              pairs=pairs, cache=self._cache_ctx(rows, algo))
             out = {k: getattr(dec, k).detach().cpu().numpy() for k in keys}
             flags = dec.flags
@@ -265,7 +267,8 @@ class Brain:
                 dec = zoo.decide(algo, hist.index_select(0, it).contiguous(), T, cur.index_select(0, it).contiguous(),
                                  hor.index_select(0, it), len(idx),
                                  zoo.make_tables([r.alias for r in sub], self.cfg, self.device),
-                                 None if diff is None else diff.index_select(0, it), lstm_model=self.lstm_model,
+                                 None if diff is None else diff.index_select(0, it),
+                                 lstm_model=self._lstm_for(sub) if algo == "lstm" else self.lstm_model,
                                  pairs=pairs, cache=self._cache_ctx(sub, algo))
                 for k in keys:
                     v = getattr(dec, k).detach()
@@ -282,6 +285,35 @@ class Brain:
         out["flags"] = C.unpack_flags(flags, cur.shape[1])
         out["diff"] = None if diff is None else diff.cpu().numpy()
         return out
+
+    def _lstm_model(self):
+        """The configured forecaster (LSTM_HIDDEN / LSTM_LAYERS / LSTM_MULTIVARIATE),
+        built once on the brain's device."""
+        if self.lstm_model is None:
+            from ..models.lstm import LSTMForecaster
+            c = self.cfg
+            self.lstm_model = LSTMForecaster(hidden=c.lstm_hidden, window=c.lstm_window, horizon=60,
+                                             layers=c.lstm_layers, n_metrics=c.lstm_multivariate or None,
+                                             device=self.device)
+        return self.lstm_model
+
+    def _lstm_for(self, rows: list[Row]):
+        """A multivariate model scores a batch whose rows are whole jobs of
+        exactly its M metrics (one sequence per job); any other batch uses a
+        univariate forecaster of the same size."""
+        m = self._lstm_model()
+        if m.M is None:
+            return m
+        counts: dict[int, int] = {}
+        for r in rows:
+            counts[r.job] = counts.get(r.job, 0) + 1
+        if all(v == m.M for v in counts.values()):
+            return m
+        if self._lstm_uni is None:
+            from ..models.lstm import LSTMForecaster
+            self._lstm_uni = LSTMForecaster(hidden=m.H, window=m.L, horizon=m.horizon, layers=m.layers,
+                                            device=self.device)
+        return self._lstm_uni
 
     def _cache_ctx(self, rows: list[Row], algorithm: str) -> "zoo.CacheContext | None":
         if self.model_cache.capacity <= 0 or zoo.canonical(algorithm) not in zoo.ES_KINDS:

@@ -368,3 +368,31 @@ def test_downstream_annotate_mode_keeps_healthy_callers():
     brain.run_once()
     assert store.get(ids["ledger"]).status == "completed_unhealth"
     assert store.get(ids["frontend"]).status != "completed_unhealth"
+
+
+def test_brain_lstm_multivariate_model():
+    """LSTM_MULTIVARIATE=M: jobs with exactly M metrics are forecast as one
+    sequence per job over all their metrics (2 stacked layers here); a batch
+    holding a job with another metric count falls back to a univariate model."""
+    env = {"ML_ALGORITHM": "lstm", "LSTM_HIDDEN": "32", "LSTM_LAYERS": "2", "LSTM_MULTIVARIATE": "3",
+           "LSTM_WINDOW": "60"}
+    cfg = BrainConfig.from_env(env)
+    clock = Clock()
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    brain = Brain(store, cfg, sources=SourceRouter.synthetic_only(faults={"7687b9f4d7-aaaa1": 8.0},
+                                                                  fault_after=T0 - 900),
+                  clock=clock, worker_id="w0", resident_history=False)
+    client.start_analyzing("default", "demo", PODS, _metrics(), 10, "canary")
+    r = brain.run_once()
+    assert r["claimed"] == 1
+    m = brain.lstm_model
+    assert m.M == 3 and m.layers == 2 and m.H == 32 and brain._lstm_uni is None
+    two = crd.Metrics("prometheus", "http://prom/api/v1/", _metrics().monitoring[:2])
+    client.start_analyzing("default", "other", [["other-7687b9f4d7-cccc1"], ["other-5db89899b5-dddd1"]], two, 10,
+                           "canary")
+    client.start_analyzing("default", "third", [["third-7687b9f4d7-eeee1"], ["third-5db89899b5-ffff1"]],
+                           _metrics(), 10, "canary")
+    clock.t += 30
+    r = brain.run_once()
+    assert r["claimed"] >= 2 and brain._lstm_uni is not None and brain._lstm_uni.M is None
