@@ -1,18 +1,38 @@
 // K3: FFT seasonal analysis.  Real input of length Nr is packed into a
 // complex sequence of N = Nr/2 points (z_j = x_2j + i x_2j+1), transformed by a
-// mixed-radix Stockham FFT (radices 4,2,9,3,5,7) that lives entirely in LDS
+// mixed-radix Stockham FFT (radices 2,3,4,5,7,9) that lives entirely in LDS
 // (one 256-thread workgroup per series; N <= 8192 complex = 64 KB), then
 // unpacked to the one-sided real spectrum.  The periodogram peak in a
 // [kmin, kmax] band gives the dominant seasonal period (docs/dynamic_autoscaling.md:5-30,
 // "Determine TPS seasonality & trend").
 //
-// 10,080 = 7 days at 60 s (metricsquery.go:93-97) -> N = 5040 = 4*4*9*5*7:
+// 10,080 = 7 days at 60 s (metricsquery.go:93-97) -> N = 5040 = 7*4*9*4*5:
 // five passes, no zero padding, so the spectral resolution is exactly 1/week.
+//
+// CDNA4 shape of the work (r2):
+//   * the common lengths (N = 5040 / 1008 / 720: 7 days at 1 min / 5 min,
+//     1 day at 1 min) run a compile-time plan: every pass's stride, butterfly
+//     count and the j / Ns division are constants, no per-pass dispatch;
+//   * the radix order starts with an odd radix, then alternates 4 with the
+//     rest (7,4,9,4,5): the self-sorting writes of an early radix-4 pass are
+//     8-dword strided (4-way LDS bank conflicts on ds_write_b64), an odd
+//     stride spreads over all banks -- a bank model of every pass puts the
+//     order at 1.10x the conflict-free LDS cycles, vs 1.57x for 4,4,9,5,7;
+//   * butterflies are packed-fp32 (float2 ext vectors -> v_pk_fma/add/mul_f32)
+//     and odd radices use the conjugate-pair form (outputs p and R-p share
+//     one set of products): a radix-7 butterfly is ~33 packed ops, not the
+//     168 scalar FMAs of the textbook O(R^2) sum;
+//   * the total power for the strength ratio comes from Parseval over the
+//     detrended samples (sum e^2, X_0, X_N, accumulated while the row is
+//     written to LDS), so only the [kmin, kmax] band is unpacked unless the
+//     caller asked for the whole periodogram.
 #include "fm_common.h"
 
 using namespace fm;
 
 namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int R> struct RootTable;
 template <> struct RootTable<3> {
@@ -32,37 +52,48 @@ template <> struct RootTable<9> {
   static constexpr float s[9] = {0.00000000000000000e+00f, 6.42787609686539252e-01f, 9.84807753012208020e-01f, 8.66025403784438708e-01f, 3.42020143325668879e-01f, -3.42020143325668657e-01f, -8.66025403784438375e-01f, -9.84807753012208131e-01f, -6.42787609686539585e-01f};
 };
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ f2 cmul(f2 a, f2 b) { return a.xx * b + a.yy * (f2){-b.y, b.x}; }
+__device__ __forceinline__ f2 neg_i(f2 a) { return (f2){a.y, -a.x}; }   // -i a
 
 // forward DFT (W = e^{-2 pi i / R}) of R points in registers
 template <int R>
-__device__ __forceinline__ void dft(float2 (&v)[R]) {
+__device__ __forceinline__ void dft(f2 (&v)[R]) {
   if constexpr (R == 2) {
-    float2 a = v[0], b = v[1];
-    v[0] = cadd(a, b); v[1] = csub(a, b);
+    const f2 a = v[0], b = v[1];
+    v[0] = a + b;
+    v[1] = a - b;
   } else if constexpr (R == 4) {
-    const float2 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
-    const float2 s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
-    v[0] = cadd(s02, s13);
-    v[2] = csub(s02, s13);
-    v[1] = make_float2(d02.x + d13.y, d02.y - d13.x);   // d02 - i d13
-    v[3] = make_float2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
+    const f2 s02 = v[0] + v[2], d02 = v[0] - v[2], s13 = v[1] + v[3], d13 = neg_i(v[1] - v[3]);
+    v[0] = s02 + s13;
+    v[2] = s02 - s13;
+    v[1] = d02 + d13;
+    v[3] = d02 - d13;
   } else {
-    float2 o[R];
+    // conjugate pairs: X_p = v0 + sum_q c_pq S_q - i sum_q s_pq D_q,
+    // X_{R-p} = v0 + sum_q c_pq S_q + i sum_q s_pq D_q  (q = 1..(R-1)/2)
+    constexpr int H = (R - 1) / 2;
+    f2 S[H], D[H];
+    f2 x0 = v[0];
 #pragma unroll
-    for (int p = 0; p < R; ++p) {
-      float2 acc = v[0];
+    for (int q = 1; q <= H; ++q) {
+      S[q - 1] = v[q] + v[R - q];
+      D[q - 1] = v[q] - v[R - q];
+      x0 += S[q - 1];
+    }
+    f2 o[R];
+    o[0] = x0;
 #pragma unroll
-      for (int q = 1; q < R; ++q) {
+    for (int p = 1; p <= H; ++p) {
+      f2 A = v[0], B = (f2){0.f, 0.f};
+#pragma unroll
+      for (int q = 1; q <= H; ++q) {
         const int m = (p * q) % R;
-        const float c = RootTable<R>::c[m], s = RootTable<R>::s[m];
-        // v[q] * (c - i s)
-        acc.x += v[q].x * c + v[q].y * s;
-        acc.y += v[q].y * c - v[q].x * s;
+        A += RootTable<R>::c[m] * S[q - 1];
+        B += RootTable<R>::s[m] * D[q - 1];
       }
-      o[p] = acc;
+      const f2 t = neg_i(B);
+      o[p] = A + t;
+      o[R - p] = A - t;
     }
 #pragma unroll
     for (int p = 0; p < R; ++p) v[p] = o[p];
@@ -72,31 +103,72 @@ __device__ __forceinline__ void dft(float2 (&v)[R]) {
 constexpr int kMaxN = 8192;
 constexpr int kThreads = 256;
 
+// Twiddles w^q, q = 0..R-1, for w = exp(2 pi i r), r in revolutions (v_sin_f32
+// / v_cos_f32 take revolutions, so r is the exact fraction -m / N); the
+// powers by complex products (R <= 9: a few ulps) instead of R-1 gathers.
+template <int R>
+__device__ __forceinline__ void twiddles(float r, f2 (&w)[R]) {
+  w[0] = (f2){1.f, 0.f};
+  w[1] = (f2){__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r)};
+#pragma unroll
+  for (int q = 2; q < R; ++q) w[q] = cmul(w[q - 1], w[1]);
+}
+
+// One Stockham pass, compile-time N / R / Ns.
+template <int N, int R, int Ns>
+__device__ __forceinline__ void pass_ct(f2* buf) {
+  constexpr int nb = N / R;
+  constexpr int MAXB = (nb + kThreads - 1) / kThreads;
+  constexpr float inv = -1.f / (float)(Ns * R);
+  f2 v[MAXB][R];
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) {
+    const int j = threadIdx.x + b * kThreads;
+    if ((b + 1) * kThreads <= nb || j < nb) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) v[b][q] = buf[j + q * nb];
+      if constexpr (Ns > 1) {
+        f2 w[R];
+        twiddles<R>((float)(j % Ns) * inv, w);
+#pragma unroll
+        for (int q = 1; q < R; ++q) v[b][q] = cmul(v[b][q], w[q]);
+      }
+      dft<R>(v[b]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b) {
+    const int j = threadIdx.x + b * kThreads;
+    if ((b + 1) * kThreads <= nb || j < nb) {
+      const int g = j / Ns, k = j - g * Ns;
+      const int base = g * Ns * R + k;
+#pragma unroll
+      for (int p = 0; p < R; ++p) buf[base + p * Ns] = v[b][p];
+    }
+  }
+  __syncthreads();
+}
+
+template <int N, int Ns, int R, int... Rest>
+__device__ __forceinline__ void passes_ct(f2* buf) {
+  pass_ct<N, R, Ns>(buf);
+  if constexpr (sizeof...(Rest) > 0) passes_ct<N, Ns * R, Rest...>(buf);
+}
+
 // j / Ns and j % Ns by a multiply-high with a per-pass magic number (exact
 // for j, Ns < 2^13: the 32-bit reciprocal's error times j stays below one
 // part in 2^19, less than the smallest fractional part 1/Ns).
 __device__ __forceinline__ int div_magic(int j, unsigned magic) { return (int)__umulhi((unsigned)j, magic); }
 
-// Twiddle w^q, q = 1..R-1, for w = exp(-2 pi i m / N): w from the hardware
-// sine / cosine (v_sin_f32 / v_cos_f32 take revolutions, so the argument is
-// the exact fraction m / N), the powers by complex products (R <= 9: a few
-// ulps) instead of R-1 gathers from a global table.
-template <int R>
-__device__ __forceinline__ void twiddles(int m, float invN, float2 (&w)[R]) {
-  const float r = -(float)m * invN;
-  w[0] = make_float2(1.f, 0.f);
-  w[1] = make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
-#pragma unroll
-  for (int q = 2; q < R; ++q) w[q] = cmul(w[q - 1], w[1]);
-}
-
+// One Stockham pass with a run-time plan (lengths without a fixed plan).
 template <int R, int MAXN>
-__device__ __forceinline__ void stockham_pass(float2* buf, int N, int Ns, float invN) {
+__device__ __forceinline__ void stockham_pass(f2* buf, int N, int Ns) {
   constexpr int MAXB = (MAXN / R + kThreads - 1) / kThreads;
   const int nb = N / R;
-  const int step = N / (Ns * R);
+  const float inv = -1.f / (float)(Ns * R);
   const unsigned magic = 0xFFFFFFFFu / (unsigned)Ns + 1u;   // scalar
-  float2 v[MAXB][R];
+  f2 v[MAXB][R];
 #pragma unroll
   for (int b = 0; b < MAXB; ++b) {
     const int j = threadIdx.x + b * kThreads;
@@ -105,8 +177,8 @@ __device__ __forceinline__ void stockham_pass(float2* buf, int N, int Ns, float 
 #pragma unroll
       for (int q = 0; q < R; ++q) v[b][q] = buf[j + q * nb];
       if (k > 0) {
-        float2 w[R];
-        twiddles<R>(k * step, invN, w);
+        f2 w[R];
+        twiddles<R>((float)k * inv, w);
 #pragma unroll
         for (int q = 1; q < R; ++q) v[b][q] = cmul(v[b][q], w[q]);
       }
@@ -128,6 +200,20 @@ __device__ __forceinline__ void stockham_pass(float2* buf, int N, int Ns, float 
   __syncthreads();
 }
 
+template <int FN> struct FixedPlan { static constexpr bool ok = false; };
+template <> struct FixedPlan<5040> {
+  static constexpr bool ok = true;
+  static __device__ __forceinline__ void run(f2* b) { passes_ct<5040, 1, 7, 4, 9, 4, 5>(b); }
+};
+template <> struct FixedPlan<1008> {
+  static constexpr bool ok = true;
+  static __device__ __forceinline__ void run(f2* b) { passes_ct<1008, 1, 7, 4, 9, 4>(b); }
+};
+template <> struct FixedPlan<720> {
+  static constexpr bool ok = true;
+  static __device__ __forceinline__ void run(f2* b) { passes_ct<720, 1, 5, 4, 9, 4>(b); }
+};
+
 }  // namespace
 
 struct FftPlan {
@@ -135,118 +221,133 @@ struct FftPlan {
   int radix[16];
 };
 
-// MAXN: compile-time bound on N (register arrays are sized by it; the
-// 7-day series has N = 5040 and runs the 5120 variant at 4 workgroups/CU).
-template <int MAXN>
+// MAXN: compile-time bound on N (register arrays are sized by it); FN: the
+// compile-time N of a fixed plan (0: the run-time plan in `plan`).
+template <int MAXN, int FN>
 __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
     const float* __restrict__ x, int64_t ld, int Nr, int64_t R, const float2* __restrict__ tw,
     const float2* __restrict__ tw2, FftPlan plan, int kmin, int kmax, float* __restrict__ power, int64_t ld_p,
     float2* __restrict__ spec, int64_t ld_s, int* __restrict__ period_bin, float* __restrict__ strength,
     float* __restrict__ mean_out, float* __restrict__ slope_out) {
-  extern __shared__ __attribute__((aligned(16))) float2 buf[];
+  extern __shared__ __attribute__((aligned(16))) f2 buf[];
   (void)tw;   // twiddles are computed in-kernel (kept in the C ABI)
-  __shared__ float redf[8];
-  __shared__ int redi[8];
+  __shared__ float redf[6][kThreads / 64];
+  __shared__ int redi[kThreads / 64];
+  __shared__ double red5[5][kThreads / 64];
   const int64_t row = blockIdx.x;
-  const int N = Nr >> 1;
+  const int N = FN > 0 ? FN : Nr >> 1;
   const float* xr = x + row * ld;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wv = wave_id();
   // The row is read ONCE: its complex pairs z_j = (x_2j, x_2j+1) go to
   // registers (all loads issued up front), the least-squares linear detrend
   // sums over finite samples are taken from there, and the detrended values
   // are written to LDS.  (NaN -> trend line, so a slow trend does not leak
-  // into the low-frequency bins.)
+  // into the low-frequency bins.)  Per-thread partials in fp32 over centred
+  // time (t - (Nr-1)/2: |t| <= Nr/2, 40 terms), the cross-lane sums in fp64.
   constexpr int NPT = MAXN / kThreads;        // complex values per thread
-  float2 z[NPT];
+  f2 z[NPT];
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const int j = tid + i * kThreads;
-    z[i] = j < N ? reinterpret_cast<const float2*>(xr)[j] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
+    z[i] = j < N ? reinterpret_cast<const f2*>(xr)[j] : (f2){__builtin_nanf(""), __builtin_nanf("")};
   }
-  double s = 0.0, st = 0.0, stt = 0.0, sx = 0.0, c = 0.0;
+  const float tmid = 0.5f * (float)(Nr - 1);
+  float s = 0.f, st = 0.f, stt = 0.f, sx = 0.f, c = 0.f;
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
-    const double t0 = 2.0 * (tid + i * kThreads);
-    if (isfinite(z[i].x)) { s += z[i].x; st += t0; stt += t0 * t0; sx += t0 * z[i].x; c += 1.0; }
-    if (isfinite(z[i].y)) { const double t1 = t0 + 1.0; s += z[i].y; st += t1; stt += t1 * t1; sx += t1 * z[i].y; c += 1.0; }
+    const float t0 = (float)(2 * (tid + i * kThreads)) - tmid;
+    if (isfinite(z[i].x)) { s += z[i].x; st += t0; stt += t0 * t0; sx += t0 * z[i].x; c += 1.f; }
+    if (isfinite(z[i].y)) { const float t1 = t0 + 1.f; s += z[i].y; st += t1; stt += t1 * t1; sx += t1 * z[i].y; c += 1.f; }
   }
-  // the five block sums in one LDS round trip
-  __shared__ double red5[5][kThreads / 64];
-  s = wave_sum(s); st = wave_sum(st); stt = wave_sum(stt); sx = wave_sum(sx); c = wave_sum(c);
-  if (lane_id() == 0) {
-    red5[0][wave_id()] = s; red5[1][wave_id()] = st; red5[2][wave_id()] = stt; red5[3][wave_id()] = sx;
-    red5[4][wave_id()] = c;
-  }
+  double ds = wave_sum((double)s), dst = wave_sum((double)st), dstt = wave_sum((double)stt),
+         dsx = wave_sum((double)sx), dc = wave_sum((double)c);
+  if (lane_id() == 0) { red5[0][wv] = ds; red5[1][wv] = dst; red5[2][wv] = dstt; red5[3][wv] = dsx; red5[4][wv] = dc; }
   __syncthreads();
-  s = st = stt = sx = c = 0.0;
+  ds = dst = dstt = dsx = dc = 0.0;
 #pragma unroll
   for (int w = 0; w < kThreads / 64; ++w) {
-    s += red5[0][w]; st += red5[1][w]; stt += red5[2][w]; sx += red5[3][w]; c += red5[4][w];
+    ds += red5[0][w]; dst += red5[1][w]; dstt += red5[2][w]; dsx += red5[3][w]; dc += red5[4][w];
   }
-  const double dc = c > 0 ? c : 1.0;
-  const double tbar = st / dc, xbar = s / dc;
-  const double vt = stt / dc - tbar * tbar;
-  const double slope_d = vt > 0 ? (sx / dc - tbar * xbar) / vt : 0.0;
-  const float mu = c > 0 ? (float)xbar : 0.f;
-  const float slope = (float)slope_d, tb = (float)tbar;
+  const double cnt = dc > 0 ? dc : 1.0;
+  const double tbar = dst / cnt, xbar = ds / cnt;
+  const double vt = dstt / cnt - tbar * tbar;
+  const double slope_d = vt > 0 ? (dsx / cnt - tbar * xbar) / vt : 0.0;
+  const float mu = dc > 0 ? (float)xbar : 0.f;
+  const float slope = (float)slope_d, tb = (float)tbar + tmid;
+  // detrended samples -> LDS, with the Parseval terms: sum e^2, X_0 = sum e,
+  // X_N = sum (-1)^t e
+  float e2 = 0.f, x0 = 0.f, xn = 0.f;
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const int j = tid + i * kThreads;
     if (j < N) {
       const float t0 = (float)(2 * j) - tb;
-      buf[j] = make_float2(isfinite(z[i].x) ? z[i].x - mu - slope * t0 : 0.f,
-                           isfinite(z[i].y) ? z[i].y - mu - slope * (t0 + 1.f) : 0.f);
+      const f2 e = (f2){isfinite(z[i].x) ? z[i].x - mu - slope * t0 : 0.f,
+                        isfinite(z[i].y) ? z[i].y - mu - slope * (t0 + 1.f) : 0.f};
+      buf[j] = e;
+      e2 += e.x * e.x + e.y * e.y;
+      x0 += e.x + e.y;
+      xn += e.x - e.y;
     }
   }
   __syncthreads();
-  const float invN = 1.f / (float)N;
-  int Ns = 1;
-  for (int ps = 0; ps < plan.n_pass; ++ps) {
-    const int r = plan.radix[ps];
-    switch (r) {
-      case 2: stockham_pass<2, MAXN>(buf, N, Ns, invN); break;
-      case 3: stockham_pass<3, MAXN>(buf, N, Ns, invN); break;
-      case 4: stockham_pass<4, MAXN>(buf, N, Ns, invN); break;
-      case 5: stockham_pass<5, MAXN>(buf, N, Ns, invN); break;
-      case 7: stockham_pass<7, MAXN>(buf, N, Ns, invN); break;
-      case 9: stockham_pass<9, MAXN>(buf, N, Ns, invN); break;
-      default: break;
+  if constexpr (FN > 0) {
+    FixedPlan<FN>::run(buf);
+  } else {
+    int Ns = 1;
+    for (int ps = 0; ps < plan.n_pass; ++ps) {
+      const int r = plan.radix[ps];
+      switch (r) {
+        case 2: stockham_pass<2, MAXN>(buf, N, Ns); break;
+        case 3: stockham_pass<3, MAXN>(buf, N, Ns); break;
+        case 4: stockham_pass<4, MAXN>(buf, N, Ns); break;
+        case 5: stockham_pass<5, MAXN>(buf, N, Ns); break;
+        case 7: stockham_pass<7, MAXN>(buf, N, Ns); break;
+        case 9: stockham_pass<9, MAXN>(buf, N, Ns); break;
+        default: break;
+      }
+      Ns *= r;
     }
-    Ns *= r;
   }
-  // unpack the real spectrum X[k], k = 0..N
+  // unpack the real spectrum X[k]: the search band, or k = 0..N when the
+  // periodogram / spectrum is wanted
+  const bool full = power != nullptr || spec != nullptr;
+  const int k0 = full ? 0 : kmin, k1 = full ? N : kmax;
   float best = -1.f;
   int bk = 0;
-  float tot = 0.f;
-  for (int k = tid; k <= N; k += kThreads) {
-    const float2 zk = buf[k == N ? 0 : k];
-    const float2 zn = buf[k == 0 ? 0 : N - k];
-    const float2 zc = make_float2(zn.x, -zn.y);
-    const float2 e = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y));
-    const float2 d = make_float2(0.5f * (zk.x - zc.x), 0.5f * (zk.y - zc.y));
-    const float2 o = make_float2(d.y, -d.x);  // -i * d
-    const float2 X = cadd(e, cmul(tw2[k], o));
+  for (int k = k0 + tid; k <= k1; k += kThreads) {
+    const f2 zk = buf[k == N ? 0 : k];
+    const f2 zn = buf[k == 0 ? 0 : N - k];
+    const f2 zc = (f2){zn.x, -zn.y};
+    const f2 e = 0.5f * (zk + zc);
+    const f2 o = neg_i(0.5f * (zk - zc));
+    const float2 t2 = tw2[k];
+    const f2 X = e + cmul((f2){t2.x, t2.y}, o);
     const float pw = X.x * X.x + X.y * X.y;
     if (power) power[row * ld_p + k] = pw;
-    if (spec) spec[row * ld_s + k] = X;
-    if (k >= 1) tot += pw;
+    if (spec) spec[row * ld_s + k] = make_float2(X.x, X.y);
     if (k >= kmin && k <= kmax && pw > best) { best = pw; bk = k; }
   }
-  // block argmax (value, index) and total
+  // block argmax (value, index) and the Parseval sums
   for (int o = 32; o > 0; o >>= 1) {
     const float ob = __shfl_xor(best, o);
     const int ok = __shfl_xor(bk, o);
     if (ob > best || (ob == best && ok < bk)) { best = ob; bk = ok; }
-    tot += __shfl_xor(tot, o);
   }
-  if (lane_id() == 0) { redf[wave_id()] = best; redi[wave_id()] = bk; redf[4 + wave_id()] = tot; }
+  e2 = wave_sum(e2);
+  x0 = wave_sum(x0);
+  xn = wave_sum(xn);
+  if (lane_id() == 0) { redf[0][wv] = best; redi[wv] = bk; redf[1][wv] = e2; redf[2][wv] = x0; redf[3][wv] = xn; }
   __syncthreads();
   if (tid == 0) {
-    float b = redf[0]; int k = redi[0]; float t = redf[4];
+    float b = redf[0][0], se = redf[1][0], s0 = redf[2][0], sn = redf[3][0];
+    int k = redi[0];
     for (int w = 1; w < kThreads / 64; ++w) {
-      if (redf[w] > b || (redf[w] == b && redi[w] < k)) { b = redf[w]; k = redi[w]; }
-      t += redf[4 + w];
+      if (redf[0][w] > b || (redf[0][w] == b && redi[w] < k)) { b = redf[0][w]; k = redi[w]; }
+      se += redf[1][w]; s0 += redf[2][w]; sn += redf[3][w];
     }
+    // sum_{k=1..N} |X_k|^2 = (Nr sum e^2 - X_0^2 + X_N^2) / 2 (Parseval, real input)
+    const float t = 0.5f * ((float)Nr * se - s0 * s0 + sn * sn);
     period_bin[row] = k;
     strength[row] = t > 0.f ? b / t : 0.f;
     mean_out[row] = mu;
@@ -260,18 +361,23 @@ FM_API int fm_fft_seasonal(const float* x, int64_t ld, int Nr, int64_t R, const 
                            hipStream_t stream) {
   if (R <= 0) return 0;
   if ((Nr & 1) || Nr / 2 > kMaxN || n_pass > 16 || (ld & 1) || (((uintptr_t)x) & 7)) return (int)hipErrorInvalidValue;
+  if (kmin < 0 || kmax > Nr / 2) return (int)hipErrorInvalidValue;
   FftPlan plan;
   plan.n_pass = n_pass;
   int prod = 1;
   for (int i = 0; i < n_pass; ++i) { plan.radix[i] = radices[i]; prod *= radices[i]; }
   if (prod != Nr / 2) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)(Nr / 2) * sizeof(float2);
-#define FM_FFT(MN)                                                                                            \
-  hipLaunchKernelGGL(fft_seasonal_kernel<MN>, dim3((unsigned)R), dim3(kThreads), lds, stream, x, ld, Nr, R, tw, tw2, \
-                     plan, kmin, kmax, power, ld_p, spec, ld_s, period_bin, strength, mean_out, slope_out)
-  if (Nr / 2 <= 2048) FM_FFT(2048);
-  else if (Nr / 2 <= 5120) FM_FFT(5120);
-  else FM_FFT(kMaxN);
+  const int N = Nr / 2;
+  const size_t lds = (size_t)N * sizeof(float2);
+#define FM_FFT(MN, FN)                                                                                        \
+  hipLaunchKernelGGL((fft_seasonal_kernel<MN, FN>), dim3((unsigned)R), dim3(kThreads), lds, stream, x, ld, Nr, R, \
+                     tw, tw2, plan, kmin, kmax, power, ld_p, spec, ld_s, period_bin, strength, mean_out, slope_out)
+  if (N == 5040) FM_FFT(5120, 5040);
+  else if (N == 1008) FM_FFT(1024, 1008);
+  else if (N == 720) FM_FFT(768, 720);
+  else if (N <= 2048) FM_FFT(2048, 0);
+  else if (N <= 5120) FM_FFT(5120, 0);
+  else FM_FFT(kMaxN, 0);
 #undef FM_FFT
   FM_LAUNCH_CHECK();
   return 0;

@@ -14,14 +14,33 @@ MAX_COMPLEX = 8192
 
 
 def plan_radices(n: int) -> list[int] | None:
-    """Radix schedule for a complex length n = 2^a 3^b 5^c 7^d (4s, then 2,
-    9s, then 3, 5s, 7s); None if n has another prime factor."""
-    out = []
+    """Radix schedule for a complex length n = 2^a 3^b 5^c 7^d; None if n has
+    another prime factor.  Factors: 4s, a 2, 9s, 3, 5s, 7s; order: the largest
+    odd radix first, then 4s interleaved with the rest.  An early radix-4
+    pass writes 8-dword-strided (4-way LDS bank conflicts), an odd stride
+    spreads over the banks (fft.hip header; 5040 -> 7,4,9,4,5, the order the
+    kernel's fixed plan uses)."""
+    fac = []
     for r in (4, 2, 9, 3, 5, 7):
         while n % r == 0:
-            out.append(r)
+            fac.append(r)
             n //= r
-    return out if n == 1 else None
+    if n != 1:
+        return None
+    odd = [r for r in fac if r % 2]
+    if not odd:
+        return fac
+    first = max(odd, key=lambda r: (r in (5, 7), r))
+    fac.remove(first)
+    fours = [r for r in fac if r == 4]
+    rest = [r for r in fac if r != 4]
+    out = [first]
+    while fours or rest:
+        if fours:
+            out.append(fours.pop())
+        if rest:
+            out.append(rest.pop(0))
+    return out
 
 
 def supported_length(nr: int) -> bool:

@@ -143,7 +143,7 @@ def test_model_cache_advances_lru_and_refit():
 
 
 def test_ref_fft_detects_daily_period():
-    assert FF.plan_radices(5040) == [4, 4, 9, 5, 7]
+    assert FF.plan_radices(5040) == [7, 4, 9, 4, 5]
     assert FF.supported_length(10080) and not FF.supported_length(10082)
     x = _seasonal(4, 10080, period=1440)
     s = FF.fft_seasonal(torch.from_numpy(x))
@@ -286,10 +286,15 @@ def test_gpu_band_decide(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nr,period", [(10080, 1440), (2016, 288), (1440, 60), (4096, 128)])
+@pytest.mark.parametrize("nr,period", [(10080, 1440), (2016, 288), (1440, 60), (4096, 128), (6048, 288)])
 def test_gpu_fft_seasonal(cuda, nr, period):
     x = _seasonal(50, nr, period=period, seed=nr)
     x[2, 10:20] = np.nan
+    # band-only unpack (the production call): same peak, Parseval total
+    b = FF.fft_seasonal(torch.from_numpy(x).to(cuda))
+    c0 = FF.fft_seasonal(torch.from_numpy(x))
+    np.testing.assert_array_equal(b.period_bin.cpu().numpy(), c0.period_bin.numpy())
+    np.testing.assert_allclose(b.strength.cpu().numpy(), c0.strength.numpy(), rtol=1e-3, atol=1e-5)
     g = FF.fft_seasonal(torch.from_numpy(x).to(cuda), return_power=True)
     c = FF.fft_seasonal(torch.from_numpy(x), return_power=True)
     np.testing.assert_array_equal(g.period_bin.cpu().numpy(), c.period_bin.numpy())
