@@ -52,7 +52,26 @@ template <> struct RootTable<9> {
   static constexpr float s[9] = {0.00000000000000000e+00f, 6.42787609686539252e-01f, 9.84807753012208020e-01f, 8.66025403784438708e-01f, 3.42020143325668879e-01f, -3.42020143325668657e-01f, -8.66025403784438375e-01f, -9.84807753012208131e-01f, -6.42787609686539585e-01f};
 };
 
-__device__ __forceinline__ f2 cmul(f2 a, f2 b) { return a.xx * b + a.yy * (f2){-b.y, b.x}; }
+// The half-swapped, half-negated operands of complex arithmetic folded into
+// the VOP3P source modifiers (op_sel / op_sel_hi pick the half feeding each
+// result lane, neg_lo / neg_hi negate it): one v_pk_* each.  Written out
+// because the compiler builds (b.y, -b.x) with a v_mov + v_xor pair per use.
+__device__ __forceinline__ f2 cmul(f2 a, f2 b) {   // a * b
+  f2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ f2 add_negi(f2 a, f2 b) {   // a - i b = (a.x + b.y, a.y - b.x)
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 add_posi(f2 a, f2 b) {   // a + i b = (a.x - b.y, a.y + b.x)
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ f2 neg_i(f2 a) { return (f2){a.y, -a.x}; }   // -i a
 
 // forward DFT (W = e^{-2 pi i / R}) of R points in registers
@@ -63,11 +82,11 @@ __device__ __forceinline__ void dft(f2 (&v)[R]) {
     v[0] = a + b;
     v[1] = a - b;
   } else if constexpr (R == 4) {
-    const f2 s02 = v[0] + v[2], d02 = v[0] - v[2], s13 = v[1] + v[3], d13 = neg_i(v[1] - v[3]);
+    const f2 s02 = v[0] + v[2], d02 = v[0] - v[2], s13 = v[1] + v[3], d13 = v[1] - v[3];
     v[0] = s02 + s13;
     v[2] = s02 - s13;
-    v[1] = d02 + d13;
-    v[3] = d02 - d13;
+    v[1] = add_negi(d02, d13);
+    v[3] = add_posi(d02, d13);
   } else {
     // conjugate pairs: X_p = v0 + sum_q c_pq S_q - i sum_q s_pq D_q,
     // X_{R-p} = v0 + sum_q c_pq S_q + i sum_q s_pq D_q  (q = 1..(R-1)/2)
@@ -91,9 +110,8 @@ __device__ __forceinline__ void dft(f2 (&v)[R]) {
         A += RootTable<R>::c[m] * S[q - 1];
         B += RootTable<R>::s[m] * D[q - 1];
       }
-      const f2 t = neg_i(B);
-      o[p] = A + t;
-      o[R - p] = A - t;
+      o[p] = add_negi(A, B);
+      o[R - p] = add_posi(A, B);
     }
 #pragma unroll
     for (int p = 0; p < R; ++p) v[p] = o[p];
@@ -109,7 +127,12 @@ constexpr int kThreads = 256;
 template <int R>
 __device__ __forceinline__ void twiddles(float r, f2 (&w)[R]) {
   w[0] = (f2){1.f, 0.f};
-  w[1] = (f2){__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r)};
+  // in asm with the trailing wait states: the hazard recognizer does not see
+  // the transcendental-result -> VALU-use hazard when the user is inline asm
+  // (cmul below), so the asm block carries its own s_nop
+  f2 w1;
+  asm("v_cos_f32 %0, %2\n\tv_sin_f32 %1, %2\n\ts_nop 1" : "=&v"(w1.x), "=&v"(w1.y) : "v"(r));
+  w[1] = w1;
 #pragma unroll
   for (int q = 2; q < R; ++q) w[q] = cmul(w[q - 1], w[1]);
 }
@@ -233,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
   (void)tw;   // twiddles are computed in-kernel (kept in the C ABI)
   __shared__ float redf[6][kThreads / 64];
   __shared__ int redi[kThreads / 64];
-  __shared__ double red5[5][kThreads / 64];
+  __shared__ float red5[5][kThreads / 64];
   const int64_t row = blockIdx.x;
   const int N = FN > 0 ? FN : Nr >> 1;
   const float* xr = x + row * ld;
@@ -242,54 +265,87 @@ __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
   // registers (all loads issued up front), the least-squares linear detrend
   // sums over finite samples are taken from there, and the detrended values
   // are written to LDS.  (NaN -> trend line, so a slow trend does not leak
-  // into the low-frequency bins.)  Per-thread partials in fp32 over centred
-  // time (t - (Nr-1)/2: |t| <= Nr/2, 40 terms), the cross-lane sums in fp64.
+  // into the low-frequency bins.)  Time is centred (tc = t - (Nr-1)/2), so
+  // sum tc and sum tc^2 over ALL samples are closed forms and only the
+  // missing samples' terms are accumulated (a branch no wave takes on a
+  // complete row); the sample sums are packed (x, y) fp32 per thread, the
+  // cross-lane sums fp64.  Branch-free: a wave of 40 divergent if-blocks
+  // per row cost more than the butterflies of a pass.
   constexpr int NPT = MAXN / kThreads;        // complex values per thread
+  constexpr bool FULL = FN > 0 && FN % kThreads == 0;
   f2 z[NPT];
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const int j = tid + i * kThreads;
-    z[i] = j < N ? reinterpret_cast<const f2*>(xr)[j] : (f2){__builtin_nanf(""), __builtin_nanf("")};
+    z[i] = (FULL || j < N) ? reinterpret_cast<const f2*>(xr)[j] : (f2){0.f, 0.f};
   }
   const float tmid = 0.5f * (float)(Nr - 1);
-  float s = 0.f, st = 0.f, stt = 0.f, sx = 0.f, c = 0.f;
+  const f2 tbase = (f2){(float)(2 * tid) - tmid, (float)(2 * tid) + 1.f - tmid};
+  f2 s2 = (f2){0.f, 0.f}, sx2 = (f2){0.f, 0.f};
+  bool bad = false;
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
-    const float t0 = (float)(2 * (tid + i * kThreads)) - tmid;
-    if (isfinite(z[i].x)) { s += z[i].x; st += t0; stt += t0 * t0; sx += t0 * z[i].x; c += 1.f; }
-    if (isfinite(z[i].y)) { const float t1 = t0 + 1.f; s += z[i].y; st += t1; stt += t1 * t1; sx += t1 * z[i].y; c += 1.f; }
+    const f2 t2 = tbase + (float)(2 * kThreads * i);
+    const bool okx = isfinite(z[i].x), oky = isfinite(z[i].y);
+    const f2 xv = (f2){okx ? z[i].x : 0.f, oky ? z[i].y : 0.f};
+    s2 += xv;
+    sx2 += t2 * xv;
+    bad |= !(okx && oky);
   }
-  double ds = wave_sum((double)s), dst = wave_sum((double)st), dstt = wave_sum((double)stt),
-         dsx = wave_sum((double)sx), dc = wave_sum((double)c);
-  if (lane_id() == 0) { red5[0][wv] = ds; red5[1][wv] = dst; red5[2][wv] = dstt; red5[3][wv] = dsx; red5[4][wv] = dc; }
+  // wave partials in fp32 (64 per-thread partials of 40 samples each), the
+  // block combine in fp64; the missing-sample terms only in a wave that has one
+  float cn = 0.f, stn = 0.f, sttn = 0.f;      // missing samples: count, sum tc, sum tc^2
+  if (__any(bad)) {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const f2 t2 = tbase + (float)(2 * kThreads * i);
+      const bool inb = FULL || tid + i * kThreads < N;
+      const float mx = (inb && !isfinite(z[i].x)) ? 1.f : 0.f, my = (inb && !isfinite(z[i].y)) ? 1.f : 0.f;
+      cn += mx + my;
+      stn += mx * t2.x + my * t2.y;
+      sttn += mx * t2.x * t2.x + my * t2.y * t2.y;
+    }
+    cn = wave_sum(cn);
+    stn = wave_sum(stn);
+    sttn = wave_sum(sttn);
+  }
+  const float ws = wave_sum(s2.x + s2.y), wsx = wave_sum(sx2.x + sx2.y);
+  if (lane_id() == 0) { red5[0][wv] = ws; red5[1][wv] = wsx; red5[2][wv] = cn; red5[3][wv] = stn; red5[4][wv] = sttn; }
   __syncthreads();
-  ds = dst = dstt = dsx = dc = 0.0;
+  double ds = 0.0, dsx = 0.0, dcn = 0.0, dstn = 0.0, dsttn = 0.0;
 #pragma unroll
   for (int w = 0; w < kThreads / 64; ++w) {
-    ds += red5[0][w]; dst += red5[1][w]; dstt += red5[2][w]; dsx += red5[3][w]; dc += red5[4][w];
+    ds += red5[0][w]; dsx += red5[1][w]; dcn += red5[2][w]; dstn += red5[3][w]; dsttn += red5[4][w];
   }
+  const double nr = (double)Nr;
+  const double dc = nr - dcn;                                     // finite samples
+  const double dst = -dstn;                                       // sum tc over all = 0
+  const double dstt = nr * (nr * nr - 1.0) / 12.0 - dsttn;        // sum tc^2 over all
   const double cnt = dc > 0 ? dc : 1.0;
   const double tbar = dst / cnt, xbar = ds / cnt;
   const double vt = dstt / cnt - tbar * tbar;
   const double slope_d = vt > 0 ? (dsx / cnt - tbar * xbar) / vt : 0.0;
   const float mu = dc > 0 ? (float)xbar : 0.f;
-  const float slope = (float)slope_d, tb = (float)tbar + tmid;
-  // detrended samples -> LDS, with the Parseval terms: sum e^2, X_0 = sum e,
-  // X_N = sum (-1)^t e
-  float e2 = 0.f, x0 = 0.f, xn = 0.f;
+  const float slope = (float)slope_d;
+  // e = x - mu - slope (tc - tbar) = x - c0 - slope tc
+  const float c0 = (float)((dc > 0 ? xbar : 0.0) - slope_d * tbar);
+  // detrended samples -> LDS, with the Parseval terms: sum e^2, and
+  // ex = (sum e_even, sum e_odd): X_0 = ex.x + ex.y, X_N = ex.x - ex.y
+  f2 e2v = (f2){0.f, 0.f}, ex = (f2){0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const int j = tid + i * kThreads;
-    if (j < N) {
-      const float t0 = (float)(2 * j) - tb;
-      const f2 e = (f2){isfinite(z[i].x) ? z[i].x - mu - slope * t0 : 0.f,
-                        isfinite(z[i].y) ? z[i].y - mu - slope * (t0 + 1.f) : 0.f};
+    if (FULL || (FN > 0 && i < NPT - 1) || j < N) {
+      const f2 t2 = tbase + (float)(2 * kThreads * i);
+      f2 e = (z[i] - c0) - slope * t2;
+      e.x = isfinite(z[i].x) ? e.x : 0.f;
+      e.y = isfinite(z[i].y) ? e.y : 0.f;
       buf[j] = e;
-      e2 += e.x * e.x + e.y * e.y;
-      x0 += e.x + e.y;
-      xn += e.x - e.y;
+      e2v += e * e;
+      ex += e;
     }
   }
+  float e2 = e2v.x + e2v.y, x0 = ex.x + ex.y, xn = ex.x - ex.y;
   __syncthreads();
   if constexpr (FN > 0) {
     FixedPlan<FN>::run(buf);
@@ -322,7 +378,7 @@ __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
     const f2 e = 0.5f * (zk + zc);
     const f2 o = neg_i(0.5f * (zk - zc));
     const float2 t2 = tw2[k];
-    const f2 X = e + cmul((f2){t2.x, t2.y}, o);
+    const f2 X = e + cmul(o, (f2){t2.x, t2.y});
     const float pw = X.x * X.x + X.y * X.y;
     if (power) power[row * ld_p + k] = pw;
     if (spec) spec[row * ld_s + k] = make_float2(X.x, X.y);

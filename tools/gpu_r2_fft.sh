@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-true &&
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_model_ops.py tests/test_library.py -m gpu -k "fft or library" > gpurun_out/fft_tests.log 2>&1 &&
 timeout -k 10 200 python tools/fft_bench.py > gpurun_out/fft_bench.jsonl 2>&1 &&
 timeout -k 10 200 python benchmarks/bench_configs.py --config 2 --detect-period > gpurun_out/c2fft.jsonl 2>&1 &&
 cd /tmp && export TMPDIR=/tmp &&
