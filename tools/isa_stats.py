@@ -18,7 +18,7 @@ TRANS = ("v_sin_", "v_cos_", "v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_")
 
 
 def kernels(text: str):
-    for m in re.finditer(r"^([A-Za-z_][\w.$]*):\s*; @\1\n(.*?)^\s*s_endpgm", text, re.S | re.M):
+    for m in re.finditer(r"^([A-Za-z_][\w.$]*):\s*; @\1\n(.*?)^\.Lfunc_end", text, re.S | re.M):
         yield m.group(1), m.group(2)
 
 
