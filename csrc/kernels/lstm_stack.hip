@@ -121,7 +121,9 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack_kernel(
       for (int ct = 0; ct < NCT; ++ct) acc[rt][ct] = (f32x16){};
     // not unrolled: unrolling lets the scheduler hoist every k-step's A
     // fragments (33 x RT x 16 B per lane at H = 256) and spill; one k-step of
-    // lookahead is what the L2 latency needs with 2 waves per SIMD
+    // lookahead is what the L2 latency needs with 2 waves per SIMD (at 4 x 2
+    // tiling the lookahead costs 65 spilled VGPRs and still wins: without it
+    // config 4 at H = 256 x 2 layers runs 10.1 instead of 9.0 ms)
 #pragma unroll 1
     for (int ks = 0; ks < KS; ++ks) {
       if (ks + 1 < KS) {
@@ -220,9 +222,15 @@ static int launch_stack(const void* xa, int64_t B, int L, const void* W0, const 
 }
 
 // Row tiles per wave / column tiles per workgroup (see ops/lstm.py STACK_TILING):
-// H=256: 4 x 1 (8 waves, 32 sequences); H<=128: 2 x 2 (H/16 waves, 64 sequences).
+// H=256: 4 x 2 (8 waves, 64 sequences share every streamed weight fragment:
+// half the L2 weight traffic of 4 x 1, which wins despite 65 spilled VGPRs
+// and half the workgroups -- config 4 at 2 layers 10.8 -> 9.0 ms,
+// profiles/lstm_tile_ab_r2.txt); H<=128: 2 x 2 (H/16 waves, 64 sequences).
+// rt / nct = 0 pick that default; the other H = 256 tilings (4 x 1, 2 x 2,
+// 2 x 1) stay instantiated for the A/B (ops/lstm.py FM_LSTM_STACK_TILING)
+// and need weights packed with the same RT.
 FM_API int fm_lstm_stack(const void* xa, int64_t B, int L, int H, int layers, const void* W0, const void* W1,
-                         float* h_out, float* c_out, hipStream_t stream) {
+                         float* h_out, float* c_out, int rt, int nct, hipStream_t stream) {
   if (B <= 0 || L <= 0) return 0;
   if (layers != 1 && layers != 2) return (int)hipErrorInvalidValue;
   if (layers == 2 && W1 == nullptr) return (int)hipErrorInvalidValue;
@@ -230,10 +238,15 @@ FM_API int fm_lstm_stack(const void* xa, int64_t B, int L, int H, int layers, co
   return layers == 2 ? launch_stack<HH, RTT, NCC, 2>(xa, B, L, W0, W1, h_out, c_out, stream)            \
                      : launch_stack<HH, RTT, NCC, 1>(xa, B, L, W0, W1, h_out, c_out, stream)
   switch (H) {
-    case 256: FM_STK(256, 4, 1);
-    case 128: FM_STK(128, 2, 2);
-    case 64: FM_STK(64, 2, 2);
-    case 32: FM_STK(32, 2, 2);
+    case 256:
+      if (rt == 0 || (rt == 4 && nct == 2)) FM_STK(256, 4, 2);
+      if (rt == 4 && nct == 1) FM_STK(256, 4, 1);
+      if (rt == 2 && nct == 2) FM_STK(256, 2, 2);
+      if (rt == 2 && nct == 1) FM_STK(256, 2, 1);
+      return (int)hipErrorInvalidValue;
+    case 128: if (rt == 0 || (rt == 2 && nct == 2)) FM_STK(128, 2, 2); return (int)hipErrorInvalidValue;
+    case 64: if (rt == 0 || (rt == 2 && nct == 2)) FM_STK(64, 2, 2); return (int)hipErrorInvalidValue;
+    case 32: if (rt == 0 || (rt == 2 && nct == 2)) FM_STK(32, 2, 2); return (int)hipErrorInvalidValue;
     default: return (int)hipErrorInvalidValue;
   }
 #undef FM_STK

@@ -89,7 +89,8 @@ _SIGS: dict[str, list] = {
     "fm_copy_d2h_async": [c_void_p, c_void_p, c_i64, c_void_p],
     "fm_rolling_stats": [c_void_p, c_i64, c_int, c_i64, c_int, c_int, c_void_p, c_void_p, c_i64, c_void_p],
     "fm_pvalues_range": [c_void_p, c_i64, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
-    "fm_lstm_stack": [c_void_p, c_i64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "fm_lstm_stack": [c_void_p, c_i64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                      c_void_p],
     "fm_lstm_features_mv": [c_void_p, c_i64, c_int, c_i64, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
                             c_void_p],
     "fm_lstm_features": [c_void_p, c_i64, c_int, c_i64, c_int, c_float, c_int, c_void_p, c_void_p, c_void_p,

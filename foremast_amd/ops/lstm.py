@@ -13,7 +13,22 @@ from ._lib import LIB, check, ptr, require_native, stream_of
 
 SUPPORTED_H = (32, 64, 128)              # register-resident single-layer kernel (lstm.hip)
 STACK_H = (32, 64, 128, 256)             # streamed-weight 1-2 layer kernel (lstm_stack.hip)
-STACK_TILING = {256: (4, 1), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row tiles / wave, column tiles)
+STACK_TILING = {256: (4, 2), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row tiles / wave, column tiles)
+STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1))}           # instantiated alternatives (lstm_stack.hip)
+
+
+def stack_tiling(H: int) -> tuple[int, int]:
+    """(row tiles per wave, column tiles per workgroup) of the stacked kernel
+    at hidden size H; ``FM_LSTM_STACK_TILING=RT:NCT`` overrides it at H = 256
+    (A/B of fill vs streamed-weight reuse; the packed weights depend on RT,
+    so pack and run under the same setting)."""
+    import os
+    env = os.environ.get("FM_LSTM_STACK_TILING")
+    if env and H in STACK_TILING_ALT:
+        rt, nct = (int(v) for v in env.split(":"))
+        check((rt, nct) in STACK_TILING_ALT[H], f"FM_LSTM_STACK_TILING {env} not instantiated for H={H}")
+        return rt, nct
+    return STACK_TILING[H]
 
 
 def _bf16_bits(a: np.ndarray) -> np.ndarray:
@@ -79,7 +94,7 @@ def pack_aug(aug: np.ndarray, H: int, RT: int) -> np.ndarray:
 def pack_stack(layers: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]], H: int) -> list[torch.Tensor]:
     """[(W_ih, W_hh, b_ih + b_hh)] per layer (torch.nn.LSTM conventions) ->
     the stacked kernel's per-layer fragment buffers (uint8)."""
-    RT = STACK_TILING[H][0]
+    RT = stack_tiling(H)[0]
     out = []
     for li, (w_ih, w_hh, b) in enumerate(layers):
         w_ih, w_hh, b = (t.detach().float().cpu().numpy() for t in (w_ih, w_hh, b))
@@ -113,7 +128,9 @@ def lstm_stack_forward(xa: torch.Tensor, packed: list[torch.Tensor], H: int):
     cT = torch.empty((B, H), dtype=torch.float32, device=d)
     w0 = packed[0].to(d)
     w1 = packed[1].to(d) if len(packed) > 1 else None
-    LIB.call("fm_lstm_stack", ptr(xa), B, L, H, len(packed), ptr(w0), ptr(w1), ptr(hT), ptr(cT), stream_of(xa))
+    rt, nct = stack_tiling(H)
+    LIB.call("fm_lstm_stack", ptr(xa), B, L, H, len(packed), ptr(w0), ptr(w1), ptr(hT), ptr(cT), rt, nct,
+             stream_of(xa))
     return hT, cT
 
 

@@ -471,6 +471,24 @@ def test_gpu_lstm_stack_matches_fp32_lstm(cuda, H, layers, I):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tiling", ["4:1", "2:1", "4:2", "2:2"])
+def test_gpu_lstm_stack_tilings_agree(cuda, tiling, monkeypatch):
+    """Every instantiated H = 256 tiling (row tiles per wave x column tiles)
+    computes the same recurrence as the bf16-emulating reference."""
+    monkeypatch.setenv("FM_LSTM_STACK_TILING", tiling)
+    torch.manual_seed(5)
+    H, layers, I, B, L = 256, 2, 11, 100, 48
+    m = torch.nn.LSTM(I, H, num_layers=layers, batch_first=True)
+    x = torch.randn(B, L, I)
+    ws = [(getattr(m, f"weight_ih_l{k}"), getattr(m, f"weight_hh_l{k}"),
+           getattr(m, f"bias_ih_l{k}") + getattr(m, f"bias_hh_l{k}")) for k in range(layers)]
+    hg, cg = LS.lstm_stack_forward(LS.augment(x.to(cuda).contiguous()), LS.pack_stack(ws, H), H)
+    hr, cr = LS.ref_lstm_stack(x, ws, emulate_bf16=True)
+    torch.testing.assert_close(hg.cpu(), hr, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(cg.cpu(), cr, atol=5e-2, rtol=5e-2)
+
+
+@pytest.mark.gpu
 def test_gpu_lstm_multivariate_forecaster(cuda):
     from foremast_amd.models.lstm import LSTMForecaster
     S, M, T = 40, 8, 600
