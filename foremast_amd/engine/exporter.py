@@ -72,7 +72,15 @@ class GaugeTable:
                 self.vals = np.concatenate([self.vals, grow])
         return out
 
-    def set(self, slots: np.ndarray, values, track: bool = True) -> None:
+    def set(self, slots, values, track: bool = True) -> None:
+        """``slots``: slot indices, or a ``slice`` of consecutive slots (a
+        strided store instead of an 80k-element scatter per cycle)."""
+        if isinstance(slots, slice):
+            with self.lock:
+                self.vals[slots] = values
+            if track and slots.stop > slots.start:
+                self.dirty.append(np.arange(slots.start, slots.stop, slots.step or 1))
+            return
         slots = np.asarray(slots, np.int64)
         with self.lock:
             self.vals[slots] = values
@@ -150,9 +158,28 @@ class BrainExporter:
         s = self.table.slots([(u, namespace, app), (l, namespace, app), (a, namespace, app)])
         self.table.set(s, [upper, lower, anomaly])
 
-    def set_bounds_many(self, slots: np.ndarray, upper: np.ndarray, lower: np.ndarray, anomaly: np.ndarray) -> None:
-        """``slots`` [n, 3] from :meth:`bound_slots`; one vectorised store."""
+    def set_bounds_many(self, slots, upper: np.ndarray, lower: np.ndarray, anomaly: np.ndarray) -> None:
+        """``slots`` [n, 3] from :meth:`bound_slots` (one vectorised store), or
+        the first slot of n consecutive triples (``contiguous_start``): three
+        strided stores, no scatter."""
+        if isinstance(slots, (int, np.integer)):
+            n = len(upper)
+            t = self.table
+            with t.lock:
+                t.vals[slots:slots + 3 * n:3] = upper
+                t.vals[slots + 1:slots + 3 * n:3] = lower
+                t.vals[slots + 2:slots + 3 * n:3] = anomaly
+            t.dirty.append(np.arange(slots, slots + 3 * n))
+            return
         self.table.set(slots.reshape(-1), np.stack([upper, lower, anomaly], 1).reshape(-1))
+
+    @staticmethod
+    def contiguous_start(slots: np.ndarray):
+        """First slot if ``slots`` ([n, 3]) are consecutive, else None."""
+        flat = np.asarray(slots).reshape(-1)
+        if len(flat) and flat[-1] - flat[0] == len(flat) - 1 and bool(np.all(np.diff(flat) == 1)):
+            return int(flat[0])
+        return None
 
     def bound_slots(self, base_metrics: list[str], namespaces: list[str], apps: list[str]) -> np.ndarray:
         keys = []
@@ -201,7 +228,7 @@ class BrainExporter:
         import torch.distributed as dist
         from ..parallel import dist as D
         if not D.is_dist():
-            self.table.take_dirty()
+            self.table.dirty = []               # nothing to merge: drop the change log unsorted
             self.table.new_from = len(self.table.keys)
             return 0
         rank, world = dist.get_rank(group), dist.get_world_size(group)

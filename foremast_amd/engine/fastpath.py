@@ -106,6 +106,9 @@ class FastWork:
     failed: str = ""
 
 
+USED_STAMP_EVERY = 16           # cycles between row last-use stamps (must stay < max_idle_cycles)
+
+
 @dataclass
 class GroupArrays:
     """Host/device arrays of one group, reused while the group's job list
@@ -122,11 +125,13 @@ class GroupArrays:
     end: np.ndarray
     missing: np.ndarray                        # [S, M] no history or no current data
     export_slots: np.ndarray | None = None
+    export_start: int | None = None            # first slot when export_slots are consecutive
     handles: np.ndarray | None = None          # store rows of the jobs (ClaimBatch.handles)
     works: list | None = None                  # the job list object these arrays were built for
     impact_ids: np.ndarray | None = None       # call-graph node per job (-1: none)
     impact_version: int = -1
     impact_slots: np.ndarray | None = None     # exporter slots of the downstream-impact gauge
+    marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
 
 
 def _label(q: str, name: str) -> str:
@@ -492,6 +497,7 @@ class FastPath:
                     p.export_slots = exp.bound_slots(p.base_metrics, [p.namespace] * M, [p.app] * M)
                 slots.append(p.export_slots)
             ga.export_slots = np.concatenate(slots)
+            ga.export_start = exp.contiguous_start(ga.export_slots)
         for w in works:
             w.dirty = False
         self._garr[key] = ga
@@ -505,7 +511,12 @@ class FastPath:
         dev = self.b.device
         store = self.sliding if p0.sliding else self.static
         ga = self._arrays(works, key if key is not None else ("adhoc",) + p0.group)
-        store.used[ga.rowmap] = self.cycle
+        # last-use stamps for idle eviction (max_idle_cycles = 64): refreshed
+        # every 16 cycles, not every cycle -- an 80k-row scatter is ~0.25 ms
+        # of host time, and a stamp at most 15 cycles old never evicts a live row
+        if self.cycle - ga.marked >= USED_STAMP_EVERY:
+            store.used[ga.rowmap] = self.cycle
+            ga.marked = self.cycle
         n = ga.cur.shape[1]
         o = self._scorer(p0.aliases).score_resident(store.view(), ga.rm_d, ga.cur_d, ga.base_d)
         dec = o.decide
@@ -524,8 +535,11 @@ class FastPath:
             ix, _ = C.compact_anomalies(dec, ga.cur_d)
             idx = ix.numpy()
         # (row, point) sorted: the order of atomically appended rows is arbitrary
+        # (one int64 key sort: 7x faster than a two-key lexsort on the host)
         if len(idx):
-            idx = idx[np.lexsort((idx[:, 1], idx[:, 0]))]
+            key = idx[:, 0].astype(np.int64) * n + idx[:, 1]
+            key.sort()
+            idx = np.stack([key // n, key % n], 1).astype(np.int32)
         return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
                 "packed": packed, "stats": stats, "count": count, "anom": idx, "hist_rows": ga.rowmap,
                 "store": store}
@@ -577,8 +591,8 @@ class FastPath:
             anom_ts = np.full(R, np.nan)
             if len(anom):
                 np.fmax.at(anom_ts, anom[:, 0], cur_t[anom[:, 0], anom[:, 1]])
-            exp.set_bounds_many(ga.export_slots, stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64),
-                                anom_ts)
+            exp.set_bounds_many(ga.export_slots if ga.export_start is None else ga.export_start,
+                                stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64), anom_ts)
         if works[0].plan.hpa:
             self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome)
             return

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Host profile of the production brain cycle (config 3e2e): cProfile over
+the timed cycles only (the untimed first cycle, dominated by the synthetic
+generator, is excluded).  Prints the top functions by own time."""
+import cProfile
+import io
+import os
+import pstats
+import sys
+
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, root)
+sys.path.insert(0, os.path.join(root, "benchmarks"))
+import bench_configs as B  # noqa: E402
+from benchmarks import harness  # noqa: E402
+
+prof = cProfile.Profile()
+_orig = harness.time_steps
+
+
+def timed(step, steps, warmup, dev):
+    for _ in range(warmup):
+        step()
+    prof.enable()
+    try:
+        return _orig(step, steps, 0, dev)
+    finally:
+        prof.disable()
+
+
+B.time_steps = timed
+sys.argv = ["bench_configs.py", "--config", "3e2e"] + sys.argv[1:]
+B.main()
+s = io.StringIO()
+pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(35)
+print(s.getvalue())
