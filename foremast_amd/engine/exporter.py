@@ -51,7 +51,7 @@ class GaugeTable:
         self.vals = np.zeros(0, np.float64)
         self.help: dict[str, str] = {}
         self.lock = threading.Lock()
-        self.dirty: list[np.ndarray] = []        # slots changed since the last sync
+        self.dirty: list = []                    # slots changed since the last sync (arrays / (lo, hi) ranges)
         self.new_from = 0                        # keys[new_from:] not yet announced
 
     def __len__(self) -> int:
@@ -79,7 +79,7 @@ class GaugeTable:
             with self.lock:
                 self.vals[slots] = values
             if track and slots.stop > slots.start:
-                self.dirty.append(np.arange(slots.start, slots.stop, slots.step or 1))
+                self.dirty.append((slots.start, slots.stop))
             return
         slots = np.asarray(slots, np.int64)
         with self.lock:
@@ -92,7 +92,8 @@ class GaugeTable:
         return None if s is None else float(self.vals[s])
 
     def take_dirty(self) -> np.ndarray:
-        d = np.unique(np.concatenate(self.dirty)) if self.dirty else np.zeros(0, np.int64)
+        parts = [np.arange(p[0], p[1]) if isinstance(p, tuple) else p for p in self.dirty]
+        d = np.unique(np.concatenate(parts)) if parts else np.zeros(0, np.int64)
         self.dirty = []
         return d
 
@@ -169,7 +170,7 @@ class BrainExporter:
                 t.vals[slots:slots + 3 * n:3] = upper
                 t.vals[slots + 1:slots + 3 * n:3] = lower
                 t.vals[slots + 2:slots + 3 * n:3] = anomaly
-            t.dirty.append(np.arange(slots, slots + 3 * n))
+            t.dirty.append((slots, slots + 3 * n))
             return
         self.table.set(slots.reshape(-1), np.stack([upper, lower, anomaly], 1).reshape(-1))
 
