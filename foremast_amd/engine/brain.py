@@ -107,9 +107,6 @@ def _app_level(ss: list[Series]) -> tuple[np.ndarray, float]:
     return v, float(t[-1])
 
 
-PIPELINE_MIN_JOBS = 2048   # fast-path groups at least this large are scored in two pipelined chunks
-
-
 class Brain:
     def __init__(self, store, cfg: BrainConfig | None = None, device="cpu", sources: SourceRouter | None = None,
                  worker_id: str | None = None, batch_size: int = 512, exporter: BrainExporter | None = None,
@@ -441,25 +438,17 @@ class Brain:
             groups = fp.groups(fast)
         scored = []
         self._n_contained = 0
-        # without the downstream-impact step (which needs every verdict before
-        # any job is finished) large groups are scored in two chunks on two
-        # buffer sets: the host finishes chunk 0 while the GPU scores chunk 1
-        pipelined = not self.impact.enabled
         for key, grp in groups.items():
             M = len(key[0])
-            parts = 2 if pipelined and len(grp) >= PIPELINE_MIN_JOBS else 1
-            for slot, (k2, g2) in enumerate(fp.chunks(key, grp, parts)):
-                try:
-                    with self.spans.span("score"):
-                        g = fp.launch_group(g2, now, k2, slot=slot)
-                        if not pipelined:
-                            g = fp.collect_group(g)
-                    scored.append((k2, g2, g))
-                    if self.impact.enabled:
-                        fp.observe_impact(g, self.impact, now)
-                except Exception:                       # contain: re-score job by job
-                    log.exception("fast-path group of %d jobs failed; re-scoring per job", len(g2))
-                    self._n_contained += self._fast_per_job(g2, M, now, updates, hpalogs, outcome)
+            try:
+                with self.spans.span("score"):
+                    g = fp.score_group(grp, now, key)
+                scored.append((key, grp, g))
+                if self.impact.enabled:
+                    fp.observe_impact(g, self.impact, now)
+            except Exception:                       # contain: re-score job by job
+                log.exception("fast-path group of %d jobs failed; re-scoring per job", len(grp))
+                self._n_contained += self._fast_per_job(grp, M, now, updates, hpalogs, outcome)
         return scored
 
     def _finish_fast(self, scored: list, now: float, updates: list, hpalogs: list, outcome: dict,
@@ -469,9 +458,6 @@ class Brain:
         for key, grp, g in scored:
             M = len(key[0])
             try:
-                if g.get("pending"):
-                    with self.spans.span("score_wait"):
-                        g = fp.collect_group(g)
                 with self.spans.span("finish"):
                     gb: list = []
                     fp.finish_group(g, now, updates, hpalogs, outcome, gb,

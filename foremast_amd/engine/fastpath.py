@@ -218,8 +218,7 @@ class FastPath:
         self.hpa = HpaTable(brain.device)
         self.cycle = 0
         self.max_idle_cycles = 64
-        self._cmp = {}            # device compaction buffers per (device, slot)
-        self._chunk_cache: dict = {}   # group key -> (job list, its chunks) for pipelined scoring
+        self._cmp = {}            # device compaction buffers per capacity
 
     # ------------------------------------------------------------------ planning
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
@@ -505,14 +504,6 @@ class FastPath:
         return ga
 
     def score_group(self, works: list[FastWork], now: float, key: tuple | None = None) -> dict:
-        return self.collect_group(self.launch_group(works, now, key))
-
-    def launch_group(self, works: list[FastWork], now: float, key: tuple | None = None, slot: int = 0) -> dict:
-        """Enqueue a group's tick (front kernel, decision, anomaly compaction)
-        and the copies of its results into pinned host memory; returns a
-        pending handle for :meth:`collect_group`.  ``slot`` selects the
-        scorer's and the compaction's buffer set, so a second group (or chunk)
-        can be enqueued behind this one while the host finishes this one."""
         p0 = works[0].plan
         M = len(p0.aliases)
         S = len(works)
@@ -527,40 +518,21 @@ class FastPath:
             store.used[ga.rowmap] = self.cycle
             ga.marked = self.cycle
         n = ga.cur.shape[1]
-        o = self._scorer(p0.aliases).score_resident(store.view(), ga.rm_d, ga.cur_d, ga.base_d, slot=slot)
-        g = {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
-             "hist_rows": ga.rowmap, "store": store, "pending": True, "o": o, "R": R, "n": n, "slot": slot}
+        o = self._scorer(p0.aliases).score_resident(store.view(), ga.rm_d, ga.cur_d, ga.base_d)
+        dec = o.decide
         if dev.type == "cuda":
             cap = max(1024, min(R * n, 1 << 16))
-            idx_d, _, ctr = self._compact(o.decide, ga.cur_d, R, n, cap, slot)
-            # everything the verdicts need, in one batch of async copies (the
-            # whole compaction buffer: collecting must not wait on a later
-            # group's kernels queued behind this one)
-            g["host"] = [t.to("cpu", non_blocking=True)
-                         for t in (o.packed, o.decide.stats, o.decide.count, ctr, idx_d[:cap])]
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            g["event"], g["cap"] = ev, cap
-        return g
-
-    def collect_group(self, g: dict) -> dict:
-        """Wait for a launched group and build its verdict inputs."""
-        if not g.pop("pending", False):
-            return g
-        o, R, n = g.pop("o"), g["R"], g["n"]
-        dec = o.decide
-        if "event" in g:
-            g.pop("event").synchronize()
-            packed, stats, count, total, idx_all = (t.numpy() for t in g.pop("host"))
+            idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, cap)
+            host = [t.to("cpu", non_blocking=True) for t in (o.packed, dec.stats, dec.count, ctr)]
+            torch.cuda.current_stream(dev).synchronize()
+            packed, stats, count, total = (t.numpy() for t in host)
             total = int(total[0])
-            if total > g["cap"]:          # more anomalies than the buffer: compact again at full size
-                idx_d, _, _ = self._compact(dec, g["ga"].cur_d, R, n, total, g["slot"])
-                idx = idx_d[:total].cpu().numpy()
-            else:
-                idx = idx_all[:total]
+            if total > cap:
+                idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, total)
+            idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
         else:
             packed, stats, count = o.packed.numpy(), dec.stats.numpy(), dec.count.numpy()
-            ix, _ = C.compact_anomalies(dec, g["ga"].cur_d)
+            ix, _ = C.compact_anomalies(dec, ga.cur_d)
             idx = ix.numpy()
         # (row, point) sorted: the order of atomically appended rows is arbitrary
         # (one int64 key sort: 7x faster than a two-key lexsort on the host)
@@ -568,26 +540,15 @@ class FastPath:
             key = idx[:, 0].astype(np.int64) * n + idx[:, 1]
             key.sort()
             idx = np.stack([key // n, key % n], 1).astype(np.int32)
-        g.update(packed=packed, stats=stats, count=count, anom=idx)
-        return g
+        return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
+                "packed": packed, "stats": stats, "count": count, "anom": idx, "hist_rows": ga.rowmap,
+                "store": store}
 
-    def chunks(self, key: tuple, works: list[FastWork], parts: int) -> list[tuple[tuple, list[FastWork]]]:
-        """``works`` split into ``parts`` contiguous chunks with stable keys
-        and list objects (so each chunk's arrays stay cached across cycles)."""
-        if parts <= 1:
-            return [(key, works)]
-        c = self._chunk_cache.get(key)
-        if c is None or c[0] is not works or len(c[1]) != parts:
-            b = np.linspace(0, len(works), parts + 1).astype(int)
-            c = (works, [(key + ("chunk", i), works[b[i]:b[i + 1]]) for i in range(parts) if b[i + 1] > b[i]])
-            self._chunk_cache[key] = c
-        return c[1]
-
-    def _compact(self, dec, cur_d, R: int, n: int, cap: int, slot: int = 0):
+    def _compact(self, dec, cur_d, R: int, n: int, cap: int):
         dev = cur_d.device
-        buf = self._cmp.get((dev, slot))
+        buf = self._cmp.get(dev)
         if buf is None or buf[0].shape[0] < cap:
-            buf = self._cmp[(dev, slot)] = (torch.empty((cap, 2), dtype=torch.int32, device=dev),
+            buf = self._cmp[dev] = (torch.empty((cap, 2), dtype=torch.int32, device=dev),
                                     torch.empty((cap,), dtype=torch.float32, device=dev),
                                     torch.zeros((1,), dtype=torch.int32, device=dev))
         idx, val, ctr = buf

@@ -130,24 +130,6 @@ def test_fast_path_equals_general_path_over_cycles():
     assert len(a[3].fast.sliding) > 0
 
 
-def test_chunked_pipelined_scoring_equals_general(monkeypatch):
-    """Groups scored in two pipelined chunks (launch both, then collect and
-    finish one while the other is in flight) give the general path's results."""
-    import foremast_amd.engine.brain as B
-    monkeypatch.setattr(B, "PIPELINE_MIN_JOBS", 2)
-    a, b, ids, hist = _run_pair()
-    assert hist[0][0]["fast_jobs"] == len(ids)
-    assert any(len(k) > 2 and k[-2] == "chunk" for k in a[3].fast._garr)
-
-
-@pytest.mark.gpu
-def test_gpu_chunked_pipelined_scoring_equals_general(cuda, monkeypatch):
-    import foremast_amd.engine.brain as B
-    monkeypatch.setattr(B, "PIPELINE_MIN_JOBS", 2)
-    a, b, ids, hist = _run_pair(cuda)
-    assert any(len(k) > 2 and k[-2] == "chunk" for k in a[3].fast._garr)
-
-
 def test_wide_pairwise_window_does_not_abort_cycle():
     a, b, ids, hist = _run_pair()
     wide = ids[-1]
@@ -157,13 +139,13 @@ def test_wide_pairwise_window_does_not_abort_cycle():
 def test_failing_group_is_contained_per_job(monkeypatch):
     clock, store, client, brain, exp = _brain(True, {})
     ids = _submit(client)
-    orig = brain.fast.launch_group
+    orig = brain.fast.score_group
 
-    def boom(works, now, key=None, slot=0):
+    def boom(works, now):
         if any(w.doc.app_name == "canary2" for w in works):
             raise RuntimeError("injected kernel failure")
-        return orig(works, now, key, slot)
-    monkeypatch.setattr(brain.fast, "launch_group", boom)
+        return orig(works, now)
+    monkeypatch.setattr(brain.fast, "score_group", boom)
     r = brain.run_once()
     assert r["claimed"] == len(ids)
     bad = [j for j in ids if store.get(j).app_name == "canary2"][0]
