@@ -32,5 +32,7 @@ B.time_steps = timed
 sys.argv = ["bench_configs.py", "--config", "3e2e"] + sys.argv[1:]
 B.main()
 s = io.StringIO()
-pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(35)
+st = pstats.Stats(prof, stream=s)
+st.sort_stats("tottime").print_stats(30)
+st.print_callees("finish_group|claim_batch|_cycle")
 print(s.getvalue())
