@@ -403,6 +403,25 @@ def test_gpu_lstm_matches_reference(cuda, H, I):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H,I", [(128, 1), (64, 3)])
+def test_gpu_lstm_config4_length_matches_fp32_lstm(cuda, H, I):
+    """the register-resident kernel at the config-4
+    lookback (L = 240) against fp32 torch.nn.LSTM -- the bf16 drift over 240
+    steps is pinned, not only the 24-step bf16-emulating agreement."""
+    torch.manual_seed(7 * H + I)
+    B, L = 200, 240
+    m = torch.nn.LSTM(I, H, batch_first=True)
+    x = torch.randn(B, L, I)
+    with torch.no_grad():
+        _, (h32, c32) = m(x)
+    pk = LS.pack_lstm(m.weight_ih_l0.detach(), m.weight_hh_l0.detach(), (m.bias_ih_l0 + m.bias_hh_l0).detach())
+    z = torch.zeros(B, H, device=cuda)
+    hg, cg, _ = LS.lstm_forward(x.to(cuda).contiguous(), pk, H, z, z.clone())
+    err = (hg.cpu() - h32[0]).abs()
+    assert float(err.max()) < 0.08 and float(err.mean()) < 0.01, (float(err.max()), float(err.mean()))
+
+
+@pytest.mark.gpu
 def test_gpu_lstm_features_and_forecast(cuda):
     """fm_lstm_features == the CPU feature path (bf16-rounded), and the GPU
     forecaster agrees with the CPU nn.LSTM forecaster."""
