@@ -223,18 +223,24 @@ __device__ __forceinline__ void stockham_pass(f2* buf, int N, int Ns) {
   __syncthreads();
 }
 
-template <int FN> struct FixedPlan { static constexpr bool ok = false; };
+// Fixed plans: the first radix R1 (its pass is fused with the row load:
+// the butterflies read their inputs straight from the detrended registers)
+// and the remaining passes, which start at Ns = R1.
+template <int FN> struct FixedPlan { static constexpr bool ok = false; static constexpr int R1 = 1; };
 template <> struct FixedPlan<5040> {
   static constexpr bool ok = true;
-  static __device__ __forceinline__ void run(f2* b) { passes_ct<5040, 1, 7, 4, 9, 4, 5>(b); }
+  static constexpr int R1 = 7;
+  static __device__ __forceinline__ void run_rest(f2* b) { passes_ct<5040, 7, 4, 9, 4, 5>(b); }
 };
 template <> struct FixedPlan<1008> {
   static constexpr bool ok = true;
-  static __device__ __forceinline__ void run(f2* b) { passes_ct<1008, 1, 7, 4, 9, 4>(b); }
+  static constexpr int R1 = 7;
+  static __device__ __forceinline__ void run_rest(f2* b) { passes_ct<1008, 7, 4, 9, 4>(b); }
 };
 template <> struct FixedPlan<720> {
   static constexpr bool ok = true;
-  static __device__ __forceinline__ void run(f2* b) { passes_ct<720, 1, 5, 4, 9, 4>(b); }
+  static constexpr int R1 = 5;
+  static __device__ __forceinline__ void run_rest(f2* b) { passes_ct<720, 5, 4, 9, 4>(b); }
 };
 
 }  // namespace
@@ -264,30 +270,44 @@ __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
   // The row is read ONCE: its complex pairs z_j = (x_2j, x_2j+1) go to
   // registers (all loads issued up front), the least-squares linear detrend
   // sums over finite samples are taken from there, and the detrended values
-  // are written to LDS.  (NaN -> trend line, so a slow trend does not leak
+  // feed the transform.  (NaN -> trend line, so a slow trend does not leak
   // into the low-frequency bins.)  Time is centred (tc = t - (Nr-1)/2), so
   // sum tc and sum tc^2 over ALL samples are closed forms and only the
   // missing samples' terms are accumulated (a branch no wave takes on a
   // complete row); the sample sums are packed (x, y) fp32 per thread, the
   // cross-lane sums fp64.  Branch-free: a wave of 40 divergent if-blocks
   // per row cost more than the butterflies of a pass.
-  constexpr int NPT = MAXN / kThreads;        // complex values per thread
-  constexpr bool FULL = FN > 0 && FN % kThreads == 0;
-  f2 z[NPT];
+  // Element e of a thread: fixed plans load in the first pass's order
+  // (butterfly jb = tid + 256 (e / R1), input q = e % R1 at jb + q N/R1), so
+  // that pass runs on the registers -- no LDS write + read of the row and
+  // one barrier fewer; the run-time plan loads z_j, j = tid + 256 e.
+  constexpr bool FIX = FN > 0;
+  constexpr int R1 = FIX ? FixedPlan<FN>::R1 : 1;
+  constexpr int NB1 = FIX ? FN / R1 : 1;                          // first-pass butterflies
+  constexpr int MB = FIX ? (NB1 + kThreads - 1) / kThreads : 1;   // butterflies per thread
+  constexpr int NE = FIX ? MB * R1 : MAXN / kThreads;             // elements per thread
+  auto eidx = [&](int e) -> int {
+    return FIX ? tid + kThreads * (e / R1) + (e % R1) * NB1 : tid + kThreads * e;
+  };
+  auto evalid = [&](int e) -> bool {
+    if constexpr (FIX) return (e / R1 + 1) * kThreads <= NB1 || tid + kThreads * (e / R1) < NB1;
+    else return tid + kThreads * e < N;
+  };
+  f2 z[NE];
 #pragma unroll
-  for (int i = 0; i < NPT; ++i) {
-    const int j = tid + i * kThreads;
-    z[i] = (FULL || j < N) ? reinterpret_cast<const f2*>(xr)[j] : (f2){0.f, 0.f};
-  }
+  for (int e = 0; e < NE; ++e) z[e] = evalid(e) ? reinterpret_cast<const f2*>(xr)[eidx(e)] : (f2){0.f, 0.f};
   const float tmid = 0.5f * (float)(Nr - 1);
-  const f2 tbase = (f2){(float)(2 * tid) - tmid, (float)(2 * tid) + 1.f - tmid};
+  auto etime = [&](int e) -> f2 {
+    const float t = (float)(2 * eidx(e)) - tmid;
+    return (f2){t, t + 1.f};
+  };
   f2 s2 = (f2){0.f, 0.f}, sx2 = (f2){0.f, 0.f};
   bool bad = false;
 #pragma unroll
-  for (int i = 0; i < NPT; ++i) {
-    const f2 t2 = tbase + (float)(2 * kThreads * i);
-    const bool okx = isfinite(z[i].x), oky = isfinite(z[i].y);
-    const f2 xv = (f2){okx ? z[i].x : 0.f, oky ? z[i].y : 0.f};
+  for (int e = 0; e < NE; ++e) {
+    const f2 t2 = etime(e);
+    const bool okx = isfinite(z[e].x), oky = isfinite(z[e].y);
+    const f2 xv = (f2){okx ? z[e].x : 0.f, oky ? z[e].y : 0.f};
     s2 += xv;
     sx2 += t2 * xv;
     bad |= !(okx && oky);
@@ -297,10 +317,10 @@ __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
   float cn = 0.f, stn = 0.f, sttn = 0.f;      // missing samples: count, sum tc, sum tc^2
   if (__any(bad)) {
 #pragma unroll
-    for (int i = 0; i < NPT; ++i) {
-      const f2 t2 = tbase + (float)(2 * kThreads * i);
-      const bool inb = FULL || tid + i * kThreads < N;
-      const float mx = (inb && !isfinite(z[i].x)) ? 1.f : 0.f, my = (inb && !isfinite(z[i].y)) ? 1.f : 0.f;
+    for (int e = 0; e < NE; ++e) {
+      const f2 t2 = etime(e);
+      const bool inb = evalid(e);
+      const float mx = (inb && !isfinite(z[e].x)) ? 1.f : 0.f, my = (inb && !isfinite(z[e].y)) ? 1.f : 0.f;
       cn += mx + my;
       stn += mx * t2.x + my * t2.y;
       sttn += mx * t2.x * t2.x + my * t2.y * t2.y;
@@ -329,27 +349,42 @@ __global__ __launch_bounds__(kThreads) void fft_seasonal_kernel(
   const float slope = (float)slope_d;
   // e = x - mu - slope (tc - tbar) = x - c0 - slope tc
   const float c0 = (float)((dc > 0 ? xbar : 0.0) - slope_d * tbar);
-  // detrended samples -> LDS, with the Parseval terms: sum e^2, and
+  // detrended samples (in place), with the Parseval terms: sum e^2, and
   // ex = (sum e_even, sum e_odd): X_0 = ex.x + ex.y, X_N = ex.x - ex.y
   f2 e2v = (f2){0.f, 0.f}, ex = (f2){0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < NPT; ++i) {
-    const int j = tid + i * kThreads;
-    if (FULL || (FN > 0 && i < NPT - 1) || j < N) {
-      const f2 t2 = tbase + (float)(2 * kThreads * i);
-      f2 e = (z[i] - c0) - slope * t2;
-      e.x = isfinite(z[i].x) ? e.x : 0.f;
-      e.y = isfinite(z[i].y) ? e.y : 0.f;
-      buf[j] = e;
-      e2v += e * e;
-      ex += e;
+  for (int e = 0; e < NE; ++e) {
+    if (evalid(e)) {
+      f2 v = (z[e] - c0) - slope * etime(e);
+      v.x = isfinite(z[e].x) ? v.x : 0.f;
+      v.y = isfinite(z[e].y) ? v.y : 0.f;
+      z[e] = v;
+      e2v += v * v;
+      ex += v;
     }
   }
   float e2 = e2v.x + e2v.y, x0 = ex.x + ex.y, xn = ex.x - ex.y;
-  __syncthreads();
-  if constexpr (FN > 0) {
-    FixedPlan<FN>::run(buf);
+  if constexpr (FIX) {
+    // first pass (Ns = 1: no twiddles) on the registers, outputs to LDS
+#pragma unroll
+    for (int bb = 0; bb < MB; ++bb) {
+      if (evalid(bb * R1)) {
+        f2 v[R1];
+#pragma unroll
+        for (int q = 0; q < R1; ++q) v[q] = z[bb * R1 + q];
+        dft<R1>(v);
+        const int jb = tid + kThreads * bb;
+#pragma unroll
+        for (int p = 0; p < R1; ++p) buf[jb * R1 + p] = v[p];
+      }
+    }
+    __syncthreads();
+    FixedPlan<FN>::run_rest(buf);
   } else {
+#pragma unroll
+    for (int e = 0; e < NE; ++e)
+      if (evalid(e)) buf[eidx(e)] = z[e];
+    __syncthreads();
     int Ns = 1;
     for (int ps = 0; ps < plan.n_pass; ++ps) {
       const int r = plan.radix[ps];
