@@ -134,12 +134,17 @@ def main(argv=None) -> int:
         return 0
     if cmd == "manifests":
         from .deploy.manifests import write
-        for p in write(rest[0] if rest else "deploy/foremast"):
+        mp = argparse.ArgumentParser(prog="foremast manifests", description="write the deploy bundle")
+        mp.add_argument("out_dir", nargs="?", default="deploy/foremast")
+        for p in write(mp.parse_args(rest).out_dir):
             print(p)
         return 0
     if cmd == "validate":
         import yaml
-        docs = [d for f in rest for d in yaml.safe_load_all(open(f))]
+        vp = argparse.ArgumentParser(prog="foremast validate",
+                                     description="check DeploymentMonitor / DeploymentMetadata YAML against the CRD schema")
+        vp.add_argument("files", nargs="+")
+        docs = [d for f in vp.parse_args(rest).files for d in yaml.safe_load_all(open(f))]
         errs = validate_docs(docs)
         for e in errs:
             print(e)

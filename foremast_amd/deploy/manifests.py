@@ -451,6 +451,34 @@ def elasticsearch(replicas: int = 1) -> list[dict]:
     return [svc, sts]
 
 
+def sidecar_example(app: str = "example-app", namespace: str = "default", app_port: int = 8080,
+                    side_port: int = 8081) -> list[dict]:
+    """An app WITHOUT the metrics starter (any runtime; a Spring Boot JVM
+    here) with the foremast-metrics sidecar in its pod: the Service sends
+    traffic to the sidecar, which proxies to the app on localhost, records the
+    request series (caller tag from X-CALLER) and, with the actuator bridge,
+    re-exports the app's JVM / Tomcat meters.  Prometheus scrapes the sidecar's
+    /actuator/prometheus (pod annotations).  The app container is a
+    placeholder image."""
+    side = {"name": "foremast-metrics-sidecar", "image": IMAGE,
+            "command": ["python", "-m", "foremast_amd.cli", "sidecar"],
+            "env": _env({"SIDECAR_PORT": side_port, "SIDECAR_UPSTREAM": f"http://127.0.0.1:{app_port}",
+                         "SIDECAR_ACTUATOR_BRIDGE": "true", "APP_NAME": app}),
+            "ports": [{"name": "http", "containerPort": side_port}],
+            "readinessProbe": {"httpGet": {"path": "/actuator/prometheus", "port": side_port}}}
+    main = {"name": app, "image": f"{app}:latest",
+            "env": _env({"MANAGEMENT_ENDPOINTS_WEB_EXPOSURE_INCLUDE": "health,metrics"}),
+            "ports": [{"name": "app", "containerPort": app_port}]}
+    dep = _deployment(app, [main, side])
+    dep["metadata"]["namespace"] = namespace
+    dep["spec"]["template"]["metadata"]["annotations"] = {
+        "prometheus.io/scrape": "true", "prometheus.io/port": str(side_port),
+        "prometheus.io/path": "/actuator/prometheus"}
+    svc = _service(app, 80, side_port)
+    svc["metadata"]["namespace"] = namespace
+    return [dep, svc]
+
+
 def bundle() -> dict[str, list[dict]]:
     return {
         "00-namespace.yaml": [{"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NS}}],
@@ -463,6 +491,7 @@ def bundle() -> dict[str, list[dict]]:
         "31-brain.yaml": brain(),
         "40-custom-metrics.yaml": custom_metrics(),
         "50-elasticsearch.yaml": elasticsearch(),
+        "60-sidecar-example.yaml": sidecar_example(),
     }
 
 

@@ -175,3 +175,18 @@ def test_custom_metrics_adapter_and_es_objects():
     env = {e["name"]: e["value"] for e in dep["spec"]["template"]["spec"]["containers"][1]["env"]}
     assert env["BRAIN_CHECKPOINT_DIR"].startswith("/data/")
     assert dep["spec"]["template"]["spec"]["terminationGracePeriodSeconds"] >= 30
+
+
+def test_sidecar_example_manifest():
+    from foremast_amd.deploy import manifests as MF
+    dep, svc = MF.sidecar_example("shop", "prod", 8080, 8081)
+    cs = {c["name"]: c for c in dep["spec"]["template"]["spec"]["containers"]}
+    side = cs["foremast-metrics-sidecar"]
+    assert side["command"][-1] == "sidecar"
+    env = {e["name"]: e["value"] for e in side["env"]}
+    assert env["SIDECAR_UPSTREAM"] == "http://127.0.0.1:8080" and env["SIDECAR_ACTUATOR_BRIDGE"] == "true"
+    assert env["APP_NAME"] == "shop"
+    assert svc["spec"]["ports"][0]["targetPort"] == 8081 and svc["metadata"]["namespace"] == "prod"
+    ann = dep["spec"]["template"]["metadata"]["annotations"]
+    assert ann["prometheus.io/port"] == "8081" and ann["prometheus.io/path"] == "/actuator/prometheus"
+    assert "60-sidecar-example.yaml" in MF.bundle()
