@@ -136,6 +136,9 @@ def main() -> None:
                          "ahead of the previous tick's decision / RCCL all-gather / copy kernels; 1:3 and 1:4 "
                          "measure within 1%% of each other on one GPU)")
     ap.add_argument("--trace", default="", help="write a torch.profiler chrome trace of 5 extra steps (rank 0)")
+    ap.add_argument("--rccl-self", action="store_true",
+                    help="one GPU only: publish through a world-1 RCCL group (real all_gather_into_tensor host path "
+                         "and kernel) to rehearse the multi-rank publish cost on a 1-GPU box")
     args = ap.parse_args()
 
     if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -155,6 +158,16 @@ def main() -> None:
     torch.cuda.set_device(dev)
     info = D.init_distributed(device=dev)
     world = info.world
+    gather = D.all_gather_rows
+    if args.rccl_self and world == 1:
+        import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        tdist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=dev)
+
+        def gather(local, out):
+            tdist.all_gather_into_tensor(out, local)
+            return out
     S, M = args.services, args.metrics
     aliases = (ALIASES * ((M + len(ALIASES) - 1) // len(ALIASES)))[:M]
 
@@ -211,7 +224,7 @@ def main() -> None:
         with torch.cuda.stream(comm):
             if split:
                 decides[slot]()
-            g = D.all_gather_rows(packed[slot], gathered)
+            g = gather(packed[slot], gathered)
             if info.is_main:
                 LIB.call("fm_copy_d2h_async", hosts[slot].data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
         done.record(comm)
@@ -293,6 +306,7 @@ def main() -> None:
                 "comm_overlap": "decision + all-gather + host copy of tick k on a comm stream || tick k+1"
                                 if split else "all-gather + host copy of tick k on a comm stream || tick k+1",
                 "pipeline_depth": depth,
+                **({"rccl_self": True} if args.rccl_self and world == 1 else {}),
             },
             "services_flagged": n_anom,
         }
@@ -309,7 +323,7 @@ def main() -> None:
                 run(1)
         if info.is_main:
             prof.export_chrome_trace(args.trace)
-    if D.is_dist():
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 
@@ -362,7 +376,7 @@ def run_cpu(args, info) -> None:
                        "device": "cpu"},
             "services_flagged": int((verdict[:, 0] == 1).sum()),
         }))
-    if D.is_dist():
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 
