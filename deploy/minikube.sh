@@ -11,6 +11,15 @@ minikube start \
   --memory="${MEMORY:-8192}" \
   --extra-config=kubelet.authentication-token-webhook=true \
   --extra-config=kubelet.authorization-mode=Webhook
+# The recording rules (22-recording-rules.yaml, a PrometheusRule) and the
+# scrape annotations need the Prometheus operator (the reference vendors the
+# coreos bundle under deploy/prometheus-operator/).  Point KUBE_PROMETHEUS at
+# a kube-prometheus checkout to install it first.
+if [ -n "${KUBE_PROMETHEUS:-}" ]; then
+  kubectl apply --server-side -f "$KUBE_PROMETHEUS/manifests/setup"
+  kubectl wait --for condition=Established --all CustomResourceDefinition --namespace=monitoring
+  kubectl apply -f "$KUBE_PROMETHEUS/manifests/"
+fi
 python -m foremast_amd.cli manifests deploy/foremast
 kubectl apply -f deploy/foremast/00-namespace.yaml -f deploy/foremast/10-crds.yaml
 kubectl apply -f deploy/foremast/
