@@ -139,6 +139,12 @@ def main() -> None:
     ap.add_argument("--rccl-self", action="store_true",
                     help="one GPU only: publish through a world-1 RCCL group (real all_gather_into_tensor host path "
                          "and kernel) to rehearse the multi-rank publish cost on a 1-GPU box")
+    ap.add_argument("--publish", choices=["eager", "graph"], default="eager",
+                    help="verdict publish of a step (decision + all-gather + host copy on the comm stream): eager "
+                         "calls, or one HIP graph per slot with the RCCL all-gather captured in it")
+    ap.add_argument("--warmup-min-ms", type=float, default=300.0,
+                    help="after the --warmup steps, keep stepping (untimed) until this much warm-up wall time has "
+                         "passed, so the timed steps start at steady-state clocks (all ranks run the same count)")
     args = ap.parse_args()
 
     if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -217,16 +223,25 @@ def main() -> None:
     ev_tick = [torch.cuda.Event() for _ in range(depth)]
     ev1 = [torch.cuda.Event() for _ in range(depth)]
 
+    pub_graphs: list = []
+
+    def publish_body(slot: int) -> None:
+        if split:
+            decides[slot]()
+        g = gather(packed[slot], gathered)
+        if info.is_main:
+            LIB.call("fm_copy_d2h_async", hosts[slot].data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
+
     def publish(slot: int, done) -> None:
         """comm stream: all-gather of the slot's verdicts (RCCL over xGMI) and
-        rank 0's copy of the fleet verdict to pinned host memory."""
+        rank 0's copy of the fleet verdict to pinned host memory (eager, or
+        the slot's captured graph: one launch instead of three host calls)."""
         comm.wait_event(ev_tick[slot])
         with torch.cuda.stream(comm):
-            if split:
-                decides[slot]()
-            g = gather(packed[slot], gathered)
-            if info.is_main:
-                LIB.call("fm_copy_d2h_async", hosts[slot].data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
+            if pub_graphs:
+                pub_graphs[slot].replay()
+            else:
+                publish_body(slot)
         done.record(comm)
 
     # Steps are issued up to `depth` ahead, so the GPU runs ticks back to back
@@ -243,7 +258,26 @@ def main() -> None:
                 ev_tick[slot].record(compute)
                 publish(slot, ev1[slot])
 
+    tw = time.perf_counter()
     run(args.warmup)
+    if args.publish == "graph":
+        graphs = []
+        for slot in range(depth):
+            gr = torch.cuda.CUDAGraph()
+            comm.wait_event(ev_tick[slot])
+            with torch.cuda.graph(gr, stream=comm):
+                publish_body(slot)
+            graphs.append(gr)
+        pub_graphs[:] = graphs
+        run(max(1, args.warmup))
+    torch.cuda.synchronize(dev)
+    # untimed steps until the warm-up has lasted --warmup-min-ms: every rank
+    # derives the same count from the MAX over ranks of the measured step time
+    w_ms = (time.perf_counter() - tw) * 1e3
+    per = D.all_reduce_max(w_ms / max(1, args.warmup + (args.warmup if args.publish == "graph" else 0)), dev)
+    w_ms = D.all_reduce_max(w_ms, dev)
+    extra = 0 if w_ms >= args.warmup_min_ms else min(100000, int((args.warmup_min_ms - w_ms) / max(per, 1e-3)) + 1)
+    run(extra)
     D.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -284,6 +318,7 @@ def main() -> None:
             "backend": backend,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_extra_steps": extra,
             "ms_per_step": ms,
             "p50_decision_latency_ms": p50 * 1e3,
             "higher_is_better": True,
@@ -306,6 +341,7 @@ def main() -> None:
                 "comm_overlap": "decision + all-gather + host copy of tick k on a comm stream || tick k+1"
                                 if split else "all-gather + host copy of tick k on a comm stream || tick k+1",
                 "pipeline_depth": depth,
+                "publish": args.publish,
                 **({"rccl_self": True} if args.rccl_self and world == 1 else {}),
             },
             "services_flagged": n_anom,
