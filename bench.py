@@ -95,6 +95,15 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
     return rc
 
 
+def extra_warmup_steps(warm_ms: float, per_step_ms: float, min_ms: float, cap: int = 100000) -> int:
+    """Untimed steps still needed for the warm-up to last ``min_ms``.  Called
+    with MAX-reduced inputs, so every rank gets the same count and the
+    collectives of those steps pair up."""
+    if warm_ms >= min_ms:
+        return 0
+    return min(cap, int((min_ms - warm_ms) / max(per_step_ms, 1e-3)) + 1)
+
+
 def _device_census(info, dev) -> tuple[int, str]:
     """(distinct devices across ranks, backend).  Ranks sharing one GPU
     (FOREMAST_DEVICE_INDEX rehearsal over gloo) count once."""
@@ -287,7 +296,7 @@ def main() -> None:
     w_ms = (time.perf_counter() - tw) * 1e3
     per = D.all_reduce_max(w_ms / max(1, args.warmup + (args.warmup if args.publish == "graph" else 0)), dev)
     w_ms = D.all_reduce_max(w_ms, dev)
-    extra = 0 if w_ms >= args.warmup_min_ms else min(100000, int((args.warmup_min_ms - w_ms) / max(per, 1e-3)) + 1)
+    extra = extra_warmup_steps(w_ms, per, args.warmup_min_ms)
     run(extra)
     D.barrier()
     torch.cuda.synchronize(dev)

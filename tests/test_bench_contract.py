@@ -72,3 +72,17 @@ def test_bench_rejects_gpus_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = _bench_cpu("--gpus", "2", env=env)
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_extra_warmup_steps_count():
+    """The untimed warm-up top-up: zero once the warm-up lasted long enough,
+    otherwise enough steps to reach the minimum at the (MAX-reduced) step
+    time, capped; a pure function of its inputs, so ranks agree."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.extra_warmup_steps(400.0, 0.5, 300.0) == 0
+    assert bench.extra_warmup_steps(300.0, 0.5, 300.0) == 0
+    n = bench.extra_warmup_steps(2.75, 0.55, 300.0)
+    assert 2.75 + n * 0.55 >= 300.0 and 2.75 + (n - 2) * 0.55 < 300.0
+    assert bench.extra_warmup_steps(0.0, 0.0, 300.0, cap=1000) == 1000
+    assert bench.extra_warmup_steps(1.0, 0.08, 0.0) == 0
