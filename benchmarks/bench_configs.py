@@ -56,6 +56,32 @@ def _common(args, info, ms, p50, metric, value, unit, model, global_batch, seq_l
     emit(info, **out)
 
 
+def start_service(store_spec: str):
+    """The REST service in its own process (uvicorn on 127.0.0.1), as
+    deployed next to the brain (deploy/foremast/31-brain.yaml).  -> (proc, port)"""
+    import socket
+    import subprocess
+    import httpx
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    server = subprocess.Popen([sys.executable, "-m", "foremast_amd.cli", "service", "--port", str(port), "--store",
+                               store_spec], cwd=root, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    deadline = time.time() + 120
+    while True:
+        try:
+            if httpx.get(f"http://127.0.0.1:{port}/healthz", timeout=1).status_code == 200:
+                return server, port
+        except Exception:
+            pass
+        if time.time() > deadline or server.poll() is not None:
+            server.kill()
+            raise SystemExit("REST service did not start")
+        time.sleep(0.2)
+
+
 # --------------------------------------------------------------------------- config 1
 def config1(args):
     from foremast_amd.api import crd
@@ -72,31 +98,11 @@ def config1(args):
     # own process (uvicorn on 127.0.0.1) sharing a WAL SQLite job store with the
     # brain; the client side (barrelman / trigger role) talks HTTP with a pooled
     # keep-alive connection
-    import socket
-    import subprocess
     import tempfile
-
-    sock = socket.socket()
-    sock.bind(("127.0.0.1", 0))
-    port = sock.getsockname()[1]
-    sock.close()
     db = os.path.join(tempfile.mkdtemp(prefix="fm_c1_"), "jobs.db")
     store = SQLiteStore(db)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    server = subprocess.Popen([sys.executable, "-m", "foremast_amd.cli", "service", "--port", str(port), "--store",
-                               f"sqlite:{db}"], cwd=root, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    server, port = start_service(f"sqlite:{db}")
     client = AnalystClient(f"http://127.0.0.1:{port}/v1/healthcheck/", clock=clock)
-    deadline = time.time() + 120
-    while True:
-        try:
-            import httpx
-            if httpx.get(f"http://127.0.0.1:{port}/healthz", timeout=1).status_code == 200:
-                break
-        except Exception:
-            pass
-        if time.time() > deadline or server.poll() is not None:
-            raise SystemExit("REST service did not start")
-        time.sleep(0.2)
     cfg = BrainConfig()
     cfg.pairwise_algorithm = "TTEST"
     cfg.ml_algorithm = "moving_average_all"
@@ -209,13 +215,19 @@ def config3(args):
 # --------------------------------------------------------------------------- config 3e2e
 def config3e2e(args):
     """The production brain (``Brain.run_once``) on the config-3 fleet: 10k
-    canary jobs x 8 metrics (5 + 5 pods x 10 points, 7-day history) in the job
-    store, one cycle = claim -> fetch current/baseline -> stage -> resident
-    tick (pairwise + moving_average_all + decision, GPU) -> compaction ->
-    verdicts -> exporter gauges -> bulk store update (+ the C2 exporter
-    gather on several ranks).  Series are pre-staged in memory (the first,
-    untimed cycle fetches and stages them, history into the device-resident
-    store); the fetch span is reported separately."""
+    canary jobs x 8 metrics (5 + 5 pods x 10 points, 7-day history), one
+    cycle = claim -> fetch current/baseline -> stage -> resident tick
+    (pairwise + moving_average_all + decision, GPU) -> compaction -> verdicts
+    -> exporter gauges -> store update.
+
+    ``--store sqlite`` (default) is the shipped topology
+    (deploy/foremast/31-brain.yaml): the REST service runs in its own process
+    on a WAL SQLite file, jobs are submitted over HTTP, every brain rank opens
+    the same file, and while the cycles are timed a barrelman-shaped poller
+    (``--rest-poll-rps``, default: every job every 10 s) reads job statuses
+    through the service.  ``--store memory`` is the single-process store.
+    Series are pre-staged in memory (the first, untimed cycle fetches and
+    stages them, history into the device-resident store)."""
     from foremast_amd.api import crd
     from foremast_amd.api import jobs as J
     from foremast_amd.api.models import ApplicationHealthAnalyzeRequest
@@ -223,43 +235,76 @@ def config3e2e(args):
     from foremast_amd.engine.brain import Brain
     from foremast_amd.engine.exporter import BrainExporter
     from foremast_amd.engine.sources import SourceRouter, StagedSource, SyntheticSource
-    from foremast_amd.service.store import MemoryStore
+    from foremast_amd.service.store import MemoryStore, SQLiteStore
     import json as _json
+    import subprocess
+    import tempfile
 
     info, dev = setup(gpus_required=args.device != "cpu")
     dev = torch.device("cpu") if args.device == "cpu" else dev
     S, M, P = args.services, args.metrics, args.pods
     t = {"now": 1_760_000_000.0}
     clock = lambda: t["now"]
-    store = MemoryStore()
-
-    def do(method, url, body):                 # the service's create handler, in-process
-        req = ApplicationHealthAnalyzeRequest.from_dict(_json.loads(body))
-        jid, _ = store.create(J.build_document(req))
-        return Response(200, _json.dumps(J.new_response(jid, 0, "new")).encode())
-    client = AnalystClient("http://foremast-service/v1/healthcheck/", do, clock)
     names = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
     mons = [crd.Monitoring(f"http_server_requests_{a}", "gauge", a) for a in (names * 2)[:M]]
     metrics = crd.Metrics("prometheus", "http://prom/api/v1/", mons)
+    server = poller = None
+    t_sub = 0.0
+    ids: list[str] = []
+
+    def submit(client):
+        for j in range(S):
+            ids.append(client.start_analyzing("default", f"svc{j}",
+                                              [[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
+                                               [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]],
+                                              metrics, args.window, "canary"))
+
+    if args.store == "memory":
+        store = MemoryStore()
+
+        def do(method, url, body):                 # the service's create handler, in-process
+            req = ApplicationHealthAnalyzeRequest.from_dict(_json.loads(body))
+            jid, _ = store.create(J.build_document(req))
+            return Response(200, _json.dumps(J.new_response(jid, 0, "new")).encode())
+        if info.is_main:
+            t_sub = time.perf_counter()
+            submit(AnalystClient("http://foremast-service/v1/healthcheck/", do, clock))
+            t_sub = time.perf_counter() - t_sub
+        if D.is_dist():
+            raise SystemExit("--store memory is one process; use --store sqlite for several ranks")
+    else:
+        db = os.path.join(tempfile.mkdtemp(prefix="fm_3e2e_"), "jobs.db") if info.is_main else None
+        db = D.broadcast_object(db)
+        if info.is_main:
+            SQLiteStore(db)
+            server, port = start_service(f"sqlite:{db}")
+            t_sub = time.perf_counter()
+            submit(AnalystClient(f"http://127.0.0.1:{port}/v1/healthcheck/", clock=clock))
+            t_sub = time.perf_counter() - t_sub
+        D.barrier()
+        store = SQLiteStore(db)
+    print(f"[3e2e] rank {info.rank}: {S} jobs submitted in {t_sub:.1f}s ({args.store})", file=sys.stderr, flush=True)
     faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, S, 50)}    # 2% of services regress
     staged = StagedSource(SyntheticSource(faults=faults, fault_after=t["now"] - 3600))
     cfg = BrainConfig()
     exp = BrainExporter()
     brain = Brain(store, cfg, device=dev, sources=SourceRouter(synthetic=staged, force="synthetic"), clock=clock,
                   batch_size=S + 1, worker_id=f"bench-{info.rank}", exporter=exp, history_days=args.history_days)
-    t_sub = time.perf_counter()
-    for j in range(S):
-        client.start_analyzing("default", f"svc{j}", [[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
-                                                      [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]],
-                               metrics, args.window, "canary")
-    t_sub = time.perf_counter() - t_sub
-    print(f"[3e2e] submitted {S} jobs in {t_sub:.1f}s", file=sys.stderr, flush=True)
     t["now"] += args.poll_seconds
     t_first = time.perf_counter()
     first = brain.run_once()                    # fetch + stage history (untimed)
     t_first = time.perf_counter() - t_first
-    print(f"[3e2e] first cycle (fetch + stage history) {t_first:.1f}s: {first}", file=sys.stderr, flush=True)
+    print(f"[3e2e] rank {info.rank}: first cycle (fetch + stage history) {t_first:.1f}s: "
+          f"claimed {first.get('claimed')}", file=sys.stderr, flush=True)
     rows, spans = [], {}
+    if server is not None and args.rest_poll_rps > 0:
+        idf = os.path.join(os.path.dirname(db), "ids.txt")
+        with open(idf, "w") as f:
+            f.write("\n".join(ids))
+        poller = subprocess.Popen([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                "rest_poller.py"), "--url", f"http://127.0.0.1:{port}",
+                                   "--ids", idf, "--rps", str(args.rest_poll_rps)],
+                                  stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
 
     def step():
         # cycles every poll interval inside the jobs' watch window (the
@@ -270,20 +315,39 @@ def config3e2e(args):
         for k, v in brain.spans.last.items():
             spans.setdefault(k, []).append(v * 1e3)
 
-    ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    poll = None
+    try:
+        ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+    finally:
+        if poller is not None:
+            poller.terminate()
+            try:
+                out, _ = poller.communicate(timeout=30)
+                poll = _json.loads(out.strip().splitlines()[-1]) if out.strip() else None
+            except Exception:  # noqa: BLE001 - the poller's report is informational
+                poller.kill()
+        if server is not None:
+            server.terminate()
+            server.wait(30)
     timed = rows[args.warmup:]
     per_cycle = sum(timed) / max(1, len(timed))
-    windows = D.all_reduce_max(float(per_cycle), torch.device("cpu") if dev.type == "cpu" else dev)
-    total_rows = per_cycle * info.world if D.is_dist() else per_cycle
+    cpu = torch.device("cpu") if dev.type == "cpu" else dev
+    windows = D.all_reduce_max(float(per_cycle), cpu)
+    total_rows = sum(D.all_gather_object(per_cycle)) if D.is_dist() else per_cycle
     span_ms = {k: round(statistics.median(v[args.warmup:] or v), 3) for k, v in spans.items()}
+    # per-rank claim / persist spans, max over ranks (the store is shared)
+    worst = {k: round(D.all_reduce_max(span_ms.get(k, 0.0), cpu), 3) for k in ("claim", "persist")}
     _common(args, info, ms, p50, "metric windows scored/sec (node), production brain cycle (Brain.run_once) "
             "on the 10k-service canary fleet", total_rows / (ms / 1e3), "windows/s",
             "Brain.run_once: claim + fetch (pre-staged) + resident tick (moving_average_all + pairwise ALL) + "
-            "compaction + verdicts + exporter + bulk store update", S * M, int(args.history_days * 1440) + 1,
+            "compaction + verdicts + exporter + store update", S * M, int(args.history_days * 1440) + 1,
             "strong", "fp32" if dev.type != "cpu" else "fp32 data / fp64 statistics",
             "synthetic Prometheus-shaped series (pre-staged in memory; 2% of services regress)",
-            {"services": S, "metrics": M, "pods_per_side": P, "rows_per_cycle_rank0": per_cycle,
-             "rows_per_cycle_max_rank": windows, "span_ms_median_rank0": span_ms,
+            {"services": S, "metrics": M, "pods_per_side": P, "store": args.store,
+             "topology": ("REST service in its own process + every rank on one WAL SQLite file"
+                          if args.store == "sqlite" else "single process, in-memory store"),
+             "rest_poller": poll, "rows_per_cycle_rank0": per_cycle, "rows_per_cycle_max_rank": windows,
+             "span_ms_median_rank0": span_ms, "span_ms_median_max_rank": worst,
              # untimed: dominated by the host-side synthetic generator (counter-hash noise for 80k
              # 7-day series in numpy, ~1 ms per series), not by the brain's fetch / stage path
              "first_cycle_s (synthetic generation + fetch + stage history, untimed)": round(t_first, 3),
@@ -389,9 +453,15 @@ def main():
     ap.add_argument("--history-days", type=float, default=7.0, help="config 3e2e: history window")
     ap.add_argument("--poll-seconds", type=float, default=1.0, help="config 3e2e: clock advance per cycle (the "
                     "jobs' 10-minute watch window must outlive warmup + steps)")
+    ap.add_argument("--store", default="sqlite", choices=["sqlite", "memory"], help="config 3e2e: job store "
+                    "(sqlite: the shipped topology, REST service in its own process)")
+    ap.add_argument("--rest-poll-rps", type=float, default=None, help="config 3e2e + sqlite: barrelman-shaped "
+                    "GET /v1/healthcheck/id load during the timed cycles (default: services / 10 s)")
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "
                     "the fitted-model cache")
     args = ap.parse_args()
+    if args.rest_poll_rps is None:
+        args.rest_poll_rps = args.services / 10.0
     {"1": config1, "2": config2, "3": config3, "3e2e": config3e2e, "4": config4, "5": config5}[args.config](args)
 
 

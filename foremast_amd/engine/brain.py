@@ -51,6 +51,9 @@ from .sources import Series, SourceError, SourceRouter, substitute_window
 log = logging.getLogger("foremast.brain")
 
 MAX_T = 16384
+# the verdict of a job re-examined next cycle (store.keep: back to
+# ``preprocess_completed``, or simply kept leased by a sticky-lease store)
+KEEP = {"status": ST.PREPROCESS_COMPLETED}
 
 
 @dataclass
@@ -414,8 +417,15 @@ class Brain:
             if hpalogs:
                 self.store.add_hpalogs(hpalogs)
             for ids, fields, handles in bulk:
-                self.store.update_uniform(ids, fields, now=now, handles=handles)
-            self.store.update_many(updates)
+                if fields == KEEP:
+                    self.store.keep(self.worker, ids, now=now, handles=handles)
+                else:
+                    self.store.update_uniform(ids, fields, now=now, handles=handles, worker=self.worker)
+            keep = [i for i, f in updates if f == KEEP]
+            if keep:
+                self.store.keep(self.worker, keep, now=now)
+                updates = [u for u in updates if u[1] != KEEP]
+            self.store.update_many(updates, now=now, worker=self.worker)
         if self.exporter is not None:
             self.exporter.tick_seconds.observe(time.perf_counter() - t0)
             self.exporter.windows.inc(n_rows)

@@ -129,6 +129,15 @@ def broadcast_object(obj, src: int = 0):
     return lst[0]
 
 
+def all_gather_object(obj) -> list:
+    """Small host objects from every rank (end-of-run reports)."""
+    if not is_dist():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def cluster_groups(n_clusters: int):
     """C5: one process subgroup per synthetic cluster (ranks split round-robin
     when world >= n_clusters, otherwise every rank hosts several clusters and

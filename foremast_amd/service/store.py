@@ -3,9 +3,12 @@ foremast-service/pkg/search/elasticsearchstore.go:17-21, behind one interface
 with three backends:
 
 * :class:`MemoryStore` — in-process (tests, single-process deployments);
-* :class:`SQLiteStore` — file-backed, safe for several brain/service processes
-  on one host (lease claims are single SQL transactions);
-* :class:`ElasticsearchStore` — the reference's ES 6 indexes over the REST API.
+* :class:`SQLiteStore` — file-backed, shared by the REST service and every
+  brain rank of a node: columnar status / lease / owner-hash columns, claims
+  as one ``UPDATE ... RETURNING`` per cycle, sticky per-worker leases with a
+  change feed (see the class docstring);
+* :class:`ElasticsearchStore` — the reference's ES 6 indexes over the REST API
+  (claims as one ``search_after`` scan + one conditional ``_bulk``).
 
 Lease semantics (docs/guides/design.md:37-41, foremast-brain/README.md:29):
 ``claim`` atomically moves claimable jobs (``initial``/``preprocess_completed``)
@@ -16,7 +19,9 @@ taken over.
 """
 from __future__ import annotations
 
+import collections
 import dataclasses
+import hashlib
 import json
 import sqlite3
 import threading
@@ -112,17 +117,26 @@ class JobStore(ABC):
         self.put(d)
         return d
 
-    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None, worker: str | None = None) -> None:
         """Apply ``(job id, fields)`` updates in one batch (one transaction /
-        one ``_bulk`` request on the persistent backends)."""
+        one ``_bulk`` request on the persistent backends).  With ``worker``
+        (a brain's verdicts) a store may skip jobs no longer leased to it."""
         for jid, fields in updates:
             self.update(jid, **fields)
 
-    def update_uniform(self, ids, fields: dict, now: float | None = None, handles=None) -> None:
+    def update_uniform(self, ids, fields: dict, now: float | None = None, handles=None,
+                       worker: str | None = None) -> None:
         """The same ``fields`` for many jobs (the brain's per-cycle "still in
         progress" / "healthy" verdicts): one batch.  ``handles`` are the
         store rows a :class:`ClaimBatch` of this store handed out (optional)."""
-        self.update_many([(i, fields) for i in ids], now=now)
+        self.update_many([(i, fields) for i in ids], now=now, worker=worker)
+
+    def keep(self, worker: str, ids, now: float | None = None, handles=None) -> None:
+        """Jobs ``worker`` re-examines next cycle (end time not reached, no
+        anomaly): back to ``preprocess_completed`` ("reprogress" in the state
+        diagram) for the next claim.  Stores with sticky leases keep them
+        leased instead (no write)."""
+        self.update_uniform(ids, {"status": ST.PREPROCESS_COMPLETED}, now=now, handles=handles)
 
     def add_hpalogs(self, logs: list[HPALog]) -> None:
         for lg in logs:
@@ -173,7 +187,7 @@ class MemoryStore(JobStore):
     claiming or updating a 10k-job batch is a few vectorised operations plus
     one attribute store per job, not a decode of every live document."""
 
-    def __init__(self) -> None:
+    def __init__(self, hpalog_keep: int = 256) -> None:
         self._objs: list[Document] = []
         self._index: dict[str, int] = {}
         self._codes: dict[str, int] = {}
@@ -181,7 +195,8 @@ class MemoryStore(JobStore):
         self._st = np.zeros(0, np.int16)
         self._mod = np.zeros(0, np.float64)
         self._owners: dict[int, np.ndarray] = {}
-        self._logs: list[dict] = []
+        self.hpalog_keep = hpalog_keep
+        self._logs: dict[str, collections.deque] = {}
         self._lock = threading.RLock()
         self._claimable = np.zeros(0, bool)
         self._inprog = np.zeros(0, bool)
@@ -289,7 +304,7 @@ class MemoryStore(JobStore):
             self._mod[i] = _ts(d)
             return Document.from_dict(d.to_dict())
 
-    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None, worker: str | None = None) -> None:
         now = time.time() if now is None else now
         stamp = _stamp(now)
         with self._lock:
@@ -308,7 +323,8 @@ class MemoryStore(JobStore):
             self._st[idx[ok]] = codes[ok]
             self._mod[idx[ok]] = _ts_str(stamp)
 
-    def update_uniform(self, ids, fields: dict, now: float | None = None, handles=None) -> None:
+    def update_uniform(self, ids, fields: dict, now: float | None = None, handles=None,
+                       worker: str | None = None) -> None:
         """Vectorised: status codes and lease times are array stores; the
         document objects pick the fields up lazily when next read."""
         if len(ids) == 0:
@@ -399,157 +415,490 @@ class MemoryStore(JobStore):
         return ClaimBatch(ids, vers, resolve, handles=idx)
 
     def add_hpalog(self, log: HPALog) -> None:
-        with self._lock:
-            self._logs.append(log.to_dict())
+        self.add_hpalogs([log])
 
     def add_hpalogs(self, logs: list[HPALog]) -> None:
-        rows = [lg.to_dict() for lg in logs]
+        """Logs are indexed by job and bounded: the newest ``hpalog_keep`` per
+        job are kept (the HPA alert reads the last 4-6, HpaController.go:109-131;
+        GET /v1/healthcheck/id the last 10, main.go:227-255)."""
         with self._lock:
-            self._logs.extend(rows)
+            for lg in logs:
+                q = self._logs.get(lg.job_id)
+                if q is None:
+                    q = self._logs[lg.job_id] = collections.deque(maxlen=self.hpalog_keep)
+                q.append(lg)
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
         with self._lock:
-            rows = [l for l in self._logs if l.get("job_id") == job_id]
-        rows.sort(key=lambda l: l.get("timestamp", 0.0), reverse=True)
-        return [HPALog.from_dict(r) for r in rows[:size]]
+            rows = list(self._logs.get(job_id, ()))
+        rows.sort(key=lambda l: l.timestamp, reverse=True)
+        return [HPALog.from_dict(r.to_dict()) for r in rows[:size]]
+
+
+OWNER_MOD = 720720          # lcm(1..16): owner_key % world == service_owner(...) for every world | OWNER_MOD
+
+
+def owner_hash(namespace: str, app: str) -> int:
+    """The 64-bit hash behind ``parallel.dist.service_owner`` (owner rank =
+    hash % world)."""
+    h = hashlib.blake2b(f"{namespace}:{app}".encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little")
+
+
+# Document fields the brain mutates live in columns; the JSON body keeps the
+# request part, written once per submission (a status change never decodes or
+# re-encodes a body).
+_MUTABLE_JSON = ("status", "modified_at", "processingContent", "reason", "anomalyInfo")
+_COLUMN_OF = {"status": "status", "processing_content": "worker", "reason": "reason", "anomaly_info": "anomaly"}
+_SEL = "status, modified_at, worker, reason, anomaly, body"
+
+
+def _decode_row(status, modified_at, worker, reason, anomaly, body) -> Document:
+    d = json.loads(body)
+    d["status"] = status
+    d["modified_at"] = modified_at
+    if worker:
+        d["processingContent"] = worker
+    if reason:
+        d["reason"] = reason
+    if anomaly:
+        d["anomalyInfo"] = anomaly
+    return Document.from_dict(d)
+
+
+class _Session:
+    """The jobs one worker holds a lease on (SQLiteStore sticky leases):
+    id -> (row id, version), plus the change-feed position."""
+
+    def __init__(self) -> None:
+        self.held: dict[str, tuple[int, int]] = {}
+        self.last_seq = 0
+        self.last_gc = -float("inf")
+        self.last_beat = -float("inf")
+        self.rot = 0
+        self._snap = None
+
+    def add(self, jid: str, rid: int, ver: int) -> None:
+        self.held[jid] = (rid, ver)
+        self._snap = None
+
+    def drop(self, jid: str) -> None:
+        if self.held.pop(jid, None) is not None:
+            self._snap = None
+
+    def snapshot(self, limit: int):
+        if self._snap is None:
+            ids = list(self.held)
+            rv = list(self.held.values())
+            self._snap = (ids, [v for _, v in rv], np.fromiter((r for r, _ in rv), np.int64, len(rv)))
+        ids, vers, rids = self._snap
+        n = len(ids)
+        if n <= limit:
+            return ids, vers, rids
+        # more held than one batch: rotate so every held job is examined in turn
+        off = self.rot % n
+        self.rot += limit
+        sel = (np.arange(limit) + off) % n
+        return [ids[i] for i in sel], [vers[i] for i in sel], rids[sel]
 
 
 class SQLiteStore(JobStore):
-    def __init__(self, path: str) -> None:
-        self.path = path
-        self._local = threading.local()
-        c = self._conn()
-        c.execute("create table if not exists documents (id text primary key, status text, modified real, body text)")
-        c.execute("create table if not exists hpalogs (job_id text, ts real, body text)")
-        c.execute("create index if not exists hpalogs_job on hpalogs(job_id, ts)")
-        c.commit()
+    """File-backed store shared by the REST service and every brain rank of a
+    node (``sqlite:/data/jobs.db`` in deploy/foremast/31-brain.yaml), in WAL
+    mode so readers never block the one writer.
 
+    Fleet-scale layout (the reference claims over ES with a takeover lease,
+    foremast-service/pkg/search/elasticsearchstore.go:98-180,
+    docs/guides/design.md:37-41):
+
+    * ``status`` / ``modified`` / ``worker`` / ``reason`` / ``anomaly`` are
+      columns, authoritative; the JSON body holds the immutable request part
+      and is decoded only when a document is read or first planned;
+    * ``okey`` = the owner hash of ``namespace:app`` (signed 64 bit), so a
+      rank's shard filter is SQL arithmetic, not a body decode;
+    * ``seq`` = a store-wide change counter stamped by every write, ``ver`` =
+      the counter at the last (re)submission;
+    * **sticky leases**: :meth:`claim_batch` keeps a per-worker session of the
+      jobs it leased.  A job the brain re-examines stays
+      ``preprocess_inprogress`` under its lease (externally both that and
+      ``preprocess_completed`` read ``inprogress``, converter.go:10-29) instead
+      of being written back and re-claimed every cycle.  Per cycle the claim is
+      one IMMEDIATE transaction of indexed statements: the change feed
+      (``seq >`` the session's position: resubmissions, aborts, takeovers),
+      an ``UPDATE ... RETURNING`` of newly claimable or stuck jobs, and ONE
+      worker-level lease heartbeat (``leases`` table): a job is stuck when its
+      worker's lease is older than ``MAX_STUCK_IN_SECONDS``, so a live brain's
+      jobs never look stuck while a dead one's are taken over;
+    * verdicts are set-based ``UPDATE``s over ``json_each`` row lists, guarded
+      so a job resubmitted since it was leased is never overwritten.
+    """
+
+    def __init__(self, path: str, hpalog_retention_s: float = 86400.0) -> None:
+        self.path = path
+        self.hpalog_retention_s = hpalog_retention_s
+        self._local = threading.local()
+        self._sessions: dict[str, _Session] = {}
+        self._log_writes = 0
+        self._last_prune = 0.0
+        c = self._conn()
+        c.execute("begin immediate")
+        try:
+            cols = [r[1] for r in c.execute("pragma table_info(documents)")]
+            legacy = bool(cols) and "okey" not in cols
+            if legacy:
+                c.execute("alter table documents rename to documents_v1")
+            c.execute("create table if not exists documents (rid integer primary key, id text not null unique, "
+                      "status text not null, modified real not null, modified_at text not null, "
+                      "worker text not null default '', reason text not null default '', "
+                      "anomaly text not null default '', ver integer not null, seq integer not null, "
+                      "okey integer not null, body text not null)")
+            c.execute("create index if not exists documents_claim on documents(status, modified)")
+            c.execute("create index if not exists documents_seq on documents(seq)")
+            c.execute("create index if not exists documents_worker on documents(worker, status)")
+            c.execute("create table if not exists leases (worker text primary key, beat real not null)")
+            c.execute("create table if not exists meta (k text primary key, v integer not null)")
+            c.execute("insert or ignore into meta values ('seq', 0)")
+            c.execute("create table if not exists hpalogs (job_id text, ts real, body text)")
+            c.execute("create index if not exists hpalogs_job on hpalogs(job_id, ts)")
+            c.execute("create index if not exists hpalogs_ts on hpalogs(ts)")
+            if legacy:                          # round-2 layout: one JSON body per row
+                seq = self._next_seq(c)
+                rows = [self._row(Document.from_dict(json.loads(b)), seq)
+                        for (b,) in c.execute("select body from documents_v1")]
+                c.executemany(self._INSERT, rows)
+                c.execute("drop table documents_v1")
+            # invariant: the worker of every in-progress job has a lease row
+            ip = tuple(sorted(ST.IN_PROGRESS))
+            c.execute(f"insert or ignore into leases select worker, max(modified) from documents "
+                      f"where status in ({','.join('?' * len(ip))}) group by worker", ip)
+            c.execute("commit")
+        except Exception:
+            c.execute("rollback")
+            raise
+
+    # ------------------------------------------------------------------ plumbing
     def _conn(self) -> sqlite3.Connection:
         c = getattr(self._local, "c", None)
         if c is None:
             c = sqlite3.connect(self.path, timeout=30, isolation_level=None)
             c.execute("pragma journal_mode=wal")
-            # WAL + NORMAL: no fsync per autocommit statement; the database stays
-            # consistent on a crash (a power loss may drop the last commits, which
-            # the brain re-derives: job ids are deterministic and claims lease out)
+            # WAL + NORMAL: no fsync per commit; the database stays consistent
+            # on a crash (a power loss may drop the last commits, which the
+            # brain re-derives: job ids are deterministic and claims lease out)
             c.execute("pragma synchronous=normal")
+            c.execute("pragma cache_size=-65536")
+            c.execute("pragma temp_store=memory")
             self._local.c = c
         return c
 
+    class _Txn:
+        def __init__(self, c):
+            self.c = c
+
+        def __enter__(self):
+            self.c.execute("begin immediate")
+            return self.c
+
+        def __exit__(self, et, ev, tb):
+            self.c.execute("commit" if et is None else "rollback")
+            return False
+
+    def _txn(self):
+        return self._Txn(self._conn())
+
+    @staticmethod
+    def _next_seq(c) -> int:
+        return c.execute("update meta set v = v + 1 where k = 'seq' returning v").fetchone()[0]
+
+    _INSERT = ("insert into documents (id, status, modified, modified_at, worker, reason, anomaly, ver, seq, okey, "
+               "body) values (?,?,?,?,?,?,?,?,?,?,?) on conflict(id) do update set status=excluded.status, "
+               "modified=excluded.modified, modified_at=excluded.modified_at, worker=excluded.worker, "
+               "reason=excluded.reason, anomaly=excluded.anomaly, ver=excluded.ver, seq=excluded.seq, "
+               "okey=excluded.okey, body=excluded.body")
+
+    @staticmethod
+    def _row(d: Document, seq: int) -> tuple:
+        body = d.to_dict()
+        for k in _MUTABLE_JSON:
+            body.pop(k, None)
+        h = owner_hash(d.namespace, d.app_name)
+        okey = h - (1 << 64) if h >= (1 << 63) else h
+        return (d.id, d.status, _ts(d), d.modified_at, d.processing_content, d.reason, d.anomaly_info, seq, seq,
+                okey, json.dumps(body))
+
+    @staticmethod
+    def _shard_sql(shard) -> tuple[str, tuple]:
+        """``okey`` (a signed 64-bit view of the unsigned hash) -> owner rank
+        == hash % world, in SQL."""
+        if shard is None or shard[1] <= 1:
+            return "", ()
+        rank, world = shard
+        return (" and (((okey % ?) + (case when okey < 0 then ? else 0 end) + ?) % ?) = ?",
+                (world, (1 << 64) % world, world, world, rank))
+
+    def _sessions_drop(self, ids) -> None:
+        for s in self._sessions.values():
+            if s.held:
+                for j in ids:
+                    s.drop(j)
+
+    @staticmethod
+    def _guard(worker: str | None) -> tuple[str, tuple]:
+        """A brain's verdicts apply only to jobs still leased to it: not
+        resubmitted (worker reset), aborted, or taken over since."""
+        if not worker:
+            return "", ()
+        ip = tuple(sorted(ST.IN_PROGRESS))
+        return f" and worker = ? and status in ({','.join('?' * len(ip))})", (worker,) + ip
+
+    # ------------------------------------------------------------------ documents
+    @staticmethod
+    def _adopt(c, rows) -> None:
+        """In-progress rows written directly (not claimed) get a lease row
+        for their worker, dated at their ``modified``."""
+        live = [(r[4], r[2]) for r in rows if r[1] in ST.IN_PROGRESS]
+        if live:
+            c.executemany("insert or ignore into leases values (?,?)", live)
+
     def put(self, doc: Document) -> None:
-        self._conn().execute("insert or replace into documents values (?,?,?,?)",
-                             (doc.id, doc.status, _ts(doc), json.dumps(doc.to_dict())))
+        self.put_many([doc])
+
+    def put_many(self, docs: list[Document]) -> None:
+        with self._txn() as c:
+            seq = self._next_seq(c)
+            rows = [self._row(d, seq) for d in docs]
+            c.executemany(self._INSERT, rows)
+            self._adopt(c, rows)
 
     def get(self, job_id: str) -> Document | None:
-        r = self._conn().execute("select body from documents where id=?", (job_id,)).fetchone()
-        return Document.from_dict(json.loads(r[0])) if r else None
+        r = self._conn().execute(f"select {_SEL} from documents where id=?", (job_id,)).fetchone()
+        return _decode_row(*r) if r else None
 
     def all_docs(self) -> list[Document]:
-        return [Document.from_dict(json.loads(r[0])) for r in self._conn().execute("select body from documents")]
+        return [_decode_row(*r) for r in self._conn().execute(f"select {_SEL} from documents order by rid")]
+
+    def update(self, job_id: str, **fields) -> Document | None:
+        """A field update (e.g. the REST abort) keeps the submission's
+        version: it is a status change, not a resubmission."""
+        self.update_many([(job_id, fields)])
+        return self.get(job_id)
+
+    def docs_by_status(self, status: str) -> list[Document]:
+        return [_decode_row(*r) for r in self._conn().execute(
+            f"select {_SEL} from documents where status=? order by rid", (status,))]
 
     def _claim_candidates(self) -> list[Document]:
         st = tuple(ST.CLAIMABLE | ST.IN_PROGRESS)
-        q = f"select body from documents where status in ({','.join('?' * len(st))}) order by modified"
-        return [Document.from_dict(json.loads(r[0])) for r in self._conn().execute(q, st)]
+        q = f"select {_SEL} from documents where status in ({','.join('?' * len(st))}) order by modified"
+        return [_decode_row(*r) for r in self._conn().execute(q, st)]
 
     def _cas_claim(self, d: Document, worker: str, now: float) -> bool:
-        """Compare-and-swap on (status, modified) inside one IMMEDIATE transaction."""
-        c = self._conn()
-        c.execute("begin immediate")
-        try:
-            r = c.execute("select status, modified from documents where id=?", (d.id,)).fetchone()
-            if r is None or r[0] != d.status or abs(r[1] - _ts(d)) > 1e-6:
-                c.execute("rollback")
-                return False
-            d.status = ST.PREPROCESS_INPROGRESS
-            d.processing_content = worker
-            d.modified_at = rfc3339(datetime.fromtimestamp(now, timezone.utc))
-            c.execute("insert or replace into documents values (?,?,?,?)",
-                      (d.id, d.status, _ts(d), json.dumps(d.to_dict())))
-            c.execute("commit")
-            return True
-        except Exception:
-            c.execute("rollback")
-            raise
+        with self._txn() as c:
+            self._beat(c, worker, now)
+            r = c.execute("update documents set status=?, worker=?, modified=?, modified_at=?, seq=? where id=? "
+                          "and status=? and modified=? returning rid",
+                          (ST.PREPROCESS_INPROGRESS, worker, now, _stamp(now), self._next_seq(c), d.id, d.status,
+                           _ts(d))).fetchone()
+        return r is not None
 
-    def add_hpalog(self, log: HPALog) -> None:
-        self._conn().execute("insert into hpalogs values (?,?,?)", (log.job_id, log.timestamp,
-                                                                    json.dumps(log.to_dict())))
+    # ------------------------------------------------------------------ claims
+    def _claim_new(self, c, worker: str, limit: int, max_stuck_s: float, now: float, shard, seq: int,
+                   cols: str = "rid, id, ver") -> list:
+        if limit <= 0:
+            return []
+        cl, ip = tuple(sorted(ST.CLAIMABLE)), tuple(sorted(ST.IN_PROGRESS))
+        sw, sa = self._shard_sql(shard)
+        # stuck = in progress under a worker whose lease expired: the
+        # (few) expired leases drive an index lookup per worker (CROSS JOIN
+        # fixes that loop order), never a scan of the live in-progress rows
+        q = (f"update documents set status=?, worker=?, modified=?, modified_at=?, seq=? where rid in ("
+             f"select rid from (select rid, modified from documents where status in ({','.join('?' * len(cl))}){sw} "
+             f"union all select d.rid, d.modified from leases l cross join documents d on d.worker = l.worker "
+             f"where l.beat < ? and d.status in ({','.join('?' * len(ip))}){sw.replace('okey', 'd.okey')}) "
+             f"order by modified limit ?) returning {cols}")
+        args = (ST.PREPROCESS_INPROGRESS, worker, now, _stamp(now), seq) + cl + sa + (now - max_stuck_s,) + ip + sa \
+            + (limit,)
+        self._beat(c, worker, now)
+        return c.execute(q, args).fetchall()
 
-    def add_hpalogs(self, logs: list[HPALog]) -> None:
-        c = self._conn()
-        c.execute("begin")
-        try:
-            c.executemany("insert into hpalogs values (?,?,?)",
-                          [(lg.job_id, lg.timestamp, json.dumps(lg.to_dict())) for lg in logs])
-            c.execute("commit")
-        except Exception:
-            c.execute("rollback")
-            raise
-
-    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
-        """One IMMEDIATE transaction: read the bodies, apply, ``executemany``."""
-        if not updates:
-            return
-        stamp = _stamp(time.time() if now is None else now)
-        c = self._conn()
-        c.execute("begin immediate")
-        try:
-            bodies = {}
-            ids = [j for j, _ in updates]
-            for k in range(0, len(ids), 500):
-                chunk = ids[k:k + 500]
-                q = f"select id, body from documents where id in ({','.join('?' * len(chunk))})"
-                bodies.update({r[0]: r[1] for r in c.execute(q, chunk)})
-            rows = []
-            for jid, fields in updates:
-                b = bodies.get(jid)
-                if b is None:
-                    continue
-                d = Document.from_dict(json.loads(b))
-                for f, v in fields.items():
-                    setattr(d, f, v)
-                d.modified_at = stamp
-                rows.append((d.id, d.status, _ts(d), json.dumps(d.to_dict())))
-            c.executemany("insert or replace into documents values (?,?,?,?)", rows)
-            c.execute("commit")
-        except Exception:
-            c.execute("rollback")
-            raise
+    @staticmethod
+    def _beat(c, worker: str, now: float) -> None:
+        """The worker-level lease heartbeat: ONE row per claim, however many
+        jobs the worker holds (their ``modified`` stays at claim time)."""
+        c.execute("insert into leases values (?,?) on conflict(worker) do update set beat=excluded.beat "
+                  "where excluded.beat > beat", (worker, now))
 
     def claim(self, worker, limit, max_stuck_s, now=None, owner=None, shard=None):
-        """The whole batch in one IMMEDIATE transaction (the write lock makes
-        it atomic against other brain processes sharing the file)."""
+        """Reserve up to ``limit`` claimable or stuck jobs in ONE statement
+        (``UPDATE ... RETURNING`` inside an IMMEDIATE transaction: atomic
+        against every other process sharing the file)."""
+        if owner is not None:
+            return JobStore.claim(self, worker, limit, max_stuck_s, now=now, owner=owner)
         now = time.time() if now is None else now
-        if shard is not None and owner is None:
-            owner = _shard_filter(*shard)
-        st = tuple(ST.CLAIMABLE | ST.IN_PROGRESS)
-        stamp = _stamp(now)
+        with self._txn() as c:
+            rows = self._claim_new(c, worker, limit, max_stuck_s, now, shard, self._next_seq(c),
+                                   cols=f"modified, {_SEL}")
+        rows.sort(key=lambda r: r[0])
+        return [_decode_row(*r[1:]) for r in rows]
+
+    @staticmethod
+    def _feed(c, s: "_Session", worker: str, upto: int) -> None:
+        """Change feed: rows other writers touched in (last_seq, upto) --
+        resubmissions, aborts, takeovers -- leave the session."""
+        if not s.held or upto <= s.last_seq + 1:
+            return
+        for jid, st, wk, ver in c.execute("select id, status, worker, ver from documents where seq > ? and seq < ?",
+                                          (s.last_seq, upto)):
+            h = s.held.get(jid)
+            if h is not None and (st not in ST.IN_PROGRESS or wk != worker or ver != h[1]):
+                s.drop(jid)
+
+    def _claimable(self, c, max_stuck_s: float, now: float, shard) -> bool:
+        """Is anything claimable or stuck in this shard?  (index probes)"""
+        cl, ip = tuple(sorted(ST.CLAIMABLE)), tuple(sorted(ST.IN_PROGRESS))
+        sw, sa = self._shard_sql(shard)
+        q = (f"select exists(select 1 from documents where status in ({','.join('?' * len(cl))}){sw}) or "
+             f"exists(select 1 from leases l cross join documents d on d.worker = l.worker where l.beat < ? and "
+             f"d.status in ({','.join('?' * len(ip))}){sw.replace('okey', 'd.okey')})")
+        return bool(c.execute(q, cl + sa + (now - max_stuck_s,) + ip + sa).fetchone()[0])
+
+    def claim_batch(self, worker, limit, max_stuck_s, now=None, shard=None) -> ClaimBatch:
+        """The jobs ``worker`` holds a lease on (sticky session), topped up
+        with newly claimable / stuck jobs of its shard.
+
+        The steady state of a re-examined fleet is READ-ONLY: one snapshot
+        reads the change feed and probes (through indexes) whether anything
+        is claimable or stuck for this shard.  The write lock -- which every
+        rank and the REST service contend for -- is taken only to claim, and
+        for the worker's lease heartbeat every ``MAX_STUCK_IN_SECONDS`` / 6."""
+        now = time.time() if now is None else now
+        s = self._sessions.get(worker)
+        if s is None:
+            s = self._sessions[worker] = _Session()
         c = self._conn()
-        c.execute("begin immediate")
+        c.execute("begin")                              # deferred: a read snapshot, no write lock
         try:
-            q = f"select body from documents where status in ({','.join('?' * len(st))}) order by modified"
-            out = []
-            for (b,) in c.execute(q, st).fetchall():
-                if len(out) >= limit:
-                    break
-                d = Document.from_dict(json.loads(b))
-                stuck = d.status in ST.IN_PROGRESS and now - _ts(d) > max_stuck_s
-                if not (d.status in ST.CLAIMABLE or stuck):
-                    continue
-                if owner is not None and not owner(d):
-                    continue
-                d.status = ST.PREPROCESS_INPROGRESS
-                d.processing_content = worker
-                d.modified_at = stamp
-                out.append(d)
-            c.executemany("insert or replace into documents values (?,?,?,?)",
-                          [(d.id, d.status, _ts(d), json.dumps(d.to_dict())) for d in out])
+            seq = c.execute("select v from meta where k = 'seq'").fetchone()[0]
+            self._feed(c, s, worker, seq + 1)
+            room = limit - len(s.held)
+            need = room > 0 and self._claimable(c, max_stuck_s, now, shard)
+        finally:
             c.execute("commit")
+        s.last_seq = seq
+        if need or now - s.last_beat >= max_stuck_s / 6:
+            with self._txn() as c:
+                seq = self._next_seq(c)
+                self._feed(c, s, worker, seq)           # writes since the snapshot
+                room = limit - len(s.held)
+                if need and room > 0:
+                    for rid, jid, ver in self._claim_new(c, worker, room, max_stuck_s, now, shard, seq):
+                        s.add(jid, rid, ver)
+                else:
+                    self._beat(c, worker, now)
+                if now - s.last_gc > max_stuck_s:
+                    # leases of workers that hold nothing any more
+                    s.last_gc = now
+                    ip = tuple(sorted(ST.IN_PROGRESS))
+                    c.execute(f"delete from leases where beat < ? and not exists (select 1 from documents d where "
+                              f"d.worker = leases.worker and d.status in ({','.join('?' * len(ip))}))",
+                              (now - max_stuck_s,) + ip)
+            s.last_seq = seq
+            s.last_beat = now
+        ids, vers, rids = s.snapshot(limit)
+
+        def resolve(pos):
+            out = []
+            sel = [int(rids[p]) for p in pos]
+            for k in range(0, len(sel), 500):
+                chunk = sel[k:k + 500]
+                got = {r[0]: r[1:] for r in self._conn().execute(
+                    f"select rid, {_SEL} from documents where rid in ({','.join('?' * len(chunk))})", chunk)}
+                out += [_decode_row(*got[r]) for r in chunk if r in got]
             return out
-        except Exception:
-            c.execute("rollback")
-            raise
+        return ClaimBatch(ids, vers, resolve, handles=rids)
+
+    def keep(self, worker: str, ids, now: float | None = None, handles=None) -> None:
+        """Jobs that stay alive: a session's leased jobs simply stay leased."""
+        if worker in self._sessions:
+            return
+        self.update_uniform(ids, {"status": ST.PREPROCESS_COMPLETED}, now=now, handles=handles, worker=worker)
+
+    # ------------------------------------------------------------------ verdicts
+    def update_uniform(self, ids, fields: dict, now: float | None = None, handles=None,
+                       worker: str | None = None) -> None:
+        if len(ids) == 0:
+            return
+        if any(k not in _COLUMN_OF for k in fields):
+            return self.update_many([(i, fields) for i in ids], now=now, worker=worker)
+        now = time.time() if now is None else now
+        cols = [_COLUMN_OF[k] for k in fields]
+        gs, ga = self._guard(worker)
+        if handles is not None and len(handles) == len(ids):
+            key, keys = "rid", json.dumps(np.asarray(handles, np.int64).tolist())
+        else:
+            key, keys = "id", json.dumps(list(ids))
+        with self._txn() as c:
+            seq = self._next_seq(c)
+            c.execute(f"update documents set {''.join(f'{x}=?, ' for x in cols)}modified=?, modified_at=?, seq=? "
+                      f"where {key} in (select value from json_each(?)){gs}",
+                      tuple(fields.values()) + (now, _stamp(now), seq, keys) + ga)
+        if fields.get("status", ST.PREPROCESS_INPROGRESS) not in ST.IN_PROGRESS:
+            self._sessions_drop(ids)
+
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None, worker: str | None = None) -> None:
+        """Column updates grouped by field set (one ``executemany`` per
+        shape); a field outside the columns patches that job's body."""
+        if not updates:
+            return
+        now = time.time() if now is None else now
+        stamp = _stamp(now)
+        gs, ga = self._guard(worker)
+        shapes: dict[tuple, list] = {}
+        patch = []
+        for jid, fields in updates:
+            if all(k in _COLUMN_OF for k in fields):
+                shapes.setdefault(tuple(fields), []).append((jid, fields))
+            else:
+                patch.append((jid, fields))
+        with self._txn() as c:
+            seq = self._next_seq(c)
+            for shape, rows in shapes.items():
+                c.executemany(f"update documents set {''.join(f'{_COLUMN_OF[k]}=?, ' for k in shape)}modified=?, "
+                              f"modified_at=?, seq=? where id=?{gs}",
+                              [tuple(f[k] for k in shape) + (now, stamp, seq, jid) + ga for jid, f in rows])
+            for jid, fields in patch:                # rare: a field outside the columns
+                r = c.execute(f"select {_SEL} from documents where id=?{gs}", (jid,) + ga).fetchone()
+                if r is None:
+                    continue
+                d = _decode_row(*r)
+                for k, v in fields.items():
+                    setattr(d, k, v)
+                row = self._row(d, seq)
+                c.execute("update documents set status=?, worker=?, reason=?, anomaly=?, modified=?, modified_at=?, "
+                          "seq=?, body=? where id=?", (d.status, d.processing_content, d.reason, d.anomaly_info, now,
+                                                       stamp, seq, row[-1], jid))
+        gone = [jid for jid, f in updates if f.get("status", ST.PREPROCESS_INPROGRESS) not in ST.IN_PROGRESS]
+        if gone:
+            self._sessions_drop(gone)
+
+    # ------------------------------------------------------------------ hpalogs
+    def add_hpalog(self, log: HPALog) -> None:
+        self.add_hpalogs([log])
+
+    def add_hpalogs(self, logs: list[HPALog]) -> None:
+        if not logs:
+            return
+        with self._txn() as c:
+            c.executemany("insert into hpalogs values (?,?,?)",
+                          [(lg.job_id, lg.timestamp, json.dumps(lg.to_dict())) for lg in logs])
+            self._log_writes += len(logs)
+            newest = max(lg.timestamp for lg in logs)
+            # bounded retention (the HPA alert reads the last 4-6 entries,
+            # GET /v1/healthcheck/id the last 10): drop entries older than
+            # the retention window, at most once a minute
+            if self.hpalog_retention_s > 0 and newest - self._last_prune > 60.0:
+                c.execute("delete from hpalogs where ts < ?", (newest - self.hpalog_retention_s,))
+                self._last_prune = newest
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
         rows = self._conn().execute("select body from hpalogs where job_id=? order by ts desc limit ?",
@@ -558,15 +907,32 @@ class SQLiteStore(JobStore):
 
 
 class ElasticsearchStore(JobStore):
-    """ES 6.x REST adapter (indexes ``documents``/type ``document`` and ``hpalogs``)."""
+    """ES 6.x REST adapter (indexes ``documents``/type ``document`` and
+    ``hpalogs``), the reference's store (elasticsearchstore.go:17-21).
+
+    Claims never go document by document: one ``search_after`` scan of the
+    claimable / stuck documents of this worker's shard (``ownerKey`` is
+    written into every document: the owner hash mod 720720, so a painless
+    ``ownerKey % world == rank`` filter selects a rank's shard for every world
+    size up to 16), then ONE ``_bulk`` of ``update`` actions conditional on
+    each hit's ``if_seq_no`` / ``if_primary_term``: a 409 item is a job
+    another brain won.  No ``refresh=true`` on the claim or verdict path."""
+
+    PAGE = 1000
 
     def __init__(self, url: str, client=None) -> None:
         import httpx
         self.url = url.rstrip("/")
         self.http = client or httpx.Client(timeout=30)
 
+    @staticmethod
+    def _source(doc: Document) -> dict:
+        s = doc.to_dict()
+        s["ownerKey"] = owner_hash(doc.namespace, doc.app_name) % OWNER_MOD
+        return s
+
     def put(self, doc: Document) -> None:
-        r = self.http.put(f"{self.url}/documents/document/{doc.id}?refresh=true", json=doc.to_dict())
+        r = self.http.put(f"{self.url}/documents/document/{doc.id}?refresh=true", json=self._source(doc))
         r.raise_for_status()
 
     def get(self, job_id: str) -> Document | None:
@@ -578,57 +944,106 @@ class ElasticsearchStore(JobStore):
         hits = r.json().get("hits", {}).get("hits", [])
         return Document.from_dict(hits[0]["_source"]) if hits else None
 
+    def _scan(self, query: dict, limit: int | None = None, extra: dict | None = None) -> list[dict]:
+        """``search_after`` pages sorted by (modified_at, id)."""
+        out: list[dict] = []
+        after = None
+        while limit is None or len(out) < limit:
+            size = self.PAGE if limit is None else min(self.PAGE, limit - len(out))
+            body = {"query": query, "size": size, "sort": [{"modified_at": {"order": "asc", "unmapped_type": "date"}},
+                                                           {"id.keyword": {"order": "asc"}}]}
+            body.update(extra or {})
+            if after is not None:
+                body["search_after"] = after
+            r = self.http.post(f"{self.url}/documents/_search", json=body)
+            if r.status_code == 404:
+                break
+            r.raise_for_status()
+            hits = r.json().get("hits", {}).get("hits", [])
+            out += hits
+            if len(hits) < size:
+                break
+            after = hits[-1].get("sort")
+            if after is None:
+                break
+        return out
+
     def all_docs(self) -> list[Document]:
-        r = self.http.post(f"{self.url}/documents/_search", json={"query": {"match_all": {}}, "size": 10000})
-        if r.status_code == 404:
-            return []
-        r.raise_for_status()
-        return [Document.from_dict(h["_source"]) for h in r.json().get("hits", {}).get("hits", [])]
+        return [Document.from_dict(h["_source"]) for h in self._scan({"match_all": {}})]
 
-    def _claim_candidates(self) -> list[Document]:
-        states = sorted(ST.CLAIMABLE | ST.IN_PROGRESS)
-        q = {"query": {"terms": {"status.keyword": states}}, "size": 10000}
-        r = self.http.post(f"{self.url}/documents/_search", json=q)
-        if r.status_code == 404:
-            return []
-        r.raise_for_status()
-        return [Document.from_dict(h["_source"]) for h in r.json().get("hits", {}).get("hits", [])]
+    def _claim_query(self, max_stuck_s: float, now: float, shard) -> tuple[dict, bool]:
+        stuck_before = _stamp(now - max_stuck_s)
+        q = {"bool": {"should": [
+            {"terms": {"status.keyword": sorted(ST.CLAIMABLE)}},
+            {"bool": {"filter": [{"terms": {"status.keyword": sorted(ST.IN_PROGRESS)}},
+                                 {"range": {"modified_at": {"lt": stuck_before}}}]}}],
+            "minimum_should_match": 1}}
+        py_shard = False
+        if shard is not None and shard[1] > 1:
+            rank, world = shard
+            if OWNER_MOD % world == 0:
+                q["bool"]["filter"] = [{"script": {"script": {
+                    "source": "doc['ownerKey'].value % params.w == params.r", "lang": "painless",
+                    "params": {"w": world, "r": rank}}}}]
+            else:
+                py_shard = True
+        return q, py_shard
 
-    def _cas_claim(self, d: Document, worker: str, now: float) -> bool:
-        """Optimistic concurrency: re-read the document with its sequence
-        number, re-check that it is still claimable, write conditionally
-        (``if_seq_no``/``if_primary_term``); a 409 means another brain won."""
-        r = self.http.get(f"{self.url}/documents/document/{d.id}")
-        if r.status_code != 200:
-            return False
-        body = r.json()
-        cur = Document.from_dict(body.get("_source", {}))
-        stuck = cur.status in ST.IN_PROGRESS
-        if cur.status not in ST.CLAIMABLE and not (stuck and cur.modified_at == d.modified_at):
-            return False
-        cur.status = ST.PREPROCESS_INPROGRESS
-        cur.processing_content = worker
-        cur.modified_at = rfc3339(datetime.fromtimestamp(now, timezone.utc))
-        w = self.http.put(f"{self.url}/documents/document/{d.id}?refresh=true&if_seq_no={body.get('_seq_no', 0)}"
-                          f"&if_primary_term={body.get('_primary_term', 1)}", json=cur.to_dict())
-        if w.status_code == 409:
-            return False
-        w.raise_for_status()
-        return True
+    def claim(self, worker, limit, max_stuck_s, now=None, owner=None, shard=None):
+        now = time.time() if now is None else now
+        q, py_shard = self._claim_query(max_stuck_s, now, shard)
+        scan_limit = None if (owner is not None or py_shard) else limit
+        hits = self._scan(q, scan_limit, {"seq_no_primary_term": True})
+        if py_shard:
+            sh = _shard_filter(*shard)
+            hits = [h for h in hits if sh(Document.from_dict(h["_source"]))]
+        cand = []
+        for h in hits:
+            d = Document.from_dict(h["_source"])
+            stuck = d.status in ST.IN_PROGRESS and now - _ts(d) > max_stuck_s
+            if not (d.status in ST.CLAIMABLE or stuck):
+                continue
+            if owner is not None and not owner(d):
+                continue
+            cand.append((h, d))
+            if len(cand) >= limit:
+                break
+        if not cand:
+            return []
+        stamp = _stamp(now)
+        lines = []
+        for h, d in cand:
+            lines += [{"update": {"_index": "documents", "_type": "document", "_id": h.get("_id", d.id),
+                                  "if_seq_no": h.get("_seq_no", 0), "if_primary_term": h.get("_primary_term", 1)}},
+                      {"doc": {"status": ST.PREPROCESS_INPROGRESS, "processingContent": worker,
+                               "modified_at": stamp}}]
+        items = self._bulk(lines, allow_conflict=True).get("items", [])
+        out = []
+        for (h, d), it in zip(cand, items):
+            res = next(iter(it.values()), {})
+            if res.get("status", 200) >= 300:        # 409: another brain won this job
+                continue
+            d.status = ST.PREPROCESS_INPROGRESS
+            d.processing_content = worker
+            d.modified_at = stamp
+            out.append(d)
+        return out
 
     def add_hpalog(self, log: HPALog) -> None:
-        r = self.http.post(f"{self.url}/hpalogs/hpalog?refresh=true", json=log.to_dict())
+        r = self.http.post(f"{self.url}/hpalogs/hpalog", json=log.to_dict())
         r.raise_for_status()
 
-    def _bulk(self, lines: list[dict]) -> dict:
+    def _bulk(self, lines: list[dict], allow_conflict: bool = False) -> dict:
         body = "".join(json.dumps(x) + "\n" for x in lines)
-        r = self.http.post(f"{self.url}/_bulk?refresh=true", content=body.encode(),
+        r = self.http.post(f"{self.url}/_bulk", content=body.encode(),
                            headers={"Content-Type": "application/x-ndjson"})
         r.raise_for_status()
         out = r.json()
         if out.get("errors"):
-            bad = [it for it in out.get("items", []) for v in it.values() if v.get("status", 200) >= 300]
-            raise RuntimeError(f"ES _bulk: {len(bad)} failed actions, first {bad[:1]}")
+            bad = [v for it in out.get("items", []) for v in it.values() if v.get("status", 200) >= 300
+                   and not (allow_conflict and v.get("status") == 409)]
+            if bad:
+                raise RuntimeError(f"ES _bulk: {len(bad)} failed actions, first {bad[:1]}")
         return out
 
     def add_hpalogs(self, logs: list[HPALog]) -> None:
@@ -639,7 +1054,7 @@ class ElasticsearchStore(JobStore):
         if lines:
             self._bulk(lines)
 
-    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None) -> None:
+    def update_many(self, updates: list[tuple[str, dict]], now: float | None = None, worker: str | None = None) -> None:
         """One ``_bulk`` request of partial-document ``update`` actions."""
         stamp = _stamp(time.time() if now is None else now)
         names = {f.name: f.metadata.get("json", f.name) for f in dataclasses.fields(Document)}

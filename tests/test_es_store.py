@@ -1,6 +1,8 @@
 """ElasticsearchStore against an in-process fake ES (httpx MockTransport):
-document/hpalog round trips, status queries, and the optimistic-concurrency
-claim (if_seq_no / if_primary_term) under a lost race."""
+document/hpalog round trips, and the claim path: one ``search_after`` scan
+of the claimable / stuck documents of a shard + ONE conditional ``_bulk``
+(``if_seq_no`` / ``if_primary_term``), never a request per document and never
+``refresh=true``; a lost race (409 item) drops that job only."""
 import json
 import urllib.parse
 
@@ -8,7 +10,33 @@ import httpx
 
 from foremast_amd.api import status as ST
 from foremast_amd.api.models import Document, HPALog, HPALogBody, HPALogDetail
+from foremast_amd.parallel.dist import service_owner
 from foremast_amd.service.store import ElasticsearchStore
+
+
+def _matches(q: dict, d: dict) -> bool:
+    """The query subset ElasticsearchStore sends."""
+    if not q or "match_all" in q:
+        return True
+    if "terms" in q:
+        (f, vals), = q["terms"].items()
+        return d.get(f.replace(".keyword", "")) in vals
+    if "match" in q:
+        (f, v), = q["match"].items()
+        return d.get(f.replace(".keyword", "")) == v
+    if "range" in q:
+        (f, cond), = q["range"].items()
+        v = d.get(f, "")
+        return all({"lt": v < x, "lte": v <= x, "gt": v > x, "gte": v >= x}[op] for op, x in cond.items())
+    if "script" in q:
+        p = q["script"]["script"]["params"]
+        assert q["script"]["script"]["source"] == "doc['ownerKey'].value % params.w == params.r"
+        return d["ownerKey"] % p["w"] == p["r"]
+    b = q["bool"]
+    ok = all(_matches(x, d) for x in b.get("must", []) + b.get("filter", []))
+    if "should" in b:
+        ok = ok and sum(_matches(x, d) for x in b["should"]) >= b.get("minimum_should_match", 1)
+    return ok
 
 
 class FakeES:
@@ -16,20 +44,17 @@ class FakeES:
         self.docs: dict[str, tuple[int, dict]] = {}
         self.logs: list[dict] = []
         self.seq = 0
-        self.interfere = None   # callable run once before a conditional write
+        self.interfere = None   # callable run once before a conditional bulk update
+        self.requests: list[tuple[str, str, dict]] = []
 
     def handler(self, req: httpx.Request) -> httpx.Response:
         path, q = req.url.path, dict(urllib.parse.parse_qsl(req.url.query.decode()))
-        body = json.loads(req.content) if req.content else {}
+        self.requests.append((req.method, path, q))
         parts = path.strip("/").split("/")
+        if parts == ["_bulk"]:
+            return self._bulk(req.content.decode())
+        body = json.loads(req.content) if req.content else {}
         if parts[0] == "documents" and len(parts) == 3 and req.method == "PUT":
-            if "if_seq_no" in q:
-                if self.interfere:
-                    f, self.interfere = self.interfere, None
-                    f()
-                cur = self.docs.get(parts[2])
-                if cur is None or cur[0] != int(q["if_seq_no"]):
-                    return httpx.Response(409, json={"error": "version_conflict"})
             self.seq += 1
             self.docs[parts[2]] = (self.seq, body)
             return httpx.Response(200, json={"result": "updated"})
@@ -39,14 +64,24 @@ class FakeES:
                 return httpx.Response(404, json={"found": False})
             return httpx.Response(200, json={"_source": d[1], "_seq_no": d[0], "_primary_term": 1})
         if parts == ["documents", "_search"]:
-            qq = body.get("query", {})
-            hits = [v for _, v in self.docs.values()]
-            if "terms" in qq:
-                hits = [h for h in hits if h.get("status") in qq["terms"]["status.keyword"]]
-            elif "bool" in qq:
-                want = qq["bool"]["must"][0]["match"]["id.keyword"]
-                hits = [h for h in hits if h.get("id") == want]
-            return httpx.Response(200, json={"hits": {"hits": [{"_source": h} for h in hits]}})
+            rows = [(k, s, v) for k, (s, v) in self.docs.items() if _matches(body.get("query", {}), v)]
+            sort = body.get("sort")
+            if sort:
+                key = lambda r: (r[2].get("modified_at", ""), r[2].get("id", ""))
+                rows.sort(key=key)
+                if "search_after" in body:
+                    after = tuple(body["search_after"])
+                    rows = [r for r in rows if key(r) > after]
+            rows = rows[: body.get("size", 10)]
+            hits = []
+            for k, s, v in rows:
+                h = {"_id": k, "_source": v}
+                if sort:
+                    h["sort"] = [v.get("modified_at", ""), v.get("id", "")]
+                if body.get("seq_no_primary_term"):
+                    h.update(_seq_no=s, _primary_term=1)
+                hits.append(h)
+            return httpx.Response(200, json={"hits": {"hits": hits}})
         if parts == ["hpalogs", "hpalog"]:
             self.logs.append(body)
             return httpx.Response(201, json={})
@@ -55,6 +90,31 @@ class FakeES:
             hs = sorted([l for l in self.logs if l.get("job_id") == want], key=lambda l: -l["timestamp"])
             return httpx.Response(200, json={"hits": {"hits": [{"_source": h} for h in hs[: body["size"]]]}})
         return httpx.Response(400, json={"path": path})
+
+    def _bulk(self, text: str) -> httpx.Response:
+        lines = [json.loads(x) for x in text.splitlines() if x.strip()]
+        items, errors = [], False
+        if self.interfere and any("update" in a and "if_seq_no" in a["update"] for a in lines[::2]):
+            f, self.interfere = self.interfere, None
+            f()
+        for action, src in zip(lines[::2], lines[1::2]):
+            (op, meta), = action.items()
+            if op == "index" and meta["_index"] == "hpalogs":
+                self.logs.append(src)
+                items.append({"index": {"status": 201}})
+            elif op == "update":
+                cur = self.docs.get(meta["_id"])
+                if cur is None:
+                    items.append({"update": {"status": 404}})
+                    errors = True
+                elif "if_seq_no" in meta and cur[0] != meta["if_seq_no"]:
+                    items.append({"update": {"status": 409}})
+                    errors = True
+                else:
+                    self.seq += 1
+                    self.docs[meta["_id"]] = (self.seq, dict(cur[1], **src["doc"]))
+                    items.append({"update": {"status": 200}})
+        return httpx.Response(200, json={"errors": errors, "items": items})
 
 
 def _store():
@@ -73,23 +133,52 @@ def test_es_roundtrip_and_logs():
     assert [l.timestamp for l in st.hpalogs("j1", 2)] == [3.0, 2.0]
 
 
-def test_es_claim_is_conditional():
+def test_es_claim_is_one_scan_and_one_conditional_bulk():
     es, st = _store()
     for i in range(3):
         st.put(Document(id=f"j{i}", app_name=f"a{i}", status=ST.INITIAL, modified_at="2025-01-01T00:00:00Z"))
     st.put(Document(id="done", app_name="x", status=ST.COMPLETED_HEALTH))
 
-    # another brain claims j0 between our read and our conditional write
+    # another brain claims j0 between our scan and our conditional bulk write
     def steal():
         seq, doc = es.docs["j0"]
         es.seq += 1
-        es.docs["j0"] = (es.seq, dict(doc, status=ST.PREPROCESS_INPROGRESS, processing_content="other",
+        es.docs["j0"] = (es.seq, dict(doc, status=ST.PREPROCESS_INPROGRESS, processingContent="other",
                                          modified_at="2025-10-09T08:53:20Z"))
     es.interfere = steal
+    es.requests.clear()
     got = st.claim("me", 10, 90.0, now=1_760_000_000.0)
     ids = sorted(d.id for d in got)
     assert ids == ["j1", "j2"]
-    assert es.docs["j0"][1]["processing_content"] == "other"
+    # one search + one _bulk, no per-document request, no forced refresh
+    assert [(m, p) for m, p, _ in es.requests] == [("POST", "/documents/_search"), ("POST", "/_bulk")]
+    assert all("refresh" not in q for _, _, q in es.requests)
+    assert es.docs["j0"][1]["processingContent"] == "other"
     assert all(es.docs[i][1]["status"] == ST.PREPROCESS_INPROGRESS for i in ids)
     # nothing claimable left (in-progress within the lease)
     assert st.claim("me", 10, 90.0, now=1_760_000_010.0) == []
+    # after MAX_STUCK_IN_SECONDS the stuck jobs are taken over
+    taken = st.claim("late", 10, 90.0, now=1_760_000_000.0 + 120)
+    assert sorted(d.id for d in taken) == ["j0", "j1", "j2"]
+
+
+def test_es_claim_pages_and_shards():
+    es, st = _store()
+    st.PAGE = 7                                            # force several search_after pages
+    n = 40
+    for i in range(n):
+        st.put(Document(id=f"j{i:03d}", app_name=f"svc{i}", status=ST.INITIAL,
+                        modified_at=f"2025-01-01T00:00:{i:02d}Z"))
+    world = 3
+    claimed = {}
+    for r in range(world):
+        got = st.claim(f"r{r}", 100, 90.0, now=1_760_000_000.0, shard=(r, world))
+        for d in got:
+            assert service_owner(d.namespace, d.app_name, world) == r
+            claimed[d.id] = r
+    assert len(claimed) == n
+    # limit is honoured and oldest-first
+    es2, st2 = _store()
+    for i in range(10):
+        st2.put(Document(id=f"k{i}", app_name=f"a{i}", status=ST.INITIAL, modified_at=f"2025-01-01T00:00:0{i}Z"))
+    assert [d.id for d in st2.claim("w", 4, 90.0, now=1_760_000_000.0)] == ["k0", "k1", "k2", "k3"]

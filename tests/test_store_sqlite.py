@@ -1,0 +1,175 @@
+"""SQLiteStore, the store the shipped topology uses (REST service + every
+brain rank of a node on one WAL file, deploy/foremast/31-brain.yaml):
+columnar claims, sticky worker leases with a change feed, takeover of a dead
+worker's jobs after MAX_STUCK_IN_SECONDS, guarded verdicts, bounded HPA logs,
+and mutual exclusion between processes."""
+import json
+import multiprocessing as mp
+import sqlite3
+import time
+
+import numpy as np
+import pytest
+
+from foremast_amd.api import status as ST
+from foremast_amd.api.models import Document, HPALog, HPALogBody
+from foremast_amd.parallel.dist import service_owner
+from foremast_amd.service.store import SQLiteStore
+
+T0 = 1_760_000_000.0
+
+
+def _docs(n, prefix="job", status=ST.INITIAL):
+    return [Document(id=f"{prefix}{i:05d}", app_name=f"svc{i}", namespace="default" if i % 3 else "",
+                     status=status, strategy="canary", modified_at="2025-10-09T08:00:00Z",
+                     current_config=f"m== http://prom/api/v1/query_range?query=q{i}") for i in range(n)]
+
+
+def test_sticky_session_claims_once_and_stays_leased(tmp_path):
+    st = SQLiteStore(str(tmp_path / "j.db"))
+    st.put_many(_docs(50))
+    b = st.claim_batch("w1", 100, 90.0, now=T0)
+    assert len(b) == 50 and sorted(b.ids) == sorted(d.id for d in _docs(50))
+    assert {d.id for d in b.docs([0, 1])} == set(b.ids[:2])
+    seq0 = st._conn().execute("select v from meta").fetchone()[0]
+    st.keep("w1", b.ids, now=T0 + 1, handles=b.handles)          # alive: no write
+    b2 = st.claim_batch("w1", 100, 90.0, now=T0 + 2)
+    assert b2.ids == b.ids and b2.versions == b.versions
+    # the steady-state cycle wrote no job row (one seq bump per claim transaction only)
+    assert st._conn().execute("select count(*) from documents where seq > ?", (seq0,)).fetchone()[0] == 0
+    assert st.get(b.ids[0]).status == ST.PREPROCESS_INPROGRESS
+    assert st.get(b.ids[0]).processing_content == "w1"
+    # another worker sees nothing claimable while w1's lease lives (w1 keeps beating)
+    for k in range(5):
+        assert len(st.claim_batch("w1", 100, 90.0, now=T0 + 60 * k)) == 50
+        assert st.claim("w2", 100, 90.0, now=T0 + 60 * k + 1) == []
+
+
+def test_dead_worker_is_taken_over_and_its_session_notices(tmp_path):
+    st = SQLiteStore(str(tmp_path / "j.db"))
+    st.put_many(_docs(20))
+    b = st.claim_batch("w1", 100, 90.0, now=T0)
+    assert len(b) == 20
+    # w1 stops beating; 91 s later w2's claim takes every job over
+    other = SQLiteStore(st.path)                    # another process's view
+    got = other.claim_batch("w2", 100, 90.0, now=T0 + 91)
+    assert sorted(got.ids) == sorted(b.ids)
+    assert all(st.get(i).processing_content == "w2" for i in b.ids)
+    # w1 comes back: the change feed drops what it lost, nothing is double-held
+    assert len(st.claim_batch("w1", 100, 90.0, now=T0 + 92)) == 0
+    # w1's stale verdicts on the lost jobs are not applied
+    st.update_uniform(b.ids, {"status": ST.COMPLETED_HEALTH, "reason": ""}, now=T0 + 93, worker="w1")
+    assert all(st.get(i).status == ST.PREPROCESS_INPROGRESS for i in b.ids)
+
+
+def test_resubmission_and_abort_reach_the_session(tmp_path):
+    st = SQLiteStore(str(tmp_path / "j.db"))
+    st.put_many(_docs(4))
+    b = st.claim_batch("w", 10, 90.0, now=T0)
+    v = dict(zip(b.ids, b.versions))
+    rest = SQLiteStore(st.path)                     # the REST service process
+    d = _docs(4)[1]
+    rest.put(d)                                     # resubmitted under the same id: re-armed
+    rest.update(_docs(4)[2].id, status=ST.ABORT, reason="aborted by client")
+    # a verdict computed for the old submission must not clobber the new one
+    st.update_many([(d.id, {"status": ST.COMPLETED_UNHEALTH, "reason": "old"})], now=T0 + 1, worker="w")
+    st.update_many([(_docs(4)[2].id, {"status": ST.COMPLETED_HEALTH, "reason": ""})], now=T0 + 1, worker="w")
+    assert st.get(d.id).status == ST.INITIAL
+    b2 = st.claim_batch("w", 10, 90.0, now=T0 + 2)
+    assert sorted(b2.ids) == sorted(i for i in b.ids if i != _docs(4)[2].id)
+    v2 = dict(zip(b2.ids, b2.versions))
+    assert v2[d.id] != v[d.id] and all(v2[i] == v[i] for i in v2 if i != d.id)
+    assert st.get(_docs(4)[2].id).status == ST.ABORT
+    # verdicts close jobs and leave the session
+    st.update_uniform(b2.ids, {"status": ST.COMPLETED_HEALTH, "reason": ""}, now=T0 + 3, handles=b2.handles,
+                      worker="w")
+    assert len(st.claim_batch("w", 10, 90.0, now=T0 + 4)) == 0
+    assert all(st.get(i).status == ST.COMPLETED_HEALTH for i in b2.ids)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8, 16, 17])
+def test_shard_filter_matches_service_owner(tmp_path, world):
+    st = SQLiteStore(str(tmp_path / "j.db"))
+    docs = _docs(300)
+    st.put_many(docs)
+    seen = {}
+    for r in range(world):
+        for d in st.claim(f"r{r}", 1000, 90.0, now=T0, shard=(r, world)):
+            assert service_owner(d.namespace, d.app_name, world) == r
+            seen[d.id] = r
+    assert len(seen) == len(docs)
+
+
+def test_hpalog_retention_and_order(tmp_path):
+    st = SQLiteStore(str(tmp_path / "j.db"), hpalog_retention_s=3600.0)
+    for k in range(5):
+        st.add_hpalogs([HPALog(job_id=f"a:ns:hpa{j}", timestamp=T0 + 600 * k, log=HPALogBody(50 + k, "x", []))
+                        for j in range(3)])
+    assert [l.timestamp for l in st.hpalogs("a:ns:hpa1", 3)] == [T0 + 2400, T0 + 1800, T0 + 1200]
+    st.add_hpalogs([HPALog(job_id="a:ns:hpa0", timestamp=T0 + 9000, log=HPALogBody(60, "x", []))])
+    left = st._conn().execute("select min(ts) from hpalogs").fetchone()[0]
+    assert left >= T0 + 9000 - 3600
+
+
+def test_migrates_round2_layout(tmp_path):
+    path = str(tmp_path / "old.db")
+    c = sqlite3.connect(path)
+    c.execute("create table documents (id text primary key, status text, modified real, body text)")
+    for d in _docs(3):
+        c.execute("insert into documents values (?,?,?,?)", (d.id, d.status, 0.0, json.dumps(d.to_dict())))
+    c.commit()
+    c.close()
+    st = SQLiteStore(path)
+    assert [d.id for d in st.all_docs()] == [d.id for d in _docs(3)]
+    assert len(st.claim_batch("w", 10, 90.0, now=T0)) == 3
+
+
+def _proc_claimer(path, worker, cycles, out, go):
+    st = SQLiteStore(path)
+    go.wait(120)                                     # both claim concurrently
+    mine = set()
+    now = T0
+    for k in range(cycles):
+        now += 1.0
+        b = st.claim_batch(worker, 150, 1e9, now=now)
+        mine.update(b.ids)
+        if len(b):                                   # close a third of what it holds
+            sel = np.arange(0, len(b), 3)
+            st.update_uniform([b.ids[i] for i in sel], {"status": ST.COMPLETED_HEALTH, "reason": ""}, now=now,
+                              handles=b.handles[sel], worker=worker)
+        time.sleep(0.002)
+    out.put((worker, sorted(mine)))
+
+
+def test_two_processes_never_claim_the_same_job(tmp_path):
+    path = str(tmp_path / "j.db")
+    st = SQLiteStore(path)
+    st.put_many(_docs(1200))
+    ctx = mp.get_context("spawn")
+    q, go = ctx.Queue(), ctx.Barrier(2)
+    ps = [ctx.Process(target=_proc_claimer, args=(path, f"w{i}", 40, q, go)) for i in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    a, b = set(got["w0"]), set(got["w1"])
+    assert not (a & b)
+    assert len(a) + len(b) == 1200 and a and b
+    # every claimed job is recorded with exactly its claimer
+    for jid in list(a)[:50] + list(b)[:50]:
+        assert st.get(jid).processing_content == ("w0" if jid in a else "w1")
+
+
+def test_steady_claim_cost_is_independent_of_fleet_size(tmp_path):
+    st = SQLiteStore(str(tmp_path / "j.db"))
+    st.put_many(_docs(5000))
+    st.claim_batch("w", 10000, 90.0, now=T0)
+    ts = []
+    for k in range(20):
+        t = time.perf_counter()
+        b = st.claim_batch("w", 10000, 90.0, now=T0 + 1 + k)
+        st.keep("w", b.ids, now=T0 + 1 + k, handles=b.handles)
+        ts.append(time.perf_counter() - t)
+    assert len(b) == 5000
+    assert float(np.median(ts)) < 0.005          # a handful of indexed statements, not 5000 rows
