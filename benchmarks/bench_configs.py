@@ -315,10 +315,26 @@ def config3e2e(args):
         for k, v in brain.spans.last.items():
             spans.setdefault(k, []).append(v * 1e3)
 
+    scrapes = []
+    stop_scrape = None
+    if args.scrape_interval > 0 and info.is_main:
+        # a Prometheus scraper on rank 0's /metrics body while the cycles run
+        import threading
+        stop_scrape = threading.Event()
+
+        def scraper():
+            while not stop_scrape.is_set():
+                t0 = time.perf_counter()
+                n = sum(len(p) for p in exp.render_parts())
+                scrapes.append((time.perf_counter() - t0, n))
+                stop_scrape.wait(args.scrape_interval)
+        threading.Thread(target=scraper, daemon=True).start()
     poll = None
     try:
         ms, p50 = time_steps(step, args.steps, args.warmup, dev)
     finally:
+        if stop_scrape is not None:
+            stop_scrape.set()
         if poller is not None:
             poller.terminate()
             try:
@@ -346,7 +362,10 @@ def config3e2e(args):
             {"services": S, "metrics": M, "pods_per_side": P, "store": args.store,
              "topology": ("REST service in its own process + every rank on one WAL SQLite file"
                           if args.store == "sqlite" else "single process, in-memory store"),
-             "rest_poller": poll, "rows_per_cycle_rank0": per_cycle, "rows_per_cycle_max_rank": windows,
+             "rest_poller": poll, "rows_per_cycle_rank0": per_cycle,
+             "scraper": {"interval_s": args.scrape_interval, "scrapes": len(scrapes),
+                         "render_ms_median": round(1e3 * statistics.median([x for x, _ in scrapes]), 2)
+                         if scrapes else None, "bytes": scrapes[-1][1] if scrapes else None}, "rows_per_cycle_max_rank": windows,
              "span_ms_median_rank0": span_ms, "span_ms_median_max_rank": worst,
              # untimed: dominated by the host-side synthetic generator (counter-hash noise for 80k
              # 7-day series in numpy, ~1 ms per series), not by the brain's fetch / stage path
@@ -457,6 +476,8 @@ def main():
                     "(sqlite: the shipped topology, REST service in its own process)")
     ap.add_argument("--rest-poll-rps", type=float, default=None, help="config 3e2e + sqlite: barrelman-shaped "
                     "GET /v1/healthcheck/id load during the timed cycles (default: services / 10 s)")
+    ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "
+                    "body every N seconds in a thread while the cycles are timed (0: off)")
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "
                     "the fitted-model cache")
     args = ap.parse_args()

@@ -60,33 +60,35 @@ FM_API int64_t fm_render_lines(const char* prefix, const int64_t* poff, const in
   if (n <= 0) return 0;
   if (cap < fm_render_bound(poff, order, n)) return -1;
   threads = threads < 1 ? 1 : threads;
-  if (threads == 1 || n < 16384) {
+  if (threads == 1 || n < 2048) {
     return render_range(prefix, poff, order, 0, n, vals, out) - out;
   }
-  // each thread renders its chunk into its own scratch, then the chunks are
-  // copied back to back (a memcpy of the finished text is cheap next to
-  // formatting)
-  std::vector<std::vector<char>> parts(threads);
-  std::vector<int64_t> used(threads, 0);
-  std::vector<std::thread> pool;
+  // each thread formats its chunk in place at the chunk's worst-case offset
+  // inside ``out`` (no scratch allocation), then the chunks are slid down
+  // back to back
   const int64_t per = (n + threads - 1) / threads;
+  std::vector<int64_t> start(threads + 1, 0), used(threads, 0);
   for (int t = 0; t < threads; ++t) {
+    const int64_t lo = t * per < n ? t * per : n, hi = lo + per < n ? lo + per : n;
+    int64_t bound = 0;
+    for (int64_t i = lo; i < hi; ++i) {
+      const int64_t s = order ? order[i] : i;
+      bound += poff[s + 1] - poff[s] + 33;
+    }
+    start[t + 1] = start[t] + bound;
+  }
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) {
     pool.emplace_back([&, t] {
-      const int64_t lo = t * per, hi = lo + per < n ? lo + per : n;
-      if (lo >= hi) return;
-      int64_t bound = 0;
-      for (int64_t i = lo; i < hi; ++i) {
-        const int64_t s = order ? order[i] : i;
-        bound += poff[s + 1] - poff[s] + 33;
-      }
-      parts[t].resize(static_cast<size_t>(bound));
-      used[t] = render_range(prefix, poff, order, lo, hi, vals, parts[t].data()) - parts[t].data();
+      const int64_t lo = t * per < n ? t * per : n, hi = lo + per < n ? lo + per : n;
+      used[t] = render_range(prefix, poff, order, lo, hi, vals, out + start[t]) - (out + start[t]);
     });
   }
+  used[0] = render_range(prefix, poff, order, 0, per < n ? per : n, vals, out) - out;
   for (auto& th : pool) th.join();
-  char* o = out;
-  for (int t = 0; t < threads; ++t) {
-    if (used[t]) std::memcpy(o, parts[t].data(), static_cast<size_t>(used[t]));
+  char* o = out + used[0];
+  for (int t = 1; t < threads; ++t) {
+    if (used[t]) std::memmove(o, out + start[t], static_cast<size_t>(used[t]));
     o += used[t];
   }
   return o - out;

@@ -92,6 +92,11 @@ class BrainConfig:
     downstream_hops: int = 2               # DOWNSTREAM_IMPACT_HOPS
     downstream_refresh_cycles: int = 30    # DOWNSTREAM_REFRESH_CYCLES: re-read the call graph every N cycles
     downstream_ttl_s: float = 600.0        # DOWNSTREAM_SCORE_TTL_SECONDS: a callee verdict counts this long
+    downstream_sync_s: float = 0.5         # DOWNSTREAM_SYNC_SECONDS: verdict exchange cadence between ranks
+    # cluster of the jobs whose queries carry no ``cluster`` label matcher
+    # (one brain per cluster, or a federated Prometheus that drops the label)
+    brain_cluster: str = ""                # BRAIN_CLUSTER
+    export_sync_s: float = 1.0             # EXPORT_SYNC_SECONDS: ranks > 0 publish their gauges to rank 0
 
     def rule_for(self, alias: str) -> MetricRule:
         """Per-metric override: exact alias match first, then substring match
@@ -156,6 +161,9 @@ class BrainConfig:
         c.downstream_hops = _i(env, "DOWNSTREAM_IMPACT_HOPS", c.downstream_hops)
         c.downstream_refresh_cycles = _i(env, "DOWNSTREAM_REFRESH_CYCLES", c.downstream_refresh_cycles)
         c.downstream_ttl_s = _f(env, "DOWNSTREAM_SCORE_TTL_SECONDS", c.downstream_ttl_s)
+        c.downstream_sync_s = _f(env, "DOWNSTREAM_SYNC_SECONDS", c.downstream_sync_s)
+        c.brain_cluster = env.get("BRAIN_CLUSTER", c.brain_cluster)
+        c.export_sync_s = _f(env, "EXPORT_SYNC_SECONDS", c.export_sync_s)
         return c
 
 

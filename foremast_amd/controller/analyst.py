@@ -6,6 +6,7 @@ against an in-process service (``AnalystClient.for_app(fastapi_app)``)."""
 from __future__ import annotations
 
 import json
+import os
 import time
 import urllib.parse
 from dataclasses import dataclass
@@ -47,10 +48,13 @@ class Response:
 
 class AnalystClient:
     def __init__(self, base_url: str, do: Callable[[str, str, bytes | None], Response] | None = None,
-                 clock=time.time):
+                 clock=time.time, cluster: str | None = None):
         self.base_url = base_url if base_url.endswith("/") else base_url + "/"
         self.do = do or self._http_do
         self.clock = clock
+        # the cluster this barrelman watches (CLUSTER_NAME): added to every
+        # PromQL matcher so a central brain can tell clusters apart
+        self.cluster = os.environ.get("CLUSTER_NAME", "") if cluster is None else cluster
         self._http = None
 
     def _http_do(self, method: str, url: str, body: bytes | None) -> Response:
@@ -64,7 +68,8 @@ class AnalystClient:
         return Response(r.status_code, r.content)
 
     @classmethod
-    def for_app(cls, app, base_url: str = "http://foremast-service/v1/healthcheck/", clock=time.time):
+    def for_app(cls, app, base_url: str = "http://foremast-service/v1/healthcheck/", clock=time.time,
+                cluster: str | None = None):
         """In-process transport against a FastAPI app (tests / single binary)."""
         from fastapi.testclient import TestClient
         tc = TestClient(app)
@@ -73,7 +78,7 @@ class AnalystClient:
             path = urllib.parse.urlsplit(url).path
             r = tc.request(method, path, content=body, headers={"Content-Type": "application/json"})
             return Response(r.status_code, r.content)
-        return cls(base_url, do, clock)
+        return cls(base_url, do, clock, cluster)
 
     def _url(self, rel: str) -> str:
         return urllib.parse.urljoin(self.base_url, rel)
@@ -81,7 +86,8 @@ class AnalystClient:
     def start_analyzing(self, namespace: str, app: str, pod_names, metrics: crd.Metrics, window_min: float,
                         strategy: str, aliases: list[str] | None = None) -> str:
         now = self.clock()
-        info = MQ.create_metrics_info(namespace, app, pod_names, metrics, window_min, strategy, aliases, now)
+        info = MQ.create_metrics_info(namespace, app, pod_names, metrics, window_min, strategy, aliases, now,
+                                      self.cluster)
         req = ApplicationHealthAnalyzeRequest(app_name=app, start_time=rfc3339_local(now),
                                               end_time=rfc3339_local(now + window_min * 60), metrics=info,
                                               strategy=strategy, namespace=namespace)

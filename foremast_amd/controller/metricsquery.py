@@ -10,6 +10,10 @@
   app-level ``namespace_app_pod_<m>{namespace,app}``; HPA/continuous jobs
   query app level for current too.
 * priorities follow the HPA template order when ``metric_aliases`` is given.
+* multi-cluster (README.md:27): with a ``cluster`` name (barrelman's
+  ``CLUSTER_NAME``) every matcher also carries ``cluster="<name>"``, so a
+  central brain over a federated Prometheus knows which cluster a job's
+  service runs in (downstream impact keys services by cluster).
 """
 from __future__ import annotations
 
@@ -34,8 +38,10 @@ class BadRequest(ValueError):
 
 
 def _create_map(namespace: str, app: str, pods: list[str], metrics: Metrics, category: str, window_min: float,
-                strategy: str, aliases: list[str] | None, now: float | None = None) -> dict[str, MetricQuery]:
+                strategy: str, aliases: list[str] | None, now: float | None = None,
+                cluster: str = "") -> dict[str, MetricQuery]:
     now = time.time() if now is None else now
+    cl = f',cluster="{cluster}"' if cluster else ""
     out: dict[str, MetricQuery] = {}
     for i, mon in enumerate(metrics.monitoring):
         priority = i + 1
@@ -46,11 +52,11 @@ def _create_map(namespace: str, app: str, pods: list[str], metrics: Metrics, cat
         now_u = int(now) // STEP * STEP
         before = int(now - window_min * 60) // STEP * STEP
         p = {"endpoint": metrics.endpoint, "step": STEP}
-        app_q = f'namespace_app_pod_{mon.metric_name}{{namespace="{namespace}",app="{app}"}}'
+        app_q = f'namespace_app_pod_{mon.metric_name}{{namespace="{namespace}",app="{app}"{cl}}}'
         if len(pods) > 1:
-            pod_q = f'namespace_pod_{mon.metric_name}{{namespace="{namespace}",pod=~"{"|".join(pods)}"}}'
+            pod_q = f'namespace_pod_{mon.metric_name}{{namespace="{namespace}",pod=~"{"|".join(pods)}"{cl}}}'
         elif pods:
-            pod_q = f'namespace_pod_{mon.metric_name}{{namespace="{namespace}",pod="{pods[0]}"}}'
+            pod_q = f'namespace_pod_{mon.metric_name}{{namespace="{namespace}",pod="{pods[0]}"{cl}}}'
         else:
             pod_q = app_q
         if category == CATEGORY_CURRENT:
@@ -71,7 +77,7 @@ def _create_map(namespace: str, app: str, pods: list[str], metrics: Metrics, cat
 
 def create_metrics_info(namespace: str, app: str, pod_names: list[list[str]] | None, metrics: Metrics,
                         window_min: float, strategy: str, aliases: list[str] | None = None,
-                        now: float | None = None) -> MetricsInfo:
+                        now: float | None = None, cluster: str = "") -> MetricsInfo:
     pod_names = pod_names or []
     if strategy not in (STRATEGY_CONTINUOUS, STRATEGY_HPA) and not pod_names:
         raise BadRequest("No valid pod names")
@@ -79,12 +85,12 @@ def create_metrics_info(namespace: str, app: str, pod_names: list[list[str]] | N
         raise BadRequest("Unsupported DataSourceType:" + metrics.data_source_type)
     pods = [] if strategy in (STRATEGY_CONTINUOUS, STRATEGY_HPA) else pod_names[0]
     info = MetricsInfo(current=_create_map(namespace, app, pods, metrics, CATEGORY_CURRENT, window_min, strategy,
-                                           aliases, now))
+                                           aliases, now, cluster))
     if strategy != STRATEGY_ROLLING_UPDATE and len(pod_names) > 1:
         info.baseline = _create_map(namespace, app, pod_names[1], metrics, CATEGORY_BASELINE, window_min, strategy,
-                                    aliases, now)
+                                    aliases, now, cluster)
     info.historical = _create_map(namespace, app, pods, metrics, CATEGORY_HISTORICAL, window_min, strategy, aliases,
-                                  now)
+                                  now, cluster)
     return info
 
 

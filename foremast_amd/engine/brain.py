@@ -78,6 +78,7 @@ class Work:
     end_ts: float = 0.0
     missing: list[str] = field(default_factory=list)
     namespace: str = ""
+    cluster: str = ""           # ``cluster`` label matcher of the job's queries (multi-cluster impact)
 
     @property
     def hpa(self) -> bool:
@@ -124,6 +125,8 @@ class Brain:
         self.worker = worker_id or f"{socket.gethostname()}-{os.getpid()}"
         self.batch_size = batch_size
         self.exporter = exporter
+        if exporter is not None:
+            exporter.sync_seconds = self.cfg.export_sync_s
         self.clock = clock
         self.step = step
         self.watch_s = watch_minutes * 60.0
@@ -211,6 +214,8 @@ class Brain:
             base_metric = (promql_metric_name(q) or alias).replace("namespace_pod_", "namespace_app_pod_", 1)
             if not wk.namespace:
                 wk.namespace = _label(q, "namespace")
+            if not wk.cluster:
+                wk.cluster = _label(q, "cluster")
             wk.rows.append(Row(-1, alias, base_metric, hv, ht, cv, ct, bv))
         return wk
 
@@ -342,19 +347,18 @@ class Brain:
 
     # ------------------------------------------------------------------ cycle
     def run_once(self) -> dict:
-        """One brain cycle.  Collective discipline under DP: every rank calls
-        the export sync exactly once per cycle, from ``finally`` (a cycle that
-        raises still joins it, so the ranks' collective sequences never
-        diverge); there is no other per-cycle collective."""
+        """One brain cycle.  Under DP the ranks are shared-nothing
+        (docs/guides/design.md:41): no collective runs in a cycle.  The call
+        graph, the verdicts downstream impact needs and rank 0's exporter
+        view travel through the non-blocking world mailbox
+        (parallel/mailbox.py), so a slow or stopped rank only makes its
+        published data older -- it never stalls another rank's cycle."""
         t0 = time.perf_counter()
         self.cycles += 1
         imp = self.impact
         if imp.enabled:
-            # collectives in a fixed order on every rank: graph refresh
-            # (broadcast) every N cycles, the verdict all-reduce once per cycle
-            # (mid-cycle when the cycle scores jobs, else here in ``finally``)
             self._impact_done = False
-            if (self.cycles - 1) % max(1, self.cfg.downstream_refresh_cycles) == 0:
+            if (self.cycles - 1) % max(1, self.cfg.downstream_refresh_cycles) == 0 or imp.needs_graph():
                 with self.spans.span("impact_graph"):
                     imp.refresh()
         try:
@@ -364,10 +368,10 @@ class Brain:
                 self._impact_step(self.clock())
             if self.exporter is not None and D.is_dist():
                 with self.spans.span("export_sync"):
-                    self.exporter.sync()
+                    self.exporter.exchange()
 
     def _impact_step(self, now: float) -> None:
-        """Global verdict vector + K9 impact (collective, once per cycle)."""
+        """Verdict exchange + K9 impact (once per cycle, non-blocking)."""
         if not self.impact.enabled or self._impact_done:
             return
         self._impact_done = True
@@ -453,9 +457,11 @@ class Brain:
             try:
                 with self.spans.span("score"):
                     g = fp.score_group(grp, now, key)
-                scored.append((key, grp, g))
                 if self.impact.enabled:
                     fp.observe_impact(g, self.impact, now)
+                # only a fully scored group is finished as a group (a failure
+                # above re-scores it job by job: never both)
+                scored.append((key, grp, g))
             except Exception:                       # contain: re-score job by job
                 log.exception("fast-path group of %d jobs failed; re-scoring per job", len(grp))
                 self._n_contained += self._fast_per_job(grp, M, now, updates, hpalogs, outcome)
@@ -543,15 +549,17 @@ class Brain:
             return [b for wk in works for b in self._score_general([wk], updates, outcome)]
         if res is not None and self.impact.enabled:
             offs = 0
-            nss, apps, bad = [], [], []
+            nss, apps, cls, bad = [], [], [], []
             for wk in works:
                 k = len(wk.rows)
                 if not wk.hpa:
                     nss.append(wk.namespace or wk.doc.namespace)
                     apps.append(wk.doc.app_name)
+                    cls.append(wk.cluster)
                     bad.append(bool(res["flags"][offs:offs + k].any()))
                 offs += k
-            self.impact.observe(self.impact.ids(nss, apps), np.asarray(bad, bool), self.clock())
+            self.impact.observe(self.impact.ids(nss, apps, cls), np.asarray(bad, bool), self.clock(),
+                                keys=list(zip(cls, nss, apps)))
         return [(works, rows, res)]
 
     def _finish_general(self, batches: list, now: float, updates: list, hpalogs: list, outcome: dict) -> int:
@@ -630,7 +638,7 @@ class Brain:
                                 "upper": float(up[idx[0]]), "lower": float(lo[idx[0]])})
         if wk.hpa:
             return self._finish_hpa(wk, rows, res, sl, now, updates, hpalogs)
-        down = self._downstream(ns, app, bool(anomalies))
+        down = self._downstream(ns, app, bool(anomalies), wk.cluster)
         if down:
             reasons.append(down)
             anomalies["downstream"] = {"tags": "", "values": []}
@@ -649,14 +657,14 @@ class Brain:
         updates.append((doc.id, {"status": ST.PREPROCESS_COMPLETED}))
         return ST.PREPROCESS_COMPLETED
 
-    def _downstream(self, namespace: str, app: str, unhealthy: bool) -> dict | None:
+    def _downstream(self, namespace: str, app: str, unhealthy: bool, cluster: str = "") -> dict | None:
         """The ``downstream`` reason entry of a job whose service sends at
         least ``DOWNSTREAM_IMPACT_THRESHOLD`` of its traffic (over <= hops
         hops) to an anomalous service (None if not, or mode forbids)."""
         imp = self.impact
         if not imp.enabled or (imp.cfg.downstream_mode == "annotate" and not unhealthy):
             return None
-        u = imp.node.get(("", namespace, app), -1)
+        u = int(imp.ids([namespace], [app], [cluster])[0])
         if u < 0 or u >= len(imp.impact) or imp.impact[u] < self.cfg.downstream_threshold:
             return None
         return {"name": "downstream", "impact": round(float(imp.impact[u]), 4), "callees": imp.explain(u)}
@@ -798,7 +806,7 @@ def _hpa_owner_of(job_id: str) -> tuple[str, str]:
 
 def _label(q: str, name: str) -> str:
     import re
-    m = re.search(name + r'\s*=\s*"([^"]*)"', q or "")
+    m = re.search(r'(?<![\w])' + name + r'\s*=\s*"([^"]*)"', q or "")
     return m.group(1) if m else ""
 
 

@@ -14,27 +14,38 @@
 
 Fleet-scale layout: the gauges are one columnar table (a slot per
 ``(series, namespace, app)``, float64 values) written with vectorised numpy
-stores and rendered by a custom collector at scrape time, instead of one
-``Gauge.labels().set()`` call per value (80k rows x 3 series per cycle would
-cost ~0.5 s of lock-protected Python).
+stores.  The exposition text of a slot's labels is rendered ONCE, when the
+slot is created; a scrape formats only the values, in native code
+(csrc/runtime/exposition.cpp: shortest round-trip decimals, several threads,
+no GIL), grouped by family.  240k gauges render in tens of milliseconds, not
+the seconds a per-sample ``GaugeMetricFamily`` walk took.
 
 Data-parallel brains (one rank per GPU, services sharded by owner hash) keep
-the table per rank and :meth:`BrainExporter.sync` merges every rank's changed
-slots into rank 0's table each cycle over the world process group (SURVEY §2.5
-C2): the new keys (rare) as objects, the changed values as one padded
-``all_gather`` of a float64 ``[n, 2]`` (slot, value) tensor, so the one
-scrape target on rank 0 publishes every service's bounds and HPA score.
+the table per rank.  Rank 0 is the one scrape target, so every other rank
+**publishes** its table to rank 0 through the world mailbox
+(parallel/mailbox.py): new slot keys as an append-only log,
+the values as one float64 vector, on a cadence (``EXPORT_SYNC_SECONDS``) and
+only when something changed.  Rank 0 merges whatever has arrived when it is
+scraped (or on the same cadence in its loop).  Nothing waits: a slow rank
+leaves its last published values in place (``foremast_brain_rank_export_age_seconds``
+shows how old), it never stalls rank 0's brain or scrape.
 """
 from __future__ import annotations
 
+import ctypes
+import json
 import re
+import struct
 import threading
+import time
 
 import numpy as np
-from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, start_http_server
-from prometheus_client.core import GaugeMetricFamily
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+
+from . import native_rt
 
 _NAME_OK = re.compile(r"[^a-zA-Z0-9_:]")
+CONTENT_TYPE = "text/plain; version=0.0.4; charset=utf-8"
 
 
 def sanitize(name: str) -> str:
@@ -42,8 +53,21 @@ def sanitize(name: str) -> str:
     return n if not n[0].isdigit() else "_" + n
 
 
+def _esc(v: str) -> str:
+    """Label-value escaping of the text exposition format."""
+    return v.replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
+
+
+def _grow(a: np.ndarray, n: int, fill) -> np.ndarray:
+    if n <= len(a):
+        return a
+    return np.concatenate([a, np.full(max(n, 2 * len(a)) - len(a), fill, a.dtype)])
+
+
 class GaugeTable:
-    """Columnar gauge storage: slot -> (series name, namespace, app, value)."""
+    """Columnar gauge storage: slot -> (series name, namespace, app, value),
+    plus the pre-rendered sample-line prefix of every slot, kept per family
+    (a scrape walks each family's prefixes sequentially)."""
 
     def __init__(self) -> None:
         self.index: dict[tuple[str, str, str], int] = {}
@@ -51,8 +75,13 @@ class GaugeTable:
         self.vals = np.zeros(0, np.float64)
         self.help: dict[str, str] = {}
         self.lock = threading.Lock()
-        self.dirty: list = []                    # slots changed since the last sync (arrays / (lo, hi) ranges)
-        self.new_from = 0                        # keys[new_from:] not yet announced
+        self.version = 0                         # bumped by every write (publication cadence)
+        self._fam_of: dict[str, int] = {}
+        self._fam_names: list[str] = []
+        self._fprefix: list[bytearray] = []      # per family: concatenated line prefixes
+        self._fpoff: list[np.ndarray] = []       # per family: prefix offsets (count + 1)
+        self._fslots: list[np.ndarray] = []      # per family: slot of each line
+        self._fn: list[int] = []
 
     def __len__(self) -> int:
         return len(self.keys)
@@ -66,69 +95,88 @@ class GaugeTable:
                 if s is None:
                     s = idx[k] = len(self.keys)
                     self.keys.append(k)
+                    self._add_line(k, s)
                 out[i] = s
-            if len(self.keys) > len(self.vals):
-                grow = np.full(max(len(self.keys), 2 * len(self.vals)) - len(self.vals), np.nan)
-                self.vals = np.concatenate([self.vals, grow])
+            n = len(self.keys)
+            if n > len(self.vals):
+                self.vals = _grow(self.vals, n, np.nan)
         return out
+
+    def _add_line(self, key, slot: int) -> None:
+        name, ns, app = key[:3]
+        extra = f',cluster="{_esc(key[3])}"' if len(key) > 3 and key[3] else ""
+        f = self._fam_of.get(name)
+        if f is None:
+            f = self._fam_of[name] = len(self._fam_names)
+            self._fam_names.append(name)
+            self._fprefix.append(bytearray())
+            self._fpoff.append(np.zeros(1, np.int64))
+            self._fslots.append(np.zeros(0, np.int64))
+            self._fn.append(0)
+        k = self._fn[f]
+        buf = self._fprefix[f]
+        buf += f'{name}{{namespace="{_esc(ns)}",app="{_esc(app)}"{extra}}} '.encode()
+        self._fpoff[f] = po = _grow(self._fpoff[f], k + 2, 0)
+        po[k + 1] = len(buf)
+        self._fslots[f] = sl = _grow(self._fslots[f], k + 1, 0)
+        sl[k] = slot
+        self._fn[f] = k + 1
 
     def set(self, slots, values, track: bool = True) -> None:
         """``slots``: slot indices, or a ``slice`` of consecutive slots (a
         strided store instead of an 80k-element scatter per cycle)."""
-        if isinstance(slots, slice):
-            with self.lock:
-                self.vals[slots] = values
-            if track and slots.stop > slots.start:
-                self.dirty.append((slots.start, slots.stop))
-            return
-        slots = np.asarray(slots, np.int64)
+        if not isinstance(slots, slice):
+            slots = np.asarray(slots, np.int64)
         with self.lock:
             self.vals[slots] = values
-        if track and len(slots):
-            self.dirty.append(slots)
+            self.version += 1
 
     def get(self, key) -> float | None:
         s = self.index.get(key)
         return None if s is None else float(self.vals[s])
 
-    def take_dirty(self) -> np.ndarray:
-        parts = [np.arange(p[0], p[1]) if isinstance(p, tuple) else p for p in self.dirty]
-        d = np.unique(np.concatenate(parts)) if parts else np.zeros(0, np.int64)
-        self.dirty = []
-        return d
+    # ---------------------------------------------------------------- exposition
+    def render_parts(self, threads: int = 4) -> list:
+        """The text exposition of every slot as a list of byte buffers (one
+        header + one block of lines per family)."""
+        with self.lock:                          # snapshot; formatting runs unlocked
+            fams = [(name, bytes(self._fprefix[f]), self._fpoff[f][:self._fn[f] + 1].copy(),
+                     self.vals[self._fslots[f][:self._fn[f]]]) for f, name in enumerate(self._fam_names)
+                    if self._fn[f]]
+        lib = native_rt._load()
+        parts = []
+        for name, prefix, poff, vals in fams:
+            parts.append(f"# HELP {name} {self.help.get(name, name)}\n# TYPE {name} gauge\n".encode())
+            n = len(vals)
+            if lib is None:                       # pure-Python fallback (library not built)
+                parts.append(b"".join(prefix[poff[i]:poff[i + 1]] + _fmt(vals[i]) + b"\n" for i in range(n)))
+                continue
+            cap = int(poff[-1]) + 33 * n
+            out = np.empty(cap, np.uint8)
+            used = lib.fm_render_lines(prefix, poff.ctypes.data, None, n, vals.ctypes.data,
+                                       ctypes.c_char_p(out.ctypes.data), cap, threads)
+            parts.append(memoryview(out)[:used])
+        return parts
 
-    def collect(self):
-        with self.lock:
-            keys = list(self.keys)
-            vals = self.vals[:len(keys)].copy()
-        fams: dict[str, GaugeMetricFamily] = {}
-        for (name, ns, app), v in zip(keys, vals):
-            f = fams.get(name)
-            if f is None:
-                f = fams[name] = GaugeMetricFamily(name, self.help.get(name, name), labels=["namespace", "app"])
-            f.add_metric([ns, app], float(v))
-        return list(fams.values())
+    def render(self, threads: int = 4) -> bytes:
+        return b"".join(self.render_parts(threads))
 
 
-class _TableCollector:
-    def __init__(self, table: GaugeTable):
-        self.table = table
-
-    def collect(self):
-        return self.table.collect()
-
-    def describe(self):
-        return []
+def _fmt(v: float) -> bytes:
+    if v != v:
+        return b"NaN"
+    if v in (float("inf"), float("-inf")):
+        return b"+Inf" if v > 0 else b"-Inf"
+    return repr(float(v)).encode()
 
 
 class BrainExporter:
     HPA_SCORE = "namespace_app_pod_hpa_score"
     HPA_SCORE_ALT = "foremastbrain:namespace_app_per_pod:hpa_score"     # examples/hpa/README.MD:59 name
 
-    def __init__(self, registry: CollectorRegistry | None = None):
+    def __init__(self, registry: CollectorRegistry | None = None, sync_seconds: float = 1.0):
         self.registry = registry or CollectorRegistry()
         self.table = GaugeTable()
-        self.registry.register(_TableCollector(self.table))
         self.tick_seconds = Histogram("foremast_brain_tick_seconds", "wall time of one brain scoring cycle",
                                       registry=self.registry,
                                       buckets=(1e-4, 5e-4, 1e-3, 5e-3, 0.01, 0.05, 0.1, 0.5, 1, 5, 30))
@@ -136,16 +184,33 @@ class BrainExporter:
                             registry=self.registry)
         self.windows = Counter("foremast_brain_windows_scored_total", "metric windows scored",
                                registry=self.registry)
-        self._remote: dict[int, np.ndarray] = {}      # rank 0: remote slot -> local slot, per rank
         # multi-cluster aggregate of the downstream-impact step (engine/impact.py)
         self.cluster_impact = Gauge("foremastbrain:cluster_impact_max",
                                     "max over a cluster's services of max(anomaly, downstream impact)", ["cluster"],
                                     registry=self.registry)
+        self.rank_age = Gauge("foremast_brain_rank_export_age_seconds",
+                              "age of the newest gauge table rank 0 holds from each brain rank", ["rank"],
+                              registry=self.registry)
+        self.sync_seconds = sync_seconds
+        self._mb = None                          # parallel.mailbox.Mailbox (distributed brains)
+        self._mb_tried = False
+        self._pub_version = -1
+        self._pub_keys = 0
+        self._pub_t = -float("inf")
+        self._pull_t = -float("inf")
+        self._pull_lock = threading.Lock()
+        self._remote: dict[int, np.ndarray] = {}     # rank 0: remote slot -> local slot, per rank
+        self._klog: dict[int, int] = {}              # rank 0: key-log entries consumed, per rank
+        self._seen: dict[int, float] = {}            # rank 0: publish time of the merged values, per rank
 
     IMPACT = "foremastbrain:namespace_app_pod_downstream_impact"
 
-    def impact_slots(self, namespaces, apps) -> np.ndarray:
-        return self.table.slots([(self.IMPACT, ns, a) for ns, a in zip(namespaces, apps)])
+    def impact_slots(self, namespaces, apps, clusters=None) -> np.ndarray:
+        """Per-job downstream-impact gauges; jobs of a named cluster carry a
+        ``cluster`` label (the same namespace/app may run in several)."""
+        clusters = clusters or [""] * len(apps)
+        return self.table.slots([(self.IMPACT, ns, a, c) if c else (self.IMPACT, ns, a)
+                                 for ns, a, c in zip(namespaces, apps, clusters)])
 
     # ---------------------------------------------------------------- writes
     @staticmethod
@@ -170,7 +235,7 @@ class BrainExporter:
                 t.vals[slots:slots + 3 * n:3] = upper
                 t.vals[slots + 1:slots + 3 * n:3] = lower
                 t.vals[slots + 2:slots + 3 * n:3] = anomaly
-            t.dirty.append((slots, slots + 3 * n))
+                t.version += 1
             return
         self.table.set(slots.reshape(-1), np.stack([upper, lower, anomaly], 1).reshape(-1))
 
@@ -195,6 +260,10 @@ class BrainExporter:
         name = "foremastbrain:" + sanitize(base_metric) + "_forecast_max"
         self.table.set(self.table.slots([(name, namespace, app)]), [value])
 
+    def set_forecasts(self, base_metrics, namespaces, apps, values) -> None:
+        names = ["foremastbrain:" + sanitize(b) + "_forecast_max" for b in base_metrics]
+        self.table.set(self.table.slots(list(zip(names, namespaces, apps))), np.asarray(values, np.float64))
+
     def set_gauge(self, name: str, namespace: str, app: str, value: float) -> None:
         self.table.set(self.table.slots([(name, namespace, app)]), [value])
 
@@ -211,8 +280,48 @@ class BrainExporter:
         self.table.set(slots.reshape(-1), np.repeat(np.asarray(scores, np.float64), 2))
 
     # ---------------------------------------------------------------- reads
+    def render_parts(self) -> list:
+        """The whole ``/metrics`` body as buffers (merging the other ranks'
+        latest tables first on rank 0)."""
+        self.pull(force=True)
+        return [generate_latest(self.registry)] + self.table.render_parts()
+
+    def render(self) -> bytes:
+        return b"".join(self.render_parts())
+
     def serve(self, port: int = 8000, addr: str = "0.0.0.0"):
-        return start_http_server(port, addr=addr, registry=self.registry)
+        """``/metrics`` on a threaded HTTP server (the scrape never runs on
+        the brain's thread; rendering is native and releases the GIL)."""
+        from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+        exp = self
+
+        class H(BaseHTTPRequestHandler):
+            def do_GET(self):  # noqa: N802 - http.server API
+                if self.path.split("?")[0] not in ("/metrics", "/"):
+                    self.send_error(404)
+                    return
+                parts = exp.render_parts()
+                gz = "gzip" in (self.headers.get("Accept-Encoding") or "")
+                if gz:
+                    import zlib
+                    c = zlib.compressobj(1, zlib.DEFLATED, 31)
+                    parts = [b"".join(c.compress(p) for p in parts) + c.flush()]
+                self.send_response(200)
+                self.send_header("Content-Type", CONTENT_TYPE)
+                if gz:
+                    self.send_header("Content-Encoding", "gzip")
+                self.send_header("Content-Length", str(sum(len(p) for p in parts)))
+                self.end_headers()
+                for p in parts:
+                    self.wfile.write(p)
+
+            def log_message(self, *a):
+                pass
+
+        srv = ThreadingHTTPServer((addr, port), H)
+        srv.daemon_threads = True
+        threading.Thread(target=srv.serve_forever, name="brain-metrics", daemon=True).start()
+        return srv
 
     def sample(self, name: str, namespace: str, app: str) -> float | None:
         v = self.table.get((name, namespace, app))
@@ -220,69 +329,74 @@ class BrainExporter:
             return v
         return self.registry.get_sample_value(name, {"namespace": namespace, "app": app})
 
-    # ---------------------------------------------------------------- C2
-    def sync(self, group=None, device=None) -> int:
-        """Merge every rank's changed gauges into rank 0's table (collective:
-        every rank of ``group`` must call it once per cycle).  Returns the
-        number of remote values merged on rank 0 (0 elsewhere)."""
-        import torch
-        import torch.distributed as dist
-        from ..parallel import dist as D
-        if not D.is_dist():
-            self.table.dirty = []               # nothing to merge: drop the change log unsorted
-            self.table.new_from = len(self.table.keys)
+    # ---------------------------------------------------------------- C2 (mailbox)
+    def _mailbox(self):
+        if not self._mb_tried:
+            self._mb_tried = True
+            from ..parallel.mailbox import Mailbox
+            self._mb = Mailbox.for_world()
+        return self._mb
+
+    def exchange(self, force: bool = False) -> int:
+        """Once per brain cycle (never blocks): ranks > 0 publish their table
+        when it changed and ``sync_seconds`` passed; rank 0 merges what has
+        arrived on the same cadence.  Returns the number of values merged."""
+        mb = self._mailbox()
+        if mb is None:
             return 0
-        rank, world = dist.get_rank(group), dist.get_world_size(group)
-        dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
-                                                 if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+        if mb.rank != 0:
+            self.publish(force)
+            return 0
+        return self.pull(force)
+
+    def publish(self, force: bool = False) -> bool:
+        mb = self._mailbox()
+        if mb is None or mb.rank == 0:
+            return False
+        now = time.monotonic()
         t = self.table
-        new_keys = t.keys[t.new_from:] if rank != 0 else []
-        first_new = t.new_from
-        t.new_from = len(t.keys)
-        dirty = t.take_dirty()
-        if rank == 0:
-            dirty = dirty[:0]                  # rank 0's own values are already in its table
-        # sizes: [n new keys, n dirty] per rank, one small all-gather
-        sz = torch.tensor([len(new_keys), len(dirty)], dtype=torch.int64, device=dev)
-        sizes = torch.empty((world * 2,), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(sizes, sz, group=group)
-        sizes = sizes.cpu().numpy().reshape(world, 2)
-        if sizes[:, 0].any():
-            objs = [None] * world
-            dist.all_gather_object(objs, (first_new, new_keys), group=group)
-            if rank == 0:
-                for r in range(1, world):
-                    f0, ks = objs[r]
-                    if not ks:
-                        continue
-                    loc = t.slots(ks)
-                    m = self._remote.get(r, np.zeros(0, np.int64))
-                    if len(m) < f0 + len(ks):
-                        m = np.concatenate([m, np.full(f0 + len(ks) - len(m), -1, np.int64)])
-                    m[f0:f0 + len(ks)] = loc
-                    self._remote[r] = m
-        mx = int(sizes[:, 1].max())
-        if mx == 0:
+        if not force and (t.version == self._pub_version or now - self._pub_t < self.sync_seconds):
+            return False
+        with t.lock:
+            n = len(t.keys)
+            new = t.keys[self._pub_keys:n]
+            vals = t.vals[:n].copy()
+            ver = t.version
+        if new:
+            mb.append("gk", json.dumps(new).encode())
+        mb.put("gv", struct.pack("<q", n) + vals.tobytes())
+        self._pub_keys, self._pub_version, self._pub_t = n, ver, now
+        return True
+
+    def pull(self, force: bool = False) -> int:
+        mb = self._mailbox()
+        if mb is None or mb.rank != 0:
             return 0
-        pay = torch.full((mx, 2), -1.0, dtype=torch.float64)
-        if len(dirty):
-            pay[:len(dirty), 0] = torch.from_numpy(dirty.astype(np.float64))
-            with t.lock:
-                pay[:len(dirty), 1] = torch.from_numpy(t.vals[dirty])
-        out = torch.empty((world * mx, 2), dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(out, pay.to(dev), group=group)
-        if rank != 0:
+        now = time.monotonic()
+        if not force and now - self._pull_t < self.sync_seconds:
             return 0
-        got = out.cpu().numpy().reshape(world, mx, 2)
-        n = 0
-        for r in range(1, world):
-            k = int(sizes[r, 1])
-            if k == 0:
-                continue
-            rs = got[r, :k, 0].astype(np.int64)
-            m = self._remote.get(r)
-            loc = m[rs]
-            ok = loc >= 0
-            t.set(loc[ok], got[r, :k, 1][ok], track=False)
-            n += int(ok.sum())
-        return n
+        merged = 0
+        with self._pull_lock:
+            self._pull_t = now
+            for r in range(1, mb.world):
+                for chunk in mb.read_log("gk", r, self._klog.get(r, 0)):
+                    keys = [tuple(k) for k in json.loads(chunk)]
+                    loc = self.table.slots(keys)
+                    self._remote[r] = np.concatenate([self._remote.get(r, np.zeros(0, np.int64)), loc])
+                    self._klog[r] = self._klog.get(r, 0) + 1
+                got = mb.get("gv", r)
+                if got is None:
+                    continue
+                ts, raw = got
+                self.rank_age.labels(str(r)).set(max(0.0, time.time() - ts))
+                if self._seen.get(r) == ts:
+                    continue
+                n = struct.unpack_from("<q", raw)[0]
+                vals = np.frombuffer(raw, np.float64, count=n, offset=8)
+                m = self._remote.get(r, np.zeros(0, np.int64))
+                k = min(len(m), n)               # keys logged after this snapshot are picked up next time
+                with self.table.lock:
+                    self.table.vals[m[:k]] = vals[:k]
+                self._seen[r] = ts
+                merged += k
+        return merged

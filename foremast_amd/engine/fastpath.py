@@ -77,6 +77,7 @@ class JobPlan:
     group: tuple
     export_slots: np.ndarray | None = None
     hpa_slots: np.ndarray | None = None
+    cluster: str = ""                      # ``cluster`` label matcher of the job's queries
 
 
 @dataclass
@@ -136,7 +137,7 @@ class GroupArrays:
 
 def _label(q: str, name: str) -> str:
     import re
-    m = re.search(name + r'\s*=\s*"([^"]*)"', q or "")
+    m = re.search(r'(?<![\w])' + name + r'\s*=\s*"([^"]*)"', q or "")
     return m.group(1) if m else ""
 
 
@@ -246,6 +247,7 @@ class FastPath:
         if sliding and not all((START_PLACEHOLDER in u) or not u for u in hu):
             return None
         ns = doc.namespace
+        cluster = ""
         bms = []
         for a in aliases:
             url = cur.get(a) or hist.get(a, "")
@@ -253,13 +255,15 @@ class FastPath:
             bms.append((promql_metric_name(q) or a).replace("namespace_pod_", "namespace_app_pod_", 1))
             if not ns:
                 ns = _label(q, "namespace")
+            if not cluster:
+                cluster = _label(q, "cluster")
         keys = [((hs.get(a, "prometheus")), hu[i]) if sliding else (doc.id, a) for i, a in enumerate(aliases)]
         gsig = (tuple(aliases), hpa, sliding,
                 None if tmpl is None else (tuple(tmpl.priority), tuple(tmpl.is_increase), tuple(tmpl.is_absolute)))
         return JobPlan(fp, tuple(aliases), [cur.get(a, "") for a in aliases], [cs.get(a, "prometheus") for a in aliases],
                        [base.get(a, "") for a in aliases], [bs.get(a, "prometheus") for a in aliases], hu,
                        [hs.get(a, "prometheus") for a in aliases], sliding, keys, bms, ns or doc.namespace,
-                       doc.app_name, hpa, tmpl, gsig)
+                       doc.app_name, hpa, tmpl, gsig, cluster=cluster)
 
     @staticmethod
     def _canon(a: str) -> str:
@@ -561,7 +565,8 @@ class FastPath:
     # ------------------------------------------------------------------ finish
     def _impact_ids(self, ga: GroupArrays, works: list[FastWork], impact) -> np.ndarray:
         if ga.impact_version != impact.version:
-            ga.impact_ids = impact.ids([w.plan.namespace for w in works], [w.doc.app_name for w in works])
+            ga.impact_ids = impact.ids([w.plan.namespace for w in works], [w.doc.app_name for w in works],
+                                       [w.plan.cluster for w in works])
             ga.impact_version = impact.version
         return ga.impact_ids
 
@@ -570,7 +575,8 @@ class FastPath:
         if g["works"][0].plan.hpa:
             return
         ids = self._impact_ids(g["ga"], g["works"], impact)
-        impact.observe(ids, g["packed"][:, 0] == 1, now)
+        keys = None if impact.names else [(w.plan.cluster, w.plan.namespace, w.doc.app_name) for w in g["works"]]
+        impact.observe(ids, g["packed"][:, 0] == 1, now, keys=keys)
 
     def finish_group(self, g: dict, now: float, updates: list, hpalogs: list, outcome: dict,
                      bulk: list | None = None, impact=None) -> None:
@@ -605,7 +611,8 @@ class FastPath:
             if exp is not None:
                 if ga.impact_slots is None:
                     ga.impact_slots = exp.impact_slots([w.plan.namespace for w in works],
-                                                       [w.doc.app_name for w in works])
+                                                       [w.doc.app_name for w in works],
+                                                       [w.plan.cluster for w in works])
                 exp.table.set(ga.impact_slots, val.astype(np.float64))
             down = val >= self.b.cfg.downstream_threshold
             if impact.cfg.downstream_mode == "judge":

@@ -12,13 +12,19 @@ therefore [inferred]:
   series, weighted by that caller's share of its outgoing request rate;
 * impact[u] = max over callee paths of length <= hops of (product of weights)
   x callee anomaly score (K9, max-times semiring, fm_downstream_impact);
-* one process group per cluster (``dist.cluster_groups``); every rank scores
-  its own services (the canary tick), then ONE world all-gather of the
-  per-rank score shards builds the global score vector (C5) and every rank
-  runs K9 on the global graph (tens of thousands of nodes: microseconds),
-  keeping the verdict replicated so any rank can serve it.
+* benchmark path (:class:`FleetImpact`, config 5): every rank scores its
+  own services (the canary tick), then ONE world all-gather of the per-rank
+  score shards builds the global score vector (C5) and every rank runs K9 on
+  the global graph (tens of thousands of nodes: microseconds);
+* product path (:class:`DownstreamImpact`): the running brain exchanges
+  verdicts through the non-blocking world mailbox instead, so the ranks stay
+  shared-nothing (docs/guides/design.md:41).
 """
 from __future__ import annotations
+
+import hashlib
+import json
+import time
 
 import numpy as np
 import torch
@@ -111,16 +117,25 @@ class DownstreamImpact:
     downstream services", :27 multi-cluster aggregation).
 
     * the call graph is read every ``refresh_cycles`` cycles from the
-      ``caller``-tagged request-rate series (rank 0 queries, the edge list is
-      broadcast so every rank holds the same node ids); nodes are services
-      ``namespace/app`` (plus ``cluster`` when the series carry one), edges
-      ``caller -> app`` weighted by the caller's share of its outgoing rate,
-      with the per-API (``uri``) split of each edge kept for the reason;
+      ``caller``-tagged request-rate series by rank 0 and published through
+      the world mailbox (parallel/mailbox.py); the other ranks adopt the
+      newest published graph, so every rank builds the same node ids.  Nodes
+      are services ``(cluster, namespace, app)`` (``cluster`` from the series'
+      label, "" when the recording rule drops it), edges ``caller -> app``
+      weighted by the caller's share of its outgoing rate, with the per-API
+      (``uri``) split of each edge kept for the reason;
+    * a job maps to its node by its cluster (the ``cluster`` label matcher of
+      its queries, else ``BRAIN_CLUSTER``), falling back to the (namespace,
+      app) node when that is unique and the job or the graph carries no
+      cluster;
     * every cycle the verdicts of the services this rank scored are recorded
-      (1 = anomalous, expires after ``ttl_s``), ONE all-reduce(MAX) of the
-      node vector makes it global (C5), and K9 (``fm_downstream_impact``,
-      max-times over <= ``hops`` hops) gives impact[u] = the largest traffic
-      share of u that reaches an anomalous service;
+      (1 = anomalous, expires after ``ttl_s``); ranks exchange their verdict
+      vectors through the mailbox on a cadence (``DOWNSTREAM_SYNC_SECONDS``,
+      and whenever they change) -- never a collective, so a slow rank only
+      makes its verdicts older, it never stalls the others -- and K9
+      (``fm_downstream_impact``, max-times over <= ``hops`` hops) on the
+      element-wise max gives impact[u] = the largest traffic share of u that
+      reaches an anomalous service;
     * ``judge``: a job whose service has impact >= ``threshold`` is judged
       unhealthy with a ``downstream`` reason naming the callee path and its
       APIs; ``annotate``: the reason entry is added to unhealthy verdicts only.
@@ -140,14 +155,32 @@ class DownstreamImpact:
         self.clusters: list[str] = []
         self.local = np.zeros(0, np.float32)       # this rank's verdicts
         self.local_t = np.zeros(0)                  # when recorded
-        self.score = np.zeros(0, np.float32)        # global (after sync)
+        self.score = np.zeros(0, np.float32)        # global (after the exchange)
         self.impact = np.zeros(0, np.float32)
         self.version = 0
         self.cycles = 0
+        self.sig = b""                              # content hash of the graph (exchange compatibility)
+        self._unique: dict[tuple, int] = {}         # (namespace, app) -> node when unique
+        self._mb = None
+        self._mb_tried = False
+        self._graph_ts = None                       # publish time of the adopted graph (ranks > 0)
+        self._sync_t = -float("inf")
+        self._pub_t = -float("inf")
+        self._pub = None
+        self._peer: dict[int, tuple[float, np.ndarray]] = {}
+        self._peer_seen: dict[int, float] = {}
+        self._orphans: dict[tuple, tuple[float, float]] = {}
 
     @property
     def enabled(self) -> bool:
         return bool(self.cfg.downstream_edges_url) and self.cfg.downstream_mode != "off"
+
+    def _mailbox(self):
+        if not self._mb_tried:
+            self._mb_tried = True
+            from ..parallel.mailbox import Mailbox
+            self._mb = Mailbox.for_world("fm/impact/")
+        return self._mb
 
     # ------------------------------------------------------------------ graph
     def _fetch_edges(self) -> list:
@@ -167,13 +200,27 @@ class DownstreamImpact:
                         lb.get("uri", ""), float(v[-1])))
         return out
 
+    def needs_graph(self) -> bool:
+        """A rank > 0 that has not adopted rank 0's graph yet."""
+        mb = self._mailbox()
+        return mb is not None and mb.rank != 0 and self._graph_ts is None
+
     def refresh(self) -> None:
-        """Re-read the call graph (rank 0) and broadcast it (collective: every
-        rank calls this in the same cycle)."""
-        edges = self._fetch_edges() if self.info.rank == 0 else None
-        if D.is_dist():
-            edges = D.broadcast_object(edges)
-        self.set_edges(edges or [])
+        """Rank 0 re-reads the call graph and publishes it; the other ranks
+        adopt the newest published one (never waits for rank 0)."""
+        mb = self._mailbox()
+        if mb is None:
+            self.set_edges(self._fetch_edges())
+            return
+        if mb.rank == 0:
+            edges = self._fetch_edges()
+            self.set_edges(edges)
+            mb.put("graph", json.dumps(edges).encode())
+            return
+        got = mb.get("graph", 0)
+        if got is not None and got[0] != self._graph_ts:
+            self._graph_ts = got[0]
+            self.set_edges([tuple(e) for e in json.loads(got[1])])
 
     def set_edges(self, edges: list) -> None:
         keys = sorted({(c, ns, a) for c, ns, a, _, _, _, _ in edges} |
@@ -201,6 +248,10 @@ class DownstreamImpact:
         self.clusters = sorted({k[0] for k in keys})
         cid = {c: i for i, c in enumerate(self.clusters)}
         self.cluster_of = np.asarray([cid[k[0]] for k in keys], np.int64)
+        cnt: dict[tuple, int] = {}
+        for (c, ns, a), i in node.items():
+            cnt[(ns, a)] = cnt.get((ns, a), 0) + 1
+        self._unique = {(ns, a): i for (c, ns, a), i in node.items() if cnt[(ns, a)] == 1}
         loc, lt = np.zeros(len(keys), np.float32), np.full(len(keys), -np.inf)
         for k, i in old.items():                    # carry verdicts over to the new ids
             j = node.get(k)
@@ -209,34 +260,93 @@ class DownstreamImpact:
         self.local, self.local_t = loc, lt
         self.score = np.zeros(len(keys), np.float32)
         self.impact = np.zeros(len(keys), np.float32)
+        if self._orphans and keys:
+            ok = list(self._orphans.items())
+            j = self.ids([k[1] for k, _ in ok], [k[2] for k, _ in ok], [k[0] for k, _ in ok])
+            for (k, (v, t)), i in zip(ok, j):
+                if i >= 0:
+                    self.local[i], self.local_t[i] = v, t
+            self._orphans.clear()
+        self.sig = hashlib.blake2b(json.dumps([keys, src, dst]).encode(), digest_size=16).digest()
+        self._peer.clear()
+        self._peer_seen.clear()
+        self._pub = None
         self.version += 1
 
-    def ids(self, namespaces, apps, cluster: str = "") -> np.ndarray:
-        """Graph node of each (namespace, app) (-1: not in the call graph)."""
-        g = self.node.get
-        return np.fromiter((g((cluster, n, a), -1) for n, a in zip(namespaces, apps)), np.int64, len(apps))
+    def ids(self, namespaces, apps, clusters=None) -> np.ndarray:
+        """Graph node of each job's service (-1: not in the call graph).
+        ``clusters`` per job ("" / None: ``BRAIN_CLUSTER``)."""
+        g, u = self.node.get, self._unique.get
+        dflt = getattr(self.cfg, "brain_cluster", "") or ""
+        unlabelled = self.clusters == [""]
+        if clusters is None:
+            clusters = [dflt] * len(apps)
+        out = np.empty(len(apps), np.int64)
+        for i, (n, a, c) in enumerate(zip(namespaces, apps, clusters)):
+            c = c or dflt
+            k = g((c, n, a), -1)
+            if k < 0 and (not c or unlabelled):
+                k = u((n, a), -1)
+            out[i] = k
+        return out
 
     # ------------------------------------------------------------------ per cycle
-    def observe(self, ids: np.ndarray, anomalous: np.ndarray, now: float) -> None:
+    def observe(self, ids: np.ndarray, anomalous: np.ndarray, now: float, keys=None) -> None:
+        """Record verdicts.  Before any graph is known (a rank waiting for
+        rank 0's first graph) ``keys`` ((cluster, namespace, app) per entry)
+        are kept and mapped onto the graph when it arrives, so a one-shot
+        canary verdict is not lost to that start-up race."""
+        if not self.names and keys is not None:
+            for k, v in zip(keys, anomalous):
+                self._orphans[tuple(k)] = (float(v), now)
+            return
         ok = ids >= 0
         if ok.any():
             self.local[ids[ok]] = anomalous[ok].astype(np.float32)
             self.local_t[ids[ok]] = now
 
     def step(self, now: float) -> None:
-        """Global verdict vector (one all-reduce MAX) and K9 impact.  Every
-        rank calls it once per cycle (collective)."""
+        """This rank's live verdicts, max-merged with the latest verdicts the
+        other ranks published, then K9 impact.  Never blocks on a peer."""
         self.cycles += 1
         n = len(self.names)
         if n == 0:
             return
         live = np.where(now - self.local_t <= self.cfg.downstream_ttl_s, self.local, 0.0).astype(np.float32)
-        t = torch.from_numpy(live).to(self.device)
-        if D.is_dist():
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        imp = downstream_impact(self.graph, t.contiguous(), max(1, self.cfg.downstream_hops))
-        self.score = t.cpu().numpy()
+        mb = self._mailbox()
+        merged = live
+        if mb is not None:
+            t = time.monotonic()
+            if t - self._sync_t >= getattr(self.cfg, "downstream_sync_s", 0.5):
+                self._sync_t = t
+                self._exchange(mb, live, t)
+            wall = time.time()
+            for ts, v in self._peer.values():
+                if wall - ts <= self.cfg.downstream_ttl_s and len(v) == n:
+                    merged = np.maximum(merged, v)
+        tt = torch.from_numpy(np.ascontiguousarray(merged)).to(self.device)
+        imp = downstream_impact(self.graph, tt.contiguous(), max(1, self.cfg.downstream_hops))
+        self.score = merged
         self.impact = imp.cpu().numpy()
+
+    def _exchange(self, mb, live: np.ndarray, t: float) -> None:
+        # publish when the verdicts changed, and as a keep-alive so peers
+        # can tell a quiet rank from a dead one
+        if self._pub is None or not np.array_equal(live, self._pub) or \
+                t - self._pub_t > self.cfg.downstream_ttl_s / 4:
+            mb.put("verdict", self.sig + live.astype(np.uint8).tobytes())
+            self._pub, self._pub_t = live.copy(), t
+        for r in range(mb.world):
+            if r == mb.rank:
+                continue
+            got = mb.get("verdict", r)
+            if got is None or got[0] == self._peer_seen.get(r):
+                continue
+            self._peer_seen[r] = got[0]
+            if got[1][:16] == self.sig:           # same graph: same node ids
+                self._peer[r] = (got[0], np.frombuffer(got[1], np.uint8, offset=16).astype(np.float32))
+            else:
+                self._peer.pop(r, None)
 
     def cluster_health(self) -> dict[str, float]:
         """Per cluster: max over its services of max(anomaly, impact) (the

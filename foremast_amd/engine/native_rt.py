@@ -1,5 +1,5 @@
 """ctypes binding of ``libforemast_rt.so`` (csrc/runtime): native Prometheus
-response parsing and row packing.  Pure-Python fallbacks exist for both, so
+response parsing, row packing and the exporter's text exposition.  Pure-Python fallbacks exist for both, so
 the host runtime degrades gracefully when the library is not built."""
 from __future__ import annotations
 
@@ -33,6 +33,10 @@ def _load():
     lib.fm_pack_right.restype = None
     lib.fm_pack_left.argtypes = [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, ctypes.c_int]
     lib.fm_pack_left.restype = None
+    lib.fm_render_bound.argtypes = [c_vp, c_vp, c_i64]
+    lib.fm_render_bound.restype = c_i64
+    lib.fm_render_lines.argtypes = [ctypes.c_char_p, c_vp, c_vp, c_i64, c_vp, ctypes.c_char_p, c_i64, ctypes.c_int]
+    lib.fm_render_lines.restype = c_i64
     _lib = lib
     return lib
 

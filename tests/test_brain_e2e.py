@@ -396,3 +396,45 @@ def test_brain_lstm_multivariate_model():
     clock.t += 30
     r = brain.run_once()
     assert r["claimed"] >= 2 and brain._lstm_uni is not None and brain._lstm_uni.M is None
+
+
+def test_multi_cluster_impact_keys_jobs_by_cluster():
+    """two clusters run the same namespace/app set; only
+    cluster b's ledger fails.  Jobs carry their cluster (barrelman's
+    CLUSTER_NAME -> a ``cluster`` matcher in every query), the call graph
+    keys nodes by the edge series' ``cluster`` label, so only cluster b's
+    callers are judged ``downstream`` and only b's cluster gauge fires."""
+    from foremast_amd.engine.sources import Series, StaticSource, SyntheticSource
+    clock = Clock()
+    store = MemoryStore()
+    app = create_app(store)
+    clients = {c: AnalystClient.for_app(app, clock=clock, cluster=c) for c in ("a", "b")}
+    cfg = BrainConfig()
+    cfg.downstream_edges_url = "http://prom/api/v1/query?query=namespace_app_caller_uri_http_server_requests_rate"
+    e = lambda c, app_, caller, uri, r: Series({"cluster": c, "namespace": "default", "app": app_, "caller": caller,
+                                                "uri": uri}, np.array([T0]), np.array([r], np.float32))
+    edges = [e(c, "payments", "frontend", "/pay", 80.0) for c in ("a", "b")] + \
+            [e(c, "ledger", "payments", "/post", 5.0) for c in ("a", "b")]
+    src = SourceRouter(synthetic=StaticSource({"caller_uri": edges}, fallback=SyntheticSource(
+        faults={'app="ledger",cluster="b"': 6.0}, fault_after=T0 - 900)), force="synthetic")
+    exp = BrainExporter()
+    brain = Brain(store, cfg, sources=src, clock=clock, exporter=exp, worker_id="w0")
+    ids = {(c, a): clients[c].start_analyzing("default", a, None, _metrics(), 10, "continuous")
+           for c in ("a", "b") for a in ("frontend", "payments", "ledger")}
+    assert len(set(ids.values())) == 6                       # the cluster matcher makes the job ids distinct
+    brain.run_once()
+    st = {k: store.get(j) for k, j in ids.items()}
+    assert st[("b", "ledger")].status == "completed_unhealth"
+    for caller in ("payments", "frontend"):
+        d = st[("b", caller)]
+        assert d.status == "completed_unhealth", (caller, d.reason)
+        down = [r for r in json.loads(html.unescape(d.reason)) if r["name"] == "downstream"][0]
+        assert down["callees"][0]["callee"] == "default/ledger"
+    for a in ("frontend", "payments", "ledger"):
+        assert st[("a", a)].status != "completed_unhealth", (a, st[("a", a)].reason)
+    g = lambda c: exp.registry.get_sample_value("foremastbrain:cluster_impact_max", {"cluster": c})
+    assert g("b") == 1.0 and g("a") == 0.0
+    imp = "foremastbrain:namespace_app_pod_downstream_impact"
+    assert exp.table.get((imp, "default", "frontend", "b")) == pytest.approx(1.0)
+    assert exp.table.get((imp, "default", "frontend", "a")) == 0.0
+    assert 'cluster="b"' in exp.render().decode()

@@ -156,8 +156,15 @@ def _w_brain(rank, world, db, n_apps):
     brain = Brain(store, BrainConfig(), sources=SourceRouter.synthetic_only(faults={"app3": 8.0}, fault_after=1_760_000_000.0 - 600),
                   clock=clock, worker_id=f"rank{rank}", exporter=exp)
     r1 = brain.run_once()
-    r2 = brain.run_once()                  # a rank with no claim still joins the export sync
+    r2 = brain.run_once()
+    # C2 over the mailbox: ranks > 0 publish on a cadence (forced here),
+    # rank 0 merges whatever has arrived -- nobody waits inside a cycle
+    exp.exchange(force=True)
+    import torch.distributed as dist
+    dist.barrier()
+    exp.exchange(force=True)
     ups = {k[2]: v for k in exp.table.keys if k[0].endswith("_upper") for v in [exp.table.get(k)]}
+    dist.barrier()                         # rank 0 hosts the mailbox: leave together
     return r1.get("claimed", 0), r2.get("claimed", 0), ups
 
 
@@ -278,15 +285,29 @@ def _w_brain_impact(rank, world, db, caller, callee):
                     np.array([10.0], np.float32))]
     src = SourceRouter(synthetic=StaticSource({"caller_uri": edges}, fallback=SyntheticSource(
         faults={callee: 6.0}, fault_after=t0 - 900)), force="synthetic")
+    cfg.downstream_sync_s = 0.0
     brain = Brain(SQLiteStore(db), cfg, sources=src, clock=lambda: t0, worker_id=f"rank{rank}")
-    r = brain.run_once()
-    return r.get("claimed", 0), float(brain.impact.impact.max()) if len(brain.impact.impact) else 0.0
+    import time
+    import torch.distributed as dist
+    claimed = 0
+    for _ in range(200):                   # no lockstep: each rank cycles at its own pace
+        claimed += brain.run_once().get("claimed", 0) if claimed == 0 else 0
+        if rank == 1:
+            brain.run_once()
+        if len(brain.impact.impact) and brain.impact.impact.max() > 0.99:
+            break
+        time.sleep(0.02)
+    imp = float(brain.impact.impact.max()) if len(brain.impact.impact) else 0.0
+    for _ in range(5):                     # the caller's job is judged once the callee verdict arrived
+        brain.run_once()
+    dist.barrier()
+    return claimed, imp
 
 
 def test_downstream_impact_across_ranks(tmp_path):
     """The caller is owned by rank 0, its anomalous callee by rank 1: the
-    verdict all-reduce (C5) lets rank 0 judge its caller ``downstream`` in the
-    same cycle."""
+    verdict exchange over the mailbox (C5) lets rank 0 judge its caller
+    ``downstream`` without any per-cycle collective."""
     import html
     import json
     from foremast_amd.api import crd
@@ -308,3 +329,70 @@ def test_downstream_impact_across_ranks(tmp_path):
     assert d.status == "completed_unhealth", d.reason
     down = [r for r in json.loads(html.unescape(d.reason)) if r["name"] == "downstream"][0]
     assert down["callees"][0]["callee"] == f"default/{callee}" and down["callees"][0]["apis"] == ["/api"]
+
+
+def _w_slow_rank(rank, world, db, stall_s, run_s):
+    import time
+    from datetime import timedelta
+    from foremast_amd.config import BrainConfig
+    from foremast_amd.engine.brain import Brain
+    from foremast_amd.engine.exporter import BrainExporter
+    from foremast_amd.engine.sources import SourceRouter
+    from foremast_amd.parallel.mailbox import Mailbox
+    from foremast_amd.service.store import SQLiteStore
+    cfg = BrainConfig()
+    cfg.export_sync_s = 0.0
+    cfg.downstream_edges_url = "http://prom/api/v1/query?query=namespace_app_caller_uri_http_server_requests_rate"
+    cfg.downstream_sync_s = 0.0
+    cfg.downstream_refresh_cycles = 5
+    exp = BrainExporter()
+    t = {"now": 1_760_000_000.0}
+    brain = Brain(SQLiteStore(db), cfg, sources=SourceRouter.synthetic_only(), clock=lambda: t["now"],
+                  worker_id=f"rank{rank}", exporter=exp)
+    mb = Mailbox.for_world("test/")
+    cycles = 0
+    t0 = time.monotonic()
+    if rank == 1:
+        brain.run_once()
+        brain.run_once()                              # published its gauges
+        time.sleep(stall_s)                           # one very long cycle: >> the collective timeout
+        brain.run_once()
+        mb.put("done", b"1")                          # ...then it stops early (SIGTERM on this rank only)
+        return {"cycles": 3}
+    stalled_cycles = 0
+    while time.monotonic() - t0 < run_s:
+        t["now"] += 1.0
+        brain.run_once()
+        cycles += 1
+        if 1.0 < time.monotonic() - t0 < stall_s:
+            stalled_cycles += 1
+        time.sleep(0.01)
+    exp.pull(force=True)
+    r1 = {k[2] for k in exp.table.keys if k[0].endswith("_upper")}
+    age = exp.registry.get_sample_value("foremast_brain_rank_export_age_seconds", {"rank": "1"})
+    mb.store.wait(["test/done/1"], timedelta(seconds=60))
+    return {"cycles": cycles, "during_stall": stalled_cycles, "apps": sorted(r1), "age": age}
+
+
+def test_slow_rank_never_stalls_peers(tmp_path, monkeypatch):
+    """VERDICT r2 #3 / ADVICE r2: no collective runs in a brain cycle.  With
+    a 2 s collective timeout, rank 1 spends 5 s in one cycle and then stops
+    on its own: rank 0 keeps cycling the whole time (never blocks, never
+    aborts) and still exports rank 1's last published gauges, now stale."""
+    from foremast_amd.api import crd
+    from foremast_amd.controller.analyst import AnalystClient
+    from foremast_amd.service.app import create_app
+    from foremast_amd.service.store import SQLiteStore
+    monkeypatch.setenv("FOREMAST_COLLECTIVE_TIMEOUT_S", "2")
+    db = str(tmp_path / "jobs.db")
+    client = AnalystClient.for_app(create_app(SQLiteStore(db)), clock=lambda: 1_760_000_000.0)
+    m = crd.Metrics("prometheus", "http://prom/api/v1/", [crd.Monitoring("cpu_usage", "gauge", "cpu")])
+    apps = [f"app{i}" for i in range(8)]
+    for a in apps:
+        client.start_analyzing("default", a, None, m, 10, "continuous")
+    out = _run(_w_slow_rank, 2, db, 5.0, 7.0)
+    r0 = out[0]
+    assert r0["during_stall"] >= 20, r0            # rank 0 kept cycling while rank 1 was stuck
+    owners = {a: D.service_owner("", a, 2) for a in apps}
+    assert {a for a in apps if owners[a] == 1} <= set(r0["apps"])   # rank 1's gauges reached rank 0
+    assert r0["age"] is not None and r0["age"] >= 1.0                # ...and are reported stale
