@@ -291,13 +291,24 @@ def main() -> None:
         pub_graphs[:] = graphs
         run(max(1, args.warmup))
     torch.cuda.synchronize(dev)
-    # untimed steps until the warm-up has lasted --warmup-min-ms: every rank
-    # derives the same count from the MAX over ranks of the measured step time
-    w_ms = (time.perf_counter() - tw) * 1e3
-    per = D.all_reduce_max(w_ms / max(1, args.warmup + (args.warmup if args.publish == "graph" else 0)), dev)
-    w_ms = D.all_reduce_max(w_ms, dev)
-    extra = extra_warmup_steps(w_ms, per, args.warmup_min_ms)
-    run(extra)
+    # untimed steps until the warm-up has lasted --warmup-min-ms, in chunks:
+    # each chunk is sized from the steady-state step time of the previous
+    # one (the first chunk's estimate includes first-launch and capture cost,
+    # so it is re-measured rather than trusted); the elapsed time is
+    # MAX-reduced after every chunk so every rank runs the same steps
+    w_ms = D.all_reduce_max((time.perf_counter() - tw) * 1e3, dev)
+    per = w_ms / max(1, args.warmup + (args.warmup if args.publish == "graph" else 0))
+    extra = 0
+    while w_ms < args.warmup_min_ms and extra < 100000:
+        k = extra_warmup_steps(w_ms, per, args.warmup_min_ms)
+        k = max(1, min(k, 100000 - extra))
+        tc = time.perf_counter()
+        run(k)
+        torch.cuda.synchronize(dev)
+        dt = D.all_reduce_max((time.perf_counter() - tc) * 1e3, dev)
+        per = dt / k
+        extra += k
+        w_ms = D.all_reduce_max((time.perf_counter() - tw) * 1e3, dev)
     D.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -339,6 +350,7 @@ def main() -> None:
             "steps": args.steps,
             "warmup": args.warmup,
             "warmup_extra_steps": extra,
+            "warmup_ms": round(w_ms, 1),
             "ms_per_step": ms,
             "p50_decision_latency_ms": p50 * 1e3,
             "higher_is_better": True,

@@ -305,6 +305,8 @@ def config3e2e(args):
                                                                 "rest_poller.py"), "--url", f"http://127.0.0.1:{port}",
                                    "--ids", idf, "--rps", str(args.rest_poll_rps)],
                                   stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+        if poller.stdout.readline().strip() != "ready":       # timing starts under the REST load
+            raise SystemExit("REST poller did not start")
 
     def step():
         # cycles every poll interval inside the jobs' watch window (the

@@ -60,6 +60,9 @@ def main() -> None:
             elif sl < -1.0:
                 t_next = time.perf_counter()      # fell behind: do not burst
 
+    c0 = httpx.Client(base_url=a.url, timeout=30)
+    c0.get(f"/v1/healthcheck/id/{ids[0]}")
+    print("ready", flush=True)                        # the bench starts timing after this line
     t0 = time.perf_counter()
     ts = [threading.Thread(target=run, args=(k,), daemon=True) for k in range(a.threads)]
     for t in ts:

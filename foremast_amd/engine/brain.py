@@ -763,13 +763,20 @@ class Brain:
         return D.service_owner(namespace, app, self.info.world) == self.info.rank
 
     def load_checkpoint(self, dirpath: str) -> bool:
-        """Resume from this rank's latest checkpoint, or — after a world-size
-        change — from every rank's checkpoint of the previous world, keeping
-        only the HPA hysteresis and fitted models of services this rank owns
-        now (``service_owner`` of ``namespace:app``)."""
+        """Resume from this rank's latest checkpoint, or -- after a world-size
+        change, or when another world saved more recently than this rank's own
+        file -- from every rank's checkpoint of the newest world, keeping only
+        the HPA hysteresis and fitted models of services this rank owns now
+        (``service_owner`` of ``namespace:app``)."""
         from . import checkpoint
-        own = checkpoint.load_latest(dirpath, checkpoint.rank_tag(self.info.rank, self.info.world))
-        sets = [own] if own is not None else checkpoint.load_any_world(dirpath)
+        own = checkpoint.load_latest(dirpath, checkpoint.rank_tag(self.info.rank, self.info.world), with_time=True)
+        newest = checkpoint.newest_save(dirpath)
+        # this rank's own file is authoritative unless a DIFFERENT world saved
+        # after it (world 2 -> 4 -> 2: the 4-rank run's state is the newer one)
+        if own is not None and (newest is None or newest[0] == self.info.world or newest[1] <= own[2]):
+            sets = [own[:2]]
+        else:
+            sets = checkpoint.load_any_world(dirpath)
         if not sets:
             return False
         first = True

@@ -57,18 +57,15 @@ def _read(path: Path) -> tuple[dict[str, torch.Tensor], dict, float] | None:
     return load_file(str(path)), json.loads(md.get("meta", "{}")), float(md.get("saved_at", "0"))
 
 
-def load_latest(dirpath: str, tag: str = "") -> tuple[dict[str, torch.Tensor], dict] | None:
-    d = Path(dirpath)
-    lf = d / f"LATEST{tag}"
-    if not lf.exists():
-        return None
-    got = _read(d / lf.read_text().strip())
-    return None if got is None else got[:2]
+def saved_at(path: Path) -> float:
+    """The ``saved_at`` stamp of a checkpoint (header only, no tensor load)."""
+    from safetensors import safe_open
+    with safe_open(str(path), framework="pt") as f:
+        return float((f.metadata() or {}).get("saved_at", "0"))
 
 
-def load_any_world(dirpath: str) -> list[tuple[dict[str, torch.Tensor], dict]]:
-    """Every rank's latest checkpoint of the most recently saved world size
-    (a restart with a different world re-shards from all of them)."""
+def _latest_files(dirpath: str) -> dict[int, list[tuple[float, Path]]]:
+    """world size -> [(saved_at, file)] of every rank's LATEST pointer."""
     d = Path(dirpath)
     sets: dict[int, list[tuple[float, Path]]] = {}
     for lf in d.glob("LATEST*"):
@@ -83,7 +80,36 @@ def load_any_world(dirpath: str) -> list[tuple[dict[str, torch.Tensor], dict]]:
             continue
         p = d / lf.read_text().strip()
         if p.exists():
-            sets.setdefault(world, []).append((p.stat().st_mtime, p))
+            sets.setdefault(world, []).append((saved_at(p), p))
+    return sets
+
+
+def newest_save(dirpath: str) -> tuple[int, float] | None:
+    """(world size, saved_at) of the most recent checkpoint of any world."""
+    sets = _latest_files(dirpath)
+    if not sets:
+        return None
+    w = max(sets, key=lambda k: max(t for t, _ in sets[k]))
+    return w, max(t for t, _ in sets[w])
+
+
+def load_latest(dirpath: str, tag: str = "", with_time: bool = False):
+    """This tag's latest checkpoint as (tensors, meta), or with
+    ``with_time`` (tensors, meta, saved_at)."""
+    d = Path(dirpath)
+    lf = d / f"LATEST{tag}"
+    if not lf.exists():
+        return None
+    got = _read(d / lf.read_text().strip())
+    if got is None:
+        return None
+    return got if with_time else got[:2]
+
+
+def load_any_world(dirpath: str) -> list[tuple[dict[str, torch.Tensor], dict]]:
+    """Every rank's latest checkpoint of the most recently saved world size
+    (a restart with a different world re-shards from all of them)."""
+    sets = _latest_files(dirpath)
     if not sets:
         return []
     world = max(sets, key=lambda w: max(t for t, _ in sets[w]))

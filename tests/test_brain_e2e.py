@@ -438,3 +438,46 @@ def test_multi_cluster_impact_keys_jobs_by_cluster():
     assert exp.table.get((imp, "default", "frontend", "b")) == pytest.approx(1.0)
     assert exp.table.get((imp, "default", "frontend", "a")) == 0.0
     assert 'cluster="b"' in exp.render().decode()
+
+
+def test_checkpoint_prefers_newer_world_over_stale_own_file(tmp_path):
+    """world 2 -> 4 -> 2.  The 2-rank restart must resume from the
+    4-rank run's (newer) state, not from its own leftover world-2 files."""
+    from foremast_amd.ops import misc as MI
+    from foremast_amd.parallel import dist as D
+    import time as _time
+    import torch
+    apps = [f"app{i}" for i in range(16)]
+
+    def save_world(world, flips):
+        for rank in range(world):
+            b = Brain(MemoryStore(), BrainConfig(), worker_id=f"r{rank}")
+            b.info = D.DistInfo(rank, world, rank)
+            mine = [a for a in apps if D.service_owner("ns", a, world) == rank]
+            ids = [f"{a}:ns:hpa" for a in mine]
+            sl = b.hpa.slots(ids)
+            for a, j in zip(mine, ids):
+                b.hpa.owner[j] = ("ns", a)
+            n = len(ids)
+            b.hpa.scatter(sl, MI.HpaState(torch.ones(n, dtype=b.hpa.state.last_dir.dtype),
+                                          torch.zeros(n, dtype=b.hpa.state.last_time.dtype),
+                                          torch.full((n,), flips, dtype=b.hpa.state.flips.dtype),
+                                          torch.zeros(n, dtype=b.hpa.state.flip_t0.dtype)))
+            b.save_checkpoint(str(tmp_path))
+            _time.sleep(0.01)
+    save_world(2, 1)            # first run: 2 ranks
+    save_world(4, 7)            # then 4 ranks (newer state)
+    got = {}
+    for rank in range(2):       # back to 2 ranks
+        b = Brain(MemoryStore(), BrainConfig(), worker_id=f"n{rank}")
+        b.info = D.DistInfo(rank, 2, rank)
+        assert b.load_checkpoint(str(tmp_path))
+        for j, st in b.hpa_state.items():
+            got[j] = int(st.flips[0])
+    assert set(got) == {f"{a}:ns:hpa" for a in apps} and set(got.values()) == {7}
+    # the same world saving again afterwards is authoritative once more
+    save_world(2, 3)
+    b = Brain(MemoryStore(), BrainConfig(), worker_id="n0")
+    b.info = D.DistInfo(0, 2, 0)
+    assert b.load_checkpoint(str(tmp_path))
+    assert {int(st.flips[0]) for st in b.hpa_state.values()} == {3}
