@@ -309,13 +309,15 @@ class Brain:
         """A multivariate model scores a batch whose rows are whole jobs of
         exactly its M metrics (one sequence per job); any other batch uses a
         univariate forecaster of the same size."""
-        m = self._lstm_model()
-        if m.M is None:
-            return m
         counts: dict[int, int] = {}
         for r in rows:
             counts[r.job] = counts.get(r.job, 0) + 1
-        if all(v == m.M for v in counts.values()):
+        return self.lstm_for_jobs_of(set(counts.values()))
+
+    def lstm_for_jobs_of(self, sizes: set[int]):
+        """The forecaster for a batch of whole jobs with these metric counts."""
+        m = self._lstm_model()
+        if m.M is None or sizes == {m.M}:
             return m
         if self._lstm_uni is None:
             from ..models.lstm import LSTMForecaster
@@ -502,29 +504,17 @@ class Brain:
 
     def _fast_hpa_forecasts(self, g: dict) -> None:
         works, M = g["works"], g["M"]
-        store = g["store"]
-        view = store.view()
-        rows = torch.as_tensor(g["hist_rows"].astype(np.int64), device=view.hist.device)
-        h = view.hist.index_select(0, rows).contiguous()
-        algo = self.cfg.hpa_forecast_algorithm
-        keys = [(f"{w.plan.namespace}/{w.doc.app_name}", a, bm, zoo.canonical(algo))
-                for w in works for a, bm in zip(w.plan.aliases, w.plan.base_metrics)]
-        ctx = None
-        if self.model_cache.capacity > 0 and zoo.canonical(algo) in zoo.ES_KINDS:
-            ctx = zoo.CacheContext(self.model_cache, keys, store.last_t[g["hist_rows"]].astype(np.float64),
-                                   self.step, self.clock())
         try:
-            fc, _ = zoo.forecast(algo, h, view.T, max(1, self.cfg.hpa_forecast_steps), lstm_model=self.lstm_model,
-                                 cache=ctx)
+            peak = self.fast.hpa_forecast(g)
         except (ValueError, RuntimeError) as e:
             log.warning("HPA forecast skipped: %s", e)
             return
-        peak = torch.nan_to_num(fc, nan=float("-inf")).amax(1).cpu().numpy()
-        for j, w in enumerate(works):
-            for m in range(M):
-                v = peak[j * M + m]
-                if np.isfinite(v):
-                    self.exporter.set_forecast(w.plan.base_metrics[m], w.plan.namespace, w.doc.app_name, float(v))
+        ok = np.isfinite(peak)
+        if ok.any():
+            j = np.flatnonzero(ok)
+            self.exporter.set_forecasts([works[k // M].plan.base_metrics[k % M] for k in j],
+                                        [works[k // M].plan.namespace for k in j],
+                                        [works[k // M].doc.app_name for k in j], peak[j])
 
     def _score_general(self, works: list[Work], updates: list, outcome: dict) -> list:
         """Score the general-path jobs: one batch, or job by job when the

@@ -78,6 +78,7 @@ class JobPlan:
     export_slots: np.ndarray | None = None
     hpa_slots: np.ndarray | None = None
     cluster: str = ""                      # ``cluster`` label matcher of the job's queries
+    algos: tuple = ()                      # canonical ML_ALGORITHM per metric (metric_typeN overrides)
 
 
 @dataclass
@@ -133,6 +134,88 @@ class GroupArrays:
     impact_version: int = -1
     impact_slots: np.ndarray | None = None     # exporter slots of the downstream-impact gauge
     marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
+    models: object = None                      # ModelArrays of a forecasting group (cached with the arrays)
+
+
+@dataclass
+class ModelSub:
+    """The rows of a group scored by one model."""
+    algo: str
+    ms: list                                   # metric indices of the group
+    idx: torch.Tensor | None                   # rows of the group (None: all)
+    rm: torch.Tensor                           # int32 resident rows
+    shift: torch.Tensor | None                 # int32: dense column c <- buffer column c - shift
+    lim: torch.Tensor | None                   # int32: buffer columns < lim are the row's
+    T: int                                     # dense (right-aligned) history length
+    tables: object
+    keys: list                                 # fitted-model cache keys
+    t_last: np.ndarray | None                  # time of each row's last dense column
+    valid: torch.Tensor | None                 # int32 bit0 history gate, bit1 current present
+    hor: torch.Tensor | None                   # int64 [rows, n] horizon of every current point
+    H: int
+    M: int
+
+
+@dataclass
+class ModelArrays:
+    stamp: object
+    subs: list
+    lastk: torch.Tensor                        # [R] newest finite current point of each row
+
+
+@dataclass
+class _Flags:
+    flags: torch.Tensor
+    count: torch.Tensor
+
+
+class LazyHist:
+    """Right-aligned ``[R, T]`` history of a group's resident rows,
+    materialised (``fm_gather_cols``) only as far as a model reads it: a
+    cached Holt-Winters fit advanced over k new samples gathers k columns, an
+    LSTM its lookback window, a cold fit the whole window.  Supports what the
+    model zoo and the fitted-model cache use: ``shape``, ``device``,
+    ``hist[:, a:b]`` and ``index_select(0, rows)``."""
+
+    def __init__(self, src: torch.Tensor, rm: torch.Tensor, shift: torch.Tensor, lim: torch.Tensor, T: int):
+        self.src, self.rm, self.shift, self.lim, self.T = src, rm, shift, lim, int(T)
+        self.shape = (int(rm.numel()), self.T)
+        self.device = src.device
+        self.dtype = torch.float32
+        self.is_cuda = src.is_cuda
+        self._buf = None
+        self._lo = None
+
+    def materialize(self, lo: int = 0) -> torch.Tensor:
+        """The dense buffer with columns ``[lo, T)`` filled."""
+        from ..ops import misc as MI
+        lo = max(0, min(int(lo), self.T))
+        if self._buf is None:
+            self._buf = torch.empty((self.shape[0], max(1, self.T)), dtype=torch.float32, device=self.device)
+            self._lo = self.T
+        if lo < self._lo:
+            MI.gather_cols(self.src, self.rm, (lo - self.shift).to(torch.int32), self.lim, self._lo - lo,
+                           self._buf[:, lo:])
+            self._lo = lo
+        return self._buf
+
+    def __getitem__(self, key):
+        rows, cols = key
+        if rows != slice(None) or not isinstance(cols, slice):
+            raise IndexError("LazyHist supports hist[:, a:b] only")
+        return self.materialize(cols.start or 0)[:, cols]
+
+    def index_select(self, dim: int, idx: torch.Tensor) -> torch.Tensor:
+        from ..ops import misc as MI
+        assert dim == 0
+        idx = idx.to(self.rm.device).long()
+        out = torch.empty((int(idx.numel()), max(1, self.T)), dtype=torch.float32, device=self.device)
+        MI.gather_cols(self.src, self.rm.index_select(0, idx), (-self.shift.index_select(0, idx)).to(torch.int32),
+                       self.lim.index_select(0, idx), self.T, out)
+        return out
+
+    def contiguous(self) -> torch.Tensor:
+        return self.materialize(0)
 
 
 def _label(q: str, name: str) -> str:
@@ -233,8 +316,6 @@ class FastPath:
         aliases = list(cur) if not hpa else (list(hist) or list(cur))
         if not aliases or len(aliases) > MAX_M:
             return None
-        if any(self._canon(cfg.algorithm_for(a)) != "moving_average_all" for a in aliases):
-            return None
         tmpl = None
         if hpa:
             cfgs = {k: {"priority": v.priority, "isIncrease": v.is_increase, "isAbsolute": v.is_absolute}
@@ -258,12 +339,14 @@ class FastPath:
             if not cluster:
                 cluster = _label(q, "cluster")
         keys = [((hs.get(a, "prometheus")), hu[i]) if sliding else (doc.id, a) for i, a in enumerate(aliases)]
+        algos = tuple(self._canon(cfg.algorithm_for(a)) for a in aliases)
         gsig = (tuple(aliases), hpa, sliding,
-                None if tmpl is None else (tuple(tmpl.priority), tuple(tmpl.is_increase), tuple(tmpl.is_absolute)))
+                None if tmpl is None else (tuple(tmpl.priority), tuple(tmpl.is_increase), tuple(tmpl.is_absolute)),
+                algos)
         return JobPlan(fp, tuple(aliases), [cur.get(a, "") for a in aliases], [cs.get(a, "prometheus") for a in aliases],
                        [base.get(a, "") for a in aliases], [bs.get(a, "prometheus") for a in aliases], hu,
                        [hs.get(a, "prometheus") for a in aliases], sliding, keys, bms, ns or doc.namespace,
-                       doc.app_name, hpa, tmpl, gsig, cluster=cluster)
+                       doc.app_name, hpa, tmpl, gsig, cluster=cluster, algos=algos)
 
     @staticmethod
     def _canon(a: str) -> str:
@@ -515,6 +598,8 @@ class FastPath:
         dev = self.b.device
         store = self.sliding if p0.sliding else self.static
         ga = self._arrays(works, key if key is not None else ("adhoc",) + p0.group)
+        if any(a != "moving_average_all" for a in p0.algos):
+            return self._score_models(works, now, ga, store)
         # last-use stamps for idle eviction (max_idle_cycles = 64): refreshed
         # every 16 cycles, not every cycle -- an 80k-row scatter is ~0.25 ms
         # of host time, and a stamp at most 15 cycles old never evicts a live row
@@ -561,6 +646,206 @@ class FastPath:
         LIB.call("fm_compact_anomalies", ptr(dec.flags), dec.flags.shape[1], ptr(cur_d), cur_d.stride(0), n,
                  ptr(dec.count), R, idx.shape[0], ptr(ctr), ptr(idx), ptr(val), stream_of(cur_d))
         return idx, val, ctr
+
+    # ------------------------------------------------------------------ forecasting models
+    def _model_arrays(self, ga: GroupArrays, works: list[FastWork], store: ResidentHistory) -> "ModelArrays":
+        """Per-algorithm row subsets of a group with everything that does not
+        change while the group's arrays are reused: row map, alignment of
+        each row's right end, history gate, horizons, tables, cache keys."""
+        stamp = (store.e, store.ws, store.t0) if store.sliding else None
+        md = ga.models
+        if md is not None and md.stamp == stamp:
+            return md
+        from ..models import zoo
+        b = self.b
+        cfg = b.cfg
+        p0 = works[0].plan
+        M, S = len(p0.aliases), len(works)
+        dev = b.device
+        rowmap = ga.rowmap.astype(np.int64)
+        T, shift, lim = self._alignment(rowmap, store)
+        t_last = store.last_t[rowmap]
+        cur_t = ga.cur_t
+        ok = np.isfinite(cur_t) & np.isfinite(t_last)[:, None]
+        with np.errstate(invalid="ignore"):
+            h = np.where(ok, np.rint((cur_t - t_last[:, None]) / b.step), 1.0)
+        hor = np.maximum(1, h).astype(np.int64)
+        valid = ((store.nfin[rowmap] >= max(cfg.min_historical_points, 1)).astype(np.int32)
+                 | (np.isfinite(ga.cur).any(1).astype(np.int32) << 1))
+        series = [f"{w.plan.namespace}/{w.doc.app_name}" for w in works]
+        i32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=dev)
+        subs = []
+        by_algo: dict[str, list[int]] = {}
+        for m, a in enumerate(p0.algos):
+            by_algo.setdefault(a, []).append(m)
+        for algo, ms in by_algo.items():
+            if len(ms) == M:
+                idx = None
+                rows = np.arange(S * M)
+            else:
+                rows = (np.arange(S)[:, None] * M + np.asarray(ms)[None, :]).reshape(-1)
+                idx = torch.as_tensor(rows, device=dev)
+            keys = [(series[r // M], p0.aliases[r % M], p0.base_metrics[r % M], algo) for r in rows]
+            hr = hor[rows]
+            subs.append(ModelSub(algo, ms, idx, i32(rowmap[rows]), i32(shift[rows]), i32(lim[rows]), T,
+                                 zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev), keys, t_last[rows],
+                                 torch.as_tensor(valid[rows], device=dev),
+                                 torch.as_tensor(hr, device=dev), max(1, int(hr.max()) if hr.size else 1), len(ms)))
+        fin = np.isfinite(ga.cur)
+        n = ga.cur.shape[1]
+        lastk = np.where(fin.any(1), n - 1 - np.argmax(fin[:, ::-1], axis=1), n - 1)
+        md = ga.models = ModelArrays(stamp, subs, torch.as_tensor(lastk.astype(np.int64), device=dev))
+        return md
+
+    def _score_models(self, works: list[FastWork], now: float, ga: GroupArrays, store: ResidentHistory) -> dict:
+        """A group whose metrics use forecasting / other models: pairwise
+        tests, then per algorithm one batched model call over the group's
+        rows read out of the resident store, then the band decision, the
+        service reduction and GPU compaction -- the same verdict data the
+        moving_average_all tick hands to ``finish_group``."""
+        from ..models import zoo
+        b = self.b
+        cfg = b.cfg
+        p0 = works[0].plan
+        M, S = len(p0.aliases), len(works)
+        R = S * M
+        dev = b.device
+        n = ga.cur.shape[1]
+        if self.cycle - ga.marked >= USED_STAMP_EVERY:
+            store.used[ga.rowmap] = self.cycle
+            ga.marked = self.cycle
+        md = self._model_arrays(ga, works, store)
+        diff = None
+        if ga.base_d is not None:
+            pcfg = C.PairwiseConfig(cfg.pairwise_algorithm, cfg.pairwise_threshold, cfg.min_mann_white,
+                                    cfg.min_wilcoxon, cfg.min_kruskal)
+            _, _, diff = C.pairwise_tests(ga.cur_d, ga.base_d, pcfg)
+        NW = max(1, (n + 63) // 64)
+        single = len(md.subs) == 1
+        if not single:
+            up = torch.full((R, n), float("nan"), device=dev)
+            lo = torch.full((R, n), float("nan"), device=dev)
+            flags = torch.zeros((R, NW), dtype=torch.int64, device=dev)
+            count = torch.zeros((R,), dtype=torch.int32, device=dev)
+            score = torch.zeros((R,), dtype=torch.float32, device=dev)
+            valid = torch.zeros((R,), dtype=torch.int32, device=dev)
+        fc_keep = {}
+        hpa_algo = zoo.canonical(cfg.hpa_forecast_algorithm) if (p0.hpa and cfg.hpa_forecast_algorithm) else None
+        for sub in md.subs:
+            cur = ga.cur_d if sub.idx is None else ga.cur_d.index_select(0, sub.idx)
+            dsub = None if diff is None or sub.idx is None else diff.index_select(0, sub.idx)
+            dsub = diff if sub.idx is None else dsub
+            lazy = LazyHist(store.buf, sub.rm, sub.shift, sub.lim, sub.T)
+            algo = sub.algo
+            if algo in ("moving_average_all", "bivariate_normal", "moving_average"):
+                lo_col = 0
+                if algo == "moving_average":
+                    w = min(sub.T, max(4, (60 + 3) // 4 * 4))
+                    lo_col = (sub.T - w) // 4 * 4
+                dec = zoo.decide(algo, lazy.materialize(lo_col), sub.T, cur, sub.hor, sub.M, sub.tables, dsub)
+            else:
+                H = sub.H
+                if hpa_algo == algo:
+                    H = max(H, max(1, cfg.hpa_forecast_steps))
+                fc, sigma = self._forecast(algo, lazy, sub, H)
+                if hpa_algo == algo:
+                    fc_keep[algo] = (sub, fc)
+                dec = zoo.band(fc, sigma, sub.hor, cur, sub.M, sub.tables, dsub, sub.valid)
+            if single:
+                up, lo, flags, count, score, valid = dec.upper, dec.lower, dec.flags, dec.count, dec.score, dec.valid
+            else:
+                i = sub.idx
+                up[i], lo[i], flags[i] = dec.upper, dec.lower, dec.flags
+                count[i], score[i], valid[i] = dec.count, dec.score, dec.valid.to(torch.int32)
+        valid = valid.to(torch.int32).contiguous()
+        packed = C.service_reduce(count.contiguous(), score.contiguous(), valid, M)
+        up = up.contiguous()
+        lo = lo.contiguous()
+        li = md.lastk[:, None]
+        stats = torch.stack([torch.full((R,), float("nan"), device=dev), torch.full((R,), float("nan"), device=dev),
+                             up.gather(1, li).squeeze(1), lo.gather(1, li).squeeze(1)], 1)
+        dec = _Flags(flags.contiguous(), count.contiguous())
+        if dev.type == "cuda":
+            cap = max(1024, min(R * n, 1 << 16))
+            idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, cap)
+            host = [t.to("cpu", non_blocking=True) for t in (packed, stats, dec.count, ctr)]
+            torch.cuda.current_stream(dev).synchronize()
+            packed_h, stats_h, count_h, total = (t.numpy() for t in host)
+            total = int(total[0])
+            if total > cap:
+                idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, total)
+            idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
+        else:
+            packed_h, stats_h, count_h = packed.numpy(), stats.numpy(), dec.count.numpy()
+            ix, _ = C.compact_anomalies(dec, ga.cur_d)
+            idx = ix.numpy()
+        if len(idx):
+            k = idx[:, 0].astype(np.int64) * n + idx[:, 1]
+            k.sort()
+            idx = np.stack([k // n, k % n], 1).astype(np.int32)
+        return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
+                "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "hist_rows": ga.rowmap,
+                "store": store, "pts": (up, lo), "fc": fc_keep}
+
+    def _forecast(self, algo: str, lazy: "LazyHist", sub: "ModelSub", H: int):
+        from ..models import zoo
+        b = self.b
+        ctx = None
+        if algo in zoo.ES_KINDS and b.model_cache.capacity > 0:
+            ctx = zoo.CacheContext(b.model_cache, sub.keys, sub.t_last, b.step, b.clock())
+        lstm = b.lstm_for_jobs_of({sub.M}) if algo == "lstm" else b.lstm_model
+        if ctx is not None:
+            hist = lazy                                   # hits read only their new columns
+        elif algo == "lstm":
+            hist = lazy.materialize(sub.T - min(lstm.L, sub.T))
+        else:
+            hist = lazy.materialize(0)
+        return zoo.forecast(algo, hist, sub.T, H, lstm_model=lstm, cache=ctx)
+
+    def hpa_forecast(self, g: dict) -> np.ndarray:
+        """Peak of the ``HPA_FORECAST_STEPS`` forecast per row of an HPA group
+        (reusing the scoring forecast when the scoring model is the same)."""
+        from ..models import zoo
+        b = self.b
+        algo = zoo.canonical(b.cfg.hpa_forecast_algorithm)
+        steps = max(1, b.cfg.hpa_forecast_steps)
+        works, M, ga, store = g["works"], g["M"], g["ga"], g["store"]
+        got = g.get("fc", {}).get(algo)
+        if got is not None and got[0].idx is None:
+            fc = got[1][:, :steps]
+        else:
+            T, shift, lim = self._align(ga, store)
+            rm = torch.as_tensor(ga.rowmap.astype(np.int32), device=b.device)
+            keys = [(f"{w.plan.namespace}/{w.doc.app_name}", a, bm, algo) for w in works
+                    for a, bm in zip(w.plan.aliases, w.plan.base_metrics)]
+            sub = ModelSub(algo, list(range(M)), None, rm, shift, lim, T, None, keys,
+                           store.last_t[ga.rowmap.astype(np.int64)], None, None, steps, M)
+            fc, _ = self._forecast(algo, LazyHist(store.buf, rm, shift, lim, T), sub, steps)
+        return torch.nan_to_num(fc, nan=float("-inf")).amax(1).cpu().numpy()
+
+    @staticmethod
+    def _alignment(rowmap: np.ndarray, store: ResidentHistory) -> tuple[int, np.ndarray, np.ndarray]:
+        """Right-align every row at its newest sample: (dense length T,
+        shift, lim) with dense column c <- buffer column c - shift[r] for
+        buffer columns < lim[r].  T = the longest row of the group (static:
+        columns written; sliding: window start .. newest sample), as the
+        general path packs a batch right-aligned to its longest history."""
+        if store.sliding:
+            lt = store.last_t[rowmap]
+            end = np.where(np.isfinite(lt), store.col(np.where(np.isfinite(lt), lt, store.t0)) + 1, store.ws)
+            end = np.clip(end, store.ws, store.e)
+            start = np.full(len(rowmap), store.ws)
+        else:
+            end = store.nlen[rowmap]
+            start = np.zeros(len(rowmap), np.int64)
+        T = max(1, int((end - start).max()) if len(end) else 1)
+        return T, (T - end).astype(np.int64), end.astype(np.int64)
+
+    def _align(self, ga: GroupArrays, store: ResidentHistory):
+        dev = self.b.device
+        T, shift, lim = self._alignment(ga.rowmap.astype(np.int64), store)
+        i32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=dev)
+        return T, i32(shift), i32(lim)
 
     # ------------------------------------------------------------------ finish
     def _impact_ids(self, ga: GroupArrays, works: list[FastWork], impact) -> np.ndarray:
@@ -652,13 +937,23 @@ class FastPath:
             outcome[ST.COMPLETED_UNKNOWN] = outcome.get(ST.COMPLETED_UNKNOWN, 0) + int(unknown.sum())
         if unh.any():
             row_start = np.searchsorted(anom[:, 0], np.arange(S) * M) if len(anom) else None
-            for j in np.flatnonzero(unh):
+            js = np.flatnonzero(unh)
+            pts = None
+            if g.get("pts") is not None:
+                # per-point bands (forecasting models): one gather + copy for
+                # every unhealthy job's rows
+                rows = (js[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+                ri = torch.as_tensor(rows, device=g["pts"][0].device)
+                up_h = g["pts"][0].index_select(0, ri).cpu().numpy()
+                lo_h = g["pts"][1].index_select(0, ri).cpu().numpy()
+                pts = {int(r): k for k, r in enumerate(rows)}, up_h, lo_h
+            for j in js:
                 extra = None
                 if down is not None and down[j]:
                     u = int(ga.impact_ids[j])
                     extra = {"name": "downstream", "impact": round(float(impact.impact[u]), 4),
                              "callees": impact.explain(u)}
-                st, fields = self._unhealthy(works[j], j, M, anom, row_start, cur, cur_t, stats, extra)
+                st, fields = self._unhealthy(works[j], j, M, anom, row_start, cur, cur_t, stats, extra, pts)
                 updates.append((works[j].doc.id, fields))
             outcome[ST.COMPLETED_UNHEALTH] = outcome.get(ST.COMPLETED_UNHEALTH, 0) + int(unh.sum())
         if flush:
@@ -667,7 +962,7 @@ class FastPath:
         if closed.any():
             self._release([works[j] for j in np.flatnonzero(closed)])
 
-    def _unhealthy(self, w: FastWork, j: int, M: int, anom, row_start, cur, cur_t, stats, extra=None):
+    def _unhealthy(self, w: FastWork, j: int, M: int, anom, row_start, cur, cur_t, stats, extra=None, pts=None):
         r0 = j * M
         a0 = row_start[j] if row_start is not None else 0
         a1 = np.searchsorted(anom[:, 0], r0 + M) if len(anom) else 0
@@ -683,8 +978,12 @@ class FastPath:
             flat = [x for pair in zip(ts, vals) for x in pair]
             alias = w.plan.aliases[m]
             anomalies[alias] = {"tags": "", "values": flat}
-            reasons.append({"name": alias, "ts": ts, "values": vals, "upper": float(stats[r, 2]),
-                            "lower": float(stats[r, 3])})
+            if pts is None:
+                ub, lb = float(stats[r, 2]), float(stats[r, 3])
+            else:                                   # the band at the first anomalous point
+                k = pts[0][r]
+                ub, lb = float(pts[1][k, e[0, 1]]), float(pts[2][k, e[0, 1]])
+            reasons.append({"name": alias, "ts": ts, "values": vals, "upper": ub, "lower": lb})
         if extra is not None:
             reasons.append(extra)
             anomalies["downstream"] = {"tags": "", "values": []}

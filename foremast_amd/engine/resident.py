@@ -31,8 +31,15 @@ Two layouts:
 moving_average_all (the deployed default, foremast-brain.yaml:24-25) skips
 non-finite samples, so a row's statistics depend only on which samples sit in
 its window, not on their column: both layouts reproduce the per-cycle
-re-fetch exactly.  Rows whose model depends on sample position (forecasters)
-keep the per-cycle packed path.
+re-fetch exactly, and the statistics kernels read rows in place.  Models
+whose output depends on sample position (exponential smoothing /
+Holt-Winters, Prophet, LSTM, bivariate) read each row right-aligned at its
+newest sample: ``fm_gather_cols`` (csrc/kernels/gather.hip) copies exactly
+the columns a model needs (``nlen`` locates a static row's end; a sliding
+row ends at the window end), so a cached fit advanced over k new samples
+moves k columns per row, not the 7-day window.  ``nfin`` counts each row's
+finite samples in the window (the ``MIN_HISTORICAL_DATA_POINT_TO_MEASURE``
+gate) without reading the row.
 """
 from __future__ import annotations
 
@@ -72,6 +79,8 @@ class ResidentHistory:
         self.slot: dict = {}
         self.free: list[int] = []
         self.last_t = np.zeros(0, np.float64)       # time of each row's newest sample (-inf: none)
+        self.nlen = np.zeros(0, np.int64)           # static: columns written (the row's right end)
+        self.nfin = np.zeros(0, np.int64)           # finite samples inside the window (history gate)
         self.used = np.zeros(0, np.int64)           # cycle of last use (eviction)
         self.occ = np.zeros(0, bool)                # row holds a key
         self.keys: list = []
@@ -99,6 +108,8 @@ class ResidentHistory:
         self.buf = nb
         self.free.extend(range(new_cap - 1, cap - 1, -1))
         self.last_t = np.concatenate([self.last_t, np.full(new_cap - cap, -np.inf)])
+        self.nlen = np.concatenate([self.nlen, np.zeros(new_cap - cap, np.int64)])
+        self.nfin = np.concatenate([self.nfin, np.zeros(new_cap - cap, np.int64)])
         self.used = np.concatenate([self.used, np.zeros(new_cap - cap, np.int64)])
         self.occ = np.concatenate([self.occ, np.zeros(new_cap - cap, bool)])
         self.keys.extend([None] * (new_cap - cap))
@@ -137,6 +148,8 @@ class ResidentHistory:
             for r in rows:
                 self.keys[r] = None
                 self.last_t[r] = -np.inf
+            self.nlen[rows] = 0
+            self.nfin[rows] = 0
             self.occ[rows] = False
             self.free.extend(rows)
         return len(rows)
@@ -162,6 +175,8 @@ class ResidentHistory:
             src = src.pin_memory().to(self.device, non_blocking=True)
         self.buf.index_copy_(0, torch.as_tensor(rows, dtype=torch.int64).to(self.device), src)
         self.last_t[rows] = t_last
+        self.nlen[rows] = [min(len(v), self.width) for v in values]
+        self.nfin[rows] = [int(np.isfinite(np.asarray(v[:self.width], np.float32)).sum()) for v in values]
         self.bytes_in += packed.nbytes
 
     def view(self) -> HistView:
@@ -198,6 +213,9 @@ class ResidentHistory:
         # included) must read as missing
         lo, hi = max(0, self.ws), max(0, ws_new)
         if hi > lo and self.buf.shape[0]:
+            # finite samples leaving the window no longer count (history gate)
+            gone = torch.isfinite(self.buf[:, lo:min(hi, self.width)]).sum(1).cpu().numpy()
+            self.nfin -= gone.astype(np.int64)
             self.buf[:, lo:min(hi, self.width)] = float("nan")
         self.e, self.ws = e_new, max(ws_new, 0)
 
@@ -238,6 +256,9 @@ class ResidentHistory:
         ok = (c >= self.ws) & (c < self.e) & np.isfinite(v)
         r, c, v, t = r[ok], c[ok], v[ok], t[ok]
         if len(r):
+            prev = np.where(np.isfinite(self.last_t[r]), self.col(np.where(np.isfinite(self.last_t[r]),
+                                                                            self.last_t[r], self.t0)), -1)
+            np.add.at(self.nfin, r[c > prev], 1)          # new columns only (a re-sent sample counts once)
             np.maximum.at(self.last_t, r, t)
             flat = torch.from_numpy(r * self.width + c)
             vals = torch.from_numpy(np.ascontiguousarray(v))

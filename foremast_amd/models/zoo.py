@@ -132,13 +132,22 @@ def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizo
     H = int(horizon.max().item()) if horizon.numel() else 1
     H = max(H, 1)
     fc, sigma = forecast(algo, hist, T, H, period=period, lstm_model=lstm_model, cache=cache)
+    return band(fc, sigma, horizon, cur, M, tables, diff, _valid(hist, T, cur, tables.min_hist))
+
+
+def band(fc: torch.Tensor, sigma: torch.Tensor, horizon: torch.Tensor, cur: torch.Tensor, M: int, tables: Tables,
+         diff: torch.Tensor | None, valid: torch.Tensor) -> RowDecision:
+    """Forecast -> per-point bands and decisions: each current point is
+    judged against the forecast at its own horizon, centre +/- thr * sigma.
+    Rows without enough history (``valid`` bit 0) flag nothing."""
+    H = fc.shape[1]
     idx = (horizon.clamp(1, H) - 1).to(fc.device)
     center = torch.gather(fc, 1, idx).contiguous()
     up, lo, flags, cnt, sc = SM.band_decide(cur, center, sigma.contiguous(), M, tables.thr, tables.bound,
                                             tables.minlb, diff, tables.pair_factor)
-    valid = _valid(hist, T, cur, tables.min_hist)
-    has = (valid & 1).bool()
+    has = (valid & 1).bool().to(cnt.device)
     cnt = torch.where(has, cnt, torch.zeros_like(cnt))
+    flags = torch.where(has[:, None], flags, torch.zeros_like(flags))
     return RowDecision(up, lo, flags, cnt, sc, valid, center)
 
 

@@ -58,6 +58,7 @@ _SIGS: dict[str, list] = {
                      c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_downstream_impact": [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p],
     "fm_segment_max": [c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p],
+    "fm_gather_cols": [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p],
     "fm_selftest_lanes": [c_void_p, c_void_p, c_void_p],
     "fm_decide_services": [c_void_p, c_void_p, c_i64, c_int, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_float,
                            c_void_p, c_int, c_int, c_float, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,

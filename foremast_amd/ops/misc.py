@@ -295,3 +295,34 @@ def ref_rolling_stats(x: np.ndarray, w: int, min_count: int = 1) -> tuple[np.nda
         var = np.maximum(q / n - m * m, 0.0)
     ok = (n >= min_count) & (n > 0)
     return (np.where(ok, c + m, np.nan).astype(np.float32), np.where(ok, np.sqrt(var), np.nan).astype(np.float32))
+
+
+# ---------------------------------------------------------------------------
+# resident-history row gather (csrc/kernels/gather.hip)
+def gather_cols(src: torch.Tensor, rm: torch.Tensor | None, off: torch.Tensor, lim: torch.Tensor, ncols: int,
+                out: torch.Tensor) -> torch.Tensor:
+    """``out[r, j] = src[rm[r], off[r] + j]`` when ``0 <= off[r] + j <
+    lim[r]``, NaN otherwise, for ``j < ncols`` (``out`` may be a column view
+    of a wider buffer).  ``rm``/``off``/``lim`` are int32 [R]."""
+    R = off.numel()
+    check(src.dim() == 2 and src.stride(1) == 1 and out.stride(1) == 1, "row-major float32 operands")
+    check(out.shape[0] >= R and out.shape[1] >= ncols, "output too small")
+    if R == 0 or ncols <= 0:
+        return out
+    if not src.is_cuda:
+        return ref_gather_cols(src, rm, off, lim, ncols, out)
+    require_native(src)
+    check(int(lim.max().item()) <= src.shape[1] if R else True, "limit past the source rows")
+    check(rm is None or (int(rm.max().item()) < src.shape[0] and int(rm.min().item()) >= 0), "row map out of range")
+    LIB.call("fm_gather_cols", ptr(src), src.stride(0), ptr(rm), ptr(off), ptr(lim), R, int(ncols), ptr(out),
+             out.stride(0), stream_of(src))
+    return out
+
+
+def ref_gather_cols(src, rm, off, lim, ncols, out):
+    rows = src if rm is None else src.index_select(0, rm.long())
+    c = off.long()[:, None] + torch.arange(ncols)[None, :]
+    ok = (c >= 0) & (c < lim.long()[:, None])
+    vals = torch.gather(rows, 1, c.clamp(0, max(0, src.shape[1] - 1)))
+    out[:len(off), :ncols] = torch.where(ok, vals, torch.full_like(vals, float("nan")))
+    return out

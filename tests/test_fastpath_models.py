@@ -1,0 +1,204 @@
+"""Every ML_ALGORITHM on the brain's resident fast path:
+exponential smoothing / Holt / Holt-Winters (with the fitted-model cache),
+Prophet, LSTM, bivariate normal, windowed moving average and a per-metric
+mix.  Fast path == general model-zoo path, cycle by cycle: statuses,
+reasons, anomaly maps, HPA logs and exporter gauges.  Job sets are
+homogeneous in history length (the general path pads a whole batch to its
+longest history, which position-dependent models see)."""
+import dataclasses
+import html
+import json
+
+import numpy as np
+import pytest
+
+from foremast_amd.api import crd
+from foremast_amd.api import status as ST
+from foremast_amd.config import BrainConfig
+from foremast_amd.controller.analyst import AnalystClient
+from foremast_amd.engine.brain import Brain
+from foremast_amd.engine.exporter import BrainExporter
+from foremast_amd.engine.sources import SourceRouter
+from foremast_amd.service.app import create_app
+from foremast_amd.service.store import MemoryStore
+
+T0 = 1_760_000_000.0
+
+
+class Clock:
+    def __init__(self, t=T0):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+def _metrics(n=3):
+    ms = [crd.Monitoring("http_server_requests_errors_5xx", "counter", "error5xx"),
+          crd.Monitoring("http_server_requests_latency", "gauge", "latency"),
+          crd.Monitoring("cpu_usage_seconds_total", "gauge", "cpu"),
+          crd.Monitoring("memory_usage_bytes", "gauge", "memory")]
+    return crd.Metrics("prometheus", "http://prom/api/v1/", ms[:n])
+
+
+def _pods(app, n, tag):
+    return [f"{app}-{tag}{'a' * 9}-p{k:04d}" for k in range(n)]
+
+
+def _cfg(algo):
+    cfg = BrainConfig()
+    cfg.lstm_hidden = 32
+    cfg.lstm_window = 60
+    if algo == "mixed":
+        cfg.ml_algorithm = "holt_winters"
+        cfg.metric_rules["latency"] = dataclasses.replace(cfg.rule_for("latency"), algorithm="lstm")
+        cfg.metric_rules["cpu"] = dataclasses.replace(cfg.rule_for("cpu"), algorithm="moving_average_all")
+    else:
+        cfg.ml_algorithm = algo
+    return cfg
+
+
+def _brain(resident, algo, faults, device="cpu"):
+    clock = Clock()
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    exp = BrainExporter()
+    brain = Brain(store, _cfg(algo), device=device,
+                  sources=SourceRouter.synthetic_only(faults=faults, fault_after=T0 + 120),
+                  clock=clock, exporter=exp, worker_id="w0", resident_history=resident)
+    return clock, store, client, brain, exp
+
+
+def _submit(client, kind):
+    ids = []
+    if kind == "static":
+        for j in range(4):
+            app = f"canary{j}"
+            ids.append(client.start_analyzing("default", app, [_pods(app, 2, "7687b9f4d"), _pods(app, 2, "5db89899b")],
+                                              _metrics(4), 10, "canary"))
+        for j in range(2):
+            ids.append(client.start_analyzing("default", f"roll{j}", [_pods(f"roll{j}", 2, "7687b9f4d")],
+                                              _metrics(4), 10, "rollingUpdate"))
+    elif kind == "continuous":
+        for j in range(4):
+            ids.append(client.start_analyzing("prod", f"cont{j}", None, _metrics(4), 10, "continuous"))
+    else:
+        for j in range(3):
+            ids.append(client.start_analyzing("prod", f"hpa{j}", None, _metrics(4), 10, "hpa",
+                                              ["cpu", "latency", "error5xx", "memory"]))
+    return ids
+
+
+FAULTS = {"canary1-7687b9f4daaaaaaaaa-p0000": 5.0, "roll1-7687b9f4daaaaaaaaa-p0001": 0.1, "cont1": 4.0,
+          "hpa2": 3.0}
+
+
+def _reason(r):
+    try:
+        return json.loads(html.unescape(r))
+    except ValueError:
+        return r
+
+
+def _compare(a, b, ids, cyc):
+    for jid in ids:
+        da, db = a[1].get(jid), b[1].get(jid)
+        assert da.status == db.status, (cyc, jid, da.status, db.status, da.reason, db.reason)
+        ra, rb = _reason(da.reason), _reason(db.reason)
+        if isinstance(ra, list):
+            assert len(ra) == len(rb), (cyc, jid)
+            for x, y in zip(ra, rb):
+                assert x["name"] == y["name"] and x["ts"] == y["ts"] and x["values"] == y["values"], (cyc, jid)
+                for k in ("upper", "lower"):
+                    assert x[k] == pytest.approx(y[k], rel=1e-5, abs=1e-6), (cyc, jid, k)
+        else:
+            assert ra == rb, (cyc, jid)
+        assert (json.loads(da.anomaly_info) if da.anomaly_info else {}) == \
+               (json.loads(db.anomaly_info) if db.anomaly_info else {}), (cyc, jid)
+        la = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current) for d in l.log.details])
+              for l in a[1].hpalogs(jid)]
+        lb = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current) for d in l.log.details])
+              for l in b[1].hpalogs(jid)]
+        assert la == lb, (cyc, jid)
+        ua = [(d.upper, d.lower) for l in a[1].hpalogs(jid) for d in l.log.details]
+        ub = [(d.upper, d.lower) for l in b[1].hpalogs(jid) for d in l.log.details]
+        np.testing.assert_allclose(np.array(ua, float).reshape(-1, 2), np.array(ub, float).reshape(-1, 2),
+                                   rtol=1e-5, atol=1e-6)
+    ta, tb = a[4].table, b[4].table
+    assert set(ta.index) == set(tb.index)
+    for k in ta.index:
+        va, vb = ta.get(k), tb.get(k)
+        assert (np.isnan(va) and np.isnan(vb)) or va == pytest.approx(vb, rel=1e-5, abs=1e-6), (cyc, k, va, vb)
+
+
+@pytest.mark.parametrize("algo,kind", [
+    ("holt_winters", "static"), ("holt_winters", "continuous"), ("exponential_smoothing", "continuous"),
+    ("double_exponential_smoothing", "hpa"), ("prophet", "static"), ("lstm", "continuous"), ("lstm", "hpa"),
+    ("bivariate_normal", "static"), ("moving_average", "continuous"), ("mixed", "static"), ("mixed", "hpa")])
+def test_models_fast_path_equals_general_path(algo, kind, device="cpu"):
+    a = _brain(True, algo, FAULTS, device)
+    b = _brain(False, algo, FAULTS, device)
+    ids = _submit(a[2], kind)
+    assert ids == _submit(b[2], kind)
+    for cyc in range(4):
+        ra, rb = a[3].run_once(), b[3].run_once()
+        assert ra["claimed"] == rb["claimed"]
+        if cyc == 0:
+            assert ra["fast_jobs"] == len(ids)               # every job took the fast path
+        _compare(a, b, ids, cyc)
+        a[0].t += 60
+        b[0].t += 60
+
+
+def test_cached_holt_winters_steady_state_reads_only_new_columns(monkeypatch):
+    """Continuous Holt-Winters: after the first cycle the fits come from the
+    model cache and each cycle gathers only the new columns of each row."""
+    from foremast_amd.ops import misc as MI
+    a = _brain(True, "holt_winters", {})
+    ids = _submit(a[2], "continuous")
+    a[3].run_once()
+    widths = []
+    real = MI.gather_cols
+
+    def spy(src, rm, off, lim, ncols, out):
+        widths.append(int(ncols))
+        return real(src, rm, off, lim, ncols, out)
+    monkeypatch.setattr(MI, "gather_cols", spy)
+    h0 = a[3].model_cache.hits
+    for _ in range(3):
+        a[0].t += 60
+        a[3].run_once()
+    assert a[3].model_cache.hits > h0
+    assert widths and max(widths) <= 2, widths      # one new sample per row per 60 s cycle
+    assert all(a[1].get(j).status in (ST.PREPROCESS_INPROGRESS, ST.PREPROCESS_COMPLETED, ST.COMPLETED_UNHEALTH)
+               for j in ids)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo,kind", [("holt_winters", "static"), ("holt_winters", "continuous"), ("lstm", "hpa"),
+                                       ("prophet", "static"), ("bivariate_normal", "static"), ("mixed", "hpa")])
+def test_gpu_models_fast_path_equals_general_path(algo, kind):
+    """The same parity on the MI355X kernels (fm_gather_cols feeding the ES /
+    LSTM / LSQ / bivariate kernels vs the general path's packed batch)."""
+    test_models_fast_path_equals_general_path(algo, kind, device="cuda")
+
+
+@pytest.mark.gpu
+def test_gpu_gather_cols_matches_reference():
+    import torch
+    from foremast_amd.ops import misc as MI
+    g = torch.Generator().manual_seed(3)
+    src = torch.randn(300, 1031, generator=g)
+    src[:, 1000:] = float("nan")
+    R = 257
+    rm = torch.randint(0, 300, (R,), generator=g, dtype=torch.int32)
+    off = torch.randint(-40, 900, (R,), generator=g, dtype=torch.int32)
+    lim = torch.randint(1, 1031, (R,), generator=g, dtype=torch.int32)
+    for ncols in (1, 7, 64, 300, 1031):
+        ref = MI.ref_gather_cols(src, rm, off, lim, ncols, torch.empty(R, ncols))
+        d = src.cuda()
+        out = torch.full((R, ncols + 5), 7.0, device="cuda")
+        MI.gather_cols(d, rm.cuda(), off.cuda(), lim.cuda(), ncols, out[:, 3:])
+        got = out[:, 3:3 + ncols].cpu()
+        torch.testing.assert_close(got, ref, equal_nan=True, rtol=0, atol=0)
+        assert (out[:, :3] == 7).all() and (out[:, 3 + ncols:] == 7).all()
