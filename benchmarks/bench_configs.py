@@ -213,12 +213,32 @@ def config3(args):
 
 
 # --------------------------------------------------------------------------- config 3e2e
+E2E = {
+    # config: (strategy, ML_ALGORITHM, default metrics, poll seconds, metric aliases)
+    "3e2e": ("canary", "moving_average_all", 8, None,
+             ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]),
+    "2e2e": ("continuous", "holt_winters", 4, 60.0, ["error5xx", "traffic", "latency", "error4xx"]),
+    "4e2e": ("hpa", "lstm", 8, 60.0,
+             ["cpu", "memory", "latency", "traffic", "error5xx", "error4xx", "tomcat_threads", "jvm_heap"]),
+}
+
+
 def config3e2e(args):
-    """The production brain (``Brain.run_once``) on the config-3 fleet: 10k
-    canary jobs x 8 metrics (5 + 5 pods x 10 points, 7-day history), one
-    cycle = claim -> fetch current/baseline -> stage -> resident tick
-    (pairwise + moving_average_all + decision, GPU) -> compaction -> verdicts
-    -> exporter gauges -> store update.
+    """The production brain (``Brain.run_once``) on a BASELINE fleet.
+
+    * ``3e2e`` -- config 3: 10k canary jobs x 8 metrics (5 + 5 pods x 10
+      points, 7-day history), moving_average_all + pairwise ALL; one cycle =
+      claim -> fetch current/baseline -> stage -> resident tick (GPU) ->
+      compaction -> verdicts -> exporter gauges -> store update.
+    * ``2e2e`` -- config 2 in the product: 10k continuous jobs x 4 metrics
+      (error%, TPS, p99, 4xx) judged by Holt-Winters; every cycle is one
+      60-s poll: each row's ONE new sample is fetched column-wise and
+      appended to the device-resident grid, the cached fits advance over it
+      (the grid fit ran once, in the untimed first cycle), band decision.
+    * ``4e2e`` -- config 4 in the product: 10k HPA jobs x 8 metrics judged by
+      the LSTM forecaster (bf16 MFMA), HPA score per job against the device
+      hysteresis table, hpalogs, and the forecast gauge a cluster autoscaler
+      reads (the same LSTM forward).
 
     ``--store sqlite`` (default) is the shipped topology
     (deploy/foremast/31-brain.yaml): the REST service runs in its own process
@@ -242,22 +262,30 @@ def config3e2e(args):
 
     info, dev = setup(gpus_required=args.device != "cpu")
     dev = torch.device("cpu") if args.device == "cpu" else dev
-    S, M, P = args.services, args.metrics, args.pods
+    kind = args.config
+    strategy, algo, m_default, poll_default, names = E2E[kind]
+    S, P = args.services, args.pods
+    M = args.metrics if args.metrics_set else m_default
+    poll = args.poll_seconds if poll_default is None or args.poll_set else poll_default
     t = {"now": 1_760_000_000.0}
     clock = lambda: t["now"]
-    names = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
     mons = [crd.Monitoring(f"http_server_requests_{a}", "gauge", a) for a in (names * 2)[:M]]
+    aliases = [m.metric_alias for m in mons]
     metrics = crd.Metrics("prometheus", "http://prom/api/v1/", mons)
     server = poller = None
     t_sub = 0.0
     ids: list[str] = []
+    # continuous / HPA jobs stay alive for the whole run (their end time is
+    # the submission window); canary jobs use the 10-minute watch window
+    n_cycles = args.steps + args.warmup + 3
+    window = args.window if strategy == "canary" else max(args.window, int(n_cycles * poll / 60) + 20)
 
     def submit(client):
         for j in range(S):
-            ids.append(client.start_analyzing("default", f"svc{j}",
-                                              [[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
-                                               [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]],
-                                              metrics, args.window, "canary"))
+            pods = ([[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
+                     [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]] if strategy == "canary" else None)
+            ids.append(client.start_analyzing("default", f"svc{j}", pods, metrics, window, strategy,
+                                              aliases if strategy == "hpa" else None))
 
     if args.store == "memory":
         store = MemoryStore()
@@ -283,18 +311,34 @@ def config3e2e(args):
             t_sub = time.perf_counter() - t_sub
         D.barrier()
         store = SQLiteStore(db)
-    print(f"[3e2e] rank {info.rank}: {S} jobs submitted in {t_sub:.1f}s ({args.store})", file=sys.stderr, flush=True)
-    faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, S, 50)}    # 2% of services regress
-    staged = StagedSource(SyntheticSource(faults=faults, fault_after=t["now"] - 3600))
+    print(f"[{kind}] rank {info.rank}: {S} jobs submitted in {t_sub:.1f}s ({args.store})", file=sys.stderr,
+          flush=True)
+    if strategy == "canary":
+        faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, S, 50)}    # 2% of services regress
+        staged = StagedSource(SyntheticSource(faults=faults, fault_after=t["now"] - 3600))
+    else:
+        # 2% of services regress mid-run; every series is staged column-wise
+        # over [history start, end of run] (the bench's stand-in for Prometheus)
+        faults = {f'app="svc{j}"': 3.0 for j in range(0, S, 50)}
+        t_hi = t["now"] + (n_cycles + 2) * poll
+        staged = StagedSource(SyntheticSource(faults=faults, fault_after=t["now"] + (args.warmup + 2) * poll),
+                              window=(t["now"] - args.history_days * 86400 - 3600, t_hi))
     cfg = BrainConfig()
+    cfg.ml_algorithm = algo
+    cfg.hpa_log_interval_s = args.hpa_log_interval
+    if kind == "4e2e":
+        cfg.hpa_forecast_algorithm = "lstm"
+        cfg.lstm_hidden = args.hidden
+        cfg.lstm_layers = args.layers
+        cfg.lstm_window = args.lookback
     exp = BrainExporter()
     brain = Brain(store, cfg, device=dev, sources=SourceRouter(synthetic=staged, force="synthetic"), clock=clock,
                   batch_size=S + 1, worker_id=f"bench-{info.rank}", exporter=exp, history_days=args.history_days)
-    t["now"] += args.poll_seconds
+    t["now"] += poll
     t_first = time.perf_counter()
-    first = brain.run_once()                    # fetch + stage history (untimed)
+    first = brain.run_once()                    # fetch + stage history (+ fit models), untimed
     t_first = time.perf_counter() - t_first
-    print(f"[3e2e] rank {info.rank}: first cycle (fetch + stage history) {t_first:.1f}s: "
+    print(f"[{kind}] rank {info.rank}: first cycle (fetch + stage history) {t_first:.1f}s: "
           f"claimed {first.get('claimed')}", file=sys.stderr, flush=True)
     rows, spans = [], {}
     if server is not None and args.rest_poll_rps > 0:
@@ -311,7 +355,7 @@ def config3e2e(args):
     def step():
         # cycles every poll interval inside the jobs' watch window (the
         # synthetic source serves the whole window: pre-staged series)
-        t["now"] += args.poll_seconds
+        t["now"] += poll
         r = brain.run_once()
         rows.append(r.get("rows", 0))
         for k, v in brain.spans.last.items():
@@ -331,7 +375,7 @@ def config3e2e(args):
                 scrapes.append((time.perf_counter() - t0, n))
                 stop_scrape.wait(args.scrape_interval)
         threading.Thread(target=scraper, daemon=True).start()
-    poll = None
+    poll_out = None
     try:
         ms, p50 = time_steps(step, args.steps, args.warmup, dev)
     finally:
@@ -341,7 +385,7 @@ def config3e2e(args):
             poller.terminate()
             try:
                 out, _ = poller.communicate(timeout=30)
-                poll = _json.loads(out.strip().splitlines()[-1]) if out.strip() else None
+                poll_out = _json.loads(out.strip().splitlines()[-1]) if out.strip() else None
             except Exception:  # noqa: BLE001 - the poller's report is informational
                 poller.kill()
         if server is not None:
@@ -355,23 +399,35 @@ def config3e2e(args):
     span_ms = {k: round(statistics.median(v[args.warmup:] or v), 3) for k, v in spans.items()}
     # per-rank claim / persist spans, max over ranks (the store is shared)
     worst = {k: round(D.all_reduce_max(span_ms.get(k, 0.0), cpu), 3) for k in ("claim", "persist")}
+    desc = {"3e2e": ("the 10k-service canary fleet", "moving_average_all + pairwise ALL (resident tick)",
+                     "synthetic Prometheus-shaped series (pre-staged in memory; 2% of services regress)"),
+            "2e2e": ("10k continuous Holt-Winters jobs", "Holt-Winters (cached fits advanced over each new "
+                     "sample, grid fit in the untimed first cycle) + band decision",
+                     "synthetic Prometheus-shaped series, staged column-wise; each cycle fetches every row's new "
+                     "sample (60-s poll); 2% of services regress mid-run"),
+            "4e2e": ("10k HPA jobs with the LSTM forecaster", f"LSTM H={args.hidden} x {args.layers} (bf16 MFMA) "
+                     "forecast -> band decision + HPA score + forecast gauge",
+                     "synthetic Prometheus-shaped series, staged column-wise; each cycle fetches every row's new "
+                     "sample (60-s poll), random-init LSTM weights; 2% of services regress mid-run")}[kind]
     _common(args, info, ms, p50, "metric windows scored/sec (node), production brain cycle (Brain.run_once) "
-            "on the 10k-service canary fleet", total_rows / (ms / 1e3), "windows/s",
-            "Brain.run_once: claim + fetch (pre-staged) + resident tick (moving_average_all + pairwise ALL) + "
-            "compaction + verdicts + exporter + store update", S * M, int(args.history_days * 1440) + 1,
-            "strong", "fp32" if dev.type != "cpu" else "fp32 data / fp64 statistics",
-            "synthetic Prometheus-shaped series (pre-staged in memory; 2% of services regress)",
-            {"services": S, "metrics": M, "pods_per_side": P, "store": args.store,
+            f"on {desc[0]}", total_rows / (ms / 1e3), "windows/s",
+            f"Brain.run_once: claim + fetch + {desc[1]} + compaction + verdicts + exporter + store update", S * M,
+            int(args.history_days * 1440) + 1, "strong",
+            ("bf16 recurrence / fp32 cell" if kind == "4e2e" else "fp32") if dev.type != "cpu"
+            else "fp32 data / fp64 statistics", desc[2],
+            {"services": S, "metrics": M, "strategy": strategy, "algorithm": algo, "poll_seconds": poll,
+             "hpa_log_interval_s": args.hpa_log_interval if strategy == "hpa" else None,
+             "pods_per_side": P if strategy == "canary" else 0, "store": args.store,
              "topology": ("REST service in its own process + every rank on one WAL SQLite file"
                           if args.store == "sqlite" else "single process, in-memory store"),
-             "rest_poller": poll, "rows_per_cycle_rank0": per_cycle,
+             "rest_poller": poll_out, "rows_per_cycle_rank0": per_cycle,
              "scraper": {"interval_s": args.scrape_interval, "scrapes": len(scrapes),
                          "render_ms_median": round(1e3 * statistics.median([x for x, _ in scrapes]), 2)
-                         if scrapes else None, "bytes": scrapes[-1][1] if scrapes else None}, "rows_per_cycle_max_rank": windows,
+                         if scrapes else None, "bytes": scrapes[-1][1] if scrapes else None},
+             "rows_per_cycle_max_rank": windows,
              "span_ms_median_rank0": span_ms, "span_ms_median_max_rank": worst,
-             # untimed: dominated by the host-side synthetic generator (counter-hash noise for 80k
-             # 7-day series in numpy, ~1 ms per series), not by the brain's fetch / stage path
-             "first_cycle_s (synthetic generation + fetch + stage history, untimed)": round(t_first, 3),
+             "model_cache": {"hits": brain.model_cache.hits, "misses": brain.model_cache.misses},
+             "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),
              "submit_s": round(t_sub, 3),
              "fast_jobs_first_cycle": first.get("fast_jobs"), "device": str(dev)})
 
@@ -452,7 +508,7 @@ def config5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True, choices=["1", "2", "3", "3e2e", "4", "5"])
+    ap.add_argument("--config", required=True, choices=["1", "2", "2e2e", "3", "3e2e", "4", "4e2e", "5"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -478,14 +534,20 @@ def main():
                     "(sqlite: the shipped topology, REST service in its own process)")
     ap.add_argument("--rest-poll-rps", type=float, default=None, help="config 3e2e + sqlite: barrelman-shaped "
                     "GET /v1/healthcheck/id load during the timed cycles (default: services / 10 s)")
+    ap.add_argument("--hpa-log-interval", type=float, default=0.0, help="e2e configs: HPA_LOG_INTERVAL_SECONDS "
+                    "(0: an hpalogs entry per job per cycle)")
     ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "
                     "body every N seconds in a thread while the cycles are timed (0: off)")
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "
                     "the fitted-model cache")
+    argv = sys.argv[1:]
     args = ap.parse_args()
+    args.metrics_set = any(a == "--metrics" or a.startswith("--metrics=") for a in argv)
+    args.poll_set = any(a == "--poll-seconds" or a.startswith("--poll-seconds=") for a in argv)
     if args.rest_poll_rps is None:
         args.rest_poll_rps = args.services / 10.0
-    {"1": config1, "2": config2, "3": config3, "3e2e": config3e2e, "4": config4, "5": config5}[args.config](args)
+    {"1": config1, "2": config2, "2e2e": config3e2e, "3": config3, "3e2e": config3e2e, "4": config4,
+     "4e2e": config3e2e, "5": config5}[args.config](args)
 
 
 if __name__ == "__main__":

@@ -77,6 +77,11 @@ class BrainConfig:
     # load forecast published for HPA jobs (cluster-autoscaler prediction)
     hpa_forecast_algorithm: str = "double_exponential_smoothing"   # HPA_FORECAST_ALGORITHM ("" disables)
     hpa_forecast_steps: int = 15                                    # HPA_FORECAST_STEPS (60 s samples)
+    # HPA_LOG_INTERVAL_SECONDS: 0 = an hpalogs entry per scoring (every cycle);
+    # > 0 = an entry when the score or its reason changes, else at most once
+    # per interval (the alert letter reads the last 4-6 entries around a
+    # replica change, HpaController.go:94-138: changes are what it needs)
+    hpa_log_interval_s: float = 0.0
     # LSTM model (ML_ALGORITHM=lstm, docs/guides/design.md:81-85)
     lstm_hidden: int = 128                 # LSTM_HIDDEN: 32 | 64 | 128 | 256
     lstm_layers: int = 1                   # LSTM_LAYERS: 1 | 2
@@ -150,6 +155,7 @@ class BrainConfig:
         c.hpa_breath_down = _f(env, "HPA_BREATH_DOWN_SECONDS", c.hpa_breath_down)
         c.hpa_forecast_algorithm = env.get("HPA_FORECAST_ALGORITHM", c.hpa_forecast_algorithm)
         c.hpa_forecast_steps = _i(env, "HPA_FORECAST_STEPS", c.hpa_forecast_steps)
+        c.hpa_log_interval_s = _f(env, "HPA_LOG_INTERVAL_SECONDS", c.hpa_log_interval_s)
         c.lstm_hidden = _i(env, "LSTM_HIDDEN", c.lstm_hidden)
         c.lstm_layers = _i(env, "LSTM_LAYERS", c.lstm_layers)
         c.lstm_multivariate = _i(env, "LSTM_MULTIVARIATE", c.lstm_multivariate)

@@ -710,9 +710,11 @@ class Brain:
                                  self.cfg.hpa_breath_down, self.cfg.hpa_max_flips, self.cfg.hpa_flip_window)
         self.hpa.scatter(sl_, state)
         score = int(sc[0])
-        details = [HPALogDetail(a, _f(cur[0, c]), _f(up[0, c]), _f(lo[0, c])) for c, a in enumerate(aliases)]
-        hpalogs.append(HPALog(job_id=doc.id, timestamp=float(now), created_at=rfc3339(
-            datetime.fromtimestamp(now, timezone.utc)), log=HPALogBody(score, MI.REASONS[int(rs[0])], details)))
+        if self.hpa.log_due(sl_.cpu().numpy(), np.asarray([score], np.int64), np.asarray([int(rs[0])], np.int64),
+                            now, self.cfg.hpa_log_interval_s)[0]:
+            details = [HPALogDetail(a, _f(cur[0, c]), _f(up[0, c]), _f(lo[0, c])) for c, a in enumerate(aliases)]
+            hpalogs.append(HPALog(job_id=doc.id, timestamp=float(now), created_at=rfc3339(
+                datetime.fromtimestamp(now, timezone.utc)), log=HPALogBody(score, MI.REASONS[int(rs[0])], details)))
         if self.exporter is not None:
             self.exporter.set_hpa_score(doc.namespace, doc.app_name, score)
         updates.append((doc.id, {"status": ST.PREPROCESS_COMPLETED}))

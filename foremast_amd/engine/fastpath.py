@@ -248,6 +248,26 @@ class HpaTable:
         self.slot: dict[str, int] = {}
         self.owner: dict[str, tuple[str, str]] = {}     # job id -> (namespace, app): checkpoint re-sharding
         self.state = MI.HpaState.zeros(0, self.device)
+        # last hpalogs entry per slot (HPA_LOG_INTERVAL_SECONDS policy)
+        self.log_score = np.zeros(0, np.int64)
+        self.log_reason = np.zeros(0, np.int64)
+        self.log_t = np.zeros(0)
+
+    def log_due(self, sl: np.ndarray, score: np.ndarray, reason: np.ndarray, now: float, interval: float) -> np.ndarray:
+        """Which of these slots write an hpalogs entry now; records them."""
+        n = int(sl.max()) + 1 if len(sl) else 0
+        if n > len(self.log_t):
+            grow = n - len(self.log_t)
+            self.log_score = np.concatenate([self.log_score, np.full(grow, -1, np.int64)])
+            self.log_reason = np.concatenate([self.log_reason, np.full(grow, -1, np.int64)])
+            self.log_t = np.concatenate([self.log_t, np.full(grow, -np.inf)])
+        if interval <= 0:
+            due = np.ones(len(sl), bool)
+        else:
+            due = (self.log_score[sl] != score) | (self.log_reason[sl] != reason) | (now - self.log_t[sl] >= interval)
+        d = sl[due]
+        self.log_score[d], self.log_reason[d], self.log_t[d] = score[due], reason[due], now
+        return due
 
     def slots(self, ids: list[str]) -> torch.Tensor:
         new = [i for i in ids if i not in self.slot]
@@ -303,6 +323,8 @@ class FastPath:
         self.cycle = 0
         self.max_idle_cycles = 64
         self._cmp = {}            # device compaction buffers per capacity
+        self._col: dict = {}      # column-wise fetched windows of sliding groups (consumed by _arrays)
+        self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
 
     # ------------------------------------------------------------------ planning
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
@@ -363,6 +385,7 @@ class FastPath:
         fetch this cycle; a batch identical to the previous cycle's (the
         steady state of a re-examined fleet) reuses the previous lists."""
         self.cycle += 1
+        self._col.clear()
         self.sliding.advance(now, now - self.history_s)
         immutable = self._immutable
         last = self._last
@@ -412,12 +435,115 @@ class FastPath:
         immutable source a static job whose windows and history are resident
         needs nothing and is not in it)."""
         todo = self.todo
+        # sliding-window jobs (continuous / HPA) of one plan group share their
+        # windows: fetched column-wise, a few batched queries per metric
+        # instead of one per job and metric
+        slide: dict[tuple, list[FastWork]] = {}
+        rest = []
+        for fw in todo:
+            (slide.setdefault(fw.plan.group, []) if fw.plan.sliding else rest).append(fw)
+        for grp in slide.values():
+            self._fetch_sliding(grp, now)
         if pool is None:
-            for fw in todo:
+            for fw in rest:
                 self.fetch(fw, now)
         else:
-            list(pool.map(lambda fw: self.fetch(fw, now), todo))
+            list(pool.map(lambda fw: self.fetch(fw, now), rest))
         return works
+
+    def _columns(self, store_types: list, tpls: list, lo: float, hi: float):
+        """-> (lens [n], t, v) in request order ('' templates: no samples)."""
+        n = len(tpls)
+        lens = np.zeros(n, np.int64)
+        have = [i for i, u in enumerate(tpls) if u]
+        if not have:
+            return lens, np.zeros(0), np.zeros(0, np.float32)
+        by_store: dict[str, list[int]] = {}
+        for i in have:
+            by_store.setdefault(store_types[i], []).append(i)
+        ts = []
+        for st_name, idx in by_store.items():
+            sub = tpls if len(idx) == n else [tpls[i] for i in idx]     # keep the caller's list object
+            cols = self.b.sources.fetch_columns(st_name, sub, lo, hi)
+            lens[idx] = np.diff(cols.off)
+            ts.append((idx, cols))
+        if len(ts) == 1 and len(ts[0][0]) == n:
+            return lens, ts[0][1].t, ts[0][1].v
+        # several stores / empty templates: reorder the flat answers by request
+        parts_t, parts_v = [None] * n, [None] * n
+        for idx, cols in ts:
+            for k, i in enumerate(idx):
+                parts_t[i] = cols.t[cols.off[k]:cols.off[k + 1]]
+                parts_v[i] = cols.v[cols.off[k]:cols.off[k + 1]]
+        cat = lambda xs, dt: np.concatenate([x for x in xs if x is not None]).astype(dt, copy=False) \
+            if any(x is not None for x in xs) else np.zeros(0, dt)
+        return lens, cat(parts_t, np.float64), cat(parts_v, np.float32)
+
+    def _fetch_sliding(self, ws: list[FastWork], now: float) -> None:
+        """Column-wise fetch of a sliding group: per metric, the current (and
+        baseline) windows of every job in one batched call, and only the
+        history samples newer than each row's newest (rows grouped by that
+        start); the history goes straight into the resident grid."""
+        b = self.b
+        p0 = ws[0].plan
+        M, S = len(p0.aliases), len(ws)
+        wins = b._windows(ws[0].doc, now)
+        st = self.sliding
+        ids = tuple(map(id, ws))
+        memo = self._tpl.get(p0.group)
+        if memo is None or memo[0] != ids:
+            # template lists and row map of this job list, reused while it is
+            # unchanged (stable list objects let a staged source memoise them)
+            lists = {(f, m): [getattr(fw.plan, f)[m] for fw in ws]
+                     for f in ("cur_urls", "cur_stores", "base_urls", "base_stores", "hist_urls", "hist_stores")
+                     for m in range(M)}
+            memo = self._tpl[p0.group] = (ids, lists, np.stack([fw.rows for fw in ws]).astype(np.int64))
+        _, lists, rows = memo                                                # rows [S, M]
+        cur_p, base_p = [], []
+        for m in range(M):
+            for cat, urls, stores, acc in (("current", "cur_urls", "cur_stores", cur_p),
+                                           ("baseline", "base_urls", "base_stores", base_p)):
+                acc.append(self._columns(lists[(stores, m)], lists[(urls, m)], *wins[cat]))
+        hlo, hhi = wins["historical"]
+        wr, wt, wv = [], [], []
+        for m in range(M):
+            tpls = lists[("hist_urls", m)]
+            stores = lists[("hist_stores", m)]
+            since = st.last_t[rows[:, m]]
+            lo = np.where(np.isfinite(since), np.maximum(hlo, since + b.step), hlo)
+            for lo_v in np.unique(lo):
+                if hhi < lo_v:
+                    continue
+                sel = np.flatnonzero(lo == lo_v)
+                if len(sel) == len(tpls):
+                    lens, t, v = self._columns(stores, tpls, float(lo_v), hhi)
+                else:
+                    lens, t, v = self._columns([stores[i] for i in sel], [tpls[i] for i in sel], float(lo_v), hhi)
+                if len(t):
+                    wr.append(np.repeat(rows[sel, m], lens))
+                    wt.append(t)
+                    wv.append(v)
+        if wr:
+            st.write_sliding_flat(np.concatenate(wr), np.concatenate(wt), np.concatenate(wv))
+
+        def pack(parts):
+            lens = np.stack([p[0] for p in parts], 1)                   # [S, M]
+            w = max(1, int(lens.max()) if lens.size else 1)
+            v = np.stack([pack_left(p[2], p[0], w) for p in parts], 1).reshape(S * M, w)
+            t = np.stack([pack_left(p[1], p[0], w, np.float64) for p in parts], 1).reshape(S * M, w)
+            return lens.reshape(-1), v, t, int(lens.max()) if lens.size else 0
+        cur_len, cur, cur_t, c = pack(cur_p)
+        base_len, base, _, bb = pack(base_p)
+        wclass = 0 if max(c, bb) <= 128 else (1 if max(c, bb) <= 256 else 2)
+        for fw in ws:
+            fw.has_window = True
+            fw.dirty = True
+            fw.settled = False
+            fw.wclass = wclass
+            fw.hist = []
+        ids = tuple(map(id, ws))
+        self._col[p0.group] = {"ids": ids, "pos": {i: j for j, i in enumerate(ids)}, "cur": cur, "cur_t": cur_t,
+                               "cur_len": cur_len, "base": base if bb else None, "base_len": base_len}
 
     def fetch(self, fw: FastWork, now: float) -> FastWork:
         b = self.b
@@ -555,14 +681,25 @@ class FastPath:
         S = len(works)
         dev = self.b.device
         store = self.sliding if p0.sliding else self.static
-        cur_len = np.concatenate([w.cur_len for w in works])
-        base_len = np.concatenate([w.base_len for w in works])
         R = S * M
-        n = max(1, int(cur_len.max()) if R else 1)
-        nb = int(base_len.max()) if R else 0
-        cur = pack_left(np.concatenate([w.cur for w in works]), cur_len, n)
-        cur_t = pack_left(np.concatenate([w.cur_t for w in works]), cur_len, n, np.float64)
-        base = pack_left(np.concatenate([w.base for w in works]), base_len, nb) if nb else None
+        col = self._col.get(p0.group)
+        pos = None
+        if col is not None:                               # column-wise fetched this cycle
+            pos = col["pos"]
+            j = [pos.get(i, -1) for i in ident]
+            pos = None if min(j, default=-1) < 0 else np.asarray(j, np.int64)
+        if pos is not None:
+            sel = None if col["ids"] == ident else (pos[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+            pick = (lambda a: a) if sel is None else (lambda a: None if a is None else a[sel])
+            cur_len, cur, cur_t, base = pick(col["cur_len"]), pick(col["cur"]), pick(col["cur_t"]), pick(col["base"])
+        else:
+            cur_len = np.concatenate([w.cur_len for w in works])
+            base_len = np.concatenate([w.base_len for w in works])
+            n = max(1, int(cur_len.max()) if R else 1)
+            nb = int(base_len.max()) if R else 0
+            cur = pack_left(np.concatenate([w.cur for w in works]), cur_len, n)
+            cur_t = pack_left(np.concatenate([w.cur_t for w in works]), cur_len, n, np.float64)
+            base = pack_left(np.concatenate([w.base for w in works]), base_len, nb) if nb else None
         rowmap = np.concatenate([w.rows for w in works]).astype(np.int32)
         up = lambda a: (torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"
                         else torch.from_numpy(a))
@@ -885,7 +1022,11 @@ class FastPath:
             exp.set_bounds_many(ga.export_slots if ga.export_start is None else ga.export_start,
                                 stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64), anom_ts)
         if works[0].plan.hpa:
-            self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome)
+            if bulk is None:
+                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, updates_bulk := [], ga)
+                updates.extend((i, f) for ids, f, _ in updates_bulk for i in ids)
+            else:
+                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga)
             return
         status = packed[:, 0]
         unh = status == 1
@@ -990,7 +1131,7 @@ class FastPath:
         return ST.COMPLETED_UNHEALTH, {"status": ST.COMPLETED_UNHEALTH, "reason": html.escape(json.dumps(reasons)),
                                        "anomaly_info": json.dumps(anomalies)}
 
-    def _finish_hpa(self, works, M, cur, stats, now, updates, hpalogs, outcome) -> None:
+    def _finish_hpa(self, works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga=None) -> None:
         S = len(works)
         fin = np.isfinite(cur)
         n = cur.shape[1]
@@ -1012,6 +1153,8 @@ class FastPath:
                                  cfg.hpa_max_flips, cfg.hpa_flip_window)
         self.hpa.scatter(sl, sub)
         sc, rs = sc.cpu().numpy(), rs.cpu().numpy()
+        due = self.hpa.log_due(sl.cpu().numpy(), sc.astype(np.int64), rs.astype(np.int64), now,
+                               cfg.hpa_log_interval_s)
         created = rfc3339(datetime.fromtimestamp(now, timezone.utc))
         exp = self.b.exporter
         if exp is not None:
@@ -1022,11 +1165,16 @@ class FastPath:
                 hs.append(w.plan.hpa_slots)
             exp.set_hpa_scores(np.stack(hs), sc.astype(np.float64))
         al = works[0].plan.aliases
-        for j, w in enumerate(works):
+        for j in np.flatnonzero(due):
+            w = works[j]
             det = [HPALogDetail(a, _f(cl[j, c]), _f(up[j, c]), _f(lo[j, c])) for c, a in enumerate(al)]
             hpalogs.append(HPALog(job_id=w.doc.id, timestamp=float(now), created_at=created,
                                   log=HPALogBody(int(sc[j]), MI.REASONS[int(rs[j])], det)))
-            updates.append((w.doc.id, {"status": ST.PREPROCESS_COMPLETED}))
+        # HPA jobs stay alive: one uniform "keep" for the whole group
+        if ga is not None and len(ga.ids) == S:
+            bulk.append((ga.ids, {"status": ST.PREPROCESS_COMPLETED}, ga.handles))
+        else:
+            updates.extend((w.doc.id, {"status": ST.PREPROCESS_COMPLETED}) for w in works)
         outcome["hpa_scored"] = outcome.get("hpa_scored", 0) + S
 
     def _release(self, works: list[FastWork]) -> None:

@@ -249,9 +249,14 @@ class ResidentHistory:
         lens = np.fromiter((len(t) for t in times), np.int64, len(times))
         if lens.sum() == 0:
             return
-        t = np.concatenate(times)
-        v = np.concatenate(values).astype(np.float32, copy=False)
-        r = np.repeat(np.asarray(rows, np.int64), lens)
+        self.write_sliding_flat(np.repeat(np.asarray(rows, np.int64), lens), np.concatenate(times),
+                                np.concatenate(values).astype(np.float32, copy=False))
+
+    def write_sliding_flat(self, r: np.ndarray, t: np.ndarray, v: np.ndarray) -> None:
+        """:meth:`write_sliding` for samples already flattened (row per sample)."""
+        assert self.sliding and self.t0 is not None
+        if len(r) == 0:
+            return
         c = self.col(t)
         ok = (c >= self.ws) & (c < self.e) & np.isfinite(v)
         r, c, v, t = r[ok], c[ok], v[ok], t[ok]

@@ -38,6 +38,76 @@ class SourceError(RuntimeError):
     pass
 
 
+@dataclass
+class Columns:
+    """Answers to many queries over ONE window, flattened: request i's
+    app-level samples are ``t[off[i]:off[i+1]]`` / ``v[...]`` (several series
+    of one request merged per timestamp), ``err[i]`` a message or None."""
+    off: np.ndarray
+    t: np.ndarray
+    v: np.ndarray
+    err: list
+
+    @classmethod
+    def from_series(cls, got: list) -> "Columns":
+        ts, vs, lens, err = [], [], [], []
+        for g in got:
+            if isinstance(g, BaseException):
+                err.append(f"{type(g).__name__}: {g}")
+                lens.append(0)
+                continue
+            err.append(None)
+            t, v = merge_series(g)
+            ts.append(t)
+            vs.append(v)
+            lens.append(len(t))
+        off = np.zeros(len(got) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        cat = lambda xs, dt: np.concatenate(xs).astype(dt, copy=False) if xs else np.zeros(0, dt)
+        return cls(off, cat(ts, np.float64), cat(vs, np.float32), err)
+
+
+def merge_series(ss: list["Series"]) -> tuple[np.ndarray, np.ndarray]:
+    """App-level samples of several series (per-timestamp mean of finite values)."""
+    if not ss:
+        return np.zeros(0), np.zeros(0, np.float32)
+    if len(ss) == 1:
+        return np.asarray(ss[0].times, np.float64), np.asarray(ss[0].values, np.float32)
+    t = np.unique(np.concatenate([s.times for s in ss]))
+    acc = np.zeros(len(t))
+    cnt = np.zeros(len(t))
+    for s in ss:
+        i = np.searchsorted(t, s.times)
+        ok = np.isfinite(s.values)
+        np.add.at(acc, i[ok], s.values[ok])
+        np.add.at(cnt, i[ok], 1)
+    return t, np.where(cnt > 0, acc / np.maximum(cnt, 1), np.nan).astype(np.float32)
+
+
+_SEL = None
+
+
+def parse_selector(q: str):
+    """``metric{l1="v1",l2="v2"}`` with only equality matchers ->
+    (metric, [(label, value)]), else None (not batchable)."""
+    import re
+    global _SEL
+    if _SEL is None:
+        _SEL = (re.compile(r'^\s*([A-Za-z_:][\w:]*)\s*\{(.*)\}\s*$'),
+                re.compile(r'\s*([A-Za-z_]\w*)\s*(=~|!=|!~|=)\s*"((?:[^"\\]|\\.)*)"\s*(?:,|$)'))
+    m = _SEL[0].match(q)
+    if not m:
+        return None
+    body, labels, pos = m.group(2), [], 0
+    while pos < len(body):
+        mm = _SEL[1].match(body, pos)
+        if not mm or mm.group(2) != "=":
+            return None
+        labels.append((mm.group(1), mm.group(3)))
+        pos = mm.end()
+    return m.group(1), labels
+
+
 def substitute_window(url: str, start: float, end: float) -> str:
     return url.replace(START_PLACEHOLDER, f"{int(start)}").replace(END_PLACEHOLDER, f"{int(end)}")
 
@@ -71,15 +141,74 @@ def parse_wavefront(body: bytes | str) -> list[Series]:
 
 
 class PrometheusSource:
-    def __init__(self, client=None, timeout: float = 90.0):
+    """``query_range`` over HTTP.  :meth:`fetch_columns` answers the same
+    query for many services in a few requests: app-level selectors that
+    differ only in their ``app`` value are merged into one
+    ``app=~"a|b|..."`` query (``batch`` apps per request) and the result is
+    split by the series' ``app`` label -- 10k continuous jobs x 4 metrics
+    cost 4 x 10k / ``batch`` requests per cycle, not 40k."""
+
+    def __init__(self, client=None, timeout: float = 90.0, batch: int = 256):
         import httpx
         self.http = client or httpx.Client(timeout=timeout)
+        self.batch = batch
+        self._tpl: dict[str, object] = {}
 
     def fetch(self, url: str) -> list[Series]:
         r = self.http.get(url)
         if r.status_code != 200:
             raise SourceError(f"GET {url} -> {r.status_code}")
         return parse_prometheus(r.content)
+
+    def _parse_template(self, tpl: str):
+        got = self._tpl.get(tpl)
+        if got is None:
+            got = False
+            if "query_range?" in tpl:
+                base, qs = tpl.split("?", 1)
+                params = urllib.parse.parse_qsl(qs, keep_blank_values=True)
+                q = dict(params).get("query", "")
+                sel = parse_selector(q)
+                if sel is not None and sum(1 for k, _ in sel[1] if k == "app") == 1:
+                    metric, labels = sel
+                    app = next(v for k, v in labels if k == "app")
+                    rest = tuple((k, v) for k, v in labels if k != "app")
+                    step = dict(params).get("step", "60")
+                    got = (base, metric, rest, step, app)
+            self._tpl[tpl] = got
+        return got
+
+    def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
+        out: list = [None] * len(templates)
+        groups: dict[tuple, list[int]] = {}
+        for i, tpl in enumerate(templates):
+            info = self._parse_template(tpl)
+            if not info:
+                try:
+                    out[i] = self.fetch(substitute_window(tpl, start, end))
+                except (SourceError, OSError, ValueError) as e:
+                    out[i] = e
+                continue
+            groups.setdefault(info[:4], []).append(i)
+        for (base, metric, rest, step), idx in groups.items():
+            for k in range(0, len(idx), self.batch):
+                chunk = idx[k:k + self.batch]
+                apps = sorted({self._tpl[templates[i]][4] for i in chunk})
+                esc = lambda v: v.replace("\\", "\\\\").replace('"', '\\"')
+                sel = ",".join([f'{a}="{esc(b)}"' for a, b in rest] +
+                               ['app=~"' + "|".join(_re_escape(a) for a in apps) + '"'])
+                url = base + "?" + urllib.parse.urlencode({"query": f"{metric}{{{sel}}}", "start": f"{int(start)}",
+                                                          "end": f"{int(end)}", "step": step})
+                try:
+                    by_app: dict[str, list[Series]] = {}
+                    for s_ in self.fetch(url):
+                        by_app.setdefault(s_.labels.get("app", ""), []).append(s_)
+                    for i in chunk:
+                        out[i] = by_app.get(self._tpl[templates[i]][4], [])
+                except (SourceError, OSError, ValueError) as e:
+                    for i in chunk:
+                        out[i] = e
+        return Columns.from_series(out)
 
 
 class WavefrontSource:
@@ -146,6 +275,59 @@ class SyntheticSource:
                 v = np.where(t >= self.fault_after, v * mag, v)
         return Series({"__name__": key.split("|")[0]}, t, np.maximum(v, 0).astype(np.float32))
 
+    def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
+        """Vectorised answer for many app-level queries over one window
+        (the same samples :meth:`fetch` returns for each)."""
+        t = np.arange(np.ceil(start / self.step) * self.step, end + 1e-9, self.step)
+        info = getattr(self, "_cinfo", None)
+        if info is None:
+            info = self._cinfo = {}
+        rows, slow = [], []
+        for i, tpl in enumerate(templates):
+            g = info.get(tpl)
+            if g is None:
+                qs = dict(urllib.parse.parse_qsl(tpl.split("?", 1)[1])) if "query_range?" in tpl else None
+                q = qs.get("query", "") if qs else ""
+                if qs is None or _pod_selector(q):
+                    g = False
+                else:
+                    metric = q.split("{")[0].replace("namespace_pod_", "").replace("namespace_app_pod_", "")
+                    key = metric + "|" + _app_of(q)
+                    level, ad, aw, ph = self._params(key)
+                    mag = 1.0
+                    for sub, m in self.faults.items():
+                        if sub in q:
+                            mag *= m
+                    g = (np.uint32(zlib.crc32(key.encode()) ^ self.seed), level, ad, aw, ph, mag)
+                info[tpl] = g
+            (rows if g else slow).append(i)
+        K, nt = len(rows), len(t)
+        out_t = np.tile(t, (K, 1))
+        vals = np.zeros((K, nt), np.float32)
+        if K and nt:
+            from ..ops.reference import hash3, u01
+            p = [info[templates[i]] for i in rows]
+            kh = np.array([g[0] for g in p], np.uint32)[:, None]
+            level, ad, aw, ph, mag = (np.array([g[j] for g in p])[:, None] for j in range(1, 6))
+            season = 1 + ad * np.sin(2 * np.pi * t[None, :] / 86400.0 + ph) + \
+                aw * np.sin(2 * np.pi * t[None, :] / 604800.0 + ph)
+            ti = ((t / self.step).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)[None, :]
+            h1 = hash3(np.broadcast_to(kh, (K, nt)), np.broadcast_to(ti, (K, nt)), np.uint32(0))
+            h2 = hash3(h1, np.uint32(0x68E31DA4), np.uint32(0))
+            noise = np.sqrt(-2.0 * np.log(u01(h1).astype(np.float64))) * np.cos(2 * np.pi * u01(h2))
+            v = level * season * (1 + self.noise * noise)
+            v = np.where(t[None, :] >= self.fault_after, v * mag, v)
+            vals = np.maximum(v, 0).astype(np.float32)
+        got: list = [None] * len(templates)
+        for k, i in enumerate(rows):
+            got[i] = [Series({}, out_t[k], vals[k])]
+        for i in slow:
+            try:
+                got[i] = self.fetch(substitute_window(templates[i], start, end))
+            except (SourceError, OSError, ValueError) as e:
+                got[i] = e
+        return Columns.from_series(got)
+
     def fetch(self, url: str) -> list[Series]:
         if "query_range?" in url:
             qs = dict(urllib.parse.parse_qsl(url.split("?", 1)[1]))
@@ -177,11 +359,69 @@ class StagedSource:
     local = True
     immutable = True        # a query's answer never changes (absolute-time windows need no re-fetch)
 
-    def __init__(self, inner, cache_history: bool = False):
+    def __init__(self, inner, cache_history: bool = False, window: tuple[float, float] | None = None,
+                 step: float = 60.0):
         self.inner = inner
         self.cache: dict[str, list[Series]] = {}
         self.cache_history = cache_history
         self.misses = 0
+        # column-wise staging (sliding-window jobs): every template's samples
+        # over ``window`` on one time grid, one row per template
+        self.window = window
+        self.step = step
+        self._row: dict[str, int] = {}
+        self._mat = np.zeros((0, 0), np.float32)
+        self._n = 0
+        self._lists: dict[int, tuple] = {}
+
+    def fetch_columns(self, templates: list[str], start: float, end: float) -> "Columns":
+        """Windows of many templates from the staged grid (vectorised
+        slicing; a template is generated once, by ``inner.fetch_columns``
+        over the whole staging window)."""
+        inner = getattr(self.inner, "fetch_columns", None)
+        if self.window is None or inner is None or not (self.window[0] <= start and end <= self.window[1]):
+            got = []
+            for tpl in templates:
+                try:
+                    got.append(self.fetch(substitute_window(tpl, start, end)))
+                except (SourceError, OSError, ValueError) as e:
+                    got.append(e)
+            return Columns.from_series(got)
+        g0 = np.ceil(self.window[0] / self.step) * self.step
+        G = int(np.floor((self.window[1] - g0) / self.step)) + 1
+        ent = self._lists.get(id(templates))
+        if ent is None or ent[0] is not templates:
+            new = list(dict.fromkeys(t for t in templates if t not in self._row))
+            if new:
+                self.misses += len(new)
+                cols = inner(new, g0, g0 + (G - 1) * self.step)
+                n0 = self._n
+                if n0 + len(new) > self._mat.shape[0] or self._mat.shape[1] != G:
+                    cap = max(n0 + len(new), 2 * self._mat.shape[0])
+                    m = np.full((cap, G), np.nan, np.float32)
+                    if n0:
+                        m[:n0] = self._mat[:n0]
+                    self._mat = m
+                for k, t in enumerate(new):
+                    a, b = cols.off[k], cols.off[k + 1]
+                    c = np.rint((cols.t[a:b] - g0) / self.step).astype(np.int64)
+                    ok = (c >= 0) & (c < G)
+                    self._mat[n0 + k, c[ok]] = cols.v[a:b][ok]
+                    self._row[t] = n0 + k
+                self._n = n0 + len(new)
+            ent = (templates, np.fromiter((self._row[t] for t in templates), np.int64, len(templates)))
+            self._lists[id(templates)] = ent
+        rows = ent[1]
+        c0 = max(0, int(np.ceil((start - g0) / self.step - 1e-9)))
+        c1 = min(G, int(np.floor((end - g0) / self.step + 1e-9)) + 1)
+        nc = max(0, c1 - c0)
+        v = self._mat[rows, c0:c0 + nc]
+        keep = np.isfinite(v)
+        t = np.broadcast_to(g0 + self.step * np.arange(c0, c0 + nc), v.shape)
+        lens = keep.sum(1)
+        off = np.zeros(len(rows) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        return Columns(off, t[keep], v[keep], [None] * len(rows))
 
     def fetch(self, url: str) -> list[Series]:
         got = self.cache.get(url)
@@ -214,6 +454,12 @@ class StaticSource:
         if self.fallback is None:
             raise SourceError(f"no static answer for {url}")
         return self.fallback.fetch(url)
+
+
+def _re_escape(v: str) -> str:
+    """A literal inside a PromQL (RE2) regex alternative."""
+    import re
+    return re.sub(r"([\\.^$|?*+()\[\]{}])", r"\\\1", v)
 
 
 def dict_set(s: Series, k: str, v: str) -> Series:
@@ -260,6 +506,33 @@ class SourceRouter:
     def immutable(self) -> bool:
         srcs = [self.sources.get(self.force)] if self.force else [v for v in self.sources.values() if v is not None]
         return bool(srcs) and all(getattr(s, "immutable", False) for s in srcs)
+
+    def fetch_columns(self, store_type: str, templates: list[str], start: float, end: float) -> Columns:
+        """Many queries over one window (``START_TIME``/``END_TIME`` templates)
+        in a source's batched form when it has one."""
+        src = self._source(store_type)
+        fc = getattr(src, "fetch_columns", None)
+        if fc is not None:
+            return fc(templates, start, end)
+        got = []
+        for tpl in templates:
+            try:
+                got.append(src.fetch(substitute_window(tpl, start, end)))
+            except (SourceError, OSError, ValueError) as e:
+                got.append(e)
+        return Columns.from_series(got)
+
+    def _source(self, store_type: str):
+        kind = self.force or store_type or "prometheus"
+        src = self.sources.get(kind)
+        if src is None:
+            if kind == "prometheus":
+                src = self.sources["prometheus"] = PrometheusSource()
+            elif kind == "wavefront":
+                src = self.sources["wavefront"] = WavefrontSource()
+            else:
+                raise SourceError(f"no source for metric store {kind!r}")
+        return src
 
     def fetch(self, store_type: str, url: str) -> list[Series]:
         kind = self.force or store_type or "prometheus"

@@ -483,3 +483,66 @@ def test_checkpoint_prefers_newer_world_over_stale_own_file(tmp_path):
     b.info = D.DistInfo(0, 2, 0)
     assert b.load_checkpoint(str(tmp_path))
     assert {int(st.flips[0]) for st in b.hpa_state.values()} == {3}
+
+
+def test_prometheus_fetch_columns_batches_apps_into_few_queries():
+    """Continuous / HPA jobs of one group share their window: the fast path
+    asks the source column-wise, and PrometheusSource merges app-level
+    selectors into ``app=~"a|b|..."`` queries (batch apps per request), then
+    splits the matrix by the ``app`` label."""
+    import httpx
+    import urllib.parse
+    from foremast_amd.engine.sources import PrometheusSource, substitute_window
+    seen = []
+
+    def handler(req):
+        q = dict(urllib.parse.parse_qsl(req.url.query.decode()))
+        seen.append(q["query"])
+        import re
+        m = re.search(r'app=~"([^"]*)"', q["query"])
+        m1 = re.search(r'app="([^"]*)"', q["query"])
+        apps = m.group(1).split("|") if m else [m1.group(1) if m1 else "none"]
+        apps = [a.replace("\\", "") for a in apps]
+        t0, t1 = int(q["start"]), int(q["end"])
+        res = [{"metric": {"app": a, "namespace": "ns"},
+                "values": [[t, str(float(len(a) + k))] for k, t in enumerate(range(t0, t1 + 1, 60))]} for a in apps]
+        return httpx.Response(200, json={"status": "success", "data": {"resultType": "matrix", "result": res}})
+    src = PrometheusSource(client=httpx.Client(transport=httpx.MockTransport(handler)), batch=256)
+    tpl = lambda a: ("http://prom/api/v1/query_range?" + urllib.parse.urlencode(
+        {"query": f'namespace_app_pod_cpu{{namespace="ns",app="{a}"}}', "start": "START_TIME", "end": "END_TIME",
+         "step": "60"}))
+    apps = [f"svc.{i}" for i in range(600)]
+    cols = src.fetch_columns([tpl(a) for a in apps] + ["http://prom/api/v1/query_range?query=up&start=START_TIME"
+                                                       "&end=END_TIME&step=60"], T0, T0 + 240)
+    assert len(seen) == 3 + 1                      # 600 apps in 3 merged queries + the non-batchable one
+    merged = [q for q in seen if "app=~" in q]
+    assert len(merged) == 3 and r"svc\.1" in merged[0]
+    for i, a in enumerate(apps[:5] + apps[-5:]):
+        k = apps.index(a)
+        np.testing.assert_array_equal(cols.v[cols.off[k]:cols.off[k + 1]], len(a) + np.arange(5, dtype=np.float32))
+        np.testing.assert_array_equal(cols.t[cols.off[k]:cols.off[k + 1]], T0 + 60.0 * np.arange(5))
+    one = src.fetch(substitute_window(tpl(apps[7]), T0, T0 + 240))[0]
+    np.testing.assert_array_equal(one.values, cols.v[cols.off[7]:cols.off[8]])
+
+
+def test_hpa_log_interval_writes_changes_and_keepalives():
+    """HPA_LOG_INTERVAL_SECONDS > 0: an hpalogs entry when the score or its
+    reason changes, else at most once per interval (0: every scoring)."""
+    clock, store, client, brain, exp = _setup()
+    brain.cfg.hpa_log_interval_s = 300.0
+    jid = client.start_analyzing("default", "demo", None, _metrics(), 10, "hpa", ["cpu"])
+    brain.run_once()
+    assert len(store.hpalogs(jid, 100)) == 1
+    slot = brain.hpa.slot[jid]
+    for _ in range(3):                               # same score, inside the interval: no entry
+        clock.t += 60
+        brain.run_once()
+    n = len(store.hpalogs(jid, 100))
+    assert n == 1 or brain.hpa.log_score[slot] != store.hpalogs(jid, 1)[0].log.hpa_score
+    clock.t += 300                                   # keep-alive after the interval
+    brain.run_once()
+    assert len(store.hpalogs(jid, 100)) == n + 1
+    brain.cfg.hpa_log_interval_s = 0.0               # reference behaviour: every scoring
+    clock.t += 60
+    brain.run_once()
+    assert len(store.hpalogs(jid, 100)) == n + 2
