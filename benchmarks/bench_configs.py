@@ -168,7 +168,7 @@ def config2(args):
 
     def step():
         h, c = (hist, None) if not args.cached else window()
-        d = zoo.decide("holt_winters", h, T_HIST, cur, hor, M, tables, period=period, cache=c)
+        d = zoo.decide("holt_winters", h, T_HIST, cur, hor, M, tables, period=period, cache=c, H=args.window)
         C.service_reduce(d.count, d.score, d.valid, M)
 
     ms, p50 = time_steps(step, args.steps, args.warmup, dev)

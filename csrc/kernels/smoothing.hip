@@ -320,7 +320,8 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
                                                     const float* __restrict__ cand, int G, int m,
                                                     ST* __restrict__ season /*[m][R*G]*/, float* __restrict__ sse,
                                                     float* __restrict__ state /*[R*G,3]*/, int* __restrict__ nobs,
-                                                    int t_store_end, float* __restrict__ sscale /*[R]*/) {
+                                                    int t_store_end, float* __restrict__ sscale /*[R]*/,
+                                                    int* __restrict__ nfin /*[R] or null*/) {
   const int64_t P = R * G;
   const int64_t pid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if ((pid_raw & ~(int64_t)63) >= P) return;      // whole wave past the end
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
   const float* xr = x + row * ld;
   const int base = first_finite(xr, T);
   int t0;
+  int nf0 = 0;                // finite samples consumed by the initialisation
   SeasonInit<KIND> sinit{0.f, 0.f, false};
   SeasonIO<ST> io{1.f, 1.f};
   if (base >= T) {
@@ -356,10 +358,12 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
     const bool mul_ok = fabsf(s1) > kDivEps;
     sinit = SeasonInit<KIND>{s1, mul_ok ? 1.f / s1 : 0.f, mul_ok};
     t0 = base + m;
+    nf0 = c1;
   } else {
     md.lvl = xr[base];
     if (KIND == 1 && base + 1 < T && isfinite(xr[base + 1])) md.tr = xr[base + 1] - xr[base];
     t0 = base + 1;
+    nf0 = 1;
   }
   double err2 = 0.0;
   int n = 0;
@@ -406,6 +410,9 @@ __global__ __launch_bounds__(256) void es_fit_kernel(const float* __restrict__ x
   // addresses) and then store no results of their own
   if (!live) return;
   if (g == 0) sscale[row] = io.sc;
+  // the row's finite history samples (the MIN_HISTORICAL_DATA_POINT gate),
+  // a by-product of the fit: no separate pass over the history
+  if (g == 0 && nfin) nfin[row] = nf0 + n;
   sse[pid] = (float)err2;
   state[pid * 3 + 0] = md.lvl;
   state[pid * 3 + 1] = md.tr;
@@ -524,7 +531,8 @@ __global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ 
                                                       const float* __restrict__ cand, int G, int m,
                                                       h8v* __restrict__ season, float* __restrict__ sse,
                                                       float* __restrict__ state, int* __restrict__ nobs,
-                                                      int t_store_end, float* __restrict__ sscale) {
+                                                      int t_store_end, float* __restrict__ sscale,
+                                                      int* __restrict__ nfin) {
   const int GP = (G + 1) >> 1;
   const int64_t NT = R * GP;
   const int64_t tid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -540,7 +548,7 @@ __global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ 
   const int base = first_finite(xr, T);
   f2v l = {0.f, 0.f}, tr = {0.f, 0.f};
   float sc = 1.f, s1 = 0.f;
-  int t0;
+  int t0, nf0 = 0;
   if (base >= T) {
     l = (f2v){__builtin_nanf(""), __builtin_nanf("")};
     t0 = T;
@@ -556,6 +564,7 @@ __global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ 
     l = (f2v){s1, s1};
     tr = (f2v){trend, trend};
     t0 = base + m;
+    nf0 = c1;
   }
   const float isc = 1.f / sc;
   f2v acc = {0.f, 0.f};
@@ -608,6 +617,7 @@ __global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ 
     nobs[pb] = n;
   }
   if (j == 0) sscale[row] = sc;
+  if (j == 0 && nfin) nfin[row] = nf0 + n;
 }
 
 __global__ __launch_bounds__(256) void hw2_forecast_kernel(const float* __restrict__ sse,
@@ -742,7 +752,7 @@ __global__ __launch_bounds__(256) void es_forecast_kernel(const float* __restric
 // (the scale written to sscale[R]); 0: fp32 [m][R*G] (sscale[R] = 1).
 FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int kind,
                      void* season, float* sse, float* state, int* nobs, int H, float* fc, float* sigma, int* best,
-                     int keep_season, int season_half, float* sscale, hipStream_t stream) {
+                     int keep_season, int season_half, float* sscale, int* nfin, hipStream_t stream) {
   if (R <= 0) return 0;
   if (kind < 0 || kind > 3) return (int)hipErrorInvalidValue;
   if (kind >= 2 && (m < 2 || 2 * m > T)) return (int)hipErrorInvalidValue;
@@ -756,13 +766,13 @@ FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* 
     // packed two-candidates-per-thread additive fit (hw2_fit_kernel)
     const int64_t NT = R * ((G + 1) / 2);
     hipLaunchKernelGGL(hw2_fit_kernel, dim3((unsigned)((NT + 255) / 256)), dim3(256), 0, stream, x, ld, T, R, cand, G,
-                       m, (h8v*)season, sse, state, nobs, t_store_end, sscale);
+                       m, (h8v*)season, sse, state, nobs, t_store_end, sscale, nfin);
     FM_LAUNCH_CHECK();
     hipLaunchKernelGGL(hw2_forecast_kernel, gr, dim3(256), 0, stream, sse, state, nobs, (const _Float16*)season,
                        sscale, R, G, m, H, fc, sigma, best);
   } else {
     FM_ES_DISPATCH_T(es_fit_kernel, float, gf, x, ld, T, R, cand, G, m, (float*)season, sse, state, nobs, t_store_end,
-                     sscale);
+                     sscale, nfin);
     FM_LAUNCH_CHECK();
     hipLaunchKernelGGL(es_forecast_kernel<float>, gr, dim3(256), 0, stream, sse, state, nobs, (const float*)season,
                        sscale, R, G, m, kind, H, fc, sigma, best);

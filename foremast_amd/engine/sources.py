@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import json
 import os
+import sys
+import time
 import urllib.parse
 import zlib
 from dataclasses import dataclass, field
@@ -394,7 +396,11 @@ class StagedSource:
             new = list(dict.fromkeys(t for t in templates if t not in self._row))
             if new:
                 self.misses += len(new)
+                t_gen = time.perf_counter()
                 cols = inner(new, g0, g0 + (G - 1) * self.step)
+                if len(new) * G > 1e7:
+                    print(f"[staged] {len(new)} series x {G} samples in {time.perf_counter() - t_gen:.1f}s",
+                          file=sys.stderr, flush=True)
                 n0 = self._n
                 if n0 + len(new) > self._mat.shape[0] or self._mat.shape[1] != G:
                     cap = max(n0 + len(new), 2 * self._mat.shape[0])

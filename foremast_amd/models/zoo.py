@@ -109,11 +109,12 @@ def _valid(hist: torch.Tensor, T: int, cur: torch.Tensor, min_hist: int) -> torc
 
 def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizon: torch.Tensor, M: int,
            tables: Tables, diff: torch.Tensor | None = None, window: int = 60, period: int | None = None,
-           lstm_model=None, pairs=None, cache: CacheContext | None = None) -> RowDecision:
+           lstm_model=None, pairs=None, cache: CacheContext | None = None, H: int | None = None) -> RowDecision:
     """Score current points of every row.
 
     ``horizon`` [R, n] int64: steps past the end of the history of each current
-    point (1 = the next sample), used by forecasting models."""
+    point (1 = the next sample), used by forecasting models; ``H`` its
+    maximum when the caller knows it (saves a device sync)."""
     algo = canonical(algorithm)
     n = cur.shape[1]
     if algo == "moving_average_all":
@@ -129,8 +130,21 @@ def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizo
         return _expand_stats(dec, n)
     if algo == "bivariate_normal":
         return _bivariate(hist, T, cur, M, tables, pairs)
-    H = int(horizon.max().item()) if horizon.numel() else 1
-    H = max(H, 1)
+    if H is None:
+        H = int(horizon.max().item()) if horizon.numel() else 1
+    H = max(int(H), 1)
+    if algo in ES_KINDS and cache is None:
+        # the grid fit counts each row's finite samples on its way through the
+        # history: no separate history pass for the MIN_HISTORICAL_DATA gate
+        kind, m = ES_KINDS[algo], 1
+        if kind >= 2:
+            m = period or _detect_period(hist, T)
+            if 2 * m > T:
+                kind, m = 1, 1
+        fit = SM.es_fit(hist, T, kind, H, m)
+        has_cur = torch.isfinite(cur).any(1).to(torch.int32)
+        valid = (fit.nfin.to(cur.device) >= max(tables.min_hist, 1)).to(torch.int32) | (has_cur << 1)
+        return band(fit.forecast, fit.sigma, horizon, cur, M, tables, diff, valid)
     fc, sigma = forecast(algo, hist, T, H, period=period, lstm_model=lstm_model, cache=cache)
     return band(fc, sigma, horizon, cur, M, tables, diff, _valid(hist, T, cur, tables.min_hist))
 
@@ -199,10 +213,13 @@ def _detect_period(hist: torch.Tensor, T: int, default: int = 1440) -> int:
     off -= off % 2
     view = hist[:, off:off + nr] if off % 4 == 0 else hist[:, :nr]
     s = FF.fft_seasonal(view.contiguous() if off % 2 else view, nr, min_period=12, max_period=nr / 2)
-    strong = s.strength > 0.1
-    if int(strong.sum()) == 0:
+    # the period is a launch parameter of the fit: one small copy of the
+    # per-row peaks and a host median (no device sort pipeline)
+    per, strength = s.period.cpu().numpy(), s.strength.cpu().numpy()
+    strong = strength > 0.1
+    if not strong.any():
         return min(default, T // 2)
-    p = int(torch.median(s.period[strong]).item())
+    p = int(np.median(per[strong]))
     return max(2, min(p, T // 2))
 
 

@@ -42,7 +42,7 @@ _SIGS: dict[str, list] = {
     "fm_synth_fleet": [c_void_p, c_i64, c_i64, c_i64, c_int, c_i64, c_int, c_int, c_int, c_int, c_float, c_float,
                        c_u32, c_void_p],
     "fm_es_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                  c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+                  c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fm_es_update": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fm_band_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p, c_i64, c_int, c_void_p, c_void_p,

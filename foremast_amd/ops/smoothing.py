@@ -55,6 +55,7 @@ class ESFit:
     best: torch.Tensor       # [R] candidate index
     sse: torch.Tensor        # [R, G]
     model: ESState | None = None
+    nfin: torch.Tensor | None = None   # [R] int32 finite history samples (a by-product of the fit)
 
 
 HALF_SEASON_MIN_M = 1000     # <= ~10 laps of a 7-day history: measured within 2e-3 of fp32 (tests)
@@ -84,7 +85,9 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
                 grid[best], st["state"], st["season"] if kind >= 2 else np.zeros((0,)), st["sse"], st["nobs"])))
             if kind < 2:
                 model.season = None
-        return ESFit(torch.from_numpy(fc), torch.from_numpy(sig), torch.from_numpy(best), torch.from_numpy(sse), model)
+        nfin = torch.from_numpy(np.isfinite(x.numpy()[:, :T]).sum(1).astype(np.int32))
+        return ESFit(torch.from_numpy(fc), torch.from_numpy(sig), torch.from_numpy(best), torch.from_numpy(sse), model,
+                     nfin)
     require_native(x)
     d = x.device
     cand = torch.from_numpy(grid).to(d)
@@ -107,8 +110,10 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     fc = torch.empty((R, H), dtype=torch.float32, device=d)
     sig = torch.empty((R,), dtype=torch.float32, device=d)
     best = torch.empty((R,), dtype=torch.int32, device=d)
+    nfin = torch.empty((R,), dtype=torch.int32, device=d)
     LIB.call("fm_es_fit", ptr(x), x.stride(0), T, R, ptr(cand), G, m, kind, ptr(season), ptr(sse), ptr(state),
-             ptr(nobs), H, ptr(fc), ptr(sig), ptr(best), int(keep_state), int(half), ptr(sscale), stream_of(x))
+             ptr(nobs), H, ptr(fc), ptr(sig), ptr(best), int(keep_state), int(half), ptr(sscale), ptr(nfin),
+             stream_of(x))
     model = None
     if keep_state:
         b = best.long()
@@ -117,7 +122,7 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
                         _half_season_of(season, b, R, GP, m, sscale) if half else
                         (season[:, pid].t().contiguous() if kind >= 2 else None),
                         sse.gather(1, b[:, None])[:, 0].contiguous(), nobs[pid].contiguous())
-    return ESFit(fc, sig, best, sse, model)
+    return ESFit(fc, sig, best, sse, model, nfin)
 
 
 def _half_season_of(season: torch.Tensor, best: torch.Tensor, R: int, GP: int, m: int,

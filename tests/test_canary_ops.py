@@ -8,7 +8,7 @@ import torch
 from foremast_amd.ops import canary as C
 from foremast_amd.ops import reference as ref
 
-from boundary import assert_only_boundary, diff_boundary, point_boundary, service_boundary
+from boundary import B_EPS, assert_only_boundary, diff_boundary, point_boundary, service_boundary
 
 
 def _data(R, n1, n2, seed=0, ties=True, nan_frac=0.0, shift=0.3):
@@ -204,6 +204,15 @@ def test_gpu_stats_decide_matches_reference(cuda, T):
     minlb = np.zeros(M, np.float32)
     diff = (rng.random(R) < 0.3).astype(np.int8)
     r0 = ref.stats_decide(hist[:, :T], cur, M, thr, bound, minlb, diff, 0.8, 10)
+    # move the (rare) current points that sit within B_EPS of a band edge off
+    # it, so the boundary set stays within the default 2 % at every level
+    th_rows = np.tile(thr, S) * np.where(diff.astype(bool), 0.8, 1.0)
+    near = point_boundary(cur, r0[0], th_rows, np.tile(bound, S))
+    if near.any():
+        mean, sd = r0[0][:, 0:1], r0[0][:, 1:2]
+        scale = np.abs(mean) + th_rows[:, None] * np.abs(sd) + 1e-6
+        cur = np.where(near, cur + (1e3 * B_EPS * scale).astype(np.float32), cur).astype(np.float32)
+        r0 = ref.stats_decide(hist[:, :T], cur, M, thr, bound, minlb, diff, 0.8, 10)
     t = lambda a: torch.from_numpy(a).to(cuda)
     o = C.stats_decide(t(hist), t(cur), T, M, t(thr), t(bound), t(minlb), t(diff), 0.8, 10)
     np.testing.assert_allclose(o.stats.cpu().numpy(), r0[0], rtol=2e-5, atol=1e-5)
@@ -211,15 +220,14 @@ def test_gpu_stats_decide_matches_reference(cuda, T):
     fr = C.unpack_flags(torch.from_numpy(r0[1]), 50)
     # exact agreement except points within B_EPS of a band edge (the band is
     # widened by the pairwise factor where diff is set)
-    th_rows = np.tile(thr, S) * np.where(diff.astype(bool), 0.8, 1.0)
     pb = point_boundary(cur, r0[0], th_rows, np.tile(bound, S))
     assert_only_boundary(fl != fr, pb, "anomaly flags")
     rb = pb.any(1)
-    assert_only_boundary(o.count.cpu().numpy() != r0[2], rb, "anomaly counts", max_frac=0.05)
+    assert_only_boundary(o.count.cpu().numpy() != r0[2], rb, "anomaly counts")
     np.testing.assert_array_equal(o.valid.cpu().numpy(), r0[4])
     packed = C.service_reduce(o.count, o.score, o.valid, M).cpu().numpy()
     p0 = ref.service_reduce(r0[2], r0[3], r0[4], M)
-    assert_only_boundary(packed[:, 0] != p0[:, 0], service_boundary(rb, M), "service status", max_frac=0.2)
+    assert_only_boundary(packed[:, 0] != p0[:, 0], service_boundary(rb, M), "service status")
     idx, val = C.compact_anomalies(o, t(cur))
     assert idx.shape[0] == int(o.count.sum())
     ii = idx.cpu().numpy()
@@ -258,7 +266,7 @@ def test_gpu_scorer_graph_equals_eager_and_cpu(cuda):
     th_rows = np.tile(sc.thr.cpu().numpy(), S) * np.where(d_cpu, sc.cfg.pairwise_threshold_factor, 1.0)
     pb = point_boundary(cc.numpy(), co.decide.stats.numpy(), th_rows, np.tile(sc.bound.cpu().numpy(), S))
     sb = service_boundary(db | pb.any(1), 8)
-    assert_only_boundary(cpu[:, 0].numpy() != eager.cpu()[:, 0].numpy(), sb, "scorer service status", max_frac=0.1)
+    assert_only_boundary(cpu[:, 0].numpy() != eager.cpu()[:, 0].numpy(), sb, "scorer service status")
     assert int((eager[:, 0] == 1).sum()) > 0
 
 
