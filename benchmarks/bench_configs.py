@@ -326,6 +326,15 @@ def config3e2e(args):
     cfg = BrainConfig()
     cfg.ml_algorithm = algo
     cfg.hpa_log_interval_s = args.hpa_log_interval
+    if strategy != "canary" and args.band_threshold:
+        # a monitored fleet that stays whole: at the 2-sigma default a job with
+        # 10 current points of iid noise closes completed_unhealth in ~20 % of
+        # cycles, and the timed cycles would score a shrinking fleet; the
+        # injected 3x regressions are caught at any of these thresholds
+        import dataclasses as _dc
+        thr = args.band_threshold
+        cfg.threshold = max(cfg.threshold, thr)
+        cfg.metric_rules = {k: _dc.replace(r, threshold=max(r.threshold, thr)) for k, r in cfg.metric_rules.items()}
     if kind == "4e2e":
         cfg.hpa_forecast_algorithm = "lstm"
         cfg.lstm_hidden = args.hidden
@@ -417,6 +426,7 @@ def config3e2e(args):
             else "fp32 data / fp64 statistics", desc[2],
             {"services": S, "metrics": M, "strategy": strategy, "algorithm": algo, "poll_seconds": poll,
              "hpa_log_interval_s": args.hpa_log_interval if strategy == "hpa" else None,
+             "band_threshold_min": args.band_threshold if strategy != "canary" else None,
              "pods_per_side": P if strategy == "canary" else 0, "store": args.store,
              "topology": ("REST service in its own process + every rank on one WAL SQLite file"
                           if args.store == "sqlite" else "single process, in-memory store"),
@@ -534,6 +544,8 @@ def main():
                     "(sqlite: the shipped topology, REST service in its own process)")
     ap.add_argument("--rest-poll-rps", type=float, default=None, help="config 3e2e + sqlite: barrelman-shaped "
                     "GET /v1/healthcheck/id load during the timed cycles (default: services / 10 s)")
+    ap.add_argument("--band-threshold", type=float, default=4.0, help="e2e continuous / HPA configs: minimum band "
+                    "threshold (sigma) of every metric rule, so the monitored fleet stays whole (0: defaults)")
     ap.add_argument("--hpa-log-interval", type=float, default=0.0, help="e2e configs: HPA_LOG_INTERVAL_SECONDS "
                     "(0: an hpalogs entry per job per cycle)")
     ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "

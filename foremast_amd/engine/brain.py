@@ -511,10 +511,15 @@ class Brain:
             return
         ok = np.isfinite(peak)
         if ok.any():
+            ga = g["ga"]
+            sl = ga.forecast_slots
+            if sl is None or len(sl) != len(peak):        # gauge slots are append-only: kept with the arrays
+                R = range(len(peak))
+                sl = ga.forecast_slots = self.exporter.forecast_slots(
+                    [works[k // M].plan.base_metrics[k % M] for k in R], [works[k // M].plan.namespace for k in R],
+                    [works[k // M].doc.app_name for k in R])
             j = np.flatnonzero(ok)
-            self.exporter.set_forecasts([works[k // M].plan.base_metrics[k % M] for k in j],
-                                        [works[k // M].plan.namespace for k in j],
-                                        [works[k // M].doc.app_name for k in j], peak[j])
+            self.exporter.set_slots(sl[j], peak[j])
 
     def _score_general(self, works: list[Work], updates: list, outcome: dict) -> list:
         """Score the general-path jobs: one batch, or job by job when the

@@ -261,8 +261,17 @@ class BrainExporter:
         self.table.set(self.table.slots([(name, namespace, app)]), [value])
 
     def set_forecasts(self, base_metrics, namespaces, apps, values) -> None:
-        names = ["foremastbrain:" + sanitize(b) + "_forecast_max" for b in base_metrics]
-        self.table.set(self.table.slots(list(zip(names, namespaces, apps))), np.asarray(values, np.float64))
+        self.set_slots(self.forecast_slots(base_metrics, namespaces, apps), values)
+
+    def forecast_slots(self, base_metrics, namespaces, apps) -> np.ndarray:
+        """Slots of the forecast gauges (stable: callers may keep them)."""
+        memo: dict[str, str] = {}
+        names = [memo.get(b) or memo.setdefault(b, "foremastbrain:" + sanitize(b) + "_forecast_max")
+                 for b in base_metrics]
+        return self.table.slots(list(zip(names, namespaces, apps)))
+
+    def set_slots(self, slots: np.ndarray, values) -> None:
+        self.table.set(slots, np.asarray(values, np.float64))
 
     def set_gauge(self, name: str, namespace: str, app: str, value: float) -> None:
         self.table.set(self.table.slots([(name, namespace, app)]), [value])

@@ -50,7 +50,7 @@ from ..ops import canary as C
 from ..ops import misc as MI
 from .resident import ResidentHistory
 from .scorer import CanaryScorer
-from .sources import SourceError, substitute_window
+from .sources import SourceError, TemplateList, substitute_window
 
 log = logging.getLogger("foremast.brain.fast")
 
@@ -135,6 +135,7 @@ class GroupArrays:
     impact_slots: np.ndarray | None = None     # exporter slots of the downstream-impact gauge
     marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
     models: object = None                      # ModelArrays of a forecasting group (cached with the arrays)
+    forecast_slots: np.ndarray | None = None   # exporter slots of the HPA forecast gauges [S * M]
 
 
 @dataclass
@@ -230,7 +231,11 @@ def pack_left(flat: np.ndarray, lens: np.ndarray, width: int, dtype=np.float32) 
     n = len(lens)
     out = np.full((n, max(1, width)), np.nan, dtype)
     tot = int(lens.sum())
-    if tot:
+    if tot and (lens == lens[0]).all():             # every row the same length (the steady state)
+        L = int(lens[0])
+        k = min(L, out.shape[1])
+        out[:, :k] = flat[:tot].reshape(n, L)[:, :k]
+    elif tot:
         starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
         row = np.repeat(np.arange(n), lens)
         col = np.arange(tot) - np.repeat(starts, lens)
@@ -325,6 +330,9 @@ class FastPath:
         self._cmp = {}            # device compaction buffers per capacity
         self._col: dict = {}      # column-wise fetched windows of sliding groups (consumed by _arrays)
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
+        self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
+        self._gstat: dict = {}    # group key -> (job ids, positions, per-job static columns)
+        self._pos_cache = None
 
     # ------------------------------------------------------------------ planning
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
@@ -455,12 +463,27 @@ class FastPath:
         """-> (lens [n], t, v) in request order ('' templates: no samples)."""
         n = len(tpls)
         lens = np.zeros(n, np.int64)
-        have = [i for i, u in enumerate(tpls) if u]
-        if not have:
+        split = getattr(tpls, "split", None)              # TemplateList: analysed once per list object
+        if split is None or split[0] is not store_types:
+            tp = np.empty(n, object)
+            tp[:] = tpls
+            st = np.empty(n, object)
+            st[:] = store_types
+            have = np.flatnonzero(tp != "")
+            by_store: dict[str, list[int]] = {}
+            if len(have):
+                s0 = st[have[0]]
+                if (st[have] == s0).all():               # one store (the common case): no per-job loop
+                    by_store[s0] = have
+                else:
+                    for i in have.tolist():
+                        by_store.setdefault(store_types[i], []).append(i)
+            split = (store_types, by_store)
+            if isinstance(tpls, TemplateList):
+                tpls.split = split
+        by_store = split[1]
+        if not by_store:
             return lens, np.zeros(0), np.zeros(0, np.float32)
-        by_store: dict[str, list[int]] = {}
-        for i in have:
-            by_store.setdefault(store_types[i], []).append(i)
         ts = []
         for st_name, idx in by_store.items():
             sub = tpls if len(idx) == n else [tpls[i] for i in idx]     # keep the caller's list object
@@ -493,12 +516,39 @@ class FastPath:
         memo = self._tpl.get(p0.group)
         if memo is None or memo[0] != ids:
             # template lists and row map of this job list, reused while it is
-            # unchanged (stable list objects let a staged source memoise them)
-            lists = {(f, m): [getattr(fw.plan, f)[m] for fw in ws]
-                     for f in ("cur_urls", "cur_stores", "base_urls", "base_stores", "hist_urls", "hist_stores")
-                     for m in range(M)}
-            memo = self._tpl[p0.group] = (ids, lists, np.stack([fw.rows for fw in ws]).astype(np.int64))
-        _, lists, rows = memo                                                # rows [S, M]
+            # unchanged (stable list objects let a staged source memoise them);
+            # a list that only lost / reordered jobs (fleet churn: a job closed)
+            # is a fancy-index of the previous one, not a per-job rebuild
+            ix = None
+            if memo is not None:
+                pos = memo[3]
+                ix = np.fromiter((pos.get(i, -1) for i in ids), np.int64, len(ids))
+                ix = ix if len(ix) and ix.min() >= 0 else None
+            if ix is not None:
+                arrs = {k: a[ix] for k, a in memo[4].items()}
+                rows = memo[2][ix]
+            else:
+                arrs = {}
+                for f in ("cur_urls", "cur_stores", "base_urls", "base_stores", "hist_urls", "hist_stores"):
+                    col = [getattr(fw.plan, f) for fw in ws]
+                    for m in range(M):
+                        a = arrs[(f, m)] = np.empty(S, object)
+                        a[:] = [c[m] for c in col]
+                rows = np.stack([fw.rows for fw in ws]).astype(np.int64)
+            if ix is not None:
+                lists = {k: TemplateList.subset(memo[1][k], a.tolist(), ix) for k, a in arrs.items()}
+                for (f, m), tl in lists.items():          # one store, every job queried: so is the subset
+                    if f.endswith("_urls"):
+                        sp = memo[1][(f, m)].split
+                        stl = lists[(f.replace("_urls", "_stores"), m)]
+                        if sp is not None and len(sp[1]) == 1:
+                            (s0, have), = sp[1].items()
+                            if len(have) == len(memo[1][(f, m)]):
+                                tl.split = (stl, {s0: np.arange(S)})
+            else:
+                lists = {k: TemplateList(a.tolist()) for k, a in arrs.items()}
+            memo = self._tpl[p0.group] = (ids, lists, rows, self._positions(ids), arrs)
+        lists, rows = memo[1], memo[2]                                       # rows [S, M]
         cur_p, base_p = [], []
         for m in range(M):
             for cat, urls, stores, acc in (("current", "cur_urls", "cur_stores", cur_p),
@@ -685,11 +735,14 @@ class FastPath:
         col = self._col.get(p0.group)
         pos = None
         if col is not None:                               # column-wise fetched this cycle
-            pos = col["pos"]
-            j = [pos.get(i, -1) for i in ident]
-            pos = None if min(j, default=-1) < 0 else np.asarray(j, np.int64)
+            if col["ids"] == ident:
+                pos = True
+            else:
+                pp = col["pos"]
+                j = np.fromiter((pp.get(i, -1) for i in ident), np.int64, len(ident))
+                pos = None if not len(j) or j.min() < 0 else j
         if pos is not None:
-            sel = None if col["ids"] == ident else (pos[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+            sel = None if pos is True else (pos[:, None] * M + np.arange(M)[None, :]).reshape(-1)
             pick = (lambda a: a) if sel is None else (lambda a: None if a is None else a[sel])
             cur_len, cur, cur_t, base = pick(col["cur_len"]), pick(col["cur"]), pick(col["cur_t"]), pick(col["base"])
         else:
@@ -700,32 +753,70 @@ class FastPath:
             cur = pack_left(np.concatenate([w.cur for w in works]), cur_len, n)
             cur_t = pack_left(np.concatenate([w.cur_t for w in works]), cur_len, n, np.float64)
             base = pack_left(np.concatenate([w.base for w in works]), base_len, nb) if nb else None
-        rowmap = np.concatenate([w.rows for w in works]).astype(np.int32)
+        rowmap, ids, handles, end, xslots = self._static_cols(works, ident, key, M)
         up = lambda a: (torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"
                         else torch.from_numpy(a))
         has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
         has_cur = np.isfinite(cur).any(1).reshape(S, M)
-        ids = np.empty(S, object)
-        ids[:] = [w.doc.id for w in works]
-        hd = [w.handle for w in works]
-        handles = None if any(h is None for h in hd) else np.asarray(hd, np.int64)
         ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
-                         up(rowmap), np.fromiter((w.end_ts for w in works), np.float64, S), ~(has_hist & has_cur),
-                         handles=handles, works=works)
-        exp = self.b.exporter
-        if exp is not None:
-            slots = []
-            for w in works:
-                p = w.plan
-                if p.export_slots is None:
-                    p.export_slots = exp.bound_slots(p.base_metrics, [p.namespace] * M, [p.app] * M)
-                slots.append(p.export_slots)
-            ga.export_slots = np.concatenate(slots)
-            ga.export_start = exp.contiguous_start(ga.export_slots)
+                         up(rowmap), end, ~(has_hist & has_cur), handles=handles, works=works)
+        if xslots is not None:
+            ga.export_slots = xslots
+            ga.export_start = self.b.exporter.contiguous_start(xslots)
         for w in works:
             w.dirty = False
         self._garr[key] = ga
         return ga
+
+    def _positions(self, ident: tuple) -> dict:
+        """{id(job): position} of a job list (one dict per cycle shared by
+        the fetch / arrays / cache-key memos of the same list)."""
+        pc = self._pos_cache
+        if pc is not None and pc[0] == ident:
+            return pc[1]
+        d = {i: j for j, i in enumerate(ident)}
+        self._pos_cache = (ident, d)
+        return d
+
+    def _static_cols(self, works: list[FastWork], ident: tuple, key: tuple, M: int):
+        """Per-job columns of a job list that do not change with its data
+        (resident rows, ids, store handles, end times, exporter slots): kept
+        per group, and a fancy-index of the previous list's when the list only
+        lost or reordered jobs (fleet churn) -- a sliding group rebuilds its
+        arrays every cycle, its job list rarely changes more than that."""
+        memo = self._gstat.get(key)
+        if memo is not None and memo[0] == ident:
+            return memo[2]
+        S = len(works)
+        ix = None
+        if memo is not None:
+            pos = memo[1]
+            ix = np.fromiter((pos.get(i, -1) for i in ident), np.int64, S)
+            ix = ix if S and ix.min() >= 0 else None
+        exp = self.b.exporter
+        if ix is not None:
+            rowmap, ids, handles, end, xs = memo[2]
+            r = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+            cols = (rowmap[r], ids[ix], None if handles is None else handles[ix], end[ix],
+                    None if xs is None else xs[r])
+        else:
+            rowmap = np.concatenate([w.rows for w in works]).astype(np.int32)
+            ids = np.empty(S, object)
+            ids[:] = [w.doc.id for w in works]
+            hd = [w.handle for w in works]
+            handles = None if any(h is None for h in hd) else np.asarray(hd, np.int64)
+            xs = None
+            if exp is not None:
+                slots = []
+                for w in works:
+                    p = w.plan
+                    if p.export_slots is None:
+                        p.export_slots = exp.bound_slots(p.base_metrics, [p.namespace] * M, [p.app] * M)
+                    slots.append(p.export_slots)
+                xs = np.concatenate(slots)
+            cols = (rowmap, ids, handles, np.fromiter((w.end_ts for w in works), np.float64, S), xs)
+        self._gstat[key] = (ident, self._positions(ident), cols)
+        return cols
 
     def score_group(self, works: list[FastWork], now: float, key: tuple | None = None) -> dict:
         p0 = works[0].plan
@@ -785,6 +876,29 @@ class FastPath:
         return idx, val, ctr
 
     # ------------------------------------------------------------------ forecasting models
+    def _cache_keys(self, works: list[FastWork], p0: JobPlan, algo: str) -> np.ndarray:
+        """Fitted-model cache keys of a group's rows ([S * M] object array),
+        a fancy-index of the previous job list's when the list only lost or
+        reordered jobs (fleet churn)."""
+        ids = tuple(map(id, works))
+        M = len(p0.aliases)
+        memo = self._keys.get((p0.group, algo))
+        if memo is not None and memo[0] == ids:
+            return memo[2]
+        ix = None
+        if memo is not None:
+            pos = memo[1]
+            ix = np.fromiter((pos.get(i, -1) for i in ids), np.int64, len(ids))
+            ix = ix if len(ix) and ix.min() >= 0 else None
+        if ix is not None:
+            kv = memo[2].reshape(-1, M)[ix].reshape(-1)
+        else:
+            kv = np.empty(len(works) * M, object)
+            kv[:] = [(f"{w.plan.namespace}/{w.doc.app_name}", a, b, algo) for w in works
+                     for a, b in zip(p0.aliases, p0.base_metrics)]
+        self._keys[(p0.group, algo)] = (ids, self._positions(ids), kv)
+        return kv
+
     def _model_arrays(self, ga: GroupArrays, works: list[FastWork], store: ResidentHistory) -> "ModelArrays":
         """Per-algorithm row subsets of a group with everything that does not
         change while the group's arrays are reused: row map, alignment of
@@ -809,7 +923,6 @@ class FastPath:
         hor = np.maximum(1, h).astype(np.int64)
         valid = ((store.nfin[rowmap] >= max(cfg.min_historical_points, 1)).astype(np.int32)
                  | (np.isfinite(ga.cur).any(1).astype(np.int32) << 1))
-        series = [f"{w.plan.namespace}/{w.doc.app_name}" for w in works]
         i32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=dev)
         subs = []
         by_algo: dict[str, list[int]] = {}
@@ -822,7 +935,11 @@ class FastPath:
             else:
                 rows = (np.arange(S)[:, None] * M + np.asarray(ms)[None, :]).reshape(-1)
                 idx = torch.as_tensor(rows, device=dev)
-            keys = [(series[r // M], p0.aliases[r % M], p0.base_metrics[r % M], algo) for r in rows]
+            # model-cache keys (ES family only) depend on the job list, not on the
+            # sliding window: kept from the arrays' previous ModelArrays
+            keys = next((s.keys for s in md.subs if s.algo == algo), None) if md is not None else None
+            if keys is None and algo in zoo.ES_KINDS:
+                keys = self._cache_keys(works, p0, algo)[rows].tolist()
             hr = hor[rows]
             subs.append(ModelSub(algo, ms, idx, i32(rowmap[rows]), i32(shift[rows]), i32(lim[rows]), T,
                                  zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev), keys, t_last[rows],
@@ -1165,11 +1282,15 @@ class FastPath:
                 hs.append(w.plan.hpa_slots)
             exp.set_hpa_scores(np.stack(hs), sc.astype(np.float64))
         al = works[0].plan.aliases
-        for j in np.flatnonzero(due):
-            w = works[j]
-            det = [HPALogDetail(a, _f(cl[j, c]), _f(up[j, c]), _f(lo[j, c])) for c, a in enumerate(al)]
-            hpalogs.append(HPALog(job_id=w.doc.id, timestamp=float(now), created_at=created,
-                                  log=HPALogBody(int(sc[j]), MI.REASONS[int(rs[j])], det)))
+        dj = np.flatnonzero(due)
+        if len(dj):
+            z = lambda a: np.where(np.isfinite(a[dj]), a[dj], 0.0).astype(np.float64).tolist()   # noqa: E731
+            CL, UP, LO = z(cl), z(up), z(lo)
+            ts = float(now)
+            for q, (j, s_, r_) in enumerate(zip(dj.tolist(), sc[dj].tolist(), rs[dj].tolist())):
+                det = [HPALogDetail(a, c, u, lw) for a, c, u, lw in zip(al, CL[q], UP[q], LO[q])]
+                hpalogs.append(HPALog(job_id=works[j].doc.id, timestamp=ts, created_at=created,
+                                      log=HPALogBody(int(s_), MI.REASONS[int(r_)], det)))
         # HPA jobs stay alive: one uniform "keep" for the whole group
         if ga is not None and len(ga.ids) == S:
             bulk.append((ga.ids, {"status": ST.PREPROCESS_COMPLETED}, ga.handles))

@@ -352,6 +352,23 @@ class SyntheticSource:
                                      fault_key=q + "|" + p), "pod", p) for i, p in enumerate(pods)]
 
 
+class TemplateList(list):
+    """The query templates of a job list.  ``root`` / ``ix``: this list is
+    ``root[ix]`` (a job list that lost or reordered jobs: fleet churn), so a
+    source that memoises per list (StagedSource) indexes the root's answer
+    instead of re-resolving every template."""
+    root = None
+    ix = None
+    split = None            # (store list, {store: positions}) memo of the brain's column fetch
+
+    @classmethod
+    def subset(cls, parent: "TemplateList", items: list, ix: np.ndarray) -> "TemplateList":
+        out = cls(items)
+        out.root = parent.root if parent.root is not None else parent
+        out.ix = ix if parent.ix is None else parent.ix[ix]
+        return out
+
+
 class StagedSource:
     """Pre-staged series: every distinct query is answered once by ``inner``
     and served from memory afterwards (a Prometheus response cache / the
@@ -392,8 +409,16 @@ class StagedSource:
         g0 = np.ceil(self.window[0] / self.step) * self.step
         G = int(np.floor((self.window[1] - g0) / self.step)) + 1
         ent = self._lists.get(id(templates))
+        root = getattr(templates, "root", None)
+        if (ent is None or ent[0] is not templates) and root is not None:
+            rent = self._lists.pop(id(root), None)
+            if rent is not None and rent[0] is root:       # a subset of a staged list: index its rows
+                self._lists[id(root)] = rent                  # (kept most recently used)
+                ent = (templates, rent[1][templates.ix])
+                self._remember(templates, ent)
         if ent is None or ent[0] is not templates:
-            new = list(dict.fromkeys(t for t in templates if t not in self._row))
+            miss = self._rows_of(templates) < 0
+            new = list(dict.fromkeys(t for t, m in zip(templates, miss.tolist()) if m)) if miss.any() else []
             if new:
                 self.misses += len(new)
                 t_gen = time.perf_counter()
@@ -415,8 +440,8 @@ class StagedSource:
                     self._mat[n0 + k, c[ok]] = cols.v[a:b][ok]
                     self._row[t] = n0 + k
                 self._n = n0 + len(new)
-            ent = (templates, np.fromiter((self._row[t] for t in templates), np.int64, len(templates)))
-            self._lists[id(templates)] = ent
+            ent = (templates, self._rows_of(templates))
+            self._remember(templates, ent)
         rows = ent[1]
         c0 = max(0, int(np.ceil((start - g0) / self.step - 1e-9)))
         c1 = min(G, int(np.floor((end - g0) / self.step + 1e-9)) + 1)
@@ -428,6 +453,25 @@ class StagedSource:
         off = np.zeros(len(rows) + 1, np.int64)
         np.cumsum(lens, out=off[1:])
         return Columns(off, t[keep], v[keep], [None] * len(rows))
+
+    def _remember(self, templates, ent) -> None:
+        if len(self._lists) >= 64:                       # bounded: job lists change with fleet churn
+            self._lists.pop(next(iter(self._lists)))
+        self._lists[id(templates)] = ent
+
+    def _rows_of(self, templates: list[str]) -> np.ndarray:
+        """Staged row of every template, -1 if not staged (a C hash lookup through a pandas
+        Index when pandas is importable: a 10k-job list changes every cycle
+        under fleet churn)."""
+        try:
+            import pandas as pd
+        except ImportError:
+            return np.fromiter((self._row.get(t, -1) for t in templates), np.int64, len(templates))
+        if getattr(self, "_index_n", -1) != len(self._row):
+            self._index = pd.Index(list(self._row))
+            self._index_rows = np.append(np.fromiter(self._row.values(), np.int64, len(self._row)), -1)
+            self._index_n = len(self._row)
+        return self._index_rows[self._index.get_indexer(templates)]   # -1 (absent) picks the trailing -1
 
     def fetch(self, url: str) -> list[Series]:
         got = self.cache.get(url)

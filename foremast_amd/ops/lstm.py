@@ -14,18 +14,22 @@ from ._lib import LIB, check, ptr, require_native, stream_of
 SUPPORTED_H = (32, 64, 128)              # register-resident single-layer kernel (lstm.hip)
 STACK_H = (32, 64, 128, 256)             # streamed-weight 1-2 layer kernel (lstm_stack.hip)
 STACK_TILING = {256: (4, 2), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row tiles / wave, column tiles)
-STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1))}           # instantiated alternatives (lstm_stack.hip)
+STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1),            # instantiated alternatives (lstm_stack.hip);
+                          (4, 102), (4, 101), (2, 102))}             # nct >= 100: LDS-DMA weight ring, nct-100 tiles
 
 
 def stack_tiling(H: int) -> tuple[int, int]:
     """(row tiles per wave, column tiles per workgroup) of the stacked kernel
     at hidden size H; ``FM_LSTM_STACK_TILING=RT:NCT`` overrides it at H = 256
     (A/B of fill vs streamed-weight reuse; the packed weights depend on RT,
-    so pack and run under the same setting)."""
+    so pack and run under the same setting).  A ``g`` suffix (``4:1g``)
+    selects the LDS-DMA weight-ring kernel at that tiling (nct + 100)."""
     import os
     env = os.environ.get("FM_LSTM_STACK_TILING")
     if env and H in STACK_TILING_ALT:
-        rt, nct = (int(v) for v in env.split(":"))
+        ring = env.endswith("g")
+        rt, nct = (int(v) for v in env.rstrip("g").split(":"))
+        nct += 100 if ring else 0
         check((rt, nct) in STACK_TILING_ALT[H], f"FM_LSTM_STACK_TILING {env} not instantiated for H={H}")
         return rt, nct
     return STACK_TILING[H]

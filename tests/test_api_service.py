@@ -190,3 +190,15 @@ def test_store_lease_claim_and_takeover(tmp_path):
         import time
         taken = store.claim("w2", 10, 90.0, now=time.time() + 120)  # lease expired -> take over
         assert [d.processing_content for d in taken] == ["w2"]
+
+
+@pytest.mark.parametrize("job_id,mod,created", [("j1", None, "2026-01-01T00:00:00Z"), ("", "m", None), ("x", "", "")])
+def test_hpalog_to_dict_matches_reflective_encoder(job_id, mod, created):
+    from foremast_amd.api.jsonmodel import to_json
+    from foremast_amd.api.models import HPALog, HPALogBody, HPALogDetail
+    lg = HPALog(job_id=job_id, modified_at=mod, created_at=created, timestamp=12.5,
+                log=HPALogBody(3, "cpu up", [HPALogDetail("cpu", 1.5, 2.0, 0.0), HPALogDetail("latency", 0.0, 0.0, -1.0)]))
+    assert lg.to_dict() == to_json(lg)
+    assert list(lg.to_dict()) == list(to_json(lg))
+    assert HPALog.from_dict(lg.to_dict()).to_dict() == lg.to_dict()
+    assert HPALog().to_dict() == to_json(HPALog())

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Host profile of the production brain cycle (config 3e2e): cProfile over
+"""Host profile of the production brain cycle (config 3e2e, or ``--config
+2e2e / 4e2e``): cProfile over
 the timed cycles only (the untimed first cycle, dominated by the synthetic
 generator, is excluded).  Prints the top functions by own time."""
 import cProfile
@@ -29,10 +30,10 @@ def timed(step, steps, warmup, dev):
 
 
 B.time_steps = timed
-sys.argv = ["bench_configs.py", "--config", "3e2e"] + sys.argv[1:]
+sys.argv = ["bench_configs.py"] + ([] if "--config" in sys.argv else ["--config", "3e2e"]) + sys.argv[1:]
 B.main()
 s = io.StringIO()
 st = pstats.Stats(prof, stream=s)
 st.sort_stats("tottime").print_stats(30)
-st.print_callees("finish_group|claim_batch|_cycle")
+st.print_callees("finish_group|claim_batch|_cycle|_finish_hpa")
 print(s.getvalue())
