@@ -23,6 +23,8 @@
 //     k-step ahead of the MFMAs that use them.
 #include "fm_common.h"
 
+#include <type_traits>
+
 using namespace fm;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -469,6 +471,373 @@ static int launch_stack(const void* xa, int64_t B, int L, const void* W0, const 
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Two layers, software-pipelined across the layer boundary so that the cell
+// updates (VALU: 5 exp + 2 rcp per unit) issue beside MFMAs instead of
+// between barriers.  Layer 0 at step t+1 needs only h0_t, and layer 1's
+// k-steps over h1_t do not need h0_{t+1}, so one step is two barrier-separated
+// phases:
+//
+//   A: L1(t)   k-steps over [h0_t; 1]      -> accB  (MFMA only)
+//      L0(t+1) k-steps over [x_{t+1}; h0_t] -> accA  ||  cell L1(t)   -> h1_t
+//   B: L1(t+1) k-steps over h1_t           -> accB  ||  cell L0(t+1) -> h0_{t+1}
+//
+// Two barriers per step instead of four, single-buffered h images, one cell
+// (4 gate values of one unit per lane) per k-step, interleaved with that
+// k-step's MFMAs -- the k-loops are unrolled so every cell's accumulator
+// registers are static.  BT = 32 sequences (one column tile); the A fragments
+// stay one k-step ahead across phase boundaries, and the barriers wait only
+// for LDS (workgroup fence on the local address space), so those loads stay
+// in flight across them.
+namespace {
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+template <int N>
+using ic = std::integral_constant<int, N>;
+// f(ic<0>{}), ..., f(ic<N-1>{}): a compile-time-indexed unrolled sequence
+template <class F, int... Gs>
+__device__ __forceinline__ void for_each_ic(F&& f, std::integer_sequence<int, Gs...>) {
+  (f(ic<Gs>{}), ...);
+}
+}  // namespace
+
+template <int H, int RT>
+__global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
+    const uint4* __restrict__ xa, int64_t B, int L, const uint4* __restrict__ W0, const uint4* __restrict__ W1,
+    float* __restrict__ h_out, float* __restrict__ c_out) {
+  constexpr int NW = H / (8 * RT);
+  constexpr int KH = H / 16;
+  constexpr int KS0 = KH + 1;
+  constexpr int KS1 = 2 * KH + 1;
+  constexpr int HP = H + 8;
+  constexpr int BT = 32;
+  constexpr int NC = 4 * RT;                           // cells per lane per layer-step
+  static_assert(NC <= KH, "one cell per k-step of the h1 phase");
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  unsigned short* h0b = lds;                           // [BT][HP] h0 (single-buffered)
+  unsigned short* h1b = lds + BT * HP;                 // [BT][HP] h1
+  const int lane = lane_id(), w = wave_id();
+  const int hf = lane >> 5, col = lane & 31;
+  const int64_t b0 = (int64_t)blockIdx.x * BT;
+
+  for (int i = threadIdx.x; i < 2 * BT * HP; i += 64 * NW) lds[i] = 0;   // h_{-1} = 0
+  float c0[RT][4], c1[RT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c0[rt][j] = c1[rt][j] = 0.f;
+  __syncthreads();
+
+  int64_t bb = b0 + col;
+  const bool inb = bb < B;
+  bb = inb ? bb : B - 1;
+  const uint4* xp = xa + (bb * L) * 2 + hf;
+  // weights through buffer loads: a wave-uniform resource (SGPRs), the lane's
+  // 16 B as the VGPR offset and the k-step as a scalar offset -- no per-load
+  // 64-bit VGPR address (with 268 loads in the unrolled step those addresses
+  // are what the compiler hoists and spills)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t W0w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W0 + (int64_t)wu * RT * KS0 * 64), (short)0, RT * KS0 * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t W1w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W1 + (int64_t)wu * RT * KS1 * 64), (short)0, RT * KS1 * 1024, 0x00020000);
+  const int voff = 16 * lane;
+  const uint4 onesv = make_uint4(hf == 0 ? 0x3F80u : 0u, 0u, 0u, 0u);
+  const unsigned short* h0r = h0b + col * HP + 8 * hf;     // this lane's B-fragment row
+  const unsigned short* h1r = h1b + col * HP + 8 * hf;
+  unsigned short* h0w = h0b + col * HP;
+  unsigned short* h1w = h1b + col * HP;
+  auto lds16 = [](const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); };
+
+  Frag a[RT];                                          // A fragments of the current k-step
+  auto loadA = [&](Frag (&f)[RT], __amdgpu_buffer_rsrc_t Ww, int KS, int ks) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(Ww, voff, (rt * KS + ks) * 1024, 0);
+      f[rt].u = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+  // NK unrolled k-steps: A of step i from (Ww, KS, ks_of(i)), B = b_of(i),
+  // then cell_at(i); the A fragments of (Wn, KSn, ksn) are prefetched during
+  // the last step (the first k-step of whatever follows)
+  auto segment = [&](auto NK, f32x16 (&acc)[RT], __amdgpu_buffer_rsrc_t Ww, int KS, auto ks_of, auto b_of,
+                     __amdgpu_buffer_rsrc_t Wn, int KSn, int ksn, auto cell_at) {
+#pragma unroll
+    for (int i = 0; i < decltype(NK)::value; ++i) {
+      __builtin_amdgcn_sched_barrier(0);             // k-steps stay in order: no hoisted loads
+      Frag an[RT];
+      if (i + 1 < decltype(NK)::value) loadA(an, Ww, KS, ks_of(i + 1));
+      else loadA(an, Wn, KSn, ksn);
+      Frag bf;
+      bf.u = b_of(i);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rt].v, bf.v, acc[rt], 0, 0, 0);
+      cell_at(i);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) a[rt] = an[rt];
+    }
+  };
+  auto zero = [](f32x16 (&acc)[RT]) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x16){};
+  };
+  // cell q (row tile q / 4, unit q % 4 of the lane's 4) of a finished layer
+  // accumulator; the tile's 4 h values go to LDS with its last cell
+  float hv[4];
+  auto cell_q = [&](int q, const f32x16 (&acc)[RT], float (&c)[RT][4], unsigned short* hw, bool out) {
+    const int rt = q >> 2, j = q & 3;
+    cell(acc[rt][j], acc[rt][4 + j], acc[rt][8 + j], acc[rt][12 + j], c[rt][j], hv[j]);
+    if (j == 3) {
+      const int u0 = 8 * RT * w + 8 * rt + 4 * hf;
+      uint2 pk;
+      pk.x = pack_bf2(hv[0], hv[1]);
+      pk.y = pack_bf2(hv[2], hv[3]);
+      *reinterpret_cast<uint2*>(&hw[u0]) = pk;
+      if (out && inb) {
+        *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        *reinterpret_cast<float4*>(&c_out[bb * H + u0]) = make_float4(c[rt][0], c[rt][1], c[rt][2], c[rt][3]);
+      }
+    }
+  };
+  const auto ks_l0 = [](int i) { return i == 0 ? KH : i - 1; };        // layer 0: x/bias step first
+  const auto ks_l1b = [](int i) { return KH + i; };                    // layer 1 over [h0; 1]
+  const auto ks_l1a = [](int i) { return i; };                         // layer 1 over h1
+  const auto no_cell = [](int) {};
+
+  f32x16 accA[RT], accB[RT];
+  uint4 xt = xp[0];
+  // prologue: L0(0) (h0_{-1} = 0), its cells, barrier; L1(0)'s k-steps over
+  // h1_{-1} = 0 contribute nothing: accB starts at zero
+  loadA(a, W0w, KS0, KH);
+  zero(accA);
+  segment(ic<KS0>{}, accA, W0w, KS0, ks_l0,
+          [&](int i) { const uint4 v = lds16(h0r + 16 * (i == 0 ? 0 : i - 1)); return i == 0 ? xt : v; },
+          W1w, KS1, KH, no_cell);
+#pragma unroll
+  for (int q = 0; q < NC; ++q) cell_q(q, accA, c0, h0w, false);
+  lds_barrier();
+  zero(accB);
+  const auto b_l1b = [&](int i) { const uint4 v = lds16(h0r + 16 * (i < KH ? i : KH - 1)); return i == KH ? onesv : v; };
+  for (int t = 0; t < L - 1; ++t) {
+    xt = xp[(t + 1) * 2];
+    // phase A: L1(t) over [h0_t; 1]
+    segment(ic<KH + 1>{}, accB, W1w, KS1, ks_l1b, b_l1b, W0w, KS0, KH, no_cell);
+    //          L0(t+1) over [x_{t+1}; h0_t]  ||  cells of L1(t)
+    zero(accA);
+    segment(ic<KS0>{}, accA, W0w, KS0, ks_l0,
+            [&](int i) { const uint4 v = lds16(h0r + 16 * (i == 0 ? 0 : i - 1)); return i == 0 ? xt : v; },
+            W1w, KS1, 0, [&](int i) { if (i < NC) cell_q(i, accB, c1, h1w, false); });
+    lds_barrier();                                   // h1_t complete; every read of h0_t done
+    // phase B: L1(t+1) over h1_t  ||  cells of L0(t+1)
+    zero(accB);
+    segment(ic<KH>{}, accB, W1w, KS1, ks_l1a, [&](int i) { return lds16(h1r + 16 * i); },
+            W1w, KS1, KH, [&](int i) { if (i < NC) cell_q(i, accA, c0, h0w, false); });
+    lds_barrier();                                   // h0_{t+1} complete; every read of h1_t done
+  }
+  // the last step's layer 1 (out of the loop: its output addresses are not
+  // live across the time loop)
+  segment(ic<KH + 1>{}, accB, W1w, KS1, ks_l1b, b_l1b, W1w, KS1, 0, no_cell);
+#pragma unroll
+  for (int q = 0; q < NC; ++q) cell_q(q, accB, c1, h1w, true);
+}
+
+// The same two-phase schedule as one flat, unrolled sequence of the step's
+// NG = 3 H/16 + 2 k-steps (L1 over [h0; 1], L0 over [x; h0], L1 over h1), so
+// the A fragments run D k-steps ahead through a ring of D + 1 register sets
+// -- across phase boundaries, barriers and time steps (NG % (D + 1) == 0
+// keeps the ring aligned from one step to the next).  c of both layers lives
+// in LDS (lane-linear float4 per row tile) to leave the registers to the ring.
+template <int H, int RT, int D>
+__global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_flow_kernel(
+    const uint4* __restrict__ xa, int64_t B, int L, const uint4* __restrict__ W0, const uint4* __restrict__ W1,
+    float* __restrict__ h_out, float* __restrict__ c_out) {
+  constexpr int NW = H / (8 * RT);
+  constexpr int KH = H / 16;
+  constexpr int KS0 = KH + 1;
+  constexpr int KS1 = 2 * KH + 1;
+  constexpr int HP = H + 8;
+  constexpr int BT = 32;
+  constexpr int NC = 4 * RT;
+  constexpr int NG = 3 * KH + 2;
+  constexpr int G2 = KH + 1, G3 = 2 * KH + 2;          // first k-step of the L0 / L1-over-h1 phases
+  constexpr int R = D + 1;
+  static_assert(NC <= KH && NG % R == 0, "ring must stay aligned across steps");
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  unsigned short* h0b = lds;                           // [BT][HP]
+  unsigned short* h1b = lds + BT * HP;                 // [BT][HP]
+  float4* cst = reinterpret_cast<float4*>(lds + 2 * BT * HP);   // [2][NW][RT][64] c of both layers
+  const int lane = lane_id(), w = wave_id();
+  const int hf = lane >> 5, col = lane & 31;
+  const int64_t b0 = (int64_t)blockIdx.x * BT;
+  {
+    unsigned* z = reinterpret_cast<unsigned*>(lds);
+    constexpr int NZ = BT * HP + 2 * NW * RT * 64 * 4;           // dwords: h images + c
+    for (int i = threadIdx.x; i < NZ; i += 64 * NW) z[i] = 0u;
+  }
+  __syncthreads();
+
+  int64_t bb = b0 + col;
+  const bool inb = bb < B;
+  bb = inb ? bb : B - 1;
+  const uint4* xp = xa + (bb * L) * 2 + hf;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t W0w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W0 + (int64_t)wu * RT * KS0 * 64), (short)0, RT * KS0 * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t W1w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W1 + (int64_t)wu * RT * KS1 * 64), (short)0, RT * KS1 * 1024, 0x00020000);
+  const int voff = 16 * lane;
+  const unsigned short* h0r = h0b + col * HP + 8 * hf;
+  const unsigned short* h1r = h1b + col * HP + 8 * hf;
+  unsigned short* h0w = h0b + col * HP;
+  unsigned short* h1w = h1b + col * HP;
+  auto lds16 = [](const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); };
+  auto ones = [&]() { return make_uint4(hf == 0 ? 0x3F80u : 0u, 0u, 0u, 0u); };
+
+  auto loadA = [&](Frag (&f)[RT], __amdgpu_buffer_rsrc_t Ww, int KS, int ks) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(Ww, voff, (rt * KS + ks) * 1024, 0);
+      f[rt].u = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+  // k-step g of a time step -> A fragments
+  auto load_g = [&](Frag (&f)[RT], int g) {
+    if (g < G2) loadA(f, W1w, KS1, KH + g);                          // L1 over [h0; 1]
+    else if (g < G3) loadA(f, W0w, KS0, g == G2 ? KH : g - G2 - 1);  // L0: x/bias step first
+    else loadA(f, W1w, KS1, g - G3);                                 // L1 over h1
+  };
+  auto mfma = [&](f32x16 (&acc)[RT], const Frag (&f)[RT], uint4 b) {
+    Frag bf;
+    bf.u = b;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[rt].v, bf.v, acc[rt], 0, 0, 0);
+  };
+  auto zero = [](f32x16 (&acc)[RT]) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = (f32x16){};
+  };
+  float hv[4], cq[4];
+  auto cell_q = [&](int q, const f32x16 (&acc)[RT], int layer, unsigned short* hw, bool out) {
+    const int rt = q >> 2, j = q & 3;
+    float4* cp = cst + ((layer * NW + w) * RT + rt) * 64 + lane;
+    if (j == 0) {
+      const float4 c4 = *cp;
+      cq[0] = c4.x; cq[1] = c4.y; cq[2] = c4.z; cq[3] = c4.w;
+    }
+    cell(acc[rt][j], acc[rt][4 + j], acc[rt][8 + j], acc[rt][12 + j], cq[j], hv[j]);
+    if (j == 3) {
+      const int u0 = 8 * RT * w + 8 * rt + 4 * hf;
+      uint2 pk;
+      pk.x = pack_bf2(hv[0], hv[1]);
+      pk.y = pack_bf2(hv[2], hv[3]);
+      *reinterpret_cast<uint2*>(&hw[u0]) = pk;
+      *cp = make_float4(cq[0], cq[1], cq[2], cq[3]);
+      if (out && inb) {
+        *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        *reinterpret_cast<float4*>(&c_out[bb * H + u0]) = make_float4(cq[0], cq[1], cq[2], cq[3]);
+      }
+    }
+  };
+
+  f32x16 accA[RT], accB[RT];
+  Frag fr[R][RT];
+  // prologue: L0(0) with h0_{-1} = 0 (one k-step lookahead), its cells, barrier
+  {
+    uint4 x0 = xp[0];
+    Frag a[RT], an[RT];
+    loadA(a, W0w, KS0, KH);
+    zero(accA);
+#pragma unroll
+    for (int i = 0; i < KS0; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < KS0) loadA(an, W0w, KS0, i);
+      const uint4 v = lds16(h0r + 16 * (i == 0 ? 0 : i - 1));
+      mfma(accA, a, i == 0 ? x0 : v);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) a[rt] = an[rt];
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_g(fr[d], d);      // the ring: first k-steps of step 0
+#pragma unroll
+    for (int q = 0; q < NC; ++q) cell_q(q, accA, 0, h0w, false);
+    lds_barrier();
+  }
+  zero(accB);                                          // L1(0) over h1_{-1} = 0
+  uint4 xt = make_uint4(0u, 0u, 0u, 0u);
+  for (int t = 0; t < L - 1; ++t) {
+    for_each_ic([&](auto G) {
+      constexpr int g = decltype(G)::value;
+      __builtin_amdgcn_sched_barrier(0);               // k-steps stay in order
+      load_g(fr[(g + D) % R], (g + D) % NG);           // D ahead (wrapping into step t + 1)
+      if constexpr (g == 0) xt = xp[(t + 1) * 2];
+      if constexpr (g < G2) {                          // phase A: L1(t) over [h0_t; 1]
+        const uint4 v = lds16(h0r + 16 * (g < KH ? g : KH - 1));
+        mfma(accB, fr[g % R], g == KH ? ones() : v);
+      } else if constexpr (g < G3) {                   //   L0(t+1) over [x_{t+1}; h0_t] || cells L1(t)
+        constexpr int i = g - G2;
+        if constexpr (i == 0) zero(accA);
+        const uint4 v = lds16(h0r + 16 * (i == 0 ? 0 : i - 1));
+        mfma(accA, fr[g % R], i == 0 ? xt : v);
+        if constexpr (i < NC) cell_q(i, accB, 1, h1w, false);
+        if constexpr (g == G3 - 1) lds_barrier();      // h1_t complete; every read of h0_t done
+      } else {                                         // phase B: L1(t+1) over h1_t || cells L0(t+1)
+        constexpr int i = g - G3;
+        if constexpr (i == 0) zero(accB);
+        mfma(accB, fr[g % R], lds16(h1r + 16 * i));
+        if constexpr (i < NC) cell_q(i, accA, 0, h0w, false);
+        if constexpr (g == NG - 1) lds_barrier();      // h0_{t+1} complete; every read of h1_t done
+      }
+    }, std::make_integer_sequence<int, NG>{});
+  }
+  // the last step's layer 1 over [h0; 1] (its ring sets were loaded ahead)
+#pragma unroll
+  for (int g = 0; g < G2; ++g) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + D < G2) load_g(fr[(g + D) % R], g + D);
+    const uint4 v = lds16(h0r + 16 * (g < KH ? g : KH - 1));
+    mfma(accB, fr[g % R], g == KH ? ones() : v);
+  }
+#pragma unroll
+  for (int q = 0; q < NC; ++q) cell_q(q, accB, 1, h1w, true);
+}
+
+template <int H, int RT, int D>
+static int launch_stack2_flow(const void* xa, int64_t B, int L, const void* W0, const void* W1, float* h_out,
+                              float* c_out, hipStream_t stream) {
+  constexpr int NW = H / (8 * RT);
+  const size_t lds = (size_t)2 * 32 * (H + 8) * sizeof(unsigned short) + (size_t)2 * NW * RT * 64 * 16;
+  auto k = lstm_stack2_flow_kernel<H, RT, D>;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)((B + 31) / 32)), dim3(64 * NW), lds, stream, (const uint4*)xa, B, L,
+                     (const uint4*)W0, (const uint4*)W1, h_out, c_out);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int H, int RT>
+static int launch_stack2_pipe(const void* xa, int64_t B, int L, const void* W0, const void* W1, float* h_out,
+                              float* c_out, hipStream_t stream) {
+  constexpr int NW = H / (8 * RT);
+  const size_t lds = (size_t)2 * 32 * (H + 8) * sizeof(unsigned short);
+  auto k = lstm_stack2_pipe_kernel<H, RT>;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)((B + 31) / 32)), dim3(64 * NW), lds, stream, (const uint4*)xa, B, L,
+                     (const uint4*)W0, (const uint4*)W1, h_out, c_out);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
 // Row tiles per wave / column tiles per workgroup (see ops/lstm.py STACK_TILING):
 // H=256: 4 x 2 (8 waves, 64 sequences share every streamed weight fragment:
 // half the L2 weight traffic of 4 x 1, which wins despite 65 spilled VGPRs
@@ -485,6 +854,16 @@ FM_API int fm_lstm_stack(const void* xa, int64_t B, int L, int H, int layers, co
 #define FM_STK(HH, RTT, NCC)                                                                              \
   return layers == 2 ? launch_stack<HH, RTT, NCC, 2>(xa, B, L, W0, W1, h_out, c_out, stream)            \
                      : launch_stack<HH, RTT, NCC, 1>(xa, B, L, W0, W1, h_out, c_out, stream)
+  if (nct == 202 && layers == 2) {     // flat-sequence pipelined kernel (lstm_stack2_flow_kernel), ring depth 4
+    if (H == 256 && rt == 4) return launch_stack2_flow<256, 4, 4>(xa, B, L, W0, W1, h_out, c_out, stream);
+    if (H == 256 && rt == 2) return launch_stack2_flow<256, 2, 4>(xa, B, L, W0, W1, h_out, c_out, stream);
+    return (int)hipErrorInvalidValue;
+  }
+  if (nct == 201 && layers == 2) {     // layer-pipelined 2-layer kernel (lstm_stack2_pipe_kernel), 1 column tile
+    if (H == 256 && rt == 4) return launch_stack2_pipe<256, 4>(xa, B, L, W0, W1, h_out, c_out, stream);
+    if (H == 256 && rt == 2) return launch_stack2_pipe<256, 2>(xa, B, L, W0, W1, h_out, c_out, stream);
+    return (int)hipErrorInvalidValue;
+  }
   if (nct >= 100) {                    // LDS-DMA weight ring (lstm_stack_glds_kernel), nct - 100 column tiles
 #define FM_GLDS(HH, RTT, NCC, DD)                                                                              \
   return layers == 2 ? launch_stack_glds<HH, RTT, NCC, 2, DD>(xa, B, L, W0, W1, h_out, c_out, stream)         \

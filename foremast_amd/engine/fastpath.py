@@ -136,6 +136,7 @@ class GroupArrays:
     marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
     models: object = None                      # ModelArrays of a forecasting group (cached with the arrays)
     forecast_slots: np.ndarray | None = None   # exporter slots of the HPA forecast gauges [S * M]
+    key: tuple | None = None                   # the group key these arrays were built under
 
 
 @dataclass
@@ -765,6 +766,7 @@ class FastPath:
             ga.export_start = self.b.exporter.contiguous_start(xslots)
         for w in works:
             w.dirty = False
+        ga.key = key
         self._garr[key] = ga
         return ga
 
@@ -794,11 +796,13 @@ class FastPath:
             ix = np.fromiter((pos.get(i, -1) for i in ident), np.int64, S)
             ix = ix if S and ix.min() >= 0 else None
         exp = self.b.exporter
+        extra: dict = {}
         if ix is not None:
             rowmap, ids, handles, end, xs = memo[2]
             r = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)
             cols = (rowmap[r], ids[ix], None if handles is None else handles[ix], end[ix],
                     None if xs is None else xs[r])
+            extra = {k: v[ix] for k, v in memo[3].items()}          # per-job extras ride along
         else:
             rowmap = np.concatenate([w.rows for w in works]).astype(np.int32)
             ids = np.empty(S, object)
@@ -815,8 +819,20 @@ class FastPath:
                     slots.append(p.export_slots)
                 xs = np.concatenate(slots)
             cols = (rowmap, ids, handles, np.fromiter((w.end_ts for w in works), np.float64, S), xs)
-        self._gstat[key] = (ident, self._positions(ident), cols)
+        self._gstat[key] = (ident, self._positions(ident), cols, extra)
         return cols
+
+    def _extra(self, key: tuple, ident: tuple, name: str, make):
+        """A per-job array of a group's static memo (first axis = job), built
+        by ``make()`` when the job list gained jobs; fancy-indexed with the
+        static columns under churn."""
+        memo = self._gstat.get(key)
+        if memo is None or memo[0] != ident:
+            return make()
+        v = memo[3].get(name)
+        if v is None:
+            v = memo[3][name] = make()
+        return v
 
     def score_group(self, works: list[FastWork], now: float, key: tuple | None = None) -> dict:
         p0 = works[0].plan
@@ -1259,10 +1275,15 @@ class FastPath:
         lo = np.where(has, stats[:, 3], np.nan).astype(np.float32).reshape(S, M)
         tmpl = works[0].plan.tmpl
         dev = self.b.device
-        ids = [w.doc.id for w in works]
-        sl = self.hpa.slots(ids)
-        for w in works:
-            self.hpa.owner[w.doc.id] = (w.plan.namespace, w.doc.app_name)
+
+        def hpa_slots():
+            ids = [w.doc.id for w in works]
+            for w in works:
+                self.hpa.owner[w.doc.id] = (w.plan.namespace, w.doc.app_name)
+            return self.hpa.slots(ids).cpu().numpy()
+        key = ga.key if ga is not None else None
+        sl_np = self._extra(key, ga.ident, "hpa", hpa_slots) if key is not None else hpa_slots()
+        sl = torch.as_tensor(sl_np, device=dev)
         sub = self.hpa.gather(sl)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         cfg = self.b.cfg
@@ -1270,17 +1291,19 @@ class FastPath:
                                  cfg.hpa_max_flips, cfg.hpa_flip_window)
         self.hpa.scatter(sl, sub)
         sc, rs = sc.cpu().numpy(), rs.cpu().numpy()
-        due = self.hpa.log_due(sl.cpu().numpy(), sc.astype(np.int64), rs.astype(np.int64), now,
-                               cfg.hpa_log_interval_s)
+        due = self.hpa.log_due(sl_np, sc.astype(np.int64), rs.astype(np.int64), now, cfg.hpa_log_interval_s)
         created = rfc3339(datetime.fromtimestamp(now, timezone.utc))
         exp = self.b.exporter
         if exp is not None:
-            hs = []
-            for w in works:
-                if w.plan.hpa_slots is None:
-                    w.plan.hpa_slots = exp.hpa_slots([w.doc.namespace], [w.doc.app_name])[0]
-                hs.append(w.plan.hpa_slots)
-            exp.set_hpa_scores(np.stack(hs), sc.astype(np.float64))
+            def xhpa():
+                hs = []
+                for w in works:
+                    if w.plan.hpa_slots is None:
+                        w.plan.hpa_slots = exp.hpa_slots([w.doc.namespace], [w.doc.app_name])[0]
+                    hs.append(w.plan.hpa_slots)
+                return np.stack(hs)
+            hs = self._extra(key, ga.ident, "xhpa", xhpa) if key is not None else xhpa()
+            exp.set_hpa_scores(hs, sc.astype(np.float64))
         al = works[0].plan.aliases
         dj = np.flatnonzero(due)
         if len(dj):
