@@ -165,6 +165,49 @@ class HPALog:
         return from_json(cls, d)
 
 
+class HPALogBatch:
+    """The hpalogs entries of one brain cycle, columnar (the fast path writes
+    one per due HPA job: engine/fastpath.py ``_finish_hpa``).  Stores persist
+    :meth:`bodies` -- the JSON of each entry's :meth:`HPALog.to_dict`,
+    formatted natively -- and never build the per-entry objects; reads parse
+    the few entries they return.
+
+    ``score`` int [n]; ``reason`` int [n] indexes ``reasons``; ``current`` /
+    ``upper`` / ``lower`` float [n, len(aliases)], finite."""
+
+    __slots__ = ("job_ids", "timestamp", "created_at", "score", "reason", "reasons", "aliases", "current", "upper",
+                 "lower")
+
+    def __init__(self, job_ids: list[str], timestamp: float, created_at: str, score, reason, reasons: list[str],
+                 aliases: list[str], current, upper, lower) -> None:
+        self.job_ids = list(job_ids)
+        self.timestamp = float(timestamp)
+        self.created_at = created_at
+        self.score, self.reason, self.reasons, self.aliases = score, reason, list(reasons), list(aliases)
+        self.current, self.upper, self.lower = current, upper, lower
+
+    def __len__(self) -> int:
+        return len(self.job_ids)
+
+    def log(self, i: int) -> HPALog:
+        det = [HPALogDetail(a, float(self.current[i][k]), float(self.upper[i][k]), float(self.lower[i][k]))
+               for k, a in enumerate(self.aliases)]
+        return HPALog(job_id=self.job_ids[i], timestamp=self.timestamp, created_at=self.created_at,
+                      log=HPALogBody(int(self.score[i]), self.reasons[int(self.reason[i])], det))
+
+    def logs(self) -> list[HPALog]:
+        return [self.log(i) for i in range(len(self))]
+
+    def bodies(self) -> list[str]:
+        import json
+        try:
+            from ..engine import native_rt
+            out = native_rt.hpalog_bodies(self)
+        except ImportError:
+            out = None
+        return out if out is not None else [json.dumps(lg.to_dict()) for lg in self.logs()]
+
+
 @dataclass
 class HPALogResponse:
     job_id: str = jf("jobId", default="")

@@ -512,12 +512,13 @@ class Brain:
         ok = np.isfinite(peak)
         if ok.any():
             ga = g["ga"]
-            sl = ga.forecast_slots
-            if sl is None or len(sl) != len(peak):        # gauge slots are append-only: kept with the arrays
+
+            def make():                                   # gauge slots are append-only: kept per job list
                 R = range(len(peak))
-                sl = ga.forecast_slots = self.exporter.forecast_slots(
+                return self.exporter.forecast_slots(
                     [works[k // M].plan.base_metrics[k % M] for k in R], [works[k // M].plan.namespace for k in R],
-                    [works[k // M].doc.app_name for k in R])
+                    [works[k // M].doc.app_name for k in R]).reshape(len(works), M)
+            sl = (self.fast._extra(ga.key, ga.ident, "xfc", make) if ga.key is not None else make()).reshape(-1)
             j = np.flatnonzero(ok)
             self.exporter.set_slots(sl[j], peak[j])
 

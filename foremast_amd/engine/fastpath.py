@@ -44,7 +44,7 @@ import torch
 
 from ..api import status as ST
 from ..api.jobs import parse_rfc3339, rfc3339
-from ..api.models import Document, HPALog, HPALogBody, HPALogDetail
+from ..api.models import Document, HPALogBatch
 from ..api.urls import END_PLACEHOLDER, START_PLACEHOLDER, parse_config, prometheus_query_of, promql_metric_name
 from ..ops import canary as C
 from ..ops import misc as MI
@@ -135,7 +135,6 @@ class GroupArrays:
     impact_slots: np.ndarray | None = None     # exporter slots of the downstream-impact gauge
     marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
     models: object = None                      # ModelArrays of a forecasting group (cached with the arrays)
-    forecast_slots: np.ndarray | None = None   # exporter slots of the HPA forecast gauges [S * M]
     key: tuple | None = None                   # the group key these arrays were built under
 
 
@@ -1307,13 +1306,13 @@ class FastPath:
         al = works[0].plan.aliases
         dj = np.flatnonzero(due)
         if len(dj):
-            z = lambda a: np.where(np.isfinite(a[dj]), a[dj], 0.0).astype(np.float64).tolist()   # noqa: E731
-            CL, UP, LO = z(cl), z(up), z(lo)
-            ts = float(now)
-            for q, (j, s_, r_) in enumerate(zip(dj.tolist(), sc[dj].tolist(), rs[dj].tolist())):
-                det = [HPALogDetail(a, c, u, lw) for a, c, u, lw in zip(al, CL[q], UP[q], LO[q])]
-                hpalogs.append(HPALog(job_id=works[j].doc.id, timestamp=ts, created_at=created,
-                                      log=HPALogBody(int(s_), MI.REASONS[int(r_)], det)))
+            # one columnar batch: the store formats the bodies natively
+            z = lambda a: np.where(np.isfinite(a[dj]), a[dj], 0.0).astype(np.float64)   # noqa: E731
+            ids = ga.ids[dj].tolist() if ga is not None and len(ga.ids) == S else [works[j].doc.id for j in dj]
+            codes = sorted(MI.REASONS)
+            hpalogs.append(HPALogBatch(ids, float(now), created, sc[dj].astype(np.int64),
+                                       np.searchsorted(codes, rs[dj]).astype(np.int32),
+                                       [MI.REASONS[c] for c in codes], list(al), z(cl), z(up), z(lo)))
         # HPA jobs stay alive: one uniform "keep" for the whole group
         if ga is not None and len(ga.ids) == S:
             bulk.append((ga.ids, {"status": ST.PREPROCESS_COMPLETED}, ga.handles))

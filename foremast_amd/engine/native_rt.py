@@ -37,6 +37,12 @@ def _load():
     lib.fm_render_bound.restype = c_i64
     lib.fm_render_lines.argtypes = [ctypes.c_char_p, c_vp, c_vp, c_i64, c_vp, ctypes.c_char_p, c_i64, ctypes.c_int]
     lib.fm_render_lines.restype = c_i64
+    lib.fm_hpalog_bound.argtypes = [c_i64, ctypes.c_int, c_i64, c_i64, c_vp, c_vp, c_i64]
+    lib.fm_hpalog_bound.restype = c_i64
+    lib.fm_hpalog_json.argtypes = [c_i64, ctypes.c_int, ctypes.c_char_p, c_vp, ctypes.c_char_p, c_i64,
+                                   ctypes.c_double, c_vp, c_vp, ctypes.c_char_p, c_vp, ctypes.c_char_p, c_vp,
+                                   c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, ctypes.c_int]
+    lib.fm_hpalog_json.restype = c_i64
     _lib = lib
     return lib
 
@@ -103,3 +109,43 @@ def pack_right(rows: list[np.ndarray], ncols: int, ld: int, threads: int = 4) ->
     lens = np.array([len(r) for r in rows], np.int64)
     lib.fm_pack_right(ptrs, lens.ctypes.data, len(rows), out.ctypes.data, ld, ncols, threads)
     return out
+
+
+def _joined(strs) -> tuple[bytes, np.ndarray]:
+    enc = [x.encode() for x in strs]
+    off = np.zeros(len(enc) + 1, np.int64)
+    np.cumsum(np.fromiter(map(len, enc), np.int64, len(enc)), out=off[1:])
+    return b"".join(enc), off
+
+
+def hpalog_bodies(batch) -> list[str] | None:
+    """JSON bodies (HPALog.to_dict) of an api.models.HPALogBatch, formatted
+    natively (csrc/runtime/hpalog_json.cpp); None without the library."""
+    lib = _load()
+    n = len(batch)
+    if lib is None or not hasattr(lib, "fm_hpalog_json"):
+        return None
+    if n == 0:
+        return []
+    m = len(batch.aliases)
+    ids, id_off = _joined(batch.job_ids)
+    rs, r_off = _joined(batch.reasons)
+    al, a_off = _joined(batch.aliases)
+    created = (batch.created_at or "").encode()
+    score = np.ascontiguousarray(batch.score, np.int64)
+    ridx = np.ascontiguousarray(batch.reason, np.int32)
+    cur, up, lo = (np.ascontiguousarray(a, np.float64).reshape(n, m) for a in (batch.current, batch.upper, batch.lower))
+    cap = lib.fm_hpalog_bound(n, m, len(ids), len(created), r_off.ctypes.data, ridx.ctypes.data, len(al))
+    out = np.empty(max(cap, 1), np.uint8)
+    boff = np.empty(n + 1, np.int64)
+    w = lib.fm_hpalog_json(n, m, ids, id_off.ctypes.data, created, len(created), float(batch.timestamp),
+                           score.ctypes.data, ridx.ctypes.data, rs, r_off.ctypes.data, al, a_off.ctypes.data,
+                           cur.ctypes.data, up.ctypes.data, lo.ctypes.data, out.ctypes.data, cap, boff.ctypes.data,
+                           4)
+    if w < 0:
+        raise RuntimeError("fm_hpalog_json: output bound exceeded")
+    mv = memoryview(out)[:w]
+    text = str(mv, "utf-8")                 # one decode straight from the buffer
+    if text.isascii():                      # byte offsets are character offsets
+        return [text[a:b] for a, b in zip(boff[:-1].tolist(), boff[1:].tolist())]
+    return [str(mv[a:b], "utf-8") for a, b in zip(boff[:-1].tolist(), boff[1:].tolist())]

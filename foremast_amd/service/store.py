@@ -34,7 +34,7 @@ from datetime import datetime, timezone
 from ..api import status as ST
 from ..api.jobs import parse_rfc3339, rfc3339
 from ..api.jsonmodel import to_json
-from ..api.models import Document, HPALog
+from ..api.models import Document, HPALog, HPALogBatch
 
 
 def _ts(doc: Document) -> float:
@@ -138,9 +138,14 @@ class JobStore(ABC):
         leased instead (no write)."""
         self.update_uniform(ids, {"status": ST.PREPROCESS_COMPLETED}, now=now, handles=handles)
 
-    def add_hpalogs(self, logs: list[HPALog]) -> None:
+    def add_hpalogs(self, logs: list) -> None:
+        """``logs``: HPALog entries and/or HPALogBatch batches."""
         for lg in logs:
-            self.add_hpalog(lg)
+            if isinstance(lg, HPALogBatch):
+                for x in lg.logs():
+                    self.add_hpalog(x)
+            else:
+                self.add_hpalog(lg)
 
     def claim(self, worker: str, limit: int, max_stuck_s: float, now: float | None = None,
               owner=None, shard: tuple[int, int] | None = None) -> list[Document]:
@@ -417,22 +422,35 @@ class MemoryStore(JobStore):
     def add_hpalog(self, log: HPALog) -> None:
         self.add_hpalogs([log])
 
-    def add_hpalogs(self, logs: list[HPALog]) -> None:
+    def add_hpalogs(self, logs: list) -> None:
         """Logs are indexed by job and bounded: the newest ``hpalog_keep`` per
         job are kept (the HPA alert reads the last 4-6, HpaController.go:109-131;
-        GET /v1/healthcheck/id the last 10, main.go:227-255)."""
+        GET /v1/healthcheck/id the last 10, main.go:227-255).  Kept as JSON
+        bodies (an HPALogBatch is formatted natively); reads parse them."""
+        rows = _log_rows(logs)
         with self._lock:
-            for lg in logs:
-                q = self._logs.get(lg.job_id)
+            for jid, ts, body in rows:
+                q = self._logs.get(jid)
                 if q is None:
-                    q = self._logs[lg.job_id] = collections.deque(maxlen=self.hpalog_keep)
-                q.append(lg)
+                    q = self._logs[jid] = collections.deque(maxlen=self.hpalog_keep)
+                q.append((ts, body))
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
         with self._lock:
             rows = list(self._logs.get(job_id, ()))
-        rows.sort(key=lambda l: l.timestamp, reverse=True)
-        return [HPALog.from_dict(r.to_dict()) for r in rows[:size]]
+        rows.sort(key=lambda r: r[0], reverse=True)
+        return [HPALog.from_dict(json.loads(b)) for _, b in rows[:size]]
+
+
+def _log_rows(logs: list) -> list[tuple[str, float, str]]:
+    """(job id, timestamp, JSON body) of HPALog entries and HPALogBatch batches."""
+    out: list = []
+    for lg in logs:
+        if isinstance(lg, HPALogBatch):
+            out.extend(zip(lg.job_ids, [lg.timestamp] * len(lg), lg.bodies()))
+        else:
+            out.append((lg.job_id, lg.timestamp, json.dumps(lg.to_dict())))
+    return out
 
 
 OWNER_MOD = 720720          # lcm(1..16): owner_key % world == service_owner(...) for every world | OWNER_MOD
@@ -885,14 +903,14 @@ class SQLiteStore(JobStore):
     def add_hpalog(self, log: HPALog) -> None:
         self.add_hpalogs([log])
 
-    def add_hpalogs(self, logs: list[HPALog]) -> None:
-        if not logs:
+    def add_hpalogs(self, logs: list) -> None:
+        rows = _log_rows(logs)
+        if not rows:
             return
         with self._txn() as c:
-            c.executemany("insert into hpalogs values (?,?,?)",
-                          [(lg.job_id, lg.timestamp, json.dumps(lg.to_dict())) for lg in logs])
-            self._log_writes += len(logs)
-            newest = max(lg.timestamp for lg in logs)
+            c.executemany("insert into hpalogs values (?,?,?)", rows)
+            self._log_writes += len(rows)
+            newest = max(r[1] for r in rows)
             # bounded retention (the HPA alert reads the last 4-6 entries,
             # GET /v1/healthcheck/id the last 10): drop entries older than
             # the retention window, at most once a minute
@@ -1046,13 +1064,20 @@ class ElasticsearchStore(JobStore):
                 raise RuntimeError(f"ES _bulk: {len(bad)} failed actions, first {bad[:1]}")
         return out
 
-    def add_hpalogs(self, logs: list[HPALog]) -> None:
-        """One ``_bulk`` request of index actions."""
-        lines = []
-        for lg in logs:
-            lines += [{"index": {"_index": "hpalogs", "_type": "hpalog"}}, lg.to_dict()]
-        if lines:
-            self._bulk(lines)
+    def add_hpalogs(self, logs: list) -> None:
+        """One ``_bulk`` request of index actions (bodies pre-rendered)."""
+        rows = _log_rows(logs)
+        if not rows:
+            return
+        act = json.dumps({"index": {"_index": "hpalogs", "_type": "hpalog"}})
+        body = "".join(f"{act}\n{b}\n" for _, _, b in rows)
+        r = self.http.post(f"{self.url}/_bulk", content=body.encode(), headers={"Content-Type": "application/x-ndjson"})
+        r.raise_for_status()
+        out = r.json()
+        if out.get("errors"):
+            bad = [v for it in out.get("items", []) for v in it.values() if v.get("status", 200) >= 300]
+            if bad:
+                raise RuntimeError(f"ES _bulk: {len(bad)} failed actions, first {bad[:1]}")
 
     def update_many(self, updates: list[tuple[str, dict]], now: float | None = None, worker: str | None = None) -> None:
         """One ``_bulk`` request of partial-document ``update`` actions."""

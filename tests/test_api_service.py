@@ -202,3 +202,65 @@ def test_hpalog_to_dict_matches_reflective_encoder(job_id, mod, created):
     assert list(lg.to_dict()) == list(to_json(lg))
     assert HPALog.from_dict(lg.to_dict()).to_dict() == lg.to_dict()
     assert HPALog().to_dict() == to_json(HPALog())
+
+
+def test_hpalog_batch_native_bodies_parse_to_to_dict():
+    """HPALogBatch bodies (csrc/runtime/hpalog_json.cpp) are the JSON of each
+    entry's HPALog.to_dict: escaping, float repr (integral values, tiny and
+    huge magnitudes) and the optional created_at."""
+    import json as _json
+    import numpy as np
+    from foremast_amd.api.models import HPALogBatch
+    from foremast_amd.engine import native_rt
+    ids = ["a-1", 'q"uo\\te', "tab\tnl\n", "ünï-çødé", "x" * 300]
+    n, m = len(ids), 3
+    rng = np.random.default_rng(0)
+    cur = rng.normal(size=(n, m)) * 10.0 ** rng.integers(-12, 12, size=(n, m))
+    cur[0, 0], cur[1, 1], cur[2, 2] = 1.0, 0.0, 1e16
+    for created in ("2026-10-17T00:00:00Z", ""):
+        b = HPALogBatch(ids, 1760000000.0, created, np.arange(n) - 2, np.array([0, 1, 2, 1, 0]),
+                        ["hold", 'up "x"', "down\\"], ["cpu", "laténcy", "e5"], cur, cur * 2, -cur)
+        bodies = b.bodies()
+        assert len(bodies) == n
+        for i, body in enumerate(bodies):
+            assert _json.loads(body) == b.log(i).to_dict()
+        if native_rt.available():
+            assert bodies == [_json.dumps(lg.to_dict(), ensure_ascii=False) for lg in b.logs()]
+
+
+def test_stores_persist_hpalog_batches_and_entries():
+    import numpy as np
+    from foremast_amd.api.models import HPALog, HPALogBatch, HPALogBody, HPALogDetail
+    from foremast_amd.service.store import MemoryStore, SQLiteStore
+    import tempfile, os
+    d = tempfile.mkdtemp()
+    for st in (MemoryStore(), SQLiteStore(os.path.join(d, "j.db"))):
+        b = HPALogBatch(["j1", "j2"], 100.0, "c", np.array([1, 0]), np.array([1, 0]), ["hold", "up"], ["cpu"],
+                        np.array([[1.5], [2.0]]), np.array([[3.0], [4.0]]), np.array([[0.5], [0.0]]))
+        st.add_hpalogs([b, HPALog(job_id="j1", timestamp=160.0, log=HPALogBody(2, "x", [HPALogDetail("cpu", 9.0)]))])
+        got = st.hpalogs("j1")
+        assert [g.timestamp for g in got] == [160.0, 100.0]
+        assert got[1].log.hpa_score == 1 and got[1].log.reason == "up"
+        assert got[1].log.details[0].current == 1.5 and got[1].log.details[0].upper == 3.0
+        assert st.hpalogs("j2")[0].log.details[0].lower == 0.0
+
+
+def test_hpalog_batch_bodies_threaded_match_json_dumps():
+    """A batch large enough for the threaded native formatter: every body is
+    json.dumps(to_dict) byte for byte (entries keep their order and offsets)."""
+    import json as _json
+    import numpy as np
+    from foremast_amd.api.models import HPALogBatch
+    from foremast_amd.engine import native_rt
+    n, m = 5000, 4
+    rng = np.random.default_rng(1)
+    cur = rng.normal(size=(n, m)) * 10.0 ** rng.integers(-8, 20, size=(n, m))
+    ids = [f"job-{i}-{'é' if i % 7 == 0 else ''}" for i in range(n)]
+    b = HPALogBatch(ids, 1.5e9 + 0.25, "c", rng.integers(-3, 3, n), rng.integers(0, 3, n), ["a", "b", "c"],
+                    ["m0", "m1", "m2", "m3"], cur, -cur, cur * 0.5)
+    bodies = b.bodies()
+    want = [_json.dumps(lg.to_dict(), ensure_ascii=False) for lg in b.logs()]
+    if native_rt.available():
+        assert bodies == want
+    else:
+        assert [_json.loads(x) for x in bodies] == [_json.loads(x) for x in want]
