@@ -565,20 +565,25 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
   // the last step (the first k-step of whatever follows)
   auto segment = [&](auto NK, f32x16 (&acc)[RT], __amdgpu_buffer_rsrc_t Ww, int KS, auto ks_of, auto b_of,
                      __amdgpu_buffer_rsrc_t Wn, int KSn, int ksn, auto cell_at) {
+    // the B fragment (h image in LDS, stable for the whole segment) is read
+    // one k-step ahead too, so its LDS latency hides behind the MFMAs
+    uint4 bcur = b_of(0);
 #pragma unroll
     for (int i = 0; i < decltype(NK)::value; ++i) {
       __builtin_amdgcn_sched_barrier(0);             // k-steps stay in order: no hoisted loads
       Frag an[RT];
       if (i + 1 < decltype(NK)::value) loadA(an, Ww, KS, ks_of(i + 1));
       else loadA(an, Wn, KSn, ksn);
+      const uint4 bnext = i + 1 < decltype(NK)::value ? b_of(i + 1) : bcur;
       Frag bf;
-      bf.u = b_of(i);
+      bf.u = bcur;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
         acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rt].v, bf.v, acc[rt], 0, 0, 0);
       cell_at(i);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) a[rt] = an[rt];
+      bcur = bnext;
     }
   };
   auto zero = [](f32x16 (&acc)[RT]) {

@@ -28,7 +28,8 @@ def main() -> None:
                     "select kernel_name, dispatch_id, counter_name, value, duration from counters_collection"):
                 if want and want not in name:
                     continue
-                k = (name.split("(")[0][:60], f"{db}:{disp}")
+                nm = name.replace("(anonymous namespace)::", "")
+                k = (nm.split("(")[0][:60], f"{db}:{disp}")
                 per[k][cnt] += val
                 dur[k] = d
     agg = defaultdict(lambda: defaultdict(list))
