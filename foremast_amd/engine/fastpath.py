@@ -891,15 +891,16 @@ class FastPath:
         return idx, val, ctr
 
     # ------------------------------------------------------------------ forecasting models
-    def _cache_keys(self, works: list[FastWork], p0: JobPlan, algo: str) -> np.ndarray:
-        """Fitted-model cache keys of a group's rows ([S * M] object array),
+    def _cache_keys(self, works: list[FastWork], p0: JobPlan, algo: str) -> tuple[np.ndarray, list]:
+        """Fitted-model cache keys of a group's rows ([S * M] object array and
+        the same as one list object),
         a fancy-index of the previous job list's when the list only lost or
         reordered jobs (fleet churn)."""
         ids = tuple(map(id, works))
         M = len(p0.aliases)
         memo = self._keys.get((p0.group, algo))
         if memo is not None and memo[0] == ids:
-            return memo[2]
+            return memo[2], memo[3]
         ix = None
         if memo is not None:
             pos = memo[1]
@@ -911,8 +912,15 @@ class FastPath:
             kv = np.empty(len(works) * M, object)
             kv[:] = [(f"{w.plan.namespace}/{w.doc.app_name}", a, b, algo) for w in works
                      for a, b in zip(p0.aliases, p0.base_metrics)]
-        self._keys[(p0.group, algo)] = (ids, self._positions(ids), kv)
-        return kv
+        # a churned list is root[ix] of the previous one: the model cache then
+        # indexes its previous lookups instead of hashing every key again
+        if ix is not None:
+            rix = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)       # job positions -> row positions
+            full = TemplateList.subset(memo[3], kv.tolist(), rix)
+        else:
+            full = TemplateList(kv.tolist())
+        self._keys[(p0.group, algo)] = (ids, self._positions(ids), kv, full)
+        return kv, full
 
     def _model_arrays(self, ga: GroupArrays, works: list[FastWork], store: ResidentHistory) -> "ModelArrays":
         """Per-algorithm row subsets of a group with everything that does not
@@ -954,7 +962,10 @@ class FastPath:
             # sliding window: kept from the arrays' previous ModelArrays
             keys = next((s.keys for s in md.subs if s.algo == algo), None) if md is not None else None
             if keys is None and algo in zoo.ES_KINDS:
-                keys = self._cache_keys(works, p0, algo)[rows].tolist()
+                kv, full = self._cache_keys(works, p0, algo)
+                # every row of the group: the memo's list object, stable while the
+                # job list is (the model cache skips its per-row lookups for it)
+                keys = full if idx is None else kv[rows].tolist()
             hr = hor[rows]
             subs.append(ModelSub(algo, ms, idx, i32(rowmap[rows]), i32(shift[rows]), i32(lim[rows]), T,
                                  zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev), keys, t_last[rows],

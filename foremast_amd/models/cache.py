@@ -181,10 +181,16 @@ class ModelCache:
         fc = torch.empty((R, H), dtype=torch.float32, device=dev)
         sig = torch.empty((R,), dtype=torch.float32, device=dev)
         memo = self._memo
+        root = getattr(keys, "root", None)
         if memo is not None and memo[0] is keys and memo[1] == self._gen:
             # same batch object and no key -> slot change since: a steady-state
             # shard re-scoring its series skips the per-row lookups
             g = memo[2].copy()
+        elif memo is not None and root is not None and memo[0] is root and memo[1] == self._gen:
+            # the batch is root[ix] of the last one (jobs left the fleet):
+            # index the previous lookups
+            g = memo[2][keys.ix]
+            self._memo = (keys, self._gen, g.copy())
         else:
             g = np.fromiter((-1 if v is None else v for v in map(self.entries.get, keys)), np.int64, R)
             if len(set(keys)) != R:                # a key seen twice in one batch is fitted, not advanced twice
