@@ -14,13 +14,17 @@ from ._lib import LIB, check, ptr, require_native, stream_of
 SUPPORTED_H = (32, 64, 128)              # register-resident single-layer kernel (lstm.hip)
 STACK_H = (32, 64, 128, 256)             # streamed-weight 1-2 layer kernel (lstm_stack.hip)
 STACK_TILING = {256: (4, 2), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row tiles / wave, column tiles)
+# two layers at H = 256: the layer-pipelined kernel (cells beside the next
+# layer's MFMAs; 6.8 vs 8.2 ms at 10k x 240, 37.0 vs 42.0 ms at 80k x 240,
+# profiles/lstm_stack_ab_r3b.jsonl); weights packed with the same RT = 4
+STACK_TILING_2L = {256: (4, 201)}
 STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1),            # instantiated alternatives (lstm_stack.hip);
                           (4, 102), (4, 101), (2, 102),              # nct 10x: LDS-DMA weight ring, x tiles;
                           (4, 201), (2, 201),                        # nct 201: layer-pipelined, 2 layers, 1 tile;
                           (4, 202), (2, 202))}                       # nct 202: same, flat step + 4-deep A ring
 
 
-def stack_tiling(H: int) -> tuple[int, int]:
+def stack_tiling(H: int, layers: int = 1) -> tuple[int, int]:
     """(row tiles per wave, column tiles per workgroup) of the stacked kernel
     at hidden size H; ``FM_LSTM_STACK_TILING=RT:NCT`` overrides it at H = 256
     (A/B of fill vs streamed-weight reuse; the packed weights depend on RT,
@@ -35,7 +39,11 @@ def stack_tiling(H: int) -> tuple[int, int]:
         rt, nct = (int(v) for v in env.rstrip("gpf").split(":"))
         nct += {"g": 100, "p": 200, "f": 201}.get(kind, 0)
         check((rt, nct) in STACK_TILING_ALT[H], f"FM_LSTM_STACK_TILING {env} not instantiated for H={H}")
+        if nct > 200 and layers != 2:
+            return rt, 2 if rt == 4 else 1                  # the pipelined kernels are two-layer only
         return rt, nct
+    if layers == 2 and H in STACK_TILING_2L:
+        return STACK_TILING_2L[H]
     return STACK_TILING[H]
 
 
@@ -136,7 +144,7 @@ def lstm_stack_forward(xa: torch.Tensor, packed: list[torch.Tensor], H: int):
     cT = torch.empty((B, H), dtype=torch.float32, device=d)
     w0 = packed[0].to(d)
     w1 = packed[1].to(d) if len(packed) > 1 else None
-    rt, nct = stack_tiling(H)
+    rt, nct = stack_tiling(H, len(packed))
     LIB.call("fm_lstm_stack", ptr(xa), B, L, H, len(packed), ptr(w0), ptr(w1), ptr(hT), ptr(cT), rt, nct,
              stream_of(xa))
     return hT, cT

@@ -350,6 +350,16 @@ def _w_slow_rank(rank, world, db, stall_s, run_s):
     brain = Brain(SQLiteStore(db), cfg, sources=SourceRouter.synthetic_only(), clock=lambda: t["now"],
                   worker_id=f"rank{rank}", exporter=exp)
     mb = Mailbox.for_world("test/")
+    # no collective may run inside a brain cycle: any call raises here
+    import torch.distributed as _dist
+
+    def _forbidden(*a, **k):
+        raise AssertionError("collective called inside a brain cycle")
+    for name in ("all_reduce", "all_gather", "all_gather_object", "all_gather_into_tensor", "broadcast",
+                 "broadcast_object_list", "barrier", "reduce_scatter", "reduce_scatter_tensor", "all_to_all",
+                 "all_to_all_single", "gather", "scatter", "reduce"):
+        if hasattr(_dist, name):
+            setattr(_dist, name, _forbidden)
     cycles = 0
     t0 = time.monotonic()
     if rank == 1:
@@ -375,15 +385,15 @@ def _w_slow_rank(rank, world, db, stall_s, run_s):
 
 
 def test_slow_rank_never_stalls_peers(tmp_path, monkeypatch):
-    """VERDICT r2 #3 / ADVICE r2: no collective runs in a brain cycle.  With
-    a 2 s collective timeout, rank 1 spends 5 s in one cycle and then stops
-    on its own: rank 0 keeps cycling the whole time (never blocks, never
-    aborts) and still exports rank 1's last published gauges, now stale."""
+    """VERDICT r2 #3 / ADVICE r2: no collective runs in a brain cycle (every
+    torch.distributed collective raises inside the workers).  Rank 1 spends
+    5 s in one cycle and then stops on its own: rank 0 keeps cycling the
+    whole time (never blocks, never aborts) and still exports rank 1's last
+    published gauges, now stale."""
     from foremast_amd.api import crd
     from foremast_amd.controller.analyst import AnalystClient
     from foremast_amd.service.app import create_app
     from foremast_amd.service.store import SQLiteStore
-    monkeypatch.setenv("FOREMAST_COLLECTIVE_TIMEOUT_S", "2")
     db = str(tmp_path / "jobs.db")
     client = AnalystClient.for_app(create_app(SQLiteStore(db)), clock=lambda: 1_760_000_000.0)
     m = crd.Metrics("prometheus", "http://prom/api/v1/", [crd.Monitoring("cpu_usage", "gauge", "cpu")])
