@@ -445,7 +445,7 @@ template <bool GATED, bool LAP1, bool NOSTORE>
 __device__ __forceinline__ void hw2_run(f2v& l, f2v& tr, const f2v al, const f2v be, const f2v ga,
                                         const float* __restrict__ xr, float isc, float s1, int t, int T, int t_act,
                                         int m, h8v* __restrict__ sv8, int64_t NT, int64_t tid, int& ph, f2v& acc,
-                                        double& ea, double& eb, int& n, int& chunk) {
+                                        double& ea, double& eb, int& n, int& chunk, bool xal) {
   // Closed forms of the additive recursion in the one-step error e = x - pred:
   //   l' = lt + a e,  t' = t + a b e,  s' = s + g (1 - a) e   (lt = l + t)
   // (algebraically the textbook updates; 3 packed adds + 4 packed FMAs per
@@ -507,8 +507,15 @@ __device__ __forceinline__ void hw2_run(f2v& l, f2v& tr, const f2v al, const f2v
       for (int u = 0; u < 8; ++u) { sa[u] = (float)a[u]; sb[u] = (float)c[u]; }
     }
     float xv[8];
+    if (xal && (t & 3) == 0) {        // wave-uniform; xal: x and its row stride are 16-B aligned
+      const float4 x0 = *reinterpret_cast<const float4*>(xr + t);
+      const float4 x1 = *reinterpret_cast<const float4*>(xr + t + 4);
+      xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w;
+      xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
+    } else {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xv[u] = xr[t + u];
+      for (int u = 0; u < 8; ++u) xv[u] = xr[t + u];
+    }
     ph += 8;
     if (ph >= m) ph -= m;
 #pragma unroll
@@ -532,7 +539,7 @@ __global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ 
                                                       h8v* __restrict__ season, float* __restrict__ sse,
                                                       float* __restrict__ state, int* __restrict__ nobs,
                                                       int t_store_end, float* __restrict__ sscale,
-                                                      int* __restrict__ nfin) {
+                                                      int* __restrict__ nfin, int xal) {
   const int GP = (G + 1) >> 1;
   const int64_t NT = R * GP;
   const int64_t tid_raw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -576,11 +583,11 @@ __global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ 
   if (lo == hi && lo + m <= T) {
     const int ts = max(lo + m, min(t_store_end, T));
     hw2_run<false, true, false>(l, tr, al, be, gm, xr, isc, s1, lo, lo + m, lo, m, season, NT, tid, ph, acc, ea, eb, n,
-                                chunk);
+                                chunk, xal != 0);
     hw2_run<false, false, false>(l, tr, al, be, gm, xr, isc, s1, lo + m, ts, lo, m, season, NT, tid, ph, acc, ea, eb,
-                                 n, chunk);
+                                 n, chunk, xal != 0);
     hw2_run<false, false, true>(l, tr, al, be, gm, xr, isc, s1, ts, T, lo, m, season, NT, tid, ph, acc, ea, eb, n,
-                                chunk);
+                                chunk, xal != 0);
   } else {
     // ragged rows in this wave: materialise each row's initial seasons, then
     // run with per-lane start gating
@@ -596,7 +603,7 @@ __global__ __launch_bounds__(256) void hw2_fit_kernel(const float* __restrict__ 
       }
     }
     hw2_run<true, false, false>(l, tr, al, be, gm, xr, isc, s1, lo, T, t0, m, season, NT, tid, ph, acc, ea, eb, n,
-                                chunk);
+                                chunk, xal != 0);
   }
   ea += acc.x;
   eb += acc.y;
@@ -763,10 +770,12 @@ FM_API int fm_es_fit(const float* x, int64_t ld, int T, int64_t R, const float* 
   const int t_store_end = keep_season || kind < 2 || H >= m ? T : T - m + H;
   const dim3 gf((unsigned)((P + 255) / 256)), gr((unsigned)((R + 255) / 256));
   if (season_half) {
-    // packed two-candidates-per-thread additive fit (hw2_fit_kernel)
+    // packed two-candidates-per-thread additive fit (hw2_fit_kernel; two
+    // pairs per thread measured slower: profiles/hw_pairs_ab_r3.jsonl)
     const int64_t NT = R * ((G + 1) / 2);
+    const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
     hipLaunchKernelGGL(hw2_fit_kernel, dim3((unsigned)((NT + 255) / 256)), dim3(256), 0, stream, x, ld, T, R, cand, G,
-                       m, (h8v*)season, sse, state, nobs, t_store_end, sscale, nfin);
+                       m, (h8v*)season, sse, state, nobs, t_store_end, sscale, nfin, xal);
     FM_LAUNCH_CHECK();
     hipLaunchKernelGGL(hw2_forecast_kernel, gr, dim3(256), 0, stream, sse, state, nobs, (const _Float16*)season,
                        sscale, R, G, m, H, fc, sigma, best);
