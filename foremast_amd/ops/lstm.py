@@ -19,25 +19,21 @@ STACK_TILING = {256: (4, 2), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row 
 # profiles/lstm_stack_ab_r3b.jsonl); weights packed with the same RT = 4
 STACK_TILING_2L = {256: (4, 201)}
 STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1),            # instantiated alternatives (lstm_stack.hip);
-                          (4, 102), (4, 101), (2, 102),              # nct 10x: LDS-DMA weight ring, x tiles;
-                          (4, 201), (2, 201),                        # nct 201: layer-pipelined, 2 layers, 1 tile;
-                          (4, 202), (2, 202))}                       # nct 202: same, flat step + 4-deep A ring
+                          (4, 201), (2, 201))}                       # nct 201: layer-pipelined, 2 layers, 1 tile
 
 
 def stack_tiling(H: int, layers: int = 1) -> tuple[int, int]:
     """(row tiles per wave, column tiles per workgroup) of the stacked kernel
     at hidden size H; ``FM_LSTM_STACK_TILING=RT:NCT`` overrides it at H = 256
     (A/B of fill vs streamed-weight reuse; the packed weights depend on RT,
-    so pack and run under the same setting).  A ``g`` suffix (``4:1g``)
-    selects the LDS-DMA weight-ring kernel at that tiling (nct + 100), ``p``
-    (``4:1p``) the layer-pipelined two-layer kernel (nct 201), ``f``
-    (``4:1f``) its flat-step variant with a 4-deep fragment ring (nct 202)."""
+    so pack and run under the same setting).  A ``p`` suffix (``4:1p``)
+    selects the layer-pipelined two-layer kernel (nct 201)."""
     import os
     env = os.environ.get("FM_LSTM_STACK_TILING")
     if env and H in STACK_TILING_ALT:
-        kind = env[-1] if env[-1] in "gpf" else ""
-        rt, nct = (int(v) for v in env.rstrip("gpf").split(":"))
-        nct += {"g": 100, "p": 200, "f": 201}.get(kind, 0)
+        kind = env[-1] if env[-1] == "p" else ""
+        rt, nct = (int(v) for v in env.rstrip("p").split(":"))
+        nct += 200 if kind else 0
         check((rt, nct) in STACK_TILING_ALT[H], f"FM_LSTM_STACK_TILING {env} not instantiated for H={H}")
         if nct > 200 and layers != 2:
             return rt, 2 if rt == 4 else 1                  # the pipelined kernels are two-layer only

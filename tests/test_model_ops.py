@@ -490,7 +490,7 @@ def test_gpu_lstm_stack_matches_fp32_lstm(cuda, H, layers, I):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tiling", ["4:1", "2:1", "4:2", "2:2", "4:2g", "4:1g", "2:2g", "4:1p", "2:1p", "4:1f", "2:1f"])
+@pytest.mark.parametrize("tiling", ["4:1", "2:1", "4:2", "2:2", "4:1p", "2:1p"])
 def test_gpu_lstm_stack_tilings_agree(cuda, tiling, monkeypatch):
     """Every instantiated H = 256 tiling (row tiles per wave x column tiles)
     computes the same recurrence as the bf16-emulating reference."""

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--layers", type=int, default=2)
-    ap.add_argument("--tilings", default="4:2,4:1,2:2,4:1p,2:1p,4:1f,2:1f")
+    ap.add_argument("--tilings", default="4:2,4:1,2:2,4:1p,2:1p")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
