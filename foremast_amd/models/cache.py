@@ -111,6 +111,7 @@ class ModelCache:
         self.misses = 0
         self._gen = 0            # bumped on every key -> slot change
         self._memo = None        # (keys list object, gen, resolved slots); keys lists are never mutated
+        self._root_g = None      # (root keys list, gen, slots per root position; -2 = not looked up)
 
     def __len__(self) -> int:
         return len(self.entries)
@@ -182,14 +183,16 @@ class ModelCache:
         sig = torch.empty((R,), dtype=torch.float32, device=dev)
         memo = self._memo
         root = getattr(keys, "root", None)
+        rg = self._root_g
         if memo is not None and memo[0] is keys and memo[1] == self._gen:
             # same batch object and no key -> slot change since: a steady-state
             # shard re-scoring its series skips the per-row lookups
             g = memo[2].copy()
-        elif memo is not None and root is not None and memo[0] is root and memo[1] == self._gen:
-            # the batch is root[ix] of the last one (jobs left the fleet):
-            # index the previous lookups
-            g = memo[2][keys.ix]
+        elif root is not None and rg is not None and rg[0] is root and rg[1] == self._gen and \
+                (rg[2][keys.ix] != -2).all():
+            # the batch is root[ix] of an earlier one (jobs left the fleet):
+            # index the lookups kept per root position
+            g = rg[2][keys.ix]
             self._memo = (keys, self._gen, g.copy())
         else:
             g = np.fromiter((-1 if v is None else v for v in map(self.entries.get, keys)), np.int64, R)
@@ -200,6 +203,13 @@ class ModelCache:
                         g[i] = -1
                     seen.add(key)
             self._memo = (keys, self._gen, g.copy())
+        # lookups per root position (-2: not looked up), for later subsets
+        if root is None:
+            self._root_g = (keys, self._gen, g.copy())
+        else:
+            if rg is None or rg[0] is not root or rg[1] != self._gen:
+                rg = self._root_g = (root, self._gen, np.full(len(root), -2, np.int64))
+            rg[2][keys.ix] = g
         sid = np.where(g >= 0, g >> _SLOT_BITS, -1)
         slot = g & ((1 << _SLOT_BITS) - 1)
         usable = np.zeros(R, bool)

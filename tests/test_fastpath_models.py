@@ -202,3 +202,41 @@ def test_gpu_gather_cols_matches_reference():
         got = out[:, 3:3 + ncols].cpu()
         torch.testing.assert_close(got, ref, equal_nan=True, rtol=0, atol=0)
         assert (out[:, :3] == 7).all() and (out[:, 3 + ncols:] == 7).all()
+
+
+def test_model_cache_subset_key_lists_match_fresh_lookups():
+    """Fleet churn hands the model cache key lists that are root[ix] of an
+    earlier list (TemplateList); two successive removals resolve the same
+    cache slots -- hence the same forecasts -- as plain lists of the same keys."""
+    import torch
+    from foremast_amd.engine.sources import TemplateList
+    from foremast_amd.models.cache import ModelCache
+    rng = np.random.default_rng(0)
+    R, T, H, step = 12, 400, 5, 60.0
+    t = np.arange(T + 3)
+    hist = (10 + np.sin(2 * np.pi * t / 24)[None, :] + 0.1 * rng.normal(size=(R, T + 3))).astype(np.float32)
+    keys = [(f"ns/app{i}", "cpu", "cpu", "exponential_smoothing") for i in range(R)]
+
+    def run(cache, key_list, rows, k):
+        h = torch.from_numpy(np.ascontiguousarray(hist[rows, k:k + T]))
+        tl = np.full(len(rows), 1e9 + step * (T + k))
+        return cache.es_forecast(key_list, tl, step, 1e9, h, T, 1, H, lambda sub: 24)
+
+    a, b = ModelCache(), ModelCache()
+    root = TemplateList(keys)
+    fa, _ = run(a, root, np.arange(R), 0)
+    fb, _ = run(b, list(keys), np.arange(R), 0)
+    torch.testing.assert_close(fa, fb)
+    ix1 = np.array([0, 2, 3, 5, 6, 7, 9, 10, 11])
+    s1 = TemplateList.subset(root, [keys[i] for i in ix1], np.arange(len(ix1)))
+    s1.ix = ix1
+    fa, _ = run(a, s1, ix1, 1)
+    fb, _ = run(b, [keys[i] for i in ix1], ix1, 1)
+    torch.testing.assert_close(fa, fb)
+    sel = np.array([0, 1, 3, 4, 6, 8])
+    s2 = TemplateList.subset(s1, [keys[i] for i in ix1[sel]], sel)
+    assert s2.root is root and list(s2.ix) == list(ix1[sel])
+    fa, _ = run(a, s2, ix1[sel], 2)
+    fb, _ = run(b, [keys[i] for i in ix1[sel]], ix1[sel], 2)
+    torch.testing.assert_close(fa, fb)
+    assert a.hits == b.hits and a.misses == b.misses
