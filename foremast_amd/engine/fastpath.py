@@ -946,7 +946,15 @@ class FastPath:
         hor = np.maximum(1, h).astype(np.int64)
         valid = ((store.nfin[rowmap] >= max(cfg.min_historical_points, 1)).astype(np.int32)
                  | (np.isfinite(ga.cur).any(1).astype(np.int32) << 1))
-        i32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=dev)
+        # every per-row int array of this call goes up in ONE pinned,
+        # non-blocking copy (a pageable torch.as_tensor(..., device) per array
+        # is a synchronous copy ordered behind the queued GPU work)
+        parts: list[np.ndarray] = []
+
+        def i64(a) -> int:
+            parts.append(np.ascontiguousarray(a, np.int64).reshape(-1))
+            return len(parts) - 1
+        pending = []
         subs = []
         by_algo: dict[str, list[int]] = {}
         for m, a in enumerate(p0.algos):
@@ -967,14 +975,22 @@ class FastPath:
                 # job list is (the model cache skips its per-row lookups for it)
                 keys = full if idx is None else kv[rows].tolist()
             hr = hor[rows]
-            subs.append(ModelSub(algo, ms, idx, i32(rowmap[rows]), i32(shift[rows]), i32(lim[rows]), T,
-                                 zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev), keys, t_last[rows],
-                                 torch.as_tensor(valid[rows], device=dev),
-                                 torch.as_tensor(hr, device=dev), max(1, int(hr.max()) if hr.size else 1), len(ms)))
+            pending.append((algo, ms, idx, (i64(rowmap[rows]), i64(shift[rows]), i64(lim[rows]), i64(valid[rows]),
+                                            i64(hr)), hr.shape, keys, t_last[rows],
+                            max(1, int(hr.max()) if hr.size else 1)))
         fin = np.isfinite(ga.cur)
         n = ga.cur.shape[1]
         lastk = np.where(fin.any(1), n - 1 - np.argmax(fin[:, ::-1], axis=1), n - 1)
-        md = ga.models = ModelArrays(stamp, subs, torch.as_tensor(lastk.astype(np.int64), device=dev))
+        k_last = i64(lastk)
+        off = np.concatenate([[0], np.cumsum([len(a) for a in parts])])
+        host = torch.from_numpy(np.concatenate(parts))
+        flat = host.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else host
+        view = lambda k: flat[off[k]:off[k + 1]]                                     # noqa: E731
+        for algo, ms, idx, (kr, ks, kl, kv, kh), hshape, keys, tl, hmax in pending:
+            subs.append(ModelSub(algo, ms, idx, view(kr).to(torch.int32), view(ks).to(torch.int32),
+                                 view(kl).to(torch.int32), T, zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev),
+                                 keys, tl, view(kv).to(torch.int32), view(kh).reshape(hshape), hmax, len(ms)))
+        md = ga.models = ModelArrays(stamp, subs, view(k_last))
         return md
 
     def _score_models(self, works: list[FastWork], now: float, ga: GroupArrays, store: ResidentHistory) -> dict:
