@@ -332,6 +332,7 @@ class FastPath:
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
         self._gstat: dict = {}    # group key -> (job ids, positions, per-job static columns)
+        self._gsigs: dict = {}    # interned plan-group signatures
         self._pos_cache = None
 
     # ------------------------------------------------------------------ planning
@@ -373,6 +374,7 @@ class FastPath:
         gsig = (tuple(aliases), hpa, sliding,
                 None if tmpl is None else (tuple(tmpl.priority), tuple(tmpl.is_increase), tuple(tmpl.is_absolute)),
                 algos)
+        gsig = self._gsigs.setdefault(gsig, gsig)        # interned: one group object per signature
         return JobPlan(fp, tuple(aliases), [cur.get(a, "") for a in aliases], [cs.get(a, "prometheus") for a in aliases],
                        [base.get(a, "") for a in aliases], [bs.get(a, "prometheus") for a in aliases], hu,
                        [hs.get(a, "prometheus") for a in aliases], sliding, keys, bms, ns or doc.namespace,
@@ -448,8 +450,15 @@ class FastPath:
         # instead of one per job and metric
         slide: dict[tuple, list[FastWork]] = {}
         rest = []
-        for fw in todo:
-            (slide.setdefault(fw.plan.group, []) if fw.plan.sliding else rest).append(fw)
+        grp = [fw.plan.group for fw in todo]
+        if grp and grp.count(grp[0]) == len(grp):        # one (interned) group: the usual fleet
+            if grp[0][2]:
+                slide[grp[0]] = todo
+            else:
+                rest = todo
+        else:
+            for fw in todo:
+                (slide.setdefault(fw.plan.group, []) if fw.plan.sliding else rest).append(fw)
         for grp in slide.values():
             self._fetch_sliding(grp, now)
         if pool is None:
