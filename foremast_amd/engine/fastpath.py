@@ -115,7 +115,7 @@ USED_STAMP_EVERY = 16           # cycles between row last-use stamps (must stay 
 class GroupArrays:
     """Host/device arrays of one group, reused while the group's job list
     and data are unchanged (the steady state of a re-examined fleet)."""
-    ident: tuple
+    ident: "JobIds"
     ids: np.ndarray                            # object array of job ids
     cur: np.ndarray
     cur_t: np.ndarray
@@ -244,6 +244,40 @@ def pack_left(flat: np.ndarray, lens: np.ndarray, width: int, dtype=np.float32) 
     return out
 
 
+class JobIds:
+    """Identity of a job list (the ids of its FastWork objects, in order):
+    equality is an array compare, and ``index_in(old)`` finds the positions
+    of this list's jobs in an earlier list (sorted search, no per-job dict)
+    -- how a churned list (jobs left) re-indexes the previous list's memos."""
+
+    __slots__ = ("arr", "_order")
+
+    def __init__(self, works) -> None:
+        self.arr = np.fromiter(map(id, works), np.int64, len(works))
+        self._order = None
+
+    def __len__(self) -> int:
+        return len(self.arr)
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, JobIds) and (other is self or np.array_equal(self.arr, other.arr))
+
+    def __ne__(self, other) -> bool:
+        return not self.__eq__(other)
+
+    __hash__ = None
+
+    def index_in(self, old: "JobIds") -> np.ndarray | None:
+        if not len(self.arr) or not len(old.arr):
+            return None
+        if old._order is None:
+            old._order = np.argsort(old.arr, kind="stable")
+        srt = old.arr[old._order]
+        p = np.minimum(np.searchsorted(srt, self.arr), len(srt) - 1)
+        cand = old._order[p]
+        return cand if np.array_equal(old.arr[cand], self.arr) else None
+
+
 class HpaTable:
     """Device-resident HPA hysteresis state (docs/dynamic_autoscaling.md:117-130)
     of every HPA job this rank scores: one slot per job id."""
@@ -333,7 +367,8 @@ class FastPath:
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
         self._gstat: dict = {}    # group key -> (job ids, positions, per-job static columns)
         self._gsigs: dict = {}    # interned plan-group signatures
-        self._pos_cache = None
+        self._gcount: dict = {}   # plan group -> jobs in self.works
+        self._jid_cache: dict = {}  # id(job list) -> (list, JobIds), cleared every cycle
 
     # ------------------------------------------------------------------ planning
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
@@ -396,6 +431,7 @@ class FastPath:
         steady state of a re-examined fleet) reuses the previous lists."""
         self.cycle += 1
         self._col.clear()
+        self._jid_cache.clear()
         self.sliding.advance(now, now - self.history_s)
         immutable = self._immutable
         last = self._last
@@ -421,6 +457,7 @@ class FastPath:
             for k, d in zip(unknown, batch.docs(unknown)):
                 old = works.pop(d.id, None)
                 if old is not None:              # resubmitted under the same id
+                    self._gcount_add(old.plan.group, -1)
                     self._release([old])
                 p = self._make_plan(d, batch.versions[k])
                 if p is None:
@@ -434,6 +471,7 @@ class FastPath:
                     end_ts = now
                 fw = works[d.id] = FastWork(d, p, rows, end_ts, version=batch.versions[k],
                                             handle=None if handles is None else int(handles[k]))
+                self._gcount_add(p.group, 1)
                 fast.append(fw)
                 todo.append(fw)
         self.todo = todo
@@ -450,10 +488,10 @@ class FastPath:
         # instead of one per job and metric
         slide: dict[tuple, list[FastWork]] = {}
         rest = []
-        grp = [fw.plan.group for fw in todo]
-        if grp and grp.count(grp[0]) == len(grp):        # one (interned) group: the usual fleet
-            if grp[0][2]:
-                slide[grp[0]] = todo
+        if todo and len(self._gcount) == 1:               # every known job in one group: the usual fleet
+            g0 = todo[0].plan.group
+            if g0[2]:
+                slide[g0] = todo
             else:
                 rest = todo
         else:
@@ -521,18 +559,14 @@ class FastPath:
         M, S = len(p0.aliases), len(ws)
         wins = b._windows(ws[0].doc, now)
         st = self.sliding
-        ids = tuple(map(id, ws))
+        ids = self._jid(ws)
         memo = self._tpl.get(p0.group)
         if memo is None or memo[0] != ids:
             # template lists and row map of this job list, reused while it is
             # unchanged (stable list objects let a staged source memoise them);
             # a list that only lost / reordered jobs (fleet churn: a job closed)
             # is a fancy-index of the previous one, not a per-job rebuild
-            ix = None
-            if memo is not None:
-                pos = memo[3]
-                ix = np.fromiter((pos.get(i, -1) for i in ids), np.int64, len(ids))
-                ix = ix if len(ix) and ix.min() >= 0 else None
+            ix = ids.index_in(memo[0]) if memo is not None else None
             if ix is not None:
                 arrs = {k: a[ix] for k, a in memo[4].items()}
                 rows = memo[2][ix]
@@ -556,7 +590,7 @@ class FastPath:
                                 tl.split = (stl, {s0: np.arange(S)})
             else:
                 lists = {k: TemplateList(a.tolist()) for k, a in arrs.items()}
-            memo = self._tpl[p0.group] = (ids, lists, rows, self._positions(ids), arrs)
+            memo = self._tpl[p0.group] = (ids, lists, rows, None, arrs)
         lists, rows = memo[1], memo[2]                                       # rows [S, M]
         cur_p, base_p = [], []
         for m in range(M):
@@ -600,8 +634,7 @@ class FastPath:
             fw.settled = False
             fw.wclass = wclass
             fw.hist = []
-        ids = tuple(map(id, ws))
-        self._col[p0.group] = {"ids": ids, "pos": {i: j for j, i in enumerate(ids)}, "cur": cur, "cur_t": cur_t,
+        self._col[p0.group] = {"ids": ids, "cur": cur, "cur_t": cur_t,
                                "cur_len": cur_len, "base": base if bb else None, "base_len": base_len}
 
     def fetch(self, fw: FastWork, now: float) -> FastWork:
@@ -731,7 +764,7 @@ class FastPath:
         ga = self._garr.get(key)
         if ga is not None and ga.works is works and self._reused and not self.todo:
             return ga                     # same job list object, nothing fetched: nothing changed
-        ident = tuple(map(id, works))
+        ident = self._jid(works)
         if ga is not None and ga.ident == ident and not any(fw.dirty for fw in works):
             ga.works = works
             return ga
@@ -744,12 +777,7 @@ class FastPath:
         col = self._col.get(p0.group)
         pos = None
         if col is not None:                               # column-wise fetched this cycle
-            if col["ids"] == ident:
-                pos = True
-            else:
-                pp = col["pos"]
-                j = np.fromiter((pp.get(i, -1) for i in ident), np.int64, len(ident))
-                pos = None if not len(j) or j.min() < 0 else j
+            pos = True if col["ids"] == ident else ident.index_in(col["ids"])
         if pos is not None:
             sel = None if pos is True else (pos[:, None] * M + np.arange(M)[None, :]).reshape(-1)
             pick = (lambda a: a) if sel is None else (lambda a: None if a is None else a[sel])
@@ -778,17 +806,24 @@ class FastPath:
         self._garr[key] = ga
         return ga
 
-    def _positions(self, ident: tuple) -> dict:
-        """{id(job): position} of a job list (one dict per cycle shared by
-        the fetch / arrays / cache-key memos of the same list)."""
-        pc = self._pos_cache
-        if pc is not None and pc[0] == ident:
-            return pc[1]
-        d = {i: j for j, i in enumerate(ident)}
-        self._pos_cache = (ident, d)
-        return d
+    def _gcount_add(self, group: tuple, n: int) -> None:
+        """Jobs per plan group among ``self.works`` (one group: no per-job grouping)."""
+        c = self._gcount.get(group, 0) + n
+        if c > 0:
+            self._gcount[group] = c
+        else:
+            self._gcount.pop(group, None)
 
-    def _static_cols(self, works: list[FastWork], ident: tuple, key: tuple, M: int):
+    def _jid(self, works: list) -> JobIds:
+        """JobIds of a job list, computed once per list object per cycle."""
+        c = self._jid_cache.get(id(works))
+        if c is not None and c[0] is works and len(c[1]) == len(works):
+            return c[1]
+        j = JobIds(works)
+        self._jid_cache[id(works)] = (works, j)
+        return j
+
+    def _static_cols(self, works: list[FastWork], ident: "JobIds", key: tuple, M: int):
         """Per-job columns of a job list that do not change with its data
         (resident rows, ids, store handles, end times, exporter slots): kept
         per group, and a fancy-index of the previous list's when the list only
@@ -798,11 +833,7 @@ class FastPath:
         if memo is not None and memo[0] == ident:
             return memo[2]
         S = len(works)
-        ix = None
-        if memo is not None:
-            pos = memo[1]
-            ix = np.fromiter((pos.get(i, -1) for i in ident), np.int64, S)
-            ix = ix if S and ix.min() >= 0 else None
+        ix = ident.index_in(memo[0]) if memo is not None else None
         exp = self.b.exporter
         extra: dict = {}
         if ix is not None:
@@ -827,10 +858,10 @@ class FastPath:
                     slots.append(p.export_slots)
                 xs = np.concatenate(slots)
             cols = (rowmap, ids, handles, np.fromiter((w.end_ts for w in works), np.float64, S), xs)
-        self._gstat[key] = (ident, self._positions(ident), cols, extra)
+        self._gstat[key] = (ident, None, cols, extra)
         return cols
 
-    def _extra(self, key: tuple, ident: tuple, name: str, make):
+    def _extra(self, key: tuple, ident: "JobIds", name: str, make):
         """A per-job array of a group's static memo (first axis = job), built
         by ``make()`` when the job list gained jobs; fancy-indexed with the
         static columns under churn."""
@@ -905,16 +936,12 @@ class FastPath:
         the same as one list object),
         a fancy-index of the previous job list's when the list only lost or
         reordered jobs (fleet churn)."""
-        ids = tuple(map(id, works))
+        ids = self._jid(works)
         M = len(p0.aliases)
         memo = self._keys.get((p0.group, algo))
         if memo is not None and memo[0] == ids:
             return memo[2], memo[3]
-        ix = None
-        if memo is not None:
-            pos = memo[1]
-            ix = np.fromiter((pos.get(i, -1) for i in ids), np.int64, len(ids))
-            ix = ix if len(ix) and ix.min() >= 0 else None
+        ix = ids.index_in(memo[0]) if memo is not None else None
         if ix is not None:
             kv = memo[2].reshape(-1, M)[ix].reshape(-1)
         else:
@@ -928,7 +955,7 @@ class FastPath:
             full = TemplateList.subset(memo[3], kv.tolist(), rix)
         else:
             full = TemplateList(kv.tolist())
-        self._keys[(p0.group, algo)] = (ids, self._positions(ids), kv, full)
+        self._keys[(p0.group, algo)] = (ids, None, kv, full)
         return kv, full
 
     def _model_arrays(self, ga: GroupArrays, works: list[FastWork], store: ResidentHistory) -> "ModelArrays":
@@ -1364,6 +1391,7 @@ class FastPath:
         for w in works:
             if self.works.get(w.doc.id) is w:
                 del self.works[w.doc.id]
+                self._gcount_add(w.plan.group, -1)
 
     def fail_job(self, fw: FastWork, err: str, updates: list, outcome: dict) -> None:
         st = ST.COMPLETED_UNKNOWN
@@ -1379,7 +1407,7 @@ class FastPath:
             stale = [k for k, w in self.works.items()
                      if (self.sliding if w.plan.sliding else self.static).keys[int(w.rows[0])] != w.plan.keys[0]]
             for k in stale:
-                del self.works[k]
+                self._gcount_add(self.works.pop(k).plan.group, -1)
 
 
 def _merge_series(ss) -> tuple[np.ndarray, np.ndarray]:
