@@ -292,3 +292,15 @@ def test_gpu_resident_tick_masked_rows_match_cpu(cuda):
     np.testing.assert_allclose(o.decide.stats.cpu().numpy(), ref.decide.stats.numpy(), rtol=3e-5, atol=1e-4)
     np.testing.assert_array_equal(o.decide.valid.cpu().numpy(), ref.decide.valid.numpy())
     assert (o.packed[:, 0].cpu() == ref.packed[:, 0]).float().mean() >= 0.99
+
+
+def test_job_ids_index_in_finds_survivors_or_none():
+    from foremast_amd.engine.fastpath import JobIds
+    objs = [object() for _ in range(50)]
+    old = JobIds(objs)
+    keep = [objs[i] for i in (3, 1, 7, 49, 0)]
+    ix = JobIds(keep).index_in(old)
+    assert list(ix) == [3, 1, 7, 49, 0]
+    assert JobIds(objs[:10] + [object()]).index_in(old) is None      # a new job: no subset
+    assert JobIds([]).index_in(old) is None
+    assert JobIds(objs) == old and JobIds(objs[::-1]) != old
