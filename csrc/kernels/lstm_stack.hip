@@ -249,9 +249,23 @@ __device__ __forceinline__ void lds_barrier() {
 }
 template <int N>
 using ic = std::integral_constant<int, N>;
+// f(ic<0>{}), ..., f(ic<N-1>{}): a compile-time unrolled loop of any length
+// (#pragma unroll gives up on long bodies and falls back to a rolled loop
+// with dynamically indexed -- scratch -- register arrays)
+template <class F, int... I>
+__device__ __forceinline__ void static_for_(F&& f, std::integer_sequence<int, I...>) {
+  (f(ic<I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_(f, std::make_integer_sequence<int, N>{});
+}
 }  // namespace
 
-template <int H, int RT>
+// ABL (measurement only, 0 in production): bit 0 replaces the cell math by a
+// copy, bit 1 reads every A fragment from one k-step's address (L2-hot), bit
+// 2 keeps the A fragments one k-step ahead instead of two
+template <int H, int RT, int ABL = 0>
 __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
     const uint4* __restrict__ xa, int64_t B, int L, const uint4* __restrict__ W0, const uint4* __restrict__ W1,
     float* __restrict__ h_out, float* __restrict__ c_out) {
@@ -299,11 +313,12 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
   unsigned short* h1w = h1b + col * HP;
   auto lds16 = [](const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); };
 
-  Frag a[RT];                                          // A fragments of the current k-step
+  Frag a[RT], an[RT];                                  // A fragments of the current / next k-step
   auto loadA = [&](Frag (&f)[RT], __amdgpu_buffer_rsrc_t Ww, int KS, int ks) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(Ww, voff, (rt * KS + ks) * 1024, 0);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(Ww, voff, (ABL & 2) ? rt * 1024 : (rt * KS + ks) * 1024,
+                                                            0);
       f[rt].u = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
@@ -311,17 +326,27 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
   // then cell_at(i); the A fragments of (Wn, KSn, ksn) are prefetched during
   // the last step (the first k-step of whatever follows)
   auto segment = [&](auto NK, f32x16 (&acc)[RT], __amdgpu_buffer_rsrc_t Ww, int KS, auto ks_of, auto b_of,
-                     __amdgpu_buffer_rsrc_t Wn, int KSn, int ksn, auto cell_at) {
-    // the B fragment (h image in LDS, stable for the whole segment) is read
-    // one k-step ahead too, so its LDS latency hides behind the MFMAs
+                     __amdgpu_buffer_rsrc_t Wn, int KSn, int kn0, int kn1, auto cell_at) {
+    // A fragments run two k-steps ahead (a: this step, an: the next; on
+    // entry both were issued by whatever ran before), across segments: the
+    // last two steps prefetch the next segment's (Wn, KSn) k-steps kn0, kn1.
+    // The B fragment (h image in LDS, stable for the whole segment) is read
+    // one k-step ahead.
+    constexpr int N = decltype(NK)::value;
     uint4 bcur = b_of(0);
 #pragma unroll
-    for (int i = 0; i < decltype(NK)::value; ++i) {
+    for (int i = 0; i < N; ++i) {
       __builtin_amdgcn_sched_barrier(0);             // k-steps stay in order: no hoisted loads
-      Frag an[RT];
-      if (i + 1 < decltype(NK)::value) loadA(an, Ww, KS, ks_of(i + 1));
-      else loadA(an, Wn, KSn, ksn);
-      const uint4 bnext = i + 1 < decltype(NK)::value ? b_of(i + 1) : bcur;
+      Frag ann[RT];
+      if (ABL & 4) {                                 // one k-step ahead only
+        if (i + 1 < N) loadA(an, Ww, KS, ks_of(i + 1));
+        else loadA(an, Wn, KSn, kn0);
+      } else if (i + 2 < N) {
+        loadA(ann, Ww, KS, ks_of(i + 2));
+      } else {
+        loadA(ann, Wn, KSn, i + 2 == N ? kn0 : kn1);
+      }
+      const uint4 bnext = i + 1 < N ? b_of(i + 1) : bcur;
       Frag bf;
       bf.u = bcur;
 #pragma unroll
@@ -329,7 +354,10 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
         acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rt].v, bf.v, acc[rt], 0, 0, 0);
       cell_at(i);
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) a[rt] = an[rt];
+      for (int rt = 0; rt < RT; ++rt) {
+        a[rt] = an[rt];
+        if (!(ABL & 4)) an[rt] = ann[rt];
+      }
       bcur = bnext;
     }
   };
@@ -342,7 +370,12 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
   float hv[4];
   auto cell_q = [&](int q, const f32x16 (&acc)[RT], float (&c)[RT][4], unsigned short* hw, bool out) {
     const int rt = q >> 2, j = q & 3;
-    cell(acc[rt][j], acc[rt][4 + j], acc[rt][8 + j], acc[rt][12 + j], c[rt][j], hv[j]);
+    if (ABL & 1) {
+      hv[j] = acc[rt][j] * 1e-3f;
+      c[rt][j] = acc[rt][4 + j];
+    } else {
+      cell(acc[rt][j], acc[rt][4 + j], acc[rt][8 + j], acc[rt][12 + j], c[rt][j], hv[j]);
+    }
     if (j == 3) {
       const int u0 = 8 * RT * w + 8 * rt + 4 * hf;
       uint2 pk;
@@ -365,10 +398,11 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
   // prologue: L0(0) (h0_{-1} = 0), its cells, barrier; L1(0)'s k-steps over
   // h1_{-1} = 0 contribute nothing: accB starts at zero
   loadA(a, W0w, KS0, KH);
+  if (!(ABL & 4)) loadA(an, W0w, KS0, 0);
   zero(accA);
   segment(ic<KS0>{}, accA, W0w, KS0, ks_l0,
           [&](int i) { const uint4 v = lds16(h0r + 16 * (i == 0 ? 0 : i - 1)); return i == 0 ? xt : v; },
-          W1w, KS1, KH, no_cell);
+          W1w, KS1, KH, KH + 1, no_cell);
 #pragma unroll
   for (int q = 0; q < NC; ++q) cell_q(q, accA, c0, h0w, false);
   lds_barrier();
@@ -377,32 +411,32 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
   for (int t = 0; t < L - 1; ++t) {
     xt = xp[(t + 1) * 2];
     // phase A: L1(t) over [h0_t; 1]
-    segment(ic<KH + 1>{}, accB, W1w, KS1, ks_l1b, b_l1b, W0w, KS0, KH, no_cell);
+    segment(ic<KH + 1>{}, accB, W1w, KS1, ks_l1b, b_l1b, W0w, KS0, KH, 0, no_cell);
     //          L0(t+1) over [x_{t+1}; h0_t]  ||  cells of L1(t)
     zero(accA);
     segment(ic<KS0>{}, accA, W0w, KS0, ks_l0,
             [&](int i) { const uint4 v = lds16(h0r + 16 * (i == 0 ? 0 : i - 1)); return i == 0 ? xt : v; },
-            W1w, KS1, 0, [&](int i) { if (i < NC) cell_q(i, accB, c1, h1w, false); });
+            W1w, KS1, 0, 1, [&](int i) { if (i < NC) cell_q(i, accB, c1, h1w, false); });
     lds_barrier();                                   // h1_t complete; every read of h0_t done
     // phase B: L1(t+1) over h1_t  ||  cells of L0(t+1)
     zero(accB);
     segment(ic<KH>{}, accB, W1w, KS1, ks_l1a, [&](int i) { return lds16(h1r + 16 * i); },
-            W1w, KS1, KH, [&](int i) { if (i < NC) cell_q(i, accA, c0, h0w, false); });
+            W1w, KS1, KH, KH + 1, [&](int i) { if (i < NC) cell_q(i, accA, c0, h0w, false); });
     lds_barrier();                                   // h0_{t+1} complete; every read of h1_t done
   }
   // the last step's layer 1 (out of the loop: its output addresses are not
   // live across the time loop)
-  segment(ic<KH + 1>{}, accB, W1w, KS1, ks_l1b, b_l1b, W1w, KS1, 0, no_cell);
+  segment(ic<KH + 1>{}, accB, W1w, KS1, ks_l1b, b_l1b, W1w, KS1, 0, 1, no_cell);
 #pragma unroll
   for (int q = 0; q < NC; ++q) cell_q(q, accB, c1, h1w, true);
 }
 
-template <int H, int RT>
+template <int H, int RT, int ABL = 0>
 static int launch_stack2_pipe(const void* xa, int64_t B, int L, const void* W0, const void* W1, float* h_out,
                               float* c_out, hipStream_t stream) {
   constexpr int NW = H / (8 * RT);
   const size_t lds = (size_t)2 * 32 * (H + 8) * sizeof(unsigned short);
-  auto k = lstm_stack2_pipe_kernel<H, RT>;
+  auto k = lstm_stack2_pipe_kernel<H, RT, ABL>;
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
@@ -413,10 +447,215 @@ static int launch_stack2_pipe(const void* xa, int64_t B, int L, const void* W0, 
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Two layers, row-tile streamed, BT = 64 sequences per workgroup.  The
+// pipelined kernel above is bound by the weight stream: every workgroup
+// pulls all 1.6 MB of [W0 | W1] through its CU's vector-memory path each step
+// for only 32 sequences (profiles/lstm_pipe_ablation_r3.jsonl: L1-resident
+// weights 4.7 ms vs 6.7), and 64 sequences x both layers' accumulators do not
+// fit in registers.  Here a wave works through its row tiles one at a time
+// ("tasks": one row tile of one layer, both column tiles), so only two tiles'
+// accumulators are live -- the one accumulating and the one whose cells are
+// being updated beside its MFMAs -- and each weight fragment feeds 64
+// sequences, halving weight bytes per sequence.
+//
+// Iteration s runs layer 0 at step s and layer 1 at step s - 1 (both read
+// only outputs of iteration s - 1), as 8 tasks: L0 rt0..3, L1 rt0..3.  The
+// cells of task T run during task T + 1 (those of L1 rt3 in the next
+// iteration's L0 rt0).  h images are double-buffered per layer; two barriers
+// per iteration: before L0 rt0 (h0_{s-1} complete) and before L1 rt0
+// (h1_{s-2} complete: its last cells ran in L0 rt0).  Iteration 0 has no
+// layer-1 cells, iteration L no layer-0 input (x clamped, outputs unused);
+// the final L1 rt3 cells (h_out / c_out) run after the loop.
+template <int H>
+__global__ __launch_bounds__(512) void lstm_stack2_rs_kernel(
+    const uint4* __restrict__ xa, int64_t B, int L, const uint4* __restrict__ W0, const uint4* __restrict__ W1,
+    float* __restrict__ h_out, float* __restrict__ c_out) {
+  constexpr int RT = 4;
+  constexpr int NW = H / (8 * RT);
+  static_assert(NW == 8, "8 waves");
+  constexpr int KH = H / 16;
+  constexpr int KS0 = KH + 1;
+  constexpr int KS1 = 2 * KH + 1;
+  constexpr int HP = H + 8;
+  constexpr int BT = 64;
+  constexpr int IMG = BT * HP;
+  constexpr int G0 = RT * KS0;                          // k-steps of the layer-0 tasks
+  constexpr int G = G0 + RT * KS1;                      // k-steps per iteration
+  constexpr int DA = 3;                                 // A fragments DA k-steps ahead
+  static_assert(G % (DA + 1) == 0, "A ring wraps at the iteration boundary");
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  unsigned short* h0b = lds;                            // [2][BT][HP]
+  unsigned short* h1b = lds + 2 * IMG;                  // [2][BT][HP]
+  const int lane = lane_id(), w = wave_id();
+  const int hf = lane >> 5, col = lane & 31;
+  const int64_t b0 = (int64_t)blockIdx.x * BT;
+
+  for (int i = threadIdx.x; i < 4 * IMG; i += 64 * NW) lds[i] = 0;   // h_{-1} = 0
+  float c0[RT][2][4], c1[RT][2][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c0[rt][ct][j] = c1[rt][ct][j] = 0.f;
+  __syncthreads();
+
+  const uint4* xp[2];
+  bool inb[2];
+  int64_t bbo[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    int64_t bb = b0 + 32 * ct + col;
+    inb[ct] = bb < B;
+    bb = bb < B ? bb : B - 1;
+    bbo[ct] = bb;
+    xp[ct] = xa + (bb * L) * 2 + hf;
+  }
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t W0w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W0 + (int64_t)wu * RT * KS0 * 64), (short)0, RT * KS0 * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t W1w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W1 + (int64_t)wu * RT * KS1 * 64), (short)0, RT * KS1 * 1024, 0x00020000);
+  const int voff = 16 * lane;
+  const uint4 onesv = make_uint4(hf == 0 ? 0x3F80u : 0u, 0u, 0u, 0u);
+  const int lro = col * HP + 8 * hf;                    // this lane's B-fragment row (column tile 0)
+  auto lds16 = [](const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); };
+
+  // k-step g of an iteration -> (layer, row tile, k index within the task)
+  auto lay = [](int g) { return g >= G0 ? 1 : 0; };
+  auto tsk = [](int g) { return g < G0 ? g / KS0 : RT + (g - G0) / KS1; };
+  auto kin = [](int g) { return g < G0 ? g % KS0 : (g - G0) % KS1; };
+  auto loadA = [&](Frag& f, int g) {
+    const int rt = tsk(g) & (RT - 1), i = kin(g);
+    const u32x4 v = lay(g) ? __builtin_amdgcn_raw_buffer_load_b128(W1w, voff, (rt * KS1 + i) * 1024, 0)
+                           : __builtin_amdgcn_raw_buffer_load_b128(W0w, voff, (rt * KS0 + (i == 0 ? KH : i - 1)) * 1024, 0);
+    f.u = make_uint4(v.x, v.y, v.z, v.w);
+  };
+
+  f32x16 acc[2][2];                                     // [task parity][column tile]
+  Frag ar[DA + 1];
+  float hv[4];
+  // cell q (column tile q / 4, unit q % 4) of the finished task T's
+  // accumulator; the tile's 4 h values go to image ``img`` with its last cell
+  auto cell_q = [&](int T, int q, unsigned short* img, bool out) {
+    const int rt = T & (RT - 1), ct = q >> 2, j = q & 3;
+    const f32x16& a = acc[T & 1][ct];
+    if (T >= RT) cell(a[j], a[4 + j], a[8 + j], a[12 + j], c1[rt][ct][j], hv[j]);
+    else cell(a[j], a[4 + j], a[8 + j], a[12 + j], c0[rt][ct][j], hv[j]);
+    if (j == 3) {
+      const int u0 = 8 * RT * w + 8 * rt + 4 * hf;
+      uint2 pk;
+      pk.x = pack_bf2(hv[0], hv[1]);
+      pk.y = pack_bf2(hv[2], hv[3]);
+      *reinterpret_cast<uint2*>(&img[(32 * ct + col) * HP + u0]) = pk;
+      if (out && inb[ct]) {
+        const float(&c)[RT][2][4] = c1;
+        *reinterpret_cast<float4*>(&h_out[bbo[ct] * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        *reinterpret_cast<float4*>(&c_out[bbo[ct] * H + u0]) =
+            make_float4(c[rt][ct][0], c[rt][ct][1], c[rt][ct][2], c[rt][ct][3]);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int g = 0; g < DA; ++g) loadA(ar[g], g);
+  uint4 xn[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) xn[ct] = xp[ct][0];
+
+  for (int s = 0; s <= L; ++s) {
+    const int p = s & 1;
+    const unsigned short* h0r = h0b + (p ^ 1) * IMG + lro;   // h0_{s-1}
+    const unsigned short* h1r = h1b + p * IMG + lro;         // h1_{s-2}
+    unsigned short* h0w = h0b + p * IMG;                     // h0_s
+    unsigned short* h1w_old = h1b + p * IMG;                 // h1_{s-2} (L1 rt3 cells of iteration s - 1)
+    unsigned short* h1w = h1b + (p ^ 1) * IMG;               // h1_{s-1}
+    const bool l1prev = s >= 2, l1cur = s >= 1, fin = s == L;
+    uint4 xt[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      xt[ct] = xn[ct];
+      xn[ct] = xp[ct][(s + 1 < L ? s + 1 : L - 1) * 2];
+    }
+    // B of k-step g, column tile ct (by value: see gemm above)
+    auto bread = [&](int g, int ct) {
+      const int i = kin(g);
+      if (lay(g) == 0) {
+        const uint4 v = lds16(h0r + 32 * ct * HP + 16 * (i == 0 ? 0 : i - 1));
+        return i == 0 ? xt[ct] : v;
+      }
+      if (i < KH) return lds16(h1r + 32 * ct * HP + 16 * i);
+      const uint4 v = lds16(h0r + 32 * ct * HP + 16 * (i < 2 * KH ? i - KH : KH - 1));
+      return i == 2 * KH ? onesv : v;
+    };
+    uint4 bcur[2] = {xt[0], xt[1]};
+    static_for<G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (g == 0 || g == G0) lds_barrier();
+      loadA(ar[(g + DA) % (DA + 1)], (g + DA) % G);
+      if constexpr (g == G0) {                                 // not prefetched across the barrier
+        bcur[0] = bread(g, 0);
+        bcur[1] = bread(g, 1);
+      }
+      uint4 bnext[2] = {bcur[0], bcur[1]};
+      if constexpr (g + 1 < G && g + 1 != G0) {
+        bnext[0] = bread(g + 1, 0);
+        bnext[1] = bread(g + 1, 1);
+      }
+      constexpr int T = g < G0 ? g / KS0 : RT + (g - G0) / KS1;
+      constexpr int i = g < G0 ? g % KS0 : (g - G0) % KS1;
+      const Frag& a = ar[g % (DA + 1)];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        Frag bf;
+        bf.u = bcur[ct];
+        acc[T & 1][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, bf.v, i == 0 ? (f32x16){} : acc[T & 1][ct],
+                                                                 0, 0, 0);
+      }
+      // one cell of the previous task every 2 (layer-0 task) or 4 (layer-1
+      // task) k-steps from the second k-step on
+      constexpr int stride = g >= G0 ? 4 : 2;
+      if constexpr (i >= 1 && (i - 1) % stride == 0 && (i - 1) / stride < 8) {
+        constexpr int q = (i - 1) / stride, Tp = (T + 2 * RT - 1) % (2 * RT);
+        if constexpr (T == 0) {
+          if (l1prev) cell_q(Tp, q, h1w_old, false);
+        } else if constexpr (Tp < RT) {
+          cell_q(Tp, q, h0w, false);
+        } else if (l1cur) {
+          cell_q(Tp, q, h1w, fin);
+        }
+      }
+      bcur[0] = bnext[0];
+      bcur[1] = bnext[1];
+    });
+  }
+  // L1(L-1) rt3: its cells would run in iteration L + 1
+#pragma unroll
+  for (int q = 0; q < 8; ++q) cell_q(2 * RT - 1, q, h1b + ((L + 1) & 1) * IMG, true);
+}
+
+template <int H>
+static int launch_stack2_rs(const void* xa, int64_t B, int L, const void* W0, const void* W1, float* h_out,
+                            float* c_out, hipStream_t stream) {
+  const size_t lds = (size_t)4 * 64 * (H + 8) * sizeof(unsigned short);
+  auto k = lstm_stack2_rs_kernel<H>;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)((B + 63) / 64)), dim3(512), lds, stream, (const uint4*)xa, B, L,
+                     (const uint4*)W0, (const uint4*)W1, h_out, c_out);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
 // Row tiles per wave / column tiles per workgroup (see ops/lstm.py
-// STACK_TILING / STACK_TILING_2L): two layers at H=256 run the layer-pipelined
-// kernel (nct = 201, RT = 4: 10k x 240 in 6.8 ms vs 8.2 for 4 x 2,
-// profiles/lstm_stack_ab_r3b.jsonl); one layer at H=256: 4 x 2 (8 waves, 64
+// STACK_TILING / STACK_TILING_2L): two layers at H=256 run the row-streamed
+// BT = 64 kernel (nct = 202, RT = 4: 10k x 240 in 4.6 ms, 80k in 29.6; the
+// layer-pipelined nct = 201 kernel 6.8 / 35.9, the 4 x 2 register kernel 8.2 /
+// 42.0, profiles/lstm_stack_rs_r3.jsonl); one layer at H=256: 4 x 2 (8 waves, 64
 // sequences share every streamed weight fragment); H<=128: 2 x 2 (H/16
 // waves, 64 sequences).  rt / nct = 0 pick 4 x 2 / 2 x 2; the other H = 256
 // tilings (4 x 1, 2 x 2, 2 x 1, 2 x 1 pipelined) stay instantiated for the
@@ -436,6 +675,16 @@ FM_API int fm_lstm_stack(const void* xa, int64_t B, int L, int H, int layers, co
     if (H == 256 && rt == 4) return launch_stack2_pipe<256, 4>(xa, B, L, W0, W1, h_out, c_out, stream);
     if (H == 256 && rt == 2) return launch_stack2_pipe<256, 2>(xa, B, L, W0, W1, h_out, c_out, stream);
     return (int)hipErrorInvalidValue;
+  }
+  if (nct == 202 && layers == 2) {     // row-tile streamed 2-layer kernel (lstm_stack2_rs_kernel), 2 column tiles
+    if (H == 256 && rt == 4) return launch_stack2_rs<256>(xa, B, L, W0, W1, h_out, c_out, stream);
+    return (int)hipErrorInvalidValue;
+  }
+  if (nct >= 211 && nct <= 214 && layers == 2 && H == 256 && rt == 4) {   // ablations (measurement only)
+    if (nct == 211) return launch_stack2_pipe<256, 4, 1>(xa, B, L, W0, W1, h_out, c_out, stream);
+    if (nct == 212) return launch_stack2_pipe<256, 4, 2>(xa, B, L, W0, W1, h_out, c_out, stream);
+    if (nct == 213) return launch_stack2_pipe<256, 4, 3>(xa, B, L, W0, W1, h_out, c_out, stream);
+    return launch_stack2_pipe<256, 4, 4>(xa, B, L, W0, W1, h_out, c_out, stream);
   }
   switch (H) {
     case 256:

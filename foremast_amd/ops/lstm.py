@@ -14,12 +14,16 @@ from ._lib import LIB, check, ptr, require_native, stream_of
 SUPPORTED_H = (32, 64, 128)              # register-resident single-layer kernel (lstm.hip)
 STACK_H = (32, 64, 128, 256)             # streamed-weight 1-2 layer kernel (lstm_stack.hip)
 STACK_TILING = {256: (4, 2), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row tiles / wave, column tiles)
-# two layers at H = 256: the layer-pipelined kernel (cells beside the next
-# layer's MFMAs; 6.8 vs 8.2 ms at 10k x 240, 37.0 vs 42.0 ms at 80k x 240,
-# profiles/lstm_stack_ab_r3b.jsonl); weights packed with the same RT = 4
-STACK_TILING_2L = {256: (4, 201)}
+# two layers at H = 256: the row-streamed BT = 64 kernel (one row tile at a
+# time, its cells beside the next tile's MFMAs, every weight fragment feeding
+# 64 sequences; 4.6 ms at 10k x 240 and 29.6 at 80k, vs 6.8 / 35.9 for the
+# layer-pipelined BT = 32 kernel and 8.2 / 42.0 for 4 x 2,
+# profiles/lstm_stack_rs_r3.jsonl); weights packed with the same RT = 4
+STACK_TILING_2L = {256: (4, 202)}
 STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1),            # instantiated alternatives (lstm_stack.hip);
-                          (4, 201), (2, 201))}                       # nct 201: layer-pipelined, 2 layers, 1 tile
+                          (4, 201), (2, 201), (4, 202),              # nct 201: layer-pipelined, 2 layers, 1 tile; 202: row-streamed, 2 tiles;
+                          (4, 211), (4, 212), (4, 213), (4, 214))}   # 211-213: its ablations (timing only, wrong h);
+                                                                     # 214: A one k-step ahead (correct h)
 
 
 def stack_tiling(H: int, layers: int = 1) -> tuple[int, int]:

@@ -490,13 +490,17 @@ def test_gpu_lstm_stack_matches_fp32_lstm(cuda, H, layers, I):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tiling", ["4:1", "2:1", "4:2", "2:2", "4:1p", "2:1p"])
-def test_gpu_lstm_stack_tilings_agree(cuda, tiling, monkeypatch):
-    """Every instantiated H = 256 tiling (row tiles per wave x column tiles)
-    computes the same recurrence as the bf16-emulating reference."""
+@pytest.mark.parametrize("tiling,L", [("4:1", 48), ("2:1", 48), ("4:2", 48), ("2:2", 48), ("4:1p", 48),
+                                      ("2:1p", 48), ("4:2p", 48), ("4:214", 48),
+                                      ("4:1p", 1), ("4:1p", 2), ("4:2p", 1), ("4:2p", 2), ("4:2p", 3)])
+def test_gpu_lstm_stack_tilings_agree(cuda, tiling, L, monkeypatch):
+    """Every instantiated H = 256 tiling (row tiles per wave x column tiles;
+    ``p``: the two-layer pipelined / row-streamed kernels, incl. their
+    one- to three-step prologue / epilogue paths) computes the same
+    recurrence as the bf16-emulating reference."""
     monkeypatch.setenv("FM_LSTM_STACK_TILING", tiling)
     torch.manual_seed(5)
-    H, layers, I, B, L = 256, 2, 11, 100, 48
+    H, layers, I, B = 256, 2, 11, 100
     m = torch.nn.LSTM(I, H, num_layers=layers, batch_first=True)
     x = torch.randn(B, L, I)
     ws = [(getattr(m, f"weight_ih_l{k}"), getattr(m, f"weight_hh_l{k}"),

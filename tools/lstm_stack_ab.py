@@ -5,7 +5,7 @@ multivariate shape: 10k services (one row each), lookback 240, 10 input
 features, 2 layers.  Median kernel time per tiling (HIP events) and the max
 deviation from the default tiling's h_L.
 
-  python tools/lstm_stack_ab.py [--batch 10000] [--steps 240] [--tilings 4:2,4:1,4:1g]
+  python tools/lstm_stack_ab.py [--batch 10000] [--steps 240] [--tilings 4:2,4:1,4:1p,4:2p]
 """
 import argparse
 import json
@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--layers", type=int, default=2)
-    ap.add_argument("--tilings", default="4:2,4:1,2:2,4:1p,2:1p")
+    ap.add_argument("--tilings", default="4:2,4:1,2:2,4:1p,2:1p,4:2p")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)

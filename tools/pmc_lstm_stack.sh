@@ -1,12 +1,12 @@
 #!/bin/bash
 # PMC counters of the H = 256 x 2 stacked-LSTM variants (tools/lstm_stack_ab.py:
-# 4:2 register lookahead, 4:1p layer-pipelined (the two-layer default)), two
+# 4:1p layer-pipelined, 4:2p row-streamed BT = 64 (the two-layer default)), two
 # passes of <= 8 SQ counters, kernel-trace + counters only.  Summarise with
 # tools/pmc_summary.py --kernel lstm_stack.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 set -e
-T="--tilings 4:2,4:1p"
+T="--tilings ${PMC_TILINGS:-4:1p,4:2p}"
 timeout -k 10 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VALU_TRANS_F32 \
   SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES \
   -d "$R/gpurun_out/pmc_lstm_stack_a" -o a -- python3 "$R/tools/lstm_stack_ab.py" $T > "$R/gpurun_out/pmc_lstm_stack_a.log" 2>&1
