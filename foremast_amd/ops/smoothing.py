@@ -60,15 +60,44 @@ class ESFit:
 
 HALF_SEASON_MIN_M = 1000     # <= ~10 laps of a 7-day history: measured within 2e-3 of fp32 (tests)
 
+# csrc/kernels/hw_scan.hip: lanes take chunks of these many steps of a season lap
+_SCAN_CHUNKS = (4, 5, 6, 8, 12, 16, 20, 23, 24)
+# "auto" picks the scan fit up to this season length: 40k rows x 10,080 steps,
+# m = 288: 11.3 vs 14.6 ms (10k rows: 2.9 vs 4.8); m = 1440: 8.2 vs 7.9 ms
+# (10k: 2.1 vs 2.4); m = 1008: 12.5 vs 8.6 ms (tools/hw_scan_ab.py,
+# profiles/hw_scan_ab_r3.jsonl).  Longer seasons keep the serial fp16-scratch
+# kernel unless method="scan".
+SCAN_AUTO_MAX_M = 768
+
+
+def hw_scan_supported(T: int, G: int, m: int) -> bool:
+    """Shapes the time-parallel additive Holt-Winters fit covers (mirrors
+    ``fm_hw_scan_fit``'s checks): 192 <= m <= 64 * 24, G <= 32, 2 m <= T and
+    the row (+ NaN padding for the last lap) within 64 KB of LDS."""
+    if not (1 <= G <= 32 and 192 <= m and 2 * m <= T):
+        return False
+    need = -(-m // 64)
+    cs = [c for c in _SCAN_CHUNKS if c >= need and m % c == 0] or [c for c in _SCAN_CHUNKS if c >= need]
+    if not cs:
+        return False
+    lds = (((T + 3) & ~3) + 64 * cs[0]) * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16
+    return lds <= 65536
+
 
 def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, grid: np.ndarray | None = None,
-           keep_state: bool = False, half_season: bool = True) -> ESFit:
+           keep_state: bool = False, half_season: bool = True, method: str = "auto") -> ESFit:
     """Fit SES / Holt / Holt-Winters (additive, multiplicative) by grid search
     on one-step SSE and forecast H steps past the end of the history.  With
     ``keep_state`` the best candidate's fitted state is returned as an
-    :class:`ESState` (for the model cache).  ``half_season``: the GPU grid
-    keeps its [m][R*G] seasonal scratch in fp16 scaled per row (half the HBM
-    traffic that bounds the fit; csrc/kernels/smoothing.hip)."""
+    :class:`ESState` (for the model cache).
+
+    GPU additive Holt-Winters with ``method="scan"`` (and "auto" up to
+    ``SCAN_AUTO_MAX_M``) runs the time-parallel scan fit
+    (csrc/kernels/hw_scan.hip: seasons in registers, no seasonal scratch
+    traffic) where :func:`hw_scan_supported`; otherwise the serial grid kernels
+    (csrc/kernels/smoothing.hip), whose [m][R*G] seasonal scratch is fp16
+    scaled per row when ``half_season`` (half the HBM traffic that bounds
+    that fit)."""
     check(x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1, "x must be [R, T] float32")
     check(0 <= kind <= 3, f"kind must be 0..3, got {kind}")
     R = x.shape[0]
@@ -89,9 +118,15 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
         return ESFit(torch.from_numpy(fc), torch.from_numpy(sig), torch.from_numpy(best), torch.from_numpy(sse), model,
                      nfin)
     require_native(x)
+    check(method in ("auto", "scan", "serial"), f"unknown method {method!r}")
     d = x.device
     cand = torch.from_numpy(grid).to(d)
     P = R * G
+    scan = kind == 2 and (method == "scan" or (method == "auto" and m <= SCAN_AUTO_MAX_M)) \
+        and hw_scan_supported(T, G, m)
+    check(scan or method != "scan", f"the scan fit does not cover T={T}, G={G}, m={m}")
+    if scan:
+        return _hw_scan_fit(x, T, R, cand, G, m, H, keep_state)
     # fp16 only where the scratch is big enough to be HBM traffic (daily /
     # longer seasons: a handful of laps, little rounding to accumulate; at
     # m = 288 (35 laps) SSEs moved by up to 1.2 %); short seasons stay fp32
@@ -121,6 +156,29 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
         model = ESState(kind, m, cand[b].contiguous(), state[pid].contiguous(),
                         _half_season_of(season, b, R, GP, m, sscale) if half else
                         (season[:, pid].t().contiguous() if kind >= 2 else None),
+                        sse.gather(1, b[:, None])[:, 0].contiguous(), nobs[pid].contiguous())
+    return ESFit(fc, sig, best, sse, model, nfin)
+
+
+def _hw_scan_fit(x: torch.Tensor, T: int, R: int, cand: torch.Tensor, G: int, m: int, H: int,
+                 keep_state: bool) -> ESFit:
+    d = x.device
+    sse = torch.empty((R, G), dtype=torch.float32, device=d)
+    state = torch.empty((R * G, 3), dtype=torch.float32, device=d)
+    nobs = torch.empty((R * G,), dtype=torch.int32, device=d)
+    fc = torch.empty((R, H), dtype=torch.float32, device=d)
+    sig = torch.empty((R,), dtype=torch.float32, device=d)
+    best = torch.empty((R,), dtype=torch.int32, device=d)
+    nfin = torch.empty((R,), dtype=torch.int32, device=d)
+    sscale = torch.empty((R,), dtype=torch.float32, device=d)
+    season = torch.empty((R, m), dtype=torch.float32, device=d) if keep_state else None
+    LIB.call("fm_hw_scan_fit", ptr(x), x.stride(0), T, R, ptr(cand), G, m, H, ptr(sse), ptr(state), ptr(nobs),
+             ptr(fc), ptr(sig), ptr(best), ptr(nfin), ptr(sscale), ptr(season), stream_of(x))
+    model = None
+    if keep_state:
+        b = best.long()
+        pid = torch.arange(R, device=d) * G + b
+        model = ESState(2, m, cand[b].contiguous(), state[pid].contiguous(), season,
                         sse.gather(1, b[:, None])[:, 0].contiguous(), nobs[pid].contiguous())
     return ESFit(fc, sig, best, sse, model, nfin)
 

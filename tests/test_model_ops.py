@@ -556,3 +556,146 @@ def test_gpu_es_fit_half_season_matches_fp32(cuda, kind, m):
     amp = np.abs(x[same]).mean(1, keepdims=True)
     np.testing.assert_allclose(h.forecast.cpu().numpy()[same] / amp, f.forecast.cpu().numpy()[same] / amp,
                                atol=2e-3)
+
+
+# ------------------------------------------- time-parallel Holt-Winters scan fit
+def _hw_scan_sim(xr, al, be, ga, m, C):
+    """fp64 numpy mirror of csrc/kernels/hw_scan.hip for one row and one
+    candidate: chunked laps, lane-0 seeded zero-state chunk maps, the
+    Hillis-Steele scan with lane-uniform powers A^{C d} (fast path) or explicit
+    chunk matrices (a lap with a missing sample), then pass 2."""
+    T = len(xr)
+    fin = np.isfinite(xr)
+    base = int(np.argmax(fin)) if fin.any() else T
+    if base >= T:
+        return 0.0, 0
+    e1, e2 = min(base + m, T), min(base + 2 * m, T)
+    m1 = np.nanmean(xr[base:e1])
+    m2 = np.nanmean(xr[e1:e2]) if np.isfinite(xr[e1:e2]).any() else None
+    l, t = m1, ((m2 - m1) / m if m2 is not None else 0.0)
+    s = np.zeros(64 * C)
+    for q in range(m):
+        v = xr[base + q] if base + q < T else np.nan
+        s[q] = v - m1 if np.isfinite(v) else 0.0
+    A = np.array([[1 - al, 1 - al], [-al * be, 1 - al * be]])
+    k = np.array([al, al * be])
+    J = np.array([[1.0, 1.0], [0.0, 1.0]])
+    sse, n = 0.0, 0
+    for tl in range(base + m, T, m):
+        nact = min(m, T - tl)
+        last = (nact - 1) // C
+        xl = np.full(64 * C, np.nan)
+        xl[:nact] = xr[tl:tl + nact]
+        Ms, bs, bad = [], [], False
+        for i in range(64):
+            M, b = np.eye(2), (np.array([l, t]) if i == 0 else np.zeros(2))
+            for j in range(C):
+                q = i * C + j
+                f = q < nact and np.isfinite(xl[q])
+                if i < last and not np.isfinite(xl[q]):
+                    bad = True
+                if f:
+                    b = A @ b + k * (xl[q] - s[q])
+                    M = A @ M
+                else:
+                    b = J @ b
+                    M = J @ M
+            Ms.append(M)
+            bs.append(b)
+        if not bad:        # fast path: lane i's window at level d is A^{C d}
+            B = [b.copy() for b in bs]
+            for d in (1, 2, 4, 8, 16, 32):
+                P = np.linalg.matrix_power(A, C * d)
+                B = [B[i] + P @ B[i - d] if i >= d else B[i] for i in range(64)]
+        else:
+            B, M = [b.copy() for b in bs], [x.copy() for x in Ms]
+            for d in (1, 2, 4, 8, 16, 32):
+                B, M = ([M[i] @ B[i - d] + B[i] if i >= d else B[i] for i in range(64)],
+                        [M[i] @ M[i - d] if i >= d else M[i] for i in range(64)])
+        for i in range(last + 1):
+            L, Tt = (l, t) if i == 0 else B[i - 1]
+            for j in range(C):
+                q = i * C + j
+                if q >= nact:
+                    break
+                lt = L + Tt
+                if np.isfinite(xl[q]):
+                    e = xl[q] - (lt + s[q])
+                    sse += e * e
+                    n += 1
+                else:
+                    e = 0.0
+                L, Tt, s[q] = lt + al * e, Tt + al * be * e, s[q] + ga * (1 - al) * e
+            if i == last:
+                l, t = L, Tt
+    return sse, n
+
+
+@pytest.mark.parametrize("m,C,gap", [(48, 3, False), (48, 3, True), (50, 2, True), (40, 1, False)])
+def test_hw_scan_algebra_matches_serial_reference(m, C, gap):
+    """The chunked scan (fast path, explicit-matrix path on a lap with a gap,
+    partial last laps, an inexact chunk) reproduces the serial recursion."""
+    T = 5 * m + 17
+    x = _seasonal(3, T, period=m, seed=4)
+    x[1, :11] = np.nan                      # ragged start: every lap shifted, partial last lap
+    if gap:
+        x[2, 2 * m + 5] = np.nan            # a lap with a missing sample
+        x[0, 3 * m + 1:3 * m + 4] = np.nan
+    grid = SM.default_grid(2)[[0, 13, 26]]
+    _, _, _, sse0 = SM.ref_es_fit(x, 2, 5, m, grid)
+    for r in range(3):
+        for g, (a, b, c) in enumerate(grid):
+            sse, n = _hw_scan_sim(x[r].astype(np.float64), float(a), float(b), float(c), m, C)
+            np.testing.assert_allclose(sse, sse0[r, g], rtol=1e-4)
+
+
+def test_hw_scan_supported_shapes():
+    assert SM.hw_scan_supported(10080, 27, 1440)
+    assert SM.hw_scan_supported(10080, 27, 288)
+    assert not SM.hw_scan_supported(10080, 27, 24)          # short season: the serial kernel
+    assert not SM.hw_scan_supported(10080, 40, 1440)        # > 32 candidates
+    assert not SM.hw_scan_supported(2000, 27, 1440)         # needs two seasons
+    assert not SM.hw_scan_supported(40000, 27, 1440)        # row beyond 64 KB of LDS
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [288, 1300, 1440])
+def test_gpu_hw_scan_fit_matches_references(cuda, m):
+    """The time-parallel fit (exact chunks at 288 / 1440, masked chunks at
+    1300) against the fp64 oracle and the serial fp32 kernel: gaps (the
+    explicit-matrix scan), a ragged row (partial last lap), an empty row."""
+    T = 10080
+    x = _seasonal(48, T, period=m, seed=31)
+    x[:, :] *= np.geomspace(1e-2, 1e4, 48)[:, None].astype(np.float32)
+    x[3, 5000] = np.nan
+    x[4, 7000:7200] = np.nan
+    x[5, :77] = np.nan
+    x[6, :] = np.nan
+    xt = torch.from_numpy(x).to(cuda)
+    assert SM.hw_scan_supported(T, 27, m)
+    sc = SM.es_fit(xt, T, 2, 10, m, method="scan", keep_state=True)
+    se = SM.es_fit(xt, T, 2, 10, m, method="serial", half_season=False, keep_state=True)
+    fc0, sig0, best0, sse0 = SM.ref_es_fit(x, 2, 10, m, SM.default_grid(2))
+    s_c, s_e = sc.sse.cpu().numpy(), se.sse.cpu().numpy()
+    ok = np.isfinite(sse0) & (sse0 > 0)
+    np.testing.assert_allclose(s_c[ok], sse0[ok], rtol=2e-3)
+    np.testing.assert_allclose(s_c[ok], s_e[ok], rtol=2e-3)
+    assert (s_c[6] == 0).all() and sc.best[6].item() == 0
+    bc = sc.best.cpu().numpy()
+    flip = np.flatnonzero(bc != best0)
+    for r in flip:
+        a, b = sse0[r, bc[r]], sse0[r, best0[r]]
+        assert abs(a - b) <= 2e-3 * max(a, b), (r, a, b)
+    same = np.flatnonzero((bc == best0) & np.isfinite(fc0).all(1))
+    amp = np.abs(np.nan_to_num(x[same])).mean(1, keepdims=True)
+    np.testing.assert_allclose(sc.forecast.cpu().numpy()[same] / amp, fc0[same] / amp, atol=2e-3)
+    np.testing.assert_allclose(sc.sigma.cpu().numpy()[same], sig0[same], rtol=2e-3)
+    np.testing.assert_array_equal(sc.nfin.cpu().numpy(), np.isfinite(x).sum(1))
+    # the cached state (model cache) matches the serial kernel's fp32 state
+    both = np.flatnonzero((bc == se.best.cpu().numpy()) & np.isfinite(fc0).all(1))
+    st_c, st_e = sc.model.state.cpu().numpy()[both], se.model.state.cpu().numpy()[both]
+    np.testing.assert_allclose(st_c[:, 2], st_e[:, 2])
+    scale = np.abs(np.nan_to_num(x[both])).mean(1, keepdims=True)
+    np.testing.assert_allclose(sc.model.season.cpu().numpy()[both] / scale,
+                               se.model.season.cpu().numpy()[both] / scale, atol=2e-3)
+    np.testing.assert_array_equal(sc.model.nobs.cpu().numpy()[both], se.model.nobs.cpu().numpy()[both])
