@@ -81,7 +81,23 @@ constexpr int kMaxG = 32;           // candidates per row (<= 16 waves of two)
 
 }  // namespace
 
-// LDS: xs[Tp + 64 C] (the row, NaN-padded) | pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | sse[32] | base
+// Row layout in LDS: sample t >= base (the row's first finite sample) sits at
+// xs[pad(t - base)], pad(r) = r + (r >> S) with S = ctz(C) (C = 2^S * odd,
+// S >= 2, m a multiple of C; S = 31 -- no padding -- otherwise).  A lane's chunk then starts
+// o (2^S + 1) words after its left neighbour's (o = C / 2^S): an odd stride,
+// so the 32 lanes of a ds_read_b32 group hit 32 different banks (a stride of
+// C = 24 words put them on 4 banks: 8-way conflicts, half the fit's time).
+// Lap starts are multiples of m = (lanes) * C past base in the exact case, so
+// the within-chunk offsets j + (j >> S) are compile-time immediates.
+template <int C, bool EXACT>
+struct RowPad {
+  static constexpr int S = (EXACT && C % 4 == 0) ? __builtin_ctz(C) : 31;
+  static __device__ __forceinline__ int at(int r) { return r + (r >> S); }
+  static __host__ __device__ constexpr int words(int r) { return r + (S < 31 ? (r >> S) : 0) + 1; }
+};
+
+// LDS: xs[pad(T - base + 64 C)] (the row from base on, NaN-padded) |
+// pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | sse[32] | base
 template <int C, bool EXACT>
 __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restrict__ x, int64_t ld, int T,
                                                            const float* __restrict__ cand, int G, int m, int H,
@@ -90,11 +106,11 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
                                                            float* __restrict__ sigma, int* __restrict__ best,
                                                            int* __restrict__ nfin, float* __restrict__ sscale,
                                                            float* __restrict__ season_out, int xal) {
+  using RP = RowPad<C, EXACT>;
   extern __shared__ float lds[];
   const int64_t row = blockIdx.x;
   const int GP = (G + 1) >> 1;
-  const int Tp = (T + 3) & ~3;
-  const int Tx = Tp + 64 * C;               // row + NaN padding for the last lap's tail
+  const int Tx = (RP::words(T + 64 * C) + 3) & ~3;   // padded row + NaN tail for the last lap
   float* xs = lds;
   f2* pw = reinterpret_cast<f2*>(lds + Tx);
   float* sse_s = lds + Tx + GP * kLevels * 8;
@@ -103,7 +119,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   const int lane = lane_id(), w = wave_id();
   const float* xr = x + row * ld;
 
-  // ---- stage the row in LDS; its first finite sample by LDS atomic min
+  // ---- the row's first finite sample (LDS atomic min), then the row from
+  // there on into LDS (the second read of the row hits L2)
   if (tid == 0) *ibase = T;
   __syncthreads();
   int fmin = T;
@@ -111,27 +128,23 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     for (int i = tid * 4; i < T; i += nth * 4) {
       if (i + 4 <= T) {
         const float4 v = *reinterpret_cast<const float4*>(xr + i);
-        *reinterpret_cast<float4*>(xs + i) = v;
         const int f = isfinite(v.x) ? 0 : isfinite(v.y) ? 1 : isfinite(v.z) ? 2 : isfinite(v.w) ? 3 : 4;
-        fmin = min(fmin, i + f < T && f < 4 ? i + f : T);
+        if (f < 4) fmin = min(fmin, i + f);
       } else {
-        for (int k = i; k < T; ++k) {
-          const float v = xr[k];
-          xs[k] = v;
-          if (isfinite(v)) fmin = min(fmin, k);
-        }
+        for (int k = i; k < T; ++k)
+          if (isfinite(xr[k])) fmin = min(fmin, k);
       }
     }
   } else {
-    for (int i = tid; i < T; i += nth) {
-      const float v = xr[i];
-      xs[i] = v;
-      if (isfinite(v)) fmin = min(fmin, i);
-    }
+    for (int i = tid; i < T; i += nth)
+      if (isfinite(xr[i])) fmin = min(fmin, i);
   }
-  for (int i = T + tid; i < Tp + 64 * C; i += nth) xs[i] = __builtin_nanf("");
   fmin = wave_min(fmin);
   if (lane == 0) atomicMin(ibase, fmin);
+  __syncthreads();
+  const int base = *ibase;
+  for (int i = base + tid; i < T; i += nth) xs[RP::at(i - base)] = xr[i];
+  for (int r = T - base + tid; r < T - base + 64 * C; r += nth) xs[RP::at(r)] = __builtin_nanf("");
 
   // ---- per wave: two candidates, A = J - k 1^T and its lane-uniform powers
   const int ga = 2 * w, gb = 2 * w + 1 < G ? 2 * w + 1 : 2 * w;
@@ -152,7 +165,6 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     }
   }
   __syncthreads();
-  const int base = *ibase;
 
   // ---- initial state: level = mean of the first season, trend = (mean of the
   // second - mean of the first) / m, seasonal indices from the first season
@@ -165,13 +177,13 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     float sa = 0.f, sb = 0.f;
     int ca = 0, cb = 0;
     for (int i = base + lane; i < e1; i += FM_WAVE) {
-      const float v = xs[i];
+      const float v = xs[RP::at(i - base)];
       const bool f = isfinite(v);
       sa += f ? v : 0.f;
       ca += f;
     }
     for (int i = e1 + lane; i < e2; i += FM_WAVE) {
-      const float v = xs[i];
+      const float v = xs[RP::at(i - base)];
       const bool f = isfinite(v);
       sb += f ? v : 0.f;
       cb += f;
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       const int q = q0 + j;
-      const float v = (q < m && base + q < T) ? xs[base + q] : __builtin_nanf("");
+      const float v = (q < m && base + q < T) ? xs[RP::at(q)] : __builtin_nanf("");
       const float si = isfinite(v) ? v - m1 : 0.f;
       s[j] = (f2){si, si};
     }
@@ -212,7 +224,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     const int nact = min(m, T - tl);
     const int last = (nact - 1) / C;          // lane holding the lap's last step
     const int cnt = nact - q0;                // active steps of this lane (may be <= 0 or > C)
-    const float* xl = xs + tl + q0;   // reassigned for pass 2
+    const float* xl = xs + RP::at(tl - base + q0);   // reassigned for pass 2
     // lane 0 folds the lap's entering state into its chunk, so the scanned
     // prefix of lanes 0..i-1 IS the state entering lane i (no carry matrix)
     const f2 l0 = lane == 0 ? l : zero, t0v = lane == 0 ? tr : zero;
@@ -221,7 +233,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
-      const float xq = xl[j];
+      const float xq = xl[j + (j >> RP::S)];
       bad |= !isfinite(xq);
       const f2 u = xq - s[j];
       const f2 wb = b0 + b1;
@@ -251,7 +263,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
-        const float xq = xl[j];
+        const float xq = xl[j + (j >> RP::S)];
         const bool fin = j < cnt && isfinite(xq);
         const f2 u = xq - s[j];
         const f2 wb = b0 + b1;
@@ -282,7 +294,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     if (lane == 0) { L = l; Tt = tr; }
     // re-read the lap's samples (an opaque offset: otherwise the compiler keeps
     // pass 1's C loads live across the scan)
-    int xo = tl + q0;
+    int xo = RP::at(tl - base + q0);
     asm volatile("" : "+v"(xo));
     xl = xs + xo;
     f2 acc = zero;
@@ -293,7 +305,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
-        const float xq = xl[j];
+        const float xq = xl[j + (j >> RP::S)];
         const f2 lt = L + Tt;
         const f2 e = xq - (lt + s[j]);
         L = __builtin_elementwise_fma(al, e, lt);
@@ -308,7 +320,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
-        const float xq = xl[j];
+        const float xq = xl[j + (j >> RP::S)];
         const bool fin = isfinite(xq);
         const f2 lt = L + Tt;
         const f2 pred = lt + s[j];
@@ -326,7 +338,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
-        const float xq = xl[j];
+        const float xq = xl[j + (j >> RP::S)];
         const bool act = j < cnt;
         const bool fin = act && isfinite(xq);
         const f2 lt = __builtin_elementwise_fma(Tt, (f2){act ? 1.f : 0.f, act ? 1.f : 0.f}, L);
@@ -450,7 +462,9 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
       if (c >= need) { C = c; break; }
   if (C == 0 || m < 3 * 64) return (int)hipErrorInvalidValue;
   const int GP = (G + 1) / 2;
-  const size_t lds = (size_t)(((T + 3) & ~3) + 64 * C) * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16;
+  const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
+  const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
+  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16;
   if (lds > 65536) return (int)hipErrorInvalidValue;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \

@@ -62,12 +62,10 @@ HALF_SEASON_MIN_M = 1000     # <= ~10 laps of a 7-day history: measured within 2
 
 # csrc/kernels/hw_scan.hip: lanes take chunks of these many steps of a season lap
 _SCAN_CHUNKS = (4, 5, 6, 8, 12, 16, 20, 23, 24)
-# "auto" picks the scan fit up to this season length: 40k rows x 10,080 steps,
-# m = 288: 11.3 vs 14.6 ms (10k rows: 2.9 vs 4.8); m = 1440: 8.2 vs 7.9 ms
-# (10k: 2.1 vs 2.4); m = 1008: 12.5 vs 8.6 ms (tools/hw_scan_ab.py,
-# profiles/hw_scan_ab_r3.jsonl).  Longer seasons keep the serial fp16-scratch
-# kernel unless method="scan".
-SCAN_AUTO_MAX_M = 768
+# "auto" picks the scan fit wherever it covers the shape: 40k rows x 10,080
+# steps, m = 1440: 6.35 vs 7.93 ms (serial fp16-scratch kernel); m = 1008:
+# 6.47 vs 8.66; m = 288: 11.6 vs 14.7; 10k rows: 1.4-1.6x (tools/hw_scan_ab.py,
+# profiles/hw_scan_ab_r3.jsonl)
 
 
 def hw_scan_supported(T: int, G: int, m: int) -> bool:
@@ -80,7 +78,11 @@ def hw_scan_supported(T: int, G: int, m: int) -> bool:
     cs = [c for c in _SCAN_CHUNKS if c >= need and m % c == 0] or [c for c in _SCAN_CHUNKS if c >= need]
     if not cs:
         return False
-    lds = (((T + 3) & ~3) + 64 * cs[0]) * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16
+    C = cs[0]
+    n = T + 64 * C
+    S = (C & -C).bit_length() - 1 if (m % C == 0 and C % 4 == 0) else None    # bank-skew padding shift
+    words = (n + (n >> S if S is not None else 0) + 1 + 3) & ~3
+    lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16
     return lds <= 65536
 
 
@@ -91,8 +93,8 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     ``keep_state`` the best candidate's fitted state is returned as an
     :class:`ESState` (for the model cache).
 
-    GPU additive Holt-Winters with ``method="scan"`` (and "auto" up to
-    ``SCAN_AUTO_MAX_M``) runs the time-parallel scan fit
+    GPU additive Holt-Winters (``method`` "auto" / "scan") runs the
+    time-parallel scan fit
     (csrc/kernels/hw_scan.hip: seasons in registers, no seasonal scratch
     traffic) where :func:`hw_scan_supported`; otherwise the serial grid kernels
     (csrc/kernels/smoothing.hip), whose [m][R*G] seasonal scratch is fp16
@@ -122,8 +124,7 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     d = x.device
     cand = torch.from_numpy(grid).to(d)
     P = R * G
-    scan = kind == 2 and (method == "scan" or (method == "auto" and m <= SCAN_AUTO_MAX_M)) \
-        and hw_scan_supported(T, G, m)
+    scan = kind == 2 and method != "serial" and hw_scan_supported(T, G, m)
     check(scan or method != "scan", f"the scan fit does not cover T={T}, G={G}, m={m}")
     if scan:
         return _hw_scan_fit(x, T, R, cand, G, m, H, keep_state)

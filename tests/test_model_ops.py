@@ -541,8 +541,8 @@ def test_gpu_es_fit_half_season_matches_fp32(cuda, kind, m):
     x[:, :] *= np.geomspace(1e-3, 1e5, 64)[:, None].astype(np.float32)     # wide dynamic range across rows
     x[5, :300] = np.nan
     xt = torch.from_numpy(x).to(cuda)
-    h = SM.es_fit(xt, T, kind, 10, m, half_season=True)
-    f = SM.es_fit(xt, T, kind, 10, m, half_season=False)
+    h = SM.es_fit(xt, T, kind, 10, m, half_season=True, method="serial")
+    f = SM.es_fit(xt, T, kind, 10, m, half_season=False, method="serial")
     s_h, s_f = h.sse.cpu().numpy(), f.sse.cpu().numpy()
     stable = s_f < 1e3 * np.median(s_f, axis=1, keepdims=True)
     np.testing.assert_allclose(s_h[stable], s_f[stable], rtol=2e-3)
