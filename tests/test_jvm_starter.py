@@ -1,0 +1,53 @@
+"""The JVM starter (jvm/foremast-spring-boot-k8s-metrics-starter, source-only:
+no JDK in this image) is checked against the Python emitter it mirrors: the
+same k8s.metrics.* properties with the same defaults, and the same meter-name
+normalisation rule."""
+import re
+from dataclasses import fields
+from pathlib import Path
+
+from foremast_amd.emitter import metrics as EM
+
+ROOT = Path(__file__).resolve().parent.parent / "jvm" / "foremast-spring-boot-k8s-metrics-starter"
+SRC = ROOT / "src" / "main" / "java" / "ai" / "foremast" / "metrics" / "k8s" / "starter"
+
+
+def _java_fields():
+    txt = (SRC / "K8sMetricsProperties.java").read_text()
+    out = {}
+    for typ, name, default in re.findall(r"private (String|boolean) (\w+)(?: = ([^;]+))?;", txt):
+        snake = re.sub(r"([A-Z])", lambda m: "_" + m.group(1).lower(), name)
+        if default is None or default == "":
+            val = None
+        elif typ == "boolean":
+            val = default.strip() == "true"
+        else:
+            val = default.strip().strip('"')
+        out[snake] = val
+    return out
+
+
+def test_properties_match_python_emitter():
+    jf = _java_fields()
+    py = {f.name: f.default for f in fields(EM.K8sMetricsProperties) if isinstance(f.default, (str, bool, type(None)))}
+    shared = set(jf) & set(py)
+    assert {"common_tag_name_value_pairs", "initialize_for_statuses", "caller_header",
+            "enable_common_metrics_filter", "enable_common_metrics_filter_action", "common_metrics_whitelist",
+            "common_metrics_blacklist", "common_metrics_prefix", "common_metrics_tag_rules"} <= shared
+    for k in shared:
+        assert jf[k] == py[k], (k, jf[k], py[k])
+
+
+def test_meter_name_rule_matches():
+    txt = (SRC / "MeterGate.java").read_text()
+    suffixes = re.search(r'new String\[\] \{([^}]*)\}', txt).group(1)
+    java = [s.strip().strip('"') for s in suffixes.split(",")]
+    assert tuple(java) == EM._UNIT_SUFFIXES
+    assert EM._meter_name("http_server_requests_seconds") == "http.server.requests"
+
+
+def test_autoconfiguration_registered():
+    imports = (ROOT / "src" / "main" / "resources" / "META-INF" / "spring" /
+               "org.springframework.boot.autoconfigure.AutoConfiguration.imports").read_text().split()
+    for cls in imports:
+        assert (SRC / (cls.rsplit(".", 1)[1] + ".java")).exists(), cls
