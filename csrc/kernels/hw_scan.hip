@@ -77,32 +77,6 @@ __device__ __forceinline__ f2 rdl(f2 v, int l) {
 }
 
 constexpr int kLevels = 6;          // log2(64) scan levels
-
-// DPP row_shr:D with zero for lanes whose source lies before their 16-lane row
-template <int D>
-__device__ __forceinline__ float row_shr(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x110 + D, 0xF, 0xF,
-                                                               false));
-}
-template <int D>
-__device__ __forceinline__ f2 row_shr2(f2 v) {
-  const float a = v.x, b = v.y;
-  return (f2){row_shr<D>(a), row_shr<D>(b)};
-}
-
-// Hillis-Steele inside each 16-lane row over affine chunk maps with
-// lane-uniform powers pw[lv] = A^{C 2^lv}: b_i += A^{C d} b_{i-d}
-__device__ __forceinline__ void row_scan(f2& b0, f2& b1, const f2* pw) {
-#define FM_ROW_LEVEL(LV, D)                                                            \
-  {                                                                                    \
-    const f2 n0 = row_shr2<D>(b0), n1 = row_shr2<D>(b1);                               \
-    const f2 p0 = pw[LV * 4 + 0], p1 = pw[LV * 4 + 1], p2 = pw[LV * 4 + 2], p3 = pw[LV * 4 + 3]; \
-    b0 = b0 + p0 * n0 + p1 * n1;                                                       \
-    b1 = b1 + p2 * n0 + p3 * n1;                                                       \
-  }
-  FM_ROW_LEVEL(0, 1) FM_ROW_LEVEL(1, 2) FM_ROW_LEVEL(2, 4) FM_ROW_LEVEL(3, 8)
-#undef FM_ROW_LEVEL
-}
 constexpr int kMaxG = 32;           // candidates per row (<= 16 waves of two)
 
 }  // namespace
@@ -270,27 +244,17 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     // only the lanes before the last active one feed the scan
     if (!__any(bad && lane < last)) {
       // those chunks are full and finite: lane i's window at level d is
-      // A^{C d}, the same for every lane >= d.  Scan inside each 16-lane row
-      // on DPP (no LDS round trips), carry the row totals across rows with
-      // A^{16 C}, inject each row's carry into its first chunk and scan the
-      // rows again.
-      const f2 ob0 = b0, ob1 = b1;
-      row_scan(b0, b1, pwv);
-      const f2 r15a = rdl(b0, 15), r15b = rdl(b1, 15), r31a = rdl(b0, 31), r31b = rdl(b1, 31);
-      const f2 r47a = rdl(b0, 47), r47b = rdl(b1, 47);
-      const f2 q0 = pwv[16], q1 = pwv[17], q2 = pwv[18], q3 = pwv[19];       // A^{16 C}
-      const f2 c31a = r31a + q0 * r15a + q1 * r15b, c31b = r31b + q2 * r15a + q3 * r15b;
-      const f2 c47a = r47a + q0 * c31a + q1 * c31b, c47b = r47b + q2 * c31a + q3 * c31b;
-      // the first lane of row r (r >= 1) takes A^C carry_r + its own chunk
-      const int rw = lane >> 4;
-      const bool head = (lane & 15) == 0 && rw > 0;
-      const f2 ka = rw == 1 ? r15a : rw == 2 ? c31a : c47a;
-      const f2 kb = rw == 1 ? r15b : rw == 2 ? c31b : c47b;
-      const f2 p0 = pwv[0], p1 = pwv[1], p2 = pwv[2], p3 = pwv[3];
-      const f2 ia = ob0 + p0 * ka + p1 * kb, ib = ob1 + p2 * ka + p3 * kb;
-      b0 = (f2){head ? ia.x : ob0.x, head ? ia.y : ob0.y};
-      b1 = (f2){head ? ib.x : ob1.x, head ? ib.y : ob1.y};
-      row_scan(b0, b1, pwv);
+      // A^{C d}, the same for every lane >= d
+#pragma unroll
+      for (int lv = 0; lv < kLevels; ++lv) {
+        const int d = 1 << lv;
+        const f2 n0 = up(b0, d), n1 = up(b1, d);
+        const f2 p0 = pwv[lv * 4 + 0], p1 = pwv[lv * 4 + 1], p2 = pwv[lv * 4 + 2], p3 = pwv[lv * 4 + 3];
+        if (lane >= d) {
+          b0 = b0 + p0 * n0 + p1 * n1;
+          b1 = b1 + p2 * n0 + p3 * n1;
+        }
+      }
     } else {
       // general chunks: explicit 2x2 maps (missing or inactive step: J, no input)
       M2 Mm = {one, zero, zero, one};

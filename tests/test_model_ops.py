@@ -602,20 +602,11 @@ def _hw_scan_sim(xr, al, be, ga, m, C):
                     M = J @ M
             Ms.append(M)
             bs.append(b)
-        if not bad:        # fast path: in-row scans with A^{C d}, row carries with A^{16 C}
-            def row_scan(B):
-                for d in (1, 2, 4, 8):
-                    P = np.linalg.matrix_power(A, C * d)
-                    B = [B[i] + P @ B[i - d] if i % 16 >= d else B[i] for i in range(64)]
-                return B
-            R = row_scan([b.copy() for b in bs])
-            A16 = np.linalg.matrix_power(A, 16 * C)
-            c31 = R[31] + A16 @ R[15]
-            carry = {1: R[15], 2: c31, 3: R[47] + A16 @ c31}
+        if not bad:        # fast path: lane i's window at level d is A^{C d}
             B = [b.copy() for b in bs]
-            for r in (1, 2, 3):
-                B[16 * r] = B[16 * r] + np.linalg.matrix_power(A, C) @ carry[r]
-            B = row_scan(B)
+            for d in (1, 2, 4, 8, 16, 32):
+                P = np.linalg.matrix_power(A, C * d)
+                B = [B[i] + P @ B[i - d] if i >= d else B[i] for i in range(64)]
         else:
             B, M = [b.copy() for b in bs], [x.copy() for x in Ms]
             for d in (1, 2, 4, 8, 16, 32):
