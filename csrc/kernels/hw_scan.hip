@@ -78,7 +78,6 @@ __device__ __forceinline__ f2 rdl(f2 v, int l) {
 
 constexpr int kLevels = 6;          // log2(64) scan levels
 constexpr int kMaxG = 32;           // candidates per row (<= 16 waves of two)
-constexpr int kMaxLaps = 128;       // season laps per row (T / m)
 
 }  // namespace
 
@@ -98,8 +97,7 @@ struct RowPad {
 };
 
 // LDS: xs[pad(T - base + 64 C)] (the row from base on, NaN-padded) |
-// pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | cw[GP][C][2] f2 (pass-1 coefficients
-// A^{C-1-j} k per wave) | sse[32] | base, pad[3] | lap NaN flags[kMaxLaps] | wave sums[16][4]
+// pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | sse[32] | base
 template <int C, bool EXACT>
 __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restrict__ x, int64_t ld, int T,
                                                            const float* __restrict__ cand, int G, int m, int H,
@@ -115,11 +113,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   const int Tx = (RP::words(T + 64 * C) + 3) & ~3;   // padded row + NaN tail for the last lap
   float* xs = lds;
   f2* pw = reinterpret_cast<f2*>(lds + Tx);
-  f2* cw = pw + GP * kLevels * 4;
-  float* sse_s = reinterpret_cast<float*>(cw + GP * C * 2);
+  float* sse_s = lds + Tx + GP * kLevels * 8;
   int* ibase = reinterpret_cast<int*>(sse_s + kMaxG);
-  int* lapnan = ibase + 4;
-  float* wsum = reinterpret_cast<float*>(lapnan + kMaxLaps);
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = lane_id(), w = wave_id();
   const float* xr = x + row * ld;
@@ -127,7 +122,6 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // ---- the row's first finite sample (LDS atomic min), then the row from
   // there on into LDS (the second read of the row hits L2)
   if (tid == 0) *ibase = T;
-  for (int i = tid; i < kMaxLaps; i += nth) lapnan[i] = 0;
   __syncthreads();
   int fmin = T;
   if (xal) {
@@ -149,11 +143,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   if (lane == 0) atomicMin(ibase, fmin);
   __syncthreads();
   const int base = *ibase;
-  for (int i = base + tid; i < T; i += nth) {
-    const float v = xr[i];
-    xs[RP::at(i - base)] = v;
-    if (!isfinite(v) && i >= base + m) lapnan[(i - base - m) / m] = 1;   // that lap takes the general scan
-  }
+  for (int i = base + tid; i < T; i += nth) xs[RP::at(i - base)] = xr[i];
   for (int r = T - base + tid; r < T - base + 64 * C; r += nth) xs[RP::at(r)] = __builtin_nanf("");
 
   // ---- per wave: two candidates, A = J - k 1^T and its lane-uniform powers
@@ -163,12 +153,9 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
   const f2 ab = al * be, gs = gm * (one - al);
   const M2 A = {one - al, one - al, -ab, one - ab};
-  M2 Q = {one, zero, zero, one}, Pw = A;
-#pragma unroll
-  for (int k = C; k > 0; k >>= 1) {                    // A^C by squaring
-    if (k & 1) Q = mmul(Q, Pw);
-    Pw = mmul(Pw, Pw);
-  }
+  M2 Q = A;
+#pragma unroll 1
+  for (int k = 1; k < C; ++k) Q = mmul(Q, A);          // A^C
   if (lane == 0) {
 #pragma unroll 1
     for (int lv = 0; lv < kLevels; ++lv) {             // A^{C 2^lv}
@@ -176,33 +163,9 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       p[0] = Q.a; p[1] = Q.b; p[2] = Q.c; p[3] = Q.d;
       Q = mmul(Q, Q);
     }
-    // pass 1 folds a chunk as sum_j c_j u_j with c_j = A^{C-1-j} k
-    f2 c0 = al, c1 = ab;
-    f2* cwv = cw + w * C * 2;
-#pragma unroll 1
-    for (int j = C - 1; j >= 0; --j) {
-      cwv[2 * j] = c0;
-      cwv[2 * j + 1] = c1;
-      const f2 n0 = A.a * c0 + A.b * c1, n1 = A.c * c0 + A.d * c1;
-      c0 = n0;
-      c1 = n1;
-    }
-  }
-  __syncthreads();                         // the staged row, powers and coefficients
-  // first- and second-season sums, split over the workgroup's waves
-  if (base < T) {
-    const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
-    float sa = 0.f, sb = 0.f, ca = 0.f, cb = 0.f;
-    for (int i = base + tid; i < e2; i += nth) {
-      const float v = xs[RP::at(i - base)];
-      const bool f = isfinite(v);
-      if (i < e1) { sa += f ? v : 0.f; ca += f ? 1.f : 0.f; }
-      else { sb += f ? v : 0.f; cb += f ? 1.f : 0.f; }
-    }
-    sa = wave_sum(sa); sb = wave_sum(sb); ca = wave_sum(ca); cb = wave_sum(cb);
-    if (lane == 0) { wsum[4 * w] = sa; wsum[4 * w + 1] = sb; wsum[4 * w + 2] = ca; wsum[4 * w + 3] = cb; }
   }
   __syncthreads();
+
   // ---- initial state: level = mean of the first season, trend = (mean of the
   // second - mean of the first) / m, seasonal indices from the first season
   f2 l, tr;
@@ -210,11 +173,22 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   f2 s[C];
   const int q0 = lane * C;
   if (base < T) {
-    float sa = 0.f, sb = 0.f, fa = 0.f, fb = 0.f;
-    for (int v = 0; v < GP; ++v) {
-      sa += wsum[4 * v]; sb += wsum[4 * v + 1]; fa += wsum[4 * v + 2]; fb += wsum[4 * v + 3];
+    const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
+    float sa = 0.f, sb = 0.f;
+    int ca = 0, cb = 0;
+    for (int i = base + lane; i < e1; i += FM_WAVE) {
+      const float v = xs[RP::at(i - base)];
+      const bool f = isfinite(v);
+      sa += f ? v : 0.f;
+      ca += f;
     }
-    const int ca = (int)fa, cb = (int)fb;
+    for (int i = e1 + lane; i < e2; i += FM_WAVE) {
+      const float v = xs[RP::at(i - base)];
+      const bool f = isfinite(v);
+      sb += f ? v : 0.f;
+      cb += f;
+    }
+    sa = wave_sum(sa); sb = wave_sum(sb); ca = wave_sum(ca); cb = wave_sum(cb);
     const float m1 = ca > 0 ? sa / ca : 0.f, m2 = cb > 0 ? sb / cb : 0.f;
     const float trd = cb > 0 ? (m2 - m1) / m : 0.f;
     l = (f2){m1, m1};
@@ -254,24 +228,21 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     // lane 0 folds the lap's entering state into its chunk, so the scanned
     // prefix of lanes 0..i-1 IS the state entering lane i (no carry matrix)
     const f2 l0 = lane == 0 ? l : zero, t0v = lane == 0 ? tr : zero;
-    const bool gaps = lapnan[(tl - base - m) / m] != 0;    // a missing sample in this lap
-    f2 b0, b1;
-    if (!gaps) {
-      // chunk map b = A^C v0 + sum_j c_j (x_j - s_j): 3 packed ops per step
-      const f2* cwv = cw + w * C * 2;
-      const f2 p0 = pwv[0], p1 = pwv[1], p2 = pwv[2], p3 = pwv[3];
-      b0 = p0 * l0 + p1 * t0v;
-      b1 = p2 * l0 + p3 * t0v;
+    bool bad = false;
+    f2 b0 = l0, b1 = t0v;
 #pragma unroll
-      for (int j = 0; j < C; ++j) {
-        if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
-        const float xq = xl[j + (j >> RP::S)];
-        const f2 u = xq - s[j];
-        b0 = __builtin_elementwise_fma(cwv[2 * j], u, b0);
-        b1 = __builtin_elementwise_fma(cwv[2 * j + 1], u, b1);
-      }
+    for (int j = 0; j < C; ++j) {
+      if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
+      const float xq = xl[j + (j >> RP::S)];
+      bad |= !isfinite(xq);
+      const f2 u = xq - s[j];
+      const f2 wb = b0 + b1;
+      const f2 e = u - wb;
+      b0 = __builtin_elementwise_fma(al, e, wb);
+      b1 = __builtin_elementwise_fma(ab, e, b1);
     }
-    if (!gaps) {
+    // only the lanes before the last active one feed the scan
+    if (!__any(bad && lane < last)) {
       // those chunks are full and finite: lane i's window at level d is
       // A^{C d}, the same for every lane >= d
 #pragma unroll
@@ -328,7 +299,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     xl = xs + xo;
     f2 acc = zero;
     int nn = 0;
-    if (EXACT && nact == m && !gaps) {
+    if (EXACT && nact == m && !__any(bad && q0 < m)) {
       // full lap without a missing sample, m = C * (lanes in use): no
       // inactive or missing step in a used lane, so no per-step select
 #pragma unroll
@@ -453,27 +424,11 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 namespace {
 constexpr int kChunks[] = {4, 5, 6, 8, 12, 16, 20, 23, 24};
 
-constexpr size_t kMaxLds = 160 * 1024;   // a single gfx950 workgroup may take the whole LDS
-
-template <int C, bool EXACT>
-void allow_big_lds() {
-  static bool done = false;            // once per instantiation (idempotent if raced)
-  if (!done) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(hw_scan_fit_kernel<C, EXACT>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
-    done = true;
-  }
-}
-
 template <int C>
 int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
                float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
                float* season_out, size_t lds, int xal, hipStream_t stream) {
   const int GP = (G + 1) / 2;
-  if (lds > 65536) {
-    if (m % C == 0) allow_big_lds<C, true>();
-    else allow_big_lds<C, false>();
-  }
   if (m % C == 0)
     hipLaunchKernelGGL((hw_scan_fit_kernel<C, true>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, cand, G,
                        m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);
@@ -492,7 +447,7 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
 // candidate's seasonal indices [R, m] by absolute phase.  Returns
 // hipErrorInvalidValue for shapes it does not cover (the caller then uses the
 // serial kernel): m > 64 * 24 or m < 192 (chunks of 4..24 steps per lane),
-// G > 32, 2 m > T, more than 128 laps or a row beyond the 160 KB of LDS.
+// G > 32, 2 m > T, or a row larger than 64 KB of LDS.
 FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H,
                           float* sse, float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin,
                           float* sscale, float* season_out, hipStream_t stream) {
@@ -509,9 +464,8 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   const int GP = (G + 1) / 2;
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
-  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + (size_t)GP * C * 4 * 4 + kMaxG * 4 + 16 +
-                     kMaxLaps * 4 + 16 * 4 * 4;
-  if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return (int)hipErrorInvalidValue;
+  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16;
+  if (lds > 65536) return (int)hipErrorInvalidValue;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \

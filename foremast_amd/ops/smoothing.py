@@ -70,10 +70,9 @@ _SCAN_CHUNKS = (4, 5, 6, 8, 12, 16, 20, 23, 24)
 
 def hw_scan_supported(T: int, G: int, m: int) -> bool:
     """Shapes the time-parallel additive Holt-Winters fit covers (mirrors
-    ``fm_hw_scan_fit``'s checks): 192 <= m <= 64 * 24, G <= 32, 2 m <= T,
-    fewer than 128 season laps and the row (+ NaN padding for the last lap)
-    within the 160 KB a gfx950 workgroup may allocate."""
-    if not (1 <= G <= 32 and 192 <= m and 2 * m <= T and (T - m) // m < 128):
+    ``fm_hw_scan_fit``'s checks): 192 <= m <= 64 * 24, G <= 32, 2 m <= T and
+    the row (+ NaN padding for the last lap) within 64 KB of LDS."""
+    if not (1 <= G <= 32 and 192 <= m and 2 * m <= T):
         return False
     need = -(-m // 64)
     cs = [c for c in _SCAN_CHUNKS if c >= need and m % c == 0] or [c for c in _SCAN_CHUNKS if c >= need]
@@ -83,9 +82,8 @@ def hw_scan_supported(T: int, G: int, m: int) -> bool:
     n = T + 64 * C
     S = (C & -C).bit_length() - 1 if (m % C == 0 and C % 4 == 0) else None    # bank-skew padding shift
     words = (n + (n >> S if S is not None else 0) + 1 + 3) & ~3
-    GP = (G + 1) // 2
-    lds = words * 4 + GP * 6 * 8 * 4 + GP * C * 16 + 32 * 4 + 16 + 128 * 4 + 16 * 4 * 4
-    return lds <= 160 * 1024
+    lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16
+    return lds <= 65536
 
 
 def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, grid: np.ndarray | None = None,
