@@ -1,0 +1,527 @@
+// K2: additive Holt-Winters grid fit as a TIME-PARALLEL scan -- variant 2 under
+// measurement (hw_scan.hip is the validated default): pass 1 as sum_j c_j u_j
+// with LDS coefficients, per-lap NaN flags from staging, cooperative season
+// means, A^C by squaring, up to 160 KB of LDS per workgroup.
+//
+// Why: the serial grid fit (smoothing.hip hw2_fit_kernel, one thread per
+// (row, candidate pair) running all T steps) has to park m seasonal indices
+// per candidate somewhere between laps; at the config-2 shape (40k rows x 27
+// candidates x m = 1440) that is 37 GB of fp16 scratch traffic per fit, and
+// the fit sat at 76 % of the read+write HBM floor (profiles/pmc_c2_requests_r3.txt).
+//
+// The additive recursion is LINEAR in its (level, trend) state.  In the
+// one-step error e = x - (l + t + s):
+//     l' = l + t + a e,   t' = t + a b e,   s' = s + g (1 - a) e
+// i.e. v' = A v + k u with v = (l, t), u = x - s, k = (a, a b) and
+// A = J - k 1^T (J = [[1, 1], [0, 1]]); a missing sample gives e = 0, v' = J v.
+// Inside one season lap every seasonal index s(p) is read once, so the lap's
+// inputs u are all known at the lap's start.  One WAVE owns one (row,
+// candidate pair) and splits the lap's m steps into 64 contiguous chunks of C
+// (lane i: lap offsets [iC, iC + C)), keeping its C seasonal indices of both
+// candidates in VGPRs for the whole fit:
+//   pass 1  each lane folds its chunk into an affine map v -> A^C v + b
+//           (zero-state response; lane 0 starts from the lap's entering state
+//           instead of zero; 5 packed ops / step);
+//   scan    Hillis-Steele over the 64 lanes: b_i += A^{C d} b_{i-d}, d = 1..32
+//           (the lane-uniform powers A^{C 2^j} sit in LDS); the prefix of
+//           lanes 0..i-1 is then the (level, trend) entering lane i;
+//   pass 2  the textbook recursion over the chunk from that state, updating
+//           the lane's seasonal indices and the SSE (exactly the serial
+//           kernel's arithmetic).
+// A lap that contains a missing sample (rare: rows are right-aligned, the
+// left NaN padding is skipped via the row's first finite sample) runs pass 1
+// and the scan with explicit 2x2 chunk matrices (J for missing steps).
+//
+// Work per step is ~12 packed VALU ops instead of ~7, but there is no
+// seasonal traffic left: the row's history is staged once in LDS (the 14
+// waves of a row read it from there) and the fit becomes VALU-bound.  One
+// workgroup per row (ceil(G/2) waves): after the fit the workgroup picks the
+// best candidate (hw2_forecast_kernel's rule), and only the winning wave
+// writes its seasons (the model cache's fp32 [R, m] state, by absolute phase)
+// and the H-step forecast.  Seasons stay fp32 end to end (the serial kernel's
+// fp16 scratch rounded them by 2^-11 per lap).
+//
+// Reference: foremast-brain's Holt-Winters model (docs/guides/design.md:62-72,
+// deploy/foremast/3_brain/foremast-brain.yaml ML_ALGORITHM); the recursion and
+// its initialisation follow docs/BRAIN_SPEC.md §3.2 and ops/smoothing.py's
+// fp64 reference (ref_es_fit).
+#include "fm_common.h"
+
+using namespace fm;
+
+namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+struct M2 {      // [[a, b], [c, d]] for two candidates at once
+  f2 a, b, c, d;
+};
+
+__device__ __forceinline__ M2 mmul(const M2& p, const M2& q) {
+  return {p.a * q.a + p.b * q.c, p.a * q.b + p.b * q.d, p.c * q.a + p.d * q.c, p.c * q.b + p.d * q.d};
+}
+
+// value of lane (lane - d) & 63 (callers ignore lanes < d); d = 1 rides DPP wave_shr:1
+__device__ __forceinline__ float up1(float v, int d) {
+  if (d == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(((lane_id() - d) & 63) << 2, __builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ f2 up(f2 v, int d) { return (f2){up1(v.x, d), up1(v.y, d)}; }
+
+// lane l's pair, for every lane.  The halves go through named floats:
+// __builtin_bit_cast of a vector element (bit_cast(int, v.y)) reads the
+// vector's FIRST element with this clang, which silently turned every .y
+// broadcast into a copy of .x.
+__device__ __forceinline__ f2 rdl(f2 v, int l) {
+  const float vx = v.x, vy = v.y;
+  return (f2){__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vx), l)),
+              __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vy), l))};
+}
+
+constexpr int kLevels = 6;          // log2(64) scan levels
+constexpr int kMaxG = 32;           // candidates per row (<= 16 waves of two)
+constexpr int kMaxLaps = 128;       // season laps per row (T / m)
+
+}  // namespace
+
+// Row layout in LDS: sample t >= base (the row's first finite sample) sits at
+// xs[pad(t - base)], pad(r) = r + (r >> S) with S = ctz(C) (C = 2^S * odd,
+// S >= 2, m a multiple of C; S = 31 -- no padding -- otherwise).  A lane's chunk then starts
+// o (2^S + 1) words after its left neighbour's (o = C / 2^S): an odd stride,
+// so the 32 lanes of a ds_read_b32 group hit 32 different banks (a stride of
+// C = 24 words put them on 4 banks: 8-way conflicts, half the fit's time).
+// Lap starts are multiples of m = (lanes) * C past base in the exact case, so
+// the within-chunk offsets j + (j >> S) are compile-time immediates.
+template <int C, bool EXACT>
+struct RowPad {
+  static constexpr int S = (EXACT && C % 4 == 0) ? __builtin_ctz(C) : 31;
+  static __device__ __forceinline__ int at(int r) { return r + (r >> S); }
+  static __host__ __device__ constexpr int words(int r) { return r + (S < 31 ? (r >> S) : 0) + 1; }
+};
+
+// LDS: xs[pad(T - base + 64 C)] (the row from base on, NaN-padded) |
+// pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | cw[GP][C][2] f2 (pass-1 coefficients
+// A^{C-1-j} k per wave) | sse[32] | base, pad[3] | lap NaN flags[kMaxLaps] | wave sums[16][4]
+template <int C, bool EXACT>
+__global__ __launch_bounds__(1024) void hw_scan2_fit_kernel(const float* __restrict__ x, int64_t ld, int T,
+                                                           const float* __restrict__ cand, int G, int m, int H,
+                                                           float* __restrict__ sse, float* __restrict__ state,
+                                                           int* __restrict__ nobs, float* __restrict__ fc,
+                                                           float* __restrict__ sigma, int* __restrict__ best,
+                                                           int* __restrict__ nfin, float* __restrict__ sscale,
+                                                           float* __restrict__ season_out, int xal) {
+  using RP = RowPad<C, EXACT>;
+  extern __shared__ float lds[];
+  const int64_t row = blockIdx.x;
+  const int GP = (G + 1) >> 1;
+  const int Tx = (RP::words(T + 64 * C) + 3) & ~3;   // padded row + NaN tail for the last lap
+  float* xs = lds;
+  f2* pw = reinterpret_cast<f2*>(lds + Tx);
+  f2* cw = pw + GP * kLevels * 4;
+  float* sse_s = reinterpret_cast<float*>(cw + GP * C * 2);
+  int* ibase = reinterpret_cast<int*>(sse_s + kMaxG);
+  int* lapnan = ibase + 4;
+  float* wsum = reinterpret_cast<float*>(lapnan + kMaxLaps);
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int lane = lane_id(), w = wave_id();
+  const float* xr = x + row * ld;
+
+  // ---- the row's first finite sample (LDS atomic min), then the row from
+  // there on into LDS (the second read of the row hits L2)
+  if (tid == 0) *ibase = T;
+  for (int i = tid; i < kMaxLaps; i += nth) lapnan[i] = 0;
+  __syncthreads();
+  int fmin = T;
+  if (xal) {
+    for (int i = tid * 4; i < T; i += nth * 4) {
+      if (i + 4 <= T) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + i);
+        const int f = isfinite(v.x) ? 0 : isfinite(v.y) ? 1 : isfinite(v.z) ? 2 : isfinite(v.w) ? 3 : 4;
+        if (f < 4) fmin = min(fmin, i + f);
+      } else {
+        for (int k = i; k < T; ++k)
+          if (isfinite(xr[k])) fmin = min(fmin, k);
+      }
+    }
+  } else {
+    for (int i = tid; i < T; i += nth)
+      if (isfinite(xr[i])) fmin = min(fmin, i);
+  }
+  fmin = wave_min(fmin);
+  if (lane == 0) atomicMin(ibase, fmin);
+  __syncthreads();
+  const int base = *ibase;
+  for (int i = base + tid; i < T; i += nth) {
+    const float v = xr[i];
+    xs[RP::at(i - base)] = v;
+    if (!isfinite(v) && i >= base + m) lapnan[(i - base - m) / m] = 1;   // that lap takes the general scan
+  }
+  for (int r = T - base + tid; r < T - base + 64 * C; r += nth) xs[RP::at(r)] = __builtin_nanf("");
+
+  // ---- per wave: two candidates, A = J - k 1^T and its lane-uniform powers
+  const int ga = 2 * w, gb = 2 * w + 1 < G ? 2 * w + 1 : 2 * w;
+  const f2 al = {cand[3 * ga], cand[3 * gb]}, be = {cand[3 * ga + 1], cand[3 * gb + 1]},
+           gm = {cand[3 * ga + 2], cand[3 * gb + 2]};
+  const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
+  const f2 ab = al * be, gs = gm * (one - al);
+  const M2 A = {one - al, one - al, -ab, one - ab};
+  M2 Q = {one, zero, zero, one}, Pw = A;
+#pragma unroll
+  for (int k = C; k > 0; k >>= 1) {                    // A^C by squaring
+    if (k & 1) Q = mmul(Q, Pw);
+    Pw = mmul(Pw, Pw);
+  }
+  if (lane == 0) {
+#pragma unroll 1
+    for (int lv = 0; lv < kLevels; ++lv) {             // A^{C 2^lv}
+      f2* p = pw + (w * kLevels + lv) * 4;
+      p[0] = Q.a; p[1] = Q.b; p[2] = Q.c; p[3] = Q.d;
+      Q = mmul(Q, Q);
+    }
+    // pass 1 folds a chunk as sum_j c_j u_j with c_j = A^{C-1-j} k
+    f2 c0 = al, c1 = ab;
+    f2* cwv = cw + w * C * 2;
+#pragma unroll 1
+    for (int j = C - 1; j >= 0; --j) {
+      cwv[2 * j] = c0;
+      cwv[2 * j + 1] = c1;
+      const f2 n0 = A.a * c0 + A.b * c1, n1 = A.c * c0 + A.d * c1;
+      c0 = n0;
+      c1 = n1;
+    }
+  }
+  __syncthreads();                         // the staged row, powers and coefficients
+  // first- and second-season sums, split over the workgroup's waves
+  if (base < T) {
+    const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
+    float sa = 0.f, sb = 0.f, ca = 0.f, cb = 0.f;
+    for (int i = base + tid; i < e2; i += nth) {
+      const float v = xs[RP::at(i - base)];
+      const bool f = isfinite(v);
+      if (i < e1) { sa += f ? v : 0.f; ca += f ? 1.f : 0.f; }
+      else { sb += f ? v : 0.f; cb += f ? 1.f : 0.f; }
+    }
+    sa = wave_sum(sa); sb = wave_sum(sb); ca = wave_sum(ca); cb = wave_sum(cb);
+    if (lane == 0) { wsum[4 * w] = sa; wsum[4 * w + 1] = sb; wsum[4 * w + 2] = ca; wsum[4 * w + 3] = cb; }
+  }
+  __syncthreads();
+  // ---- initial state: level = mean of the first season, trend = (mean of the
+  // second - mean of the first) / m, seasonal indices from the first season
+  f2 l, tr;
+  int c1 = 0;
+  f2 s[C];
+  const int q0 = lane * C;
+  if (base < T) {
+    float sa = 0.f, sb = 0.f, fa = 0.f, fb = 0.f;
+    for (int v = 0; v < GP; ++v) {
+      sa += wsum[4 * v]; sb += wsum[4 * v + 1]; fa += wsum[4 * v + 2]; fb += wsum[4 * v + 3];
+    }
+    const int ca = (int)fa, cb = (int)fb;
+    const float m1 = ca > 0 ? sa / ca : 0.f, m2 = cb > 0 ? sb / cb : 0.f;
+    const float trd = cb > 0 ? (m2 - m1) / m : 0.f;
+    l = (f2){m1, m1};
+    tr = (f2){trd, trd};
+    c1 = ca;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int q = q0 + j;
+      const float v = (q < m && base + q < T) ? xs[RP::at(q)] : __builtin_nanf("");
+      const float si = isfinite(v) ? v - m1 : 0.f;
+      s[j] = (f2){si, si};
+    }
+  } else {
+    l = (f2){__builtin_nanf(""), __builtin_nanf("")};
+    tr = zero;
+#pragma unroll
+    for (int j = 0; j < C; ++j) s[j] = zero;
+  }
+
+  // ---- season laps.  Steps past the lap's end (the last active lane's tail,
+  // later lanes) act as missing samples (e = 0: seasons, SSE and count stay
+  // unchanged), so the step loops carry no per-step branches; xs is padded
+  // with NaN past T so their reads stay inside the allocation.
+  double ea = 0.0, eb = 0.0;
+  int n = 0;
+#pragma unroll 1
+  for (int tl = base + m; tl < T; tl += m) {
+    // re-read the powers every lap (an opaque offset keeps the compiler from
+    // hoisting 24 loop-invariant LDS loads into 48 live VGPRs)
+    int pwo = w * kLevels * 4;
+    asm volatile("" : "+s"(pwo));
+    const f2* pwv = pw + pwo;
+    const int nact = min(m, T - tl);
+    const int last = (nact - 1) / C;          // lane holding the lap's last step
+    const int cnt = nact - q0;                // active steps of this lane (may be <= 0 or > C)
+    const float* xl = xs + RP::at(tl - base + q0);   // reassigned for pass 2
+    // lane 0 folds the lap's entering state into its chunk, so the scanned
+    // prefix of lanes 0..i-1 IS the state entering lane i (no carry matrix)
+    const f2 l0 = lane == 0 ? l : zero, t0v = lane == 0 ? tr : zero;
+    const bool gaps = lapnan[(tl - base - m) / m] != 0;    // a missing sample in this lap
+    f2 b0, b1;
+    if (!gaps) {
+      // chunk map b = A^C v0 + sum_j c_j (x_j - s_j): 3 packed ops per step
+      const f2* cwv = cw + w * C * 2;
+      const f2 p0 = pwv[0], p1 = pwv[1], p2 = pwv[2], p3 = pwv[3];
+      b0 = p0 * l0 + p1 * t0v;
+      b1 = p2 * l0 + p3 * t0v;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
+        const float xq = xl[j + (j >> RP::S)];
+        const f2 u = xq - s[j];
+        b0 = __builtin_elementwise_fma(cwv[2 * j], u, b0);
+        b1 = __builtin_elementwise_fma(cwv[2 * j + 1], u, b1);
+      }
+    }
+    if (!gaps) {
+      // those chunks are full and finite: lane i's window at level d is
+      // A^{C d}, the same for every lane >= d
+#pragma unroll
+      for (int lv = 0; lv < kLevels; ++lv) {
+        const int d = 1 << lv;
+        const f2 n0 = up(b0, d), n1 = up(b1, d);
+        const f2 p0 = pwv[lv * 4 + 0], p1 = pwv[lv * 4 + 1], p2 = pwv[lv * 4 + 2], p3 = pwv[lv * 4 + 3];
+        if (lane >= d) {
+          b0 = b0 + p0 * n0 + p1 * n1;
+          b1 = b1 + p2 * n0 + p3 * n1;
+        }
+      }
+    } else {
+      // general chunks: explicit 2x2 maps (missing or inactive step: J, no input)
+      M2 Mm = {one, zero, zero, one};
+      b0 = l0;
+      b1 = t0v;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
+        const float xq = xl[j + (j >> RP::S)];
+        const bool fin = j < cnt && isfinite(xq);
+        const f2 u = xq - s[j];
+        const f2 wb = b0 + b1;
+        const f2 e = fin ? u - wb : zero;
+        b0 = __builtin_elementwise_fma(al, e, wb);
+        b1 = __builtin_elementwise_fma(ab, e, b1);
+        const f2 ka = fin ? al : zero, kb = fin ? ab : zero;
+        const f2 w0 = Mm.a + Mm.c, w1 = Mm.b + Mm.d;
+        Mm.a = w0 - ka * w0;
+        Mm.b = w1 - ka * w1;
+        Mm.c = Mm.c - kb * w0;
+        Mm.d = Mm.d - kb * w1;
+      }
+#pragma unroll
+      for (int lv = 0; lv < kLevels; ++lv) {
+        const int d = 1 << lv;
+        const M2 nm = {up(Mm.a, d), up(Mm.b, d), up(Mm.c, d), up(Mm.d, d)};
+        const f2 n0 = up(b0, d), n1 = up(b1, d);
+        if (lane >= d) {
+          b0 = b0 + Mm.a * n0 + Mm.b * n1;
+          b1 = b1 + Mm.c * n0 + Mm.d * n1;
+          Mm = mmul(Mm, nm);
+        }
+      }
+    }
+    // exclusive prefix: the (level, trend) entering this lane's chunk
+    f2 L = up(b0, 1), Tt = up(b1, 1);
+    if (lane == 0) { L = l; Tt = tr; }
+    // re-read the lap's samples (an opaque offset: otherwise the compiler keeps
+    // pass 1's C loads live across the scan)
+    int xo = RP::at(tl - base + q0);
+    asm volatile("" : "+v"(xo));
+    xl = xs + xo;
+    f2 acc = zero;
+    int nn = 0;
+    if (EXACT && nact == m && !gaps) {
+      // full lap without a missing sample, m = C * (lanes in use): no
+      // inactive or missing step in a used lane, so no per-step select
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
+        const float xq = xl[j + (j >> RP::S)];
+        const f2 lt = L + Tt;
+        const f2 e = xq - (lt + s[j]);
+        L = __builtin_elementwise_fma(al, e, lt);
+        Tt = __builtin_elementwise_fma(ab, e, Tt);
+        s[j] = __builtin_elementwise_fma(gs, e, s[j]);
+        acc = __builtin_elementwise_fma(e, e, acc);
+      }
+      nn = C;
+      if (q0 >= m) { acc = zero; nn = 0; }   // idle lanes ran the next lap's samples
+    } else if (EXACT && nact == m) {
+      // full lap, m = C * (lanes in use): no inactive step in a used lane
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
+        const float xq = xl[j + (j >> RP::S)];
+        const bool fin = isfinite(xq);
+        const f2 lt = L + Tt;
+        const f2 pred = lt + s[j];
+        const f2 e = fin ? xq - pred : zero;
+        L = __builtin_elementwise_fma(al, e, lt);
+        Tt = __builtin_elementwise_fma(ab, e, Tt);
+        s[j] = __builtin_elementwise_fma(gs, e, s[j]);
+        acc = __builtin_elementwise_fma(e, e, acc);
+        nn += fin ? 1 : 0;
+      }
+      if (q0 >= m) { acc = zero; nn = 0; }   // idle lanes ran the next lap's samples
+    } else {
+      // inactive steps are exact no-ops (lt = L, e = 0), so the last active
+      // lane ends on the lap's end state
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
+        const float xq = xl[j + (j >> RP::S)];
+        const bool act = j < cnt;
+        const bool fin = act && isfinite(xq);
+        const f2 lt = __builtin_elementwise_fma(Tt, (f2){act ? 1.f : 0.f, act ? 1.f : 0.f}, L);
+        const f2 pred = lt + s[j];
+        const f2 e = fin ? xq - pred : zero;
+        L = __builtin_elementwise_fma(al, e, lt);
+        Tt = __builtin_elementwise_fma(ab, e, Tt);
+        s[j] = __builtin_elementwise_fma(gs, e, s[j]);
+        acc = __builtin_elementwise_fma(e, e, acc);
+        nn += fin ? 1 : 0;
+      }
+    }
+    ea += acc.x;
+    eb += acc.y;
+    n += nn;
+    l = rdl(L, last);
+    tr = rdl(Tt, last);
+  }
+  ea = wave_sum(ea);
+  eb = wave_sum(eb);
+  n = wave_sum(n);
+
+  // ---- per-candidate results, then the row's best candidate
+  const float fa = (float)ea, fb = (float)eb;
+  const float tph = (float)(T % m);
+  if (lane == 0) {
+    const int64_t pa = row * G + ga;
+    sse[pa] = fa;
+    state[pa * 3 + 0] = l.x;
+    state[pa * 3 + 1] = tr.x;
+    state[pa * 3 + 2] = tph;
+    nobs[pa] = n;
+    sse_s[ga] = fa;
+    if (2 * w + 1 < G) {
+      const int64_t pb = pa + 1;
+      sse[pb] = fb;
+      state[pb * 3 + 0] = l.y;
+      state[pb * 3 + 1] = tr.y;
+      state[pb * 3 + 2] = tph;
+      nobs[pb] = n;
+      sse_s[gb] = fb;
+    }
+  }
+  __syncthreads();                         // every wave is done with xs too
+  int bg = 0;
+  float bs = sse_s[0];
+  for (int g = 1; g < G; ++g) {
+    const float v = sse_s[g];
+    if (v < bs || !isfinite(bs)) { bs = v; bg = g; }
+  }
+  const bool mine = (bg >> 1) == w;
+  const bool hi = (bg & 1) != 0;
+  if (mine) {
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int q = q0 + j;
+      if (q < m) {
+        int p = (base + q) % m;
+        xs[p] = hi ? s[j].y : s[j].x;     // seasons by absolute phase
+      }
+    }
+  }
+  __syncthreads();
+  if (mine) {
+    const float lb = hi ? l.y : l.x, tb = hi ? tr.y : tr.x;
+    const int t0 = T % m;
+    for (int h = 1 + lane; h <= H; h += FM_WAVE) {
+      int p = t0 + h - 1;
+      p %= m;
+      fc[row * H + (h - 1)] = lb + h * tb + xs[p];
+    }
+    if (season_out != nullptr)
+      for (int p = lane; p < m; p += FM_WAVE) season_out[row * m + p] = xs[p];
+    if (lane == 0) {
+      sigma[row] = n > 1 ? sqrtf(bs / (float)(n - 1)) : 0.f;
+      best[row] = bg;
+      sscale[row] = 1.f;
+      if (nfin != nullptr) nfin[row] = c1 + n;
+    }
+  }
+}
+
+namespace {
+constexpr int kChunks[] = {4, 5, 6, 8, 12, 16, 20, 23, 24};
+
+constexpr size_t kMaxLds = 160 * 1024;   // a single gfx950 workgroup may take the whole LDS
+
+template <int C, bool EXACT>
+void allow_big_lds() {
+  static bool done = false;            // once per instantiation (idempotent if raced)
+  if (!done) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(hw_scan2_fit_kernel<C, EXACT>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
+    done = true;
+  }
+}
+
+template <int C>
+int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
+               float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
+               float* season_out, size_t lds, int xal, hipStream_t stream) {
+  const int GP = (G + 1) / 2;
+  if (lds > 65536) {
+    if (m % C == 0) allow_big_lds<C, true>();
+    else allow_big_lds<C, false>();
+  }
+  if (m % C == 0)
+    hipLaunchKernelGGL((hw_scan2_fit_kernel<C, true>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, cand, G,
+                       m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);
+  else
+    hipLaunchKernelGGL((hw_scan2_fit_kernel<C, false>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, cand,
+                       G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+}  // namespace
+
+// Additive Holt-Winters grid fit + best-candidate forecast in one launch
+// (one workgroup per row).  Same outputs as fm_es_fit(kind = 2) --
+// sse [R, G], state [R*G, 3], nobs [R*G], fc [R, H], sigma / best / nfin [R],
+// sscale [R] (= 1: data units) -- plus, when season_out is not null, the best
+// candidate's seasonal indices [R, m] by absolute phase.  Returns
+// hipErrorInvalidValue for shapes it does not cover (the caller then uses the
+// serial kernel): m > 64 * 24 or m < 192 (chunks of 4..24 steps per lane),
+// G > 32, 2 m > T, more than 128 laps or a row beyond the 160 KB of LDS.
+FM_API int fm_hw_scan2_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H,
+                          float* sse, float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin,
+                          float* sscale, float* season_out, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if (G < 1 || G > kMaxG || m < 2 || 2 * m > T || H < 0) return (int)hipErrorInvalidValue;
+  const int need = (m + 63) / 64;
+  int C = 0;
+  for (int c : kChunks)                      // an exact chunk (no masked steps in full laps) ...
+    if (c >= need && m % c == 0) { C = c; break; }
+  if (C == 0)
+    for (int c : kChunks)                    // ... else the shortest that covers the lap
+      if (c >= need) { C = c; break; }
+  if (C == 0 || m < 3 * 64) return (int)hipErrorInvalidValue;
+  const int GP = (G + 1) / 2;
+  const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
+  const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
+  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + (size_t)GP * C * 4 * 4 + kMaxG * 4 + 16 +
+                     kMaxLaps * 4 + 16 * 4 * 4;
+  if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return (int)hipErrorInvalidValue;
+  const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
+#define FM_HWS(CC)                                                                                         \
+  case CC:                                                                                                 \
+    return launch_one<CC>(x, ld, T, R, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale,    \
+                          season_out, lds, xal, stream);
+  switch (C) {
+    FM_HWS(4) FM_HWS(5) FM_HWS(6) FM_HWS(8) FM_HWS(12) FM_HWS(16) FM_HWS(20) FM_HWS(23) FM_HWS(24)
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FM_HWS
+}

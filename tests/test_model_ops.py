@@ -659,8 +659,9 @@ def test_hw_scan_supported_shapes():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("method", ["scan", "scan2"])
 @pytest.mark.parametrize("m", [288, 1300, 1440])
-def test_gpu_hw_scan_fit_matches_references(cuda, m):
+def test_gpu_hw_scan_fit_matches_references(cuda, m, method):
     """The time-parallel fit (exact chunks at 288 / 1440, masked chunks at
     1300) against the fp64 oracle and the serial fp32 kernel: gaps (the
     explicit-matrix scan), a ragged row (partial last lap), an empty row."""
@@ -672,8 +673,8 @@ def test_gpu_hw_scan_fit_matches_references(cuda, m):
     x[5, :77] = np.nan
     x[6, :] = np.nan
     xt = torch.from_numpy(x).to(cuda)
-    assert SM.hw_scan_supported(T, 27, m)
-    sc = SM.es_fit(xt, T, 2, 10, m, method="scan", keep_state=True)
+    assert SM.hw_scan_supported(T, 27, m) and SM.hw_scan2_supported(T, 27, m)
+    sc = SM.es_fit(xt, T, 2, 10, m, method=method, keep_state=True)
     se = SM.es_fit(xt, T, 2, 10, m, method="serial", half_season=False, keep_state=True)
     fc0, sig0, best0, sse0 = SM.ref_es_fit(x, 2, 10, m, SM.default_grid(2))
     s_c, s_e = sc.sse.cpu().numpy(), se.sse.cpu().numpy()
@@ -699,3 +700,17 @@ def test_gpu_hw_scan_fit_matches_references(cuda, m):
     np.testing.assert_allclose(sc.model.season.cpu().numpy()[both] / scale,
                                se.model.season.cpu().numpy()[both] / scale, atol=2e-3)
     np.testing.assert_array_equal(sc.model.nobs.cpu().numpy()[both], se.model.nobs.cpu().numpy()[both])
+
+
+@pytest.mark.gpu
+def test_gpu_hw_scan2_long_history_big_lds(cuda):
+    """14 days at 1-min resolution: the row needs > 64 KB of LDS (the launch
+    raises the workgroup's dynamic LDS limit); a lap with a gap."""
+    T, m = 20160, 1440
+    x = _seasonal(8, T, period=m, seed=7)
+    x[2, 15000] = np.nan
+    assert SM.hw_scan2_supported(T, 27, m)
+    r = SM.es_fit(torch.from_numpy(x).to(cuda), T, 2, 10, m, method="scan2")
+    fc0, sig0, best0, sse0 = SM.ref_es_fit(x, 2, 10, m, SM.default_grid(2))
+    np.testing.assert_allclose(r.sse.cpu().numpy(), sse0, rtol=2e-3)
+    assert (r.best.cpu().numpy() == best0).mean() >= 0.85

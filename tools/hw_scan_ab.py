@@ -20,6 +20,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from foremast_amd.ops import smoothing as SM  # noqa: E402
 
 
+METHODS = ["scan", "serial"]
+
+
 def timed(fn, reps):
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in ev:
@@ -36,7 +39,10 @@ def main() -> None:
     ap.add_argument("--m", type=int, nargs="+", default=[1440])
     ap.add_argument("--T", type=int, default=10080)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--methods", default="scan,serial", help="comma list; the first is compared to serial")
     a = ap.parse_args()
+    global METHODS
+    METHODS = a.methods.split(",")
     dev = torch.device("cuda", 0)
     for R in a.rows:
         for m in a.m:
@@ -45,14 +51,15 @@ def main() -> None:
             ph = torch.rand((R, 1), device=dev, generator=g) * 6.283
             x = (10 + torch.sin(6.283 * t / m + ph) + 0.05 * torch.randn((R, a.T), device=dev, generator=g)).contiguous()
             out = {}
-            for meth in ("scan", "serial"):
+            for meth in METHODS:
                 f = lambda: SM.es_fit(x, a.T, 2, 10, m, method=meth)
                 r = f()
                 torch.cuda.synchronize()
                 out[meth] = (timed(f, a.reps), r)
-            sc, se = out["scan"][1], out["serial"][1]
+            sc, se = out[METHODS[0]][1], out["serial"][1]
             rel = ((sc.sse - se.sse).abs() / se.sse.abs().clamp_min(1e-30)).max().item()
-            print(json.dumps({"rows": R, "T": a.T, "m": m, "scan_ms": round(out["scan"][0], 3),
+            extra = {f"{k}_ms": round(v[0], 3) for k, v in out.items() if k not in ("scan", "serial")}
+            print(json.dumps({"rows": R, "T": a.T, "m": m, "scan_ms": round(out["scan"][0], 3), **extra,
                               "serial_ms": round(out["serial"][0], 3),
                               "speedup": round(out["serial"][0] / out["scan"][0], 2),
                               "max_rel_sse_diff": rel,
