@@ -741,6 +741,12 @@ class FastPath:
         and one wide canary never widens the whole fleet's batch."""
         if self._reused and not self.todo and self._last_groups is not None:
             return self._last_groups
+        if works and len(self._gcount) == 1 and works[0].plan.sliding and len(self.todo) == len(works):
+            # one sliding group fetched whole this cycle: _fetch_sliding gave
+            # every job the same width class, so no per-job bucketing
+            g = {works[0].plan.group + (works[0].wclass,): works}
+            self._last_groups = g
+            return g
         g: dict[tuple, list[FastWork]] = {}
         for fw in works:
             k = fw.gkey
