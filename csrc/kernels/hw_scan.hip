@@ -424,11 +424,27 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 namespace {
 constexpr int kChunks[] = {4, 5, 6, 8, 12, 16, 20, 23, 24};
 
+constexpr size_t kMaxLds = 160 * 1024;   // a single gfx950 workgroup may take the whole LDS
+
+template <int C, bool EXACT>
+void allow_big_lds() {
+  static bool done = false;            // once per instantiation (idempotent if raced)
+  if (!done) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(hw_scan_fit_kernel<C, EXACT>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
+    done = true;
+  }
+}
+
 template <int C>
 int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
                float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
                float* season_out, size_t lds, int xal, hipStream_t stream) {
   const int GP = (G + 1) / 2;
+  if (lds > 65536) {
+    if (m % C == 0) allow_big_lds<C, true>();
+    else allow_big_lds<C, false>();
+  }
   if (m % C == 0)
     hipLaunchKernelGGL((hw_scan_fit_kernel<C, true>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, cand, G,
                        m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);
@@ -447,7 +463,7 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
 // candidate's seasonal indices [R, m] by absolute phase.  Returns
 // hipErrorInvalidValue for shapes it does not cover (the caller then uses the
 // serial kernel): m > 64 * 24 or m < 192 (chunks of 4..24 steps per lane),
-// G > 32, 2 m > T, or a row larger than 64 KB of LDS.
+// G > 32, 2 m > T, or a row beyond the 160 KB of LDS a workgroup may take.
 FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H,
                           float* sse, float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin,
                           float* sscale, float* season_out, hipStream_t stream) {
@@ -465,7 +481,7 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
   const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16;
-  if (lds > 65536) return (int)hipErrorInvalidValue;
+  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \

@@ -71,7 +71,8 @@ _SCAN_CHUNKS = (4, 5, 6, 8, 12, 16, 20, 23, 24)
 def hw_scan_supported(T: int, G: int, m: int) -> bool:
     """Shapes the time-parallel additive Holt-Winters fit covers (mirrors
     ``fm_hw_scan_fit``'s checks): 192 <= m <= 64 * 24, G <= 32, 2 m <= T and
-    the row (+ NaN padding for the last lap) within 64 KB of LDS."""
+    the row (+ NaN padding for the last lap) within the 160 KB of LDS a gfx950
+    workgroup may take."""
     if not (1 <= G <= 32 and 192 <= m and 2 * m <= T):
         return False
     need = -(-m // 64)
@@ -83,26 +84,6 @@ def hw_scan_supported(T: int, G: int, m: int) -> bool:
     S = (C & -C).bit_length() - 1 if (m % C == 0 and C % 4 == 0) else None    # bank-skew padding shift
     words = (n + (n >> S if S is not None else 0) + 1 + 3) & ~3
     lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16
-    return lds <= 65536
-
-
-def hw_scan2_supported(T: int, G: int, m: int) -> bool:
-    """Shapes the time-parallel additive Holt-Winters fit covers (mirrors
-    ``fm_hw_scan_fit``'s checks): 192 <= m <= 64 * 24, G <= 32, 2 m <= T,
-    fewer than 128 season laps and the row (+ NaN padding for the last lap)
-    within the 160 KB a gfx950 workgroup may allocate."""
-    if not (1 <= G <= 32 and 192 <= m and 2 * m <= T and (T - m) // m < 128):
-        return False
-    need = -(-m // 64)
-    cs = [c for c in _SCAN_CHUNKS if c >= need and m % c == 0] or [c for c in _SCAN_CHUNKS if c >= need]
-    if not cs:
-        return False
-    C = cs[0]
-    n = T + 64 * C
-    S = (C & -C).bit_length() - 1 if (m % C == 0 and C % 4 == 0) else None    # bank-skew padding shift
-    words = (n + (n >> S if S is not None else 0) + 1 + 3) & ~3
-    GP = (G + 1) // 2
-    lds = words * 4 + GP * 6 * 8 * 4 + GP * C * 16 + 32 * 4 + 16 + 128 * 4 + 16 * 4 * 4
     return lds <= 160 * 1024
 
 
@@ -140,13 +121,10 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
         return ESFit(torch.from_numpy(fc), torch.from_numpy(sig), torch.from_numpy(best), torch.from_numpy(sse), model,
                      nfin)
     require_native(x)
-    check(method in ("auto", "scan", "scan2", "serial"), f"unknown method {method!r}")
+    check(method in ("auto", "scan", "serial"), f"unknown method {method!r}")
     d = x.device
     cand = torch.from_numpy(grid).to(d)
     P = R * G
-    if method == "scan2":
-        check(kind == 2 and hw_scan2_supported(T, G, m), f"scan2 does not cover T={T}, G={G}, m={m}")
-        return _hw_scan_fit(x, T, R, cand, G, m, H, keep_state, entry="fm_hw_scan2_fit")
     scan = kind == 2 and method != "serial" and hw_scan_supported(T, G, m)
     check(scan or method != "scan", f"the scan fit does not cover T={T}, G={G}, m={m}")
     if scan:
@@ -185,7 +163,7 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
 
 
 def _hw_scan_fit(x: torch.Tensor, T: int, R: int, cand: torch.Tensor, G: int, m: int, H: int,
-                 keep_state: bool, entry: str = "fm_hw_scan_fit") -> ESFit:
+                 keep_state: bool) -> ESFit:
     d = x.device
     sse = torch.empty((R, G), dtype=torch.float32, device=d)
     state = torch.empty((R * G, 3), dtype=torch.float32, device=d)
@@ -196,7 +174,7 @@ def _hw_scan_fit(x: torch.Tensor, T: int, R: int, cand: torch.Tensor, G: int, m:
     nfin = torch.empty((R,), dtype=torch.int32, device=d)
     sscale = torch.empty((R,), dtype=torch.float32, device=d)
     season = torch.empty((R, m), dtype=torch.float32, device=d) if keep_state else None
-    LIB.call(entry, ptr(x), x.stride(0), T, R, ptr(cand), G, m, H, ptr(sse), ptr(state), ptr(nobs),
+    LIB.call("fm_hw_scan_fit", ptr(x), x.stride(0), T, R, ptr(cand), G, m, H, ptr(sse), ptr(state), ptr(nobs),
              ptr(fc), ptr(sig), ptr(best), ptr(nfin), ptr(sscale), ptr(season), stream_of(x))
     model = None
     if keep_state:

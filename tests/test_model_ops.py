@@ -655,13 +655,13 @@ def test_hw_scan_supported_shapes():
     assert not SM.hw_scan_supported(10080, 27, 24)          # short season: the serial kernel
     assert not SM.hw_scan_supported(10080, 40, 1440)        # > 32 candidates
     assert not SM.hw_scan_supported(2000, 27, 1440)         # needs two seasons
-    assert not SM.hw_scan_supported(40000, 27, 1440)        # row beyond 64 KB of LDS
+    assert SM.hw_scan_supported(30000, 27, 1440)            # up to 160 KB of LDS per workgroup
+    assert not SM.hw_scan_supported(40000, 27, 1440)        # row beyond the LDS
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("method", ["scan", "scan2"])
 @pytest.mark.parametrize("m", [288, 1300, 1440])
-def test_gpu_hw_scan_fit_matches_references(cuda, m, method):
+def test_gpu_hw_scan_fit_matches_references(cuda, m):
     """The time-parallel fit (exact chunks at 288 / 1440, masked chunks at
     1300) against the fp64 oracle and the serial fp32 kernel: gaps (the
     explicit-matrix scan), a ragged row (partial last lap), an empty row."""
@@ -673,8 +673,8 @@ def test_gpu_hw_scan_fit_matches_references(cuda, m, method):
     x[5, :77] = np.nan
     x[6, :] = np.nan
     xt = torch.from_numpy(x).to(cuda)
-    assert SM.hw_scan_supported(T, 27, m) and SM.hw_scan2_supported(T, 27, m)
-    sc = SM.es_fit(xt, T, 2, 10, m, method=method, keep_state=True)
+    assert SM.hw_scan_supported(T, 27, m)
+    sc = SM.es_fit(xt, T, 2, 10, m, method="scan", keep_state=True)
     se = SM.es_fit(xt, T, 2, 10, m, method="serial", half_season=False, keep_state=True)
     fc0, sig0, best0, sse0 = SM.ref_es_fit(x, 2, 10, m, SM.default_grid(2))
     s_c, s_e = sc.sse.cpu().numpy(), se.sse.cpu().numpy()
@@ -703,14 +703,14 @@ def test_gpu_hw_scan_fit_matches_references(cuda, m, method):
 
 
 @pytest.mark.gpu
-def test_gpu_hw_scan2_long_history_big_lds(cuda):
+def test_gpu_hw_scan_long_history_big_lds(cuda):
     """14 days at 1-min resolution: the row needs > 64 KB of LDS (the launch
     raises the workgroup's dynamic LDS limit); a lap with a gap."""
     T, m = 20160, 1440
     x = _seasonal(8, T, period=m, seed=7)
     x[2, 15000] = np.nan
-    assert SM.hw_scan2_supported(T, 27, m)
-    r = SM.es_fit(torch.from_numpy(x).to(cuda), T, 2, 10, m, method="scan2")
+    assert SM.hw_scan_supported(T, 27, m)
+    r = SM.es_fit(torch.from_numpy(x).to(cuda), T, 2, 10, m, method="scan")
     fc0, sig0, best0, sse0 = SM.ref_es_fit(x, 2, 10, m, SM.default_grid(2))
     np.testing.assert_allclose(r.sse.cpu().numpy(), sse0, rtol=2e-3)
     assert (r.best.cpu().numpy() == best0).mean() >= 0.85

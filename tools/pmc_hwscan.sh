@@ -5,7 +5,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 set -e
-A="--rows 40000 --m ${PMC_M:-1440} --reps 2"
+A="--rows 40000 --m ${PMC_M:-1440} --reps 2 --methods ${PMC_METHODS:-scan,serial}"
 timeout -k 10 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM \
   SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
   -d "$R/gpurun_out/pmc_hwscan_a" -o a -- python3 "$R/tools/hw_scan_ab.py" $A > "$R/gpurun_out/pmc_hwscan_a.log" 2>&1
