@@ -714,3 +714,19 @@ def test_gpu_hw_scan_long_history_big_lds(cuda):
     fc0, sig0, best0, sse0 = SM.ref_es_fit(x, 2, 10, m, SM.default_grid(2))
     np.testing.assert_allclose(r.sse.cpu().numpy(), sse0, rtol=2e-3)
     assert (r.best.cpu().numpy() == best0).mean() >= 0.85
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="probes the launcher with null pointers: CPU-only")
+def test_hw_scan_supported_mirrors_native_checks():
+    """hw_scan_supported (Python) and fm_hw_scan_fit's own shape checks agree:
+    without a device the launcher answers hipErrorInvalidValue (1) for shapes
+    it does not cover and only reaches the (failing) launch for the others."""
+    from foremast_amd.ops._lib import LIB
+    if not LIB.available():
+        pytest.skip("native library not built")
+    f = LIB.load().fm_hw_scan_fit
+    for T in (400, 2880, 10080, 20160, 30000, 36000):
+        for m in (24, 150, 192, 288, 1008, 1300, 1440, 1536, 1600):
+            for G in (1, 27, 32, 33):
+                rc = f(None, T, T, 1, None, G, m, 10, *([None] * 10))
+                assert (rc != 1) == SM.hw_scan_supported(T, G, m), (T, m, G, rc)
