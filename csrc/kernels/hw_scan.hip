@@ -43,6 +43,8 @@
 // deploy/foremast/3_brain/foremast-brain.yaml ML_ALGORITHM); the recursion and
 // its initialisation follow docs/BRAIN_SPEC.md §3.2 and ops/smoothing.py's
 // fp64 reference (ref_es_fit).
+#include <cstdlib>
+
 #include "fm_common.h"
 
 using namespace fm;
@@ -78,6 +80,7 @@ __device__ __forceinline__ f2 rdl(f2 v, int l) {
 
 constexpr int kLevels = 6;          // log2(64) scan levels
 constexpr int kMaxG = 32;           // candidates per row (<= 16 waves of two)
+constexpr int kMaxLaps = 128;       // season laps per row (T / m)
 
 }  // namespace
 
@@ -98,7 +101,7 @@ struct RowPad {
 
 // LDS: xs[pad(T - base + 64 C)] (the row from base on, NaN-padded) |
 // pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | sse[32] | base
-template <int C, bool EXACT>
+template <int C, bool EXACT, bool FS>
 __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restrict__ x, int64_t ld, int T,
                                                            const float* __restrict__ cand, int G, int m, int H,
                                                            float* __restrict__ sse, float* __restrict__ state,
@@ -115,6 +118,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   f2* pw = reinterpret_cast<f2*>(lds + Tx);
   float* sse_s = lds + Tx + GP * kLevels * 8;
   int* ibase = reinterpret_cast<int*>(sse_s + kMaxG);
+  int* lapnan = ibase + 4;                                     // FS: a missing sample in lap k
+  float* wsum = reinterpret_cast<float*>(lapnan + kMaxLaps);  // FS: per-wave season sums
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = lane_id(), w = wave_id();
   const float* xr = x + row * ld;
@@ -122,6 +127,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // ---- the row's first finite sample (LDS atomic min), then the row from
   // there on into LDS (the second read of the row hits L2)
   if (tid == 0) *ibase = T;
+  if constexpr (FS)
+    for (int i = tid; i < kMaxLaps; i += nth) lapnan[i] = 0;
   __syncthreads();
   int fmin = T;
   if (xal) {
@@ -143,7 +150,12 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   if (lane == 0) atomicMin(ibase, fmin);
   __syncthreads();
   const int base = *ibase;
-  for (int i = base + tid; i < T; i += nth) xs[RP::at(i - base)] = xr[i];
+  for (int i = base + tid; i < T; i += nth) {
+    const float v = xr[i];
+    xs[RP::at(i - base)] = v;
+    if constexpr (FS)
+      if (!isfinite(v) && i >= base + m) lapnan[(i - base - m) / m] = 1;   // that lap takes the general scan
+  }
   for (int r = T - base + tid; r < T - base + 64 * C; r += nth) xs[RP::at(r)] = __builtin_nanf("");
 
   // ---- per wave: two candidates, A = J - k 1^T and its lane-uniform powers
@@ -154,8 +166,18 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   const f2 ab = al * be, gs = gm * (one - al);
   const M2 A = {one - al, one - al, -ab, one - ab};
   M2 Q = A;
+  if constexpr (FS) {
+    M2 Pw = A;
+    Q = {one, zero, zero, one};
+#pragma unroll
+    for (int k = C; k > 0; k >>= 1) {                  // A^C by squaring
+      if (k & 1) Q = mmul(Q, Pw);
+      Pw = mmul(Pw, Pw);
+    }
+  } else {
 #pragma unroll 1
-  for (int k = 1; k < C; ++k) Q = mmul(Q, A);          // A^C
+    for (int k = 1; k < C; ++k) Q = mmul(Q, A);        // A^C
+  }
   if (lane == 0) {
 #pragma unroll 1
     for (int lv = 0; lv < kLevels; ++lv) {             // A^{C 2^lv}
@@ -172,23 +194,49 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   int c1 = 0;
   f2 s[C];
   const int q0 = lane * C;
+  if constexpr (FS) {
+    // first- and second-season sums split over the workgroup's waves, then
+    // added in a fixed order (deterministic, the same in every wave)
+    if (base < T) {
+      const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
+      float sa = 0.f, sb = 0.f, fa = 0.f, fb = 0.f;
+      for (int i = base + tid; i < e2; i += nth) {
+        const float v = xs[RP::at(i - base)];
+        const bool f = isfinite(v);
+        if (i < e1) { sa += f ? v : 0.f; fa += f ? 1.f : 0.f; }
+        else { sb += f ? v : 0.f; fb += f ? 1.f : 0.f; }
+      }
+      sa = wave_sum(sa); sb = wave_sum(sb); fa = wave_sum(fa); fb = wave_sum(fb);
+      if (lane == 0) { wsum[4 * w] = sa; wsum[4 * w + 1] = sb; wsum[4 * w + 2] = fa; wsum[4 * w + 3] = fb; }
+    }
+    __syncthreads();
+  }
   if (base < T) {
     const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
     float sa = 0.f, sb = 0.f;
     int ca = 0, cb = 0;
-    for (int i = base + lane; i < e1; i += FM_WAVE) {
-      const float v = xs[RP::at(i - base)];
-      const bool f = isfinite(v);
-      sa += f ? v : 0.f;
-      ca += f;
+    if constexpr (FS) {
+      float fa = 0.f, fb = 0.f;
+      for (int v = 0; v < GP; ++v) {
+        sa += wsum[4 * v]; sb += wsum[4 * v + 1]; fa += wsum[4 * v + 2]; fb += wsum[4 * v + 3];
+      }
+      ca = (int)fa;
+      cb = (int)fb;
+    } else {
+      for (int i = base + lane; i < e1; i += FM_WAVE) {
+        const float v = xs[RP::at(i - base)];
+        const bool f = isfinite(v);
+        sa += f ? v : 0.f;
+        ca += f;
+      }
+      for (int i = e1 + lane; i < e2; i += FM_WAVE) {
+        const float v = xs[RP::at(i - base)];
+        const bool f = isfinite(v);
+        sb += f ? v : 0.f;
+        cb += f;
+      }
+      sa = wave_sum(sa); sb = wave_sum(sb); ca = wave_sum(ca); cb = wave_sum(cb);
     }
-    for (int i = e1 + lane; i < e2; i += FM_WAVE) {
-      const float v = xs[RP::at(i - base)];
-      const bool f = isfinite(v);
-      sb += f ? v : 0.f;
-      cb += f;
-    }
-    sa = wave_sum(sa); sb = wave_sum(sb); ca = wave_sum(ca); cb = wave_sum(cb);
     const float m1 = ca > 0 ? sa / ca : 0.f, m2 = cb > 0 ? sb / cb : 0.f;
     const float trd = cb > 0 ? (m2 - m1) / m : 0.f;
     l = (f2){m1, m1};
@@ -229,12 +277,14 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     // prefix of lanes 0..i-1 IS the state entering lane i (no carry matrix)
     const f2 l0 = lane == 0 ? l : zero, t0v = lane == 0 ? tr : zero;
     bool bad = false;
+    bool gaps = false;                      // FS: the staging flagged a missing sample in this lap
+    if constexpr (FS) gaps = lapnan[(tl - base - m) / m] != 0;
     f2 b0 = l0, b1 = t0v;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       if (j % 8 == 0 && j > 0) __builtin_amdgcn_sched_barrier(0);   // bound the loads in flight (VGPRs)
       const float xq = xl[j + (j >> RP::S)];
-      bad |= !isfinite(xq);
+      if constexpr (!FS) bad |= !isfinite(xq);
       const f2 u = xq - s[j];
       const f2 wb = b0 + b1;
       const f2 e = u - wb;
@@ -242,7 +292,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       b1 = __builtin_elementwise_fma(ab, e, b1);
     }
     // only the lanes before the last active one feed the scan
-    if (!__any(bad && lane < last)) {
+    if (FS ? !gaps : !__any(bad && lane < last)) {
       // those chunks are full and finite: lane i's window at level d is
       // A^{C d}, the same for every lane >= d
 #pragma unroll
@@ -299,7 +349,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     xl = xs + xo;
     f2 acc = zero;
     int nn = 0;
-    if (EXACT && nact == m && !__any(bad && q0 < m)) {
+    if (EXACT && nact == m && (FS ? !gaps : !__any(bad && q0 < m))) {
       // full lap without a missing sample, m = C * (lanes in use): no
       // inactive or missing step in a used lane, so no per-step select
 #pragma unroll
@@ -426,11 +476,11 @@ constexpr int kChunks[] = {4, 5, 6, 8, 12, 16, 20, 23, 24};
 
 constexpr size_t kMaxLds = 160 * 1024;   // a single gfx950 workgroup may take the whole LDS
 
-template <int C, bool EXACT>
+template <int C, bool EXACT, bool FS>
 void allow_big_lds() {
   static bool done = false;            // once per instantiation (idempotent if raced)
   if (!done) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(hw_scan_fit_kernel<C, EXACT>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(hw_scan_fit_kernel<C, EXACT, FS>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
     done = true;
   }
@@ -441,16 +491,24 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
                float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
                float* season_out, size_t lds, int xal, hipStream_t stream) {
   const int GP = (G + 1) / 2;
-  if (lds > 65536) {
-    if (m % C == 0) allow_big_lds<C, true>();
-    else allow_big_lds<C, false>();
-  }
-  if (m % C == 0)
-    hipLaunchKernelGGL((hw_scan_fit_kernel<C, true>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, cand, G,
-                       m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);
-  else
-    hipLaunchKernelGGL((hw_scan_fit_kernel<C, false>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, cand,
-                       G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);
+  // FOREMAST_HW_SCAN_SETUP=0: the original setup (per-wave season means, A^C
+  // by C - 1 products, per-step NaN ballots) for A/B runs
+  static const bool fs = [] {
+    const char* e = getenv("FOREMAST_HW_SCAN_SETUP");
+    return e == nullptr || e[0] != '0';
+  }();
+#define FM_HWS_LAUNCH(EX, FSV)                                                                              \
+  do {                                                                                                     \
+    if (lds > 65536) allow_big_lds<C, EX, FSV>();                                                           \
+    hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, \
+                       cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);      \
+  } while (0)
+  const bool ex = m % C == 0;
+  if (ex && fs) FM_HWS_LAUNCH(true, true);
+  else if (ex) FM_HWS_LAUNCH(true, false);
+  else if (fs) FM_HWS_LAUNCH(false, true);
+  else FM_HWS_LAUNCH(false, false);
+#undef FM_HWS_LAUNCH
   FM_LAUNCH_CHECK();
   return 0;
 }
@@ -480,8 +538,8 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   const int GP = (G + 1) / 2;
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
-  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16;
-  if (lds > kMaxLds) return (int)hipErrorInvalidValue;
+  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4;
+  if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return (int)hipErrorInvalidValue;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \

@@ -73,7 +73,7 @@ def hw_scan_supported(T: int, G: int, m: int) -> bool:
     ``fm_hw_scan_fit``'s checks): 192 <= m <= 64 * 24, G <= 32, 2 m <= T and
     the row (+ NaN padding for the last lap) within the 160 KB of LDS a gfx950
     workgroup may take."""
-    if not (1 <= G <= 32 and 192 <= m and 2 * m <= T):
+    if not (1 <= G <= 32 and 192 <= m and 2 * m <= T and (T - m) // m < 128):
         return False
     need = -(-m // 64)
     cs = [c for c in _SCAN_CHUNKS if c >= need and m % c == 0] or [c for c in _SCAN_CHUNKS if c >= need]
@@ -83,7 +83,7 @@ def hw_scan_supported(T: int, G: int, m: int) -> bool:
     n = T + 64 * C
     S = (C & -C).bit_length() - 1 if (m % C == 0 and C % 4 == 0) else None    # bank-skew padding shift
     words = (n + (n >> S if S is not None else 0) + 1 + 3) & ~3
-    lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16
+    lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16 + 128 * 4 + 16 * 4 * 4
     return lds <= 160 * 1024
 
 
