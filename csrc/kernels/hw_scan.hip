@@ -108,7 +108,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
                                                            int* __restrict__ nobs, float* __restrict__ fc,
                                                            float* __restrict__ sigma, int* __restrict__ best,
                                                            int* __restrict__ nfin, float* __restrict__ sscale,
-                                                           float* __restrict__ season_out, int xal) {
+                                                           float* __restrict__ season_out, int xal, int64_t nrows,
+                                                           int ahead) {
   using RP = RowPad<C, EXACT>;
   extern __shared__ float lds[];
   const int64_t row = blockIdx.x;
@@ -157,6 +158,20 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       if (!isfinite(v) && i >= base + m) lapnan[(i - base - m) / m] = 1;   // that lap takes the general scan
   }
   for (int r = T - base + tid; r < T - base + 64 * C; r += nth) xs[RP::at(r)] = __builtin_nanf("");
+  if constexpr (FS) {
+    // warm L2 (and the Infinity Cache) with the row the workgroup `ahead`
+    // dispatches later will read -- the same XCD when ahead % 8 == 0: one dword
+    // per 128-B line, DMA'd into a scratch LDS word (no VGPR, nothing waits on it
+    // until the end-of-row barriers, long after it landed)
+    const int64_t nxt = row + ahead;
+    if (ahead > 0 && nxt < nrows) {
+      const float* src = x + nxt * ld;
+      const int lines = (T + 31) / 32;
+      for (int c = tid; c < lines; c += nth)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + c * 32),
+                                         (__attribute__((address_space(3))) void*)(wsum + 16 * 4), 4, 0, 0);
+    }
+  }
 
   // ---- per wave: two candidates, A = J - k 1^T and its lane-uniform powers
   const int ga = 2 * w, gb = 2 * w + 1 < G ? 2 * w + 1 : 2 * w;
@@ -469,6 +484,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       if (nfin != nullptr) nfin[row] = c1 + n;
     }
   }
+  if constexpr (FS) __builtin_amdgcn_s_waitcnt(0);   // no L2 warm-up DMA outlives the workgroup's LDS
 }
 
 namespace {
@@ -501,8 +517,18 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
   do {                                                                                                     \
     if (lds > 65536) allow_big_lds<C, EX, FSV>();                                                           \
     hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, \
-                       cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal);      \
+                       cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal, R,    \
+                       ahead);                                                                             \
   } while (0)
+  // L2 warm-up distance: the workgroups resident at once (one per CU at 14
+  // waves), a multiple of the 8 XCDs so the warmed row is read on the same XCD
+  static const int ahead = [] {
+    int dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const char* e = getenv("FOREMAST_HW_SCAN_AHEAD");
+    return e != nullptr ? atoi(e) : (cus / 8) * 8;
+  }();
   const bool ex = m % C == 0;
   if (ex && fs) FM_HWS_LAUNCH(true, true);
   else if (ex) FM_HWS_LAUNCH(true, false);
@@ -538,7 +564,7 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   const int GP = (G + 1) / 2;
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
-  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4;
+  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4 + 64 * 4;
   if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return (int)hipErrorInvalidValue;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \

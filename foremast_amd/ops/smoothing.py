@@ -83,7 +83,7 @@ def hw_scan_supported(T: int, G: int, m: int) -> bool:
     n = T + 64 * C
     S = (C & -C).bit_length() - 1 if (m % C == 0 and C % 4 == 0) else None    # bank-skew padding shift
     words = (n + (n >> S if S is not None else 0) + 1 + 3) & ~3
-    lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16 + 128 * 4 + 16 * 4 * 4
+    lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16 + 128 * 4 + 16 * 4 * 4 + 64 * 4
     return lds <= 160 * 1024
 
 
