@@ -578,7 +578,9 @@ class SQLiteStore(JobStore):
             c.execute("insert or ignore into meta values ('seq', 0)")
             c.execute("create table if not exists hpalogs (job_id text, ts real, body text)")
             c.execute("create index if not exists hpalogs_job on hpalogs(job_id, ts)")
-            c.execute("create index if not exists hpalogs_ts on hpalogs(ts)")
+            # no ts index: rows arrive in time order, so retention deletes a
+            # rowid prefix (one B-tree less to update per log: 10k logs per cycle)
+            c.execute("drop index if exists hpalogs_ts")
             if legacy:                          # round-2 layout: one JSON body per row
                 seq = self._next_seq(c)
                 rows = [self._row(Document.from_dict(json.loads(b)), seq)
@@ -915,7 +917,12 @@ class SQLiteStore(JobStore):
             # GET /v1/healthcheck/id the last 10): drop entries older than
             # the retention window, at most once a minute
             if self.hpalog_retention_s > 0 and newest - self._last_prune > 60.0:
-                c.execute("delete from hpalogs where ts < ?", (newest - self.hpalog_retention_s,))
+                # the oldest rowid inside the window (a scan over the rows that
+                # are about to go), then the rowid prefix before it
+                cut = newest - self.hpalog_retention_s
+                first = c.execute("select rowid from hpalogs where ts >= ? order by rowid limit 1", (cut,)).fetchone()
+                if first is not None:
+                    c.execute("delete from hpalogs where rowid < ?", (first[0],))
                 self._last_prune = newest
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
