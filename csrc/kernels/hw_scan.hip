@@ -79,6 +79,22 @@ __device__ __forceinline__ f2 rdl(f2 v, int l) {
 }
 
 constexpr int kLevels = 6;          // log2(64) scan levels
+
+// lane l's pair (per-lane l)
+__device__ __forceinline__ f2 bperm2(f2 v, int l) {
+  const float vx = v.x, vy = v.y;
+  return (f2){__builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(l << 2, __builtin_bit_cast(int, vx))),
+              __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(l << 2, __builtin_bit_cast(int, vy)))};
+}
+
+// sum over each group of N lanes (N = 64: the whole wave, 32: each half)
+template <int N, typename T>
+__device__ __forceinline__ T group_sum(T v) {
+  v += xor_lane<1>(v); v += xor_lane<2>(v); v += xor_lane<4>(v);
+  v += xor_lane<8>(v); v += xor_lane<16>(v);
+  if constexpr (N == 64) v += xor_lane<32>(v);
+  return v;
+}
 constexpr int kMaxG = 32;           // candidates per row (<= 16 waves of two)
 constexpr int kMaxLaps = 128;       // season laps per row (T / m)
 
@@ -101,7 +117,7 @@ struct RowPad {
 
 // LDS: xs[pad(T - base + 64 C)] (the row from base on, NaN-padded) |
 // pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | sse[32] | base
-template <int C, bool EXACT, bool FS>
+template <int C, bool EXACT, bool FS, int LPP>
 __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restrict__ x, int64_t ld, int T,
                                                            const float* __restrict__ cand, int G, int m, int H,
                                                            float* __restrict__ sse, float* __restrict__ state,
@@ -123,6 +139,13 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   float* wsum = reinterpret_cast<float*>(lapnan + kMaxLaps);  // FS: per-wave season sums
   const int tid = threadIdx.x, nth = blockDim.x;
   const int lane = lane_id(), w = wave_id();
+  // LPP lanes per candidate pair: 64 (one pair per wave) or 32 (two pairs per
+  // wave, half-waves scanning 32 chunks: short seasons, fewer scan levels)
+  static_assert(LPP == 64 || (LPP == 32 && FS), "half-wave pairs need the cooperative setup");
+  constexpr int PPW = 64 / LPP, NLV = LPP == 64 ? 6 : 5;
+  const int half = lane / LPP, li = lane % LPP;
+  const bool pvalid = w * PPW + half < GP;
+  const int pair = pvalid ? w * PPW + half : GP - 1;    // an idle half shadows the last pair
   const float* xr = x + row * ld;
 
   // ---- the row's first finite sample (LDS atomic min), then the row from
@@ -174,7 +197,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   }
 
   // ---- per wave: two candidates, A = J - k 1^T and its lane-uniform powers
-  const int ga = 2 * w, gb = 2 * w + 1 < G ? 2 * w + 1 : 2 * w;
+  const int ga = 2 * pair, gb = 2 * pair + 1 < G ? 2 * pair + 1 : 2 * pair;
   const f2 al = {cand[3 * ga], cand[3 * gb]}, be = {cand[3 * ga + 1], cand[3 * gb + 1]},
            gm = {cand[3 * ga + 2], cand[3 * gb + 2]};
   const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
@@ -193,10 +216,10 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 #pragma unroll 1
     for (int k = 1; k < C; ++k) Q = mmul(Q, A);        // A^C
   }
-  if (lane == 0) {
+  if (li == 0 && pvalid) {
 #pragma unroll 1
     for (int lv = 0; lv < kLevels; ++lv) {             // A^{C 2^lv}
-      f2* p = pw + (w * kLevels + lv) * 4;
+      f2* p = pw + (pair * kLevels + lv) * 4;
       p[0] = Q.a; p[1] = Q.b; p[2] = Q.c; p[3] = Q.d;
       Q = mmul(Q, Q);
     }
@@ -208,7 +231,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   f2 l, tr;
   int c1 = 0;
   f2 s[C];
-  const int q0 = lane * C;
+  const int q0 = li * C;
   if constexpr (FS) {
     // first- and second-season sums split over the workgroup's waves, then
     // added in a fixed order (deterministic, the same in every wave)
@@ -232,7 +255,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     int ca = 0, cb = 0;
     if constexpr (FS) {
       float fa = 0.f, fb = 0.f;
-      for (int v = 0; v < GP; ++v) {
+      for (int v = 0; v < nth / FM_WAVE; ++v) {
         sa += wsum[4 * v]; sb += wsum[4 * v + 1]; fa += wsum[4 * v + 2]; fb += wsum[4 * v + 3];
       }
       ca = (int)fa;
@@ -281,8 +304,9 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   for (int tl = base + m; tl < T; tl += m) {
     // re-read the powers every lap (an opaque offset keeps the compiler from
     // hoisting 24 loop-invariant LDS loads into 48 live VGPRs)
-    int pwo = w * kLevels * 4;
-    asm volatile("" : "+s"(pwo));
+    int pwo = pair * kLevels * 4;
+    if constexpr (LPP == 64) asm volatile("" : "+s"(pwo));
+    else asm volatile("" : "+v"(pwo));
     const f2* pwv = pw + pwo;
     const int nact = min(m, T - tl);
     const int last = (nact - 1) / C;          // lane holding the lap's last step
@@ -290,7 +314,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     const float* xl = xs + RP::at(tl - base + q0);   // reassigned for pass 2
     // lane 0 folds the lap's entering state into its chunk, so the scanned
     // prefix of lanes 0..i-1 IS the state entering lane i (no carry matrix)
-    const f2 l0 = lane == 0 ? l : zero, t0v = lane == 0 ? tr : zero;
+    const f2 l0 = li == 0 ? l : zero, t0v = li == 0 ? tr : zero;
     bool bad = false;
     bool gaps = false;                      // FS: the staging flagged a missing sample in this lap
     if constexpr (FS) gaps = lapnan[(tl - base - m) / m] != 0;
@@ -311,11 +335,11 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       // those chunks are full and finite: lane i's window at level d is
       // A^{C d}, the same for every lane >= d
 #pragma unroll
-      for (int lv = 0; lv < kLevels; ++lv) {
+      for (int lv = 0; lv < NLV; ++lv) {
         const int d = 1 << lv;
         const f2 n0 = up(b0, d), n1 = up(b1, d);
         const f2 p0 = pwv[lv * 4 + 0], p1 = pwv[lv * 4 + 1], p2 = pwv[lv * 4 + 2], p3 = pwv[lv * 4 + 3];
-        if (lane >= d) {
+        if (li >= d) {
           b0 = b0 + p0 * n0 + p1 * n1;
           b1 = b1 + p2 * n0 + p3 * n1;
         }
@@ -343,11 +367,11 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
         Mm.d = Mm.d - kb * w1;
       }
 #pragma unroll
-      for (int lv = 0; lv < kLevels; ++lv) {
+      for (int lv = 0; lv < NLV; ++lv) {
         const int d = 1 << lv;
         const M2 nm = {up(Mm.a, d), up(Mm.b, d), up(Mm.c, d), up(Mm.d, d)};
         const f2 n0 = up(b0, d), n1 = up(b1, d);
-        if (lane >= d) {
+        if (li >= d) {
           b0 = b0 + Mm.a * n0 + Mm.b * n1;
           b1 = b1 + Mm.c * n0 + Mm.d * n1;
           Mm = mmul(Mm, nm);
@@ -356,7 +380,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     }
     // exclusive prefix: the (level, trend) entering this lane's chunk
     f2 L = up(b0, 1), Tt = up(b1, 1);
-    if (lane == 0) { L = l; Tt = tr; }
+    if (li == 0) { L = l; Tt = tr; }
     // re-read the lap's samples (an opaque offset: otherwise the compiler keeps
     // pass 1's C loads live across the scan)
     int xo = RP::at(tl - base + q0);
@@ -419,17 +443,22 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     ea += acc.x;
     eb += acc.y;
     n += nn;
-    l = rdl(L, last);
-    tr = rdl(Tt, last);
+    if constexpr (LPP == 64) {
+      l = rdl(L, last);
+      tr = rdl(Tt, last);
+    } else {                                 // each half reads its own last lane
+      l = bperm2(L, (lane & ~(LPP - 1)) + last);
+      tr = bperm2(Tt, (lane & ~(LPP - 1)) + last);
+    }
   }
-  ea = wave_sum(ea);
-  eb = wave_sum(eb);
-  n = wave_sum(n);
+  ea = group_sum<LPP>(ea);
+  eb = group_sum<LPP>(eb);
+  n = group_sum<LPP>(n);
 
   // ---- per-candidate results, then the row's best candidate
   const float fa = (float)ea, fb = (float)eb;
   const float tph = (float)(T % m);
-  if (lane == 0) {
+  if (li == 0 && pvalid) {
     const int64_t pa = row * G + ga;
     sse[pa] = fa;
     state[pa * 3 + 0] = l.x;
@@ -437,7 +466,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     state[pa * 3 + 2] = tph;
     nobs[pa] = n;
     sse_s[ga] = fa;
-    if (2 * w + 1 < G) {
+    if (2 * pair + 1 < G) {
       const int64_t pb = pa + 1;
       sse[pb] = fb;
       state[pb * 3 + 0] = l.y;
@@ -454,7 +483,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     const float v = sse_s[g];
     if (v < bs || !isfinite(bs)) { bs = v; bg = g; }
   }
-  const bool mine = (bg >> 1) == w;
+  const bool mine = (bg >> 1) == pair && pvalid;
   const bool hi = (bg & 1) != 0;
   if (mine) {
 #pragma unroll
@@ -470,14 +499,14 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   if (mine) {
     const float lb = hi ? l.y : l.x, tb = hi ? tr.y : tr.x;
     const int t0 = T % m;
-    for (int h = 1 + lane; h <= H; h += FM_WAVE) {
+    for (int h = 1 + li; h <= H; h += LPP) {
       int p = t0 + h - 1;
       p %= m;
       fc[row * H + (h - 1)] = lb + h * tb + xs[p];
     }
     if (season_out != nullptr)
-      for (int p = lane; p < m; p += FM_WAVE) season_out[row * m + p] = xs[p];
-    if (lane == 0) {
+      for (int p = li; p < m; p += LPP) season_out[row * m + p] = xs[p];
+    if (li == 0) {
       sigma[row] = n > 1 ? sqrtf(bs / (float)(n - 1)) : 0.f;
       best[row] = bg;
       sscale[row] = 1.f;
@@ -488,38 +517,51 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
 }
 
 namespace {
-constexpr int kChunks[] = {4, 5, 6, 8, 12, 16, 20, 23, 24};
+constexpr int kChunks[] = {4, 5, 6, 8, 9, 12, 16, 18, 20, 23, 24};
+constexpr int kHalfMaxM = 32 * 24;       // seasons up to this length scan in 32-lane half-waves
 
 constexpr size_t kMaxLds = 160 * 1024;   // a single gfx950 workgroup may take the whole LDS
 
-template <int C, bool EXACT, bool FS>
+template <int C, bool EXACT, bool FS, int LPP>
 void allow_big_lds() {
   static bool done = false;            // once per instantiation (idempotent if raced)
   if (!done) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(hw_scan_fit_kernel<C, EXACT, FS>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(hw_scan_fit_kernel<C, EXACT, FS, LPP>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
     done = true;
   }
 }
 
-template <int C>
-int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
-               float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
-               float* season_out, size_t lds, int xal, hipStream_t stream) {
-  const int GP = (G + 1) / 2;
-  // FOREMAST_HW_SCAN_SETUP=0: the original setup (per-wave season means, A^C
-  // by C - 1 products, per-step NaN ballots) for A/B runs
+// FOREMAST_HW_SCAN_SETUP=0: the original setup (per-wave season means, A^C by
+// C - 1 products, per-step NaN ballots; one pair per wave) for A/B runs
+bool scan_fast_setup() {
   static const bool fs = [] {
     const char* e = getenv("FOREMAST_HW_SCAN_SETUP");
     return e == nullptr || e[0] != '0';
   }();
-#define FM_HWS_LAUNCH(EX, FSV)                                                                              \
-  do {                                                                                                     \
-    if (lds > 65536) allow_big_lds<C, EX, FSV>();                                                           \
-    hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV>), dim3((unsigned)R), dim3(64 * GP), lds, stream, x, ld, T, \
-                       cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal, R,    \
-                       ahead);                                                                             \
-  } while (0)
+  return fs;
+}
+
+// lanes per candidate pair for a season of m steps
+int scan_lpp(int m) {
+  static const int force = [] {
+    const char* e = getenv("FOREMAST_HW_SCAN_LPP");
+    return e == nullptr ? 0 : atoi(e);
+  }();
+  // half-wave pairs for short seasons (FOREMAST_HW_SCAN_LPP=64 for A/B runs):
+  // 40k rows x 10,080, m = 288: 5.36 vs 11.3 ms; m = 720: 4.36 vs 6.37 ms
+  // (profiles/hw_scan_halfwave_ab_r3.jsonl)
+  if (!scan_fast_setup() || force == 64) return 64;
+  return m <= kHalfMaxM ? 32 : 64;
+}
+
+template <int C>
+int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
+               float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
+               float* season_out, size_t lds, int xal, int lpp, hipStream_t stream) {
+  const int GP = (G + 1) / 2;
+  const int waves = lpp == 64 ? GP : (GP + 1) / 2;
+  const bool fs = scan_fast_setup();
   // L2 warm-up distance: the workgroups resident at once (one per CU at 14
   // waves), a multiple of the 8 XCDs so the warmed row is read on the same XCD
   static const int ahead = [] {
@@ -529,11 +571,21 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
     const char* e = getenv("FOREMAST_HW_SCAN_AHEAD");
     return e != nullptr ? atoi(e) : (cus / 8) * 8;
   }();
+#define FM_HWS_LAUNCH(EX, FSV, LP)                                                                          \
+  do {                                                                                                     \
+    if (lds > 65536) allow_big_lds<C, EX, FSV, LP>();                                                       \
+    hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV, LP>), dim3((unsigned)R), dim3(64 * waves), lds, stream, x, \
+                       ld, T, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal,  \
+                       R, ahead);                                                                          \
+  } while (0)
   const bool ex = m % C == 0;
-  if (ex && fs) FM_HWS_LAUNCH(true, true);
-  else if (ex) FM_HWS_LAUNCH(true, false);
-  else if (fs) FM_HWS_LAUNCH(false, true);
-  else FM_HWS_LAUNCH(false, false);
+  if (lpp == 32) {
+    if (ex) FM_HWS_LAUNCH(true, true, 32);
+    else FM_HWS_LAUNCH(false, true, 32);
+  } else if (ex && fs) FM_HWS_LAUNCH(true, true, 64);
+  else if (ex) FM_HWS_LAUNCH(true, false, 64);
+  else if (fs) FM_HWS_LAUNCH(false, true, 64);
+  else FM_HWS_LAUNCH(false, false, 64);
 #undef FM_HWS_LAUNCH
   FM_LAUNCH_CHECK();
   return 0;
@@ -546,20 +598,25 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
 // sscale [R] (= 1: data units) -- plus, when season_out is not null, the best
 // candidate's seasonal indices [R, m] by absolute phase.  Returns
 // hipErrorInvalidValue for shapes it does not cover (the caller then uses the
-// serial kernel): m > 64 * 24 or m < 192 (chunks of 4..24 steps per lane),
+// serial kernel): m > 64 * 24 or m < 192 (chunks of 4..24 steps per lane; seasons
+// up to 768 steps run two candidate pairs per wave, 32 lanes each),
 // G > 32, 2 m > T, or a row beyond the 160 KB of LDS a workgroup may take.
 FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H,
                           float* sse, float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin,
                           float* sscale, float* season_out, hipStream_t stream) {
   if (R <= 0) return 0;
   if (G < 1 || G > kMaxG || m < 2 || 2 * m > T || H < 0) return (int)hipErrorInvalidValue;
-  const int need = (m + 63) / 64;
+  const int lpp = scan_lpp(m);
+  const int need = (m + lpp - 1) / lpp;
   int C = 0;
+  // 9 and 18 (the 32-lane chunks of 288 / 576-step seasons) only for half-waves:
+  // the one-pair-per-wave kernel keeps its measured chunk choice
+  auto usable = [lpp](int c) { return lpp == 32 || (c != 9 && c != 18); };
   for (int c : kChunks)                      // an exact chunk (no masked steps in full laps) ...
-    if (c >= need && m % c == 0) { C = c; break; }
+    if (usable(c) && c >= need && m % c == 0) { C = c; break; }
   if (C == 0)
     for (int c : kChunks)                    // ... else the shortest that covers the lap
-      if (c >= need) { C = c; break; }
+      if (usable(c) && c >= need) { C = c; break; }
   if (C == 0 || m < 3 * 64) return (int)hipErrorInvalidValue;
   const int GP = (G + 1) / 2;
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
@@ -570,9 +627,10 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \
     return launch_one<CC>(x, ld, T, R, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale,    \
-                          season_out, lds, xal, stream);
+                          season_out, lds, xal, lpp, stream);
   switch (C) {
-    FM_HWS(4) FM_HWS(5) FM_HWS(6) FM_HWS(8) FM_HWS(12) FM_HWS(16) FM_HWS(20) FM_HWS(23) FM_HWS(24)
+    FM_HWS(4) FM_HWS(5) FM_HWS(6) FM_HWS(8) FM_HWS(9) FM_HWS(12) FM_HWS(16) FM_HWS(18) FM_HWS(20) FM_HWS(23)
+    FM_HWS(24)
     default: return (int)hipErrorInvalidValue;
   }
 #undef FM_HWS

@@ -3,6 +3,7 @@ decision (csrc/kernels/smoothing.hip), with fp64 numpy references."""
 from __future__ import annotations
 
 import itertools
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -61,7 +62,8 @@ class ESFit:
 HALF_SEASON_MIN_M = 1000     # <= ~10 laps of a 7-day history: measured within 2e-3 of fp32 (tests)
 
 # csrc/kernels/hw_scan.hip: lanes take chunks of these many steps of a season lap
-_SCAN_CHUNKS = (4, 5, 6, 8, 12, 16, 20, 23, 24)
+_SCAN_CHUNKS = (4, 5, 6, 8, 9, 12, 16, 18, 20, 23, 24)
+_SCAN_HALF_MAX_M = 32 * 24          # seasons up to this length scan in 32-lane half-waves
 # "auto" picks the scan fit wherever it covers the shape: 40k rows x 10,080
 # steps, m = 1440: 6.35 vs 7.93 ms (serial fp16-scratch kernel); m = 1008:
 # 6.47 vs 8.66; m = 288: 11.6 vs 14.7; 10k rows: 1.4-1.6x (tools/hw_scan_ab.py,
@@ -75,8 +77,13 @@ def hw_scan_supported(T: int, G: int, m: int) -> bool:
     workgroup may take."""
     if not (1 <= G <= 32 and 192 <= m and 2 * m <= T and (T - m) // m < 128):
         return False
-    need = -(-m // 64)
-    cs = [c for c in _SCAN_CHUNKS if c >= need and m % c == 0] or [c for c in _SCAN_CHUNKS if c >= need]
+    # 32-lane half-wave pairs for m <= _SCAN_HALF_MAX_M (the launcher's scan_lpp)
+    half = m <= _SCAN_HALF_MAX_M and os.environ.get("FOREMAST_HW_SCAN_LPP") != "64" \
+        and os.environ.get("FOREMAST_HW_SCAN_SETUP") != "0"
+    lanes = 32 if half else 64
+    need = -(-m // lanes)
+    chunks = [c for c in _SCAN_CHUNKS if half or c not in (9, 18)]   # 9 / 18: half-wave chunks only
+    cs = [c for c in chunks if c >= need and m % c == 0] or [c for c in chunks if c >= need]
     if not cs:
         return False
     C = cs[0]

@@ -660,7 +660,7 @@ def test_hw_scan_supported_shapes():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("m", [288, 1300, 1440])
+@pytest.mark.parametrize("m", [288, 720, 1300, 1440])
 def test_gpu_hw_scan_fit_matches_references(cuda, m):
     """The time-parallel fit (exact chunks at 288 / 1440, masked chunks at
     1300) against the fp64 oracle and the serial fp32 kernel: gaps (the
