@@ -66,8 +66,9 @@ _SCAN_CHUNKS = (4, 5, 6, 8, 9, 12, 16, 18, 20, 23, 24)
 _SCAN_HALF_MAX_M = 32 * 24          # seasons up to this length scan in 32-lane half-waves
 # "auto" picks the scan fit wherever it covers the shape: 40k rows x 10,080
 # steps, m = 1440: 6.35 vs 7.93 ms (serial fp16-scratch kernel); m = 1008:
-# 6.47 vs 8.66; m = 288: 11.6 vs 14.7; 10k rows: 1.4-1.6x (tools/hw_scan_ab.py,
-# profiles/hw_scan_ab_r3.jsonl)
+# 6.47 vs 8.66; m = 288: 5.39 vs 14.7 and m = 720: 4.17 vs 15.8 (half-wave
+# pairs); 10k rows: 1.4-4.3x (tools/hw_scan_ab.py, profiles/hw_scan_ab_r3.jsonl,
+# profiles/hw_scan_halfwave_default_r3.jsonl)
 
 
 def hw_scan_supported(T: int, G: int, m: int) -> bool:
