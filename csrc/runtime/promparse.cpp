@@ -9,8 +9,11 @@
 // entry point.  Labels ("metric" objects) are returned as byte spans for the
 // caller to decode (they are tiny).
 #include <atomic>
+#include <charconv>
+#include <system_error>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -104,7 +107,119 @@ struct Sink {
   int64_t* offsets = nullptr;     // [nseries + 1]
   int64_t* label_spans = nullptr; // [nseries, 2] (begin, end) byte offsets of the "metric" object
   int64_t nseries = 0, npoints = 0;
+  // keyed mode: FNV-1a 64 of the decoded value of label `key` per series
+  // (0 when the series has no such label)
+  const char* key = nullptr;
+  int64_t keylen = 0;
+  uint64_t* key_hash = nullptr;
 };
+
+constexpr uint64_t kFnvBasis = 1469598103934665603ull;
+constexpr uint64_t kFnvPrime = 1099511628211ull;
+
+inline uint64_t fnv_byte(uint64_t h, unsigned char b) { return (h ^ b) * kFnvPrime; }
+
+int hexval(char ch) {
+  if (ch >= '0' && ch <= '9') return ch - '0';
+  if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+  if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+  return -1;
+}
+
+bool read_hex4(Cursor& c, uint32_t& u) {
+  if (c.e - c.p < 4) return false;
+  u = 0;
+  for (int i = 0; i < 4; ++i) {
+    const int h = hexval(c.p[i]);
+    if (h < 0) return false;
+    u = (u << 4) | (uint32_t)h;
+  }
+  c.p += 4;
+  return true;
+}
+
+uint64_t fnv_codepoint(uint64_t h, uint32_t cp) {
+  if (cp < 0x80) return fnv_byte(h, (unsigned char)cp);
+  if (cp < 0x800) {
+    h = fnv_byte(h, (unsigned char)(0xC0 | (cp >> 6)));
+    return fnv_byte(h, (unsigned char)(0x80 | (cp & 0x3F)));
+  }
+  if (cp < 0x10000) {
+    h = fnv_byte(h, (unsigned char)(0xE0 | (cp >> 12)));
+    h = fnv_byte(h, (unsigned char)(0x80 | ((cp >> 6) & 0x3F)));
+    return fnv_byte(h, (unsigned char)(0x80 | (cp & 0x3F)));
+  }
+  h = fnv_byte(h, (unsigned char)(0xF0 | (cp >> 18)));
+  h = fnv_byte(h, (unsigned char)(0x80 | ((cp >> 12) & 0x3F)));
+  h = fnv_byte(h, (unsigned char)(0x80 | ((cp >> 6) & 0x3F)));
+  return fnv_byte(h, (unsigned char)(0x80 | (cp & 0x3F)));
+}
+
+// hash the decoded UTF-8 bytes of the JSON string at the cursor (JSON escapes
+// incl. \uXXXX surrogate pairs decoded), so the hash equals FNV-1a of the
+// label value's UTF-8 encoding on the Python side
+bool hash_string(Cursor& c, uint64_t& out) {
+  c.ws();
+  if (c.p >= c.e || *c.p != '"') return false;
+  ++c.p;
+  uint64_t h = kFnvBasis;
+  while (c.p < c.e) {
+    const char ch = *c.p;
+    if (ch == '"') { ++c.p; out = h; return true; }
+    if (ch != '\\') { h = fnv_byte(h, (unsigned char)ch); ++c.p; continue; }
+    if (c.e - c.p < 2) return false;
+    const char e = c.p[1];
+    c.p += 2;
+    switch (e) {
+      case '"': h = fnv_byte(h, '"'); break;
+      case '\\': h = fnv_byte(h, '\\'); break;
+      case '/': h = fnv_byte(h, '/'); break;
+      case 'b': h = fnv_byte(h, '\b'); break;
+      case 'f': h = fnv_byte(h, '\f'); break;
+      case 'n': h = fnv_byte(h, '\n'); break;
+      case 'r': h = fnv_byte(h, '\r'); break;
+      case 't': h = fnv_byte(h, '\t'); break;
+      case 'u': {
+        uint32_t u;
+        if (!read_hex4(c, u)) return false;
+        if (u >= 0xD800 && u < 0xDC00 && c.e - c.p >= 6 && c.p[0] == '\\' && c.p[1] == 'u') {
+          Cursor d{c.p + 2, c.e};
+          uint32_t lo;
+          if (read_hex4(d, lo) && lo >= 0xDC00 && lo < 0xE000) {
+            u = 0x10000 + ((u - 0xD800) << 10) + (lo - 0xDC00);
+            c.p = d.p;
+          }
+        }
+        h = fnv_codepoint(h, u);
+        break;
+      }
+      default: return false;
+    }
+  }
+  return false;
+}
+
+// the "metric" object in keyed mode: hash the value of label s.key
+bool parse_metric_keyed(Cursor& c, Sink& s, uint64_t& kh) {
+  kh = 0;
+  if (!c.eat('{')) return false;
+  if (c.eat('}')) return true;
+  for (;;) {
+    c.ws();
+    if (c.p >= c.e || *c.p != '"') return false;
+    const char* ks = c.p + 1;
+    if (!skip_string(c)) return false;
+    const int64_t klen = (c.p - 1) - ks;
+    if (!c.eat(':')) return false;
+    if (klen == s.keylen && std::memcmp(ks, s.key, (size_t)klen) == 0) {
+      if (!hash_string(c, kh)) return false;
+    } else if (!skip_value(c)) {
+      return false;
+    }
+    if (c.eat(',')) continue;
+    return c.eat('}');
+  }
+}
 
 bool parse_pairs(Cursor& c, Sink& s, bool single) {
   auto pair = [&]() -> bool {
@@ -133,6 +248,7 @@ bool parse_result_array(Cursor& c, const char* base, Sink& s) {
   for (;;) {
     if (!c.eat('{')) return false;
     int64_t lb = -1, le = -1;
+    uint64_t kh = 0;
     if (s.offsets) s.offsets[s.nseries] = s.npoints;
     if (!c.eat('}')) {
       for (;;) {
@@ -141,7 +257,11 @@ bool parse_result_array(Cursor& c, const char* base, Sink& s) {
         if (k == "metric") {
           c.ws();
           lb = c.p - base;
-          if (!skip_value(c)) return false;
+          if (s.key) {
+            if (!parse_metric_keyed(c, s, kh)) return false;
+          } else if (!skip_value(c)) {
+            return false;
+          }
           le = c.p - base;
         } else if (k == "values") {
           if (!parse_pairs(c, s, false)) return false;
@@ -156,6 +276,7 @@ bool parse_result_array(Cursor& c, const char* base, Sink& s) {
       }
     }
     if (s.label_spans) { s.label_spans[2 * s.nseries] = lb; s.label_spans[2 * s.nseries + 1] = le; }
+    if (s.key_hash) s.key_hash[s.nseries] = kh;
     ++s.nseries;
     if (s.offsets) s.offsets[s.nseries] = s.npoints;
     if (c.eat(',')) continue;
@@ -223,6 +344,110 @@ FM_API int fm_prom_fill(const char* buf, int64_t len, double* times, float* valu
   s.label_spans = label_spans;
   if (offsets) offsets[0] = 0;
   return parse_doc(buf, len, s);
+}
+
+// Keyed parse (the brain's batched queries: one response answers many jobs,
+// split by the value of one label, e.g. `pod` or `app`).  Count, then fill:
+// key_hash[i] = FNV-1a 64 of series i's decoded `key` label value (0: absent).
+// The GIL is released by ctypes for the duration of the call, so the fetch
+// threads parse their responses in parallel.
+FM_API int fm_prom_keyed_count(const char* buf, int64_t len, const char* key, int64_t keylen, int64_t* nseries,
+                               int64_t* npoints) {
+  Sink s;
+  s.key = key;
+  s.keylen = keylen;
+  int rc = parse_doc(buf, len, s);
+  *nseries = s.nseries;
+  *npoints = s.npoints;
+  return rc;
+}
+
+FM_API int fm_prom_keyed_fill(const char* buf, int64_t len, const char* key, int64_t keylen, double* times,
+                              float* values, int64_t* offsets, uint64_t* key_hash) {
+  Sink s;
+  s.key = key;
+  s.keylen = keylen;
+  s.times = times;
+  s.values = values;
+  s.offsets = offsets;
+  s.key_hash = key_hash;
+  if (offsets) offsets[0] = 0;
+  return parse_doc(buf, len, s);
+}
+
+// FNV-1a 64 of n strings packed in buf at [off[i], off[i+1]) (UTF-8 bytes).
+FM_API void fm_fnv1a_many(const char* buf, const int64_t* off, int64_t n, uint64_t* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t h = kFnvBasis;
+    for (int64_t j = off[i]; j < off[i + 1]; ++j) h = fnv_byte(h, (unsigned char)buf[j]);
+    out[i] = h;
+  }
+}
+
+// The other direction (demo/promserver.py, the fake Prometheus the HTTP benches
+// and tests talk to): a query_range matrix response from a dense
+// [nseries, npts] float32 grid on the times t0 + k*step; NaN samples are left
+// out, as Prometheus leaves out steps without a sample.  Series i's "metric"
+// object is the pre-rendered JSON at labels[loff[i], loff[i+1]).  Returns the
+// bytes written, or -1 when cap is too small (bound: fm_prom_format_bound).
+FM_API int64_t fm_prom_format_bound(int64_t nseries, int64_t npts, int64_t label_bytes) {
+  return 64 + label_bytes + nseries * 32 + nseries * npts * 48;
+}
+
+FM_API int64_t fm_prom_format(int64_t nseries, const char* labels, const int64_t* loff, double t0, double step,
+                              int64_t npts, const float* values, char* out, int64_t cap) {
+  char* p = out;
+  char* const e = out + cap;
+  auto put = [&](const char* s, size_t n) -> bool {
+    if (e - p < (ptrdiff_t)n) return false;
+    std::memcpy(p, s, n);
+    p += n;
+    return true;
+  };
+  static const char head[] = "{\"status\":\"success\",\"data\":{\"resultType\":\"matrix\",\"result\":[";
+  if (!put(head, sizeof(head) - 1)) return -1;
+  for (int64_t i = 0; i < nseries; ++i) {
+    if (i && !put(",", 1)) return -1;
+    if (!put("{\"metric\":", 10) || !put(labels + loff[i], (size_t)(loff[i + 1] - loff[i])) ||
+        !put(",\"values\":[", 11))
+      return -1;
+    bool first = true;
+    const float* row = values + i * npts;
+    for (int64_t k = 0; k < npts; ++k) {
+      const float v = row[k];
+      if (std::isnan(v)) continue;
+      if (e - p < 48) return -1;
+      if (!first) *p++ = ',';
+      first = false;
+      *p++ = '[';
+      const double t = t0 + step * (double)k;
+      const double tr = std::nearbyint(t);
+      std::to_chars_result r;
+      if (t == tr && std::fabs(t) < 9e15) {
+        r = std::to_chars(p, e, (long long)tr);
+      } else {
+        r = std::to_chars(p, e, t, std::chars_format::fixed, 3);
+      }
+      if (r.ec != std::errc()) return -1;
+      p = r.ptr;
+      *p++ = ',';
+      *p++ = '"';
+      if (std::isinf(v)) {
+        const char* s = v > 0 ? "+Inf" : "-Inf";
+        std::memcpy(p, s, 4);
+        p += 4;
+      } else {
+        r = std::to_chars(p, e, v);          // shortest text that reads back as this float
+        if (r.ec != std::errc()) return -1;
+        p = r.ptr;
+      }
+      *p++ = '"';
+      *p++ = ']';
+    }
+    if (!put("]}", 2)) return -1;
+  }
+  if (!put("]}}", 3)) return -1;
+  return p - out;
 }
 
 // Batch: count every document on a thread pool (the caller then allocates and

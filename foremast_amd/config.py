@@ -102,6 +102,12 @@ class BrainConfig:
     # (one brain per cluster, or a federated Prometheus that drops the label)
     brain_cluster: str = ""                # BRAIN_CLUSTER
     export_sync_s: float = 1.0             # EXPORT_SYNC_SECONDS: ranks > 0 publish their gauges to rank 0
+    # canary window ingestion (engine/ingest.py): a grid point of a live
+    # metric store is read once, METRIC_SETTLE_SECONDS after its time (a
+    # recording rule's value for t is final once its evaluation landed)
+    metric_settle_s: float = 15.0          # METRIC_SETTLE_SECONDS
+    fetch_batch: int = 256                 # FETCH_BATCH: windows (jobs x metric) per batched query_range
+    fetch_max_values: int = 4096           # FETCH_MAX_VALUES: key values (pods) per batched query_range
 
     def rule_for(self, alias: str) -> MetricRule:
         """Per-metric override: exact alias match first, then substring match
@@ -170,6 +176,9 @@ class BrainConfig:
         c.downstream_sync_s = _f(env, "DOWNSTREAM_SYNC_SECONDS", c.downstream_sync_s)
         c.brain_cluster = env.get("BRAIN_CLUSTER", c.brain_cluster)
         c.export_sync_s = _f(env, "EXPORT_SYNC_SECONDS", c.export_sync_s)
+        c.metric_settle_s = _f(env, "METRIC_SETTLE_SECONDS", c.metric_settle_s)
+        c.fetch_batch = _i(env, "FETCH_BATCH", c.fetch_batch)
+        c.fetch_max_values = _i(env, "FETCH_MAX_VALUES", c.fetch_max_values)
         return c
 
 

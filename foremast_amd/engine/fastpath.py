@@ -106,6 +106,10 @@ class FastWork:
     hist: list = field(default_factory=list)   # (metric index, times, values) to write
     errors: list = field(default_factory=list)
     failed: str = ""
+    # canary windows held in the brain's WindowTable (engine/ingest.py): one
+    # window id per metric (-1: no query), None = fetched per job
+    wcur: np.ndarray | None = None
+    wbase: np.ndarray | None = None
 
 
 USED_STAMP_EVERY = 16           # cycles between row last-use stamps (must stay < max_idle_cycles)
@@ -136,6 +140,10 @@ class GroupArrays:
     marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
     models: object = None                      # ModelArrays of a forecasting group (cached with the arrays)
     key: tuple | None = None                   # the group key these arrays were built under
+    wcur: np.ndarray | None = None             # [S * M] window-table ids of a table group's rows
+    wbase: np.ndarray | None = None
+    base: np.ndarray | None = None
+    hist_epoch: int = -1                       # FastPath._hist_epoch the missing-data mask was built at
 
 
 @dataclass
@@ -369,6 +377,11 @@ class FastPath:
         self._gsigs: dict = {}    # interned plan-group signatures
         self._gcount: dict = {}   # plan group -> jobs in self.works
         self._jid_cache: dict = {}  # id(job list) -> (list, JobIds), cleared every cycle
+        from .ingest import WindowTable
+        cfg = brain.cfg
+        self.wt = WindowTable(cfg.metric_settle_s, cfg.fetch_batch, cfg.fetch_max_values)
+        self._wt_changed = False
+        self._hist_epoch = 0       # bumped whenever static history rows were written
 
     # ------------------------------------------------------------------ planning
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
@@ -430,6 +443,7 @@ class FastPath:
         fetch this cycle; a batch identical to the previous cycle's (the
         steady state of a re-examined fleet) reuses the previous lists."""
         self.cycle += 1
+        self._wt_changed = False
         self._col.clear()
         self._jid_cache.clear()
         self.sliding.advance(now, now - self.history_s)
@@ -437,7 +451,7 @@ class FastPath:
         last = self._last
         if last is not None and batch.ids == last[0] and batch.versions == last[1]:
             fast = last[2]
-            self.todo = [fw for fw in last[3] if not (immutable and fw.settled)] if immutable else fast
+            self.todo = [fw for fw in last[3] if not ((immutable or fw.wcur is not None) and fw.settled)]
             self._reused = True
             return fast, []
         self._reused = False
@@ -448,7 +462,7 @@ class FastPath:
             fw = works.get(jid)
             if fw is not None and fw.version == ver:
                 fast.append(fw)
-                if not (immutable and fw.settled):
+                if not ((immutable or fw.wcur is not None) and fw.settled):
                     todo.append(fw)
             else:
                 unknown.append(k)
@@ -471,6 +485,8 @@ class FastPath:
                     end_ts = now
                 fw = works[d.id] = FastWork(d, p, rows, end_ts, version=batch.versions[k],
                                             handle=None if handles is None else int(handles[k]))
+                if not p.sliding:
+                    self._register_windows(fw)
                 self._gcount_add(p.group, 1)
                 fast.append(fw)
                 todo.append(fw)
@@ -499,12 +515,119 @@ class FastPath:
                 (slide.setdefault(fw.plan.group, []) if fw.plan.sliding else rest).append(fw)
         for grp in slide.values():
             self._fetch_sliding(grp, now)
+        tab = [fw for fw in rest if fw.wcur is not None]
+        if tab:
+            # static history of table jobs: app-level 7-day windows, batched
+            # app=~ queries where the source answers them (the rest per job)
+            rest = [fw for fw in rest if fw.wcur is None] + self._fetch_static_history(tab, now, pool)
         if pool is None:
             for fw in rest:
                 self.fetch(fw, now)
         else:
             list(pool.map(lambda fw: self.fetch(fw, now), rest))
+        # canary windows: one incremental, batched round over the whole table
+        self._wt_changed = self.wt.fetch(self.b.sources, now, pool) > 0 or self._wt_changed
         return works
+
+    def _register_windows(self, fw: FastWork) -> None:
+        """Put a static job's current / baseline windows into the window
+        table when every one of them is batchable (a plain selector with one
+        pod / app matcher, absolute times, a source with ``fetch_keyed``);
+        otherwise the job keeps the per-job fetch."""
+        import os
+        if os.environ.get("FM_NO_TABLE"):
+            return
+        from .ingest import parse_range
+        p = fw.plan
+        router = self.b.sources
+        rows = []
+        live = False
+        for urls, stores in ((p.cur_urls, p.cur_stores), (p.base_urls, p.base_stores)):
+            row = []
+            for u, st in zip(urls, stores):
+                if not u:
+                    row.append(None)
+                    continue
+                if router.keyed_source(st) is None:
+                    return
+                spec = parse_range(u)
+                if spec is None:
+                    return
+                row.append((spec, st))
+                live = live or router.live(st)
+            rows.append(row)
+        wt = self.wt
+        fw.wcur, fw.wbase = (np.array([-1 if x is None else wt.add(x[0], router.live(x[1]), x[1]) for x in row],
+                                      np.int64) for row in rows)
+        fw.has_window = True
+        if live:
+            fw.end_ts += wt.settle          # the last grid point is read settle seconds after its time
+        w = max(wt.max_points(fw.wcur), wt.max_points(fw.wbase))
+        fw.wclass = 0 if w <= 128 else (1 if w <= 256 else 2)
+
+    def _fetch_static_history(self, ws: list[FastWork], now: float, pool=None) -> list[FastWork]:
+        """Batched static history (``namespace_app_pod_<m>{namespace,app}`` over
+        the job's 7 days): jobs whose needed history rows all parse as
+        app-keyed selectors of a batched source share ``app=~`` requests of up
+        to ``fetch_batch`` apps per (selector, window).  Returns the jobs left
+        for the per-job fetch."""
+        from .brain import _app_level
+        from .ingest import KeyedQuery, keyed_split, parse_range
+        from .sources import Series
+        router = self.b.sources
+        groups: dict[tuple, list] = {}
+        left = []
+        for fw in ws:
+            p = fw.plan
+            need = ~np.isfinite(self.static.last_t[fw.rows])
+            fw.hist = []
+            items = []
+            ok = True
+            for i in np.flatnonzero(need).tolist():
+                u = p.hist_urls[i]
+                if not u:
+                    continue
+                spec = parse_range(u, keys=("app",))
+                if spec is None or len(spec.values) != 1 or router.keyed_source(p.hist_stores[i]) is None:
+                    ok = False
+                    break
+                items.append((i, spec, p.hist_stores[i]))
+            if not ok:
+                left.append(fw)
+                continue
+            for i, spec, st in items:
+                groups.setdefault((st, spec.group, spec.start, spec.end), []).append((fw, i, spec.values[0]))
+        reqs = []
+        B = max(1, self.b.cfg.fetch_batch)
+        for (st, grp, a, b), items in groups.items():
+            for k in range(0, len(items), B):
+                chunk = items[k:k + B]
+                q = KeyedQuery(grp, sorted({x[2] for x in chunk}), a, b)
+                q.store = st
+                reqs.append((q, chunk))
+        by_store: dict[str, list[int]] = {}
+        for j, (q, _) in enumerate(reqs):
+            by_store.setdefault(q.store, []).append(j)
+        got: list = [None] * len(reqs)
+        for st, idx in by_store.items():
+            for j, g in zip(idx, router.keyed_source(st).fetch_keyed([reqs[j][0] for j in idx], pool=pool)):
+                got[j] = g
+        for (q, chunk), g in zip(reqs, got):
+            if isinstance(g, BaseException):
+                for fw, i, _ in chunk:
+                    fw.errors.append(f"historical/{fw.plan.aliases[i]}: {g}")
+                continue
+            per = dict(zip(q.values, keyed_split(g, q.values)))
+            for fw, i, app in chunk:
+                ss = [Series({}, t, v) for t, v in per.get(app, [])]
+                v, _ = _app_level(ss)
+                fw.hist.append((i, np.asarray([_app_level_last(ss)]), v))
+        lid = {id(fw) for fw in left}
+        for fw in ws:
+            if id(fw) not in lid:
+                fw.dirty = True
+                fw.settled = False
+        return left
 
     def _columns(self, store_types: list, tpls: list, lo: float, hi: float):
         """-> (lens [n], t, v) in request order ('' templates: no samples)."""
@@ -657,9 +780,11 @@ class FastPath:
         fw.errors = []
         wins = b._windows(fw.doc, now)
         cv, ct, cl, bv, bl = [], [], [], [], []
+        tab = fw.wcur is not None                  # windows come from the window table
         for i, a in enumerate(p.aliases):
-            for cat, urls, stores, vals, lens, times in (("current", p.cur_urls, p.cur_stores, cv, cl, ct),
-                                                         ("baseline", p.base_urls, p.base_stores, bv, bl, None)):
+            for cat, urls, stores, vals, lens, times in (() if tab else
+                                                         (("current", p.cur_urls, p.cur_stores, cv, cl, ct),
+                                                          ("baseline", p.base_urls, p.base_stores, bv, bl, None))):
                 url = urls[i]
                 got = []
                 if url:
@@ -691,6 +816,10 @@ class FastPath:
                         fw.hist.append((i, t, v))
                     except (SourceError, OSError, ValueError) as e:
                         fw.errors.append(f"historical/{a}: {e}")
+        if tab:
+            fw.dirty = True
+            fw.settled = fw.hist_complete
+            return fw
         cat = lambda xs, dt: np.concatenate(xs).astype(dt, copy=False) if xs else np.zeros(0, dt)
         fw.cur, fw.cur_t, fw.base = cat(cv, np.float32), cat(ct, np.float64), cat(bv, np.float32)
         fw.cur_len, fw.base_len = np.asarray(cl, np.int64), np.asarray(bl, np.int64)
@@ -725,6 +854,7 @@ class FastPath:
                     stl.append(t[0] if len(t) else -np.inf)
         if srows:
             self.static.write_static(np.asarray(srows, np.int64), svals, np.asarray(stl, np.float64))
+            self._hist_epoch += 1
         if drows:
             self.sliding.write_sliding(np.asarray(drows, np.int64), dts, dvs)
         for fw in got:
@@ -744,14 +874,14 @@ class FastPath:
         if works and len(self._gcount) == 1 and works[0].plan.sliding and len(self.todo) == len(works):
             # one sliding group fetched whole this cycle: _fetch_sliding gave
             # every job the same width class, so no per-job bucketing
-            g = {works[0].plan.group + (works[0].wclass,): works}
+            g = {works[0].plan.group + (works[0].wclass, False): works}
             self._last_groups = g
             return g
         g: dict[tuple, list[FastWork]] = {}
         for fw in works:
             k = fw.gkey
-            if k is None or k[-1] != fw.wclass:
-                k = fw.gkey = fw.plan.group + (fw.wclass,)
+            if k is None or k[-2] != fw.wclass:
+                k = fw.gkey = fw.plan.group + (fw.wclass, fw.wcur is not None)
             g.setdefault(k, []).append(fw)
         self._last_groups = g
         return g
@@ -767,6 +897,8 @@ class FastPath:
     def _arrays(self, works: list[FastWork], key: tuple) -> GroupArrays:
         """The group's packed arrays: rebuilt only when its job list or any
         job's data changed since the last cycle."""
+        if works[0].wcur is not None:
+            return self._arrays_table(works, key)
         ga = self._garr.get(key)
         if ga is not None and ga.works is works and self._reused and not self.todo:
             return ga                     # same job list object, nothing fetched: nothing changed
@@ -803,6 +935,69 @@ class FastPath:
         has_cur = np.isfinite(cur).any(1).reshape(S, M)
         ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
                          up(rowmap), end, ~(has_hist & has_cur), handles=handles, works=works)
+        if xslots is not None:
+            ga.export_slots = xslots
+            ga.export_start = self.b.exporter.contiguous_start(xslots)
+        for w in works:
+            w.dirty = False
+        ga.key = key
+        self._garr[key] = ga
+        return ga
+
+    def _arrays_table(self, works: list[FastWork], key: tuple) -> GroupArrays:
+        """Packed arrays of a group whose windows live in the window table:
+        built once per job list, then only the rows whose windows gained
+        samples are re-packed (``fm_window_pack``) and re-uploaded -- a live
+        canary fleet gets one new step per window per minute."""
+        wt = self.wt
+        p0 = works[0].plan
+        M, S = len(p0.aliases), len(works)
+        dev = self.b.device
+        store = self.static
+        up = lambda a: (torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"  # noqa: E731
+                        else torch.from_numpy(a))
+        ga = self._garr.get(key)
+        if ga is not None and ga.wcur is not None and (ga.works is works or ga.ident == self._jid(works)):
+            ga.works = works
+            changed = False
+            if self._wt_changed:
+                wc, wb = ga.wcur, ga.wbase
+                d = wt.dirty[np.maximum(wc, 0)] & (wc >= 0)
+                if wb is not None:
+                    d |= wt.dirty[np.maximum(wb, 0)] & (wb >= 0)
+                rows = np.flatnonzero(d)
+                if len(rows):
+                    changed = True
+                    ri = torch.from_numpy(rows).to(dev)
+                    v, t, ln = wt.pack(wc[rows], ga.cur.shape[1])
+                    ga.cur[rows], ga.cur_t[rows], ga.cur_len[rows] = v, t, ln
+                    ga.cur_d.index_copy_(0, ri, up(v))
+                    wt.dirty[wc[rows][wc[rows] >= 0]] = False
+                    if ga.base_d is not None:
+                        bv, _, _ = wt.pack(wb[rows], ga.base.shape[1], times=False)
+                        ga.base[rows] = bv
+                        ga.base_d.index_copy_(0, ri, up(bv))
+                        wt.dirty[wb[rows][wb[rows] >= 0]] = False
+            if changed or ga.hist_epoch != self._hist_epoch:
+                has_hist = np.isfinite(store.last_t[ga.rowmap]).reshape(S, M)
+                ga.missing = ~(has_hist & (ga.cur_len > 0).reshape(S, M))
+                ga.hist_epoch = self._hist_epoch
+                ga.models = None
+            return ga
+        ident = self._jid(works)
+        rowmap, ids, handles, end, xslots = self._static_cols(works, ident, key, M)
+        wc = self._extra(key, ident, "wcur", lambda: np.stack([w.wcur for w in works])).reshape(-1)
+        wb = self._extra(key, ident, "wbase", lambda: np.stack([w.wbase for w in works])).reshape(-1)
+        n = max(1, wt.max_points(wc))
+        cur, cur_t, cur_len = wt.pack(wc, n)
+        nb = wt.max_points(wb)
+        base = wt.pack(wb, nb, times=False)[0] if nb else None
+        has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
+        ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
+                         up(rowmap), end, ~(has_hist & (cur_len > 0).reshape(S, M)), handles=handles, works=works)
+        ga.wcur, ga.wbase, ga.base, ga.hist_epoch = wc, (wb if base is not None else None), base, self._hist_epoch
+        wt.dirty[wc[wc >= 0]] = False
+        wt.dirty[wb[wb >= 0]] = False
         if xslots is not None:
             ga.export_slots = xslots
             ga.export_start = self.b.exporter.contiguous_start(xslots)
@@ -1390,10 +1585,14 @@ class FastPath:
         outcome["hpa_scored"] = outcome.get("hpa_scored", 0) + S
 
     def _release(self, works: list[FastWork]) -> None:
-        """Terminal jobs: their static history rows and plans are dropped."""
+        """Terminal jobs: their static history rows, table windows and plans
+        are dropped."""
         keys = [k for w in works if not w.plan.sliding for k in w.plan.keys]
         if keys:
             self.static.release(keys)
+        wins = [a for w in works if w.wcur is not None for a in (w.wcur, w.wbase)]
+        if wins:
+            self.wt.release(np.concatenate(wins))
         for w in works:
             if self.works.get(w.doc.id) is w:
                 del self.works[w.doc.id]
@@ -1413,7 +1612,10 @@ class FastPath:
             stale = [k for k, w in self.works.items()
                      if (self.sliding if w.plan.sliding else self.static).keys[int(w.rows[0])] != w.plan.keys[0]]
             for k in stale:
-                self._gcount_add(self.works.pop(k).plan.group, -1)
+                w = self.works.pop(k)
+                self._gcount_add(w.plan.group, -1)
+                if w.wcur is not None:
+                    self.wt.release(np.concatenate([w.wcur, w.wbase]))
 
 
 def _merge_series(ss) -> tuple[np.ndarray, np.ndarray]:

@@ -1,0 +1,506 @@
+"""Fleet-scale ingestion of canary windows: batched, incremental query_range.
+
+Barrelman gives every canary job pod-level windows per metric
+(foremast-barrelman/pkg/client/metrics/metricsquery.go:72-92):
+
+* **current** ``namespace_pod_<m>{namespace="ns",pod=~"a|b"}`` over
+  [now+60 s, now+(W+1) min] -- a window in the *future* at submission, so its
+  samples arrive while the job runs;
+* **baseline** the same selector on the old pods over the fixed past
+  [now-W, now].
+
+Fetched per job, that is 2·M HTTP requests per job per cycle (160k per
+cycle at 10k jobs x 8 metrics).  Here every window is a row block of one
+columnar table instead:
+
+* **batched** -- windows whose selectors differ only in the key label
+  (``pod`` / ``app``) and share the step grid (same step and start mod step)
+  are answered by ONE ``query_range`` with the union of their key values
+  (``pod=~"<union>"``, up to ``batch`` windows / ``max_values`` key values
+  per request), split back by the series' key label -- the native keyed
+  parser (``csrc/runtime/promparse.cpp``) reports a hash of that label per
+  series, so the split is array work, not per-series Python;
+* **incremental** -- a window remembers through which grid time it is
+  complete (``settled``).  A live source (real Prometheus: nothing exists
+  after *now*) is asked only for grid points in (settled, now - settle];
+  a past window (baseline) is therefore fetched once, a future one (current)
+  one new step at a time, and a cycle in which no window gained a grid point
+  sends no request at all.  A non-live source (synthetic, pre-staged)
+  answers the whole window at once, so its windows settle in one fetch.
+* **columnar** -- samples live in a dense [slots, columns] grid (one slot per
+  pod, one column per step); scoring reads any subset of (job, metric) rows
+  out of it packed pod-major / time-minor, NaN-padded -- exactly the
+  concatenation of the per-job answer's series (``fm_window_pack``).
+
+Series order inside a window is the order Prometheus returns them in: sorted
+by label set, i.e. by the key value for one metric and namespace.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import urllib.parse
+from dataclasses import dataclass
+
+import numpy as np
+
+from ..api.urls import END_PLACEHOLDER, START_PLACEHOLDER
+from . import native_rt
+from . import promql
+
+KEY_LABELS = ("pod", "app")
+
+
+def parse_step(s: str) -> float | None:
+    """A query_range ``step``: seconds as a float or a Prometheus duration."""
+    try:
+        return float(s)
+    except ValueError:
+        pass
+    units = {"ms": 1e-3, "s": 1.0, "m": 60.0, "h": 3600.0, "d": 86400.0, "w": 604800.0, "y": 31536000.0}
+    import re
+    parts = re.findall(r"(\d+(?:\.\d+)?)(ms|s|m|h|d|w|y)", s)
+    if not parts or "".join(a + b for a, b in parts) != s:
+        return None
+    return sum(float(a) * units[b] for a, b in parts)
+
+
+@dataclass(frozen=True)
+class RangeSpec:
+    """A ``query_range`` URL whose query is a plain selector with exactly one
+    matcher on a key label: the batchable form.  ``matchers`` holds the other
+    matchers, with ``(key, "", "")`` where the key matcher was (rendering keeps
+    the original label order)."""
+    base: str
+    metric: str
+    matchers: tuple
+    key: str
+    values: tuple
+    start: float
+    end: float
+    step: float
+    extra: tuple = ()
+
+    @property
+    def group(self) -> tuple:
+        return (self.base, self.metric, self.matchers, self.key, self.step, self.extra)
+
+
+def parse_range(url: str, keys=KEY_LABELS, windowed: bool = True) -> RangeSpec | None:
+    """``windowed``: start / end must be absolute times (static windows); else
+    ``START_TIME`` / ``END_TIME`` placeholders are accepted (start = end = nan)."""
+    if "query_range?" not in url:
+        return None
+    base, qs = url.split("?", 1)
+    params = urllib.parse.parse_qsl(qs, keep_blank_values=True)
+    d = dict(params)
+    if len(d) != len(params) or "query" not in d:
+        return None
+    sel = promql.parse_selector(d["query"])
+    if sel is None:
+        return None
+    metric, ms = sel
+    kpos = [i for i, (k, op, _) in enumerate(ms) if k in keys and op in ("=", "=~")]
+    if len(kpos) != 1 or sum(1 for k, _, _ in ms if k == ms[kpos[0]][0]) != 1:
+        return None
+    k, op, v = ms[kpos[0]]
+    values = (v,) if op == "=" else promql.literal_alternatives(v)
+    if not values or any(x == "" for x in values):
+        return None
+    step = parse_step(d.get("step", "60"))
+    if step is None or step <= 0:
+        return None
+    s, e = d.get("start", ""), d.get("end", "")
+    if windowed:
+        try:
+            start, end = float(s), float(e)
+        except ValueError:
+            return None
+    elif s == START_PLACEHOLDER and e == END_PLACEHOLDER:
+        start = end = math.nan
+    else:
+        return None
+    extra = tuple(sorted((a, b) for a, b in params if a not in ("query", "start", "end", "step")))
+    mt = tuple((kk, "", "") if i == kpos[0] else (kk, oo, vv) for i, (kk, oo, vv) in enumerate(ms))
+    return RangeSpec(base, metric, mt, k, tuple(values), start, end, step, extra)
+
+
+def render_query(group: tuple, values, alt: str | None = None) -> str:
+    """The PromQL text of a batched selector: the group's matchers with the key
+    matcher as ``key="v"`` (one value) or ``key=~"v1|v2"`` (escaped literals;
+    ``alt``: that regex already joined)."""
+    _, metric, matchers, key, _, _ = group
+    values = list(values) if values is not None else None
+    parts = []
+    for k, op, v in matchers:
+        if k == key and op == "":
+            if alt is not None:
+                parts.append(k + "=~" + promql.quote(alt))
+            else:
+                parts.append(promql.equal_matcher(k, values[0]) if len(values) == 1
+                             else promql.regex_matcher(k, values))
+        else:
+            parts.append(k + op + promql.quote(v))
+    return metric + "{" + ",".join(parts) + "}"
+
+
+def series_identity(group: tuple, value: str) -> str:
+    """The selector of ONE series of a batched query (its key value pinned):
+    what a per-job query for just that series would read."""
+    return render_query(group, [value])
+
+
+def identities(group: tuple, values) -> list[str]:
+    """:func:`series_identity` of many values (one template render)."""
+    mark = "\x00"
+    pre, post = render_query(group, [mark]).split(promql.quote(mark))
+    return [pre + promql.quote(v) + post for v in values]
+
+
+@dataclass
+class KeyedQuery:
+    """One batched request: the group's selector over the key ``values`` on
+    [start, end] (grid start + k * step).  ``alt``: the key regex
+    pre-joined from per-window fragments (``values`` is then derived lazily)."""
+    group: tuple
+    values: list | None
+    start: float
+    end: float
+    alt: str | None = None
+    parts: list | None = None            # the key values per window (alt's source)
+    store: str = "prometheus"            # metric store type the query goes to
+
+    def key_values(self) -> list:
+        if self.values is None:
+            self.values = [v for p in self.parts for v in p]
+        return self.values
+
+    @property
+    def query(self) -> str:
+        return render_query(self.group, self.values, self.alt)
+
+    @property
+    def url_params(self) -> dict:
+        return {"query": self.query, "start": _fmt_t(self.start),
+                "end": _fmt_t(self.end), "step": _fmt_t(self.group[4]), **dict(self.group[5])}
+
+
+def _fmt_t(x: float) -> str:
+    return str(int(x)) if float(x).is_integer() else repr(float(x))
+
+
+def _ranges(starts: np.ndarray, counts: np.ndarray) -> np.ndarray:
+    """concat(arange(s, s + c) for s, c) without a Python loop."""
+    tot = int(counts.sum())
+    if tot == 0:
+        return np.zeros(0, np.int64)
+    rep = np.repeat(starts - np.concatenate([[0], np.cumsum(counts)[:-1]]), counts)
+    return rep + np.arange(tot)
+
+
+class WindowTable:
+    """Every static window of the brain's canary jobs, columnar (see the
+    module docstring).  Window ids are stable until :meth:`release`."""
+
+    def __init__(self, settle: float = 0.0, batch: int = 256, max_values: int = 4096):
+        self.settle = float(settle)
+        self.batch = int(batch)
+        self.max_values = int(max_values)
+        self.n = 0
+        self._cap = 0
+        self.start = np.zeros(0)
+        self.end = np.zeros(0)
+        self.step = np.zeros(0)
+        self.settled = np.zeros(0)           # complete through this grid time (start - step: nothing yet)
+        self.gid = np.zeros(0, np.int64)
+        self.slot0 = np.zeros(0, np.int64)
+        self.nslot = np.zeros(0, np.int64)
+        self.ncol = np.zeros(0, np.int64)
+        self.live = np.zeros(0, bool)
+        self.alive = np.zeros(0, bool)
+        self.dirty = np.zeros(0, bool)       # data changed since the scoring arrays last read it
+        self.err = np.zeros(0, bool)         # last fetch of the window failed
+        self.toff = np.zeros(0)              # sample phase vs start (0 for Prometheus; nan: not seen yet)
+        self.values: list = []               # key values (sorted) per window
+        self.frag: list = []                 # their escaped regex alternation
+        self.groups: dict[tuple, int] = {}
+        self.group_keys: list[tuple] = []
+        self._free_w: list[int] = []
+        # slots
+        self.C = 16
+        self.V = np.full((0, self.C), np.nan, np.float32)
+        self.khash = np.zeros(0, np.uint64)
+        self.kwin = np.zeros(0, np.int64)
+        self.ns = 0
+        self._free_s: dict[int, list[int]] = {}
+        self.next_due = -math.inf            # earliest time a live window can gain a grid point
+        self.requests = 0                    # counters (bench / tests)
+        self.last_requests = 0
+
+    # ------------------------------------------------------------ membership
+    def _grow_w(self, need: int) -> None:
+        if need <= self._cap:
+            return
+        cap = max(need, 2 * self._cap, 1024)
+        for name, fill in (("start", 0.0), ("end", 0.0), ("step", 1.0), ("settled", 0.0), ("gid", 0),
+                           ("slot0", -1), ("nslot", 0), ("ncol", 0), ("live", False), ("alive", False),
+                           ("dirty", False), ("err", False), ("toff", np.nan)):
+            old = getattr(self, name)
+            a = np.full(cap, fill, old.dtype)
+            a[:len(old)] = old
+            setattr(self, name, a)
+        self._cap = cap
+
+    def _alloc_slots(self, k: int) -> int:
+        fl = self._free_s.get(k)
+        if fl:
+            return fl.pop()
+        s0 = self.ns
+        self.ns += k
+        if self.ns > self.V.shape[0]:
+            cap = max(self.ns, 2 * self.V.shape[0], 4096)
+            V = np.full((cap, self.C), np.nan, np.float32)
+            V[:self.V.shape[0]] = self.V
+            self.V = V
+            kh = np.zeros(cap, np.uint64)
+            kh[:len(self.khash)] = self.khash
+            self.khash = kh
+            kw = np.full(cap, -1, np.int64)
+            kw[:len(self.kwin)] = self.kwin
+            self.kwin = kw
+        return s0
+
+    def add(self, spec: RangeSpec, live: bool, store: str = "prometheus") -> int:
+        """A new window (its key values sorted as Prometheus orders series)."""
+        vals = sorted(set(spec.values))
+        ncol = max(0, int(math.floor((spec.end - spec.start) / spec.step + 1e-9)) + 1)
+        if ncol > self.C:
+            C = max(ncol, 2 * self.C)
+            V = np.full((self.V.shape[0], C), np.nan, np.float32)
+            V[:, :self.C] = self.V
+            self.V, self.C = V, C
+        w = self._free_w.pop() if self._free_w else self.n
+        if w == self.n:
+            self._grow_w(self.n + 1)
+            self.n += 1
+            self.values.append(None)
+            self.frag.append(None)
+        gk = (spec.group, store)
+        g = self.groups.get(gk)
+        if g is None:
+            g = self.groups[gk] = len(self.group_keys)
+            self.group_keys.append(gk)
+        s0 = self._alloc_slots(len(vals))
+        self.V[s0:s0 + len(vals)] = np.nan
+        self.khash[s0:s0 + len(vals)] = native_rt.fnv1a(vals)
+        self.kwin[s0:s0 + len(vals)] = w
+        self.start[w], self.end[w], self.step[w] = spec.start, spec.end, spec.step
+        self.settled[w] = spec.start - spec.step
+        self.gid[w], self.slot0[w], self.nslot[w], self.ncol[w] = g, s0, len(vals), ncol
+        self.live[w], self.alive[w], self.dirty[w], self.err[w] = live, True, True, False
+        self.toff[w] = np.nan
+        self.values[w] = vals
+        self.frag[w] = "|".join(promql.re_literal(v) for v in vals)
+        self.next_due = -math.inf
+        return w
+
+    def release(self, wids) -> None:
+        for w in np.asarray(wids, np.int64).reshape(-1).tolist():
+            if w < 0 or w >= self.n or not self.alive[w]:
+                continue
+            s0, k = int(self.slot0[w]), int(self.nslot[w])
+            self.V[s0:s0 + k] = np.nan
+            self.kwin[s0:s0 + k] = -1
+            self._free_s.setdefault(k, []).append(s0)
+            self.alive[w] = False
+            self.dirty[w] = False
+            self.values[w] = None
+            self.frag[w] = None
+            self._free_w.append(w)
+
+    def complete(self, wids: np.ndarray) -> np.ndarray:
+        """Windows that hold every grid point they will ever get."""
+        w = np.asarray(wids, np.int64)
+        return self.settled[w] >= self.end[w] - 1e-6
+
+    # ------------------------------------------------------------ fetching
+    def _limit(self, w: np.ndarray, now: float) -> np.ndarray:
+        """Newest grid time each window may be asked for now."""
+        st, sp = self.start[w], self.step[w]
+        lim = np.where(self.live[w], np.minimum(self.end[w], now - self.settle), self.end[w])
+        return st + np.floor((lim - st) / sp + 1e-9) * sp
+
+    def pending(self, now: float) -> list[tuple[KeyedQuery, np.ndarray, np.ndarray, np.ndarray]]:
+        """The requests this cycle needs: (query, window ids, lo, hi) per
+        batched request, lo / hi = the grid range each window takes from it."""
+        if self.n == 0 or now < self.next_due:
+            return []
+        w = np.flatnonzero(self.alive[:self.n] & (self.settled[:self.n] < self.end[:self.n] - 1e-6))
+        if not len(w):
+            self.next_due = math.inf
+            return []
+        lo = self.settled[w] + self.step[w]
+        hi = self._limit(w, now)
+        need = lo <= hi + 1e-6
+        # the earliest time a waiting live window gains a point (skip cycles before it)
+        wait = ~need & self.live[w]
+        self.next_due = float((lo[wait] + self.settle).min()) if wait.any() else math.inf
+        if not need.any():
+            return []
+        if (~need & ~self.live[w]).any():
+            self.next_due = -math.inf
+        w, lo, hi = w[need], lo[need], hi[need]
+        phase = np.round(np.mod(self.start[w], self.step[w]), 3)
+        order = np.lexsort((w, phase, self.gid[w]))
+        w, lo, hi, phase = w[order], lo[order], hi[order], phase[order]
+        g = self.gid[w]
+        brk = np.flatnonzero((g[1:] != g[:-1]) | (phase[1:] != phase[:-1])) + 1
+        out = []
+        frag, values = self.frag, self.values
+        for a, b in zip(np.concatenate([[0], brk]).tolist(), np.concatenate([brk, [len(w)]]).tolist()):
+            # fixed chunk size per run: <= batch windows and <= max_values key values
+            per = max(1, min(self.batch, self.max_values // max(1, int(self.nslot[w[a:b]].max()))))
+            for i in range(a, b, per):
+                j = min(b, i + per)
+                wl = w[i:j].tolist()
+                grp, store = self.group_keys[int(g[i])]
+                q = KeyedQuery(grp, None, float(lo[i:j].min()), float(hi[i:j].max()),
+                               alt="|".join([frag[x] for x in wl]), parts=[values[x] for x in wl])
+                q.store = store
+                out.append((q, w[i:j], lo[i:j], hi[i:j]))
+        return out
+
+    def apply(self, ws: np.ndarray, lo: np.ndarray, hi: np.ndarray, got) -> None:
+        """Write one batched answer (a native_rt.Keyed, or an exception) into
+        its windows; each window takes the samples on its own grid in
+        [lo, hi]."""
+        if isinstance(got, BaseException):
+            self.err[ws] = True
+            return
+        self.err[ws] = False
+        kslots = _ranges(self.slot0[ws], self.nslot[ws])
+        kw_lo = np.repeat(lo, self.nslot[ws])
+        kw_hi = np.repeat(hi, self.nslot[ws])
+        if len(got.key) and len(kslots):
+            kh = self.khash[kslots]
+            order = np.argsort(kh, kind="stable")
+            skh = kh[order]
+            a = np.searchsorted(skh, got.key, "left")
+            b = np.searchsorted(skh, got.key, "right")
+            cnt = b - a                                                   # slots per series
+            if cnt.any():
+                ser = np.repeat(np.arange(len(got.key)), cnt)             # (series, slot) pairs
+                pos = order[_ranges(a, cnt)]                              # index into kslots
+                slen = np.diff(got.off)[ser]
+                samp = _ranges(got.off[:-1][ser], slen)                   # (pair, sample)
+                pidx = np.repeat(pos, slen)
+                slot = kslots[pidx]
+                wv = self.kwin[slot]
+                t = got.t[samp]
+                # samples sit at start + toff + c * step: toff = 0 for a Prometheus
+                # query_range; a source on an absolute grid (synthetic) has its phase
+                d = np.mod(t - self.start[wv], self.step[wv])
+                d = np.where(self.step[wv] - d < 1e-3, 0.0, d)
+                unseen = np.isnan(self.toff[wv])
+                if unseen.any():
+                    self.toff[wv[unseen]] = d[unseen]
+                to = self.toff[wv]
+                c = np.rint((t - self.start[wv] - to) / self.step[wv]).astype(np.int64)
+                ok = ((t >= kw_lo[pidx] - 1e-6) & (t <= kw_hi[pidx] + 1e-6) & (c >= 0) & (c < self.ncol[wv])
+                      & (np.abs(d - to) < 1e-3))
+                self.V[slot[ok], c[ok]] = got.v[samp[ok]]
+        self.settled[ws] = np.maximum(self.settled[ws], hi)
+        self.dirty[ws] = True
+
+    def fetch(self, router, now: float, pool=None) -> int:
+        """One incremental round: every due request, per metric store through
+        its source's ``fetch_keyed`` (``router``: a SourceRouter, or one source
+        for every store).  Returns the number of requests sent."""
+        reqs = self.pending(now)
+        self.last_requests = len(reqs)
+        if not reqs:
+            return 0
+        by_store: dict[str, list[int]] = {}
+        for i, r in enumerate(reqs):
+            by_store.setdefault(r[0].store, []).append(i)
+        from .sources import SourceError
+        for store, idx in by_store.items():
+            src = router.keyed_source(store) if hasattr(router, "keyed_source") else router
+            if src is None:
+                got = [SourceError(f"no batched source for metric store {store!r}")] * len(idx)
+            else:
+                got = src.fetch_keyed([reqs[i][0] for i in idx], pool=pool)
+            for i, g in zip(idx, got):
+                _, ws, lo, hi = reqs[i]
+                self.apply(ws, lo, hi, g)
+        self.requests += len(reqs)
+        return len(reqs)
+
+    # ------------------------------------------------------------ read-out
+    def max_points(self, wids) -> int:
+        w = np.asarray(wids, np.int64)
+        w = w[w >= 0]
+        return int((self.nslot[w] * self.ncol[w]).max()) if len(w) else 0
+
+    def pack(self, wids: np.ndarray, width: int | None = None, times: bool = True):
+        """(values [R, n] float32, times [R, n] float64 or None, lens [R]):
+        row r = window ``wids[r]``'s samples pod-major / time-minor, missing
+        steps squeezed out, NaN-padded; ``wids[r] < 0`` -> an empty row."""
+        w = np.ascontiguousarray(wids, np.int64).reshape(-1)
+        R = len(w)
+        n = max(1, self.max_points(w) if width is None else int(width))
+        ok = w >= 0
+        wz = np.where(ok, w, 0)
+        slot0 = np.where(ok, self.slot0[wz], -1).astype(np.int64)
+        nslot = np.where(ok, self.nslot[wz], 0).astype(np.int64)
+        ncol = np.where(ok, self.ncol[wz], 0).astype(np.int64)
+        start = np.ascontiguousarray(self.start[wz] + np.nan_to_num(self.toff[wz]), np.float64)
+        step = np.ascontiguousarray(self.step[wz], np.float64)
+        out_v = np.empty((R, n), np.float32)
+        out_t = np.empty((R, n), np.float64) if times else None
+        lens = np.empty(R, np.int64)
+        lib = native_rt._load()
+        if lib is not None and hasattr(lib, "fm_window_pack") and R:
+            if not getattr(lib, "_wp_typed", False):
+                c_vp, c_i64 = ctypes.c_void_p, ctypes.c_int64
+                lib.fm_window_pack.argtypes = [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
+                                               c_vp, ctypes.c_int]
+                lib.fm_window_pack.restype = None
+                lib._wp_typed = True
+            V = self.V if self.V.flags.c_contiguous else np.ascontiguousarray(self.V)
+            lib.fm_window_pack(V.ctypes.data, V.shape[1], slot0.ctypes.data, nslot.ctypes.data, ncol.ctypes.data,
+                               start.ctypes.data, step.ctypes.data, R, out_v.ctypes.data,
+                               out_t.ctypes.data if times else None, n, lens.ctypes.data, 4)
+            return out_v, out_t, lens
+        out_v.fill(np.nan)
+        if times:
+            out_t.fill(np.nan)
+        for r in range(R):
+            if slot0[r] < 0:
+                lens[r] = 0
+                continue
+            blk = self.V[slot0[r]:slot0[r] + nslot[r], :ncol[r]]
+            fin = np.isfinite(blk)
+            vals = blk[fin][:n]
+            lens[r] = len(vals)
+            out_v[r, :len(vals)] = vals
+            if times:
+                tt = np.broadcast_to(start[r] + step[r] * np.arange(ncol[r]), blk.shape)[fin][:n]
+                out_t[r, :len(tt)] = tt
+        return out_v, out_t, lens
+
+
+def keyed_split(got, values: list[str]) -> list[list[tuple[np.ndarray, np.ndarray]]]:
+    """Per key value, its series' (times, values) from a batched answer."""
+    out: list[list] = [[] for _ in values]
+    if isinstance(got, BaseException) or not len(got.key):
+        return out
+    kh = native_rt.fnv1a(values)
+    order = np.argsort(kh, kind="stable")
+    skh = kh[order]
+    a = np.searchsorted(skh, got.key, "left")
+    b = np.searchsorted(skh, got.key, "right")
+    for i in np.flatnonzero(b > a).tolist():
+        for j in order[a[i]:b[i]].tolist():
+            out[j].append((got.t[got.off[i]:got.off[i + 1]], got.v[got.off[i]:got.off[i + 1]]))
+    return out

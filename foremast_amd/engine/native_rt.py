@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import ctypes
 import json
+from dataclasses import dataclass
 from pathlib import Path
 
 import numpy as np
@@ -43,6 +44,18 @@ def _load():
                                    ctypes.c_double, c_vp, c_vp, ctypes.c_char_p, c_vp, ctypes.c_char_p, c_vp,
                                    c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, ctypes.c_int]
     lib.fm_hpalog_json.restype = c_i64
+    lib.fm_prom_keyed_count.argtypes = [ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64, ctypes.POINTER(c_i64),
+                                        ctypes.POINTER(c_i64)]
+    lib.fm_prom_keyed_count.restype = ctypes.c_int
+    lib.fm_prom_keyed_fill.argtypes = [ctypes.c_char_p, c_i64, ctypes.c_char_p, c_i64, c_vp, c_vp, c_vp, c_vp]
+    lib.fm_prom_keyed_fill.restype = ctypes.c_int
+    lib.fm_fnv1a_many.argtypes = [ctypes.c_char_p, c_vp, c_i64, c_vp]
+    lib.fm_fnv1a_many.restype = None
+    lib.fm_prom_format_bound.argtypes = [c_i64, c_i64, c_i64]
+    lib.fm_prom_format_bound.restype = c_i64
+    lib.fm_prom_format.argtypes = [c_i64, ctypes.c_char_p, c_vp, ctypes.c_double, ctypes.c_double, c_i64, c_vp,
+                                   c_vp, c_i64]
+    lib.fm_prom_format.restype = c_i64
     _lib = lib
     return lib
 
@@ -72,6 +85,103 @@ def parse_prometheus(body: bytes):
         labels = json.loads(body[a:b]) if a >= 0 else {}
         out.append(Series(labels, t[off[i]:off[i + 1]], v[off[i]:off[i + 1]]))
     return out
+
+
+_FNV_BASIS = 1469598103934665603
+_FNV_PRIME = 1099511628211
+_M64 = (1 << 64) - 1
+
+
+def fnv1a(names) -> np.ndarray:
+    """FNV-1a 64 of each string's UTF-8 bytes (uint64) -- the hash the keyed
+    parser reports for a series' key label."""
+    names = list(names)
+    out = np.empty(len(names), np.uint64)
+    if not names:
+        return out
+    lib = _load()
+    if lib is None:
+        for i, s in enumerate(names):
+            h = _FNV_BASIS
+            for b in s.encode():
+                h = ((h ^ b) * _FNV_PRIME) & _M64
+            out[i] = h
+        return out
+    buf, off = _joined(names)
+    lib.fm_fnv1a_many(buf, off.ctypes.data, len(names), out.ctypes.data)
+    return out
+
+
+@dataclass
+class Keyed:
+    """A query_range matrix split by one label: series i has key hash
+    ``key[i]`` (FNV-1a of the label's value, 0 if absent) and samples
+    ``t[off[i]:off[i+1]]`` / ``v[...]``."""
+    key: np.ndarray
+    off: np.ndarray
+    t: np.ndarray
+    v: np.ndarray
+
+
+def parse_keyed(body: bytes, label: str) -> Keyed:
+    from .sources import SourceError
+    lib = _load()
+    if lib is None:
+        d = json.loads(body)
+        if d.get("status") != "success":
+            raise SourceError(f"prometheus error: {d.get('error', d.get('status'))}")
+        res = d.get("data", {}).get("result", [])
+        keys = [r.get("metric", {}).get(label) for r in res]
+        kh = fnv1a([k or "" for k in keys])
+        kh[[k is None for k in keys]] = 0
+        vals = [r.get("values") or ([r["value"]] if "value" in r else []) for r in res]
+        off = np.zeros(len(res) + 1, np.int64)
+        np.cumsum([len(v) for v in vals], out=off[1:])
+        flat = [p for v in vals for p in v]
+        return Keyed(kh, off, np.array([float(p[0]) for p in flat], np.float64),
+                     np.array([float(p[1]) for p in flat], np.float32))
+    lb = label.encode()
+    ns, npts = c_i64(), c_i64()
+    rc = lib.fm_prom_keyed_count(body, len(body), lb, len(lb), ctypes.byref(ns), ctypes.byref(npts))
+    if rc == 1:
+        try:
+            d = json.loads(body)
+            msg = d.get("error", d.get("status"))
+        except ValueError:
+            msg = "status != success"
+        raise SourceError(f"prometheus error: {msg}")
+    if rc != 0:
+        raise SourceError("malformed prometheus response")
+    kh = np.empty(ns.value, np.uint64)
+    off = np.empty(ns.value + 1, np.int64)
+    t = np.empty(npts.value, np.float64)
+    v = np.empty(npts.value, np.float32)
+    lib.fm_prom_keyed_fill(body, len(body), lb, len(lb), t.ctypes.data, v.ctypes.data, off.ctypes.data,
+                           kh.ctypes.data)
+    return Keyed(kh, off, t, v)
+
+
+def format_matrix(labels_json: list[str], t0: float, step: float, values: np.ndarray) -> bytes:
+    """A query_range matrix response body: series i has the pre-rendered
+    ``labels_json[i]`` and the samples ``values[i, k]`` at ``t0 + k * step``
+    (NaN samples left out)."""
+    values = np.ascontiguousarray(values, np.float32)
+    n, npts = values.shape if values.ndim == 2 else (len(labels_json), 0)
+    lib = _load()
+    if lib is None:
+        parts = []
+        for i, lab in enumerate(labels_json):
+            pts = ",".join(f'[{t0 + step * k:g},"{float(x)!r}"]' for k, x in enumerate(values[i]) if x == x)
+            parts.append('{"metric":' + lab + ',"values":[' + pts + "]}")
+        return ('{"status":"success","data":{"resultType":"matrix","result":[' + ",".join(parts) + "]}}").encode()
+    lbuf, loff = _joined(labels_json)
+    cap = lib.fm_prom_format_bound(n, npts, len(lbuf))
+    out = np.empty(cap, np.uint8)
+    w = lib.fm_prom_format(n, lbuf, loff.ctypes.data, float(t0), float(step), npts, values.ctypes.data,
+                           out.ctypes.data, cap)
+    if w < 0:
+        raise RuntimeError("fm_prom_format: output bound exceeded")
+    return out[:w].tobytes()
 
 
 def pack_left(rows: list[np.ndarray], ncols: int, ld: int, threads: int = 4) -> np.ndarray:

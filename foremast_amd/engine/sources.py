@@ -17,6 +17,7 @@ foremast-service/cmd/manager/main.go:59-63) are substituted by the caller.
 from __future__ import annotations
 
 import json
+import math
 import os
 import sys
 import time
@@ -86,30 +87,6 @@ def merge_series(ss: list["Series"]) -> tuple[np.ndarray, np.ndarray]:
     return t, np.where(cnt > 0, acc / np.maximum(cnt, 1), np.nan).astype(np.float32)
 
 
-_SEL = None
-
-
-def parse_selector(q: str):
-    """``metric{l1="v1",l2="v2"}`` with only equality matchers ->
-    (metric, [(label, value)]), else None (not batchable)."""
-    import re
-    global _SEL
-    if _SEL is None:
-        _SEL = (re.compile(r'^\s*([A-Za-z_:][\w:]*)\s*\{(.*)\}\s*$'),
-                re.compile(r'\s*([A-Za-z_]\w*)\s*(=~|!=|!~|=)\s*"((?:[^"\\]|\\.)*)"\s*(?:,|$)'))
-    m = _SEL[0].match(q)
-    if not m:
-        return None
-    body, labels, pos = m.group(2), [], 0
-    while pos < len(body):
-        mm = _SEL[1].match(body, pos)
-        if not mm or mm.group(2) != "=":
-            return None
-        labels.append((mm.group(1), mm.group(3)))
-        pos = mm.end()
-    return m.group(1), labels
-
-
 def substitute_window(url: str, start: float, end: float) -> str:
     return url.replace(START_PLACEHOLDER, f"{int(start)}").replace(END_PLACEHOLDER, f"{int(end)}")
 
@@ -143,44 +120,92 @@ def parse_wavefront(body: bytes | str) -> list[Series]:
 
 
 class PrometheusSource:
-    """``query_range`` over HTTP.  :meth:`fetch_columns` answers the same
-    query for many services in a few requests: app-level selectors that
-    differ only in their ``app`` value are merged into one
-    ``app=~"a|b|..."`` query (``batch`` apps per request) and the result is
-    split by the series' ``app`` label -- 10k continuous jobs x 4 metrics
-    cost 4 x 10k / ``batch`` requests per cycle, not 40k."""
+    """``query_range`` over HTTP.
 
-    def __init__(self, client=None, timeout: float = 90.0, batch: int = 256):
+    * :meth:`fetch` -- one URL, one request (the general path);
+    * :meth:`fetch_keyed` -- batched requests built by the brain's ingest
+      layer (engine/ingest.py): one selector with the union of many jobs' key
+      values (``pod=~"a|b|..."``), answered as one matrix and split by the key
+      label natively; requests run concurrently on ``workers`` connections,
+      long queries go as a form POST (Prometheus accepts ``POST
+      /api/v1/query_range``), and each response is parsed on the thread that
+      received it (the native parser releases the GIL);
+    * :meth:`fetch_columns` -- app-level ``START_TIME``/``END_TIME`` templates
+      of continuous / HPA jobs, merged into ``app=~`` batches of ``batch``
+      apps and split by the ``app`` label: 10k jobs x 4 metrics cost
+      4 x 10k / ``batch`` requests per cycle, not 40k.
+
+    ``live``: a real Prometheus has no samples after *now*, so the ingest
+    layer never asks it for the future (incremental windows)."""
+
+    live = True
+
+    def __init__(self, client=None, timeout: float = 90.0, batch: int = 256, workers: int = 8,
+                 post_over: int = 4096):
         import httpx
-        self.http = client or httpx.Client(timeout=timeout)
+        self.http = client or httpx.Client(timeout=timeout, limits=httpx.Limits(max_connections=workers,
+                                                                                 max_keepalive_connections=workers))
         self.batch = batch
+        self.workers = workers
+        self.post_over = post_over
         self._tpl: dict[str, object] = {}
+        self._pool = None
+        self.requests = 0
+        self.bytes = 0
 
     def fetch(self, url: str) -> list[Series]:
         r = self.http.get(url)
+        self.requests += 1
         if r.status_code != 200:
             raise SourceError(f"GET {url} -> {r.status_code}")
+        self.bytes += len(r.content)
         return parse_prometheus(r.content)
+
+    def _request(self, base: str, params: dict) -> bytes:
+        q = params.get("query", "")
+        if len(q) > self.post_over:
+            r = self.http.post(base, data=params)
+        else:
+            r = self.http.get(base, params=params)
+        if r.status_code != 200:
+            raise SourceError(f"query_range {q[:120]!r}... -> {r.status_code}: {r.text[:200]}")
+        return r.content
+
+    def fetch_keyed(self, queries: list, pool=None) -> list:
+        """Answers (native_rt.Keyed, split by the query's key label) or the
+        exception per request, in order."""
+        from . import native_rt
+
+        def one(q):
+            try:
+                body = self._request(q.group[0], q.url_params)
+                self.bytes += len(body)
+                return native_rt.parse_keyed(body, q.group[3])
+            except (SourceError, OSError, ValueError) as e:
+                return e
+            except Exception as e:  # noqa: BLE001 - httpx transport errors are not OSError
+                return SourceError(f"{type(e).__name__}: {e}")
+        self.requests += len(queries)
+        if len(queries) <= 1:
+            return [one(q) for q in queries]
+        if pool is None:
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._pool = ThreadPoolExecutor(self.workers, thread_name_prefix="prom")
+            pool = self._pool
+        return list(pool.map(one, queries))
 
     def _parse_template(self, tpl: str):
         got = self._tpl.get(tpl)
         if got is None:
-            got = False
-            if "query_range?" in tpl:
-                base, qs = tpl.split("?", 1)
-                params = urllib.parse.parse_qsl(qs, keep_blank_values=True)
-                q = dict(params).get("query", "")
-                sel = parse_selector(q)
-                if sel is not None and sum(1 for k, _ in sel[1] if k == "app") == 1:
-                    metric, labels = sel
-                    app = next(v for k, v in labels if k == "app")
-                    rest = tuple((k, v) for k, v in labels if k != "app")
-                    step = dict(params).get("step", "60")
-                    got = (base, metric, rest, step, app)
-            self._tpl[tpl] = got
+            from .ingest import parse_range
+            spec = parse_range(tpl, keys=("app",), windowed=False)
+            got = self._tpl[tpl] = (spec.group, spec.values[0]) if spec is not None and len(spec.values) == 1 \
+                else False
         return got
 
     def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
+        from .ingest import KeyedQuery, keyed_split
         out: list = [None] * len(templates)
         groups: dict[tuple, list[int]] = {}
         for i, tpl in enumerate(templates):
@@ -191,25 +216,22 @@ class PrometheusSource:
                 except (SourceError, OSError, ValueError) as e:
                     out[i] = e
                 continue
-            groups.setdefault(info[:4], []).append(i)
-        for (base, metric, rest, step), idx in groups.items():
+            groups.setdefault(info[0], []).append(i)
+        reqs = []
+        for grp, idx in groups.items():
             for k in range(0, len(idx), self.batch):
                 chunk = idx[k:k + self.batch]
-                apps = sorted({self._tpl[templates[i]][4] for i in chunk})
-                esc = lambda v: v.replace("\\", "\\\\").replace('"', '\\"')
-                sel = ",".join([f'{a}="{esc(b)}"' for a, b in rest] +
-                               ['app=~"' + "|".join(_re_escape(a) for a in apps) + '"'])
-                url = base + "?" + urllib.parse.urlencode({"query": f"{metric}{{{sel}}}", "start": f"{int(start)}",
-                                                          "end": f"{int(end)}", "step": step})
-                try:
-                    by_app: dict[str, list[Series]] = {}
-                    for s_ in self.fetch(url):
-                        by_app.setdefault(s_.labels.get("app", ""), []).append(s_)
-                    for i in chunk:
-                        out[i] = by_app.get(self._tpl[templates[i]][4], [])
-                except (SourceError, OSError, ValueError) as e:
-                    for i in chunk:
-                        out[i] = e
+                apps = sorted({self._tpl[templates[i]][1] for i in chunk})
+                reqs.append((KeyedQuery(grp, apps, float(int(start)), float(int(end))), chunk))
+        got = self.fetch_keyed([q for q, _ in reqs])
+        for (q, chunk), g in zip(reqs, got):
+            if isinstance(g, BaseException):
+                for i in chunk:
+                    out[i] = g
+                continue
+            per = dict(zip(q.values, keyed_split(g, q.values)))
+            for i in chunk:
+                out[i] = [Series({}, t, v) for t, v in per.get(self._tpl[templates[i]][1], [])]
         return Columns.from_series(out)
 
 
@@ -248,17 +270,58 @@ class SyntheticSource:
         self.noise = noise
         self.seed = seed
 
+    def grid(self, start: float, end: float) -> np.ndarray:
+        """Raw sample times in [start, end]: the multiples of ``step`` (an
+        integer count, so an on-grid ``end`` is never lost to float rounding)."""
+        k0 = math.ceil(start / self.step - 1e-9)
+        k1 = math.floor(end / self.step + 1e-9)
+        return self.step * np.arange(k0, k1 + 1, dtype=np.float64)
+
+    def _params_of(self, keys: list[str]):
+        """(level, daily amplitude, weekly amplitude, phase) per signal key:
+        counter-based draws from the key's CRC (vectorised)."""
+        from ..ops.reference import hash3, u01
+        h = np.array([zlib.crc32(k.encode()) ^ self.seed for k in keys], np.uint32)
+        u = [u01(hash3(h, np.uint32(i), np.uint32(0x51ED27))).astype(np.float64) for i in range(4)]
+        return 1.0 + 99.0 * u[0], 0.1 + 0.3 * u[1], 0.01 + 0.04 * u[2], 2 * np.pi * u[3]
+
     def _params(self, key: str):
-        h = zlib.crc32(key.encode()) ^ self.seed
-        rng = np.random.default_rng(h)
-        return (1.0 + 99.0 * rng.random(), 0.1 + 0.3 * rng.random(), 0.01 + 0.04 * rng.random(),
-                2 * np.pi * rng.random())
+        return tuple(float(a[0]) for a in self._params_of([key]))
+
+    def many(self, keys: list[str], noise_keys: list[str], fault_keys: list[str], t: np.ndarray,
+             stream: int = 0) -> np.ndarray:
+        """[len(keys), len(t)] samples at the raw times ``t`` (multiples of
+        ``step``): one vectorised pass for many series (the fake Prometheus
+        server answers a 1,000-pod union this way).  Same numbers as
+        :meth:`series` per key."""
+        from ..ops.reference import hash3, u01
+        K, nt = len(keys), len(t)
+        if K == 0 or nt == 0:
+            return np.zeros((K, nt), np.float32)
+        level, ad, aw, ph = (a[:, None] for a in self._params_of(keys))
+        tt = np.asarray(t, np.float64)[None, :]
+        season = 1 + ad * np.sin(2 * np.pi * tt / 86400.0 + ph) + aw * np.sin(2 * np.pi * tt / 604800.0 + ph)
+        kh = np.array([zlib.crc32(k.encode()) ^ self.seed for k in noise_keys], np.uint32)[:, None]
+        ti = ((np.asarray(t) / self.step).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)[None, :]
+        h1 = hash3(np.broadcast_to(kh, (K, nt)), np.broadcast_to(ti, (K, nt)), np.uint32(stream))
+        h2 = hash3(h1, np.uint32(0x68E31DA4), np.uint32(stream))
+        noise = np.sqrt(-2.0 * np.log(u01(h1).astype(np.float64))) * np.cos(2 * np.pi * u01(h2))
+        v = level * season * (1 + self.noise * noise)
+        if self.faults:
+            mag = np.ones((K, 1))
+            for i, fk in enumerate(fault_keys):
+                for sub, m in self.faults.items():
+                    if sub in fk:
+                        mag[i, 0] *= m
+            if (mag != 1).any():
+                v = np.where(tt >= self.fault_after, v * mag, v)
+        return np.maximum(v, 0).astype(np.float32)
 
     def series(self, key: str, start: float, end: float, stream: int = 0, noise_key: str | None = None,
                fault_key: str | None = None) -> Series:
         """``key`` sets the signal (level, seasonality), ``noise_key`` the
         noise stream (one per pod), ``fault_key`` is matched against ``faults``."""
-        t = np.arange(np.ceil(start / self.step) * self.step, end + 1e-9, self.step)
+        t = self.grid(start, end)
         level, ad, aw, ph = self._params(key)
         fault_key = key if fault_key is None else fault_key
         key = key if noise_key is None else noise_key
@@ -280,7 +343,7 @@ class SyntheticSource:
     def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
         """Vectorised answer for many app-level queries over one window
         (the same samples :meth:`fetch` returns for each)."""
-        t = np.arange(np.ceil(start / self.step) * self.step, end + 1e-9, self.step)
+        t = self.grid(start, end)
         info = getattr(self, "_cinfo", None)
         if info is None:
             info = self._cinfo = {}
@@ -347,9 +410,35 @@ class SyntheticSource:
         if not pods:
             app = _app_of(q)
             return [self.series(metric + "|" + app, start, end, fault_key=q)]
-        # pods of one app share the app's signal (k8s pod names: <app>-<rs hash>-<pod hash>)
-        return [dict_set(self.series(metric + "|" + _app_of_pod(p), start, end, i, noise_key=metric + "|" + p,
-                                     fault_key=q + "|" + p), "pod", p) for i, p in enumerate(pods)]
+        # pods of one app share the app's signal (k8s pod names: <app>-<rs hash>-<pod hash>);
+        # a series depends on its own labels only, never on the query that asked
+        # for it (a batched pod=~ union reads the same samples as a per-job query)
+        ident = _pod_identity(q)
+        return [dict_set(self.series(metric + "|" + _app_of_pod(p), start, end, 0, noise_key=metric + "|" + p,
+                                     fault_key=ident(p)), "pod", p) for p in sorted(set(pods))]
+
+    def fetch_keyed(self, queries: list, pool=None) -> list:
+        """Batched answers (engine/ingest.py KeyedQuery) generated directly as
+        native_rt.Keyed -- the same samples :meth:`fetch` gives per job."""
+        from . import native_rt
+        from .ingest import identities
+        out = []
+        for q in queries:
+            vals = q.key_values()
+            metric = q.group[1].replace("namespace_pod_", "").replace("namespace_app_pod_", "")
+            key = q.group[3]
+            uniq = list(dict.fromkeys(vals))
+            t = self.grid(q.start, q.end)
+            if key == "pod":
+                sig = [metric + "|" + _app_of_pod(v) for v in uniq]
+                noise = [metric + "|" + v for v in uniq]
+            else:
+                sig = noise = [metric + "|" + v for v in uniq]
+            fk = identities(q.group, uniq)
+            vals2 = self.many(sig, noise, fk, t)
+            off = np.arange(len(uniq) + 1, dtype=np.int64) * len(t)
+            out.append(native_rt.Keyed(native_rt.fnv1a(uniq), off, np.tile(t, len(uniq)), vals2.reshape(-1)))
+        return out
 
 
 class TemplateList(list):
@@ -454,6 +543,12 @@ class StagedSource:
         np.cumsum(lens, out=off[1:])
         return Columns(off, t[keep], v[keep], [None] * len(rows))
 
+    def fetch_keyed(self, queries: list, pool=None) -> list:
+        inner = getattr(self.inner, "fetch_keyed", None)
+        if inner is None:
+            raise SourceError("inner source has no batched form")
+        return inner(queries, pool=pool)
+
     def _remember(self, templates, ent) -> None:
         if len(self._lists) >= 64:                       # bounded: job lists change with fleet churn
             self._lists.pop(next(iter(self._lists)))
@@ -506,21 +601,35 @@ class StaticSource:
         return self.fallback.fetch(url)
 
 
-def _re_escape(v: str) -> str:
-    """A literal inside a PromQL (RE2) regex alternative."""
-    import re
-    return re.sub(r"([\\.^$|?*+()\[\]{}])", r"\\\1", v)
-
-
 def dict_set(s: Series, k: str, v: str) -> Series:
     s.labels[k] = v
     return s
 
 
 def _pod_selector(q: str) -> list[str]:
+    from .promql import literal_alternatives, parse_selector
+    sel = parse_selector(q)
+    if sel is not None:
+        for k, op, v in sel[1]:
+            if k == "pod" and op in ("=", "=~"):
+                vals = [v] if op == "=" else (literal_alternatives(v) or [])
+                return [p for p in vals if p]
+        return []
     import re
     m = re.search(r'pod=~"([^"]*)"', q) or re.search(r'pod="([^"]*)"', q)
     return [p for p in m.group(1).split("|") if p] if m else []
+
+
+def _pod_identity(q: str):
+    """pod -> the selector of that one pod's series (the query with its pod
+    matcher pinned to the pod): a series' identity independent of the union
+    it was asked in."""
+    from .ingest import parse_range, series_identity
+    spec = parse_range("http://x/api/v1/query_range?" + urllib.parse.urlencode({"query": q, "start": "0",
+                                                                              "end": "0"}), keys=("pod",))
+    if spec is None:
+        return lambda p: q + "|" + p
+    return lambda p: series_identity(spec.group, p)
 
 
 def _app_of_pod(pod: str) -> str:
@@ -556,6 +665,21 @@ class SourceRouter:
     def immutable(self) -> bool:
         srcs = [self.sources.get(self.force)] if self.force else [v for v in self.sources.values() if v is not None]
         return bool(srcs) and all(getattr(s, "immutable", False) for s in srcs)
+
+    def live(self, store_type: str) -> bool:
+        """The source has no samples after *now* (a real metric store)."""
+        try:
+            return bool(getattr(self._source(store_type), "live", False))
+        except SourceError:
+            return False
+
+    def keyed_source(self, store_type: str):
+        """The source behind ``store_type`` if it answers batched keyed queries."""
+        try:
+            src = self._source(store_type)
+        except SourceError:
+            return None
+        return src if getattr(src, "fetch_keyed", None) is not None else None
 
     def fetch_columns(self, store_type: str, templates: list[str], start: float, end: float) -> Columns:
         """Many queries over one window (``START_TIME``/``END_TIME`` templates)

@@ -485,29 +485,48 @@ def test_checkpoint_prefers_newer_world_over_stale_own_file(tmp_path):
     assert {int(st.flips[0]) for st in b.hpa_state.values()} == {3}
 
 
+def _prom_mock(seen):
+    """A query_range handler that reads the selector the way Prometheus does
+    (PromQL string escapes decoded, ``=~`` an anchored RE2 regex) and answers
+    one series per matched ``app``."""
+    import httpx
+    import urllib.parse
+    from foremast_amd.engine import promql
+
+    def handler(req):
+        q = dict(urllib.parse.parse_qsl(req.url.query.decode()))
+        if req.method == "POST":
+            q.update(urllib.parse.parse_qsl(req.content.decode()))
+        seen.append(q["query"])
+        sel = promql.parse_selector(q["query"])
+        if sel is None:
+            return httpx.Response(400, json={"status": "error", "errorType": "bad_data", "error": "parse error"})
+        apps = []
+        for k, op, v in sel[1]:
+            if k == "app":
+                apps = [v] if op == "=" else promql.literal_alternatives(v)
+        if apps is None:
+            return httpx.Response(400, json={"status": "error", "errorType": "bad_data", "error": "regex"})
+        t0, t1 = int(q["start"]), int(q["end"])
+        res = [{"metric": {"app": a, "namespace": "ns"},
+                "values": [[t, str(float(len(a) + k))] for k, t in enumerate(range(t0, t1 + 1, 60))]}
+               for a in (apps or ["none"])]
+        return httpx.Response(200, json={"status": "success", "data": {"resultType": "matrix", "result": res}})
+    return handler
+
+
 def test_prometheus_fetch_columns_batches_apps_into_few_queries():
     """Continuous / HPA jobs of one group share their window: the fast path
     asks the source column-wise, and PrometheusSource merges app-level
     selectors into ``app=~"a|b|..."`` queries (batch apps per request), then
-    splits the matrix by the ``app`` label."""
+    splits the matrix by the ``app`` label.  App names with regex
+    metacharacters are escaped twice -- RE2 (``svc\\.1``) inside a PromQL
+    string (``"svc\\\\.1"``), ADVICE r3 -- and decode back to themselves."""
     import httpx
     import urllib.parse
     from foremast_amd.engine.sources import PrometheusSource, substitute_window
     seen = []
-
-    def handler(req):
-        q = dict(urllib.parse.parse_qsl(req.url.query.decode()))
-        seen.append(q["query"])
-        import re
-        m = re.search(r'app=~"([^"]*)"', q["query"])
-        m1 = re.search(r'app="([^"]*)"', q["query"])
-        apps = m.group(1).split("|") if m else [m1.group(1) if m1 else "none"]
-        apps = [a.replace("\\", "") for a in apps]
-        t0, t1 = int(q["start"]), int(q["end"])
-        res = [{"metric": {"app": a, "namespace": "ns"},
-                "values": [[t, str(float(len(a) + k))] for k, t in enumerate(range(t0, t1 + 1, 60))]} for a in apps]
-        return httpx.Response(200, json={"status": "success", "data": {"resultType": "matrix", "result": res}})
-    src = PrometheusSource(client=httpx.Client(transport=httpx.MockTransport(handler)), batch=256)
+    src = PrometheusSource(client=httpx.Client(transport=httpx.MockTransport(_prom_mock(seen))), batch=256)
     tpl = lambda a: ("http://prom/api/v1/query_range?" + urllib.parse.urlencode(
         {"query": f'namespace_app_pod_cpu{{namespace="ns",app="{a}"}}', "start": "START_TIME", "end": "END_TIME",
          "step": "60"}))
@@ -516,7 +535,8 @@ def test_prometheus_fetch_columns_batches_apps_into_few_queries():
                                                        "&end=END_TIME&step=60"], T0, T0 + 240)
     assert len(seen) == 3 + 1                      # 600 apps in 3 merged queries + the non-batchable one
     merged = [q for q in seen if "app=~" in q]
-    assert len(merged) == 3 and r"svc\.1" in merged[0]
+    assert len(merged) == 3 and r'"svc\\.0|' in merged[0] and r"svc\\.1|" in merged[0]
+    assert all(e is None for e in cols.err[:600])
     for i, a in enumerate(apps[:5] + apps[-5:]):
         k = apps.index(a)
         np.testing.assert_array_equal(cols.v[cols.off[k]:cols.off[k + 1]], len(a) + np.arange(5, dtype=np.float32))
