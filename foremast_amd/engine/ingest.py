@@ -376,6 +376,7 @@ class WindowTable:
         [lo, hi]."""
         if isinstance(got, BaseException):
             self.err[ws] = True
+            self.next_due = -math.inf                                     # retry next cycle
             return
         self.err[ws] = False
         kslots = _ranges(self.slot0[ws], self.nslot[ws])
@@ -411,6 +412,12 @@ class WindowTable:
                 self.V[slot[ok], c[ok]] = got.v[samp[ok]]
         self.settled[ws] = np.maximum(self.settled[ws], hi)
         self.dirty[ws] = True
+        # when the windows that stay incomplete gain their next point
+        inc = self.settled[ws] < self.end[ws] - 1e-6
+        if inc.any():
+            w = ws[inc]
+            due = np.where(self.live[w], self.settled[w] + self.step[w] + self.settle, -math.inf)
+            self.next_due = min(self.next_due, float(due.min()))
 
     def fetch(self, router, now: float, pool=None) -> int:
         """One incremental round: every due request, per metric store through

@@ -1,0 +1,234 @@
+"""Fleet-scale canary ingestion (engine/ingest.py, engine/promql.py, the keyed
+native parser and demo/promserver.py): batched pod=~ unions answer exactly
+what per-job queries answer, windows are fetched incrementally (a past window
+once, a future one a step at a time, no request when nothing is due), and the
+fast path over a live HTTP Prometheus judges like the general path."""
+import json
+import urllib.parse
+
+import httpx
+import numpy as np
+import pytest
+
+from foremast_amd.engine import native_rt, promql
+from foremast_amd.engine.ingest import KeyedQuery, WindowTable, keyed_split, parse_range, render_query
+from foremast_amd.engine.sources import PrometheusSource, SyntheticSource
+
+T0 = 1_760_000_000.0
+
+
+class SimClock:
+    def __init__(self, t):
+        self.t = t
+
+    def now(self):
+        return self.t
+
+    def __call__(self):
+        return self.t
+
+
+def _fake(clock, faults=None):
+    from foremast_amd.demo.promserver import FakePrometheus
+    fp = FakePrometheus(SyntheticSource(faults=faults or {}, fault_after=T0 - 3600), clock)
+    calls = []
+
+    def handler(req):
+        q = dict(urllib.parse.parse_qsl(req.url.query.decode(), keep_blank_values=True))
+        if req.method == "POST":
+            q.update(urllib.parse.parse_qsl(req.content.decode(), keep_blank_values=True))
+        calls.append(q)
+        code, body = fp.answer(q)
+        return httpx.Response(code, content=body, headers={"Content-Type": "application/json"})
+    return PrometheusSource(client=httpx.Client(transport=httpx.MockTransport(handler))), calls
+
+
+def _url(q, start, end, step=60, base="http://prom/api/v1/query_range"):
+    return base + "?" + urllib.parse.urlencode({"query": q, "start": str(start), "end": str(end), "step": str(step)})
+
+
+# ----------------------------------------------------------------------------- PromQL text
+@pytest.mark.parametrize("v", ["svc.1", "a|b", 'q"x', "back\\slash", "new\nline", "ünï☃", "plain-name-7"])
+def test_promql_regex_matcher_roundtrips_literals(v):
+    m = promql.regex_matcher("app", [v, "other"])
+    sel = promql.parse_selector("m{" + m + "}")
+    assert sel is not None
+    (k, op, body), = sel[1]
+    assert (k, op) == ("app", "=~")
+    assert promql.literal_alternatives(body) == [v, "other"]
+    assert promql.compile_matchers(sel[1])({"app": v}) and not promql.compile_matchers(sel[1])({"app": v + "x"})
+
+
+def test_promql_unknown_escape_is_an_error_like_prometheus():
+    # a single-escaped regex literal inside a PromQL string is what Prometheus rejects
+    assert promql.parse_selector(r'm{app=~"svc\.1"}') is None
+    assert promql.parse_selector(r'm{app=~"svc\\.1"}')[1] == [("app", "=~", r"svc\.1")]
+    with pytest.raises(promql.PromQLError):
+        promql.unquote(r"svc\.1")
+
+
+def test_parse_range_and_render_keep_label_order():
+    u = _url('namespace_pod_cpu{namespace="default",pod=~"b-1|a-2",cluster="c"}', 100, 700)
+    spec = parse_range(u)
+    assert spec.key == "pod" and spec.values == ("b-1", "a-2") and spec.step == 60.0
+    assert render_query(spec.group, ["x.y"]) == 'namespace_pod_cpu{namespace="default",pod="x.y",cluster="c"}'
+    assert render_query(spec.group, ["a", "b.c"]) == \
+        'namespace_pod_cpu{namespace="default",pod=~"a|b\\\\.c",cluster="c"}'
+    assert parse_range(_url("rate(m[5m])", 0, 60)) is None                         # not a plain selector
+    assert parse_range(_url('m{pod=~"a.*"}', 0, 60)) is None                         # not a literal union
+    assert parse_range(_url('m{pod="a",app="b"}', 0, 60), keys=("pod",)).key == "pod"
+
+
+# ----------------------------------------------------------------------------- native parser
+def test_keyed_parser_matches_python_and_decodes_escapes():
+    labels = [json.dumps({"__name__": "m", "pod": p}) for p in ["a\"b", "é☃𝄞", "plain", "x\\y"]]
+    vals = np.array([[1.5, np.nan, 2.25], [3, 4, 5], [np.nan] * 3, [0.1, 1e-7, 3.4e38]], np.float32)
+    body = native_rt.format_matrix(labels, 1000.0, 60.0, vals)
+    k = native_rt.parse_keyed(body, "pod")
+    assert list(k.key) == list(native_rt.fnv1a(["a\"b", "é☃𝄞", "plain", "x\\y"]))
+    np.testing.assert_array_equal(np.diff(k.off), [2, 3, 0, 3])
+    np.testing.assert_array_equal(k.v, vals[np.isfinite(vals)])           # float32 round trip is exact
+    np.testing.assert_array_equal(k.t[:2], [1000.0, 1120.0])
+    # the same document re-encoded by Python's json (\\u escapes) hashes the same
+    k2 = native_rt.parse_keyed(json.dumps(json.loads(body)).encode(), "pod")
+    np.testing.assert_array_equal(k.key, k2.key)
+    # a missing label hashes to 0
+    assert native_rt.parse_keyed(body, "app").key.tolist() == [0, 0, 0, 0]
+
+
+# ----------------------------------------------------------------------------- batched == per job
+def test_batched_pod_union_equals_per_job_queries():
+    clock = SimClock(T0 + 3600)
+    src, calls = _fake(clock, faults={"svc3-7687b9f4d7-p0001": 4.0})
+    jobs = {f"svc{j}": [f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(4)] for j in range(40)}
+    jobs["svc.odd"] = ["svc.odd-1", "svc.odd-2"]                      # regex metacharacters in pod names
+    q = lambda pods: 'namespace_pod_latency{namespace="default",pod=~"' + "|".join(
+        promql.re_literal(p).replace("\\", "\\\\") for p in pods) + '"}'
+    per_job = {a: src.fetch(_url(q(p), T0, T0 + 600)) for a, p in jobs.items()}
+    calls.clear()
+    wt = WindowTable(settle=0.0, batch=16)
+    wid = {a: wt.add(parse_range(_url(q(p), T0, T0 + 600)), live=True) for a, p in jobs.items()}
+    n = wt.fetch(src, clock.now())
+    assert n == len(calls) == 3                                       # 41 windows / 16 per request
+    v, t, ln = wt.pack(np.array(list(wid.values())))
+    for r, a in enumerate(wid):
+        want_v = np.concatenate([s.values for s in per_job[a]])
+        want_t = np.concatenate([s.times for s in per_job[a]])
+        assert ln[r] == len(want_v) == 11 * len(jobs[a])
+        np.testing.assert_array_equal(v[r, :ln[r]], want_v)
+        np.testing.assert_array_equal(t[r, :ln[r]], want_t)
+    assert np.isnan(v[:, 11 * 4:]).all()
+    # the injected fault reached exactly its pod's series
+    r3 = list(wid).index("svc3")
+    assert v[r3, 11:22].mean() > 3 * v[r3, :11].mean()
+
+
+def test_incremental_windows_fetch_each_step_once():
+    """A current window in the future: no request before its first point is
+    due, one new step per request round, complete after its end; a past
+    (baseline) window is fetched once."""
+    clock = SimClock(T0)
+    src, calls = _fake(clock)
+    pods = [f"app-abc-p{k}" for k in range(3)]
+    sel = 'namespace_pod_cpu{namespace="ns",pod=~"' + "|".join(pods) + '"}'
+    wt = WindowTable(settle=10.0)
+    cur = wt.add(parse_range(_url(sel, T0 + 60, T0 + 660)), live=True)
+    base = wt.add(parse_range(_url(sel.replace("-abc-", "-old-"), T0 - 600, T0)), live=True)
+    clock.t = T0 + 5                       # baseline end not settled yet (settle 10 s)
+    assert wt.fetch(src, clock.now()) == 1
+    assert not wt.complete([base])[0]
+    clock.t = T0 + 10
+    assert wt.fetch(src, clock.now()) == 1 and wt.complete([base])[0]
+    fetched = []
+    for k in range(0, 700, 5):             # 5-s brain cycles for 700 s
+        clock.t = T0 + 10 + k
+        calls.clear()
+        if wt.fetch(src, clock.now()):
+            fetched.append((k, calls[0]["start"], calls[0]["end"]))
+    # one request per new grid point (11 points: T0+60 .. T0+660), never a repeat
+    assert len(fetched) == 11
+    assert [int(float(f[1])) for f in fetched] == [int(T0 + 60 * (i + 1)) for i in range(11)]
+    assert wt.complete([cur])[0]
+    v, _, ln = wt.pack(np.array([cur, base]))
+    assert ln.tolist() == [33, 33]
+    assert wt.fetch(src, clock.now() + 3600) == 0                      # complete windows are never asked again
+
+
+def test_http_fast_path_judges_like_general_path_over_live_cycles():
+    """The brain on a live (clock-bounded) HTTP Prometheus: the fast path's
+    batched incremental windows and the general path's per-job fetches give
+    the same verdicts and gauges cycle after cycle, with far fewer requests."""
+    from foremast_amd.api import crd
+    from foremast_amd.config import BrainConfig
+    from foremast_amd.controller.analyst import AnalystClient
+    from foremast_amd.engine.brain import Brain
+    from foremast_amd.engine.exporter import BrainExporter
+    from foremast_amd.engine.sources import SourceRouter
+    from foremast_amd.service.app import create_app
+    from foremast_amd.service.store import MemoryStore
+    faults = {"c2-7687b9f4d7-p0000": 5.0, "c5-7687b9f4d7-p0001": 5.0}
+    rigs = []
+    for resident in (True, False):
+        clock = SimClock(T0)
+        src, calls = _fake(clock, faults)
+        store = MemoryStore()
+        client = AnalystClient.for_app(create_app(store), clock=clock)
+        cfg = BrainConfig()
+        cfg.metric_settle_s = 0.0
+        brain = Brain(store, cfg, sources=SourceRouter(prometheus=src), clock=clock, exporter=BrainExporter(),
+                      worker_id="w", resident_history=resident)
+        ms = [crd.Monitoring("http_server_requests_latency", "gauge", "latency"),
+              crd.Monitoring("http_server_requests_errors_5xx", "counter", "error5xx")]
+        mets = crd.Metrics("prometheus", "http://prom/api/v1/", ms)
+        ids = [client.start_analyzing("default", f"c{j}", [[f"c{j}-7687b9f4d7-p{k:04d}" for k in range(3)],
+                                                          [f"c{j}-5db89899b5-q{k:04d}" for k in range(3)]],
+                                      mets, 10, "canary") for j in range(8)]
+        rigs.append((clock, store, brain, calls, ids))
+    (ca, sa, ba, calls_a, ids), (cb, sb, bb, calls_b, _) = rigs
+    seen = set()
+    tot_a = tot_b = 0
+    for cyc in range(16):
+        for clock in (ca, cb):
+            clock.t = T0 + 50 * cyc
+        calls_a.clear()
+        calls_b.clear()
+        ba.run_once()
+        bb.run_once()
+        assert len(calls_a) <= max(1, len(calls_b))
+        tot_a += len(calls_a)
+        tot_b += len(calls_b)
+        for j in ids:
+            da, db = sa.get(j), sb.get(j)
+            assert da.status == db.status, (cyc, j, da.status, db.status, da.reason, db.reason)
+            assert da.reason == db.reason, (cyc, j, da.reason, db.reason)
+            seen.add(da.status)
+        ta, tb = ba.exporter.table, bb.exporter.table
+        # the general path exports a job's bands once its current window has a
+        # point; the fast path from the first cycle (history-based bands)
+        assert set(tb.index) <= set(ta.index)
+        for k in tb.index:
+            va, vb = ta.get(k), tb.get(k)
+            assert (np.isnan(va) and np.isnan(vb)) or va == pytest.approx(vb, rel=1e-6, abs=1e-9), (cyc, k)
+    from foremast_amd.api import status as ST
+    assert ST.COMPLETED_UNHEALTH in seen and ST.COMPLETED_HEALTH in seen
+    # batched + incremental: a small fraction of per-job fetching's requests
+    assert ba.fast.wt.requests > 0 and 8 * tot_a <= tot_b, (tot_a, tot_b)
+
+
+def test_keyed_split_assigns_duplicate_and_missing_keys():
+    got = native_rt.Keyed(native_rt.fnv1a(["a", "b", "a"]), np.array([0, 1, 3, 4]), np.arange(4.0),
+                          np.arange(4, dtype=np.float32))
+    out = keyed_split(got, ["a", "c", "b"])
+    assert [len(x) for x in out] == [2, 0, 1]
+    np.testing.assert_array_equal(out[2][0][1], [1, 2])
+
+
+def test_synthetic_keyed_answer_matches_fetch():
+    s = SyntheticSource(faults={"svc1-abc-p1": 3.0}, fault_after=T0 - 100)
+    u = _url('namespace_pod_cpu{namespace="default",pod=~"svc1-abc-p1|svc1-abc-p0"}', T0 - 20, T0 + 600)
+    per = s.fetch(u)
+    spec = parse_range(u)
+    k = s.fetch_keyed([KeyedQuery(spec.group, list(spec.values), spec.start, spec.end)])[0]
+    for ser, part in zip(per, keyed_split(k, [x.labels["pod"] for x in per])):
+        np.testing.assert_array_equal(ser.values, part[0][1])
+        np.testing.assert_array_equal(ser.times, part[0][0])
