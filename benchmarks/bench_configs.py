@@ -271,8 +271,35 @@ def config3e2e(args):
     clock = lambda: t["now"]
     mons = [crd.Monitoring(f"http_server_requests_{a}", "gauge", a) for a in (names * 2)[:M]]
     aliases = [m.metric_alias for m in mons]
-    metrics = crd.Metrics("prometheus", "http://prom/api/v1/", mons)
-    server = poller = None
+    http = args.source == "http"
+    spread = (60.0 if args.spread_seconds is None else args.spread_seconds) if http else 0.0
+    server = poller = prom = cw = None
+    if strategy == "canary":
+        faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, S, 50)}    # 2% of services regress
+        fault_after = t["now"] - 3600
+    else:
+        faults = {f'app="svc{j}"': 3.0 for j in range(0, S, 50)}
+        fault_after = t["now"] + spread + (args.warmup + 2) * poll
+    prom_url = "http://prom/api/v1/"
+    if http:
+        # the fake Prometheus (demo/promserver.py) in its own processes, on the
+        # bench's simulated clock (an 8-byte mmap'd file: nothing after now)
+        from foremast_amd.demo.promserver import ClockWriter
+        clock_file = os.path.join(tempfile.mkdtemp(prefix="fm_prom_"), "now") if info.is_main else None
+        clock_file = D.broadcast_object(clock_file)
+        if info.is_main:
+            cw = ClockWriter(clock_file, t["now"])
+            prom = subprocess.Popen([sys.executable, "-m", "foremast_amd.demo.promserver", "--port", "0",
+                                     "--clock-file", clock_file, "--faults", _json.dumps(faults),
+                                     "--fault-after", str(fault_after), "--workers", str(args.prom_workers)],
+                                    cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    stdout=subprocess.PIPE, text=True)
+            prom_port = int(prom.stdout.readline().split()[1])
+        else:
+            prom_port = None
+        prom_port = D.broadcast_object(prom_port)
+        prom_url = f"http://127.0.0.1:{prom_port}/api/v1/"
+    metrics = crd.Metrics("prometheus", prom_url, mons)
     t_sub = 0.0
     ids: list[str] = []
     # continuous / HPA jobs stay alive for the whole run (their end time is
@@ -281,11 +308,15 @@ def config3e2e(args):
     window = args.window if strategy == "canary" else max(args.window, int(n_cycles * poll / 60) + 20)
 
     def submit(client):
+        t0_sub = t["now"]
         for j in range(S):
+            if spread:
+                t["now"] = t0_sub + spread * j / S
             pods = ([[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
                      [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]] if strategy == "canary" else None)
             ids.append(client.start_analyzing("default", f"svc{j}", pods, metrics, window, strategy,
                                               aliases if strategy == "hpa" else None))
+        t["now"] = t0_sub + spread
 
     if args.store == "memory":
         store = MemoryStore()
@@ -314,15 +345,20 @@ def config3e2e(args):
     print(f"[{kind}] rank {info.rank}: {S} jobs submitted in {t_sub:.1f}s ({args.store})", file=sys.stderr,
           flush=True)
     if strategy == "canary":
-        faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, S, 50)}    # 2% of services regress
-        staged = StagedSource(SyntheticSource(faults=faults, fault_after=t["now"] - 3600))
+        staged = StagedSource(SyntheticSource(faults=faults, fault_after=fault_after))
     else:
         # 2% of services regress mid-run; every series is staged column-wise
         # over [history start, end of run] (the bench's stand-in for Prometheus)
-        faults = {f'app="svc{j}"': 3.0 for j in range(0, S, 50)}
-        t_hi = t["now"] + (n_cycles + 2) * poll
-        staged = StagedSource(SyntheticSource(faults=faults, fault_after=t["now"] + (args.warmup + 2) * poll),
+        t_hi = t["now"] + (n_cycles + 2) * poll + (150.0 if http else 0.0)
+        staged = StagedSource(SyntheticSource(faults=faults, fault_after=fault_after),
                               window=(t["now"] - args.history_days * 86400 - 3600, t_hi))
+    if http:
+        from foremast_amd.engine.sources import PrometheusSource, TieredSource
+        live = PrometheusSource(workers=16)
+        router = SourceRouter(prometheus=TieredSource(live, staged, span_s=86400.0))
+    else:
+        live = None
+        router = SourceRouter(synthetic=staged, force="synthetic")
     cfg = BrainConfig()
     cfg.ml_algorithm = algo
     cfg.hpa_log_interval_s = args.hpa_log_interval
@@ -341,9 +377,13 @@ def config3e2e(args):
         cfg.lstm_layers = args.layers
         cfg.lstm_window = args.lookback
     exp = BrainExporter()
-    brain = Brain(store, cfg, device=dev, sources=SourceRouter(synthetic=staged, force="synthetic"), clock=clock,
+    brain = Brain(store, cfg, device=dev, sources=router, clock=clock,
                   batch_size=S + 1, worker_id=f"bench-{info.rank}", exporter=exp, history_days=args.history_days)
-    t["now"] += poll
+    # HTTP canaries: the first cycle runs 90 s after the last submission, so
+    # the timed cycles sit inside the watch windows (points arriving)
+    t["now"] += poll + (90.0 if http and strategy == "canary" else 0.0)
+    if cw is not None:
+        cw.set(t["now"])
     t_first = time.perf_counter()
     first = brain.run_once()                    # fetch + stage history (+ fit models), untimed
     t_first = time.perf_counter() - t_first
@@ -361,12 +401,23 @@ def config3e2e(args):
         if poller.stdout.readline().strip() != "ready":       # timing starts under the REST load
             raise SystemExit("REST poller did not start")
 
+    req_log = []
+    cyc_ms: list[float] = []
+
     def step():
-        # cycles every poll interval inside the jobs' watch window (the
-        # synthetic source serves the whole window: pre-staged series)
+        # cycles every poll interval inside the jobs' watch window (staged:
+        # the synthetic source serves the whole window; http: the fake
+        # Prometheus answers up to the simulated now)
         t["now"] += poll
+        if cw is not None:
+            cw.set(t["now"])
+        n0 = (live.requests, live.bytes) if live is not None else (0, 0)
+        tc = time.perf_counter()
         r = brain.run_once()
+        cyc_ms.append(1e3 * (time.perf_counter() - tc))
         rows.append(r.get("rows", 0))
+        if live is not None:
+            req_log.append((live.requests - n0[0], live.bytes - n0[1]))
         for k, v in brain.spans.last.items():
             spans.setdefault(k, []).append(v * 1e3)
 
@@ -400,12 +451,16 @@ def config3e2e(args):
         if server is not None:
             server.terminate()
             server.wait(30)
+        if prom is not None:
+            prom.terminate()
+            prom.wait(30)
     timed = rows[args.warmup:]
     per_cycle = sum(timed) / max(1, len(timed))
     cpu = torch.device("cpu") if dev.type == "cpu" else dev
     windows = D.all_reduce_max(float(per_cycle), cpu)
     total_rows = sum(D.all_gather_object(per_cycle)) if D.is_dist() else per_cycle
     span_ms = {k: round(statistics.median(v[args.warmup:] or v), 3) for k, v in spans.items()}
+    span_max = {k: round(max(v[args.warmup:] or v), 3) for k, v in spans.items()}
     # per-rank claim / persist spans, max over ranks (the store is shared)
     worst = {k: round(D.all_reduce_max(span_ms.get(k, 0.0), cpu), 3) for k in ("claim", "persist")}
     desc = {"3e2e": ("the 10k-service canary fleet", "moving_average_all + pairwise ALL (resident tick)",
@@ -418,6 +473,10 @@ def config3e2e(args):
                      "forecast -> band decision + HPA score + forecast gauge",
                      "synthetic Prometheus-shaped series, staged column-wise; each cycle fetches every row's new "
                      "sample (60-s poll), random-init LSTM weights; 2% of services regress mid-run")}[kind]
+    if http:
+        desc = (desc[0], desc[1], "synthetic Prometheus-shaped series served over HTTP by a fake Prometheus in its own "
+                "processes (query_range evaluated up to the simulated now: batched pod=~ / app=~ unions, incremental "
+                "windows); 7-day histories from the in-memory archive (TieredSource); 2% of services regress")
     _common(args, info, ms, p50, "metric windows scored/sec (node), production brain cycle (Brain.run_once) "
             f"on {desc[0]}", total_rows / (ms / 1e3), "windows/s",
             f"Brain.run_once: claim + fetch + {desc[1]} + compaction + verdicts + exporter + store update", S * M,
@@ -431,11 +490,20 @@ def config3e2e(args):
              "topology": ("REST service in its own process + every rank on one WAL SQLite file"
                           if args.store == "sqlite" else "single process, in-memory store"),
              "rest_poller": poll_out, "rows_per_cycle_rank0": per_cycle,
+             "source": args.source, "submission_spread_s": spread,
+             "http": ({"requests_per_cycle_mean": round(statistics.mean(x for x, _ in req_log[args.warmup:]), 2),
+                       "requests_per_cycle_max": max(x for x, _ in req_log[args.warmup:]),
+                       "kbytes_per_cycle_mean": round(statistics.mean(b for _, b in req_log[args.warmup:]) / 1e3, 1),
+                       "requests_total_timed": sum(x for x, _ in req_log[args.warmup:]),
+                       "window_table_requests_total": brain.fast.wt.requests if brain.fast is not None else None,
+                       "prom_workers": args.prom_workers}
+                      if live is not None and req_log[args.warmup:] else None),
              "scraper": {"interval_s": args.scrape_interval, "scrapes": len(scrapes),
                          "render_ms_median": round(1e3 * statistics.median([x for x, _ in scrapes]), 2)
                          if scrapes else None, "bytes": scrapes[-1][1] if scrapes else None},
              "rows_per_cycle_max_rank": windows,
-             "span_ms_median_rank0": span_ms, "span_ms_median_max_rank": worst,
+             "span_ms_median_rank0": span_ms, "span_ms_median_max_rank": worst, "span_ms_max_rank0": span_max,
+             "cycle_ms_max_rank0": round(max(cyc_ms[args.warmup:] or cyc_ms or [0.0]), 3),
              "model_cache": {"hits": brain.model_cache.hits, "misses": brain.model_cache.misses},
              "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),
              "submit_s": round(t_sub, 3),
@@ -548,6 +616,12 @@ def main():
                     "threshold (sigma) of every metric rule, so the monitored fleet stays whole (0: defaults)")
     ap.add_argument("--hpa-log-interval", type=float, default=0.0, help="e2e configs: HPA_LOG_INTERVAL_SECONDS "
                     "(0: an hpalogs entry per job per cycle)")
+    ap.add_argument("--source", default="staged", choices=["staged", "http"],
+                    help="e2e configs: series pre-staged in memory (staged) or live windows over HTTP from a fake "
+                         "Prometheus in its own process (http; 7-day histories from the staged archive)")
+    ap.add_argument("--spread-seconds", type=float, default=None, help="e2e --source http: job submissions spread "
+                    "over this many seconds (canary windows at every phase of the 60-s grid; default 60)")
+    ap.add_argument("--prom-workers", type=int, default=4, help="e2e --source http: fake Prometheus processes")
     ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "
                     "body every N seconds in a thread while the cycles are timed (0: off)")
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "

@@ -37,8 +37,16 @@ def main() -> None:
     lock = threading.Lock()
     per = a.rps / max(1, a.threads)
 
+    go = threading.Event()
+    warm = threading.Barrier(a.threads + 1)
+
     def run(k: int) -> None:
+        # client + first request before "ready": building an httpx client (its
+        # SSL context) takes tens of ms, longer than a short timed region
         c = httpx.Client(base_url=a.url, timeout=10)
+        c.get(f"/v1/healthcheck/id/{ids[k % len(ids)]}")
+        warm.wait()
+        go.wait()
         i = k
         t_next = time.perf_counter()
         while not stop.is_set():
@@ -60,13 +68,13 @@ def main() -> None:
             elif sl < -1.0:
                 t_next = time.perf_counter()      # fell behind: do not burst
 
-    c0 = httpx.Client(base_url=a.url, timeout=30)
-    c0.get(f"/v1/healthcheck/id/{ids[0]}")
-    print("ready", flush=True)                        # the bench starts timing after this line
-    t0 = time.perf_counter()
     ts = [threading.Thread(target=run, args=(k,), daemon=True) for k in range(a.threads)]
     for t in ts:
         t.start()
+    warm.wait()                                       # every thread has its client and one answer
+    t0 = time.perf_counter()
+    go.set()
+    print("ready", flush=True)                        # the bench starts timing after this line
     stop.wait(a.seconds)
     stop.set()
     for t in ts:

@@ -81,6 +81,43 @@ class FakePrometheus:
         self.src = source
         self.clock = clock or Clock(None)
         self.requests = 0
+        self._plans: dict = {}           # query text -> parsed series plan (a brain repeats its unions)
+
+    def _plan(self, q: str, step: float):
+        got = self._plans.get(q)
+        if got is not None:
+            return got
+        sel = promql.parse_selector(q)
+        if sel is None:
+            return "unsupported query"
+        metric, ms = sel
+        keyp = [i for i, (k, op, _) in enumerate(ms) if k in KEY_LABELS and op in ("=", "=~")]
+        if len(keyp) != 1 or any(op != "=" for i, (_, op, _) in enumerate(ms) if i != keyp[0]):
+            return "fake prometheus: unsupported matchers"
+        key, op, v = ms[keyp[0]]
+        vals = [v] if op == "=" else promql.literal_alternatives(v)
+        if vals is None:
+            return "fake prometheus: non-literal regex"
+        vals = sorted({x for x in vals if x})
+        group = ("", metric, tuple((k, "", "") if i == keyp[0] else (k, o, x) for i, (k, o, x) in enumerate(ms)),
+                 key, step, ())
+        base = metric.replace("namespace_pod_", "").replace("namespace_app_pod_", "")
+        if key == "pod":
+            sig = [base + "|" + _app_of_pod(p) for p in vals]
+            noise = [base + "|" + p for p in vals]
+        else:
+            sig = noise = [base + "|" + a for a in vals]
+        eq = {k: x for i, (k, o, x) in enumerate(ms) if i != keyp[0]}
+        mark = "\x00"
+        lab = dict(eq)
+        lab[key] = mark
+        pre, post = json.dumps({"__name__": metric, **dict(sorted(lab.items()))},
+                               separators=(",", ":")).split(json.dumps(mark))
+        plan = (sig, noise, identities(group, vals), [pre + json.dumps(x) + post for x in vals], len(vals))
+        if len(self._plans) > 4096:
+            self._plans.clear()
+        self._plans[q] = plan
+        return plan
 
     def answer(self, params: dict) -> tuple[int, bytes]:
         self.requests += 1
@@ -90,40 +127,18 @@ class FakePrometheus:
             step = parse_step(params.get("step", "60"))
         except (KeyError, ValueError):
             return 400, b'{"status":"error","errorType":"bad_data","error":"missing or bad parameters"}'
-        sel = promql.parse_selector(q)
-        if sel is None or step is None or step <= 0:
-            return 400, b'{"status":"error","errorType":"bad_data","error":"unsupported query"}'
-        metric, ms = sel
-        keyp = [i for i, (k, op, _) in enumerate(ms) if k in KEY_LABELS and op in ("=", "=~")]
-        if len(keyp) != 1 or any(op != "=" for i, (_, op, _) in enumerate(ms) if i != keyp[0]):
-            return 400, b'{"status":"error","errorType":"bad_data","error":"fake prometheus: unsupported matchers"}'
-        key, op, v = ms[keyp[0]]
-        vals = [v] if op == "=" else promql.literal_alternatives(v)
-        if vals is None:
-            return 400, b'{"status":"error","errorType":"bad_data","error":"fake prometheus: non-literal regex"}'
-        vals = sorted({x for x in vals if x})
-        group = ("", metric, tuple((k, "", "") if i == keyp[0] else (k, o, x) for i, (k, o, x) in enumerate(ms)),
-                 key, step, ())
+        if step is None or step <= 0:
+            return 400, b'{"status":"error","errorType":"bad_data","error":"bad step"}'
+        plan = self._plan(q, step)
+        if isinstance(plan, str):
+            return 400, json.dumps({"status": "error", "errorType": "bad_data", "error": plan}).encode()
+        sig, noise, fk, labels, nv = plan
         hi = min(end, self.clock.now())
         n = int(math.floor((hi - start) / step + 1e-9)) + 1 if hi >= start else 0
         tg = start + step * np.arange(max(n, 0))
         raw = self.src.step
         tr = np.floor(tg / raw + 1e-9) * raw                     # newest raw sample at or before each point
-        base = metric.replace("namespace_pod_", "").replace("namespace_app_pod_", "")
-        if key == "pod":
-            sig = [base + "|" + _app_of_pod(p) for p in vals]
-            noise = [base + "|" + p for p in vals]
-        else:
-            sig = noise = [base + "|" + a for a in vals]
-        fk = identities(group, vals)
-        grid = self.src.many(sig, noise, fk, tr) if n > 0 else np.zeros((len(vals), 0), np.float32)
-        eq = {k: x for i, (k, o, x) in enumerate(ms) if i != keyp[0]}
-        mark = "\x00"
-        lab = dict(eq)
-        lab[key] = mark
-        pre, post = json.dumps({"__name__": metric, **dict(sorted(lab.items()))},
-                               separators=(",", ":")).split(json.dumps(mark))
-        labels = [pre + json.dumps(x) + post for x in vals]
+        grid = self.src.many(sig, noise, fk, tr) if n > 0 else np.zeros((nv, 0), np.float32)
         return 200, native_rt.format_matrix(labels, float(start), float(step), grid)
 
 
@@ -163,6 +178,17 @@ def make_handler(fp: FakePrometheus):
     return H
 
 
+def _die_with_parent() -> None:
+    """A pre-forked worker exits with the process that forked it (Linux
+    PR_SET_PDEATHSIG), so a killed server never leaves listeners behind."""
+    try:
+        import ctypes
+        import signal
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))   # PR_SET_PDEATHSIG
+    except (OSError, AttributeError):
+        pass
+
+
 def serve(port: int, source: SyntheticSource, clock_file: str | None, workers: int = 1,
           ready=sys.stdout) -> None:
     sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
@@ -171,12 +197,24 @@ def serve(port: int, source: SyntheticSource, clock_file: str | None, workers: i
     sock.listen(256)
     print(f"port {sock.getsockname()[1]}", file=ready, flush=True)
     kids = []
+    import signal
     for _ in range(max(0, workers - 1)):
         pid = os.fork()
         if pid == 0:
             kids = []
+            _die_with_parent()
             break
         kids.append(pid)
+    if kids:
+        def _stop(*_):
+            for k in kids:
+                try:
+                    os.kill(k, signal.SIGTERM)
+                except OSError:
+                    pass
+            os._exit(0)
+        signal.signal(signal.SIGTERM, _stop)
+        signal.signal(signal.SIGINT, _stop)
     fp = FakePrometheus(source, Clock(clock_file))
     from socketserver import ThreadingMixIn
 

@@ -578,6 +578,52 @@ class StagedSource:
         return got
 
 
+class TieredSource:
+    """Two metric stores behind one store type: short, recent ranges from the
+    live store (Prometheus: canary windows, the newest samples of sliding
+    jobs) and long ranges from an archive (a long-term store such as Thanos /
+    Cortex, or a pre-staged copy: the 7-day histories).  A range longer than
+    ``span_s`` goes to the archive.  The bench's HTTP configs use it with the
+    fake Prometheus as ``recent`` and the in-memory staged fleet as
+    ``archive``, so the timed cycles read every live sample over HTTP while
+    the untimed first cycle does not push 16 GB of history JSON through
+    loopback."""
+
+    def __init__(self, recent, archive, span_s: float = 86400.0):
+        self.recent = recent
+        self.archive = archive
+        self.span_s = span_s
+        self.live = bool(getattr(recent, "live", False))
+        self.local = False
+        self.immutable = False
+
+    def _pick(self, start: float, end: float):
+        return self.archive if end - start > self.span_s else self.recent
+
+    def fetch(self, url: str) -> list[Series]:
+        qs = dict(urllib.parse.parse_qsl(url.split("?", 1)[1])) if "?" in url else {}
+        try:
+            src = self._pick(float(qs.get("start", 0)), float(qs.get("end", 0)))
+        except ValueError:
+            src = self.recent
+        return src.fetch(url)
+
+    def fetch_keyed(self, queries: list, pool=None) -> list:
+        out: list = [None] * len(queries)
+        parts: dict[int, list[int]] = {}
+        for i, q in enumerate(queries):
+            parts.setdefault(id(self._pick(q.start, q.end)), []).append(i)
+        for src in (self.recent, self.archive):
+            idx = parts.get(id(src))
+            if idx:
+                for i, g in zip(idx, src.fetch_keyed([queries[i] for i in idx], pool=pool)):
+                    out[i] = g
+        return out
+
+    def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
+        return self._pick(start, end).fetch_columns(templates, start, end)
+
+
 class StaticSource:
     """Fixed answers by URL substring (tests, demos, and operator-provided
     series such as a static call graph)."""
