@@ -55,6 +55,7 @@ from .sources import SourceError, TemplateList, substitute_window
 log = logging.getLogger("foremast.brain.fast")
 
 MAX_M = 16
+_MERGED = __import__("os").environ.get("FOREMAST_SLIDING_MERGED", "1") not in ("0", "false")
 
 
 @dataclass
@@ -144,6 +145,7 @@ class GroupArrays:
     wbase: np.ndarray | None = None
     base: np.ndarray | None = None
     hist_epoch: int = -1                       # FastPath._hist_epoch the missing-data mask was built at
+    hist_end: float | None = None              # merged sliding group: end of the history window
 
 
 @dataclass
@@ -371,6 +373,9 @@ class FastPath:
         self.max_idle_cycles = 64
         self._cmp = {}            # device compaction buffers per capacity
         self._col: dict = {}      # column-wise fetched windows of sliding groups (consumed by _arrays)
+        self._ring = None         # merged sliding mode: host ring of the newest grid columns
+        self._ring_c = None
+        self._slide_state: dict = {}
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
         self._gstat: dict = {}    # group key -> (job ids, positions, per-job static columns)
@@ -713,7 +718,19 @@ class FastPath:
                                 tl.split = (stl, {s0: np.arange(S)})
             else:
                 lists = {k: TemplateList(a.tolist()) for k, a in arrs.items()}
-            memo = self._tpl[p0.group] = (ids, lists, rows, None, arrs)
+            # merged mode: per metric the current (and baseline) query is the
+            # history query on the same store -- one incremental fetch feeds
+            # the resident grid and every window is read back from it
+            merged = all((arrs[("cur_urls", m)] == arrs[("hist_urls", m)]).all()
+                         and (arrs[("cur_stores", m)] == arrs[("hist_stores", m)]).all()
+                         and ((arrs[("base_urls", m)] == "").all() or
+                              ((arrs[("base_urls", m)] == arrs[("hist_urls", m)]).all()
+                               and (arrs[("base_stores", m)] == arrs[("hist_stores", m)]).all()))
+                         for m in range(M))
+            has_base = merged and any((arrs[("base_urls", m)] != "").any() for m in range(M))
+            memo = self._tpl[p0.group] = (ids, lists, rows, (merged, has_base), arrs)
+        if memo[3][0] and _MERGED:
+            return self._fetch_sliding_merged(ws, now, memo)
         lists, rows = memo[1], memo[2]                                       # rows [S, M]
         cur_p, base_p = [], []
         for m in range(M):
@@ -759,6 +776,96 @@ class FastPath:
             fw.hist = []
         self._col[p0.group] = {"ids": ids, "cur": cur, "cur_t": cur_t,
                                "cur_len": cur_len, "base": base if bb else None, "base_len": base_len}
+
+    def _fetch_sliding_merged(self, ws: list[FastWork], now: float, memo) -> None:
+        """Merged sliding fetch: per metric, every row's samples newer than its
+        newest resident one, through now, on the step grid -- at a 60-s poll
+        ONE sample per row, written to the device grid and to a host ring of
+        the newest columns; the current / baseline windows are then read out
+        of the ring (no per-window query, no per-job packing) and the model
+        reads the grid only up to the history window's end."""
+        b = self.b
+        p0 = ws[0].plan
+        M, S = len(p0.aliases), len(ws)
+        st = self.sliding
+        step = b.step
+        wins = b._windows(ws[0].doc, now)
+        ids, lists, rows = memo[0], memo[1], memo[2]
+        hlo = wins["historical"][0]
+        hi = math.floor(now / step + 1e-9) * step
+        wr, wt, wv = [], [], []
+        for m in range(M):
+            tpls, stores = lists[("hist_urls", m)], lists[("hist_stores", m)]
+            since = st.last_t[rows[:, m]]
+            lo = np.where(np.isfinite(since), since + step, math.ceil(hlo / step - 1e-9) * step)
+            for lo_v in np.unique(lo):
+                if hi < lo_v:
+                    continue
+                sel = np.flatnonzero(lo == lo_v)
+                if len(sel) == len(tpls):
+                    lens, t, v = self._columns(stores, tpls, float(lo_v), hi)
+                else:
+                    lens, t, v = self._columns([stores[i] for i in sel], [tpls[i] for i in sel], float(lo_v), hi)
+                if len(t):
+                    wr.append(np.repeat(rows[sel, m], lens))
+                    wt.append(t)
+                    wv.append(v)
+        if wr:
+            r, t, v = np.concatenate(wr), np.concatenate(wt), np.concatenate(wv)
+            st.write_sliding_flat(r, t, v)
+            self._ring_write(r, t, v)
+        flat = rows.reshape(-1).astype(np.int64)
+        (clo, chi), (blo, bhi) = wins["current"], wins["baseline"]
+        cur, cur_t = self._ring_read(flat, clo, chi)
+        base = self._ring_read(flat, blo, bhi)[0] if memo[3][1] else None
+        cur_len = np.isfinite(cur).sum(1)
+        wclass = 0 if cur.shape[1] <= 128 else (1 if cur.shape[1] <= 256 else 2)
+        if self._slide_state.get(p0.group) != (id(ws), wclass):
+            for fw in ws:
+                fw.has_window = True
+                fw.dirty = True
+                fw.settled = False
+                fw.wclass = wclass
+                fw.hist = []
+            self._slide_state[p0.group] = (id(ws), wclass)
+        self._col[p0.group] = {"ids": ids, "cur": cur, "cur_t": cur_t, "cur_len": cur_len, "base": base,
+                               "base_len": None, "hist_end": wins["historical"][1]}
+
+    # host ring of the newest grid columns of every sliding row (merged mode)
+    RING = 64
+
+    def _ring_write(self, r: np.ndarray, t: np.ndarray, v: np.ndarray) -> None:
+        n = self.sliding.buf.shape[0]
+        if self._ring is None or self._ring.shape[0] < n:
+            ring = np.full((n, self.RING), np.nan, np.float32)
+            rc = np.full((n, self.RING), -1, np.int64)
+            if self._ring is not None:
+                ring[:self._ring.shape[0]] = self._ring
+                rc[:self._ring.shape[0]] = self._ring_c
+            self._ring, self._ring_c = ring, rc
+        ck = np.rint(t / self.b.step).astype(np.int64)
+        ok = np.isfinite(v)
+        r, ck, v = r[ok], ck[ok], v[ok]
+        j = ck % self.RING
+        self._ring[r, j] = v
+        self._ring_c[r, j] = ck
+
+    def _ring_read(self, rows: np.ndarray, lo: float, hi: float) -> tuple[np.ndarray, np.ndarray]:
+        """Values [R, n] / times [R, n] of the grid points in [lo, hi] (NaN:
+        no sample) from the host ring."""
+        step = self.b.step
+        c0, c1 = math.ceil(lo / step - 1e-9), math.floor(hi / step + 1e-9)
+        n = max(0, c1 - c0 + 1)
+        if n > self.RING:
+            raise ValueError(f"window of {n} steps exceeds the sliding ring ({self.RING})")
+        ck = np.arange(c0, c0 + n, dtype=np.int64)
+        if self._ring is None or n == 0 or not len(rows):
+            return np.full((len(rows), max(1, n)), np.nan, np.float32), np.full((len(rows), max(1, n)), np.nan)
+        j = ck % self.RING
+        v = self._ring[rows[:, None], j[None, :]]
+        v = np.where(self._ring_c[rows[:, None], j[None, :]] == ck[None, :], v, np.float32(np.nan))
+        t = np.broadcast_to(ck * step, v.shape).astype(np.float64)
+        return v, t
 
     def fetch(self, fw: FastWork, now: float) -> FastWork:
         b = self.b
@@ -935,6 +1042,8 @@ class FastPath:
         has_cur = np.isfinite(cur).any(1).reshape(S, M)
         ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
                          up(rowmap), end, ~(has_hist & has_cur), handles=handles, works=works)
+        if col is not None and pos is not None:
+            ga.hist_end = col.get("hist_end")
         if xslots is not None:
             ga.export_slots = xslots
             ga.export_start = self.b.exporter.contiguous_start(xslots)
@@ -1091,7 +1200,7 @@ class FastPath:
             store.used[ga.rowmap] = self.cycle
             ga.marked = self.cycle
         n = ga.cur.shape[1]
-        o = self._scorer(p0.aliases).score_resident(store.view(), ga.rm_d, ga.cur_d, ga.base_d)
+        o = self._scorer(p0.aliases).score_resident(store.view_until(ga.hist_end), ga.rm_d, ga.cur_d, ga.base_d)
         dec = o.decide
         if dev.type == "cuda":
             cap = max(1024, min(R * n, 1 << 16))
@@ -1163,7 +1272,7 @@ class FastPath:
         """Per-algorithm row subsets of a group with everything that does not
         change while the group's arrays are reused: row map, alignment of
         each row's right end, history gate, horizons, tables, cache keys."""
-        stamp = (store.e, store.ws, store.t0) if store.sliding else None
+        stamp = (store.e, store.ws, store.t0, ga.hist_end) if store.sliding else None
         md = ga.models
         if md is not None and md.stamp == stamp:
             return md
@@ -1174,8 +1283,9 @@ class FastPath:
         M, S = len(p0.aliases), len(works)
         dev = b.device
         rowmap = ga.rowmap.astype(np.int64)
-        T, shift, lim = self._alignment(rowmap, store)
-        t_last = store.last_t[rowmap]
+        T, shift, lim = self._alignment(rowmap, store, ga.hist_end)
+        t_last = self._hist_last(store.last_t[rowmap], store.step, ga.hist_end) if store.sliding \
+            else store.last_t[rowmap]
         cur_t = ga.cur_t
         ok = np.isfinite(cur_t) & np.isfinite(t_last)[:, None]
         with np.errstate(invalid="ignore"):
@@ -1352,19 +1462,23 @@ class FastPath:
             keys = [(f"{w.plan.namespace}/{w.doc.app_name}", a, bm, algo) for w in works
                     for a, bm in zip(w.plan.aliases, w.plan.base_metrics)]
             sub = ModelSub(algo, list(range(M)), None, rm, shift, lim, T, None, keys,
-                           store.last_t[ga.rowmap.astype(np.int64)], None, None, steps, M)
+                           self._hist_last(store.last_t[ga.rowmap.astype(np.int64)], store.step, ga.hist_end),
+                           None, None, steps, M)
             fc, _ = self._forecast(algo, LazyHist(store.buf, rm, shift, lim, T), sub, steps)
         return torch.nan_to_num(fc, nan=float("-inf")).amax(1).cpu().numpy()
 
     @staticmethod
-    def _alignment(rowmap: np.ndarray, store: ResidentHistory) -> tuple[int, np.ndarray, np.ndarray]:
+    def _alignment(rowmap: np.ndarray, store: ResidentHistory,
+                   hist_end: float | None = None) -> tuple[int, np.ndarray, np.ndarray]:
         """Right-align every row at its newest sample: (dense length T,
         shift, lim) with dense column c <- buffer column c - shift[r] for
         buffer columns < lim[r].  T = the longest row of the group (static:
         columns written; sliding: window start .. newest sample), as the
-        general path packs a batch right-aligned to its longest history."""
+        general path packs a batch right-aligned to its longest history.
+        ``hist_end``: a merged sliding group's grid also holds the current
+        window -- the model's history stops at the history window's end."""
         if store.sliding:
-            lt = store.last_t[rowmap]
+            lt = FastPath._hist_last(store.last_t[rowmap], store.step, hist_end)
             end = np.where(np.isfinite(lt), store.col(np.where(np.isfinite(lt), lt, store.t0)) + 1, store.ws)
             end = np.clip(end, store.ws, store.e)
             start = np.full(len(rowmap), store.ws)
@@ -1374,9 +1488,17 @@ class FastPath:
         T = max(1, int((end - start).max()) if len(end) else 1)
         return T, (T - end).astype(np.int64), end.astype(np.int64)
 
+    @staticmethod
+    def _hist_last(last_t: np.ndarray, step: float, hist_end: float | None) -> np.ndarray:
+        """Newest history sample of each row: the row's newest sample, capped
+        at the history window's last grid point (merged sliding groups)."""
+        if hist_end is None:
+            return last_t
+        return np.minimum(last_t, math.floor(hist_end / step + 1e-9) * step)
+
     def _align(self, ga: GroupArrays, store: ResidentHistory):
         dev = self.b.device
-        T, shift, lim = self._alignment(ga.rowmap.astype(np.int64), store)
+        T, shift, lim = self._alignment(ga.rowmap.astype(np.int64), store, ga.hist_end)
         i32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=dev)
         return T, i32(shift), i32(lim)
 

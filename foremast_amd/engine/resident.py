@@ -185,6 +185,16 @@ class ResidentHistory:
         vs = max(0, self.ws // 4 * 4)
         return HistView(self.buf[:, vs:], self.width, self.e - vs)
 
+    def view_until(self, t_end: float | None) -> HistView:
+        """Sliding view whose logical length stops at the grid point <= t_end
+        (a merged sliding group's grid also holds its current window)."""
+        v = self.view()
+        if not self.sliding or t_end is None or self.t0 is None:
+            return v
+        vs = max(0, self.ws // 4 * 4)
+        e = int(self.col(math.floor(t_end / self.step + 1e-9) * self.step)) + 1
+        return HistView(v.hist, v.ld, max(0, min(self.e, e) - vs))
+
     # ------------------------------------------------------------------ sliding grid
     def col(self, t) -> np.ndarray:
         return np.rint((np.asarray(t, np.float64) - self.t0) / self.step).astype(np.int64)
@@ -263,8 +273,12 @@ class ResidentHistory:
         if len(r):
             prev = np.where(np.isfinite(self.last_t[r]), self.col(np.where(np.isfinite(self.last_t[r]),
                                                                             self.last_t[r], self.t0)), -1)
-            np.add.at(self.nfin, r[c > prev], 1)          # new columns only (a re-sent sample counts once)
-            np.maximum.at(self.last_t, r, t)
+            if np.bincount(r).max() <= 1:                 # one sample per row (a 60-s poll): plain indexing
+                self.nfin[r] += c > prev
+                self.last_t[r] = np.maximum(self.last_t[r], t)
+            else:
+                np.add.at(self.nfin, r[c > prev], 1)      # new columns only (a re-sent sample counts once)
+                np.maximum.at(self.last_t, r, t)
             flat = torch.from_numpy(r * self.width + c)
             vals = torch.from_numpy(np.ascontiguousarray(v))
             if self.device.type == "cuda":
