@@ -176,10 +176,11 @@ class HPALogBatch:
     ``upper`` / ``lower`` float [n, len(aliases)], finite."""
 
     __slots__ = ("job_ids", "timestamp", "created_at", "score", "reason", "reasons", "aliases", "current", "upper",
-                 "lower")
+                 "lower", "handles")
 
     def __init__(self, job_ids: list[str], timestamp: float, created_at: str, score, reason, reasons: list[str],
-                 aliases: list[str], current, upper, lower) -> None:
+                 aliases: list[str], current, upper, lower, handles=None) -> None:
+        self.handles = handles           # store-side rows of the jobs (SQLite rids), if the caller has them
         self.job_ids = list(job_ids)
         self.timestamp = float(timestamp)
         self.created_at = created_at

@@ -707,6 +707,23 @@ class FastPath:
                         a[:] = [c[m] for c in col]
                 rows = np.stack([fw.rows for fw in ws]).astype(np.int64)
             if ix is not None:
+                # a subset of the previous list: same templates, so the same mode
+                flags = memo[3]
+            else:
+                # merged mode: per metric the current (and baseline) query is the
+                # history query on the same store -- one incremental fetch feeds
+                # the resident grid and every window is read back from it
+                merged = all((arrs[("cur_urls", m)] == arrs[("hist_urls", m)]).all()
+                             and (arrs[("cur_stores", m)] == arrs[("hist_stores", m)]).all()
+                             and ((arrs[("base_urls", m)] == "").all() or
+                                  ((arrs[("base_urls", m)] == arrs[("hist_urls", m)]).all()
+                                   and (arrs[("base_stores", m)] == arrs[("hist_stores", m)]).all()))
+                             for m in range(M))
+                has_base = merged and any((arrs[("base_urls", m)] != "").any() for m in range(M))
+                flags = (merged, has_base)
+                if merged and _MERGED:                    # only the history templates are ever read
+                    arrs = {k: a for k, a in arrs.items() if k[0] in ("hist_urls", "hist_stores")}
+            if ix is not None:
                 lists = {k: TemplateList.subset(memo[1][k], a.tolist(), ix) for k, a in arrs.items()}
                 for (f, m), tl in lists.items():          # one store, every job queried: so is the subset
                     if f.endswith("_urls"):
@@ -718,17 +735,7 @@ class FastPath:
                                 tl.split = (stl, {s0: np.arange(S)})
             else:
                 lists = {k: TemplateList(a.tolist()) for k, a in arrs.items()}
-            # merged mode: per metric the current (and baseline) query is the
-            # history query on the same store -- one incremental fetch feeds
-            # the resident grid and every window is read back from it
-            merged = all((arrs[("cur_urls", m)] == arrs[("hist_urls", m)]).all()
-                         and (arrs[("cur_stores", m)] == arrs[("hist_stores", m)]).all()
-                         and ((arrs[("base_urls", m)] == "").all() or
-                              ((arrs[("base_urls", m)] == arrs[("hist_urls", m)]).all()
-                               and (arrs[("base_stores", m)] == arrs[("hist_stores", m)]).all()))
-                         for m in range(M))
-            has_base = merged and any((arrs[("base_urls", m)] != "").any() for m in range(M))
-            memo = self._tpl[p0.group] = (ids, lists, rows, (merged, has_base), arrs)
+            memo = self._tpl[p0.group] = (ids, lists, rows, flags, arrs)
         if memo[3][0] and _MERGED:
             return self._fetch_sliding_merged(ws, now, memo)
         lists, rows = memo[1], memo[2]                                       # rows [S, M]
@@ -1696,9 +1703,10 @@ class FastPath:
             z = lambda a: np.where(np.isfinite(a[dj]), a[dj], 0.0).astype(np.float64)   # noqa: E731
             ids = ga.ids[dj].tolist() if ga is not None and len(ga.ids) == S else [works[j].doc.id for j in dj]
             codes = sorted(MI.REASONS)
+            hd = ga.handles[dj] if ga is not None and ga.handles is not None and len(ga.ids) == S else None
             hpalogs.append(HPALogBatch(ids, float(now), created, sc[dj].astype(np.int64),
                                        np.searchsorted(codes, rs[dj]).astype(np.int32),
-                                       [MI.REASONS[c] for c in codes], list(al), z(cl), z(up), z(lo)))
+                                       [MI.REASONS[c] for c in codes], list(al), z(cl), z(up), z(lo), handles=hd))
         # HPA jobs stay alive: one uniform "keep" for the whole group
         if ga is not None and len(ga.ids) == S:
             bulk.append((ga.ids, {"status": ST.PREPROCESS_COMPLETED}, ga.handles))

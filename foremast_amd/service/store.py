@@ -23,6 +23,7 @@ import collections
 import dataclasses
 import hashlib
 import json
+import math
 import sqlite3
 import threading
 import time
@@ -34,7 +35,7 @@ from datetime import datetime, timezone
 from ..api import status as ST
 from ..api.jobs import parse_rfc3339, rfc3339
 from ..api.jsonmodel import to_json
-from ..api.models import Document, HPALog, HPALogBatch
+from ..api.models import Document, HPALog, HPALogBatch, HPALogBody, HPALogDetail
 
 
 def _ts(doc: Document) -> float:
@@ -577,6 +578,11 @@ class SQLiteStore(JobStore):
             c.execute("create table if not exists meta (k text primary key, v integer not null)")
             c.execute("insert or ignore into meta values ('seq', 0)")
             c.execute("create table if not exists hpalogs (job_id text, ts real, body text)")
+            # the brain's per-cycle HPA logs, columnar: one row per batch (the
+            # entries of one cycle of one rank), rows sorted by job rid
+            c.execute("create table if not exists hpalog_batches (bid integer primary key, ts real not null, "
+                      "created text not null, aliases text not null, reasons text not null, n integer not null, "
+                      "rids blob not null, score blob not null, reason blob not null, vals blob not null)")
             c.execute("create index if not exists hpalogs_job on hpalogs(job_id, ts)")
             # no ts index: rows arrive in time order, so retention deletes a
             # rowid prefix (one B-tree less to update per log: 10k logs per cycle)
@@ -906,13 +912,40 @@ class SQLiteStore(JobStore):
         self.add_hpalogs([log])
 
     def add_hpalogs(self, logs: list) -> None:
-        rows = _log_rows(logs)
-        if not rows:
+        """HPALogBatch batches go in as ONE columnar row each (job rids,
+        scores, reason codes, a float32 [n, 3, M] block of current / upper /
+        lower): a 10k-job cycle is one insert of ~1 MB instead of 10k indexed
+        rows; the JSON of an entry is rendered only when it is read.  Single
+        HPALog entries (the general path) keep the row-per-entry table."""
+        batches = [lg for lg in logs if isinstance(lg, HPALogBatch) and len(lg)]
+        rows = _log_rows([lg for lg in logs if not isinstance(lg, HPALogBatch)])
+        if not rows and not batches:
             return
         with self._txn() as c:
-            c.executemany("insert into hpalogs values (?,?,?)", rows)
-            self._log_writes += len(rows)
-            newest = max(r[1] for r in rows)
+            newest = -math.inf
+            for b in batches:
+                rid = self._rids_of(c, b)
+                ok = rid >= 0
+                if not ok.all():                  # entries of unknown jobs: one row each
+                    rows.extend(_log_rows([b.log(i) for i in np.flatnonzero(~ok)]))
+                if not ok.any():
+                    continue
+                o = np.argsort(rid[ok], kind="stable")
+                sel = np.flatnonzero(ok)[o]
+                vals = np.stack([np.asarray(b.current, np.float32).reshape(len(b), -1)[sel],
+                                 np.asarray(b.upper, np.float32).reshape(len(b), -1)[sel],
+                                 np.asarray(b.lower, np.float32).reshape(len(b), -1)[sel]], 1)
+                c.execute("insert into hpalog_batches (ts, created, aliases, reasons, n, rids, score, reason, vals) "
+                          "values (?,?,?,?,?,?,?,?,?)",
+                          (b.timestamp, b.created_at or "", json.dumps(b.aliases), json.dumps(b.reasons), len(sel),
+                           rid[sel].astype(np.int64).tobytes(), np.asarray(b.score, np.int32)[sel].tobytes(),
+                           np.asarray(b.reason, np.int32)[sel].tobytes(), np.ascontiguousarray(vals).tobytes()))
+                self._log_writes += len(sel)
+                newest = max(newest, b.timestamp)
+            if rows:
+                c.executemany("insert into hpalogs values (?,?,?)", rows)
+                self._log_writes += len(rows)
+                newest = max(newest, max(r[1] for r in rows))
             # bounded retention (the HPA alert reads the last 4-6 entries,
             # GET /v1/healthcheck/id the last 10): drop entries older than
             # the retention window, at most once a minute
@@ -923,12 +956,64 @@ class SQLiteStore(JobStore):
                 first = c.execute("select rowid from hpalogs where ts >= ? order by rowid limit 1", (cut,)).fetchone()
                 if first is not None:
                     c.execute("delete from hpalogs where rowid < ?", (first[0],))
+                c.execute("delete from hpalog_batches where ts < ?", (cut,))
                 self._last_prune = newest
 
+    @staticmethod
+    def _rids_of(c, b: HPALogBatch) -> np.ndarray:
+        if b.handles is not None and len(b.handles) == len(b):
+            return np.asarray(b.handles, np.int64)
+        got = dict(c.execute("select id, rid from documents where id in (select value from json_each(?))",
+                             (json.dumps(list(b.job_ids)),)).fetchall())
+        return np.fromiter((got.get(j, -1) for j in b.job_ids), np.int64, len(b))
+
+    def _batch(self, c, bid: int):
+        """A decoded batch row (immutable once written: cached per process)."""
+        cache = self.__dict__.setdefault("_bcache", collections.OrderedDict())
+        got = cache.get(bid)
+        if got is not None:
+            cache.move_to_end(bid)
+            return got
+        r = c.execute("select ts, created, aliases, reasons, n, rids, score, reason, vals from hpalog_batches "
+                      "where bid=?", (bid,)).fetchone()
+        if r is None:
+            return None
+        ts, created, aliases, reasons, n, rids, score, reason, vals = r
+        al = json.loads(aliases)
+        got = (ts, created, al, json.loads(reasons), np.frombuffer(rids, np.int64), np.frombuffer(score, np.int32),
+               np.frombuffer(reason, np.int32), np.frombuffer(vals, np.float32).reshape(n, 3, len(al)))
+        cache[bid] = got
+        if len(cache) > 512:
+            cache.popitem(last=False)
+        return got
+
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
-        rows = self._conn().execute("select body from hpalogs where job_id=? order by ts desc limit ?",
-                                    (job_id, size)).fetchall()
-        return [HPALog.from_dict(json.loads(r[0])) for r in rows]
+        c = self._conn()
+        rows = c.execute("select ts, body from hpalogs where job_id=? order by ts desc limit ?",
+                         (job_id, size)).fetchall()
+        out = [(ts, HPALog.from_dict(json.loads(b))) for ts, b in rows]
+        r = c.execute("select rid from documents where id=?", (job_id,)).fetchone()
+        if r is not None and size > 0:
+            rid = r[0]
+            found = 0
+            # newest batches first; an entry per cycle means the last `size`
+            # batches answer it, a sparse log policy scans further back
+            for (bid,) in c.execute("select bid from hpalog_batches order by bid desc").fetchall():
+                b = self._batch(c, bid)
+                if b is None:
+                    continue
+                ts, created, al, reasons, rids, score, reason, vals = b
+                i = int(np.searchsorted(rids, rid))
+                if i < len(rids) and rids[i] == rid:
+                    det = [HPALogDetail(a, float(vals[i, 0, k]), float(vals[i, 1, k]), float(vals[i, 2, k]))
+                           for k, a in enumerate(al)]
+                    out.append((ts, HPALog(job_id=job_id, timestamp=ts, created_at=created or None,
+                                           log=HPALogBody(int(score[i]), reasons[int(reason[i])], det))))
+                    found += 1
+                    if found >= size:
+                        break
+        out.sort(key=lambda x: -x[0])
+        return [lg for _, lg in out[:size]]
 
 
 class ElasticsearchStore(JobStore):

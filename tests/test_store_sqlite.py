@@ -173,3 +173,36 @@ def test_steady_claim_cost_is_independent_of_fleet_size(tmp_path):
         ts.append(time.perf_counter() - t)
     assert len(b) == 5000
     assert float(np.median(ts)) < 0.005          # a handful of indexed statements, not 5000 rows
+
+
+def test_hpalog_batches_are_columnar_and_read_back_per_job(tmp_path):
+    """A cycle's HPALogBatch is ONE row (rids, scores, reasons, float32
+    current/upper/lower): reads render the job's newest entries from the
+    batches (rid lookup), with or without the claim handles, sparse logs
+    included; retention drops whole batches."""
+    from foremast_amd.api.models import HPALogBatch
+    st = SQLiteStore(str(tmp_path / "j.db"), hpalog_retention_s=3600.0)
+    docs = _docs(40)
+    st.put_many(docs)
+    rid = dict(st._conn().execute("select id, rid from documents").fetchall())
+    ids = [d.id for d in docs]
+    for k in range(30):
+        sel = ids if k % 3 else ids[::2]                   # every third cycle logs half of the jobs
+        n = len(sel)
+        cur = np.arange(n * 2, dtype=np.float64).reshape(n, 2) + k
+        b = HPALogBatch(sel[::-1], T0 + 60 * k, "c", np.full(n, k), np.zeros(n, np.int32), ["hold"], ["cpu", "mem"],
+                        cur[::-1], cur[::-1] + 0.5, cur[::-1] - 0.5,
+                        handles=np.array([rid[j] for j in sel[::-1]]) if k % 2 else None)
+        st.add_hpalogs([b])
+    n_rows = st._conn().execute("select count(*) from hpalog_batches").fetchone()[0]
+    assert n_rows == 30 and st._conn().execute("select count(*) from hpalogs").fetchone()[0] == 0
+    got = st.hpalogs(ids[1], 10)                           # an odd job: absent from every third batch
+    want = [k for k in range(29, -1, -1) if k % 3][:10]
+    assert [g.log.hpa_score for g in got] == want
+    assert [g.timestamp for g in got] == [T0 + 60 * k for k in want]
+    k = want[0]
+    assert got[0].log.details[0].current == float(2 * 1 + k) and got[0].log.details[1].upper == 2 * 1 + 1 + k + 0.5
+    assert got[0].job_id == ids[1] and got[0].log.reason == "hold"
+    st.add_hpalogs([HPALogBatch([ids[0]], T0 + 60 * 30 + 7200, "c", [1], [0], ["hold"], ["cpu", "mem"],
+                                [[1.0, 2.0]], [[1.0, 2.0]], [[1.0, 2.0]])])
+    assert st._conn().execute("select count(*) from hpalog_batches").fetchone()[0] == 1

@@ -28,9 +28,9 @@ for s in $steps; do
          e2e c3e2e --config 3e2e --steps 30 --warmup 3 &&
          e2e c2e2e --config 2e2e --steps 30 --warmup 3 &&
          e2e c4e2e --config 4e2e --steps 20 --warmup 3 || exit $rc ;;
-    e2ehttp) rm -f gpurun_out/check_e2ehttp.jsonl
-         e2e c3e2e_http --config 3e2e --source http --steps 20 --warmup 3 &&
-         e2e c2e2e_http --config 2e2e --source http --steps 20 --warmup 3 || exit $rc ;;
+    e2ehttp) e2e c3e2e_http --config 3e2e --source http --steps 70 --warmup 3 --prom-workers 8 &&
+         e2e c3e2e_http60 --config 3e2e --source http --poll-seconds 60 --window 60 --steps 12 --warmup 2 --prom-workers 8 &&
+         e2e c2e2e_http --config 2e2e --source http --steps 20 --warmup 3 --prom-workers 8 || exit $rc ;;
     configs) for c in 1 2 3 4 5; do run "c$c" 300 python benchmarks/bench_configs.py --config $c || exit $rc; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
