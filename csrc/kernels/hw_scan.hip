@@ -590,7 +590,6 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
   FM_LAUNCH_CHECK();
   return 0;
 }
-}  // namespace
 
 // Additive Holt-Winters grid fit + best-candidate forecast in one launch
 // (one workgroup per row).  Same outputs as fm_es_fit(kind = 2) --
@@ -601,11 +600,18 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
 // serial kernel): m > 64 * 24 or m < 192 (chunks of 4..24 steps per lane; seasons
 // up to 768 steps run two candidate pairs per wave, 32 lanes each),
 // G > 32, 2 m > T, or a row beyond the 160 KB of LDS a workgroup may take.
-FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H,
-                          float* sse, float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin,
-                          float* sscale, float* season_out, hipStream_t stream) {
-  if (R <= 0) return 0;
-  if (G < 1 || G > kMaxG || m < 2 || 2 * m > T || H < 0) return (int)hipErrorInvalidValue;
+// The plan of a scan fit for (T, G, m): chunk length C, lanes per pair and
+// the dynamic LDS bytes, or C = 0 when the shape is not covered.  One place
+// decides, for the launcher and for the Python-side shape query
+// (fm_hw_scan_supported), so the two can never disagree.
+struct ScanPlan {
+  int C = 0, lpp = 64;
+  size_t lds = 0;
+};
+
+ScanPlan scan_plan(int T, int G, int m) {
+  ScanPlan p;
+  if (G < 1 || G > kMaxG || m < 2 || 2 * m > T) return p;
   const int lpp = scan_lpp(m);
   const int need = (m + lpp - 1) / lpp;
   int C = 0;
@@ -617,12 +623,32 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   if (C == 0)
     for (int c : kChunks)                    // ... else the shortest that covers the lap
       if (usable(c) && c >= need) { C = c; break; }
-  if (C == 0 || m < 3 * 64) return (int)hipErrorInvalidValue;
+  if (C == 0 || m < 3 * 64) return p;
   const int GP = (G + 1) / 2;
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
   const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4 + 64 * 4;
-  if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return (int)hipErrorInvalidValue;
+  if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return p;
+  p.C = C;
+  p.lpp = lpp;
+  p.lds = lds;
+  return p;
+}
+}  // namespace
+
+// 1 when fm_hw_scan_fit covers (T, G, m) in this process (environment
+// overrides included, read once), else 0.
+FM_API int fm_hw_scan_supported(int T, int G, int m) { return scan_plan(T, G, m).C != 0; }
+
+FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H,
+                          float* sse, float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin,
+                          float* sscale, float* season_out, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if (H < 0) return (int)hipErrorInvalidValue;
+  const ScanPlan pl = scan_plan(T, G, m);
+  if (pl.C == 0) return (int)hipErrorInvalidValue;
+  const int C = pl.C, lpp = pl.lpp;
+  const size_t lds = pl.lds;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \

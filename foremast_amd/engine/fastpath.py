@@ -111,7 +111,14 @@ class FastWork:
     # window id per metric (-1: no query), None = fetched per job
     wcur: np.ndarray | None = None
     wbase: np.ndarray | None = None
+    serial: int = 0                            # unique per FastWork ever created (JobIds identity)
 
+    def __post_init__(self) -> None:
+        self.serial = next(_SERIAL)
+
+
+_SERIAL = __import__("itertools").count(1)
+_serial_of = __import__("operator").attrgetter("serial")
 
 USED_STAMP_EVERY = 16           # cycles between row last-use stamps (must stay < max_idle_cycles)
 
@@ -255,7 +262,8 @@ def pack_left(flat: np.ndarray, lens: np.ndarray, width: int, dtype=np.float32) 
 
 
 class JobIds:
-    """Identity of a job list (the ids of its FastWork objects, in order):
+    """Identity of a job list (the serials of its FastWork objects, in order --
+    never ``id()``, which CPython reuses once an object is freed):
     equality is an array compare, and ``index_in(old)`` finds the positions
     of this list's jobs in an earlier list (sorted search, no per-job dict)
     -- how a churned list (jobs left) re-indexes the previous list's memos."""
@@ -263,7 +271,7 @@ class JobIds:
     __slots__ = ("arr", "_order")
 
     def __init__(self, works) -> None:
-        self.arr = np.fromiter(map(id, works), np.int64, len(works))
+        self.arr = np.fromiter(map(_serial_of, works), np.int64, len(works))
         self._order = None
 
     def __len__(self) -> int:

@@ -44,6 +44,7 @@ _SIGS: dict[str, list] = {
     "fm_es_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                   c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fm_hw_scan_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int] + [c_void_p] * 10,
+    "fm_hw_scan_supported": [c_int, c_int, c_int],
     "fm_es_update": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fm_band_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p, c_i64, c_int, c_void_p, c_void_p,

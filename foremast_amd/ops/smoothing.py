@@ -71,16 +71,27 @@ _SCAN_HALF_MAX_M = 32 * 24          # seasons up to this length scan in 32-lane 
 # profiles/hw_scan_halfwave_default_r3.jsonl)
 
 
+# the launcher reads its A/B overrides once per process; so does the mirror below
+_ENV_LPP64 = os.environ.get("FOREMAST_HW_SCAN_LPP") == "64"
+_ENV_SETUP0 = os.environ.get("FOREMAST_HW_SCAN_SETUP") == "0"
+
+
 def hw_scan_supported(T: int, G: int, m: int) -> bool:
-    """Shapes the time-parallel additive Holt-Winters fit covers (mirrors
-    ``fm_hw_scan_fit``'s checks): 192 <= m <= 64 * 24, G <= 32, 2 m <= T and
-    the row (+ NaN padding for the last lap) within the 160 KB of LDS a gfx950
-    workgroup may take."""
+    """Shapes the time-parallel additive Holt-Winters fit covers: the native
+    ``fm_hw_scan_supported`` (the launcher's own plan function, so the two
+    sides cannot disagree), else a Python mirror of it: 192 <= m <= 64 * 24,
+    G <= 32, 2 m <= T and the row (+ NaN padding for the last lap) within the
+    160 KB of LDS a gfx950 workgroup may take."""
+    if LIB.available() and hasattr(LIB.load(), "fm_hw_scan_supported"):
+        return bool(LIB.load().fm_hw_scan_supported(int(T), int(G), int(m)))
+    return _hw_scan_supported_py(T, G, m)
+
+
+def _hw_scan_supported_py(T: int, G: int, m: int) -> bool:
     if not (1 <= G <= 32 and 192 <= m and 2 * m <= T and (T - m) // m < 128):
         return False
     # 32-lane half-wave pairs for m <= _SCAN_HALF_MAX_M (the launcher's scan_lpp)
-    half = m <= _SCAN_HALF_MAX_M and os.environ.get("FOREMAST_HW_SCAN_LPP") != "64" \
-        and os.environ.get("FOREMAST_HW_SCAN_SETUP") != "0"
+    half = m <= _SCAN_HALF_MAX_M and not _ENV_LPP64 and not _ENV_SETUP0
     lanes = 32 if half else 64
     need = -(-m // lanes)
     chunks = [c for c in _SCAN_CHUNKS if half or c not in (9, 18)]   # 9 / 18: half-wave chunks only

@@ -295,12 +295,23 @@ def test_gpu_resident_tick_masked_rows_match_cpu(cuda):
 
 
 def test_job_ids_index_in_finds_survivors_or_none():
+    import itertools
     from foremast_amd.engine.fastpath import JobIds
-    objs = [object() for _ in range(50)]
+    ctr = itertools.count(1)
+
+    class W:                                        # FastWork's identity: a never-reused serial
+        def __init__(self):
+            self.serial = next(ctr)
+    objs = [W() for _ in range(50)]
     old = JobIds(objs)
     keep = [objs[i] for i in (3, 1, 7, 49, 0)]
     ix = JobIds(keep).index_in(old)
     assert list(ix) == [3, 1, 7, 49, 0]
-    assert JobIds(objs[:10] + [object()]).index_in(old) is None      # a new job: no subset
+    assert JobIds(objs[:10] + [W()]).index_in(old) is None           # a new job: no subset
     assert JobIds([]).index_in(old) is None
     assert JobIds(objs) == old and JobIds(objs[::-1]) != old
+    # a new job object at a freed job's address is still a different job
+    dead = objs.pop()
+    sid = dead.serial
+    del dead
+    assert JobIds(objs[:3] + [W()]).index_in(JobIds(objs)) is None and sid not in JobIds(objs).arr

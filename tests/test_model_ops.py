@@ -730,3 +730,43 @@ def test_hw_scan_supported_mirrors_native_checks():
             for G in (1, 27, 32, 33):
                 rc = f(None, T, T, 1, None, G, m, 10, *([None] * 10))
                 assert (rc != 1) == SM.hw_scan_supported(T, G, m), (T, m, G, rc)
+
+
+def test_hw_scan_shape_query_native_matches_python_mirror():
+    """the Python shape check and the launcher must not drift --
+    the native query is the launcher's own plan; the mirror agrees with it."""
+    from foremast_amd.ops import smoothing as SM
+    from foremast_amd.ops._lib import LIB
+    if not LIB.available() or not hasattr(LIB.load(), "fm_hw_scan_supported"):
+        pytest.skip("native library not built")
+    for T in (500, 2880, 10080, 20160, 40000):
+        for G in (1, 14, 27, 32, 33):
+            for m in (100, 191, 192, 288, 576, 720, 768, 769, 1008, 1440, 1536, 1537, 5000):
+                assert SM.hw_scan_supported(T, G, m) == SM._hw_scan_supported_py(T, G, m), (T, G, m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,G", [(288, 25), (288, 1), (720, 25), (720, 3)])
+def test_gpu_hw_scan_fit_odd_pair_count_idle_half(cuda, m, G):
+    """an odd number of candidate pairs leaves the last half-wave
+    idle (pvalid false: shadowed pair, guarded SSE / state writes).  Every
+    row's SSE -- the NEXT row's candidate 0 included, which the prototype
+    overwrote -- matches the fp64 oracle and the serial kernel."""
+    T = 10080
+    grid = SM.default_grid(2)[:G]
+    assert SM.hw_scan_supported(T, G, m)
+    x = _seasonal(20, T, period=m, seed=7 + G)
+    x *= np.geomspace(1e-1, 1e3, 20)[:, None].astype(np.float32)
+    xt = torch.from_numpy(x).to(cuda)
+    sc = SM.es_fit(xt, T, 2, 5, m, grid=grid, method="scan", keep_state=True)
+    se = SM.es_fit(xt, T, 2, 5, m, grid=grid, method="serial", half_season=False, keep_state=True)
+    _, _, best0, sse0 = SM.ref_es_fit(x, 2, 5, m, grid)
+    s_c, s_e = sc.sse.cpu().numpy(), se.sse.cpu().numpy()
+    assert s_c.shape == (20, G)
+    np.testing.assert_allclose(s_c, sse0, rtol=2e-3)
+    np.testing.assert_allclose(s_c, s_e, rtol=2e-3)
+    np.testing.assert_allclose(s_c[1:, 0], sse0[1:, 0], rtol=2e-3)
+    bc = sc.best.cpu().numpy()
+    for r in np.flatnonzero(bc != best0):
+        a, b = sse0[r, bc[r]], sse0[r, best0[r]]
+        assert abs(a - b) <= 2e-3 * max(a, b), (r, a, b)
