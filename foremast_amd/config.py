@@ -102,6 +102,9 @@ class BrainConfig:
     # (one brain per cluster, or a federated Prometheus that drops the label)
     brain_cluster: str = ""                # BRAIN_CLUSTER
     export_sync_s: float = 1.0             # EXPORT_SYNC_SECONDS: ranks > 0 publish their gauges to rank 0
+    # a closed / expired / moved job's gauges stay this long (final verdict
+    # visible), then leave /metrics
+    export_series_ttl_s: float = 300.0     # EXPORT_SERIES_TTL_SECONDS
     # canary window ingestion (engine/ingest.py): a grid point of a live
     # metric store is read once, METRIC_SETTLE_SECONDS after its time (a
     # recording rule's value for t is final once its evaluation landed)
@@ -176,6 +179,7 @@ class BrainConfig:
         c.downstream_sync_s = _f(env, "DOWNSTREAM_SYNC_SECONDS", c.downstream_sync_s)
         c.brain_cluster = env.get("BRAIN_CLUSTER", c.brain_cluster)
         c.export_sync_s = _f(env, "EXPORT_SYNC_SECONDS", c.export_sync_s)
+        c.export_series_ttl_s = _f(env, "EXPORT_SERIES_TTL_SECONDS", c.export_series_ttl_s)
         c.metric_settle_s = _f(env, "METRIC_SETTLE_SECONDS", c.metric_settle_s)
         c.fetch_batch = _i(env, "FETCH_BATCH", c.fetch_batch)
         c.fetch_max_values = _i(env, "FETCH_MAX_VALUES", c.fetch_max_values)

@@ -127,6 +127,8 @@ class Brain:
         self.exporter = exporter
         if exporter is not None:
             exporter.sync_seconds = self.cfg.export_sync_s
+            exporter.series_ttl = self.cfg.export_series_ttl_s
+            exporter.clock = clock
         self.clock = clock
         self.step = step
         self.watch_s = watch_minutes * 60.0
@@ -440,6 +442,8 @@ class Brain:
         if self.fast is not None:
             with self.spans.span("housekeeping"):
                 self.fast.housekeeping()
+        if self.exporter is not None:
+            self.exporter.sweep(now)
         return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast),
                 "seconds": time.perf_counter() - t0}
 
@@ -572,6 +576,9 @@ class Brain:
                     offs += k
                     st = self._finish(wk, rows[sl], res, sl, now, updates, hpalogs)
                     outcome[st] = outcome.get(st, 0) + 1
+                    if st not in ST.IN_PROGRESS and st != ST.PREPROCESS_COMPLETED and self.exporter is not None:
+                        self.exporter.retire_jobs([([r.base_metric for r in rows[sl]], wk.namespace,
+                                                    wk.doc.app_name, "")], now)
             n += len(rows)
         return n
 

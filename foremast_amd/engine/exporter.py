@@ -67,24 +67,42 @@ def _grow(a: np.ndarray, n: int, fill) -> np.ndarray:
 class GaugeTable:
     """Columnar gauge storage: slot -> (series name, namespace, app, value),
     plus the pre-rendered sample-line prefix of every slot, kept per family
-    (a scrape walks each family's prefixes sequentially)."""
+    (a scrape walks each family's prefixes sequentially).
+
+    **Series lifecycle.**  A job's series are *retired* when the job closes,
+    expires or leaves the shard (:meth:`retire`): they keep their last value
+    for ``ttl`` seconds -- the dashboard still shows the final verdict -- and
+    are then dropped by :meth:`sweep`: gone from ``/metrics``, their slot
+    freed for reuse.  A write to a retiring slot revives it (another live job
+    exports the same series).  Dropped lines are skipped at render time and a
+    family's prefix buffer is compacted once half of it is dead, so the table
+    stays bounded by the live series under any amount of deployment churn.
+    Slot events (new key, dropped slot) are logged for rank 0's merged view
+    (:class:`BrainExporter` publication)."""
 
     def __init__(self) -> None:
         self.index: dict[tuple[str, str, str], int] = {}
-        self.keys: list[tuple[str, str, str]] = []
+        self.keys: list = []                     # slot -> key (None: free)
         self.vals = np.zeros(0, np.float64)
+        self.expire = np.zeros(0)                # slot -> inf live, t: drop at t, nan: free
         self.help: dict[str, str] = {}
         self.lock = threading.Lock()
         self.version = 0                         # bumped by every write (publication cadence)
+        self._free: list[int] = []
+        self._nret = 0                           # slots retiring (finite expire)
         self._fam_of: dict[str, int] = {}
         self._fam_names: list[str] = []
         self._fprefix: list[bytearray] = []      # per family: concatenated line prefixes
         self._fpoff: list[np.ndarray] = []       # per family: prefix offsets (count + 1)
-        self._fslots: list[np.ndarray] = []      # per family: slot of each line
+        self._fslots: list[np.ndarray] = []      # per family: slot of each line (-1: dropped line)
         self._fn: list[int] = []
+        self._fdead: list[int] = []              # per family: dropped lines not compacted yet
+        self._sline = np.zeros(0, np.int64)      # slot -> (family << 32 | line)
+        self.events: list = []                   # (slot, key | None) since the last drain (C2 publication)
+        self.dropped = 0
 
     def __len__(self) -> int:
-        return len(self.keys)
+        return len(self.index)
 
     def slots(self, keys: list[tuple[str, str, str]]) -> np.ndarray:
         out = np.empty(len(keys), np.int64)
@@ -93,13 +111,26 @@ class GaugeTable:
             for i, k in enumerate(keys):
                 s = idx.get(k)
                 if s is None:
-                    s = idx[k] = len(self.keys)
-                    self.keys.append(k)
+                    if self._free:
+                        s = self._free.pop()
+                        self.keys[s] = k
+                    else:
+                        s = len(self.keys)
+                        self.keys.append(k)
+                    idx[k] = s
+                    n = len(self.keys)
+                    if n > len(self.vals):
+                        self.vals = _grow(self.vals, n, np.nan)
+                        self.expire = _grow(self.expire, n, np.nan)
+                        self._sline = _grow(self._sline, n, -1)
+                    self.vals[s] = np.nan
+                    self.expire[s] = np.inf
                     self._add_line(k, s)
+                    self.events.append((s, k))
+                elif self._nret and self.expire[s] < np.inf:
+                    self.expire[s] = np.inf          # looked up again: live again
+                    self._nret -= 1
                 out[i] = s
-            n = len(self.keys)
-            if n > len(self.vals):
-                self.vals = _grow(self.vals, n, np.nan)
         return out
 
     def _add_line(self, key, slot: int) -> None:
@@ -113,23 +144,115 @@ class GaugeTable:
             self._fpoff.append(np.zeros(1, np.int64))
             self._fslots.append(np.zeros(0, np.int64))
             self._fn.append(0)
+            self._fdead.append(0)
         k = self._fn[f]
         buf = self._fprefix[f]
         buf += f'{name}{{namespace="{_esc(ns)}",app="{_esc(app)}"{extra}}} '.encode()
         self._fpoff[f] = po = _grow(self._fpoff[f], k + 2, 0)
         po[k + 1] = len(buf)
-        self._fslots[f] = sl = _grow(self._fslots[f], k + 1, 0)
+        self._fslots[f] = sl = _grow(self._fslots[f], k + 1, -1)
         sl[k] = slot
         self._fn[f] = k + 1
+        self._sline[slot] = (f << 32) | k
 
     def set(self, slots, values, track: bool = True) -> None:
         """``slots``: slot indices, or a ``slice`` of consecutive slots (a
-        strided store instead of an 80k-element scatter per cycle)."""
+        strided store instead of an 80k-element scatter per cycle).  Writing a
+        retiring slot revives it."""
         if not isinstance(slots, slice):
             slots = np.asarray(slots, np.int64)
         with self.lock:
             self.vals[slots] = values
             self.version += 1
+            if self._nret:
+                self._revive(slots)
+
+    def _revive(self, slots) -> None:
+        ex = self.expire[slots]
+        back = ex < np.inf                       # nan (free) compares false
+        if back.any():
+            idx = np.arange(len(self.expire))[slots][back] if isinstance(slots, slice) else slots[back]
+            self.expire[idx] = np.inf
+            self._nret = int(np.count_nonzero(self.expire < np.inf))
+
+    def retire(self, slots, now: float, ttl: float) -> int:
+        """Schedule live slots to be dropped at ``now + ttl`` (an earlier
+        schedule stands).  Returns how many newly retire."""
+        slots = np.unique(np.asarray(slots, np.int64).reshape(-1))
+        slots = slots[(slots >= 0) & (slots < len(self.expire))]
+        with self.lock:
+            ex = self.expire[slots]
+            new = ex == np.inf
+            self.expire[slots[new]] = now + ttl
+            self._nret += int(new.sum())
+            return int(new.sum())
+
+    def retire_keys(self, keys, now: float, ttl: float) -> int:
+        idx = self.index
+        sl = [s for s in (idx.get(k) for k in keys) if s is not None]
+        return self.retire(sl, now, ttl) if sl else 0
+
+    def sweep(self, now: float) -> int:
+        """Drop every retired slot whose time has come.  Returns the count."""
+        if not self._nret:
+            return 0
+        with self.lock:
+            n = len(self.keys)
+            dead = np.flatnonzero(self.expire[:n] <= now)
+            if not len(dead):
+                return 0
+            fams = set()
+            for s in dead.tolist():
+                k = self.keys[s]
+                del self.index[k]
+                self.keys[s] = None
+                fl = int(self._sline[s])
+                f, ln = fl >> 32, fl & 0xFFFFFFFF
+                self._fslots[f][ln] = -1
+                self._fdead[f] += 1
+                fams.add(f)
+                self._sline[s] = -1
+                self._free.append(s)
+                self.events.append((s, None))
+            self.vals[dead] = np.nan
+            self.expire[dead] = np.nan
+            self._nret -= len(dead)
+            self.dropped += len(dead)
+            self.version += 1
+            for f in fams:
+                if self._fdead[f] > max(256, self._fn[f] // 2):
+                    self._compact_family(f)
+            return len(dead)
+
+    def _compact_family(self, f: int) -> None:
+        """Rewrite a family's prefix buffer without its dropped lines."""
+        n = self._fn[f]
+        sl = self._fslots[f][:n]
+        live = np.flatnonzero(sl >= 0)
+        po = self._fpoff[f]
+        a, b = po[live], po[live + 1]
+        src = np.frombuffer(bytes(self._fprefix[f]), np.uint8)
+        lens = b - a
+        idx = (np.repeat(a - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
+               if len(live) else np.zeros(0, np.int64))
+        self._fprefix[f] = bytearray(src[idx].tobytes())
+        npo = np.zeros(len(live) + 1, np.int64)
+        np.cumsum(lens, out=npo[1:])
+        self._fpoff[f] = npo
+        self._fslots[f] = sl[live].copy()
+        self._fn[f] = len(live)
+        self._fdead[f] = 0
+        self._sline[self._fslots[f]] = (f << 32) | np.arange(len(live), dtype=np.int64)
+
+    def drain_events(self) -> list:
+        with self.lock:
+            ev, self.events = self.events, []
+        return ev
+
+    def live_items(self) -> list:
+        """(slot, key) of every live slot (a publication epoch's snapshot)."""
+        with self.lock:
+            return [(s, k) for s, k in enumerate(self.keys) if k is not None]
 
     def get(self, key) -> float | None:
         s = self.index.get(key)
@@ -137,24 +260,31 @@ class GaugeTable:
 
     # ---------------------------------------------------------------- exposition
     def render_parts(self, threads: int = 4) -> list:
-        """The text exposition of every slot as a list of byte buffers (one
-        header + one block of lines per family)."""
+        """The text exposition of every live slot as a list of byte buffers
+        (one header + one block of lines per family)."""
         with self.lock:                          # snapshot; formatting runs unlocked
-            fams = [(name, bytes(self._fprefix[f]), self._fpoff[f][:self._fn[f] + 1].copy(),
-                     self.vals[self._fslots[f][:self._fn[f]]]) for f, name in enumerate(self._fam_names)
-                    if self._fn[f]]
+            fams = []
+            for f, name in enumerate(self._fam_names):
+                n = self._fn[f]
+                if not n or self._fdead[f] >= n:
+                    continue
+                sl = self._fslots[f][:n]
+                order = np.flatnonzero(sl >= 0) if self._fdead[f] else None
+                fams.append((name, bytes(self._fprefix[f]), self._fpoff[f][:n + 1].copy(),
+                             self.vals[np.maximum(sl, 0)], order))
         lib = native_rt._load()
         parts = []
-        for name, prefix, poff, vals in fams:
+        for name, prefix, poff, vals, order in fams:
             parts.append(f"# HELP {name} {self.help.get(name, name)}\n# TYPE {name} gauge\n".encode())
-            n = len(vals)
+            lines = range(len(vals)) if order is None else order.tolist()
+            n = len(vals) if order is None else len(order)
             if lib is None:                       # pure-Python fallback (library not built)
-                parts.append(b"".join(prefix[poff[i]:poff[i + 1]] + _fmt(vals[i]) + b"\n" for i in range(n)))
+                parts.append(b"".join(prefix[poff[i]:poff[i + 1]] + _fmt(vals[i]) + b"\n" for i in lines))
                 continue
-            cap = int(poff[-1]) + 33 * n
+            cap = int(poff[-1]) + 33 * len(vals)
             out = np.empty(cap, np.uint8)
-            used = lib.fm_render_lines(prefix, poff.ctypes.data, None, n, vals.ctypes.data,
-                                       ctypes.c_char_p(out.ctypes.data), cap, threads)
+            used = lib.fm_render_lines(prefix, poff.ctypes.data, None if order is None else order.ctypes.data, n,
+                                       vals.ctypes.data, ctypes.c_char_p(out.ctypes.data), cap, threads)
             parts.append(memoryview(out)[:used])
         return parts
 
@@ -199,9 +329,15 @@ class BrainExporter:
         self._pub_t = -float("inf")
         self._pull_t = -float("inf")
         self._pull_lock = threading.Lock()
-        self._remote: dict[int, np.ndarray] = {}     # rank 0: remote slot -> local slot, per rank
+        self._remote: dict[int, np.ndarray] = {}     # rank 0: remote slot -> local slot (-1 none), per rank
         self._klog: dict[int, int] = {}              # rank 0: key-log entries consumed, per rank
+        self._kep: dict[int, int] = {}               # rank 0: key-log epoch being read, per rank
         self._seen: dict[int, float] = {}            # rank 0: publish time of the merged values, per rank
+        self.series_ttl = 300.0                      # EXPORT_SERIES_TTL_SECONDS
+        self.clock = time.time                       # the brain's clock (retirement times use it)
+        self._epoch = 0                              # ranks > 0: key-log epoch
+        self._logged = 0                             # ranks > 0: events logged in this epoch
+        self._acked = 0                              # ranks > 0: epochs below this one are trimmed
 
     IMPACT = "foremastbrain:namespace_app_pod_downstream_impact"
 
@@ -288,6 +424,30 @@ class BrainExporter:
     def set_hpa_scores(self, slots: np.ndarray, scores: np.ndarray) -> None:
         self.table.set(slots.reshape(-1), np.repeat(np.asarray(scores, np.float64), 2))
 
+    # ---------------------------------------------------------------- lifecycle
+    def job_keys(self, base_metrics, namespace: str, app: str, cluster: str = "") -> list:
+        """Every series key a job may export: bands per metric, HPA score,
+        forecast, downstream impact."""
+        keys = []
+        for bm in base_metrics:
+            u, l, a = self.bound_names(bm)
+            keys += [(u, namespace, app), (l, namespace, app), (a, namespace, app),
+                     ("foremastbrain:" + sanitize(bm) + "_forecast_max", namespace, app)]
+        keys += [(self.HPA_SCORE, namespace, app), (self.HPA_SCORE_ALT, namespace, app),
+                 (self.IMPACT, namespace, app, cluster) if cluster else (self.IMPACT, namespace, app)]
+        return keys
+
+    def retire_jobs(self, jobs, now: float, ttl: float | None = None) -> int:
+        """Jobs that closed / expired / left this rank's shard: their series
+        stay ``ttl`` seconds (the final verdict stays visible), then leave
+        ``/metrics``.  ``jobs``: (base metrics, namespace, app, cluster)."""
+        ttl = self.series_ttl if ttl is None else ttl
+        keys = [k for bms, ns, app, cl in jobs for k in self.job_keys(bms, ns, app, cl)]
+        return self.table.retire_keys(keys, now, ttl) if keys else 0
+
+    def sweep(self, now: float) -> int:
+        return self.table.sweep(now)
+
     # ---------------------------------------------------------------- reads
     def render_parts(self) -> list:
         """The whole ``/metrics`` body as buffers (merging the other ranks'
@@ -359,6 +519,11 @@ class BrainExporter:
         return self.pull(force)
 
     def publish(self, force: bool = False) -> bool:
+        """Ranks > 0: slot events (new key, dropped slot) go to an ordered key
+        log, the values as one vector.  The log is per *epoch*: once it holds
+        far more events than live slots, a new epoch starts with a snapshot of
+        the live keys, and the epochs rank 0 has acknowledged are deleted from
+        the store -- the log stays bounded under churn."""
         mb = self._mailbox()
         if mb is None or mb.rank == 0:
             return False
@@ -366,15 +531,33 @@ class BrainExporter:
         t = self.table
         if not force and (t.version == self._pub_version or now - self._pub_t < self.sync_seconds):
             return False
+        ev = t.drain_events()
+        if ev and self._logged + len(ev) > 2 * len(t) + 4096:
+            # new epoch: the live keys as its first entry (events of the old epoch are moot)
+            self._epoch += 1
+            self._logged = 0
+            ev = [(sl, list(k)) for sl, k in t.live_items()]
+            mb.append(f"gk{self._epoch}", json.dumps(ev).encode())
+            mb.put("gke", struct.pack("<q", self._epoch))
+            self._logged = len(ev)
+        elif ev:
+            mb.append(f"gk{self._epoch}", json.dumps([(sl, None if k is None else list(k)) for sl, k in ev]).encode())
+            self._logged += len(ev)
+            if self._epoch == 0 and self._logged == len(ev):
+                mb.put("gke", struct.pack("<q", 0))
         with t.lock:
             n = len(t.keys)
-            new = t.keys[self._pub_keys:n]
             vals = t.vals[:n].copy()
             ver = t.version
-        if new:
-            mb.append("gk", json.dumps(new).encode())
         mb.put("gv", struct.pack("<q", n) + vals.tobytes())
-        self._pub_keys, self._pub_version, self._pub_t = n, ver, now
+        self._pub_version, self._pub_t = ver, now
+        # trim the epochs rank 0 is done with
+        ack = mb.get(f"gka{mb.rank}", 0)
+        if ack is not None:
+            a = struct.unpack_from("<q", ack[1])[0]
+            while self._acked < a:
+                mb.trim(f"gk{self._acked}")
+                self._acked += 1
         return True
 
     def pull(self, force: bool = False) -> int:
@@ -388,11 +571,28 @@ class BrainExporter:
         with self._pull_lock:
             self._pull_t = now
             for r in range(1, mb.world):
-                for chunk in mb.read_log("gk", r, self._klog.get(r, 0)):
-                    keys = [tuple(k) for k in json.loads(chunk)]
-                    loc = self.table.slots(keys)
-                    self._remote[r] = np.concatenate([self._remote.get(r, np.zeros(0, np.int64)), loc])
+                got_e = mb.get("gke", r)
+                if got_e is not None:
+                    ep = struct.unpack_from("<q", got_e[1])[0]
+                    if ep != self._kep.get(r, 0):
+                        # a new epoch: its first entry is the full live key set; the
+                        # series of the old mapping not in it are dropped below
+                        old = self._remote.pop(r, np.zeros(0, np.int64))
+                        self._kep[r], self._klog[r] = ep, 0
+                        self._stale = getattr(self, "_stale", {})
+                        self._stale[r] = old[old >= 0]
+                for chunk in mb.read_log(f"gk{self._kep.get(r, 0)}", r, self._klog.get(r, 0)):
+                    self._apply_events(r, json.loads(chunk))
                     self._klog[r] = self._klog.get(r, 0) + 1
+                stale = getattr(self, "_stale", {}).pop(r, None)
+                if stale is not None and self._klog.get(r, 0) > 0:
+                    keep = set(self._remote.get(r, np.zeros(0, np.int64)).tolist())
+                    gone = [s_ for s_ in stale.tolist() if s_ not in keep]
+                    if gone:
+                        self.table.retire(gone, self.clock(), 0.0)
+                    mb.put(f"gka{r}", struct.pack("<q", self._kep.get(r, 0)))
+                elif stale is not None:
+                    self._stale[r] = stale
                 got = mb.get("gv", r)
                 if got is None:
                     continue
@@ -404,8 +604,33 @@ class BrainExporter:
                 vals = np.frombuffer(raw, np.float64, count=n, offset=8)
                 m = self._remote.get(r, np.zeros(0, np.int64))
                 k = min(len(m), n)               # keys logged after this snapshot are picked up next time
+                ok = m[:k] >= 0
                 with self.table.lock:
-                    self.table.vals[m[:k]] = vals[:k]
+                    self.table.vals[m[:k][ok]] = vals[:k][ok]
                 self._seen[r] = ts
-                merged += k
+                merged += int(ok.sum())
+        self.table.sweep(self.clock())
         return merged
+
+    def _apply_events(self, r: int, events: list) -> None:
+        """Rank 0: a remote rank's slot events, in order, -> its remote ->
+        local slot map.  Per touched remote slot only the last event counts
+        (a slot dropped and reused inside one publication is just re-keyed):
+        the previous local slot retires at once, the final key (if any) maps
+        to a local slot -- the same one when the key is unchanged, revived."""
+        m = self._remote.get(r, np.zeros(0, np.int64))
+        final: dict[int, object] = {}
+        for sl, k in events:
+            final[int(sl)] = k
+        top = max(final, default=-1) + 1
+        if top > len(m):
+            m = np.concatenate([m, np.full(top - len(m), -1, np.int64)])
+        touched = np.fromiter(final.keys(), np.int64, len(final))
+        prev = m[touched]
+        if (prev >= 0).any():
+            self.table.retire(prev[prev >= 0], self.clock(), 0.0)
+        m[touched] = -1
+        new = [(sl, tuple(k)) for sl, k in final.items() if k is not None]
+        if new:
+            m[[sl for sl, _ in new]] = self.table.slots([k for _, k in new])
+        self._remote[r] = m

@@ -1731,6 +1731,10 @@ class FastPath:
         wins = [a for w in works if w.wcur is not None for a in (w.wcur, w.wbase)]
         if wins:
             self.wt.release(np.concatenate(wins))
+        exp = self.b.exporter
+        if exp is not None and works:
+            exp.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name, w.plan.cluster)
+                             for w in works], self.b.clock())
         for w in works:
             if self.works.get(w.doc.id) is w:
                 del self.works[w.doc.id]
@@ -1749,11 +1753,16 @@ class FastPath:
             # jobs whose rows were evicted re-plan (and re-fetch) if they come back
             stale = [k for k, w in self.works.items()
                      if (self.sliding if w.plan.sliding else self.static).keys[int(w.rows[0])] != w.plan.keys[0]]
+            gone_w = []
             for k in stale:
                 w = self.works.pop(k)
+                gone_w.append(w)
                 self._gcount_add(w.plan.group, -1)
                 if w.wcur is not None:
                     self.wt.release(np.concatenate([w.wcur, w.wbase]))
+            if gone_w and self.b.exporter is not None:         # jobs that stopped coming (shard moved)
+                self.b.exporter.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name,
+                                              w.plan.cluster) for w in gone_w], self.b.clock())
 
 
 def _merge_series(ss) -> tuple[np.ndarray, np.ndarray]:

@@ -65,6 +65,24 @@ class Mailbox:
         self.store.set(f"{k}#n", str(n + 1).encode())       # count last: readers never see a gap
         return n
 
+    def trim(self, key: str) -> int:
+        """Delete this rank's whole ``key`` log from the store (a reader must
+        be done with it: the exporter trims only epochs rank 0 acknowledged).
+        Returns the entries deleted."""
+        k = self._k(key, self.rank)
+        n = self._logn.pop(key, None)
+        if n is None:
+            if not self.store.check([f"{k}#n"]):
+                return 0
+            n = int(self.store.get(f"{k}#n"))
+        try:
+            self.store.delete_key(f"{k}#n")
+            for i in range(n):
+                self.store.delete_key(f"{k}#{i}")
+        except (AttributeError, RuntimeError, NotImplementedError):
+            return 0                                   # a store without deletes keeps the log
+        return n
+
     def read_log(self, key: str, rank: int, start: int) -> list[bytes]:
         """Entries ``start..`` of ``rank``'s ``key`` log available now."""
         k = self._k(key, rank)

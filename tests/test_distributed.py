@@ -163,7 +163,7 @@ def _w_brain(rank, world, db, n_apps):
     import torch.distributed as dist
     dist.barrier()
     exp.exchange(force=True)
-    ups = {k[2]: v for k in exp.table.keys if k[0].endswith("_upper") for v in [exp.table.get(k)]}
+    ups = {k[2]: v for k in exp.table.index if k[0].endswith("_upper") for v in [exp.table.get(k)]}
     dist.barrier()                         # rank 0 hosts the mailbox: leave together
     return r1.get("claimed", 0), r2.get("claimed", 0), ups
 
@@ -378,7 +378,7 @@ def _w_slow_rank(rank, world, db, stall_s, run_s):
             stalled_cycles += 1
         time.sleep(0.01)
     exp.pull(force=True)
-    r1 = {k[2] for k in exp.table.keys if k[0].endswith("_upper")}
+    r1 = {k[2] for k in exp.table.index if k[0].endswith("_upper")}
     age = exp.registry.get_sample_value("foremast_brain_rank_export_age_seconds", {"rank": "1"})
     mb.store.wait(["test/done/1"], timedelta(seconds=60))
     return {"cycles": cycles, "during_stall": stalled_cycles, "apps": sorted(r1), "age": age}
@@ -406,3 +406,53 @@ def test_slow_rank_never_stalls_peers(tmp_path, monkeypatch):
     owners = {a: D.service_owner("", a, 2) for a in apps}
     assert {a for a in apps if owners[a] == 1} <= set(r0["apps"])   # rank 1's gauges reached rank 0
     assert r0["age"] is not None and r0["age"] >= 1.0                # ...and are reported stale
+
+
+def _w_export_churn(rank, world):
+    """Rank 1 churns its series (retire + sweep + new keys) for 12 rounds;
+    rank 0's merged /metrics view follows, and the key log rolls over to a
+    new epoch whose predecessor is deleted from the store once rank 0 acked."""
+    import struct
+    import torch.distributed as dist
+    from foremast_amd.engine.exporter import BrainExporter
+    exp = BrainExporter()
+    t = 1000.0
+    live = []
+    for rnd in range(12):
+        if rank == 1:
+            if live:
+                exp.retire_jobs([(["m"], "ns", a, "") for a in live[:400]], t, 0.0)
+                exp.sweep(t)
+                live = live[400:]
+            new = [f"r{rnd}-a{j}" for j in range(400 if rnd else 500)]
+            for a in new:
+                exp.set_bounds("m", "ns", a, float(rnd), 0.0, float("nan"))
+            live += new
+            exp.exchange(force=True)
+        dist.barrier()
+        if rank == 0:
+            exp.exchange(force=True)
+        dist.barrier()
+        if rank == 1:
+            exp.exchange(force=True)                 # picks up rank 0's acks, trims old epochs
+        dist.barrier()
+    out = None
+    if rank == 0:
+        apps = sorted({k[2] for k in exp.table.index})
+        out = (apps, exp._kep.get(1, 0))
+    else:
+        mb = exp._mailbox()
+        gone = not mb.store.check([mb._k("gk0", 1) + "#n"])
+        out = (sorted(live), exp._epoch, gone)
+    got = D.all_gather_object(out)
+    dist.barrier()
+    return got
+
+
+def test_exporter_series_churn_across_ranks_with_epoch_trim():
+    got = _run(_w_export_churn, 2)
+    apps0, ep0 = got[0][0]
+    live1, ep1, gone = got[0][1]
+    assert apps0 == live1                            # rank 0 lists exactly rank 1's live series
+    assert ep1 >= 1 and ep0 == ep1                   # the log rolled over and rank 0 follows
+    assert gone                                      # epoch 0's entries were deleted from the store

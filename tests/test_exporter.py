@@ -89,3 +89,93 @@ def test_serve_metrics_over_http():
         assert r.headers["Content-Encoding"] == "gzip" and gzip.decompress(r.read()) == e.render()
     finally:
         srv.shutdown()
+
+
+def test_churn_rounds_keep_the_table_bounded_by_live_jobs():
+    """20 churn rounds of a 10k canary fleet (8 metrics).  Each
+    round's jobs retire when the next round's arrive; after the TTL their
+    series leave /metrics and their slots are reused -- the table (keys,
+    value vector, prefix buffers) stays bounded by the live jobs."""
+    e = BrainExporter()
+    bms = [f"namespace_app_pod_m{k}" for k in range(8)]
+    n_jobs, ttl = 10_000, 300.0
+    now = 1_760_000_000.0
+    prev = None
+    sizes = []
+    for rnd in range(20):
+        apps = [f"r{rnd}-svc{j}" for j in range(n_jobs)]
+        sl = e.bound_slots([b for _ in apps for b in bms], [a for a in apps for _ in bms],
+                           [a for a in apps for _ in bms])
+        e.set_bounds_many(sl, np.full(len(sl), 1.0), np.zeros(len(sl)), np.full(len(sl), np.nan))
+        if prev is not None:
+            e.retire_jobs([(bms, a, a, "") for a in prev], now, ttl)
+        now += ttl + 1
+        e.sweep(now)
+        sizes.append((len(e.table), len(e.table.vals), sum(len(b) for b in e.table._fprefix)))
+        prev = apps
+    live = n_jobs * 8 * 3
+    assert all(n <= live for n, _, _ in sizes[1:])
+    assert max(v for _, v, _ in sizes) <= 3 * live          # slot reuse: the value vector stops growing
+    assert sizes[-1][1] == sizes[5][1]
+    assert sizes[-1][2] <= 2.2 * sizes[0][2]                  # prefix buffers compacted (names grew a char)
+    body = e.render()
+    assert b"r18-svc" not in body and b"r19-svc9999" in body
+    got = _parse(body)
+    assert len(got) == live
+
+
+def test_retired_series_stay_for_the_ttl_and_revive_on_write():
+    e = BrainExporter()
+    e.set_bounds("namespace_app_pod_cpu", "ns", "a", 1.0, 0.0, float("nan"))
+    e.set_bounds("namespace_app_pod_cpu", "ns", "b", 2.0, 0.0, float("nan"))
+    t = 1000.0
+    e.retire_jobs([(["namespace_app_pod_cpu"], "ns", "a", ""), (["namespace_app_pod_cpu"], "ns", "b", "")], t, 60)
+    e.sweep(t + 30)
+    assert b'app="a"' in e.render()                        # final verdict still visible
+    e.set_bounds("namespace_app_pod_cpu", "ns", "b", 3.0, 0.0, float("nan"))     # another job writes b
+    e.sweep(t + 61)
+    body = e.render()
+    assert b'app="a"' not in body and b'app="b"' in body
+    assert _parse(body)[("foremastbrain:namespace_app_pod_cpu_upper", "ns", "b", "")] == 3.0
+    # the freed slots are reused by new series
+    n = len(e.table.vals)
+    e.set_bounds("namespace_app_pod_cpu", "ns", "c", 4.0, 0.0, float("nan"))
+    assert len(e.table.vals) == n and _parse(e.render())[("foremastbrain:namespace_app_pod_cpu_upper", "ns", "c", "")] == 4.0
+
+
+def test_brain_retires_closed_jobs_gauges_after_ttl():
+    """Through the brain: canary jobs close, their gauges stay the TTL, then
+    /metrics no longer lists them; the newest round's are still listed."""
+    from foremast_amd.api import crd
+    from foremast_amd.config import BrainConfig
+    from foremast_amd.controller.analyst import AnalystClient
+    from foremast_amd.engine.brain import Brain
+    from foremast_amd.engine.sources import SourceRouter
+    from foremast_amd.service.app import create_app
+    from foremast_amd.service.store import MemoryStore
+
+    class Clock:
+        t = 1_760_000_000.0
+
+        def __call__(self):
+            return self.t
+    clock = Clock()
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    exp = BrainExporter()
+    cfg = BrainConfig()
+    cfg.export_series_ttl_s = 120.0
+    brain = Brain(store, cfg, sources=SourceRouter.synthetic_only(), clock=clock, exporter=exp, worker_id="w")
+    mets = crd.Metrics("prometheus", "http://prom/api/v1/", [crd.Monitoring("http_server_requests_latency", "gauge",
+                                                                           "latency")])
+    for rnd in range(4):
+        for j in range(6):
+            client.start_analyzing("default", f"c{rnd}-{j}", [[f"c{rnd}-{j}-7687b9f4d7-p0"],
+                                                             [f"c{rnd}-{j}-5db89899b5-q0"]], mets, 10, "canary")
+        for _ in range(3):
+            brain.run_once()
+            clock.t += 400                              # past the 11-minute window: canaries close
+    body = exp.render()
+    assert b'app="c0-' not in body and b'app="c1-' not in body
+    assert b'app="c3-5"' in body
+    assert len(exp.table) <= 3 * 6 * 2
