@@ -20,13 +20,13 @@ def _matches(q: dict, d: dict) -> bool:
         return True
     if "terms" in q:
         (f, vals), = q["terms"].items()
-        return d.get(f.replace(".keyword", "")) in vals
+        return d.get(f.replace(".keyword", ""), "") in vals
     if "match" in q:
         (f, v), = q["match"].items()
         return d.get(f.replace(".keyword", "")) == v
     if "range" in q:
         (f, cond), = q["range"].items()
-        v = d.get(f, "")
+        v = d.get(f, 0.0 if f == "chg" else "")
         return all({"lt": v < x, "lte": v <= x, "gt": v > x, "gte": v >= x}[op] for op, x in cond.items())
     if "script" in q:
         p = q["script"]["script"]["params"]
@@ -34,6 +34,7 @@ def _matches(q: dict, d: dict) -> bool:
         return d["ownerKey"] % p["w"] == p["r"]
     b = q["bool"]
     ok = all(_matches(x, d) for x in b.get("must", []) + b.get("filter", []))
+    ok = ok and not any(_matches(x, d) for x in b.get("must_not", []))
     if "should" in b:
         ok = ok and sum(_matches(x, d) for x in b["should"]) >= b.get("minimum_should_match", 1)
     return ok
@@ -42,6 +43,7 @@ def _matches(q: dict, d: dict) -> bool:
 class FakeES:
     def __init__(self):
         self.docs: dict[str, tuple[int, dict]] = {}
+        self.leases: dict[str, dict] = {}
         self.logs: list[dict] = []
         self.seq = 0
         self.interfere = None   # callable run once before a conditional bulk update
@@ -54,6 +56,11 @@ class FakeES:
         if parts == ["_bulk"]:
             return self._bulk(req.content.decode())
         body = json.loads(req.content) if req.content else {}
+        if parts[0] == "leases" and len(parts) == 3 and req.method == "PUT":
+            self.leases[urllib.parse.unquote(parts[2])] = body
+            return httpx.Response(200, json={"result": "updated"})
+        if parts == ["leases", "_search"]:
+            return httpx.Response(200, json={"hits": {"hits": [{"_id": k, "_source": v} for k, v in self.leases.items()]}})
         if parts[0] == "documents" and len(parts) == 3 and req.method == "PUT":
             self.seq += 1
             self.docs[parts[2]] = (self.seq, body)
@@ -102,6 +109,10 @@ class FakeES:
             if op == "index" and meta["_index"] == "hpalogs":
                 self.logs.append(src)
                 items.append({"index": {"status": 201}})
+            elif op == "index" and meta["_index"] == "documents":
+                self.seq += 1
+                self.docs[meta["_id"]] = (self.seq, src)
+                items.append({"index": {"status": 201, "_seq_no": self.seq, "_primary_term": 1}})
             elif op == "update":
                 cur = self.docs.get(meta["_id"])
                 if cur is None:
@@ -113,7 +124,7 @@ class FakeES:
                 else:
                     self.seq += 1
                     self.docs[meta["_id"]] = (self.seq, dict(cur[1], **src["doc"]))
-                    items.append({"update": {"status": 200}})
+                    items.append({"update": {"status": 200, "_seq_no": self.seq, "_primary_term": 1}})
         return httpx.Response(200, json={"errors": errors, "items": items})
 
 
@@ -150,8 +161,10 @@ def test_es_claim_is_one_scan_and_one_conditional_bulk():
     got = st.claim("me", 10, 90.0, now=1_760_000_000.0)
     ids = sorted(d.id for d in got)
     assert ids == ["j1", "j2"]
-    # one search + one _bulk, no per-document request, no forced refresh
-    assert [(m, p) for m, p, _ in es.requests] == [("POST", "/documents/_search"), ("POST", "/_bulk")]
+    # the lease table, one search, the worker's lease beat and one _bulk: no
+    # per-document request, no forced refresh
+    assert [(m, p) for m, p, _ in es.requests] == [("POST", "/leases/_search"), ("POST", "/documents/_search"),
+                                                   ("PUT", "/leases/lease/me"), ("POST", "/_bulk")]
     assert all("refresh" not in q for _, _, q in es.requests)
     assert es.docs["j0"][1]["processingContent"] == "other"
     assert all(es.docs[i][1]["status"] == ST.PREPROCESS_INPROGRESS for i in ids)
@@ -182,3 +195,59 @@ def test_es_claim_pages_and_shards():
     for i in range(10):
         st2.put(Document(id=f"k{i}", app_name=f"a{i}", status=ST.INITIAL, modified_at=f"2025-01-01T00:00:0{i}Z"))
     assert [d.id for d in st2.claim("w", 4, 90.0, now=1_760_000_000.0)] == ["k0", "k1", "k2", "k3"]
+
+
+def test_es_takeover_rejects_the_stale_verdict():
+    """Mirror of the SQLite lease test: worker A holds a job, stops beating,
+    B takes it over after MAX_STUCK_IN_SECONDS; A's late verdict is rejected
+    (409 on its if_seq_no) and the job leaves A's session."""
+    es, st = _store()
+    t0 = 1_760_000_000.0
+    st.put(Document(id="j1", app_name="a1", status=ST.INITIAL, modified_at="2025-01-01T00:00:00Z"))
+    ba = st.claim_batch("A", 10, 90.0, now=t0)
+    assert ba.ids == ["j1"] and ba.docs([0])[0].processing_content == "A"
+    bb = st.claim_batch("B", 10, 90.0, now=t0 + 30)            # A's lease is fresh: nothing for B
+    assert bb.ids == []
+    bb = st.claim_batch("B", 10, 90.0, now=t0 + 200)           # A stopped beating: B takes over
+    assert bb.ids == ["j1"] and es.docs["j1"][1]["processingContent"] == "B"
+    st.update_many([("j1", {"status": ST.COMPLETED_UNHEALTH, "reason": "stale"})], now=t0 + 201, worker="A")
+    assert es.docs["j1"][1]["status"] == ST.PREPROCESS_INPROGRESS and es.docs["j1"][1]["processingContent"] == "B"
+    assert "j1" not in st._sessions["A"].held
+    # the new owner's verdict goes through
+    st.update_many([("j1", {"status": ST.COMPLETED_HEALTH, "reason": ""})], now=t0 + 202, worker="B")
+    assert es.docs["j1"][1]["status"] == ST.COMPLETED_HEALTH
+    assert "j1" not in st._sessions["B"].held
+
+
+def test_es_resubmission_and_abort_leave_the_session():
+    es, st = _store()
+    t0 = 1_760_000_000.0
+    for i in range(3):
+        st.put(Document(id=f"j{i}", app_name=f"a{i}", status=ST.INITIAL, created_at="c1"))
+    assert sorted(st.claim_batch("W", 10, 90.0, now=t0).ids) == ["j0", "j1", "j2"]
+    st.update_many([("j1", {"status": ST.ABORT})])               # the service's abort (no worker)
+    st.put(Document(id="j2", app_name="a2", status=ST.INITIAL, created_at="c2"))    # resubmission
+    b = st.claim_batch("W", 10, 90.0, now=t0 + 5)
+    assert sorted(b.ids) == ["j0", "j2"]                         # j1 aborted; j2 re-claimed as the new version
+    assert [d.created_at for d in b.docs([b.ids.index("j2")])] == ["c2"]
+
+
+def test_es_steady_state_cycle_is_constant_requests_at_10k():
+    """10k held jobs: after the first claim, a brain cycle (claim_batch +
+    keep) costs a constant number of requests -- no per-job write, no
+    re-claim, no re-scan of the held fleet."""
+    es, st = _store()
+    st.put_many([Document(id=f"j{i:05d}", app_name=f"svc{i}", status=ST.INITIAL,
+                          modified_at="2025-01-01T00:00:00Z") for i in range(10_000)])
+    t0 = 1_760_000_000.0
+    b = st.claim_batch("W", 20_000, 90.0, now=t0)
+    assert len(b.ids) == 10_000
+    counts = []
+    for k in range(1, 8):
+        es.requests.clear()
+        b = st.claim_batch("W", 20_000, 90.0, now=t0 + 10 * k)
+        st.keep("W", b.ids, now=t0 + 10 * k)
+        assert len(b.ids) == 10_000
+        counts.append(len(es.requests))
+    assert max(counts) <= 5, counts                   # feed + lease probe + claim probe (+ a beat)
+    assert all(m != "PUT" or p.startswith("/leases") for m, p, _ in es.requests)
