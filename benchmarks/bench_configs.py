@@ -454,6 +454,39 @@ def config3e2e(args):
         if prom is not None:
             prom.terminate()
             prom.wait(30)
+    restart = None
+    if args.restart:
+        # warm restart: checkpoint engine + resident history,
+        # a NEW brain (and store client, same worker id) restores them; the
+        # clock is its first cycle: claim (adopting its jobs) + the gap-only
+        # fetch + scoring + verdicts
+        ck = tempfile.mkdtemp(prefix="fm_ckpt_")
+        t_s = time.perf_counter()
+        brain.save_checkpoint(ck)
+        hp = brain.save_history(ck)
+        save_s = time.perf_counter() - t_s
+        n_req0 = live.requests if live is not None else 0
+        store2 = SQLiteStore(db) if args.store == "sqlite" else store
+        t["now"] += poll
+        if cw is not None:
+            cw.set(t["now"])
+        t_r = time.perf_counter()
+        brain2 = Brain(store2, cfg, device=dev, sources=router, clock=clock, batch_size=S + 1,
+                       worker_id=f"bench-{info.rank}", exporter=BrainExporter(), history_days=args.history_days)
+        brain2.load_checkpoint(ck)
+        n_rest = brain2.load_history(ck)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        load_s = time.perf_counter() - t_r
+        r2 = brain2.run_once()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        restart = {"restart_to_first_verdict_s": round(time.perf_counter() - t_r, 3), "load_s": round(load_s, 3),
+                   "save_s": round(save_s, 3), "history_file_gb": round(os.path.getsize(hp) / 1e9, 3) if hp else None,
+                   "rows_restored": n_rest, "first_cycle_claimed": r2.get("claimed"),
+                   "first_cycle_http_requests": (live.requests - n_req0) if live is not None else None,
+                   "first_cycle_spans_ms": {k: round(v * 1e3, 2) for k, v in brain2.spans.last.items()}}
+        print(f"[{kind}] rank {info.rank}: warm restart {restart}", file=sys.stderr, flush=True)
     timed = rows[args.warmup:]
     per_cycle = sum(timed) / max(1, len(timed))
     cpu = torch.device("cpu") if dev.type == "cpu" else dev
@@ -489,7 +522,7 @@ def config3e2e(args):
              "pods_per_side": P if strategy == "canary" else 0, "store": args.store,
              "topology": ("REST service in its own process + every rank on one WAL SQLite file"
                           if args.store == "sqlite" else "single process, in-memory store"),
-             "rest_poller": poll_out, "rows_per_cycle_rank0": per_cycle,
+             "rest_poller": poll_out, "rows_per_cycle_rank0": per_cycle, "warm_restart": restart,
              "source": args.source, "submission_spread_s": spread,
              "http": ({"requests_per_cycle_mean": round(statistics.mean(x for x, _ in req_log[args.warmup:]), 2),
                        "requests_per_cycle_max": max(x for x, _ in req_log[args.warmup:]),
@@ -621,6 +654,8 @@ def main():
                          "Prometheus in its own process (http; 7-day histories from the staged archive)")
     ap.add_argument("--spread-seconds", type=float, default=None, help="e2e --source http: job submissions spread "
                     "over this many seconds (canary windows at every phase of the 60-s grid; default 60)")
+    ap.add_argument("--restart", action="store_true", help="e2e configs: after the timed cycles, checkpoint and "
+                    "restart the brain (engine state + resident history) and time restart-to-first-verdict")
     ap.add_argument("--prom-workers", type=int, default=4, help="e2e --source http: fake Prometheus processes")
     ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "
                     "body every N seconds in a thread while the cycles are timed (0: off)")

@@ -147,9 +147,47 @@ def promql_metric_name(query: str) -> str:
     return m.group(1) if m else ""
 
 
+_COMMON_ESC = (("%7B", "{"), ("%7D", "}"), ("%3D", "="), ("%22", '"'), ("%2C", ","), ("%7E", "~"), ("%7C", "|"),
+               ("%3A", ":"), ("%5C", "\\"))
+_OTHER_ESC = re.compile(r"%(?!7B|7D|3D|22|2C|7E|7C|3A|5C)")
+
+
+def fast_unquote_plus(v: str) -> str:
+    """``urllib.parse.unquote_plus`` with a fast path for the escapes a
+    PromQL selector produces (braces, quotes, ``=``, ``,``, ``~``, ``|``)."""
+    if "%" not in v:
+        return v.replace("+", " ") if "+" in v else v
+    if _OTHER_ESC.search(v) is None:
+        if "+" in v:
+            v = v.replace("+", " ")
+        for a, b in _COMMON_ESC:
+            if a in v:
+                v = v.replace(a, b)
+        return v
+    return urllib.parse.unquote_plus(v)
+
+
+def fast_qsl(qs: str) -> list[tuple[str, str]]:
+    """``urllib.parse.parse_qsl(qs, keep_blank_values=True)`` for the URLs the
+    brain parses per job (a canary query carries a 1-KB pod union): values
+    are unquoted only when they contain an escape."""
+    out = []
+    uq = fast_unquote_plus
+    for part in qs.split("&"):
+        if not part:
+            continue
+        k, _, v = part.partition("=")
+        if "%" in k or "+" in k:
+            k = uq(k)
+        if "%" in v or "+" in v:
+            v = uq(v)
+        out.append((k, v))
+    return out
+
+
 def prometheus_query_of(url: str) -> dict[str, str]:
     """Split a query_range URL into its parameters (query unescaped)."""
     base, _, qs = url.partition("?")
-    params = dict(urllib.parse.parse_qsl(qs, keep_blank_values=True))
+    params = dict(fast_qsl(qs))
     params["_endpoint"] = base[: -len("query_range")] if base.endswith("query_range") else base
     return params

@@ -87,6 +87,8 @@ def brain_main(argv=None) -> None:  # pragma: no cover - process entry
     ckpt = os.environ.get("BRAIN_CHECKPOINT_DIR")
     if ckpt:
         brain.load_checkpoint(ckpt)
+        n = brain.load_history(ckpt)                  # warm restart: resident history without a re-fetch
+        print(f"restored {n} resident history rows from {ckpt}", file=sys.stderr, flush=True)
     # SIGTERM (pod shutdown; torchrun forwards it to every rank) ends the
     # loop after the current cycle and writes a final checkpoint
     import signal

@@ -105,6 +105,9 @@ class BrainConfig:
     # a closed / expired / moved job's gauges stay this long (final verdict
     # visible), then leave /metrics
     export_series_ttl_s: float = 300.0     # EXPORT_SERIES_TTL_SECONDS
+    # warm restart: the resident history grids are checkpointed on this
+    # cadence and at shutdown (a restarted rank re-fetches only the gap)
+    history_checkpoint_s: float = 600.0    # HISTORY_CHECKPOINT_SECONDS (0: only at shutdown)
     # canary window ingestion (engine/ingest.py): a grid point of a live
     # metric store is read once, METRIC_SETTLE_SECONDS after its time (a
     # recording rule's value for t is final once its evaluation landed)
@@ -180,6 +183,7 @@ class BrainConfig:
         c.brain_cluster = env.get("BRAIN_CLUSTER", c.brain_cluster)
         c.export_sync_s = _f(env, "EXPORT_SYNC_SECONDS", c.export_sync_s)
         c.export_series_ttl_s = _f(env, "EXPORT_SERIES_TTL_SECONDS", c.export_series_ttl_s)
+        c.history_checkpoint_s = _f(env, "HISTORY_CHECKPOINT_SECONDS", c.history_checkpoint_s)
         c.metric_settle_s = _f(env, "METRIC_SETTLE_SECONDS", c.metric_settle_s)
         c.fetch_batch = _i(env, "FETCH_BATCH", c.fetch_batch)
         c.fetch_max_values = _i(env, "FETCH_MAX_VALUES", c.fetch_max_values)

@@ -590,6 +590,7 @@ class Brain:
         and its fitted-model cache."""
         poll = self.cfg.poll_interval if poll is None else poll
         n = 0
+        hist_t = time.monotonic()
         try:
             while stop is None or not stop.is_set():
                 try:
@@ -597,6 +598,10 @@ class Brain:
                     n += 1
                     if checkpoint_dir and checkpoint_every > 0 and n % checkpoint_every == 0:
                         self.save_checkpoint(checkpoint_dir)
+                    if checkpoint_dir and self.cfg.history_checkpoint_s > 0 and \
+                            time.monotonic() - hist_t >= self.cfg.history_checkpoint_s:
+                        self.save_history(checkpoint_dir)
+                        hist_t = time.monotonic()
                     if r.get("claimed", 0) == 0:
                         (stop.wait(poll) if stop is not None else time.sleep(poll))
                 except Exception:
@@ -606,6 +611,7 @@ class Brain:
             if checkpoint_dir:
                 try:
                     self.save_checkpoint(checkpoint_dir)
+                    self.save_history(checkpoint_dir)
                 except Exception:  # noqa: BLE001 - shutting down
                     log.exception("final checkpoint failed")
 
@@ -761,6 +767,40 @@ class Brain:
         from . import checkpoint
         t, meta = self.state_tensors()
         return checkpoint.save(dirpath, t, meta, tag=checkpoint.rank_tag(self.info.rank, self.info.world))
+
+    def save_history(self, dirpath: str):
+        """The device-resident history grids of every live job
+        (``history-r<rank>of<world>-<ms>.safetensors``), for a warm restart:
+        :meth:`load_history` puts them back and the first cycle fetches only
+        the gap since each row's newest sample."""
+        from . import checkpoint
+        from .fastpath import history_state
+        if self.fast is None:
+            return None
+        t, meta = history_state(self.fast)
+        meta.update(rank=self.info.rank, world=self.info.world)
+        return checkpoint.save(dirpath, t, meta, tag=checkpoint.rank_tag(self.info.rank, self.info.world),
+                               keep=2, kind="history")
+
+    def load_history(self, dirpath: str) -> int:
+        """Restore the history rows this rank owns from its own latest history
+        checkpoint, or -- after a world-size change -- from every rank's of the
+        newest world.  Returns the rows restored."""
+        from . import checkpoint
+        from .fastpath import load_history
+        if self.fast is None:
+            return 0
+        tag = checkpoint.rank_tag(self.info.rank, self.info.world)
+        own = checkpoint.load_latest(dirpath, tag, with_time=True, kind="history")
+        newest = checkpoint.newest_save(dirpath, kind="history")
+        if own is not None and (newest is None or newest[0] == self.info.world or newest[1] <= own[2]):
+            sets = [own[:2]]
+        else:
+            sets = checkpoint.load_any_world(dirpath, kind="history")
+        n = 0
+        for t, meta in sets:
+            n += load_history(self.fast, t, meta, self.clock(), owns=self._owns_key)
+        return n
 
     def _owns_key(self, namespace: str, app: str) -> bool:
         if self.info.world <= 1:

@@ -23,23 +23,30 @@ def rank_tag(rank: int, world: int) -> str:
     return f"-r{rank}of{world}" if world > 1 else ""
 
 
+def _pointer(kind: str) -> str:
+    return "LATEST" if kind == "engine" else f"LATEST_{kind.upper()}"
+
+
 def save(dirpath: str, tensors: dict[str, torch.Tensor], meta: dict, step: int | None = None, tag: str = "",
-         keep: int = 3) -> Path:
+         keep: int = 3, kind: str = "engine") -> Path:
     """``tag`` separates the ranks of a data-parallel brain
     (``-r<rank>of<world>``): each rank writes its own file and LATEST pointer.
-    The ``keep`` newest files of the tag are retained."""
+    The ``keep`` newest files of the tag are retained.  ``kind``: ``engine``
+    (small, every few cycles) or ``history`` (the device-resident history
+    grids: large, on its own cadence and at shutdown)."""
     d = Path(dirpath)
     d.mkdir(parents=True, exist_ok=True)
     step = int(time.time() * 1000) if step is None else step
-    path = d / f"engine{tag}-{step}.safetensors"
-    tmp = d / f".engine{tag}-{step}.tmp"
+    path = d / f"{kind}{tag}-{step}.safetensors"
+    tmp = d / f".{kind}{tag}-{step}.tmp"
     md = {"format": FORMAT_VERSION, "meta": json.dumps(meta), "saved_at": str(time.time())}
     save_file({k: v.detach().contiguous().cpu() for k, v in tensors.items()}, str(tmp), metadata=md)
     os.replace(tmp, path)
-    latest_tmp = d / f".LATEST{tag}.tmp"
+    ptr = _pointer(kind)
+    latest_tmp = d / f".{ptr}{tag}.tmp"
     latest_tmp.write_text(path.name)
-    os.replace(latest_tmp, d / f"LATEST{tag}")
-    old = sorted(d.glob(f"engine{tag}-*.safetensors"), key=lambda p: p.stat().st_mtime)
+    os.replace(latest_tmp, d / f"{ptr}{tag}")
+    old = sorted(d.glob(f"{kind}{tag}-*.safetensors"), key=lambda p: p.stat().st_mtime)
     for p in old[:-keep] if keep > 0 else []:
         if p != path:
             p.unlink(missing_ok=True)
@@ -64,12 +71,13 @@ def saved_at(path: Path) -> float:
         return float((f.metadata() or {}).get("saved_at", "0"))
 
 
-def _latest_files(dirpath: str) -> dict[int, list[tuple[float, Path]]]:
+def _latest_files(dirpath: str, kind: str = "engine") -> dict[int, list[tuple[float, Path]]]:
     """world size -> [(saved_at, file)] of every rank's LATEST pointer."""
     d = Path(dirpath)
     sets: dict[int, list[tuple[float, Path]]] = {}
-    for lf in d.glob("LATEST*"):
-        name = lf.name[len("LATEST"):]
+    ptr = _pointer(kind)
+    for lf in d.glob(f"{ptr}*"):
+        name = lf.name[len(ptr):]
         world = 1
         if name.startswith("-r") and "of" in name:
             try:
@@ -84,20 +92,20 @@ def _latest_files(dirpath: str) -> dict[int, list[tuple[float, Path]]]:
     return sets
 
 
-def newest_save(dirpath: str) -> tuple[int, float] | None:
+def newest_save(dirpath: str, kind: str = "engine") -> tuple[int, float] | None:
     """(world size, saved_at) of the most recent checkpoint of any world."""
-    sets = _latest_files(dirpath)
+    sets = _latest_files(dirpath, kind)
     if not sets:
         return None
     w = max(sets, key=lambda k: max(t for t, _ in sets[k]))
     return w, max(t for t, _ in sets[w])
 
 
-def load_latest(dirpath: str, tag: str = "", with_time: bool = False):
+def load_latest(dirpath: str, tag: str = "", with_time: bool = False, kind: str = "engine"):
     """This tag's latest checkpoint as (tensors, meta), or with
     ``with_time`` (tensors, meta, saved_at)."""
     d = Path(dirpath)
-    lf = d / f"LATEST{tag}"
+    lf = d / f"{_pointer(kind)}{tag}"
     if not lf.exists():
         return None
     got = _read(d / lf.read_text().strip())
@@ -106,10 +114,10 @@ def load_latest(dirpath: str, tag: str = "", with_time: bool = False):
     return got if with_time else got[:2]
 
 
-def load_any_world(dirpath: str) -> list[tuple[dict[str, torch.Tensor], dict]]:
+def load_any_world(dirpath: str, kind: str = "engine") -> list[tuple[dict[str, torch.Tensor], dict]]:
     """Every rank's latest checkpoint of the most recently saved world size
     (a restart with a different world re-shards from all of them)."""
-    sets = _latest_files(dirpath)
+    sets = _latest_files(dirpath, kind)
     if not sets:
         return []
     world = max(sets, key=lambda w: max(t for t, _ in sets[w]))

@@ -480,6 +480,7 @@ class FastPath:
             else:
                 unknown.append(k)
         rest = []
+        reg: list[FastWork] = []
         if unknown:
             for k, d in zip(unknown, batch.docs(unknown)):
                 old = works.pop(d.id, None)
@@ -499,10 +500,12 @@ class FastPath:
                 fw = works[d.id] = FastWork(d, p, rows, end_ts, version=batch.versions[k],
                                             handle=None if handles is None else int(handles[k]))
                 if not p.sliding:
-                    self._register_windows(fw)
+                    reg.append(fw)
                 self._gcount_add(p.group, 1)
                 fast.append(fw)
                 todo.append(fw)
+        if reg:
+            self._register_windows(reg)
         self.todo = todo
         self._last = (batch.ids, batch.versions, fast, todo) if not rest else None
         return fast, rest
@@ -542,41 +545,67 @@ class FastPath:
         self._wt_changed = self.wt.fetch(self.b.sources, now, pool) > 0 or self._wt_changed
         return works
 
-    def _register_windows(self, fw: FastWork) -> None:
-        """Put a static job's current / baseline windows into the window
-        table when every one of them is batchable (a plain selector with one
-        pod / app matcher, absolute times, a source with ``fetch_keyed``);
-        otherwise the job keeps the per-job fetch."""
+    def _register_windows(self, fws: list[FastWork]) -> None:
+        """Put new static jobs' current / baseline windows into the window
+        table (one batched ``add_many``) when every one of a job's windows is
+        batchable (a plain selector with one pod / app matcher, absolute
+        times, a source with ``fetch_keyed``); otherwise the job keeps the
+        per-job fetch."""
         import os
         if os.environ.get("FM_NO_TABLE"):
             return
         from .ingest import parse_range
-        p = fw.plan
         router = self.b.sources
-        rows = []
-        live = False
-        for urls, stores in ((p.cur_urls, p.cur_stores), (p.base_urls, p.base_stores)):
-            row = []
-            for u, st in zip(urls, stores):
-                if not u:
-                    row.append(None)
-                    continue
-                if router.keyed_source(st) is None:
-                    return
-                spec = parse_range(u)
-                if spec is None:
-                    return
-                row.append((spec, st))
-                live = live or router.live(st)
-            rows.append(row)
+        keyed: dict[str, bool] = {}
+        live_of: dict[str, bool] = {}
+        specs, lives, stores, owners = [], [], [], []
+        for fw in fws:
+            p = fw.plan
+            mine = []
+            ok = True
+            for urls, st_list in ((p.cur_urls, p.cur_stores), (p.base_urls, p.base_stores)):
+                for u, st in zip(urls, st_list):
+                    if not u:
+                        mine.append(None)
+                        continue
+                    if st not in keyed:
+                        keyed[st] = router.keyed_source(st) is not None
+                        live_of[st] = router.live(st) if keyed[st] else False
+                    spec = parse_range(u) if keyed[st] else None
+                    if spec is None:
+                        ok = False
+                        break
+                    mine.append((spec, st))
+                if not ok:
+                    break
+            if not ok:
+                continue
+            owners.append((fw, mine))
+            for x in mine:
+                if x is not None:
+                    specs.append(x[0])
+                    stores.append(x[1])
+                    lives.append(live_of[x[1]])
+        if not owners:
+            return
         wt = self.wt
-        fw.wcur, fw.wbase = (np.array([-1 if x is None else wt.add(x[0], router.live(x[1]), x[1]) for x in row],
-                                      np.int64) for row in rows)
-        fw.has_window = True
-        if live:
-            fw.end_ts += wt.settle          # the last grid point is read settle seconds after its time
-        w = max(wt.max_points(fw.wcur), wt.max_points(fw.wbase))
-        fw.wclass = 0 if w <= 128 else (1 if w <= 256 else 2)
+        wids = wt.add_many(specs, lives, stores)
+        k = 0
+        for fw, mine in owners:
+            ids = np.full(len(mine), -1, np.int64)
+            live = False
+            for i, x in enumerate(mine):
+                if x is not None:
+                    ids[i] = wids[k]
+                    live = live or live_of[x[1]]
+                    k += 1
+            M = len(fw.plan.aliases)
+            fw.wcur, fw.wbase = ids[:M], ids[M:]
+            fw.has_window = True
+            if live:
+                fw.end_ts += wt.settle          # the last grid point is read settle seconds after its time
+            w = int(max((wt.nslot[x] * wt.ncol[x] for x in ids if x >= 0), default=0))
+            fw.wclass = 0 if w <= 128 else (1 if w <= 256 else 2)
 
     def _fetch_static_history(self, ws: list[FastWork], now: float, pool=None) -> list[FastWork]:
         """Batched static history (``namespace_app_pod_<m>{namespace,app}`` over
@@ -607,6 +636,10 @@ class FastPath:
                 items.append((i, spec, p.hist_stores[i]))
             if not ok:
                 left.append(fw)
+                continue
+            if not need.any():                     # every row resident (a warm restart)
+                fw.hist_complete = True
+                fw.settled = True
                 continue
             for i, spec, st in items:
                 groups.setdefault((st, spec.group, spec.start, spec.end), []).append((fw, i, spec.values[0]))
@@ -1763,6 +1796,93 @@ class FastPath:
             if gone_w and self.b.exporter is not None:         # jobs that stopped coming (shard moved)
                 self.b.exporter.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name,
                                               w.plan.cluster) for w in gone_w], self.b.clock())
+
+
+def _history_rows(fp: "FastPath"):
+    """(store name, store, rows, keys, owners) of every resident row a live
+    job references -- what a warm restart needs."""
+    per = {"static": {}, "sliding": {}}
+    for w in fp.works.values():
+        p = w.plan
+        d = per["sliding" if p.sliding else "static"]
+        for r, k in zip(w.rows.tolist(), p.keys):
+            d.setdefault(int(r), (k, (p.namespace, w.doc.app_name)))
+    for name, st in (("static", fp.static), ("sliding", fp.sliding)):
+        d = per[name]
+        rows = np.array([r for r in sorted(d) if st.keys[r] == d[r][0]], np.int64)
+        yield name, st, rows, [d[int(r)][0] for r in rows], [d[int(r)][1] for r in rows]
+
+
+def history_state(fp: "FastPath") -> tuple[dict, dict]:
+    """The device-resident history of every live job (static rows: the
+    left-aligned samples; sliding rows: the window's columns) + their row
+    keys, owners and times, for a warm restart (``Brain.save_history``)."""
+    t: dict[str, torch.Tensor] = {}
+    meta: dict = {"step": fp.b.step}
+    for name, st, rows, keys, owners in _history_rows(fp):
+        if not len(rows):
+            continue
+        ri = torch.as_tensor(rows, device=st.device)
+        if st.sliding:
+            if st.t0 is None or st.e <= st.ws:
+                continue
+            t[f"{name}.values"] = st.buf.index_select(0, ri)[:, st.ws:st.e].cpu()
+            meta[f"{name}.t_first"] = st.t0 + st.ws * st.step
+        else:
+            w = max(1, int(st.nlen[rows].max()))
+            t[f"{name}.values"] = st.buf.index_select(0, ri)[:, :w].cpu()
+            t[f"{name}.nlen"] = torch.from_numpy(st.nlen[rows].copy())
+        t[f"{name}.last_t"] = torch.from_numpy(st.last_t[rows].copy())
+        meta[f"{name}.keys"] = [list(k) for k in keys]
+        meta[f"{name}.owners"] = [list(o) for o in owners]
+    return t, meta
+
+
+def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> int:
+    """Restore saved rows (``owns(namespace, app)`` selects this rank's after a
+    re-shard).  Sliding rows land on the current grid by time (columns that
+    left the 7-day window are dropped); a restored row's ``last_t`` makes the
+    next fetch ask only for the gap since.  Returns the rows restored."""
+    n_rows = 0
+    for name, st in (("static", fp.static), ("sliding", fp.sliding)):
+        vals = t.get(f"{name}.values")
+        if vals is None:
+            continue
+        keys = [tuple(k) for k in meta.get(f"{name}.keys", [])]
+        owners = meta.get(f"{name}.owners", [])
+        sel = [i for i, (ns, app) in enumerate(owners) if owns is None or owns(ns, app)]
+        if not sel:
+            continue
+        keys = [keys[i] for i in sel]
+        ix = torch.as_tensor(sel, dtype=torch.int64)
+        v = vals.index_select(0, ix)
+        last_t = t[f"{name}.last_t"].numpy()[sel]
+        rows, _ = st.rows_for(keys, fp.cycle)
+        rows = rows.astype(np.int64)
+        if st.sliding:
+            st.advance(now, now - fp.history_s)
+            t_first = float(meta[f"{name}.t_first"])
+            c0 = int(st.col(t_first))                      # grid column of the saved block's column 0
+            lo, hi = max(st.ws, c0), min(st.e, c0 + v.shape[1])
+            if hi > lo:
+                blk = v[:, lo - c0:hi - c0].contiguous().to(st.device)
+                st.buf[torch.as_tensor(rows, device=st.device), lo:hi] = blk
+            keep_t = np.where(np.isfinite(last_t) & (last_t <= st.t0 + (st.e - 1) * st.step), last_t, -np.inf)
+            st.last_t[rows] = keep_t
+            st.nfin[rows] = torch.isfinite(st.buf.index_select(0, torch.as_tensor(rows, device=st.device))
+                                           [:, st.ws:st.e]).sum(1).cpu().numpy()
+        else:
+            w = min(v.shape[1], st.width)
+            full = torch.full((len(rows), st.width), float("nan"))
+            full[:, :w] = v[:, :w]
+            st.buf.index_copy_(0, torch.as_tensor(rows, device=st.device), full.to(st.device))
+            nlen = t[f"{name}.nlen"].numpy()[sel]
+            st.nlen[rows] = np.minimum(nlen, st.width)
+            st.nfin[rows] = torch.isfinite(full).sum(1).numpy()
+            st.last_t[rows] = last_t
+            st.max_len = max(st.max_len, int(st.nlen[rows].max()) if len(rows) else 0)
+        n_rows += len(rows)
+    return n_rows
 
 
 def _merge_series(ss) -> tuple[np.ndarray, np.ndarray]:

@@ -41,10 +41,11 @@ import ctypes
 import math
 import urllib.parse
 from dataclasses import dataclass
+from typing import NamedTuple
 
 import numpy as np
 
-from ..api.urls import END_PLACEHOLDER, START_PLACEHOLDER
+from ..api.urls import END_PLACEHOLDER, START_PLACEHOLDER, fast_qsl, fast_unquote_plus
 from . import native_rt
 from . import promql
 
@@ -65,8 +66,7 @@ def parse_step(s: str) -> float | None:
     return sum(float(a) * units[b] for a, b in parts)
 
 
-@dataclass(frozen=True)
-class RangeSpec:
+class RangeSpec(NamedTuple):
     """A ``query_range`` URL whose query is a plain selector with exactly one
     matcher on a key label: the batchable form.  ``matchers`` holds the other
     matchers, with ``(key, "", "")`` where the key matcher was (rendering keeps
@@ -86,13 +86,49 @@ class RangeSpec:
         return (self.base, self.metric, self.matchers, self.key, self.step, self.extra)
 
 
+import re as _re
+
+# the shape barrelman writes (metricsquery.go:72-99 through the service's
+# URL builder): one regex for the URL, one for the selector
+_FAST_URL = _re.compile(r"^([^?]*query_range)\?query=([^&]*)&start=(\d+(?:\.\d+)?)&end=(\d+(?:\.\d+)?)"
+                        r"&step=(\d+)$")
+_FAST_SEL = _re.compile(r'^([A-Za-z_:][\w:]*)\{namespace="([^"\\]*)",(pod|app)(=~|=)"([^"\\|]*(?:\|[^"\\|]+)*)"\}$')
+_PLAIN = _re.compile(r"^[\w-]*$")                 # no regex metacharacter (an unescaped "." is one)
+
+
+def _parse_fast(url: str, keys) -> RangeSpec | None:
+    m = _FAST_URL.match(url)
+    if m is None:
+        return None
+    q = fast_unquote_plus(m.group(2))
+    sm = _FAST_SEL.match(q)
+    if sm is None or sm.group(3) not in keys:
+        return None
+    v = sm.group(5)
+    if sm.group(4) == "=":
+        values = (v,)
+    else:
+        values = tuple(v.split("|"))
+        if not all(_PLAIN.match(x) for x in values):      # regex metacharacters: the general path decides
+            return None
+    if not values or any(x == "" for x in values):
+        return None
+    key = sm.group(3)
+    return RangeSpec(m.group(1), sm.group(1), (("namespace", "=", sm.group(2)), (key, "", "")), key, values,
+                     float(m.group(3)), float(m.group(4)), float(m.group(5)), ())
+
+
 def parse_range(url: str, keys=KEY_LABELS, windowed: bool = True) -> RangeSpec | None:
     """``windowed``: start / end must be absolute times (static windows); else
     ``START_TIME`` / ``END_TIME`` placeholders are accepted (start = end = nan)."""
     if "query_range?" not in url:
         return None
+    if windowed:
+        got = _parse_fast(url, keys)
+        if got is not None:
+            return got
     base, qs = url.split("?", 1)
-    params = urllib.parse.parse_qsl(qs, keep_blank_values=True)
+    params = fast_qsl(qs)
     d = dict(params)
     if len(d) != len(params) or "query" not in d:
         return None
@@ -303,6 +339,77 @@ class WindowTable:
         self.frag[w] = "|".join(promql.re_literal(v) for v in vals)
         self.next_due = -math.inf
         return w
+
+    def add_many(self, specs: list, lives, stores) -> np.ndarray:
+        """:meth:`add` for many windows at once (a claim batch of new jobs):
+        one hash call for every key value, vectorised bookkeeping."""
+        k = len(specs)
+        if k == 0:
+            return np.zeros(0, np.int64)
+        vals = [sorted(set(sp.values)) for sp in specs]
+        nsl = np.fromiter(map(len, vals), np.int64, k)
+        start = np.fromiter((sp.start for sp in specs), np.float64, k)
+        end = np.fromiter((sp.end for sp in specs), np.float64, k)
+        step = np.fromiter((sp.step for sp in specs), np.float64, k)
+        ncol = np.maximum(0, np.floor((end - start) / step + 1e-9).astype(np.int64) + 1)
+        if int(ncol.max()) > self.C:
+            C = max(int(ncol.max()), 2 * self.C)
+            V = np.full((self.V.shape[0], C), np.nan, np.float32)
+            V[:, :self.C] = self.V
+            self.V, self.C = V, C
+        # window ids: freed ones first, then new
+        nfree = min(len(self._free_w), k)
+        wids = np.empty(k, np.int64)
+        for i in range(nfree):
+            wids[i] = self._free_w.pop()
+        nnew = k - nfree
+        if nnew:
+            self._grow_w(self.n + nnew)
+            wids[nfree:] = np.arange(self.n, self.n + nnew)
+            self.n += nnew
+            self.values.extend([None] * nnew)
+            self.frag.extend([None] * nnew)
+        # slots: a freed block of the same size, else a new contiguous run
+        slot0 = np.empty(k, np.int64)
+        fresh = []
+        for i in range(k):
+            fl = self._free_s.get(int(nsl[i]))
+            if fl:
+                slot0[i] = fl.pop()
+            else:
+                fresh.append(i)
+        if fresh:
+            fi = np.asarray(fresh, np.int64)
+            tot = int(nsl[fi].sum())
+            base = self._alloc_slots(tot) if tot else self.ns
+            slot0[fi] = base + np.concatenate([[0], np.cumsum(nsl[fi])[:-1]])
+        flat = [v for vs in vals for v in vs]
+        sl = _ranges(slot0, nsl)
+        self.V[sl] = np.nan
+        self.khash[sl] = native_rt.fnv1a(flat)
+        self.kwin[sl] = np.repeat(wids, nsl)
+        groups = self.groups
+        gid = np.empty(k, np.int64)
+        # every window's regex fragment from ONE escape pass over all values
+        frags = promql.re_literal("\x00".join("\x01".join(vs) for vs in vals)).replace("\x01", "|").split("\x00")
+        for i, (sp, st) in enumerate(zip(specs, stores)):
+            gk = (sp.group, st)
+            g = groups.get(gk)
+            if g is None:
+                g = groups[gk] = len(self.group_keys)
+                self.group_keys.append(gk)
+            gid[i] = g
+            w = int(wids[i])
+            self.values[w] = vals[i]
+            self.frag[w] = frags[i]
+        self.start[wids], self.end[wids], self.step[wids] = start, end, step
+        self.settled[wids] = start - step
+        self.gid[wids], self.slot0[wids], self.nslot[wids], self.ncol[wids] = gid, slot0, nsl, ncol
+        self.live[wids] = np.asarray(lives, bool)
+        self.alive[wids], self.dirty[wids], self.err[wids] = True, True, False
+        self.toff[wids] = np.nan
+        self.next_due = -math.inf
+        return wids
 
     def release(self, wids) -> None:
         for w in np.asarray(wids, np.int64).reshape(-1).tolist():

@@ -730,21 +730,25 @@ class SQLiteStore(JobStore):
 
     # ------------------------------------------------------------------ claims
     def _claim_new(self, c, worker: str, limit: int, max_stuck_s: float, now: float, shard, seq: int,
-                   cols: str = "rid, id, ver") -> list:
+                   cols: str = "rid, id, ver", adopt: bool = False) -> list:
         if limit <= 0:
             return []
         cl, ip = tuple(sorted(ST.CLAIMABLE)), tuple(sorted(ST.IN_PROGRESS))
         sw, sa = self._shard_sql(shard)
         # stuck = in progress under a worker whose lease expired: the
         # (few) expired leases drive an index lookup per worker (CROSS JOIN
-        # fixes that loop order), never a scan of the live in-progress rows
+        # fixes that loop order), never a scan of the live in-progress rows.
+        # ``adopt``: a restarted worker (same id, new session) takes back the
+        # jobs it still holds a lease on instead of waiting for the lease to lapse
+        own = (f"union all select rid, modified from documents where worker = ? and "
+               f"status in ({','.join('?' * len(ip))}){sw} ") if adopt else ""
         q = (f"update documents set status=?, worker=?, modified=?, modified_at=?, seq=? where rid in ("
              f"select rid from (select rid, modified from documents where status in ({','.join('?' * len(cl))}){sw} "
              f"union all select d.rid, d.modified from leases l cross join documents d on d.worker = l.worker "
-             f"where l.beat < ? and d.status in ({','.join('?' * len(ip))}){sw.replace('okey', 'd.okey')}) "
+             f"where l.beat < ? and d.status in ({','.join('?' * len(ip))}){sw.replace('okey', 'd.okey')} {own}) "
              f"order by modified limit ?) returning {cols}")
         args = (ST.PREPROCESS_INPROGRESS, worker, now, _stamp(now), seq) + cl + sa + (now - max_stuck_s,) + ip + sa \
-            + (limit,)
+            + (((worker,) + ip + sa) if adopt else ()) + (limit,)
         self._beat(c, worker, now)
         return c.execute(q, args).fetchall()
 
@@ -800,6 +804,7 @@ class SQLiteStore(JobStore):
         for the worker's lease heartbeat every ``MAX_STUCK_IN_SECONDS`` / 6."""
         now = time.time() if now is None else now
         s = self._sessions.get(worker)
+        fresh = s is None
         if s is None:
             s = self._sessions[worker] = _Session()
         c = self._conn()
@@ -808,7 +813,7 @@ class SQLiteStore(JobStore):
             seq = c.execute("select v from meta where k = 'seq'").fetchone()[0]
             self._feed(c, s, worker, seq + 1)
             room = limit - len(s.held)
-            need = room > 0 and self._claimable(c, max_stuck_s, now, shard)
+            need = room > 0 and (fresh or self._claimable(c, max_stuck_s, now, shard))
         finally:
             c.execute("commit")
         s.last_seq = seq
@@ -818,7 +823,7 @@ class SQLiteStore(JobStore):
                 self._feed(c, s, worker, seq)           # writes since the snapshot
                 room = limit - len(s.held)
                 if need and room > 0:
-                    for rid, jid, ver in self._claim_new(c, worker, room, max_stuck_s, now, shard, seq):
+                    for rid, jid, ver in self._claim_new(c, worker, room, max_stuck_s, now, shard, seq, adopt=fresh):
                         s.add(jid, rid, ver)
                 else:
                     self._beat(c, worker, now)
@@ -1171,10 +1176,15 @@ class ElasticsearchStore(JobStore):
             return [], True
         return [], False
 
-    def _claim_query(self, max_stuck_s: float, now: float, shard, live=None, dead=None) -> tuple[dict, bool]:
+    def _claim_query(self, max_stuck_s: float, now: float, shard, live=None, dead=None,
+                     adopt: str | None = None) -> tuple[dict, bool]:
         stuck_before = _stamp(now - max_stuck_s)
         ip = sorted(ST.IN_PROGRESS)
         should = [{"terms": {"status.keyword": sorted(ST.CLAIMABLE)}}]
+        if adopt:
+            # a restarted worker (same id, new session) takes back what it still holds
+            should.append({"bool": {"filter": [{"terms": {"status.keyword": ip}},
+                                               {"terms": {"processingContent.keyword": [adopt]}}]}})
         if dead:
             # held by a worker whose lease expired
             should.append({"bool": {"filter": [{"terms": {"status.keyword": ip}},
@@ -1195,11 +1205,12 @@ class ElasticsearchStore(JobStore):
         now = time.time() if now is None else now
         return [d for d, _, _ in self._claim_hits(worker, limit, max_stuck_s, now, owner, shard)]
 
-    def _claim_hits(self, worker, limit, max_stuck_s, now, owner=None, shard=None, beat=True) -> list:
+    def _claim_hits(self, worker, limit, max_stuck_s, now, owner=None, shard=None, beat=True,
+                    adopt: bool = False) -> list:
         """(document, seq_no, primary_term) of every job claimed."""
         live, dead = self._leases(now, max_stuck_s)
         live = [w for w in live if w != worker]
-        q, py_shard = self._claim_query(max_stuck_s, now, shard, live, dead)
+        q, py_shard = self._claim_query(max_stuck_s, now, shard, live, dead, adopt=worker if adopt else None)
         scan_limit = None if (owner is not None or py_shard) else limit
         hits = self._scan(q, scan_limit, {"seq_no_primary_term": True})
         if beat:
@@ -1213,7 +1224,7 @@ class ElasticsearchStore(JobStore):
         for h in hits:
             d = Document.from_dict(h["_source"])
             held = d.status in ST.IN_PROGRESS
-            stuck = held and (d.processing_content in dead_s or
+            stuck = held and (d.processing_content in dead_s or (adopt and d.processing_content == worker) or
                               (d.processing_content not in live_s and d.processing_content != worker
                                and now - _ts(d) > max_stuck_s))
             if not (d.status in ST.CLAIMABLE or stuck):
@@ -1274,13 +1285,15 @@ class ElasticsearchStore(JobStore):
         claimable / stuck jobs of its shard: see the class docstring."""
         now = time.time() if now is None else now
         s = self._sessions.get(worker)
+        fresh = s is None
         if s is None:
             s = self._sessions[worker] = _ESSession()
         self._feed(s, worker, shard)
         room = limit - len(s.held)
         beat_due = now - s.last_beat >= max_stuck_s / 6
         if room > 0:
-            for d, seq, term in self._claim_hits(worker, room, max_stuck_s, now, shard=shard, beat=beat_due):
+            for d, seq, term in self._claim_hits(worker, room, max_stuck_s, now, shard=shard, beat=beat_due,
+                                                 adopt=fresh):
                 s.add(d.id, seq, term, d)
             if beat_due:
                 s.last_beat = now

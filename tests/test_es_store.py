@@ -251,3 +251,13 @@ def test_es_steady_state_cycle_is_constant_requests_at_10k():
         counts.append(len(es.requests))
     assert max(counts) <= 5, counts                   # feed + lease probe + claim probe (+ a beat)
     assert all(m != "PUT" or p.startswith("/leases") for m, p, _ in es.requests)
+
+
+def test_es_restarted_worker_adopts_its_held_jobs():
+    es, st = _store()
+    for i in range(5):
+        st.put(Document(id=f"j{i}", app_name=f"a{i}", status=ST.INITIAL))
+    assert len(st.claim_batch("w", 10, 90.0, now=1_760_000_000.0).ids) == 5
+    st2 = ElasticsearchStore("http://es:9200", client=st.http)        # a new process
+    assert st2.claim_batch("other", 10, 90.0, now=1_760_000_005.0).ids == []
+    assert sorted(st2.claim_batch("w", 10, 90.0, now=1_760_000_005.0).ids) == [f"j{i}" for i in range(5)]

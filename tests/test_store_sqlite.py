@@ -206,3 +206,17 @@ def test_hpalog_batches_are_columnar_and_read_back_per_job(tmp_path):
     st.add_hpalogs([HPALogBatch([ids[0]], T0 + 60 * 30 + 7200, "c", [1], [0], ["hold"], ["cpu", "mem"],
                                 [[1.0, 2.0]], [[1.0, 2.0]], [[1.0, 2.0]])])
     assert st._conn().execute("select count(*) from hpalog_batches").fetchone()[0] == 1
+
+
+def test_restarted_worker_adopts_its_held_jobs(tmp_path):
+    """A brain restarted under the same worker id (a StatefulSet pod, the
+    warm-restart path) takes back the jobs it holds at once -- it does not
+    wait MAX_STUCK_IN_SECONDS for its own lease to lapse; other workers still
+    cannot take them."""
+    path = str(tmp_path / "j.db")
+    st = SQLiteStore(path)
+    st.put_many(_docs(20))
+    assert len(st.claim_batch("w", 100, 90.0, now=T0)) == 20
+    assert len(SQLiteStore(path).claim_batch("other", 100, 90.0, now=T0 + 5)) == 0
+    st2 = SQLiteStore(path)                           # a new process, same worker id
+    assert len(st2.claim_batch("w", 100, 90.0, now=T0 + 5)) == 20
