@@ -155,11 +155,13 @@ def main() -> None:
     ap.add_argument("--rccl-self", action="store_true",
                     help="one GPU only: publish through a world-1 RCCL group (real all_gather_into_tensor host path "
                          "and kernel) to rehearse the multi-rank publish cost on a 1-GPU box")
-    ap.add_argument("--publish", choices=["auto", "eager", "graph"], default="auto",
+    ap.add_argument("--publish", choices=["auto", "eager", "graph", "peer"], default="auto",
                     help="verdict publish of a step (decision + all-gather + host copy on the comm stream): eager "
                          "calls, or one HIP graph per slot with the RCCL all-gather captured in it (1,250-service "
-                         "shard with a real RCCL group: 0.120 -> 0.101 ms/step).  auto = graph on one rank, eager "
-                         "with several ranks (captured multi-rank collectives are not yet measured on a node)")
+                         "shard with a real RCCL group: 0.120 -> 0.101 ms/step), or peer: every rank writes its "
+                         "verdict rows straight into rank 0's memory over xGMI (HIP IPC, parallel/peer.py; no "
+                         "collective per step).  auto = graph on one rank; with several ranks peer if its "
+                         "start-up self-test against the all-gather passes, else eager")
     ap.add_argument("--warmup-min-ms", type=float, default=300.0,
                     help="after the --warmup steps, keep stepping (untimed) until this much warm-up wall time has "
                          "passed, so the timed steps start at steady-state clocks (all ranks run the same count)")
@@ -242,6 +244,20 @@ def main() -> None:
     ev1 = [torch.cuda.Event() for _ in range(depth)]
 
     pub_graphs: list = []
+    peer = None
+    step_no = [0]
+    if args.publish in ("auto", "peer") and world > 1:
+        from foremast_amd.parallel.peer import PeerPublisher, selftest
+        try:
+            peer = PeerPublisher(info.rank, world, depth, s_pad, dev)
+            if not selftest(peer):
+                raise RuntimeError("peer publish self-test mismatch")
+            args.publish = "peer"
+        except Exception as e:  # noqa: BLE001 - the eager all-gather is the fallback
+            if args.publish == "peer":
+                raise
+            print(f"bench.py: peer publish unavailable ({e}); eager all-gather", file=sys.stderr)
+            peer = None
 
     def publish_body(slot: int) -> None:
         if split:
@@ -256,7 +272,17 @@ def main() -> None:
         the slot's captured graph: one launch instead of three host calls)."""
         comm.wait_event(ev_tick[slot])
         with torch.cuda.stream(comm):
-            if pub_graphs:
+            if peer is not None:
+                if split:
+                    decides[slot]()
+                # the publisher's ring follows its own step counter (the bench
+                # slot only picks this step's packed / host buffers)
+                k = step_no[0]
+                step_no[0] += 1
+                peer.publish(k % depth, k, packed[slot])
+                if info.is_main:
+                    peer.collect(k % depth, k, hosts[slot], S)
+            elif pub_graphs:
                 pub_graphs[slot].replay()
             else:
                 publish_body(slot)
@@ -334,6 +360,8 @@ def main() -> None:
         t_b.synchronize()
         lat.append(t_a.elapsed_time(t_b))
     p50 = D.all_reduce_max(statistics.median(lat) / 1e3, dev)
+    if peer is not None:
+        peer.check()
     n_dev, backend = _device_census(info, dev)
     ms = elapsed / args.steps * 1e3
     windows = S * M

@@ -1,0 +1,135 @@
+// Peer publish of the per-step fleet verdict:
+// every rank's decision rows land straight in rank 0's device buffer over
+// xGMI, no collective and no host call on the critical path.
+//
+// * rank 0 exports a [depth][world * shard][4] fleet buffer and a
+//   [depth][world] arrival-flag array through HIP IPC handles; every other
+//   rank exports a [depth] ack array the other way round;
+// * a rank publishes step k (slot k % depth) with ONE kernel: its shard's
+//   rows are copied into rank 0's buffer (vector stores through the peer
+//   mapping), then, after a system-scope release fence, its flag for the
+//   slot is set to k + 1;
+// * rank 0's comm stream waits (one wave polling the flags with acquire
+//   loads, bounded by a clock budget) until every rank's flag reached k + 1,
+//   copies the fleet verdict to pinned host memory, and acks slot k to every
+//   rank; a rank waits for that ack before it reuses the slot (k + depth).
+//
+// The waits are bounded: a wave that sees no progress for `budget` cycles
+// gives up, records it in a status word and exits, so a rank that died never
+// leaves a kernel spinning on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "fm_common.h"
+
+namespace {
+
+__device__ inline void store_release_sys(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ inline unsigned load_acquire_sys(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Copy n4 float4 rows src -> dst, then publish `value` to *flag.  Blocks
+// count their arrival on `arrive` (device-local); the last one fences and
+// sets the flag, then re-arms the counter.
+__global__ void __launch_bounds__(256) peer_publish_kernel(const float4* __restrict__ src, float4* dst, int64_t n4,
+                                                           unsigned* flag, unsigned value, unsigned* arrive) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1 == gridDim.x) {
+      __threadfence_system();
+      store_release_sys(flag, value);
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// One wave: lane r < n waits until flags[r * stride] >= value.  status[0]
+// gets 1 if the budget ran out (the caller checks it after the run).
+__global__ void __launch_bounds__(64) peer_wait_kernel(const unsigned* flags, int n, int64_t stride, unsigned value,
+                                                       long long budget, unsigned* status) {
+  const int r = threadIdx.x;
+  bool done = r >= n;
+  const long long t0 = clock64();
+  long long spins = 0;
+  while (true) {
+    if (!done) done = (int)(load_acquire_sys(flags + (int64_t)r * stride) - value) >= 0;
+    // every lane leaves together: the wave exits once all flags arrived or
+    // the budget is spent (no lane can keep the wave alive forever)
+    const bool all = __all(done);
+    if (all) break;
+    if (clock64() - t0 > budget) {
+      if (!done) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    ++spins;
+  }
+  (void)spins;
+}
+
+// Release `value` to n remote words (rank 0 -> every rank's ack for a slot).
+__global__ void peer_ack_kernel(unsigned* const* dst, int n, unsigned value) {
+  const int r = threadIdx.x;
+  __threadfence_system();
+  if (r < n && dst[r] != nullptr) store_release_sys(dst[r], value);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- IPC handles
+FM_API int fm_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+FM_API int fm_ipc_get_handle(void* ptr, void* out) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, ptr);
+  if (e != hipSuccess) return (int)e;
+  std::memcpy(out, &h, sizeof(h));
+  return 0;
+}
+
+FM_API int fm_ipc_open(const void* handle, void** out) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+FM_API int fm_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// ---------------------------------------------------------------- kernels
+// src / dst 16-byte aligned, bytes a multiple of 16.
+FM_API int fm_peer_publish(const void* src, void* dst, int64_t bytes, unsigned* flag, unsigned value,
+                           unsigned* arrive, hipStream_t stream) {
+  if (bytes < 0 || bytes % 16 != 0 || ((uintptr_t)src | (uintptr_t)dst) % 16 != 0) return (int)hipErrorInvalidValue;
+  const int64_t n4 = bytes / 16;
+  int blocks = (int)((n4 + 256 * 8 - 1) / (256 * 8));
+  blocks = blocks < 1 ? 1 : (blocks > 64 ? 64 : blocks);
+  hipLaunchKernelGGL(peer_publish_kernel, dim3(blocks), dim3(256), 0, stream, (const float4*)src, (float4*)dst, n4,
+                     flag, value, arrive);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+FM_API int fm_peer_wait(const unsigned* flags, int n, int64_t stride, unsigned value, long long budget_cycles,
+                        unsigned* status, hipStream_t stream) {
+  if (n < 0 || n > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_wait_kernel, dim3(1), dim3(64), 0, stream, flags, n, stride, value, budget_cycles, status);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+FM_API int fm_peer_ack(unsigned* const* dst, int n, unsigned value, hipStream_t stream) {
+  if (n < 0 || n > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_ack_kernel, dim3(1), dim3(64), 0, stream, dst, n, value);
+  FM_LAUNCH_CHECK();
+  return 0;
+}

@@ -45,6 +45,13 @@ _SIGS: dict[str, list] = {
                   c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fm_hw_scan_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int] + [c_void_p] * 10,
     "fm_hw_scan_supported": [c_int, c_int, c_int],
+    "fm_ipc_handle_size": [],
+    "fm_ipc_get_handle": [c_void_p, c_void_p],
+    "fm_ipc_open": [c_void_p, c_void_p],
+    "fm_ipc_close": [c_void_p],
+    "fm_peer_publish": [c_void_p, c_void_p, c_i64, c_void_p, ctypes.c_uint, c_void_p, c_void_p],
+    "fm_peer_wait": [c_void_p, c_int, c_i64, ctypes.c_uint, ctypes.c_longlong, c_void_p, c_void_p],
+    "fm_peer_ack": [c_void_p, c_int, ctypes.c_uint, c_void_p],
     "fm_es_update": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fm_band_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p, c_i64, c_int, c_void_p, c_void_p,
