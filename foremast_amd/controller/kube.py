@@ -199,23 +199,36 @@ class KubeAPI(ABC):
         """Roll a Deployment back to ``to_revision``: what the extensions/v1beta1
         DeploymentRollback subresource did (MonitorController.go:225-237) and
         ``kubectl rollout undo`` does today — copy that revision's ReplicaSet
-        pod template into the Deployment."""
+        pod template into the Deployment.  The write goes through
+        :meth:`update_retry`: a concurrent change of the Deployment (the
+        deployment controller bumping status / annotations) re-reads it and
+        re-applies the template instead of failing the remediation."""
         depl = self.get(DEPLOYMENTS, namespace, name)
         uid = depl["metadata"].get("uid")
+        tmpl = None
         for rs in self.list(REPLICASETS, namespace):
             owners = rs["metadata"].get("ownerReferences") or []
             if owners and owners[0].get("uid") == uid and revision(rs) == to_revision:
                 tmpl = copy.deepcopy(rs["spec"]["template"])
                 (tmpl.get("metadata", {}).get("labels") or {}).pop("pod-template-hash", None)
-                depl["spec"]["template"] = tmpl
-                ann = depl["metadata"].setdefault("annotations", {})
-                ann.update(annotations or {})
-                ann["deprecated.deployment.rollback.to"] = str(to_revision)
-                return self._write_rollback(namespace, depl, to_revision)
-        raise NotFound(f"revision {to_revision} of deployment {namespace}/{name}")
+                break
+        if tmpl is None:
+            raise NotFound(f"revision {to_revision} of deployment {namespace}/{name}")
 
-    def _write_rollback(self, namespace: str, depl: dict, to_revision: int) -> dict:
-        return self.update(DEPLOYMENTS, namespace, depl)
+        def mut(d: dict) -> dict:
+            if (d["metadata"].get("uid") or uid) != uid:
+                raise NotFound(f"deployment {namespace}/{name} was replaced")
+            d["spec"]["template"] = copy.deepcopy(tmpl)
+            ann = d["metadata"].setdefault("annotations", {})
+            ann.update(annotations or {})
+            ann["deprecated.deployment.rollback.to"] = str(to_revision)
+            return self._rollback_object(d, to_revision)
+        return self.update_retry(DEPLOYMENTS, namespace, name, mut)
+
+    def _rollback_object(self, depl: dict, to_revision: int) -> dict:
+        """Hook: the Deployment as written by a rollback (FakeKube adds what the
+        deployment controller would do next)."""
+        return depl
 
     def event(self, namespace: str, involved: dict, etype: str, reason: str, message: str, component: str) -> None:
         ev = {"metadata": {"generateName": involved["metadata"]["name"] + ".", "namespace": namespace},
@@ -335,14 +348,15 @@ class FakeKube(KubeAPI):
         for o in existing:
             handler("ADDED", None, o)
 
-    def _write_rollback(self, namespace, depl, to_revision):
+    def _rollback_object(self, depl, to_revision):
         """As the API server, plus what the real deployment controller does
         next: the Deployment's revision becomes that of the restored template
         (written in the same update, so watchers see one consistent event)."""
         with self._lock:
-            self.actions.append(("rollback", DEPLOYMENTS, namespace, depl["metadata"]["name"]))
+            self.actions.append(("rollback", DEPLOYMENTS, depl["metadata"].get("namespace", ""),
+                                 depl["metadata"]["name"]))
         depl["metadata"].setdefault("annotations", {})[REVISION_ANNOTATION] = str(to_revision)
-        return self.update(DEPLOYMENTS, namespace, depl)
+        return depl
 
     def verbs(self, resource: str | None = None) -> list[tuple]:
         return [a for a in self.actions if resource is None or a[1] == resource]

@@ -18,7 +18,10 @@ text{font-size:10px;fill:#555}
 <h1>Foremast &mdash; <span id="title"></span></h1>
 <div class="grid" id="grid"></div>
 <script>
-const NS = "__NS__", APP = "__APP__";
+const NS = __NS_JS__, APP = __APP_JS__;
+// every label-derived string (chart titles, units, kube_pod_labels versions)
+// is text, never markup
+const esc = v => String(v).replace(/[&<>"']/g, ch => ({"&": "&amp;", "<": "&lt;", ">": "&gt;", '"': "&quot;", "'": "&#39;"}[ch]));
 function scaleFn(d0, d1, r0, r1) { const k = (d1 - d0) || 1; return v => r0 + (v - d0) * (r1 - r0) / k; }
 function chart(c, t0, t1, ann) {
   const W = 600, H = 220, P = 30, s = c.series;
@@ -26,15 +29,15 @@ function chart(c, t0, t1, ann) {
   const lo = Math.min(0, ...all), hi = Math.max(1e-9, ...all);
   const x = scaleFn(t0, t1, P, W - 5), y = scaleFn(lo, hi, H - P, 5);
   let g = `<line class="axis" x1="${P}" y1="${H-P}" x2="${W-5}" y2="${H-P}"/>`;
-  g += `<text x="2" y="12">${hi.toPrecision(3)} ${c.unit}</text><text x="2" y="${H-P}">${lo.toPrecision(3)}</text>`;
+  g += `<text x="2" y="12">${hi.toPrecision(3)} ${esc(c.unit)}</text><text x="2" y="${H-P}">${lo.toPrecision(3)}</text>`;
   if (s.upper.length && s.lower.length) {
     const up = s.upper.map(p => `${x(p[0])},${y(p[1])}`), dn = s.lower.slice().reverse().map(p => `${x(p[0])},${y(p[1])}`);
     g += `<polygon class="band" points="${up.concat(dn).join(" ")}"/>`;
   }
   if (s.base.length) g += `<polyline class="base" points="${s.base.map(p => `${x(p[0])},${y(p[1])}`).join(" ")}"/>`;
   for (const p of s.anomaly) g += `<circle class="anom" cx="${x(p[0])}" cy="${y(p[1])}" r="3.5"/>`;
-  for (const a of ann) if (a.time >= t0) g += `<line class="ann" x1="${x(a.time)}" y1="5" x2="${x(a.time)}" y2="${H-P}"/><text x="${x(a.time)+2}" y="14">${a.version}</text>`;
-  return `<div class="card"><h2>${c.title}</h2><svg viewBox="0 0 ${W} ${H}">${g}</svg></div>`;
+  for (const a of ann) if (a.time >= t0) g += `<line class="ann" x1="${x(a.time)}" y1="5" x2="${x(a.time)}" y2="${H-P}"/><text x="${x(a.time)+2}" y="14">${esc(a.version)}</text>`;
+  return `<div class="card"><h2>${esc(c.title)}</h2><svg viewBox="0 0 ${W} ${H}">${g}</svg></div>`;
 }
 function scatter(pts) {
   const W = 600, H = 220, P = 30;
@@ -55,6 +58,13 @@ refresh(); setInterval(refresh, 15000);
 """
 
 
+def _js(v: str) -> str:
+    """A JavaScript string literal safe inside <script> (no ``</script>`` break-out)."""
+    import json
+    return json.dumps(v).replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+
+
 def render(namespace: str, app: str) -> str:
     import html
-    return PAGE.replace("__NS__", html.escape(namespace, quote=True)).replace("__APP__", html.escape(app, quote=True))
+    return (PAGE.replace("__NS_JS__", _js(namespace)).replace("__APP_JS__", _js(app))
+            .replace("__APP__", html.escape(app, quote=True)))

@@ -55,3 +55,18 @@ def test_service_dashboard_routes():
     assert len(d["charts"]) == 4 and d["annotations"][1]["version"] == "v2"
     page = c.get('/dashboard/prod/de"mo').text
     assert 'de&quot;mo' in page and "/dashboard/api/" in page
+
+
+def test_page_never_inlines_label_text_as_markup():
+    """chart titles, units and kube_pod_labels versions come
+    from label values -- the page builds them through esc(), and the app /
+    namespace are JS string literals that cannot close the <script> block."""
+    import re
+    from foremast_amd.dashboard.page import PAGE, render
+    for field in ("c.title", "c.unit", "a.version"):
+        assert f"esc({field})" in PAGE
+        assert re.search(r"\$\{" + re.escape(field) + r"\}", PAGE) is None
+    h = render("ns", "</script><img src=x onerror=alert(1)>")
+    script = h[h.index("<script>"):]
+    assert "</script><img" not in script and "\\u003c/script\\u003e" in script
+    assert "<img src=x" not in h

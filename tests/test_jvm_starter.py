@@ -51,3 +51,13 @@ def test_autoconfiguration_registered():
                "org.springframework.boot.autoconfigure.AutoConfiguration.imports").read_text().split()
     for cls in imports:
         assert (SRC / (cls.rsplit(".", 1)[1] + ".java")).exists(), cls
+
+
+def test_endpoint_keeps_the_reference_get_toggle():
+    """the reference's K8sMetricsEndpoint toggles through a
+    @ReadOperation (GET); ours offers GET and POST on the same selectors."""
+    import pathlib
+    src = next(pathlib.Path(__file__).resolve().parents[1].joinpath("jvm").rglob("K8sMetricsEndpoint.java")).read_text()
+    assert "@ReadOperation" in src and "@WriteOperation" in src
+    read = src[src.index("@ReadOperation"):]
+    assert "@Selector String action, @Selector String metric" in read.split("}")[0]

@@ -203,3 +203,36 @@ def test_update_retry_rereads_on_conflict():
     kube2.create(K.MONITORS, "default", {"metadata": {"name": "demo", "namespace": "default"}, "spec": {}})
     with pytest.raises(K.Conflict):
         kube2.update_retry(K.MONITORS, "default", "demo", lambda o: o, attempts=3, backoff=0.0)
+
+
+def test_rollback_survives_a_concurrent_deployment_write(api):
+    """the rollback PUT goes through update_retry -- a
+    Deployment bumped between our GET and PUT (409) is re-read and the
+    revision's template re-applied, not a failed remediation."""
+    srv, hk = api
+    d = hk.create(K.DEPLOYMENTS, "default", {
+        "metadata": {"name": "demo", "namespace": "default", "annotations": {K.REVISION_ANNOTATION: "2"}},
+        "spec": {"template": {"metadata": {"labels": {"app": "demo"}},
+                              "spec": {"containers": [{"name": "c", "image": "demo:v2"}]}}}})
+    hk.create(K.REPLICASETS, "default", {
+        "metadata": {"name": "demo-h1", "namespace": "default", "annotations": {K.REVISION_ANNOTATION: "1"},
+                     "ownerReferences": [{"uid": d["metadata"]["uid"]}]},
+        "spec": {"template": {"metadata": {"labels": {"app": "demo", "pod-template-hash": "h1"}},
+                              "spec": {"containers": [{"name": "c", "image": "demo:v1"}]}}}})
+    orig = srv.kube.update
+    raced = []
+
+    def racy_update(res, ns, obj):
+        if res == K.DEPLOYMENTS and not raced:
+            raced.append(1)
+            cur = srv.kube.get(res, ns, obj["metadata"]["name"])
+            cur.setdefault("status", {})["observedGeneration"] = 5
+            orig(res, ns, cur)                              # someone else wrote first
+        return orig(res, ns, obj)
+    srv.kube.update = racy_update
+    hk.rollback("default", "demo", 1)
+    got = hk.get(K.DEPLOYMENTS, "default", "demo")
+    assert raced and got["spec"]["template"]["spec"]["containers"][0]["image"] == "demo:v1"
+    assert got["status"]["observedGeneration"] == 5
+    puts = [r for r in srv.requests if r[0] == "PUT" and "deployments" in r[1]]
+    assert len(puts) == 2                                   # the 409, then the re-read write
