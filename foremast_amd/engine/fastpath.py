@@ -209,7 +209,10 @@ class LazyHist:
         from ..ops import misc as MI
         lo = max(0, min(int(lo), self.T))
         if self._buf is None:
-            self._buf = torch.empty((self.shape[0], max(1, self.T)), dtype=torch.float32, device=self.device)
+            # rows padded to a multiple of 4 columns: the scoring kernels take
+            # 16-B aligned rows whatever the logical length T
+            w = max(4, (self.T + 3) // 4 * 4)
+            self._buf = torch.empty((self.shape[0], w), dtype=torch.float32, device=self.device)[:, :max(1, self.T)]
             self._lo = self.T
         if lo < self._lo:
             MI.gather_cols(self.src, self.rm, (lo - self.shift).to(torch.int32), self.lim, self._lo - lo,
@@ -227,7 +230,8 @@ class LazyHist:
         from ..ops import misc as MI
         assert dim == 0
         idx = idx.to(self.rm.device).long()
-        out = torch.empty((int(idx.numel()), max(1, self.T)), dtype=torch.float32, device=self.device)
+        w = max(4, (self.T + 3) // 4 * 4)
+        out = torch.empty((int(idx.numel()), w), dtype=torch.float32, device=self.device)[:, :max(1, self.T)]
         MI.gather_cols(self.src, self.rm.index_select(0, idx), (-self.shift.index_select(0, idx)).to(torch.int32),
                        self.lim.index_select(0, idx), self.T, out)
         return out

@@ -254,7 +254,7 @@ class ModelCache:
                 self._drop_slot(slab, int(sl[j]))
         if len(miss):
             idx = torch.as_tensor(miss, device=dev)
-            sub = hist.index_select(0, idx).contiguous()
+            sub = hist.index_select(0, idx)       # rows stay 16-B aligned (LazyHist pads them)
             k_eff, m = kind, 1
             if kind >= 2:
                 m = int(period_for(sub))

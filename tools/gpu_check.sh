@@ -21,7 +21,7 @@ e2e() { tag=$1; shift; echo "== e2e $tag" >&2
         return $rc; }
 for s in $steps; do
   case $s in
-    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread || exit $rc ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu --maxfail 8 -v --timeout 120 --timeout-method thread || exit $rc ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $rc ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 || exit $rc ;;
     e2e) rm -f gpurun_out/check_e2e.jsonl
