@@ -250,10 +250,16 @@ def main() -> None:
         from foremast_amd.parallel.peer import PeerPublisher, selftest
         try:
             peer = PeerPublisher(info.rank, world, depth, s_pad, dev)
-            if not selftest(peer):
-                raise RuntimeError("peer publish self-test mismatch")
+            rep: dict = {}
+            if not selftest(peer, report=rep):
+                raise RuntimeError(f"peer publish self-test failed {rep}")
             args.publish = "peer"
         except Exception as e:  # noqa: BLE001 - the eager all-gather is the fallback
+            if peer is not None:
+                try:
+                    peer.close()
+                except Exception:  # noqa: BLE001
+                    pass
             if args.publish == "peer":
                 raise
             print(f"bench.py: peer publish unavailable ({e}); eager all-gather", file=sys.stderr)

@@ -32,6 +32,8 @@ fails is closed ``completed_unknown`` with the error as reason.
 """
 from __future__ import annotations
 
+import functools
+
 import html
 import json
 import logging
@@ -240,6 +242,17 @@ class LazyHist:
         return self.materialize(0)
 
 
+_NOSPEC = object()
+
+
+@functools.lru_cache(maxsize=65536)
+def _parse_config_cached(config: str) -> dict:
+    """api/urls.parse_config, memoised (read-only result): a job's config
+    strings are parsed by intake and again by planning, and the store /
+    history strings repeat across a fleet."""
+    return parse_config(config)
+
+
 def _label(q: str, name: str) -> str:
     import re
     m = re.search(r'(?<![\w])' + name + r'\s*=\s*"([^"]*)"', q or "")
@@ -399,15 +412,17 @@ class FastPath:
         self.wt = WindowTable(cfg.metric_settle_s, cfg.fetch_batch, cfg.fetch_max_values)
         self._wt_changed = False
         self._hist_epoch = 0       # bumped whenever static history rows were written
+        self._specs: dict = {}     # url -> RangeSpec | None of the claim being prepared
+        self._algos: dict = {}     # alias tuple -> canonical algorithms
 
     # ------------------------------------------------------------------ planning
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
         cfg = self.b.cfg
-        cur = parse_config(doc.current_config)
-        base = parse_config(doc.baseline_config)
-        hist = parse_config(doc.historical_config)
-        cs, bs, hs = (parse_config(doc.current_metric_store), parse_config(doc.baseline_metric_store),
-                      parse_config(doc.historical_metric_store))
+        pc = _parse_config_cached
+        cur = pc(doc.current_config)
+        base = pc(doc.baseline_config)
+        hist = pc(doc.historical_config)
+        cs, bs, hs = (pc(doc.current_metric_store), pc(doc.baseline_metric_store), pc(doc.historical_metric_store))
         hpa = doc.strategy == "hpa"
         aliases = list(cur) if not hpa else (list(hist) or list(cur))
         if not aliases or len(aliases) > MAX_M:
@@ -426,8 +441,16 @@ class FastPath:
         ns = doc.namespace
         cluster = ""
         bms = []
+        specs = self._specs
         for a in aliases:
             url = cur.get(a) or hist.get(a, "")
+            sp = specs.get(url)
+            if sp is not None:
+                # batched intake parse (fast shape: namespace + pod / app only)
+                bms.append((sp.metric or a).replace("namespace_pod_", "namespace_app_pod_", 1))
+                if not ns:
+                    ns = sp.matchers[0][2]
+                continue
             q = prometheus_query_of(url).get("query", "") if "query_range?" in url else url
             bms.append((promql_metric_name(q) or a).replace("namespace_pod_", "namespace_app_pod_", 1))
             if not ns:
@@ -435,7 +458,10 @@ class FastPath:
             if not cluster:
                 cluster = _label(q, "cluster")
         keys = [((hs.get(a, "prometheus")), hu[i]) if sliding else (doc.id, a) for i, a in enumerate(aliases)]
-        algos = tuple(self._canon(cfg.algorithm_for(a)) for a in aliases)
+        ak = tuple(aliases)
+        algos = self._algos.get(ak)
+        if algos is None:
+            algos = self._algos[ak] = tuple(self._canon(cfg.algorithm_for(a)) for a in aliases)
         gsig = (tuple(aliases), hpa, sliding,
                 None if tmpl is None else (tuple(tmpl.priority), tuple(tmpl.is_increase), tuple(tmpl.is_absolute)),
                 algos)
@@ -444,6 +470,26 @@ class FastPath:
                        [base.get(a, "") for a in aliases], [bs.get(a, "prometheus") for a in aliases], hu,
                        [hs.get(a, "prometheus") for a in aliases], sliding, keys, bms, ns or doc.namespace,
                        doc.app_name, hpa, tmpl, gsig, cluster=cluster, algos=algos)
+
+    def _prefill_specs(self, docs) -> None:
+        """Parse every current / baseline URL of a claim's new jobs in one
+        native call (engine/ingest.py parse_ranges): what planning and the
+        window table read per URL."""
+        from .ingest import parse_ranges
+        if len(docs) < 16:
+            self._specs = {}
+            return
+        urls = []
+        for d in docs:
+            urls.extend(_parse_config_cached(d.current_config).values())
+            urls.extend(_parse_config_cached(d.baseline_config).values())
+        urls = list(dict.fromkeys(u for u in urls if u))
+        self._specs = dict(zip(urls, parse_ranges(urls)))
+
+    def _spec_of(self, url: str):
+        from .ingest import parse_range
+        sp = self._specs.get(url, _NOSPEC)
+        return parse_range(url) if sp is _NOSPEC else sp
 
     @staticmethod
     def _canon(a: str) -> str:
@@ -486,7 +532,9 @@ class FastPath:
         rest = []
         reg: list[FastWork] = []
         if unknown:
-            for k, d in zip(unknown, batch.docs(unknown)):
+            docs = batch.docs(unknown)
+            self._prefill_specs(docs)
+            for k, d in zip(unknown, docs):
                 old = works.pop(d.id, None)
                 if old is not None:              # resubmitted under the same id
                     self._gcount_add(old.plan.group, -1)
@@ -510,6 +558,7 @@ class FastPath:
                 todo.append(fw)
         if reg:
             self._register_windows(reg)
+        self._specs = {}
         self.todo = todo
         self._last = (batch.ids, batch.versions, fast, todo) if not rest else None
         return fast, rest
@@ -558,7 +607,6 @@ class FastPath:
         import os
         if os.environ.get("FM_NO_TABLE"):
             return
-        from .ingest import parse_range
         router = self.b.sources
         keyed: dict[str, bool] = {}
         live_of: dict[str, bool] = {}
@@ -575,7 +623,7 @@ class FastPath:
                     if st not in keyed:
                         keyed[st] = router.keyed_source(st) is not None
                         live_of[st] = router.live(st) if keyed[st] else False
-                    spec = parse_range(u) if keyed[st] else None
+                    spec = self._spec_of(u) if keyed[st] else None
                     if spec is None:
                         ok = False
                         break

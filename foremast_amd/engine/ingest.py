@@ -161,6 +161,46 @@ def parse_range(url: str, keys=KEY_LABELS, windowed: bool = True) -> RangeSpec |
     return RangeSpec(base, metric, mt, k, tuple(values), start, end, step, extra)
 
 
+_KEYS_BY_ID = ("pod", "app")
+
+
+def parse_ranges(urls, keys=KEY_LABELS) -> list[RangeSpec | None]:
+    """:func:`parse_range` (windowed) of many URLs: the fast shape natively
+    (csrc/runtime/urlparse.cpp, one call), the rest through the general
+    parser.  The values tuple of a pod union is shared by every URL that
+    carries the same union (a job's M metrics)."""
+    from . import native_rt
+    urls = list(urls)
+    got = native_rt.parse_ranges(urls) if urls else None
+    if got is None:
+        return [parse_range(u, keys) for u in urls]
+    f, dec = got
+    out: list[RangeSpec | None] = []
+    vcache: dict = {}
+    mcache: dict = {}
+    fl = f.tolist()
+    sel = np.ascontiguousarray(f[:, 11:14]).view(np.float64).tolist()
+    for u, r, se in zip(urls, fl, sel):
+        if not r[0]:
+            out.append(parse_range(u, keys))
+            continue
+        key = _KEYS_BY_ID[r[7]]
+        if key not in keys:
+            out.append(None if key not in KEY_LABELS else parse_range(u, keys))
+            continue
+        raw = dec[r[9]:r[10]]
+        vals = vcache.get((raw, r[8]))
+        if vals is None:
+            vals = (raw,) if r[8] == 0 else tuple(raw.split("|"))
+            vcache[(raw, r[8])] = vals
+        ns = dec[r[5]:r[6]]
+        mt = mcache.get((ns, key))
+        if mt is None:
+            mt = mcache[(ns, key)] = (("namespace", "=", ns), (key, "", ""))
+        out.append(RangeSpec(u[:r[2]], dec[r[3]:r[4]], mt, key, vals, se[0], se[1], se[2], ()))
+    return out
+
+
 def render_query(group: tuple, values, alt: str | None = None) -> str:
     """The PromQL text of a batched selector: the group's matchers with the key
     matcher as ``key="v"`` (one value) or ``key=~"v1|v2"`` (escaped literals;
@@ -346,8 +386,22 @@ class WindowTable:
         k = len(specs)
         if k == 0:
             return np.zeros(0, np.int64)
-        vals = [sorted(set(sp.values)) for sp in specs]
-        nsl = np.fromiter(map(len, vals), np.int64, k)
+        # key-value lists by union: a job's M windows share one pod union
+        # (one tuple object from parse_ranges): sort, hash and escape it once
+        uid: dict = {}
+        uvals: list = []
+        wu = np.empty(k, np.int64)
+        for i, sp in enumerate(specs):
+            key = id(sp.values)
+            u = uid.get(key)
+            if u is None:
+                u = uid[key] = len(uvals)
+                uvals.append(sorted(set(sp.values)))
+            wu[i] = u
+        ulen = np.fromiter(map(len, uvals), np.int64, len(uvals))
+        uoff = np.zeros(len(uvals) + 1, np.int64)
+        np.cumsum(ulen, out=uoff[1:])
+        nsl = ulen[wu]
         start = np.fromiter((sp.start for sp in specs), np.float64, k)
         end = np.fromiter((sp.end for sp in specs), np.float64, k)
         step = np.fromiter((sp.step for sp in specs), np.float64, k)
@@ -383,25 +437,30 @@ class WindowTable:
             tot = int(nsl[fi].sum())
             base = self._alloc_slots(tot) if tot else self.ns
             slot0[fi] = base + np.concatenate([[0], np.cumsum(nsl[fi])[:-1]])
-        flat = [v for vs in vals for v in vs]
+        uh = native_rt.fnv1a([v for vs in uvals for v in vs])
         sl = _ranges(slot0, nsl)
         self.V[sl] = np.nan
-        self.khash[sl] = native_rt.fnv1a(flat)
+        self.khash[sl] = uh[_ranges(uoff[wu], nsl)]
         self.kwin[sl] = np.repeat(wids, nsl)
         groups = self.groups
         gid = np.empty(k, np.int64)
-        # every window's regex fragment from ONE escape pass over all values
-        frags = promql.re_literal("\x00".join("\x01".join(vs) for vs in vals)).replace("\x01", "|").split("\x00")
-        for i, (sp, st) in enumerate(zip(specs, stores)):
-            gk = (sp.group, st)
-            g = groups.get(gk)
+        # every union's regex fragment from ONE escape pass over all values
+        frags = promql.re_literal("\x00".join("\x01".join(vs) for vs in uvals)).replace("\x01", "|").split("\x00")
+        gcache: dict = {}
+        values, frag = self.values, self.frag
+        for i, (sp, st, w, u) in enumerate(zip(specs, stores, wids.tolist(), wu.tolist())):
+            gk0 = (id(sp.matchers), sp.metric, sp.base, sp.step, sp.extra, st)
+            g = gcache.get(gk0)
             if g is None:
-                g = groups[gk] = len(self.group_keys)
-                self.group_keys.append(gk)
+                gk = (sp.group, st)
+                g = groups.get(gk)
+                if g is None:
+                    g = groups[gk] = len(self.group_keys)
+                    self.group_keys.append(gk)
+                gcache[gk0] = g
             gid[i] = g
-            w = int(wids[i])
-            self.values[w] = vals[i]
-            self.frag[w] = frags[i]
+            values[w] = uvals[u]
+            frag[w] = frags[u]
         self.start[wids], self.end[wids], self.step[wids] = start, end, step
         self.settled[wids] = start - step
         self.gid[wids], self.slot0[wids], self.nslot[wids], self.ncol[wids] = gid, slot0, nsl, ncol

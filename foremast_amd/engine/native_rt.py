@@ -56,6 +56,9 @@ def _load():
     lib.fm_prom_format.argtypes = [c_i64, ctypes.c_char_p, c_vp, ctypes.c_double, ctypes.c_double, c_i64, c_vp,
                                    c_vp, c_i64]
     lib.fm_prom_format.restype = c_i64
+    if hasattr(lib, "fm_parse_ranges"):
+        lib.fm_parse_ranges.argtypes = [ctypes.c_char_p, c_vp, c_i64, ctypes.c_char_p, c_i64, c_vp]
+        lib.fm_parse_ranges.restype = c_i64
     _lib = lib
     return lib
 
@@ -226,6 +229,25 @@ def _joined(strs) -> tuple[bytes, np.ndarray]:
     off = np.zeros(len(enc) + 1, np.int64)
     np.cumsum(np.fromiter(map(len, enc), np.int64, len(enc)), out=off[1:])
     return b"".join(enc), off
+
+
+def parse_ranges(urls) -> tuple[np.ndarray, str] | None:
+    """Native batched parse of query_range URLs of the fast shape
+    (csrc/runtime/urlparse.cpp): ``(fields [n, 14] int64, decoded)`` where a
+    row with ``fields[i, 0] == 1`` gives the base end in the URL, then
+    metric / namespace / values spans in ``decoded`` (ASCII), key (0 pod,
+    1 app), op (0 ``=``, 1 ``=~``) and start / end / step as float64 bits.
+    None without the library."""
+    lib = _load()
+    if lib is None or not hasattr(lib, "fm_parse_ranges"):
+        return None
+    n = len(urls)
+    buf, off = _joined(urls)
+    out = ctypes.create_string_buffer(max(1, len(buf)))
+    f = np.zeros((n, 14), np.int64)
+    if n:
+        lib.fm_parse_ranges(buf, off.ctypes.data, n, out, len(buf), f.ctypes.data)
+    return f, out.raw[: int(f[:, 10].max()) if n else 0].decode("ascii")
 
 
 def hpalog_bodies(batch) -> list[str] | None:

@@ -223,6 +223,15 @@ def _detect_period(hist: torch.Tensor, T: int, default: int = 1440) -> int:
     return max(2, min(p, T // 2))
 
 
+def _aligned_rows(hist, idx, T: int) -> torch.Tensor:
+    """Rows ``idx`` of ``hist[:, :T]`` in a buffer whose rows stay 16-B
+    aligned (ld a multiple of 4 floats) for the vector-load kernels."""
+    w = max(4, (T + 3) // 4 * 4)
+    out = torch.empty((int(idx.numel()), w), dtype=torch.float32, device=hist.device)
+    out[:, :T] = hist[idx, :T]
+    return out[:, :T]
+
+
 def _bivariate(hist, T, cur, M, tables, pairs=None) -> RowDecision:
     """Metric pairs scored jointly; both rows of a pair get the pair's decision
     (bounds reported in Mahalanobis units: upper = threshold, lower = 0).
@@ -245,7 +254,7 @@ def _bivariate(hist, T, cur, M, tables, pairs=None) -> RowDecision:
     up_all = torch.full((R, n), float("nan"), device=device)
     lo_all = torch.full((R, n), float("nan"), device=device)
     if ia.numel():
-        ha, hb = hist[ia].contiguous(), hist[ib].contiguous()
+        ha, hb = _aligned_rows(hist, ia, T), _aligned_rows(hist, ib, T)
         ca, cb = cur[ia].contiguous(), cur[ib].contiguous()
         thr = float(tables.thr[0].item()) if tables.thr.numel() == 1 else float(tables.thr.max().item())
         params, dist, flags, cnt = MI.bivariate(ha, hb, T, ca, cb, thr)
@@ -257,7 +266,7 @@ def _bivariate(hist, T, cur, M, tables, pairs=None) -> RowDecision:
             up_all[i] = thr
             lo_all[i] = 0.0
     if singles.numel():
-        sub = C.stats_decide(hist[singles].contiguous(), cur[singles].contiguous(), T, 1,
+        sub = C.stats_decide(_aligned_rows(hist, singles, T), cur[singles].contiguous(), T, 1,
                              tables.thr[:1].contiguous(), tables.bound[:1].contiguous(), tables.minlb[:1].contiguous(),
                              None, tables.pair_factor, tables.min_hist)
         flags_all[singles], count_all[singles], score_all[singles] = sub.flags, sub.count, sub.score

@@ -32,7 +32,11 @@ import torch.distributed as dist
 
 from ..ops._lib import LIB, stream_of
 
-_BUDGET = 10_000_000_000          # wait budget in GPU clock cycles (~4 s at 2.4 GHz)
+import os
+
+# wait budget in GPU clock cycles (~1 s at 2.1 GHz): a publish waits for at
+# most one step of another rank, milliseconds
+_BUDGET = int(os.environ.get("FOREMAST_PEER_BUDGET", 2_000_000_000))
 
 
 def _store():
@@ -133,13 +137,14 @@ class PeerPublisher:
         self._opened = []
 
 
-def selftest(pub: PeerPublisher, steps: int = 8) -> bool:
+def selftest(pub: PeerPublisher, steps: int = 8, report: dict | None = None) -> bool:
     """Publish ``steps`` known patterns through the peer path and compare rank
     0's collected fleet with the process group's all-gather of the same
-    shards.  Every rank returns the same verdict."""
+    shards.  Every rank returns the same verdict; the first failing step ends
+    the test on every rank (``report`` gets the step and the status words)."""
     dev = pub.dev
-    ok = True
     host = torch.empty((pub.world * pub.shard, 4), dtype=torch.float32, pin_memory=True)
+    flag_dev = dev if dist.get_backend() == "nccl" else "cpu"
     for k in range(steps):
         slot = k % pub.depth
         x = (torch.arange(pub.shard * 4, device=dev, dtype=torch.float32).reshape(pub.shard, 4)
@@ -148,15 +153,18 @@ def selftest(pub: PeerPublisher, steps: int = 8) -> bool:
         xs = x if dist.get_backend() == "nccl" else x.cpu()
         ref = [torch.empty_like(xs) for _ in range(pub.world)]
         dist.all_gather(ref, xs)
+        ok = True
         if pub.rank == 0:
             pub.collect(slot, k, host, pub.world * pub.shard)
             torch.cuda.synchronize(dev)
-            ok = ok and torch.equal(host, torch.cat(ref).cpu())
+            ok = torch.equal(host, torch.cat(ref).cpu())
         torch.cuda.synchronize(dev)
-    try:
-        pub.check()
-    except RuntimeError:
-        ok = False
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    return bool(flag.item())
+        st = pub.status.cpu()
+        ok = ok and not bool(st[0]) and not bool(st[1])
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=flag_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not bool(flag.item()):
+            if report is not None:
+                report.update(step=k, status=st.tolist(), data_ok=ok)
+            return False
+    return True

@@ -232,3 +232,46 @@ def test_synthetic_keyed_answer_matches_fetch():
     for ser, part in zip(per, keyed_split(k, [x.labels["pod"] for x in per])):
         np.testing.assert_array_equal(ser.values, part[0][1])
         np.testing.assert_array_equal(ser.times, part[0][0])
+
+
+def test_native_batched_url_parse_equals_python_parse():
+    """csrc/runtime/urlparse.cpp (job intake) against parse_range on the
+    fast shape, escapes, and every shape the fast path must hand back."""
+    from foremast_amd.api.urls import go_query_escape
+    from foremast_amd.engine.ingest import parse_ranges
+
+    def url(q, start="1700000000", end="1700000600", step="60", base="http://prom:9090/api/v1/"):
+        return f"{base}query_range?query={go_query_escape(q)}&start={start}&end={end}&step={step}"
+
+    pods = "|".join(f"demo-7687b9f4d7-{i:05d}" for i in range(60))
+    qs = [
+        f'namespace_pod_cpu{{namespace="default",pod=~"{pods}"}}',
+        'namespace_pod_cpu{namespace="default",pod="one-pod"}',
+        'namespace_app_pod_x{namespace="ns",app="demo"}',
+        'namespace_app_pod_x{namespace="",app=~"a|b_c|d-e"}',
+        'm:rate5m{namespace="n",pod=~"a|b"}',
+        'm{namespace="n",pod=~"a.b|c"}',            # regex metacharacter: general path decides
+        'm{namespace="n",pod=~"a||b"}',              # empty alternative
+        'm{namespace="n",pod=~""}',                  # empty union
+        'm{namespace="n",pod=""}',
+        'm{namespace="n",pod="a|b"}',                # = keeps the literal
+        'm{namespace="n",job="x"}',                  # no key label
+        'm{pod="a",namespace="n"}',                  # other label order
+        'm{namespace="n\\"q",pod="a"}',              # escaped quote
+        'm{namespace="n",pod="ünï"}',                # non-ASCII
+        'rate(m{namespace="n",pod="a"}[5m])',        # not a plain selector
+        'm{namespace="n",pod="a b"}',                # space (+ in the URL)
+        'm{namespace="n",pod=~"a|b",cluster="c"}',   # extra matcher
+    ]
+    urls = [url(q) for q in qs]
+    urls += [url(qs[0], start="1700000000.5"), url(qs[1], step="15"), url(qs[1], step="1m"),
+             url(qs[1], start="START_TIME", end="END_TIME"), url(qs[1]) + "&x=1",
+             url(qs[1]).replace("&start=", "&end=1&start="), url(qs[1], base="http://h/query_range?a=b&"),
+             "http://h/api/v1/query?query=up", url(qs[1]).replace("%22", "%2"), url(qs[2], base="")]
+    got = parse_ranges(urls)
+    want = [parse_range(u) for u in urls]
+    assert got == want
+    assert sum(g is not None for g in got) >= 10
+    if native_rt.available():
+        f, _ = native_rt.parse_ranges(urls)
+        assert int(f[:, 0].sum()) >= 6           # the fast shapes went native

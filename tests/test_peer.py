@@ -21,13 +21,17 @@ def _port():
 
 def _worker(rank, world, port, q):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FOREMAST_PEER_BUDGET="400000000")
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         from foremast_amd.parallel.peer import PeerPublisher, selftest
         pub = PeerPublisher(rank, world, depth=2, shard=1250, device="cuda:0")
-        ok = selftest(pub, steps=24)
+        rep = {}
+        ok = selftest(pub, steps=24, report=rep)
+        if not ok:
+            q.put((rank, f"ERR selftest failed {rep}"))
+            return
         # steady stream of steps with no host sync in between (the bench's
         # pattern): rank 1 runs ahead until the ack of the slot stops it
         dev = torch.device("cuda", 0)
@@ -61,9 +65,14 @@ def test_peer_publish_two_processes_one_gpu():
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = dict(q.get(timeout=110) for _ in ps)
-    for p in ps:
-        p.join(30)
+    try:
+        out = dict(q.get(timeout=100) for _ in ps)
+    finally:
+        for p in ps:
+            p.join(20)
+            if p.is_alive():          # never leave a rank spinning on the GPU
+                p.kill()
+                p.join(10)
     for r, v in out.items():
         assert not (isinstance(v, str) and v.startswith("ERR")), v
     assert out[0][0] and out[1][0]

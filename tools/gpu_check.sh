@@ -31,11 +31,15 @@ for s in $steps; do
     e2ehttp) e2e c3e2e_http --config 3e2e --source http --steps 70 --warmup 3 --prom-workers 8 &&
          e2e c3e2e_http60 --config 3e2e --source http --poll-seconds 60 --window 60 --steps 12 --warmup 2 --prom-workers 8 &&
          e2e c2e2e_http --config 2e2e --source http --steps 20 --warmup 3 --prom-workers 8 || exit $rc ;;
+    peerprobe) run peer_probe 150 python -u tools/peer_probe.py || exit $rc ;;
     peer) run peer_test 200 python -u -m pytest tests/test_peer.py -x -v --timeout 150 --timeout-method thread || exit $rc
           run peer_bench 240 env FOREMAST_DEVICE_INDEX=0 FOREMAST_DIST_BACKEND=gloo python bench.py --gpus 2 \
               --services 2500 --publish peer --steps 300 --warmup 20 || exit $rc ;;
     restart) e2e c3e2e_restart --config 3e2e --steps 5 --warmup 2 --restart &&
          e2e c2e2e_restart --config 2e2e --steps 5 --warmup 2 --restart || exit $rc ;;
+    scanprobe) run scanprobe 200 python -u tools/hw_scan_probe.py || exit $rc
+          run scanab 300 python -u tools/hw_scan_ab.py --rows 40000 --m 1440 288 720 --reps 5 || exit $rc ;;
+    pmcscan) run pmcscan 420 bash tools/pmc_hwscan.sh || exit $rc ;;
     configs) for c in 1 2 3 4 5; do run "c$c" 300 python benchmarks/bench_configs.py --config $c || exit $rc; done ;;
     prof) cd /tmp && export TMPDIR=/tmp
           timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_headline" -o headline -- \
