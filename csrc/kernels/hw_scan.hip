@@ -116,7 +116,8 @@ struct RowPad {
 };
 
 // LDS: xs[pad(T - base + 64 C)] (the row from base on, NaN-padded) |
-// pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | sse[32] | base
+// pw[GP][kLevels][4] f2 (A^{C 2^j} per wave) | sse[32] | base, lap flags | wave sums,
+// the L2 warm-up DMA landing zone, wave minima and the winner's state
 template <int C, bool EXACT, bool FS, int LPP>
 __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restrict__ x, int64_t ld, int T,
                                                            const float* __restrict__ cand, int G, int m, int H,
@@ -125,15 +126,16 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
                                                            float* __restrict__ sigma, int* __restrict__ best,
                                                            int* __restrict__ nfin, float* __restrict__ sscale,
                                                            float* __restrict__ season_out, int xal, int64_t nrows,
-                                                           int ahead) {
+                                                           int ahead, int npass, long long* __restrict__ probe) {
   using RP = RowPad<C, EXACT>;
+  const long long pc0 = probe != nullptr ? clock64() : 0, pw0 = probe != nullptr ? wall_clock64() : 0;
   extern __shared__ float lds[];
   const int64_t row = blockIdx.x;
   const int GP = (G + 1) >> 1;
   const int Tx = (RP::words(T + 64 * C) + 3) & ~3;   // padded row + NaN tail for the last lap
   float* xs = lds;
   f2* pw = reinterpret_cast<f2*>(lds + Tx);
-  float* sse_s = lds + Tx + GP * kLevels * 8;
+  float* sse_s = lds + Tx + (kMaxG / 2) * kLevels * 8;      // pw: one entry per pair slot
   int* ibase = reinterpret_cast<int*>(sse_s + kMaxG);
   int* lapnan = ibase + 4;                                     // FS: a missing sample in lap k
   float* wsum = reinterpret_cast<float*>(lapnan + kMaxLaps);  // FS: per-wave season sums
@@ -144,18 +146,85 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   static_assert(LPP == 64 || (LPP == 32 && FS), "half-wave pairs need the cooperative setup");
   constexpr int PPW = 64 / LPP, NLV = LPP == 64 ? 6 : 5;
   const int half = lane / LPP, li = lane % LPP;
-  const bool pvalid = w * PPW + half < GP;
-  const int pair = pvalid ? w * PPW + half : GP - 1;    // an idle half shadows the last pair
+  // pair slots: slot `slot` fits pairs slot, slot + SL, ... in npass passes
+  // (fewer waves per row, so two rows share a CU: one's setup and selection
+  // run beside the other's laps); an idle slot shadows the last pair
+  const int slot = w * PPW + half, SL = (nth / FM_WAVE) * PPW;
+  const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
   const float* xr = x + row * ld;
 
-  // ---- the row's first finite sample (LDS atomic min), then the row from
-  // there on into LDS (the second read of the row hits L2)
-  if (tid == 0) *ibase = T;
+  // ---- stage the row.  FS with an aligned row of <= 16 floats per thread
+  // (config 2: 10,080 over 896 threads): ONE read of the row, held in
+  // registers while the first finite sample is found, then written to LDS
+  // from base on -- with the lap flags and the first two seasons' sums on the
+  // way.  Otherwise: find base, then re-read the row (L2) into LDS.  The
+  // candidate powers are computed while the row's loads are in flight.
+  constexpr int KREG = 4;
+  const bool rs = FS && xal && T <= KREG * 4 * nth;
+  // wsum[64..128) is the L2 warm-up DMA's landing zone (one dword per lane of
+  // a wave): the per-wave minima and the winner's state live past it
+  int* wmin = reinterpret_cast<int*>(wsum + 128);             // per-wave first finite sample
   if constexpr (FS)
     for (int i = tid; i < kMaxLaps; i += nth) lapnan[i] = 0;
-  __syncthreads();
+  float4 rv[KREG];
+  if (rs) {
+#pragma unroll
+    for (int k = 0; k < KREG; ++k) {
+      const int i = (k * nth + tid) * 4;
+      if (i + 4 <= T) {
+        rv[k] = *reinterpret_cast<const float4*>(xr + i);
+      } else {
+        const float nan = __builtin_nanf("");
+        rv[k] = make_float4(nan, nan, nan, nan);
+        if (i < T) rv[k].x = xr[i];
+        if (i + 1 < T) rv[k].y = xr[i + 1];
+        if (i + 2 < T) rv[k].z = xr[i + 2];
+      }
+    }
+  }
+  // ---- per slot: two candidates, A = J - k 1^T and its lane-uniform powers
+  // A^{C 2^lv} into the slot's LDS entry
+  f2 al, ab, gs;
+  auto powers = [&](int pair) {
+    const int ga = 2 * pair, gb = 2 * pair + 1 < G ? 2 * pair + 1 : 2 * pair;
+    al = (f2){cand[3 * ga], cand[3 * gb]};
+    const f2 be = {cand[3 * ga + 1], cand[3 * gb + 1]}, gm = {cand[3 * ga + 2], cand[3 * gb + 2]};
+    ab = al * be;
+    gs = gm * (one - al);
+    const M2 A = {one - al, one - al, -ab, one - ab};
+    M2 Q = A;
+    if constexpr (FS) {
+      M2 Pw = A;
+      Q = {one, zero, zero, one};
+#pragma unroll
+      for (int k = C; k > 0; k >>= 1) {                  // A^C by squaring
+        if (k & 1) Q = mmul(Q, Pw);
+        Pw = mmul(Pw, Pw);
+      }
+    } else {
+#pragma unroll 1
+      for (int k = 1; k < C; ++k) Q = mmul(Q, A);        // A^C
+    }
+    if (li == 0) {
+#pragma unroll 1
+      for (int lv = 0; lv < kLevels; ++lv) {
+        f2* p = pw + (slot * kLevels + lv) * 4;
+        p[0] = Q.a; p[1] = Q.b; p[2] = Q.c; p[3] = Q.d;
+        Q = mmul(Q, Q);
+      }
+    }
+  };
+  powers(min(slot, GP - 1));                   // pass 0, while the row's loads are in flight
+
   int fmin = T;
-  if (xal) {
+  if (rs) {
+#pragma unroll
+    for (int k = 0; k < KREG; ++k) {
+      const float4 v = rv[k];
+      const int f = isfinite(v.x) ? 0 : isfinite(v.y) ? 1 : isfinite(v.z) ? 2 : isfinite(v.w) ? 3 : 4;
+      if (f < 4) fmin = min(fmin, (k * nth + tid) * 4 + f);
+    }
+  } else if (xal) {
     for (int i = tid * 4; i < T; i += nth * 4) {
       if (i + 4 <= T) {
         const float4 v = *reinterpret_cast<const float4*>(xr + i);
@@ -171,21 +240,64 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       if (isfinite(xr[i])) fmin = min(fmin, i);
   }
   fmin = wave_min(fmin);
-  if (lane == 0) atomicMin(ibase, fmin);
-  __syncthreads();
-  const int base = *ibase;
-  for (int i = base + tid; i < T; i += nth) {
-    const float v = xr[i];
-    xs[RP::at(i - base)] = v;
-    if constexpr (FS)
-      if (!isfinite(v) && i >= base + m) lapnan[(i - base - m) / m] = 1;   // that lap takes the general scan
+  if (lane == 0) wmin[w] = fmin;
+  __syncthreads();                          // wmin, pw, lapnan zeroed
+  const long long pcb = probe != nullptr ? clock64() : 0;
+  int base = T;
+  for (int v = 0; v < nth / FM_WAVE; ++v) base = min(base, wmin[v]);
+  base = __builtin_amdgcn_readfirstlane(base);    // uniform (SGPR): it outlives the passes
+  float sa1 = 0.f, sb1 = 0.f, fa1 = 0.f, fb1 = 0.f;   // FS: this thread's first / second season sums
+  {
+    const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
+    if (rs) {
+#pragma unroll
+      for (int k = 0; k < KREG; ++k) {
+        const float vv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int i = (k * nth + tid) * 4 + c;
+          if (i >= base && i < T) {
+            const float v = vv[c];
+            const bool f = isfinite(v);
+            xs[RP::at(i - base)] = v;
+            if (!f && i >= base + m) lapnan[(i - base - m) / m] = 1;   // that lap takes the general scan
+            if (i < e1) { sa1 += f ? v : 0.f; fa1 += f ? 1.f : 0.f; }
+            else if (i < e2) { sb1 += f ? v : 0.f; fb1 += f ? 1.f : 0.f; }
+          }
+        }
+      }
+    } else {
+      for (int i = base + tid; i < T; i += nth) {
+        const float v = xr[i];
+        xs[RP::at(i - base)] = v;
+        if constexpr (FS)
+          if (!isfinite(v) && i >= base + m) lapnan[(i - base - m) / m] = 1;   // that lap takes the general scan
+      }
+    }
+    for (int r = T - base + tid; r < T - base + 64 * C; r += nth) xs[RP::at(r)] = __builtin_nanf("");
+    if constexpr (FS) {
+      // first- and second-season sums split over the workgroup's waves, then
+      // added in a fixed order (deterministic, the same in every wave)
+      if (!rs) {
+        __syncthreads();                    // the staged row
+        for (int i = base + tid; i < e2; i += nth) {
+          const float v = xs[RP::at(i - base)];
+          const bool f = isfinite(v);
+          if (i < e1) { sa1 += f ? v : 0.f; fa1 += f ? 1.f : 0.f; }
+          else { sb1 += f ? v : 0.f; fb1 += f ? 1.f : 0.f; }
+        }
+      }
+      sa1 = wave_sum(sa1); sb1 = wave_sum(sb1); fa1 = wave_sum(fa1); fb1 = wave_sum(fb1);
+      if (lane == 0) { wsum[4 * w] = sa1; wsum[4 * w + 1] = sb1; wsum[4 * w + 2] = fa1; wsum[4 * w + 3] = fb1; }
+    }
   }
-  for (int r = T - base + tid; r < T - base + 64 * C; r += nth) xs[RP::at(r)] = __builtin_nanf("");
+  __syncthreads();                          // the row, lap flags and season sums
   if constexpr (FS) {
     // warm L2 (and the Infinity Cache) with the row the workgroup `ahead`
     // dispatches later will read -- the same XCD when ahead % 8 == 0: one dword
-    // per 128-B line, DMA'd into a scratch LDS word (no VGPR, nothing waits on it
-    // until the end-of-row barriers, long after it landed)
+    // per 128-B line, DMA'd into a scratch LDS zone (no VGPR).  Issued after
+    // the setup's last barrier: a barrier waits for every outstanding memory
+    // operation, so the next one (after the laps) finds it long landed
     const int64_t nxt = row + ahead;
     if (ahead > 0 && nxt < nrows) {
       const float* src = x + nxt * ld;
@@ -196,59 +308,11 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     }
   }
 
-  // ---- per wave: two candidates, A = J - k 1^T and its lane-uniform powers
-  const int ga = 2 * pair, gb = 2 * pair + 1 < G ? 2 * pair + 1 : 2 * pair;
-  const f2 al = {cand[3 * ga], cand[3 * gb]}, be = {cand[3 * ga + 1], cand[3 * gb + 1]},
-           gm = {cand[3 * ga + 2], cand[3 * gb + 2]};
-  const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
-  const f2 ab = al * be, gs = gm * (one - al);
-  const M2 A = {one - al, one - al, -ab, one - ab};
-  M2 Q = A;
-  if constexpr (FS) {
-    M2 Pw = A;
-    Q = {one, zero, zero, one};
-#pragma unroll
-    for (int k = C; k > 0; k >>= 1) {                  // A^C by squaring
-      if (k & 1) Q = mmul(Q, Pw);
-      Pw = mmul(Pw, Pw);
-    }
-  } else {
-#pragma unroll 1
-    for (int k = 1; k < C; ++k) Q = mmul(Q, A);        // A^C
-  }
-  if (li == 0 && pvalid) {
-#pragma unroll 1
-    for (int lv = 0; lv < kLevels; ++lv) {             // A^{C 2^lv}
-      f2* p = pw + (pair * kLevels + lv) * 4;
-      p[0] = Q.a; p[1] = Q.b; p[2] = Q.c; p[3] = Q.d;
-      Q = mmul(Q, Q);
-    }
-  }
-  __syncthreads();
 
-  // ---- initial state: level = mean of the first season, trend = (mean of the
-  // second - mean of the first) / m, seasonal indices from the first season
-  f2 l, tr;
+  // ---- initial level / trend (the same for every candidate): level = mean of
+  // the first season, trend = (mean of the second - mean of the first) / m
+  float m1 = __builtin_nanf(""), trd = 0.f;
   int c1 = 0;
-  f2 s[C];
-  const int q0 = li * C;
-  if constexpr (FS) {
-    // first- and second-season sums split over the workgroup's waves, then
-    // added in a fixed order (deterministic, the same in every wave)
-    if (base < T) {
-      const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
-      float sa = 0.f, sb = 0.f, fa = 0.f, fb = 0.f;
-      for (int i = base + tid; i < e2; i += nth) {
-        const float v = xs[RP::at(i - base)];
-        const bool f = isfinite(v);
-        if (i < e1) { sa += f ? v : 0.f; fa += f ? 1.f : 0.f; }
-        else { sb += f ? v : 0.f; fb += f ? 1.f : 0.f; }
-      }
-      sa = wave_sum(sa); sb = wave_sum(sb); fa = wave_sum(fa); fb = wave_sum(fb);
-      if (lane == 0) { wsum[4 * w] = sa; wsum[4 * w + 1] = sb; wsum[4 * w + 2] = fa; wsum[4 * w + 3] = fb; }
-    }
-    __syncthreads();
-  }
   if (base < T) {
     const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
     float sa = 0.f, sb = 0.f;
@@ -275,36 +339,187 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       }
       sa = wave_sum(sa); sb = wave_sum(sb); ca = wave_sum(ca); cb = wave_sum(cb);
     }
-    const float m1 = ca > 0 ? sa / ca : 0.f, m2 = cb > 0 ? sb / cb : 0.f;
-    const float trd = cb > 0 ? (m2 - m1) / m : 0.f;
-    l = (f2){m1, m1};
-    tr = (f2){trd, trd};
+    m1 = ca > 0 ? sa / ca : 0.f;
+    const float m2 = cb > 0 ? sb / cb : 0.f;
+    trd = cb > 0 ? (m2 - m1) / m : 0.f;
     c1 = ca;
+  }
+  // uniform across the workgroup: SGPRs, not VGPRs held through the passes
+  m1 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m1)));
+  trd = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, trd)));
+  c1 = __builtin_amdgcn_readfirstlane(c1);
+  const int q0 = li * C;
+  f2 s[C];
+  int n = 0;                                // finite steps after the first season (every candidate)
+  int bg = 0;                               // the best candidate so far and its SSE (uniform)
+  float bs = 0.f;
+  float* lbt = wsum + 144;                  // the winner's level, trend
+  float* sbst = wsum + 160;                 // the winner's seasons by absolute phase [m]
+  long long pc1 = 0, pc2 = 0, pcs = 0;
+#pragma unroll 1
+  for (int pass = 0; pass < npass; ++pass) {
+  const int pidx = slot + pass * SL;
+  const bool pvalid = pidx < GP;
+  const int pair = pvalid ? pidx : GP - 1;
+  if (pass > 0) {
+    powers(pair);
+    __syncthreads();                        // the slot's powers (every wave runs every pass)
+  }
+  const int ga = 2 * pair, gb = 2 * pair + 1 < G ? 2 * pair + 1 : 2 * pair;
+  // ---- initial state, seasonal indices from the first season (an opaque
+  // lane offset: hoisted out of the pass loop, the C per-step conditions and
+  // addresses took 70 registers for the whole loop)
+  f2 l = (f2){m1, m1}, tr = (f2){trd, trd};
+  int q0p = q0;
+  asm volatile("" : "+v"(q0p));
+  if (base < T) {
 #pragma unroll
     for (int j = 0; j < C; ++j) {
-      const int q = q0 + j;
+      const int q = q0p + j;
       const float v = (q < m && base + q < T) ? xs[RP::at(q)] : __builtin_nanf("");
       const float si = isfinite(v) ? v - m1 : 0.f;
       s[j] = (f2){si, si};
     }
   } else {
-    l = (f2){__builtin_nanf(""), __builtin_nanf("")};
-    tr = zero;
 #pragma unroll
     for (int j = 0; j < C; ++j) s[j] = zero;
   }
 
+  if (probe != nullptr && pass == 0) pc1 = clock64();
   // ---- season laps.  Steps past the lap's end (the last active lane's tail,
   // later lanes) act as missing samples (e = 0: seasons, SSE and count stay
   // unchanged), so the step loops carry no per-step branches; xs is padded
   // with NaN past T so their reads stay inside the allocation.
   double ea = 0.0, eb = 0.0;
-  int n = 0;
+  n = 0;
+  if constexpr (FS) {
+  // One code path for every lap: the general arithmetic (missing samples,
+  // inactive steps) sits behind lap-uniform scalar branches inside the step
+  // loops.  Separate lap variants each produced their own updated seasons and
+  // the register allocator copied all C of them back at the join (+48 VGPRs
+  // and 24 v_mov_b64 per lap at C = 24).
+  int lap = 0;
+#pragma unroll 1
+  for (int tl = base + m; tl < T; tl += m, ++lap) {
+    int pwo = slot * kLevels * 4;
+    if constexpr (LPP == 64) asm volatile("" : "+s"(pwo));
+    else asm volatile("" : "+v"(pwo));
+    const f2* pwv = pw + pwo;
+    const int nact = min(m, T - tl);
+    const int last = (nact - 1) / C;          // lane holding the lap's last step
+    const int cnt = nact - q0;                // active steps of this lane (may be <= 0 or > C)
+    const bool gaps = lapnan[lap] != 0;       // a missing sample (the staging's flags)
+    // pass 2 needs the masked arithmetic for gaps and for inactive steps
+    // (a partial last lap; every lap when the chunks do not tile the season)
+    const bool gen2 = gaps || !EXACT || nact != m;
+    const float* xl = xs + RP::at(tl - base + q0);
+    // pass 1 (lanes before `last` feed the scan; their chunks are full)
+    f2 b0 = li == 0 ? l : zero, b1 = li == 0 ? tr : zero;
+    M2 Mm = {one, zero, zero, one};
+    // the step loops read their samples in groups of 8 issued together: the
+    // lap-uniform branches split every step into its own basic block, so the
+    // compiler would otherwise wait on each step's LDS read in turn
+    float xg[8];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      if (j % 8 == 0) {
+        if (j > 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 8 && j + k < C; ++k) xg[k] = xl[(j + k) + ((j + k) >> RP::S)];
+      }
+      const float xq = xg[j % 8];
+      const f2 u = xq - s[j];
+      const f2 wb = b0 + b1;
+      f2 e = u - wb;
+      if (gaps) {                             // uniform branch: missing sample -> J, no input
+        asm volatile("");
+        const bool fin = isfinite(xq);
+        e = fin ? e : zero;
+        const f2 ka = fin ? al : zero, kb = fin ? ab : zero;
+        const f2 w0 = Mm.a + Mm.c, w1 = Mm.b + Mm.d;
+        Mm.a = w0 - ka * w0;
+        Mm.b = w1 - ka * w1;
+        Mm.c = Mm.c - kb * w0;
+        Mm.d = Mm.d - kb * w1;
+      }
+      b0 = __builtin_elementwise_fma(al, e, wb);
+      b1 = __builtin_elementwise_fma(ab, e, b1);
+    }
+    if (!gaps) {
+      // full, finite chunks: lane i's window at level d is A^{C d}
+#pragma unroll
+      for (int lv = 0; lv < NLV; ++lv) {
+        const int d = 1 << lv;
+        const f2 n0 = up(b0, d), n1 = up(b1, d);
+        const f2 p0 = pwv[lv * 4 + 0], p1 = pwv[lv * 4 + 1], p2 = pwv[lv * 4 + 2], p3 = pwv[lv * 4 + 3];
+        if (li >= d) {
+          b0 = b0 + p0 * n0 + p1 * n1;
+          b1 = b1 + p2 * n0 + p3 * n1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int lv = 0; lv < NLV; ++lv) {
+        const int d = 1 << lv;
+        const M2 nm = {up(Mm.a, d), up(Mm.b, d), up(Mm.c, d), up(Mm.d, d)};
+        const f2 n0 = up(b0, d), n1 = up(b1, d);
+        if (li >= d) {
+          b0 = b0 + Mm.a * n0 + Mm.b * n1;
+          b1 = b1 + Mm.c * n0 + Mm.d * n1;
+          Mm = mmul(Mm, nm);
+        }
+      }
+    }
+    // exclusive prefix: the (level, trend) entering this lane's chunk
+    f2 L = up(b0, 1), Tt = up(b1, 1);
+    if (li == 0) { L = l; Tt = tr; }
+    int xo = RP::at(tl - base + q0);
+    asm volatile("" : "+v"(xo));
+    xl = xs + xo;
+    f2 acc = zero;
+    int nn = 0;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      if (j % 8 == 0) {
+        if (j > 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 8 && j + k < C; ++k) xg[k] = xl[(j + k) + ((j + k) >> RP::S)];
+      }
+      const float xq = xg[j % 8];
+      f2 lt = L + Tt;
+      f2 e = xq - (lt + s[j]);
+      if (gen2) {                             // uniform branch: inactive steps are exact no-ops,
+        asm volatile("");                     // missing samples leave e = 0
+        const bool act = j < cnt;
+        const bool fin = act && isfinite(xq);
+        lt = act ? lt : L;
+        e = fin ? e : zero;
+        nn += fin ? 1 : 0;
+      }
+      L = __builtin_elementwise_fma(al, e, lt);
+      Tt = __builtin_elementwise_fma(ab, e, Tt);
+      s[j] = __builtin_elementwise_fma(gs, e, s[j]);
+      acc = __builtin_elementwise_fma(e, e, acc);
+    }
+    if (!gen2) nn = C;
+    if (q0 >= m) { acc = zero; nn = 0; }      // idle lanes ran past the season
+    ea += acc.x;
+    eb += acc.y;
+    n += nn;
+    if constexpr (LPP == 64) {
+      l = rdl(L, last);
+      tr = rdl(Tt, last);
+    } else {                                  // each half reads its own last lane
+      l = bperm2(L, (lane & ~(LPP - 1)) + last);
+      tr = bperm2(Tt, (lane & ~(LPP - 1)) + last);
+    }
+  }
+  } else {
 #pragma unroll 1
   for (int tl = base + m; tl < T; tl += m) {
     // re-read the powers every lap (an opaque offset keeps the compiler from
     // hoisting 24 loop-invariant LDS loads into 48 live VGPRs)
-    int pwo = pair * kLevels * 4;
+    int pwo = slot * kLevels * 4;
     if constexpr (LPP == 64) asm volatile("" : "+s"(pwo));
     else asm volatile("" : "+v"(pwo));
     const f2* pwv = pw + pwo;
@@ -451,11 +666,13 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       tr = bperm2(Tt, (lane & ~(LPP - 1)) + last);
     }
   }
+  }  // !FS
+  if (probe != nullptr) pc2 = clock64();
   ea = group_sum<LPP>(ea);
   eb = group_sum<LPP>(eb);
-  n = group_sum<LPP>(n);
+  n = __builtin_amdgcn_readfirstlane(group_sum<LPP>(n));   // the same for every candidate
 
-  // ---- per-candidate results, then the row's best candidate
+  // ---- per-candidate results
   const float fa = (float)ea, fb = (float)eb;
   const float tph = (float)(T % m);
   if (li == 0 && pvalid) {
@@ -476,37 +693,47 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       sse_s[gb] = fb;
     }
   }
-  __syncthreads();                         // every wave is done with xs too
-  int bg = 0;
-  float bs = sse_s[0];
-  for (int g = 1; g < G; ++g) {
+  __syncthreads();
+  if (probe != nullptr) pcs = clock64();
+  // ---- the best candidate so far: this pass covers candidates [g0, g1), so
+  // continuing the ascending scan picks as one scan over all G would
+  // (hw2_forecast_kernel's rule); a new winner parks its state in LDS
+  const int g0 = 2 * pass * SL, g1 = min(G, 2 * (pass + 1) * SL);
+  int g = g0;
+  if (pass == 0) { bs = sse_s[0]; bg = 0; g = 1; }
+  for (; g < g1; ++g) {
     const float v = sse_s[g];
     if (v < bs || !isfinite(bs)) { bs = v; bg = g; }
   }
-  const bool mine = (bg >> 1) == pair && pvalid;
-  const bool hi = (bg & 1) != 0;
-  if (mine) {
+  bs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, bs)));
+  bg = __builtin_amdgcn_readfirstlane(bg);
+  if (bg >= g0 && (bg >> 1) == pair && pvalid) {
+    const bool hi = (bg & 1) != 0;
+    int p = (base + q0p) % m;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
-      const int q = q0 + j;
-      if (q < m) {
-        int p = (base + q) % m;
-        xs[p] = hi ? s[j].y : s[j].x;     // seasons by absolute phase
-      }
+      if (q0p + j < m) sbst[p] = hi ? s[j].y : s[j].x;     // seasons by absolute phase
+      p = p + 1 == m ? 0 : p + 1;
+    }
+    if (li == 0) {
+      lbt[0] = hi ? l.y : l.x;
+      lbt[1] = hi ? tr.y : tr.x;
     }
   }
+  }  // passes
   __syncthreads();
-  if (mine) {
-    const float lb = hi ? l.y : l.x, tb = hi ? tr.y : tr.x;
+  // the winner's forecast and seasons, spread over the whole workgroup
+  {
+    const float lb = lbt[0], tb = lbt[1];
     const int t0 = T % m;
-    for (int h = 1 + li; h <= H; h += LPP) {
+    for (int h = 1 + tid; h <= H; h += nth) {
       int p = t0 + h - 1;
       p %= m;
-      fc[row * H + (h - 1)] = lb + h * tb + xs[p];
+      fc[row * H + (h - 1)] = lb + h * tb + sbst[p];
     }
     if (season_out != nullptr)
-      for (int p = li; p < m; p += LPP) season_out[row * m + p] = xs[p];
-    if (li == 0) {
+      for (int p = tid; p < m; p += nth) season_out[row * m + p] = sbst[p];
+    if (tid == 0) {
       sigma[row] = n > 1 ? sqrtf(bs / (float)(n - 1)) : 0.f;
       best[row] = bg;
       sscale[row] = 1.f;
@@ -514,6 +741,16 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     }
   }
   if constexpr (FS) __builtin_amdgcn_s_waitcnt(0);   // no L2 warm-up DMA outlives the workgroup's LDS
+  if (probe != nullptr && lane == 0) {
+    // phase timing (fm_hw_scan_set_probe), per wave: clocks at start, after
+    // the first barrier, at the laps, after the laps, after the selection
+    // barrier and at exit; the wall clock at start; HW_ID (SIMD, CU, SE)
+    long long* pr = probe + (row * 16 + w) * 8;
+    pr[0] = pc0; pr[1] = pcb; pr[2] = pc1; pr[3] = pc2; pr[4] = pcs; pr[5] = clock64();
+    const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);      // HW_REG_XCC_ID [3:0]
+    pr[6] = pw0; pr[7] = ((long long)xcc << 32) | hwid;
+  }
 }
 
 namespace {
@@ -521,6 +758,7 @@ constexpr int kChunks[] = {4, 5, 6, 8, 9, 12, 16, 18, 20, 23, 24};
 constexpr int kHalfMaxM = 32 * 24;       // seasons up to this length scan in 32-lane half-waves
 
 constexpr size_t kMaxLds = 160 * 1024;   // a single gfx950 workgroup may take the whole LDS
+constexpr int kPassWaves = 8;            // waves per row when candidates run in passes (2 rows / CU)
 
 template <int C, bool EXACT, bool FS, int LPP>
 void allow_big_lds() {
@@ -542,6 +780,16 @@ bool scan_fast_setup() {
   return fs;
 }
 
+// FOREMAST_HW_SCAN_PASSES=1: one pass over the candidate pairs (one wave per
+// pair, one row per CU at config 2) for A/B runs
+bool scan_passes_allowed() {
+  static const bool ok = [] {
+    const char* e = getenv("FOREMAST_HW_SCAN_PASSES");
+    return e == nullptr || e[0] != '1';
+  }();
+  return ok;
+}
+
 // lanes per candidate pair for a season of m steps
 int scan_lpp(int m) {
   static const int force = [] {
@@ -555,12 +803,15 @@ int scan_lpp(int m) {
   return m <= kHalfMaxM ? 32 : 64;
 }
 
+long long* g_probe = nullptr;            // fm_hw_scan_set_probe: [R, 16, 8] int64 phase timings, or null
+
 template <int C>
 int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
                float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
-               float* season_out, size_t lds, int xal, int lpp, hipStream_t stream) {
+               float* season_out, size_t lds, int xal, int lpp, int npass, hipStream_t stream) {
   const int GP = (G + 1) / 2;
-  const int waves = lpp == 64 ? GP : (GP + 1) / 2;
+  const int slots = lpp == 64 ? GP : (GP + 1) / 2;          // waves for one pass over the pairs
+  const int waves = (slots + npass - 1) / npass;
   const bool fs = scan_fast_setup();
   // L2 warm-up distance: the workgroups resident at once (one per CU at 14
   // waves), a multiple of the 8 XCDs so the warmed row is read on the same XCD
@@ -576,7 +827,7 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
     if (lds > 65536) allow_big_lds<C, EX, FSV, LP>();                                                       \
     hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV, LP>), dim3((unsigned)R), dim3(64 * waves), lds, stream, x, \
                        ld, T, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal,  \
-                       R, ahead);                                                                          \
+                       R, ahead * (npass > 1 ? 2 : 1), npass, g_probe);                                    \
   } while (0)
   const bool ex = m % C == 0;
   if (lpp == 32) {
@@ -605,7 +856,7 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
 // decides, for the launcher and for the Python-side shape query
 // (fm_hw_scan_supported), so the two can never disagree.
 struct ScanPlan {
-  int C = 0, lpp = 64;
+  int C = 0, lpp = 64, npass = 1;
   size_t lds = 0;
 };
 
@@ -627,14 +878,28 @@ ScanPlan scan_plan(int T, int G, int m) {
   const int GP = (G + 1) / 2;
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
-  const size_t lds = words * 4 + (size_t)GP * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4 + 64 * 4;
+  const size_t lds = words * 4 + (size_t)(kMaxG / 2) * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4 + 64 * 4 +
+                     32 * 4 + (size_t)((m + 3) & ~3) * 4;   // wsum | DMA landing zone | wmin, lbt | seasons
   if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return p;
   p.C = C;
   p.lpp = lpp;
   p.lds = lds;
+  // candidate passes: a row's waves beyond kPassWaves leave room for one
+  // workgroup per CU (4 waves / SIMD at 128 VGPRs); in passes of at most
+  // kPassWaves waves two rows share a CU when their LDS fits twice
+  const int slots = lpp == 64 ? GP : (GP + 1) / 2;
+  if (scan_fast_setup() && slots > kPassWaves && 2 * lds <= kMaxLds && scan_passes_allowed())
+    p.npass = (slots + kPassWaves - 1) / kPassWaves;
   return p;
 }
 }  // namespace
+
+// Phase-timing buffer for the next fits (tools/hw_scan_probe.py): [R, 16
+// waves, 8] int64, null to switch it off.
+FM_API int fm_hw_scan_set_probe(void* p) {
+  g_probe = static_cast<long long*>(p);
+  return 0;
+}
 
 // 1 when fm_hw_scan_fit covers (T, G, m) in this process (environment
 // overrides included, read once), else 0.
@@ -647,13 +912,13 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   if (H < 0) return (int)hipErrorInvalidValue;
   const ScanPlan pl = scan_plan(T, G, m);
   if (pl.C == 0) return (int)hipErrorInvalidValue;
-  const int C = pl.C, lpp = pl.lpp;
+  const int C = pl.C, lpp = pl.lpp, npass = pl.npass;
   const size_t lds = pl.lds;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \
     return launch_one<CC>(x, ld, T, R, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale,    \
-                          season_out, lds, xal, lpp, stream);
+                          season_out, lds, xal, lpp, npass, stream);
   switch (C) {
     FM_HWS(4) FM_HWS(5) FM_HWS(6) FM_HWS(8) FM_HWS(9) FM_HWS(12) FM_HWS(16) FM_HWS(18) FM_HWS(20) FM_HWS(23)
     FM_HWS(24)

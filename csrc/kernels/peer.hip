@@ -89,11 +89,19 @@ __global__ void peer_ack_kernel(unsigned* const* dst, int n, unsigned value) {
 // ---------------------------------------------------------------- IPC handles
 FM_API int fm_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
-FM_API int fm_ipc_get_handle(void* ptr, void* out) {
+// The handle names the whole allocation `ptr` lives in (a caching allocator
+// sub-allocates tensors from larger blocks): `offset` is ptr's distance from
+// the allocation's base, which the importer adds to its mapping.
+FM_API int fm_ipc_get_handle(void* ptr, void* out, int64_t* offset) {
   hipIpcMemHandle_t h;
   hipError_t e = hipIpcGetMemHandle(&h, ptr);
   if (e != hipSuccess) return (int)e;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  e = hipMemGetAddressRange(&base, &size, ptr);
+  if (e != hipSuccess) return (int)e;
   std::memcpy(out, &h, sizeof(h));
+  *offset = (int64_t)((char*)ptr - (char*)base);
   return 0;
 }
 

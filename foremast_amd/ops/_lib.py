@@ -47,7 +47,7 @@ _SIGS: dict[str, list] = {
     "fm_hw_scan_supported": [c_int, c_int, c_int],
     "fm_hw_scan_set_probe": [c_void_p],
     "fm_ipc_handle_size": [],
-    "fm_ipc_get_handle": [c_void_p, c_void_p],
+    "fm_ipc_get_handle": [c_void_p, c_void_p, c_void_p],
     "fm_ipc_open": [c_void_p, c_void_p],
     "fm_ipc_close": [c_void_p],
     "fm_peer_publish": [c_void_p, c_void_p, c_i64, c_void_p, ctypes.c_uint, c_void_p, c_void_p],

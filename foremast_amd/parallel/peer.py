@@ -45,17 +45,22 @@ def _store():
 
 
 def _handle(t: torch.Tensor) -> bytes:
+    """IPC handle of the allocation holding ``t`` + ``t``'s byte offset in it
+    (the caching allocator sub-allocates: the handle names the block)."""
     lib = LIB.load()
     n = lib.fm_ipc_handle_size()
     buf = ctypes.create_string_buffer(n)
-    LIB.call("fm_ipc_get_handle", t.data_ptr(), buf)
-    return buf.raw
+    off = ctypes.c_int64()
+    LIB.call("fm_ipc_get_handle", t.data_ptr(), buf, ctypes.byref(off))
+    return buf.raw + int(off.value).to_bytes(8, "little")
 
 
-def _open(h: bytes) -> int:
+def _open(h: bytes) -> tuple[int, int]:
+    """-> (base of the opened mapping (for close), the tensor's address)."""
     out = ctypes.c_void_p()
-    LIB.call("fm_ipc_open", ctypes.c_char_p(h), ctypes.byref(out))
-    return int(out.value)
+    LIB.call("fm_ipc_open", ctypes.c_char_p(h[:-8]), ctypes.byref(out))
+    base = int(out.value)
+    return base, base + int.from_bytes(h[-8:], "little")
 
 
 class PeerPublisher:
@@ -68,26 +73,30 @@ class PeerPublisher:
         self._opened: list[int] = []
         self.status = torch.zeros(4, dtype=torch.int32, device=self.dev)
         self.arrive = torch.zeros(depth, dtype=torch.int32, device=self.dev)
+        # fleet rows and arrival flags share ONE exported buffer (one handle,
+        # one mapping per importer): [fleet | pad to 256 B | flags]
+        fbytes = depth * world * shard * 16
+        self._flag_off = (fbytes + 255) // 256 * 256
         if rank == 0:
-            self.fleet = torch.zeros((depth, world * shard, 4), dtype=torch.float32, device=self.dev)
-            self.flags = torch.zeros((depth, world), dtype=torch.int32, device=self.dev)
+            self._shared = torch.zeros(self._flag_off + depth * world * 4, dtype=torch.uint8, device=self.dev)
+            self.fleet = self._shared[:fbytes].view(torch.float32).view(depth, world * shard, 4)
+            self.flags = self._shared[self._flag_off:].view(torch.int32).view(depth, world)
             torch.cuda.synchronize(self.dev)
-            st.set(f"{tag}/fleet", _handle(self.fleet))
-            st.set(f"{tag}/flags", _handle(self.flags))
+            st.set(f"{tag}/fleet", _handle(self._shared))
             self.fleet_ptr, self.flags_ptr = self.fleet.data_ptr(), self.flags.data_ptr()
         else:
             self.ack = torch.zeros(depth, dtype=torch.int32, device=self.dev)
             torch.cuda.synchronize(self.dev)
             st.set(f"{tag}/ack/{rank}", _handle(self.ack))
-            self.fleet_ptr = _open(st.get(f"{tag}/fleet"))
-            self.flags_ptr = _open(st.get(f"{tag}/flags"))
-            self._opened += [self.fleet_ptr, self.flags_ptr]
+            base, self.fleet_ptr = _open(st.get(f"{tag}/fleet"))
+            self.flags_ptr = self.fleet_ptr + self._flag_off
+            self._opened.append(base)
         if rank == 0:
             # remote ack words: one pointer per (rank, slot), rank 0's own entry unused
             self._acks = []
             for r in range(1, world):
-                p = _open(st.get(f"{tag}/ack/{r}"))
-                self._opened.append(p)
+                b, p = _open(st.get(f"{tag}/ack/{r}"))
+                self._opened.append(b)
                 self._acks.append(p)
             self.ack_ptrs = torch.tensor([[p + 4 * s for p in self._acks] for s in range(depth)] or [[0]],
                                          dtype=torch.int64, device=self.dev)

@@ -770,3 +770,34 @@ def test_gpu_hw_scan_fit_odd_pair_count_idle_half(cuda, m, G):
     for r in np.flatnonzero(bc != best0):
         a, b = sse0[r, bc[r]], sse0[r, best0[r]]
         assert abs(a - b) <= 2e-3 * max(a, b), (r, a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [288, 1440])
+def test_gpu_hw_scan_fit_many_rows_matches_serial(cuda, m):
+    """More rows than the L2 warm-up distance (the DMA of the row 256
+    workgroups ahead lands in LDS while the fit runs) and the one-read
+    register staging at m = 1440: every row's SSE, pick and forecast match
+    the serial kernel; ragged starts, gaps and empty rows on the way."""
+    T, R = 4 * m, 1500
+    x = _seasonal(R, T, period=m, seed=11)
+    x *= np.geomspace(1e-1, 1e3, R)[:, None].astype(np.float32)
+    x[7, :31] = np.nan
+    x[300, m + 17] = np.nan
+    x[900, :] = np.nan
+    x[1400, 2 * m:2 * m + 40] = np.nan
+    xt = torch.from_numpy(x).to(cuda)
+    sc = SM.es_fit(xt, T, 2, 10, m, method="scan", keep_state=True)
+    se = SM.es_fit(xt, T, 2, 10, m, method="serial", half_season=False, keep_state=True)
+    s_c, s_e = sc.sse.cpu().numpy(), se.sse.cpu().numpy()
+    ok = np.isfinite(s_e) & (s_e > 0)
+    np.testing.assert_allclose(s_c[ok], s_e[ok], rtol=2e-3)
+    bc, be = sc.best.cpu().numpy(), se.best.cpu().numpy()
+    for r in np.flatnonzero((bc != be) & ok.all(1)):
+        a, b = s_e[r, bc[r]], s_e[r, be[r]]
+        assert abs(a - b) <= 2e-3 * max(a, b), (r, a, b)
+    same = np.flatnonzero(bc == be)
+    amp = np.abs(np.nan_to_num(x[same])).mean(1, keepdims=True) + 1e-6
+    np.testing.assert_allclose(sc.forecast.cpu().numpy()[same] / amp, se.forecast.cpu().numpy()[same] / amp,
+                               atol=2e-3)
+    np.testing.assert_array_equal(sc.nfin.cpu().numpy(), np.isfinite(x).sum(1))

@@ -38,7 +38,9 @@ for s in $steps; do
     restart) e2e c3e2e_restart --config 3e2e --steps 5 --warmup 2 --restart &&
          e2e c2e2e_restart --config 2e2e --steps 5 --warmup 2 --restart || exit $rc ;;
     scanprobe) run scanprobe 200 python -u tools/hw_scan_probe.py || exit $rc
-          run scanab 300 python -u tools/hw_scan_ab.py --rows 40000 --m 1440 288 720 --reps 5 || exit $rc ;;
+          run scanab 300 python -u tools/hw_scan_ab.py --rows 40000 --m 1440 288 720 --reps 5 || exit $rc
+          run scanab_1pass 300 env FOREMAST_HW_SCAN_PASSES=1 python -u tools/hw_scan_ab.py --rows 40000 --m 1440 \
+              --reps 5 --methods scan || exit $rc ;;
     pmcscan) run pmcscan 420 bash tools/pmc_hwscan.sh || exit $rc ;;
     configs) for c in 1 2 3 4 5; do run "c$c" 300 python benchmarks/bench_configs.py --config $c || exit $rc; done ;;
     prof) cd /tmp && export TMPDIR=/tmp

@@ -46,7 +46,7 @@ def main() -> None:
     ev1.record()
     torch.cuda.synchronize()
     plain_ms = ev0.elapsed_time(ev1)
-    probe = torch.zeros((a.rows, 8), dtype=torch.int64, device=dev)
+    probe = torch.zeros((a.rows, 16, 8), dtype=torch.int64, device=dev)
     LIB.call("fm_hw_scan_set_probe", probe.data_ptr())
     try:
         ev0.record()
@@ -57,23 +57,43 @@ def main() -> None:
         LIB.call("fm_hw_scan_set_probe", None)
     probe_ms = ev0.elapsed_time(ev1)
     p = probe.cpu().numpy()
-    setup, laps, tail = p[:, 1] - p[:, 0], p[:, 2] - p[:, 1], p[:, 3] - p[:, 2]
-    w0, w1, cu = p[:, 4], p[:, 5], p[:, 6]
-    span_us = (w1.max() - w0.min()) / 100.0
-    cyc = p[:, 3] - p[:, 0]
-    wall = (w1 - w0) / 100.0
-    mhz = float(np.median(cyc / np.maximum(wall, 1e-3)))
-    # rows in flight per CU: total row-time / the CU's busy span
-    conc = []
-    for c in np.unique(cu):
-        k = cu == c
-        conc.append(float((w1[k] - w0[k]).sum()) / max(1.0, float(w1[k].max() - w0[k].min())))
-    q = lambda v: {"p50": float(np.median(v)), "p90": float(np.percentile(v, 90))}
+    nw = int((p[0, :, 0] != 0).sum())                  # waves per row
+    p = p[:, :nw]
+    c0, cb, c1, c2, cs, ce = (p[:, :, k].astype(np.float64) for k in range(6))
+    t0 = c0.min(1)
+    rel = lambda v: v - t0[:, None]
+    row_cyc = ce.max(1) - t0
+    hw = p[:, :, 7] & 0xFFFFFFFF
+    xcc = (p[:, 0, 7] >> 32) & 15
+    simd = (hw >> 4) & 3
+    per_simd = np.stack([(simd == k).sum(1) for k in range(4)], 1)
+    q = lambda v: {"p50": round(float(np.median(v)), 1), "p90": round(float(np.percentile(v, 90)), 1)}
+    lap = c2 - c1
+    # consecutive rows on one CU: idle wall time between a row's end and the next row's start
+    cu = (hw[:, 0] >> 8) & 15
+    se = (hw[:, 0] >> 13) & 7
+    mhz = 2100.0
+    w0 = p[:, 0, 6].astype(np.float64) / 100.0                  # us
+    w1 = w0 + row_cyc / mhz
+    gaps = []
+    key = (xcc * 8 + se) * 16 + cu
+    for k in np.unique(key):
+        idx = np.nonzero(key == k)[0]
+        o = idx[np.argsort(w0[idx])]
+        gaps.extend((w0[o[1:]] - w1[o[:-1]]).tolist())
     print(json.dumps({"rows": a.rows, "T": a.T, "m": a.m, "fit_ms": round(plain_ms, 3),
-                      "fit_ms_probed": round(probe_ms, 3), "span_us": round(span_us, 1),
-                      "cycles_setup": q(setup), "cycles_laps": q(laps), "cycles_tail": q(tail),
-                      "row_us": q(wall), "clock_mhz": round(mhz, 1), "cus": int(len(np.unique(cu))),
-                      "rows_in_flight_per_cu": round(float(np.mean(conc)), 2)}), flush=True)
+                      "fit_ms_probed": round(probe_ms, 3), "waves": nw,
+                      "row_cycles": q(row_cyc),
+                      "start_skew": q(c0.max(1) - t0),
+                      "barrier1_at": q(cb.max(1) - t0),
+                      "laps_start": q(rel(c1).mean(1)),
+                      "lap_cycles_wave": q(lap.ravel()), "lap_cycles_min": q(lap.min(1)), "lap_cycles_max": q(lap.max(1)),
+                      "laps_end_max": q(c2.max(1) - t0),
+                      "select_barrier_at": q(cs.max(1) - t0),
+                      "end_at": q(ce.max(1) - t0),
+                      "waves_per_simd_sorted": np.sort(per_simd, 1)[:, ::-1].mean(0).round(2).tolist(),
+                      "cus_seen": int(len(np.unique(key))),
+                      "gap_between_rows_us": q(np.asarray(gaps)) if gaps else None}), flush=True)
 
 
 if __name__ == "__main__":
