@@ -478,7 +478,13 @@ def config3e2e(args):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         load_s = time.perf_counter() - t_r
-        r2 = brain2.run_once()
+        if os.environ.get("FOREMAST_PROFILE_RESTART"):
+            import cProfile
+            prof = cProfile.Profile()
+            r2 = prof.runcall(brain2.run_once)
+            prof.dump_stats(os.environ["FOREMAST_PROFILE_RESTART"])
+        else:
+            r2 = brain2.run_once()
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         restart = {"restart_to_first_verdict_s": round(time.perf_counter() - t_r, 3), "load_s": round(load_s, 3),

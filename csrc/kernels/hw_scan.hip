@@ -62,11 +62,21 @@ __device__ __forceinline__ M2 mmul(const M2& p, const M2& q) {
 }
 
 // value of lane (lane - d) & 63 (callers ignore lanes < d); d = 1 rides DPP wave_shr:1
+// (bound_ctrl: lane 0 reads 0, no old value to materialise)
 __device__ __forceinline__ float up1(float v, int d) {
-  if (d == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+  if (d == 1) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
   return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(((lane_id() - d) & 63) << 2, __builtin_bit_cast(int, v)));
 }
 __device__ __forceinline__ f2 up(f2 v, int d) { return (f2){up1(v.x, d), up1(v.y, d)}; }
+// lane - 1's pair, zeros into lane 0 (row_shr-style DPP with bound_ctrl: no
+// old value to materialise first)
+__device__ __forceinline__ float up0_1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xF, 0xF, true));
+}
+__device__ __forceinline__ f2 up0(f2 v) {
+  const float vx = v.x, vy = v.y;
+  return (f2){up0_1(vx), up0_1(vy)};
+}
 
 // lane l's pair, for every lane.  The halves go through named floats:
 // __builtin_bit_cast of a vector element (bit_cast(int, v.y)) reads the
@@ -128,6 +138,10 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
                                                            float* __restrict__ season_out, int xal, int64_t nrows,
                                                            int ahead, int npass, long long* __restrict__ probe) {
   using RP = RowPad<C, EXACT>;
+  // FOREMAST_HW_SCAN_DEBUG (instruction accounting with PMC, results are
+  // garbage): 1 = stop after the row setup, 2 = skip the season laps
+  const int dbg = npass >> 8;
+  npass &= 255;
   const long long pc0 = probe != nullptr ? clock64() : 0, pw0 = probe != nullptr ? wall_clock64() : 0;
   extern __shared__ float lds[];
   const int64_t row = blockIdx.x;
@@ -151,6 +165,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // run beside the other's laps); an idle slot shadows the last pair
   const int slot = w * PPW + half, SL = (nth / FM_WAVE) * PPW;
   const f2 one = {1.f, 1.f}, zero = {0.f, 0.f};
+  const f2 m0 = li == 0 ? one : zero;                 // the lane that starts a lap's scan
   const float* xr = x + row * ld;
 
   // ---- stage the row.  FS with an aligned row of <= 16 floats per thread
@@ -191,7 +206,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     const f2 be = {cand[3 * ga + 1], cand[3 * gb + 1]}, gm = {cand[3 * ga + 2], cand[3 * gb + 2]};
     ab = al * be;
     gs = gm * (one - al);
-    const M2 A = {one - al, one - al, -ab, one - ab};
+    // FS laps run in (P, T) coordinates (see the lap loop), the others in (L, T)
+    const M2 A = FS ? M2{one - al - ab, one, -ab, one} : M2{one - al, one - al, -ab, one - ab};
     M2 Q = A;
     if constexpr (FS) {
       M2 Pw = A;
@@ -292,6 +308,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     }
   }
   __syncthreads();                          // the row, lap flags and season sums
+  if (dbg == 1) return;
   if constexpr (FS) {
     // warm L2 (and the Infinity Cache) with the row the workgroup `ahead`
     // dispatches later will read -- the same XCD when ahead % 8 == 0: one dword
@@ -370,6 +387,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // lane offset: hoisted out of the pass loop, the C per-step conditions and
   // addresses took 70 registers for the whole loop)
   f2 l = (f2){m1, m1}, tr = (f2){trd, trd};
+  if constexpr (FS) l = l + tr;             // the FS laps carry P = level + trend
   int q0p = q0;
   asm volatile("" : "+v"(q0p));
   if (base < T) {
@@ -398,9 +416,17 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // loops.  Separate lap variants each produced their own updated seasons and
   // the register allocator copied all C of them back at the join (+48 VGPRs
   // and 24 v_mov_b64 per lap at C = 24).
+  //
+  // The state is carried as (P, T), P = level + trend (the prediction before
+  // the season): e = x - s - P;  P' = P + T + c e  (c = a + a b);  T' = T + a b e;
+  // s' = s + g (1 - a) e.  The same recursion as (level, trend), but each step
+  // has two dependent ops on its critical path (e, then P') instead of four,
+  // so the scheduler has independent work for the hazard slots.  The powers
+  // in pw are of A = [[1 - c, 1], [-a b, 1]] (powers() for FS).
+  const f2 cc = al + ab;
   int lap = 0;
 #pragma unroll 1
-  for (int tl = base + m; tl < T; tl += m, ++lap) {
+  for (int tl = dbg == 2 ? T : base + m; tl < T; tl += m, ++lap) {
     int pwo = slot * kLevels * 4;
     if constexpr (LPP == 64) asm volatile("" : "+s"(pwo));
     else asm volatile("" : "+v"(pwo));
@@ -413,8 +439,9 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     // (a partial last lap; every lap when the chunks do not tile the season)
     const bool gen2 = gaps || !EXACT || nact != m;
     const float* xl = xs + RP::at(tl - base + q0);
-    // pass 1 (lanes before `last` feed the scan; their chunks are full)
-    f2 b0 = li == 0 ? l : zero, b1 = li == 0 ? tr : zero;
+    // pass 1 (lanes before `last` feed the scan; their chunks are full):
+    // lane 0 starts from the lap's entering state, the others from zero
+    f2 bP = l * m0, bT = tr * m0;
     M2 Mm = {one, zero, zero, one};
     // the step loops read their samples in groups of 8 issued together: the
     // lap-uniform branches split every step into its own basic block, so the
@@ -429,32 +456,34 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       }
       const float xq = xg[j % 8];
       const f2 u = xq - s[j];
-      const f2 wb = b0 + b1;
-      f2 e = u - wb;
+      f2 e = u - bP;
+      const f2 w = bP + bT;
       if (gaps) {                             // uniform branch: missing sample -> J, no input
         asm volatile("");
         const bool fin = isfinite(xq);
         e = fin ? e : zero;
-        const f2 ka = fin ? al : zero, kb = fin ? ab : zero;
+        // Mm <- (J - k e1^T) Mm with k = (c, a b) on a sample, 0 when missing
+        const f2 kP = fin ? cc : zero, kT = fin ? ab : zero;
         const f2 w0 = Mm.a + Mm.c, w1 = Mm.b + Mm.d;
-        Mm.a = w0 - ka * w0;
-        Mm.b = w1 - ka * w1;
-        Mm.c = Mm.c - kb * w0;
-        Mm.d = Mm.d - kb * w1;
+        const f2 na = w0 - kP * Mm.a, nb = w1 - kP * Mm.b;
+        Mm.c = Mm.c - kT * Mm.a;
+        Mm.d = Mm.d - kT * Mm.b;
+        Mm.a = na;
+        Mm.b = nb;
       }
-      b0 = __builtin_elementwise_fma(al, e, wb);
-      b1 = __builtin_elementwise_fma(ab, e, b1);
+      bP = __builtin_elementwise_fma(cc, e, w);
+      bT = __builtin_elementwise_fma(ab, e, bT);
     }
     if (!gaps) {
       // full, finite chunks: lane i's window at level d is A^{C d}
 #pragma unroll
       for (int lv = 0; lv < NLV; ++lv) {
         const int d = 1 << lv;
-        const f2 n0 = up(b0, d), n1 = up(b1, d);
+        const f2 n0 = up(bP, d), n1 = up(bT, d);
         const f2 p0 = pwv[lv * 4 + 0], p1 = pwv[lv * 4 + 1], p2 = pwv[lv * 4 + 2], p3 = pwv[lv * 4 + 3];
         if (li >= d) {
-          b0 = b0 + p0 * n0 + p1 * n1;
-          b1 = b1 + p2 * n0 + p3 * n1;
+          bP = bP + p0 * n0 + p1 * n1;
+          bT = bT + p2 * n0 + p3 * n1;
         }
       }
     } else {
@@ -462,17 +491,29 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       for (int lv = 0; lv < NLV; ++lv) {
         const int d = 1 << lv;
         const M2 nm = {up(Mm.a, d), up(Mm.b, d), up(Mm.c, d), up(Mm.d, d)};
-        const f2 n0 = up(b0, d), n1 = up(b1, d);
+        const f2 n0 = up(bP, d), n1 = up(bT, d);
         if (li >= d) {
-          b0 = b0 + Mm.a * n0 + Mm.b * n1;
-          b1 = b1 + Mm.c * n0 + Mm.d * n1;
+          bP = bP + Mm.a * n0 + Mm.b * n1;
+          bT = bT + Mm.c * n0 + Mm.d * n1;
           Mm = mmul(Mm, nm);
         }
       }
     }
-    // exclusive prefix: the (level, trend) entering this lane's chunk
-    f2 L = up(b0, 1), Tt = up(b1, 1);
-    if (li == 0) { L = l; Tt = tr; }
+    // exclusive prefix: the state entering this lane's chunk (lane 0: the
+    // lap's entering state; the shift brings lane 0 zeros)
+    f2 P, Tt;
+    if constexpr (LPP == 64) {
+      P = __builtin_elementwise_fma(l, m0, up0(bP));
+      Tt = __builtin_elementwise_fma(tr, m0, up0(bT));
+    } else {
+      // lane 32 reads lane 31 (the other half, possibly an idle lane's NaN):
+      // selected, with the shifts taken first in uniform control flow (inside
+      // a ?: arm the DPP would run under a divergent exec mask, and a DPP read
+      // from an inactive lane returns 0)
+      const f2 shP = up0(bP), shT = up0(bT);
+      P = li == 0 ? l : shP;
+      Tt = li == 0 ? tr : shT;
+    }
     int xo = RP::at(tl - base + q0);
     asm volatile("" : "+v"(xo));
     xl = xs + xo;
@@ -486,17 +527,18 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
         for (int k = 0; k < 8 && j + k < C; ++k) xg[k] = xl[(j + k) + ((j + k) >> RP::S)];
       }
       const float xq = xg[j % 8];
-      f2 lt = L + Tt;
-      f2 e = xq - (lt + s[j]);
+      const f2 d = xq - s[j];                 // off the critical path
+      f2 e = d - P;
+      f2 w = P + Tt;
       if (gen2) {                             // uniform branch: inactive steps are exact no-ops,
         asm volatile("");                     // missing samples leave e = 0
         const bool act = j < cnt;
         const bool fin = act && isfinite(xq);
-        lt = act ? lt : L;
+        w = act ? w : P;
         e = fin ? e : zero;
         nn += fin ? 1 : 0;
       }
-      L = __builtin_elementwise_fma(al, e, lt);
+      P = __builtin_elementwise_fma(cc, e, w);
       Tt = __builtin_elementwise_fma(ab, e, Tt);
       s[j] = __builtin_elementwise_fma(gs, e, s[j]);
       acc = __builtin_elementwise_fma(e, e, acc);
@@ -507,13 +549,14 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     eb += acc.y;
     n += nn;
     if constexpr (LPP == 64) {
-      l = rdl(L, last);
+      l = rdl(P, last);
       tr = rdl(Tt, last);
     } else {                                  // each half reads its own last lane
-      l = bperm2(L, (lane & ~(LPP - 1)) + last);
+      l = bperm2(P, (lane & ~(LPP - 1)) + last);
       tr = bperm2(Tt, (lane & ~(LPP - 1)) + last);
     }
   }
+  l = l - tr;                                 // (P, T) -> (level, trend)
   } else {
 #pragma unroll 1
   for (int tl = base + m; tl < T; tl += m) {
@@ -698,15 +741,27 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // ---- the best candidate so far: this pass covers candidates [g0, g1), so
   // continuing the ascending scan picks as one scan over all G would
   // (hw2_forecast_kernel's rule); a new winner parks its state in LDS
+  // The rule's outcome over [0, g1): the first smallest finite SSE, else the
+  // last candidate -- one lane per candidate (G <= 32), a wave min and two ballots
   const int g0 = 2 * pass * SL, g1 = min(G, 2 * (pass + 1) * SL);
-  int g = g0;
-  if (pass == 0) { bs = sse_s[0]; bg = 0; g = 1; }
-  for (; g < g1; ++g) {
-    const float v = sse_s[g];
-    if (v < bs || !isfinite(bs)) { bs = v; bg = g; }
+  {
+    const float inf = __builtin_inff();
+    const float v = lane < g1 ? sse_s[lane] : inf;
+    const bool fv = lane < g1 && isfinite(v);
+    float mn = fv ? v : inf;
+    mn = fminf(mn, xor_lane<1>(mn)); mn = fminf(mn, xor_lane<2>(mn)); mn = fminf(mn, xor_lane<4>(mn));
+    mn = fminf(mn, xor_lane<8>(mn)); mn = fminf(mn, xor_lane<16>(mn)); mn = fminf(mn, xor_lane<32>(mn));
+    const uint64_t at_min = __ballot(fv && v == mn);
+    if (at_min != 0) {
+      bg = (int)__builtin_ctzll(at_min);
+      bs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mn)));
+    } else {
+      bg = g1 - 1;
+      bs = sse_s[g1 - 1];
+    }
+    bs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, bs)));
+    bg = __builtin_amdgcn_readfirstlane(bg);
   }
-  bs = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, bs)));
-  bg = __builtin_amdgcn_readfirstlane(bg);
   if (bg >= g0 && (bg >> 1) == pair && pvalid) {
     const bool hi = (bg & 1) != 0;
     int p = (base + q0p) % m;
@@ -726,13 +781,16 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   {
     const float lb = lbt[0], tb = lbt[1];
     const int t0 = T % m;
+    float* fcr = fc + row * H;
     for (int h = 1 + tid; h <= H; h += nth) {
       int p = t0 + h - 1;
-      p %= m;
-      fc[row * H + (h - 1)] = lb + h * tb + sbst[p];
+      while (p >= m) p -= m;
+      fcr[h - 1] = lb + h * tb + sbst[p];
     }
-    if (season_out != nullptr)
-      for (int p = tid; p < m; p += nth) season_out[row * m + p] = sbst[p];
+    if (season_out != nullptr) {
+      float* so = season_out + row * m;
+      for (int p = tid; p < m; p += nth) so[p] = sbst[p];
+    }
     if (tid == 0) {
       sigma[row] = n > 1 ? sqrtf(bs / (float)(n - 1)) : 0.f;
       best[row] = bg;
@@ -803,6 +861,14 @@ int scan_lpp(int m) {
   return m <= kHalfMaxM ? 32 : 64;
 }
 
+int scan_debug() {
+  static const int d = [] {
+    const char* e = getenv("FOREMAST_HW_SCAN_DEBUG");
+    return e == nullptr ? 0 : atoi(e);
+  }();
+  return d;
+}
+
 long long* g_probe = nullptr;            // fm_hw_scan_set_probe: [R, 16, 8] int64 phase timings, or null
 
 template <int C>
@@ -827,7 +893,7 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
     if (lds > 65536) allow_big_lds<C, EX, FSV, LP>();                                                       \
     hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV, LP>), dim3((unsigned)R), dim3(64 * waves), lds, stream, x, \
                        ld, T, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal,  \
-                       R, ahead * (npass > 1 ? 2 : 1), npass, g_probe);                                    \
+                       R, ahead * (npass > 1 ? 2 : 1), npass | (scan_debug() << 8), g_probe);              \
   } while (0)
   const bool ex = m % C == 0;
   if (lpp == 32) {

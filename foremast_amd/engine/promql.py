@@ -32,9 +32,12 @@ class PromQLError(ValueError):
     pass
 
 
+_NEEDS_ESC = re.compile(r'[\\"\n\r\t]')
+
+
 def quote(v: str) -> str:
     """A PromQL double-quoted string literal of ``v``."""
-    if not any(c in v for c in _ESC):
+    if _NEEDS_ESC.search(v) is None:
         return '"' + v + '"'
     return '"' + "".join(_ESC.get(c, c) for c in v) + '"'
 

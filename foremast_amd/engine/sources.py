@@ -292,19 +292,30 @@ class SyntheticSource:
              stream: int = 0) -> np.ndarray:
         """[len(keys), len(t)] samples at the raw times ``t`` (multiples of
         ``step``): one vectorised pass for many series (the fake Prometheus
-        server answers a 1,000-pod union this way).  Same numbers as
-        :meth:`series` per key."""
-        from ..ops.reference import hash3, u01
+        server answers a 1,000-pod union this way; :meth:`series` is its
+        one-key case).  The seasonal terms come from per-time and per-key
+        sines (angle addition) and the parts of the counter hash that do not
+        depend on the key are computed once per time."""
+        from ..ops.reference import hash_u32, u01
         K, nt = len(keys), len(t)
         if K == 0 or nt == 0:
             return np.zeros((K, nt), np.float32)
         level, ad, aw, ph = (a[:, None] for a in self._params_of(keys))
-        tt = np.asarray(t, np.float64)[None, :]
-        season = 1 + ad * np.sin(2 * np.pi * tt / 86400.0 + ph) + aw * np.sin(2 * np.pi * tt / 604800.0 + ph)
+        tt = np.asarray(t, np.float64)
+        wd, ww = 2 * np.pi * tt / 86400.0, 2 * np.pi * tt / 604800.0
+        sph, cph = np.sin(ph), np.cos(ph)
+        season = 1 + ad * (np.sin(wd)[None, :] * cph + np.cos(wd)[None, :] * sph) \
+            + aw * (np.sin(ww)[None, :] * cph + np.cos(ww)[None, :] * sph)
+        # hash3(key, t, stream) = hash(key * P1 ^ hash(t * P2 ^ hash(stream + P3))):
+        # the key-independent part once per time
+        U = np.uint32
         kh = np.array([zlib.crc32(k.encode()) ^ self.seed for k in noise_keys], np.uint32)[:, None]
-        ti = ((np.asarray(t) / self.step).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)[None, :]
-        h1 = hash3(np.broadcast_to(kh, (K, nt)), np.broadcast_to(ti, (K, nt)), np.uint32(stream))
-        h2 = hash3(h1, np.uint32(0x68E31DA4), np.uint32(stream))
+        ti = ((tt / self.step).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
+        hs = hash_u32(np.uint32((stream + 0x165667B1) & 0xFFFFFFFF))[0]
+        inner = hash_u32((ti * U(0x85EBCA77)) ^ hs)[None, :]
+        h1 = hash_u32((kh * U(0x9E3779B1)) ^ inner)
+        c2 = hash_u32(np.uint32((0x68E31DA4 * 0x85EBCA77) & 0xFFFFFFFF) ^ hs)[0]
+        h2 = hash_u32((h1 * U(0x9E3779B1)) ^ c2)
         noise = np.sqrt(-2.0 * np.log(u01(h1).astype(np.float64))) * np.cos(2 * np.pi * u01(h2))
         v = level * season * (1 + self.noise * noise)
         if self.faults:
@@ -314,31 +325,19 @@ class SyntheticSource:
                     if sub in fk:
                         mag[i, 0] *= m
             if (mag != 1).any():
-                v = np.where(tt >= self.fault_after, v * mag, v)
+                v = np.where(tt[None, :] >= self.fault_after, v * mag, v)
         return np.maximum(v, 0).astype(np.float32)
 
     def series(self, key: str, start: float, end: float, stream: int = 0, noise_key: str | None = None,
                fault_key: str | None = None) -> Series:
         """``key`` sets the signal (level, seasonality), ``noise_key`` the
-        noise stream (one per pod), ``fault_key`` is matched against ``faults``."""
+        noise stream (one per pod), ``fault_key`` is matched against ``faults``
+        (per-(series, timestamp) counter-based noise: a sample has the same
+        value whichever window fetches it)."""
         t = self.grid(start, end)
-        level, ad, aw, ph = self._params(key)
-        fault_key = key if fault_key is None else fault_key
-        key = key if noise_key is None else noise_key
-        season = 1 + ad * np.sin(2 * np.pi * t / 86400.0 + ph) + aw * np.sin(2 * np.pi * t / 604800.0 + ph)
-        # per-(series, timestamp) counter-based noise: a sample has the same
-        # value whichever window fetches it
-        from ..ops.reference import hash3, u01
-        ti = (t / self.step).astype(np.int64) & 0xFFFFFFFF
-        kh = np.uint32(zlib.crc32(key.encode()) ^ self.seed)
-        h1 = hash3(np.full(ti.shape, kh, np.uint32), ti.astype(np.uint32), np.uint32(stream))
-        h2 = hash3(h1, np.uint32(0x68E31DA4), np.uint32(stream))
-        noise = np.sqrt(-2.0 * np.log(u01(h1).astype(np.float64))) * np.cos(2 * np.pi * u01(h2))
-        v = level * season * (1 + self.noise * noise)
-        for sub, mag in self.faults.items():
-            if sub in fault_key:
-                v = np.where(t >= self.fault_after, v * mag, v)
-        return Series({"__name__": key.split("|")[0]}, t, np.maximum(v, 0).astype(np.float32))
+        v = self.many([key], [key if noise_key is None else noise_key], [key if fault_key is None else fault_key],
+                      t, stream)[0]
+        return Series({"__name__": key.split("|")[0]}, t, v)
 
     def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
         """Vectorised answer for many app-level queries over one window
@@ -357,32 +356,17 @@ class SyntheticSource:
                     g = False
                 else:
                     metric = q.split("{")[0].replace("namespace_pod_", "").replace("namespace_app_pod_", "")
-                    key = metric + "|" + _app_of(q)
-                    level, ad, aw, ph = self._params(key)
-                    mag = 1.0
-                    for sub, m in self.faults.items():
-                        if sub in q:
-                            mag *= m
-                    g = (np.uint32(zlib.crc32(key.encode()) ^ self.seed), level, ad, aw, ph, mag)
+                    g = (metric + "|" + _app_of(q), q)
                 info[tpl] = g
             (rows if g else slow).append(i)
         K, nt = len(rows), len(t)
         out_t = np.tile(t, (K, 1))
         vals = np.zeros((K, nt), np.float32)
         if K and nt:
-            from ..ops.reference import hash3, u01
+            # the same generator as fetch (series): identical samples
             p = [info[templates[i]] for i in rows]
-            kh = np.array([g[0] for g in p], np.uint32)[:, None]
-            level, ad, aw, ph, mag = (np.array([g[j] for g in p])[:, None] for j in range(1, 6))
-            season = 1 + ad * np.sin(2 * np.pi * t[None, :] / 86400.0 + ph) + \
-                aw * np.sin(2 * np.pi * t[None, :] / 604800.0 + ph)
-            ti = ((t / self.step).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)[None, :]
-            h1 = hash3(np.broadcast_to(kh, (K, nt)), np.broadcast_to(ti, (K, nt)), np.uint32(0))
-            h2 = hash3(h1, np.uint32(0x68E31DA4), np.uint32(0))
-            noise = np.sqrt(-2.0 * np.log(u01(h1).astype(np.float64))) * np.cos(2 * np.pi * u01(h2))
-            v = level * season * (1 + self.noise * noise)
-            v = np.where(t[None, :] >= self.fault_after, v * mag, v)
-            vals = np.maximum(v, 0).astype(np.float32)
+            keys = [g[0] for g in p]
+            vals = self.many(keys, keys, [g[1] for g in p], t)
         got: list = [None] * len(templates)
         for k, i in enumerate(rows):
             got[i] = [Series({}, out_t[k], vals[k])]
