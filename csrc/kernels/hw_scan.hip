@@ -372,6 +372,19 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   float bs = 0.f;
   float* lbt = wsum + 144;                  // the winner's level, trend
   float* sbst = wsum + 160;                 // the winner's seasons by absolute phase [m]
+  // FS: the first season's indices (the same for every candidate) in the
+  // lanes' register order, [C][LPP] pairs: a pass loads its C seasons with C
+  // conflict-free ds_read_b64 instead of recomputing them
+  f2* s0T = reinterpret_cast<f2*>(sbst + ((m + 3) & ~3));
+  if constexpr (FS) {
+    for (int i = tid; i < C * LPP; i += nth) {
+      const int j = i / LPP, q = (i % LPP) * C + j;
+      const float v = (q < m && base + q < T) ? xs[RP::at(q)] : __builtin_nanf("");
+      const float si = isfinite(v) ? v - m1 : 0.f;
+      s0T[i] = (f2){si, si};
+    }
+    __syncthreads();
+  }
   long long pc1 = 0, pc2 = 0, pcs = 0;
 #pragma unroll 1
   for (int pass = 0; pass < npass; ++pass) {
@@ -390,7 +403,10 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   if constexpr (FS) l = l + tr;             // the FS laps carry P = level + trend
   int q0p = q0;
   asm volatile("" : "+v"(q0p));
-  if (base < T) {
+  if constexpr (FS) {
+#pragma unroll
+    for (int j = 0; j < C; ++j) s[j] = s0T[j * LPP + li];
+  } else if (base < T) {
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       const int q = q0p + j;
@@ -711,12 +727,11 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   }
   }  // !FS
   if (probe != nullptr) pc2 = clock64();
-  ea = group_sum<LPP>(ea);
-  eb = group_sum<LPP>(eb);
+  // lanes' fp64 lap sums, reduced across the lanes in fp32 (the SSE is fp32)
+  const float fa = group_sum<LPP>((float)ea), fb = group_sum<LPP>((float)eb);
   n = __builtin_amdgcn_readfirstlane(group_sum<LPP>(n));   // the same for every candidate
 
   // ---- per-candidate results
-  const float fa = (float)ea, fb = (float)eb;
   const float tph = (float)(T % m);
   if (li == 0 && pvalid) {
     const int64_t pa = row * G + ga;
@@ -945,7 +960,8 @@ ScanPlan scan_plan(int T, int G, int m) {
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
   const size_t lds = words * 4 + (size_t)(kMaxG / 2) * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4 + 64 * 4 +
-                     32 * 4 + (size_t)((m + 3) & ~3) * 4;   // wsum | DMA landing zone | wmin, lbt | seasons
+                     32 * 4 + (size_t)((m + 3) & ~3) * 4 +  // wsum | DMA landing zone | wmin, lbt | seasons
+                     (size_t)C * lpp * 8;                     // | first-season pairs (FS)
   if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return p;
   p.C = C;
   p.lpp = lpp;

@@ -75,12 +75,13 @@ def main() -> None:
     mhz = 2100.0
     w0 = p[:, 0, 6].astype(np.float64) / 100.0                  # us
     w1 = w0 + row_cyc / mhz
-    gaps = []
+    gaps, sdiff = [], []
     key = (xcc * 8 + se) * 16 + cu
     for k in np.unique(key):
         idx = np.nonzero(key == k)[0]
         o = idx[np.argsort(w0[idx])]
         gaps.extend((w0[o[1:]] - w1[o[:-1]]).tolist())
+        sdiff.extend(np.diff(w0[o]).tolist())        # lockstep rows: ~0 / ~row; staggered: ~row / 2
     print(json.dumps({"rows": a.rows, "T": a.T, "m": a.m, "fit_ms": round(plain_ms, 3),
                       "fit_ms_probed": round(probe_ms, 3), "waves": nw,
                       "row_cycles": q(row_cyc),
@@ -93,7 +94,9 @@ def main() -> None:
                       "end_at": q(ce.max(1) - t0),
                       "waves_per_simd_sorted": np.sort(per_simd, 1)[:, ::-1].mean(0).round(2).tolist(),
                       "cus_seen": int(len(np.unique(key))),
-                      "gap_between_rows_us": q(np.asarray(gaps)) if gaps else None}), flush=True)
+                      "gap_between_rows_us": q(np.asarray(gaps)) if gaps else None,
+                      "start_diff_us": {f"p{k}": round(float(np.percentile(sdiff, k)), 1) for k in (10, 25, 50, 75, 90)}
+                      if sdiff else None}), flush=True)
 
 
 if __name__ == "__main__":
