@@ -440,6 +440,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // so the scheduler has independent work for the hazard slots.  The powers
   // in pw are of A = [[1 - c, 1], [-a b, 1]] (powers() for FS).
   const f2 cc = al + ab;
+  f2 accp = zero;                             // this lane's SSE over the laps (fp32: <= C * laps terms)
   int lap = 0;
 #pragma unroll 1
   for (int tl = dbg == 2 ? T : base + m; tl < T; tl += m, ++lap) {
@@ -454,7 +455,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     // pass 2 needs the masked arithmetic for gaps and for inactive steps
     // (a partial last lap; every lap when the chunks do not tile the season)
     const bool gen2 = gaps || !EXACT || nact != m;
-    const float* xl = xs + RP::at(tl - base + q0);
+    const int xo0 = RP::at(tl - base + q0);
+    const float* xl = xs + xo0;
     // pass 1 (lanes before `last` feed the scan; their chunks are full):
     // lane 0 starts from the lap's entering state, the others from zero
     f2 bP = l * m0, bT = tr * m0;
@@ -530,10 +532,10 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       P = li == 0 ? l : shP;
       Tt = li == 0 ? tr : shT;
     }
-    int xo = RP::at(tl - base + q0);
+    int xo = xo0;
     asm volatile("" : "+v"(xo));
     xl = xs + xo;
-    f2 acc = zero;
+    f2 acc = accp;
     int nn = 0;
 #pragma unroll
     for (int j = 0; j < C; ++j) {
@@ -559,11 +561,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
       s[j] = __builtin_elementwise_fma(gs, e, s[j]);
       acc = __builtin_elementwise_fma(e, e, acc);
     }
-    if (!gen2) nn = C;
-    if (q0 >= m) { acc = zero; nn = 0; }      // idle lanes ran past the season
-    ea += acc.x;
-    eb += acc.y;
-    n += nn;
+    accp = acc;
+    n += gen2 ? nn : C;
     if constexpr (LPP == 64) {
       l = rdl(P, last);
       tr = rdl(Tt, last);
@@ -573,6 +572,9 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     }
   }
   l = l - tr;                                 // (P, T) -> (level, trend)
+  if (q0 >= m) { accp = zero; n = 0; }        // idle lanes ran past the season
+  ea = accp.x;
+  eb = accp.y;
   } else {
 #pragma unroll 1
   for (int tl = base + m; tl < T; tl += m) {
