@@ -403,6 +403,11 @@ def config3e2e(args):
 
     req_log = []
     cyc_ms: list[float] = []
+    # FOREMAST_PROFILE_CYCLES=<path>: cProfile of the timed cycles only
+    _prof = None
+    if os.environ.get("FOREMAST_PROFILE_CYCLES"):
+        import cProfile
+        _prof = cProfile.Profile()
 
     def step():
         # cycles every poll interval inside the jobs' watch window (staged:
@@ -413,7 +418,10 @@ def config3e2e(args):
             cw.set(t["now"])
         n0 = (live.requests, live.bytes) if live is not None else (0, 0)
         tc = time.perf_counter()
-        r = brain.run_once()
+        if _prof is not None and len(cyc_ms) >= args.warmup:
+            r = _prof.runcall(brain.run_once)
+        else:
+            r = brain.run_once()
         cyc_ms.append(1e3 * (time.perf_counter() - tc))
         rows.append(r.get("rows", 0))
         if live is not None:
@@ -454,6 +462,8 @@ def config3e2e(args):
         if prom is not None:
             prom.terminate()
             prom.wait(30)
+    if _prof is not None:
+        _prof.dump_stats(os.environ["FOREMAST_PROFILE_CYCLES"])
     restart = None
     if args.restart:
         # warm restart: checkpoint engine + resident history,

@@ -316,7 +316,8 @@ class SyntheticSource:
         h1 = hash_u32((kh * U(0x9E3779B1)) ^ inner)
         c2 = hash_u32(np.uint32((0x68E31DA4 * 0x85EBCA77) & 0xFFFFFFFF) ^ hs)[0]
         h2 = hash_u32((h1 * U(0x9E3779B1)) ^ c2)
-        noise = np.sqrt(-2.0 * np.log(u01(h1).astype(np.float64))) * np.cos(2 * np.pi * u01(h2))
+        # Box-Muller in fp32 (the samples are fp32)
+        noise = np.sqrt(np.float32(-2.0) * np.log(u01(h1))) * np.cos(np.float32(2 * np.pi) * u01(h2))
         v = level * season * (1 + self.noise * noise)
         if self.faults:
             mag = np.ones((K, 1))
