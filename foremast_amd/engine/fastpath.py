@@ -399,7 +399,7 @@ class FastPath:
         self._cmp = {}            # device compaction buffers per capacity
         self._col: dict = {}      # column-wise fetched windows of sliding groups (consumed by _arrays)
         self._ring = None         # merged sliding mode: host ring of the newest grid columns
-        self._ring_c = None
+        self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
         self._slide_state: dict = {}
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
@@ -894,9 +894,11 @@ class FastPath:
         hlo = wins["historical"][0]
         hi = math.floor(now / step + 1e-9) * step
         wr, wt, wv = [], [], []
+        fresh = []                                # rows without a sample yet: empty ring rows
         for m in range(M):
             tpls, stores = lists[("hist_urls", m)], lists[("hist_stores", m)]
             since = st.last_t[rows[:, m]]
+            fresh.append(rows[~np.isfinite(since), m])
             lo = np.where(np.isfinite(since), since + step, math.ceil(hlo / step - 1e-9) * step)
             for lo_v in np.unique(lo):
                 if hi < lo_v:
@@ -910,10 +912,11 @@ class FastPath:
                     wr.append(np.repeat(rows[sel, m], lens))
                     wt.append(t)
                     wv.append(v)
+        fresh_rows = np.concatenate(fresh) if fresh else None
         if wr:
             r, t, v = np.concatenate(wr), np.concatenate(wt), np.concatenate(wv)
             st.write_sliding_flat(r, t, v)
-            self._ring_write(r, t, v)
+            self._ring_write(r, t, v, fresh_rows)
         flat = rows.reshape(-1).astype(np.int64)
         (clo, chi), (blo, bhi) = wins["current"], wins["baseline"]
         cur, cur_t = self._ring_read(flat, clo, chi)
@@ -934,37 +937,59 @@ class FastPath:
     # host ring of the newest grid columns of every sliding row (merged mode)
     RING = 64
 
-    def _ring_write(self, r: np.ndarray, t: np.ndarray, v: np.ndarray) -> None:
+    def _ring_write(self, r: np.ndarray, t: np.ndarray, v: np.ndarray, fresh: np.ndarray | None = None) -> None:
+        """Samples (row r, time t, value v) into the ring, slot = grid column
+        mod RING.  The ring holds only the newest RING columns: a slot is
+        cleared (NaN) when its column comes into range, so a read needs no
+        per-slot column check; ``fresh`` rows (newly assigned) start empty."""
         n = self.sliding.buf.shape[0]
         if self._ring is None or self._ring.shape[0] < n:
-            ring = np.full((n, self.RING), np.nan, np.float32)
-            rc = np.full((n, self.RING), -1, np.int64)
+            ring = np.full((max(n, 1), self.RING), np.nan, np.float32)
             if self._ring is not None:
                 ring[:self._ring.shape[0]] = self._ring
-                rc[:self._ring.shape[0]] = self._ring_c
-            self._ring, self._ring_c = ring, rc
+            self._ring = ring
+        if fresh is not None and len(fresh):
+            self._ring[fresh] = np.nan
         ck = np.rint(t / self.b.step).astype(np.int64)
-        ok = np.isfinite(v)
-        r, ck, v = r[ok], ck[ok], v[ok]
-        j = ck % self.RING
-        self._ring[r, j] = v
-        self._ring_c[r, j] = ck
+        if not len(ck):
+            return
+        top = int(ck.max())
+        if self._ring_top is None or top - self._ring_top >= self.RING:
+            if self._ring_top is not None:
+                self._ring[:] = np.nan
+            self._ring_top = top
+        elif top > self._ring_top:
+            cols = np.arange(self._ring_top + 1, top + 1) % self.RING
+            self._ring[:, cols] = np.nan
+            self._ring_top = top
+        keep = np.isfinite(v) & (ck > self._ring_top - self.RING)
+        self._ring[r[keep], ck[keep] % self.RING] = v[keep]
 
     def _ring_read(self, rows: np.ndarray, lo: float, hi: float) -> tuple[np.ndarray, np.ndarray]:
         """Values [R, n] / times [R, n] of the grid points in [lo, hi] (NaN:
-        no sample) from the host ring."""
+        no sample) from the host ring: row gathers of at most two contiguous
+        slot ranges; the times are one broadcast row (read-only)."""
         step = self.b.step
         c0, c1 = math.ceil(lo / step - 1e-9), math.floor(hi / step + 1e-9)
         n = max(0, c1 - c0 + 1)
         if n > self.RING:
             raise ValueError(f"window of {n} steps exceeds the sliding ring ({self.RING})")
-        ck = np.arange(c0, c0 + n, dtype=np.int64)
-        if self._ring is None or n == 0 or not len(rows):
+        if self._ring is None or n == 0 or not len(rows) or self._ring_top is None:
             return np.full((len(rows), max(1, n)), np.nan, np.float32), np.full((len(rows), max(1, n)), np.nan)
-        j = ck % self.RING
-        v = self._ring[rows[:, None], j[None, :]]
-        v = np.where(self._ring_c[rows[:, None], j[None, :]] == ck[None, :], v, np.float32(np.nan))
-        t = np.broadcast_to(ck * step, v.shape).astype(np.float64)
+        t = np.broadcast_to(np.arange(c0, c0 + n, dtype=np.float64) * step, (len(rows), n))
+        if c1 <= self._ring_top - self.RING or c0 > self._ring_top:
+            return np.full((len(rows), n), np.nan, np.float32), t
+        sub = self._ring[rows]
+        j0 = c0 % self.RING
+        if j0 + n <= self.RING:
+            v = sub[:, j0:j0 + n]
+        else:
+            v = np.concatenate([sub[:, j0:], sub[:, :j0 + n - self.RING]], axis=1)
+        lo_ok, hi_ok = max(c0, self._ring_top - self.RING + 1), min(c1, self._ring_top)
+        if lo_ok > c0 or hi_ok < c1:           # columns outside the ring's range read NaN
+            v = v.copy()
+            v[:, :lo_ok - c0] = np.nan
+            v[:, hi_ok - c0 + 1:] = np.nan
         return v, t
 
     def fetch(self, fw: FastWork, now: float) -> FastWork:
