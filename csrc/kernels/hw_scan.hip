@@ -140,7 +140,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   using RP = RowPad<C, EXACT>;
   // FOREMAST_HW_SCAN_DEBUG (instruction accounting with PMC, results are
   // garbage): 1 = stop after the row setup, 2 = skip the season laps
-  const int dbg = npass >> 8;
+  const int dbg = (npass >> 8) & 255;
+  const bool use_s0 = FS && (npass >> 16) != 0;   // LDS room for the first-season pairs
   npass &= 255;
   const long long pc0 = probe != nullptr ? clock64() : 0, pw0 = probe != nullptr ? wall_clock64() : 0;
   extern __shared__ float lds[];
@@ -266,12 +267,26 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   {
     const int e1 = min(base + m, T), e2 = min(base + 2 * m, T);
     if (rs) {
+      const bool b4 = (base & 3) == 0;        // float4s stay whole in the padded row (S >= 2)
 #pragma unroll
       for (int k = 0; k < KREG; ++k) {
         const float vv[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+        const int i0 = (k * nth + tid) * 4;
+        if (b4 && i0 >= base && i0 + 4 <= T) {
+          // whole float4 inside the row: 4 stores at consecutive padded slots;
+          // all finite and inside one season -> the sums without selects
+          const int r0 = i0 - base;
+          float* dst = xs + RP::at(r0);
+          dst[0] = vv[0]; dst[1] = vv[1]; dst[2] = vv[2]; dst[3] = vv[3];
+          const bool fin = isfinite(vv[0]) && isfinite(vv[1]) && isfinite(vv[2]) && isfinite(vv[3]);
+          const float s4 = (vv[0] + vv[1]) + (vv[2] + vv[3]);
+          if (fin && i0 + 4 <= e1) { sa1 += s4; fa1 += 4.f; continue; }
+          if (fin && i0 >= e1 && i0 + 4 <= e2) { sb1 += s4; fb1 += 4.f; continue; }
+          if (fin && i0 >= e2) continue;
+        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const int i = (k * nth + tid) * 4 + c;
+          const int i = i0 + c;
           if (i >= base && i < T) {
             const float v = vv[c];
             const bool f = isfinite(v);
@@ -376,7 +391,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // lanes' register order, [C][LPP] pairs: a pass loads its C seasons with C
   // conflict-free ds_read_b64 instead of recomputing them
   f2* s0T = reinterpret_cast<f2*>(sbst + ((m + 3) & ~3));
-  if constexpr (FS) {
+  if (use_s0) {
     for (int i = tid; i < C * LPP; i += nth) {
       const int j = i / LPP, q = (i % LPP) * C + j;
       const float v = (q < m && base + q < T) ? xs[RP::at(q)] : __builtin_nanf("");
@@ -403,7 +418,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   if constexpr (FS) l = l + tr;             // the FS laps carry P = level + trend
   int q0p = q0;
   asm volatile("" : "+v"(q0p));
-  if constexpr (FS) {
+  if (use_s0) {
 #pragma unroll
     for (int j = 0; j < C; ++j) s[j] = s0T[j * LPP + li];
   } else if (base < T) {
@@ -891,7 +906,7 @@ long long* g_probe = nullptr;            // fm_hw_scan_set_probe: [R, 16, 8] int
 template <int C>
 int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
                float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
-               float* season_out, size_t lds, int xal, int lpp, int npass, hipStream_t stream) {
+               float* season_out, size_t lds, int xal, int lpp, int npass, int s0, hipStream_t stream) {
   const int GP = (G + 1) / 2;
   const int slots = lpp == 64 ? GP : (GP + 1) / 2;          // waves for one pass over the pairs
   const int waves = (slots + npass - 1) / npass;
@@ -910,7 +925,7 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
     if (lds > 65536) allow_big_lds<C, EX, FSV, LP>();                                                       \
     hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV, LP>), dim3((unsigned)R), dim3(64 * waves), lds, stream, x, \
                        ld, T, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal,  \
-                       R, ahead * (npass > 1 ? 2 : 1), npass | (scan_debug() << 8), g_probe);              \
+                       R, ahead * (npass > 1 ? 2 : 1), npass | (scan_debug() << 8) | (s0 << 16), g_probe);  \
   } while (0)
   const bool ex = m % C == 0;
   if (lpp == 32) {
@@ -939,7 +954,7 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
 // decides, for the launcher and for the Python-side shape query
 // (fm_hw_scan_supported), so the two can never disagree.
 struct ScanPlan {
-  int C = 0, lpp = 64, npass = 1;
+  int C = 0, lpp = 64, npass = 1, s0 = 0;
   size_t lds = 0;
 };
 
@@ -962,8 +977,7 @@ ScanPlan scan_plan(int T, int G, int m) {
   const int S = (m % C == 0 && C % 4 == 0) ? __builtin_ctz(C) : 31;   // RowPad<C, EXACT>::S
   const size_t words = ((size_t)(T + 64 * C) + (S < 31 ? (size_t)(T + 64 * C) >> S : 0) + 1 + 3) & ~(size_t)3;
   const size_t lds = words * 4 + (size_t)(kMaxG / 2) * kLevels * 8 * 4 + kMaxG * 4 + 16 + kMaxLaps * 4 + 16 * 4 * 4 + 64 * 4 +
-                     32 * 4 + (size_t)((m + 3) & ~3) * 4 +  // wsum | DMA landing zone | wmin, lbt | seasons
-                     (size_t)C * lpp * 8;                     // | first-season pairs (FS)
+                     32 * 4 + (size_t)((m + 3) & ~3) * 4;   // wsum | DMA landing zone | wmin, lbt | seasons
   if (lds > kMaxLds || (T - m) / m >= kMaxLaps) return p;
   p.C = C;
   p.lpp = lpp;
@@ -974,6 +988,13 @@ ScanPlan scan_plan(int T, int G, int m) {
   const int slots = lpp == 64 ? GP : (GP + 1) / 2;
   if (scan_fast_setup() && slots > kPassWaves && 2 * lds <= kMaxLds && scan_passes_allowed())
     p.npass = (slots + kPassWaves - 1) / kPassWaves;
+  // the first-season pairs (C x lpp, FS) when they fit beside the row (and
+  // keep two rows per CU when the candidates run in passes)
+  const size_t s0b = (size_t)C * lpp * 8;
+  if (scan_fast_setup() && (p.npass > 1 ? 2 : 1) * (lds + s0b) <= kMaxLds) {
+    p.lds = lds + s0b;
+    p.s0 = 1;
+  }
   return p;
 }
 }  // namespace
@@ -996,13 +1017,13 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   if (H < 0) return (int)hipErrorInvalidValue;
   const ScanPlan pl = scan_plan(T, G, m);
   if (pl.C == 0) return (int)hipErrorInvalidValue;
-  const int C = pl.C, lpp = pl.lpp, npass = pl.npass;
+  const int C = pl.C, lpp = pl.lpp, npass = pl.npass, s0 = pl.s0;
   const size_t lds = pl.lds;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \
     return launch_one<CC>(x, ld, T, R, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale,    \
-                          season_out, lds, xal, lpp, npass, stream);
+                          season_out, lds, xal, lpp, npass, s0, stream);
   switch (C) {
     FM_HWS(4) FM_HWS(5) FM_HWS(6) FM_HWS(8) FM_HWS(9) FM_HWS(12) FM_HWS(16) FM_HWS(18) FM_HWS(20) FM_HWS(23)
     FM_HWS(24)
