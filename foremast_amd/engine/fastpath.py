@@ -243,6 +243,7 @@ class LazyHist:
 
 
 _NOSPEC = object()
+_version_of = __import__("operator").attrgetter("version")
 
 
 @functools.lru_cache(maxsize=65536)
@@ -519,6 +520,15 @@ class FastPath:
             return fast, []
         self._reused = False
         works = self.works
+        # every job known at its version (the steady state of a fleet that only
+        # lost jobs since the last claim): the lists through C-level passes
+        fws = list(map(works.get, batch.ids))
+        if None not in fws and list(map(_version_of, fws)) == list(batch.versions):
+            todo = [fw for fw in fws if not ((immutable or fw.wcur is not None) and fw.settled)]
+            self._specs = {}
+            self.todo = todo
+            self._last = (batch.ids, batch.versions, fws, todo)
+            return fws, []
         fast, unknown, todo = [], [], []
         handles = getattr(batch, "handles", None)
         for k, (jid, ver) in enumerate(zip(batch.ids, batch.versions)):
@@ -923,14 +933,15 @@ class FastPath:
         base = self._ring_read(flat, blo, bhi)[0] if memo[3][1] else None
         cur_len = np.isfinite(cur).sum(1)
         wclass = 0 if cur.shape[1] <= 128 else (1 if cur.shape[1] <= 256 else 2)
-        if self._slide_state.get(p0.group) != (id(ws), wclass):
+        prev = self._slide_state.get(p0.group)
+        if prev is None or prev[0] is not ws or prev[1] != wclass:   # holds ws: an id() could be reused
             for fw in ws:
                 fw.has_window = True
                 fw.dirty = True
                 fw.settled = False
                 fw.wclass = wclass
                 fw.hist = []
-            self._slide_state[p0.group] = (id(ws), wclass)
+            self._slide_state[p0.group] = (ws, wclass)
         self._col[p0.group] = {"ids": ids, "cur": cur, "cur_t": cur_t, "cur_len": cur_len, "base": base,
                                "base_len": None, "hist_end": wins["historical"][1]}
 

@@ -102,7 +102,9 @@ def _hw_scan_supported_py(T: int, G: int, m: int) -> bool:
     n = T + 64 * C
     S = (C & -C).bit_length() - 1 if (m % C == 0 and C % 4 == 0) else None    # bank-skew padding shift
     words = (n + (n >> S if S is not None else 0) + 1 + 3) & ~3
-    lds = words * 4 + ((G + 1) // 2) * 6 * 8 * 4 + 32 * 4 + 16 + 128 * 4 + 16 * 4 * 4 + 64 * 4
+    # row | pw (16 pair slots x 6 levels x 4 pairs) | sse | base, lap flags | wave sums, DMA zone,
+    # minima, winner state | winner seasons (the first-season pairs are optional)
+    lds = words * 4 + 16 * 6 * 8 * 4 + 32 * 4 + 16 + 128 * 4 + 16 * 4 * 4 + 64 * 4 + 32 * 4 + ((m + 3) & ~3) * 4
     return lds <= 160 * 1024
 
 
