@@ -38,7 +38,7 @@ import html
 import json
 import logging
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from datetime import datetime, timezone
 
 import numpy as np
@@ -149,6 +149,7 @@ class GroupArrays:
     impact_slots: np.ndarray | None = None     # exporter slots of the downstream-impact gauge
     marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
     models: object = None                      # ModelArrays of a forecasting group (cached with the arrays)
+    prev_models: object = None                 # the previous arrays' ModelArrays (sliding: shift-only update)
     key: tuple | None = None                   # the group key these arrays were built under
     wcur: np.ndarray | None = None             # [S * M] window-table ids of a table group's rows
     wbase: np.ndarray | None = None
@@ -181,6 +182,7 @@ class ModelArrays:
     stamp: object
     subs: list
     lastk: torch.Tensor                        # [R] newest finite current point of each row
+    inc: tuple | None = None                   # sliding groups: state of the shift-only update
 
 
 @dataclass
@@ -402,6 +404,7 @@ class FastPath:
         self._ring = None         # merged sliding mode: host ring of the newest grid columns
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
         self._slide_state: dict = {}
+        self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
         self._gstat: dict = {}    # group key -> (job ids, positions, per-job static columns)
@@ -933,15 +936,17 @@ class FastPath:
         base = self._ring_read(flat, blo, bhi)[0] if memo[3][1] else None
         cur_len = np.isfinite(cur).sum(1)
         wclass = 0 if cur.shape[1] <= 128 else (1 if cur.shape[1] <= 256 else 2)
+        # per-job state only when the job set or the window class changed (the
+        # group's arrays are rebuilt from self._col every cycle regardless)
         prev = self._slide_state.get(p0.group)
-        if prev is None or prev[0] is not ws or prev[1] != wclass:   # holds ws: an id() could be reused
+        if prev is None or prev[1] != wclass or prev[0] != ids:
             for fw in ws:
                 fw.has_window = True
                 fw.dirty = True
                 fw.settled = False
                 fw.wclass = wclass
                 fw.hist = []
-            self._slide_state[p0.group] = (ws, wclass)
+            self._slide_state[p0.group] = (ids, wclass)
         self._col[p0.group] = {"ids": ids, "cur": cur, "cur_t": cur_t, "cur_len": cur_len, "base": base,
                                "base_len": None, "hist_end": wins["historical"][1]}
 
@@ -1143,19 +1148,19 @@ class FastPath:
         if works[0].wcur is not None:
             return self._arrays_table(works, key)
         ga = self._garr.get(key)
-        if ga is not None and ga.works is works and self._reused and not self.todo:
+        p0 = works[0].plan
+        col = self._col.get(p0.group)                     # column-wise fetched this cycle: rebuild
+        if col is None and ga is not None and ga.works is works and self._reused and not self.todo:
             return ga                     # same job list object, nothing fetched: nothing changed
         ident = self._jid(works)
-        if ga is not None and ga.ident == ident and not any(fw.dirty for fw in works):
+        if col is None and ga is not None and ga.ident == ident and not any(fw.dirty for fw in works):
             ga.works = works
             return ga
-        p0 = works[0].plan
         M = len(p0.aliases)
         S = len(works)
         dev = self.b.device
         store = self.sliding if p0.sliding else self.static
         R = S * M
-        col = self._col.get(p0.group)
         pos = None
         if col is not None:                               # column-wise fetched this cycle
             pos = True if col["ids"] == ident else ident.index_in(col["ids"])
@@ -1180,6 +1185,9 @@ class FastPath:
                          up(rowmap), end, ~(has_hist & has_cur), handles=handles, works=works)
         if col is not None and pos is not None:
             ga.hist_end = col.get("hist_end")
+            old = self._garr.get(key)
+            if old is not None and old.ident == ident:
+                ga.prev_models = old.models if old.models is not None else old.prev_models
         if xslots is not None:
             ga.export_slots = xslots
             ga.export_start = self.b.exporter.contiguous_start(xslots)
@@ -1412,6 +1420,14 @@ class FastPath:
         md = ga.models
         if md is not None and md.stamp == stamp:
             return md
+        prev = md if md is not None else ga.prev_models
+        ga.prev_models = None
+        if prev is not None and store.sliding and prev.inc is not None:
+            nd = self._model_arrays_slid(prev, ga, store, stamp)
+            if nd is not None:
+                self.model_slides += 1
+                ga.models = nd
+                return nd
         from ..models import zoo
         b = self.b
         cfg = b.cfg
@@ -1474,7 +1490,57 @@ class FastPath:
                                  view(kl).to(torch.int32), T, zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev),
                                  keys, tl, view(kv).to(torch.int32), view(kh).reshape(hshape), hmax, len(ms)))
         md = ga.models = ModelArrays(stamp, subs, view(k_last))
+        if store.sliding and np.isfinite(t_last).all() and ga.cur_t.shape[0] and ga.cur_t.strides[0] == 0:
+            # state for the next cycle's shift-only update (_model_arrays_slid)
+            md.inc = (t_last, T, store.t0, store.ws, n, float(ga.cur_t[0, 0]), valid, lastk)
         return md
+
+    def _model_arrays_slid(self, md: "ModelArrays", ga: GroupArrays, store: ResidentHistory, stamp):
+        """The previous cycle's ModelArrays moved by a sliding step: when every
+        row's newest history sample, the window start and the current
+        window's times all advanced by the same k grid columns (the steady
+        state of a polled fleet: one new sample per row), the dense length,
+        the horizons and the cache keys are unchanged and the row alignment
+        moves by k -- two device adds instead of rebuilding and uploading
+        every per-row array.  None: anything else changed (rebuild)."""
+        t_prev, T, t0, ws, n, ct0, valid_prev, lastk_prev = md.inc
+        if store.t0 != t0 or ga.cur.shape[1] != n or ga.cur_t.strides[0] != 0:
+            return None
+        step = store.step
+        rowmap = ga.rowmap.astype(np.int64)
+        lt = self._hist_last(store.last_t[rowmap], step, ga.hist_end)
+        d = lt - t_prev
+        dt = float(d[0]) if len(d) else 0.0
+        k = int(round(dt / step))
+        if (k <= 0 or abs(k * step - dt) > 1e-6 * step or store.ws - ws != k
+                or float(ga.cur_t[0, 0]) - ct0 != dt or not (d == dt).all()):
+            return None
+        # the row ends (lim) moved by k: none may pass the grid's end
+        if int(store.col(float(lt.max()))) + 1 > store.e:
+            return None
+        cfg = self.b.cfg
+        dev = self.b.device
+        fin = np.isfinite(ga.cur)
+        valid = ((store.nfin[rowmap] >= max(cfg.min_historical_points, 1)).astype(np.int32)
+                 | (fin.any(1).astype(np.int32) << 1))
+        if fin[:, -1].all():
+            lastk = lastk_prev if (lastk_prev == n - 1).all() else np.full(len(rowmap), n - 1, np.int64)
+        else:
+            lastk = np.where(fin.any(1), n - 1 - np.argmax(fin[:, ::-1], axis=1), n - 1)
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=False)  # noqa: E731
+        vchg = not np.array_equal(valid, valid_prev)
+        subs = []
+        for s in md.subs:
+            rows = None if s.idx is None else (np.arange(len(ga.ids))[:, None] * (len(rowmap) // len(ga.ids))
+                                               + np.asarray(s.ms)[None, :]).reshape(-1)
+            pick = (lambda a: a) if rows is None else (lambda a: a[rows])  # noqa: E731
+            subs.append(replace(
+                s, shift=s.shift - k, lim=s.lim + k, t_last=pick(lt),
+                valid=up(pick(valid).astype(np.int32)) if vchg else s.valid))
+        lk = md.lastk if lastk is lastk_prev or np.array_equal(lastk, lastk_prev) else up(lastk.astype(np.int64))
+        nd = ModelArrays(stamp, subs, lk)
+        nd.inc = (lt, T, t0, store.ws, n, float(ga.cur_t[0, 0]), valid, lastk)
+        return nd
 
     def _score_models(self, works: list[FastWork], now: float, ga: GroupArrays, store: ResidentHistory) -> dict:
         """A group whose metrics use forecasting / other models: pairwise

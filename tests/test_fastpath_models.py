@@ -148,6 +148,9 @@ def test_models_fast_path_equals_general_path(algo, kind, device="cpu"):
         _compare(a, b, ids, cyc)
         a[0].t += 60
         b[0].t += 60
+    if kind != "static" and algo not in ("moving_average", "bivariate_normal"):
+        # the sliding group's model arrays moved by the poll step, not rebuilt
+        assert a[3].fast.model_slides > 0
 
 
 def test_cached_holt_winters_steady_state_reads_only_new_columns(monkeypatch):
