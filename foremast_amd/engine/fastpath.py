@@ -245,6 +245,37 @@ class LazyHist:
 
 
 _NOSPEC = object()
+
+
+def _bcast_row(a: np.ndarray) -> np.ndarray | None:
+    """The row of a [R, n] array that is one finite row broadcast over R
+    (merged sliding windows' times), else None."""
+    if a.ndim != 2 or not a.shape[0] or a.strides[0] != 0:
+        return None
+    r = a[0]
+    return r if np.isfinite(r).all() else None
+
+
+def _last_finite(cur: np.ndarray) -> np.ndarray:
+    """Column of the newest finite point of every row (n - 1 for rows with
+    none): the last column decides for almost every row, only the rest are
+    searched."""
+    R, n = cur.shape
+    last = np.full(R, max(n - 1, 0), np.int64)
+    if not n or not R:
+        return last
+    bad = np.flatnonzero(~np.isfinite(cur[:, -1]))
+    if len(bad):
+        f = np.isfinite(cur[bad])
+        last[bad] = np.where(f.any(1), n - 1 - np.argmax(f[:, ::-1], axis=1), n - 1)
+    return last
+
+
+def _device_horizons(trow: torch.Tensor, t_last: torch.Tensor, step: float) -> torch.Tensor:
+    """[rows, n] int64 horizons max(1, rint((t - t_last) / step)) of a
+    broadcast time row (1 where a row has no history)."""
+    h = torch.round((trow[None, :] - t_last[:, None]) / step)
+    return torch.nan_to_num(h, nan=1.0).clamp_(min=1).to(torch.int64)
 _version_of = __import__("operator").attrgetter("version")
 
 
@@ -995,12 +1026,11 @@ class FastPath:
         t = np.broadcast_to(np.arange(c0, c0 + n, dtype=np.float64) * step, (len(rows), n))
         if c1 <= self._ring_top - self.RING or c0 > self._ring_top:
             return np.full((len(rows), n), np.nan, np.float32), t
-        sub = self._ring[rows]
         j0 = c0 % self.RING
         if j0 + n <= self.RING:
-            v = sub[:, j0:j0 + n]
+            v = self._ring[rows, j0:j0 + n]                # gathers only the window's slots
         else:
-            v = np.concatenate([sub[:, j0:], sub[:, :j0 + n - self.RING]], axis=1)
+            v = np.concatenate([self._ring[rows, j0:], self._ring[rows, :j0 + n - self.RING]], axis=1)
         lo_ok, hi_ok = max(c0, self._ring_top - self.RING + 1), min(c1, self._ring_top)
         if lo_ok > c0 or hi_ok < c1:           # columns outside the ring's range read NaN
             v = v.copy()
@@ -1167,7 +1197,11 @@ class FastPath:
         if pos is not None:
             sel = None if pos is True else (pos[:, None] * M + np.arange(M)[None, :]).reshape(-1)
             pick = (lambda a: a) if sel is None else (lambda a: None if a is None else a[sel])
-            cur_len, cur, cur_t, base = pick(col["cur_len"]), pick(col["cur"]), pick(col["cur_t"]), pick(col["base"])
+            cur_len, cur, base = pick(col["cur_len"]), pick(col["cur"]), pick(col["base"])
+            ct = col["cur_t"]
+            # merged mode: the window times are one broadcast row -- kept broadcast
+            cur_t = np.broadcast_to(ct[0], (len(sel), ct.shape[1])) if (
+                sel is not None and ct.ndim == 2 and ct.shape[0] and ct.strides[0] == 0) else pick(ct)
         else:
             cur_len = np.concatenate([w.cur_len for w in works])
             base_len = np.concatenate([w.base_len for w in works])
@@ -1439,12 +1473,21 @@ class FastPath:
         t_last = self._hist_last(store.last_t[rowmap], store.step, ga.hist_end) if store.sliding \
             else store.last_t[rowmap]
         cur_t = ga.cur_t
-        ok = np.isfinite(cur_t) & np.isfinite(t_last)[:, None]
-        with np.errstate(invalid="ignore"):
-            h = np.where(ok, np.rint((cur_t - t_last[:, None]) / b.step), 1.0)
-        hor = np.maximum(1, h).astype(np.int64)
+        # merged sliding mode: the current window's times are one broadcast
+        # grid row -- the [rows, n] horizons are computed on the device from
+        # each row's last history time (no host pass over rows x points)
+        trow = _bcast_row(cur_t)
+        if trow is None:
+            ok = np.isfinite(cur_t) & np.isfinite(t_last)[:, None]
+            with np.errstate(invalid="ignore"):
+                h = np.where(ok, np.rint((cur_t - t_last[:, None]) / b.step), 1.0)
+            hor = np.maximum(1, h).astype(np.int64)
+            has_cur = np.isfinite(ga.cur).any(1)
+        else:
+            hor = None
+            has_cur = ga.cur_len > 0
         valid = ((store.nfin[rowmap] >= max(cfg.min_historical_points, 1)).astype(np.int32)
-                 | (np.isfinite(ga.cur).any(1).astype(np.int32) << 1))
+                 | (has_cur.astype(np.int32) << 1))
         # every per-row int array of this call goes up in ONE pinned,
         # non-blocking copy (a pageable torch.as_tensor(..., device) per array
         # is a synchronous copy ordered behind the queued GPU work)
@@ -1473,22 +1516,32 @@ class FastPath:
                 # every row of the group: the memo's list object, stable while the
                 # job list is (the model cache skips its per-row lookups for it)
                 keys = full if idx is None else kv[rows].tolist()
-            hr = hor[rows]
+            if hor is not None:
+                hr = hor[rows]
+                kh, hshape, hmax = i64(hr), hr.shape, max(1, int(hr.max()) if hr.size else 1)
+            else:
+                tl = t_last[rows]
+                kh, hshape = i64(tl.view(np.int64)), (len(tl), len(trow))     # float64 bits, device-side horizons
+                fin_tl = tl[np.isfinite(tl)]
+                hmax = max(1, int(np.rint((trow.max() - fin_tl.min()) / b.step))) if fin_tl.size and len(trow) else 1
             pending.append((algo, ms, idx, (i64(rowmap[rows]), i64(shift[rows]), i64(lim[rows]), i64(valid[rows]),
-                                            i64(hr)), hr.shape, keys, t_last[rows],
-                            max(1, int(hr.max()) if hr.size else 1)))
-        fin = np.isfinite(ga.cur)
+                                            kh), hshape, keys, t_last[rows], hmax))
         n = ga.cur.shape[1]
-        lastk = np.where(fin.any(1), n - 1 - np.argmax(fin[:, ::-1], axis=1), n - 1)
+        lastk = _last_finite(ga.cur)
         k_last = i64(lastk)
         off = np.concatenate([[0], np.cumsum([len(a) for a in parts])])
         host = torch.from_numpy(np.concatenate(parts))
         flat = host.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else host
         view = lambda k: flat[off[k]:off[k + 1]]                                     # noqa: E731
+        trow_d = None if trow is None else torch.from_numpy(np.ascontiguousarray(trow, np.float64)).to(dev)
         for algo, ms, idx, (kr, ks, kl, kv, kh), hshape, keys, tl, hmax in pending:
+            if trow_d is None:
+                hr_d = view(kh).reshape(hshape)
+            else:
+                hr_d = _device_horizons(trow_d, view(kh).view(torch.float64), b.step)
             subs.append(ModelSub(algo, ms, idx, view(kr).to(torch.int32), view(ks).to(torch.int32),
                                  view(kl).to(torch.int32), T, zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev),
-                                 keys, tl, view(kv).to(torch.int32), view(kh).reshape(hshape), hmax, len(ms)))
+                                 keys, tl, view(kv).to(torch.int32), hr_d, hmax, len(ms)))
         md = ga.models = ModelArrays(stamp, subs, view(k_last))
         if store.sliding and np.isfinite(t_last).all() and ga.cur_t.shape[0] and ga.cur_t.strides[0] == 0:
             # state for the next cycle's shift-only update (_model_arrays_slid)
@@ -1520,13 +1573,9 @@ class FastPath:
             return None
         cfg = self.b.cfg
         dev = self.b.device
-        fin = np.isfinite(ga.cur)
         valid = ((store.nfin[rowmap] >= max(cfg.min_historical_points, 1)).astype(np.int32)
-                 | (fin.any(1).astype(np.int32) << 1))
-        if fin[:, -1].all():
-            lastk = lastk_prev if (lastk_prev == n - 1).all() else np.full(len(rowmap), n - 1, np.int64)
-        else:
-            lastk = np.where(fin.any(1), n - 1 - np.argmax(fin[:, ::-1], axis=1), n - 1)
+                 | ((ga.cur_len > 0).astype(np.int32) << 1))
+        lastk = _last_finite(ga.cur)
         up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=False)  # noqa: E731
         vchg = not np.array_equal(valid, valid_prev)
         subs = []
