@@ -979,7 +979,22 @@ class FastPath:
                 fw.hist = []
             self._slide_state[p0.group] = (ids, wclass)
         self._col[p0.group] = {"ids": ids, "cur": cur, "cur_t": cur_t, "cur_len": cur_len, "base": base,
-                               "base_len": None, "hist_end": wins["historical"][1]}
+                               "base_len": None, "hist_end": wins["historical"][1],
+                               # the same windows as column ranges of the device grid (the
+                               # device copy is gathered there, not uploaded)
+                               "dev": (self._grid_cols(clo, chi, cur.shape[1]),
+                                       self._grid_cols(blo, bhi, base.shape[1]) if base is not None else None)}
+
+    def _grid_cols(self, lo: float, hi: float, n: int) -> tuple[int, int] | None:
+        """Device-grid columns [a, a + n) of the grid points in [lo, hi] when
+        all of them lie inside the sliding grid's live range, else None."""
+        st = self.sliding
+        step = self.b.step
+        c0, c1 = math.ceil(lo / step - 1e-9), math.floor(hi / step + 1e-9)
+        if c1 - c0 + 1 != n or st.t0 is None:
+            return None
+        a = int(st.col(c0 * step))
+        return (a, a + n) if st.ws <= a and a + n <= st.e else None
 
     # host ring of the newest grid columns of every sliding row (merged mode)
     RING = 64
@@ -1214,9 +1229,20 @@ class FastPath:
         up = lambda a: (torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"
                         else torch.from_numpy(a))
         has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
-        has_cur = np.isfinite(cur).any(1).reshape(S, M)
-        ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
-                         up(rowmap), end, ~(has_hist & has_cur), handles=handles, works=works)
+        rm_d = up(rowmap)
+        devc = col.get("dev") if pos is not None else None
+        if devc is not None and devc[0] is not None and (base is None or devc[1] is not None):
+            # merged sliding windows: read out of the device grid the samples
+            # were just written to (no rows x points upload)
+            rml = rm_d.long()
+            grab = lambda ab: store.buf[:, ab[0]:ab[1]].index_select(0, rml)   # noqa: E731
+            cur_d, base_d = grab(devc[0]), (grab(devc[1]) if base is not None else None)
+            has_cur = (cur_len > 0).reshape(S, M)
+        else:
+            cur_d, base_d = up(cur), (up(base) if base is not None else None)
+            has_cur = np.isfinite(cur).any(1).reshape(S, M)
+        ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, cur_d, base_d,
+                         rm_d, end, ~(has_hist & has_cur), handles=handles, works=works)
         if col is not None and pos is not None:
             ga.hist_end = col.get("hist_end")
             old = self._garr.get(key)

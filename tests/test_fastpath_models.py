@@ -151,6 +151,12 @@ def test_models_fast_path_equals_general_path(algo, kind, device="cpu"):
     if kind != "static" and algo not in ("moving_average", "bivariate_normal"):
         # the sliding group's model arrays moved by the poll step, not rebuilt
         assert a[3].fast.model_slides > 0
+    for ga in a[3].fast._garr.values():
+        # merged sliding windows are gathered from the device grid: the same
+        # values as the host ring's copy
+        np.testing.assert_array_equal(ga.cur_d.cpu().numpy(), ga.cur)
+        if ga.base_d is not None and getattr(ga, "base", None) is not None:
+            np.testing.assert_array_equal(ga.base_d.cpu().numpy(), ga.base)
 
 
 def test_cached_holt_winters_steady_state_reads_only_new_columns(monkeypatch):
