@@ -108,6 +108,7 @@ class GaugeTable:
         out = np.empty(len(keys), np.int64)
         idx = self.index
         with self.lock:
+            new_k, new_s = [], []
             for i, k in enumerate(keys):
                 s = idx.get(k)
                 if s is None:
@@ -118,24 +119,53 @@ class GaugeTable:
                         s = len(self.keys)
                         self.keys.append(k)
                     idx[k] = s
-                    n = len(self.keys)
-                    if n > len(self.vals):
-                        self.vals = _grow(self.vals, n, np.nan)
-                        self.expire = _grow(self.expire, n, np.nan)
-                        self._sline = _grow(self._sline, n, -1)
-                    self.vals[s] = np.nan
-                    self.expire[s] = np.inf
-                    self._add_line(k, s)
-                    self.events.append((s, k))
+                    new_k.append(k)
+                    new_s.append(s)
                 elif self._nret and self.expire[s] < np.inf:
                     self.expire[s] = np.inf          # looked up again: live again
                     self._nret -= 1
                 out[i] = s
+            if new_k:
+                n = len(self.keys)
+                if n > len(self.vals):
+                    self.vals = _grow(self.vals, n, np.nan)
+                    self.expire = _grow(self.expire, n, np.nan)
+                    self._sline = _grow(self._sline, n, -1)
+                ns = np.asarray(new_s, np.int64)
+                self.vals[ns] = np.nan
+                self.expire[ns] = np.inf
+                self._add_lines(new_k, new_s)
+                self.events.extend(zip(new_s, new_k))
         return out
 
-    def _add_line(self, key, slot: int) -> None:
-        name, ns, app = key[:3]
-        extra = f',cluster="{_esc(key[3])}"' if len(key) > 3 and key[3] else ""
+    def _add_lines(self, keys: list, slots: list) -> None:
+        """:meth:`_add_line` for many new keys: lines grouped by family, each
+        family's prefix buffer and offset / slot arrays extended once."""
+        if len(keys) < 8:
+            for k, s in zip(keys, slots):
+                self._add_line(k, s)
+            return
+        fams: dict = {}
+        for k, s in zip(keys, slots):
+            fams.setdefault(k[0], []).append((k, s))
+        for name, items in fams.items():
+            f = self._family(name)
+            k0 = self._fn[f]
+            enc = [(f'{name}{{namespace="{_esc(k[1])}",app="{_esc(k[2])}"'
+                    + (f',cluster="{_esc(k[3])}"' if len(k) > 3 and k[3] else "") + "} ").encode() for k, _ in items]
+            buf = self._fprefix[f]
+            base = len(buf)
+            buf += b"".join(enc)
+            m = len(items)
+            self._fpoff[f] = po = _grow(self._fpoff[f], k0 + m + 1, 0)
+            po[k0 + 1:k0 + m + 1] = base + np.cumsum(np.fromiter(map(len, enc), np.int64, m))
+            self._fslots[f] = sl = _grow(self._fslots[f], k0 + m, -1)
+            ss = np.fromiter((s for _, s in items), np.int64, m)
+            sl[k0:k0 + m] = ss
+            self._fn[f] = k0 + m
+            self._sline[ss] = (f << 32) | np.arange(k0, k0 + m, dtype=np.int64)
+
+    def _family(self, name: str) -> int:
         f = self._fam_of.get(name)
         if f is None:
             f = self._fam_of[name] = len(self._fam_names)
@@ -145,6 +175,12 @@ class GaugeTable:
             self._fslots.append(np.zeros(0, np.int64))
             self._fn.append(0)
             self._fdead.append(0)
+        return f
+
+    def _add_line(self, key, slot: int) -> None:
+        name, ns, app = key[:3]
+        extra = f',cluster="{_esc(key[3])}"' if len(key) > 3 and key[3] else ""
+        f = self._family(name)
         k = self._fn[f]
         buf = self._fprefix[f]
         buf += f'{name}{{namespace="{_esc(ns)}",app="{_esc(app)}"{extra}}} '.encode()
@@ -389,6 +425,22 @@ class BrainExporter:
             u, l, a = self.bound_names(bm)
             keys += [(u, ns, app), (l, ns, app), (a, ns, app)]
         return self.table.slots(keys).reshape(-1, 3)
+
+    def bound_slots_many(self, jobs: list) -> list[np.ndarray]:
+        """:meth:`bound_slots` of many jobs ``(base_metrics, namespaces, apps)``
+        through one table lookup."""
+        keys, counts = [], []
+        for bms, nss, apps in jobs:
+            for bm, ns, app in zip(bms, nss, apps):
+                u, l, a = self.bound_names(bm)
+                keys += [(u, ns, app), (l, ns, app), (a, ns, app)]
+            counts.append(len(bms))
+        flat = self.table.slots(keys).reshape(-1, 3)
+        out, o = [], 0
+        for c in counts:
+            out.append(flat[o:o + c])
+            o += c
+        return out
 
     def set_forecast(self, base_metric: str, namespace: str, app: str, value: float) -> None:
         """Peak of the H-step load forecast (HPA jobs): the cluster-autoscaler

@@ -1364,13 +1364,12 @@ class FastPath:
             handles = None if any(h is None for h in hd) else np.asarray(hd, np.int64)
             xs = None
             if exp is not None:
-                slots = []
-                for w in works:
-                    p = w.plan
-                    if p.export_slots is None:
-                        p.export_slots = exp.bound_slots(p.base_metrics, [p.namespace] * M, [p.app] * M)
-                    slots.append(p.export_slots)
-                xs = np.concatenate(slots)
+                need = [w.plan for w in works if w.plan.export_slots is None]
+                if need:
+                    got = exp.bound_slots_many([(p.base_metrics, [p.namespace] * M, [p.app] * M) for p in need])
+                    for p, sl in zip(need, got):
+                        p.export_slots = sl
+                xs = np.concatenate([w.plan.export_slots for w in works])
             cols = (rowmap, ids, handles, np.fromiter((w.end_ts for w in works), np.float64, S), xs)
         self._gstat[key] = (ident, None, cols, extra)
         return cols

@@ -56,6 +56,10 @@ def _load():
     lib.fm_prom_format.argtypes = [c_i64, ctypes.c_char_p, c_vp, ctypes.c_double, ctypes.c_double, c_i64, c_vp,
                                    c_vp, c_i64]
     lib.fm_prom_format.restype = c_i64
+    if hasattr(lib, "fm_synth_many"):
+        lib.fm_synth_many.argtypes = [c_i64, c_i64] + [c_vp] * 12 + [ctypes.c_uint32, ctypes.c_float, c_vp,
+                                                                      ctypes.c_double, c_vp, ctypes.c_int]
+        lib.fm_synth_many.restype = None
     if hasattr(lib, "fm_parse_ranges"):
         lib.fm_parse_ranges.argtypes = [ctypes.c_char_p, c_vp, c_i64, ctypes.c_char_p, c_i64, c_vp]
         lib.fm_parse_ranges.restype = c_i64
@@ -281,3 +285,22 @@ def hpalog_bodies(batch) -> list[str] | None:
     if text.isascii():                      # byte offsets are character offsets
         return [text[a:b] for a, b in zip(boff[:-1].tolist(), boff[1:].tolist())]
     return [str(mv[a:b], "utf-8") for a, b in zip(boff[:-1].tolist(), boff[1:].tolist())]
+
+
+def synth_many(level, ad, aw, sph, cph, kh, t, swd, cwd, sww, cww, inner, c2: int, noise: float, mag,
+               fault_after: float, threads: int = 8):
+    """[K, nt] float32 samples of SyntheticSource.many (sources.py) from its
+    per-key and per-time terms; None when the library lacks it."""
+    lib = _load()
+    if lib is None or not hasattr(lib, "fm_synth_many"):
+        return None
+    K, nt = len(level), len(t)
+    f64 = lambda a: np.ascontiguousarray(a, np.float64)          # noqa: E731
+    u32 = lambda a: np.ascontiguousarray(a, np.uint32)           # noqa: E731
+    arrs = [f64(level), f64(ad), f64(aw), f64(sph), f64(cph), u32(kh), f64(t), f64(swd), f64(cwd), f64(sww),
+            f64(cww), u32(inner)]
+    mg = None if mag is None else f64(mag)
+    out = np.empty((K, nt), np.float32)
+    lib.fm_synth_many(K, nt, *[a.ctypes.data for a in arrs], int(c2) & 0xFFFFFFFF, float(noise),
+                      None if mg is None else mg.ctypes.data, float(fault_after), out.ctypes.data, int(threads))
+    return out

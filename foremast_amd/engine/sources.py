@@ -304,6 +304,9 @@ class SyntheticSource:
         tt = np.asarray(t, np.float64)
         wd, ww = 2 * np.pi * tt / 86400.0, 2 * np.pi * tt / 604800.0
         sph, cph = np.sin(ph), np.cos(ph)
+        got = self._many_native(level, ad, aw, sph, cph, noise_keys, fault_keys, tt, wd, ww, stream)
+        if got is not None:                      # every call (a sample reads the same from any window)
+            return got
         season = 1 + ad * (np.sin(wd)[None, :] * cph + np.cos(wd)[None, :] * sph) \
             + aw * (np.sin(ww)[None, :] * cph + np.cos(ww)[None, :] * sph)
         # hash3(key, t, stream) = hash(key * P1 ^ hash(t * P2 ^ hash(stream + P3))):
@@ -328,6 +331,31 @@ class SyntheticSource:
             if (mag != 1).any():
                 v = np.where(tt[None, :] >= self.fault_after, v * mag, v)
         return np.maximum(v, 0).astype(np.float32)
+
+    def _fault_mag(self, fault_keys: list[str]) -> np.ndarray | None:
+        if not self.faults:
+            return None
+        mag = np.ones(len(fault_keys))
+        for i, fk in enumerate(fault_keys):
+            for sub, m in self.faults.items():
+                if sub in fk:
+                    mag[i] *= m
+        return mag if (mag != 1).any() else None
+
+    def _many_native(self, level, ad, aw, sph, cph, noise_keys, fault_keys, tt, wd, ww, stream: int):
+        """The [keys x times] pass of :meth:`many` in C++ (csrc/runtime/synth.cpp),
+        same terms and expression order; None without the native library."""
+        from ..ops.reference import hash_u32
+        from . import native_rt
+        U = np.uint32
+        kh = np.array([zlib.crc32(k.encode()) ^ self.seed for k in noise_keys], np.uint32)
+        ti = ((tt / self.step).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
+        hs = hash_u32(np.uint32((stream + 0x165667B1) & 0xFFFFFFFF))[0]
+        inner = hash_u32((ti * U(0x85EBCA77)) ^ hs)
+        c2 = hash_u32(np.uint32((0x68E31DA4 * 0x85EBCA77) & 0xFFFFFFFF) ^ hs)[0]
+        return native_rt.synth_many(level.ravel(), ad.ravel(), aw.ravel(), sph.ravel(), cph.ravel(), kh, tt,
+                                    np.sin(wd), np.cos(wd), np.sin(ww), np.cos(ww), inner, int(c2), self.noise,
+                                    self._fault_mag(fault_keys), self.fault_after)
 
     def series(self, key: str, start: float, end: float, stream: int = 0, noise_key: str | None = None,
                fault_key: str | None = None) -> Series:

@@ -275,3 +275,21 @@ def test_native_batched_url_parse_equals_python_parse():
     if native_rt.available():
         f, _ = native_rt.parse_ranges(urls)
         assert int(f[:, 0].sum()) >= 6           # the fast shapes went native
+
+
+def test_native_synthetic_generator_matches_numpy():
+    """SyntheticSource.many's [keys x times] pass in C++ (csrc/runtime/synth.cpp)
+    gives the numpy expression's samples (fp32 libm last-ulp differences only),
+    faults included."""
+    from foremast_amd.engine import native_rt
+    from foremast_amd.engine.sources import SyntheticSource
+    if not native_rt.available():
+        pytest.skip("native runtime not built")
+    s = SyntheticSource(faults={"pod1": 1.5}, fault_after=1.7e9 + 3000)
+    keys = [f'm{{pod="pod{i}"}}' for i in range(300)]
+    t = s.grid(1.7e9, 1.7e9 + 60 * 200)
+    a = s.many(keys, keys, keys, t, 3)
+    s._many_native = lambda *x, **k: None
+    b = s.many(keys, keys, keys, t, 3)
+    np.testing.assert_allclose(a, b, rtol=2e-6, atol=0)
+    assert (a[1, t >= s.fault_after] > 0).all()
