@@ -14,7 +14,11 @@
 #include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <climits>
+#include <cstring>
+#include <string_view>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #define FM_API extern "C" __attribute__((visibility("default")))
@@ -67,4 +71,77 @@ FM_API void fm_synth_many(int64_t K, int64_t nt, const double* level, const doub
   for (int i = 1; i < nt_; ++i) pool.emplace_back(work);
   work();
   for (auto& th : pool) th.join();
+}
+
+// Fault multipliers of the synthetic source: out[i] = product of mags[j] over
+// the fault substrings j contained in key i (each counted once, multiplied in
+// j order -- the Python loop's `for sub, m in faults.items(): if sub in key`).
+// A restart asks for ~800k keys against ~200 faults.  Each substring of 8+
+// bytes is indexed by its RAREST 8-byte window among all substrings' windows
+// (fault lists share prefixes like `app="svc`), looked up at every key
+// position behind a 16-bit filter, then verified; shorter substrings by a
+// plain search.
+FM_API void fm_fault_mag(const char* kbuf, const int64_t* koff, int64_t n, const char* sbuf, const int64_t* soff,
+                         int64_t nsub, const double* mags, double* out) {
+  constexpr int64_t W = 8;
+  auto win = [](const char* p) {
+    uint64_t h;
+    std::memcpy(&h, p, (size_t)W);
+    return h;
+  };
+  auto mix = [](uint64_t h) { return (size_t)((h * 0x9E3779B97F4A7C15ull) >> 48); };
+  std::unordered_map<uint64_t, int64_t> freq;
+  std::vector<int64_t> shorts;
+  for (int64_t j = 0; j < nsub; ++j) {
+    const int64_t sl = soff[j + 1] - soff[j];
+    if (sl < W) {
+      shorts.push_back(j);
+      continue;
+    }
+    for (int64_t o = 0; o + W <= sl; ++o) ++freq[win(sbuf + soff[j] + o)];
+  }
+  struct Cand { int64_t j, o; };
+  std::unordered_multimap<uint64_t, Cand> index;
+  index.reserve((size_t)nsub * 2);
+  std::vector<uint8_t> seen(1 << 16, 0);
+  for (int64_t j = 0; j < nsub; ++j) {
+    const int64_t sl = soff[j + 1] - soff[j];
+    if (sl < W) continue;
+    int64_t best = 0, bf = INT64_MAX;
+    for (int64_t o = 0; o + W <= sl; ++o) {
+      const int64_t f = freq[win(sbuf + soff[j] + o)];
+      if (f < bf) { bf = f; best = o; }
+    }
+    const uint64_t h = win(sbuf + soff[j] + best);
+    index.emplace(h, Cand{j, best});
+    seen[mix(h)] = 1;
+  }
+  std::vector<int64_t> hits;
+  for (int64_t i = 0; i < n; ++i) {
+    const char* k = kbuf + koff[i];
+    const int64_t L = koff[i + 1] - koff[i];
+    const std::string_view kv(k, (size_t)L);
+    hits.clear();
+    for (int64_t j : shorts)
+      if (kv.find(std::string_view(sbuf + soff[j], (size_t)(soff[j + 1] - soff[j]))) != std::string_view::npos)
+        hits.push_back(j);
+    if (!index.empty()) {
+      for (int64_t p = 0; p + W <= L; ++p) {
+        const uint64_t h = win(k + p);
+        if (!seen[mix(h)]) continue;
+        auto r = index.equal_range(h);
+        for (auto it = r.first; it != r.second; ++it) {
+          const int64_t j = it->second.j, st = p - it->second.o, sl = soff[j + 1] - soff[j];
+          if (st >= 0 && st + sl <= L && std::memcmp(k + st, sbuf + soff[j], (size_t)sl) == 0) hits.push_back(j);
+        }
+      }
+    }
+    double m = 1.0;
+    if (!hits.empty()) {
+      std::sort(hits.begin(), hits.end());
+      hits.erase(std::unique(hits.begin(), hits.end()), hits.end());
+      for (int64_t j : hits) m *= mags[j];
+    }
+    out[i] = m;
+  }
 }

@@ -60,6 +60,9 @@ def _load():
         lib.fm_synth_many.argtypes = [c_i64, c_i64] + [c_vp] * 12 + [ctypes.c_uint32, ctypes.c_float, c_vp,
                                                                       ctypes.c_double, c_vp, ctypes.c_int]
         lib.fm_synth_many.restype = None
+    if hasattr(lib, "fm_fault_mag"):
+        lib.fm_fault_mag.argtypes = [ctypes.c_char_p, c_vp, c_i64, ctypes.c_char_p, c_vp, c_i64, c_vp, c_vp]
+        lib.fm_fault_mag.restype = None
     if hasattr(lib, "fm_parse_ranges"):
         lib.fm_parse_ranges.argtypes = [ctypes.c_char_p, c_vp, c_i64, ctypes.c_char_p, c_i64, c_vp]
         lib.fm_parse_ranges.restype = c_i64
@@ -303,4 +306,23 @@ def synth_many(level, ad, aw, sph, cph, kh, t, swd, cwd, sww, cww, inner, c2: in
     out = np.empty((K, nt), np.float32)
     lib.fm_synth_many(K, nt, *[a.ctypes.data for a in arrs], int(c2) & 0xFFFFFFFF, float(noise),
                       None if mg is None else mg.ctypes.data, float(fault_after), out.ctypes.data, int(threads))
+    return out
+
+
+def fault_mag(keys: list[str], subs: list[str], mags: list[float]) -> np.ndarray | None:
+    """Per key the product of ``mags[j]`` over the substrings ``subs[j]`` it
+    contains (csrc/runtime/synth.cpp); None without the library."""
+    lib = _load()
+    if lib is None or not hasattr(lib, "fm_fault_mag"):
+        return None
+    kb = [k.encode() for k in keys]
+    sb = [s.encode() for s in subs]
+    koff = np.zeros(len(kb) + 1, np.int64)
+    np.cumsum(np.fromiter(map(len, kb), np.int64, len(kb)), out=koff[1:])
+    soff = np.zeros(len(sb) + 1, np.int64)
+    np.cumsum(np.fromiter(map(len, sb), np.int64, len(sb)), out=soff[1:])
+    m = np.ascontiguousarray(mags, np.float64)
+    out = np.empty(len(kb), np.float64)
+    lib.fm_fault_mag(b"".join(kb), koff.ctypes.data, len(kb), b"".join(sb), soff.ctypes.data, len(sb),
+                     m.ctypes.data, out.ctypes.data)
     return out

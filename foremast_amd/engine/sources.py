@@ -335,6 +335,10 @@ class SyntheticSource:
     def _fault_mag(self, fault_keys: list[str]) -> np.ndarray | None:
         if not self.faults:
             return None
+        from . import native_rt
+        mag = native_rt.fault_mag(fault_keys, list(self.faults), list(self.faults.values()))
+        if mag is not None:
+            return mag if (mag != 1).any() else None
         mag = np.ones(len(fault_keys))
         for i, fk in enumerate(fault_keys):
             for sub, m in self.faults.items():

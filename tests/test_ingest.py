@@ -293,3 +293,25 @@ def test_native_synthetic_generator_matches_numpy():
     b = s.many(keys, keys, keys, t, 3)
     np.testing.assert_allclose(a, b, rtol=2e-6, atol=0)
     assert (a[1, t >= s.fault_after] > 0).all()
+
+
+def test_native_fault_matcher_equals_substring_loop():
+    """fm_fault_mag: product over the fault substrings a key contains (each
+    once, in order), for short, long, shared-prefix, repeated and empty
+    substrings -- the Python `sub in key` loop's answer."""
+    from foremast_amd.engine import native_rt
+    if not native_rt.available():
+        pytest.skip("native runtime not built")
+    rng = np.random.default_rng(3)
+    faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, 400, 7)}
+    faults.update({f'app="svc{j}"': 3.0 for j in range(0, 400, 11)})
+    faults.update({"p0": 1.1, "": 1.01, '"svc1"': 1.3, "svc1": 1.7, "7687b9f4d7": 0.5})
+    keys = [f'm{{namespace="ns",pod="svc{i}-7687b9f4d7-p{i % 7:04d}",app="svc{i}"}}' for i in rng.integers(0, 500, 3000)]
+    keys += ["", "svc1", "x" * 3]
+    got = native_rt.fault_mag(keys, list(faults), list(faults.values()))
+    want = np.ones(len(keys))
+    for i, k in enumerate(keys):
+        for sub, m in faults.items():
+            if sub in k:
+                want[i] *= m
+    np.testing.assert_array_equal(got, want)
