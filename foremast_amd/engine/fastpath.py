@@ -543,14 +543,19 @@ class FastPath:
         self.cycle += 1
         self._wt_changed = False
         self._col.clear()
+        keep_jid = self._jid_cache.get(id(self._last[2])) if self._last is not None else None
         self._jid_cache.clear()
         self.sliding.advance(now, now - self.history_s)
         immutable = self._immutable
         last = self._last
         if last is not None and batch.ids == last[0] and batch.versions == last[1]:
             fast = last[2]
-            self.todo = [fw for fw in last[3] if not ((immutable or fw.wcur is not None) and fw.settled)]
+            todo = [fw for fw in last[3] if not ((immutable or fw.wcur is not None) and fw.settled)]
+            # every job due (sliding fleets): the job list itself, one JobIds per cycle
+            self.todo = fast if len(todo) == len(fast) else todo
             self._reused = True
+            if keep_jid is not None and keep_jid[0] is fast:     # same list object: same ids
+                self._jid_cache[id(fast)] = keep_jid
             return fast, []
         self._reused = False
         works = self.works
@@ -559,6 +564,8 @@ class FastPath:
         fws = list(map(works.get, batch.ids))
         if None not in fws and list(map(_version_of, fws)) == list(batch.versions):
             todo = [fw for fw in fws if not ((immutable or fw.wcur is not None) and fw.settled)]
+            if len(todo) == len(fws):
+                todo = fws
             self._specs = {}
             self.todo = todo
             self._last = (batch.ids, batch.versions, fws, todo)
@@ -603,6 +610,8 @@ class FastPath:
         if reg:
             self._register_windows(reg)
         self._specs = {}
+        if len(todo) == len(fast):
+            todo = fast
         self.todo = todo
         self._last = (batch.ids, batch.versions, fast, todo) if not rest else None
         return fast, rest
