@@ -170,12 +170,12 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   const float* xr = x + row * ld;
 
   // ---- stage the row.  FS with an aligned row of <= 16 floats per thread
-  // (config 2: 10,080 over 896 threads): ONE read of the row, held in
+  // (config 2: 10,080 over 448 threads, KREG = 6): ONE read of the row, held in
   // registers while the first finite sample is found, then written to LDS
   // from base on -- with the lap flags and the first two seasons' sums on the
   // way.  Otherwise: find base, then re-read the row (L2) into LDS.  The
   // candidate powers are computed while the row's loads are in flight.
-  constexpr int KREG = 4;
+  constexpr int KREG = 6;
   const bool rs = FS && xal && T <= KREG * 4 * nth;
   // wsum[64..128) is the L2 warm-up DMA's landing zone (one dword per lane of
   // a wave): the per-wave minima and the winner's state live past it
