@@ -510,3 +510,37 @@ FM_API void fm_pack_right(const float* const* srcs, const int64_t* lens, int64_t
   work();
   for (auto& th : pool) th.join();
 }
+
+// Finite values per row of a [R, n] float32 matrix with row stride ld (the
+// sliding windows' point counts, one pass instead of numpy's mask + sum).
+FM_API void fm_count_finite(const float* a, int64_t R, int64_t n, int64_t ld, int64_t* out) {
+  for (int64_t r = 0; r < R; ++r) {
+    const float* p = a + r * ld;
+    int64_t c = 0;
+    for (int64_t i = 0; i < n; ++i) c += std::isfinite(p[i]) ? 1 : 0;
+    out[r] = c;
+  }
+}
+
+// Host ring of the newest grid columns of every sliding row
+// (engine/fastpath.py _ring_write): clear the slots of the columns
+// (top_old, top_new] in every row, then store the samples whose column is
+// inside the ring (finite values only).  ring [nrows, width] float32,
+// slot = column mod width.
+FM_API void fm_ring_write(float* ring, int64_t nrows, int64_t width, int64_t top_old, int64_t top_new,
+                          const int64_t* r, const double* t, const float* v, int64_t n, double step) {
+  if (top_new > top_old) {
+    const int64_t k = top_new - top_old >= width ? width : top_new - top_old;
+    for (int64_t row = 0; row < nrows; ++row) {
+      float* p = ring + row * width;
+      for (int64_t c = top_new - k + 1; c <= top_new; ++c) p[((c % width) + width) % width] = NAN;
+    }
+  }
+  const int64_t lo = top_new - width;
+  for (int64_t i = 0; i < n; ++i) {
+    if (!std::isfinite(v[i])) continue;
+    const int64_t c = (int64_t)std::nearbyint(t[i] / step);
+    if (c <= lo || c > top_new) continue;
+    ring[r[i] * width + ((c % width) + width) % width] = v[i];
+  }
+}

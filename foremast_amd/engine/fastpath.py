@@ -50,6 +50,7 @@ from ..api.models import Document, HPALogBatch
 from ..api.urls import END_PLACEHOLDER, START_PLACEHOLDER, parse_config, prometheus_query_of, promql_metric_name
 from ..ops import canary as C
 from ..ops import misc as MI
+from . import native_rt
 from .resident import ResidentHistory
 from .scorer import CanaryScorer
 from .sources import SourceError, TemplateList, substitute_window
@@ -953,16 +954,19 @@ class FastPath:
             since = st.last_t[rows[:, m]]
             fresh.append(rows[~np.isfinite(since), m])
             lo = np.where(np.isfinite(since), since + step, math.ceil(hlo / step - 1e-9) * step)
-            for lo_v in np.unique(lo):
+            l0 = lo.min() if len(lo) else 0.0
+            # every row at the same newest sample (the steady state): no sort
+            starts = (l0,) if len(lo) and l0 == lo.max() else np.unique(lo)
+            for lo_v in starts:
                 if hi < lo_v:
                     continue
-                sel = np.flatnonzero(lo == lo_v)
-                if len(sel) == len(tpls):
+                sel = np.flatnonzero(lo == lo_v) if len(starts) > 1 else None
+                if sel is None or len(sel) == len(tpls):
                     lens, t, v = self._columns(stores, tpls, float(lo_v), hi)
                 else:
                     lens, t, v = self._columns([stores[i] for i in sel], [tpls[i] for i in sel], float(lo_v), hi)
                 if len(t):
-                    wr.append(np.repeat(rows[sel, m], lens))
+                    wr.append(np.repeat(rows[:, m] if sel is None else rows[sel, m], lens))
                     wt.append(t)
                     wv.append(v)
         fresh_rows = np.concatenate(fresh) if fresh else None
@@ -974,12 +978,13 @@ class FastPath:
         (clo, chi), (blo, bhi) = wins["current"], wins["baseline"]
         cur, cur_t = self._ring_read(flat, clo, chi)
         base = self._ring_read(flat, blo, bhi)[0] if memo[3][1] else None
-        cur_len = np.isfinite(cur).sum(1)
+        cur_len = native_rt.count_finite(cur)
         wclass = 0 if cur.shape[1] <= 128 else (1 if cur.shape[1] <= 256 else 2)
         # per-job state only when the job set or the window class changed (the
         # group's arrays are rebuilt from self._col every cycle regardless)
         prev = self._slide_state.get(p0.group)
-        if prev is None or prev[1] != wclass or prev[0] != ids:
+        if prev is None or prev[1] != wclass or (prev[0] != ids and ids.index_in(prev[0]) is None):
+            # (a list that only lost jobs since: the survivors' state is set)
             for fw in ws:
                 fw.has_window = True
                 fw.dirty = True
@@ -1021,10 +1026,14 @@ class FastPath:
             self._ring = ring
         if fresh is not None and len(fresh):
             self._ring[fresh] = np.nan
-        ck = np.rint(t / self.b.step).astype(np.int64)
-        if not len(ck):
+        if not len(t):
             return
-        top = int(ck.max())
+        top = int(np.rint(t.max() / self.b.step))
+        if (self._ring_top is not None and 0 < top - self._ring_top < self.RING or top == self._ring_top) and \
+                native_rt.ring_write(self._ring, self._ring_top, max(top, self._ring_top), r, t, v, self.b.step):
+            self._ring_top = max(top, self._ring_top)
+            return
+        ck = np.rint(t / self.b.step).astype(np.int64)
         if self._ring_top is None or top - self._ring_top >= self.RING:
             if self._ring_top is not None:
                 self._ring[:] = np.nan

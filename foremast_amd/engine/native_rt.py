@@ -60,6 +60,12 @@ def _load():
         lib.fm_synth_many.argtypes = [c_i64, c_i64] + [c_vp] * 12 + [ctypes.c_uint32, ctypes.c_float, c_vp,
                                                                       ctypes.c_double, c_vp, ctypes.c_int]
         lib.fm_synth_many.restype = None
+    if hasattr(lib, "fm_ring_write"):
+        lib.fm_ring_write.argtypes = [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, ctypes.c_double]
+        lib.fm_ring_write.restype = None
+    if hasattr(lib, "fm_count_finite"):
+        lib.fm_count_finite.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp]
+        lib.fm_count_finite.restype = None
     if hasattr(lib, "fm_fault_mag"):
         lib.fm_fault_mag.argtypes = [ctypes.c_char_p, c_vp, c_i64, ctypes.c_char_p, c_vp, c_i64, c_vp, c_vp]
         lib.fm_fault_mag.restype = None
@@ -326,3 +332,28 @@ def fault_mag(keys: list[str], subs: list[str], mags: list[float]) -> np.ndarray
     lib.fm_fault_mag(b"".join(kb), koff.ctypes.data, len(kb), b"".join(sb), soff.ctypes.data, len(sb),
                      m.ctypes.data, out.ctypes.data)
     return out
+
+
+def count_finite(a: np.ndarray) -> np.ndarray:
+    """np.isfinite(a).sum(1) of a 2-D float32 array with unit column stride."""
+    lib = _load()
+    if (lib is None or not hasattr(lib, "fm_count_finite") or a.dtype != np.float32 or a.ndim != 2
+            or a.strides[1] != 4 or a.strides[0] % 4):
+        return np.isfinite(a).sum(1)
+    out = np.empty(a.shape[0], np.int64)
+    lib.fm_count_finite(a.ctypes.data, a.shape[0], a.shape[1], a.strides[0] // 4, out.ctypes.data)
+    return out
+
+
+def ring_write(ring: np.ndarray, top_old: int, top_new: int, r: np.ndarray, t: np.ndarray, v: np.ndarray,
+               step: float) -> bool:
+    """fm_ring_write (False: no library, the caller does it in numpy)."""
+    lib = _load()
+    if lib is None or not hasattr(lib, "fm_ring_write") or not ring.flags.c_contiguous:
+        return False
+    r = np.ascontiguousarray(r, np.int64)
+    t = np.ascontiguousarray(t, np.float64)
+    v = np.ascontiguousarray(v, np.float32)
+    lib.fm_ring_write(ring.ctypes.data, ring.shape[0], ring.shape[1], int(top_old), int(top_new), r.ctypes.data,
+                      t.ctypes.data, v.ctypes.data, len(r), float(step))
+    return True

@@ -315,3 +315,28 @@ def test_job_ids_index_in_finds_survivors_or_none():
     sid = dead.serial
     del dead
     assert JobIds(objs[:3] + [W()]).index_in(JobIds(objs)) is None and sid not in JobIds(objs).arr
+
+
+def test_native_ring_write_and_finite_count_match_numpy():
+    """fm_ring_write (clear the columns entering the ring, store in-range
+    finite samples) and fm_count_finite against their numpy forms."""
+    from foremast_amd.engine import native_rt
+    if not native_rt.available():
+        pytest.skip("native runtime not built")
+    rng = np.random.default_rng(5)
+    W, R, step = 64, 300, 60.0
+    a = rng.normal(size=(R, W)).astype(np.float32)
+    a[rng.random((R, W)) < 0.2] = np.nan
+    b = a.copy()
+    top_old, top_new = 1000, 1003
+    r = rng.integers(0, R, 500)
+    c = rng.integers(top_new - 70, top_new + 1, 500)
+    t = c * step
+    v = rng.normal(size=500).astype(np.float32)
+    v[::7] = np.nan
+    assert native_rt.ring_write(a, top_old, top_new, r, t, v, step)
+    b[:, np.arange(top_old + 1, top_new + 1) % W] = np.nan
+    keep = np.isfinite(v) & (c > top_new - W)
+    b[r[keep], c[keep] % W] = v[keep]
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(native_rt.count_finite(a[:, 5:40]), np.isfinite(a[:, 5:40]).sum(1))
