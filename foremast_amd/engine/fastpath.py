@@ -437,6 +437,7 @@ class FastPath:
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
         self._slide_state: dict = {}
         self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
+        self._hist_pending = False  # a per-job fetch left history in some FastWork.hist this cycle
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
         self._gstat: dict = {}    # group key -> (job ids, positions, per-job static columns)
@@ -774,6 +775,7 @@ class FastPath:
                 ss = [Series({}, t, v) for t, v in per.get(app, [])]
                 v, _ = _app_level(ss)
                 fw.hist.append((i, np.asarray([_app_level_last(ss)]), v))
+                self._hist_pending = True
         lid = {id(fw) for fw in left}
         for fw in ws:
             if id(fw) not in lid:
@@ -984,10 +986,11 @@ class FastPath:
         # group's arrays are rebuilt from self._col every cycle regardless)
         prev = self._slide_state.get(p0.group)
         if prev is None or prev[1] != wclass or (prev[0] != ids and ids.index_in(prev[0]) is None):
-            # (a list that only lost jobs since: the survivors' state is set)
+            # (a list that only lost jobs since: the survivors' state is set;
+            # the group's arrays rebuild from self._col, so not dirty)
             for fw in ws:
                 fw.has_window = True
-                fw.dirty = True
+                fw.dirty = False
                 fw.settled = False
                 fw.wclass = wclass
                 fw.hist = []
@@ -1125,6 +1128,7 @@ class FastPath:
                             v, _ = _app_level(got)
                             t = np.asarray([_app_level_last(got)])
                         fw.hist.append((i, t, v))
+                        self._hist_pending = True
                     except (SourceError, OSError, ValueError) as e:
                         fw.errors.append(f"historical/{a}: {e}")
         if tab:
@@ -1150,6 +1154,9 @@ class FastPath:
     def stage_history(self, works: list[FastWork] | None = None) -> None:
         """Scatter the history fetched this cycle (jobs in ``self.todo``)
         into the resident stores."""
+        if works is None and not self._hist_pending:
+            return                       # nothing fetched per job this cycle (column-wise groups write directly)
+        self._hist_pending = False
         srows, svals, stl = [], [], []
         drows, dts, dvs = [], [], []
         got = [fw for fw in (self.todo if works is None else works) if fw.hist]
@@ -1269,8 +1276,11 @@ class FastPath:
         if xslots is not None:
             ga.export_slots = xslots
             ga.export_start = self.b.exporter.contiguous_start(xslots)
-        for w in works:
-            w.dirty = False
+        if col is None:
+            # (a column-wise fetched group rebuilds from self._col every cycle
+            # whatever its jobs' flags: no per-job reset)
+            for w in works:
+                w.dirty = False
         ga.key = key
         self._garr[key] = ga
         return ga
