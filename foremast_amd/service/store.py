@@ -509,11 +509,8 @@ class _Session:
     def snapshot(self, limit: int):
         if self._snap is None:
             ids = list(self.held)
-            if ids:
-                rids, vers = zip(*self.held.values())          # C-level transpose of (rid, version)
-                self._snap = (ids, list(vers), np.array(rids, np.int64))
-            else:
-                self._snap = (ids, [], np.zeros(0, np.int64))
+            rv = list(self.held.values())
+            self._snap = (ids, [v for _, v in rv], np.fromiter((r for r, _ in rv), np.int64, len(rv)))
         ids, vers, rids = self._snap
         n = len(ids)
         if n <= limit:
