@@ -1955,11 +1955,10 @@ class FastPath:
 
     def _finish_hpa(self, works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga=None) -> None:
         S = len(works)
-        fin = np.isfinite(cur)
-        n = cur.shape[1]
-        last = n - 1 - np.argmax(fin[:, ::-1], axis=1)
-        has = fin.any(1)
-        cl = np.where(has, cur[np.arange(len(cur)), last], np.nan).astype(np.float32).reshape(S, M)
+        last = _last_finite(cur)                    # (rows with no point: the last column, NaN)
+        lastv = cur[np.arange(len(cur)), last]
+        has = np.isfinite(lastv)
+        cl = lastv.astype(np.float32).reshape(S, M)
         up = np.where(has, stats[:, 2], np.nan).astype(np.float32).reshape(S, M)
         lo = np.where(has, stats[:, 3], np.nan).astype(np.float32).reshape(S, M)
         tmpl = works[0].plan.tmpl
