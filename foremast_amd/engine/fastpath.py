@@ -85,7 +85,7 @@ class JobPlan:
     algos: tuple = ()                      # canonical ML_ALGORITHM per metric (metric_typeN overrides)
 
 
-@dataclass(eq=False)          # identity: list membership tests are C-level (no field compare)
+@dataclass(eq=False, slots=True)   # identity compare (C-level list membership), slotted attributes
 class FastWork:
     """A job's fast-path state.  It persists across the cycles the job is
     re-examined (keyed by job id), so the steady state costs no per-job
