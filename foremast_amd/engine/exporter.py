@@ -90,6 +90,7 @@ class GaugeTable:
         self.version = 0                         # bumped by every write (publication cadence)
         self._free: list[int] = []
         self._nret = 0                           # slots retiring (finite expire)
+        self._next_exp = np.inf                  # lower bound of the retiring slots' expiry times
         self._fam_of: dict[str, int] = {}
         self._fam_names: list[str] = []
         self._fprefix: list[bytearray] = []      # per family: concatenated line prefixes
@@ -220,6 +221,8 @@ class GaugeTable:
             ex = self.expire[slots]
             new = ex == np.inf
             self.expire[slots[new]] = now + ttl
+            if new.any():
+                self._next_exp = min(self._next_exp, now + ttl)
             self._nret += int(new.sum())
             return int(new.sum())
 
@@ -230,11 +233,14 @@ class GaugeTable:
 
     def sweep(self, now: float) -> int:
         """Drop every retired slot whose time has come.  Returns the count."""
-        if not self._nret:
-            return 0
+        if not self._nret or now < self._next_exp:
+            return 0                      # nothing retiring, or nothing due yet (no pass over the slots)
         with self.lock:
             n = len(self.keys)
-            dead = np.flatnonzero(self.expire[:n] <= now)
+            ex = self.expire[:n]
+            dead = np.flatnonzero(ex <= now)
+            later = ex[(ex > now) & (ex < np.inf)]
+            self._next_exp = float(later.min()) if len(later) else np.inf
             if not len(dead):
                 return 0
             fams = set()
