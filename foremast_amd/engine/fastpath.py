@@ -320,11 +320,12 @@ class JobIds:
     of this list's jobs in an earlier list (sorted search, no per-job dict)
     -- how a churned list (jobs left) re-indexes the previous list's memos."""
 
-    __slots__ = ("arr", "_order")
+    __slots__ = ("arr", "_order", "_ixc")
 
     def __init__(self, works) -> None:
         self.arr = np.fromiter(map(_serial_of, works), np.int64, len(works))
         self._order = None
+        self._ixc = None          # (old, positions): the group memos all ask about the same old list
 
     def __len__(self) -> int:
         return len(self.arr)
@@ -338,6 +339,14 @@ class JobIds:
     __hash__ = None
 
     def index_in(self, old: "JobIds") -> np.ndarray | None:
+        c = self._ixc
+        if c is not None and c[0] is old:
+            return c[1]
+        ix = self._index_in(old)
+        self._ixc = (old, ix)
+        return ix
+
+    def _index_in(self, old: "JobIds") -> np.ndarray | None:
         if not len(self.arr) or not len(old.arr):
             return None
         if old._order is None:
