@@ -561,7 +561,10 @@ class FastPath:
         last = self._last
         if last is not None and batch.ids == last[0] and batch.versions == last[1]:
             fast = last[2]
-            todo = [fw for fw in last[3] if not ((immutable or fw.wcur is not None) and fw.settled)]
+            if len(self._gcount) == 1 and fast and fast[0].plan.sliding:
+                todo = fast                           # one sliding group: every job is due every cycle
+            else:
+                todo = [fw for fw in last[3] if not ((immutable or fw.wcur is not None) and fw.settled)]
             # every job due (sliding fleets): the job list itself, one JobIds per cycle
             self.todo = fast if len(todo) == len(fast) else todo
             self._reused = True
@@ -574,9 +577,12 @@ class FastPath:
         # lost jobs since the last claim): the lists through C-level passes
         fws = list(map(works.get, batch.ids))
         if None not in fws and list(map(_version_of, fws)) == list(batch.versions):
-            todo = [fw for fw in fws if not ((immutable or fw.wcur is not None) and fw.settled)]
-            if len(todo) == len(fws):
-                todo = fws
+            if len(self._gcount) == 1 and fws and fws[0].plan.sliding:
+                todo = fws                            # one sliding group: every job is due every cycle
+            else:
+                todo = [fw for fw in fws if not ((immutable or fw.wcur is not None) and fw.settled)]
+                if len(todo) == len(fws):
+                    todo = fws
             self._specs = {}
             self.todo = todo
             self._last = (batch.ids, batch.versions, fws, todo)
