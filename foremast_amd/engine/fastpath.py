@@ -859,8 +859,19 @@ class FastPath:
             # a list that only lost / reordered jobs (fleet churn: a job closed)
             # is a fancy-index of the previous one, not a per-job rebuild
             ix = ids.index_in(memo[0]) if memo is not None else None
+            one_store: dict = {}                  # (f, m) -> the store every job's query uses
             if ix is not None:
-                arrs = {k: a[ix] for k, a in memo[4].items()}
+                arrs = {}
+                for k, a in memo[4].items():
+                    if k[0].endswith("_stores"):
+                        sp = memo[1][(k[0][:-len("_stores")] + "_urls", k[1])].split
+                        if sp is not None and len(sp[1]) == 1:
+                            (s0, have), = sp[1].items()
+                            if len(have) == len(a):
+                                one_store[k] = s0
+                                arrs[k] = np.full(S, s0, object)
+                                continue
+                    arrs[k] = a[ix]
                 rows = memo[2][ix]
             else:
                 arrs = {}
@@ -888,7 +899,8 @@ class FastPath:
                 if merged and _MERGED:                    # only the history templates are ever read
                     arrs = {k: a for k, a in arrs.items() if k[0] in ("hist_urls", "hist_stores")}
             if ix is not None:
-                lists = {k: TemplateList.subset(memo[1][k], a.tolist(), ix) for k, a in arrs.items()}
+                lists = {k: TemplateList.subset(memo[1][k], [one_store[k]] * S if k in one_store else a.tolist(), ix)
+                         for k, a in arrs.items()}
                 for (f, m), tl in lists.items():          # one store, every job queried: so is the subset
                     if f.endswith("_urls"):
                         sp = memo[1][(f, m)].split
