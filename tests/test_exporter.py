@@ -179,3 +179,23 @@ def test_brain_retires_closed_jobs_gauges_after_ttl():
     assert b'app="c0-' not in body and b'app="c1-' not in body
     assert b'app="c3-5"' in body
     assert len(exp.table) <= 3 * 6 * 2
+
+
+def test_sweep_waits_for_each_retirement_in_turn():
+    """The sweep skips cycles until the earliest retiring slot is due, then
+    re-arms for the next one (no per-cycle pass over every slot)."""
+    e = BrainExporter()
+    for app in ("a", "b"):
+        e.set_bounds("namespace_app_pod_cpu", "ns", app, 1.0, 0.0, float("nan"))
+    t = 1000.0
+    e.retire_jobs([(["namespace_app_pod_cpu"], "ns", "a", "")], t, 60)
+    e.retire_jobs([(["namespace_app_pod_cpu"], "ns", "b", "")], t + 100, 60)
+    e.sweep(t + 59)
+    assert b'app="a"' in e.render() and b'app="b"' in e.render()
+    e.sweep(t + 61)
+    body = e.render()
+    assert b'app="a"' not in body and b'app="b"' in body
+    e.sweep(t + 159)
+    assert b'app="b"' in e.render()
+    e.sweep(t + 161)
+    assert b'app="b"' not in e.render()

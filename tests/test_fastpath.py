@@ -340,3 +340,30 @@ def test_native_ring_write_and_finite_count_match_numpy():
     b[r[keep], c[keep] % W] = v[keep]
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(native_rt.count_finite(a[:, 5:40]), np.isfinite(a[:, 5:40]).sum(1))
+
+
+def test_window_helpers_match_numpy_forms():
+    """_last_finite / _bcast_row / _device_horizons (merged sliding groups)
+    against the straightforward numpy expressions they replace."""
+    import torch
+    from foremast_amd.engine.fastpath import _bcast_row, _device_horizons, _last_finite
+    rng = np.random.default_rng(11)
+    cur = rng.normal(size=(200, 9)).astype(np.float32)
+    cur[rng.random(cur.shape) < 0.3] = np.nan
+    cur[5] = np.nan                                             # a row with no point
+    fin = np.isfinite(cur)
+    want = np.where(fin.any(1), 9 - 1 - np.argmax(fin[:, ::-1], axis=1), 9 - 1)
+    np.testing.assert_array_equal(_last_finite(cur), want)
+    step = 60.0
+    trow = step * np.arange(100, 109, dtype=np.float64)
+    ct = np.broadcast_to(trow, (200, 9))
+    assert _bcast_row(ct) is trow or np.array_equal(_bcast_row(ct), trow)
+    assert _bcast_row(np.ascontiguousarray(ct)) is None             # a materialised copy is not broadcast
+    t_last = step * rng.integers(90, 108, 200).astype(np.float64)
+    t_last[::17] = np.nan
+    ok = np.isfinite(ct) & np.isfinite(t_last)[:, None]
+    with np.errstate(invalid="ignore"):
+        h = np.where(ok, np.rint((ct - t_last[:, None]) / step), 1.0)
+    want_h = np.maximum(1, h).astype(np.int64)
+    got = _device_horizons(torch.from_numpy(trow), torch.from_numpy(t_last), step).numpy()
+    np.testing.assert_array_equal(got, want_h)
