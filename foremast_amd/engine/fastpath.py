@@ -2136,8 +2136,8 @@ def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> 
         if not sel:
             continue
         keys = [keys[i] for i in sel]
-        ix = torch.as_tensor(sel, dtype=torch.int64)
-        v = vals.index_select(0, ix)
+        # every saved row is this rank's (no re-shard): no host copy of the block
+        v = vals if len(sel) == vals.shape[0] else vals.index_select(0, torch.as_tensor(sel, dtype=torch.int64))
         last_t = t[f"{name}.last_t"].numpy()[sel]
         rows, _ = st.rows_for(keys, fp.cycle)
         rows = rows.astype(np.int64)
@@ -2155,12 +2155,16 @@ def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> 
                                            [:, st.ws:st.e]).sum(1).cpu().numpy()
         else:
             w = min(v.shape[1], st.width)
-            full = torch.full((len(rows), st.width), float("nan"))
-            full[:, :w] = v[:, :w]
-            st.buf.index_copy_(0, torch.as_tensor(rows, device=st.device), full.to(st.device))
+            vd = (v if w == v.shape[1] else v[:, :w]).to(st.device)        # one host -> device copy
+            if w < st.width:
+                full = torch.full((len(rows), st.width), float("nan"), device=st.device)
+                full[:, :w] = vd
+            else:
+                full = vd
+            st.buf.index_copy_(0, torch.as_tensor(rows, device=st.device), full)
             nlen = t[f"{name}.nlen"].numpy()[sel]
             st.nlen[rows] = np.minimum(nlen, st.width)
-            st.nfin[rows] = torch.isfinite(full).sum(1).numpy()
+            st.nfin[rows] = torch.isfinite(vd).sum(1).cpu().numpy()
             st.last_t[rows] = last_t
             st.max_len = max(st.max_len, int(st.nlen[rows].max()) if len(rows) else 0)
         n_rows += len(rows)
