@@ -711,7 +711,32 @@ class FastPath:
         if not owners:
             return
         wt = self.wt
-        wids = wt.add_many(specs, lives, stores)
+        wids = np.asarray(wt.add_many(specs, lives, stores), np.int64)
+        # window ids of every job as one [jobs, windows] matrix (jobs of one
+        # shape, the usual claim): presence mask, ids, liveness and the widest
+        # window per job in array passes
+        W = len(owners[0][1])
+        if all(len(m) == W for _, m in owners):
+            n = len(owners)
+            present = np.fromiter((x is not None for _, m in owners for x in m), bool, n * W).reshape(n, W)
+            ids_m = np.full((n, W), -1, np.int64)
+            ids_m[present] = wids
+            lv = np.zeros((n, W), bool)
+            lv[present] = np.asarray(lives, bool)
+            live_j = lv.any(1).tolist()
+            ok = np.maximum(ids_m, 0)
+            size = np.where(present, wt.nslot[ok] * wt.ncol[ok], 0)
+            wmax = size.max(1).tolist() if W else [0] * n
+            for j, (fw, _) in enumerate(owners):
+                M = len(fw.plan.aliases)
+                ids = ids_m[j]
+                fw.wcur, fw.wbase = ids[:M], ids[M:]
+                fw.has_window = True
+                if live_j[j]:
+                    fw.end_ts += wt.settle      # the last grid point is read settle seconds after its time
+                w = int(wmax[j])
+                fw.wclass = 0 if w <= 128 else (1 if w <= 256 else 2)
+            return
         k = 0
         for fw, mine in owners:
             ids = np.full(len(mine), -1, np.int64)
