@@ -271,11 +271,12 @@ class ResidentHistory:
         ok = (c >= self.ws) & (c < self.e) & np.isfinite(v)
         r, c, v, t = r[ok], c[ok], v[ok], t[ok]
         if len(r):
-            prev = np.where(np.isfinite(self.last_t[r]), self.col(np.where(np.isfinite(self.last_t[r]),
-                                                                            self.last_t[r], self.t0)), -1)
+            lt = self.last_t[r]
+            fl = np.isfinite(lt)
+            prev = np.where(fl, self.col(np.where(fl, lt, self.t0)), -1)
             if np.bincount(r).max() <= 1:                 # one sample per row (a 60-s poll): plain indexing
                 self.nfin[r] += c > prev
-                self.last_t[r] = np.maximum(self.last_t[r], t)
+                self.last_t[r] = np.maximum(lt, t)
             else:
                 np.add.at(self.nfin, r[c > prev], 1)      # new columns only (a re-sent sample counts once)
                 np.maximum.at(self.last_t, r, t)
