@@ -291,7 +291,8 @@ def config3e2e(args):
             cw = ClockWriter(clock_file, t["now"])
             prom = subprocess.Popen([sys.executable, "-m", "foremast_amd.demo.promserver", "--port", "0",
                                      "--clock-file", clock_file, "--faults", _json.dumps(faults),
-                                     "--fault-after", str(fault_after), "--workers", str(args.prom_workers)],
+                                     "--fault-after", str(fault_after), "--workers", str(args.prom_workers)]
+                                    + (["--python"] if args.prom_python else []),
                                     cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     stdout=subprocess.PIPE, text=True)
             prom_port = int(prom.stdout.readline().split()[1])
@@ -402,6 +403,7 @@ def config3e2e(args):
             raise SystemExit("REST poller did not start")
 
     req_log = []
+    http_stats: list = []                   # PrometheusSource.stats deltas per cycle (attributed fetch span)
     cyc_ms: list[float] = []
     # FOREMAST_PROFILE_CYCLES=<path>: cProfile of the timed cycles only
     _prof = None
@@ -417,6 +419,8 @@ def config3e2e(args):
         if cw is not None:
             cw.set(t["now"])
         n0 = (live.requests, live.bytes) if live is not None else (0, 0)
+        st0 = dict(live.stats) if live is not None else None
+        wt0 = brain.fast.wt.apply_s if brain.fast is not None else 0.0
         tc = time.perf_counter()
         if _prof is not None and len(cyc_ms) >= args.warmup:
             r = _prof.runcall(brain.run_once)
@@ -426,6 +430,9 @@ def config3e2e(args):
         rows.append(r.get("rows", 0))
         if live is not None:
             req_log.append((live.requests - n0[0], live.bytes - n0[1]))
+            d = {k: live.stats[k] - st0[k] for k in st0}
+            d["split_s"] += (brain.fast.wt.apply_s - wt0) if brain.fast is not None else 0.0
+            http_stats.append(d)
         for k, v in brain.spans.last.items():
             spans.setdefault(k, []).append(v * 1e3)
 
@@ -545,7 +552,19 @@ def config3e2e(args):
                        "kbytes_per_cycle_mean": round(statistics.mean(b for _, b in req_log[args.warmup:]) / 1e3, 1),
                        "requests_total_timed": sum(x for x, _ in req_log[args.warmup:]),
                        "window_table_requests_total": brain.fast.wt.requests if brain.fast is not None else None,
-                       "prom_workers": args.prom_workers}
+                       "prom_workers": args.prom_workers,
+                       "server": "native (csrc/runtime/fakeprom.cpp)" if not args.prom_python else
+                                 f"python x {args.prom_workers}",
+                       # the fetch span attributed (median per cycle): summed over the
+                       # cycle's requests (they overlap on the client's connections) --
+                       # the server's own time (X-Fm-Server-Us), wait for the first
+                       # byte, receive, parse; join = writing the answers into the
+                       # window table / joining them to the templates (wall)
+                       "per_cycle_ms_summed_over_requests": {
+                           k: round(1e3 * statistics.median(d[k] for d in http_stats[args.warmup:]), 2)
+                           for k in ("server_s", "wait_s", "recv_s", "parse_s", "request_s")},
+                       "join_ms": round(1e3 * statistics.median(d["split_s"] for d in http_stats[args.warmup:]), 2),
+                       "client_connections": live.workers}
                       if live is not None and req_log[args.warmup:] else None),
              "scraper": {"interval_s": args.scrape_interval, "scrapes": len(scrapes),
                          "render_ms_median": round(1e3 * statistics.median([x for x, _ in scrapes]), 2)
@@ -672,7 +691,10 @@ def main():
                     "over this many seconds (canary windows at every phase of the 60-s grid; default 60)")
     ap.add_argument("--restart", action="store_true", help="e2e configs: after the timed cycles, checkpoint and "
                     "restart the brain (engine state + resident history) and time restart-to-first-verdict")
-    ap.add_argument("--prom-workers", type=int, default=4, help="e2e --source http: fake Prometheus processes")
+    ap.add_argument("--prom-workers", type=int, default=4, help="e2e --source http: fake Prometheus processes "
+                    "(--prom-python)")
+    ap.add_argument("--prom-python", action="store_true", help="e2e --source http: the Python fake Prometheus "
+                    "instead of the native responder")
     ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "
                     "body every N seconds in a thread while the cycles are timed (0: off)")
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "

@@ -84,16 +84,26 @@ bool read_key(Cursor& c, std::string& out) {
 }
 
 double parse_number_token(Cursor& c) {
-  // in place: strtod stops at the closing quote / ',' / ']' and understands
-  // Prometheus' "NaN", "+Inf", "-Inf" spellings; the document buffer is
-  // terminated by its closing brace so strtod cannot run off the end.
+  // in place, std::from_chars (no locale, no allocation); Prometheus' "NaN",
+  // "+Inf", "-Inf" spellings: from_chars reads "NaN" / "Inf" / "-Inf" but not
+  // a leading '+', which is skipped first.
   c.ws();
   const bool quoted = c.p < c.e && *c.p == '"';
   if (quoted) ++c.p;
-  char* end = nullptr;
-  const double v = std::strtod(c.p, &end);
-  if (end == c.p || end > c.e) { c.ok = false; return NAN; }
-  c.p = end;
+  const char* s = c.p;
+  if (s < c.e && *s == '+') ++s;
+  double v = NAN;
+  const auto r = std::from_chars(s, c.e, v);
+  if (r.ec != std::errc() || r.ptr == s) {
+    // a spelling from_chars does not take (e.g. a hex float): strtod, bounded by
+    // the document's closing brace
+    char* end = nullptr;
+    v = std::strtod(c.p, &end);
+    if (end == c.p || end > c.e) { c.ok = false; return NAN; }
+    c.p = end;
+  } else {
+    c.p = r.ptr;
+  }
   if (quoted) {
     if (c.p < c.e && *c.p == '"') ++c.p; else c.ok = false;
   }

@@ -14,13 +14,19 @@
 Only plain vector selectors whose key matcher is ``=`` or a ``=~``
 alternation of literals are supported (what barrelman and the brain send,
 foremast-barrelman/pkg/client/metrics/metricsquery.go:72-99); anything else is
-a 400 ``bad_data``.  The response body is formatted natively
-(``fm_prom_format``).  ``--workers N`` pre-forks N processes on one listening
-socket (keep-alive HTTP/1.1).
+a 400 ``bad_data``.
+
+Two responders give the same answers: the native one
+(``csrc/runtime/fakeprom.cpp``, the default: one process, a thread per
+keep-alive connection, query plans shared by all of them -- the HTTP benches
+measure the brain's client, not this server) and :class:`FakePrometheus`
+here (``--python``; ``--workers N`` single-threaded event-loop processes on
+SO_REUSEPORT listeners; tests call :meth:`FakePrometheus.answer` in-process).
+Every answer carries ``X-Fm-Server-Us``, the server's own time for it.
 
 Run: ``python -m foremast_amd.demo.promserver --port 0 [--clock-file F]
-[--faults JSON] [--fault-after T] [--workers N]`` prints ``port <n>`` once it
-listens.
+[--faults JSON] [--fault-after T] [--python [--workers N]]`` prints
+``port <n>`` once it listens.
 """
 from __future__ import annotations
 
@@ -31,8 +37,8 @@ import mmap
 import os
 import socket
 import sys
+import time
 import urllib.parse
-from http.server import BaseHTTPRequestHandler, HTTPServer
 
 import numpy as np
 
@@ -82,6 +88,7 @@ class FakePrometheus:
         self.clock = clock or Clock(None)
         self.requests = 0
         self._plans: dict = {}           # query text -> parsed series plan (a brain repeats its unions)
+        self._plans_raw: dict = {}       # encoded query bytes -> query text
 
     def _plan(self, q: str, step: float):
         got = self._plans.get(q)
@@ -113,7 +120,9 @@ class FakePrometheus:
         lab[key] = mark
         pre, post = json.dumps({"__name__": metric, **dict(sorted(lab.items()))},
                                separators=(",", ":")).split(json.dumps(mark))
-        plan = (sig, noise, identities(group, vals), [pre + json.dumps(x) + post for x in vals], len(vals))
+        fk = identities(group, vals)
+        plan = (sig, noise, fk, native_rt.joined_labels([pre + json.dumps(x) + post for x in vals]), len(vals),
+                self.src.prepare(sig, noise, fk))
         if len(self._plans) > 4096:
             self._plans.clear()
         self._plans[q] = plan
@@ -132,50 +141,99 @@ class FakePrometheus:
         plan = self._plan(q, step)
         if isinstance(plan, str):
             return 400, json.dumps({"status": "error", "errorType": "bad_data", "error": plan}).encode()
-        sig, noise, fk, labels, nv = plan
+        sig, noise, fk, labels, nv, prep = plan
         hi = min(end, self.clock.now())
         n = int(math.floor((hi - start) / step + 1e-9)) + 1 if hi >= start else 0
         tg = start + step * np.arange(max(n, 0))
         raw = self.src.step
         tr = np.floor(tg / raw + 1e-9) * raw                     # newest raw sample at or before each point
-        grid = self.src.many(sig, noise, fk, tr) if n > 0 else np.zeros((nv, 0), np.float32)
+        if n <= 0:
+            grid = np.zeros((nv, 0), np.float32)
+        else:
+            grid = self.src.many_prepared(prep, tr)
+            if grid is None:
+                grid = self.src.many(sig, noise, fk, tr)
         return 200, native_rt.format_matrix(labels, float(start), float(step), grid)
 
 
-def make_handler(fp: FakePrometheus):
-    class H(BaseHTTPRequestHandler):
-        protocol_version = "HTTP/1.1"
+    def answer_raw(self, raw: bytes) -> tuple[int, bytes]:
+        """:meth:`answer` from the raw (still percent-encoded) parameter
+        string of a GET query or a form POST body: a brain repeats its unions
+        every cycle, so the plan is looked up by the encoded query text and
+        only a new query is decoded."""
+        params: dict = {}
+        for part in raw.split(b"&"):
+            k, _, v = part.partition(b"=")
+            params[k] = v
+        q = params.get(b"query")
+        if q is not None:
+            plan = self._plans_raw.get(q)
+            if plan is None:
+                text = urllib.parse.unquote_plus(q.decode("ascii", "replace"))
+                if len(self._plans_raw) > 4096:
+                    self._plans_raw.clear()
+                plan = self._plans_raw[q] = text
+            params[b"query"] = plan
+        dec = {k.decode(): (v if isinstance(v, str) else urllib.parse.unquote_plus(v.decode("ascii", "replace")))
+               for k, v in params.items()}
+        return self.answer(dec)
 
-        def log_message(self, *a):                          # quiet
-            pass
 
-        def _send(self, code: int, body: bytes) -> None:
-            self.send_response(code)
-            self.send_header("Content-Type", "application/json")
-            self.send_header("Content-Length", str(len(body)))
-            self.end_headers()
-            self.wfile.write(body)
+class _Conn:
+    """One keep-alive HTTP/1.1 connection of the single-threaded event loop
+    (GET or form POST, Content-Length bodies): :meth:`feed` takes received
+    bytes and answers every complete request (one sendmsg each; TCP_NODELAY,
+    as Go sets it).  Returns False when the connection is done."""
 
-        def _route(self, params: dict) -> None:
-            path = urllib.parse.urlsplit(self.path).path
-            if path.endswith("/api/v1/query_range"):
-                self._send(*fp.answer(params))
-            elif path.endswith("/-/healthy"):
-                self._send(200, b"ok")
+    def __init__(self, conn: socket.socket, fp: FakePrometheus):
+        self.conn = conn
+        self.fp = fp
+        self.buf = b""
+        conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+
+    def feed(self, data: bytes) -> bool:
+        self.buf += data
+        while True:
+            i = self.buf.find(b"\r\n\r\n")
+            if i < 0:
+                return True
+            head = self.buf[:i]
+            lines = head.split(b"\r\n")
+            try:
+                method, target, ver = lines[0].split(b" ", 2)
+            except ValueError:
+                return False
+            hdrs = {}
+            for ln in lines[1:]:
+                k, _, v = ln.partition(b":")
+                hdrs[k.strip().lower()] = v.strip()
+            n = int(hdrs.get(b"content-length", b"0") or 0)
+            if len(self.buf) < i + 4 + n:
+                return True                               # the body is still arriving
+            t0 = time.perf_counter()
+            body = self.buf[i + 4:i + 4 + n]
+            self.buf = self.buf[i + 4 + n:]
+            path, _, qs = target.partition(b"?")
+            if path.endswith(b"/api/v1/query_range"):
+                raw = qs + (b"&" if qs and body else b"") + body if method == b"POST" else qs
+                code, out = self.fp.answer_raw(raw)
+            elif path.endswith(b"/-/healthy"):
+                code, out = 200, b"ok"
             else:
-                self._send(404, b'{"status":"error","error":"not found"}')
-
-        def do_GET(self):
-            self._route(dict(urllib.parse.parse_qsl(urllib.parse.urlsplit(self.path).query,
-                                                    keep_blank_values=True)))
-
-        def do_POST(self):
-            n = int(self.headers.get("Content-Length", "0"))
-            body = self.rfile.read(n).decode()
-            params = dict(urllib.parse.parse_qsl(urllib.parse.urlsplit(self.path).query, keep_blank_values=True))
-            params.update(urllib.parse.parse_qsl(body, keep_blank_values=True))
-            self._route(params)
-    return H
+                code, out = 404, b'{"status":"error","error":"not found"}'
+            keep = ver.strip() == b"HTTP/1.1" and hdrs.get(b"connection", b"").lower() != b"close"
+            hdr = (f"HTTP/1.1 {code} {'OK' if code == 200 else 'Error'}\r\nContent-Type: application/json\r\n"
+                   f"Content-Length: {len(out)}\r\nX-Fm-Server-Us: {int(1e6 * (time.perf_counter() - t0))}\r\n"
+                   + ("" if keep else "Connection: close\r\n") + "\r\n").encode()
+            self.conn.setblocking(True)                   # write the whole answer, then back to the loop
+            try:
+                self.conn.sendall(hdr + out if len(out) < 65536 else hdr)
+                if len(out) >= 65536:
+                    self.conn.sendall(out)
+            finally:
+                self.conn.setblocking(False)
+            if not keep:
+                return False
 
 
 def _die_with_parent() -> None:
@@ -189,22 +247,38 @@ def _die_with_parent() -> None:
         pass
 
 
-def serve(port: int, source: SyntheticSource, clock_file: str | None, workers: int = 1,
-          ready=sys.stdout) -> None:
+def _listener(port: int) -> socket.socket:
     sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
     sock.bind(("127.0.0.1", port))
     sock.listen(256)
-    print(f"port {sock.getsockname()[1]}", file=ready, flush=True)
-    kids = []
+    sock.setblocking(False)
+    return sock
+
+
+def serve(port: int, source: SyntheticSource, clock_file: str | None, workers: int = 1,
+          ready=sys.stdout) -> None:
+    """``workers`` processes, each a single-threaded event loop on its own
+    SO_REUSEPORT listener (the kernel spreads connections over them): no GIL
+    hand-offs between requests of one process."""
+    import selectors
     import signal
+    from ..ops import reference  # noqa: F401 - imported once here, not by every forked worker's first answer
+    sock = _listener(port)
+    port = sock.getsockname()[1]
+    kids = []
     for _ in range(max(0, workers - 1)):
         pid = os.fork()
         if pid == 0:
             kids = []
             _die_with_parent()
+            sock.close()
+            sock = _listener(port)
             break
         kids.append(pid)
+    if kids or workers <= 1:
+        print(f"port {port}", file=ready, flush=True)
     if kids:
         def _stop(*_):
             for k in kids:
@@ -216,20 +290,30 @@ def serve(port: int, source: SyntheticSource, clock_file: str | None, workers: i
         signal.signal(signal.SIGTERM, _stop)
         signal.signal(signal.SIGINT, _stop)
     fp = FakePrometheus(source, Clock(clock_file))
-    from socketserver import ThreadingMixIn
-
-    class Server(ThreadingMixIn, HTTPServer):
-        daemon_threads = True
-
-        def server_bind(self):                               # the shared, already listening socket
-            pass
-
-        def server_activate(self):
-            pass
-    srv = Server(("127.0.0.1", 0), make_handler(fp), bind_and_activate=False)
-    srv.socket = sock
+    sel = selectors.DefaultSelector()
+    sel.register(sock, selectors.EVENT_READ, None)
     try:
-        srv.serve_forever(poll_interval=0.2)
+        while True:
+            for key, _ in sel.select():
+                if key.data is None:
+                    try:
+                        conn, _ = sock.accept()
+                    except (BlockingIOError, InterruptedError):
+                        continue
+                    conn.setblocking(False)
+                    sel.register(conn, selectors.EVENT_READ, _Conn(conn, fp))
+                    continue
+                c = key.data
+                try:
+                    data = c.conn.recv(1 << 16)
+                    alive = bool(data) and c.feed(data)
+                except (BlockingIOError, InterruptedError):
+                    continue
+                except OSError:
+                    alive = False
+                if not alive:
+                    sel.unregister(c.conn)
+                    c.conn.close()
     except KeyboardInterrupt:
         pass
     finally:
@@ -240,16 +324,45 @@ def serve(port: int, source: SyntheticSource, clock_file: str | None, workers: i
                 pass
 
 
+def serve_native(port: int, source: SyntheticSource, clock_file: str | None, ready=sys.stdout) -> bool:
+    """The same answers from the native responder (csrc/runtime/fakeprom.cpp:
+    one process, a thread per connection, plans shared by every connection):
+    what the HTTP benches run, so a fetch span measures the brain's client and
+    not a Python server.  False when the library lacks it."""
+    import ctypes
+    lib = native_rt._load()
+    if lib is None or not hasattr(lib, "fm_fakeprom_serve"):
+        return False
+    c_vp = ctypes.c_void_p
+    lib.fm_fakeprom_serve.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, c_vp, ctypes.c_int64, c_vp,
+                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_uint32]
+    lib.fm_fakeprom_serve.restype = ctypes.c_int
+    sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    sock.bind(("127.0.0.1", port))
+    sock.listen(1024)
+    subs = list(source.faults)
+    fbuf, foff = native_rt.joined_labels(subs)
+    mags = np.ascontiguousarray([float(source.faults[k]) for k in subs] or [1.0], np.float64)
+    print(f"port {sock.getsockname()[1]}", file=ready, flush=True)
+    rc = lib.fm_fakeprom_serve(sock.fileno(), (clock_file or "").encode(), fbuf, foff.ctypes.data, len(subs),
+                               mags.ctypes.data, float(source.fault_after), float(source.step), float(source.noise),
+                               int(source.seed) & 0xFFFFFFFF)
+    raise SystemExit(f"native fake prometheus stopped (rc {rc})")
+
+
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--port", type=int, default=9090)
     ap.add_argument("--clock-file", default=None)
     ap.add_argument("--faults", default="{}", help="JSON {substring of a series identity: factor}")
     ap.add_argument("--fault-after", type=float, default=0.0)
-    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=1, help="Python responder: processes")
+    ap.add_argument("--python", action="store_true", help="the Python responder instead of the native one")
     a = ap.parse_args(argv)
     src = SyntheticSource(faults=json.loads(a.faults), fault_after=a.fault_after)
-    serve(a.port, src, a.clock_file, a.workers)
+    if a.python or not serve_native(a.port, src, a.clock_file):
+        serve(a.port, src, a.clock_file, a.workers)
 
 
 if __name__ == "__main__":

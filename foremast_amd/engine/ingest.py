@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import time
 import urllib.parse
 from dataclasses import dataclass
 from typing import NamedTuple
@@ -296,6 +297,7 @@ class WindowTable:
         self.alive = np.zeros(0, bool)
         self.dirty = np.zeros(0, bool)       # data changed since the scoring arrays last read it
         self.err = np.zeros(0, bool)         # last fetch of the window failed
+        self.dup = np.zeros(0, np.uint8)     # an answer carried two series of one key value (see apply)
         self.toff = np.zeros(0)              # sample phase vs start (0 for Prometheus; nan: not seen yet)
         self.values: list = []               # key values (sorted) per window
         self.frag: list = []                 # their escaped regex alternation
@@ -312,6 +314,7 @@ class WindowTable:
         self.next_due = -math.inf            # earliest time a live window can gain a grid point
         self.requests = 0                    # counters (bench / tests)
         self.last_requests = 0
+        self.apply_s = 0.0                   # time spent writing answers into the table
 
     # ------------------------------------------------------------ membership
     def _grow_w(self, need: int) -> None:
@@ -320,7 +323,7 @@ class WindowTable:
         cap = max(need, 2 * self._cap, 1024)
         for name, fill in (("start", 0.0), ("end", 0.0), ("step", 1.0), ("settled", 0.0), ("gid", 0),
                            ("slot0", -1), ("nslot", 0), ("ncol", 0), ("live", False), ("alive", False),
-                           ("dirty", False), ("err", False), ("toff", np.nan)):
+                           ("dirty", False), ("err", False), ("toff", np.nan), ("dup", 0)):
             old = getattr(self, name)
             a = np.full(cap, fill, old.dtype)
             a[:len(old)] = old
@@ -374,6 +377,7 @@ class WindowTable:
         self.settled[w] = spec.start - spec.step
         self.gid[w], self.slot0[w], self.nslot[w], self.ncol[w] = g, s0, len(vals), ncol
         self.live[w], self.alive[w], self.dirty[w], self.err[w] = live, True, True, False
+        self.dup[w] = 0
         self.toff[w] = np.nan
         self.values[w] = vals
         self.frag[w] = "|".join(promql.re_literal(v) for v in vals)
@@ -466,6 +470,7 @@ class WindowTable:
         self.gid[wids], self.slot0[wids], self.nslot[wids], self.ncol[wids] = gid, slot0, nsl, ncol
         self.live[wids] = np.asarray(lives, bool)
         self.alive[wids], self.dirty[wids], self.err[wids] = True, True, False
+        self.dup[wids] = 0
         self.toff[wids] = np.nan
         self.next_due = -math.inf
         return wids
@@ -558,6 +563,9 @@ class WindowTable:
             if cnt.any():
                 ser = np.repeat(np.arange(len(got.key)), cnt)             # (series, slot) pairs
                 pos = order[_ranges(a, cnt)]                              # index into kslots
+                many = np.bincount(pos, minlength=len(kslots)) > 1         # two series of one key value
+                if many.any():
+                    self.dup[self.kwin[kslots[many]]] = 1
                 slen = np.diff(got.off)[ser]
                 samp = _ranges(got.off[:-1][ser], slen)                   # (pair, sample)
                 pidx = np.repeat(pos, slen)
@@ -585,6 +593,58 @@ class WindowTable:
             due = np.where(self.live[w], self.settled[w] + self.step[w] + self.settle, -math.inf)
             self.next_due = min(self.next_due, float(due.min()))
 
+    def apply_many(self, parts: list, got: list) -> None:
+        """:meth:`apply` for one round's answers at once (``parts``: the
+        (window ids, lo, hi) of each request): the joins and grid writes run
+        natively (``fm_window_apply``), request-parallel; failed requests and
+        the settled / due bookkeeping as in :meth:`apply`."""
+        lib = native_rt._load()
+        if lib is None or not hasattr(lib, "fm_window_apply") or len(parts) < 2:
+            for (ws, lo, hi), g in zip(parts, got):
+                self.apply(ws, lo, hi, g)
+            return
+        ok = [i for i, g in enumerate(got) if not isinstance(g, BaseException)]
+        for i, g in enumerate(got):
+            if isinstance(g, BaseException):
+                self.apply(*parts[i], g)
+        if not ok:
+            return
+        if not getattr(lib, "_wa_typed", False):
+            c_vp, c_i64 = ctypes.c_void_p, ctypes.c_int64
+            lib.fm_window_apply.argtypes = [c_vp, c_i64] + [c_vp] * 7 + [c_i64] + [c_vp] * 10 + [ctypes.c_int]
+            lib.fm_window_apply.restype = None
+            lib._wa_typed = True
+        ws = np.concatenate([parts[i][0] for i in ok]).astype(np.int64, copy=False)
+        lo = np.concatenate([parts[i][1] for i in ok]).astype(np.float64, copy=False)
+        hi = np.concatenate([parts[i][2] for i in ok]).astype(np.float64, copy=False)
+        woff = np.zeros(len(ok) + 1, np.int64)
+        np.cumsum([len(parts[i][0]) for i in ok], out=woff[1:])
+        gs = [got[i] for i in ok]
+        soff = np.zeros(len(ok) + 1, np.int64)
+        np.cumsum([len(g.key) for g in gs], out=soff[1:])
+        kh = np.ascontiguousarray(np.concatenate([g.key for g in gs]), np.uint64)
+        pts = np.cumsum([0] + [len(g.t) for g in gs])
+        off = np.concatenate([g.off[:-1] + p for g, p in zip(gs, pts[:-1])] + [[pts[-1]]]).astype(np.int64)
+        t = np.ascontiguousarray(np.concatenate([g.t for g in gs]), np.float64)
+        v = np.ascontiguousarray(np.concatenate([g.v for g in gs]), np.float32)
+        if not self.V.flags.c_contiguous:
+            self.V = np.ascontiguousarray(self.V)
+        arrs = [self.khash, self.start, self.step, self.toff, self.ncol, self.slot0, self.nslot]
+        assert all(a.flags.c_contiguous for a in arrs)
+        lib.fm_window_apply(self.V.ctypes.data, self.V.shape[1], self.khash.ctypes.data, self.start.ctypes.data,
+                            self.step.ctypes.data, self.toff.ctypes.data, self.ncol.ctypes.data,
+                            self.slot0.ctypes.data, self.nslot.ctypes.data, len(ok), woff.ctypes.data,
+                            ws.ctypes.data, lo.ctypes.data, hi.ctypes.data, soff.ctypes.data, kh.ctypes.data,
+                            off.ctypes.data, t.ctypes.data, v.ctypes.data, self.dup.ctypes.data, 8)
+        self.err[ws] = False
+        self.settled[ws] = np.maximum(self.settled[ws], hi)
+        self.dirty[ws] = True
+        inc = self.settled[ws] < self.end[ws] - 1e-6
+        if inc.any():
+            w = ws[inc]
+            due = np.where(self.live[w], self.settled[w] + self.step[w] + self.settle, -math.inf)
+            self.next_due = min(self.next_due, float(due.min()))
+
     def fetch(self, router, now: float, pool=None) -> int:
         """One incremental round: every due request, per metric store through
         its source's ``fetch_keyed`` (``router``: a SourceRouter, or one source
@@ -603,9 +663,9 @@ class WindowTable:
                 got = [SourceError(f"no batched source for metric store {store!r}")] * len(idx)
             else:
                 got = src.fetch_keyed([reqs[i][0] for i in idx], pool=pool)
-            for i, g in zip(idx, got):
-                _, ws, lo, hi = reqs[i]
-                self.apply(ws, lo, hi, g)
+            t0 = time.perf_counter()
+            self.apply_many([reqs[i][1:] for i in idx], got)
+            self.apply_s += time.perf_counter() - t0
         self.requests += len(reqs)
         return len(reqs)
 

@@ -177,20 +177,30 @@ def parse_keyed(body: bytes, label: str) -> Keyed:
     return Keyed(kh, off, t, v)
 
 
-def format_matrix(labels_json: list[str], t0: float, step: float, values: np.ndarray) -> bytes:
+def format_matrix(labels_json, t0: float, step: float, values: np.ndarray) -> bytes:
     """A query_range matrix response body: series i has the pre-rendered
     ``labels_json[i]`` and the samples ``values[i, k]`` at ``t0 + k * step``
-    (NaN samples left out)."""
+    (NaN samples left out).  ``labels_json`` may be the ``(bytes, offsets)``
+    of :func:`joined_labels` (a server answering the same union repeatedly)."""
     values = np.ascontiguousarray(values, np.float32)
-    n, npts = values.shape if values.ndim == 2 else (len(labels_json), 0)
+    if isinstance(labels_json, tuple):
+        lbuf, loff = labels_json
+        labels_json = None
+        n = len(loff) - 1
+    else:
+        lbuf = loff = None
+    n, npts = values.shape if values.ndim == 2 else ((len(labels_json) if labels_json is not None else n), 0)
     lib = _load()
     if lib is None:
+        if labels_json is None:
+            labels_json = [lbuf[a:b].decode() for a, b in zip(loff[:-1].tolist(), loff[1:].tolist())]
         parts = []
         for i, lab in enumerate(labels_json):
             pts = ",".join(f'[{t0 + step * k:g},"{float(x)!r}"]' for k, x in enumerate(values[i]) if x == x)
             parts.append('{"metric":' + lab + ',"values":[' + pts + "]}")
         return ('{"status":"success","data":{"resultType":"matrix","result":[' + ",".join(parts) + "]}}").encode()
-    lbuf, loff = _joined(labels_json)
+    if lbuf is None:
+        lbuf, loff = _joined(labels_json)
     cap = lib.fm_prom_format_bound(n, npts, len(lbuf))
     out = np.empty(cap, np.uint8)
     w = lib.fm_prom_format(n, lbuf, loff.ctypes.data, float(t0), float(step), npts, values.ctypes.data,
@@ -235,6 +245,10 @@ def pack_right(rows: list[np.ndarray], ncols: int, ld: int, threads: int = 4) ->
     lens = np.array([len(r) for r in rows], np.int64)
     lib.fm_pack_right(ptrs, lens.ctypes.data, len(rows), out.ctypes.data, ld, ncols, threads)
     return out
+
+
+def joined_labels(labels_json: list[str]) -> tuple[bytes, np.ndarray]:
+    return _joined(labels_json)
 
 
 def _joined(strs) -> tuple[bytes, np.ndarray]:
@@ -310,6 +324,7 @@ def synth_many(level, ad, aw, sph, cph, kh, t, swd, cwd, sww, cww, inner, c2: in
             f64(cww), u32(inner)]
     mg = None if mag is None else f64(mag)
     out = np.empty((K, nt), np.float32)
+    threads = max(1, min(int(threads), (K * nt) // 65536))    # small grids (a server answer): no thread spawn
     lib.fm_synth_many(K, nt, *[a.ctypes.data for a in arrs], int(c2) & 0xFFFFFFFF, float(noise),
                       None if mg is None else mg.ctypes.data, float(fault_after), out.ctypes.data, int(threads))
     return out
@@ -357,3 +372,87 @@ def ring_write(ring: np.ndarray, top_old: int, top_new: int, r: np.ndarray, t: n
     lib.fm_ring_write(ring.ctypes.data, ring.shape[0], ring.shape[1], int(top_old), int(top_new), r.ctypes.data,
                       t.ctypes.data, v.ctypes.data, len(r), float(step))
     return True
+
+
+class HttpClient:
+    """Keep-alive HTTP/1.1 client of one ``host:port`` (csrc/runtime/httpfetch.cpp):
+    :meth:`batch` sends many pre-rendered requests over ``conns`` connections
+    and parses every 200 answer as a keyed query_range matrix on the thread
+    that received it.  ``None`` from :meth:`create` when the library lacks it
+    or the host does not resolve."""
+
+    def __init__(self, handle, lib):
+        self._h = handle
+        self._lib = lib
+
+    @classmethod
+    def create(cls, host: str, port: int, timeout_s: float = 90.0) -> "HttpClient | None":
+        lib = _load()
+        if lib is None or not hasattr(lib, "fm_http_client_new"):
+            return None
+        if not getattr(lib, "_http_typed", False):
+            lib.fm_http_client_new.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+            lib.fm_http_client_new.restype = c_vp
+            lib.fm_http_client_free.argtypes = [c_vp]
+            lib.fm_http_client_free.restype = None
+            lib.fm_http_batch.argtypes = [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_vp, c_i64, c_i64, ctypes.c_int]
+            lib.fm_http_batch.restype = c_vp
+            lib.fm_http_batch_info.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]
+            lib.fm_http_batch_info.restype = None
+            lib.fm_http_batch_error.argtypes = [c_vp, c_i64, ctypes.c_char_p, c_i64]
+            lib.fm_http_batch_error.restype = c_i64
+            lib.fm_http_batch_fill.argtypes = [c_vp, c_vp, c_vp, c_vp, c_vp]
+            lib.fm_http_batch_fill.restype = None
+            lib.fm_http_batch_free.argtypes = [c_vp]
+            lib.fm_http_batch_free.restype = None
+            lib._http_typed = True
+        h = lib.fm_http_client_new(host.encode(), int(port), int(timeout_s * 1000))
+        return cls(h, lib) if h else None
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.fm_http_client_free(self._h)
+            self._h = None
+
+    def batch(self, host: str, path: str, queries: list[str], tails: list[str], keys: list[str], conns: int,
+              post_over: int = 4096):
+        """Request i: ``path?query=<queries[i] encoded><tails[i]>`` (a form
+        POST past ``post_over`` bytes), answer split by label ``keys[i]``.
+        -> (answers, timing [n, 4], bytes [n]): answer i is a :class:`Keyed`
+        or ``(status, error text)``; timing = (wait, receive, parse, server)
+        seconds (server -1 when the server does not report it)."""
+        n = len(queries)
+        parts = [x for q, t, k in zip(queries, tails, keys) for x in (path, q, t, k)]
+        buf, soff = _joined(parts)
+        lib = self._lib
+        bh = lib.fm_http_batch(self._h, host.encode(), buf, soff.ctypes.data, n, int(post_over), int(conns))
+        try:
+            status = np.empty(n, np.int64)
+            ns = np.empty(n, np.int64)
+            npts = np.empty(n, np.int64)
+            nbytes = np.empty(n, np.int64)
+            timing = np.empty((n, 4), np.float64)
+            lib.fm_http_batch_info(bh, status.ctypes.data, ns.ctypes.data, npts.ctypes.data, nbytes.ctypes.data,
+                                   timing.ctypes.data)
+            S, P = int(ns.sum()), int(npts.sum())
+            t = np.empty(P, np.float64)
+            v = np.empty(P, np.float32)
+            off = np.empty(S + 1, np.int64)
+            kh = np.empty(S, np.uint64)
+            lib.fm_http_batch_fill(bh, t.ctypes.data, v.ctypes.data, off.ctypes.data, kh.ctypes.data)
+            out = []
+            s0 = 0
+            for i, (st, k) in enumerate(zip(status.tolist(), ns.tolist())):
+                if st != 200:
+                    ln = lib.fm_http_batch_error(bh, i, None, 0)
+                    buf = ctypes.create_string_buffer(max(1, ln))
+                    lib.fm_http_batch_error(bh, i, buf, ln)
+                    out.append((st, buf.raw[:ln].decode("utf-8", "replace")))
+                    continue
+                o = off[s0:s0 + k + 1]
+                p0 = int(o[0])
+                out.append(Keyed(kh[s0:s0 + k], o - p0, t[p0:int(o[-1])], v[p0:int(o[-1])]))
+                s0 += k
+            return out, timing, nbytes
+        finally:
+            lib.fm_http_batch_free(bh)

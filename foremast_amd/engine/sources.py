@@ -28,6 +28,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ..api.urls import END_PLACEHOLDER, START_PLACEHOLDER
+from . import promql
 
 
 @dataclass
@@ -141,59 +142,138 @@ class PrometheusSource:
     live = True
 
     def __init__(self, client=None, timeout: float = 90.0, batch: int = 256, workers: int = 8,
-                 post_over: int = 4096):
+                 post_over: int = 4096, native: bool = True):
         import httpx
         self.http = client or httpx.Client(timeout=timeout, limits=httpx.Limits(max_connections=workers,
                                                                                  max_keepalive_connections=workers))
+        self.timeout = timeout
         self.batch = batch
         self.workers = workers
         self.post_over = post_over
+        # batched requests through the native keep-alive client
+        # (csrc/runtime/httpfetch.cpp) unless a client was injected (tests) or
+        # native=False; an https store always takes the Python client
+        self.native = native and client is None
+        self._native: dict[str, object] = {}
         self._tpl: dict[str, object] = {}
+        self._plans: dict[int, tuple] = {}
         self._pool = None
         self.requests = 0
         self.bytes = 0
+        # summed over requests (concurrent requests overlap: these are busy
+        # times, the fetch span is the wall clock): the server's own time
+        # (X-Fm-Server-Us, when it reports one), wait for the first byte,
+        # receive, parse; request_s = the whole request; split_s = joining the
+        # answers back to the templates (fetch_columns)
+        self.stats = {"requests": 0, "bytes": 0, "server_s": 0.0, "wait_s": 0.0, "recv_s": 0.0, "parse_s": 0.0,
+                      "request_s": 0.0, "split_s": 0.0}
+
+    def _count(self, n: int, nbytes: int, **times) -> None:
+        st = self.stats
+        st["requests"] += n
+        st["bytes"] += nbytes
+        for k, v in times.items():
+            st[k] += v
 
     def fetch(self, url: str) -> list[Series]:
+        t0 = time.perf_counter()
         r = self.http.get(url)
         self.requests += 1
         if r.status_code != 200:
             raise SourceError(f"GET {url} -> {r.status_code}")
         self.bytes += len(r.content)
-        return parse_prometheus(r.content)
+        t1 = time.perf_counter()
+        out = parse_prometheus(r.content)
+        self._count(1, len(r.content), request_s=time.perf_counter() - t0, parse_s=time.perf_counter() - t1)
+        return out
 
     def _request(self, base: str, params: dict) -> bytes:
         q = params.get("query", "")
+        t0 = time.perf_counter()
         if len(q) > self.post_over:
             r = self.http.post(base, data=params)
         else:
             r = self.http.get(base, params=params)
         if r.status_code != 200:
             raise SourceError(f"query_range {q[:120]!r}... -> {r.status_code}: {r.text[:200]}")
+        srv = r.headers.get("x-fm-server-us")
+        self._count(0, 0, request_s=time.perf_counter() - t0, server_s=float(srv) * 1e-6 if srv else 0.0)
         return r.content
+
+    def _client_of(self, base: str):
+        """(native client, host header, path) of a plain-http base URL, else None."""
+        got = self._native.get(base)
+        if got is None:
+            from . import native_rt
+            u = urllib.parse.urlsplit(base)
+            cl = None
+            if self.native and u.scheme == "http" and u.hostname:
+                cl = native_rt.HttpClient.create(u.hostname, u.port or 80, self.timeout)
+            got = self._native[base] = (cl, u.netloc, u.path or "/") if cl is not None else False
+        return got or None
 
     def fetch_keyed(self, queries: list, pool=None) -> list:
         """Answers (native_rt.Keyed, split by the query's key label) or the
         exception per request, in order."""
         from . import native_rt
+        out: list = [None] * len(queries)
+        self.requests += len(queries)
+        by_base: dict[str, list[int]] = {}
+        slow = []
+        for i, q in enumerate(queries):
+            if self.native and self._client_of(q.group[0]) is not None:
+                by_base.setdefault(q.group[0], []).append(i)
+            else:
+                slow.append(i)
+        for base, idx in by_base.items():
+            cl, host, path = self._client_of(base)
+            t0 = time.perf_counter()
+            qs = [queries[i] for i in idx]
+            tails = ["&" + urllib.parse.urlencode([("start", _fmt_t(q.start)), ("end", _fmt_t(q.end)),
+                                                   ("step", _fmt_t(q.group[4])), *q.group[5]]) for q in qs]
+            got, timing, nbytes = cl.batch(host, path, [q.query for q in qs], tails, [q.group[3] for q in qs],
+                                           self.workers, self.post_over)
+            srv = timing[:, 3]
+            self._count(0, int(nbytes.sum()), request_s=float(timing[:, :3].sum()), wait_s=float(timing[:, 0].sum()),
+                        recv_s=float(timing[:, 1].sum()), parse_s=float(timing[:, 2].sum()),
+                        server_s=float(srv[srv > 0].sum()))
+            self.stats["requests"] += len(idx)
+            self.bytes += int(nbytes.sum())
+            for i, q, g in zip(idx, qs, got):
+                if isinstance(g, native_rt.Keyed):
+                    out[i] = g
+                else:
+                    st, msg = g
+                    out[i] = SourceError(f"query_range {q.query[:120]!r}... -> {st}: {msg[:200]}")
+            _ = t0
+        if not slow:
+            return out
 
         def one(q):
             try:
                 body = self._request(q.group[0], q.url_params)
                 self.bytes += len(body)
-                return native_rt.parse_keyed(body, q.group[3])
+                t1 = time.perf_counter()
+                got = native_rt.parse_keyed(body, q.group[3])
+                self._count(1, len(body), parse_s=time.perf_counter() - t1)
+                return got
             except (SourceError, OSError, ValueError) as e:
                 return e
             except Exception as e:  # noqa: BLE001 - httpx transport errors are not OSError
                 return SourceError(f"{type(e).__name__}: {e}")
-        self.requests += len(queries)
-        if len(queries) <= 1:
-            return [one(q) for q in queries]
-        if pool is None:
-            if self._pool is None:
-                from concurrent.futures import ThreadPoolExecutor
-                self._pool = ThreadPoolExecutor(self.workers, thread_name_prefix="prom")
-            pool = self._pool
-        return list(pool.map(one, queries))
+        sq = [queries[i] for i in slow]
+        if len(sq) <= 1:
+            got = [one(q) for q in sq]
+        else:
+            if pool is None:
+                if self._pool is None:
+                    from concurrent.futures import ThreadPoolExecutor
+                    self._pool = ThreadPoolExecutor(self.workers, thread_name_prefix="prom")
+                pool = self._pool
+            got = list(pool.map(one, sq))
+        for i, g in zip(slow, got):
+            out[i] = g
+        return out
 
     def _parse_template(self, tpl: str):
         got = self._tpl.get(tpl)
@@ -204,35 +284,166 @@ class PrometheusSource:
                 else False
         return got
 
+    def _columns_plan(self, templates: list[str]):
+        """Request plan of a template list (memoised per list object: the
+        brain's TemplateLists live while the job set is unchanged; a subset of
+        a planned root list -- fleet churn -- indexes the root's plan):
+        (per template: group id, app hash; slow template indices; per group
+        its app-chunk requests)."""
+        from .ingest import KeyedQuery
+        ent = self._plans.get(id(templates))
+        if ent is not None and ent[0] is templates:
+            return ent[1]
+        root = getattr(templates, "root", None)
+        rent = self._plans.get(id(root)) if root is not None else None
+        if rent is not None and rent[0] is root and len(templates) >= 0.9 * len(root):
+            rp = rent[1]
+            ix = np.asarray(templates.ix, np.int64)
+            plan = (rp[0][ix], rp[1][ix], np.flatnonzero(rp[0][ix] < 0), rp[3])
+        else:
+            n = len(templates)
+            gid = np.full(n, -1, np.int64)
+            apps = np.empty(n, object)
+            gmap: dict = {}
+            for i, tpl in enumerate(templates):
+                info = self._parse_template(tpl)
+                if info:
+                    g = gmap.get(info[0])
+                    if g is None:
+                        g = gmap[info[0]] = len(gmap)
+                    gid[i] = g
+                    apps[i] = info[1]
+            ok = gid >= 0
+            from . import native_rt
+            hs = np.zeros(n, np.uint64)
+            if ok.any():
+                hs[ok] = native_rt.fnv1a(apps[ok].tolist())
+            chunks = []
+            for grp, g in gmap.items():
+                uniq = sorted(set(apps[gid == g].tolist()))
+                for k in range(0, len(uniq), self.batch):
+                    part = uniq[k:k + self.batch]
+                    alt = "|".join(promql.re_literal(a) for a in part) if len(part) > 1 else None
+                    chunks.append((g, KeyedQuery(grp, part, 0.0, 0.0, alt=alt)))
+            plan = (gid, hs, np.flatnonzero(~ok), chunks)
+        if len(self._plans) >= 32:
+            self._plans.pop(next(iter(self._plans)))
+        self._plans[id(templates)] = (templates, plan)
+        return plan
+
     def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
-        from .ingest import KeyedQuery, keyed_split
-        out: list = [None] * len(templates)
-        groups: dict[tuple, list[int]] = {}
-        for i, tpl in enumerate(templates):
-            info = self._parse_template(tpl)
-            if not info:
-                try:
-                    out[i] = self.fetch(substitute_window(tpl, start, end))
-                except (SourceError, OSError, ValueError) as e:
-                    out[i] = e
-                continue
-            groups.setdefault(info[0], []).append(i)
-        reqs = []
-        for grp, idx in groups.items():
-            for k in range(0, len(idx), self.batch):
-                chunk = idx[k:k + self.batch]
-                apps = sorted({self._tpl[templates[i]][1] for i in chunk})
-                reqs.append((KeyedQuery(grp, apps, float(int(start)), float(int(end))), chunk))
-        got = self.fetch_keyed([q for q, _ in reqs])
-        for (q, chunk), g in zip(reqs, got):
+        """App-level windows of many ``START_TIME``/``END_TIME`` templates over
+        one window: batched ``app=~`` requests (planned once per template
+        list), answers joined back to the templates by the app label's hash
+        in array passes -- no per-series objects.  An app answered by several
+        series (extra labels) gets their per-timestamp mean of finite values,
+        as the per-job path (merge_series)."""
+        import dataclasses
+        from .ingest import _ranges
+        gid, th, slow, chunks = self._columns_plan(templates)
+        n = len(templates)
+        reqs = [dataclasses.replace(q, start=float(int(start)), end=float(int(end))) for _, q in chunks]
+        got = self.fetch_keyed(reqs) if reqs else []
+        t0 = time.perf_counter()
+        err: list = [None] * n
+        ks, offs, ts, vs, bad, sg = [], [], [], [], [], []
+        p0 = 0
+        for (cg, _), q, g in zip(chunks, reqs, got):
             if isinstance(g, BaseException):
-                for i in chunk:
-                    out[i] = g
+                bad.append((cg, q, g))
                 continue
-            per = dict(zip(q.values, keyed_split(g, q.values)))
-            for i in chunk:
-                out[i] = [Series({}, t, v) for t, v in per.get(self._tpl[templates[i]][1], [])]
-        return Columns.from_series(out)
+            ks.append(g.key)
+            offs.append(g.off[:-1] + p0)
+            sg.append(np.full(len(g.key), cg, np.int64))
+            ts.append(g.t)
+            vs.append(g.v)
+            p0 += len(g.t)
+        key = np.concatenate(ks) if ks else np.zeros(0, np.uint64)
+        sgid = np.concatenate(sg) if sg else np.zeros(0, np.int64)
+        soff = np.concatenate(offs) if offs else np.zeros(0, np.int64)
+        t_all = np.concatenate(ts) if ts else np.zeros(0)
+        v_all = np.concatenate(vs) if vs else np.zeros(0, np.float32)
+        slen = np.diff(np.append(soff, p0)) if len(soff) else np.zeros(0, np.int64)
+        # join (group, app hash): series sorted by group then hash, each
+        # template searched inside its group's run
+        order = np.lexsort((key, sgid))
+        sk, sgs = key[order], sgid[order]
+        ok = gid >= 0
+        a = np.zeros(n, np.int64)
+        b = np.zeros(n, np.int64)
+        for g in np.unique(gid[ok]).tolist():
+            lo_g, hi_g = np.searchsorted(sgs, g, "left"), np.searchsorted(sgs, g, "right")
+            sel = np.flatnonzero(gid == g)
+            a[sel] = lo_g + np.searchsorted(sk[lo_g:hi_g], th[sel], "left")
+            b[sel] = lo_g + np.searchsorted(sk[lo_g:hi_g], th[sel], "right")
+        cnt = np.where(ok, b - a, 0)
+        # one series per app (the usual answer): a gather; several: merged below
+        one = cnt == 1
+        src = np.full(n, -1, np.int64)
+        src[one] = order[a[one]]
+        lens = np.zeros(n, np.int64)
+        lens[one] = slen[src[one]]
+        starts = np.zeros(n, np.int64)
+        starts[one] = soff[src[one]]
+        extra_t, extra_v = [], []
+        if (cnt > 1).any():
+            p1 = p0
+            for i in np.flatnonzero(cnt > 1).tolist():
+                ss = [Series({}, t_all[soff[j]:soff[j] + slen[j]], v_all[soff[j]:soff[j] + slen[j]])
+                      for j in order[a[i]:b[i]].tolist()]
+                mt, mv = merge_series(ss)
+                starts[i] = p1
+                lens[i] = len(mt)
+                p1 += len(mt)
+                extra_t.append(mt)
+                extra_v.append(mv)
+            t_all = np.concatenate([t_all, *extra_t])
+            v_all = np.concatenate([v_all, *extra_v])
+        if bad:                                  # a failed request: its apps' templates carry the error
+            for cg, q, e in bad:
+                hs = native_rt_fnv(q.key_values())
+                for i in np.flatnonzero((gid == cg) & np.isin(th, hs)).tolist():
+                    err[i] = f"{type(e).__name__}: {e}"
+        idx = _ranges(starts, lens)
+        off = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        self.stats["split_s"] += time.perf_counter() - t0
+        if len(slow):
+            # templates outside the batched shape: per-template requests, spliced in
+            parts = []
+            for i in slow.tolist():
+                try:
+                    parts.append(merge_series(self.fetch(substitute_window(templates[i], start, end))))
+                except (SourceError, OSError, ValueError) as e:
+                    err[i] = f"{type(e).__name__}: {e}"
+                    parts.append((np.zeros(0), np.zeros(0, np.float32)))
+            cols_t = [t_all[idx]]
+            cols_v = [v_all[idx]]
+            lens2 = lens.copy()
+            for i, (pt, pv) in zip(slow.tolist(), parts):
+                lens2[i] = len(pt)
+            off = np.zeros(n + 1, np.int64)
+            np.cumsum(lens2, out=off[1:])
+            out_t = np.empty(int(off[-1]), np.float64)
+            out_v = np.empty(int(off[-1]), np.float32)
+            fast_rows = np.flatnonzero(lens2 == lens)
+            pos = _ranges(off[:-1][fast_rows], lens[fast_rows])
+            out_t[pos] = cols_t[0]
+            out_v[pos] = cols_v[0]
+            for i, (pt, pv) in zip(slow.tolist(), parts):
+                out_t[off[i]:off[i + 1]] = pt
+                out_v[off[i]:off[i + 1]] = pv
+            return Columns(off, out_t, out_v, err)
+        return Columns(off, t_all[idx].astype(np.float64, copy=False), v_all[idx].astype(np.float32, copy=False), err)
+
+
+def native_rt_fnv(values) -> np.ndarray:
+    from . import native_rt
+    return native_rt.fnv1a(list(values))
+
+
+def _fmt_t(x: float) -> str:
+    return str(int(x)) if float(x).is_integer() else repr(float(x))
 
 
 class WavefrontSource:
@@ -300,13 +511,13 @@ class SyntheticSource:
         K, nt = len(keys), len(t)
         if K == 0 or nt == 0:
             return np.zeros((K, nt), np.float32)
+        got = self.many_prepared(self.prepare(keys, noise_keys, fault_keys), t, stream)
+        if got is not None:                      # every call (a sample reads the same from any window)
+            return got
         level, ad, aw, ph = (a[:, None] for a in self._params_of(keys))
         tt = np.asarray(t, np.float64)
         wd, ww = 2 * np.pi * tt / 86400.0, 2 * np.pi * tt / 604800.0
         sph, cph = np.sin(ph), np.cos(ph)
-        got = self._many_native(level, ad, aw, sph, cph, noise_keys, fault_keys, tt, wd, ww, stream)
-        if got is not None:                      # every call (a sample reads the same from any window)
-            return got
         season = 1 + ad * (np.sin(wd)[None, :] * cph + np.cos(wd)[None, :] * sph) \
             + aw * (np.sin(ww)[None, :] * cph + np.cos(ww)[None, :] * sph)
         # hash3(key, t, stream) = hash(key * P1 ^ hash(t * P2 ^ hash(stream + P3))):
@@ -346,20 +557,39 @@ class SyntheticSource:
                     mag[i] *= m
         return mag if (mag != 1).any() else None
 
-    def _many_native(self, level, ad, aw, sph, cph, noise_keys, fault_keys, tt, wd, ww, stream: int):
-        """The [keys x times] pass of :meth:`many` in C++ (csrc/runtime/synth.cpp),
-        same terms and expression order; None without the native library."""
+    def prepare(self, keys: list[str], noise_keys: list[str], fault_keys: list[str]) -> dict | None:
+        """The key-dependent terms of :meth:`many` (signal parameters, noise
+        key hash, fault magnitude), computed once: the fake Prometheus keeps
+        them per query (a brain repeats its unions every cycle) and
+        :meth:`many_prepared` then costs only the [keys x times] pass.  None
+        without the native library."""
+        from . import native_rt
+        if not native_rt.available():
+            return None
+        level, ad, aw, ph = self._params_of(keys)
+        kh = np.array([zlib.crc32(k.encode()) ^ self.seed for k in noise_keys], np.uint32)
+        return {"level": level, "ad": ad, "aw": aw, "sph": np.sin(ph), "cph": np.cos(ph), "kh": kh,
+                "mag": self._fault_mag(fault_keys), "K": len(keys)}
+
+    def many_prepared(self, prep: dict | None, t: np.ndarray, stream: int = 0) -> np.ndarray | None:
+        """:meth:`many` from :meth:`prepare`'s terms (csrc/runtime/synth.cpp,
+        same terms and expression order); None without the native library."""
+        if prep is None:
+            return None
         from ..ops.reference import hash_u32
         from . import native_rt
+        tt = np.asarray(t, np.float64)
+        if prep["K"] == 0 or len(tt) == 0:
+            return np.zeros((prep["K"], len(tt)), np.float32)
         U = np.uint32
-        kh = np.array([zlib.crc32(k.encode()) ^ self.seed for k in noise_keys], np.uint32)
+        wd, ww = 2 * np.pi * tt / 86400.0, 2 * np.pi * tt / 604800.0
         ti = ((tt / self.step).astype(np.int64) & 0xFFFFFFFF).astype(np.uint32)
         hs = hash_u32(np.uint32((stream + 0x165667B1) & 0xFFFFFFFF))[0]
         inner = hash_u32((ti * U(0x85EBCA77)) ^ hs)
         c2 = hash_u32(np.uint32((0x68E31DA4 * 0x85EBCA77) & 0xFFFFFFFF) ^ hs)[0]
-        return native_rt.synth_many(level.ravel(), ad.ravel(), aw.ravel(), sph.ravel(), cph.ravel(), kh, tt,
+        return native_rt.synth_many(prep["level"], prep["ad"], prep["aw"], prep["sph"], prep["cph"], prep["kh"], tt,
                                     np.sin(wd), np.cos(wd), np.sin(ww), np.cos(ww), inner, int(c2), self.noise,
-                                    self._fault_mag(fault_keys), self.fault_after)
+                                    prep["mag"], self.fault_after)
 
     def series(self, key: str, start: float, end: float, stream: int = 0, noise_key: str | None = None,
                fault_key: str | None = None) -> Series:

@@ -289,7 +289,7 @@ def test_native_synthetic_generator_matches_numpy():
     keys = [f'm{{pod="pod{i}"}}' for i in range(300)]
     t = s.grid(1.7e9, 1.7e9 + 60 * 200)
     a = s.many(keys, keys, keys, t, 3)
-    s._many_native = lambda *x, **k: None
+    s.many_prepared = lambda *x, **k: None
     b = s.many(keys, keys, keys, t, 3)
     np.testing.assert_allclose(a, b, rtol=2e-6, atol=0)
     assert (a[1, t >= s.fault_after] > 0).all()
