@@ -406,6 +406,14 @@ class Brain:
                 if fast:
                     self.fast.fetch_all(fast, now, ex)
                 works = [f.result() for f in gf]
+            if fast:
+                # jobs the window table could not hold (two series of one pod):
+                # scored per job from now on, starting this cycle
+                ev = self.fast.take_evicted()
+                if ev:
+                    gone = {id(fw) for fw in ev}
+                    fast = [fw for fw in fast if id(fw) not in gone]
+                    works += [self._fetch_job(fw.doc, now) for fw in ev]
         updates: list = []
         bulk: list = []          # uniform (ids, fields) updates of the fast path
         hpalogs: list = []

@@ -459,10 +459,13 @@ class FastPath:
         self._wt_changed = False
         self._hist_epoch = 0       # bumped whenever static history rows were written
         self._specs: dict = {}     # url -> RangeSpec | None of the claim being prepared
+        self.evicted: set = set()  # job ids moved to the general path (take_evicted)
         self._algos: dict = {}     # alias tuple -> canonical algorithms
 
     # ------------------------------------------------------------------ planning
     def _make_plan(self, doc: Document, fp: tuple) -> JobPlan | None:
+        if doc.id in self.evicted:                  # see take_evicted
+            return None
         cfg = self.b.cfg
         pc = _parse_config_cached
         cur = pc(doc.current_config)
@@ -2079,6 +2082,41 @@ class FastPath:
             if self.works.get(w.doc.id) is w:
                 del self.works[w.doc.id]
                 self._gcount_add(w.plan.group, -1)
+
+    def take_evicted(self) -> list[FastWork]:
+        """Jobs a window-table answer could not hold: two series of one key
+        value in one window (a pod selector that also matches series with
+        extra labels; the table has one slot per key value).  They leave the
+        fast path for good -- their windows are released and their ids go to
+        the general per-job path, which concatenates every series of a
+        window (engine/ingest.py WindowTable.dup).  The brain re-fetches them
+        per job in the same cycle."""
+        wt = self.wt
+        if not wt.n or not wt.dup[:wt.n].any():
+            return []
+        out = []
+        for fw in list(self.works.values()):
+            if fw.wcur is None:
+                continue
+            ids = np.concatenate([fw.wcur, fw.wbase])
+            ids = ids[ids >= 0]
+            if len(ids) and wt.dup[ids].any():
+                out.append(fw)
+        wt.dup[:wt.n] = 0
+        keys = [k for w in out if not w.plan.sliding for k in w.plan.keys]
+        if keys:
+            self.static.release(keys)
+        for fw in out:
+            self.evicted.add(fw.doc.id)
+            wt.release(np.concatenate([fw.wcur, fw.wbase]))
+            if self.works.get(fw.doc.id) is fw:
+                del self.works[fw.doc.id]
+                self._gcount_add(fw.plan.group, -1)
+        if out:
+            log.warning("%d job(s) moved to the per-job path: a window answer carried two series of one %s",
+                        len(out), "key value")
+            self._last = None
+        return out
 
     def fail_job(self, fw: FastWork, err: str, updates: list, outcome: dict) -> None:
         st = ST.COMPLETED_UNKNOWN

@@ -1177,7 +1177,7 @@ class ElasticsearchStore(JobStore):
         return [], False
 
     def _claim_query(self, max_stuck_s: float, now: float, shard, live=None, dead=None,
-                     adopt: str | None = None) -> tuple[dict, bool]:
+                     adopt: str | None = None, worker: str | None = None) -> tuple[dict, bool]:
         stuck_before = _stamp(now - max_stuck_s)
         ip = sorted(ST.IN_PROGRESS)
         should = [{"terms": {"status.keyword": sorted(ST.CLAIMABLE)}}]
@@ -1192,8 +1192,12 @@ class ElasticsearchStore(JobStore):
         # held by a worker without a lease document: the job's own modified_at is the lease
         legacy = {"bool": {"filter": [{"terms": {"status.keyword": ip}},
                                       {"range": {"modified_at": {"lt": stuck_before}}}]}}
-        if live:
-            legacy["bool"]["must_not"] = [{"terms": {"processingContent.keyword": sorted(live)}}]
+        # never this worker's own jobs: it holds them (sticky sessions do not
+        # rewrite a held job, so its modified_at ages past the stuck age), and
+        # matching them would fill the scan page with jobs it already has
+        excl = set(live or ()) | ({worker} if worker else set())
+        if excl:
+            legacy["bool"]["must_not"] = [{"terms": {"processingContent.keyword": sorted(excl)}}]
         should.append(legacy)
         q = {"bool": {"should": should, "minimum_should_match": 1}}
         filt, py_shard = self._shard_filter_q(shard)
@@ -1210,7 +1214,8 @@ class ElasticsearchStore(JobStore):
         """(document, seq_no, primary_term) of every job claimed."""
         live, dead = self._leases(now, max_stuck_s)
         live = [w for w in live if w != worker]
-        q, py_shard = self._claim_query(max_stuck_s, now, shard, live, dead, adopt=worker if adopt else None)
+        q, py_shard = self._claim_query(max_stuck_s, now, shard, live, dead, adopt=worker if adopt else None,
+                                        worker=worker)
         scan_limit = None if (owner is not None or py_shard) else limit
         hits = self._scan(q, scan_limit, {"seq_no_primary_term": True})
         if beat:

@@ -261,3 +261,23 @@ def test_es_restarted_worker_adopts_its_held_jobs():
     st2 = ElasticsearchStore("http://es:9200", client=st.http)        # a new process
     assert st2.claim_batch("other", 10, 90.0, now=1_760_000_005.0).ids == []
     assert sorted(st2.claim_batch("w", 10, 90.0, now=1_760_000_005.0).ids) == [f"j{i}" for i in range(5)]
+
+
+def test_es_worker_keeps_claiming_new_jobs_after_its_held_jobs_age():
+    """a sticky worker never rewrites a held job, so its own
+    jobs age past MAX_STUCK_IN_SECONDS.  They must not match the 'held without
+    a lease' clause for their own worker: otherwise the oldest-first scan page
+    (room = limit - held) fills with them, the Python filter drops them, and a
+    newly submitted job is never claimed."""
+    es, st = _store()
+    st.PAGE = 4
+    t0 = 1_760_000_000.0
+    for i in range(6):
+        st.put(Document(id=f"j{i}", app_name=f"a{i}", status=ST.INITIAL, modified_at="2025-01-01T00:00:00Z"))
+    assert len(st.claim_batch("W", 8, 90.0, now=t0).ids) == 6          # room afterwards: 2 < 6 held
+    for k in range(1, 30):                                              # 290 s of cycles: held jobs age
+        b = st.claim_batch("W", 8, 90.0, now=t0 + 10 * k)
+        st.keep("W", b.ids, now=t0 + 10 * k)
+    st.put(Document(id="new", app_name="fresh", status=ST.INITIAL, modified_at="2025-10-10T00:00:00Z"))
+    b = st.claim_batch("W", 8, 90.0, now=t0 + 300)
+    assert "new" in b.ids and len(b.ids) == 7

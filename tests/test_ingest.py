@@ -28,7 +28,10 @@ class SimClock:
         return self.t
 
 
-def _fake(clock, faults=None):
+def _fake(clock, faults=None, dup_pod=None):
+    """PrometheusSource over the fake Prometheus (in-process).  ``dup_pod``:
+    that pod's series is answered twice, the copy with an extra label and
+    other values (a selector that also matches a sidecar's series)."""
     from foremast_amd.demo.promserver import FakePrometheus
     fp = FakePrometheus(SyntheticSource(faults=faults or {}, fault_after=T0 - 3600), clock)
     calls = []
@@ -39,6 +42,16 @@ def _fake(clock, faults=None):
             q.update(urllib.parse.parse_qsl(req.content.decode(), keep_blank_values=True))
         calls.append(q)
         code, body = fp.answer(q)
+        if dup_pod is not None and code == 200:
+            d = json.loads(body)
+            res = []
+            for r in d["data"]["result"]:
+                res.append(r)
+                if r["metric"].get("pod") == dup_pod:
+                    res.append({"metric": dict(r["metric"], container="sidecar"),
+                                "values": [[t, str(1.5 * float(v))] for t, v in r["values"]]})
+            d["data"]["result"] = res
+            body = json.dumps(d).encode()
         return httpx.Response(code, content=body, headers={"Content-Type": "application/json"})
     return PrometheusSource(client=httpx.Client(transport=httpx.MockTransport(handler))), calls
 
@@ -154,7 +167,8 @@ def test_incremental_windows_fetch_each_step_once():
     assert wt.fetch(src, clock.now() + 3600) == 0                      # complete windows are never asked again
 
 
-def test_http_fast_path_judges_like_general_path_over_live_cycles():
+@pytest.mark.parametrize("dup", [False, True])
+def test_http_fast_path_judges_like_general_path_over_live_cycles(dup):
     """The brain on a live (clock-bounded) HTTP Prometheus: the fast path's
     batched incremental windows and the general path's per-job fetches give
     the same verdicts and gauges cycle after cycle, with far fewer requests."""
@@ -170,7 +184,7 @@ def test_http_fast_path_judges_like_general_path_over_live_cycles():
     rigs = []
     for resident in (True, False):
         clock = SimClock(T0)
-        src, calls = _fake(clock, faults)
+        src, calls = _fake(clock, faults, dup_pod="c3-7687b9f4d7-p0001" if dup else None)
         store = MemoryStore()
         client = AnalystClient.for_app(create_app(store), clock=clock)
         cfg = BrainConfig()
@@ -211,6 +225,9 @@ def test_http_fast_path_judges_like_general_path_over_live_cycles():
             assert (np.isnan(va) and np.isnan(vb)) or va == pytest.approx(vb, rel=1e-6, abs=1e-9), (cyc, k)
     from foremast_amd.api import status as ST
     assert ST.COMPLETED_UNHEALTH in seen and ST.COMPLETED_HEALTH in seen
+    # two series of one pod: that job left the window table for the per-job
+    # path (which concatenates them), the verdicts above stayed equal
+    assert ba.fast.evicted == ({ids[3]} if dup else set())
     # batched + incremental: a small fraction of per-job fetching's requests
     assert ba.fast.wt.requests > 0 and 8 * tot_a <= tot_b, (tot_a, tot_b)
 
