@@ -101,6 +101,11 @@ class GaugeTable:
         self._sline = np.zeros(0, np.int64)      # slot -> (family << 32 | line)
         self.events: list = []                   # (slot, key | None) since the last drain (C2 publication)
         self.dropped = 0
+        # key -> live owners that keep its slot number cached (fast-path jobs,
+        # rank 0's map of another rank's slots): such a slot is never freed,
+        # however long its owners stay quiet -- a cached writer must not land
+        # in a free or re-keyed slot (see bind_keys)
+        self.krefs: dict = {}
 
     def __len__(self) -> int:
         return len(self.index)
@@ -226,6 +231,24 @@ class GaugeTable:
             self._nret += int(new.sum())
             return int(new.sum())
 
+    def bind_keys(self, keys) -> None:
+        """An owner that caches these keys' slots (and writes through them
+        later, without a lookup) is live: the sweep keeps their slots."""
+        kr = self.krefs
+        with self.lock:
+            for k in keys:
+                kr[k] = kr.get(k, 0) + 1
+
+    def unbind_keys(self, keys) -> None:
+        kr = self.krefs
+        with self.lock:
+            for k in keys:
+                c = kr.get(k, 0) - 1
+                if c > 0:
+                    kr[k] = c
+                else:
+                    kr.pop(k, None)
+
     def retire_keys(self, keys, now: float, ttl: float) -> int:
         idx = self.index
         sl = [s for s in (idx.get(k) for k in keys) if s is not None]
@@ -241,6 +264,14 @@ class GaugeTable:
             dead = np.flatnonzero(ex <= now)
             later = ex[(ex > now) & (ex < np.inf)]
             self._next_exp = float(later.min()) if len(later) else np.inf
+            if len(dead) and self.krefs:
+                # retired by one owner, still bound by another: live again
+                kr = self.krefs
+                bound = np.fromiter((self.keys[s] in kr for s in dead.tolist()), bool, len(dead))
+                if bound.any():
+                    self.expire[dead[bound]] = np.inf
+                    self._nret -= int(bound.sum())
+                    dead = dead[~bound]
             if not len(dead):
                 return 0
             fams = set()
@@ -495,13 +526,28 @@ class BrainExporter:
                  (self.IMPACT, namespace, app, cluster) if cluster else (self.IMPACT, namespace, app)]
         return keys
 
-    def retire_jobs(self, jobs, now: float, ttl: float | None = None) -> int:
+    def bind_jobs(self, jobs) -> None:
+        """Jobs that keep their series' slots cached (the fast path): their
+        keys are not freed while they live, whoever else retires them.
+        ``jobs``: (base metrics, namespace, app, cluster)."""
+        keys = [k for bms, ns, app, cl in jobs for k in self.job_keys(bms, ns, app, cl)]
+        if keys:
+            self.table.bind_keys(keys)
+
+    def retire_jobs(self, jobs, now: float, ttl: float | None = None, unbind: bool = False,
+                    retire: bool = True) -> int:
         """Jobs that closed / expired / left this rank's shard: their series
         stay ``ttl`` seconds (the final verdict stays visible), then leave
-        ``/metrics``.  ``jobs``: (base metrics, namespace, app, cluster)."""
+        ``/metrics`` -- unless another live owner still binds them.
+        ``jobs``: (base metrics, namespace, app, cluster); ``unbind``: the jobs
+        were bound (:meth:`bind_jobs`)."""
         ttl = self.series_ttl if ttl is None else ttl
         keys = [k for bms, ns, app, cl in jobs for k in self.job_keys(bms, ns, app, cl)]
-        return self.table.retire_keys(keys, now, ttl) if keys else 0
+        if not keys:
+            return 0
+        if unbind:
+            self.table.unbind_keys(keys)
+        return self.table.retire_keys(keys, now, ttl) if retire else 0
 
     def sweep(self, now: float) -> int:
         return self.table.sweep(now)
@@ -646,8 +692,14 @@ class BrainExporter:
                 if stale is not None and self._klog.get(r, 0) > 0:
                     keep = set(self._remote.get(r, np.zeros(0, np.int64)).tolist())
                     gone = [s_ for s_ in stale.tolist() if s_ not in keep]
+                    # the old epoch's map lets go of every slot it bound (the new
+                    # epoch's snapshot re-bound the live ones); the series it
+                    # alone exported retire at once
+                    t = self.table
+                    t.unbind_keys([t.keys[s_] for s_ in stale.tolist()
+                                   if 0 <= s_ < len(t.keys) and t.keys[s_] is not None])
                     if gone:
-                        self.table.retire(gone, self.clock(), 0.0)
+                        t.retire(gone, self.clock(), 0.0)
                     mb.put(f"gka{r}", struct.pack("<q", self._kep.get(r, 0)))
                 elif stale is not None:
                     self._stale[r] = stale
@@ -685,10 +737,20 @@ class BrainExporter:
             m = np.concatenate([m, np.full(top - len(m), -1, np.int64)])
         touched = np.fromiter(final.keys(), np.int64, len(final))
         prev = m[touched]
-        if (prev >= 0).any():
-            self.table.retire(prev[prev >= 0], self.clock(), 0.0)
-        m[touched] = -1
         new = [(sl, tuple(k)) for sl, k in final.items() if k is not None]
+        if new:                                  # bound before the old mapping lets go (a re-keyed same key)
+            self.table.bind_keys([k for _, k in new])
+        if (prev >= 0).any():
+            self._unmap(prev[prev >= 0].tolist())
+        m[touched] = -1
         if new:
             m[[sl for sl, _ in new]] = self.table.slots([k for _, k in new])
         self._remote[r] = m
+
+    def _unmap(self, slots: list) -> None:
+        """Rank 0: local slots another rank no longer maps onto -- its binding
+        goes, and the series retires at once unless a live owner binds it."""
+        t = self.table
+        keys = [t.keys[s_] for s_ in slots if 0 <= s_ < len(t.keys) and t.keys[s_] is not None]
+        t.unbind_keys(keys)
+        t.retire(slots, self.clock(), 0.0)

@@ -602,13 +602,13 @@ class FastPath:
                 unknown.append(k)
         rest = []
         reg: list[FastWork] = []
+        new_fw: list[FastWork] = []
         if unknown:
             docs = batch.docs(unknown)
             self._prefill_specs(docs)
             for k, d in zip(unknown, docs):
-                old = works.pop(d.id, None)
-                if old is not None:              # resubmitted under the same id
-                    self._gcount_add(old.plan.group, -1)
+                old = works.get(d.id)
+                if old is not None:              # resubmitted under the same id (dropped, unbound)
                     self._release([old])
                 p = self._make_plan(d, batch.versions[k])
                 if p is None:
@@ -622,6 +622,7 @@ class FastPath:
                     end_ts = now
                 fw = works[d.id] = FastWork(d, p, rows, end_ts, version=batch.versions[k],
                                             handle=None if handles is None else int(handles[k]))
+                new_fw.append(fw)
                 if not p.sliding:
                     reg.append(fw)
                 self._gcount_add(p.group, 1)
@@ -629,6 +630,10 @@ class FastPath:
                 todo.append(fw)
         if reg:
             self._register_windows(reg)
+        if new_fw and self.b.exporter is not None:
+            # fast-path jobs cache their series' slots: bound while they live
+            self.b.exporter.bind_jobs([(fw.plan.base_metrics, fw.plan.namespace, fw.doc.app_name, fw.plan.cluster)
+                                       for fw in new_fw])
         self._specs = {}
         if len(todo) == len(fast):
             todo = fast
@@ -2077,7 +2082,11 @@ class FastPath:
         exp = self.b.exporter
         if exp is not None and works:
             exp.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name, w.plan.cluster)
-                             for w in works], self.b.clock())
+                             for w in works if self.works.get(w.doc.id) is w], self.b.clock(), unbind=True)
+            rest = [w for w in works if self.works.get(w.doc.id) is not w]
+            if rest:                                  # no longer (or never) bound: retire only
+                exp.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name, w.plan.cluster)
+                                 for w in rest], self.b.clock())
         for w in works:
             if self.works.get(w.doc.id) is w:
                 del self.works[w.doc.id]
@@ -2106,12 +2115,16 @@ class FastPath:
         keys = [k for w in out if not w.plan.sliding for k in w.plan.keys]
         if keys:
             self.static.release(keys)
+        exp = self.b.exporter
         for fw in out:
             self.evicted.add(fw.doc.id)
             wt.release(np.concatenate([fw.wcur, fw.wbase]))
             if self.works.get(fw.doc.id) is fw:
                 del self.works[fw.doc.id]
                 self._gcount_add(fw.plan.group, -1)
+                if exp is not None:                   # the per-job path looks its series up every write
+                    exp.retire_jobs([(fw.plan.base_metrics, fw.plan.namespace, fw.doc.app_name, fw.plan.cluster)],
+                                    self.b.clock(), unbind=True, retire=False)
         if out:
             log.warning("%d job(s) moved to the per-job path: a window answer carried two series of one %s",
                         len(out), "key value")
@@ -2140,7 +2153,7 @@ class FastPath:
                     self.wt.release(np.concatenate([w.wcur, w.wbase]))
             if gone_w and self.b.exporter is not None:         # jobs that stopped coming (shard moved)
                 self.b.exporter.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name,
-                                              w.plan.cluster) for w in gone_w], self.b.clock())
+                                              w.plan.cluster) for w in gone_w], self.b.clock(), unbind=True)
 
 
 def _history_rows(fp: "FastPath"):

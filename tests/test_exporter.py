@@ -199,3 +199,28 @@ def test_sweep_waits_for_each_retirement_in_turn():
     assert b'app="b"' in e.render()
     e.sweep(t + 161)
     assert b'app="b"' not in e.render()
+
+
+def test_bound_series_outlive_another_owners_retirement():
+    """a job closing retires keys that another live job of
+    the same app still exports through cached slots.  While that job is bound
+    the slot is never freed -- it stays quiet past the TTL, then writes, and
+    the value lands in its own series; once it unbinds, the series retires
+    and leaves after the TTL."""
+    from foremast_amd.engine.exporter import BrainExporter
+    exp = BrainExporter()
+    exp.series_ttl = 10.0
+    job = (["namespace_app_pod_cpu"], "ns", "app1", "")
+    hpa_slots = exp.hpa_slots(["ns"], ["app1"]).reshape(-1)          # the HPA job's cached slots
+    exp.bind_jobs([job])
+    exp.set_hpa_scores(hpa_slots, np.array([60.0]))
+    exp.retire_jobs([job], now=100.0)                                # a canary of the same app closed
+    assert exp.sweep(200.0) == 0                                     # quiet past the TTL: kept
+    other = exp.table.slots([("foremastbrain:other", "ns", "x")])    # a new key must not reuse the slot
+    assert not set(other.tolist()) & set(hpa_slots.tolist())
+    exp.set_hpa_scores(hpa_slots, np.array([70.0]))
+    assert exp.table.get((exp.HPA_SCORE, "ns", "app1")) == 70.0
+    assert b'app="app1"' in exp.render()
+    exp.retire_jobs([job], now=300.0, unbind=True)                   # the HPA job closes
+    assert exp.sweep(305.0) == 0 and exp.sweep(311.0) >= 2
+    assert exp.table.get((exp.HPA_SCORE, "ns", "app1")) is None and not exp.table.krefs
