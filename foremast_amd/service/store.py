@@ -584,6 +584,17 @@ class SQLiteStore(JobStore):
             c.execute("create table if not exists hpalog_batches (bid integer primary key, ts real not null, "
                       "created text not null, aliases text not null, reasons text not null, n integer not null, "
                       "rids blob not null, score blob not null, reason blob not null, vals blob not null)")
+            # per job the batches that may hold its entries: a read scans only
+            # [first_bid, last_bid], a job without HPA entries none
+            c.execute("create table if not exists hpalog_jobs (rid integer primary key, first_bid integer not null, "
+                      "last_bid integer not null)")
+            if (c.execute("select 1 from hpalog_batches limit 1").fetchone() is not None
+                    and c.execute("select 1 from hpalog_jobs limit 1").fetchone() is None):
+                rng: dict = {}                    # a store written before the index: built once
+                for bid, rids in c.execute("select bid, rids from hpalog_batches order by bid"):
+                    for r_ in np.frombuffer(rids, np.int64).tolist():
+                        rng[r_] = (rng.get(r_, (bid,))[0], bid)
+                c.executemany("insert into hpalog_jobs values (?,?,?)", [(r_, a, b) for r_, (a, b) in rng.items()])
             c.execute("create index if not exists hpalogs_job on hpalogs(job_id, ts)")
             # no ts index: rows arrive in time order, so retention deletes a
             # rowid prefix (one B-tree less to update per log: 10k logs per cycle)
@@ -946,6 +957,10 @@ class SQLiteStore(JobStore):
                           (b.timestamp, b.created_at or "", json.dumps(b.aliases), json.dumps(b.reasons), len(sel),
                            rid[sel].astype(np.int64).tobytes(), np.asarray(b.score, np.int32)[sel].tobytes(),
                            np.asarray(b.reason, np.int32)[sel].tobytes(), np.ascontiguousarray(vals).tobytes()))
+                bid = c.execute("select last_insert_rowid()").fetchone()[0]
+                c.execute("insert into hpalog_jobs (rid, first_bid, last_bid) select value, ?1, ?1 from json_each(?2) "
+                          "where true on conflict(rid) do update set last_bid = excluded.last_bid",
+                          (bid, json.dumps(rid[sel].tolist())))
                 self._log_writes += len(sel)
                 newest = max(newest, b.timestamp)
             if rows:
@@ -963,6 +978,8 @@ class SQLiteStore(JobStore):
                 if first is not None:
                     c.execute("delete from hpalogs where rowid < ?", (first[0],))
                 c.execute("delete from hpalog_batches where ts < ?", (cut,))
+                c.execute("delete from hpalog_jobs where last_bid < coalesce((select min(bid) from hpalog_batches), "
+                          "1 << 62)")
                 self._last_prune = newest
 
     @staticmethod
@@ -998,13 +1015,16 @@ class SQLiteStore(JobStore):
         rows = c.execute("select ts, body from hpalogs where job_id=? order by ts desc limit ?",
                          (job_id, size)).fetchall()
         out = [(ts, HPALog.from_dict(json.loads(b))) for ts, b in rows]
-        r = c.execute("select rid from documents where id=?", (job_id,)).fetchone()
+        r = c.execute("select d.rid, j.first_bid, j.last_bid from documents d join hpalog_jobs j on j.rid = d.rid "
+                      "where d.id=?", (job_id,)).fetchone()
         if r is not None and size > 0:
-            rid = r[0]
+            rid, b0, b1 = r
             found = 0
-            # newest batches first; an entry per cycle means the last `size`
-            # batches answer it, a sparse log policy scans further back
-            for (bid,) in c.execute("select bid from hpalog_batches order by bid desc").fetchall():
+            # newest batches first, only inside the job's own batch range (a job
+            # with no batch entries -- every canary -- has no range: no scan);
+            # an entry per cycle means the last `size` batches answer it
+            for (bid,) in c.execute("select bid from hpalog_batches where bid between ? and ? order by bid desc",
+                                    (b0, b1)).fetchall():
                 b = self._batch(c, bid)
                 if b is None:
                     continue

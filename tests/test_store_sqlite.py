@@ -220,3 +220,29 @@ def test_restarted_worker_adopts_its_held_jobs(tmp_path):
     assert len(SQLiteStore(path).claim_batch("other", 100, 90.0, now=T0 + 5)) == 0
     st2 = SQLiteStore(path)                           # a new process, same worker id
     assert len(st2.claim_batch("w", 100, 90.0, now=T0 + 5)) == 20
+
+
+def test_hpalog_reads_scan_only_the_jobs_batches(tmp_path):
+    """a job without batch entries (a canary polled through
+    GET /v1/healthcheck/id) reads no batch at all; an HPA job reads only the
+    batches of its own range, newest first."""
+    import numpy as np
+    from foremast_amd.api.models import HPALogBatch
+    st = SQLiteStore(str(tmp_path / "j.db"))
+    st.put_many([Document(id=f"h{i}", app_name=f"a{i}", status=ST.INITIAL) for i in range(3)]
+                + [Document(id="canary", app_name="c", status=ST.INITIAL)])
+    for cyc in range(40):
+        ids = ["h0", "h1"] if cyc < 30 else ["h2"]
+        n = len(ids)
+        st.add_hpalogs([HPALogBatch(ids, 1000.0 + 60 * cyc, "", np.full(n, 50 + cyc), np.zeros(n, np.int32),
+                                    ["hpa is holding"], ["cpu"], np.ones((n, 1)), np.ones((n, 1)) * 2,
+                                    np.zeros((n, 1)))])
+    reads = []
+    orig = st._batch
+    st._batch = lambda c, bid: reads.append(bid) or orig(c, bid)
+    assert st.hpalogs("canary", 10) == [] and reads == []
+    got = st.hpalogs("h2", 4)
+    assert [lg.log.hpa_score for lg in got] == [89, 88, 87, 86] and len(reads) == 4
+    reads.clear()
+    got = st.hpalogs("h0", 3)
+    assert [lg.log.hpa_score for lg in got] == [79, 78, 77] and max(reads) <= 30
