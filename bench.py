@@ -245,7 +245,6 @@ def main() -> None:
 
     pub_graphs: list = []
     peer = None
-    step_no = [0]
     if args.publish in ("auto", "peer") and world > 1:
         from foremast_amd.parallel.peer import PeerPublisher, selftest
         try:
@@ -253,6 +252,7 @@ def main() -> None:
             rep: dict = {}
             if not selftest(peer, report=rep):
                 raise RuntimeError(f"peer publish self-test failed {rep}")
+            peer.reset()                         # the ring restarts at step 0 on every rank
             args.publish = "peer"
         except Exception as e:  # noqa: BLE001 - the eager all-gather is the fallback
             if peer is not None:
@@ -268,6 +268,13 @@ def main() -> None:
     def publish_body(slot: int) -> None:
         if split:
             decides[slot]()
+        if peer is not None:
+            # the step number is a device word (parallel/peer.py captured form):
+            # this whole body is one graph launch per slot
+            peer.publish_dev(slot, packed[slot])
+            if info.is_main:
+                peer.collect_dev(slot, hosts[slot], S)
+            return
         g = gather(packed[slot], gathered)
         if info.is_main:
             LIB.call("fm_copy_d2h_async", hosts[slot].data_ptr(), g.data_ptr(), S * 4 * 4, stream_of(g))
@@ -278,17 +285,7 @@ def main() -> None:
         the slot's captured graph: one launch instead of three host calls)."""
         comm.wait_event(ev_tick[slot])
         with torch.cuda.stream(comm):
-            if peer is not None:
-                if split:
-                    decides[slot]()
-                # the publisher's ring follows its own step counter (the bench
-                # slot only picks this step's packed / host buffers)
-                k = step_no[0]
-                step_no[0] += 1
-                peer.publish(k % depth, k, packed[slot])
-                if info.is_main:
-                    peer.collect(k % depth, k, hosts[slot], S)
-            elif pub_graphs:
+            if pub_graphs:
                 pub_graphs[slot].replay()
             else:
                 publish_body(slot)
@@ -303,6 +300,8 @@ def main() -> None:
             slot = k % depth
             if k >= depth:                       # retire step k - depth
                 ev1[slot].synchronize()
+                if peer is not None and not peer.step_ok(slot):
+                    raise RuntimeError(f"peer publish: a wait of step {k - depth} timed out on rank {info.rank}")
             if k < n:
                 ticks[slot]()
                 ev_tick[slot].record(compute)
@@ -312,7 +311,7 @@ def main() -> None:
         args.publish = "graph" if world == 1 else "eager"
     tw = time.perf_counter()
     run(args.warmup)
-    if args.publish == "graph":
+    if args.publish in ("graph", "peer"):
         graphs = []
         for slot in range(depth):
             gr = torch.cuda.CUDAGraph()
@@ -329,7 +328,7 @@ def main() -> None:
     # so it is re-measured rather than trusted); the elapsed time is
     # MAX-reduced after every chunk so every rank runs the same steps
     w_ms = D.all_reduce_max((time.perf_counter() - tw) * 1e3, dev)
-    per = w_ms / max(1, args.warmup + (args.warmup if args.publish == "graph" else 0))
+    per = w_ms / max(1, args.warmup + (args.warmup if args.publish in ("graph", "peer") else 0))
     extra = 0
     while w_ms < args.warmup_min_ms and extra < 100000:
         k = extra_warmup_steps(w_ms, per, args.warmup_min_ms)

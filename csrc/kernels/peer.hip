@@ -84,6 +84,80 @@ __global__ void peer_ack_kernel(unsigned* const* dst, int n, unsigned value) {
   if (r < n && dst[r] != nullptr) store_release_sys(dst[r], value);
 }
 
+// ---------------------------------------------------------------- device step counter
+// The captured-graph form (one graph launch per slot, no host argument that
+// changes per step): every rank keeps its step number k in a device word
+// `ctr`; the kernels of a step read it, and the step's last kernel stores
+// k + 1.  `slot` is fixed per graph (the ring slot k % depth of the steps it
+// serves); `slot_status[slot]` records whether this step's wait timed out, so
+// the rest of the step skips its writes (no overwrite of a slot rank 0 did
+// not consume, no ack of a partial fleet) and the host reads it per retired
+// step.
+
+// Wait until every lane's word (base + r * stride, r < n) reached k + 1 - lag
+// (lag = depth for the slot-reuse ack wait: nothing to wait for while
+// k < lag).  status[0] |= 1 and slot_status[slot] = 1 on timeout, else
+// slot_status[slot] = 0.
+__global__ void __launch_bounds__(64) peer_wait_ctr_kernel(const unsigned* base, int n, int64_t stride,
+                                                           const unsigned* ctr, unsigned lag, long long budget,
+                                                           unsigned* status, unsigned* slot_status, int slot) {
+  const unsigned k = *ctr;
+  const int r = threadIdx.x;
+  bool done = r >= n || k < lag;
+  const unsigned value = k + 1u - lag;
+  const long long t0 = clock64();
+  bool timed_out = false;
+  while (true) {
+    if (!done) done = (int)(load_acquire_sys(base + (int64_t)r * stride) - value) >= 0;
+    if (__all(done)) break;
+    if (clock64() - t0 > budget) {
+      timed_out = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  const bool bad = __any(timed_out && !done);
+  if (r == 0) {
+    slot_status[slot] = bad ? 1u : 0u;
+    if (bad) __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Publish step k = *ctr: src rows -> dst, then flag = k + 1 (skipped when
+// this slot's ack wait timed out).  bump: the last block stores *ctr = k + 1.
+__global__ void __launch_bounds__(256) peer_publish_ctr_kernel(const float4* __restrict__ src, float4* dst, int64_t n4,
+                                                               unsigned* flag, unsigned* ctr, unsigned* arrive,
+                                                               const unsigned* slot_status, int slot, int bump) {
+  const unsigned k = *ctr;
+  const bool skip = slot_status != nullptr && slot_status[slot] != 0u;
+  if (!skip)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+      dst[i] = src[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1 == gridDim.x) {
+      __threadfence_system();
+      if (!skip) store_release_sys(flag, k + 1u);
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (bump) __hip_atomic_store(ctr, k + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Rank 0: ack step k = *ctr of the slot to every rank (skipped when the
+// collect wait timed out: the fleet copy is partial), then *ctr = k + 1.
+__global__ void peer_ack_ctr_kernel(unsigned* const* dst, int n, unsigned* ctr, const unsigned* slot_status,
+                                    int slot) {
+  const unsigned k = *ctr;
+  const int r = threadIdx.x;
+  __threadfence_system();
+  if (r < n && dst[r] != nullptr && slot_status[slot] == 0u) store_release_sys(dst[r], k + 1u);
+  __syncthreads();
+  if (r == 0) __hip_atomic_store(ctr, k + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- IPC handles
@@ -138,6 +212,38 @@ FM_API int fm_peer_wait(const unsigned* flags, int n, int64_t stride, unsigned v
 FM_API int fm_peer_ack(unsigned* const* dst, int n, unsigned value, hipStream_t stream) {
   if (n < 0 || n > 64) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(peer_ack_kernel, dim3(1), dim3(64), 0, stream, dst, n, value);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------- device-counter forms (graph-capturable)
+FM_API int fm_peer_wait_ctr(const unsigned* base, int n, int64_t stride, const unsigned* ctr, unsigned lag,
+                            long long budget_cycles, unsigned* status, unsigned* slot_status, int slot,
+                            hipStream_t stream) {
+  if (n < 0 || n > 64 || slot < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_wait_ctr_kernel, dim3(1), dim3(64), 0, stream, base, n, stride, ctr, lag, budget_cycles,
+                     status, slot_status, slot);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+FM_API int fm_peer_publish_ctr(const void* src, void* dst, int64_t bytes, unsigned* flag, unsigned* ctr,
+                               unsigned* arrive, const unsigned* slot_status, int slot, int bump, hipStream_t stream) {
+  if (bytes < 0 || bytes % 16 != 0 || ((uintptr_t)src | (uintptr_t)dst) % 16 != 0 || slot < 0)
+    return (int)hipErrorInvalidValue;
+  const int64_t n4 = bytes / 16;
+  int blocks = (int)((n4 + 256 * 8 - 1) / (256 * 8));
+  blocks = blocks < 1 ? 1 : (blocks > 64 ? 64 : blocks);
+  hipLaunchKernelGGL(peer_publish_ctr_kernel, dim3(blocks), dim3(256), 0, stream, (const float4*)src, (float4*)dst,
+                     n4, flag, ctr, arrive, slot_status, slot, bump);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+FM_API int fm_peer_ack_ctr(unsigned* const* dst, int n, unsigned* ctr, const unsigned* slot_status, int slot,
+                           hipStream_t stream) {
+  if (n < 0 || n > 64 || slot < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_ack_ctr_kernel, dim3(1), dim3(64), 0, stream, dst, n, ctr, slot_status, slot);
   FM_LAUNCH_CHECK();
   return 0;
 }

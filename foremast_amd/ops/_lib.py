@@ -53,6 +53,10 @@ _SIGS: dict[str, list] = {
     "fm_peer_publish": [c_void_p, c_void_p, c_i64, c_void_p, ctypes.c_uint, c_void_p, c_void_p],
     "fm_peer_wait": [c_void_p, c_int, c_i64, ctypes.c_uint, ctypes.c_longlong, c_void_p, c_void_p],
     "fm_peer_ack": [c_void_p, c_int, ctypes.c_uint, c_void_p],
+    "fm_peer_wait_ctr": [c_void_p, c_int, c_i64, c_void_p, ctypes.c_uint, ctypes.c_longlong, c_void_p, c_void_p, c_int,
+                         c_void_p],
+    "fm_peer_publish_ctr": [c_void_p, c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
+    "fm_peer_ack_ctr": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "fm_es_update": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fm_band_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p, c_i64, c_int, c_void_p, c_void_p,

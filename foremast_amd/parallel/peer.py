@@ -22,6 +22,17 @@ Every wait is a bounded GPU-side poll (a status word records a timeout), so
 a dead peer never leaves a kernel spinning; :meth:`check` raises if any wait
 timed out.  ``selftest`` validates the path on the actual node against the
 process group's all-gather before a bench trusts it.
+
+**Captured form** (:meth:`publish_dev` / :meth:`collect_dev`): the step
+number lives in a device word ``ctr`` that the step's kernels read and its
+last kernel advances, so nothing in a step depends on a host argument and
+the whole per-slot sequence (decision, ack wait, publish, rank 0's wait,
+host copy, ack) is ONE captured HIP graph launch.  A timed-out wait marks its
+slot in ``slot_status``; the rest of that step skips its writes (no overwrite
+of an unconsumed slot, no ack of a partial fleet) and the host reads the
+marker per retired step (:meth:`step_ok`).  :meth:`reset` zeroes flags, acks
+and counters on every rank after the eager self-test, so the ring restarts
+at step 0 in step with the caller's slots.
 """
 from __future__ import annotations
 
@@ -73,6 +84,10 @@ class PeerPublisher:
         self._opened: list[int] = []
         self.status = torch.zeros(4, dtype=torch.int32, device=self.dev)
         self.arrive = torch.zeros(depth, dtype=torch.int32, device=self.dev)
+        # captured form: device step counter, per-slot wait status and its host copy
+        self.ctr = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.slot_status = torch.zeros(depth, dtype=torch.int32, device=self.dev)
+        self.host_status = torch.zeros(depth, dtype=torch.int32, pin_memory=True)
         # fleet rows and arrival flags share ONE exported buffer (one handle,
         # one mapping per importer): [fleet | pad to 256 B | flags]
         fbytes = depth * world * shard * 16
@@ -130,6 +145,60 @@ class PeerPublisher:
         if self.world > 1:
             LIB.call("fm_peer_ack", self.ack_ptrs[slot].data_ptr(), self.world - 1, ctypes.c_uint(step + 1), s)
         return view
+
+    # ------------------------------------------------------------------ captured form
+    def reset(self) -> None:
+        """Every rank: back to step 0 (flags, acks, counters, status words
+        zeroed between two barriers) -- after the eager self-test."""
+        torch.cuda.synchronize(self.dev)
+        dist.barrier()
+        if self.rank == 0:
+            self.flags.zero_()
+        else:
+            self.ack.zero_()
+        self.ctr.zero_()
+        self.slot_status.zero_()
+        self.arrive.zero_()
+        self.status.zero_()
+        self.host_status.zero_()
+        torch.cuda.synchronize(self.dev)
+        dist.barrier()
+
+    def publish_dev(self, slot: int, packed: torch.Tensor) -> None:
+        """Current stream (capturable): this rank's shard of step k = ctr into
+        slot ``slot`` of rank 0's fleet buffer; ranks > 0 first wait for rank
+        0's ack of the slot's previous use and advance ctr themselves."""
+        assert packed.shape == (self.shard, 4) and packed.dtype == torch.float32 and packed.is_contiguous()
+        s = stream_of(packed)
+        ss = self.slot_status.data_ptr()
+        if self.rank != 0:
+            LIB.call("fm_peer_wait_ctr", self.ack.data_ptr() + 4 * slot, 1, 1, self.ctr.data_ptr(),
+                     ctypes.c_uint(self.depth), ctypes.c_longlong(_BUDGET), self.status.data_ptr() + 4, ss, slot, s)
+        dst = self.fleet_ptr + 16 * (slot * self.world * self.shard + self.rank * self.shard)
+        flag = self.flags_ptr + 4 * (slot * self.world + self.rank)
+        LIB.call("fm_peer_publish_ctr", packed.data_ptr(), dst, 16 * self.shard, flag, self.ctr.data_ptr(),
+                 self.arrive.data_ptr() + 4 * slot, ss if self.rank != 0 else None, slot, int(self.rank != 0), s)
+        if self.rank != 0:
+            LIB.call("fm_copy_d2h_async", self.host_status.data_ptr() + 4 * slot, ss + 4 * slot, 4, s)
+
+    def collect_dev(self, slot: int, host: torch.Tensor, n_rows: int) -> None:
+        """Rank 0, current stream (capturable): wait for every rank's step
+        k = ctr in slot ``slot``, copy the first ``n_rows`` fleet rows and the
+        slot's wait status to host memory, ack the slot (unless the wait
+        timed out) and advance ctr."""
+        s = stream_of(self.status)
+        ss = self.slot_status.data_ptr()
+        LIB.call("fm_peer_wait_ctr", self.flags.data_ptr() + 4 * slot * self.world, self.world, 1,
+                 self.ctr.data_ptr(), ctypes.c_uint(0), ctypes.c_longlong(_BUDGET), self.status.data_ptr(), ss, slot, s)
+        LIB.call("fm_copy_d2h_async", host.data_ptr(), self.fleet[slot].data_ptr(), n_rows * 16, s)
+        LIB.call("fm_copy_d2h_async", self.host_status.data_ptr() + 4 * slot, ss + 4 * slot, 4, s)
+        LIB.call("fm_peer_ack_ctr", self.ack_ptrs[slot].data_ptr() if self.world > 1 else None, self.world - 1,
+                 self.ctr.data_ptr(), ss, slot, s)
+
+    def step_ok(self, slot: int) -> bool:
+        """The retired step of ``slot`` (its stream work observed) had no
+        timed-out wait on this rank: its verdict rows are whole."""
+        return int(self.host_status[slot]) == 0
 
     def check(self) -> None:
         st = self.status.cpu()

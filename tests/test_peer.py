@@ -45,9 +45,31 @@ def _worker(rank, world, port, q):
         torch.cuda.synchronize(dev)
         last = host.clone() if rank == 0 else None
         pub.check()
+        # captured form: the step number is a device word, one
+        # graph per slot holds publish (+ rank 0's wait, host copy and ack);
+        # the ring restarts at 0 after reset() on both ranks
+        pub.reset()
+        hosts = [torch.empty((world * 1250, 4), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        graphs = []
+        for slot in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                pub.publish_dev(slot, x)
+                if rank == 0:
+                    pub.collect_dev(slot, hosts[slot], world * 1250)
+            graphs.append(g)
+        bad = 0
+        for k in range(200):
+            x.fill_(rank * 1000.0 + 0.25 * k)
+            graphs[k % 2].replay()
+        torch.cuda.synchronize(dev)
+        bad = sum(not pub.step_ok(sl) for sl in range(2))
+        ctr = int(pub.ctr.item())
+        pub.check()
+        cap = None if rank != 0 else (float(hosts[1][0, 0]), float(hosts[1][-1, 0]))
         dist.barrier()
         pub.close()
-        res = (ok, None if last is None else (float(last[0, 0]), float(last[-1, 0])))
+        res = (ok, None if last is None else (float(last[0, 0]), float(last[-1, 0])), ctr, bad, cap)
         q.put((rank, res))
     except Exception as e:  # noqa: BLE001 - reported to the parent
         import traceback
@@ -77,3 +99,7 @@ def test_peer_publish_two_processes_one_gpu():
         assert not (isinstance(v, str) and v.startswith("ERR")), v
     assert out[0][0] and out[1][0]
     assert out[0][1] == (223.0, 1223.0)
+    # captured form: 200 steps on both ranks' device counters, no timed-out
+    # wait, rank 0's last copy of slot 1 (step 199) has both shards
+    assert out[0][2] == out[1][2] == 200 and out[0][3] == out[1][3] == 0
+    assert out[0][4] == (0.25 * 199, 1000.0 + 0.25 * 199)
