@@ -220,7 +220,17 @@ E2E = {
     "2e2e": ("continuous", "holt_winters", 4, 60.0, ["error5xx", "traffic", "latency", "error4xx"]),
     "4e2e": ("hpa", "lstm", 8, 60.0,
              ["cpu", "memory", "latency", "traffic", "error5xx", "error4xx", "tomcat_threads", "jvm_heap"]),
+    "mixed": ("mixed", None, None, 60.0, None),
 }
+# the mixed fleet: the three production strategies side by
+# side, as barrelman runs them (Barrelman.go:233-372 rolling-update canaries,
+# MonitorController.go:94-108 continuous monitors, HpaController.go:204-229 HPA
+# scoring): (strategy, model, single-strategy config, alias suffix, fleet share).
+# A model is chosen per metric type (ml_algorithmN), so each class's metrics
+# are their own metric types.
+E2E_MIXED = [("canary", "moving_average_all", "3e2e", "", 0.4),
+             ("continuous", "holt_winters", "2e2e", "_mon", 0.4),
+             ("hpa", "lstm", "4e2e", "_hpa", 0.2)]
 
 
 def config3e2e(args):
@@ -265,21 +275,33 @@ def config3e2e(args):
     kind = args.config
     strategy, algo, m_default, poll_default, names = E2E[kind]
     S, P = args.services, args.pods
-    M = args.metrics if args.metrics_set else m_default
     poll = args.poll_seconds if poll_default is None or args.poll_set else poll_default
     t = {"now": 1_760_000_000.0}
     clock = lambda: t["now"]
-    mons = [crd.Monitoring(f"http_server_requests_{a}", "gauge", a) for a in (names * 2)[:M]]
-    aliases = [m.metric_alias for m in mons]
+    # job classes: (strategy, model, metric aliases, first job index, job count)
+    if kind == "mixed":
+        classes, j0 = [], 0
+        for k, (st_, al_, ref, sfx, frac) in enumerate(E2E_MIXED):
+            n_ = S - j0 if k == len(E2E_MIXED) - 1 else int(round(frac * S))
+            mm = E2E[ref][2]
+            classes.append((st_, al_, [a + sfx for a in (E2E[ref][4] * 2)[:mm]], j0, n_))
+            j0 += n_
+    else:
+        M0 = args.metrics if args.metrics_set else m_default
+        classes = [(strategy, algo, (names * 2)[:M0], 0, S)]
+    M = max(len(c[2]) for c in classes)
+    sliding_any = any(c[0] != "canary" for c in classes)
+    mons_of = [[crd.Monitoring(f"http_server_requests_{a}", "gauge", a) for a in c[2]] for c in classes]
     http = args.source == "http"
     spread = (60.0 if args.spread_seconds is None else args.spread_seconds) if http else 0.0
     server = poller = prom = cw = None
-    if strategy == "canary":
-        faults = {f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(0, S, 50)}    # 2% of services regress
-        fault_after = t["now"] - 3600
-    else:
-        faults = {f'app="svc{j}"': 3.0 for j in range(0, S, 50)}
-        fault_after = t["now"] + spread + (args.warmup + 2) * poll
+    faults = {}
+    for st_, _, _, a0, n_ in classes:
+        if st_ == "canary":                      # 2% of services regress
+            faults.update({f"svc{j}-7687b9f4d7-p0000": 4.0 for j in range(a0, a0 + n_, 50)})
+        else:
+            faults.update({f'app="svc{j}"': 3.0 for j in range(a0, a0 + n_, 50)})
+    fault_after = t["now"] + spread + (args.warmup + 2) * poll if sliding_any else t["now"] - 3600
     prom_url = "http://prom/api/v1/"
     if http:
         # the fake Prometheus (demo/promserver.py) in its own processes, on the
@@ -300,23 +322,30 @@ def config3e2e(args):
             prom_port = None
         prom_port = D.broadcast_object(prom_port)
         prom_url = f"http://127.0.0.1:{prom_port}/api/v1/"
-    metrics = crd.Metrics("prometheus", prom_url, mons)
+    metrics_of = [crd.Metrics("prometheus", prom_url, ms) for ms in mons_of]
     t_sub = 0.0
     ids: list[str] = []
     # continuous / HPA jobs stay alive for the whole run (their end time is
     # the submission window); canary jobs use the 10-minute watch window
+    # (in the mixed fleet one that outlasts the run: its churn is explicit)
     n_cycles = args.steps + args.warmup + 3
-    window = args.window if strategy == "canary" else max(args.window, int(n_cycles * poll / 60) + 20)
+    long_window = max(args.window, int(n_cycles * poll / 60) + 20)
+
+    def submit_one(client, c, j):
+        st_, _, al_, _, _ = classes[c]
+        pods = ([[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
+                 [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]] if st_ == "canary" else None)
+        w_ = args.window if st_ == "canary" and kind != "mixed" else long_window
+        return client.start_analyzing("default", f"svc{j}", pods, metrics_of[c], w_, st_,
+                                      al_ if st_ == "hpa" else None)
 
     def submit(client):
         t0_sub = t["now"]
-        for j in range(S):
-            if spread:
-                t["now"] = t0_sub + spread * j / S
-            pods = ([[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
-                     [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]] if strategy == "canary" else None)
-            ids.append(client.start_analyzing("default", f"svc{j}", pods, metrics, window, strategy,
-                                              aliases if strategy == "hpa" else None))
+        for c, (_, _, _, a0, n_) in enumerate(classes):
+            for j in range(a0, a0 + n_):
+                if spread:
+                    t["now"] = t0_sub + spread * j / S
+                ids.append(submit_one(client, c, j))
         t["now"] = t0_sub + spread
 
     if args.store == "memory":
@@ -345,7 +374,7 @@ def config3e2e(args):
         store = SQLiteStore(db)
     print(f"[{kind}] rank {info.rank}: {S} jobs submitted in {t_sub:.1f}s ({args.store})", file=sys.stderr,
           flush=True)
-    if strategy == "canary":
+    if not sliding_any:
         staged = StagedSource(SyntheticSource(faults=faults, fault_after=fault_after))
     else:
         # 2% of services regress mid-run; every series is staged column-wise
@@ -361,9 +390,18 @@ def config3e2e(args):
         live = None
         router = SourceRouter(synthetic=staged, force="synthetic")
     cfg = BrainConfig()
-    cfg.ml_algorithm = algo
+    cfg.ml_algorithm = algo or "moving_average_all"
     cfg.hpa_log_interval_s = args.hpa_log_interval
-    if strategy != "canary" and args.band_threshold:
+    if kind == "mixed":
+        # per metric type: its model (and, for the monitored classes, the band
+        # threshold below) -- the ml_algorithmN overrides of foremast-brain.yaml
+        import dataclasses as _dc
+        for st_, al_, als, _, _ in classes:
+            for a in als:
+                r = cfg.rule_for(a)
+                thr = max(r.threshold, args.band_threshold or 0.0) if st_ != "canary" else r.threshold
+                cfg.metric_rules[a] = _dc.replace(r, threshold=thr, algorithm=al_)
+    elif strategy != "canary" and args.band_threshold:
         # a monitored fleet that stays whole: at the 2-sigma default a job with
         # 10 current points of iid noise closes completed_unhealth in ~20 % of
         # cycles, and the timed cycles would score a shrinking fleet; the
@@ -372,7 +410,7 @@ def config3e2e(args):
         thr = args.band_threshold
         cfg.threshold = max(cfg.threshold, thr)
         cfg.metric_rules = {k: _dc.replace(r, threshold=max(r.threshold, thr)) for k, r in cfg.metric_rules.items()}
-    if kind == "4e2e":
+    if kind == "4e2e" or any(c[0] == "hpa" for c in classes):
         cfg.hpa_forecast_algorithm = "lstm"
         cfg.lstm_hidden = args.hidden
         cfg.lstm_layers = args.layers
@@ -382,7 +420,7 @@ def config3e2e(args):
                   batch_size=S + 1, worker_id=f"bench-{info.rank}", exporter=exp, history_days=args.history_days)
     # HTTP canaries: the first cycle runs 90 s after the last submission, so
     # the timed cycles sit inside the watch windows (points arriving)
-    t["now"] += poll + (90.0 if http and strategy == "canary" else 0.0)
+    t["now"] += poll + (90.0 if http and classes[0][0] == "canary" else 0.0)
     if cw is not None:
         cw.set(t["now"])
     t_first = time.perf_counter()
@@ -411,6 +449,15 @@ def config3e2e(args):
         import cProfile
         _prof = cProfile.Profile()
 
+    churn = {"next": S, "new": 0, "resub": 0}
+    churn_client = None
+    if kind == "mixed" and info.is_main:
+        def _do(method, url, body):                # the service's create handler, into the shared store
+            req = ApplicationHealthAnalyzeRequest.from_dict(_json.loads(body))
+            jid, _ = store.create(J.build_document(req))
+            return Response(200, _json.dumps(J.new_response(jid, 0, "new")).encode())
+        churn_client = AnalystClient("http://foremast-service/v1/healthcheck/", _do, clock)
+
     def step():
         # cycles every poll interval inside the jobs' watch window (staged:
         # the synthetic source serves the whole window; http: the fake
@@ -418,6 +465,22 @@ def config3e2e(args):
         t["now"] += poll
         if cw is not None:
             cw.set(t["now"])
+        if churn_client is not None:
+            # mixed fleet churn, every cycle: new rolling-update canaries (0.5 %
+            # of the canary class) and resubmitted HPA jobs (0.5 %: a template
+            # change); the monitored class churns through its mid-run faults
+            for c, (st_, _, _, a0, n_) in enumerate(classes):
+                k = max(1, n_ // 200)
+                if st_ == "canary":
+                    for _ in range(k):
+                        submit_one(churn_client, c, churn["next"])
+                        churn["next"] += 1
+                        churn["new"] += 1
+                elif st_ == "hpa":
+                    base_j = a0 + (len(cyc_ms) * k) % max(1, n_)
+                    for j in range(base_j, min(a0 + n_, base_j + k)):
+                        submit_one(churn_client, c, j)
+                        churn["resub"] += 1
         n0 = (live.requests, live.bytes) if live is not None else (0, 0)
         st0 = dict(live.stats) if live is not None else None
         wt0 = brain.fast.wt.apply_s if brain.fast is not None else 0.0
@@ -528,7 +591,13 @@ def config3e2e(args):
             "4e2e": ("10k HPA jobs with the LSTM forecaster", f"LSTM H={args.hidden} x {args.layers} (bf16 MFMA) "
                      "forecast -> band decision + HPA score + forecast gauge",
                      "synthetic Prometheus-shaped series, staged column-wise; each cycle fetches every row's new "
-                     "sample (60-s poll), random-init LSTM weights; 2% of services regress mid-run")}[kind]
+                     "sample (60-s poll), random-init LSTM weights; 2% of services regress mid-run"),
+            "mixed": (f"a mixed fleet of {', '.join(f'{n_} {st_}' for st_, _, _, _, n_ in classes)} jobs",
+                      "per class: moving_average_all + pairwise ALL (canary) | Holt-Winters bands (continuous) | "
+                      f"LSTM H={args.hidden} x {args.layers} forecast + HPA score (hpa)",
+                      "synthetic Prometheus-shaped series, staged (canary windows per query, sliding templates "
+                      "column-wise); each cycle: 0.5% new canaries, 0.5% HPA resubmissions, 2% of the monitored "
+                      "class regresses mid-run")}[kind]
     if http:
         desc = (desc[0], desc[1], "synthetic Prometheus-shaped series served over HTTP by a fake Prometheus in its own "
                 "processes (query_range evaluated up to the simulated now: batched pod=~ / app=~ unions, incremental "
@@ -540,9 +609,12 @@ def config3e2e(args):
             ("bf16 recurrence / fp32 cell" if kind == "4e2e" else "fp32") if dev.type != "cpu"
             else "fp32 data / fp64 statistics", desc[2],
             {"services": S, "metrics": M, "strategy": strategy, "algorithm": algo, "poll_seconds": poll,
-             "hpa_log_interval_s": args.hpa_log_interval if strategy == "hpa" else None,
-             "band_threshold_min": args.band_threshold if strategy != "canary" else None,
-             "pods_per_side": P if strategy == "canary" else 0, "store": args.store,
+             "classes": [{"strategy": st_, "model": al_, "jobs": n_, "metrics": len(als)}
+                         for st_, al_, als, _, n_ in classes],
+             "churn": dict(new_canaries=churn["new"], hpa_resubmissions=churn["resub"]) if kind == "mixed" else None,
+             "hpa_log_interval_s": args.hpa_log_interval if any(c[0] == "hpa" for c in classes) else None,
+             "band_threshold_min": args.band_threshold if sliding_any else None,
+             "pods_per_side": P if any(c[0] == "canary" for c in classes) else 0, "store": args.store,
              "topology": ("REST service in its own process + every rank on one WAL SQLite file"
                           if args.store == "sqlite" else "single process, in-memory store"),
              "rest_poller": poll_out, "rows_per_cycle_rank0": per_cycle, "warm_restart": restart,
@@ -654,7 +726,7 @@ def config5(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True, choices=["1", "2", "2e2e", "3", "3e2e", "4", "4e2e", "5"])
+    ap.add_argument("--config", required=True, choices=["1", "2", "2e2e", "3", "3e2e", "4", "4e2e", "5", "mixed"])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -706,7 +778,7 @@ def main():
     if args.rest_poll_rps is None:
         args.rest_poll_rps = args.services / 10.0
     {"1": config1, "2": config2, "2e2e": config3e2e, "3": config3, "3e2e": config3e2e, "4": config4,
-     "4e2e": config3e2e, "5": config5}[args.config](args)
+     "4e2e": config3e2e, "5": config5, "mixed": config3e2e}[args.config](args)
 
 
 if __name__ == "__main__":

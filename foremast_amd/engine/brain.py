@@ -537,7 +537,19 @@ class Brain:
     def _score_general(self, works: list[Work], updates: list, outcome: dict) -> list:
         """Score the general-path jobs: one batch, or job by job when the
         batch raises (a job that still fails is closed completed_unknown).
-        Returns [(works, rows, result)] batches to finish."""
+        Returns [(works, rows, result)] batches to finish.
+
+        A batch packs its histories right-aligned to its longest row, and
+        position-dependent models (seasonal phase, the LSTM window) see that
+        alignment: jobs are batched with jobs of the same longest history, so
+        a job's verdict is what it gets scored alone, whatever else the cycle
+        holds (a mixed fleet: 7-day canary histories next to sliding windows)."""
+        if len(works) > 1:
+            by: dict[int, list[Work]] = {}
+            for wk in works:
+                by.setdefault(min(MAX_T, max([len(r.hist) for r in wk.rows] + [2])), []).append(wk)
+            if len(by) > 1:
+                return [b for ws in by.values() for b in self._score_general(ws, updates, outcome)]
         rows: list[Row] = []
         for j, wk in enumerate(works):
             for r in wk.rows:

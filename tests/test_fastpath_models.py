@@ -249,3 +249,43 @@ def test_model_cache_subset_key_lists_match_fresh_lookups():
     fb, _ = run(b, [keys[i] for i in ix1[sel]], ix1[sel], 2)
     torch.testing.assert_close(fa, fb)
     assert a.hits == b.hits and a.misses == b.misses
+
+
+def test_mixed_churning_fleet_fast_path_equals_general_path():
+    """one brain, every strategy side by side -- canary and
+    rolling-update windows (two static groups), continuous monitors of two
+    metric sets (two sliding groups) and HPA jobs -- with churn in each class
+    every cycle: a new canary, an HPA resubmission, a monitored service that
+    regresses mid-run and closes.  Fast path == general path for 10 cycles
+    (the single-group shortcuts of the fast path never hold here)."""
+    faults = dict(FAULTS, cont5=4.0)
+    a = _brain(True, "mixed", faults)
+    b = _brain(False, "mixed", faults)
+
+    def submit(client, cyc):
+        ids = []
+        if cyc == 0:
+            ids += _submit(client, "static") + _submit(client, "continuous") + _submit(client, "hpa")
+            for j in range(4, 7):
+                ids.append(client.start_analyzing("prod", f"cont{j}", None, _metrics(3), 10, "continuous"))
+        app = f"new{cyc}"
+        ids.append(client.start_analyzing("default", app, [_pods(app, 2, "7687b9f4d"), _pods(app, 2, "5db89899b")],
+                                          _metrics(4), 10, "canary"))
+        ids.append(client.start_analyzing("prod", f"hpa{cyc % 3}", None, _metrics(4), 10, "hpa",
+                                          ["cpu", "latency", "error5xx", "memory"]))
+        return ids
+    ids: list = []
+    for cyc in range(10):
+        got = submit(a[2], cyc)
+        assert got == submit(b[2], cyc)
+        ids = list(dict.fromkeys(ids + got))
+        ra, rb = a[3].run_once(), b[3].run_once()
+        assert ra["claimed"] == rb["claimed"]
+        if cyc == 0:
+            assert ra["fast_jobs"] == ra["claimed"]
+            assert len(a[3].fast._gcount) >= 4              # several plan groups: no single-group shortcut
+        _compare(a, b, ids, cyc)
+        a[0].t += 60
+        b[0].t += 60
+    st = {a[1].get(j).status for j in ids}
+    assert ST.COMPLETED_UNHEALTH in st and (ST.PREPROCESS_INPROGRESS in st or ST.PREPROCESS_COMPLETED in st)
