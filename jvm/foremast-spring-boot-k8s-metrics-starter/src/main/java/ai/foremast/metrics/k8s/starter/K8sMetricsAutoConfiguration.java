@@ -167,4 +167,26 @@ public class K8sMetricsAutoConfiguration {
             return reg;
         }
     }
+
+    /** The same for WebFlux services: caller tag and the {@code /metrics} alias. */
+    @Configuration(proxyBeanMethods = false)
+    @ConditionalOnWebApplication(type = ConditionalOnWebApplication.Type.REACTIVE)
+    @ConditionalOnClass(name = "org.springframework.boot.actuate.metrics.web.reactive.server.DefaultWebFluxTagsProvider")
+    static class ReactiveMetrics {
+
+        @Bean
+        @ConditionalOnMissingBean(org.springframework.boot.actuate.metrics.web.reactive.server.WebFluxTagsProvider.class)
+        public CallerFluxTagsProvider foremastCallerFluxTags(K8sMetricsProperties props) {
+            return new CallerFluxTagsProvider(props.getCallerHeader());
+        }
+
+        /** {@code GET /metrics} served by the actuator's Prometheus scrape (path rewrite). */
+        @Bean
+        @ConditionalOnProperty(prefix = "k8s.metrics", name = "metrics-path-alias", matchIfMissing = true)
+        public org.springframework.web.server.WebFilter foremastFluxMetricsAlias() {
+            return (exchange, chain) -> "/metrics".equals(exchange.getRequest().getPath().value())
+                    ? chain.filter(exchange.mutate().request(r -> r.path("/actuator/prometheus")).build())
+                    : chain.filter(exchange);
+        }
+    }
 }

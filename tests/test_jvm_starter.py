@@ -61,3 +61,31 @@ def test_endpoint_keeps_the_reference_get_toggle():
     assert "@ReadOperation" in src and "@WriteOperation" in src
     read = src[src.index("@ReadOperation"):]
     assert "@Selector String action, @Selector String metric" in read.split("}")[0]
+
+
+def test_environment_post_processor_and_reactive_pieces_registered():
+    """the WebFlux caller tags, the reactive actuator access
+    and the Prometheus exposure default ship with the Boot 2 starter."""
+    fac = (ROOT / "src" / "main" / "resources" / "META-INF" / "spring.factories").read_text()
+    classes = re.findall(r"ai\.foremast\.[\w.]+", fac)
+    assert classes and all((SRC / (c.rsplit(".", 1)[1] + ".java")).exists() for c in classes)
+    flux = (SRC / "CallerFluxTagsProvider.java").read_text()
+    mvc = (SRC / "CallerTagsProvider.java").read_text()
+    for src in (flux, mvc):                         # the same caller default as the Python emitter
+        assert '"caller"' in src and '"*"' in src
+    auto = (SRC / "K8sMetricsAutoConfiguration.java").read_text()
+    assert "CallerFluxTagsProvider" in auto and "Type.REACTIVE" in auto
+
+
+def test_servlet_module_emits_the_starter_series():
+    """The Spring 4 / Boot 1.x / plain-servlet module: the same meter name,
+    tag keys and zero-initialised statuses as the Boot 2 starter."""
+    srv = Path(__file__).resolve().parent.parent / "jvm" / "foremast-servlet-k8s-metrics" / "src" / "main" / \
+        "java" / "ai" / "foremast" / "metrics" / "servlet"
+    filt = (srv / "HttpRequestsFilter.java").read_text()
+    fm = (srv / "ForemastMetrics.java").read_text()
+    auto = (SRC / "K8sMetricsAutoConfiguration.java").read_text()
+    for key in ("method", "uri", "status", "outcome", "exception", "caller"):
+        assert f'"{key}"' in filt
+    assert '"http.server.requests"' in fm and '"http.server.requests"' in auto
+    assert '"403,404,500,503"' in fm and "0.95, 0.98" in fm and "0.95, 0.98" in auto
