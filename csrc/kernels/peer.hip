@@ -247,3 +247,15 @@ FM_API int fm_peer_ack_ctr(unsigned* const* dst, int n, unsigned* ctr, const uns
   FM_LAUNCH_CHECK();
   return 0;
 }
+
+// ---------------------------------------------------------------- board copies
+// Synchronous copy between any two addresses this process can name (host
+// memory, its own device memory, a peer's memory opened through IPC): the
+// brain's rank-to-rank board (parallel/board.py) moves gauge vectors and
+// verdict rows with the DMA engines over xGMI, one host-blocking copy each,
+// so a seqlock header written after the payload is only seen once the
+// payload has landed.
+FM_API int fm_memcpy_sync(void* dst, const void* src, int64_t bytes) {
+  if (bytes <= 0) return 0;
+  return (int)hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault);
+}

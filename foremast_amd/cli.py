@@ -78,6 +78,13 @@ def brain_main(argv=None) -> None:  # pragma: no cover - process entry
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     info = D.init_distributed(device=dev)
+    if info.world > 1 and dev.type == "cuda" and os.environ.get("BRAIN_XGMI_BOARD", "1") != "0":
+        # gauge vectors and verdict rows between the ranks over xGMI (HIP IPC
+        # board on rank 0, self-tested); the TCPStore mailbox otherwise
+        from .parallel import board
+        b = board.setup(dev)
+        print(f"rank {info.rank}: rank exchange over "
+              f"{'the xGMI board' if b is not None else 'the TCPStore mailbox'}", file=sys.stderr, flush=True)
     cfg = BrainConfig.from_env()
     exporter = BrainExporter()
     if info.is_main:

@@ -1,0 +1,230 @@
+"""The brain ranks' bulk exchange over xGMI.
+
+Every rank of a node publishes two large, latest-value payloads per cycle:
+its gauge value vector (rank 0 exports the whole node's ``foremastbrain:*``
+series on one ``/metrics`` port, deploy/foremast/3_brain/foremast-brain.yaml:87-122)
+and its service verdict rows (every rank reads every other rank's for
+downstream impact).  Through the TCPStore mailbox (parallel/mailbox.py) each
+of those is a TCP payload through rank 0's store thread.  Here they live in a
+**board**: one device buffer on rank 0, exported through HIP IPC and mapped
+by every rank, with a region per (key, rank):
+
+* ``header`` (seq: u64, n: i64 bytes, ts: f64) + ``capacity`` bytes;
+* a writer bumps ``seq`` to odd, copies the payload, bumps it to even --
+  each a synchronous DMA copy, so the even ``seq`` lands after the payload
+  (the writer's host memory -> rank 0's HBM over xGMI);
+* a reader copies the header, the payload, the header again and accepts
+  only an even, unchanged ``seq`` (a seqlock): a reader never waits for a
+  writer, a torn read is retried next time (the previous value stays),
+  and a rank that stopped publishing leaves its last payload readable.
+
+Only the bulk, latest-value keys use the board; ordered logs (the exporter's
+slot key log), the call graph and anything larger than a region go through
+the TCPStore as before (:class:`HybridMailbox`).  A board is installed per
+process after a self-test (:func:`setup`); without a GPU, HIP IPC or the
+native library everything stays on the mailbox.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+import time
+
+import numpy as np
+
+# bulk keys (mailbox prefix + key) and their per-rank region capacity in bytes
+KEYS = {"fm/gv": 16 << 20, "fm/impact/verdict": 4 << 20}
+HDR = 64
+_HFMT = "<QqdQ"          # seq, payload bytes (-1: on the TCP mailbox), publish time, spare
+
+_board = None
+
+
+def installed():
+    return _board
+
+
+class DeviceBoard:
+    def __init__(self, rank: int, world: int, device, keys: dict | None = None, tag: str = "fm/board"):
+        import torch
+        import torch.distributed as dist
+        from torch.distributed import distributed_c10d as c10d
+        from .peer import _handle, _open
+        self.rank, self.world = rank, world
+        self.keys = dict(KEYS if keys is None else keys)
+        self._off: dict[tuple[str, int], int] = {}
+        off = 0
+        for k, cap in self.keys.items():
+            for r in range(world):
+                self._off[(k, r)] = off
+                off += HDR + (cap + 255) // 256 * 256
+        self.size = off
+        st = c10d._get_default_store()
+        self._opened = []
+        if rank == 0:
+            self._buf = torch.zeros(off, dtype=torch.uint8, device=device)
+            torch.cuda.synchronize(device)
+            st.set(f"{tag}/h", _handle(self._buf))
+            self.base = self._buf.data_ptr()
+        else:
+            b, self.base = _open(st.get(f"{tag}/h"))
+            self._opened.append(b)
+        self._seq: dict[str, int] = {}
+        self._hbuf = ctypes.create_string_buffer(HDR)
+        self.reads = self.torn = 0
+        dist.barrier()
+
+    # ------------------------------------------------------------------ copies
+    @staticmethod
+    def _copy(dst: int, src: int, n: int) -> None:
+        from ..ops._lib import LIB
+        LIB.call("fm_memcpy_sync", dst, src, n)
+
+    def _header(self, addr: int) -> tuple:
+        self._copy(ctypes.addressof(self._hbuf), addr, struct.calcsize(_HFMT))
+        return struct.unpack_from(_HFMT, self._hbuf.raw)
+
+    def _put_header(self, addr: int, seq: int, n: int, ts: float) -> None:
+        hb = ctypes.create_string_buffer(struct.pack(_HFMT, seq, n, ts, 0), HDR)
+        self._copy(addr, ctypes.addressof(hb), struct.calcsize(_HFMT))
+
+    # ------------------------------------------------------------------ API
+    def handles(self, key: str) -> bool:
+        return key in self.keys
+
+    def put(self, key: str, payload) -> bool:
+        """This rank's latest ``key`` (bytes or a contiguous numpy array).
+        False when it does not fit the region: the caller keeps it on the
+        TCP mailbox (the header says so, so readers look there)."""
+        addr = self.base + self._off[(key, self.rank)]
+        seq = self._seq.get(key, 0)
+        if isinstance(payload, np.ndarray):
+            arr = np.ascontiguousarray(payload)
+            n, src = arr.nbytes, arr.ctypes.data
+        else:
+            arr = None
+            n = len(payload)
+            keep = ctypes.create_string_buffer(bytes(payload), max(1, n))
+            src = ctypes.addressof(keep)
+        fits = n <= self.keys[key]
+        self._put_header(addr, seq + 1, -1 if not fits else n, time.time())     # odd: being written
+        if fits and n:
+            self._copy(addr + HDR, src, n)
+        self._put_header(addr, seq + 2, -1 if not fits else n, time.time())     # even: stable
+        self._seq[key] = seq + 2
+        del arr
+        return fits
+
+    def get(self, key: str, rank: int, out: np.ndarray | None = None):
+        """``rank``'s latest ``key``: (seq, publish time, payload bytes or
+        ``out`` filled), ``(seq, ts, None)`` when the payload sits on the TCP
+        mailbox, None before the first publication or on a torn read (the
+        writer was mid-copy: try again next time)."""
+        addr = self.base + self._off[(key, rank)]
+        seq, n, ts, _ = self._header(addr)
+        if seq == 0 or seq & 1:
+            if seq & 1:
+                self.torn += 1
+            return None
+        if n < 0:
+            return seq, ts, None
+        if out is not None and out.nbytes >= n:
+            dst_arr = out
+        else:
+            dst_arr = np.empty(n, np.uint8)
+        if n:
+            self._copy(dst_arr.ctypes.data, addr + HDR, n)
+        seq2 = self._header(addr)[0]
+        self.reads += 1
+        if seq2 != seq:
+            self.torn += 1
+            return None
+        return seq, ts, (dst_arr if out is not None and dst_arr is out else dst_arr.tobytes())
+
+    def close(self) -> None:
+        from ..ops._lib import LIB
+        for p in self._opened:
+            try:
+                LIB.call("fm_ipc_close", p)
+            except RuntimeError:
+                pass
+        self._opened = []
+
+
+class HybridMailbox:
+    """The mailbox API (parallel/mailbox.py) with the board's bulk keys on
+    the board and everything else on the TCPStore."""
+
+    def __init__(self, mb, board: DeviceBoard):
+        self.mb, self.board = mb, board
+        self.rank, self.world, self.prefix = mb.rank, mb.world, mb.prefix
+
+    def put(self, key: str, payload: bytes) -> None:
+        k = self.prefix + key
+        if self.board.handles(k) and self.board.put(k, payload):
+            return
+        self.mb.put(key, payload)
+
+    def get(self, key: str, rank: int):
+        k = self.prefix + key
+        if not self.board.handles(k):
+            return self.mb.get(key, rank)
+        got = self.board.get(k, rank)
+        if got is None:
+            return None
+        seq, ts, payload = got
+        if payload is None:                      # too big for the region: on the TCP mailbox
+            return self.mb.get(key, rank)
+        return ts, payload
+
+    def __getattr__(self, name):                 # append / trim / read_log / _k: the TCP mailbox
+        return getattr(self.mb, name)
+
+
+def setup(device, keys: dict | None = None) -> DeviceBoard | None:
+    """Every rank of an initialised world (collective): create the board,
+    self-test it (each rank publishes a pattern, every rank reads every
+    rank's), and install it for :func:`parallel.mailbox.Mailbox.for_world`.
+    None (mailbox only) when not distributed, without a GPU or when the test
+    fails on any rank."""
+    global _board
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return None
+    dev = torch.device(device)
+    ok = dev.type == "cuda"
+    board = None
+    if ok:
+        try:
+            board = DeviceBoard(dist.get_rank(), dist.get_world_size(), dev, keys)
+            k0 = next(iter(board.keys))
+            pat = (np.arange(4096, dtype=np.float64) * (board.rank + 1) + 0.5)
+            board.put(k0, pat)
+            dist.barrier()
+            for r in range(board.world):
+                got = board.get(k0, r)
+                want = (np.arange(4096, dtype=np.float64) * (r + 1) + 0.5).tobytes()
+                ok = ok and got is not None and got[2] == want
+        except Exception:  # noqa: BLE001 - any failure: stay on the mailbox
+            ok = False
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if not bool(flag.item()):
+        if board is not None:
+            board.close()
+        return None
+    # the self-test's pattern is not a publication: restart every region at seq 0
+    for k in board.keys:
+        board._seq[k] = 0
+        board._put_header(board.base + board._off[(k, board.rank)], 0, 0, 0.0)
+    dist.barrier()
+    _board = board
+    return board
+
+
+def uninstall() -> None:
+    global _board
+    if _board is not None:
+        _board.close()
+    _board = None

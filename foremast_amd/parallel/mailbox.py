@@ -36,7 +36,12 @@ class Mailbox:
         if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
             return None
         from torch.distributed import distributed_c10d as c10d
-        return cls(c10d._get_default_store(), dist.get_rank(), dist.get_world_size(), prefix)
+        mb = cls(c10d._get_default_store(), dist.get_rank(), dist.get_world_size(), prefix)
+        from . import board
+        b = board.installed()
+        # bulk latest values (gauge vectors, verdict rows) over xGMI when the
+        # node's device board is up (parallel/board.py); logs stay here
+        return board.HybridMailbox(mb, b) if b is not None else mb
 
     def _k(self, key: str, rank: int) -> str:
         return f"{self.prefix}{key}/{rank}"
