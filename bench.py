@@ -246,13 +246,16 @@ def main() -> None:
     pub_graphs: list = []
     peer = None
     if args.publish in ("auto", "peer") and world > 1:
-        from foremast_amd.parallel.peer import PeerPublisher, selftest
+        from foremast_amd.parallel.peer import PeerPublisher, selftest, selftest_captured
         try:
             peer = PeerPublisher(info.rank, world, depth, s_pad, dev)
             rep: dict = {}
             if not selftest(peer, report=rep):
                 raise RuntimeError(f"peer publish self-test failed {rep}")
-            peer.reset()                         # the ring restarts at step 0 on every rank
+            # the captured form (device step counter, one graph per slot) on
+            # this node too; it leaves the ring reset at step 0 on every rank
+            if not selftest_captured(peer, report=rep):
+                raise RuntimeError(f"captured peer publish self-test failed {rep}")
             args.publish = "peer"
         except Exception as e:  # noqa: BLE001 - the eager all-gather is the fallback
             if peer is not None:
@@ -301,7 +304,8 @@ def main() -> None:
             if k >= depth:                       # retire step k - depth
                 ev1[slot].synchronize()
                 if peer is not None and not peer.step_ok(slot):
-                    raise RuntimeError(f"peer publish: a wait of step {k - depth} timed out on rank {info.rank}")
+                    raise RuntimeError(f"peer publish: a wait of step {k - depth} timed out on rank {info.rank} "
+                                       f"({peer.describe()})")
             if k < n:
                 ticks[slot]()
                 ev_tick[slot].record(compute)

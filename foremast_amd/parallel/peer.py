@@ -45,9 +45,11 @@ from ..ops._lib import LIB, stream_of
 
 import os
 
-# wait budget in GPU clock cycles (~1 s at 2.1 GHz): a publish waits for at
-# most one step of another rank, milliseconds
-_BUDGET = int(os.environ.get("FOREMAST_PEER_BUDGET", 2_000_000_000))
+# wait budget in GPU clock cycles (~5 s at 2.1 GHz): a publish waits for at
+# most one step of another rank (milliseconds), but a rank's host may be held
+# up far longer than a step (first graph launch, a page-in, CPU contention on
+# a shared node) -- the budget only bounds how long a DEAD peer can hold a wave
+_BUDGET = int(os.environ.get("FOREMAST_PEER_BUDGET", 10_000_000_000))
 
 
 def _store():
@@ -195,6 +197,14 @@ class PeerPublisher:
         LIB.call("fm_peer_ack_ctr", self.ack_ptrs[slot].data_ptr() if self.world > 1 else None, self.world - 1,
                  self.ctr.data_ptr(), ss, slot, s)
 
+    def describe(self) -> str:
+        """Counters and words of this rank (a failed step's report)."""
+        torch.cuda.synchronize(self.dev)
+        words = self.flags.tolist() if self.rank == 0 else self.ack.tolist()
+        return (f"ctr {int(self.ctr.item())} slot_status {self.slot_status.tolist()} host_status "
+                f"{self.host_status.tolist()} status {self.status.tolist()} "
+                f"{'flags' if self.rank == 0 else 'ack'} {words}")
+
     def step_ok(self, slot: int) -> bool:
         """The retired step of ``slot`` (its stream work observed) had no
         timed-out wait on this rank: its verdict rows are whole."""
@@ -213,6 +223,46 @@ class PeerPublisher:
             except RuntimeError:
                 pass
         self._opened = []
+
+
+def selftest_captured(pub: PeerPublisher, steps: int = 64, report: dict | None = None) -> bool:
+    """The captured form on this node: after :meth:`PeerPublisher.reset`, one
+    graph per slot (publish + rank 0's wait, copy, ack) replayed ``steps``
+    times without a host sync, then rank 0's last fleet copy compared with
+    the all-gather of the last step's shards and every step's wait status
+    checked; the ring is reset again afterwards.  Same verdict on every rank."""
+    dev = pub.dev
+    pub.reset()
+    x = torch.zeros((pub.shard, 4), dtype=torch.float32, device=dev)
+    hosts = [torch.zeros((pub.world * pub.shard, 4), dtype=torch.float32, pin_memory=True)
+             for _ in range(pub.depth)]
+    side = torch.cuda.Stream(dev)
+    graphs = []
+    with torch.cuda.stream(side):
+        for slot in range(pub.depth):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                pub.publish_dev(slot, x)
+                if pub.rank == 0:
+                    pub.collect_dev(slot, hosts[slot], pub.world * pub.shard)
+            graphs.append(g)
+        for k in range(steps):
+            x.fill_(1000.0 * pub.rank + 0.25 * k)
+            graphs[k % pub.depth].replay()
+        torch.cuda.synchronize(dev)
+    bad = sum(0 if pub.step_ok(s) else 1 for s in range(pub.depth))
+    ok = bad == 0 and int(pub.ctr.item()) == steps
+    xs = x if dist.get_backend() == "nccl" else x.cpu()
+    ref = [torch.empty_like(xs) for _ in range(pub.world)]
+    dist.all_gather(ref, xs)
+    if pub.rank == 0:
+        ok = ok and torch.equal(hosts[(steps - 1) % pub.depth], torch.cat(ref).cpu())
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if report is not None and not bool(flag.item()):
+        report.update(captured=pub.describe())
+    pub.reset()
+    return bool(flag.item())
 
 
 def selftest(pub: PeerPublisher, steps: int = 8, report: dict | None = None) -> bool:

@@ -32,9 +32,22 @@ for s in $steps; do
          e2e c3e2e_http60 --config 3e2e --source http --poll-seconds 60 --window 60 --steps 12 --warmup 2 --prom-workers 8 &&
          e2e c2e2e_http --config 2e2e --source http --steps 20 --warmup 3 --prom-workers 8 || exit $rc ;;
     peerprobe) run peer_probe 150 python -u tools/peer_probe.py || exit $rc ;;
-    peer) run peer_test 200 python -u -m pytest tests/test_peer.py -x -v --timeout 150 --timeout-method thread || exit $rc
+    peer) run peer_test 300 python -u -m pytest tests/test_peer.py tests/test_board.py -x -v -s --timeout 200 \
+              --timeout-method thread || exit $rc
           run peer_bench 240 env FOREMAST_DEVICE_INDEX=0 FOREMAST_DIST_BACKEND=gloo python bench.py --gpus 2 \
               --services 2500 --publish peer --steps 300 --warmup 20 || exit $rc ;;
+    mixed) e2e c_mixed --config mixed --steps 20 --warmup 3 &&
+         e2e c3e2e_60 --config 3e2e --poll-seconds 60 --window 60 --steps 20 --warmup 3 &&
+         e2e c2e2e --config 2e2e --steps 20 --warmup 3 &&
+         e2e c4e2e --config 4e2e --steps 20 --warmup 3 || exit $rc ;;
+    hostprof) for c in 2e2e 4e2e mixed; do
+           FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_$c.prof timeout -k 10 400 python -u benchmarks/bench_configs.py \
+               --config $c --steps 12 --warmup 3 > gpurun_out/check_hostprof_$c.log 2>&1; rc=$?
+           echo "hostprof $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+           python -c "import pstats,sys; p=pstats.Stats('gpurun_out/hostprof_$c.prof', stream=sys.stdout); \
+               p.sort_stats('tottime').print_stats(70); p.sort_stats('cumtime').print_stats(70)" \
+               > gpurun_out/hostprof_$c.txt || exit 1
+         done ;;
     restart) e2e c3e2e_restart --config 3e2e --steps 5 --warmup 2 --restart &&
          e2e c2e2e_restart --config 2e2e --steps 5 --warmup 2 --restart || exit $rc ;;
     scanprobe) run scanprobe 200 python -u tools/hw_scan_probe.py || exit $rc
