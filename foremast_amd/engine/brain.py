@@ -620,7 +620,7 @@ class Brain:
                         self.save_checkpoint(checkpoint_dir)
                     if checkpoint_dir and self.cfg.history_checkpoint_s > 0 and \
                             time.monotonic() - hist_t >= self.cfg.history_checkpoint_s:
-                        self.save_history(checkpoint_dir)
+                        self.save_history(checkpoint_dir, wait=False)      # off the cycle (side stream + thread)
                         hist_t = time.monotonic()
                     if r.get("claimed", 0) == 0:
                         (stop.wait(poll) if stop is not None else time.sleep(poll))
@@ -788,19 +788,47 @@ class Brain:
         t, meta = self.state_tensors()
         return checkpoint.save(dirpath, t, meta, tag=checkpoint.rank_tag(self.info.rank, self.info.world))
 
-    def save_history(self, dirpath: str):
+    def save_history(self, dirpath: str, wait: bool = True):
         """The device-resident history grids of every live job
         (``history-r<rank>of<world>-<ms>.safetensors``), for a warm restart:
         :meth:`load_history` puts them back and the first cycle fetches only
-        the gap since each row's newest sample."""
+        the gap since each row's newest sample.
+
+        ``wait=False`` (the service loop's periodic save): the rows are
+        gathered on a side stream into reusable pinned host buffers and the
+        file is written by a background thread -- the cycle only pays for the
+        launches (the next cycle's grid writes wait for the on-device gather,
+        not for the copy or the disk).  A save still in flight makes the next
+        one a no-op (returns None).  Returns the file path (``wait``) or the
+        pending future."""
         from . import checkpoint
         from .fastpath import history_state
         if self.fast is None:
             return None
-        t, meta = history_state(self.fast)
+        prev = getattr(self, "_hist_future", None)
+        if prev is not None and not prev.done():
+            if not wait:
+                log.info("history checkpoint still being written; this one skipped")
+                return None
+            prev.result()
+        tag = checkpoint.rank_tag(self.info.rank, self.info.world)
+        if wait or self.device.type != "cuda":
+            t, meta, _ = history_state(self.fast)
+            meta.update(rank=self.info.rank, world=self.info.world)
+            return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
+        if getattr(self, "_hist_stream", None) is None:
+            self._hist_stream = torch.cuda.Stream(self.device)
+            self._hist_pinned: dict = {}
+            from concurrent.futures import ThreadPoolExecutor
+            self._hist_writer = ThreadPoolExecutor(1, thread_name_prefix="history-ckpt")
+        t, meta, ev = history_state(self.fast, self._hist_pinned, self._hist_stream)
         meta.update(rank=self.info.rank, world=self.info.world)
-        return checkpoint.save(dirpath, t, meta, tag=checkpoint.rank_tag(self.info.rank, self.info.world),
-                               keep=2, kind="history")
+
+        def write():
+            ev.synchronize()
+            return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
+        self._hist_future = self._hist_writer.submit(write)
+        return self._hist_future
 
     def load_history(self, dirpath: str) -> int:
         """Restore the history rows this rank owns from its own latest history
@@ -816,7 +844,10 @@ class Brain:
         if own is not None and (newest is None or newest[0] == self.info.world or newest[1] <= own[2]):
             sets = [own[:2]]
         else:
-            sets = checkpoint.load_any_world(dirpath, kind="history")
+            # a re-shard: from every rank's file of the newest world, only the
+            # rows this rank now owns (owner blocks / row runs read from disk)
+            sets = checkpoint.load_any_world(dirpath, kind="history", owns=self._owns_key,
+                                             world=self.info.world, rank=self.info.rank)
         n = 0
         for t, meta in sets:
             n += load_history(self.fast, t, meta, self.clock(), owns=self._owns_key)

@@ -13,6 +13,7 @@ import os
 import time
 from pathlib import Path
 
+import numpy as np
 import torch
 from safetensors.torch import load_file, save_file
 
@@ -114,16 +115,73 @@ def load_latest(dirpath: str, tag: str = "", with_time: bool = False, kind: str 
     return got if with_time else got[:2]
 
 
-def load_any_world(dirpath: str, kind: str = "engine") -> list[tuple[dict[str, torch.Tensor], dict]]:
+def load_any_world(dirpath: str, kind: str = "engine", owns=None, world: int | None = None,
+                   rank: int | None = None) -> list[tuple[dict[str, torch.Tensor], dict]]:
     """Every rank's latest checkpoint of the most recently saved world size
-    (a restart with a different world re-shards from all of them)."""
+    (a restart with a different world re-shards from all of them).  With
+    ``owns(namespace, app)`` (history files): only the rows this rank owns
+    are read from disk (:func:`read_owned_rows`)."""
     sets = _latest_files(dirpath, kind)
     if not sets:
         return []
-    world = max(sets, key=lambda w: max(t for t, _ in sets[w]))
+    w_saved = max(sets, key=lambda w: max(t for t, _ in sets[w]))
     out = []
-    for _, p in sets[world]:
-        got = _read(p)
+    for _, p in sets[w_saved]:
+        got = read_owned_rows(p, owns, world, rank) if owns is not None else _read(p)
         if got is not None:
             out.append(got[:2])
     return out
+
+
+_DTYPES = {"F64": torch.float64, "F32": torch.float32, "F16": torch.float16, "BF16": torch.bfloat16,
+           "I64": torch.int64, "I32": torch.int32, "I16": torch.int16, "I8": torch.int8, "U8": torch.uint8,
+           "BOOL": torch.bool}
+
+
+def _runs(idx: np.ndarray) -> list[tuple[int, int]]:
+    """Sorted row indices -> [(start, stop)) runs of consecutive rows."""
+    if not len(idx):
+        return []
+    brk = np.flatnonzero(np.diff(idx) != 1) + 1
+    st = np.concatenate([[0], brk])
+    en = np.concatenate([brk, [len(idx)]])
+    return [(int(idx[a]), int(idx[b - 1]) + 1) for a, b in zip(st.tolist(), en.tolist())]
+
+
+def read_owned_rows(path: Path, owns, world: int | None = None, rank: int | None = None):
+    """A history checkpoint restricted to the rows ``owns(namespace, app)``
+    selects, reading only those rows from disk (safetensors slices of each
+    ``<store>.*`` row tensor).  Rows are saved in 16 owner blocks
+    (``<store>.blocks``, fastpath.history_state): for a ``world`` dividing 16
+    a rank's rows are whole blocks, a few contiguous reads; any other world
+    reads the coalesced runs of its rows.  -> (tensors, meta, saved_at)."""
+    from safetensors import safe_open
+    if not path.exists():
+        return None
+    with safe_open(str(path), framework="pt") as f:
+        md = f.metadata() or {}
+        if md.get("format") != FORMAT_VERSION:
+            raise ValueError(f"unsupported checkpoint format {md.get('format')!r}")
+        meta = json.loads(md.get("meta", "{}"))
+        names = list(f.keys())
+        out: dict[str, torch.Tensor] = {}
+        for store in sorted({n.split(".", 1)[0] for n in names}):
+            owners = meta.get(f"{store}.owners", [])
+            blocks = meta.get(f"{store}.blocks")
+            if blocks is not None and world is not None and rank is not None and 16 % max(1, world) == 0:
+                sel = np.concatenate([np.arange(blocks[b], blocks[b + 1]) for b in range(16) if b % world == rank]
+                                     + [np.zeros(0, np.int64)]).astype(np.int64)
+            else:
+                sel = np.asarray([i for i, (ns, app) in enumerate(owners) if owns(ns, app)], np.int64)
+            runs = _runs(sel)
+            for n in names:
+                if not n.startswith(store + "."):
+                    continue
+                sl = f.get_slice(n)
+                parts = [sl[a:b] for a, b in runs]
+                shape = sl.get_shape()
+                out[n] = torch.cat(parts) if parts else torch.empty((0, *shape[1:]), dtype=_DTYPES[sl.get_dtype()])
+            meta[f"{store}.keys"] = [meta[f"{store}.keys"][i] for i in sel.tolist()]
+            meta[f"{store}.owners"] = [owners[i] for i in sel.tolist()]
+            meta.pop(f"{store}.blocks", None)
+    return out, meta, float(md.get("saved_at", "0"))

@@ -2171,29 +2171,76 @@ def _history_rows(fp: "FastPath"):
         yield name, st, rows, [d[int(r)][0] for r in rows], [d[int(r)][1] for r in rows]
 
 
-def history_state(fp: "FastPath") -> tuple[dict, dict]:
+OWNER_BLOCKS = 16           # saved rows are grouped by service_owner(.., 16): one block per rank of any world | 16
+
+
+def history_state(fp: "FastPath", pinned: dict | None = None, stream=None) -> tuple[dict, dict, object]:
     """The device-resident history of every live job (static rows: the
     left-aligned samples; sliding rows: the window's columns) + their row
-    keys, owners and times, for a warm restart (``Brain.save_history``)."""
+    keys, owners and times, for a warm restart (``Brain.save_history``).
+
+    Rows are ordered by ``service_owner(namespace, app, 16)`` (``meta
+    "{name}.blocks"`` = the row offsets of the 16 owner blocks): after a
+    re-shard to a world that divides 16, a rank reads only its blocks.
+
+    ``pinned`` (a dict of reusable pinned host buffers) + ``stream``: the
+    rows are gathered on ``stream`` (after the current stream's work; the
+    current stream then waits only for the gather, not for the copy) and
+    copied into pinned host memory asynchronously; the returned event marks
+    the host copy complete (None: synchronous, tensors ready)."""
+    from ..parallel.dist import service_owner
     t: dict[str, torch.Tensor] = {}
     meta: dict = {"step": fp.b.step}
+    cur = torch.cuda.current_stream(fp.b.device) if fp.b.device.type == "cuda" else None
+    side = stream if cur is not None else None
+    if side is not None:
+        side.wait_stream(cur)
+    ev = None
+    gathered: list = []
     for name, st, rows, keys, owners in _history_rows(fp):
         if not len(rows):
             continue
+        ob = np.fromiter((service_owner(ns, app, OWNER_BLOCKS) for ns, app in owners), np.int64, len(owners))
+        order = np.argsort(ob, kind="stable")
+        rows, keys, owners = rows[order], [keys[i] for i in order], [owners[i] for i in order]
+        meta[f"{name}.blocks"] = np.searchsorted(ob[order], np.arange(OWNER_BLOCKS + 1)).tolist()
         ri = torch.as_tensor(rows, device=st.device)
         if st.sliding:
             if st.t0 is None or st.e <= st.ws:
                 continue
-            t[f"{name}.values"] = st.buf.index_select(0, ri)[:, st.ws:st.e].cpu()
+            view, w = st.buf[:, st.ws:st.e], st.e - st.ws
             meta[f"{name}.t_first"] = st.t0 + st.ws * st.step
         else:
             w = max(1, int(st.nlen[rows].max()))
-            t[f"{name}.values"] = st.buf.index_select(0, ri)[:, :w].cpu()
+            view = st.buf[:, :w]
             t[f"{name}.nlen"] = torch.from_numpy(st.nlen[rows].copy())
+        if side is None:
+            t[f"{name}.values"] = view.index_select(0, ri).cpu()
+        else:
+            with torch.cuda.stream(side):
+                gathered.append((name, view.index_select(0, ri)))  # contiguous [rows, w] on the device
         t[f"{name}.last_t"] = torch.from_numpy(st.last_t[rows].copy())
         meta[f"{name}.keys"] = [list(k) for k in keys]
         meta[f"{name}.owners"] = [list(o) for o in owners]
-    return t, meta
+    if side is not None:
+        # the next cycle's writes to the grids wait only for the gathers; the
+        # host copies run on behind them
+        sel = torch.cuda.Event()
+        sel.record(side)
+        cur.wait_event(sel)
+        with torch.cuda.stream(side):
+            for name, blk in gathered:
+                n = blk.numel() * blk.element_size()
+                host = pinned.get(name)
+                if host is None or host.numel() < n:
+                    host = pinned[name] = torch.empty(int(n * 1.25) + 64, dtype=torch.uint8, pin_memory=True)
+                hv = host[:n].view(blk.dtype).view(blk.shape)
+                hv.copy_(blk, non_blocking=True)
+                blk.record_stream(side)
+                t[f"{name}.values"] = hv
+        ev = torch.cuda.Event()
+        ev.record(side)
+    return t, meta, ev
 
 
 def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> int:

@@ -133,3 +133,70 @@ def test_history_reshards_two_to_four_ranks(tmp_path):
     allk = set().union(*got.values())
     assert allk == saved[0] | saved[1]                  # every row restored once ...
     assert sum(len(v) for v in got.values()) == len(allk)   # ... by exactly one new rank
+
+
+def test_history_reshards_two_to_three_ranks_reading_only_owned_rows(tmp_path):
+    """A world that does not divide the 16 owner blocks: each new rank reads
+    the coalesced runs of its own rows (checkpoint.read_owned_rows) -- the
+    same rows a full read + filter keeps."""
+    from pathlib import Path
+    from foremast_amd.engine import checkpoint
+    clock = Clock()
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    _submit(client, n_canary=12, n_cont=8)
+    for r in range(2):
+        b = _rig(store, clock, SyntheticSource(), worker=f"r{r}")
+        b.info = D.DistInfo(r, 2, r)
+        b.run_once()
+        b.save_history(str(tmp_path))
+        clock.t += 1
+    files = sorted(Path(tmp_path).glob("history-*.safetensors"))
+    assert len(files) == 2
+    for r in range(3):
+        owns = lambda ns, app, r=r: D.service_owner(ns, app, 3) == r       # noqa: E731
+        for p in files:
+            part, meta, _ = checkpoint.read_owned_rows(p, owns, 3, r)
+            full, fmeta, _ = checkpoint._read(p)
+            for store_name in ("static", "sliding"):
+                owners = fmeta.get(f"{store_name}.owners", [])
+                keep = [i for i, (ns, app) in enumerate(owners) if owns(ns, app)]
+                assert meta.get(f"{store_name}.owners", []) == [owners[i] for i in keep]
+                for k in full:
+                    if k.startswith(store_name + "."):
+                        assert part[k].shape[0] == len(keep)
+                        a, b_ = part[k].numpy(), full[k].numpy()[keep]
+                        assert np.array_equal(np.nan_to_num(a, nan=-7), np.nan_to_num(b_, nan=-7))
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_gpu_async_history_save_is_off_the_cycle(tmp_path):
+    """the periodic history save gathers on a side stream into
+    pinned buffers and writes on a thread: the call returns at once, the file
+    it writes restores the same rows, and a save still in flight makes the next
+    one a no-op."""
+    import time
+    import torch
+    clock = Clock()
+    store = MemoryStore()
+    client = AnalystClient.for_app(create_app(store), clock=clock)
+    _submit(client, n_canary=8, n_cont=6)
+    b = Brain(store, BrainConfig(), device=torch.device("cuda"), clock=clock, worker_id="w",
+              sources=SourceRouter(synthetic=SyntheticSource(), force="synthetic"))
+    for _ in range(2):
+        b.run_once()
+        clock.t += 60
+    live_rows = len({(w.plan.sliding, int(r)) for w in b.fast.works.values() for r in w.rows})
+    t0 = time.perf_counter()
+    fut = b.save_history(str(tmp_path), wait=False)
+    dt = time.perf_counter() - t0
+    assert fut is not None
+    b.run_once()                                    # the next cycle runs while the file is written
+    path = fut.result(timeout=60)
+    assert path.exists() and dt < 0.5
+    b2 = Brain(MemoryStore(), BrainConfig(), device=torch.device("cuda"), clock=clock, worker_id="w",
+               sources=SourceRouter(synthetic=SyntheticSource(), force="synthetic"))
+    assert b2.load_history(str(tmp_path)) == live_rows
