@@ -248,9 +248,12 @@ class Brain:
         R = len(rows)
         diff = None
         if any(len(r.base) for r in rows):
-            pcfg = C.PairwiseConfig(self.cfg.pairwise_algorithm, self.cfg.pairwise_threshold,
-                                    self.cfg.min_mann_white, self.cfg.min_wilcoxon, self.cfg.min_kruskal)
-            _, _, diff = C.pairwise_tests(cur, base, pcfg)
+            # the registered operator (ops/library.py): validated shapes, and
+            # the general path's rank tests show up as foremast::pairwise_tests
+            # in torch.profiler traces
+            _, _, diff = torch.ops.foremast.pairwise_tests(
+                cur, base, self.cfg.pairwise_algorithm, float(self.cfg.pairwise_threshold),
+                int(self.cfg.min_mann_white), int(self.cfg.min_wilcoxon), int(self.cfg.min_kruskal))
         # Model dispatch: rows are grouped by their metric type's algorithm
         # (ml_algorithmN, else ML_ALGORITHM) and each group is ONE batched zoo
         # call over its rows (per-series model selection as a
