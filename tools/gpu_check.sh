@@ -40,6 +40,11 @@ for s in $steps; do
          e2e c3e2e_60 --config 3e2e --poll-seconds 60 --window 60 --steps 20 --warmup 3 &&
          e2e c2e2e --config 2e2e --steps 20 --warmup 3 &&
          e2e c4e2e --config 4e2e --steps 20 --warmup 3 || exit $rc ;;
+    shard) run shard1250 200 python bench.py --services 1250 --steps 400 --warmup 20 || exit $rc
+           run shard1250_prof 300 bash -c "cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_shard \
+               -o shard -- python3 $R/bench.py --services 1250 --steps 200 --warmup 20" || exit $rc ;;
+    httpbench) run httpbench 600 python -u tools/http_fetch_bench.py --services 10000 --cycles 8 \
+               --out gpurun_out/http_fetch_bench.jsonl || exit $rc ;;
     hostprof) for c in 2e2e 4e2e mixed; do
            FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_$c.prof timeout -k 10 400 python -u benchmarks/bench_configs.py \
                --config $c --steps 12 --warmup 3 > gpurun_out/check_hostprof_$c.log 2>&1; rc=$?
