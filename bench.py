@@ -298,18 +298,26 @@ def main() -> None:
     # instead of idling through the host's wake-up and launch; a slot is
     # reused only after its previous step retired (verdict in host memory,
     # event observed), and every step retires inside the timed region.
+    # The slot of a step follows the GLOBAL step count (a run() of an odd
+    # number of steps must not restart the ring at slot 0): the captured peer
+    # graphs are one per slot and the ranks' device step counters advance with
+    # every step, so slot == step % depth on every rank, always.
+    gstep = [0]
+
     def run(n: int) -> None:
+        g0 = gstep[0]
         for k in range(n + depth):
-            slot = k % depth
+            slot = (g0 + k) % depth
             if k >= depth:                       # retire step k - depth
                 ev1[slot].synchronize()
                 if peer is not None and not peer.step_ok(slot):
-                    raise RuntimeError(f"peer publish: a wait of step {k - depth} timed out on rank {info.rank} "
-                                       f"({peer.describe()})")
+                    raise RuntimeError(f"peer publish: a wait of step {g0 + k - depth} timed out on rank "
+                                       f"{info.rank} ({peer.describe()})")
             if k < n:
                 ticks[slot]()
                 ev_tick[slot].record(compute)
                 publish(slot, ev1[slot])
+        gstep[0] = g0 + n
 
     if args.publish == "auto":
         args.publish = "graph" if world == 1 else "eager"
@@ -362,11 +370,13 @@ def main() -> None:
     t_a, t_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     lat: list[float] = []
     for _ in range(max(5, min(args.steps, 50))):
+        slot = gstep[0] % depth
         t_a.record(compute)
-        ticks[0]()
-        ev_tick[0].record(compute)
-        publish(0, t_b)
+        ticks[slot]()
+        ev_tick[slot].record(compute)
+        publish(slot, t_b)
         t_b.synchronize()
+        gstep[0] += 1
         lat.append(t_a.elapsed_time(t_b))
     p50 = D.all_reduce_max(statistics.median(lat) / 1e3, dev)
     if peer is not None:
@@ -374,7 +384,7 @@ def main() -> None:
     n_dev, backend = _device_census(info, dev)
     ms = elapsed / args.steps * 1e3
     windows = S * M
-    verdict = hosts[0][:S].numpy() if info.is_main else None
+    verdict = hosts[(gstep[0] - 1) % depth][:S].numpy() if info.is_main else None
     if info.is_main:
         n_anom = int((verdict[:, 0] == 1).sum())
         out = {
