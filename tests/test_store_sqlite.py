@@ -246,3 +246,24 @@ def test_hpalog_reads_scan_only_the_jobs_batches(tmp_path):
     reads.clear()
     got = st.hpalogs("h0", 3)
     assert [lg.log.hpa_score for lg in got] == [79, 78, 77] and max(reads) <= 30
+
+
+def test_session_columns_track_adds_and_drops():
+    """The sticky session's held jobs as O(1)-maintained columns: after any
+    mix of adds, re-adds (new version) and drops the snapshot holds exactly
+    the held jobs, each with its own row id and version."""
+    from foremast_amd.service.store import _Session
+    rng = np.random.default_rng(4)
+    s = _Session()
+    for step in range(3000):
+        j = f"j{int(rng.integers(0, 300))}"
+        if rng.random() < 0.6:
+            s.add(j, int(rng.integers(0, 10_000)), step)
+        else:
+            s.drop(j)
+        if step % 250 == 0 or step == 2999:
+            ids, vers, rids = s.snapshot(10_000)
+            assert sorted(ids) == sorted(s.held)
+            assert all(s.held[i] == (int(r), v) for i, v, r in zip(ids, vers, rids.tolist()))
+    ids, _, _ = s.snapshot(5)
+    assert len(ids) == 5
