@@ -96,11 +96,20 @@ def _run_pair(device="cpu"):
             assert (json.loads(da.anomaly_info) if da.anomaly_info else {}) == \
                    (json.loads(db.anomaly_info) if db.anomaly_info else {}), (cyc, jid)
         for jid in ids_a:
-            la = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current, d.upper, d.lower) for d in l.log.details])
+            la = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current) for d in l.log.details])
                   for l in a[1].hpalogs(jid)]
-            lb = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current, d.upper, d.lower) for d in l.log.details])
+            lb = [(l.log.hpa_score, l.log.reason, [(d.metric_type, d.current) for d in l.log.details])
                   for l in b[1].hpalogs(jid)]
             assert la == lb, (cyc, jid)
+            # the bands: exact on the CPU; on the GPU the resident kernel and the
+            # general path's batch (sized by its own longest history) reduce in
+            # different orders -- fp32 bounds agree to ~10 ulp, as the gauges below
+            ba = np.array([(d.upper, d.lower) for l in a[1].hpalogs(jid) for d in l.log.details], float)
+            bb = np.array([(d.upper, d.lower) for l in b[1].hpalogs(jid) for d in l.log.details], float)
+            if str(device) == "cpu":
+                np.testing.assert_array_equal(ba, bb)
+            else:
+                np.testing.assert_allclose(ba, bb, rtol=2e-5, atol=1e-9)
         ta, tb = a[4].table, b[4].table
         assert set(ta.index) == set(tb.index)
         for k in ta.index:
