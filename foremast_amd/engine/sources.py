@@ -157,6 +157,7 @@ class PrometheusSource:
         self._native: dict[str, object] = {}
         self._tpl: dict[str, object] = {}
         self._plans: dict[int, tuple] = {}
+        self._relit: dict[str, str] = {}          # app -> its escaped regex literal
         self._pool = None
         self.requests = 0
         self.bytes = 0
@@ -284,51 +285,73 @@ class PrometheusSource:
                 else False
         return got
 
+    def _chunks(self, gid: np.ndarray, apps: np.ndarray, groups: list) -> list:
+        """The batched requests of a planned list: per selector group its
+        sorted unique apps in chunks of ``batch`` (escaped literals cached)."""
+        from .ingest import KeyedQuery
+        chunks = []
+        lit = self._relit
+        for g, grp in enumerate(groups):
+            uniq = sorted(set(apps[gid == g].tolist()))
+            for a in uniq:
+                if a not in lit:
+                    lit[a] = promql.re_literal(a)
+            for k in range(0, len(uniq), self.batch):
+                part = uniq[k:k + self.batch]
+                alt = "|".join([lit[a] for a in part]) if len(part) > 1 else None
+                chunks.append((g, KeyedQuery(grp, part, 0.0, 0.0, alt=alt)))
+        return chunks
+
     def _columns_plan(self, templates: list[str]):
         """Request plan of a template list (memoised per list object: the
-        brain's TemplateLists live while the job set is unchanged; a subset of
-        a planned root list -- fleet churn -- indexes the root's plan):
-        (per template: group id, app hash; slow template indices; per group
-        its app-chunk requests)."""
-        from .ingest import KeyedQuery
+        brain's TemplateLists live while the job set is unchanged).  A subset
+        of a planned root list (fleet churn: jobs closed) indexes the root's
+        per-template columns; its requests are the root's until the subset has
+        shrunk below 90 % of what they were built for, then re-chunked from the
+        subset's apps (kept on the root entry: later subsets only shrink).
+        -> (per template: group id, app hash; slow template indices; requests)."""
         ent = self._plans.get(id(templates))
         if ent is not None and ent[0] is templates:
             return ent[1]
         root = getattr(templates, "root", None)
         rent = self._plans.get(id(root)) if root is not None else None
-        if rent is not None and rent[0] is root and len(templates) >= 0.9 * len(root):
-            rp = rent[1]
+        info = None
+        if rent is not None and rent[0] is root and rent[2] is not None:
+            self._plans.pop(id(root))                   # the root stays the most recently used
+            self._plans[id(root)] = rent
+            ri = rent[2]
             ix = np.asarray(templates.ix, np.int64)
-            plan = (rp[0][ix], rp[1][ix], np.flatnonzero(rp[0][ix] < 0), rp[3])
+            gid = ri["gid"][ix]
+            if len(templates) < 0.9 * ri["chunked_for"]:
+                ri["chunks"] = self._chunks(gid, ri["apps"][ix], ri["groups"])
+                ri["chunked_for"] = len(templates)
+            plan = (gid, ri["th"][ix], np.flatnonzero(gid < 0), ri["chunks"])
         else:
             n = len(templates)
             gid = np.full(n, -1, np.int64)
             apps = np.empty(n, object)
             gmap: dict = {}
             for i, tpl in enumerate(templates):
-                info = self._parse_template(tpl)
-                if info:
-                    g = gmap.get(info[0])
+                pt = self._parse_template(tpl)
+                if pt:
+                    g = gmap.get(pt[0])
                     if g is None:
-                        g = gmap[info[0]] = len(gmap)
+                        g = gmap[pt[0]] = len(gmap)
                     gid[i] = g
-                    apps[i] = info[1]
+                    apps[i] = pt[1]
             ok = gid >= 0
             from . import native_rt
             hs = np.zeros(n, np.uint64)
             if ok.any():
                 hs[ok] = native_rt.fnv1a(apps[ok].tolist())
-            chunks = []
-            for grp, g in gmap.items():
-                uniq = sorted(set(apps[gid == g].tolist()))
-                for k in range(0, len(uniq), self.batch):
-                    part = uniq[k:k + self.batch]
-                    alt = "|".join(promql.re_literal(a) for a in part) if len(part) > 1 else None
-                    chunks.append((g, KeyedQuery(grp, part, 0.0, 0.0, alt=alt)))
+            groups = list(gmap)
+            chunks = self._chunks(gid, apps, groups)
             plan = (gid, hs, np.flatnonzero(~ok), chunks)
+            if root is None:                            # a root list: what its subsets index
+                info = {"gid": gid, "th": hs, "apps": apps, "groups": groups, "chunks": chunks, "chunked_for": n}
         if len(self._plans) >= 32:
             self._plans.pop(next(iter(self._plans)))
-        self._plans[id(templates)] = (templates, plan)
+        self._plans[id(templates)] = (templates, plan, info)
         return plan
 
     def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:

@@ -324,3 +324,36 @@ def test_fetch_columns_merges_several_series_per_app():
     np.testing.assert_array_equal(cols.v[cols.off[1]:cols.off[2]], [7])
     assert cols.off[3] == cols.off[2]
     s.close()
+
+
+def test_fetch_columns_churned_subsets_reuse_the_root_plan(server):
+    """Fleet churn hands fetch_columns TemplateList subsets of a root list:
+    they index the root's plan (no re-parse), re-chunk once they shrank past
+    10 % (no request for closed jobs' apps beyond that), and answer exactly
+    what a fresh plan of the same templates answers."""
+    from foremast_amd.engine.sources import TemplateList
+    port, cw, _, _ = server
+    cw.set(T0)
+    base = f"http://127.0.0.1:{port}/api/v1/query_range"
+    tpl = lambda a: base + "?" + urllib.parse.urlencode({"query": f'namespace_app_pod_cpu{{namespace="d",app="{a}"}}'}) \
+        + "&start=START_TIME&end=END_TIME&step=60"
+    root = TemplateList([tpl(f"svc{j}") for j in range(60)])
+    src = PrometheusSource(workers=4, batch=16)
+    src.fetch_columns(root, T0 - 300, T0)
+    cur, ix = root, np.arange(60)
+    rng = np.random.default_rng(1)
+    for step in range(4):
+        keep = np.sort(rng.choice(len(cur), size=int(len(cur) * 0.85), replace=False))
+        cur = TemplateList.subset(cur, [cur[i] for i in keep], keep)
+        ix = ix[keep]
+        n_req = src.stats["requests"]
+        got = src.fetch_columns(cur, T0 - 300, T0)
+        want = PrometheusSource(workers=4, batch=16).fetch_columns(list(cur), T0 - 300, T0)
+        np.testing.assert_array_equal(got.off, want.off)
+        np.testing.assert_array_equal(got.t, want.t)
+        np.testing.assert_array_equal(got.v, want.v)
+        ri = src._plans[id(root)][2]
+        assert ri["chunked_for"] == len(cur)                 # re-chunked for the shrunk subset
+        assert src.stats["requests"] - n_req == len(ri["chunks"])
+        asked = {a for _, q in ri["chunks"] for a in q.values}
+        assert asked == {f"svc{j}" for j in ix}
