@@ -528,12 +528,12 @@ class Brain:
         if ok.any():
             ga = g["ga"]
 
-            def make():                                   # gauge slots are append-only: kept per job list
-                R = range(len(peak))
+            def make(sel):                                # gauge slots are append-only: kept per job list
+                ws = works if sel is None else [works[j] for j in sel]
                 return self.exporter.forecast_slots(
-                    [works[k // M].plan.base_metrics[k % M] for k in R], [works[k // M].plan.namespace for k in R],
-                    [works[k // M].doc.app_name for k in R]).reshape(len(works), M)
-            sl = (self.fast._extra(ga.key, ga.ident, "xfc", make) if ga.key is not None else make()).reshape(-1)
+                    [b for w in ws for b in w.plan.base_metrics], [w.plan.namespace for w in ws for _ in range(M)],
+                    [w.doc.app_name for w in ws for _ in range(M)]).reshape(len(ws), M)
+            sl = (self.fast._extra(ga.key, ga.ident, "xfc", make) if ga.key is not None else make(None)).reshape(-1)
             j = np.flatnonzero(ok)
             self.exporter.set_slots(sl[j], peak[j])
 

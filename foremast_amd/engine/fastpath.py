@@ -320,12 +320,13 @@ class JobIds:
     of this list's jobs in an earlier list (sorted search, no per-job dict)
     -- how a churned list (jobs left) re-indexes the previous list's memos."""
 
-    __slots__ = ("arr", "_order", "_ixc")
+    __slots__ = ("arr", "_order", "_ixc", "_mc")
 
     def __init__(self, works) -> None:
         self.arr = np.fromiter(map(_serial_of, works), np.int64, len(works))
         self._order = None
         self._ixc = None          # (old, positions): the group memos all ask about the same old list
+        self._mc = None           # (old, (positions, found, n found))
 
     def __len__(self) -> int:
         return len(self.arr)
@@ -347,6 +348,16 @@ class JobIds:
         return ix
 
     def _index_in(self, old: "JobIds") -> np.ndarray | None:
+        m = self.match_in(old)
+        return m[0] if m is not None and m[2] == len(self.arr) else None
+
+    def match_in(self, old: "JobIds"):
+        """(positions in ``old``, found mask, number found) of this list's
+        jobs; a position where the mask is False is arbitrary.  None when
+        either list is empty."""
+        c = self._mc
+        if c is not None and c[0] is old:
+            return c[1]
         if not len(self.arr) or not len(old.arr):
             return None
         if old._order is None:
@@ -354,7 +365,9 @@ class JobIds:
         srt = old.arr[old._order]
         p = np.minimum(np.searchsorted(srt, self.arr), len(srt) - 1)
         cand = old._order[p]
-        return cand if np.array_equal(old.arr[cand], self.arr) else None
+        hit = old.arr[cand] == self.arr
+        self._mc = (old, (cand, hit, int(hit.sum())))
+        return self._mc[1]
 
 
 class HpaTable:
@@ -1360,25 +1373,7 @@ class FastPath:
         ga = self._garr.get(key)
         if ga is not None and ga.wcur is not None and (ga.works is works or ga.ident == self._jid(works)):
             ga.works = works
-            changed = False
-            if self._wt_changed:
-                wc, wb = ga.wcur, ga.wbase
-                d = wt.dirty[np.maximum(wc, 0)] & (wc >= 0)
-                if wb is not None:
-                    d |= wt.dirty[np.maximum(wb, 0)] & (wb >= 0)
-                rows = np.flatnonzero(d)
-                if len(rows):
-                    changed = True
-                    ri = torch.from_numpy(rows).to(dev)
-                    v, t, ln = wt.pack(wc[rows], ga.cur.shape[1])
-                    ga.cur[rows], ga.cur_t[rows], ga.cur_len[rows] = v, t, ln
-                    ga.cur_d.index_copy_(0, ri, up(v))
-                    wt.dirty[wc[rows][wc[rows] >= 0]] = False
-                    if ga.base_d is not None:
-                        bv, _, _ = wt.pack(wb[rows], ga.base.shape[1], times=False)
-                        ga.base[rows] = bv
-                        ga.base_d.index_copy_(0, ri, up(bv))
-                        wt.dirty[wb[rows][wb[rows] >= 0]] = False
+            changed = self._wt_changed and self._refresh_rows(ga, self._dirty_rows(ga), up)
             if changed or ga.hist_epoch != self._hist_epoch:
                 has_hist = np.isfinite(store.last_t[ga.rowmap]).reshape(S, M)
                 ga.missing = ~(has_hist & (ga.cur_len > 0).reshape(S, M))
@@ -1387,8 +1382,35 @@ class FastPath:
             return ga
         ident = self._jid(works)
         rowmap, ids, handles, end, xslots = self._static_cols(works, ident, key, M)
-        wc = self._extra(key, ident, "wcur", lambda: np.stack([w.wcur for w in works])).reshape(-1)
-        wb = self._extra(key, ident, "wbase", lambda: np.stack([w.wbase for w in works])).reshape(-1)
+        wc = self._extra(key, ident, "wcur", lambda sel: np.stack([w.wcur for w in _sub(works, sel)])).reshape(-1)
+        wb = self._extra(key, ident, "wbase", lambda sel: np.stack([w.wbase for w in _sub(works, sel)])).reshape(-1)
+        old = ga if ga is not None and ga.wcur is not None else None
+        m = ident.match_in(old.ident) if old is not None else None
+        if m is not None and m[2] * 2 >= S:
+            # fleet churn (a few jobs left or arrived): the kept rows are the
+            # previous arrays' -- on the host and on the device -- and only the
+            # new jobs' and the changed windows' rows are packed and uploaded
+            ix, hit, _ = m
+            newr = np.flatnonzero(np.repeat(~hit, M))
+            nb_old = 0 if old.base is None else old.base.shape[1]
+            fits = (wt.max_points(wc[newr]) <= old.cur.shape[1]
+                    and (wt.max_points(wb[newr]) <= nb_old if old.base is not None else wt.max_points(wb[newr]) == 0))
+            if fits:
+                r = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+                r_d = torch.from_numpy(r).to(dev)
+                ga = GroupArrays(ident, ids, old.cur[r], old.cur_t[r], old.cur_len[r], rowmap,
+                                 old.cur_d.index_select(0, r_d),
+                                 None if old.base_d is None else old.base_d.index_select(0, r_d),
+                                 up(rowmap), end, None, handles=handles, works=works)
+                ga.wcur, ga.wbase = wc, (wb if old.base is not None else None)
+                ga.base = None if old.base is None else old.base[r]
+                rows = self._dirty_rows(ga)
+                rows = np.union1d(rows, newr) if len(newr) else rows
+                self._refresh_rows(ga, rows, up)
+                has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
+                ga.missing = ~(has_hist & (ga.cur_len > 0).reshape(S, M))
+                ga.hist_epoch = self._hist_epoch
+                return self._install_arrays(ga, key, works, xslots)
         n = max(1, wt.max_points(wc))
         cur, cur_t, cur_len = wt.pack(wc, n)
         nb = wt.max_points(wb)
@@ -1399,6 +1421,9 @@ class FastPath:
         ga.wcur, ga.wbase, ga.base, ga.hist_epoch = wc, (wb if base is not None else None), base, self._hist_epoch
         wt.dirty[wc[wc >= 0]] = False
         wt.dirty[wb[wb >= 0]] = False
+        return self._install_arrays(ga, key, works, xslots)
+
+    def _install_arrays(self, ga: GroupArrays, key: tuple, works: list, xslots) -> GroupArrays:
         if xslots is not None:
             ga.export_slots = xslots
             ga.export_start = self.b.exporter.contiguous_start(xslots)
@@ -1407,6 +1432,32 @@ class FastPath:
         ga.key = key
         self._garr[key] = ga
         return ga
+
+    def _dirty_rows(self, ga: GroupArrays) -> np.ndarray:
+        """Rows of a table group whose current or baseline window gained samples."""
+        wt, wc, wb = self.wt, ga.wcur, ga.wbase
+        d = wt.dirty[np.maximum(wc, 0)] & (wc >= 0)
+        if wb is not None:
+            d |= wt.dirty[np.maximum(wb, 0)] & (wb >= 0)
+        return np.flatnonzero(d)
+
+    def _refresh_rows(self, ga: GroupArrays, rows: np.ndarray, up) -> bool:
+        """Re-pack ``rows`` of a table group from the window table (host and
+        device copies); their windows are clean afterwards."""
+        if not len(rows):
+            return False
+        wt, wc, wb = self.wt, ga.wcur, ga.wbase
+        ri = torch.from_numpy(rows).to(ga.cur_d.device)
+        v, t, ln = wt.pack(wc[rows], ga.cur.shape[1])
+        ga.cur[rows], ga.cur_t[rows], ga.cur_len[rows] = v, t, ln
+        ga.cur_d.index_copy_(0, ri, up(v))
+        wt.dirty[wc[rows][wc[rows] >= 0]] = False
+        if ga.base_d is not None:
+            bv, _, _ = wt.pack(wb[rows], ga.base.shape[1], times=False)
+            ga.base[rows] = bv
+            ga.base_d.index_copy_(0, ri, up(bv))
+            wt.dirty[wb[rows][wb[rows] >= 0]] = False
+        return True
 
     def _gcount_add(self, group: tuple, n: int) -> None:
         """Jobs per plan group among ``self.works`` (one group: no per-job grouping)."""
@@ -1435,43 +1486,73 @@ class FastPath:
         if memo is not None and memo[0] == ident:
             return memo[2]
         S = len(works)
-        ix = ident.index_in(memo[0]) if memo is not None else None
-        exp = self.b.exporter
+        m = ident.match_in(memo[0]) if memo is not None else None
         extra: dict = {}
-        if ix is not None:
+        if m is not None and m[2] * 2 >= S:
+            # the list lost, reordered or gained a few jobs (fleet churn): the
+            # previous list's columns fancy-indexed, only new jobs' built
+            ix, hit, nhit = m
             rowmap, ids, handles, end, xs = memo[2]
             r = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)
-            cols = (rowmap[r], ids[ix], None if handles is None else handles[ix], end[ix],
-                    None if xs is None else xs[r])
-            extra = {k: v[ix] for k, v in memo[3].items()}          # per-job extras ride along
+            rowmap, ids, end = rowmap[r], ids[ix], end[ix]
+            handles = None if handles is None else handles[ix]
+            xs = None if xs is None else xs[r]
+            # per-job extras ride along (rows of new jobs invalid until asked for)
+            extra = {k: (v[ix], vm[ix] & hit) for k, (v, vm) in memo[3].items()}
+            if nhit < S:
+                new = np.flatnonzero(~hit)
+                nrm, nids, nhd, nend, nxs = self._cols_of([works[j] for j in new], M)
+                rn = (new[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+                rowmap[rn], ids[new], end[new] = nrm, nids, nend
+                if handles is not None:
+                    if nhd is None:
+                        handles = None
+                    else:
+                        handles[new] = nhd
+                if xs is not None and nxs is not None:
+                    xs[rn] = nxs
+            cols = (rowmap, ids, handles, end, xs)
         else:
-            rowmap = np.concatenate([w.rows for w in works]).astype(np.int32)
-            ids = np.empty(S, object)
-            ids[:] = [w.doc.id for w in works]
-            hd = [w.handle for w in works]
-            handles = None if any(h is None for h in hd) else np.asarray(hd, np.int64)
-            xs = None
-            if exp is not None:
-                need = [w.plan for w in works if w.plan.export_slots is None]
-                if need:
-                    got = exp.bound_slots_many([(p.base_metrics, [p.namespace] * M, [p.app] * M) for p in need])
-                    for p, sl in zip(need, got):
-                        p.export_slots = sl
-                xs = np.concatenate([w.plan.export_slots for w in works])
-            cols = (rowmap, ids, handles, np.fromiter((w.end_ts for w in works), np.float64, S), xs)
+            cols = self._cols_of(works, M)
         self._gstat[key] = (ident, None, cols, extra)
         return cols
 
+    def _cols_of(self, works: list[FastWork], M: int):
+        S = len(works)
+        exp = self.b.exporter
+        rowmap = np.concatenate([w.rows for w in works]).astype(np.int32) if S else np.zeros(0, np.int32)
+        ids = np.empty(S, object)
+        ids[:] = [w.doc.id for w in works]
+        hd = [w.handle for w in works]
+        handles = None if any(h is None for h in hd) else np.asarray(hd, np.int64)
+        xs = None
+        if exp is not None:
+            need = [w.plan for w in works if w.plan.export_slots is None]
+            if need:
+                got = exp.bound_slots_many([(p.base_metrics, [p.namespace] * M, [p.app] * M) for p in need])
+                for p, sl in zip(need, got):
+                    p.export_slots = sl
+            xs = np.concatenate([w.plan.export_slots for w in works]) if S else np.zeros((0, 3), np.int64)
+        return rowmap, ids, handles, np.fromiter((w.end_ts for w in works), np.float64, S), xs
+
     def _extra(self, key: tuple, ident: "JobIds", name: str, make):
-        """A per-job array of a group's static memo (first axis = job), built
-        by ``make()`` when the job list gained jobs; fancy-indexed with the
-        static columns under churn."""
+        """A per-job array of a group's static memo (first axis = job).
+        ``make(sel)`` builds the rows of the jobs at positions ``sel`` (None:
+        every job); kept per group, fancy-indexed with the static columns
+        under churn, and only a churned list's new jobs are built."""
         memo = self._gstat.get(key)
         if memo is None or memo[0] != ident:
-            return make()
-        v = memo[3].get(name)
-        if v is None:
-            v = memo[3][name] = make()
+            return make(None)
+        got = memo[3].get(name)
+        if got is None:
+            v = make(None)
+            memo[3][name] = (v, np.ones(len(v), bool))
+            return v
+        v, valid = got
+        if not valid.all():
+            sel = np.flatnonzero(~valid)
+            v[sel] = make(sel)
+            valid[:] = True
         return v
 
     def score_group(self, works: list[FastWork], now: float, key: tuple | None = None) -> dict:
@@ -2024,13 +2105,14 @@ class FastPath:
         tmpl = works[0].plan.tmpl
         dev = self.b.device
 
-        def hpa_slots():
-            ids = [w.doc.id for w in works]
-            for w in works:
+        def hpa_slots(sel):
+            ws = _sub(works, sel)
+            ids = [w.doc.id for w in ws]
+            for w in ws:
                 self.hpa.owner[w.doc.id] = (w.plan.namespace, w.doc.app_name)
             return self.hpa.slots(ids).cpu().numpy()
         key = ga.key if ga is not None else None
-        sl_np = self._extra(key, ga.ident, "hpa", hpa_slots) if key is not None else hpa_slots()
+        sl_np = self._extra(key, ga.ident, "hpa", hpa_slots) if key is not None else hpa_slots(None)
         sl = torch.as_tensor(sl_np, device=dev)
         sub = self.hpa.gather(sl)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -2043,14 +2125,15 @@ class FastPath:
         created = rfc3339(datetime.fromtimestamp(now, timezone.utc))
         exp = self.b.exporter
         if exp is not None:
-            def xhpa():
-                hs = []
-                for w in works:
-                    if w.plan.hpa_slots is None:
-                        w.plan.hpa_slots = exp.hpa_slots([w.doc.namespace], [w.doc.app_name])[0]
-                    hs.append(w.plan.hpa_slots)
-                return np.stack(hs)
-            hs = self._extra(key, ga.ident, "xhpa", xhpa) if key is not None else xhpa()
+            def xhpa(sel):
+                ws = _sub(works, sel)
+                need = [w for w in ws if w.plan.hpa_slots is None]
+                if need:
+                    got = exp.hpa_slots([w.doc.namespace for w in need], [w.doc.app_name for w in need])
+                    for w, h in zip(need, got):
+                        w.plan.hpa_slots = h
+                return np.stack([w.plan.hpa_slots for w in ws])
+            hs = self._extra(key, ga.ident, "xhpa", xhpa) if key is not None else xhpa(None)
             exp.set_hpa_scores(hs, sc.astype(np.float64))
         al = works[0].plan.aliases
         dj = np.flatnonzero(due)
@@ -2292,6 +2375,11 @@ def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> 
             st.max_len = max(st.max_len, int(st.nlen[rows].max()) if len(rows) else 0)
         n_rows += len(rows)
     return n_rows
+
+
+def _sub(works: list, sel) -> list:
+    """``works`` at positions ``sel`` (None: all of them)."""
+    return works if sel is None else [works[j] for j in sel]
 
 
 def _merge_series(ss) -> tuple[np.ndarray, np.ndarray]:
