@@ -286,6 +286,12 @@ def config3e2e(args):
             mm = E2E[ref][2]
             classes.append((st_, al_, [a + sfx for a in (E2E[ref][4] * 2)[:mm]], j0, n_))
             j0 += n_
+        if args.mixed_class >= 0:
+            # one class of the mixed fleet alone, all S jobs, same poll /
+            # windows / churn / source: the single-strategy cycle the mixed
+            # cycle is weighed against
+            st_, al_, al3, _, _ = classes[args.mixed_class]
+            classes = [(st_, al_, al3, 0, S)]
     else:
         M0 = args.metrics if args.metrics_set else m_default
         classes = [(strategy, algo, (names * 2)[:M0], 0, S)]
@@ -635,6 +641,7 @@ def config3e2e(args):
              "classes": [{"strategy": st_, "model": al_, "jobs": n_, "metrics": len(als)}
                          for st_, al_, als, _, n_ in classes],
              "churn": dict(new_canaries=churn["new"], hpa_resubmissions=churn["resub"]) if kind == "mixed" else None,
+             "mixed_class": args.mixed_class if kind == "mixed" and args.mixed_class >= 0 else None,
              "hpa_log_interval_s": args.hpa_log_interval if any(c[0] == "hpa" for c in classes) else None,
              "band_threshold_min": args.band_threshold if sliding_any else None,
              "pods_per_side": P if any(c[0] == "canary" for c in classes) else 0, "store": args.store,
@@ -750,6 +757,8 @@ def config5(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", required=True, choices=["1", "2", "2e2e", "3", "3e2e", "4", "4e2e", "5", "mixed"])
+    ap.add_argument("--mixed-class", type=int, default=-1, help="--config mixed: run only this class (0 canary, "
+                    "1 continuous, 2 HPA) with all --services jobs")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)

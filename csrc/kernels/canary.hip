@@ -98,7 +98,7 @@ template <int K>
 __device__ __forceinline__ void avg_ranks(const float (&v)[K], int n, int (&rank2)[K], bool (&is_end)[K],
                                           int& tie_term) {
   // rank2 = 2 x (1-based average rank) = start + end + 2: exact integers, so
-  // rank sums and the tie term sum(t^3 - t) (<= 512^3) need no doubles.
+  // rank sums and the tie term sum(t^3 - t) (<= 1024^3 < 2^31) need no doubles.
   const int lane = lane_id();
   int start_idx[K];
   int carry = 0;
@@ -745,6 +745,7 @@ FM_API int fm_pairwise_suff_v(const float* cur, int64_t ld_c, int n_cur, const f
   else if (n <= 128) FM_PW(2);
   else if (n <= 256) FM_PW(4);
   else if (n <= 512) FM_PW(8);
+  else if (n <= 1024) FM_PW(16);
   else return (int)hipErrorInvalidValue;
 #undef FM_PW
   FM_LAUNCH_CHECK();
@@ -776,6 +777,7 @@ FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const fl
   else if (n <= 128) FM_PW(2);
   else if (n <= 256) FM_PW(4);
   else if (n <= 512) FM_PW(8);
+  else if (n <= 1024) FM_PW(16);
   else return (int)hipErrorInvalidValue;
 #undef FM_PW
   FM_LAUNCH_CHECK();

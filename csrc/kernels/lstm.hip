@@ -1,3 +1,4 @@
+// fm-hipcc-flags: -fno-slp-vectorize
 // K6: LSTM forecaster cell on bf16 MFMA (v_mfma_f32_32x32x16_bf16, fp32
 // accumulate).  Reference: the brain's deep model is an LSTM on Keras/MXNet
 // (docs/guides/design.md:81-85, foremast-brain/faq.md:10), used for HPA /
@@ -15,6 +16,7 @@
 // and only h (bf16) crosses LDS, read back as the next step's B operand with
 // ds_read_b128 from a [batch][H + 8] image (row pad -> conflict-free).
 #include "fm_common.h"
+#include "fm_lstm_cell.h"
 
 #include <type_traits>
 
@@ -33,44 +35,9 @@ __device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
   const bf16x2 v = {(__bf16)lo, (__bf16)hi};
   return __builtin_bit_cast(unsigned, v);
 }
-// Gate nonlinearities on the transcendental unit, 2 transcendentals each:
-//   sigm(x) = 1 / (1 + 2^(-x log2 e))          v_mul, v_exp, v_add, v_rcp
-//   tanh(x) = 2 sigm(2x) - 1                    (+1 fma; saturates correctly
-//                                                 through exp -> inf/0)
-// A correctly rounded '/' would expand to a ~10-instruction
-// div_scale/div_fmas/div_fixup sequence; the cell update does 5 per unit per step.
-constexpr float kLog2e = 1.4426950408889634f;
-__device__ __forceinline__ float sigm(float x) {
-  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * -kLog2e));
-}
-__device__ __forceinline__ float tanh_f(float x) {
-  return 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * (-2.f * kLog2e))) - 1.f;
-}
-
-// Fused-fraction cell (CELL = 1): with E = e^{-x} terms,
-//   sigm(a) = 1/(1+E_a),  tanh(b) = (1-E_2b)/(1+E_2b)
-//   c' = f c + i g = [c (1+E_i)(1+E_g) + (1-E_g)(1+E_f)] / [(1+E_f)(1+E_i)(1+E_g)]
-//   h  = o tanh(c') = (1-E_c) / ((1+E_o)(1+E_c))
-// = 5 v_exp + 2 v_rcp per unit per step instead of 5 + 5.  The exp2
-// arguments are clamped (v_med3) to |.| <= 29 so the triple product stays
-// finite (<= 2^87); sigm / tanh are saturated to fp32 1 well inside that.
-constexpr float kExpClamp = 29.f;
-__device__ __forceinline__ float exp2_clamped(float x) {
-  return __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(x, -kExpClamp, kExpClamp));
-}
-__device__ __forceinline__ void cell_fused(float ai, float af, float ag, float ao, float& c, float& h) {
-  const float pi = 1.f + exp2_clamped(ai * -kLog2e);
-  const float pf = 1.f + exp2_clamped(af * -kLog2e);
-  const float eg = exp2_clamped(ag * (-2.f * kLog2e));
-  const float pg = 1.f + eg;
-  const float pig = pi * pg;
-  const float cn = (c * pig + (1.f - eg) * pf) * __builtin_amdgcn_rcpf(pf * pig);
-  c = cn;
-  const float po = 1.f + exp2_clamped(ao * -kLog2e);
-  const float ec = exp2_clamped(cn * (-2.f * kLog2e));
-  h = (1.f - ec) * __builtin_amdgcn_rcpf(po * (1.f + ec));
-}
-
+// The cell update (fm_lstm_cell.h): the packed weights carry the gate
+// scales (i, f, o rows by -log2 e, g rows by -2 log2 e) and c is kept scaled
+// (cs = -2 log2(e) c) -- 14 VALU + 8 transcendental issues per unit-step.
 union Frag {
   bf16x8 v;
   unsigned short s[8];
@@ -116,7 +83,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
       for (int j = 0; j < 4; ++j) {
         const int u = 16 * w + 8 * rt + 4 * h + j;
         const int64_t bb = b0 + 32 * ct + col;
-        c[rt][ct][j] = (c0 != nullptr && bb < B) ? c0[bb * H + u] : 0.f;
+        c[rt][ct][j] = (c0 != nullptr && bb < B) ? kLstmK * c0[bb * H + u] : 0.f;
         const float hv = (h0 != nullptr && bb < B) ? h0[bb * H + u] : 0.f;
         hbuf[0][(32 * ct + col) * HP + u] = f2bf(hv);
       }
@@ -183,18 +150,11 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
         float hv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (CELL == 1) {
-            cell_fused(acc[rt][ct][j], acc[rt][ct][4 + j], acc[rt][ct][8 + j], acc[rt][ct][12 + j], c[rt][ct][j],
-                       hv[j]);
-          } else {
-            const float ig = sigm(acc[rt][ct][j]);
-            const float fg = sigm(acc[rt][ct][4 + j]);
-            const float gg = tanh_f(acc[rt][ct][8 + j]);
-            const float og = sigm(acc[rt][ct][12 + j]);
-            const float cc = fg * c[rt][ct][j] + ig * gg;
-            c[rt][ct][j] = cc;
-            hv[j] = og * tanh_f(cc);
-          }
+          if (CELL == 1)
+            lstm_cell(acc[rt][ct][j], acc[rt][ct][4 + j], acc[rt][ct][8 + j], acc[rt][ct][12 + j], c[rt][ct][j], hv[j]);
+          else
+            lstm_cell_separate(acc[rt][ct][j], acc[rt][ct][4 + j], acc[rt][ct][8 + j], acc[rt][ct][12 + j],
+                               c[rt][ct][j], hv[j]);
         }
         const int u0 = 16 * w + 8 * rt + 4 * h;
         const int64_t bb = b0 + 32 * ct + col;
@@ -205,7 +165,8 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
           if (bb < B) {
             *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
             *reinterpret_cast<float4*>(&c_out[bb * H + u0]) =
-                make_float4(c[rt][ct][0], c[rt][ct][1], c[rt][ct][2], c[rt][ct][3]);
+                make_float4(c[rt][ct][0] * kLstmInvK, c[rt][ct][1] * kLstmInvK, c[rt][ct][2] * kLstmInvK,
+                            c[rt][ct][3] * kLstmInvK);
           }
         } else {
           *reinterpret_cast<uint2*>(&hbuf[nxt][(32 * ct + col) * HP + u0]) = pk;
@@ -266,7 +227,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __res
       for (int j = 0; j < 4; ++j) {
         const int u = 16 * w + 8 * rt + 4 * h + j;
         const int64_t bb = b0 + 32 * ct + col;
-        c[ct][rt][j] = (c0 != nullptr && bb < B) ? c0[bb * H + u] : 0.f;
+        c[ct][rt][j] = (c0 != nullptr && bb < B) ? kLstmK * c0[bb * H + u] : 0.f;
         const float hv = (h0 != nullptr && bb < B) ? h0[bb * H + u] : 0.f;
         hbuf[(32 * ct + col) * HP + u] = f2bf(hv);
       }
@@ -309,8 +270,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __res
     for (int rt = 0; rt < 2; ++rt) {
       float hv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cell_fused(acc[rt][j], acc[rt][4 + j], acc[rt][8 + j], acc[rt][12 + j], c[ct][rt][j],
-                                             hv[j]);
+      for (int j = 0; j < 4; ++j) lstm_cell(acc[rt][j], acc[rt][4 + j], acc[rt][8 + j], acc[rt][12 + j], c[ct][rt][j], hv[j]);
       const int u0 = 16 * w + 8 * rt + 4 * h;
       uint2 pk;
       pk.x = pack_bf2(hv[0], hv[1]);
@@ -319,7 +279,8 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __res
         if (inb[ct]) {
           *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
           *reinterpret_cast<float4*>(&c_out[bb * H + u0]) =
-              make_float4(c[ct][rt][0], c[ct][rt][1], c[ct][rt][2], c[ct][rt][3]);
+              make_float4(c[ct][rt][0] * kLstmInvK, c[ct][rt][1] * kLstmInvK, c[ct][rt][2] * kLstmInvK,
+                          c[ct][rt][3] * kLstmInvK);
         }
       } else {
         *reinterpret_cast<uint2*>(&hbuf[(32 * ct + col) * HP + u0]) = pk;
@@ -417,8 +378,8 @@ FM_API int fm_lstm_features(const float* hist, int64_t ld, int T, int64_t R, int
 }
 
 // nct: batch column tiles per workgroup (1 or 2); 0 = tuned default.
-// cell: 0 = separate sigm/tanh (10 transcendentals per unit-step), 1 = fused
-// fractions (7), 2 = fused fractions in the column-tile pipelined kernel
+// cell: 0 = separate sigm/tanh (10 transcendentals per unit-step), 1 = the
+// fm_lstm_cell.h cell, 2 = that cell in the column-tile pipelined kernel
 // (nct ignored); -1 = default.
 FM_API int fm_lstm_forward_v(const void* xa, int64_t B, int L, int H, const void* Wpack, const float* h0,
                              const float* c0, float* h_out, float* c_out, unsigned short* hseq, int nct, int cell,

@@ -1,3 +1,4 @@
+// fm-hipcc-flags: -fno-slp-vectorize
 // K6 at full spec: H up to 256, 1-2 stacked layers, multivariate input, on
 // bf16 MFMA (v_mfma_f32_32x32x16_bf16, fp32 accumulate).  Reference intent:
 // the brain's LSTM forecasts "3+ metrics" jointly (docs/guides/design.md:81-85)
@@ -22,6 +23,7 @@
 //   * the A fragments of each k-step are loaded (16 B per lane, L2 hits) one
 //     k-step ahead of the MFMAs that use them.
 #include "fm_common.h"
+#include "fm_lstm_cell.h"
 
 #include <type_traits>
 
@@ -32,9 +34,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kExpClamp = 29.f;
-
 __device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   const bf16x2 v = {(__bf16)lo, (__bf16)hi};
@@ -44,21 +43,9 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   const __bf16 b = (__bf16)f;
   return __builtin_bit_cast(unsigned short, b);
 }
-__device__ __forceinline__ float exp2_clamped(float x) {
-  return __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(x, -kExpClamp, kExpClamp));
-}
-// fused-fraction cell (same algebra as lstm.hip: 5 exp + 2 rcp per unit-step)
-__device__ __forceinline__ void cell(float ai, float af, float ag, float ao, float& c, float& h) {
-  const float pi = 1.f + exp2_clamped(ai * -kLog2e);
-  const float pf = 1.f + exp2_clamped(af * -kLog2e);
-  const float eg = exp2_clamped(ag * (-2.f * kLog2e));
-  const float pg = 1.f + eg;
-  const float pig = pi * pg;
-  const float cn = (c * pig + (1.f - eg) * pf) * __builtin_amdgcn_rcpf(pf * pig);
-  c = cn;
-  const float po = 1.f + exp2_clamped(ao * -kLog2e);
-  const float ec = exp2_clamped(cn * (-2.f * kLog2e));
-  h = (1.f - ec) * __builtin_amdgcn_rcpf(po * (1.f + ec));
+// the cell update: fm_lstm_cell.h (pre-scaled gates, scaled c)
+__device__ __forceinline__ void cell(float ai, float af, float ag, float ao, float& cs, float& h) {
+  lstm_cell(ai, af, ag, ao, cs, h);
 }
 
 union Frag {
@@ -174,7 +161,8 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack_kernel(
           const int64_t bb = b0 + 32 * ct + col;
           *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
           *reinterpret_cast<float4*>(&c_out[bb * H + u0]) =
-              make_float4(c[rt][ct][0], c[rt][ct][1], c[rt][ct][2], c[rt][ct][3]);
+              make_float4(c[rt][ct][0] * kLstmInvK, c[rt][ct][1] * kLstmInvK, c[rt][ct][2] * kLstmInvK,
+                          c[rt][ct][3] * kLstmInvK);
         }
       }
   };
@@ -225,7 +213,7 @@ static int launch_stack(const void* xa, int64_t B, int L, const void* W0, const 
 
 // ---------------------------------------------------------------------------
 // Two layers, software-pipelined across the layer boundary so that the cell
-// updates (VALU: 5 exp + 2 rcp per unit) issue beside MFMAs instead of
+// updates (VALU: the fm_lstm_cell.h update) issue beside MFMAs instead of
 // between barriers.  Layer 0 at step t+1 needs only h0_t, and layer 1's
 // k-steps over h1_t do not need h0_{t+1}, so one step is two barrier-separated
 // phases:
@@ -384,7 +372,8 @@ __global__ __launch_bounds__(64 * H / (8 * RT)) void lstm_stack2_pipe_kernel(
       *reinterpret_cast<uint2*>(&hw[u0]) = pk;
       if (out && inb) {
         *reinterpret_cast<float4*>(&h_out[bb * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-        *reinterpret_cast<float4*>(&c_out[bb * H + u0]) = make_float4(c[rt][0], c[rt][1], c[rt][2], c[rt][3]);
+        *reinterpret_cast<float4*>(&c_out[bb * H + u0]) =
+            make_float4(c[rt][0] * kLstmInvK, c[rt][1] * kLstmInvK, c[rt][2] * kLstmInvK, c[rt][3] * kLstmInvK);
       }
     }
   };
@@ -553,7 +542,8 @@ __global__ __launch_bounds__(512) void lstm_stack2_rs_kernel(
         const float(&c)[RT][2][4] = c1;
         *reinterpret_cast<float4*>(&h_out[bbo[ct] * H + u0]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
         *reinterpret_cast<float4*>(&c_out[bbo[ct] * H + u0]) =
-            make_float4(c[rt][ct][0], c[rt][ct][1], c[rt][ct][2], c[rt][ct][3]);
+            make_float4(c[rt][ct][0] * kLstmInvK, c[rt][ct][1] * kLstmInvK, c[rt][ct][2] * kLstmInvK,
+                        c[rt][ct][3] * kLstmInvK);
       }
     }
   };

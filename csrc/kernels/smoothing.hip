@@ -872,3 +872,242 @@ FM_API int fm_band_decide(const float* cur, int64_t ld_c, int n, const float* ce
   FM_LAUNCH_CHECK();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// The steady sliding cycle of a forecasting group in ONE launch (VERDICT r4
+// #2): advance the cached ES/Holt-Winters models over the samples the window
+// gained, judge every current point against the forecast band at its own
+// horizon, reduce the verdicts per service and stream-compact the anomalous
+// points.  Before this the cycle was gather_cols (materialise the tail) ->
+// es_update -> ~40 ATen glue kernels (horizon gather, validity masks, stats
+// stack, service reduce, counter reset, compaction).
+//
+// One workgroup per service, one wave per metric row (M waves):
+//   * the row's k new samples are read straight from the resident history
+//     grid (row rm[r], dense column c -> grid column c - (shift[r] - dk),
+//     valid below lim[r] + dk: the shift-only slide of a polled fleet is the
+//     scalar dk, no per-row rewrite) into LDS; lane 0 advances the model in
+//     the cache slab (params/state/season/sse/nobs of slot slots[r]);
+//   * the forecast at a point's horizon h is lvl + h tr (+|x) season[(ph + h
+//     - 1) % m], read per lane -- the season entries lane 0 just rewrote come
+//     from LDS (a wave's lanes do not see one lane's global stores ordered);
+//   * band / flags / count / score exactly as band_decide_kernel + zoo.band
+//     (rows without history, valid bit 0, flag nothing);
+//   * stats[r] = (nan, nan, upper, lower) at the row's last finite point;
+//   * wave 0 reduces the service (service_reduce_kernel semantics) from LDS;
+//   * anomalous points append (row, point), value through one atomic per row
+//     to ctr[par]; block 0 zeroes ctr[par ^ 1] for the next cycle.
+// Host outputs land in one buffer (hostv: packed [S,4] | stats [R,4] | count
+// [R] (int) | dead [R] (int) ) for a single device->host copy.
+// ---------------------------------------------------------------------------
+constexpr int kStepKMax = 64;      // new samples per row per cycle handled in-kernel
+constexpr int kStepMMax = 16;      // metrics per service (waves per workgroup)
+
+template <int KIND>
+__global__ __launch_bounds__(1024) void es_band_step_kernel(
+    const float* __restrict__ buf, int64_t ld, const int* __restrict__ rm, const int* __restrict__ shift,
+    const int* __restrict__ lim, int dk, int T, int kmax, const int* __restrict__ t_new,
+    const int64_t* __restrict__ slots, const float* __restrict__ params, int m, float* __restrict__ season,
+    float* __restrict__ sse, float* __restrict__ state, int* __restrict__ nobs,
+    const float* __restrict__ cur, int64_t ld_c, int n, const int64_t* __restrict__ hor, int H, int64_t S, int M,
+    const float* __restrict__ thr, const int* __restrict__ bound, const float* __restrict__ minlb,
+    const int8_t* __restrict__ diff, float pair_factor, const int* __restrict__ valid,
+    const int64_t* __restrict__ lastk, float* __restrict__ upper, float* __restrict__ lower,
+    float* __restrict__ sigma_out, float* __restrict__ fc, int Hf, float* __restrict__ hostv, int cap,
+    int* __restrict__ ctr, int par, int* __restrict__ out_idx, float* __restrict__ out_val) {
+  __shared__ float xs[kStepMMax][kStepKMax];
+  __shared__ float su[kStepMMax][kStepKMax];
+  __shared__ int s_cnt[kStepMMax];
+  __shared__ float s_score[kStepMMax];
+  __shared__ int s_valid[kStepMMax];
+  const int64_t s = blockIdx.x;
+  const int mi = wave_id();
+  const int lane = lane_id();
+  const int64_t R = S * M;
+  const int64_t row = s * M + mi;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctr[par ^ 1] = 0;
+  const int64_t sl = slots[row];
+  int k0 = t_new[row];
+  k0 = k0 < 0 ? 0 : (k0 > kmax ? kmax : k0);
+  // the tail columns [T - kmax, T) of the row, from the grid
+  {
+    const int64_t g = rm[row];
+    const int off = dk - shift[row];
+    const int lm = lim[row] + dk;
+    if (lane < kmax) {
+      const int c = T - kmax + lane + off;
+      xs[mi][lane] = (c >= 0 && c < lm) ? buf[g * ld + c] : __builtin_nanf("");
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  float lvl = 0.f, tr = 0.f, sig = 0.f;
+  int ph = 0;
+  const int k = kmax - k0;
+  if (lane == 0) {
+    EsModel<KIND> md{params[sl * 3 + 0], params[sl * 3 + 1], params[sl * 3 + 2], state[sl * 3 + 0],
+                     state[sl * 3 + 1]};
+    ph = KIND >= 2 ? (int)state[sl * 3 + 2] : 0;
+    const int ph0 = ph;
+    double err2 = sse[sl];
+    int nn = nobs[sl];
+    float* srow = KIND >= 2 ? season + sl * m : season;
+    es_run<KIND, false>(md, &xs[mi][0], k0, kmax, k0, m, srow, 1, 0, ph, err2, nn);
+    sse[sl] = (float)err2;
+    state[sl * 3 + 0] = md.lvl;
+    state[sl * 3 + 1] = md.tr;
+    state[sl * 3 + 2] = (float)ph;
+    nobs[sl] = nn;
+    lvl = md.lvl;
+    tr = md.tr;
+    sig = nn > 1 ? sqrtf((float)err2 / (float)(nn - 1)) : 0.f;
+    sigma_out[row] = sig;
+    if (KIND >= 2) {
+      int p = ph0;
+      for (int j = 0; j < k; ++j) {     // this thread's own stores: program order
+        su[mi][j] = srow[p];
+        if (++p == m) p = 0;
+      }
+    }
+    reinterpret_cast<int*>(hostv)[S * 4 + R * 4 + R + row] = (isfinite(lvl) && isfinite(tr)) ? 0 : 1;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  lvl = __shfl(lvl, 0);
+  tr = __shfl(tr, 0);
+  sig = __shfl(sig, 0);
+  ph = __shfl(ph, 0);
+  const int ph_old = KIND >= 2 ? ((ph - k) % m + m) % m : 0;
+  const float* srow = KIND >= 2 ? season + sl * m : season;
+  auto fcast = [&](int h) -> float {
+    float f = lvl + (KIND >= 1 ? (float)h * tr : 0.f);
+    if (KIND >= 2) {
+      const int idx = (ph + h - 1) % m;
+      int d = idx - ph_old;
+      d = d < 0 ? d + m : d;
+      const float sv = d < k ? su[mi][d] : srow[idx];
+      f = KIND == 3 ? f * sv : f + sv;
+    }
+    return f;
+  };
+  if (fc != nullptr) {
+    for (int h = 1 + lane; h <= Hf; h += 64) fc[row * Hf + (h - 1)] = fcast(h);
+  }
+  // band decision (band_decide_kernel + zoo.band's history gate)
+  const int mm = (int)(row % M);
+  float th = thr[mm];
+  if (diff != nullptr && diff[row]) th *= pair_factor;
+  const int bd = bound[mm];
+  const float inv = sig > 0.f ? 1.f / sig : 0.f;
+  const int vld = valid[row];
+  const bool has = (vld & 1) != 0;
+  const int lk = (int)lastk[row];
+  int cnt = 0;
+  float best = 0.f;
+  unsigned long long words[4] = {0ull, 0ull, 0ull, 0ull};
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    bool f = false;
+    if (i < n) {
+      int h = (int)hor[row * n + i];
+      h = h < 1 ? 1 : (h > H ? H : h);
+      const float c = fcast(h);
+      const float up = c + th * sig;
+      float lo = c - th * sig;
+      if (lo < minlb[mm]) lo = minlb[mm];
+      upper[row * n + i] = up;
+      lower[row * n + i] = lo;
+      if (i == lk) {
+        float* st = hostv + S * 4 + row * 4;
+        st[0] = __builtin_nanf("");
+        st[1] = __builtin_nanf("");
+        st[2] = up;
+        st[3] = lo;
+      }
+      const float x = cur[row * ld_c + i];
+      if (isfinite(x) && isfinite(c)) {
+        const bool hi = (bd & 1) && x > up;
+        const bool lw = (bd & 2) && x < lo;
+        f = hi || lw;
+        if (f) {
+          ++cnt;
+          const float z = sig > 0.f ? (hi ? x - up : lo - x) * inv : 1e30f;
+          best = z > best ? z : best;
+        }
+      }
+    }
+    const unsigned long long bal = __ballot(f && has);
+    if (i0 / 64 < 4) words[i0 / 64] = bal;
+  }
+  cnt = has ? wave_sum(cnt) : 0;
+  best = wave_max(best);
+  // compaction: one atomic per row with anomalies
+  if (cnt > 0) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&ctr[par], cnt);
+    base = __shfl(base, 0);
+    int written = 0;
+    for (int w = 0; w < 4 && w * 64 < n; ++w) {
+      const unsigned long long word = words[w];
+      if (!word) continue;
+      const unsigned long long below = lane == 0 ? 0ull : (word & ((1ull << lane) - 1ull));
+      const int slot = base + written + __popcll(below);
+      if (((word >> lane) & 1ull) && slot < cap) {
+        out_idx[2 * slot + 0] = (int)row;
+        out_idx[2 * slot + 1] = w * 64 + lane;
+        out_val[slot] = cur[row * ld_c + w * 64 + lane];
+      }
+      written += __popcll(word);
+    }
+  }
+  if (lane == 0) {
+    reinterpret_cast<int*>(hostv)[S * 4 + R * 4 + row] = cnt;
+    s_cnt[mi] = cnt;
+    s_score[mi] = best;
+    s_valid[mi] = vld;
+  }
+  __syncthreads();
+  if (mi == 0 && lane == 0) {    // service_reduce_kernel semantics
+    int tot = 0, mask = 0;
+    bool unknown = false;
+    float sb = 0.f;
+    for (int j = 0; j < M; ++j) {
+      tot += s_cnt[j];
+      if (s_cnt[j] > 0) mask |= 1 << j;
+      if ((s_valid[j] & 3) != 3) unknown = true;
+      sb = s_score[j] > sb ? s_score[j] : sb;
+    }
+    float* pk = hostv + s * 4;
+    pk[0] = (float)(tot > 0 ? 1 : (unknown ? 2 : 0));
+    pk[1] = sb;
+    pk[2] = (float)mask;
+    pk[3] = (float)tot;
+  }
+}
+
+FM_API int fm_es_band_step(const float* buf, int64_t ld, const int* rm, const int* shift, const int* lim, int dk, int T,
+                           int kmax, const int* t_new, const int64_t* slots, const float* params, int m, int kind,
+                           float* season, float* sse, float* state, int* nobs, const float* cur, int64_t ld_c, int n,
+                           const int64_t* hor, int H, int64_t S, int M, const float* thr, const int* bound,
+                           const float* minlb, const int8_t* diff, float pair_factor, const int* valid,
+                           const int64_t* lastk, float* upper, float* lower, float* sigma, float* fc, int Hf,
+                           float* hostv, int cap, int* ctr, int par, int* out_idx, float* out_val,
+                           hipStream_t stream) {
+  if (S <= 0) return 0;
+  if (kind < 0 || kind > 3 || M < 1 || M > kStepMMax || kmax < 1 || kmax > kStepKMax || kmax > T || n < 1 ||
+      n > 256 || H < 1 || (kind >= 2 && m < 2) || (fc != nullptr && Hf < 1) || (par != 0 && par != 1))
+    return (int)hipErrorInvalidValue;
+  if (kind < 2) m = 1;
+  const dim3 grid((unsigned)S), block((unsigned)(64 * M));
+#define FM_EBS(KK)                                                                                               \
+  hipLaunchKernelGGL(es_band_step_kernel<KK>, grid, block, 0, stream, buf, ld, rm, shift, lim, dk, T, kmax, t_new, \
+                     slots, params, m, season, sse, state, nobs, cur, ld_c, n, hor, H, S, M, thr, bound, minlb, diff, \
+                     pair_factor, valid, lastk, upper, lower, sigma, fc, Hf, hostv, cap, ctr, par, out_idx, out_val)
+  if (kind == 0) FM_EBS(0);
+  else if (kind == 1) FM_EBS(1);
+  else if (kind == 2) FM_EBS(2);
+  else FM_EBS(3);
+#undef FM_EBS
+  FM_LAUNCH_CHECK();
+  return 0;
+}

@@ -26,7 +26,7 @@ Per cycle (judgement sequence, .gitbook/assets/foremastjudgementsequencediagram.
    bulk update.
 
 Wide pairwise windows never fail a cycle: <= 256 points take the role-split
-kernel, <= 512 the separate pairwise kernel, wider ones the fp64 CPU oracle;
+kernel, <= 1024 the separate pairwise kernel, wider ones the fp64 CPU oracle;
 a group whose scoring raises is re-scored job by job and a job that still
 fails is closed ``completed_unknown`` with the error as reason.
 """
@@ -59,6 +59,9 @@ log = logging.getLogger("foremast.brain.fast")
 
 MAX_M = 16
 _MERGED = __import__("os").environ.get("FOREMAST_SLIDING_MERGED", "1") not in ("0", "false")
+# the steady cycle of a single-model ES / Holt-Winters group as one kernel
+# (FastPath._score_fused); FOREMAST_FUSED_STEP=0 keeps the op-by-op path
+_FUSED_STEP = __import__("os").environ.get("FOREMAST_FUSED_STEP", "1") not in ("0", "false")
 
 
 @dataclass
@@ -176,6 +179,16 @@ class ModelSub:
     hor: torch.Tensor | None                   # int64 [rows, n] horizon of every current point
     H: int
     M: int
+    dk: int = 0                                # slide since shift/lim were built: shift - dk, lim + dk
+
+    def shift_lim(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """The row alignment after the slides folded into ``dk``."""
+        if not self.dk:
+            return self.shift, self.lim
+        eff = getattr(self, "_eff", None)
+        if eff is None or eff[0] != self.dk:
+            eff = self._eff = (self.dk, self.shift - self.dk, self.lim + self.dk)
+        return eff[1], eff[2]
 
 
 @dataclass
@@ -454,6 +467,10 @@ class FastPath:
         self.cycle = 0
         self.max_idle_cycles = 64
         self._cmp = {}            # device compaction buffers per capacity
+        self._fused_cmp = {}      # the fused steady-cycle kernel's compaction buffers + counters
+        self._fused_par = 0       # which of the two counters the next fused launch appends to
+        self._es_plan = None      # (keys, cache lookup) a declined fused cycle hands to es_forecast
+        self.fused_steps = 0
         self._col: dict = {}      # column-wise fetched windows of sliding groups (consumed by _arrays)
         self._ring = None         # merged sliding mode: host ring of the newest grid columns
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
@@ -1778,7 +1795,7 @@ class FastPath:
                                                + np.asarray(s.ms)[None, :]).reshape(-1)
             pick = (lambda a: a) if rows is None else (lambda a: a[rows])  # noqa: E731
             subs.append(replace(
-                s, shift=s.shift - k, lim=s.lim + k, t_last=pick(lt),
+                s, dk=s.dk + k, t_last=pick(lt),
                 valid=up(pick(valid).astype(np.int32)) if vchg else s.valid))
         lk = md.lastk if lastk is lastk_prev or np.array_equal(lastk, lastk_prev) else up(lastk.astype(np.int64))
         nd = ModelArrays(stamp, subs, lk)
@@ -1810,6 +1827,11 @@ class FastPath:
             _, _, diff = C.pairwise_tests(ga.cur_d, ga.base_d, pcfg)
         NW = max(1, (n + 63) // 64)
         single = len(md.subs) == 1
+        hpa_algo = zoo.canonical(cfg.hpa_forecast_algorithm) if (p0.hpa and cfg.hpa_forecast_algorithm) else None
+        if single and dev.type == "cuda" and _FUSED_STEP:
+            got = self._score_fused(works, ga, md, store, diff, hpa_algo)
+            if got is not None:
+                return got
         if not single:
             up = torch.full((R, n), float("nan"), device=dev)
             lo = torch.full((R, n), float("nan"), device=dev)
@@ -1818,12 +1840,11 @@ class FastPath:
             score = torch.zeros((R,), dtype=torch.float32, device=dev)
             valid = torch.zeros((R,), dtype=torch.int32, device=dev)
         fc_keep = {}
-        hpa_algo = zoo.canonical(cfg.hpa_forecast_algorithm) if (p0.hpa and cfg.hpa_forecast_algorithm) else None
         for sub in md.subs:
             cur = ga.cur_d if sub.idx is None else ga.cur_d.index_select(0, sub.idx)
             dsub = None if diff is None or sub.idx is None else diff.index_select(0, sub.idx)
             dsub = diff if sub.idx is None else dsub
-            lazy = LazyHist(store.buf, sub.rm, sub.shift, sub.lim, sub.T)
+            lazy = LazyHist(store.buf, sub.rm, *sub.shift_lim(), sub.T)
             algo = sub.algo
             if algo in ("moving_average_all", "bivariate_normal", "moving_average"):
                 lo_col = 0
@@ -1875,12 +1896,115 @@ class FastPath:
                 "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "hist_rows": ga.rowmap,
                 "store": store, "pts": (up, lo), "fc": fc_keep}
 
+    def _score_fused(self, works: list[FastWork], ga: GroupArrays, md: "ModelArrays", store: ResidentHistory,
+                     diff, hpa_algo) -> dict | None:
+        """The steady cycle of a single-model ES / Holt-Winters group as one
+        kernel (``fm_es_band_step``: advance the cached models over the new
+        samples read straight from the resident grid, band-judge every
+        current point, reduce per service, compact the anomalies) and one
+        device->host copy.  None when the cycle is not steady (a row misses
+        the model cache, rows span several cache slabs, more than 64 new
+        samples, wider windows): the caller takes the general path."""
+        from ..models import zoo
+        from ..ops._lib import LIB, ptr, stream_of
+        sub = md.subs[0]
+        algo = sub.algo
+        b = self.b
+        kind = zoo.ES_KINDS.get(algo)
+        cache = b.model_cache
+        p0 = works[0].plan
+        M, S = len(p0.aliases), len(works)
+        R = S * M
+        n = ga.cur.shape[1]
+        if (kind is None or cache.capacity <= 0 or sub.idx is not None or sub.hor is None or not 1 <= n <= 256
+                or M > 16 or sub.keys is None or ga.cur_d.stride(1) != 1 or sub.hor.shape != (R, n)):
+            return None
+        plan = cache.es_lookup(sub.keys, sub.t_last, b.step, b.clock(), sub.T, kind)
+        if not plan.usable.all() or len(plan.slabs) != 1:
+            self._es_plan = (sub.keys, plan, self.cycle)         # es_forecast reuses the lookup
+            return None
+        slab = plan.slabs[0]
+        if (plan.sid != slab.sid).any():
+            self._es_plan = (sub.keys, plan, self.cycle)
+            return None
+        kmax = max(int(plan.knew.max()), 1)
+        if kmax > 64 or kmax > sub.T:
+            self._es_plan = (sub.keys, plan, self.cycle)
+            return None
+        H = sub.H
+        if hpa_algo == algo:
+            H = max(H, max(1, b.cfg.hpa_forecast_steps))
+        dev = ga.cur_d.device
+        # per-row inputs that only change when the job list or the cache
+        # slots do: uploaded once, kept on the arrays
+        fz = getattr(ga, "_fused", None)
+        t_new = (kmax - plan.knew).astype(np.int32)
+        if fz is None or fz["R"] != R or fz["n"] != n:
+            fz = {"R": R, "n": n, "slots": None, "t_new": None,
+                  "up": torch.empty((R, n), dtype=torch.float32, device=dev),
+                  "lo": torch.empty((R, n), dtype=torch.float32, device=dev),
+                  "sig": torch.empty((R,), dtype=torch.float32, device=dev),
+                  "hostv": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32, device=dev),
+                  "host": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32).pin_memory()}
+            ga._fused = fz
+        if fz["slots"] is None or not np.array_equal(fz["slots"][0], plan.slot):
+            fz["slots"] = (plan.slot.copy(), torch.from_numpy(plan.slot.astype(np.int64)).to(dev))
+        if fz["t_new"] is None or not np.array_equal(fz["t_new"][0], t_new):
+            fz["t_new"] = (t_new, torch.from_numpy(t_new).to(dev))
+        fc = torch.empty((R, H), dtype=torch.float32, device=dev) if hpa_algo == algo else None
+        buf = self._fused_cmp.get(dev)
+        if buf is None or buf[0].shape[0] < R * n:
+            cap = max(R * n, 1024)
+            buf = self._fused_cmp[dev] = (torch.empty((cap, 2), dtype=torch.int32, device=dev),
+                                          torch.empty((cap,), dtype=torch.float32, device=dev),
+                                          torch.zeros((2,), dtype=torch.int32, device=dev))
+        idx_d, val_d, ctr = buf
+        par = self._fused_par
+        self._fused_par ^= 1
+        hv = fz["hostv"]
+        st = slab.as_state()
+        tb = sub.tables
+        cur = ga.cur_d
+        LIB.call("fm_es_band_step", ptr(store.buf), store.buf.stride(0), ptr(sub.rm), ptr(sub.shift), ptr(sub.lim),
+                 int(sub.dk), int(sub.T), kmax, ptr(fz["t_new"][1]), ptr(fz["slots"][1]), ptr(st.params),
+                 int(slab.m), kind, ptr(st.season) if st.season is not None else None, ptr(st.sse), ptr(st.state),
+                 ptr(st.nobs), ptr(cur), cur.stride(0), n, ptr(sub.hor), int(H), S, M, ptr(tb.thr), ptr(tb.bound),
+                 ptr(tb.minlb), ptr(diff), float(tb.pair_factor), ptr(sub.valid), ptr(md.lastk), ptr(fz["up"]),
+                 ptr(fz["lo"]), ptr(fz["sig"]), ptr(fc), int(H), ptr(hv), int(idx_d.shape[0]), ptr(ctr), par,
+                 ptr(idx_d), ptr(val_d), stream_of(cur))
+        # counter of this launch into the host buffer's tail, then ONE copy
+        hv[S * 4 + R * 6:].view(torch.int32).copy_(ctr, non_blocking=True)
+        host = fz["host"]
+        host.copy_(hv, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        hn = host.numpy()
+        packed_h = hn[:S * 4].reshape(S, 4).copy()
+        stats_h = hn[S * 4:S * 4 + R * 4].reshape(R, 4).copy()
+        ints = hn[S * 4 + R * 4:].view(np.int32)
+        count_h = ints[:R].copy()
+        dead = ints[R:2 * R] != 0
+        total = int(ints[2 * R + par])
+        cache.es_commit(slab, plan.slot, plan.t_last, dead)
+        cache.hits += R
+        idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
+        if len(idx):
+            kk = idx[:, 0].astype(np.int64) * n + idx[:, 1]
+            kk.sort()
+            idx = np.stack([kk // n, kk % n], 1).astype(np.int32)
+        self.fused_steps += 1
+        return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
+                "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "hist_rows": ga.rowmap,
+                "store": store, "pts": (fz["up"], fz["lo"]), "fc": {algo: (sub, fc)} if fc is not None else {}}
+
     def _forecast(self, algo: str, lazy: "LazyHist", sub: "ModelSub", H: int):
         from ..models import zoo
         b = self.b
         ctx = None
         if algo in zoo.ES_KINDS and b.model_cache.capacity > 0:
-            ctx = zoo.CacheContext(b.model_cache, sub.keys, sub.t_last, b.step, b.clock())
+            ep = self._es_plan
+            self._es_plan = None
+            ctx = zoo.CacheContext(b.model_cache, sub.keys, sub.t_last, b.step, b.clock(),
+                                   ep[1] if ep is not None and ep[0] is sub.keys and ep[2] == self.cycle else None)
         lstm = b.lstm_for_jobs_of({sub.M}) if algo == "lstm" else b.lstm_model
         if ctx is not None:
             hist = lazy                                   # hits read only their new columns

@@ -190,8 +190,8 @@ class CanaryScorer:
         (engine/resident.py): logical row r reads history row ``rowmap[r]`` of
         ``hview.hist`` in place.  GPU: one role-split front launch when the
         pairwise windows fit a wave-sorted 256 (n_cur + n_base <= 256),
-        otherwise history stats || pairwise (<= 512 on the GPU, wider on the
-        CPU oracle) — then the decision kernel.  Rows are services x M."""
+        otherwise history stats || pairwise (<= C.PAIRWISE_MAX on the GPU,
+        wider on the CPU oracle) — then the decision kernel.  Rows are services x M."""
         R = cur.shape[0]
         has_base = base is not None and base.shape[1] > 0
         if not cur.is_cuda:
@@ -214,12 +214,12 @@ class CanaryScorer:
                      ptr(o.pstats), ptr(self._queue), ptr(rowmap), st)
         else:
             LIB.call("fm_hist_stats_rm", ptr(hview.hist), hview.ld, hview.T, R, ptr(o.hs), 0, ptr(rowmap), st)
-            if has_base and n <= 512:
+            if has_base and n <= C.PAIRWISE_MAX:
                 self._pairwise_into(cur, base, o, combine=False)
             elif has_base:
                 # padded wider than the register sort: rows bucketed by their
-                # own widths, only really wide rows (> 512 points per side
-                # pair, rare) on the fp64 CPU oracle
+                # own widths, only really wide rows (> C.PAIRWISE_MAX pooled
+                # points, rare) on the fp64 CPU oracle
                 p, s_, _ = C.pairwise_tests(cur, base, self.pcfg)
                 o.pvals.copy_(p)
                 o.pstats.copy_(s_)

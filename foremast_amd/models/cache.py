@@ -33,6 +33,16 @@ from ..ops import smoothing as SM
 _SLOT_BITS = 40
 
 
+class EsPlan:
+    """A batch's cache lookup (ModelCache.es_lookup): per row the slab id
+    (-1: none), slot, whether the cached model is usable and how many new
+    samples it advances by."""
+    __slots__ = ("t_last", "sid", "slot", "usable", "knew", "slabs")
+
+    def __init__(self, t_last, sid, slot, usable, knew, slabs):
+        self.t_last, self.sid, self.slot, self.usable, self.knew, self.slabs = t_last, sid, slot, usable, knew, slabs
+
+
 class _Slab:
     def __init__(self, sid: int, kind: int, m: int, device):
         self.sid, self.kind, self.m, self.device = sid, kind, m, torch.device(device)
@@ -170,17 +180,13 @@ class ModelCache:
             self.entries[keys[j]] = base | slot
 
     # ------------------------------------------------------------------ forecast
-    def es_forecast(self, keys: list, t_last: np.ndarray, step: float, now: float, hist: torch.Tensor, T: int,
-                    kind: int, H: int, period_for) -> tuple[torch.Tensor, torch.Tensor]:
-        """Forecast [R, H] + sigma [R] for every row of ``hist`` through the
-        cache.  ``period_for(rows)`` returns the seasonal period used to
-        grid-fit the rows that miss (kind >= 2)."""
+    def es_lookup(self, keys: list, t_last: np.ndarray, step: float, now: float, T: int, kind: int) -> "EsPlan":
+        """Which rows hit a cached model of ``kind`` and by how many new
+        samples each one advances (``es_forecast``'s first half; the fused
+        steady-cycle kernel takes the plan when every row hits one slab)."""
         self.clock += 1
-        R = hist.shape[0]
-        dev = hist.device
+        R = len(keys)
         t_last = np.asarray(t_last, np.float64)
-        fc = torch.empty((R, H), dtype=torch.float32, device=dev)
-        sig = torch.empty((R,), dtype=torch.float32, device=dev)
         memo = self._memo
         root = getattr(keys, "root", None)
         rg = self._root_g
@@ -214,6 +220,7 @@ class ModelCache:
         slot = g & ((1 << _SLOT_BITS) - 1)
         usable = np.zeros(R, bool)
         knew = np.zeros(R, np.int64)
+        slabs = []
         for slab in self.slabs:
             if slab.kind != kind:
                 continue
@@ -225,6 +232,30 @@ class ModelCache:
             ok = (now - slab.fitted_at[sl] <= self.refit_seconds) & (k >= 0) & (k < T)
             usable[rows[ok]] = True
             knew[rows] = k
+            slabs.append(slab)
+        return EsPlan(t_last, sid, slot, usable, knew, slabs)
+
+    def es_commit(self, slab: "_Slab", sl: np.ndarray, t_last: np.ndarray, dead: np.ndarray) -> None:
+        """After an update of ``slab``'s slots ``sl``: their sample time and
+        use stamp, and the slots whose state went non-finite dropped."""
+        slab.t_last[sl] = t_last
+        slab.stamp[sl] = self.clock
+        for j in np.nonzero(dead)[0]:
+            self._drop_slot(slab, int(sl[j]))
+
+    def es_forecast(self, keys: list, t_last: np.ndarray, step: float, now: float, hist: torch.Tensor, T: int,
+                    kind: int, H: int, period_for, plan: "EsPlan | None" = None) -> tuple[torch.Tensor, torch.Tensor]:
+        """Forecast [R, H] + sigma [R] for every row of ``hist`` through the
+        cache.  ``period_for(rows)`` returns the seasonal period used to
+        grid-fit the rows that miss (kind >= 2).  ``plan``: this call's
+        :meth:`es_lookup`, when the caller already made it."""
+        p = plan if plan is not None else self.es_lookup(keys, t_last, step, now, T, kind)
+        R = hist.shape[0]
+        dev = hist.device
+        t_last = p.t_last
+        sid, slot, usable, knew = p.sid, p.slot, p.usable, p.knew
+        fc = torch.empty((R, H), dtype=torch.float32, device=dev)
+        sig = torch.empty((R,), dtype=torch.float32, device=dev)
         hit = np.nonzero(usable)[0]
         miss = np.nonzero(~usable)[0]
         self.hits += len(hit)
@@ -247,11 +278,8 @@ class ModelCache:
             else:
                 idx = torch.as_tensor(rows, device=dev)
                 fc[idx], sig[idx] = f, s
-            slab.t_last[sl] = t_last[rows]
-            slab.stamp[sl] = self.clock
             dead = ~torch.isfinite(slab.state[slots_t, :2]).all(1).cpu().numpy()
-            for j in np.nonzero(dead)[0]:
-                self._drop_slot(slab, int(sl[j]))
+            self.es_commit(slab, sl, t_last[rows], dead)
         if len(miss):
             idx = torch.as_tensor(miss, device=dev)
             sub = hist.index_select(0, idx)       # rows stay 16-B aligned (LazyHist pads them)

@@ -76,6 +76,7 @@ class CacheContext:
     t_last: np.ndarray      # [R] timestamp of each row's last history sample
     step: float             # sample spacing, seconds
     now: float              # wall clock (refit age)
+    plan: object = None     # this batch's ModelCache.es_lookup, when already made
 
 
 @dataclass
@@ -182,7 +183,7 @@ def forecast(algorithm: str, hist: torch.Tensor, T: int, H: int, period: int | N
         kind = ES_KINDS[algo]
         if cache is not None:
             return cache.cache.es_forecast(cache.keys, cache.t_last, cache.step, cache.now, hist, T, kind, H,
-                                           lambda sub: period or _detect_period(sub, T))
+                                           lambda sub: period or _detect_period(sub, T), plan=cache.plan)
         m = 1
         if kind >= 2:
             m = period or _detect_period(hist, T)

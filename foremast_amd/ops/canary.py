@@ -54,6 +54,12 @@ def _rows(x: torch.Tensor) -> tuple[int, int]:
     return x.shape[0], x.stride(0)
 
 
+# widest pooled sample (n_cur + n_base) the GPU rank-test kernel sorts in
+# registers (16 values per lane: a 60-minute canary window of 8 pods per side
+# at a 1-minute step); wider rows take the fp64 CPU oracle
+PAIRWISE_MAX = 1024
+
+
 def pairwise_tests(cur: torch.Tensor, base: torch.Tensor, cfg: PairwiseConfig = PairwiseConfig()):
     """Returns (pvals [R,6] f32, stats [R,6] f32, diff [R] int8) in TEST_NAMES order.
 
@@ -70,7 +76,7 @@ def pairwise_tests(cur: torch.Tensor, base: torch.Tensor, cfg: PairwiseConfig = 
         return torch.from_numpy(p), torch.from_numpy(s), torch.from_numpy(d)
     require_native(cur)
     n_cur, n_base = cur.shape[1], base.shape[1]
-    if n_cur + n_base > 512:
+    if n_cur + n_base > PAIRWISE_MAX:
         return _pairwise_bucketed(cur, base, cfg)
     pv = torch.empty((R, N_TESTS), dtype=torch.float32, device=cur.device)
     st = torch.empty_like(pv)
@@ -91,17 +97,17 @@ def used_width(x: torch.Tensor) -> torch.Tensor:
 
 
 def _pairwise_bucketed(cur: torch.Tensor, base: torch.Tensor, cfg: PairwiseConfig):
-    """A batch padded wider than the register sort (n_cur + n_base > 512):
+    """A batch padded wider than the register sort (n_cur + n_base > PAIRWISE_MAX):
     rows are bucketed by their own used widths.  Rows whose samples fit
-    (<= 256 per side, or <= 512 together when the whole bucket does) run the
+    (<= PAIRWISE_MAX / 2 per side, or <= PAIRWISE_MAX together when the whole bucket does) run the
     GPU kernel on a narrowed copy; only rows that are really wider take the
     fp64 CPU oracle.  One wide job never moves the whole batch off the GPU
     and never fails it."""
     R = cur.shape[0]
     lc, lb = used_width(cur).cpu(), used_width(base).cpu()
-    fit = (lc + lb) <= 512
-    if fit.any() and int(lc[fit].max()) + int(lb[fit].max()) > 512:
-        fit &= (lc <= 256) & (lb <= 256)
+    fit = (lc + lb) <= PAIRWISE_MAX
+    if fit.any() and int(lc[fit].max()) + int(lb[fit].max()) > PAIRWISE_MAX:
+        fit &= (lc <= PAIRWISE_MAX // 2) & (lb <= PAIRWISE_MAX // 2)
     pv = torch.full((R, N_TESTS), float("nan"), dtype=torch.float32, device=cur.device)
     st = torch.full_like(pv, float("nan"))
     df = torch.zeros((R,), dtype=torch.int8, device=cur.device)

@@ -57,13 +57,31 @@ def bf16_round(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.bfloat16).to(torch.float32)
 
 
+LOG2E = 1.4426950408889634
+GATE_SCALES = (-LOG2E, -LOG2E, -2.0 * LOG2E, -LOG2E)   # i, f, g, o
+
+
+def gate_scales(H: int) -> np.ndarray:
+    """[4H] per-gate-row scale the packed weights carry (csrc/include/fm_lstm_cell.h):
+    exp2 of a scaled pre-activation is e^{-x} (i, f, o) or e^{-2x} (g)."""
+    return np.repeat(np.asarray(GATE_SCALES, np.float64), H).astype(np.float32)
+
+
+def _scaled_rows(a: np.ndarray, H: int) -> np.ndarray:
+    """Gate rows (first axis 4H) times their scale, in fp32."""
+    s = gate_scales(H)
+    return (a.astype(np.float32) * (s if a.ndim == 1 else s[:, None])).astype(np.float32)
+
+
 def pack_lstm(w_ih: torch.Tensor, w_hh: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
-    """-> uint8 tensor [H/16, 2, KS, 64, 16 bytes] (bf16 fragments)."""
+    """-> uint8 tensor [H/16, 2, KS, 64, 16 bytes] (bf16 fragments of the
+    gate-scaled weights, :func:`gate_scales`)."""
     w_ih = w_ih.detach().float().cpu().numpy()
     w_hh = w_hh.detach().float().cpu().numpy()
     b = bias.detach().float().cpu().numpy()
     H4, I = w_ih.shape
     H = H4 // 4
+    w_ih, w_hh, b = _scaled_rows(w_ih, H), _scaled_rows(w_hh, H), _scaled_rows(b, H)
     check(H in SUPPORTED_H, f"hidden size must be one of {SUPPORTED_H}")
     check(I <= 15, "input features must be <= 15 (folded into one K step with the bias)")
     KS = H // 16 + 1
@@ -91,10 +109,12 @@ def pack_aug(aug: np.ndarray, H: int, RT: int) -> np.ndarray:
     """Augmented gate matrix [4H, K] (columns in the B operand's k order,
     K a multiple of 16) -> bf16 A fragments [H/(8 RT) waves, RT, K/16, 64 lanes, 8]
     as uint16: wave w, row tile rt holds the gate rows [i f g o] x 8 units of
-    units 8 RT w + 8 rt + (0..7) (lane l: row l & 31, k half l >> 5)."""
+    units 8 RT w + 8 rt + (0..7) (lane l: row l & 31, k half l >> 5); the
+    rows carry their gate scale (:func:`gate_scales`)."""
     K = aug.shape[1]
     KS = K // 16
     nw = H // (8 * RT)
+    aug = _scaled_rows(aug, H)
     lane = np.arange(64)
     r, hh = lane & 31, lane >> 5
     out = np.zeros((nw, RT, KS, 64, 8), np.float32)
@@ -223,13 +243,22 @@ def lstm_features(hist: torch.Tensor, T: int, L: int, period: float, I: int = 3)
     return xa, mu, sd
 
 
+def _rd_gates(w: torch.Tensor, H: int) -> torch.Tensor:
+    """Gate-row weights as the kernel sees them: rounded to bf16 after the
+    gate scale, the scale divided out again."""
+    s = torch.from_numpy(gate_scales(H))
+    s = s if w.dim() == 1 else s[:, None]
+    return bf16_round(w.float() * s) / s
+
+
 def ref_lstm_forward(x: torch.Tensor, w_ih, w_hh, bias, h0=None, c0=None, emulate_bf16: bool = True):
-    """fp32 reference; with emulate_bf16 the weights, inputs and the recurrent h
-    are rounded to bf16 exactly where the kernel rounds them."""
+    """fp32 reference; with emulate_bf16 the (gate-scaled) weights, inputs and
+    the recurrent h are rounded to bf16 exactly where the kernel rounds them."""
     B, L, I = x.shape
     H = w_hh.shape[1]
     rd = bf16_round if emulate_bf16 else (lambda t: t)
-    Wi, Wh, b = rd(w_ih.float()), rd(w_hh.float()), rd(bias.float())
+    rw = (lambda t: _rd_gates(t, H)) if emulate_bf16 else (lambda t: t.float())
+    Wi, Wh, b = rw(w_ih.float()), rw(w_hh.float()), rw(bias.float())
     h = torch.zeros(B, H) if h0 is None else h0.float().clone()
     c = torch.zeros(B, H) if c0 is None else c0.float().clone()
     hr = rd(h)
@@ -254,7 +283,8 @@ def ref_lstm_stack(x: torch.Tensor, layers: list, emulate_bf16: bool = True):
     h = c = None
     for w_ih, w_hh, b in layers:
         H = w_hh.shape[1]
-        Wi, Wh, bb = rd(w_ih.float()), rd(w_hh.float()), rd(b.float())
+        rw = (lambda t: _rd_gates(t, H)) if emulate_bf16 else (lambda t: t.float())   # noqa: B023
+        Wi, Wh, bb = rw(w_ih.float()), rw(w_hh.float()), rw(b.float())
         h = torch.zeros(B, H)
         c = torch.zeros(B, H)
         hr = rd(h)

@@ -119,7 +119,7 @@ def test_synth_reference_deterministic_across_shards():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n1,n2,nan_frac", [(20, 25, 0.0), (50, 50, 0.0), (60, 60, 0.03), (100, 120, 0.0),
-                                            (256, 200, 0.02)])
+                                            (256, 200, 0.02), (300, 300, 0.01), (600, 420, 0.0)])
 def test_gpu_pairwise_matches_reference(cuda, n1, n2, nan_frac):
     R = 257
     cur, base = _data(R, n1, n2, seed=n1 + n2, nan_frac=nan_frac)
@@ -136,8 +136,8 @@ def test_gpu_pairwise_matches_reference(cuda, n1, n2, nan_frac):
 
 def _mixed_width_batch():
     """Left-packed rows padded to 700 + 700 columns: most rows narrow, a few
-    wide on one side (fit the kernel only in the <= 256 / side bucket) and two
-    wider than 512 together (CPU oracle)."""
+    wide on one side, one 400 + 300 (the 16-register sort) and one 700 + 700
+    (wider than C.PAIRWISE_MAX together: CPU oracle)."""
     rng = np.random.default_rng(7)
     R = 40
     cur = np.full((R, 700), np.nan, np.float32)
@@ -317,7 +317,7 @@ def test_gpu_cross_lane_primitives(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n1,n2,nan_frac", [(50, 50, 0.0), (37, 61, 0.05), (120, 100, 0.02), (7, 9, 0.0)])
+@pytest.mark.parametrize("n1,n2,nan_frac", [(50, 50, 0.0), (37, 61, 0.05), (120, 100, 0.02), (7, 9, 0.0), (480, 470, 0.01)])
 def test_gpu_pairwise_count_equals_sort(cuda, n1, n2, nan_frac):
     """The bitonic-sort (0) and counting (1) forms produce identical sufficient statistics."""
     from foremast_amd.ops._lib import LIB, ptr, stream_of

@@ -193,6 +193,37 @@ def test_gpu_models_fast_path_equals_general_path(algo, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo,kind", [("holt_winters", "continuous"), ("exponential_smoothing", "continuous"),
+                                       ("double_exponential_smoothing", "hpa"), ("holt_winters", "hpa")])
+def test_gpu_fused_steady_cycle_equals_op_by_op(algo, kind):
+    """the steady cycle of a cached ES / Holt-Winters group as
+    ONE kernel (fm_es_band_step: model advance from the resident grid, band,
+    service reduce, compaction) gives the verdicts, reasons, HPA logs and
+    gauges of the op-by-op path (gather_cols -> es_update -> band -> reduce
+    -> compact), cycle by cycle."""
+    import foremast_amd.engine.fastpath as F
+    a = _brain(True, algo, FAULTS, "cuda")
+    b = _brain(True, algo, FAULTS, "cuda")
+    ids = _submit(a[2], kind)
+    assert ids == _submit(b[2], kind)
+    keep = F._FUSED_STEP
+    try:
+        for cyc in range(6):
+            F._FUSED_STEP = True
+            a[3].run_once()
+            F._FUSED_STEP = False
+            b[3].run_once()
+            _compare(a, b, ids, cyc)
+            a[0].t += 60
+            b[0].t += 60
+    finally:
+        F._FUSED_STEP = keep
+    # cycle 0 fits; later cycles whose rows all hit the cache run fused
+    assert a[3].fast.fused_steps >= 2 and b[3].fast.fused_steps == 0
+    assert a[3].model_cache.hits == b[3].model_cache.hits
+
+
+@pytest.mark.gpu
 def test_gpu_gather_cols_matches_reference():
     import torch
     from foremast_amd.ops import misc as MI

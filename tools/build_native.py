@@ -66,7 +66,7 @@ def build(force: bool = False, jobs: int = 4) -> list[Path]:
         obj = BUILD / (src.stem + ".hip.o")
         objs.append(obj)
         if force or _stale(obj, [src, *headers]):
-            jobs_list.append([HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)])
+            jobs_list.append([HIPCC, *HIP_FLAGS, *_file_flags(src), "-c", str(src), "-o", str(obj)])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(_run, jobs_list))
     lib = OUT / "libforemast_hip.so"
@@ -93,13 +93,51 @@ def build(force: bool = False, jobs: int = 4) -> list[Path]:
     return built
 
 
+def _file_flags(src: Path) -> list[str]:
+    """Per-file hipcc flags: a ``// fm-hipcc-flags: ...`` line in the first 40 lines."""
+    with open(src) as f:
+        for _, line in zip(range(40), f):
+            if line.startswith("// fm-hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
+def build_variant(name: str, flags: list[str], stems: list[str], jobs: int = 4) -> Path:
+    """An A/B build of the HIP library: the default objects with ``stems``'
+    sources recompiled under ``flags`` in place of their own per-file flags
+    -> ``_native/variants/libforemast_hip_<name>.so`` (select it with
+    ``FOREMAST_HIP_LIB``)."""
+    build(False, jobs)
+    vdir = BUILD / f"variant_{name}"
+    vdir.mkdir(parents=True, exist_ok=True)
+    objs, cmds = [], []
+    for src in sorted((CSRC / "kernels").glob("*.hip")):
+        if src.stem in stems:
+            obj = vdir / (src.stem + ".hip.o")
+            cmds.append([HIPCC, *HIP_FLAGS, *flags, "-c", str(src), "-o", str(obj)])
+        else:
+            obj = BUILD / (src.stem + ".hip.o")
+        objs.append(obj)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(_run, cmds))
+    out = OUT / "variants" / f"libforemast_hip_{name}.so"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(out)])
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--variant", action="append", default=[],
+                    help="NAME:FILE[,FILE]:FLAG[,FLAG] -- an A/B build of the HIP library")
     a = ap.parse_args()
     for p in build(a.force, a.j):
         print(p.relative_to(ROOT))
+    for v in a.variant:
+        name, stems, flags = v.split(":", 2)
+        print(build_variant(name, flags.split(",") if flags else [], stems.split(","), a.j).relative_to(ROOT))
 
 
 if __name__ == "__main__":

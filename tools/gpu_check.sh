@@ -32,12 +32,26 @@ for s in $steps; do
          e2e c3e2e_http60 --config 3e2e --source http --poll-seconds 60 --window 60 --steps 12 --warmup 2 --prom-workers 8 &&
          e2e c2e2e_http --config 2e2e --source http --steps 20 --warmup 3 --prom-workers 8 || exit $rc ;;
     peerprobe) run peer_probe 150 python -u tools/peer_probe.py || exit $rc ;;
+    lstm) V=$R/foremast_amd/_native/variants
+          run lstm_tests 400 python -u -m pytest tests/test_model_ops.py -m gpu -k "lstm" -v --timeout 120 \
+              --timeout-method thread || exit $rc
+          run lstm_ab 200 python -u tools/lstm_ab.py || exit $rc
+          run lstm_ab_c14 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_c14.so python -u tools/lstm_ab.py || exit $rc
+          run lstm_ab_r4 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_r4.so python -u tools/lstm_ab.py || exit $rc
+          run config4 300 python -u benchmarks/bench_configs.py --config 4 || exit $rc
+          run config4_stack 300 python -u benchmarks/bench_configs.py --config 4 --hidden 256 --layers 2 --multivariate || exit $rc ;;
+    pmclstm) run pmclstm 420 bash tools/pmc_lstm.sh || exit $rc ;;
+    r5tests) run r5tests 600 python -u -m pytest tests/test_fastpath_models.py tests/test_canary_ops.py \
+                 tests/test_model_ops.py tests/test_fastpath.py -m gpu -x -v --timeout 120 --timeout-method thread \
+                 || exit $rc ;;
     peer) run peer_test 300 python -u -m pytest tests/test_peer.py tests/test_board.py -x -v -s --timeout 200 \
               --timeout-method thread || exit $rc
           run peer_bench 240 env FOREMAST_DEVICE_INDEX=0 FOREMAST_DIST_BACKEND=gloo python bench.py --gpus 2 \
               --services 2500 --publish peer --steps 300 --warmup 20 || exit $rc ;;
     mixed) e2e c_mixed --config mixed --steps 20 --warmup 3 &&
-         e2e c3e2e_60 --config 3e2e --poll-seconds 60 --window 60 --steps 20 --warmup 3 &&
+         e2e c_mixed_canary --config mixed --mixed-class 0 --steps 20 --warmup 3 &&
+         e2e c_mixed_cont --config mixed --mixed-class 1 --steps 20 --warmup 3 &&
+         e2e c_mixed_hpa --config mixed --mixed-class 2 --steps 20 --warmup 3 &&
          e2e c2e2e --config 2e2e --steps 20 --warmup 3 &&
          e2e c4e2e --config 4e2e --steps 20 --warmup 3 || exit $rc ;;
     shard) run shard1250 200 python bench.py --services 1250 --steps 400 --warmup 20 || exit $rc
@@ -53,6 +67,13 @@ for s in $steps; do
                p.sort_stats('tottime').print_stats(70); p.sort_stats('cumtime').print_stats(70)" \
                > gpurun_out/hostprof_$c.txt || exit 1
          done ;;
+    hostprof60) FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_3e2e_http60.prof timeout -k 10 500 python -u \
+               benchmarks/bench_configs.py --config 3e2e --source http --poll-seconds 60 --window 60 --steps 8 \
+               --warmup 2 --prom-workers 8 > gpurun_out/check_hostprof_3e2e_http60.log 2>&1; rc=$?
+           echo "hostprof60 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+           python -c "import pstats,sys; p=pstats.Stats('gpurun_out/hostprof_3e2e_http60.prof', stream=sys.stdout); \
+               p.sort_stats('tottime').print_stats(70); p.sort_stats('cumtime').print_stats(90)" \
+               > gpurun_out/hostprof_3e2e_http60.txt || exit 1 ;;
     restart) e2e c3e2e_restart --config 3e2e --steps 5 --warmup 2 --restart &&
          e2e c2e2e_restart --config 2e2e --steps 5 --warmup 2 --restart || exit $rc ;;
     scanprobe) run scanprobe 200 python -u tools/hw_scan_probe.py || exit $rc
