@@ -451,6 +451,7 @@ def config3e2e(args):
     cyc_ms: list[float] = []
     # FOREMAST_PROFILE_CYCLES=<path>: cProfile of the timed cycles only
     _prof = None
+    _tprof = [] if os.environ.get("FOREMAST_TORCH_PROFILE") else None
     if os.environ.get("FOREMAST_PROFILE_CYCLES"):
         import cProfile
         _prof = cProfile.Profile()
@@ -491,7 +492,23 @@ def config3e2e(args):
         st0 = dict(live.stats) if live is not None else None
         wt0 = brain.fast.wt.apply_s if brain.fast is not None else 0.0
         tc = time.perf_counter()
-        if _prof is not None and len(cyc_ms) >= args.warmup:
+        if _tprof is not None and args.warmup <= len(cyc_ms) < args.warmup + 3:
+            # FOREMAST_TORCH_PROFILE=<path>: which Python lines launch the
+            # cycle's device ops (ATen glue around the hand-written kernels)
+            from torch._C._profiler import _ExperimentalConfig
+            from torch.profiler import ProfilerActivity, profile
+            acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if dev.type == "cuda" else [])
+            with profile(activities=acts, with_stack=True, experimental_config=_ExperimentalConfig(verbose=True)) as tp:
+                r = brain.run_once()
+            rows_ = []
+            for e in tp.key_averages(group_by_stack_n=8):
+                dt = getattr(e, "self_device_time_total", 0) or getattr(e, "self_cuda_time_total", 0)
+                if e.key.startswith("aten::") and (dt > 0 or dev.type == "cpu"):
+                    st_ = [f for f in (e.stack or []) if "foremast_amd" in f or "benchmarks" in f][:4]
+                    rows_.append((dt, e.count, e.key, " <- ".join(st_)))
+            rows_.sort(key=lambda x: -x[0])
+            _tprof.append("\n".join(f"{dt:9.1f}us {n:4d} {k:28s} {st_}" for dt, n, k, st_ in rows_[:80]))
+        elif _prof is not None and len(cyc_ms) >= args.warmup:
             r = _prof.runcall(brain.run_once)
         else:
             r = brain.run_once()
@@ -540,6 +557,9 @@ def config3e2e(args):
             prom.wait(30)
     if _prof is not None:
         _prof.dump_stats(os.environ["FOREMAST_PROFILE_CYCLES"])
+    if _tprof:
+        with open(os.environ["FOREMAST_TORCH_PROFILE"], "w") as f:
+            f.write("\n\n".join(_tprof))
     restart = None
     if args.restart:
         # warm restart: checkpoint engine + resident history,
@@ -675,6 +695,8 @@ def config3e2e(args):
              "span_ms_median_rank0": span_ms, "span_ms_median_max_rank": worst, "span_ms_max_rank0": span_max,
              "cycle_ms_max_rank0": round(max(cyc_ms[args.warmup:] or cyc_ms or [0.0]), 3),
              "model_cache": {"hits": brain.model_cache.hits, "misses": brain.model_cache.misses},
+             "fused_steady_cycles": ({"groups_fused": brain.fast.fused_steps, "declined": brain.fast.fused_declined}
+                                     if brain.fast is not None else None),
              "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),
              "submit_s": round(t_sub, 3),
              "fast_jobs_first_cycle": first.get("fast_jobs"), "device": str(dev)})

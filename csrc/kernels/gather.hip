@@ -69,3 +69,33 @@ FM_API int fm_gather_cols(const float* src, int64_t ld, const int32_t* rm, const
   FM_LAUNCH_CHECK();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Sliding-grid columns leaving the window (ResidentHistory.advance): per row
+// the finite samples in columns [lo, hi) are counted into gone[row] (the
+// history gate's finite count drops by them) and the columns are set to NaN,
+// in ONE pass -- was isfinite + sum + a device->host copy + a strided fill,
+// seven launches per cycle.  One thread per row; a 60-s poll retires one
+// column per cycle.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void grid_retire_kernel(float* __restrict__ buf, int64_t ld, int64_t R, int lo,
+                                                          int hi, int* __restrict__ gone) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  float* row = buf + r * ld;
+  int n = 0;
+  for (int c = lo; c < hi; ++c) {
+    n += isfinite(row[c]) ? 1 : 0;
+    row[c] = __builtin_nanf("");
+  }
+  gone[r] = n;
+}
+
+FM_API int fm_grid_retire(float* buf, int64_t ld, int64_t R, int lo, int hi, int* gone, hipStream_t stream) {
+  if (R <= 0 || hi <= lo) return 0;
+  if (lo < 0 || hi > ld) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(grid_retire_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, stream, buf, ld, R, lo, hi,
+                     gone);
+  FM_LAUNCH_CHECK();
+  return 0;
+}

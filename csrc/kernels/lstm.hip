@@ -197,17 +197,67 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_kernel(const uint4* __restrict
 // single-buffered in LDS: it is rewritten one half-step after its last
 // reader, with a barrier in between.
 // ---------------------------------------------------------------------------
-template <int H, bool HSEQ>
-__global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __restrict__ xa /*[B, L, 2] x 16 B*/,
-                                                              int64_t B, int L, const uint4* __restrict__ Wpack,
-                                                              const float* __restrict__ h0,
-                                                              const float* __restrict__ c0,
-                                                              float* __restrict__ h_out, float* __restrict__ c_out,
-                                                              unsigned short* __restrict__ hseq) {
+// x sources of the pipelined kernel: fetch(ct, t) issues the load of step t
+// of column tile ct (one step ahead of its use), make(ct, t, raw) turns it
+// into this lane's 16-B half of the augmented K step.
+struct XaSource {            // the augmented bf16 input [B, L, 16] (fm_lstm_features)
+  using Raw = uint4;
+  const uint4* xp[2];
+  __device__ void setup(const uint4* xa, int64_t b0, int64_t B, int L, int col, int h) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      int64_t bb = b0 + 32 * ct + col;
+      bb = bb < B ? bb : B - 1;
+      xp[ct] = xa + (bb * L) * 2 + h;
+    }
+  }
+  __device__ __forceinline__ Raw fetch(int ct, int t) const { return xp[ct][t * 2]; }
+  __device__ __forceinline__ uint4 make(int, int, const Raw& r) const { return r; }
+};
+
+// The forecaster's features computed in the kernel from the history rows
+// themselves (a resident grid row through rm / shift / lim, or a plain
+// [B, ld] matrix): per sequence the last L samples z-scored over their finite
+// values (population std, >= 1e-6, missing -> 0), then sin / cos of the daily
+// phase 2 pi c / period of the dense column c, 1.0 at k = I -- the layout
+// fm_lstm_features writes, without its [B, L, 16] bf16 round trip through HBM.
+struct HistSource {
+  using Raw = float;
+  const float* row[2];
+  int off[2], lim[2];
+  float mu[2], inv[2];
+  int c0;                    // dense column of step 0 (T - L)
+  float p, ip;               // period and 1 / period
+  int I;
+  bool lo_half;              // lane holds k = 0..7 (the features), else k = 8..15 (zeros)
+  __device__ __forceinline__ Raw fetch(int ct, int t) const {
+    const int bc = c0 + t + off[ct];
+    return (lo_half && bc >= 0 && bc < lim[ct]) ? row[ct][bc] : __builtin_nanf("");
+  }
+  __device__ __forceinline__ uint4 make(int ct, int t, const Raw& v) const {
+    if (!lo_half) return make_uint4(0u, 0u, 0u, 0u);
+    const float z = isfinite(v) ? (v - mu[ct]) * inv[ct] : 0.f;
+    const float c = (float)(c0 + t);
+    const float q = floorf(c * ip);
+    const float fr = __builtin_fmaf(-q, p, c) * ip;          // phase in revolutions, [0, 1)
+    const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
+    // [z, sin, cos][:I], 1.0 at k = I, zeros above (I <= 3)
+    const float f0 = I > 0 ? z : 1.f;
+    const float f1 = I > 1 ? sn : (I == 1 ? 1.f : 0.f);
+    const float f2 = I > 2 ? cs : (I == 2 ? 1.f : 0.f);
+    const float f3 = I == 3 ? 1.f : 0.f;
+    return make_uint4(pack_bf2(f0, f1), pack_bf2(f2, f3), 0u, 0u);
+  }
+};
+
+template <int H, bool HSEQ, typename XS>
+__device__ __forceinline__ void lstm_pipe_body(const XS& xs, int64_t B, int L, const uint4* __restrict__ Wpack,
+                                               const float* __restrict__ h0, const float* __restrict__ c0,
+                                               float* __restrict__ h_out, float* __restrict__ c_out,
+                                               unsigned short* __restrict__ hseq, unsigned short* hbuf) {
   constexpr int KS = H / 16 + 1;
   constexpr int HP = H + 8;
   constexpr int BT = 64;
-  __shared__ __attribute__((aligned(16))) unsigned short hbuf[BT * HP];
   const int lane = lane_id(), w = wave_id();
   const int h = lane >> 5, col = lane & 31;
   const int64_t b0 = (int64_t)blockIdx.x * BT;
@@ -233,15 +283,9 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __res
       }
   __syncthreads();
 
-  const uint4* xp[2];
   bool inb[2];
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    int64_t bb = b0 + 32 * ct + col;
-    inb[ct] = bb < B;
-    bb = bb < B ? bb : B - 1;
-    xp[ct] = xa + (bb * L) * 2 + h;
-  }
+  for (int ct = 0; ct < 2; ++ct) inb[ct] = b0 + 32 * ct + col < B;
 
   // MFMAs of one tile for one step: h_{t-1} of the tile from LDS, x_t from xv
   auto gates = [&](int ct, const uint4& xv, f32x16 (&acc)[2]) {
@@ -290,27 +334,131 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __res
   };
 
   f32x16 acc0[2], acc1[2];
-  uint4 x0n = xp[0][0], x1n = xp[1][0];
-  gates(0, x0n, acc0);                               // tile 0, step 0
-  if (L > 1) x0n = xp[0][2];                         // x_1 of tile 0
+  typename XS::Raw x0n = xs.fetch(0, 0), x1n = xs.fetch(1, 0);
+  gates(0, xs.make(0, 0, x0n), acc0);                // tile 0, step 0
+  if (L > 1) x0n = xs.fetch(0, 1);                   // x_1 of tile 0
   __syncthreads();                                   // tile-0 h_{-1} read by all before A(0) rewrites it
   for (int t = 0; t < L; ++t) {
     const bool last = t == L - 1;
     // A(t): tile-1 MFMAs for step t || tile-0 cell of step t
-    const uint4 x1 = x1n;
-    if (!last) x1n = xp[1][(t + 1) * 2];
-    gates(1, x1, acc1);
+    const typename XS::Raw x1 = x1n;
+    if (!last) x1n = xs.fetch(1, t + 1);
+    gates(1, xs.make(1, t, x1), acc1);
     cell(0, t, acc0, last);
     __syncthreads();
     // B(t): tile-0 MFMAs for step t+1 || tile-1 cell of step t
     if (!last) {
-      const uint4 x0 = x0n;
-      if (t + 2 < L) x0n = xp[0][(t + 2) * 2];
-      gates(0, x0, acc0);
+      const typename XS::Raw x0 = x0n;
+      if (t + 2 < L) x0n = xs.fetch(0, t + 2);
+      gates(0, xs.make(0, t + 1, x0), acc0);
     }
     cell(1, t, acc1, last);
     if (!last) __syncthreads();
   }
+}
+
+template <int H, bool HSEQ>
+__global__ __launch_bounds__(H * 4) void lstm_fwd_pipe_kernel(const uint4* __restrict__ xa /*[B, L, 2] x 16 B*/,
+                                                              int64_t B, int L, const uint4* __restrict__ Wpack,
+                                                              const float* __restrict__ h0,
+                                                              const float* __restrict__ c0,
+                                                              float* __restrict__ h_out, float* __restrict__ c_out,
+                                                              unsigned short* __restrict__ hseq) {
+  __shared__ __attribute__((aligned(16))) unsigned short hbuf[64 * (H + 8)];
+  XaSource xs;
+  xs.setup(xa, (int64_t)blockIdx.x * 64, B, L, lane_id() & 31, lane_id() >> 5);
+  lstm_pipe_body<H, HSEQ>(xs, B, L, Wpack, h0, c0, h_out, c_out, hseq, hbuf);
+}
+
+// The univariate forecaster straight from the history: sequence b is row
+// rm[b] (or b) of hist [., ld], dense columns [T - L, T) read at grid column
+// c - (shift[b] - dk) below lim[b] + dk (shift / lim null: the row as is, T
+// columns).  The workgroup's 64 sequences are z-scored in a prologue (mu /
+// sd also written out for the forecast's de-normalisation).
+template <int H>
+__global__ __launch_bounds__(H * 4) void lstm_fwd_hist_kernel(const float* __restrict__ hist, int64_t ld, int T,
+                                                              const int* __restrict__ rm,
+                                                              const int* __restrict__ shift,
+                                                              const int* __restrict__ lim, int dk, int64_t B, int L,
+                                                              float period, int I, const uint4* __restrict__ Wpack,
+                                                              float* __restrict__ h_out, float* __restrict__ c_out,
+                                                              float* __restrict__ mu_out, float* __restrict__ sd_out) {
+  __shared__ __attribute__((aligned(16))) unsigned short hbuf[64 * (H + 8)];
+  __shared__ float smu[64], sinv[64];
+  const int lane = lane_id(), w = wave_id();
+  constexpr int NW = H / 16;
+  const int64_t b0 = (int64_t)blockIdx.x * 64;
+  // prologue: the window statistics of this workgroup's sequences
+  for (int q = w; q < 64; q += NW) {
+    const int64_t bb = b0 + q;
+    float mu = 0.f, sd = 1e-6f;
+    if (bb < B) {
+      const int64_t r = rm != nullptr ? rm[bb] : bb;
+      const int off = shift != nullptr ? dk - shift[bb] : 0;
+      const int lm = lim != nullptr ? lim[bb] + dk : T;
+      const float* hr = hist + r * ld;
+      float s = 0.f;
+      int n = 0;
+      for (int i = lane; i < L; i += 64) {
+        const int bc = T - L + i + off;
+        const float v = (bc >= 0 && bc < lm) ? hr[bc] : __builtin_nanf("");
+        if (isfinite(v)) { s += v; ++n; }
+      }
+      s = wave_sum(s);
+      n = wave_sum(n);
+      mu = s / (float)(n > 0 ? n : 1);
+      float qq = 0.f;
+      for (int i = lane; i < L; i += 64) {
+        const int bc = T - L + i + off;
+        const float v = (bc >= 0 && bc < lm) ? hr[bc] : __builtin_nanf("");
+        if (isfinite(v)) { const float d = v - mu; qq += d * d; }
+      }
+      qq = wave_sum(qq);
+      sd = sqrtf(qq / (float)(n > 0 ? n : 1));
+      sd = sd > 1e-6f ? sd : 1e-6f;
+      if (lane == 0) { mu_out[bb] = mu; sd_out[bb] = sd; }
+    }
+    if (lane == 0) { smu[q] = mu; sinv[q] = 1.f / sd; }
+  }
+  __syncthreads();
+  HistSource xs;
+  const int col = lane & 31;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    int64_t bb = b0 + 32 * ct + col;
+    bb = bb < B ? bb : B - 1;
+    const int64_t r = rm != nullptr ? rm[bb] : bb;
+    xs.row[ct] = hist + r * ld;
+    xs.off[ct] = shift != nullptr ? dk - shift[bb] : 0;
+    xs.lim[ct] = lim != nullptr ? lim[bb] + dk : T;
+    xs.mu[ct] = smu[32 * ct + col];
+    xs.inv[ct] = sinv[32 * ct + col];
+  }
+  xs.c0 = T - L;
+  xs.p = period;
+  xs.ip = 1.f / period;
+  xs.I = I;
+  xs.lo_half = (lane >> 5) == 0;
+  lstm_pipe_body<H, false>(xs, B, L, Wpack, nullptr, nullptr, h_out, c_out, nullptr, hbuf);
+}
+
+FM_API int fm_lstm_forward_hist(const float* hist, int64_t ld, int T, const int* rm, const int* shift, const int* lim,
+                                int dk, int64_t B, int L, int H, float period, int I, const void* Wpack, float* h_out,
+                                float* c_out, float* mu, float* sd, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (L <= 0 || L > T || I < 0 || I > 3 || !(period > 0.f) || (shift == nullptr) != (lim == nullptr))
+    return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((B + 63) / 64));
+#define FM_LSTMH(HH)                                                                                             \
+  hipLaunchKernelGGL(lstm_fwd_hist_kernel<HH>, grid, dim3(HH * 4), 0, stream, hist, ld, T, rm, shift, lim, dk, B, L, \
+                     period, I, (const uint4*)Wpack, h_out, c_out, mu, sd)
+  if (H == 128) FM_LSTMH(128);
+  else if (H == 64) FM_LSTMH(64);
+  else if (H == 32) FM_LSTMH(32);
+  else return (int)hipErrorInvalidValue;
+#undef FM_LSTMH
+  FM_LAUNCH_CHECK();
+  return 0;
 }
 
 // ---------------------------------------------------------------------------

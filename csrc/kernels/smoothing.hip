@@ -896,9 +896,12 @@ FM_API int fm_band_decide(const float* cur, int64_t ld_c, int n, const float* ce
 //   * stats[r] = (nan, nan, upper, lower) at the row's last finite point;
 //   * wave 0 reduces the service (service_reduce_kernel semantics) from LDS;
 //   * anomalous points append (row, point), value through one atomic per row
-//     to ctr[par]; block 0 zeroes ctr[par ^ 1] for the next cycle.
+//     to ctr[par]; block 0 zeroes ctr[par ^ 1] for the next cycle, and the
+//     last workgroup to finish (done count ctr[2 + par]) copies ctr[par]
+//     into hostv.
 // Host outputs land in one buffer (hostv: packed [S,4] | stats [R,4] | count
-// [R] (int) | dead [R] (int) ) for a single device->host copy.
+// [R] (int) | dead [R] (int) | counters [2] (int)) for a single device->host
+// copy.
 // ---------------------------------------------------------------------------
 constexpr int kStepKMax = 64;      // new samples per row per cycle handled in-kernel
 constexpr int kStepMMax = 16;      // metrics per service (waves per workgroup)
@@ -926,71 +929,81 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
   const int64_t R = S * M;
   const int64_t row = s * M + mi;
   if (blockIdx.x == 0 && threadIdx.x == 0) ctr[par ^ 1] = 0;
-  const int64_t sl = slots[row];
-  int k0 = t_new[row];
-  k0 = k0 < 0 ? 0 : (k0 > kmax ? kmax : k0);
-  // the tail columns [T - kmax, T) of the row, from the grid
-  {
-    const int64_t g = rm[row];
-    const int off = dk - shift[row];
-    const int lm = lim[row] + dk;
-    if (lane < kmax) {
-      const int c = T - kmax + lane + off;
-      xs[mi][lane] = (c >= 0 && c < lm) ? buf[g * ld + c] : __builtin_nanf("");
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
   float lvl = 0.f, tr = 0.f, sig = 0.f;
-  int ph = 0;
-  const int k = kmax - k0;
-  if (lane == 0) {
-    EsModel<KIND> md{params[sl * 3 + 0], params[sl * 3 + 1], params[sl * 3 + 2], state[sl * 3 + 0],
-                     state[sl * 3 + 1]};
-    ph = KIND >= 2 ? (int)state[sl * 3 + 2] : 0;
-    const int ph0 = ph;
-    double err2 = sse[sl];
-    int nn = nobs[sl];
-    float* srow = KIND >= 2 ? season + sl * m : season;
-    es_run<KIND, false>(md, &xs[mi][0], k0, kmax, k0, m, srow, 1, 0, ph, err2, nn);
-    sse[sl] = (float)err2;
-    state[sl * 3 + 0] = md.lvl;
-    state[sl * 3 + 1] = md.tr;
-    state[sl * 3 + 2] = (float)ph;
-    nobs[sl] = nn;
-    lvl = md.lvl;
-    tr = md.tr;
-    sig = nn > 1 ? sqrtf((float)err2 / (float)(nn - 1)) : 0.f;
-    sigma_out[row] = sig;
-    if (KIND >= 2) {
-      int p = ph0;
-      for (int j = 0; j < k; ++j) {     // this thread's own stores: program order
-        su[mi][j] = srow[p];
-        if (++p == m) p = 0;
+  int ph = 0, ph_old = 0, k = 0;
+  const float* srow = season;
+  if constexpr (KIND >= 0) {
+    const int64_t sl = slots[row];
+    int k0 = t_new[row];
+    k0 = k0 < 0 ? 0 : (k0 > kmax ? kmax : k0);
+    // the tail columns [T - kmax, T) of the row, from the grid
+    {
+      const int64_t g = rm[row];
+      const int off = dk - shift[row];
+      const int lm = lim[row] + dk;
+      if (lane < kmax) {
+        const int c = T - kmax + lane + off;
+        xs[mi][lane] = (c >= 0 && c < lm) ? buf[g * ld + c] : __builtin_nanf("");
       }
     }
-    reinterpret_cast<int*>(hostv)[S * 4 + R * 4 + R + row] = (isfinite(lvl) && isfinite(tr)) ? 0 : 1;
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  lvl = __shfl(lvl, 0);
-  tr = __shfl(tr, 0);
-  sig = __shfl(sig, 0);
-  ph = __shfl(ph, 0);
-  const int ph_old = KIND >= 2 ? ((ph - k) % m + m) % m : 0;
-  const float* srow = KIND >= 2 ? season + sl * m : season;
-  auto fcast = [&](int h) -> float {
-    float f = lvl + (KIND >= 1 ? (float)h * tr : 0.f);
-    if (KIND >= 2) {
-      const int idx = (ph + h - 1) % m;
-      int d = idx - ph_old;
-      d = d < 0 ? d + m : d;
-      const float sv = d < k ? su[mi][d] : srow[idx];
-      f = KIND == 3 ? f * sv : f + sv;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    k = kmax - k0;
+    if (KIND >= 2) srow = season + sl * m;
+    if (lane == 0) {
+      EsModel<KIND> md{params[sl * 3 + 0], params[sl * 3 + 1], params[sl * 3 + 2], state[sl * 3 + 0],
+                       state[sl * 3 + 1]};
+      ph = KIND >= 2 ? (int)state[sl * 3 + 2] : 0;
+      const int ph0 = ph;
+      double err2 = sse[sl];
+      int nn = nobs[sl];
+      es_run<KIND, false>(md, &xs[mi][0], k0, kmax, k0, m, season + (KIND >= 2 ? sl * m : 0), 1, 0, ph, err2, nn);
+      sse[sl] = (float)err2;
+      state[sl * 3 + 0] = md.lvl;
+      state[sl * 3 + 1] = md.tr;
+      state[sl * 3 + 2] = (float)ph;
+      nobs[sl] = nn;
+      lvl = md.lvl;
+      tr = md.tr;
+      sig = nn > 1 ? sqrtf((float)err2 / (float)(nn - 1)) : 0.f;
+      sigma_out[row] = sig;
+      if (KIND >= 2) {
+        int p = ph0;
+        for (int j = 0; j < k; ++j) {     // this thread's own stores: program order
+          su[mi][j] = srow[p];
+          if (++p == m) p = 0;
+        }
+      }
+      reinterpret_cast<int*>(hostv)[S * 4 + R * 4 + R + row] = (isfinite(lvl) && isfinite(tr)) ? 0 : 1;
     }
-    return f;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    lvl = __shfl(lvl, 0);
+    tr = __shfl(tr, 0);
+    sig = __shfl(sig, 0);
+    ph = __shfl(ph, 0);
+    ph_old = KIND >= 2 ? ((ph - k) % m + m) % m : 0;
+  } else {
+    // a forecast computed elsewhere (LSTM, Prophet): fc [R, Hf] and sigma are inputs
+    sig = sigma_out[row];
+    if (lane == 0) reinterpret_cast<int*>(hostv)[S * 4 + R * 4 + R + row] = 0;
+  }
+  auto fcast = [&](int h) -> float {
+    if constexpr (KIND < 0) {
+      return fc[row * Hf + (h - 1)];
+    } else {
+      float f = lvl + (KIND >= 1 ? (float)h * tr : 0.f);
+      if (KIND >= 2) {
+        const int idx = (ph + h - 1) % m;
+        int d = idx - ph_old;
+        d = d < 0 ? d + m : d;
+        const float sv = d < k ? su[mi][d] : srow[idx];
+        f = KIND == 3 ? f * sv : f + sv;
+      }
+      return f;
+    }
   };
-  if (fc != nullptr) {
+  if (KIND >= 0 && fc != nullptr) {
     for (int h = 1 + lane; h <= Hf; h += 64) fc[row * Hf + (h - 1)] = fcast(h);
   }
   // band decision (band_decide_kernel + zoo.band's history gate)
@@ -1067,6 +1080,17 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
     s_valid[mi] = vld;
   }
   __syncthreads();
+  if (mi == 0 && lane == 0) {
+    // the last workgroup to finish publishes the counter into hostv (one
+    // device->host copy of hostv carries everything) and re-arms its slot
+    __threadfence();
+    const int done = atomicAdd(&ctr[2 + par], 1);
+    if (done == (int)gridDim.x - 1) {
+      __threadfence();
+      reinterpret_cast<int*>(hostv)[S * 4 + R * 6 + par] = atomicAdd(&ctr[par], 0);
+      ctr[2 + par] = 0;
+    }
+  }
   if (mi == 0 && lane == 0) {    // service_reduce_kernel semantics
     int tot = 0, mask = 0;
     bool unknown = false;
@@ -1094,8 +1118,10 @@ FM_API int fm_es_band_step(const float* buf, int64_t ld, const int* rm, const in
                            float* hostv, int cap, int* ctr, int par, int* out_idx, float* out_val,
                            hipStream_t stream) {
   if (S <= 0) return 0;
-  if (kind < 0 || kind > 3 || M < 1 || M > kStepMMax || kmax < 1 || kmax > kStepKMax || kmax > T || n < 1 ||
-      n > 256 || H < 1 || (kind >= 2 && m < 2) || (fc != nullptr && Hf < 1) || (par != 0 && par != 1))
+  // kind -1: the forecast fc [R, Hf] (Hf >= H) and sigma are given (band + reduce + compaction only)
+  if (kind < -1 || kind > 3 || M < 1 || M > kStepMMax || n < 1 || n > 256 || H < 1 || (par != 0 && par != 1) ||
+      (kind >= 0 && (kmax < 1 || kmax > kStepKMax || kmax > T || (kind >= 2 && m < 2))) ||
+      (fc != nullptr && Hf < 1) || (kind < 0 && (fc == nullptr || Hf < H || sigma == nullptr)))
     return (int)hipErrorInvalidValue;
   if (kind < 2) m = 1;
   const dim3 grid((unsigned)S), block((unsigned)(64 * M));
@@ -1103,7 +1129,8 @@ FM_API int fm_es_band_step(const float* buf, int64_t ld, const int* rm, const in
   hipLaunchKernelGGL(es_band_step_kernel<KK>, grid, block, 0, stream, buf, ld, rm, shift, lim, dk, T, kmax, t_new, \
                      slots, params, m, season, sse, state, nobs, cur, ld_c, n, hor, H, S, M, thr, bound, minlb, diff, \
                      pair_factor, valid, lastk, upper, lower, sigma, fc, Hf, hostv, cap, ctr, par, out_idx, out_val)
-  if (kind == 0) FM_EBS(0);
+  if (kind == -1) FM_EBS(-1);
+  else if (kind == 0) FM_EBS(0);
   else if (kind == 1) FM_EBS(1);
   else if (kind == 2) FM_EBS(2);
   else FM_EBS(3);

@@ -468,14 +468,17 @@ class FastPath:
         self.max_idle_cycles = 64
         self._cmp = {}            # device compaction buffers per capacity
         self._fused_cmp = {}      # the fused steady-cycle kernel's compaction buffers + counters
+        self._rmd = {}            # group key -> (row map, its int32 / int64 device copies)
         self._fused_par = 0       # which of the two counters the next fused launch appends to
         self._es_plan = None      # (keys, cache lookup) a declined fused cycle hands to es_forecast
         self.fused_steps = 0
+        self.fused_declined: dict[str, int] = {}   # why a forecasting group's cycle took the op-by-op path
         self._col: dict = {}      # column-wise fetched windows of sliding groups (consumed by _arrays)
         self._ring = None         # merged sliding mode: host ring of the newest grid columns
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
         self._slide_state: dict = {}
         self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
+        self.model_churns = 0      # ModelArrays restricted to a churned job list instead of rebuilt
         self._hist_pending = False  # a per-job fetch left history in some FastWork.hist this cycle
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
@@ -1344,12 +1347,18 @@ class FastPath:
         up = lambda a: (torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"
                         else torch.from_numpy(a))
         has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
-        rm_d = up(rowmap)
+        rmc = self._rmd.get(key)
+        if rmc is not None and rmc[0] is rowmap:          # the row map of an unchanged job list: on the device
+            rm_d, rml = rmc[1], rmc[2]
+        else:
+            rm_d, rml = up(rowmap), None
         devc = col.get("dev") if pos is not None else None
         if devc is not None and devc[0] is not None and (base is None or devc[1] is not None):
             # merged sliding windows: read out of the device grid the samples
             # were just written to (no rows x points upload)
-            rml = rm_d.long()
+            if rml is None:
+                rml = rm_d.long()
+            self._rmd[key] = (rowmap, rm_d, rml)
             grab = lambda ab: store.buf[:, ab[0]:ab[1]].index_select(0, rml)   # noqa: E731
             cur_d, base_d = grab(devc[0]), (grab(devc[1]) if base is not None else None)
             has_cur = (cur_len > 0).reshape(S, M)
@@ -1361,8 +1370,14 @@ class FastPath:
         if col is not None and pos is not None:
             ga.hist_end = col.get("hist_end")
             old = self._garr.get(key)
-            if old is not None and old.ident == ident:
-                ga.prev_models = old.models if old.models is not None else old.prev_models
+            if old is not None:
+                pm = old.models if old.models is not None else old.prev_models
+                if old.ident == ident:
+                    ga.prev_models = pm
+                elif isinstance(pm, ModelArrays) and pm.inc is not None:
+                    ix = ident.index_in(old.ident)            # jobs left the list (fleet churn)
+                    if ix is not None:
+                        ga.prev_models = ("churn", pm, ix)
         if xslots is not None:
             ga.export_slots = xslots
             ga.export_start = self.b.exporter.contiguous_start(xslots)
@@ -1667,6 +1682,8 @@ class FastPath:
             return md
         prev = md if md is not None else ga.prev_models
         ga.prev_models = None
+        if isinstance(prev, tuple):
+            prev = self._model_arrays_churn(prev[1], prev[2], ga, works, store) if store.sliding else None
         if prev is not None and store.sliding and prev.inc is not None:
             nd = self._model_arrays_slid(prev, ga, store, stamp)
             if nd is not None:
@@ -1758,6 +1775,48 @@ class FastPath:
             # state for the next cycle's shift-only update (_model_arrays_slid)
             md.inc = (t_last, T, store.t0, store.ws, n, float(ga.cur_t[0, 0]), valid, lastk)
         return md
+
+    def _model_arrays_churn(self, md: "ModelArrays", ix: np.ndarray, ga: GroupArrays, works: list[FastWork],
+                            store: ResidentHistory) -> "ModelArrays | None":
+        """The previous cycle's ModelArrays of a job list that has since only
+        lost jobs (fleet churn): every per-row array restricted to the
+        surviving jobs (device rows index-selected, host rows fancy-indexed),
+        ready for the shift-only slide -- instead of rebuilding and uploading
+        them all.  None when the dense length changed (a rebuild aligns
+        differently)."""
+        from ..models import zoo
+        p0 = works[0].plan
+        M, S = len(p0.aliases), len(works)
+        T, _, _ = self._alignment(ga.rowmap.astype(np.int64), store, ga.hist_end)
+        if any(sb.T != T for sb in md.subs) or md.inc is None:
+            return None
+        dev = self.b.device
+        rsel = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+        subs = []
+        for sb in md.subs:
+            q = len(sb.ms)
+            loc = (ix[:, None] * q + np.arange(q)[None, :]).reshape(-1)
+            loc_d = torch.from_numpy(loc).to(dev)
+            pick = lambda t: None if t is None else t.index_select(0, loc_d)      # noqa: E731
+            if q == M:
+                idx, rows = None, None
+            else:
+                rows = (np.arange(S)[:, None] * M + np.asarray(sb.ms)[None, :]).reshape(-1)
+                idx = torch.as_tensor(rows, device=dev)
+            keys = sb.keys
+            if sb.algo in zoo.ES_KINDS:
+                kv, full = self._cache_keys(works, p0, sb.algo)
+                keys = full if idx is None else kv[rows].tolist()
+            elif keys is not None:
+                keys = [keys[i] for i in loc.tolist()]
+            subs.append(replace(sb, idx=idx, rm=pick(sb.rm), shift=pick(sb.shift), lim=pick(sb.lim), keys=keys,
+                                t_last=None if sb.t_last is None else sb.t_last[loc], valid=pick(sb.valid),
+                                hor=pick(sb.hor)))
+        t_prev, T0, t0, ws, n, ct0, valid_prev, lastk_prev = md.inc
+        nd = ModelArrays(md.stamp, subs, md.lastk.index_select(0, torch.from_numpy(rsel).to(dev)))
+        nd.inc = (t_prev[rsel], T0, t0, ws, n, ct0, valid_prev[rsel], lastk_prev[rsel])
+        self.model_churns += 1
+        return nd
 
     def _model_arrays_slid(self, md: "ModelArrays", ga: GroupArrays, store: ResidentHistory, stamp):
         """The previous cycle's ModelArrays moved by a sliding step: when every
@@ -1898,15 +1957,16 @@ class FastPath:
 
     def _score_fused(self, works: list[FastWork], ga: GroupArrays, md: "ModelArrays", store: ResidentHistory,
                      diff, hpa_algo) -> dict | None:
-        """The steady cycle of a single-model ES / Holt-Winters group as one
-        kernel (``fm_es_band_step``: advance the cached models over the new
-        samples read straight from the resident grid, band-judge every
-        current point, reduce per service, compact the anomalies) and one
-        device->host copy.  None when the cycle is not steady (a row misses
-        the model cache, rows span several cache slabs, more than 64 new
-        samples, wider windows): the caller takes the general path."""
+        """The steady cycle of a single-model forecasting group as one kernel
+        (``fm_es_band_step``) and one device->host copy.  ES / Holt-Winters:
+        advance the cached models over the new samples read straight from the
+        resident grid; LSTM / Prophet: their forecast first (the LSTM kernel
+        also reads the grid directly); then band-judge every current point,
+        reduce per service and compact the anomalies in the same launch.  None
+        when the cycle does not fit (a row misses the model cache, rows span
+        several cache slabs, more than 64 new samples, wider windows): the
+        caller takes the op-by-op path."""
         from ..models import zoo
-        from ..ops._lib import LIB, ptr, stream_of
         sub = md.subs[0]
         algo = sub.algo
         b = self.b
@@ -1916,29 +1976,53 @@ class FastPath:
         M, S = len(p0.aliases), len(works)
         R = S * M
         n = ga.cur.shape[1]
-        if (kind is None or cache.capacity <= 0 or sub.idx is not None or sub.hor is None or not 1 <= n <= 256
-                or M > 16 or sub.keys is None or ga.cur_d.stride(1) != 1 or sub.hor.shape != (R, n)):
-            return None
-        plan = cache.es_lookup(sub.keys, sub.t_last, b.step, b.clock(), sub.T, kind)
-        if not plan.usable.all() or len(plan.slabs) != 1:
-            self._es_plan = (sub.keys, plan, self.cycle)         # es_forecast reuses the lookup
-            return None
-        slab = plan.slabs[0]
-        if (plan.sid != slab.sid).any():
-            self._es_plan = (sub.keys, plan, self.cycle)
-            return None
-        kmax = max(int(plan.knew.max()), 1)
-        if kmax > 64 or kmax > sub.T:
-            self._es_plan = (sub.keys, plan, self.cycle)
+        why = ("model" if kind is None and algo not in ("lstm", "prophet") else "cache off"
+               if kind is not None and cache.capacity <= 0 else "metric subset" if sub.idx is not None
+               else "horizons" if sub.hor is None or sub.hor.shape != (R, n) else "window width"
+               if not 1 <= n <= 256 else "metrics" if M > 16 else "keys" if kind is not None and sub.keys is None
+               else "layout" if ga.cur_d.stride(1) != 1 else None)
+        if why is not None:
+            self.fused_declined[why] = self.fused_declined.get(why, 0) + 1
             return None
         H = sub.H
         if hpa_algo == algo:
             H = max(H, max(1, b.cfg.hpa_forecast_steps))
+        if kind is None:
+            # a forecaster without a fitted-state cache: its forecast, then the
+            # fused band / reduce / compaction over it
+            fc, sig = self._forecast(algo, LazyHist(store.buf, sub.rm, *sub.shift_lim(), sub.T), sub, H)
+            fc, sig = fc.contiguous(), sig.contiguous()
+            out = self._fused_launch(works, ga, md, store, diff, -1, None, None, 0, H=fc.shape[1], fc=fc, sig=sig)
+            self.fused_steps += 1
+            out["fc"] = {algo: (sub, fc)} if hpa_algo == algo else {}
+            return out
+        plan = cache.es_lookup(sub.keys, sub.t_last, b.step, b.clock(), sub.T, kind)
+        kmax = max(int(plan.knew.max()), 1) if len(plan.knew) else 1
+        why = ("cache miss" if not plan.usable.all() else "several slabs" if len(plan.slabs) != 1
+               or (plan.sid != plan.slabs[0].sid).any() else "gap" if kmax > 64 or kmax > sub.T else None)
+        if why is not None:
+            self.fused_declined[why] = self.fused_declined.get(why, 0) + 1
+            self._es_plan = (sub.keys, plan, self.cycle)         # es_forecast reuses the lookup
+            return None
+        fc = torch.empty((R, H), dtype=torch.float32, device=ga.cur_d.device) if hpa_algo == algo else None
+        out = self._fused_launch(works, ga, md, store, diff, kind, plan, plan.slabs[0], kmax, H=H, fc=fc)
+        cache.hits += R
+        self.fused_steps += 1
+        out["fc"] = {algo: (sub, fc)} if fc is not None else {}
+        return out
+
+    def _fused_launch(self, works, ga: GroupArrays, md: "ModelArrays", store: ResidentHistory, diff, kind: int,
+                      plan, slab, kmax: int, H: int, fc=None, sig=None) -> dict:
+        from ..ops._lib import LIB, ptr, stream_of
+        sub = md.subs[0]
+        p0 = works[0].plan
+        M, S = len(p0.aliases), len(works)
+        R = S * M
+        n = ga.cur.shape[1]
         dev = ga.cur_d.device
         # per-row inputs that only change when the job list or the cache
         # slots do: uploaded once, kept on the arrays
         fz = getattr(ga, "_fused", None)
-        t_new = (kmax - plan.knew).astype(np.int32)
         if fz is None or fz["R"] != R or fz["n"] != n:
             fz = {"R": R, "n": n, "slots": None, "t_new": None,
                   "up": torch.empty((R, n), dtype=torch.float32, device=dev),
@@ -1947,33 +2031,39 @@ class FastPath:
                   "hostv": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32, device=dev),
                   "host": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32).pin_memory()}
             ga._fused = fz
-        if fz["slots"] is None or not np.array_equal(fz["slots"][0], plan.slot):
-            fz["slots"] = (plan.slot.copy(), torch.from_numpy(plan.slot.astype(np.int64)).to(dev))
-        if fz["t_new"] is None or not np.array_equal(fz["t_new"][0], t_new):
-            fz["t_new"] = (t_new, torch.from_numpy(t_new).to(dev))
-        fc = torch.empty((R, H), dtype=torch.float32, device=dev) if hpa_algo == algo else None
+        st = None
+        if kind >= 0:
+            t_new = (kmax - plan.knew).astype(np.int32)
+            if fz["slots"] is None or not np.array_equal(fz["slots"][0], plan.slot):
+                fz["slots"] = (plan.slot.copy(), torch.from_numpy(plan.slot.astype(np.int64)).to(dev))
+            if fz["t_new"] is None or not np.array_equal(fz["t_new"][0], t_new):
+                fz["t_new"] = (t_new, torch.from_numpy(t_new).to(dev))
+            st = slab.as_state()
         buf = self._fused_cmp.get(dev)
         if buf is None or buf[0].shape[0] < R * n:
             cap = max(R * n, 1024)
             buf = self._fused_cmp[dev] = (torch.empty((cap, 2), dtype=torch.int32, device=dev),
                                           torch.empty((cap,), dtype=torch.float32, device=dev),
-                                          torch.zeros((2,), dtype=torch.int32, device=dev))
+                                          torch.zeros((4,), dtype=torch.int32, device=dev))
         idx_d, val_d, ctr = buf
         par = self._fused_par
         self._fused_par ^= 1
         hv = fz["hostv"]
-        st = slab.as_state()
         tb = sub.tables
         cur = ga.cur_d
+        sig_t = sig if kind < 0 else fz["sig"]
         LIB.call("fm_es_band_step", ptr(store.buf), store.buf.stride(0), ptr(sub.rm), ptr(sub.shift), ptr(sub.lim),
-                 int(sub.dk), int(sub.T), kmax, ptr(fz["t_new"][1]), ptr(fz["slots"][1]), ptr(st.params),
-                 int(slab.m), kind, ptr(st.season) if st.season is not None else None, ptr(st.sse), ptr(st.state),
-                 ptr(st.nobs), ptr(cur), cur.stride(0), n, ptr(sub.hor), int(H), S, M, ptr(tb.thr), ptr(tb.bound),
-                 ptr(tb.minlb), ptr(diff), float(tb.pair_factor), ptr(sub.valid), ptr(md.lastk), ptr(fz["up"]),
-                 ptr(fz["lo"]), ptr(fz["sig"]), ptr(fc), int(H), ptr(hv), int(idx_d.shape[0]), ptr(ctr), par,
+                 int(sub.dk), int(sub.T), int(kmax), ptr(fz["t_new"][1]) if st is not None else None,
+                 ptr(fz["slots"][1]) if st is not None else None, ptr(st.params) if st is not None else None,
+                 int(slab.m) if st is not None else 1, int(kind),
+                 ptr(st.season) if st is not None and st.season is not None else None,
+                 ptr(st.sse) if st is not None else None, ptr(st.state) if st is not None else None,
+                 ptr(st.nobs) if st is not None else None, ptr(cur), cur.stride(0), n, ptr(sub.hor), int(H), S, M,
+                 ptr(tb.thr), ptr(tb.bound), ptr(tb.minlb), ptr(diff), float(tb.pair_factor), ptr(sub.valid),
+                 ptr(md.lastk), ptr(fz["up"]), ptr(fz["lo"]), ptr(sig_t), ptr(fc),
+                 int(fc.shape[1]) if fc is not None else 0, ptr(hv), int(idx_d.shape[0]), ptr(ctr), par,
                  ptr(idx_d), ptr(val_d), stream_of(cur))
-        # counter of this launch into the host buffer's tail, then ONE copy
-        hv[S * 4 + R * 6:].view(torch.int32).copy_(ctr, non_blocking=True)
+        # the kernel's last workgroup wrote this launch's counter into hv: ONE copy
         host = fz["host"]
         host.copy_(hv, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
@@ -1982,19 +2072,17 @@ class FastPath:
         stats_h = hn[S * 4:S * 4 + R * 4].reshape(R, 4).copy()
         ints = hn[S * 4 + R * 4:].view(np.int32)
         count_h = ints[:R].copy()
-        dead = ints[R:2 * R] != 0
         total = int(ints[2 * R + par])
-        cache.es_commit(slab, plan.slot, plan.t_last, dead)
-        cache.hits += R
+        if kind >= 0:
+            self.b.model_cache.es_commit(slab, plan.slot, plan.t_last, ints[R:2 * R] != 0)
         idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
         if len(idx):
             kk = idx[:, 0].astype(np.int64) * n + idx[:, 1]
             kk.sort()
             idx = np.stack([kk // n, kk % n], 1).astype(np.int32)
-        self.fused_steps += 1
         return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
                 "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "hist_rows": ga.rowmap,
-                "store": store, "pts": (fz["up"], fz["lo"]), "fc": {algo: (sub, fc)} if fc is not None else {}}
+                "store": store, "pts": (fz["up"], fz["lo"])}
 
     def _forecast(self, algo: str, lazy: "LazyHist", sub: "ModelSub", H: int):
         from ..models import zoo
@@ -2008,6 +2096,11 @@ class FastPath:
         lstm = b.lstm_for_jobs_of({sub.M}) if algo == "lstm" else b.lstm_model
         if ctx is not None:
             hist = lazy                                   # hits read only their new columns
+        elif algo == "lstm" and lstm is not None and lstm.reads_rows and lazy.is_cuda:
+            # the LSTM kernel reads its window straight from the resident grid
+            # (no gather, no feature tensor: fm_lstm_forward_hist)
+            return lstm.forecast_rows(lazy.src, lazy.rm, lazy.shift.to(torch.int32), lazy.lim.to(torch.int32), 0,
+                                      sub.T, H)
         elif algo == "lstm":
             hist = lazy.materialize(sub.T - min(lstm.L, sub.T))
         else:

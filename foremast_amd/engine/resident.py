@@ -90,6 +90,7 @@ class ResidentHistory:
         if capacity:
             self._grow(capacity)
         self.compactions = 0
+        self._gone = None                           # (device, pinned) finite counts of retired columns
         self.bytes_in = 0
         self.max_len = 0                            # static: longest row written (view length)
 
@@ -224,9 +225,22 @@ class ResidentHistory:
         lo, hi = max(0, self.ws), max(0, ws_new)
         if hi > lo and self.buf.shape[0]:
             # finite samples leaving the window no longer count (history gate)
-            gone = torch.isfinite(self.buf[:, lo:min(hi, self.width)]).sum(1).cpu().numpy()
+            hi = min(hi, self.width)
+            if self.device.type == "cuda":
+                from ..ops._lib import LIB, ptr, stream_of
+                R = self.buf.shape[0]
+                if self._gone is None or self._gone[0].numel() < R:
+                    self._gone = (torch.empty((R,), dtype=torch.int32, device=self.device),
+                                  torch.empty((R,), dtype=torch.int32).pin_memory())
+                gd, gh = self._gone
+                LIB.call("fm_grid_retire", ptr(self.buf), self.buf.stride(0), R, lo, hi, ptr(gd), stream_of(self.buf))
+                gh[:R].copy_(gd[:R], non_blocking=True)
+                torch.cuda.current_stream(self.device).synchronize()
+                gone = gh[:R].numpy()
+            else:
+                gone = torch.isfinite(self.buf[:, lo:hi]).sum(1).numpy()
+                self.buf[:, lo:hi] = float("nan")
             self.nfin -= gone.astype(np.int64)
-            self.buf[:, lo:min(hi, self.width)] = float("nan")
         self.e, self.ws = e_new, max(ws_new, 0)
 
     def _compact(self, ws_new: int) -> None:
@@ -280,10 +294,17 @@ class ResidentHistory:
             else:
                 np.add.at(self.nfin, r[c > prev], 1)      # new columns only (a re-sent sample counts once)
                 np.maximum.at(self.last_t, r, t)
-            flat = torch.from_numpy(r * self.width + c)
-            vals = torch.from_numpy(np.ascontiguousarray(v))
+            n = len(r)
             if self.device.type == "cuda":
-                flat = flat.pin_memory().to(self.device, non_blocking=True)
-                vals = vals.pin_memory().to(self.device, non_blocking=True)
+                # indices and values in ONE pinned buffer, one host->device copy
+                hb = torch.empty((3 * n,), dtype=torch.int32).pin_memory()
+                hn = hb.numpy()
+                hn[:2 * n].view(np.int64)[:] = r * self.width + c
+                hn[2 * n:].view(np.float32)[:] = v
+                db = hb.to(self.device, non_blocking=True)
+                flat, vals = db[:2 * n].view(torch.int64), db[2 * n:].view(torch.float32)
+            else:
+                flat = torch.from_numpy(r * self.width + c)
+                vals = torch.from_numpy(np.ascontiguousarray(v))
             self.buf.view(-1).index_copy_(0, flat, vals)
             self.bytes_in += v.nbytes + 8 * len(r)

@@ -119,6 +119,35 @@ class LSTMForecaster:
         finally:
             self.I = I
 
+    @property
+    def reads_rows(self) -> bool:
+        """The GPU forward takes history rows directly (:meth:`forecast_rows`):
+        univariate, one layer, register-resident kernel."""
+        return self.M is None and not self.stacked
+
+    @torch.no_grad()
+    def forecast_rows(self, src: torch.Tensor, rm: torch.Tensor | None, shift: torch.Tensor | None,
+                      lim: torch.Tensor | None, dk: int, T: int, H: int, B: int | None = None):
+        """:meth:`forecast` of the rows ``src[rm]`` of a resident grid
+        (LazyHist's row map / alignment), read by the LSTM kernel itself: the
+        window is never gathered and no feature tensor is written."""
+        assert self.reads_rows and src.is_cuda
+        L = min(self.L, T)
+        hT, _, mu, sd = LS.lstm_forward_hist(src, T, L, self.period, self.I, self.packed(), self.H, rm, shift, lim,
+                                             dk, B)
+        return self._head(hT, mu, sd, hT.shape[0], H)
+
+    def _head(self, hT, mu, sd, R: int, H: int):
+        W = self.head.weight.to(hT.device)
+        b = self.head.bias.to(hT.device)
+        z = hT @ W.T + b                                    # [rows, horizon (x M)]
+        if self.M is not None:
+            z = z.reshape(-1, self.M, self.horizon).reshape(R, self.horizon)
+        if H > self.horizon:
+            z = torch.cat([z, z[:, -1:].expand(-1, H - self.horizon)], 1)
+        fc = mu[:, None] + sd[:, None] * z[:, :H]
+        return fc.contiguous(), sd.contiguous()
+
     @torch.no_grad()
     def forecast(self, hist: torch.Tensor, T: int, H: int):
         """-> (forecast [R, H] in data units, sigma [R]) with sigma = window std.
@@ -127,6 +156,8 @@ class LSTMForecaster:
         if self.M is not None:
             assert R % self.M == 0, "multivariate forecaster: rows must be services x n_metrics"
         L = min(self.L, T)
+        if hist.is_cuda and self.reads_rows and hist.stride(1) == 1 and hist.dtype == torch.float32:
+            return self.forecast_rows(hist, None, None, None, 0, T, H, B=R)
         if hist.is_cuda:
             # features written by a HIP kernel straight into the bf16 augmented layout
             if self.M is not None:
@@ -139,15 +170,7 @@ class LSTMForecaster:
             with torch.no_grad():
                 _, (h, _) = self.lstm(x)
                 hT = h[-1]
-        W = self.head.weight.to(hT.device)
-        b = self.head.bias.to(hT.device)
-        z = hT @ W.T + b                                    # [rows, horizon (x M)]
-        if self.M is not None:
-            z = z.reshape(-1, self.M, self.horizon).reshape(R, self.horizon)
-        if H > self.horizon:
-            z = torch.cat([z, z[:, -1:].expand(-1, H - self.horizon)], 1)
-        fc = mu[:, None] + sd[:, None] * z[:, :H]
-        return fc.contiguous(), sd.contiguous()
+        return self._head(hT, mu, sd, R, H)
 
     # ------------------------------------------------------------------ training
     def fit(self, hist: torch.Tensor, T: int, epochs: int = 2, batch: int = 256, lr: float = 1e-3,

@@ -226,6 +226,35 @@ def lstm_forward_packed(xa: torch.Tensor, packed: torch.Tensor, H: int, h0=None,
     return hT, cT, seq
 
 
+def lstm_forward_hist(hist: torch.Tensor, T: int, L: int, period: float, I: int, packed: torch.Tensor, H: int,
+                      rm: torch.Tensor | None = None, shift: torch.Tensor | None = None,
+                      lim: torch.Tensor | None = None, dk: int = 0, B: int | None = None):
+    """The univariate forecaster's LSTM straight from the history rows
+    (csrc/kernels/lstm.hip ``fm_lstm_forward_hist``): the window features
+    (z-score, daily phase) are computed in the kernel, no [B, L, 16] input.
+    Sequence b reads row ``rm[b]`` of ``hist`` (or row b), dense columns
+    [T - L, T) at ``c - (shift[b] - dk)`` below ``lim[b] + dk`` (a resident
+    grid row, engine/fastpath.LazyHist) or the row as is.
+    -> (h_L [B, H], c_L [B, H], mu [B], sd [B])."""
+    check(hist.dim() == 2 and hist.dtype == torch.float32 and hist.stride(1) == 1, "hist must be [R, T] float32")
+    check(H in SUPPORTED_H and 0 <= I <= 3 and 0 < L <= T and period > 0, "bad LSTM / window parameters")
+    check((shift is None) == (lim is None), "shift and lim go together")
+    require_native(hist)
+    B = int(rm.numel()) if rm is not None else (hist.shape[0] if B is None else B)
+    d = hist.device
+    for t in (rm, shift, lim):
+        check(t is None or (t.dtype == torch.int32 and t.is_contiguous() and t.numel() == B), "int32 [B] row maps")
+    if rm is None:
+        check(hist.shape[0] >= B and hist.shape[1] >= T, "hist too small")
+    hT = torch.empty((B, H), dtype=torch.float32, device=d)
+    cT = torch.empty((B, H), dtype=torch.float32, device=d)
+    mu = torch.empty((B,), dtype=torch.float32, device=d)
+    sd = torch.empty((B,), dtype=torch.float32, device=d)
+    LIB.call("fm_lstm_forward_hist", ptr(hist), hist.stride(0), T, ptr(rm), ptr(shift), ptr(lim), int(dk), B, L, H,
+             float(period), I, ptr(packed.to(d)), ptr(hT), ptr(cT), ptr(mu), ptr(sd), stream_of(hist))
+    return hT, cT, mu, sd
+
+
 def lstm_features(hist: torch.Tensor, T: int, L: int, period: float, I: int = 3):
     """Augmented forecaster input straight from the packed history (GPU):
     -> (xa [R, L, 16] bf16, mu [R], sd [R]).  Features [z, sin, cos][:I] of the

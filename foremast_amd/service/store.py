@@ -606,7 +606,9 @@ class SQLiteStore(JobStore):
                       "created text not null, aliases text not null, reasons text not null, n integer not null, "
                       "rids blob not null, score blob not null, reason blob not null, vals blob not null)")
             # per job the batches that may hold its entries: a read scans only
-            # [first_bid, last_bid], a job without HPA entries none
+            # [first_bid, last_bid], a job without HPA entries none.  Entries are
+            # keyed by documents.rid: job documents are never deleted from this
+            # store (only hpalog batches age out), so a rid is never reused
             c.execute("create table if not exists hpalog_jobs (rid integer primary key, first_bid integer not null, "
                       "last_bid integer not null)")
             if (c.execute("select 1 from hpalog_batches limit 1").fetchone() is not None

@@ -443,6 +443,49 @@ def test_gpu_lstm_features_and_forecast(cuda):
     torch.testing.assert_close(fc_g.cpu(), fc_c, rtol=5e-2, atol=5e-2 * float(sc.max()))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,I", [(64, 3), (128, 1), (32, 0)])
+def test_gpu_lstm_hist_kernel_matches_feature_path(cuda, H, I):
+    """fm_lstm_forward_hist (the window features computed inside the LSTM
+    kernel, read from the history rows -- or from a resident grid through a
+    row map, shift and limit) == fm_lstm_features + the packed-input kernel."""
+    T, L, R, P = 600, 120, 150, 144.0
+    x = _seasonal(R, T, period=144, seed=H + I)
+    x[5, T - 10] = np.nan
+    x[7, T - L:T - L + 30] = np.nan
+    h = torch.from_numpy(np.ascontiguousarray(np.pad(x, ((0, 0), (0, 4)), constant_values=np.nan))).to(cuda)
+    torch.manual_seed(H)
+    m = torch.nn.LSTM(max(I, 1), H, batch_first=True)
+    w_ih = m.weight_ih_l0.detach()[:, :I] if I else m.weight_ih_l0.detach()[:, :0]
+    pk = LS.pack_lstm(w_ih, m.weight_hh_l0.detach(), (m.bias_ih_l0 + m.bias_hh_l0).detach()).to(cuda)
+    xa, mu0, sd0 = LS.lstm_features(h, T, L, P, I)
+    h0, c0, _ = LS.lstm_forward_packed(xa, pk, H)
+    h1, c1, mu1, sd1 = LS.lstm_forward_hist(h, T, L, P, I, pk, H, B=R)
+    torch.testing.assert_close(mu1, mu0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(sd1, sd0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(h1, h0, rtol=2e-2, atol=2e-2)
+    # the same rows from a "resident grid": permuted, shifted right by a per-row
+    # offset, a slide dk folded in as the kernel's scalar
+    g = torch.Generator().manual_seed(1)
+    perm = torch.randperm(R, generator=g)
+    sh = torch.randint(0, 40, (R,), generator=g)
+    dk = 3
+    W = h.shape[1] + 48
+    grid = torch.full((R + 5, W), float("nan"), device=cuda)
+    hc = h.cpu()
+    for b in range(R):
+        r = int(perm[b])
+        o = int(sh[b])
+        grid[r, o:o + h.shape[1]] = hc[b].to(cuda)
+    rm = perm.to(torch.int32).to(cuda)
+    # dense column c -> grid column c - (shift - dk) = c + o  =>  shift = dk - o; limit: the row's own columns
+    shift = (dk - sh).to(torch.int32).to(cuda)
+    lim = (sh + T - dk).to(torch.int32).to(cuda)
+    h2, c2, mu2, sd2 = LS.lstm_forward_hist(grid, T, L, P, I, pk, H, rm, shift, lim, dk)
+    torch.testing.assert_close(mu2, mu1, rtol=0, atol=0)
+    torch.testing.assert_close(h2, h1, rtol=0, atol=0)
+
+
 def test_ref_lstm_stack_matches_torch_two_layers():
     torch.manual_seed(0)
     m = torch.nn.LSTM(5, 32, num_layers=2, batch_first=True)

@@ -82,6 +82,18 @@ for s in $steps; do
               --reps 5 --methods scan || exit $rc ;;
     pmcscan) run pmcscan 420 bash tools/pmc_hwscan.sh || exit $rc ;;
     configs) for c in 1 2 3 4 5; do run "c$c" 300 python benchmarks/bench_configs.py --config $c || exit $rc; done ;;
+    steady) e2e c2e2e --config 2e2e --steps 20 --warmup 3 &&
+            e2e c4e2e --config 4e2e --steps 20 --warmup 3 || exit $rc ;;
+    tprof) for c in 2e2e 4e2e; do
+             FOREMAST_TORCH_PROFILE=gpurun_out/tprof_$c.txt timeout -k 10 400 python -u benchmarks/bench_configs.py \
+                 --config $c --steps 8 --warmup 3 > gpurun_out/check_tprof_$c.log 2>&1; rc=$?
+             echo "tprof $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+           done ;;
+    prof2e2e) cd /tmp && export TMPDIR=/tmp
+          timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$R/gpurun_out/prof_c2e2e" -o c2e2e -- \
+              python3 "$R/benchmarks/bench_configs.py" --config 2e2e --steps 10 --warmup 2 \
+              > "$R/gpurun_out/check_prof_c2e2e.log" 2>&1; rc=$?
+          echo "prof_c2e2e rc=$rc"; cd "$R"; [ $rc -eq 0 ] || exit $rc ;;
     prof) cd /tmp && export TMPDIR=/tmp
           timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_headline" -o headline -- \
               python3 "$R/bench.py" --steps 50 --warmup 10 > "$R/gpurun_out/check_prof_headline.log" 2>&1; rc=$?
