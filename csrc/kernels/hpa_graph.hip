@@ -20,11 +20,18 @@ __global__ __launch_bounds__(256) void hpa_score_kernel(
     const float* __restrict__ cur, const float* __restrict__ upper, const float* __restrict__ lower, int64_t S, int Mt,
     const float* __restrict__ weight, const int8_t* __restrict__ is_increase, const int8_t* __restrict__ is_absolute,
     const int8_t* __restrict__ role, double now, float breath_up, float breath_down, int max_flips,
-    float flip_window, int8_t* __restrict__ last_dir, double* __restrict__ last_time, int* __restrict__ flips,
-    double* __restrict__ flip_t0, int* __restrict__ score_out, int8_t* __restrict__ reason_out,
-    float* __restrict__ raw_out) {
+    float flip_window, int8_t* __restrict__ last_dir_, double* __restrict__ last_time_, int* __restrict__ flips_,
+    double* __restrict__ flip_t0_, int* __restrict__ score_out, int8_t* __restrict__ reason_out,
+    float* __restrict__ raw_out, const int64_t* __restrict__ slots, int* __restrict__ packed_out) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S) return;
+  // the hysteresis state of service s: slot slots[s] of the device table
+  // (in place, no gather / scatter) or row s of compact state arrays
+  const int64_t q = slots != nullptr ? slots[s] : s;
+  int8_t* last_dir = last_dir_ + q;
+  double* last_time = last_time_ + q;
+  int* flips = flips_ + q;
+  double* flip_t0 = flip_t0_ + q;
   float up = 0.f, down = 0.f;
   bool has_sla = false, sla_violated = false;
   for (int j = 0; j < Mt; ++j) {
@@ -48,26 +55,27 @@ __global__ __launch_bounds__(256) void hpa_score_kernel(
   int raw = 50;
   if (up > 0.f && sla_violated) raw = 50 + (int)lrintf(50.f * fminf(1.f, up));
   else if (down > 0.f && up == 0.f && !sla_violated) raw = 50 - (int)lrintf(50.f * fminf(1.f, down));
-  raw_out[s] = (float)raw;
+  if (raw_out != nullptr) raw_out[s] = (float)raw;
   int dir = raw > 50 ? 1 : (raw < 50 ? -1 : 0);
   int8_t reason = dir > 0 ? 1 : (dir < 0 ? 2 : 0);
   int score = raw;
-  if (now - flip_t0[s] > flip_window) { flips[s] = 0; flip_t0[s] = now; }
+  if (now - *flip_t0 > flip_window) { *flips = 0; *flip_t0 = now; }
   if (dir != 0) {
-    const int ld = last_dir[s];
+    const int ld = *last_dir;
     const float wait = dir > 0 ? breath_up : breath_down;
-    if (ld != 0 && now - last_time[s] < wait) {
+    if (ld != 0 && now - *last_time < wait) {
       score = 50; reason = 3;
-    } else if (ld != 0 && dir != ld && flips[s] >= max_flips) {
+    } else if (ld != 0 && dir != ld && *flips >= max_flips) {
       score = 50; reason = 4;
     } else {
-      if (ld != 0 && dir != ld) flips[s] += 1;
-      last_dir[s] = (int8_t)dir;
-      last_time[s] = now;
+      if (ld != 0 && dir != ld) *flips += 1;
+      *last_dir = (int8_t)dir;
+      *last_time = now;
     }
   }
-  score_out[s] = score;
-  reason_out[s] = reason;
+  if (score_out != nullptr) score_out[s] = score;
+  if (reason_out != nullptr) reason_out[s] = reason;
+  if (packed_out != nullptr) packed_out[s] = score | ((int)reason << 16);
 }
 
 FM_API int fm_hpa_score(const float* cur, const float* upper, const float* lower, int64_t S, int Mt, const float* weight,
@@ -78,7 +86,24 @@ FM_API int fm_hpa_score(const float* cur, const float* upper, const float* lower
   if (S <= 0) return 0;
   hipLaunchKernelGGL(hpa_score_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, cur, upper, lower, S,
                      Mt, weight, is_increase, is_absolute, role, now, breath_up, breath_down, max_flips, flip_window,
-                     last_dir, last_time, flips, flip_t0, score, reason, raw);
+                     last_dir, last_time, flips, flip_t0, score, reason, raw, nullptr, nullptr);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
+// The brain's steady HPA cycle: the services' hysteresis state read and
+// updated in place through ``slots`` (the device HPA table), the verdict as
+// one int per service (score | reason << 16) for a single device->host copy.
+FM_API int fm_hpa_score_slots(const float* cur, const float* upper, const float* lower, int64_t S, int Mt,
+                              const float* weight, const int8_t* is_increase, const int8_t* is_absolute,
+                              const int8_t* role, double now, float breath_up, float breath_down, int max_flips,
+                              float flip_window, int8_t* last_dir, double* last_time, int* flips, double* flip_t0,
+                              const int64_t* slots, int* packed, hipStream_t stream) {
+  if (S <= 0) return 0;
+  if (slots == nullptr || packed == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(hpa_score_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, cur, upper, lower, S,
+                     Mt, weight, is_increase, is_absolute, role, now, breath_up, breath_down, max_flips, flip_window,
+                     last_dir, last_time, flips, flip_t0, nullptr, nullptr, nullptr, slots, packed);
   FM_LAUNCH_CHECK();
   return 0;
 }

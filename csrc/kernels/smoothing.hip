@@ -896,9 +896,10 @@ FM_API int fm_band_decide(const float* cur, int64_t ld_c, int n, const float* ce
 //   * stats[r] = (nan, nan, upper, lower) at the row's last finite point;
 //   * wave 0 reduces the service (service_reduce_kernel semantics) from LDS;
 //   * anomalous points append (row, point), value through one atomic per row
-//     to ctr[par]; block 0 zeroes ctr[par ^ 1] for the next cycle, and the
-//     last workgroup to finish (done count ctr[2 + par]) copies ctr[par]
-//     into hostv.
+//     to ctr[par]; block 0 zeroes ctr[par ^ 1] for the next cycle.  (A
+//     last-workgroup-publishes-the-counter epilogue -- one same-address
+//     device atomic per workgroup -- measured 43 -> 327 us at 10k workgroups:
+//     the counter is copied into hostv by the host instead.)
 // Host outputs land in one buffer (hostv: packed [S,4] | stats [R,4] | count
 // [R] (int) | dead [R] (int) | counters [2] (int)) for a single device->host
 // copy.
@@ -917,7 +918,8 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
     const int8_t* __restrict__ diff, float pair_factor, const int* __restrict__ valid,
     const int64_t* __restrict__ lastk, float* __restrict__ upper, float* __restrict__ lower,
     float* __restrict__ sigma_out, float* __restrict__ fc, int Hf, float* __restrict__ hostv, int cap,
-    int* __restrict__ ctr, int par, int* __restrict__ out_idx, float* __restrict__ out_val) {
+    int* __restrict__ ctr, int par, int* __restrict__ out_idx, float* __restrict__ out_val,
+    float* __restrict__ last3) {
   __shared__ float xs[kStepMMax][kStepKMax];
   __shared__ float su[kStepMMax][kStepKMax];
   __shared__ int s_cnt[kStepMMax];
@@ -1030,14 +1032,20 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
       if (lo < minlb[mm]) lo = minlb[mm];
       upper[row * n + i] = up;
       lower[row * n + i] = lo;
+      const float x = cur[row * ld_c + i];
       if (i == lk) {
         float* st = hostv + S * 4 + row * 4;
         st[0] = __builtin_nanf("");
         st[1] = __builtin_nanf("");
         st[2] = up;
         st[3] = lo;
+        if (last3 != nullptr) {       // the newest point and its band, NaN without one (HPA score input)
+          const bool okx = isfinite(x);
+          last3[row] = x;
+          last3[R + row] = okx ? up : __builtin_nanf("");
+          last3[2 * R + row] = okx ? lo : __builtin_nanf("");
+        }
       }
-      const float x = cur[row * ld_c + i];
       if (isfinite(x) && isfinite(c)) {
         const bool hi = (bd & 1) && x > up;
         const bool lw = (bd & 2) && x < lo;
@@ -1080,17 +1088,6 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
     s_valid[mi] = vld;
   }
   __syncthreads();
-  if (mi == 0 && lane == 0) {
-    // the last workgroup to finish publishes the counter into hostv (one
-    // device->host copy of hostv carries everything) and re-arms its slot
-    __threadfence();
-    const int done = atomicAdd(&ctr[2 + par], 1);
-    if (done == (int)gridDim.x - 1) {
-      __threadfence();
-      reinterpret_cast<int*>(hostv)[S * 4 + R * 6 + par] = atomicAdd(&ctr[par], 0);
-      ctr[2 + par] = 0;
-    }
-  }
   if (mi == 0 && lane == 0) {    // service_reduce_kernel semantics
     int tot = 0, mask = 0;
     bool unknown = false;
@@ -1115,7 +1112,7 @@ FM_API int fm_es_band_step(const float* buf, int64_t ld, const int* rm, const in
                            const int64_t* hor, int H, int64_t S, int M, const float* thr, const int* bound,
                            const float* minlb, const int8_t* diff, float pair_factor, const int* valid,
                            const int64_t* lastk, float* upper, float* lower, float* sigma, float* fc, int Hf,
-                           float* hostv, int cap, int* ctr, int par, int* out_idx, float* out_val,
+                           float* hostv, int cap, int* ctr, int par, int* out_idx, float* out_val, float* last3,
                            hipStream_t stream) {
   if (S <= 0) return 0;
   // kind -1: the forecast fc [R, Hf] (Hf >= H) and sigma are given (band + reduce + compaction only)
@@ -1128,7 +1125,8 @@ FM_API int fm_es_band_step(const float* buf, int64_t ld, const int* rm, const in
 #define FM_EBS(KK)                                                                                               \
   hipLaunchKernelGGL(es_band_step_kernel<KK>, grid, block, 0, stream, buf, ld, rm, shift, lim, dk, T, kmax, t_new, \
                      slots, params, m, season, sse, state, nobs, cur, ld_c, n, hor, H, S, M, thr, bound, minlb, diff, \
-                     pair_factor, valid, lastk, upper, lower, sigma, fc, Hf, hostv, cap, ctr, par, out_idx, out_val)
+                     pair_factor, valid, lastk, upper, lower, sigma, fc, Hf, hostv, cap, ctr, par, out_idx, out_val, \
+                     last3)
   if (kind == -1) FM_EBS(-1);
   else if (kind == 0) FM_EBS(0);
   else if (kind == 1) FM_EBS(1);

@@ -2029,6 +2029,7 @@ class FastPath:
                   "lo": torch.empty((R, n), dtype=torch.float32, device=dev),
                   "sig": torch.empty((R,), dtype=torch.float32, device=dev),
                   "hostv": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32, device=dev),
+                  "last3": torch.empty((3, R), dtype=torch.float32, device=dev) if p0.hpa else None,
                   "host": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32).pin_memory()}
             ga._fused = fz
         st = None
@@ -2062,8 +2063,9 @@ class FastPath:
                  ptr(tb.thr), ptr(tb.bound), ptr(tb.minlb), ptr(diff), float(tb.pair_factor), ptr(sub.valid),
                  ptr(md.lastk), ptr(fz["up"]), ptr(fz["lo"]), ptr(sig_t), ptr(fc),
                  int(fc.shape[1]) if fc is not None else 0, ptr(hv), int(idx_d.shape[0]), ptr(ctr), par,
-                 ptr(idx_d), ptr(val_d), stream_of(cur))
-        # the kernel's last workgroup wrote this launch's counter into hv: ONE copy
+                 ptr(idx_d), ptr(val_d), ptr(fz["last3"]), stream_of(cur))
+        # counter of this launch into the host buffer's tail, then ONE copy
+        hv[S * 4 + R * 6:].view(torch.int32).copy_(ctr[:2], non_blocking=True)
         host = fz["host"]
         host.copy_(hv, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
@@ -2082,7 +2084,7 @@ class FastPath:
             idx = np.stack([kk // n, kk % n], 1).astype(np.int32)
         return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
                 "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "hist_rows": ga.rowmap,
-                "store": store, "pts": (fz["up"], fz["lo"])}
+                "store": store, "pts": (fz["up"], fz["lo"]), "last3": fz["last3"]}
 
     def _forecast(self, algo: str, lazy: "LazyHist", sub: "ModelSub", H: int):
         from ..models import zoo
@@ -2202,11 +2204,12 @@ class FastPath:
             exp.set_bounds_many(ga.export_slots if ga.export_start is None else ga.export_start,
                                 stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64), anom_ts)
         if works[0].plan.hpa:
+            l3 = g.get("last3")
             if bulk is None:
-                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, updates_bulk := [], ga)
+                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, updates_bulk := [], ga, l3)
                 updates.extend((i, f) for ids, f, _ in updates_bulk for i in ids)
             else:
-                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga)
+                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga, l3)
             return
         status = packed[:, 0]
         unh = status == 1
@@ -2311,7 +2314,7 @@ class FastPath:
         return ST.COMPLETED_UNHEALTH, {"status": ST.COMPLETED_UNHEALTH, "reason": html.escape(json.dumps(reasons)),
                                        "anomaly_info": json.dumps(anomalies)}
 
-    def _finish_hpa(self, works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga=None) -> None:
+    def _finish_hpa(self, works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga=None, last3=None) -> None:
         S = len(works)
         last = _last_finite(cur)                    # (rows with no point: the last column, NaN)
         lastv = cur[np.arange(len(cur)), last]
@@ -2330,14 +2333,35 @@ class FastPath:
             return self.hpa.slots(ids).cpu().numpy()
         key = ga.key if ga is not None else None
         sl_np = self._extra(key, ga.ident, "hpa", hpa_slots) if key is not None else hpa_slots(None)
-        sl = torch.as_tensor(sl_np, device=dev)
-        sub = self.hpa.gather(sl)
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         cfg = self.b.cfg
-        sc, rs, _ = MI.hpa_score(t(cl), t(up), t(lo), tmpl, sub, now, cfg.hpa_breath_up, cfg.hpa_breath_down,
-                                 cfg.hpa_max_flips, cfg.hpa_flip_window)
-        self.hpa.scatter(sl, sub)
-        sc, rs = sc.cpu().numpy(), rs.cpu().numpy()
+        if last3 is not None and dev.type == "cuda":
+            # steady cycle: the newest points and bands are already on the
+            # device (the fused band kernel wrote them), the hysteresis state
+            # is updated in place through the slots -- one launch, one copy
+            from ..ops._lib import LIB, ptr, stream_of
+            hs = getattr(ga, "_hpa_dev", None)
+            if hs is None or hs[0] is not sl_np:
+                hs = ga._hpa_dev = (sl_np, torch.as_tensor(sl_np, device=dev),
+                                    torch.empty((S,), dtype=torch.int32, device=dev),
+                                    torch.empty((S,), dtype=torch.int32).pin_memory())
+            td = _hpa_tables(tmpl, dev)
+            st = self.hpa.state
+            LIB.call("fm_hpa_score_slots", ptr(last3[0]), ptr(last3[1]), ptr(last3[2]), S, M, *map(ptr, td),
+                     float(now), float(cfg.hpa_breath_up), float(cfg.hpa_breath_down), int(cfg.hpa_max_flips),
+                     float(cfg.hpa_flip_window), ptr(st.last_dir), ptr(st.last_time), ptr(st.flips), ptr(st.flip_t0),
+                     ptr(hs[1]), ptr(hs[2]), stream_of(last3))
+            hs[3].copy_(hs[2], non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            pk = hs[3].numpy()
+            sc, rs = pk & 0xFFFF, (pk >> 16).astype(np.int8)
+        else:
+            sl = torch.as_tensor(sl_np, device=dev)
+            sub = self.hpa.gather(sl)
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)    # noqa: E731
+            sc, rs, _ = MI.hpa_score(t(cl), t(up), t(lo), tmpl, sub, now, cfg.hpa_breath_up, cfg.hpa_breath_down,
+                                     cfg.hpa_max_flips, cfg.hpa_flip_window)
+            self.hpa.scatter(sl, sub)
+            sc, rs = sc.cpu().numpy(), rs.cpu().numpy()
         due = self.hpa.log_due(sl_np, sc.astype(np.int64), rs.astype(np.int64), now, cfg.hpa_log_interval_s)
         created = rfc3339(datetime.fromtimestamp(now, timezone.utc))
         exp = self.b.exporter
@@ -2592,6 +2616,21 @@ def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> 
             st.max_len = max(st.max_len, int(st.nlen[rows].max()) if len(rows) else 0)
         n_rows += len(rows)
     return n_rows
+
+
+def _hpa_tables(tmpl, dev) -> tuple:
+    """An HPA template's per-metric tables (weights, increase, absolute, role)
+    on the device, built once per template."""
+    c = getattr(tmpl, "_dev_tables", None)
+    if c is None or c[0] != dev:
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+        c = (dev, (t(tmpl.weights()), t(np.asarray(tmpl.is_increase, np.int8)),
+                   t(np.asarray(tmpl.is_absolute, np.int8)), t(tmpl.roles())))
+        try:
+            tmpl._dev_tables = c
+        except AttributeError:                 # a frozen template: rebuilt per call
+            pass
+    return c[1]
 
 
 def _sub(works: list, sel) -> list:

@@ -58,15 +58,18 @@ _SIGS: dict[str, list] = {
     "fm_peer_publish_ctr": [c_void_p, c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "fm_peer_ack_ctr": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
     # buf ld rm shift lim dk T kmax t_new slots params m kind season sse state nobs cur ld_c n hor H S M thr bound
-    # minlb diff pair_factor valid lastk upper lower sigma fc Hf hostv cap ctr par out_idx out_val stream
+    # minlb diff pair_factor valid lastk upper lower sigma fc Hf hostv cap ctr par out_idx out_val last3 stream
     "fm_es_band_step": [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                         c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int,
                         c_void_p, c_int, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
-                        c_void_p, c_void_p, c_void_p],
+                        c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_lstm_forward_hist": [c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_int, c_int,
                              c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_grid_retire": [c_void_p, c_i64, c_i64, c_int, c_int, c_void_p, c_void_p],
+    "fm_hpa_score_slots": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                           ctypes.c_double, c_float, c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p],
     "fm_es_update": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fm_band_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p, c_i64, c_int, c_void_p, c_void_p,
