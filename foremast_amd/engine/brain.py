@@ -805,7 +805,7 @@ class Brain:
         one a no-op (returns None).  Returns the file path (``wait``) or the
         pending future."""
         from . import checkpoint
-        from .fastpath import history_state
+        from .fastpath import history_snapshot, history_state
         if self.fast is None:
             return None
         prev = getattr(self, "_hist_future", None)
@@ -822,13 +822,21 @@ class Brain:
         if getattr(self, "_hist_stream", None) is None:
             self._hist_stream = torch.cuda.Stream(self.device)
             self._hist_pinned: dict = {}
+            self._hist_dev: dict = {}
             from concurrent.futures import ThreadPoolExecutor
             self._hist_writer = ThreadPoolExecutor(1, thread_name_prefix="history-ckpt")
-        t, meta, ev = history_state(self.fast, self._hist_pinned, self._hist_stream)
-        meta.update(rank=self.info.rank, world=self.info.world)
+        # in the cycle: a device copy of the live grid columns + host state
+        # copies; everything per row (keys, owner order, gather, host copy,
+        # file) on the writer thread
+        snap, _ = history_snapshot(self.fast, self._hist_dev, self._hist_stream)
+        stream, pinned, dev = self._hist_stream, self._hist_pinned, self.device
 
         def write():
-            ev.synchronize()
+            torch.cuda.set_device(dev)
+            t, meta, ev = history_state(self.fast, pinned, stream, snap=snap)
+            meta.update(rank=self.info.rank, world=self.info.world)
+            if ev is not None:
+                ev.synchronize()
             return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
         self._hist_future = self._hist_writer.submit(write)
         return self._hist_future

@@ -935,7 +935,7 @@ class FastPath:
                             (s0, have), = sp[1].items()
                             if len(have) == len(a):
                                 one_store[k] = s0
-                                arrs[k] = np.full(S, s0, object)
+                                arrs[k] = _const_objects(s0, S)
                                 continue
                     arrs[k] = a[ix]
                 rows = memo[2][ix]
@@ -2480,25 +2480,78 @@ class FastPath:
                                               w.plan.cluster) for w in gone_w], self.b.clock(), unbind=True)
 
 
-def _history_rows(fp: "FastPath"):
-    """(store name, store, rows, keys, owners) of every resident row a live
+class _StoreSnap:
+    """What a history checkpoint needs of one resident store, frozen at the
+    moment the save was issued (host arrays copied, grid columns on the
+    device or the live grid itself for a synchronous save)."""
+    __slots__ = ("sliding", "keys", "last_t", "nlen", "t0", "ws", "e", "step", "device", "grid", "c0")
+
+    def __init__(self, st, grid, c0: int):
+        self.sliding, self.keys = st.sliding, list(st.keys)
+        self.last_t, self.nlen = st.last_t.copy(), st.nlen.copy()
+        self.t0, self.ws, self.e, self.step, self.device = st.t0, st.ws, st.e, st.step, st.device
+        self.grid, self.c0 = grid, c0            # grid[:, j] is the store's column c0 + j
+
+
+def _history_rows(works, snaps: dict):
+    """(store name, snapshot, rows, keys, owners) of every resident row a live
     job references -- what a warm restart needs."""
     per = {"static": {}, "sliding": {}}
-    for w in fp.works.values():
+    for w in works:
         p = w.plan
         d = per["sliding" if p.sliding else "static"]
         for r, k in zip(w.rows.tolist(), p.keys):
             d.setdefault(int(r), (k, (p.namespace, w.doc.app_name)))
-    for name, st in (("static", fp.static), ("sliding", fp.sliding)):
+    for name in ("static", "sliding"):
+        st = snaps[name]
         d = per[name]
-        rows = np.array([r for r in sorted(d) if st.keys[r] == d[r][0]], np.int64)
+        rows = np.array([r for r in sorted(d) if r < len(st.keys) and st.keys[r] == d[r][0]], np.int64)
         yield name, st, rows, [d[int(r)][0] for r in rows], [d[int(r)][1] for r in rows]
 
 
 OWNER_BLOCKS = 16           # saved rows are grouped by service_owner(.., 16): one block per rank of any world | 16
 
 
-def history_state(fp: "FastPath", pinned: dict | None = None, stream=None) -> tuple[dict, dict, object]:
+def history_snapshot(fp: "FastPath", dev_bufs: dict | None = None, stream=None) -> tuple[dict, object]:
+    """Freeze what a history checkpoint needs, cheaply: the live jobs, the
+    stores' row keys / times, and (``dev_bufs`` + ``stream``: the periodic
+    asynchronous save) a device copy of each store's live grid columns, made on
+    ``stream`` after the current stream's work -- the current stream then
+    waits only for that copy (about 1 ms of HBM traffic per GB), and the
+    per-row bookkeeping, the row gather and the host copy happen later, off the
+    brain loop (:func:`history_state`).  -> (snapshot, event or None)."""
+    works = list(fp.works.values())
+    snaps: dict = {}
+    cur = torch.cuda.current_stream(fp.b.device) if (fp.b.device.type == "cuda" and stream is not None) else None
+    if cur is not None:
+        stream.wait_stream(cur)
+    for name, st in (("static", fp.static), ("sliding", fp.sliding)):
+        if st.sliding:
+            c0, c1 = (st.ws, st.e) if st.t0 is not None else (0, 0)
+        else:
+            c0, c1 = 0, max(1, st.max_len)
+        view = st.buf[:, c0:c1]
+        if cur is None:
+            snaps[name] = _StoreSnap(st, view, c0)
+            continue
+        R, W = view.shape
+        g = dev_bufs.get(name)
+        if g is None or g.numel() < R * W:
+            g = dev_bufs[name] = torch.empty((int(R * W * 1.25) + 64,), dtype=view.dtype, device=view.device)
+        gv = g[:R * W].view(R, W)
+        with torch.cuda.stream(stream):
+            gv.copy_(view, non_blocking=True)
+        snaps[name] = _StoreSnap(st, gv, c0)
+    ev = None
+    if cur is not None:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        cur.wait_event(ev)                       # the next cycle's grid writes wait for the copy only
+    return {"works": works, "stores": snaps, "step": fp.b.step}, ev
+
+
+def history_state(fp: "FastPath", pinned: dict | None = None, stream=None, snap: dict | None = None
+                  ) -> tuple[dict, dict, object]:
     """The device-resident history of every live job (static rows: the
     left-aligned samples; sliding rows: the window's columns) + their row
     keys, owners and times, for a warm restart (``Brain.save_history``).
@@ -2507,21 +2560,21 @@ def history_state(fp: "FastPath", pinned: dict | None = None, stream=None) -> tu
     "{name}.blocks"`` = the row offsets of the 16 owner blocks): after a
     re-shard to a world that divides 16, a rank reads only its blocks.
 
-    ``pinned`` (a dict of reusable pinned host buffers) + ``stream``: the
-    rows are gathered on ``stream`` (after the current stream's work; the
-    current stream then waits only for the gather, not for the copy) and
-    copied into pinned host memory asynchronously; the returned event marks
-    the host copy complete (None: synchronous, tensors ready)."""
+    ``snap`` (:func:`history_snapshot`): build the state from that frozen
+    snapshot (the asynchronous save runs this on its writer thread);
+    ``pinned`` (reusable pinned host buffers) + ``stream``: the rows are
+    gathered on ``stream`` and copied into pinned host memory asynchronously;
+    the returned event marks the host copy complete (None: synchronous,
+    tensors ready)."""
     from ..parallel.dist import service_owner
+    if snap is None:
+        snap, _ = history_snapshot(fp)
     t: dict[str, torch.Tensor] = {}
-    meta: dict = {"step": fp.b.step}
-    cur = torch.cuda.current_stream(fp.b.device) if fp.b.device.type == "cuda" else None
-    side = stream if cur is not None else None
-    if side is not None:
-        side.wait_stream(cur)
+    meta: dict = {"step": snap["step"]}
+    side = stream if (pinned is not None and stream is not None) else None
     ev = None
     gathered: list = []
-    for name, st, rows, keys, owners in _history_rows(fp):
+    for name, st, rows, keys, owners in _history_rows(snap["works"], snap["stores"]):
         if not len(rows):
             continue
         ob = np.fromiter((service_owner(ns, app, OWNER_BLOCKS) for ns, app in owners), np.int64, len(owners))
@@ -2532,11 +2585,11 @@ def history_state(fp: "FastPath", pinned: dict | None = None, stream=None) -> tu
         if st.sliding:
             if st.t0 is None or st.e <= st.ws:
                 continue
-            view, w = st.buf[:, st.ws:st.e], st.e - st.ws
+            view = st.grid[:, st.ws - st.c0:st.e - st.c0]
             meta[f"{name}.t_first"] = st.t0 + st.ws * st.step
         else:
             w = max(1, int(st.nlen[rows].max()))
-            view = st.buf[:, :w]
+            view = st.grid[:, :w]
             t[f"{name}.nlen"] = torch.from_numpy(st.nlen[rows].copy())
         if side is None:
             t[f"{name}.values"] = view.index_select(0, ri).cpu()
@@ -2547,11 +2600,6 @@ def history_state(fp: "FastPath", pinned: dict | None = None, stream=None) -> tu
         meta[f"{name}.keys"] = [list(k) for k in keys]
         meta[f"{name}.owners"] = [list(o) for o in owners]
     if side is not None:
-        # the next cycle's writes to the grids wait only for the gathers; the
-        # host copies run on behind them
-        sel = torch.cuda.Event()
-        sel.record(side)
-        cur.wait_event(sel)
         with torch.cuda.stream(side):
             for name, blk in gathered:
                 n = blk.numel() * blk.element_size()
@@ -2631,6 +2679,23 @@ def _hpa_tables(tmpl, dev) -> tuple:
         except AttributeError:                 # a frozen template: rebuilt per call
             pass
     return c[1]
+
+
+_CONST_OBJ: dict = {}
+
+
+def _const_objects(v, n: int) -> np.ndarray:
+    """A read-only [n] object array of ``v`` (a view of one cached array per
+    value: churned template lists of a one-store group index it, never write)."""
+    a = _CONST_OBJ.get(v)
+    if a is None or len(a) < n:
+        a = np.empty(max(n, 2 * len(a) if a is not None else n), object)
+        a[:] = [v] * len(a)
+        a.flags.writeable = False
+        if len(_CONST_OBJ) > 64:
+            _CONST_OBJ.clear()
+        _CONST_OBJ[v] = a
+    return a[:n]
 
 
 def _sub(works: list, sel) -> list:

@@ -74,6 +74,13 @@ for s in $steps; do
            python -c "import pstats,sys; p=pstats.Stats('gpurun_out/hostprof_3e2e_http60.prof', stream=sys.stdout); \
                p.sort_stats('tottime').print_stats(70); p.sort_stats('cumtime').print_stats(90)" \
                > gpurun_out/hostprof_3e2e_http60.txt || exit 1 ;;
+    hostprofhttp) FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_2e2e_http.prof timeout -k 10 500 python -u \
+               benchmarks/bench_configs.py --config 2e2e --source http --steps 8 --warmup 3 --prom-workers 8 \
+               > gpurun_out/check_hostprof_2e2e_http.log 2>&1; rc=$?
+           echo "hostprof 2e2e http rc=$rc"; [ $rc -eq 0 ] || exit $rc
+           python -c "import pstats,sys; p=pstats.Stats('gpurun_out/hostprof_2e2e_http.prof', stream=sys.stdout); \
+               p.sort_stats('tottime').print_stats(50); p.sort_stats('cumtime').print_stats(90)" \
+               > gpurun_out/hostprof_2e2e_http.txt || exit 1 ;;
     restart) e2e c3e2e_restart --config 3e2e --steps 5 --warmup 2 --restart &&
          e2e c2e2e_restart --config 2e2e --steps 5 --warmup 2 --restart || exit $rc ;;
     scanprobe) run scanprobe 200 python -u tools/hw_scan_probe.py || exit $rc
