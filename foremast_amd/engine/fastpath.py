@@ -469,6 +469,7 @@ class FastPath:
         self._cmp = {}            # device compaction buffers per capacity
         self._fused_cmp = {}      # the fused steady-cycle kernel's compaction buffers + counters
         self._rmd = {}            # group key -> (row map, its int32 / int64 device copies)
+        self._pin: dict = {}      # reusable pinned packing buffers
         self._fused_par = 0       # which of the two counters the next fused launch appends to
         self._es_plan = None      # (keys, cache lookup) a declined fused cycle hands to es_forecast
         self.fused_steps = 0
@@ -1059,7 +1060,11 @@ class FastPath:
                 if sel is None or len(sel) == len(tpls):
                     lens, t, v = self._columns(stores, tpls, float(lo_v), hi)
                 else:
-                    lens, t, v = self._columns([stores[i] for i in sel], [tpls[i] for i in sel], float(lo_v), hi)
+                    # rows at another start this cycle: subsets of the planned
+                    # lists (a source indexes their plan, no re-parse)
+                    sl = sel.tolist()
+                    lens, t, v = self._columns(TemplateList.subset(stores, [stores[i] for i in sl], sel),
+                                               TemplateList.subset(tpls, [tpls[i] for i in sl], sel), float(lo_v), hi)
                 if len(t):
                     wr.append(np.repeat(rows[:, m] if sel is None else rows[sel, m], lens))
                     wt.append(t)
@@ -1400,8 +1405,7 @@ class FastPath:
         M, S = len(p0.aliases), len(works)
         dev = self.b.device
         store = self.static
-        up = lambda a: (torch.from_numpy(a).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"  # noqa: E731
-                        else torch.from_numpy(a))
+        up = lambda a: _upload(a, dev)  # noqa: E731
         ga = self._garr.get(key)
         if ga is not None and ga.wcur is not None and (ga.works is works or ga.ident == self._jid(works)):
             ga.works = works
@@ -1422,11 +1426,18 @@ class FastPath:
             # fleet churn (a few jobs left or arrived): the kept rows are the
             # previous arrays' -- on the host and on the device -- and only the
             # new jobs' and the changed windows' rows are packed and uploaded
+            # (unless most rows changed anyway: a live 60-s canary fleet gains
+            # a sample in every window each cycle -- then a fresh pack is cheaper)
             ix, hit, _ = m
             newr = np.flatnonzero(np.repeat(~hit, M))
             nb_old = 0 if old.base is None else old.base.shape[1]
             fits = (wt.max_points(wc[newr]) <= old.cur.shape[1]
                     and (wt.max_points(wb[newr]) <= nb_old if old.base is not None else wt.max_points(wb[newr]) == 0))
+            if fits and self._wt_changed:
+                dw = wt.dirty[np.maximum(wc, 0)] & (wc >= 0)
+                if wb is not None:
+                    dw |= wt.dirty[np.maximum(wb, 0)] & (wb >= 0)
+                fits = int(dw.sum()) + len(newr) <= len(wc) // 2
             if fits:
                 r = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)
                 r_d = torch.from_numpy(r).to(dev)
@@ -1444,9 +1455,10 @@ class FastPath:
                 ga.hist_epoch = self._hist_epoch
                 return self._install_arrays(ga, key, works, xslots)
         n = max(1, wt.max_points(wc))
-        cur, cur_t, cur_len = wt.pack(wc, n)
+        pin = self._pinned(("tcur", key), (len(wc), n), dev)
+        cur, cur_t, cur_len = wt.pack(wc, n, out_v=pin)
         nb = wt.max_points(wb)
-        base = wt.pack(wb, nb, times=False)[0] if nb else None
+        base = wt.pack(wb, nb, times=False, out_v=self._pinned(("tbase", key), (len(wb), nb), dev))[0] if nb else None
         has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
         ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, up(cur), up(base) if base is not None else None,
                          up(rowmap), end, ~(has_hist & (cur_len > 0).reshape(S, M)), handles=handles, works=works)
@@ -1465,6 +1477,18 @@ class FastPath:
         self._garr[key] = ga
         return ga
 
+    def _pinned(self, name, shape: tuple, dev) -> np.ndarray | None:
+        """A reusable pinned host array (numpy view) for packing arrays bound
+        for the device: the upload is then one DMA, no staging copy.  Reused
+        next cycle, after this cycle's scoring synchronised."""
+        if dev.type != "cuda" or not shape[0] or not shape[1]:
+            return None
+        n = int(np.prod(shape))
+        buf = self._pin.get(name)
+        if buf is None or buf.numel() < n:
+            buf = self._pin[name] = torch.empty((int(n * 1.25) + 16,), dtype=torch.float32).pin_memory()
+        return buf[:n].numpy().reshape(shape)
+
     def _dirty_rows(self, ga: GroupArrays) -> np.ndarray:
         """Rows of a table group whose current or baseline window gained samples."""
         wt, wc, wb = self.wt, ga.wcur, ga.wbase
@@ -1479,7 +1503,23 @@ class FastPath:
         if not len(rows):
             return False
         wt, wc, wb = self.wt, ga.wcur, ga.wbase
-        ri = torch.from_numpy(rows).to(ga.cur_d.device)
+        dev = ga.cur_d.device
+        if len(rows) == len(wc):
+            # every window changed (a live fleet at the poll cadence): pack the
+            # whole arrays straight into pinned memory, replace, one upload each
+            key = ga.key
+            v, t, ln = wt.pack(wc, ga.cur.shape[1], out_v=self._pinned(("tcur", key), ga.cur.shape, dev))
+            ga.cur, ga.cur_t, ga.cur_len = v, t, ln
+            ga.cur_d.copy_(torch.from_numpy(v), non_blocking=True)
+            wt.dirty[wc[wc >= 0]] = False
+            if ga.base_d is not None:
+                bv, _, _ = wt.pack(wb, ga.base.shape[1], times=False,
+                                   out_v=self._pinned(("tbase", key), ga.base.shape, dev))
+                ga.base = bv
+                ga.base_d.copy_(torch.from_numpy(bv), non_blocking=True)
+                wt.dirty[wb[wb >= 0]] = False
+            return True
+        ri = torch.from_numpy(rows).to(dev)
         v, t, ln = wt.pack(wc[rows], ga.cur.shape[1])
         ga.cur[rows], ga.cur_t[rows], ga.cur_len[rows] = v, t, ln
         ga.cur_d.index_copy_(0, ri, up(v))
@@ -2682,6 +2722,18 @@ def _hpa_tables(tmpl, dev) -> tuple:
 
 
 _CONST_OBJ: dict = {}
+
+
+def _upload(a: np.ndarray, dev) -> torch.Tensor:
+    """Host array -> device tensor: one asynchronous DMA when ``a`` already
+    lives in pinned memory (FastPath._pinned), else staged through a pinned
+    copy."""
+    t = torch.from_numpy(a)
+    if dev.type != "cuda":
+        return t
+    if not t.is_pinned():
+        t = t.pin_memory()
+    return t.to(dev, non_blocking=True)
 
 
 def _const_objects(v, n: int) -> np.ndarray:

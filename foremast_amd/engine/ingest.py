@@ -246,6 +246,7 @@ class KeyedQuery:
     alt: str | None = None
     parts: list | None = None            # the key values per window (alt's source)
     store: str = "prometheus"            # metric store type the query goes to
+    qtext: str | None = None             # the rendered selector, when already known
 
     def key_values(self) -> list:
         if self.values is None:
@@ -254,7 +255,9 @@ class KeyedQuery:
 
     @property
     def query(self) -> str:
-        return render_query(self.group, self.values, self.alt)
+        if self.qtext is None:
+            self.qtext = render_query(self.group, self.values, self.alt)
+        return self.qtext
 
     @property
     def url_params(self) -> dict:
@@ -298,6 +301,8 @@ class WindowTable:
         self.dirty = np.zeros(0, bool)       # data changed since the scoring arrays last read it
         self.err = np.zeros(0, bool)         # last fetch of the window failed
         self.dup = np.zeros(0, np.uint8)     # an answer carried two series of one key value (see apply)
+        self.wgen = np.zeros(0, np.int64)    # bumped whenever a window id is (re)assigned or released
+        self._qcache: dict = {}              # (group, window ids) -> rendered request, checked against wgen
         self.toff = np.zeros(0)              # sample phase vs start (0 for Prometheus; nan: not seen yet)
         self.values: list = []               # key values (sorted) per window
         self.frag: list = []                 # their escaped regex alternation
@@ -323,7 +328,7 @@ class WindowTable:
         cap = max(need, 2 * self._cap, 1024)
         for name, fill in (("start", 0.0), ("end", 0.0), ("step", 1.0), ("settled", 0.0), ("gid", 0),
                            ("slot0", -1), ("nslot", 0), ("ncol", 0), ("live", False), ("alive", False),
-                           ("dirty", False), ("err", False), ("toff", np.nan), ("dup", 0)):
+                           ("dirty", False), ("err", False), ("toff", np.nan), ("dup", 0), ("wgen", 0)):
             old = getattr(self, name)
             a = np.full(cap, fill, old.dtype)
             a[:len(old)] = old
@@ -381,6 +386,7 @@ class WindowTable:
         self.toff[w] = np.nan
         self.values[w] = vals
         self.frag[w] = "|".join(promql.re_literal(v) for v in vals)
+        self.wgen[w] += 1
         self.next_due = -math.inf
         return w
 
@@ -465,6 +471,7 @@ class WindowTable:
             gid[i] = g
             values[w] = uvals[u]
             frag[w] = frags[u]
+            self.wgen[w] += 1
         self.start[wids], self.end[wids], self.step[wids] = start, end, step
         self.settled[wids] = start - step
         self.gid[wids], self.slot0[wids], self.nslot[wids], self.ncol[wids] = gid, slot0, nsl, ncol
@@ -487,6 +494,7 @@ class WindowTable:
             self.dirty[w] = False
             self.values[w] = None
             self.frag[w] = None
+            self.wgen[w] += 1
             self._free_w.append(w)
 
     def complete(self, wids: np.ndarray) -> np.ndarray:
@@ -534,9 +542,22 @@ class WindowTable:
             for i in range(a, b, per):
                 j = min(b, i + per)
                 wl = w[i:j].tolist()
-                grp, store = self.group_keys[int(g[i])]
-                q = KeyedQuery(grp, None, float(lo[i:j].min()), float(hi[i:j].max()),
-                               alt="|".join([frag[x] for x in wl]), parts=[values[x] for x in wl])
+                gi = int(g[i])
+                grp, store = self.group_keys[gi]
+                # the same chunk of windows asks the same selector every cycle
+                # (only the time range moves): its key regex and query text
+                # are rendered once
+                ck = (gi, tuple(wl))
+                c = self._qcache.get(ck)
+                gen = self.wgen[w[i:j]]
+                if c is None or not np.array_equal(c[3], gen):
+                    alt = "|".join([frag[x] for x in wl])
+                    c = (alt, [values[x] for x in wl], render_query(grp, None, alt), gen)
+                    if len(self._qcache) > 65536:
+                        self._qcache.clear()
+                    self._qcache[ck] = c
+                q = KeyedQuery(grp, None, float(lo[i:j].min()), float(hi[i:j].max()), alt=c[0], parts=c[1],
+                               qtext=c[2])
                 q.store = store
                 out.append((q, w[i:j], lo[i:j], hi[i:j]))
         return out
@@ -675,10 +696,12 @@ class WindowTable:
         w = w[w >= 0]
         return int((self.nslot[w] * self.ncol[w]).max()) if len(w) else 0
 
-    def pack(self, wids: np.ndarray, width: int | None = None, times: bool = True):
+    def pack(self, wids: np.ndarray, width: int | None = None, times: bool = True, out_v: np.ndarray | None = None):
         """(values [R, n] float32, times [R, n] float64 or None, lens [R]):
         row r = window ``wids[r]``'s samples pod-major / time-minor, missing
-        steps squeezed out, NaN-padded; ``wids[r] < 0`` -> an empty row."""
+        steps squeezed out, NaN-padded; ``wids[r] < 0`` -> an empty row.
+        ``out_v``: a C-contiguous [R, n] float32 array (e.g. pinned host
+        memory bound for the device) to pack the values into."""
         w = np.ascontiguousarray(wids, np.int64).reshape(-1)
         R = len(w)
         n = max(1, self.max_points(w) if width is None else int(width))
@@ -689,7 +712,8 @@ class WindowTable:
         ncol = np.where(ok, self.ncol[wz], 0).astype(np.int64)
         start = np.ascontiguousarray(self.start[wz] + np.nan_to_num(self.toff[wz]), np.float64)
         step = np.ascontiguousarray(self.step[wz], np.float64)
-        out_v = np.empty((R, n), np.float32)
+        if out_v is None or out_v.shape != (R, n) or out_v.dtype != np.float32 or not out_v.flags.c_contiguous:
+            out_v = np.empty((R, n), np.float32)
         out_t = np.empty((R, n), np.float64) if times else None
         lens = np.empty(R, np.int64)
         lib = native_rt._load()

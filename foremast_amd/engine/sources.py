@@ -322,10 +322,18 @@ class PrometheusSource:
             ri = rent[2]
             ix = np.asarray(templates.ix, np.int64)
             gid = ri["gid"][ix]
-            if len(templates) < 0.9 * ri["chunked_for"]:
-                ri["chunks"] = self._chunks(gid, ri["apps"][ix], ri["groups"])
-                ri["chunked_for"] = len(templates)
-            plan = (gid, ri["th"][ix], np.flatnonzero(gid < 0), ri["chunks"])
+            cov = ri["covered"]
+            chunks = ri["chunks"]
+            if not cov[ix].all() or len(ix) < 0.9 * ri["chunked_for"]:
+                # requests for exactly this subset's apps; a large subset (the
+                # fleet after churn) makes them the root's requests, a small
+                # one (rows at another start time this cycle) keeps its own
+                chunks = self._chunks(gid, ri["apps"][ix], ri["groups"])
+                if len(ix) >= 0.5 * ri["chunked_for"]:
+                    ri["chunks"], ri["chunked_for"] = chunks, len(ix)
+                    cov[:] = False
+                    cov[ix] = True
+            plan = (gid, ri["th"][ix], np.flatnonzero(gid < 0), chunks)
         else:
             n = len(templates)
             gid = np.full(n, -1, np.int64)
@@ -348,7 +356,8 @@ class PrometheusSource:
             chunks = self._chunks(gid, apps, groups)
             plan = (gid, hs, np.flatnonzero(~ok), chunks)
             if root is None:                            # a root list: what its subsets index
-                info = {"gid": gid, "th": hs, "apps": apps, "groups": groups, "chunks": chunks, "chunked_for": n}
+                info = {"gid": gid, "th": hs, "apps": apps, "groups": groups, "chunks": chunks, "chunked_for": n,
+                        "covered": np.ones(n, bool)}        # root positions the root's requests ask for
         if len(self._plans) >= 32:
             self._plans.pop(next(iter(self._plans)))
         self._plans[id(templates)] = (templates, plan, info)

@@ -357,3 +357,31 @@ def test_fetch_columns_churned_subsets_reuse_the_root_plan(server):
         assert src.stats["requests"] - n_req == len(ri["chunks"])
         asked = {a for _, q in ri["chunks"] for a in q.values}
         assert asked == {f"svc{j}" for j in ix}
+
+
+def test_fetch_columns_split_subsets_of_one_root(server):
+    """Rows at two different start times in one cycle hand fetch_columns two
+    disjoint subsets of the same planned root, the small one first: each is
+    answered exactly as a fresh plan answers it (the small one's requests
+    never stand in for the large one's), and neither re-parses the root."""
+    from foremast_amd.engine.sources import TemplateList
+    port, cw, _, _ = server
+    cw.set(T0)
+    base = f"http://127.0.0.1:{port}/api/v1/query_range"
+    tpl = lambda a: base + "?" + urllib.parse.urlencode({"query": f'namespace_app_pod_cpu{{namespace="d",app="{a}"}}'}) \
+        + "&start=START_TIME&end=END_TIME&step=60"
+    root = TemplateList([tpl(f"svc{j}") for j in range(80)])
+    src = PrometheusSource(workers=4, batch=16)
+    src.fetch_columns(root, T0 - 300, T0)
+    parsed = len(src._tpl)
+    small = np.array([3, 17, 40, 41])
+    large = np.setdiff1d(np.arange(80), small)
+    for sel in (small, large, small, large):
+        sub = TemplateList.subset(root, [root[i] for i in sel.tolist()], sel)
+        got = src.fetch_columns(sub, T0 - 300, T0)
+        want = PrometheusSource(workers=4, batch=16).fetch_columns(list(sub), T0 - 300, T0)
+        np.testing.assert_array_equal(got.off, want.off)
+        np.testing.assert_array_equal(got.t, want.t)
+        np.testing.assert_array_equal(got.v, want.v)
+        assert got.off[-1] > 0
+    assert len(src._tpl) == parsed
