@@ -832,12 +832,22 @@ class Brain:
         stream, pinned, dev = self._hist_stream, self._hist_pinned, self.device
 
         def write():
-            torch.cuda.set_device(dev)
-            t, meta, ev = history_state(self.fast, pinned, stream, snap=snap)
-            meta.update(rank=self.info.rank, world=self.info.world)
-            if ev is not None:
-                ev.synchronize()
-            return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
+            # the writer's Python (per-row keys, owner order, meta JSON) hands
+            # the interpreter back within 0.1 ms whenever the brain loop asks
+            # for it (the default 5-ms switch interval let a background save
+            # stretch the loop's cycles); file writes release it anyway
+            import sys
+            iv = sys.getswitchinterval()
+            sys.setswitchinterval(min(iv, 1e-4))
+            try:
+                torch.cuda.set_device(dev)
+                t, meta, ev = history_state(self.fast, pinned, stream, snap=snap)
+                meta.update(rank=self.info.rank, world=self.info.world)
+                if ev is not None:
+                    ev.synchronize()
+                return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
+            finally:
+                sys.setswitchinterval(iv)
         self._hist_future = self._hist_writer.submit(write)
         return self._hist_future
 

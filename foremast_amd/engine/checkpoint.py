@@ -28,6 +28,64 @@ def _pointer(kind: str) -> str:
     return "LATEST" if kind == "engine" else f"LATEST_{kind.upper()}"
 
 
+_ST_DTYPES = {torch.float64: "F64", torch.float32: "F32", torch.float16: "F16", torch.bfloat16: "BF16",
+              torch.int64: "I64", torch.int32: "I32", torch.int16: "I16", torch.int8: "I8", torch.uint8: "U8",
+              torch.bool: "BOOL"}
+
+
+def _json_chunked(obj: dict, chunk: int = 4096) -> str:
+    """json.dumps of a dict whose values may be long lists, encoded a chunk of
+    list items at a time with a GIL release in between: a background
+    checkpoint writer never holds the interpreter for one long C call while the
+    brain loop runs."""
+    enc = json.JSONEncoder(separators=(",", ":"))
+    parts = []
+    for k, v in obj.items():
+        if isinstance(v, list) and len(v) > chunk:
+            items = []
+            for i in range(0, len(v), chunk):
+                items.append(enc.encode(v[i:i + chunk])[1:-1])
+                time.sleep(0)
+            parts.append(enc.encode(k) + ":[" + ",".join(x for x in items if x) + "]")
+        else:
+            parts.append(enc.encode(k) + ":" + enc.encode(v))
+    return "{" + ",".join(parts) + "}"
+
+
+def write_safetensors(path, tensors: dict[str, torch.Tensor], metadata: dict[str, str]) -> None:
+    """A safetensors file written with plain file writes (each releases the
+    GIL for its syscall) -- the same format ``safetensors.torch.save_file``
+    writes and ``safe_open`` / ``load_file`` read: little-endian u64 header
+    length, the JSON header (``dtype`` / ``shape`` / ``data_offsets`` per
+    tensor, ``__metadata__``) padded to 8 bytes, then the raw tensor bytes."""
+    import struct
+    names = sorted(tensors)
+    hdr: dict = {}
+    off = 0
+    bufs = []
+    for n in names:
+        t = tensors[n].detach()
+        if t.device.type != "cpu":
+            t = t.cpu()
+        t = t.contiguous()
+        nb = t.numel() * t.element_size()
+        hdr[n] = {"dtype": _ST_DTYPES[t.dtype], "shape": list(t.shape), "data_offsets": [off, off + nb]}
+        off += nb
+        bufs.append(t)
+    hdr["__metadata__"] = metadata
+    hb = json.dumps(hdr, separators=(",", ":")).encode()
+    hb += b" " * ((8 - len(hb) % 8) % 8)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<Q", len(hb)))
+        f.write(hb)
+        for t in bufs:
+            if t.numel():
+                raw = t.view(torch.uint8).reshape(-1).numpy() if t.dtype != torch.bool else t.numpy().view(np.uint8)
+                mv = memoryview(raw)
+                for i in range(0, len(mv), 64 << 20):     # 64 MB writes
+                    f.write(mv[i:i + (64 << 20)])
+
+
 def save(dirpath: str, tensors: dict[str, torch.Tensor], meta: dict, step: int | None = None, tag: str = "",
          keep: int = 3, kind: str = "engine") -> Path:
     """``tag`` separates the ranks of a data-parallel brain
@@ -40,8 +98,8 @@ def save(dirpath: str, tensors: dict[str, torch.Tensor], meta: dict, step: int |
     step = int(time.time() * 1000) if step is None else step
     path = d / f"{kind}{tag}-{step}.safetensors"
     tmp = d / f".{kind}{tag}-{step}.tmp"
-    md = {"format": FORMAT_VERSION, "meta": json.dumps(meta), "saved_at": str(time.time())}
-    save_file({k: v.detach().contiguous().cpu() for k, v in tensors.items()}, str(tmp), metadata=md)
+    md = {"format": FORMAT_VERSION, "meta": _json_chunked(meta), "saved_at": str(time.time())}
+    write_safetensors(tmp, tensors, md)
     os.replace(tmp, path)
     ptr = _pointer(kind)
     latest_tmp = d / f".{ptr}{tag}.tmp"

@@ -2617,7 +2617,9 @@ def history_state(fp: "FastPath", pinned: dict | None = None, stream=None, snap:
     for name, st, rows, keys, owners in _history_rows(snap["works"], snap["stores"]):
         if not len(rows):
             continue
-        ob = np.fromiter((service_owner(ns, app, OWNER_BLOCKS) for ns, app in owners), np.int64, len(owners))
+        oc: dict = {}
+        ob = np.fromiter((oc[o] if o in oc else oc.setdefault(o, service_owner(o[0], o[1], OWNER_BLOCKS))
+                          for o in owners), np.int64, len(owners))
         order = np.argsort(ob, kind="stable")
         rows, keys, owners = rows[order], [keys[i] for i in order], [owners[i] for i in order]
         meta[f"{name}.blocks"] = np.searchsorted(ob[order], np.arange(OWNER_BLOCKS + 1)).tolist()

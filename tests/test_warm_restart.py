@@ -200,3 +200,30 @@ def test_gpu_async_history_save_is_off_the_cycle(tmp_path):
     b2 = Brain(MemoryStore(), BrainConfig(), device=torch.device("cuda"), clock=clock, worker_id="w",
                sources=SourceRouter(synthetic=SyntheticSource(), force="synthetic"))
     assert b2.load_history(str(tmp_path)) == live_rows
+
+
+def test_write_safetensors_reads_back_with_safetensors(tmp_path):
+    """checkpoint.write_safetensors (plain GIL-releasing writes) produces what
+    safetensors itself reads: every dtype the checkpoints use, an empty
+    tensor, the metadata; the chunked meta JSON equals json.dumps."""
+    import json
+    import torch
+    from safetensors import safe_open
+    from safetensors.torch import load_file
+    from foremast_amd.engine import checkpoint as CK
+    g = torch.Generator().manual_seed(0)
+    ts = {"a.values": torch.randn(37, 11, generator=g), "b": torch.randn(5, generator=g).to(torch.bfloat16),
+          "c": torch.arange(9, dtype=torch.int64), "d": torch.tensor([True, False, True]),
+          "e": torch.zeros(0, 4), "f": torch.arange(7, dtype=torch.int8), "g": torch.randn(3, 2, dtype=torch.float64)}
+    meta = {"format": "x", "meta": CK._json_chunked({"k": [[i, "a"] for i in range(10000)], "s": 1.5}, chunk=999)}
+    p = tmp_path / "t.safetensors"
+    CK.write_safetensors(p, ts, meta)
+    got = load_file(str(p))
+    assert set(got) == set(ts)
+    for k, v in ts.items():
+        assert got[k].dtype == v.dtype and got[k].shape == v.shape
+        assert torch.equal(got[k], v)
+    with safe_open(str(p), framework="pt") as f:
+        md = f.metadata()
+    assert md["format"] == "x"
+    assert json.loads(md["meta"]) == {"k": [[i, "a"] for i in range(10000)], "s": 1.5}
