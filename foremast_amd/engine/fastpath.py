@@ -2649,7 +2649,15 @@ def history_state(fp: "FastPath", pinned: dict | None = None, stream=None, snap:
                 if host is None or host.numel() < n:
                     host = pinned[name] = torch.empty(int(n * 1.25) + 64, dtype=torch.uint8, pin_memory=True)
                 hv = host[:n].view(blk.dtype).view(blk.shape)
-                hv.copy_(blk, non_blocking=True)
+                # in 32 MB pieces, each waited for: a gigabyte-sized copy would
+                # hold the copy engine and the brain loop's own small
+                # transfers would queue behind it
+                rb = max(1, (32 << 20) // max(1, blk.shape[1] * blk.element_size()))
+                for r0 in range(0, blk.shape[0], rb):
+                    hv[r0:r0 + rb].copy_(blk[r0:r0 + rb], non_blocking=True)
+                    e = torch.cuda.Event()
+                    e.record(side)
+                    e.synchronize()
                 blk.record_stream(side)
                 t[f"{name}.values"] = hv
         ev = torch.cuda.Event()

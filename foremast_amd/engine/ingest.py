@@ -306,6 +306,8 @@ class WindowTable:
         self.toff = np.zeros(0)              # sample phase vs start (0 for Prometheus; nan: not seen yet)
         self.values: list = []               # key values (sorted) per window
         self.frag: list = []                 # their escaped regex alternation
+        self.qfrag: list = []                # the same as the inside of a PromQL string literal
+        self._qpre: dict = {}                # group id -> (text before, after) the key regex
         self.groups: dict[tuple, int] = {}
         self.group_keys: list[tuple] = []
         self._free_w: list[int] = []
@@ -369,6 +371,7 @@ class WindowTable:
             self.n += 1
             self.values.append(None)
             self.frag.append(None)
+            self.qfrag.append(None)
         gk = (spec.group, store)
         g = self.groups.get(gk)
         if g is None:
@@ -386,6 +389,7 @@ class WindowTable:
         self.toff[w] = np.nan
         self.values[w] = vals
         self.frag[w] = "|".join(promql.re_literal(v) for v in vals)
+        self.qfrag[w] = promql.quote(self.frag[w])[1:-1]
         self.wgen[w] += 1
         self.next_due = -math.inf
         return w
@@ -433,6 +437,7 @@ class WindowTable:
             self.n += nnew
             self.values.extend([None] * nnew)
             self.frag.extend([None] * nnew)
+            self.qfrag.extend([None] * nnew)
         # slots: a freed block of the same size, else a new contiguous run
         slot0 = np.empty(k, np.int64)
         fresh = []
@@ -456,6 +461,7 @@ class WindowTable:
         gid = np.empty(k, np.int64)
         # every union's regex fragment from ONE escape pass over all values
         frags = promql.re_literal("\x00".join("\x01".join(vs) for vs in uvals)).replace("\x01", "|").split("\x00")
+        qfrags = promql.quote("\x00".join(frags))[1:-1].split("\x00")    # one string-literal escape pass too
         gcache: dict = {}
         values, frag = self.values, self.frag
         for i, (sp, st, w, u) in enumerate(zip(specs, stores, wids.tolist(), wu.tolist())):
@@ -471,6 +477,7 @@ class WindowTable:
             gid[i] = g
             values[w] = uvals[u]
             frag[w] = frags[u]
+            self.qfrag[w] = qfrags[u]
             self.wgen[w] += 1
         self.start[wids], self.end[wids], self.step[wids] = start, end, step
         self.settled[wids] = start - step
@@ -494,6 +501,7 @@ class WindowTable:
             self.dirty[w] = False
             self.values[w] = None
             self.frag[w] = None
+            self.qfrag[w] = None
             self.wgen[w] += 1
             self._free_w.append(w)
 
@@ -552,7 +560,12 @@ class WindowTable:
                 gen = self.wgen[w[i:j]]
                 if c is None or not np.array_equal(c[3], gen):
                     alt = "|".join([frag[x] for x in wl])
-                    c = (alt, [values[x] for x in wl], render_query(grp, None, alt), gen)
+                    pp = self._qpre.get(gi)
+                    if pp is None:
+                        mark = "\x02"
+                        pp = self._qpre[gi] = tuple(render_query(grp, None, mark).split(mark))
+                    qfrag = self.qfrag
+                    c = (alt, [values[x] for x in wl], pp[0] + "|".join([qfrag[x] for x in wl]) + pp[1], gen)
                     if len(self._qcache) > 65536:
                         self._qcache.clear()
                     self._qcache[ck] = c

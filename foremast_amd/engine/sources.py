@@ -315,6 +315,11 @@ class PrometheusSource:
             return ent[1]
         root = getattr(templates, "root", None)
         rent = self._plans.get(id(root)) if root is not None else None
+        if root is not None and (rent is None or rent[0] is not root):
+            # a subset of a list never planned here (its first fetch was of a
+            # subset already): plan the root once, then index it every cycle
+            self._columns_plan(root)
+            rent = self._plans.get(id(root))
         info = None
         if rent is not None and rent[0] is root and rent[2] is not None:
             self._plans.pop(id(root))                   # the root stays the most recently used
@@ -780,6 +785,12 @@ class StagedSource:
         root = getattr(templates, "root", None)
         if (ent is None or ent[0] is not templates) and root is not None:
             rent = self._lists.pop(id(root), None)
+            if rent is None or rent[0] is not root:
+                # a root never fetched here (its first fetch was of a subset):
+                # resolve it once if every template of it is staged
+                rr = self._rows_of(root)
+                if len(rr) and (rr >= 0).all():
+                    rent = (root, rr)
             if rent is not None and rent[0] is root:       # a subset of a staged list: index its rows
                 self._lists[id(root)] = rent                  # (kept most recently used)
                 ent = (templates, rent[1][templates.ix])

@@ -136,6 +136,31 @@ def test_batched_pod_union_equals_per_job_queries():
     assert v[r3, 11:22].mean() > 3 * v[r3, :11].mean()
 
 
+def test_pending_queries_render_like_render_query():
+    """The window table renders its batched selectors from per-window quoted
+    fragments (cached per chunk): the same text render_query gives, for pods
+    with regex metacharacters and string escapes, through add and add_many,
+    after a release and a reuse of window ids."""
+    from foremast_amd.engine.ingest import render_query
+    pods = {f"svc{j}": [f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(3)] for j in range(30)}
+    pods["svc.odd"] = ["svc.odd-1", 'svc"q\\-2']
+    q = lambda ps: 'namespace_pod_latency{namespace="default",pod=~"' + "|".join(
+        promql.re_literal(p).replace("\\", "\\\\").replace('"', '\\"') for p in ps) + '"}'
+    wt = WindowTable(settle=0.0, batch=8)
+    specs = [parse_range(_url(q(p), T0, T0 + 600)) for p in pods.values()]
+    wids = [wt.add(specs[0], live=True)] + list(wt.add_many(specs[1:], [True] * (len(specs) - 1),
+                                                             ["prometheus"] * (len(specs) - 1)))
+    for rnd in range(3):
+        wt.next_due = -np.inf
+        got = wt.pending(T0 + 600)
+        assert got
+        for kq, *_ in got:
+            assert kq.query == render_query(kq.group, None, kq.alt)
+        if rnd == 0:
+            wt.release(np.array(wids[3:6]))
+            wids = wids[:3] + wids[6:] + list(wt.add_many(specs[3:6], [True] * 3, ["prometheus"] * 3))
+
+
 def test_incremental_windows_fetch_each_step_once():
     """A current window in the future: no request before its first point is
     due, one new step per request round, complete after its end; a past
