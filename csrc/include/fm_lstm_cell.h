@@ -21,9 +21,10 @@
 //     K i g = K (1 - E_g) / (E_i (1 + E_g) + (1 + E_g))
 //                                                  2 v_exp, v_med3, v_add, 2 v_fma, v_mul, v_rcp
 //     cs' = fma(cs, sf, K i g)                      v_fma
-//     h = (1 - E_c) / (E_o (1 + E_c) + (1 + E_c))   2 v_exp, v_med3, v_add, v_sub, v_fma, v_rcp, v_mul
+//     h = (1 - E_c) / (E_o (1 + E_c) + (1 + E_c))   2 v_exp, v_med3, v_add, 2 v_fma, v_rcp
+//       (the numerator folded: (1 - E_c) r = fma(-E_c, r, r))
 //
-// = 12 VALU + 8 transcendental = 112 issue cycles per unit-step, against
+// = 11 VALU + 8 transcendental = 108 issue cycles per unit-step, against
 // 20 + 7 = 136 for the fused-fraction form with in-kernel scaling and clamps
 // on every exponent (152 before the weights carried the scale).
 #pragma once
@@ -43,7 +44,21 @@ __device__ __forceinline__ float lstm_exp2_clamped(float x) {
 // ai, af, ao: -log2(e) x;  ag: -2 log2(e) x (pre-scaled gate pre-activations)
 // cs: the scaled cell state (in / out);  h: the hidden output (unscaled)
 __device__ __forceinline__ void lstm_cell(float ai, float af, float ag, float ao, float& cs, float& h) {
-#ifdef FM_LSTM_CELL_AB14
+#if defined(FM_LSTM_CELL_AB) && FM_LSTM_CELL_AB == 12
+  // A/B build only (tools/build_native.py --variant): the 12-VALU form
+  {
+    const float sf1 = __builtin_amdgcn_rcpf(1.f + lstm_exp2(af));
+    const float eg1 = lstm_exp2_clamped(ag);
+    const float pg1 = 1.f + eg1;
+    const float kig1 = __builtin_fmaf(eg1, -kLstmK, kLstmK) * __builtin_amdgcn_rcpf(__builtin_fmaf(lstm_exp2(ai), pg1, pg1));
+    cs = __builtin_fmaf(cs, sf1, kig1);
+    const float ec1 = lstm_exp2_clamped(cs);
+    const float pc1 = 1.f + ec1;
+    h = (1.f - ec1) * __builtin_amdgcn_rcpf(__builtin_fmaf(lstm_exp2(ao), pc1, pc1));
+    return;
+  }
+#endif
+#if defined(FM_LSTM_CELL_AB) && FM_LSTM_CELL_AB == 14
   // A/B build only (tools/build_native.py --variant): the 14-VALU form
   const float sf0 = __builtin_amdgcn_rcpf(1.f + lstm_exp2(af));
   const float eg0 = lstm_exp2_clamped(ag);
@@ -61,7 +76,8 @@ __device__ __forceinline__ void lstm_cell(float ai, float af, float ag, float ao
   cs = __builtin_fmaf(cs, sf, kig);
   const float ec = lstm_exp2_clamped(cs);
   const float pc = 1.f + ec;
-  h = (1.f - ec) * __builtin_amdgcn_rcpf(__builtin_fmaf(lstm_exp2(ao), pc, pc));   // (1 + E_o)(1 + E_c)
+  const float r = __builtin_amdgcn_rcpf(__builtin_fmaf(lstm_exp2(ao), pc, pc));   // 1 / ((1 + E_o)(1 + E_c))
+  h = __builtin_fmaf(-ec, r, r);                                                  // (1 - E_c) r
 }
 
 // Separate-gate form of the same pre-scaled recurrence (10 transcendentals;

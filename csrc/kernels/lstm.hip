@@ -582,3 +582,65 @@ FM_API int fm_lstm_forward(const void* xa, int64_t B, int L, int H, const void* 
                            const float* c0, float* h_out, float* c_out, unsigned short* hseq, hipStream_t stream) {
   return fm_lstm_forward_nct(xa, B, L, H, Wpack, h0, c0, h_out, c_out, hseq, 0, stream);
 }
+
+// ---------------------------------------------------------------------------
+// The forecaster's linear head and de-normalisation in one pass:
+//   fc[b, j] = mu[b] + sd[b] * (h[b, :] . W[min(j, Hz - 1), :] + bias[min(j, Hz - 1)])
+// for j < Hout (a horizon past the head's Hz repeats its last step, as
+// LSTMForecaster._head).  One thread per sequence, W and bias in LDS (Hz x H
+// <= 64 x 256 floats); replaces mm + add + cat + mul + add.
+// ---------------------------------------------------------------------------
+template <int H>
+__global__ __launch_bounds__(256) void lstm_head_kernel(const float* __restrict__ h, int64_t B,
+                                                        const float* __restrict__ W, const float* __restrict__ bias,
+                                                        int Hz, const float* __restrict__ mu,
+                                                        const float* __restrict__ sd, int Hout,
+                                                        float* __restrict__ fc) {
+  extern __shared__ float sw[];            // [Hz][H] then bias [Hz]
+  for (int i = threadIdx.x; i < Hz * H; i += blockDim.x) sw[i] = W[i];
+  for (int i = threadIdx.x; i < Hz; i += blockDim.x) sw[Hz * H + i] = bias[i];
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float4* hr = reinterpret_cast<const float4*>(h + b * H);
+  float acc[64];
+  const int nz = Hz < 64 ? Hz : 64;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) acc[j] = 0.f;
+  for (int k4 = 0; k4 < H / 4; ++k4) {
+    const float4 x = hr[k4];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      if (j < nz) {
+        const float* w = sw + j * H + 4 * k4;
+        acc[j] = __builtin_fmaf(x.x, w[0], __builtin_fmaf(x.y, w[1], __builtin_fmaf(x.z, w[2], __builtin_fmaf(x.w, w[3], acc[j]))));
+      }
+    }
+  }
+  const float m = mu[b], s = sd[b];
+  for (int j = 0; j < Hout; ++j) {
+    const int jj = j < nz ? j : nz - 1;
+    float z = 0.f;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) z = q == jj ? acc[q] : z;
+    fc[b * Hout + j] = __builtin_fmaf(s, z + sw[Hz * H + jj], m);
+  }
+}
+
+FM_API int fm_lstm_head(const float* h, int64_t B, int H, const float* W, const float* bias, int Hz, const float* mu,
+                        const float* sd, int Hout, float* fc, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (Hz < 1 || Hz > 64 || Hout < 1) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((B + 255) / 256));
+  const size_t lds = (size_t)(Hz * H + Hz) * sizeof(float);
+#define FM_HEAD(HH) hipLaunchKernelGGL(lstm_head_kernel<HH>, grid, dim3(256), lds, stream, h, B, W, bias, Hz, mu, sd, \
+                                       Hout, fc)
+  if (H == 128) FM_HEAD(128);
+  else if (H == 64) FM_HEAD(64);
+  else if (H == 32) FM_HEAD(32);
+  else if (H == 256) FM_HEAD(256);
+  else return (int)hipErrorInvalidValue;
+#undef FM_HEAD
+  FM_LAUNCH_CHECK();
+  return 0;
+}

@@ -805,7 +805,7 @@ class Brain:
         one a no-op (returns None).  Returns the file path (``wait``) or the
         pending future."""
         from . import checkpoint
-        from .fastpath import history_snapshot, history_state
+        from .fastpath import history_snapshot, history_state, poll_event
         if self.fast is None:
             return None
         prev = getattr(self, "_hist_future", None)
@@ -844,7 +844,7 @@ class Brain:
                 t, meta, ev = history_state(self.fast, pinned, stream, snap=snap)
                 meta.update(rank=self.info.rank, world=self.info.world)
                 if ev is not None:
-                    ev.synchronize()
+                    poll_event(ev)
                 return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
             finally:
                 sys.setswitchinterval(iv)

@@ -2520,6 +2520,15 @@ class FastPath:
                                               w.plan.cluster) for w in gone_w], self.b.clock(), unbind=True)
 
 
+def poll_event(e, sleep: float = 2e-4) -> None:
+    """Wait for a device event from a background thread by polling it: a
+    blocking event wait there measured ~30x slower brain cycles meanwhile
+    (the loop's own HIP calls queued behind the waiting thread)."""
+    import time
+    while not e.query():
+        time.sleep(sleep)
+
+
 class _StoreSnap:
     """What a history checkpoint needs of one resident store, frozen at the
     moment the save was issued (host arrays copied, grid columns on the
@@ -2657,7 +2666,7 @@ def history_state(fp: "FastPath", pinned: dict | None = None, stream=None, snap:
                     hv[r0:r0 + rb].copy_(blk[r0:r0 + rb], non_blocking=True)
                     e = torch.cuda.Event()
                     e.record(side)
-                    e.synchronize()
+                    poll_event(e)
                 blk.record_stream(side)
                 t[f"{name}.values"] = hv
         ev = torch.cuda.Event()

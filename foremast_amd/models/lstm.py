@@ -64,6 +64,7 @@ class LSTMForecaster:
         self.lstm.load_state_dict({k[5:]: v for k, v in sd.items() if k.startswith("lstm.")})
         self.head.load_state_dict({k[5:]: v for k, v in sd.items() if k.startswith("head.")})
         self._packed = None
+        self._head_dev = None
 
     @property
     def stacked(self) -> bool:
@@ -138,6 +139,14 @@ class LSTMForecaster:
         return self._head(hT, mu, sd, hT.shape[0], H)
 
     def _head(self, hT, mu, sd, R: int, H: int):
+        if hT.is_cuda and self.M is None and self.H in (32, 64, 128, 256) and self.horizon <= 64:
+            # linear head + de-normalisation in one kernel (fm_lstm_head)
+            dev = hT.device
+            hw = getattr(self, "_head_dev", None)
+            if hw is None or hw[0] != dev:
+                hw = self._head_dev = (dev, self.head.weight.detach().float().contiguous().to(dev),
+                                       self.head.bias.detach().float().contiguous().to(dev))
+            return LS.lstm_head(hT, hw[1], hw[2], mu, sd, H), sd.contiguous()
         W = self.head.weight.to(hT.device)
         b = self.head.bias.to(hT.device)
         z = hT @ W.T + b                                    # [rows, horizon (x M)]

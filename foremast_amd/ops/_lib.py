@@ -70,6 +70,7 @@ _SIGS: dict[str, list] = {
     "fm_hpa_score_slots": [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            ctypes.c_double, c_float, c_float, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p],
+    "fm_lstm_head": [c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "fm_es_update": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "fm_band_decide": [c_void_p, c_i64, c_int, c_void_p, c_i64, c_void_p, c_i64, c_int, c_void_p, c_void_p,

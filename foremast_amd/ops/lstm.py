@@ -255,6 +255,21 @@ def lstm_forward_hist(hist: torch.Tensor, T: int, L: int, period: float, I: int,
     return hT, cT, mu, sd
 
 
+def lstm_head(hT: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, mu: torch.Tensor, sd: torch.Tensor,
+              Hout: int) -> torch.Tensor:
+    """fc [B, Hout] = mu + sd * (hT @ W.T + bias), a horizon past W's rows
+    repeating its last step (``fm_lstm_head``, one pass)."""
+    B, H = hT.shape
+    Hz = W.shape[0]
+    check(hT.is_contiguous() and hT.dtype == torch.float32 and W.shape == (Hz, H) and W.is_contiguous()
+          and bias.numel() == Hz and mu.numel() == B and sd.numel() == B and 1 <= Hz <= 64, "bad LSTM head shapes")
+    require_native(hT)
+    fc = torch.empty((B, Hout), dtype=torch.float32, device=hT.device)
+    LIB.call("fm_lstm_head", ptr(hT), B, H, ptr(W), ptr(bias.contiguous()), Hz, ptr(mu.contiguous()),
+             ptr(sd.contiguous()), int(Hout), ptr(fc), stream_of(hT))
+    return fc
+
+
 def lstm_features(hist: torch.Tensor, T: int, L: int, period: float, I: int = 3):
     """Augmented forecaster input straight from the packed history (GPU):
     -> (xa [R, L, 16] bf16, mu [R], sd [R]).  Features [z, sin, cos][:I] of the

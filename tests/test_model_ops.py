@@ -486,6 +486,26 @@ def test_gpu_lstm_hist_kernel_matches_feature_path(cuda, H, I):
     torch.testing.assert_close(h2, h1, rtol=0, atol=0)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,Hz,Hout", [(128, 10, 10), (64, 60, 75), (32, 5, 3), (256, 8, 8)])
+def test_gpu_lstm_head_matches_torch(cuda, H, Hz, Hout):
+    """fm_lstm_head == the forecaster's ATen head: mu + sd * (h W^T + b), a
+    longer horizon repeating the head's last step."""
+    g = torch.Generator().manual_seed(H + Hz)
+    B = 777
+    h = torch.randn(B, H, generator=g).to(cuda)
+    W = torch.randn(Hz, H, generator=g).to(cuda) * 0.1
+    b = torch.randn(Hz, generator=g).to(cuda)
+    mu = torch.randn(B, generator=g).to(cuda)
+    sd = torch.rand(B, generator=g).to(cuda) + 0.1
+    z = h @ W.T + b
+    if Hout > Hz:
+        z = torch.cat([z, z[:, -1:].expand(-1, Hout - Hz)], 1)
+    want = mu[:, None] + sd[:, None] * z[:, :Hout]
+    got = LS.lstm_head(h, W, b, mu, sd, Hout)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
+
+
 def test_ref_lstm_stack_matches_torch_two_layers():
     torch.manual_seed(0)
     m = torch.nn.LSTM(5, 32, num_layers=2, batch_first=True)

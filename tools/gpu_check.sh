@@ -36,6 +36,7 @@ for s in $steps; do
           run lstm_tests 400 python -u -m pytest tests/test_model_ops.py -m gpu -k "lstm" -v --timeout 120 \
               --timeout-method thread || exit $rc
           run lstm_ab 200 python -u tools/lstm_ab.py || exit $rc
+          run lstm_ab_c12 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_c12.so python -u tools/lstm_ab.py || exit $rc
           run lstm_ab_c14 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_c14.so python -u tools/lstm_ab.py || exit $rc
           run lstm_ab_r4 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_r4.so python -u tools/lstm_ab.py || exit $rc
           run config4 300 python -u benchmarks/bench_configs.py --config 4 || exit $rc
