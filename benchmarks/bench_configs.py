@@ -583,14 +583,55 @@ def config3e2e(args):
             if live is not None:
                 req_log.pop()
                 http_stats.pop()
-            for k in brain.spans.last:
-                if spans.get(k):
-                    spans[k].pop()
+            sp_ = {k: round(spans[k].pop(), 2) for k in brain.spans.last if spans.get(k)}
             t_w = time.perf_counter()
             if fut is not None and hasattr(fut, "result"):
                 fut.result()
             async_save[tag_] = {"cycle_with_async_save_ms": round(save_cycle_ms, 2), "issue_ms": round(issue_ms, 2),
-                                "writer_tail_after_cycle_s": round(time.perf_counter() - t_w, 3)}
+                                "writer_tail_after_cycle_s": round(time.perf_counter() - t_w, 3),
+                                "spans_ms": {k: v for k, v in sp_.items() if v >= 0.5}}
+        if os.environ.get("FOREMAST_SAVE_DIAG") and dev.type == "cuda":
+            # which part of the background save stretches the cycle beside it:
+            # the writer's Python only / + the side-stream gather / + the host copy
+            # / + the file
+            import threading
+            from foremast_amd.engine import fastpath as _fpm
+            diag = {}
+            sstream = torch.cuda.Stream(dev)
+            dbufs, pins = {}, {}
+            for mode in ("snap", "rows", "gather", "d2h", "file"):
+                snap_, _ = _fpm.history_snapshot(brain.fast, dbufs, sstream)
+
+                def work(mode=mode, snap_=snap_):
+                    torch.cuda.set_device(dev)
+                    if mode == "rows":
+                        list(_fpm._history_rows(snap_["works"], snap_["stores"]))
+                    elif mode == "gather":
+                        with torch.cuda.stream(sstream):
+                            for _n, st_, rr, _k, _o in _fpm._history_rows(snap_["works"], snap_["stores"]):
+                                if len(rr):
+                                    st_.grid.index_select(0, torch.as_tensor(rr, device=dev))
+                        e_ = torch.cuda.Event()
+                        e_.record(sstream)
+                        _fpm.poll_event(e_)
+                    elif mode in ("d2h", "file"):
+                        t_, m_, e_ = _fpm.history_state(brain.fast, pins, sstream, snap=snap_)
+                        if e_ is not None:
+                            _fpm.poll_event(e_)
+                        if mode == "file":
+                            from foremast_amd.engine import checkpoint as _ck
+                            _ck.save(ck_a, t_, m_, tag="diag", keep=1, kind="history")
+                th = threading.Thread(target=work) if mode != "snap" else None
+                if th is not None:
+                    th.start()
+                step()
+                c_ = cyc_ms.pop()
+                rows.pop()
+                sp_ = {k: round(spans[k].pop(), 2) for k in brain.spans.last if spans.get(k)}
+                if th is not None:
+                    th.join()
+                diag[mode] = {"cycle_ms": round(c_, 2), "spans_ms": {k: v for k, v in sp_.items() if v >= 0.5}}
+            async_save["diag"] = diag
         import shutil
         shutil.rmtree(ck_a, ignore_errors=True)
         t_s = time.perf_counter()

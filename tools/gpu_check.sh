@@ -84,6 +84,7 @@ for s in $steps; do
                > gpurun_out/hostprof_2e2e_http.txt || exit 1 ;;
     restart) e2e c3e2e_restart --config 3e2e --steps 5 --warmup 2 --restart &&
          e2e c2e2e_restart --config 2e2e --steps 5 --warmup 2 --restart || exit $rc ;;
+    savediag) FOREMAST_SAVE_DIAG=1 e2e c2e2e_savediag --config 2e2e --steps 5 --warmup 2 --restart || exit $rc ;;
     scanprobe) run scanprobe 200 python -u tools/hw_scan_probe.py || exit $rc
           run scanab 300 python -u tools/hw_scan_ab.py --rows 40000 --m 1440 288 720 --reps 5 || exit $rc
           run scanab_1pass 300 env FOREMAST_HW_SCAN_PASSES=1 python -u tools/hw_scan_ab.py --rows 40000 --m 1440 \
