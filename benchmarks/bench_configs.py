@@ -592,45 +592,59 @@ def config3e2e(args):
                                 "spans_ms": {k: v for k, v in sp_.items() if v >= 0.5}}
         if os.environ.get("FOREMAST_SAVE_DIAG") and dev.type == "cuda":
             # which part of the background save stretches the cycle beside it:
-            # the writer's Python only / + the side-stream gather / + the host copy
-            # / + the file
+            # the issue alone (device gather + host copy draining during the
+            # cycle) / + a thread polling its event / + the writer's CPU work
+            # (per-row lists, meta, file) after the copy; a sampler records
+            # where the loop's thread is meanwhile
+            import collections
             import threading
+            from foremast_amd.engine import checkpoint as _ck
             from foremast_amd.engine import fastpath as _fpm
             diag = {}
             sstream = torch.cuda.Stream(dev)
             dbufs, pins = {}, {}
-            for mode in ("snap", "rows", "gather", "d2h", "file"):
-                snap_, _ = _fpm.history_snapshot(brain.fast, dbufs, sstream)
+            main_id = threading.get_ident()
 
-                def work(mode=mode, snap_=snap_):
-                    torch.cuda.set_device(dev)
-                    if mode == "rows":
-                        list(_fpm._history_rows(snap_["works"], snap_["stores"]))
-                    elif mode == "gather":
-                        with torch.cuda.stream(sstream):
-                            for _n, st_, rr, _k, _o in _fpm._history_rows(snap_["works"], snap_["stores"]):
-                                if len(rr):
-                                    st_.grid.index_select(0, torch.as_tensor(rr, device=dev))
-                        e_ = torch.cuda.Event()
-                        e_.record(sstream)
-                        _fpm.poll_event(e_)
-                    elif mode in ("d2h", "file"):
-                        t_, m_, e_ = _fpm.history_state(brain.fast, pins, sstream, snap=snap_)
-                        if e_ is not None:
-                            _fpm.poll_event(e_)
-                        if mode == "file":
-                            from foremast_amd.engine import checkpoint as _ck
-                            _ck.save(ck_a, t_, m_, tag="diag", keep=1, kind="history")
-                th = threading.Thread(target=work) if mode != "snap" else None
+            def sampler(stop, counts):
+                while not stop.is_set():
+                    f = sys._current_frames().get(main_id)
+                    fr = []
+                    while f is not None and len(fr) < 3:
+                        if "foremast_amd" in f.f_code.co_filename or "benchmarks" in f.f_code.co_filename:
+                            fr.append(f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}:{f.f_code.co_name}")
+                        f = f.f_back
+                    counts[" <- ".join(fr)] += 1
+                    time.sleep(1e-3)
+            for mode in ("issue", "poll", "state"):
+                hs_ = _fpm.history_issue(brain.fast, dbufs, pins, sstream)
+                th = None
+                if mode == "poll":
+                    def work(hs_=hs_):
+                        while not hs_.ready():
+                            time.sleep(2e-3)
+                    th = threading.Thread(target=work)
+                elif mode == "state":
+                    hs_.ev.synchronize()
+
+                    def work(hs_=hs_):
+                        t_, m_ = hs_.state()
+                        _ck.save(ck_a, t_, m_, tag="diag", keep=1, kind="history")
+                    th = threading.Thread(target=work)
+                stop, counts = threading.Event(), collections.Counter()
+                smp = threading.Thread(target=sampler, args=(stop, counts), daemon=True)
+                smp.start()
                 if th is not None:
                     th.start()
                 step()
+                stop.set()
                 c_ = cyc_ms.pop()
                 rows.pop()
                 sp_ = {k: round(spans[k].pop(), 2) for k in brain.spans.last if spans.get(k)}
                 if th is not None:
                     th.join()
-                diag[mode] = {"cycle_ms": round(c_, 2), "spans_ms": {k: v for k, v in sp_.items() if v >= 0.5}}
+                hs_.ev.synchronize()
+                diag[mode] = {"cycle_ms": round(c_, 2), "spans_ms": {k: v for k, v in sp_.items() if v >= 0.5},
+                              "main_thread_samples": counts.most_common(6)}
             async_save["diag"] = diag
         import shutil
         shutil.rmtree(ck_a, ignore_errors=True)

@@ -455,7 +455,7 @@ class Brain:
                 self.fast.housekeeping()
         if self.exporter is not None:
             self.exporter.sweep(now)
-        return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast),
+        return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast) - (len(self.fast.ghost_ids) if fast and self.fast.ghost_mask(fast) is not None else 0),
                 "seconds": time.perf_counter() - t0}
 
     def _score_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict) -> list:
@@ -498,7 +498,8 @@ class Brain:
                     bulk.extend(gb)
                     if grp[0].plan.hpa and self.exporter is not None and self.cfg.hpa_forecast_algorithm:
                         self._fast_hpa_forecasts(g)
-                n_rows += len(grp) * M
+                gm = fp.ghost_mask(grp)
+                n_rows += (len(grp) if gm is None else int((~gm).sum())) * M
             except Exception:
                 log.exception("fast-path finish of %d jobs failed; re-scoring per job", len(grp))
                 n_rows += self._fast_per_job(grp, M, now, updates, hpalogs, outcome)
@@ -507,7 +508,7 @@ class Brain:
     def _fast_per_job(self, grp, M: int, now: float, updates: list, hpalogs: list, outcome: dict) -> int:
         n = 0
         fp = self.fast
-        for fw in grp:
+        for fw in fp.live(grp):                       # (a job that left the fleet is not judged)
             try:
                 g = fp.score_group([fw], now)
                 fp.finish_group(g, now, updates, hpalogs, outcome,
@@ -525,6 +526,9 @@ class Brain:
             log.warning("HPA forecast skipped: %s", e)
             return
         ok = np.isfinite(peak)
+        gm = self.fast.ghost_mask(works)
+        if gm is not None:
+            ok &= np.repeat(~gm, M)
         if ok.any():
             ga = g["ga"]
 
@@ -805,7 +809,7 @@ class Brain:
         one a no-op (returns None).  Returns the file path (``wait``) or the
         pending future."""
         from . import checkpoint
-        from .fastpath import history_snapshot, history_state, poll_event
+        from .fastpath import history_issue
         if self.fast is None:
             return None
         prev = getattr(self, "_hist_future", None)
@@ -816,7 +820,7 @@ class Brain:
             prev.result()
         tag = checkpoint.rank_tag(self.info.rank, self.info.world)
         if wait or self.device.type != "cuda":
-            t, meta, _ = history_state(self.fast)
+            t, meta = history_issue(self.fast).state()
             meta.update(rank=self.info.rank, world=self.info.world)
             return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
         if getattr(self, "_hist_stream", None) is None:
@@ -825,26 +829,26 @@ class Brain:
             self._hist_dev: dict = {}
             from concurrent.futures import ThreadPoolExecutor
             self._hist_writer = ThreadPoolExecutor(1, thread_name_prefix="history-ckpt")
-        # in the cycle: a device copy of the live grid columns + host state
-        # copies; everything per row (keys, owner order, gather, host copy,
-        # file) on the writer thread
-        snap, _ = history_snapshot(self.fast, self._hist_dev, self._hist_stream)
-        stream, pinned, dev = self._hist_stream, self._hist_pinned, self.device
+        # in the cycle: the row lists, a gather launch and an async host copy;
+        # the per-row key / owner lists, meta and file on the writer thread,
+        # which makes no device call (it polls the copy's event through
+        # HistorySave.ready, a non-blocking query)
+        hs = history_issue(self.fast, self._hist_dev, self._hist_pinned, self._hist_stream)
+        rank, world = self.info.rank, self.info.world
 
         def write():
-            # the writer's Python (per-row keys, owner order, meta JSON) hands
-            # the interpreter back within 0.1 ms whenever the brain loop asks
-            # for it (the default 5-ms switch interval let a background save
-            # stretch the loop's cycles); file writes release it anyway
+            # the writer's Python hands the interpreter back within 0.1 ms
+            # whenever the brain loop asks for it (the default 5-ms switch
+            # interval let a background save stretch the loop's cycles); file
+            # writes release it anyway
             import sys
             iv = sys.getswitchinterval()
             sys.setswitchinterval(min(iv, 1e-4))
             try:
-                torch.cuda.set_device(dev)
-                t, meta, ev = history_state(self.fast, pinned, stream, snap=snap)
-                meta.update(rank=self.info.rank, world=self.info.world)
-                if ev is not None:
-                    poll_event(ev)
+                while not hs.ready():
+                    time.sleep(2e-3)
+                t, meta = hs.state()
+                meta.update(rank=rank, world=world)
                 return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
             finally:
                 sys.setswitchinterval(iv)

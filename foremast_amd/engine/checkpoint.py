@@ -210,7 +210,7 @@ def read_owned_rows(path: Path, owns, world: int | None = None, rank: int | None
     """A history checkpoint restricted to the rows ``owns(namespace, app)``
     selects, reading only those rows from disk (safetensors slices of each
     ``<store>.*`` row tensor).  Rows are saved in 16 owner blocks
-    (``<store>.blocks``, fastpath.history_state): for a ``world`` dividing 16
+    (``<store>.blocks``, fastpath.history_issue): for a ``world`` dividing 16
     a rank's rows are whole blocks, a few contiguous reads; any other world
     reads the coalesced runs of its rows.  -> (tensors, meta, saved_at)."""
     from safetensors import safe_open

@@ -487,6 +487,16 @@ class FastPath:
         self._gsigs: dict = {}    # interned plan-group signatures
         self._gcount: dict = {}   # plan group -> jobs in self.works
         self._jid_cache: dict = {}  # id(job list) -> (list, JobIds), cleared every cycle
+        # stable layout of a one-sliding-group fleet: jobs that
+        # left stay in the list as masked "ghosts" -- fetched and scored with
+        # the rest, never judged -- so the list object, its template lists,
+        # static columns, cache keys and model arrays survive fleet churn; the
+        # list is compacted every LAYOUT_COMPACT_EVERY cycles or when ghosts
+        # pass LAYOUT_GHOST_FRAC of it
+        self._lay = None           # (job list, cycle it was laid out)
+        self.ghost = None          # bool [len(list)]: the list's ghosts this cycle (None: none)
+        self.ghost_ids: set = set()   # id() of this cycle's ghost FastWork objects
+        self.ghost_cycles = 0      # cycles that ran on a ghosted layout (instead of a re-laid list)
         from .ingest import WindowTable
         cfg = brain.cfg
         self.wt = WindowTable(cfg.metric_settle_s, cfg.fetch_batch, cfg.fetch_max_values)
@@ -607,6 +617,8 @@ class FastPath:
             self._reused = True
             if keep_jid is not None and keep_jid[0] is fast:     # same list object: same ids
                 self._jid_cache[id(fast)] = keep_jid
+            if self.ghost is not None:
+                self.ghost_cycles += 1
             return fast, []
         self._reused = False
         works = self.works
@@ -615,8 +627,13 @@ class FastPath:
         fws = list(map(works.get, batch.ids))
         if None not in fws and list(map(_version_of, fws)) == list(batch.versions):
             if len(self._gcount) == 1 and fws and fws[0].plan.sliding:
-                todo = fws                            # one sliding group: every job is due every cycle
+                # one sliding group: every job is due every cycle -- on the
+                # stable layout when the fleet only lost jobs since it was laid
+                if keep_jid is not None and self._lay is not None and keep_jid[0] is self._lay[0]:
+                    self._jid_cache[id(keep_jid[0])] = keep_jid
+                fws = todo = self._layout(fws)
             else:
+                self._set_layout(None)
                 todo = [fw for fw in fws if not ((immutable or fw.wcur is not None) and fw.settled)]
                 if len(todo) == len(fws):
                     todo = fws
@@ -624,6 +641,7 @@ class FastPath:
             self.todo = todo
             self._last = (batch.ids, batch.versions, fws, todo)
             return fws, []
+        self._set_layout(None)
         fast, unknown, todo = [], [], []
         handles = getattr(batch, "handles", None)
         for k, (jid, ver) in enumerate(zip(batch.ids, batch.versions)):
@@ -671,9 +689,52 @@ class FastPath:
         self._specs = {}
         if len(todo) == len(fast):
             todo = fast
+        if len(self._gcount) == 1 and fast and fast[0].plan.sliding and todo is fast and not rest:
+            self._set_layout(fast)
         self.todo = todo
         self._last = (batch.ids, batch.versions, fast, todo) if not rest else None
         return fast, rest
+
+    LAYOUT_COMPACT_EVERY = 32
+    LAYOUT_GHOST_FRAC = 0.125
+
+    def _set_layout(self, works) -> None:
+        self._lay = None if works is None else (works, self.cycle)
+        self.ghost, self.ghost_ids = None, set()
+
+    def _layout(self, fws: list) -> list:
+        """The job list a one-sliding-group fleet is scored as this cycle:
+        the laid-out list with this claim's missing jobs masked as ghosts
+        (``self.ghost``), or ``fws`` itself, laid out afresh, when it gained
+        jobs, the ghosts would pass LAYOUT_GHOST_FRAC, or the layout is
+        LAYOUT_COMPACT_EVERY cycles old."""
+        lay = self._lay
+        if lay is not None and lay[0] is not fws and self.cycle - lay[1] < self.LAYOUT_COMPACT_EVERY:
+            L = lay[0]
+            if len(fws) <= len(L) and len(L) - len(fws) <= self.LAYOUT_GHOST_FRAC * len(L):
+                ix = self._jid(fws).index_in(self._jid(L))
+                if ix is not None:
+                    ghost = np.ones(len(L), bool)
+                    ghost[ix] = False
+                    if ghost.any():
+                        self.ghost = ghost
+                        self.ghost_ids = {id(L[j]) for j in np.flatnonzero(ghost).tolist()}
+                        self.ghost_cycles += 1
+                    else:
+                        self.ghost, self.ghost_ids = None, set()
+                    return L
+        self._set_layout(fws)
+        return fws
+
+    def ghost_mask(self, works) -> np.ndarray | None:
+        """This cycle's ghost mask of a job list (None: every job is live)."""
+        lay = self._lay
+        return self.ghost if (self.ghost is not None and lay is not None and works is lay[0]) else None
+
+    def live(self, works: list) -> list:
+        """``works`` without this cycle's ghosts."""
+        g = self.ghost_ids
+        return [fw for fw in works if id(fw) not in g] if g else works
 
     def fetch_all(self, works: list[FastWork], now: float, pool=None) -> list[FastWork]:
         """Fetch what the jobs in ``self.todo`` need this cycle (from an
@@ -2220,7 +2281,13 @@ class FastPath:
             return
         ids = self._impact_ids(g["ga"], g["works"], impact)
         keys = None if impact.names else [(w.plan.cluster, w.plan.namespace, w.doc.app_name) for w in g["works"]]
-        impact.observe(ids, g["packed"][:, 0] == 1, now, keys=keys)
+        bad = g["packed"][:, 0] == 1
+        gm = self.ghost_mask(g["works"])
+        if gm is not None:                          # a job that left reports nothing
+            lv = np.flatnonzero(~gm)
+            ids, bad = ids[lv], bad[lv]
+            keys = None if keys is None else [keys[j] for j in lv.tolist()]
+        impact.observe(ids, bad, now, keys=keys)
 
     def finish_group(self, g: dict, now: float, updates: list, hpalogs: list, outcome: dict,
                      bulk: list | None = None, impact=None) -> None:
@@ -2235,24 +2302,33 @@ class FastPath:
         stats, packed = g["stats"], g["packed"]
         cur, cur_t = g["cur"], g["cur_t"]
         anom = g["anom"]
+        gm = self.ghost_mask(works)               # jobs that left the fleet: scored, never judged
         exp = self.b.exporter
         if exp is not None:
             # newest anomalous timestamp per row (dashboard reads it as a time)
             anom_ts = np.full(R, np.nan)
             if len(anom):
                 np.fmax.at(anom_ts, anom[:, 0], cur_t[anom[:, 0], anom[:, 1]])
-            exp.set_bounds_many(ga.export_slots if ga.export_start is None else ga.export_start,
-                                stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64), anom_ts)
+            if gm is None:
+                exp.set_bounds_many(ga.export_slots if ga.export_start is None else ga.export_start,
+                                    stats[:, 2].astype(np.float64), stats[:, 3].astype(np.float64), anom_ts)
+            else:
+                lr = np.repeat(~gm, M)
+                exp.set_bounds_many(ga.export_slots[lr], stats[lr, 2].astype(np.float64),
+                                    stats[lr, 3].astype(np.float64), anom_ts[lr])
         if works[0].plan.hpa:
             l3 = g.get("last3")
             if bulk is None:
-                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, updates_bulk := [], ga, l3)
+                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, updates_bulk := [], ga, l3,
+                                 gm)
                 updates.extend((i, f) for ids, f, _ in updates_bulk for i in ids)
             else:
-                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga, l3)
+                self._finish_hpa(works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga, l3, gm)
             return
         status = packed[:, 0]
         unh = status == 1
+        if gm is not None:
+            unh &= ~gm
         down = None
         if impact is not None and len(impact.impact):
             ids = self._impact_ids(ga, works, impact)
@@ -2264,6 +2340,8 @@ class FastPath:
                                                        [w.plan.cluster for w in works])
                 exp.table.set(ga.impact_slots, val.astype(np.float64))
             down = val >= self.b.cfg.downstream_threshold
+            if gm is not None:
+                down &= ~gm
             if impact.cfg.downstream_mode == "judge":
                 unh = unh | down
             else:
@@ -2271,8 +2349,12 @@ class FastPath:
             if not down.any():
                 down = None
         done = (now >= ga.end) & ~unh
+        if gm is not None:
+            done &= ~gm
         miss = ga.missing.any(1)
         alive = ~unh & ~done
+        if gm is not None:
+            alive &= ~gm
         healthy = done & ~miss
         unknown = done & miss
         if bulk is None:
@@ -2322,7 +2404,7 @@ class FastPath:
             outcome[ST.COMPLETED_UNHEALTH] = outcome.get(ST.COMPLETED_UNHEALTH, 0) + int(unh.sum())
         if flush:
             updates.extend((i, f) for ids, f, _ in bulk for i in ids)
-        closed = ~alive
+        closed = ~alive if gm is None else ~alive & ~gm
         if closed.any():
             self._release([works[j] for j in np.flatnonzero(closed)])
 
@@ -2354,7 +2436,8 @@ class FastPath:
         return ST.COMPLETED_UNHEALTH, {"status": ST.COMPLETED_UNHEALTH, "reason": html.escape(json.dumps(reasons)),
                                        "anomaly_info": json.dumps(anomalies)}
 
-    def _finish_hpa(self, works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga=None, last3=None) -> None:
+    def _finish_hpa(self, works, M, cur, stats, now, updates, hpalogs, outcome, bulk, ga=None, last3=None,
+                    gm=None) -> None:
         S = len(works)
         last = _last_finite(cur)                    # (rows with no point: the last column, NaN)
         lastv = cur[np.arange(len(cur)), last]
@@ -2403,6 +2486,8 @@ class FastPath:
             self.hpa.scatter(sl, sub)
             sc, rs = sc.cpu().numpy(), rs.cpu().numpy()
         due = self.hpa.log_due(sl_np, sc.astype(np.int64), rs.astype(np.int64), now, cfg.hpa_log_interval_s)
+        if gm is not None:
+            due &= ~gm
         created = rfc3339(datetime.fromtimestamp(now, timezone.utc))
         exp = self.b.exporter
         if exp is not None:
@@ -2415,7 +2500,10 @@ class FastPath:
                         w.plan.hpa_slots = h
                 return np.stack([w.plan.hpa_slots for w in ws])
             hs = self._extra(key, ga.ident, "xhpa", xhpa) if key is not None else xhpa(None)
-            exp.set_hpa_scores(hs, sc.astype(np.float64))
+            if gm is None:
+                exp.set_hpa_scores(hs, sc.astype(np.float64))
+            else:
+                exp.set_hpa_scores(hs[~gm], sc[~gm].astype(np.float64))
         al = works[0].plan.aliases
         dj = np.flatnonzero(due)
         if len(dj):
@@ -2429,10 +2517,16 @@ class FastPath:
                                        [MI.REASONS[c] for c in codes], list(al), z(cl), z(up), z(lo), handles=hd))
         # HPA jobs stay alive: one uniform "keep" for the whole group
         if ga is not None and len(ga.ids) == S:
-            bulk.append((ga.ids, {"status": ST.PREPROCESS_COMPLETED}, ga.handles))
+            if gm is None:
+                bulk.append((ga.ids, {"status": ST.PREPROCESS_COMPLETED}, ga.handles))
+            else:
+                lv = ~gm
+                bulk.append((ga.ids[lv], {"status": ST.PREPROCESS_COMPLETED},
+                             None if ga.handles is None else ga.handles[lv]))
         else:
-            updates.extend((w.doc.id, {"status": ST.PREPROCESS_COMPLETED}) for w in works)
-        outcome["hpa_scored"] = outcome.get("hpa_scored", 0) + S
+            updates.extend((w.doc.id, {"status": ST.PREPROCESS_COMPLETED}) for j, w in enumerate(works)
+                           if gm is None or not gm[j])
+        outcome["hpa_scored"] = outcome.get("hpa_scored", 0) + (S if gm is None else int((~gm).sum()))
 
     def _release(self, works: list[FastWork]) -> None:
         """Terminal jobs: their static history rows, table windows and plans
@@ -2505,6 +2599,8 @@ class FastPath:
         gone = self.sliding.evict_idle(self.cycle, self.max_idle_cycles) + \
             self.static.evict_idle(self.cycle, self.max_idle_cycles)
         if gone:
+            self._set_layout(None)
+            self._last = None
             # jobs whose rows were evicted re-plan (and re-fetch) if they come back
             stale = [k for k, w in self.works.items()
                      if (self.sliding if w.plan.sliding else self.static).keys[int(w.rows[0])] != w.plan.keys[0]]
@@ -2529,149 +2625,168 @@ def poll_event(e, sleep: float = 2e-4) -> None:
         time.sleep(sleep)
 
 
-class _StoreSnap:
-    """What a history checkpoint needs of one resident store, frozen at the
-    moment the save was issued (host arrays copied, grid columns on the
-    device or the live grid itself for a synchronous save)."""
-    __slots__ = ("sliding", "keys", "last_t", "nlen", "t0", "ws", "e", "step", "device", "grid", "c0")
-
-    def __init__(self, st, grid, c0: int):
-        self.sliding, self.keys = st.sliding, list(st.keys)
-        self.last_t, self.nlen = st.last_t.copy(), st.nlen.copy()
-        self.t0, self.ws, self.e, self.step, self.device = st.t0, st.ws, st.e, st.step, st.device
-        self.grid, self.c0 = grid, c0            # grid[:, j] is the store's column c0 + j
-
-
-def _history_rows(works, snaps: dict):
-    """(store name, snapshot, rows, keys, owners) of every resident row a live
-    job references -- what a warm restart needs."""
-    per = {"static": {}, "sliding": {}}
-    for w in works:
-        p = w.plan
-        d = per["sliding" if p.sliding else "static"]
-        for r, k in zip(w.rows.tolist(), p.keys):
-            d.setdefault(int(r), (k, (p.namespace, w.doc.app_name)))
-    for name in ("static", "sliding"):
-        st = snaps[name]
-        d = per[name]
-        rows = np.array([r for r in sorted(d) if r < len(st.keys) and st.keys[r] == d[r][0]], np.int64)
-        yield name, st, rows, [d[int(r)][0] for r in rows], [d[int(r)][1] for r in rows]
-
-
 OWNER_BLOCKS = 16           # saved rows are grouped by service_owner(.., 16): one block per rank of any world | 16
 
 
-def history_snapshot(fp: "FastPath", dev_bufs: dict | None = None, stream=None) -> tuple[dict, object]:
-    """Freeze what a history checkpoint needs, cheaply: the live jobs, the
-    stores' row keys / times, and (``dev_bufs`` + ``stream``: the periodic
-    asynchronous save) a device copy of each store's live grid columns, made on
-    ``stream`` after the current stream's work -- the current stream then
-    waits only for that copy (about 1 ms of HBM traffic per GB), and the
-    per-row bookkeeping, the row gather and the host copy happen later, off the
-    brain loop (:func:`history_state`).  -> (snapshot, event or None)."""
-    works = list(fp.works.values())
-    snaps: dict = {}
-    cur = torch.cuda.current_stream(fp.b.device) if (fp.b.device.type == "cuda" and stream is not None) else None
-    if cur is not None:
-        stream.wait_stream(cur)
-    for name, st in (("static", fp.static), ("sliding", fp.sliding)):
-        if st.sliding:
-            c0, c1 = (st.ws, st.e) if st.t0 is not None else (0, 0)
-        else:
-            c0, c1 = 0, max(1, st.max_len)
-        view = st.buf[:, c0:c1]
-        if cur is None:
-            snaps[name] = _StoreSnap(st, view, c0)
-            continue
-        R, W = view.shape
-        g = dev_bufs.get(name)
-        if g is None or g.numel() < R * W:
-            g = dev_bufs[name] = torch.empty((int(R * W * 1.25) + 64,), dtype=view.dtype, device=view.device)
-        gv = g[:R * W].view(R, W)
-        with torch.cuda.stream(stream):
-            gv.copy_(view, non_blocking=True)
-        snaps[name] = _StoreSnap(st, gv, c0)
-    ev = None
-    if cur is not None:
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        cur.wait_event(ev)                       # the next cycle's grid writes wait for the copy only
-    return {"works": works, "stores": snaps, "step": fp.b.step}, ev
+def _owner_block(p: JobPlan) -> int:
+    """service_owner(namespace, app, OWNER_BLOCKS) of a plan, computed once."""
+    b = p.__dict__.get("_oblk")
+    if b is None:
+        from ..parallel.dist import service_owner
+        b = p.__dict__["_oblk"] = service_owner(p.namespace, p.app, OWNER_BLOCKS)
+    return b
 
 
-def history_state(fp: "FastPath", pinned: dict | None = None, stream=None, snap: dict | None = None
-                  ) -> tuple[dict, dict, object]:
-    """The device-resident history of every live job (static rows: the
-    left-aligned samples; sliding rows: the window's columns) + their row
-    keys, owners and times, for a warm restart (``Brain.save_history``).
+class _StorePart:
+    """One resident store's share of a history checkpoint in flight: the
+    saved rows (owner-block order), the host copies of their per-row state,
+    the jobs they came from (keys / owners are listed off the loop), and the
+    gathered values (device block + pinned host copy, or a CPU tensor)."""
+    __slots__ = ("name", "ws", "flat", "jix", "rows", "keys_now", "last_t", "nlen", "blocks", "t_first", "values")
+
+
+class HistorySave:
+    """A history checkpoint issued by :func:`history_issue`: ``ready()`` once
+    the device gather and host copy are done, then ``state()`` (any thread,
+    no device calls) -> ``(tensors, meta)`` for ``checkpoint.save``."""
+
+    def __init__(self, step: int, parts: list, ev) -> None:
+        self.step, self.parts, self.ev = step, parts, ev
+
+    def ready(self) -> bool:
+        return self.ev is None or self.ev.query()
+
+    def state(self) -> tuple[dict, dict]:
+        t: dict[str, torch.Tensor] = {}
+        meta: dict = {"step": self.step}
+        for sp in self.parts:
+            name = sp.name
+            keys_flat = [k for w in sp.ws for k in w.plan.keys]
+            keys = [keys_flat[i] for i in sp.flat.tolist()]
+            own_job = [(w.plan.namespace, w.plan.app) for w in sp.ws]
+            owners = [own_job[j] for j in sp.jix.tolist()]
+            vals = sp.values
+            # a row re-assigned since (an evicted job's): not this job's history
+            ok = np.fromiter((a == b for a, b in zip(keys, sp.keys_now)), bool, len(keys))
+            if not ok.all():
+                keep = np.flatnonzero(ok)
+                vals = vals[torch.from_numpy(keep)]
+                keys, owners = [keys[i] for i in keep], [owners[i] for i in keep]
+                sp.last_t = sp.last_t[keep]
+                sp.nlen = None if sp.nlen is None else sp.nlen[keep]
+                ob = np.fromiter((_owner_of(o) for o in owners), np.int64, len(owners))
+                sp.blocks = np.searchsorted(ob, np.arange(OWNER_BLOCKS + 1)).tolist()
+            meta[f"{name}.blocks"] = sp.blocks
+            if sp.t_first is not None:
+                meta[f"{name}.t_first"] = sp.t_first
+            if sp.nlen is not None:
+                t[f"{name}.nlen"] = torch.from_numpy(sp.nlen)
+            t[f"{name}.values"] = vals
+            t[f"{name}.last_t"] = torch.from_numpy(sp.last_t)
+            meta[f"{name}.keys"] = [list(k) for k in keys]
+            meta[f"{name}.owners"] = [list(o) for o in owners]
+        return t, meta
+
+
+def _owner_of(o) -> int:
+    from ..parallel.dist import service_owner
+    return service_owner(o[0], o[1], OWNER_BLOCKS)
+
+
+def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | None = None,
+                  stream=None) -> HistorySave:
+    """Issue a history checkpoint of every live job's resident rows (static:
+    the left-aligned samples; sliding: the window's columns), for a warm
+    restart (``Brain.save_history``).
 
     Rows are ordered by ``service_owner(namespace, app, 16)`` (``meta
     "{name}.blocks"`` = the row offsets of the 16 owner blocks): after a
     re-shard to a world that divides 16, a rank reads only its blocks.
 
-    ``snap`` (:func:`history_snapshot`): build the state from that frozen
-    snapshot (the asynchronous save runs this on its writer thread);
-    ``pinned`` (reusable pinned host buffers) + ``stream``: the rows are
-    gathered on ``stream`` and copied into pinned host memory asynchronously;
-    the returned event marks the host copy complete (None: synchronous,
-    tensors ready)."""
-    from ..parallel.dist import service_owner
-    if snap is None:
-        snap, _ = history_snapshot(fp)
-    t: dict[str, torch.Tensor] = {}
-    meta: dict = {"step": snap["step"]}
-    side = stream if (pinned is not None and stream is not None) else None
-    ev = None
-    gathered: list = []
-    for name, st, rows, keys, owners in _history_rows(snap["works"], snap["stores"]):
+    On the brain loop's thread this costs a few vectorised host passes (row
+    lists per job, owner blocks cached per plan) and a few launches: with
+    ``dev_bufs`` + ``pinned`` + ``stream`` the rows are gathered on ``stream``
+    into a reusable device block straight from the live grid (the current
+    stream waits for that gather only, ~1 ms per GB) and copied into reusable
+    pinned host memory behind it, asynchronously; the loop's next cycles run
+    while the copy drains.  The per-row lists and the file are built off the
+    loop (:meth:`HistorySave.state`), with no device calls there -- a writer
+    thread that gathered, copied or waited on the device itself measured
+    5-25x slower brain cycles meanwhile."""
+    works = list(fp.works.values())
+    dev = fp.b.device
+    asyn = dev.type == "cuda" and stream is not None and pinned is not None and dev_bufs is not None
+    cur = torch.cuda.current_stream(dev) if asyn else None
+    if asyn:
+        stream.wait_stream(cur)
+    parts = []
+    gathered = []
+    for name, st in (("static", fp.static), ("sliding", fp.sliding)):
+        ws = [w for w in works if w.plan.sliding == st.sliding]
+        if not ws:
+            continue
+        lens = np.fromiter((len(w.rows) for w in ws), np.int64, len(ws))
+        rows_all = np.concatenate([w.rows for w in ws]).astype(np.int64)
+        ob_job = np.fromiter((_owner_block(w.plan) for w in ws), np.int64, len(ws))
+        jix_all = np.repeat(np.arange(len(ws)), lens)
+        u, first = np.unique(rows_all, return_index=True)      # each row once, ascending
+        keep = u < len(st.keys)
+        first = first[keep]
+        ob = ob_job[jix_all[first]]
+        order = np.argsort(ob, kind="stable")                  # owner blocks, rows ascending within
+        flat = first[order]
+        rows = rows_all[flat]
         if not len(rows):
             continue
-        oc: dict = {}
-        ob = np.fromiter((oc[o] if o in oc else oc.setdefault(o, service_owner(o[0], o[1], OWNER_BLOCKS))
-                          for o in owners), np.int64, len(owners))
-        order = np.argsort(ob, kind="stable")
-        rows, keys, owners = rows[order], [keys[i] for i in order], [owners[i] for i in order]
-        meta[f"{name}.blocks"] = np.searchsorted(ob[order], np.arange(OWNER_BLOCKS + 1)).tolist()
-        ri = torch.as_tensor(rows, device=st.device)
         if st.sliding:
             if st.t0 is None or st.e <= st.ws:
                 continue
-            view = st.grid[:, st.ws - st.c0:st.e - st.c0]
-            meta[f"{name}.t_first"] = st.t0 + st.ws * st.step
+            c0, c1 = st.ws, st.e
         else:
-            w = max(1, int(st.nlen[rows].max()))
-            view = st.grid[:, :w]
-            t[f"{name}.nlen"] = torch.from_numpy(st.nlen[rows].copy())
-        if side is None:
-            t[f"{name}.values"] = view.index_select(0, ri).cpu()
+            c0, c1 = 0, max(1, int(st.nlen[rows].max()))
+        sp = _StorePart()
+        sp.name, sp.ws, sp.flat, sp.jix, sp.rows = name, ws, flat, jix_all[flat], rows
+        sp.keys_now = [st.keys[r] for r in rows.tolist()]
+        sp.last_t = st.last_t[rows].copy()
+        sp.nlen = None if st.sliding else st.nlen[rows].copy()
+        sp.blocks = np.searchsorted(ob[order], np.arange(OWNER_BLOCKS + 1)).tolist()
+        sp.t_first = st.t0 + st.ws * st.step if st.sliding else None
+        view = st.buf[:, c0:c1]
+        if not asyn:
+            sp.values = view.index_select(0, torch.as_tensor(rows, device=view.device)).cpu()
         else:
-            with torch.cuda.stream(side):
-                gathered.append((name, view.index_select(0, ri)))  # contiguous [rows, w] on the device
-        t[f"{name}.last_t"] = torch.from_numpy(st.last_t[rows].copy())
-        meta[f"{name}.keys"] = [list(k) for k in keys]
-        meta[f"{name}.owners"] = [list(o) for o in owners]
-    if side is not None:
-        with torch.cuda.stream(side):
-            for name, blk in gathered:
-                n = blk.numel() * blk.element_size()
-                host = pinned.get(name)
-                if host is None or host.numel() < n:
-                    host = pinned[name] = torch.empty(int(n * 1.25) + 64, dtype=torch.uint8, pin_memory=True)
-                hv = host[:n].view(blk.dtype).view(blk.shape)
-                # in 32 MB pieces, each waited for: a gigabyte-sized copy would
-                # hold the copy engine and the brain loop's own small
-                # transfers would queue behind it
-                rb = max(1, (32 << 20) // max(1, blk.shape[1] * blk.element_size()))
-                for r0 in range(0, blk.shape[0], rb):
-                    hv[r0:r0 + rb].copy_(blk[r0:r0 + rb], non_blocking=True)
-                    e = torch.cuda.Event()
-                    e.record(side)
-                    poll_event(e)
-                blk.record_stream(side)
-                t[f"{name}.values"] = hv
+            R, W = len(rows), c1 - c0
+            g = dev_bufs.get(name)
+            if g is None or g.numel() < R * W:
+                g = dev_bufs[name] = torch.empty((int(R * W * 1.25) + 64,), dtype=view.dtype, device=dev)
+            n = R * W * view.element_size()
+            host = pinned.get(name)
+            if host is None or host.numel() < n:
+                host = pinned[name] = torch.empty(int(n * 1.25) + 64, dtype=torch.uint8, pin_memory=True)
+            ri = torch.from_numpy(rows).pin_memory()
+            gathered.append((g[:R * W].view(R, W), view, ri, host[:n].view(view.dtype).view(R, W)))
+            sp.values = gathered[-1][3]
+        parts.append(sp)
+    ev = None
+    if asyn and gathered:
+        with torch.cuda.stream(stream):
+            for blk, view, ri, hv in gathered:
+                torch.index_select(view, 0, ri.to(dev, non_blocking=True), out=blk)
+        g_ev = torch.cuda.Event()
+        g_ev.record(stream)
+        cur.wait_event(g_ev)                     # the loop's grid writes wait for the gather only
+        with torch.cuda.stream(stream):
+            for blk, view, ri, hv in gathered:
+                hv.copy_(blk, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(side)
-    return t, meta, ev
+        ev.record(stream)
+    return HistorySave(fp.b.step, parts, ev)
+
+
+def history_state(fp: "FastPath") -> tuple[dict, dict]:
+    """The history checkpoint of every live job, synchronously (see
+    :func:`history_issue`)."""
+    return history_issue(fp).state()
 
 
 def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> int:

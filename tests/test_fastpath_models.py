@@ -345,3 +345,37 @@ def test_mixed_churning_fleet_fast_path_equals_general_path():
         b[0].t += 60
     st = {a[1].get(j).status for j in ids}
     assert ST.COMPLETED_UNHEALTH in st and (ST.PREPROCESS_INPROGRESS in st or ST.PREPROCESS_COMPLETED in st)
+
+
+@pytest.mark.parametrize("compact_every", [32, 3])
+def test_ghost_layout_under_churn_equals_general_path(compact_every):
+    """VERDICT r4 #2 (stable layout): monitored services that regress close
+    mid-run; the fast path keeps scoring the one-sliding-group fleet on its
+    laid-out job list with the closed jobs masked as ghosts (no template-list,
+    static-column or model-array rebuild), and compacts the list every
+    ``compact_every`` cycles.  Verdicts, reasons and gauges equal the general
+    path's cycle by cycle; a closed job is never judged again."""
+    faults = {"cont3": 4.0, "cont9": 4.0}
+    a = _brain(True, "holt_winters", faults)
+    b = _brain(False, "holt_winters", faults)
+    a[3].fast.LAYOUT_COMPACT_EVERY = compact_every
+
+    def submit(client):
+        return [client.start_analyzing("prod", f"cont{j}", None, _metrics(4), 10, "continuous") for j in range(16)]
+    ids = submit(a[2])
+    assert ids == submit(b[2])
+    closed_at: dict = {}
+    for cyc in range(9):
+        ra, rb = a[3].run_once(), b[3].run_once()
+        assert ra["claimed"] == rb["claimed"] and ra["rows"] == rb["rows"], (cyc, ra, rb)
+        _compare(a, b, ids, cyc)
+        for j in ids:
+            d = a[1].get(j)
+            if d.status == ST.COMPLETED_UNHEALTH:
+                if j in closed_at:                          # judged once: never rewritten
+                    assert d.modified_at == closed_at[j], (cyc, j)
+                closed_at.setdefault(j, d.modified_at)
+        a[0].t += 60
+        b[0].t += 60
+    assert len(closed_at) >= 2                              # the faults (+ noise closes at 2 sigma)
+    assert a[3].fast.ghost_cycles > 0

@@ -200,6 +200,15 @@ def test_gpu_async_history_save_is_off_the_cycle(tmp_path):
     b2 = Brain(MemoryStore(), BrainConfig(), device=torch.device("cuda"), clock=clock, worker_id="w",
                sources=SourceRouter(synthetic=SyntheticSource(), force="synthetic"))
     assert b2.load_history(str(tmp_path)) == live_rows
+    # the asynchronous file holds exactly what a synchronous save writes
+    from safetensors import safe_open
+    da, ds = tmp_path / "a", tmp_path / "s"
+    pa = b.save_history(str(da), wait=False).result(timeout=60)
+    ps = b.save_history(str(ds))
+    with safe_open(str(pa), "pt") as fa, safe_open(str(ps), "pt") as fs:
+        assert sorted(fa.keys()) == sorted(fs.keys()) and fa.metadata()["meta"] == fs.metadata()["meta"]
+        for k in fa.keys():
+            torch.testing.assert_close(fa.get_tensor(k), fs.get_tensor(k), equal_nan=True, rtol=0, atol=0)
 
 
 def test_write_safetensors_reads_back_with_safetensors(tmp_path):

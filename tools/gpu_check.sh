@@ -42,7 +42,7 @@ for s in $steps; do
           run config4 300 python -u benchmarks/bench_configs.py --config 4 || exit $rc
           run config4_stack 300 python -u benchmarks/bench_configs.py --config 4 --hidden 256 --layers 2 --multivariate || exit $rc ;;
     pmclstm) run pmclstm 420 bash tools/pmc_lstm.sh || exit $rc ;;
-    r5tests) run r5tests 600 python -u -m pytest tests/test_fastpath_models.py tests/test_canary_ops.py \
+    r5tests) run r5tests 600 python -u -m pytest tests/test_fastpath_models.py tests/test_canary_ops.py tests/test_warm_restart.py \
                  tests/test_model_ops.py tests/test_fastpath.py -m gpu -x -v --timeout 120 --timeout-method thread \
                  || exit $rc ;;
     peer) run peer_test 300 python -u -m pytest tests/test_peer.py tests/test_board.py -x -v -s --timeout 200 \
