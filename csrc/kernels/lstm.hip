@@ -230,6 +230,10 @@ struct HistSource {
   float p, ip;               // period and 1 / period
   int I;
   bool lo_half;              // lane holds k = 0..7 (the features), else k = 8..15 (zeros)
+  // per step t: {f1, bits of pack_bf2(f2, f3)} -- the phase features are the
+  // same for every sequence, built once per workgroup in LDS (null: L too
+  // long for the table, computed per lane)
+  const float2* tab;
   __device__ __forceinline__ Raw fetch(int ct, int t) const {
     const int bc = c0 + t + off[ct];
     return (lo_half && bc >= 0 && bc < lim[ct]) ? row[ct][bc] : __builtin_nanf("");
@@ -237,6 +241,10 @@ struct HistSource {
   __device__ __forceinline__ uint4 make(int ct, int t, const Raw& v) const {
     if (!lo_half) return make_uint4(0u, 0u, 0u, 0u);
     const float z = isfinite(v) ? (v - mu[ct]) * inv[ct] : 0.f;
+    if (tab != nullptr) {
+      const float2 e = tab[t];
+      return make_uint4(pack_bf2(I > 0 ? z : 1.f, e.x), __float_as_uint(e.y), 0u, 0u);
+    }
     const float c = (float)(c0 + t);
     const float q = floorf(c * ip);
     const float fr = __builtin_fmaf(-q, p, c) * ip;          // phase in revolutions, [0, 1)
@@ -248,7 +256,20 @@ struct HistSource {
     const float f3 = I == 3 ? 1.f : 0.f;
     return make_uint4(pack_bf2(f0, f1), pack_bf2(f2, f3), 0u, 0u);
   }
+  // the table entry of step t (what make() computes per lane without it)
+  __device__ __forceinline__ float2 phase_entry(int t) const {
+    const float c = (float)(c0 + t);
+    const float q = floorf(c * ip);
+    const float fr = __builtin_fmaf(-q, p, c) * ip;
+    const float sn = __builtin_amdgcn_sinf(fr), cs = __builtin_amdgcn_cosf(fr);
+    const float f1 = I > 1 ? sn : (I == 1 ? 1.f : 0.f);
+    const float f2 = I > 2 ? cs : (I == 2 ? 1.f : 0.f);
+    const float f3 = I == 3 ? 1.f : 0.f;
+    return make_float2(f1, __uint_as_float(pack_bf2(f2, f3)));
+  }
 };
+
+constexpr int kLstmPhaseTab = 2048;     // steps of the LDS phase table (16 KB)
 
 template <int H, bool HSEQ, typename XS>
 __device__ __forceinline__ void lstm_pipe_body(const XS& xs, int64_t B, int L, const uint4* __restrict__ Wpack,
@@ -385,6 +406,7 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_hist_kernel(const float* __res
                                                               float* __restrict__ mu_out, float* __restrict__ sd_out) {
   __shared__ __attribute__((aligned(16))) unsigned short hbuf[64 * (H + 8)];
   __shared__ float smu[64], sinv[64];
+  __shared__ float2 stab[kLstmPhaseTab];
   const int lane = lane_id(), w = wave_id();
   constexpr int NW = H / 16;
   const int64_t b0 = (int64_t)blockIdx.x * 64;
@@ -439,6 +461,12 @@ __global__ __launch_bounds__(H * 4) void lstm_fwd_hist_kernel(const float* __res
   xs.ip = 1.f / period;
   xs.I = I;
   xs.lo_half = (lane >> 5) == 0;
+  xs.tab = nullptr;
+  if (L <= kLstmPhaseTab) {
+    for (int t = threadIdx.x; t < L; t += H * 4) stab[t] = xs.phase_entry(t);
+    __syncthreads();
+    xs.tab = stab;
+  }
   lstm_pipe_body<H, false>(xs, B, L, Wpack, nullptr, nullptr, h_out, c_out, nullptr, hbuf);
 }
 

@@ -112,6 +112,15 @@ def save(dirpath: str, tensors: dict[str, torch.Tensor], meta: dict, step: int |
     return path
 
 
+def _json_fields(tensors: dict, meta: dict) -> dict:
+    """Move ``<name>_json`` uint8 tensors (UTF-8 JSON a writer stored as bytes
+    instead of header metadata, e.g. a history checkpoint's row keys) into
+    ``meta[<name>]``."""
+    for n in [n for n in tensors if n.endswith("_json")]:
+        meta[n[:-len("_json")]] = json.loads(bytes(tensors.pop(n).numpy()).decode())
+    return meta
+
+
 def _read(path: Path) -> tuple[dict[str, torch.Tensor], dict, float] | None:
     if not path.exists():
         return None
@@ -120,7 +129,8 @@ def _read(path: Path) -> tuple[dict[str, torch.Tensor], dict, float] | None:
         md = f.metadata() or {}
     if md.get("format") != FORMAT_VERSION:
         raise ValueError(f"unsupported checkpoint format {md.get('format')!r}")
-    return load_file(str(path)), json.loads(md.get("meta", "{}")), float(md.get("saved_at", "0"))
+    t = load_file(str(path))
+    return t, _json_fields(t, json.loads(md.get("meta", "{}"))), float(md.get("saved_at", "0"))
 
 
 def saved_at(path: Path) -> float:
@@ -222,6 +232,9 @@ def read_owned_rows(path: Path, owns, world: int | None = None, rank: int | None
             raise ValueError(f"unsupported checkpoint format {md.get('format')!r}")
         meta = json.loads(md.get("meta", "{}"))
         names = list(f.keys())
+        js = [n for n in names if n.endswith("_json")]
+        _json_fields({n: f.get_tensor(n) for n in js}, meta)       # row keys / owners: whole
+        names = [n for n in names if n not in js]
         out: dict[str, torch.Tensor] = {}
         for store in sorted({n.split(".", 1)[0] for n in names}):
             owners = meta.get(f"{store}.owners", [])

@@ -40,6 +40,7 @@ import logging
 import math
 from dataclasses import dataclass, field, replace
 from datetime import datetime, timezone
+from itertools import chain
 
 import numpy as np
 import torch
@@ -2628,6 +2629,13 @@ def poll_event(e, sleep: float = 2e-4) -> None:
 OWNER_BLOCKS = 16           # saved rows are grouped by service_owner(.., 16): one block per rank of any world | 16
 
 
+_plan_of = __import__("operator").attrgetter("plan")
+_rows_of = __import__("operator").attrgetter("rows")
+_oblk_of = __import__("operator").attrgetter("_oblk")
+_hfr_of = __import__("operator").attrgetter("_hfr")
+_sliding_of = __import__("operator").attrgetter("sliding")
+
+
 def _owner_block(p: JobPlan) -> int:
     """service_owner(namespace, app, OWNER_BLOCKS) of a plan, computed once."""
     b = p.__dict__.get("_oblk")
@@ -2639,16 +2647,36 @@ def _owner_block(p: JobPlan) -> int:
 
 class _StorePart:
     """One resident store's share of a history checkpoint in flight: the
-    saved rows (owner-block order), the host copies of their per-row state,
-    the jobs they came from (keys / owners are listed off the loop), and the
-    gathered values (device block + pinned host copy, or a CPU tensor)."""
-    __slots__ = ("name", "ws", "flat", "jix", "rows", "keys_now", "last_t", "nlen", "blocks", "t_first", "values")
+    host copies of the saved rows' per-row state, their keys / owners as
+    ready JSON bytes, and the gathered values (pinned host copy of a device
+    gather, or a CPU tensor)."""
+    __slots__ = ("name", "last_t", "nlen", "blocks", "t_first", "values", "keys_json", "owners_json")
+
+
+def _plan_frags(p: JobPlan) -> tuple[list, str]:
+    """(JSON text of each row key, JSON text of the owner) of a plan, encoded
+    once per plan for the history checkpoints."""
+    f = p.__dict__.get("_hfr")
+    if f is None:
+        enc = json.JSONEncoder(separators=(",", ":")).encode
+        f = p.__dict__["_hfr"] = ([enc(list(k)) for k in p.keys], enc([p.namespace, p.app]))
+    return f
+
+
+def _json_list(frags: list, idx: np.ndarray) -> torch.Tensor:
+    """UTF-8 bytes of the JSON list of ``frags[idx]`` (C-level picks and joins)."""
+    from operator import itemgetter
+    ix = idx.tolist()
+    got = (frags[ix[0]],) if len(ix) == 1 else (itemgetter(*ix)(frags) if ix else ())
+    return torch.frombuffer(bytearray(("[" + ",".join(got) + "]").encode()), dtype=torch.uint8)
 
 
 class HistorySave:
     """A history checkpoint issued by :func:`history_issue`: ``ready()`` once
-    the device gather and host copy are done, then ``state()`` (any thread,
-    no device calls) -> ``(tensors, meta)`` for ``checkpoint.save``."""
+    the device gather and host copy are done, then ``state()`` -> ``(tensors,
+    meta)`` for ``checkpoint.save`` -- no device call and next to no Python
+    (the row keys / owners are ready JSON bytes saved as ``uint8`` tensors), so
+    a writer thread holds the interpreter only for moments."""
 
     def __init__(self, step: int, parts: list, ev) -> None:
         self.step, self.parts, self.ev = step, parts, ev
@@ -2661,36 +2689,16 @@ class HistorySave:
         meta: dict = {"step": self.step}
         for sp in self.parts:
             name = sp.name
-            keys_flat = [k for w in sp.ws for k in w.plan.keys]
-            keys = [keys_flat[i] for i in sp.flat.tolist()]
-            own_job = [(w.plan.namespace, w.plan.app) for w in sp.ws]
-            owners = [own_job[j] for j in sp.jix.tolist()]
-            vals = sp.values
-            # a row re-assigned since (an evicted job's): not this job's history
-            ok = np.fromiter((a == b for a, b in zip(keys, sp.keys_now)), bool, len(keys))
-            if not ok.all():
-                keep = np.flatnonzero(ok)
-                vals = vals[torch.from_numpy(keep)]
-                keys, owners = [keys[i] for i in keep], [owners[i] for i in keep]
-                sp.last_t = sp.last_t[keep]
-                sp.nlen = None if sp.nlen is None else sp.nlen[keep]
-                ob = np.fromiter((_owner_of(o) for o in owners), np.int64, len(owners))
-                sp.blocks = np.searchsorted(ob, np.arange(OWNER_BLOCKS + 1)).tolist()
             meta[f"{name}.blocks"] = sp.blocks
             if sp.t_first is not None:
                 meta[f"{name}.t_first"] = sp.t_first
             if sp.nlen is not None:
                 t[f"{name}.nlen"] = torch.from_numpy(sp.nlen)
-            t[f"{name}.values"] = vals
+            t[f"{name}.values"] = sp.values
             t[f"{name}.last_t"] = torch.from_numpy(sp.last_t)
-            meta[f"{name}.keys"] = [list(k) for k in keys]
-            meta[f"{name}.owners"] = [list(o) for o in owners]
+            t[f"{name}.keys_json"] = sp.keys_json
+            t[f"{name}.owners_json"] = sp.owners_json
         return t, meta
-
-
-def _owner_of(o) -> int:
-    from ..parallel.dist import service_owner
-    return service_owner(o[0], o[1], OWNER_BLOCKS)
 
 
 def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | None = None,
@@ -2721,13 +2729,30 @@ def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | N
         stream.wait_stream(cur)
     parts = []
     gathered = []
+    # per-job lists through C-level maps (attrgetter), the per-plan owner
+    # block and JSON fragments cached on the plan at its first save
+    plans = list(map(_plan_of, works))
+    try:
+        ob_all = np.fromiter(map(_oblk_of, plans), np.int64, len(plans))
+        fr_all = list(map(_hfr_of, plans))
+    except AttributeError:
+        for p in plans:
+            _owner_block(p)
+            _plan_frags(p)
+        ob_all = np.fromiter(map(_oblk_of, plans), np.int64, len(plans))
+        fr_all = list(map(_hfr_of, plans))
+    sl_all = np.fromiter(map(_sliding_of, plans), bool, len(plans))
+    w_obj = np.empty(len(works), object)
+    w_obj[:] = works
     for name, st in (("static", fp.static), ("sliding", fp.sliding)):
-        ws = [w for w in works if w.plan.sliding == st.sliding]
-        if not ws:
+        pick = np.flatnonzero(sl_all == st.sliding)
+        if not len(pick):
             continue
-        lens = np.fromiter((len(w.rows) for w in ws), np.int64, len(ws))
-        rows_all = np.concatenate([w.rows for w in ws]).astype(np.int64)
-        ob_job = np.fromiter((_owner_block(w.plan) for w in ws), np.int64, len(ws))
+        ws = w_obj[pick].tolist()
+        rows_l = list(map(_rows_of, ws))
+        lens = np.fromiter(map(len, rows_l), np.int64, len(ws))
+        rows_all = np.concatenate(rows_l).astype(np.int64)
+        ob_job = ob_all[pick]
         jix_all = np.repeat(np.arange(len(ws)), lens)
         u, first = np.unique(rows_all, return_index=True)      # each row once, ascending
         keep = u < len(st.keys)
@@ -2745,8 +2770,10 @@ def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | N
         else:
             c0, c1 = 0, max(1, int(st.nlen[rows].max()))
         sp = _StorePart()
-        sp.name, sp.ws, sp.flat, sp.jix, sp.rows = name, ws, flat, jix_all[flat], rows
-        sp.keys_now = [st.keys[r] for r in rows.tolist()]
+        sp.name = name
+        fr = [fr_all[i] for i in pick.tolist()]
+        sp.keys_json = _json_list(list(chain.from_iterable(f[0] for f in fr)), flat)
+        sp.owners_json = _json_list([f[1] for f in fr], jix_all[flat])
         sp.last_t = st.last_t[rows].copy()
         sp.nlen = None if st.sliding else st.nlen[rows].copy()
         sp.blocks = np.searchsorted(ob[order], np.arange(OWNER_BLOCKS + 1)).tolist()
