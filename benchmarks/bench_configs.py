@@ -334,7 +334,9 @@ def config3e2e(args):
     # continuous / HPA jobs stay alive for the whole run (their end time is
     # the submission window); canary jobs use the 10-minute watch window
     # (in the mixed fleet one that outlasts the run: its churn is explicit)
-    n_cycles = args.steps + args.warmup + 3
+    # (+ the --restart cycles: two async-save cycles, the save diagnosis's,
+    # and the restarted brain's first: inside the staged window too)
+    n_cycles = args.steps + args.warmup + 3 + (8 if args.restart else 0)
     long_window = max(args.window, int(n_cycles * poll / 60) + 20)
 
     def submit_one(client, c, j):

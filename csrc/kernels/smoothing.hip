@@ -895,14 +895,18 @@ FM_API int fm_band_decide(const float* cur, int64_t ld_c, int n, const float* ce
 //     (rows without history, valid bit 0, flag nothing);
 //   * stats[r] = (nan, nan, upper, lower) at the row's last finite point;
 //   * wave 0 reduces the service (service_reduce_kernel semantics) from LDS;
-//   * anomalous points append (row, point), value through one atomic per row
-//     to ctr[par]; block 0 zeroes ctr[par ^ 1] for the next cycle.  (A
+//   * anomalous points append (row, point, band upper, band lower), value
+//     through one atomic per row to ctr[par]; block 0 zeroes ctr[par ^ 1]
+//     for the next cycle.  The host takes the total from the per-row counts
+//     (their sum), so no counter copy follows the launch.  (A
 //     last-workgroup-publishes-the-counter epilogue -- one same-address
-//     device atomic per workgroup -- measured 43 -> 327 us at 10k workgroups:
-//     the counter is copied into hostv by the host instead.)
+//     device atomic per workgroup -- measured 43 -> 327 us at 10k
+//     workgroups.)
+//   * the current window is row r of cur, or (cur_rm) grid row cur_rm[r] of
+//     cur = the grid's first window column: read in place, no gather.
 // Host outputs land in one buffer (hostv: packed [S,4] | stats [R,4] | count
-// [R] (int) | dead [R] (int) | counters [2] (int)) for a single device->host
-// copy.
+// [R] (int) | dead [R] (int) | counters [2] (int, unused)) for a single
+// device->host copy.
 // ---------------------------------------------------------------------------
 constexpr int kStepKMax = 64;      // new samples per row per cycle handled in-kernel
 constexpr int kStepMMax = 16;      // metrics per service (waves per workgroup)
@@ -919,7 +923,7 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
     const int64_t* __restrict__ lastk, float* __restrict__ upper, float* __restrict__ lower,
     float* __restrict__ sigma_out, float* __restrict__ fc, int Hf, float* __restrict__ hostv, int cap,
     int* __restrict__ ctr, int par, int* __restrict__ out_idx, float* __restrict__ out_val,
-    float* __restrict__ last3) {
+    float* __restrict__ last3, const int* __restrict__ cur_rm) {
   __shared__ float xs[kStepMMax][kStepKMax];
   __shared__ float su[kStepMMax][kStepKMax];
   __shared__ int s_cnt[kStepMMax];
@@ -930,6 +934,8 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
   const int lane = lane_id();
   const int64_t R = S * M;
   const int64_t row = s * M + mi;
+  // the row's current window: its own row of cur, or (cur_rm) a grid row
+  const float* __restrict__ crow = cur + (cur_rm != nullptr ? (int64_t)cur_rm[row] : row) * ld_c;
   if (blockIdx.x == 0 && threadIdx.x == 0) ctr[par ^ 1] = 0;
   float lvl = 0.f, tr = 0.f, sig = 0.f;
   int ph = 0, ph_old = 0, k = 0;
@@ -1032,7 +1038,7 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
       if (lo < minlb[mm]) lo = minlb[mm];
       upper[row * n + i] = up;
       lower[row * n + i] = lo;
-      const float x = cur[row * ld_c + i];
+      const float x = crow[i];
       if (i == lk) {
         float* st = hostv + S * 4 + row * 4;
         st[0] = __builtin_nanf("");
@@ -1074,9 +1080,15 @@ __global__ __launch_bounds__(1024) void es_band_step_kernel(
       const unsigned long long below = lane == 0 ? 0ull : (word & ((1ull << lane) - 1ull));
       const int slot = base + written + __popcll(below);
       if (((word >> lane) & 1ull) && slot < cap) {
-        out_idx[2 * slot + 0] = (int)row;
-        out_idx[2 * slot + 1] = w * 64 + lane;
-        out_val[slot] = cur[row * ld_c + w * 64 + lane];
+        // [row, point, band upper, band lower] (the band at the point read
+        // back from this lane's own writes above): a verdict's reasons need
+        // no gather of the per-point bands
+        const int pt = w * 64 + lane;
+        out_idx[4 * slot + 0] = (int)row;
+        out_idx[4 * slot + 1] = pt;
+        out_idx[4 * slot + 2] = __float_as_int(upper[row * n + pt]);
+        out_idx[4 * slot + 3] = __float_as_int(lower[row * n + pt]);
+        out_val[slot] = crow[pt];
       }
       written += __popcll(word);
     }
@@ -1113,7 +1125,7 @@ FM_API int fm_es_band_step(const float* buf, int64_t ld, const int* rm, const in
                            const float* minlb, const int8_t* diff, float pair_factor, const int* valid,
                            const int64_t* lastk, float* upper, float* lower, float* sigma, float* fc, int Hf,
                            float* hostv, int cap, int* ctr, int par, int* out_idx, float* out_val, float* last3,
-                           hipStream_t stream) {
+                           const int* cur_rm, hipStream_t stream) {
   if (S <= 0) return 0;
   // kind -1: the forecast fc [R, Hf] (Hf >= H) and sigma are given (band + reduce + compaction only)
   if (kind < -1 || kind > 3 || M < 1 || M > kStepMMax || n < 1 || n > 256 || H < 1 || (par != 0 && par != 1) ||
@@ -1126,7 +1138,7 @@ FM_API int fm_es_band_step(const float* buf, int64_t ld, const int* rm, const in
   hipLaunchKernelGGL(es_band_step_kernel<KK>, grid, block, 0, stream, buf, ld, rm, shift, lim, dk, T, kmax, t_new, \
                      slots, params, m, season, sse, state, nobs, cur, ld_c, n, hor, H, S, M, thr, bound, minlb, diff, \
                      pair_factor, valid, lastk, upper, lower, sigma, fc, Hf, hostv, cap, ctr, par, out_idx, out_val, \
-                     last3)
+                     last3, cur_rm)
   if (kind == -1) FM_EBS(-1);
   else if (kind == 0) FM_EBS(0);
   else if (kind == 1) FM_EBS(1);

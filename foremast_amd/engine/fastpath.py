@@ -40,7 +40,6 @@ import logging
 import math
 from dataclasses import dataclass, field, replace
 from datetime import datetime, timezone
-from itertools import chain
 
 import numpy as np
 import torch
@@ -161,6 +160,21 @@ class GroupArrays:
     base: np.ndarray | None = None
     hist_epoch: int = -1                       # FastPath._hist_epoch the missing-data mask was built at
     hist_end: float | None = None              # merged sliding group: end of the history window
+    cur_cols: tuple | None = None              # merged sliding group: the window's grid columns [a, b)
+
+    @property
+    def cur_dev(self) -> torch.Tensor:
+        """The current windows on the device ([rows, n]).  A merged sliding
+        group's are gathered out of the grid on first use only: the fused
+        steady-cycle kernel reads them in place through the row map."""
+        c = self.cur_d
+        if callable(c):
+            c = self.cur_d = c()
+        return c
+
+    @property
+    def cur_lazy(self) -> bool:
+        return callable(self.cur_d)
 
 
 @dataclass
@@ -668,7 +682,7 @@ class FastPath:
                     rest.append(d)
                     continue
                 store = self.sliding if p.sliding else self.static
-                rows, _ = store.rows_for(p.keys, self.cycle)
+                rows, _ = store.rows_for(p.keys, self.cycle, owner=(p.namespace, p.app))
                 try:
                     end_ts = parse_rfc3339(d.end_time).timestamp() if d.end_time else now
                 except ValueError:
@@ -1427,13 +1441,15 @@ class FastPath:
                 rml = rm_d.long()
             self._rmd[key] = (rowmap, rm_d, rml)
             grab = lambda ab: store.buf[:, ab[0]:ab[1]].index_select(0, rml)   # noqa: E731
-            cur_d, base_d = grab(devc[0]), (grab(devc[1]) if base is not None else None)
+            cur_d = functools.partial(grab, devc[0])             # gathered on first use (GroupArrays.cur_dev)
+            base_d = grab(devc[1]) if base is not None else None
             has_cur = (cur_len > 0).reshape(S, M)
         else:
             cur_d, base_d = up(cur), (up(base) if base is not None else None)
             has_cur = np.isfinite(cur).any(1).reshape(S, M)
         ga = GroupArrays(ident, ids, cur, cur_t, cur_len, rowmap, cur_d, base_d,
-                         rm_d, end, ~(has_hist & has_cur), handles=handles, works=works)
+                         rm_d, end, ~(has_hist & has_cur), handles=handles, works=works,
+                         cur_cols=devc[0] if callable(cur_d) else None)
         if col is not None and pos is not None:
             ga.hist_end = col.get("hist_end")
             old = self._garr.get(key)
@@ -1504,7 +1520,7 @@ class FastPath:
                 r = (ix[:, None] * M + np.arange(M)[None, :]).reshape(-1)
                 r_d = torch.from_numpy(r).to(dev)
                 ga = GroupArrays(ident, ids, old.cur[r], old.cur_t[r], old.cur_len[r], rowmap,
-                                 old.cur_d.index_select(0, r_d),
+                                 old.cur_dev.index_select(0, r_d),
                                  None if old.base_d is None else old.base_d.index_select(0, r_d),
                                  up(rowmap), end, None, handles=handles, works=works)
                 ga.wcur, ga.wbase = wc, (wb if old.base is not None else None)
@@ -1565,14 +1581,14 @@ class FastPath:
         if not len(rows):
             return False
         wt, wc, wb = self.wt, ga.wcur, ga.wbase
-        dev = ga.cur_d.device
+        dev = ga.cur_dev.device
         if len(rows) == len(wc):
             # every window changed (a live fleet at the poll cadence): pack the
             # whole arrays straight into pinned memory, replace, one upload each
             key = ga.key
             v, t, ln = wt.pack(wc, ga.cur.shape[1], out_v=self._pinned(("tcur", key), ga.cur.shape, dev))
             ga.cur, ga.cur_t, ga.cur_len = v, t, ln
-            ga.cur_d.copy_(torch.from_numpy(v), non_blocking=True)
+            ga.cur_dev.copy_(torch.from_numpy(v), non_blocking=True)
             wt.dirty[wc[wc >= 0]] = False
             if ga.base_d is not None:
                 bv, _, _ = wt.pack(wb, ga.base.shape[1], times=False,
@@ -1584,7 +1600,7 @@ class FastPath:
         ri = torch.from_numpy(rows).to(dev)
         v, t, ln = wt.pack(wc[rows], ga.cur.shape[1])
         ga.cur[rows], ga.cur_t[rows], ga.cur_len[rows] = v, t, ln
-        ga.cur_d.index_copy_(0, ri, up(v))
+        ga.cur_dev.index_copy_(0, ri, up(v))
         wt.dirty[wc[rows][wc[rows] >= 0]] = False
         if ga.base_d is not None:
             bv, _, _ = wt.pack(wb[rows], ga.base.shape[1], times=False)
@@ -1706,21 +1722,21 @@ class FastPath:
             store.used[ga.rowmap] = self.cycle
             ga.marked = self.cycle
         n = ga.cur.shape[1]
-        o = self._scorer(p0.aliases).score_resident(store.view_until(ga.hist_end), ga.rm_d, ga.cur_d, ga.base_d)
+        o = self._scorer(p0.aliases).score_resident(store.view_until(ga.hist_end), ga.rm_d, ga.cur_dev, ga.base_d)
         dec = o.decide
         if dev.type == "cuda":
             cap = max(1024, min(R * n, 1 << 16))
-            idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, cap)
+            idx_d, val_d, ctr = self._compact(dec, ga.cur_dev, R, n, cap)
             host = [t.to("cpu", non_blocking=True) for t in (o.packed, dec.stats, dec.count, ctr)]
             torch.cuda.current_stream(dev).synchronize()
             packed, stats, count, total = (t.numpy() for t in host)
             total = int(total[0])
             if total > cap:
-                idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, total)
+                idx_d, val_d, ctr = self._compact(dec, ga.cur_dev, R, n, total)
             idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
         else:
             packed, stats, count = o.packed.numpy(), dec.stats.numpy(), dec.count.numpy()
-            ix, _ = C.compact_anomalies(dec, ga.cur_d)
+            ix, _ = C.compact_anomalies(dec, ga.cur_dev)
             idx = ix.numpy()
         # (row, point) sorted: the order of atomically appended rows is arbitrary
         # (one int64 key sort: 7x faster than a two-key lexsort on the host)
@@ -1985,7 +2001,7 @@ class FastPath:
         if ga.base_d is not None:
             pcfg = C.PairwiseConfig(cfg.pairwise_algorithm, cfg.pairwise_threshold, cfg.min_mann_white,
                                     cfg.min_wilcoxon, cfg.min_kruskal)
-            _, _, diff = C.pairwise_tests(ga.cur_d, ga.base_d, pcfg)
+            _, _, diff = C.pairwise_tests(ga.cur_dev, ga.base_d, pcfg)
         NW = max(1, (n + 63) // 64)
         single = len(md.subs) == 1
         hpa_algo = zoo.canonical(cfg.hpa_forecast_algorithm) if (p0.hpa and cfg.hpa_forecast_algorithm) else None
@@ -2002,7 +2018,7 @@ class FastPath:
             valid = torch.zeros((R,), dtype=torch.int32, device=dev)
         fc_keep = {}
         for sub in md.subs:
-            cur = ga.cur_d if sub.idx is None else ga.cur_d.index_select(0, sub.idx)
+            cur = ga.cur_dev if sub.idx is None else ga.cur_dev.index_select(0, sub.idx)
             dsub = None if diff is None or sub.idx is None else diff.index_select(0, sub.idx)
             dsub = diff if sub.idx is None else dsub
             lazy = LazyHist(store.buf, sub.rm, *sub.shift_lim(), sub.T)
@@ -2037,17 +2053,17 @@ class FastPath:
         dec = _Flags(flags.contiguous(), count.contiguous())
         if dev.type == "cuda":
             cap = max(1024, min(R * n, 1 << 16))
-            idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, cap)
+            idx_d, val_d, ctr = self._compact(dec, ga.cur_dev, R, n, cap)
             host = [t.to("cpu", non_blocking=True) for t in (packed, stats, dec.count, ctr)]
             torch.cuda.current_stream(dev).synchronize()
             packed_h, stats_h, count_h, total = (t.numpy() for t in host)
             total = int(total[0])
             if total > cap:
-                idx_d, val_d, ctr = self._compact(dec, ga.cur_d, R, n, total)
+                idx_d, val_d, ctr = self._compact(dec, ga.cur_dev, R, n, total)
             idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
         else:
             packed_h, stats_h, count_h = packed.numpy(), stats.numpy(), dec.count.numpy()
-            ix, _ = C.compact_anomalies(dec, ga.cur_d)
+            ix, _ = C.compact_anomalies(dec, ga.cur_dev)
             idx = ix.numpy()
         if len(idx):
             k = idx[:, 0].astype(np.int64) * n + idx[:, 1]
@@ -2082,7 +2098,7 @@ class FastPath:
                if kind is not None and cache.capacity <= 0 else "metric subset" if sub.idx is not None
                else "horizons" if sub.hor is None or sub.hor.shape != (R, n) else "window width"
                if not 1 <= n <= 256 else "metrics" if M > 16 else "keys" if kind is not None and sub.keys is None
-               else "layout" if ga.cur_d.stride(1) != 1 else None)
+               else "layout" if not ga.cur_lazy and ga.cur_devev.stride(1) != 1 else None)
         if why is not None:
             self.fused_declined[why] = self.fused_declined.get(why, 0) + 1
             return None
@@ -2106,7 +2122,7 @@ class FastPath:
             self.fused_declined[why] = self.fused_declined.get(why, 0) + 1
             self._es_plan = (sub.keys, plan, self.cycle)         # es_forecast reuses the lookup
             return None
-        fc = torch.empty((R, H), dtype=torch.float32, device=ga.cur_d.device) if hpa_algo == algo else None
+        fc = torch.empty((R, H), dtype=torch.float32, device=self.b.device) if hpa_algo == algo else None
         out = self._fused_launch(works, ga, md, store, diff, kind, plan, plan.slabs[0], kmax, H=H, fc=fc)
         cache.hits += R
         self.fused_steps += 1
@@ -2121,7 +2137,7 @@ class FastPath:
         M, S = len(p0.aliases), len(works)
         R = S * M
         n = ga.cur.shape[1]
-        dev = ga.cur_d.device
+        dev = self.b.device
         # per-row inputs that only change when the job list or the cache
         # slots do: uploaded once, kept on the arrays
         fz = getattr(ga, "_fused", None)
@@ -2145,7 +2161,7 @@ class FastPath:
         buf = self._fused_cmp.get(dev)
         if buf is None or buf[0].shape[0] < R * n:
             cap = max(R * n, 1024)
-            buf = self._fused_cmp[dev] = (torch.empty((cap, 2), dtype=torch.int32, device=dev),
+            buf = self._fused_cmp[dev] = (torch.empty((cap, 4), dtype=torch.int32, device=dev),
                                           torch.empty((cap,), dtype=torch.float32, device=dev),
                                           torch.zeros((4,), dtype=torch.int32, device=dev))
         idx_d, val_d, ctr = buf
@@ -2153,7 +2169,11 @@ class FastPath:
         self._fused_par ^= 1
         hv = fz["hostv"]
         tb = sub.tables
-        cur = ga.cur_d
+        if ga.cur_lazy:                # the windows in place: grid columns [a, a + n) of the rows sub.rm
+            cur_p, ld_c, cur_rm = store.buf.data_ptr() + ga.cur_cols[0] * store.buf.element_size(), \
+                store.buf.stride(0), ptr(sub.rm)
+        else:
+            cur_p, ld_c, cur_rm = ptr(ga.cur_devev), ga.cur_devev.stride(0), None
         sig_t = sig if kind < 0 else fz["sig"]
         LIB.call("fm_es_band_step", ptr(store.buf), store.buf.stride(0), ptr(sub.rm), ptr(sub.shift), ptr(sub.lim),
                  int(sub.dk), int(sub.T), int(kmax), ptr(fz["t_new"][1]) if st is not None else None,
@@ -2161,13 +2181,11 @@ class FastPath:
                  int(slab.m) if st is not None else 1, int(kind),
                  ptr(st.season) if st is not None and st.season is not None else None,
                  ptr(st.sse) if st is not None else None, ptr(st.state) if st is not None else None,
-                 ptr(st.nobs) if st is not None else None, ptr(cur), cur.stride(0), n, ptr(sub.hor), int(H), S, M,
+                 ptr(st.nobs) if st is not None else None, cur_p, ld_c, n, ptr(sub.hor), int(H), S, M,
                  ptr(tb.thr), ptr(tb.bound), ptr(tb.minlb), ptr(diff), float(tb.pair_factor), ptr(sub.valid),
                  ptr(md.lastk), ptr(fz["up"]), ptr(fz["lo"]), ptr(sig_t), ptr(fc),
                  int(fc.shape[1]) if fc is not None else 0, ptr(hv), int(idx_d.shape[0]), ptr(ctr), par,
-                 ptr(idx_d), ptr(val_d), ptr(fz["last3"]), stream_of(cur))
-        # counter of this launch into the host buffer's tail, then ONE copy
-        hv[S * 4 + R * 6:].view(torch.int32).copy_(ctr[:2], non_blocking=True)
+                 ptr(idx_d), ptr(val_d), ptr(fz["last3"]), cur_rm, stream_of(store.buf))
         host = fz["host"]
         host.copy_(hv, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
@@ -2176,17 +2194,20 @@ class FastPath:
         stats_h = hn[S * 4:S * 4 + R * 4].reshape(R, 4).copy()
         ints = hn[S * 4 + R * 4:].view(np.int32)
         count_h = ints[:R].copy()
-        total = int(ints[2 * R + par])
+        total = int(count_h.sum())                    # = the launch's append counter
         if kind >= 0:
             self.b.model_cache.es_commit(slab, plan.slot, plan.t_last, ints[R:2 * R] != 0)
-        idx = idx_d[:total].cpu().numpy() if total else np.zeros((0, 2), np.int32)
-        if len(idx):
-            kk = idx[:, 0].astype(np.int64) * n + idx[:, 1]
-            kk.sort()
-            idx = np.stack([kk // n, kk % n], 1).astype(np.int32)
+        q = idx_d[:total].cpu().numpy() if total else np.zeros((0, 4), np.int32)
+        band = None
+        if len(q):
+            # (row, point) order; the band at each point rides along
+            o = np.argsort(q[:, 0].astype(np.int64) * n + q[:, 1])
+            q = q[o]
+            band = q[:, 2:].view(np.float32)
+        idx = np.ascontiguousarray(q[:, :2])
         return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
-                "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "hist_rows": ga.rowmap,
-                "store": store, "pts": (fz["up"], fz["lo"]), "last3": fz["last3"]}
+                "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "anom_band": band,
+                "hist_rows": ga.rowmap, "store": store, "pts": (fz["up"], fz["lo"]), "last3": fz["last3"]}
 
     def _forecast(self, algo: str, lazy: "LazyHist", sub: "ModelSub", H: int):
         from ..models import zoo
@@ -2386,7 +2407,9 @@ class FastPath:
             row_start = np.searchsorted(anom[:, 0], np.arange(S) * M) if len(anom) else None
             js = np.flatnonzero(unh)
             pts = None
-            if g.get("pts") is not None:
+            if g.get("anom_band") is not None:
+                pts = g["anom_band"]                 # the band at every anomalous point (fused step)
+            elif g.get("pts") is not None:
                 # per-point bands (forecasting models): one gather + copy for
                 # every unhealthy job's rows
                 rows = (js[:, None] * M + np.arange(M)[None, :]).reshape(-1)
@@ -2416,9 +2439,10 @@ class FastPath:
         ent = anom[a0:a1]
         anomalies, reasons = {}, []
         for m in range(M):
-            e = ent[ent[:, 0] == r0 + m]
-            if not len(e):
+            sel = np.flatnonzero(ent[:, 0] == r0 + m)
+            if not len(sel):
                 continue
+            e = ent[sel]
             r = r0 + m
             ts = cur_t[r, e[:, 1]].tolist()
             vals = cur[r, e[:, 1]].astype(np.float64).tolist()
@@ -2427,6 +2451,8 @@ class FastPath:
             anomalies[alias] = {"tags": "", "values": flat}
             if pts is None:
                 ub, lb = float(stats[r, 2]), float(stats[r, 3])
+            elif isinstance(pts, np.ndarray):       # per-anomaly bands, aligned with anom
+                ub, lb = float(pts[a0 + sel[0], 0]), float(pts[a0 + sel[0], 1])
             else:                                   # the band at the first anomalous point
                 k = pts[0][r]
                 ub, lb = float(pts[1][k, e[0, 1]]), float(pts[2][k, e[0, 1]])
@@ -2629,38 +2655,12 @@ def poll_event(e, sleep: float = 2e-4) -> None:
 OWNER_BLOCKS = 16           # saved rows are grouped by service_owner(.., 16): one block per rank of any world | 16
 
 
-_plan_of = __import__("operator").attrgetter("plan")
-_rows_of = __import__("operator").attrgetter("rows")
-_oblk_of = __import__("operator").attrgetter("_oblk")
-_hfr_of = __import__("operator").attrgetter("_hfr")
-_sliding_of = __import__("operator").attrgetter("sliding")
-
-
-def _owner_block(p: JobPlan) -> int:
-    """service_owner(namespace, app, OWNER_BLOCKS) of a plan, computed once."""
-    b = p.__dict__.get("_oblk")
-    if b is None:
-        from ..parallel.dist import service_owner
-        b = p.__dict__["_oblk"] = service_owner(p.namespace, p.app, OWNER_BLOCKS)
-    return b
-
-
 class _StorePart:
     """One resident store's share of a history checkpoint in flight: the
     host copies of the saved rows' per-row state, their keys / owners as
     ready JSON bytes, and the gathered values (pinned host copy of a device
     gather, or a CPU tensor)."""
     __slots__ = ("name", "last_t", "nlen", "blocks", "t_first", "values", "keys_json", "owners_json")
-
-
-def _plan_frags(p: JobPlan) -> tuple[list, str]:
-    """(JSON text of each row key, JSON text of the owner) of a plan, encoded
-    once per plan for the history checkpoints."""
-    f = p.__dict__.get("_hfr")
-    if f is None:
-        enc = json.JSONEncoder(separators=(",", ":")).encode
-        f = p.__dict__["_hfr"] = ([enc(list(k)) for k in p.keys], enc([p.namespace, p.app]))
-    return f
 
 
 def _json_list(frags: list, idx: np.ndarray) -> torch.Tensor:
@@ -2703,25 +2703,25 @@ class HistorySave:
 
 def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | None = None,
                   stream=None) -> HistorySave:
-    """Issue a history checkpoint of every live job's resident rows (static:
-    the left-aligned samples; sliding: the window's columns), for a warm
-    restart (``Brain.save_history``).
+    """Issue a history checkpoint of the resident rows jobs have claimed
+    (static: the left-aligned samples; sliding: the window's columns), for a
+    warm restart (``Brain.save_history``).  A row stays claimed until it is
+    released or evicted, so a job that left within the last
+    ``max_idle_cycles`` may still be saved (its rows restore and are evicted
+    again unless a job claims them).
 
     Rows are ordered by ``service_owner(namespace, app, 16)`` (``meta
     "{name}.blocks"`` = the row offsets of the 16 owner blocks): after a
     re-shard to a world that divides 16, a rank reads only its blocks.
 
-    On the brain loop's thread this costs a few vectorised host passes (row
-    lists per job, owner blocks cached per plan) and a few launches: with
-    ``dev_bufs`` + ``pinned`` + ``stream`` the rows are gathered on ``stream``
-    into a reusable device block straight from the live grid (the current
-    stream waits for that gather only, ~1 ms per GB) and copied into reusable
-    pinned host memory behind it, asynchronously; the loop's next cycles run
-    while the copy drains.  The per-row lists and the file are built off the
-    loop (:meth:`HistorySave.state`), with no device calls there -- a writer
-    thread that gathered, copied or waited on the device itself measured
-    5-25x slower brain cycles meanwhile."""
-    works = list(fp.works.values())
+    On the brain loop's thread this costs array passes over the stores' per-row
+    owner records (ResidentHistory.rows_for) and C-level joins of their ready
+    JSON, plus a few launches: with ``dev_bufs`` + ``pinned`` + ``stream`` the
+    rows are gathered on ``stream`` into a reusable device block straight from
+    the live grid (the current stream waits for that gather only, ~1 ms per
+    GB) and copied into reusable pinned host memory behind it, asynchronously;
+    the loop's next cycles run while the copy drains.  The file is written off
+    the loop, with no device calls there (:meth:`HistorySave.state`)."""
     dev = fp.b.device
     asyn = dev.type == "cuda" and stream is not None and pinned is not None and dev_bufs is not None
     cur = torch.cuda.current_stream(dev) if asyn else None
@@ -2729,40 +2729,13 @@ def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | N
         stream.wait_stream(cur)
     parts = []
     gathered = []
-    # per-job lists through C-level maps (attrgetter), the per-plan owner
-    # block and JSON fragments cached on the plan at its first save
-    plans = list(map(_plan_of, works))
-    try:
-        ob_all = np.fromiter(map(_oblk_of, plans), np.int64, len(plans))
-        fr_all = list(map(_hfr_of, plans))
-    except AttributeError:
-        for p in plans:
-            _owner_block(p)
-            _plan_frags(p)
-        ob_all = np.fromiter(map(_oblk_of, plans), np.int64, len(plans))
-        fr_all = list(map(_hfr_of, plans))
-    sl_all = np.fromiter(map(_sliding_of, plans), bool, len(plans))
-    w_obj = np.empty(len(works), object)
-    w_obj[:] = works
     for name, st in (("static", fp.static), ("sliding", fp.sliding)):
-        pick = np.flatnonzero(sl_all == st.sliding)
-        if not len(pick):
+        own = np.flatnonzero(st.owned & st.occ)
+        if not len(own):
             continue
-        ws = w_obj[pick].tolist()
-        rows_l = list(map(_rows_of, ws))
-        lens = np.fromiter(map(len, rows_l), np.int64, len(ws))
-        rows_all = np.concatenate(rows_l).astype(np.int64)
-        ob_job = ob_all[pick]
-        jix_all = np.repeat(np.arange(len(ws)), lens)
-        u, first = np.unique(rows_all, return_index=True)      # each row once, ascending
-        keep = u < len(st.keys)
-        first = first[keep]
-        ob = ob_job[jix_all[first]]
+        ob = st.oblk[own]
         order = np.argsort(ob, kind="stable")                  # owner blocks, rows ascending within
-        flat = first[order]
-        rows = rows_all[flat]
-        if not len(rows):
-            continue
+        rows = own[order]
         if st.sliding:
             if st.t0 is None or st.e <= st.ws:
                 continue
@@ -2771,9 +2744,8 @@ def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | N
             c0, c1 = 0, max(1, int(st.nlen[rows].max()))
         sp = _StorePart()
         sp.name = name
-        fr = [fr_all[i] for i in pick.tolist()]
-        sp.keys_json = _json_list(list(chain.from_iterable(f[0] for f in fr)), flat)
-        sp.owners_json = _json_list([f[1] for f in fr], jix_all[flat])
+        sp.keys_json = _json_list(st.kjson, rows)
+        sp.owners_json = _json_list(st.ojson, rows)
         sp.last_t = st.last_t[rows].copy()
         sp.nlen = None if st.sliding else st.nlen[rows].copy()
         sp.blocks = np.searchsorted(ob[order], np.arange(OWNER_BLOCKS + 1)).tolist()
@@ -2835,7 +2807,7 @@ def load_history(fp: "FastPath", t: dict, meta: dict, now: float, owns=None) -> 
         # every saved row is this rank's (no re-shard): no host copy of the block
         v = vals if len(sel) == vals.shape[0] else vals.index_select(0, torch.as_tensor(sel, dtype=torch.int64))
         last_t = t[f"{name}.last_t"].numpy()[sel]
-        rows, _ = st.rows_for(keys, fp.cycle)
+        rows, _ = st.rows_for(keys, fp.cycle, owner=[tuple(owners[i]) for i in sel])
         rows = rows.astype(np.int64)
         if st.sliding:
             st.advance(now, now - fp.history_s)

@@ -84,6 +84,14 @@ class ResidentHistory:
         self.used = np.zeros(0, np.int64)           # cycle of last use (eviction)
         self.occ = np.zeros(0, bool)                # row holds a key
         self.keys: list = []
+        # per row, for history checkpoints (set when a job's plan claims the
+        # row): the key and the owner (namespace, app) as ready JSON text and
+        # the owner's service_owner(.., 16) block -- a save lists its rows
+        # with array passes and C-level joins, no per-job Python
+        self.kjson: list = []
+        self.ojson: list = []
+        self.oblk = np.zeros(0, np.int16)
+        self.owned = np.zeros(0, bool)
         self.t0: float | None = None                # sliding: time of column 0
         self.e = 0                                  # sliding: exclusive end column of the window
         self.ws = 0                                 # sliding: first column inside the window
@@ -114,10 +122,18 @@ class ResidentHistory:
         self.used = np.concatenate([self.used, np.zeros(new_cap - cap, np.int64)])
         self.occ = np.concatenate([self.occ, np.zeros(new_cap - cap, bool)])
         self.keys.extend([None] * (new_cap - cap))
+        self.kjson.extend([None] * (new_cap - cap))
+        self.ojson.extend([None] * (new_cap - cap))
+        self.oblk = np.concatenate([self.oblk, np.zeros(new_cap - cap, np.int16)])
+        self.owned = np.concatenate([self.owned, np.zeros(new_cap - cap, bool)])
 
-    def rows_for(self, keys: list, cycle: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    OWNER_BLOCKS = 16
+
+    def rows_for(self, keys: list, cycle: int = 0, owner=None) -> tuple[np.ndarray, np.ndarray]:
         """Row index of every key (allocating missing ones) and a mask of the
-        rows that were just allocated (need a full history fetch)."""
+        rows that were just allocated (need a full history fetch).  ``owner``
+        ((namespace, app), or one per key) is recorded on rows that have none
+        yet (history checkpoints order and re-shard rows by it)."""
         out = np.empty(len(keys), np.int32)
         new = np.zeros(len(keys), bool)
         missing = [i for i, k in enumerate(keys) if k not in self.slot]
@@ -136,7 +152,23 @@ class ResidentHistory:
         for i, k in enumerate(keys):
             out[i] = self.slot[k]
         self.used[out] = cycle
+        if owner is not None and not self.owned[out].all():
+            self._own(out, keys, owner)
         return out, new
+
+    def _own(self, rows, keys, owner) -> None:
+        import json
+        from ..parallel.dist import service_owner
+        enc = json.JSONEncoder(separators=(",", ":")).encode
+        one = isinstance(owner, tuple)
+        for i, r in enumerate(rows.tolist()):
+            if self.owned[r]:
+                continue
+            o = owner if one else owner[i]
+            self.kjson[r] = enc(list(keys[i]))
+            self.ojson[r] = enc([o[0], o[1]])
+            self.oblk[r] = service_owner(o[0], o[1], self.OWNER_BLOCKS)
+            self.owned[r] = True
 
     def get(self, key):
         return self.slot.get(key)
@@ -148,7 +180,9 @@ class ResidentHistory:
             self.buf.index_fill_(0, idx, float("nan"))
             for r in rows:
                 self.keys[r] = None
+                self.kjson[r] = self.ojson[r] = None
                 self.last_t[r] = -np.inf
+            self.owned[rows] = False
             self.nlen[rows] = 0
             self.nfin[rows] = 0
             self.occ[rows] = False

@@ -63,7 +63,7 @@ _SIGS: dict[str, list] = {
                         c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int,
                         c_void_p, c_int, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p,
                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
-                        c_void_p, c_void_p, c_void_p, c_void_p],
+                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_lstm_forward_hist": [c_void_p, c_i64, c_int, c_void_p, c_void_p, c_void_p, c_int, c_i64, c_int, c_int,
                              c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "fm_grid_retire": [c_void_p, c_i64, c_i64, c_int, c_int, c_void_p, c_void_p],

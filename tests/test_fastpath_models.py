@@ -154,7 +154,7 @@ def test_models_fast_path_equals_general_path(algo, kind, device="cpu"):
     for ga in a[3].fast._garr.values():
         # merged sliding windows are gathered from the device grid: the same
         # values as the host ring's copy
-        np.testing.assert_array_equal(ga.cur_d.cpu().numpy(), ga.cur)
+        np.testing.assert_array_equal(ga.cur_dev.cpu().numpy(), ga.cur)
         if ga.base_d is not None and getattr(ga, "base", None) is not None:
             np.testing.assert_array_equal(ga.base_d.cpu().numpy(), ga.base)
 
