@@ -2098,7 +2098,7 @@ class FastPath:
                if kind is not None and cache.capacity <= 0 else "metric subset" if sub.idx is not None
                else "horizons" if sub.hor is None or sub.hor.shape != (R, n) else "window width"
                if not 1 <= n <= 256 else "metrics" if M > 16 else "keys" if kind is not None and sub.keys is None
-               else "layout" if not ga.cur_lazy and ga.cur_devev.stride(1) != 1 else None)
+               else "layout" if not ga.cur_lazy and ga.cur_dev.stride(1) != 1 else None)
         if why is not None:
             self.fused_declined[why] = self.fused_declined.get(why, 0) + 1
             return None
@@ -2173,7 +2173,7 @@ class FastPath:
             cur_p, ld_c, cur_rm = store.buf.data_ptr() + ga.cur_cols[0] * store.buf.element_size(), \
                 store.buf.stride(0), ptr(sub.rm)
         else:
-            cur_p, ld_c, cur_rm = ptr(ga.cur_devev), ga.cur_devev.stride(0), None
+            cur_p, ld_c, cur_rm = ptr(ga.cur_dev), ga.cur_dev.stride(0), None
         sig_t = sig if kind < 0 else fz["sig"]
         LIB.call("fm_es_band_step", ptr(store.buf), store.buf.stride(0), ptr(sub.rm), ptr(sub.shift), ptr(sub.lim),
                  int(sub.dk), int(sub.T), int(kmax), ptr(fz["t_new"][1]) if st is not None else None,
