@@ -113,11 +113,11 @@ def save(dirpath: str, tensors: dict[str, torch.Tensor], meta: dict, step: int |
 
 
 def _json_fields(tensors: dict, meta: dict) -> dict:
-    """Move ``<name>_json`` uint8 tensors (UTF-8 JSON a writer stored as bytes
-    instead of header metadata, e.g. a history checkpoint's row keys) into
-    ``meta[<name>]``."""
+    """Move ``<name>_json`` uint8 tensors (the comma-joined UTF-8 JSON
+    elements of a list a writer stored as bytes instead of header metadata,
+    e.g. a history checkpoint's row keys) into ``meta[<name>]``."""
     for n in [n for n in tensors if n.endswith("_json")]:
-        meta[n[:-len("_json")]] = json.loads(bytes(tensors.pop(n).numpy()).decode())
+        meta[n[:-len("_json")]] = json.loads(b"[" + tensors.pop(n).numpy().tobytes() + b"]")
     return meta
 
 

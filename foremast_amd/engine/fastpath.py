@@ -2664,11 +2664,16 @@ class _StorePart:
 
 
 def _json_list(frags: list, idx: np.ndarray) -> torch.Tensor:
-    """UTF-8 bytes of the JSON list of ``frags[idx]`` (C-level picks and joins)."""
+    """The elements of a JSON list, ``frags[idx]`` (UTF-8 JSON values)
+    comma-joined, as a uint8 tensor -- one C-level pick and one join (the
+    loader adds the brackets: ``checkpoint._json_fields``)."""
     from operator import itemgetter
     ix = idx.tolist()
     got = (frags[ix[0]],) if len(ix) == 1 else (itemgetter(*ix)(frags) if ix else ())
-    return torch.frombuffer(bytearray(("[" + ",".join(got) + "]").encode()), dtype=torch.uint8)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")           # read-only: the writer only reads it
+        return torch.frombuffer(b",".join(got), dtype=torch.uint8) if got else torch.zeros(0, dtype=torch.uint8)
 
 
 class HistorySave:

@@ -85,7 +85,7 @@ class ResidentHistory:
         self.occ = np.zeros(0, bool)                # row holds a key
         self.keys: list = []
         # per row, for history checkpoints (set when a job's plan claims the
-        # row): the key and the owner (namespace, app) as ready JSON text and
+        # row): the key and the owner (namespace, app) as ready UTF-8 JSON and
         # the owner's service_owner(.., 16) block -- a save lists its rows
         # with array passes and C-level joins, no per-job Python
         self.kjson: list = []
@@ -165,8 +165,8 @@ class ResidentHistory:
             if self.owned[r]:
                 continue
             o = owner if one else owner[i]
-            self.kjson[r] = enc(list(keys[i]))
-            self.ojson[r] = enc([o[0], o[1]])
+            self.kjson[r] = enc(list(keys[i])).encode()
+            self.ojson[r] = enc([o[0], o[1]]).encode()
             self.oblk[r] = service_owner(o[0], o[1], self.OWNER_BLOCKS)
             self.owned[r] = True
 
