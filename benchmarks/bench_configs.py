@@ -400,6 +400,7 @@ def config3e2e(args):
     cfg = BrainConfig()
     cfg.ml_algorithm = algo or "moving_average_all"
     cfg.hpa_log_interval_s = args.hpa_log_interval
+    cfg.hpalog_async = 1                   # the service's default (HPALOG_ASYNC, BrainConfig.from_env)
     if kind == "mixed":
         # per metric type: its model (and, for the monitored classes, the band
         # threshold below) -- the ml_algorithmN overrides of foremast-brain.yaml
@@ -514,6 +515,8 @@ def config3e2e(args):
             r = _prof.runcall(brain.run_once)
         else:
             r = brain.run_once()
+        if len(cyc_ms) + 1 == args.warmup + args.steps:
+            brain.flush_logs()             # the last timed cycle waits for the queued HPA log writes
         cyc_ms.append(1e3 * (time.perf_counter() - tc))
         rows.append(r.get("rows", 0))
         if live is not None:

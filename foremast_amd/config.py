@@ -82,6 +82,11 @@ class BrainConfig:
     # per interval (the alert letter reads the last 4-6 entries around a
     # replica change, HpaController.go:94-138: changes are what it needs)
     hpa_log_interval_s: float = 0.0
+    # HPALOG_ASYNC: 1 = a cycle's HPA logs are written by one background
+    # thread (FIFO, its own store connection) while the next cycle runs; a
+    # reader sees them a few ms later.  Flushed at shutdown.  The service
+    # (``BrainConfig.from_env``) defaults to 1, the library to 0.
+    hpalog_async: int = 0
     # LSTM model (ML_ALGORITHM=lstm, docs/guides/design.md:81-85)
     lstm_hidden: int = 128                 # LSTM_HIDDEN: 32 | 64 | 128 | 256
     lstm_layers: int = 1                   # LSTM_LAYERS: 1 | 2
@@ -168,6 +173,7 @@ class BrainConfig:
         c.hpa_forecast_algorithm = env.get("HPA_FORECAST_ALGORITHM", c.hpa_forecast_algorithm)
         c.hpa_forecast_steps = _i(env, "HPA_FORECAST_STEPS", c.hpa_forecast_steps)
         c.hpa_log_interval_s = _f(env, "HPA_LOG_INTERVAL_SECONDS", c.hpa_log_interval_s)
+        c.hpalog_async = _i(env, "HPALOG_ASYNC", 1)       # the service writes them off the loop
         c.lstm_hidden = _i(env, "LSTM_HIDDEN", c.lstm_hidden)
         c.lstm_layers = _i(env, "LSTM_LAYERS", c.lstm_layers)
         c.lstm_multivariate = _i(env, "LSTM_MULTIVARIATE", c.lstm_multivariate)

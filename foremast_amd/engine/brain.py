@@ -434,7 +434,7 @@ class Brain:
             n_rows += self._finish_general(batches, now, updates, hpalogs, outcome)
         with self.spans.span("persist"):
             if hpalogs:
-                self.store.add_hpalogs(hpalogs)
+                self._write_hpalogs(hpalogs)
             for ids, fields, handles in bulk:
                 if fields == KEEP:
                     self.store.keep(self.worker, ids, now=now, handles=handles)
@@ -457,6 +457,35 @@ class Brain:
             self.exporter.sweep(now)
         return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast) - (len(self.fast.ghost_ids) if fast and self.fast.ghost_mask(fast) is not None else 0),
                 "seconds": time.perf_counter() - t0}
+
+    def _write_hpalogs(self, hpalogs: list) -> None:
+        """HPA logs into the store: inline, or (``hpalog_async``) queued to one
+        background writer thread -- FIFO, so the entries of a job stay in
+        cycle order; the store's connection is per thread (SQLite WAL: the
+        writer's transaction overlaps the loop's reads)."""
+        if not self.cfg.hpalog_async:
+            self.store.add_hpalogs(hpalogs)
+            return
+        ex = getattr(self, "_log_writer", None)
+        if ex is None:
+            from concurrent.futures import ThreadPoolExecutor
+            ex = self._log_writer = ThreadPoolExecutor(1, thread_name_prefix="hpalog-writer")
+            self._log_pending: list = []
+
+        def write(batch=hpalogs):
+            try:
+                self.store.add_hpalogs(batch)
+            except Exception:                 # noqa: BLE001 - a lost log batch must not stop the loop
+                log.exception("background HPA log write failed (%d batches)", len(batch))
+        self._log_pending = [f for f in self._log_pending if not f.done()]
+        self._log_pending.append(ex.submit(write))
+
+    def flush_logs(self) -> None:
+        """Wait for the background HPA log writes queued so far."""
+        for f in getattr(self, "_log_pending", []):
+            f.result()
+        if getattr(self, "_log_pending", None):
+            self._log_pending = []
 
     def _score_fast(self, fast, now: float, updates: list, hpalogs: list, outcome: dict) -> list:
         """Stage, group and score the fast-path jobs; their verdicts are
@@ -635,6 +664,7 @@ class Brain:
                     log.exception("brain cycle failed")
                     (stop.wait(poll) if stop is not None else time.sleep(poll))
         finally:
+            self.flush_logs()
             if checkpoint_dir:
                 try:
                     self.save_checkpoint(checkpoint_dir)

@@ -493,6 +493,7 @@ class FastPath:
         self._ring = None         # merged sliding mode: host ring of the newest grid columns
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
         self._slide_state: dict = {}
+        self._flat_rows = None     # (row map [S, M] object, flat int64 rows, slice when they are one run)
         self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
         self.model_churns = 0      # ModelArrays restricted to a churned job list instead of rebuilt
         self._hist_pending = False  # a per-job fetch left history in some FastWork.hist this cycle
@@ -1150,7 +1151,15 @@ class FastPath:
             r, t, v = np.concatenate(wr), np.concatenate(wt), np.concatenate(wv)
             st.write_sliding_flat(r, t, v)
             self._ring_write(r, t, v, fresh_rows)
-        flat = rows.reshape(-1).astype(np.int64)
+        fc = self._flat_rows
+        if fc is None or fc[0] is not rows:
+            flat = rows.reshape(-1).astype(np.int64)
+            # grid rows allocated in job order (the usual fleet): the ring
+            # rows are one slice, read without a row gather
+            k0 = int(flat[0]) if len(flat) else 0
+            run = len(flat) > 0 and int(flat[-1]) - k0 == len(flat) - 1 and bool((np.diff(flat) == 1).all())
+            fc = self._flat_rows = (rows, flat, slice(k0, k0 + len(flat)) if run else None)
+        flat = fc[1] if fc[2] is None else fc[2]
         (clo, chi), (blo, bhi) = wins["current"], wins["baseline"]
         cur, cur_t = self._ring_read(flat, clo, chi)
         base = self._ring_read(flat, blo, bhi)[0] if memo[3][1] else None
@@ -1225,20 +1234,24 @@ class FastPath:
     def _ring_read(self, rows: np.ndarray, lo: float, hi: float) -> tuple[np.ndarray, np.ndarray]:
         """Values [R, n] / times [R, n] of the grid points in [lo, hi] (NaN:
         no sample) from the host ring: row gathers of at most two contiguous
-        slot ranges; the times are one broadcast row (read-only)."""
+        slot ranges (``rows`` a slice: contiguous copies); the times are one
+        broadcast row (read-only)."""
         step = self.b.step
         c0, c1 = math.ceil(lo / step - 1e-9), math.floor(hi / step + 1e-9)
         n = max(0, c1 - c0 + 1)
+        nrows = (rows.stop - rows.start) if isinstance(rows, slice) else len(rows)
         if n > self.RING:
             raise ValueError(f"window of {n} steps exceeds the sliding ring ({self.RING})")
-        if self._ring is None or n == 0 or not len(rows) or self._ring_top is None:
-            return np.full((len(rows), max(1, n)), np.nan, np.float32), np.full((len(rows), max(1, n)), np.nan)
-        t = np.broadcast_to(np.arange(c0, c0 + n, dtype=np.float64) * step, (len(rows), n))
+        if self._ring is None or n == 0 or not nrows or self._ring_top is None:
+            return np.full((nrows, max(1, n)), np.nan, np.float32), np.full((nrows, max(1, n)), np.nan)
+        t = np.broadcast_to(np.arange(c0, c0 + n, dtype=np.float64) * step, (nrows, n))
         if c1 <= self._ring_top - self.RING or c0 > self._ring_top:
-            return np.full((len(rows), n), np.nan, np.float32), t
+            return np.full((nrows, n), np.nan, np.float32), t
         j0 = c0 % self.RING
         if j0 + n <= self.RING:
             v = self._ring[rows, j0:j0 + n]                # gathers only the window's slots
+            if isinstance(rows, slice):
+                v = v.copy()                               # (the ring moves on next cycle)
         else:
             v = np.concatenate([self._ring[rows, j0:], self._ring[rows, :j0 + n - self.RING]], axis=1)
         lo_ok, hi_ok = max(c0, self._ring_top - self.RING + 1), min(c1, self._ring_top)

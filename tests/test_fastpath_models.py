@@ -379,3 +379,22 @@ def test_ghost_layout_under_churn_equals_general_path(compact_every):
         b[0].t += 60
     assert len(closed_at) >= 2                              # the faults (+ noise closes at 2 sigma)
     assert a[3].fast.ghost_cycles > 0
+
+
+def test_async_hpalog_writer_matches_inline_writes():
+    """HPALOG_ASYNC: a cycle's HPA logs are queued to one background writer
+    (FIFO); after ``flush_logs`` the store holds exactly what inline writes
+    give, in the same order."""
+    a = _brain(True, "double_exponential_smoothing", FAULTS)
+    b = _brain(True, "double_exponential_smoothing", FAULTS)
+    a[3].cfg.hpalog_async = 1
+    ids = _submit(a[2], "hpa")
+    assert ids == _submit(b[2], "hpa")
+    for cyc in range(4):
+        a[3].run_once()
+        b[3].run_once()
+        a[3].flush_logs()
+        _compare(a, b, ids, cyc)
+        a[0].t += 60
+        b[0].t += 60
+    assert getattr(a[3], "_log_writer", None) is not None and getattr(b[3], "_log_writer", None) is None
