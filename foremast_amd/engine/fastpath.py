@@ -2417,7 +2417,7 @@ class FastPath:
         if unknown.any():
             outcome[ST.COMPLETED_UNKNOWN] = outcome.get(ST.COMPLETED_UNKNOWN, 0) + int(unknown.sum())
         if unh.any():
-            row_start = np.searchsorted(anom[:, 0], np.arange(S) * M) if len(anom) else None
+            row_start = None                         # (the per-job path below slices ``pre``)
             js = np.flatnonzero(unh)
             pts = None
             if g.get("anom_band") is not None:
@@ -2430,13 +2430,23 @@ class FastPath:
                 up_h = g["pts"][0].index_select(0, ri).cpu().numpy()
                 lo_h = g["pts"][1].index_select(0, ri).cpu().numpy()
                 pts = {int(r): k for k, r in enumerate(rows)}, up_h, lo_h
-            for j in js:
+            # every unhealthy job's anomalies at once: per-row [start, end) into
+            # anom, the points' times / values (and bands) as Python floats
+            ur = (js[:, None] * M + np.arange(M)[None, :]).reshape(-1)
+            a_lo = np.searchsorted(anom[:, 0], ur, "left").tolist() if len(anom) else [0] * len(ur)
+            a_hi = np.searchsorted(anom[:, 0], ur, "right").tolist() if len(anom) else [0] * len(ur)
+            pre = (a_lo, a_hi, cur_t[anom[:, 0], anom[:, 1]].tolist(),
+                   cur[anom[:, 0], anom[:, 1]].astype(np.float64).tolist(),
+                   pts[:, 0].tolist() if isinstance(pts, np.ndarray) else None,
+                   pts[:, 1].tolist() if isinstance(pts, np.ndarray) else None)
+            for q, j in enumerate(js.tolist()):
                 extra = None
                 if down is not None and down[j]:
                     u = int(ga.impact_ids[j])
                     extra = {"name": "downstream", "impact": round(float(impact.impact[u]), 4),
                              "callees": impact.explain(u)}
-                st, fields = self._unhealthy(works[j], j, M, anom, row_start, cur, cur_t, stats, extra, pts)
+                st, fields = self._unhealthy(works[j], j, M, anom, row_start, cur, cur_t, stats, extra, pts,
+                                             pre=(q, pre))
                 updates.append((works[j].doc.id, fields))
             outcome[ST.COMPLETED_UNHEALTH] = outcome.get(ST.COMPLETED_UNHEALTH, 0) + int(unh.sum())
         if flush:
@@ -2445,8 +2455,35 @@ class FastPath:
         if closed.any():
             self._release([works[j] for j in np.flatnonzero(closed)])
 
-    def _unhealthy(self, w: FastWork, j: int, M: int, anom, row_start, cur, cur_t, stats, extra=None, pts=None):
+    def _unhealthy(self, w: FastWork, j: int, M: int, anom, row_start, cur, cur_t, stats, extra=None, pts=None,
+                   pre=None):
         r0 = j * M
+        if pre is not None:
+            # the group's precomputed anomaly lists (finish_group): slices only
+            q, (a_lo, a_hi, TS, V, UB, LB) = pre
+            anomalies, reasons = {}, []
+            al = w.plan.aliases
+            for m in range(M):
+                a, b = a_lo[q * M + m], a_hi[q * M + m]
+                if a == b:
+                    continue
+                ts, vals = TS[a:b], V[a:b]
+                r = r0 + m
+                if UB is not None:
+                    ub, lb = UB[a], LB[a]
+                elif pts is None:
+                    ub, lb = float(stats[r, 2]), float(stats[r, 3])
+                else:                               # the band at the first anomalous point
+                    k = pts[0][r]
+                    ub, lb = float(pts[1][k, anom[a, 1]]), float(pts[2][k, anom[a, 1]])
+                anomalies[al[m]] = {"tags": "", "values": [x for pair in zip(ts, vals) for x in pair]}
+                reasons.append({"name": al[m], "ts": ts, "values": vals, "upper": ub, "lower": lb})
+            if extra is not None:
+                reasons.append(extra)
+                anomalies["downstream"] = {"tags": "", "values": []}
+            return ST.COMPLETED_UNHEALTH, {"status": ST.COMPLETED_UNHEALTH,
+                                           "reason": html.escape(json.dumps(reasons)),
+                                           "anomaly_info": json.dumps(anomalies)}
         a0 = row_start[j] if row_start is not None else 0
         a1 = np.searchsorted(anom[:, 0], r0 + M) if len(anom) else 0
         ent = anom[a0:a1]

@@ -599,29 +599,6 @@ class SQLiteStore(JobStore):
             c.execute("create table if not exists leases (worker text primary key, beat real not null)")
             c.execute("create table if not exists meta (k text primary key, v integer not null)")
             c.execute("insert or ignore into meta values ('seq', 0)")
-            c.execute("create table if not exists hpalogs (job_id text, ts real, body text)")
-            # the brain's per-cycle HPA logs, columnar: one row per batch (the
-            # entries of one cycle of one rank), rows sorted by job rid
-            c.execute("create table if not exists hpalog_batches (bid integer primary key, ts real not null, "
-                      "created text not null, aliases text not null, reasons text not null, n integer not null, "
-                      "rids blob not null, score blob not null, reason blob not null, vals blob not null)")
-            # per job the batches that may hold its entries: a read scans only
-            # [first_bid, last_bid], a job without HPA entries none.  Entries are
-            # keyed by documents.rid: job documents are never deleted from this
-            # store (only hpalog batches age out), so a rid is never reused
-            c.execute("create table if not exists hpalog_jobs (rid integer primary key, first_bid integer not null, "
-                      "last_bid integer not null)")
-            if (c.execute("select 1 from hpalog_batches limit 1").fetchone() is not None
-                    and c.execute("select 1 from hpalog_jobs limit 1").fetchone() is None):
-                rng: dict = {}                    # a store written before the index: built once
-                for bid, rids in c.execute("select bid, rids from hpalog_batches order by bid"):
-                    for r_ in np.frombuffer(rids, np.int64).tolist():
-                        rng[r_] = (rng.get(r_, (bid,))[0], bid)
-                c.executemany("insert into hpalog_jobs values (?,?,?)", [(r_, a, b) for r_, (a, b) in rng.items()])
-            c.execute("create index if not exists hpalogs_job on hpalogs(job_id, ts)")
-            # no ts index: rows arrive in time order, so retention deletes a
-            # rowid prefix (one B-tree less to update per log: 10k logs per cycle)
-            c.execute("drop index if exists hpalogs_ts")
             if legacy:                          # round-2 layout: one JSON body per row
                 seq = self._next_seq(c)
                 rows = [self._row(Document.from_dict(json.loads(b)), seq)
@@ -636,20 +613,83 @@ class SQLiteStore(JobStore):
         except Exception:
             c.execute("rollback")
             raise
+        self._init_logs(c)
+
+    _LOG_TABLES = ("hpalogs", "hpalog_batches", "hpalog_jobs")
+
+    def _init_logs(self, main) -> None:
+        """The HPA-log tables live in their own database file (``<path>-hpalogs``):
+        a log write (a 10k-job cycle's batch, queued to a background writer by
+        the service) takes that file's write lock only, so it never holds up a
+        claim or a verdict write on the jobs file (SQLite has one writer per
+        file).  Tables a store of an earlier layout kept in the jobs file are
+        moved over once."""
+        c = self._lconn()
+        c.execute("begin immediate")
+        try:
+            c.execute("create table if not exists hpalogs (job_id text, ts real, body text)")
+            # the brain's per-cycle HPA logs, columnar: one row per batch (the
+            # entries of one cycle of one rank), rows sorted by job rid
+            c.execute("create table if not exists hpalog_batches (bid integer primary key, ts real not null, "
+                      "created text not null, aliases text not null, reasons text not null, n integer not null, "
+                      "rids blob not null, score blob not null, reason blob not null, vals blob not null)")
+            # per job the batches that may hold its entries: a read scans only
+            # [first_bid, last_bid], a job without HPA entries none.  Entries are
+            # keyed by documents.rid: job documents are never deleted from this
+            # store (only hpalog batches age out), so a rid is never reused
+            c.execute("create table if not exists hpalog_jobs (rid integer primary key, first_bid integer not null, "
+                      "last_bid integer not null)")
+            old = {r[0] for r in main.execute("select name from sqlite_master where type='table'")} & \
+                set(self._LOG_TABLES)
+            for t in self._LOG_TABLES:          # an earlier layout's tables: moved once
+                if t in old:
+                    rows = main.execute(f"select * from {t}").fetchall()
+                    if rows:
+                        c.executemany(f"insert into {t} values ({','.join('?' * len(rows[0]))})", rows)
+            if (c.execute("select 1 from hpalog_batches limit 1").fetchone() is not None
+                    and c.execute("select 1 from hpalog_jobs limit 1").fetchone() is None):
+                rng: dict = {}                    # a store written before the index: built once
+                for bid, rids in c.execute("select bid, rids from hpalog_batches order by bid"):
+                    for r_ in np.frombuffer(rids, np.int64).tolist():
+                        rng[r_] = (rng.get(r_, (bid,))[0], bid)
+                c.executemany("insert into hpalog_jobs values (?,?,?)", [(r_, a, b) for r_, (a, b) in rng.items()])
+            c.execute("create index if not exists hpalogs_job on hpalogs(job_id, ts)")
+            # no ts index: rows arrive in time order, so retention deletes a
+            # rowid prefix (one B-tree less to update per log: 10k logs per cycle)
+            c.execute("drop index if exists hpalogs_ts")
+            c.execute("commit")
+        except Exception:
+            c.execute("rollback")
+            raise
+        if old:
+            for t in self._LOG_TABLES:
+                if t in old:
+                    main.execute(f"drop table {t}")
 
     # ------------------------------------------------------------------ plumbing
+    @staticmethod
+    def _open(path: str) -> sqlite3.Connection:
+        c = sqlite3.connect(path, timeout=30, isolation_level=None)
+        c.execute("pragma journal_mode=wal")
+        # WAL + NORMAL: no fsync per commit; the database stays consistent
+        # on a crash (a power loss may drop the last commits, which the
+        # brain re-derives: job ids are deterministic and claims lease out)
+        c.execute("pragma synchronous=normal")
+        c.execute("pragma cache_size=-65536")
+        c.execute("pragma temp_store=memory")
+        return c
+
+    def _lconn(self) -> sqlite3.Connection:
+        """This thread's connection to the HPA-log file."""
+        c = getattr(self._local, "lc", None)
+        if c is None:
+            c = self._local.lc = self._open(self.path + "-hpalogs")
+        return c
+
     def _conn(self) -> sqlite3.Connection:
         c = getattr(self._local, "c", None)
         if c is None:
-            c = sqlite3.connect(self.path, timeout=30, isolation_level=None)
-            c.execute("pragma journal_mode=wal")
-            # WAL + NORMAL: no fsync per commit; the database stays consistent
-            # on a crash (a power loss may drop the last commits, which the
-            # brain re-derives: job ids are deterministic and claims lease out)
-            c.execute("pragma synchronous=normal")
-            c.execute("pragma cache_size=-65536")
-            c.execute("pragma temp_store=memory")
-            self._local.c = c
+            c = self._local.c = self._open(self.path)
         return c
 
     class _Txn:
@@ -961,10 +1001,10 @@ class SQLiteStore(JobStore):
         rows = _log_rows([lg for lg in logs if not isinstance(lg, HPALogBatch)])
         if not rows and not batches:
             return
-        with self._txn() as c:
+        rids = [self._rids_of(self._conn(), b) for b in batches]     # a read of the jobs file, no lock held
+        with self._Txn(self._lconn()) as c:
             newest = -math.inf
-            for b in batches:
-                rid = self._rids_of(c, b)
+            for b, rid in zip(batches, rids):
                 ok = rid >= 0
                 if not ok.all():                  # entries of unknown jobs: one row each
                     rows.extend(_log_rows([b.log(i) for i in np.flatnonzero(~ok)]))
@@ -1034,12 +1074,13 @@ class SQLiteStore(JobStore):
         return got
 
     def hpalogs(self, job_id: str, size: int = 10) -> list[HPALog]:
-        c = self._conn()
+        c = self._lconn()
         rows = c.execute("select ts, body from hpalogs where job_id=? order by ts desc limit ?",
                          (job_id, size)).fetchall()
         out = [(ts, HPALog.from_dict(json.loads(b))) for ts, b in rows]
-        r = c.execute("select d.rid, j.first_bid, j.last_bid from documents d join hpalog_jobs j on j.rid = d.rid "
-                      "where d.id=?", (job_id,)).fetchone()
+        d = self._conn().execute("select rid from documents where id=?", (job_id,)).fetchone()
+        r = None if d is None else c.execute("select rid, first_bid, last_bid from hpalog_jobs where rid=?",
+                                             (d[0],)).fetchone()
         if r is not None and size > 0:
             rid, b0, b1 = r
             found = 0

@@ -107,7 +107,7 @@ def test_hpalog_retention_and_order(tmp_path):
                         for j in range(3)])
     assert [l.timestamp for l in st.hpalogs("a:ns:hpa1", 3)] == [T0 + 2400, T0 + 1800, T0 + 1200]
     st.add_hpalogs([HPALog(job_id="a:ns:hpa0", timestamp=T0 + 9000, log=HPALogBody(60, "x", []))])
-    left = st._conn().execute("select min(ts) from hpalogs").fetchone()[0]
+    left = st._lconn().execute("select min(ts) from hpalogs").fetchone()[0]
     assert left >= T0 + 9000 - 3600
 
 
@@ -194,8 +194,8 @@ def test_hpalog_batches_are_columnar_and_read_back_per_job(tmp_path):
                         cur[::-1], cur[::-1] + 0.5, cur[::-1] - 0.5,
                         handles=np.array([rid[j] for j in sel[::-1]]) if k % 2 else None)
         st.add_hpalogs([b])
-    n_rows = st._conn().execute("select count(*) from hpalog_batches").fetchone()[0]
-    assert n_rows == 30 and st._conn().execute("select count(*) from hpalogs").fetchone()[0] == 0
+    n_rows = st._lconn().execute("select count(*) from hpalog_batches").fetchone()[0]
+    assert n_rows == 30 and st._lconn().execute("select count(*) from hpalogs").fetchone()[0] == 0
     got = st.hpalogs(ids[1], 10)                           # an odd job: absent from every third batch
     want = [k for k in range(29, -1, -1) if k % 3][:10]
     assert [g.log.hpa_score for g in got] == want
@@ -205,7 +205,7 @@ def test_hpalog_batches_are_columnar_and_read_back_per_job(tmp_path):
     assert got[0].job_id == ids[1] and got[0].log.reason == "hold"
     st.add_hpalogs([HPALogBatch([ids[0]], T0 + 60 * 30 + 7200, "c", [1], [0], ["hold"], ["cpu", "mem"],
                                 [[1.0, 2.0]], [[1.0, 2.0]], [[1.0, 2.0]])])
-    assert st._conn().execute("select count(*) from hpalog_batches").fetchone()[0] == 1
+    assert st._lconn().execute("select count(*) from hpalog_batches").fetchone()[0] == 1
 
 
 def test_restarted_worker_adopts_its_held_jobs(tmp_path):
@@ -267,3 +267,45 @@ def test_session_columns_track_adds_and_drops():
             assert all(s.held[i] == (int(r), v) for i, v, r in zip(ids, vers, rids.tolist()))
     ids, _, _ = s.snapshot(5)
     assert len(ids) == 5
+
+
+def test_hpalog_writes_do_not_hold_the_jobs_file(tmp_path):
+    """HPA logs live in their own file (``<path>-hpalogs``): a log transaction
+    in flight (the service's background writer) leaves claims and verdict
+    writes on the jobs file free; a store of the single-file layout has its
+    log tables moved over once, entries intact."""
+    import threading
+    path = str(tmp_path / "j.db")
+    st = SQLiteStore(path)
+    for d in _docs(4):
+        st.put(d)
+    held, release = threading.Event(), threading.Event()
+
+    def writer():
+        c = st._lconn()
+        c.execute("begin immediate")
+        c.execute("insert into hpalogs values ('x', 1.0, '{}')")
+        held.set()
+        release.wait(10)
+        c.execute("commit")
+    th = threading.Thread(target=writer)
+    th.start()
+    held.wait(10)
+    t0 = time.perf_counter()
+    assert len(st.claim_batch("w", 10, 90.0, now=T0)) == 4      # not waiting on the log file's lock
+    assert time.perf_counter() - t0 < 5.0
+    release.set()
+    th.join()
+    # the single-file layout: log tables in the jobs file are moved once
+    old = str(tmp_path / "old.db")
+    st2 = SQLiteStore(old)
+    st2.add_hpalogs([HPALog(job_id="a:ns:h", timestamp=T0, log=HPALogBody(40, "x", []))])
+    lc = st2._lconn()
+    rows = lc.execute("select * from hpalogs").fetchall()
+    main = st2._conn()
+    main.execute("create table hpalogs (job_id text, ts real, body text)")
+    main.executemany("insert into hpalogs values (?,?,?)", rows)
+    lc.execute("delete from hpalogs")
+    st3 = SQLiteStore(old)
+    assert [l.timestamp for l in st3.hpalogs("a:ns:h", 5)] == [T0]
+    assert "hpalogs" not in {r[0] for r in st3._conn().execute("select name from sqlite_master where type='table'")}
