@@ -494,6 +494,7 @@ class FastPath:
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
         self._slide_state: dict = {}
         self._flat_rows = None     # (row map [S, M] object, flat int64 rows, slice when they are one run)
+        self.new_jobs = 0          # jobs planned by the last prepare
         self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
         self.model_churns = 0      # ModelArrays restricted to a churned job list instead of rebuilt
         self._hist_pending = False  # a per-job fetch left history in some FastWork.hist this cycle
@@ -696,6 +697,7 @@ class FastPath:
                 self._gcount_add(p.group, 1)
                 fast.append(fw)
                 todo.append(fw)
+        self.new_jobs = len(new_fw)
         if reg:
             self._register_windows(reg)
         if new_fw and self.b.exporter is not None:
@@ -2799,7 +2801,7 @@ def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | N
             c0, c1 = 0, max(1, int(st.nlen[rows].max()))
         sp = _StorePart()
         sp.name = name
-        sp.keys_json = _json_list(st.kjson, rows)
+        sp.keys_json = _json_list(st.key_json(rows), rows)
         sp.owners_json = _json_list(st.ojson, rows)
         sp.last_t = st.last_t[rows].copy()
         sp.nlen = None if st.sliding else st.nlen[rows].copy()

@@ -92,6 +92,7 @@ class ResidentHistory:
         self.ojson: list = []
         self.oblk = np.zeros(0, np.int16)
         self.owned = np.zeros(0, bool)
+        self.kdone = np.zeros(0, bool)              # kjson[r] is encoded
         self.t0: float | None = None                # sliding: time of column 0
         self.e = 0                                  # sliding: exclusive end column of the window
         self.ws = 0                                 # sliding: first column inside the window
@@ -126,6 +127,7 @@ class ResidentHistory:
         self.ojson.extend([None] * (new_cap - cap))
         self.oblk = np.concatenate([self.oblk, np.zeros(new_cap - cap, np.int16)])
         self.owned = np.concatenate([self.owned, np.zeros(new_cap - cap, bool)])
+        self.kdone = np.concatenate([self.kdone, np.zeros(new_cap - cap, bool)])
 
     OWNER_BLOCKS = 16
 
@@ -157,18 +159,35 @@ class ResidentHistory:
         return out, new
 
     def _own(self, rows, keys, owner) -> None:
+        """Record the owner of rows that have none (its JSON and block once per
+        distinct owner); a row's key JSON is encoded by the first history
+        save that needs it (:meth:`key_json`), not on the claiming cycle."""
         import json
         from ..parallel.dist import service_owner
         enc = json.JSONEncoder(separators=(",", ":")).encode
+        memo: dict = {}
         one = isinstance(owner, tuple)
         for i, r in enumerate(rows.tolist()):
             if self.owned[r]:
                 continue
-            o = owner if one else owner[i]
-            self.kjson[r] = enc(list(keys[i])).encode()
-            self.ojson[r] = enc([o[0], o[1]]).encode()
-            self.oblk[r] = service_owner(o[0], o[1], self.OWNER_BLOCKS)
+            o = owner if one else tuple(owner[i])
+            oj = memo.get(o)
+            if oj is None:
+                oj = memo[o] = (enc([o[0], o[1]]).encode(), service_owner(o[0], o[1], self.OWNER_BLOCKS))
+            self.kjson[r] = None
+            self.kdone[r] = False
+            self.ojson[r], self.oblk[r] = oj
             self.owned[r] = True
+
+    def key_json(self, rows: np.ndarray) -> list:
+        """UTF-8 JSON of the keys of ``rows`` (encoded once per row, then kept)."""
+        import json
+        enc = json.JSONEncoder(separators=(",", ":")).encode
+        kj, keys = self.kjson, self.keys
+        for r in rows[~self.kdone[rows]].tolist():
+            kj[r] = enc(list(keys[r])).encode()
+        self.kdone[rows] = True
+        return kj
 
     def get(self, key):
         return self.slot.get(key)
@@ -183,6 +202,7 @@ class ResidentHistory:
                 self.kjson[r] = self.ojson[r] = None
                 self.last_t[r] = -np.inf
             self.owned[rows] = False
+            self.kdone[rows] = False
             self.nlen[rows] = 0
             self.nfin[rows] = 0
             self.occ[rows] = False
