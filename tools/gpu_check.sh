@@ -72,6 +72,14 @@ for s in $steps; do
                p.sort_stats('tottime').print_stats(70); p.sort_stats('cumtime').print_stats(70)" \
                > gpurun_out/hostprof_$c.txt || exit 1
          done ;;
+    hostprof4) for c in 4e2e 2e2e; do
+           FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_$c.prof timeout -k 10 400 python -u benchmarks/bench_configs.py \
+               --config $c --steps 12 --warmup 3 > gpurun_out/check_hostprof_$c.log 2>&1; rc=$?
+           echo "hostprof $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+           python -c "import pstats,sys; p=pstats.Stats('gpurun_out/hostprof_$c.prof', stream=sys.stdout); \
+               p.sort_stats('tottime').print_stats(70); p.sort_stats('cumtime').print_stats(90)" \
+               > gpurun_out/hostprof_$c.txt || exit 1
+         done ;;
     hostprof60) FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_3e2e_http60.prof timeout -k 10 500 python -u \
                benchmarks/bench_configs.py --config 3e2e --source http --poll-seconds 60 --window 60 --steps 8 \
                --warmup 2 --prom-workers 8 > gpurun_out/check_hostprof_3e2e_http60.log 2>&1; rc=$?
