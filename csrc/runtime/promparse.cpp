@@ -532,6 +532,37 @@ FM_API void fm_count_finite(const float* a, int64_t R, int64_t n, int64_t ld, in
   }
 }
 
+// The host half of a sliding-grid write (engine/resident.py
+// write_sliding_flat), one pass instead of ~15 numpy passes: samples (row r,
+// time t, value v) whose grid column c = round((t - t0) / step) lies in the
+// window [ws, e) and whose value is finite go out as (r * width + c, v) into
+// out_flat / out_v; per row the finite count gains the samples newer than the
+// row's newest column BEFORE this batch (a re-sent sample counts once) and
+// last_t becomes the newest time.  Returns the samples written out.
+FM_API int64_t fm_sliding_prep(const int64_t* r, const double* t, const float* v, int64_t n, double t0, double step,
+                               int64_t ws, int64_t e, int64_t width, double* last_t, int64_t* nfin,
+                               int64_t* out_flat, float* out_v, unsigned char* inc) {
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    inc[i] = 0;
+    if (!std::isfinite(v[i])) continue;
+    const int64_t c = (int64_t)std::nearbyint((t[i] - t0) / step);
+    if (c < ws || c >= e) continue;
+    const double lt = last_t[r[i]];
+    const int64_t prev = std::isfinite(lt) ? (int64_t)std::nearbyint((lt - t0) / step) : -1;
+    inc[i] = c > prev ? 2 : 1;                 // 1: in the window, 2: and a new column
+    out_flat[k] = r[i] * width + c;
+    out_v[k] = v[i];
+    ++k;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    if (!inc[i]) continue;
+    if (inc[i] == 2) nfin[r[i]] += 1;
+    if (!(last_t[r[i]] >= t[i])) last_t[r[i]] = t[i];
+  }
+  return k;
+}
+
 // Host ring of the newest grid columns of every sliding row
 // (engine/fastpath.py _ring_write): clear the slots of the columns
 // (top_old, top_new] in every row, then store the samples whose column is

@@ -1251,9 +1251,10 @@ class FastPath:
             return np.full((nrows, n), np.nan, np.float32), t
         j0 = c0 % self.RING
         if j0 + n <= self.RING:
-            v = self._ring[rows, j0:j0 + n]                # gathers only the window's slots
-            if isinstance(rows, slice):
-                v = v.copy()                               # (the ring moves on next cycle)
+            # gathers only the window's slots; a slice of rows is a view of the
+            # ring, valid until the next cycle's ring write (the cycle's
+            # consumers -- group arrays, verdicts, HPA logs -- are done by then)
+            v = self._ring[rows, j0:j0 + n]
         else:
             v = np.concatenate([self._ring[rows, j0:], self._ring[rows, :j0 + n - self.RING]], axis=1)
         lo_ok, hi_ok = max(c0, self._ring_top - self.RING + 1), min(c1, self._ring_top)

@@ -63,6 +63,10 @@ def _load():
     if hasattr(lib, "fm_ring_write"):
         lib.fm_ring_write.argtypes = [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, ctypes.c_double]
         lib.fm_ring_write.restype = None
+    if hasattr(lib, "fm_sliding_prep"):
+        lib.fm_sliding_prep.argtypes = [c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, c_i64, c_i64,
+                                        c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]
+        lib.fm_sliding_prep.restype = c_i64
     if hasattr(lib, "fm_count_finite"):
         lib.fm_count_finite.argtypes = [c_vp, c_i64, c_i64, c_i64, c_vp]
         lib.fm_count_finite.restype = None
@@ -358,6 +362,24 @@ def count_finite(a: np.ndarray) -> np.ndarray:
     out = np.empty(a.shape[0], np.int64)
     lib.fm_count_finite(a.ctypes.data, a.shape[0], a.shape[1], a.strides[0] // 4, out.ctypes.data)
     return out
+
+
+def sliding_prep(r: np.ndarray, t: np.ndarray, v: np.ndarray, t0: float, step: float, ws: int, e: int, width: int,
+                 last_t: np.ndarray, nfin: np.ndarray, out_flat: np.ndarray, out_v: np.ndarray) -> int | None:
+    """fm_sliding_prep: the host half of a sliding-grid write in one pass
+    (None: no library, the caller does it in numpy).  ``last_t`` / ``nfin``
+    are updated in place; returns the samples written to the outputs."""
+    lib = _load()
+    if (lib is None or not hasattr(lib, "fm_sliding_prep") or last_t.dtype != np.float64 or nfin.dtype != np.int64
+            or not (last_t.flags.c_contiguous and nfin.flags.c_contiguous)):
+        return None
+    r = np.ascontiguousarray(r, np.int64)
+    t = np.ascontiguousarray(t, np.float64)
+    v = np.ascontiguousarray(v, np.float32)
+    inc = np.empty(len(r), np.uint8)
+    return int(lib.fm_sliding_prep(r.ctypes.data, t.ctypes.data, v.ctypes.data, len(r), float(t0), float(step),
+                                   int(ws), int(e), int(width), last_t.ctypes.data, nfin.ctypes.data,
+                                   out_flat.ctypes.data, out_v.ctypes.data, inc.ctypes.data))
 
 
 def ring_write(ring: np.ndarray, top_old: int, top_new: int, r: np.ndarray, t: np.ndarray, v: np.ndarray,

@@ -335,6 +335,26 @@ class ResidentHistory:
         assert self.sliding and self.t0 is not None
         if len(r) == 0:
             return
+        n = len(r)
+        if self.device.type == "cuda":
+            # indices and values in ONE pinned buffer, one host->device copy
+            hb = torch.empty((3 * n,), dtype=torch.int32).pin_memory()
+            hn = hb.numpy()
+            of, ov = hn[:2 * n].view(np.int64), hn[2 * n:].view(np.float32)
+        else:
+            of, ov = np.empty(n, np.int64), np.empty(n, np.float32)
+        k = native_rt.sliding_prep(r, t, v, self.t0, self.step, self.ws, self.e, self.width, self.last_t, self.nfin,
+                                   of, ov)
+        if k is not None:                                  # the one-pass native form
+            if k:
+                if self.device.type == "cuda":
+                    db = hb.to(self.device, non_blocking=True)
+                    flat, vals = db[:2 * n].view(torch.int64)[:k], db[2 * n:].view(torch.float32)[:k]
+                else:
+                    flat, vals = torch.from_numpy(of[:k]), torch.from_numpy(ov[:k])
+                self.buf.view(-1).index_copy_(0, flat, vals)
+                self.bytes_in += 12 * k
+            return
         c = self.col(t)
         ok = (c >= self.ws) & (c < self.e) & np.isfinite(v)
         r, c, v, t = r[ok], c[ok], v[ok], t[ok]

@@ -376,3 +376,36 @@ def test_window_helpers_match_numpy_forms():
     want_h = np.maximum(1, h).astype(np.int64)
     got = _device_horizons(torch.from_numpy(trow), torch.from_numpy(t_last), step).numpy()
     np.testing.assert_array_equal(got, want_h)
+
+
+def test_native_sliding_write_matches_numpy_path(monkeypatch):
+    """fm_sliding_prep (one native pass) == the numpy form of
+    ResidentHistory.write_sliding_flat: grid values, finite counts, newest
+    times -- with missing values, samples outside the window, a re-sent
+    sample and two samples of one row in one batch."""
+    import numpy as np
+    from foremast_amd.engine import native_rt
+    from foremast_amd.engine.resident import ResidentHistory
+    assert hasattr(native_rt._load(), "fm_sliding_prep")       # the native form is what runs first
+    out = []
+    for native in (True, False):
+        rng = np.random.default_rng(3)
+        if not native:
+            monkeypatch.setattr(native_rt, "sliding_prep", lambda *a, **k: None)
+        st = ResidentHistory(64, "cpu", 60.0, sliding=True)
+        st.rows_for([("k", i) for i in range(50)], 0)
+        st.advance(60.0 * 100, 60.0 * 40)
+        for cyc in range(3):
+            n = 120
+            r = rng.integers(0, 50, n)
+            t = 60.0 * rng.integers(30, 104, n)
+            v = rng.normal(size=n).astype(np.float32)
+            v[rng.random(n) < 0.1] = np.nan
+            if cyc == 2:                              # a re-sent sample
+                r, t, v = np.concatenate([r, r[:5]]), np.concatenate([t, t[:5]]), np.concatenate([v, v[:5]])
+            st.write_sliding_flat(r.astype(np.int64), t, v)
+        out.append((st.buf.clone(), st.nfin[:50].copy(), st.last_t[:50].copy()))
+    (ba, na, la), (bb, nb, lb) = out
+    assert torch.equal(torch.nan_to_num(ba, nan=-7.0), torch.nan_to_num(bb, nan=-7.0))
+    np.testing.assert_array_equal(na, nb)
+    np.testing.assert_array_equal(la, lb)
