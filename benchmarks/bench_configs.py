@@ -758,6 +758,8 @@ def config3e2e(args):
              "span_ms_median_rank0": span_ms, "span_ms_median_max_rank": worst, "span_ms_max_rank0": span_max,
              "cycle_ms_max_rank0": round(max(cyc_ms[args.warmup:] or cyc_ms or [0.0]), 3),
              "model_cache": {"hits": brain.model_cache.hits, "misses": brain.model_cache.misses},
+             "lstm_early_launch": ({"hits": brain.fast.prelaunch_hits, "misses": brain.fast.prelaunch_misses}
+                                   if brain.fast is not None else None),
              "fused_steady_cycles": ({"groups_fused": brain.fast.fused_steps, "declined": brain.fast.fused_declined}
                                      if brain.fast is not None else None),
              "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),

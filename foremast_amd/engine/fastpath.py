@@ -495,6 +495,11 @@ class FastPath:
         self._slide_state: dict = {}
         self._flat_rows = None     # (row map [S, M] object, flat int64 rows, slice when they are one run)
         self.new_jobs = 0          # jobs planned by the last prepare
+        self._pre_spec: dict = {}  # sliding group -> (ModelSub, H, model, grid ws) of its last LSTM forecast
+        self._pre: dict = {}       # sliding group -> a forecast launched during this cycle's fetch
+        self._pre_skip: dict = {}  # sliding group -> its last early launch was not used
+        self.prelaunch_hits = 0
+        self.prelaunch_misses = 0
         self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
         self.model_churns = 0      # ModelArrays restricted to a churned job list instead of rebuilt
         self._hist_pending = False  # a per-job fetch left history in some FastWork.hist this cycle
@@ -1152,7 +1157,10 @@ class FastPath:
         if wr:
             r, t, v = np.concatenate(wr), np.concatenate(wt), np.concatenate(wv)
             st.write_sliding_flat(r, t, v)
+            self._prelaunch(p0.group)                 # the grid holds this cycle's samples
             self._ring_write(r, t, v, fresh_rows)
+        else:
+            self._prelaunch(p0.group)
         fc = self._flat_rows
         if fc is None or fc[0] is not rows:
             flat = rows.reshape(-1).astype(np.int64)
@@ -2124,8 +2132,18 @@ class FastPath:
         if kind is None:
             # a forecaster without a fitted-state cache: its forecast, then the
             # fused band / reduce / compaction over it
-            fc, sig = self._forecast(algo, LazyHist(store.buf, sub.rm, *sub.shift_lim(), sub.T), sub, H)
+            grp = works[0].plan.group
+            lstm = b.lstm_for_jobs_of({sub.M}) if algo == "lstm" else None
+            got = self._pre_take(grp, sub, H, lstm)
+            if got is not None:
+                fc, sig = got                       # launched during the fetch (_prelaunch)
+            elif lstm is not None and lstm.reads_rows and store.buf.is_cuda:
+                fc, sig = lstm.forecast_rows(store.buf, sub.rm, sub.shift, sub.lim, int(sub.dk), sub.T, H)
+            else:
+                fc, sig = self._forecast(algo, LazyHist(store.buf, sub.rm, *sub.shift_lim(), sub.T), sub, H)
             fc, sig = fc.contiguous(), sig.contiguous()
+            if lstm is not None and lstm.reads_rows and store.sliding:
+                self._pre_spec[grp] = (sub, H, lstm, store.ws)
             out = self._fused_launch(works, ga, md, store, diff, -1, None, None, 0, H=fc.shape[1], fc=fc, sig=sig)
             self.fused_steps += 1
             out["fc"] = {algo: (sub, fc)} if hpa_algo == algo else {}
@@ -2224,6 +2242,44 @@ class FastPath:
         return {"works": works, "M": M, "ga": ga, "cur": ga.cur, "cur_t": ga.cur_t, "cur_len": ga.cur_len,
                 "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "anom_band": band,
                 "hist_rows": ga.rowmap, "store": store, "pts": (fz["up"], fz["lo"]), "last3": fz["last3"]}
+
+    # -------------------------------------------------- forecast launched early
+    # A steady LSTM group's forecast only needs the grid rows, the row
+    # alignment (its previous alignment moved by the columns the window
+    # advanced) and the model -- all known once the fetch wrote the cycle's
+    # samples into the grid.  _prelaunch queues it right there, so the
+    # recurrence runs on the device while the host reads the ring, builds the
+    # group arrays and slides the model arrays; _score_fused takes it when the
+    # slid arrays are exactly what it predicted (same row map object, same
+    # alignment offset, dense length, horizon and model), else recomputes.  A
+    # miss skips the next cycle's early launch (a churning group re-lays its
+    # arrays every cycle: no wasted recurrences).
+
+    def _prelaunch(self, group: tuple) -> None:
+        spec = self._pre_spec.get(group)
+        self._pre.pop(group, None)
+        if spec is None or self._pre_skip.pop(group, False):
+            return
+        sub, H, lstm, ws0 = spec
+        st = self.sliding
+        k = st.ws - ws0
+        if k < 0 or not st.buf.is_cuda:
+            return
+        dk = int(sub.dk) + k
+        fc, sig = lstm.forecast_rows(st.buf, sub.rm, sub.shift, sub.lim, dk, sub.T, H)
+        self._pre[group] = (sub.rm, dk, sub.T, H, lstm, self.cycle, fc, sig)
+
+    def _pre_take(self, group: tuple, sub: "ModelSub", H: int, lstm):
+        pre = self._pre.pop(group, None)
+        if pre is None:
+            return None
+        rm, dk, T, H0, m0, cyc, fc, sig = pre
+        if rm is sub.rm and dk == int(sub.dk) and T == sub.T and H0 == H and m0 is lstm and cyc == self.cycle:
+            self.prelaunch_hits += 1
+            return fc, sig
+        self.prelaunch_misses += 1
+        self._pre_skip[group] = True
+        return None
 
     def _forecast(self, algo: str, lazy: "LazyHist", sub: "ModelSub", H: int):
         from ..models import zoo

@@ -223,6 +223,9 @@ def test_gpu_fused_steady_cycle_equals_op_by_op(algo, kind):
     # cycle 0 fits; later cycles whose rows all hit the cache run fused
     assert a[3].fast.fused_steps >= 2 and b[3].fast.fused_steps == 0
     assert a[3].model_cache.hits == b[3].model_cache.hits
+    if algo == "lstm":
+        # steady cycles took the forecast launched during the fetch (_prelaunch)
+        assert a[3].fast.prelaunch_hits >= 2, (a[3].fast.prelaunch_hits, a[3].fast.prelaunch_misses)
 
 
 @pytest.mark.gpu
