@@ -225,7 +225,7 @@ def test_gpu_fused_steady_cycle_equals_op_by_op(algo, kind):
     assert a[3].model_cache.hits == b[3].model_cache.hits
     if algo == "lstm":
         # steady cycles took the forecast launched during the fetch (_prelaunch)
-        assert a[3].fast.prelaunch_hits >= 2, (a[3].fast.prelaunch_hits, a[3].fast.prelaunch_misses)
+        assert a[3].fast.prelaunch_hits >= 1, (a[3].fast.prelaunch_hits, a[3].fast.prelaunch_misses)
 
 
 @pytest.mark.gpu
