@@ -115,6 +115,11 @@ for s in $steps; do
               python3 "$R/benchmarks/bench_configs.py" --config 2e2e --steps 10 --warmup 2 \
               > "$R/gpurun_out/check_prof_c2e2e.log" 2>&1; rc=$?
           echo "prof_c2e2e rc=$rc"; cd "$R"; [ $rc -eq 0 ] || exit $rc ;;
+    profc4) cd /tmp && export TMPDIR=/tmp
+          timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_c4" -o c4 -- \
+              python3 "$R/benchmarks/bench_configs.py" --config 4 --steps 10 --warmup 3 \
+              > "$R/gpurun_out/check_prof_c4.log" 2>&1; rc=$?
+          echo "prof_c4 rc=$rc"; cd "$R"; [ $rc -eq 0 ] || exit $rc ;;
     prof) cd /tmp && export TMPDIR=/tmp
           timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_headline" -o headline -- \
               python3 "$R/bench.py" --steps 50 --warmup 10 > "$R/gpurun_out/check_prof_headline.log" 2>&1; rc=$?
