@@ -787,10 +787,11 @@ def config4(args):
     minlb = torch.tensor([r.min_lower_bound for r in rules], dtype=torch.float32, device=dev)
     gathered = torch.empty((info.world * pad, 4), dtype=torch.float32, device=dev)
 
+    valid = torch.full((pad * M,), 3, dtype=torch.int32, device=dev)     # every row gated in
+
     def step():
         fc, sig = model.forecast(hist, T_HIST, args.window)
         up, lo, flags, cnt, sc = SM.band_decide(cur, fc, sig, M, thr, bound, minlb, None, 1.0)
-        valid = torch.full_like(cnt, 3)
         packed = C.service_reduce(cnt, sc, valid, M)
         D.all_gather_rows(packed, gathered)
 

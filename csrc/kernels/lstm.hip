@@ -618,12 +618,16 @@ FM_API int fm_lstm_forward(const void* xa, int64_t B, int L, int H, const void* 
 // LSTMForecaster._head).  One thread per sequence, W and bias in LDS (Hz x H
 // <= 64 x 256 floats); replaces mm + add + cat + mul + add.
 // ---------------------------------------------------------------------------
-template <int H>
+template <int H, int NZ>
 __global__ __launch_bounds__(256) void lstm_head_kernel(const float* __restrict__ h, int64_t B,
                                                         const float* __restrict__ W, const float* __restrict__ bias,
                                                         int Hz, const float* __restrict__ mu,
                                                         const float* __restrict__ sd, int Hout,
                                                         float* __restrict__ fc) {
+  // one thread per sequence; W / bias in LDS (every lane reads the same
+  // word: a broadcast); NZ >= Hz is the compile-time bound of the head's
+  // outputs, so the accumulators stay in registers and the horizon padding
+  // (Hout > Hz repeats the last output) needs no runtime register indexing
   extern __shared__ float sw[];            // [Hz][H] then bias [Hz]
   for (int i = threadIdx.x; i < Hz * H; i += blockDim.x) sw[i] = W[i];
   for (int i = threadIdx.x; i < Hz; i += blockDim.x) sw[Hz * H + i] = bias[i];
@@ -631,28 +635,30 @@ __global__ __launch_bounds__(256) void lstm_head_kernel(const float* __restrict_
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const float4* hr = reinterpret_cast<const float4*>(h + b * H);
-  float acc[64];
-  const int nz = Hz < 64 ? Hz : 64;
+  float acc[NZ];
 #pragma unroll
-  for (int j = 0; j < 64; ++j) acc[j] = 0.f;
+  for (int j = 0; j < NZ; ++j) acc[j] = 0.f;
+#pragma unroll 4
   for (int k4 = 0; k4 < H / 4; ++k4) {
     const float4 x = hr[k4];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      if (j < nz) {
-        const float* w = sw + j * H + 4 * k4;
-        acc[j] = __builtin_fmaf(x.x, w[0], __builtin_fmaf(x.y, w[1], __builtin_fmaf(x.z, w[2], __builtin_fmaf(x.w, w[3], acc[j]))));
+    for (int j = 0; j < NZ; ++j) {
+      if (j < Hz) {
+        const float4 w = *reinterpret_cast<const float4*>(sw + j * H + 4 * k4);
+        acc[j] = __builtin_fmaf(x.x, w.x, __builtin_fmaf(x.y, w.y, __builtin_fmaf(x.z, w.z, __builtin_fmaf(x.w, w.w, acc[j]))));
       }
     }
   }
   const float m = mu[b], s = sd[b];
-  for (int j = 0; j < Hout; ++j) {
-    const int jj = j < nz ? j : nz - 1;
-    float z = 0.f;
+  float last = 0.f;
 #pragma unroll
-    for (int q = 0; q < 64; ++q) z = q == jj ? acc[q] : z;
-    fc[b * Hout + j] = __builtin_fmaf(s, z + sw[Hz * H + jj], m);
-  }
+  for (int j = 0; j < NZ; ++j)
+    if (j < Hz) acc[j] = __builtin_fmaf(s, acc[j] + sw[Hz * H + j], m), last = acc[j];
+  float* out = fc + b * Hout;
+#pragma unroll
+  for (int j = 0; j < NZ; ++j)
+    if (j < Hout) out[j] = j < Hz ? acc[j] : last;
+  for (int j = NZ; j < Hout; ++j) out[j] = last;
 }
 
 FM_API int fm_lstm_head(const float* h, int64_t B, int H, const float* W, const float* bias, int Hz, const float* mu,
@@ -661,8 +667,13 @@ FM_API int fm_lstm_head(const float* h, int64_t B, int H, const float* W, const 
   if (Hz < 1 || Hz > 64 || Hout < 1) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)((B + 255) / 256));
   const size_t lds = (size_t)(Hz * H + Hz) * sizeof(float);
-#define FM_HEAD(HH) hipLaunchKernelGGL(lstm_head_kernel<HH>, grid, dim3(256), lds, stream, h, B, W, bias, Hz, mu, sd, \
-                                       Hout, fc)
+#define FM_HEAD(HH)                                                                                              \
+  do {                                                                                                         \
+    if (Hz <= 16)                                                                                              \
+      hipLaunchKernelGGL((lstm_head_kernel<HH, 16>), grid, dim3(256), lds, stream, h, B, W, bias, Hz, mu, sd, Hout, fc); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((lstm_head_kernel<HH, 64>), grid, dim3(256), lds, stream, h, B, W, bias, Hz, mu, sd, Hout, fc); \
+  } while (0)
   if (H == 128) FM_HEAD(128);
   else if (H == 64) FM_HEAD(64);
   else if (H == 32) FM_HEAD(32);
