@@ -354,11 +354,6 @@ __device__ __forceinline__ void lstm_pipe_body(const XS& xs, int64_t B, int L, c
     }
   };
 
-#if defined(FM_LSTM_PRIO)
-  // A/B build only: the second-dispatched half of the workgroup at static
-  // priority 1 (MI355X_MICROARCH.md "static priority for the younger half")
-  if (w >= H / 32) __builtin_amdgcn_s_setprio(1);
-#endif
   f32x16 acc0[2], acc1[2];
   typename XS::Raw x0n = xs.fetch(0, 0), x1n = xs.fetch(1, 0);
   gates(0, xs.make(0, 0, x0n), acc0);                // tile 0, step 0

@@ -46,11 +46,6 @@ for s in $steps; do
           run lstm_ab 200 python -u tools/lstm_ab.py || exit $rc
           run config4 300 python -u benchmarks/bench_configs.py --config 4 || exit $rc
           run config4_w30 300 python -u benchmarks/bench_configs.py --config 4 --steps 30 --warmup 30 || exit $rc ;;
-    lstmprio) V=$R/foremast_amd/_native/variants
-          run lstm_ab 200 python -u tools/lstm_ab.py || exit $rc
-          run lstm_ab_prio 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_prio.so python -u tools/lstm_ab.py || exit $rc
-          run lstm_ab2 200 python -u tools/lstm_ab.py || exit $rc
-          run lstm_ab_prio2 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_prio.so python -u tools/lstm_ab.py || exit $rc ;;
     pmclstm) run pmclstm 420 bash tools/pmc_lstm.sh || exit $rc ;;
     r5tests) run r5tests 600 python -u -m pytest tests/test_fastpath_models.py tests/test_canary_ops.py tests/test_warm_restart.py \
                  tests/test_model_ops.py tests/test_fastpath.py -m gpu -x -v --timeout 120 --timeout-method thread \
