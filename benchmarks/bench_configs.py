@@ -334,9 +334,9 @@ def config3e2e(args):
     # continuous / HPA jobs stay alive for the whole run (their end time is
     # the submission window); canary jobs use the 10-minute watch window
     # (in the mixed fleet one that outlasts the run: its churn is explicit)
-    # (+ the --restart cycles: two async-save cycles, the save diagnosis's,
+    # (+ the --restart cycles: the async-save cycles and those its host copy spans, the save diagnosis's,
     # and the restarted brain's first: inside the staged window too)
-    n_cycles = args.steps + args.warmup + 3 + (8 if args.restart else 0)
+    n_cycles = args.steps + args.warmup + 3 + (48 if args.restart else 0)
     long_window = max(args.window, int(n_cycles * poll / 60) + 20)
 
     def submit_one(client, c, j):
@@ -589,12 +589,27 @@ def config3e2e(args):
                 req_log.pop()
                 http_stats.pop()
             sp_ = {k: round(spans[k].pop(), 2) for k in brain.spans.last if spans.get(k)}
+            # back-to-back cycles while the rest of the host copy goes out a
+            # piece per cycle (a 60-s poll leaves it the idle time instead)
+            during = []
+            while tag_ == "steady" and getattr(brain, "_hist_issue", None) is not None and len(during) < 30:
+                step()
+                during.append(round(cyc_ms.pop(), 2))
+                rows.pop()
+                if live is not None:
+                    req_log.pop()
+                    http_stats.pop()
+                for k in brain.spans.last:
+                    if spans.get(k):
+                        spans[k].pop()
             t_w = time.perf_counter()
             if fut is not None and hasattr(fut, "result"):
-                fut.result()
+                brain.wait_history()
             async_save[tag_] = {"cycle_with_async_save_ms": round(save_cycle_ms, 2), "issue_ms": round(issue_ms, 2),
                                 "writer_tail_after_cycle_s": round(time.perf_counter() - t_w, 3),
                                 "spans_ms": {k: v for k, v in sp_.items() if v >= 0.5}}
+            if during:
+                async_save[tag_]["cycles_while_copying_ms"] = during
         if os.environ.get("FOREMAST_SAVE_DIAG") and dev.type == "cuda":
             # which part of the background save stretches the cycle beside it:
             # the issue alone (device gather + host copy draining during the
@@ -622,6 +637,7 @@ def config3e2e(args):
                     time.sleep(1e-3)
             for mode in ("issue", "poll", "state"):
                 hs_ = _fpm.history_issue(brain.fast, dbufs, pins, sstream)
+                hs_.pump(None)                     # the whole host copy queued at once (the pre-pump form)
                 th = None
                 if mode == "poll":
                     def work(hs_=hs_):

@@ -49,6 +49,7 @@ from .exporter import BrainExporter
 from .sources import Series, SourceError, SourceRouter, substitute_window
 
 GC_FREEZE_AFTER = 1000        # jobs planned in one cycle that trigger gc.freeze()
+HIST_PUMP_BYTES = 128 << 20   # history-checkpoint host copy queued per cycle (~2.5 ms of copy engine)
 
 log = logging.getLogger("foremast.brain")
 
@@ -432,6 +433,7 @@ class Brain:
         self._impact_step(now)
         if scored:
             n_rows += self._finish_fast(scored, now, updates, hpalogs, outcome, bulk)
+        self._hist_pump()                  # the cycle's device->host copies are done: a piece of a save
         if batches:
             n_rows += self._finish_general(batches, now, updates, hpalogs, outcome)
         with self.spans.span("persist"):
@@ -488,6 +490,20 @@ class Brain:
                 log.exception("background HPA log write failed (%d batches)", len(batch))
         self._log_pending = [f for f in self._log_pending if not f.done()]
         self._log_pending.append(ex.submit(write))
+
+    def _hist_pump(self, budget: int | None = HIST_PUMP_BYTES) -> None:
+        hs = getattr(self, "_hist_issue", None)
+        if hs is not None and hs.pump(budget):
+            self._hist_issue = None
+
+    def wait_history(self, timeout: float | None = None):
+        """Finish the asynchronous history save in flight (its remaining host
+        copy queued now) and return its file path (None: none in flight)."""
+        fut = getattr(self, "_hist_future", None)
+        if fut is None:
+            return None
+        self._hist_pump(None)
+        return fut.result(timeout=timeout)
 
     def flush_logs(self) -> None:
         """Wait for the background HPA log writes queued so far."""
@@ -667,6 +683,7 @@ class Brain:
                             time.monotonic() - hist_t >= self.cfg.history_checkpoint_s:
                         self.save_history(checkpoint_dir, wait=False)      # off the cycle (side stream + thread)
                         hist_t = time.monotonic()
+                    self._hist_pump(None)          # between cycles: the rest of a save's host copy
                     if r.get("claimed", 0) == 0:
                         (stop.wait(poll) if stop is not None else time.sleep(poll))
                 except Exception:
@@ -674,6 +691,7 @@ class Brain:
                     (stop.wait(poll) if stop is not None else time.sleep(poll))
         finally:
             self.flush_logs()
+            self._hist_pump(None)
             if checkpoint_dir:
                 try:
                     self.save_checkpoint(checkpoint_dir)
@@ -856,7 +874,7 @@ class Brain:
             if not wait:
                 log.info("history checkpoint still being written; this one skipped")
                 return None
-            prev.result()
+            self.wait_history()
         tag = checkpoint.rank_tag(self.info.rank, self.info.world)
         if wait or self.device.type != "cuda":
             t, meta = history_issue(self.fast).state()
@@ -873,6 +891,8 @@ class Brain:
         # which makes no device call (it polls the copy's event through
         # HistorySave.ready, a non-blocking query)
         hs = history_issue(self.fast, self._hist_dev, self._hist_pinned, self._hist_stream)
+        hs.pump(HIST_PUMP_BYTES)                      # the rest: a piece per cycle (_hist_pump) or when idle
+        self._hist_issue = hs
         rank, world = self.info.rank, self.info.world
 
         def write():

@@ -2792,11 +2792,34 @@ class HistorySave:
     (the row keys / owners are ready JSON bytes saved as ``uint8`` tensors), so
     a writer thread holds the interpreter only for moments."""
 
-    def __init__(self, step: int, parts: list, ev) -> None:
+    # the device->host copy goes out in pieces of this size, a few per brain
+    # cycle in the cycle's copy-free tail (pump): one gigabyte-sized copy
+    # would hold the copy engine for ~30 ms and the loop's own small
+    # device->host copies would queue behind it
+    CHUNK = 64 << 20
+
+    def __init__(self, step: int, parts: list, ev, stream=None, chunks: list | None = None) -> None:
         self.step, self.parts, self.ev = step, parts, ev
+        self.stream, self.chunks = stream, list(chunks or [])
+
+    def pump(self, budget: int | None = None) -> bool:
+        """Enqueue pieces of the host copy worth up to ``budget`` bytes (None:
+        all); on the brain loop's thread.  True once every piece is queued."""
+        if not self.chunks:
+            return True
+        done = 0
+        with torch.cuda.stream(self.stream):
+            while self.chunks and (budget is None or done < budget):
+                dst, src = self.chunks.pop(0)
+                dst.copy_(src, non_blocking=True)
+                done += src.numel() * src.element_size()
+            if not self.chunks:
+                self.ev = torch.cuda.Event()
+                self.ev.record(self.stream)
+        return not self.chunks
 
     def ready(self) -> bool:
-        return self.ev is None or self.ev.query()
+        return not self.chunks and (self.ev is None or self.ev.query())
 
     def state(self) -> tuple[dict, dict]:
         t: dict[str, torch.Tensor] = {}
@@ -2888,11 +2911,11 @@ def history_issue(fp: "FastPath", dev_bufs: dict | None = None, pinned: dict | N
         g_ev = torch.cuda.Event()
         g_ev.record(stream)
         cur.wait_event(g_ev)                     # the loop's grid writes wait for the gather only
-        with torch.cuda.stream(stream):
-            for blk, view, ri, hv in gathered:
-                hv.copy_(blk, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(stream)
+        chunks = []
+        for blk, view, ri, hv in gathered:
+            rb = max(1, HistorySave.CHUNK // max(1, blk.shape[1] * blk.element_size()))
+            chunks += [(hv[r0:r0 + rb], blk[r0:r0 + rb]) for r0 in range(0, blk.shape[0], rb)]
+        return HistorySave(fp.b.step, parts, None, stream, chunks)      # the host copy: HistorySave.pump
     return HistorySave(fp.b.step, parts, ev)
 
 
