@@ -49,7 +49,7 @@ from .exporter import BrainExporter
 from .sources import Series, SourceError, SourceRouter, substitute_window
 
 GC_FREEZE_AFTER = 1000        # jobs planned in one cycle that trigger gc.freeze()
-HIST_PUMP_BYTES = 128 << 20   # history-checkpoint host copy queued per cycle (~2.5 ms of copy engine)
+HIST_PUMP_BYTES = 64 << 20    # history-checkpoint host copy queued per cycle (a few ms of copy engine)
 
 log = logging.getLogger("foremast.brain")
 
@@ -891,7 +891,9 @@ class Brain:
         # which makes no device call (it polls the copy's event through
         # HistorySave.ready, a non-blocking query)
         hs = history_issue(self.fast, self._hist_dev, self._hist_pinned, self._hist_stream)
-        hs.pump(HIST_PUMP_BYTES)                      # the rest: a piece per cycle (_hist_pump) or when idle
+        # the host copy: a piece per cycle in the cycle's copy-free tail
+        # (_hist_pump), the rest between cycles -- nothing queued here, where
+        # the cycle's own first device->host copy would wait behind it
         self._hist_issue = hs
         rank, world = self.info.rank, self.info.world
 
