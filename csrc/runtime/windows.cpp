@@ -57,6 +57,34 @@ FM_API void fm_window_pack(const float* V, int64_t ld, const int64_t* slot0, con
   for (auto& th : pool) th.join();
 }
 
+// The time of the k[i]-th packed sample of window row i (fm_window_pack's
+// order: pods slot by slot, time within a pod, NaNs squeezed out), NaN past
+// the row's samples -- what a verdict needs of the packed times, for its
+// anomalous points only, instead of a [R, n] float64 time matrix per cycle.
+FM_API void fm_window_times(const float* V, int64_t ld, const int64_t* slot0, const int64_t* nslot,
+                            const int64_t* ncol, const double* start, const double* step, int64_t m,
+                            const int64_t* k, double* out) {
+  for (int64_t i = 0; i < m; ++i) {
+    double t = NAN;
+    const int64_t s0 = slot0[i];
+    if (s0 >= 0 && k[i] >= 0) {
+      const int64_t nc = ncol[i] < ld ? ncol[i] : ld;
+      int64_t seen = 0;
+      for (int64_t s = 0; s < nslot[i] && std::isnan(t); ++s) {
+        const float* row = V + (s0 + s) * ld;
+        for (int64_t c = 0; c < nc; ++c) {
+          if (std::isnan(row[c])) continue;
+          if (seen++ == k[i]) {
+            t = start[i] + step[i] * (double)c;
+            break;
+          }
+        }
+      }
+    }
+    out[i] = t;
+  }
+}
+
 // Write one fetch round's batched answers into the grid (WindowTable.apply
 // for every request at once).  Request r covers the windows
 // ws[woff[r] .. woff[r+1]) -- each takes its own grid range [lo, hi] (same

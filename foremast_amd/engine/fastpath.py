@@ -276,10 +276,39 @@ class LazyHist:
 _NOSPEC = object()
 
 
+class WindowTimes:
+    """The times of a table group's packed current windows ([R, n]), read
+    from the window table on access: a verdict needs them at its anomalous
+    points only, so the per-cycle pack writes no [R, n] float64 matrix (2/3
+    of its bytes).  ``t[rows, points]`` -> float64 array, ``t[rows]`` -> the
+    rows' WindowTimes, ``np.asarray(t)`` -> the full matrix.  Valid while the
+    table holds the windows as packed (the cycle that packed them)."""
+
+    ndim = 2
+
+    def __init__(self, wt, wids: np.ndarray, n: int) -> None:
+        self.wt, self.w, self.shape = wt, np.asarray(wids, np.int64), (len(wids), int(n))
+
+    def __len__(self) -> int:
+        return self.shape[0]
+
+    def __getitem__(self, key):
+        if isinstance(key, tuple) and len(key) == 2:
+            r, k = np.broadcast_arrays(np.asarray(key[0], np.int64), np.asarray(key[1], np.int64))
+            t = self.wt.times_at(self.w[r.reshape(-1)], k.reshape(-1))
+            t = np.where(k.reshape(-1) < self.shape[1], t, np.nan)
+            return t.reshape(r.shape) if r.ndim else float(t[0])
+        return WindowTimes(self.wt, self.w[key], self.shape[1])
+
+    def __array__(self, dtype=None, copy=None):
+        t = self.wt.pack(self.w, self.shape[1])[1]
+        return t if dtype is None else t.astype(dtype)
+
+
 def _bcast_row(a: np.ndarray) -> np.ndarray | None:
     """The row of a [R, n] array that is one finite row broadcast over R
     (merged sliding windows' times), else None."""
-    if a.ndim != 2 or not a.shape[0] or a.strides[0] != 0:
+    if not isinstance(a, np.ndarray) or a.ndim != 2 or not a.shape[0] or a.strides[0] != 0:
         return None
     r = a[0]
     return r if np.isfinite(r).all() else None
@@ -1558,7 +1587,8 @@ class FastPath:
                 return self._install_arrays(ga, key, works, xslots)
         n = max(1, wt.max_points(wc))
         pin = self._pinned(("tcur", key), (len(wc), n), dev)
-        cur, cur_t, cur_len = wt.pack(wc, n, out_v=pin)
+        cur, _, cur_len = wt.pack(wc, n, times=False, out_v=pin)
+        cur_t = WindowTimes(wt, wc, n)
         nb = wt.max_points(wb)
         base = wt.pack(wb, nb, times=False, out_v=self._pinned(("tbase", key), (len(wb), nb), dev))[0] if nb else None
         has_hist = np.isfinite(store.last_t[rowmap]).reshape(S, M)
@@ -1610,8 +1640,9 @@ class FastPath:
             # every window changed (a live fleet at the poll cadence): pack the
             # whole arrays straight into pinned memory, replace, one upload each
             key = ga.key
-            v, t, ln = wt.pack(wc, ga.cur.shape[1], out_v=self._pinned(("tcur", key), ga.cur.shape, dev))
-            ga.cur, ga.cur_t, ga.cur_len = v, t, ln
+            v, _, ln = wt.pack(wc, ga.cur.shape[1], times=False,
+                               out_v=self._pinned(("tcur", key), ga.cur.shape, dev))
+            ga.cur, ga.cur_t, ga.cur_len = v, WindowTimes(wt, wc, ga.cur.shape[1]), ln
             ga.cur_dev.copy_(torch.from_numpy(v), non_blocking=True)
             wt.dirty[wc[wc >= 0]] = False
             if ga.base_d is not None:
@@ -1622,8 +1653,12 @@ class FastPath:
                 wt.dirty[wb[wb >= 0]] = False
             return True
         ri = torch.from_numpy(rows).to(dev)
-        v, t, ln = wt.pack(wc[rows], ga.cur.shape[1])
-        ga.cur[rows], ga.cur_t[rows], ga.cur_len[rows] = v, t, ln
+        v, t, ln = wt.pack(wc[rows], ga.cur.shape[1], times=not isinstance(ga.cur_t, WindowTimes))
+        ga.cur[rows], ga.cur_len[rows] = v, ln
+        if isinstance(ga.cur_t, WindowTimes):       # (read from the table when asked)
+            ga.cur_t = WindowTimes(wt, wc, ga.cur.shape[1])
+        else:
+            ga.cur_t[rows] = t
         ga.cur_dev.index_copy_(0, ri, up(v))
         wt.dirty[wc[rows][wc[rows] >= 0]] = False
         if ga.base_d is not None:

@@ -709,6 +709,42 @@ class WindowTable:
         w = w[w >= 0]
         return int((self.nslot[w] * self.ncol[w]).max()) if len(w) else 0
 
+    def times_at(self, wids: np.ndarray, k: np.ndarray) -> np.ndarray:
+        """Time of the ``k[i]``-th packed sample of window ``wids[i]`` (the
+        order :meth:`pack` lays them out; NaN past the window's samples)."""
+        w = np.ascontiguousarray(wids, np.int64).reshape(-1)
+        k = np.ascontiguousarray(k, np.int64).reshape(-1)
+        m = len(w)
+        out = np.full(m, np.nan)
+        if not m:
+            return out
+        ok = w >= 0
+        wz = np.where(ok, w, 0)
+        slot0 = np.where(ok, self.slot0[wz], -1).astype(np.int64)
+        nslot = np.where(ok, self.nslot[wz], 0).astype(np.int64)
+        ncol = np.where(ok, self.ncol[wz], 0).astype(np.int64)
+        start = np.ascontiguousarray(self.start[wz] + np.nan_to_num(self.toff[wz]), np.float64)
+        step = np.ascontiguousarray(self.step[wz], np.float64)
+        lib = native_rt._load()
+        V = self.V if self.V.flags.c_contiguous else np.ascontiguousarray(self.V)
+        if lib is not None and hasattr(lib, "fm_window_times"):
+            if not getattr(lib, "_wt_typed", False):
+                c_vp, c_i64 = ctypes.c_void_p, ctypes.c_int64
+                lib.fm_window_times.argtypes = [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]
+                lib.fm_window_times.restype = None
+                lib._wt_typed = True
+            lib.fm_window_times(V.ctypes.data, V.shape[1], slot0.ctypes.data, nslot.ctypes.data, ncol.ctypes.data,
+                                start.ctypes.data, step.ctypes.data, m, k.ctypes.data, out.ctypes.data)
+            return out
+        for i in range(m):
+            if slot0[i] < 0 or k[i] < 0:
+                continue
+            blk = V[slot0[i]:slot0[i] + nslot[i], :min(ncol[i], V.shape[1])]
+            ss, cc = np.nonzero(~np.isnan(blk))
+            if k[i] < len(cc):
+                out[i] = start[i] + step[i] * cc[k[i]]
+        return out
+
     def pack(self, wids: np.ndarray, width: int | None = None, times: bool = True, out_v: np.ndarray | None = None):
         """(values [R, n] float32, times [R, n] float64 or None, lens [R]):
         row r = window ``wids[r]``'s samples pod-major / time-minor, missing

@@ -131,6 +131,20 @@ def test_batched_pod_union_equals_per_job_queries():
         np.testing.assert_array_equal(v[r, :ln[r]], want_v)
         np.testing.assert_array_equal(t[r, :ln[r]], want_t)
     assert np.isnan(v[:, 11 * 4:]).all()
+    # times_at (what a verdict reads instead of the time matrix) == pack's
+    # times, natively and through the numpy fallback; NaN past a row's samples
+    w = np.array(list(wid.values()))
+    rr, kk = np.meshgrid(np.arange(len(w)), np.arange(t.shape[1] + 2), indexing="ij")
+    want = np.full(rr.shape, np.nan)
+    want[:, :t.shape[1]] = t
+    np.testing.assert_array_equal(wt.times_at(w[rr.ravel()], kk.ravel()).reshape(rr.shape), want)
+    import foremast_amd.engine.native_rt as NR
+    keep = NR._load
+    try:
+        NR._load = lambda: None
+        np.testing.assert_array_equal(wt.times_at(w[rr.ravel()], kk.ravel()).reshape(rr.shape), want)
+    finally:
+        NR._load = keep
     # the injected fault reached exactly its pod's series
     r3 = list(wid).index("svc3")
     assert v[r3, 11:22].mean() > 3 * v[r3, :11].mean()
