@@ -891,6 +891,7 @@ class Brain:
         # which makes no device call (it polls the copy's event through
         # HistorySave.ready, a non-blocking query)
         hs = history_issue(self.fast, self._hist_dev, self._hist_pinned, self._hist_stream)
+        dev = self.device
         # the host copy: a piece per cycle in the cycle's copy-free tail
         # (_hist_pump), the rest between cycles -- nothing queued here, where
         # the cycle's own first device->host copy would wait behind it
@@ -906,7 +907,10 @@ class Brain:
             iv = sys.getswitchinterval()
             sys.setswitchinterval(min(iv, 1e-4))
             try:
+                torch.cuda.set_device(dev)
                 while not hs.ready():
+                    if hs.stalled():             # nobody is pumping: the loop is idle or gone
+                        hs.pump(None)
                     time.sleep(2e-3)
                 t, meta = hs.state()
                 meta.update(rank=rank, world=world)

@@ -2834,24 +2834,39 @@ class HistorySave:
     CHUNK = 64 << 20
 
     def __init__(self, step: int, parts: list, ev, stream=None, chunks: list | None = None) -> None:
+        import threading
+        import time
         self.step, self.parts, self.ev = step, parts, ev
         self.stream, self.chunks = stream, list(chunks or [])
+        self._lock = threading.Lock()
+        self.t_pump = time.monotonic()
+
+    # a loop that stops pumping (idle, shut down, or a caller waiting on the
+    # future without pumping) leaves the rest to the writer after this long
+    STALL_S = 0.5
 
     def pump(self, budget: int | None = None) -> bool:
         """Enqueue pieces of the host copy worth up to ``budget`` bytes (None:
         all); on the brain loop's thread.  True once every piece is queued."""
-        if not self.chunks:
-            return True
-        done = 0
-        with torch.cuda.stream(self.stream):
-            while self.chunks and (budget is None or done < budget):
-                dst, src = self.chunks.pop(0)
-                dst.copy_(src, non_blocking=True)
-                done += src.numel() * src.element_size()
+        import time
+        with self._lock:
+            self.t_pump = time.monotonic()
             if not self.chunks:
-                self.ev = torch.cuda.Event()
-                self.ev.record(self.stream)
-        return not self.chunks
+                return True
+            done = 0
+            with torch.cuda.stream(self.stream):
+                while self.chunks and (budget is None or done < budget):
+                    dst, src = self.chunks.pop(0)
+                    dst.copy_(src, non_blocking=True)
+                    done += src.numel() * src.element_size()
+                if not self.chunks:
+                    self.ev = torch.cuda.Event()
+                    self.ev.record(self.stream)
+            return not self.chunks
+
+    def stalled(self) -> bool:
+        import time
+        return bool(self.chunks) and time.monotonic() - self.t_pump > self.STALL_S
 
     def ready(self) -> bool:
         return not self.chunks and (self.ev is None or self.ev.query())
