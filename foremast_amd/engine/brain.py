@@ -891,7 +891,7 @@ class Brain:
         # which makes no device call (it polls the copy's event through
         # HistorySave.ready, a non-blocking query)
         hs = history_issue(self.fast, self._hist_dev, self._hist_pinned, self._hist_stream)
-        dev = self.device
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         # the host copy: a piece per cycle in the cycle's copy-free tail
         # (_hist_pump), the rest between cycles -- nothing queued here, where
         # the cycle's own first device->host copy would wait behind it
