@@ -526,7 +526,7 @@ class FastPath:
         self.new_jobs = 0          # jobs planned by the last prepare
         self._pre_spec: dict = {}  # sliding group -> (ModelSub, H, model, grid ws) of its last LSTM forecast
         self._pre: dict = {}       # sliding group -> a forecast launched during this cycle's fetch
-        self._pre_skip: dict = {}  # sliding group -> its last early launch was not used
+        self._pre_skip: dict = {}  # sliding group -> (cycles left to skip, current back-off) after misses
         self.prelaunch_hits = 0
         self.prelaunch_misses = 0
         self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
@@ -2293,7 +2293,11 @@ class FastPath:
     def _prelaunch(self, group: tuple) -> None:
         spec = self._pre_spec.get(group)
         self._pre.pop(group, None)
-        if spec is None or self._pre_skip.pop(group, False):
+        skip = self._pre_skip.get(group)
+        if skip is not None and skip[0] > 0:          # backing off after misses
+            self._pre_skip[group] = (skip[0] - 1, skip[1])
+            return
+        if spec is None:
             return
         sub, H, lstm, ws0 = spec
         st = self.sliding
@@ -2311,9 +2315,15 @@ class FastPath:
         rm, dk, T, H0, m0, cyc, fc, sig = pre
         if rm is sub.rm and dk == int(sub.dk) and T == sub.T and H0 == H and m0 is lstm and cyc == self.cycle:
             self.prelaunch_hits += 1
+            self._pre_skip.pop(group, None)
             return fc, sig
+        # a miss: skip the next 1, 2, 4, ... 32 cycles' early launches (a group
+        # whose arrays are re-laid every cycle -- jobs resubmitted each cycle --
+        # stops paying for recurrences it cannot use)
         self.prelaunch_misses += 1
-        self._pre_skip[group] = True
+        prev = self._pre_skip.get(group)
+        back = 1 if prev is None else min(32, 2 * prev[1])
+        self._pre_skip[group] = (back, back)
         return None
 
     def _forecast(self, algo: str, lazy: "LazyHist", sub: "ModelSub", H: int):
