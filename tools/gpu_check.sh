@@ -121,6 +121,11 @@ for s in $steps; do
               python3 "$R/benchmarks/bench_configs.py" --config 4 --steps 10 --warmup 3 \
               > "$R/gpurun_out/check_prof_c4.log" 2>&1; rc=$?
           echo "prof_c4 rc=$rc"; cd "$R"; [ $rc -eq 0 ] || exit $rc ;;
+    prof60) cd /tmp && export TMPDIR=/tmp
+          timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_c3_60" -o c3 -- \
+              python3 "$R/benchmarks/bench_configs.py" --config 3e2e --source http --poll-seconds 60 --window 60 \
+              --steps 6 --warmup 2 --prom-workers 8 > "$R/gpurun_out/check_prof_c3_60.log" 2>&1; rc=$?
+          echo "prof_c3_60 rc=$rc"; cd "$R"; [ $rc -eq 0 ] || exit $rc ;;
     prof) cd /tmp && export TMPDIR=/tmp
           timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_headline" -o headline -- \
               python3 "$R/bench.py" --steps 50 --warmup 10 > "$R/gpurun_out/check_prof_headline.log" 2>&1; rc=$?
