@@ -36,9 +36,8 @@ for s in $steps; do
           run lstm_tests 400 python -u -m pytest tests/test_model_ops.py -m gpu -k "lstm" -v --timeout 120 \
               --timeout-method thread || exit $rc
           run lstm_ab 200 python -u tools/lstm_ab.py || exit $rc
-          run lstm_ab_c12 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_c12.so python -u tools/lstm_ab.py || exit $rc
-          run lstm_ab_c14 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_c14.so python -u tools/lstm_ab.py || exit $rc
-          run lstm_ab_r4 200 env FOREMAST_HIP_LIB=$V/libforemast_hip_r4.so python -u tools/lstm_ab.py || exit $rc
+          # (A/B builds: tools/build_native.py --variant NAME:lstm:FLAGS, then
+          #  env FOREMAST_HIP_LIB=$V/libforemast_hip_NAME.so python -u tools/lstm_ab.py)
           run config4 300 python -u benchmarks/bench_configs.py --config 4 || exit $rc
           run config4_stack 300 python -u benchmarks/bench_configs.py --config 4 --hidden 256 --layers 2 --multivariate || exit $rc ;;
     lstm5) run lstm_tests 400 python -u -m pytest tests/test_model_ops.py -m gpu -k "lstm" -v --timeout 120 \
