@@ -2477,7 +2477,10 @@ class FastPath:
                     ga.impact_slots = exp.impact_slots([w.plan.namespace for w in works],
                                                        [w.doc.app_name for w in works],
                                                        [w.plan.cluster for w in works])
-                exp.table.set(ga.impact_slots, val.astype(np.float64))
+                if gm is None:
+                    exp.table.set(ga.impact_slots, val.astype(np.float64))
+                else:                                # (a job that left exports nothing)
+                    exp.table.set(ga.impact_slots[~gm], val[~gm].astype(np.float64))
             down = val >= self.b.cfg.downstream_threshold
             if gm is not None:
                 down &= ~gm
