@@ -1,3 +1,7 @@
+// fm-hipcc-flags: -mllvm -pragma-unroll-threshold=1000000
+// (the 1024-sample pairwise sort, K = 16: past LLVM's default pragma-unroll
+// size limit the stage loops stayed rolled -- runtime register indexing
+// through scratch (132 B/lane) and s_set_gpr_idx; fully unrolled: 0 scratch)
 // Canary-scoring kernels (K4 pairwise rank tests, K1+K7 fused history-stats +
 // anomaly decision, service reduce, anomaly compaction, K11 synthetic fleet).
 //
