@@ -80,6 +80,12 @@ for s in $steps; do
                p.sort_stats('tottime').print_stats(70); p.sort_stats('cumtime').print_stats(90)" \
                > gpurun_out/hostprof_$c.txt || exit 1
          done ;;
+    hostprofmixed) FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_mixed.prof timeout -k 10 500 python -u \
+               benchmarks/bench_configs.py --config mixed --steps 10 --warmup 3 > gpurun_out/check_hostprof_mixed.log 2>&1; rc=$?
+           echo "hostprof mixed rc=$rc"; [ $rc -eq 0 ] || exit $rc
+           python -c "import pstats,sys; p=pstats.Stats('gpurun_out/hostprof_mixed.prof', stream=sys.stdout); \
+               p.sort_stats('tottime').print_stats(60); p.sort_stats('cumtime').print_stats(100)" \
+               > gpurun_out/hostprof_mixed.txt || exit 1 ;;
     hostprof60) FOREMAST_PROFILE_CYCLES=gpurun_out/hostprof_3e2e_http60.prof timeout -k 10 500 python -u \
                benchmarks/bench_configs.py --config 3e2e --source http --poll-seconds 60 --window 60 --steps 8 \
                --warmup 2 --prom-workers 8 > gpurun_out/check_hostprof_3e2e_http60.log 2>&1; rc=$?
