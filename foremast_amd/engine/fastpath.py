@@ -524,6 +524,7 @@ class FastPath:
         self._slide_state: dict = {}
         self._flat_rows = None     # (row map [S, M] object, flat int64 rows, slice when they are one run)
         self.new_jobs = 0          # jobs planned by the last prepare
+        self._wt_pool = None       # the window-table round's thread (fleets with sliding groups too)
         self._pre_spec: dict = {}  # sliding group -> (ModelSub, H, model, grid ws) of its last LSTM forecast
         self._pre: dict = {}       # sliding group -> a forecast launched during this cycle's fetch
         self._pre_skip: dict = {}  # sliding group -> (cycles left to skip, current back-off) after misses
@@ -807,6 +808,17 @@ class FastPath:
         else:
             for fw in todo:
                 (slide.setdefault(fw.plan.group, []) if fw.plan.sliding else rest).append(fw)
+        # a fleet with both kinds (a mixed fleet): the canary windows' batched
+        # round goes out on its own thread while this one fetches the sliding
+        # groups -- the two HTTP rounds wait on the server side by side (the
+        # native client's batches release the interpreter; its connection
+        # pool is shared under a lock), instead of one after the other
+        wt_job = None
+        if slide and self.wt.n and not getattr(self.b.sources, "local", False):
+            if self._wt_pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._wt_pool = ThreadPoolExecutor(1, thread_name_prefix="window-fetch")
+            wt_job = self._wt_pool.submit(self.wt.fetch, self.b.sources, now, pool)
         for grp in slide.values():
             self._fetch_sliding(grp, now)
         tab = [fw for fw in rest if fw.wcur is not None]
@@ -820,7 +832,8 @@ class FastPath:
         else:
             list(pool.map(lambda fw: self.fetch(fw, now), rest))
         # canary windows: one incremental, batched round over the whole table
-        self._wt_changed = self.wt.fetch(self.b.sources, now, pool) > 0 or self._wt_changed
+        got = wt_job.result() if wt_job is not None else self.wt.fetch(self.b.sources, now, pool)
+        self._wt_changed = got > 0 or self._wt_changed
         return works
 
     def _register_windows(self, fws: list[FastWork]) -> None:
