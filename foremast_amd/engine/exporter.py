@@ -526,6 +526,30 @@ class BrainExporter:
                  (self.IMPACT, namespace, app, cluster) if cluster else (self.IMPACT, namespace, app)]
         return keys
 
+    def plan_keys(self, plan) -> list:
+        """:meth:`job_keys` of a fast-path plan (base metrics, namespace, app,
+        cluster), built once per plan: binding and retiring a job reuse it."""
+        k = plan.__dict__.get("_xkeys")
+        if k is None:
+            k = plan.__dict__["_xkeys"] = self.job_keys(plan.base_metrics, plan.namespace, plan.app, plan.cluster)
+        return k
+
+    def bind_plans(self, plans) -> None:
+        keys = [k for p in plans for k in self.plan_keys(p)]
+        if keys:
+            self.table.bind_keys(keys)
+
+    def retire_plans(self, plans, now: float, ttl: float | None = None, unbind: bool = False,
+                     retire: bool = True) -> int:
+        """:meth:`retire_jobs` of fast-path plans (their cached keys)."""
+        ttl = self.series_ttl if ttl is None else ttl
+        keys = [k for p in plans for k in self.plan_keys(p)]
+        if not keys:
+            return 0
+        if unbind:
+            self.table.unbind_keys(keys)
+        return self.table.retire_keys(keys, now, ttl) if retire else 0
+
     def bind_jobs(self, jobs) -> None:
         """Jobs that keep their series' slots cached (the fast path): their
         keys are not freed while they live, whoever else retires them.

@@ -737,8 +737,7 @@ class FastPath:
             self._register_windows(reg)
         if new_fw and self.b.exporter is not None:
             # fast-path jobs cache their series' slots: bound while they live
-            self.b.exporter.bind_jobs([(fw.plan.base_metrics, fw.plan.namespace, fw.doc.app_name, fw.plan.cluster)
-                                       for fw in new_fw])
+            self.b.exporter.bind_plans([fw.plan for fw in new_fw])
         self._specs = {}
         if len(todo) == len(fast):
             todo = fast
@@ -2736,12 +2735,11 @@ class FastPath:
             self.wt.release(np.concatenate(wins))
         exp = self.b.exporter
         if exp is not None and works:
-            exp.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name, w.plan.cluster)
-                             for w in works if self.works.get(w.doc.id) is w], self.b.clock(), unbind=True)
+            # (the plans' exporter keys are built once, when the job is bound)
+            exp.retire_plans([w.plan for w in works if self.works.get(w.doc.id) is w], self.b.clock(), unbind=True)
             rest = [w for w in works if self.works.get(w.doc.id) is not w]
             if rest:                                  # no longer (or never) bound: retire only
-                exp.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name, w.plan.cluster)
-                                 for w in rest], self.b.clock())
+                exp.retire_plans([w.plan for w in rest], self.b.clock())
         for w in works:
             if self.works.get(w.doc.id) is w:
                 del self.works[w.doc.id]
@@ -2778,8 +2776,7 @@ class FastPath:
                 del self.works[fw.doc.id]
                 self._gcount_add(fw.plan.group, -1)
                 if exp is not None:                   # the per-job path looks its series up every write
-                    exp.retire_jobs([(fw.plan.base_metrics, fw.plan.namespace, fw.doc.app_name, fw.plan.cluster)],
-                                    self.b.clock(), unbind=True, retire=False)
+                    exp.retire_plans([fw.plan], self.b.clock(), unbind=True, retire=False)
         if out:
             log.warning("%d job(s) moved to the per-job path: a window answer carried two series of one %s",
                         len(out), "key value")
@@ -2809,8 +2806,7 @@ class FastPath:
                 if w.wcur is not None:
                     self.wt.release(np.concatenate([w.wcur, w.wbase]))
             if gone_w and self.b.exporter is not None:         # jobs that stopped coming (shard moved)
-                self.b.exporter.retire_jobs([(w.plan.base_metrics, w.plan.namespace, w.doc.app_name,
-                                              w.plan.cluster) for w in gone_w], self.b.clock(), unbind=True)
+                self.b.exporter.retire_plans([w.plan for w in gone_w], self.b.clock(), unbind=True)
 
 
 def poll_event(e, sleep: float = 2e-4) -> None:
