@@ -274,19 +274,21 @@ class GaugeTable:
                     dead = dead[~bound]
             if not len(dead):
                 return 0
-            fams = set()
-            for s in dead.tolist():
-                k = self.keys[s]
-                del self.index[k]
-                self.keys[s] = None
-                fl = int(self._sline[s])
-                f, ln = fl >> 32, fl & 0xFFFFFFFF
-                self._fslots[f][ln] = -1
-                self._fdead[f] += 1
-                fams.add(f)
-                self._sline[s] = -1
-                self._free.append(s)
-                self.events.append((s, None))
+            dl = dead.tolist()
+            keys, idx = self.keys, self.index
+            for s in dl:                              # the dict work is per key; the line bookkeeping is vectorised
+                del idx[keys[s]]
+                keys[s] = None
+            fl = self._sline[dead]
+            fam, ln = fl >> 32, fl & 0xFFFFFFFF
+            fams = np.unique(fam).tolist()
+            for f in fams:
+                sel = ln[fam == f]
+                self._fslots[f][sel] = -1
+                self._fdead[f] += len(sel)
+            self._sline[dead] = -1
+            self._free.extend(dl)
+            self.events.extend((s, None) for s in dl)
             self.vals[dead] = np.nan
             self.expire[dead] = np.nan
             self._nret -= len(dead)
