@@ -249,12 +249,48 @@ FM_API int fm_peer_ack_ctr(unsigned* const* dst, int n, unsigned* ctr, const uns
 }
 
 // ---------------------------------------------------------------- board copies
-// Synchronous copy between any two addresses this process can name (host
-// memory, its own device memory, a peer's memory opened through IPC): the
-// brain's rank-to-rank board (parallel/board.py) moves gauge vectors and
-// verdict rows with the DMA engines over xGMI, one host-blocking copy each,
-// so a seqlock header written after the payload is only seen once the
-// payload has landed.
+// Copy between any two addresses this process can name (host memory, its own
+// device memory, a peer's memory opened through IPC): the brain's
+// rank-to-rank board (parallel/board.py) moves gauge vectors and verdict rows
+// with the DMA engines over xGMI.  Every copy goes on the board's OWN
+// non-blocking stream (one per device, created on first use) and the host
+// waits for that stream only: a board copy never queues behind, or holds up,
+// work on the null / default stream (an early-launched LSTM forecast, the
+// scoring graph), and a seqlock header written after the payload is only
+// issued once the payload has landed.
+#include <mutex>
+
+namespace {
+constexpr int kMaxDevices = 64;
+hipStream_t g_board_stream[kMaxDevices] = {};
+std::mutex g_board_mu;
+
+hipError_t board_stream(hipStream_t* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> g(g_board_mu);
+  if (g_board_stream[dev] == nullptr) {
+    e = hipStreamCreateWithFlags(&g_board_stream[dev], hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+  }
+  *out = g_board_stream[dev];
+  return hipSuccess;
+}
+}  // namespace
+
+FM_API int fm_board_copy(void* dst, const void* src, int64_t bytes) {
+  if (bytes <= 0) return 0;
+  hipStream_t s = nullptr;
+  hipError_t e = board_stream(&s);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, s);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipStreamSynchronize(s);
+}
+
+// Null-stream form (kept for the A/B in tools/peer_bench.py).
 FM_API int fm_memcpy_sync(void* dst, const void* src, int64_t bytes) {
   if (bytes <= 0) return 0;
   return (int)hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault);

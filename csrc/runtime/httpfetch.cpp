@@ -74,6 +74,17 @@ struct Client {
     std::lock_guard<std::mutex> g(mu);
     idle.push_back(fd);
   }
+  // One pooled socket turned out stale (the server or a proxy dropped its
+  // idle connections between cycles): the rest of the pool is from the same
+  // idle period, so close it all instead of finding out one request at a time.
+  void drop_idle() {
+    std::vector<int> v;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      v.swap(idle);
+    }
+    for (int fd : v) ::close(fd);
+  }
   int connect_new() {
     int fd = ::socket(addr.ss_family, SOCK_STREAM | SOCK_CLOEXEC, 0);
     if (fd < 0) return -1;
@@ -126,8 +137,10 @@ bool ieq_prefix(const char* a, const char* e, const char* lit) {
 }
 
 // One response off `fd` into r (body in `body`).  Returns 0 ok, 1 the peer
-// closed before sending anything (a stale keep-alive socket: retry on a new
-// one), -1 transport error, -2 malformed.  keep = the connection may be reused.
+// closed (or reset) the connection before sending anything (a stale
+// keep-alive socket: retry on a new one), -1 transport error -- a receive
+// timeout included: a server that is slow to answer is not re-sent the
+// request --, -2 malformed.  keep = the connection may be reused.
 int read_response(int fd, std::string& buf, std::string& body, Result& r, bool& keep, double t_sent) {
   buf.clear();
   body.clear();
@@ -140,7 +153,10 @@ int read_response(int fd, std::string& buf, std::string& body, Result& r, bool& 
     ssize_t k = ::recv(fd, tmp, sizeof(tmp), 0);
     if (k < 0 && errno == EINTR) continue;
     if (k == 0) return buf.empty() ? 1 : -2;
-    if (k < 0) return buf.empty() ? 1 : -1;
+    if (k < 0) {
+      const bool reset = errno == ECONNRESET || errno == EPIPE || errno == ENOTCONN;
+      return buf.empty() && reset ? 1 : -1;
+    }
     if (first) {
       t_first = now_s();
       first = false;
@@ -348,7 +364,9 @@ FM_API void* fm_http_batch(void* client, const char* host_hdr, const char* strs,
       bool keep = false;
       for (int attempt = 0; attempt < 2 && rc == 1; ++attempt) {
         bool fresh = false;
-        if (fd < 0) fd = c->take();
+        // the retry always opens a new connection: another pooled socket
+        // from the same idle period would most likely be stale as well
+        if (fd < 0 && attempt == 0) fd = c->take();
         if (fd < 0) {
           fd = c->connect_new();
           fresh = true;
@@ -365,15 +383,22 @@ FM_API void* fm_http_batch(void* client, const char* host_hdr, const char* strs,
           fd = -1;
           rc = fresh ? -1 : 1;  // a stale keep-alive socket: one retry on a new connection
           if (rc == -1) r.err = std::string("send: ") + std::strerror(errno);
+          else c->drop_idle();
           continue;
         }
         rc = read_response(fd, buf, body, r, keep, t_sent);
+        const int rerr = errno;
         if (rc != 0) {
           ::close(fd);
           fd = -1;
           if (rc == 1 && fresh) {
             rc = -1;
             r.err = "connection closed by the server";
+          } else if (rc == 1) {
+            c->drop_idle();
+          } else if (rc == -1) {
+            r.err = rerr == EAGAIN || rerr == EWOULDBLOCK ? std::string("receive timeout")
+                                                          : std::string("recv: ") + std::strerror(rerr);
           }
         }
       }

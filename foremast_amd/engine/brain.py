@@ -886,6 +886,14 @@ class Brain:
             self._hist_dev: dict = {}
             from concurrent.futures import ThreadPoolExecutor
             self._hist_writer = ThreadPoolExecutor(1, thread_name_prefix="history-ckpt")
+            # once, process-wide, when the brain first runs a background
+            # writer: the writer's Python hands the interpreter back within
+            # 0.1 ms whenever the loop asks for it (the default 5-ms switch
+            # interval let a background save stretch the loop's cycles).  Set
+            # here, not per save: the interval is process state, and a
+            # per-save set/restore from the writer thread raced other users
+            import sys
+            sys.setswitchinterval(min(sys.getswitchinterval(), 1e-4))
         # in the cycle: the row lists, a gather launch and an async host copy;
         # the per-row key / owner lists, meta and file on the writer thread,
         # which makes no device call (it polls the copy's event through
@@ -899,24 +907,14 @@ class Brain:
         rank, world = self.info.rank, self.info.world
 
         def write():
-            # the writer's Python hands the interpreter back within 0.1 ms
-            # whenever the brain loop asks for it (the default 5-ms switch
-            # interval let a background save stretch the loop's cycles); file
-            # writes release it anyway
-            import sys
-            iv = sys.getswitchinterval()
-            sys.setswitchinterval(min(iv, 1e-4))
-            try:
-                torch.cuda.set_device(dev)
-                while not hs.ready():
-                    if hs.stalled():             # nobody is pumping: the loop is idle or gone
-                        hs.pump(None)
-                    time.sleep(2e-3)
-                t, meta = hs.state()
-                meta.update(rank=rank, world=world)
-                return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
-            finally:
-                sys.setswitchinterval(iv)
+            torch.cuda.set_device(dev)
+            while not hs.ready():
+                if hs.stalled():             # nobody is pumping: the loop is idle or gone
+                    hs.pump(None)
+                time.sleep(2e-3)
+            t, meta = hs.state()
+            meta.update(rank=rank, world=world)
+            return checkpoint.save(dirpath, t, meta, tag=tag, keep=2, kind="history")
         self._hist_future = self._hist_writer.submit(write)
         return self._hist_future
 

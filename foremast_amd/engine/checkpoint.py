@@ -80,7 +80,8 @@ def write_safetensors(path, tensors: dict[str, torch.Tensor], metadata: dict[str
         f.write(hb)
         for t in bufs:
             if t.numel():
-                raw = t.view(torch.uint8).reshape(-1).numpy() if t.dtype != torch.bool else t.numpy().view(np.uint8)
+                raw = (t.reshape(-1).view(torch.uint8).numpy() if t.dtype != torch.bool
+                       else t.reshape(-1).numpy().view(np.uint8))
                 mv = memoryview(raw)
                 for i in range(0, len(mv), 64 << 20):     # 64 MB writes
                     f.write(mv[i:i + (64 << 20)])

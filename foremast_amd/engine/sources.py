@@ -120,6 +120,20 @@ def parse_wavefront(body: bytes | str) -> list[Series]:
     return out
 
 
+def _native_ok(u) -> bool:
+    """The native client speaks plain HTTP/1.1 straight to the host: a URL
+    with credentials (``user:pass@host`` -> basic auth) or a host the proxy
+    environment applies to (what httpx honours with ``trust_env``) keeps the
+    httpx client, which handles both."""
+    import urllib.request
+    if u.username is not None or u.password is not None:
+        return False
+    px = urllib.request.getproxies_environment()
+    if ("http" in px or "all" in px) and not urllib.request.proxy_bypass_environment(u.hostname or "", px):
+        return False
+    return True
+
+
 class PrometheusSource:
     """``query_range`` over HTTP.
 
@@ -208,9 +222,11 @@ class PrometheusSource:
             from . import native_rt
             u = urllib.parse.urlsplit(base)
             cl = None
-            if self.native and u.scheme == "http" and u.hostname:
+            if self.native and u.scheme == "http" and u.hostname and _native_ok(u):
                 cl = native_rt.HttpClient.create(u.hostname, u.port or 80, self.timeout)
-            got = self._native[base] = (cl, u.netloc, u.path or "/") if cl is not None else False
+            h = f"[{u.hostname}]" if ":" in (u.hostname or "") else (u.hostname or "")
+            host = h + (f":{u.port}" if u.port else "")
+            got = self._native[base] = (cl, host, u.path or "/") if cl is not None else False
         return got or None
 
     def fetch_keyed(self, queries: list, pool=None) -> list:

@@ -117,6 +117,7 @@ _SIGS: dict[str, list] = {
     "fm_hist_stats_rm": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_void_p, c_void_p],
     "fm_copy_d2h_async": [c_void_p, c_void_p, c_i64, c_void_p],
     "fm_memcpy_sync": [c_void_p, c_void_p, c_i64],
+    "fm_board_copy": [c_void_p, c_void_p, c_i64],
     "fm_rolling_stats": [c_void_p, c_i64, c_int, c_i64, c_int, c_int, c_void_p, c_void_p, c_i64, c_void_p],
     "fm_pvalues_range": [c_void_p, c_i64, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "fm_lstm_stack": [c_void_p, c_i64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

@@ -66,6 +66,59 @@ def barrier() -> None:
         dist.barrier()
 
 
+def collective_device(device=None, group=None) -> torch.device:
+    """The device a tensor collective on ``group`` must use: an RCCL
+    (``nccl``) group only moves device tensors (torch's backend capability
+    table: ``nccl -> ['cuda']``), gloo moves host tensors.  ``device`` is
+    the rank's GPU; without one the current HIP device is used."""
+    backend = dist.get_backend(group) if is_dist() else "gloo"
+    if "nccl" in str(backend).lower():
+        if device is not None and torch.device(device).type == "cuda":
+            return torch.device(device)
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+_agree_n = [0]
+
+
+def agree_all(ok: bool, tag: str = "fm/agree", timeout_s: float | None = None) -> bool:
+    """Collective yes/no: True on every rank iff ``ok`` on every rank.
+
+    It goes through the process group's key-value store (the TCPStore the
+    world rendezvoused on), not a tensor collective, so it is the same on an
+    RCCL and a gloo world, never touches a HIP stream, and still works after
+    a rank's device is in an error state (a failed IPC open) -- the cases in
+    which a start-up self-test has to reach a verdict.  Every rank must call
+    it the same number of times (like any collective); a rank that never
+    arrives makes the others raise after ``timeout_s`` (the store's timeout by
+    default) instead of hanging."""
+    if not is_dist():
+        return bool(ok)
+    from datetime import timedelta
+    from torch.distributed import distributed_c10d as c10d
+    st = c10d._get_default_store()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = _agree_n[0]
+    _agree_n[0] += 1
+    base = f"{tag}/{n}"
+    st.set(f"{base}/{rank}", b"1" if ok else b"0")
+    keys = [f"{base}/{r}" for r in range(world)]
+    if timeout_s is None:
+        st.wait(keys)
+    else:
+        st.wait(keys, timedelta(seconds=timeout_s))
+    res = all(st.get(k) == b"1" for k in keys)
+    # the last reader removes the round's keys (a long-lived store keeps none)
+    if st.add(f"{base}/read", 1) == world:
+        for k in keys + [f"{base}/read"]:
+            try:
+                st.delete_key(k)
+            except (AttributeError, RuntimeError, NotImplementedError):
+                break
+    return res
+
+
 def shard_range(total: int, rank: int, world: int) -> tuple[int, int, int]:
     """Contiguous block sharding with equal padded shard size.
     Returns (start, count_here, padded_count)."""
@@ -112,10 +165,10 @@ def all_gather_varlen(local: torch.Tensor, group=None) -> list[torch.Tensor]:
     return [out[i * mx: i * mx + counts[i]] for i in range(world)]
 
 
-def all_reduce_max(x: float, device: torch.device) -> float:
+def all_reduce_max(x: float, device: torch.device | None = None) -> float:
     if not is_dist():
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=collective_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

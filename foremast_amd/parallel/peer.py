@@ -42,6 +42,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops._lib import LIB, stream_of
+from .dist import agree_all, collective_device
 
 import os
 
@@ -252,17 +253,16 @@ def selftest_captured(pub: PeerPublisher, steps: int = 64, report: dict | None =
         torch.cuda.synchronize(dev)
     bad = sum(0 if pub.step_ok(s) else 1 for s in range(pub.depth))
     ok = bad == 0 and int(pub.ctr.item()) == steps
-    xs = x if dist.get_backend() == "nccl" else x.cpu()
+    xs = x.to(collective_device(dev))
     ref = [torch.empty_like(xs) for _ in range(pub.world)]
     dist.all_gather(ref, xs)
     if pub.rank == 0:
         ok = ok and torch.equal(hosts[(steps - 1) % pub.depth], torch.cat(ref).cpu())
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    if report is not None and not bool(flag.item()):
+    ok = agree_all(ok, tag="fm/peer/agree")
+    if report is not None and not ok:
         report.update(captured=pub.describe())
     pub.reset()
-    return bool(flag.item())
+    return ok
 
 
 def selftest(pub: PeerPublisher, steps: int = 8, report: dict | None = None) -> bool:
@@ -272,13 +272,12 @@ def selftest(pub: PeerPublisher, steps: int = 8, report: dict | None = None) -> 
     the test on every rank (``report`` gets the step and the status words)."""
     dev = pub.dev
     host = torch.empty((pub.world * pub.shard, 4), dtype=torch.float32, pin_memory=True)
-    flag_dev = dev if dist.get_backend() == "nccl" else "cpu"
     for k in range(steps):
         slot = k % pub.depth
         x = (torch.arange(pub.shard * 4, device=dev, dtype=torch.float32).reshape(pub.shard, 4)
              + 1000.0 * pub.rank + 0.5 * k)
         pub.publish(slot, k, x)
-        xs = x if dist.get_backend() == "nccl" else x.cpu()
+        xs = x.to(collective_device(dev))
         ref = [torch.empty_like(xs) for _ in range(pub.world)]
         dist.all_gather(ref, xs)
         ok = True
@@ -289,9 +288,7 @@ def selftest(pub: PeerPublisher, steps: int = 8, report: dict | None = None) -> 
         torch.cuda.synchronize(dev)
         st = pub.status.cpu()
         ok = ok and not bool(st[0]) and not bool(st[1])
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=flag_dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if not bool(flag.item()):
+        if not agree_all(ok, tag="fm/peer/agree"):
             if report is not None:
                 report.update(step=k, status=st.tolist(), data_ok=ok)
             return False

@@ -641,11 +641,19 @@ class SQLiteStore(JobStore):
                       "last_bid integer not null)")
             old = {r[0] for r in main.execute("select name from sqlite_master where type='table'")} & \
                 set(self._LOG_TABLES)
-            for t in self._LOG_TABLES:          # an earlier layout's tables: moved once
-                if t in old:
+            # an earlier layout's tables are moved once: the copy and its
+            # "done" marker commit together in this file, so a crash before
+            # the old tables are dropped below never copies them twice (the
+            # next start sees the marker and only finishes the drop)
+            c.execute("create table if not exists log_meta (k text primary key, v text)")
+            moved = c.execute("select v from log_meta where k='moved_from_jobs_file'").fetchone() is not None
+            for t in self._LOG_TABLES:
+                if t in old and not moved:
                     rows = main.execute(f"select * from {t}").fetchall()
                     if rows:
-                        c.executemany(f"insert into {t} values ({','.join('?' * len(rows[0]))})", rows)
+                        c.executemany(f"insert or ignore into {t} values ({','.join('?' * len(rows[0]))})", rows)
+            if old:
+                c.execute("insert or replace into log_meta values ('moved_from_jobs_file', '1')")
             if (c.execute("select 1 from hpalog_batches limit 1").fetchone() is not None
                     and c.execute("select 1 from hpalog_jobs limit 1").fetchone() is None):
                 rng: dict = {}                    # a store written before the index: built once

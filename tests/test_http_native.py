@@ -200,6 +200,36 @@ def test_native_client_chunked_close_and_stale_keepalive():
     s.close()
 
 
+def test_native_client_survives_server_dropping_every_idle_connection():
+    """the server (or a proxy) closes ALL kept-alive connections
+    during the ~60 s between cycles.  The retry must open a new connection
+    instead of taking the next (equally stale) pooled socket, so no request
+    of the next batch fails."""
+    body = json.dumps({"status": "success", "data": {"resultType": "matrix", "result": [
+        {"metric": {"pod": "a"}, "values": [[1, "1.5"]]}]}}).encode()
+    conns = []
+
+    def handler(c):
+        if c not in conns:
+            conns.append(c)
+        c.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body))
+        return True
+    s = _raw_server(handler)
+    port = s.getsockname()[1]
+    cl = native_rt.HttpClient.create("127.0.0.1", port)
+    args = (f"127.0.0.1:{port}", "/api/v1/query_range")
+    got, _, _ = cl.batch(*args, ["m"] * 8, [""] * 8, ["pod"] * 8, 4)      # pools up to 4 sockets
+    assert all(isinstance(g, native_rt.Keyed) for g in got)
+    for c in list(conns):                                                 # the idle period ends them all
+        c.shutdown(socket.SHUT_RDWR)
+        c.close()
+    conns.clear()
+    for nconn in (1, 4):
+        got, _, _ = cl.batch(*args, ["m"] * 8, [""] * 8, ["pod"] * 8, nconn)
+        assert all(isinstance(g, native_rt.Keyed) for g in got), got
+    s.close()
+
+
 def test_native_client_transport_errors():
     """A refused connection and a non-200 answer come back per request."""
     s = socket.socket()
@@ -385,3 +415,20 @@ def test_fetch_columns_split_subsets_of_one_root(server):
         np.testing.assert_array_equal(got.v, want.v)
         assert got.off[-1] > 0
     assert len(src._tpl) == parsed
+
+
+def test_native_client_only_where_it_can_speak_for_httpx(monkeypatch):
+    """credentials in the URL or an applicable proxy keep the httpx
+    client (basic auth / trust_env); the Host header never carries userinfo."""
+    for k in ("http_proxy", "HTTP_PROXY", "all_proxy", "ALL_PROXY", "no_proxy", "NO_PROXY"):
+        monkeypatch.delenv(k, raising=False)
+    src = PrometheusSource(workers=2)
+    got = src._client_of("http://127.0.0.1:9090/api/v1/query_range")
+    assert got is not None and got[1] == "127.0.0.1:9090" and got[2] == "/api/v1/query_range"
+    assert src._client_of("http://user:pw@127.0.0.1:9090/api/v1/query_range") is None
+    monkeypatch.setenv("HTTP_PROXY", "http://proxy.local:3128")
+    src = PrometheusSource(workers=2)
+    assert src._client_of("http://127.0.0.1:9091/api/v1/query_range") is None
+    monkeypatch.setenv("NO_PROXY", "127.0.0.1")
+    src = PrometheusSource(workers=2)
+    assert src._client_of("http://127.0.0.1:9092/api/v1/query_range") is not None

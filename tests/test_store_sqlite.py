@@ -124,6 +124,46 @@ def test_migrates_round2_layout(tmp_path):
     assert len(st.claim_batch("w", 10, 90.0, now=T0)) == 3
 
 
+def test_hpalog_move_survives_a_crash_before_the_drop(tmp_path):
+    """the HPA-log tables of the jobs file are moved into the
+    -hpalogs file once.  A crash after the copy committed but before the old
+    tables were dropped must not copy them again (primary-key collision ->
+    the store no longer opens) nor duplicate entries."""
+    src = str(tmp_path / "src.db")
+    st = SQLiteStore(src)
+    st.add_hpalogs([HPALog(job_id=f"a:ns:hpa{j}", timestamp=T0 + j, log=HPALogBody(50 + j, "x", []))
+                    for j in range(4)])
+    want = [l.timestamp for l in st.hpalogs("a:ns:hpa1", 10)]
+    cnt = lambda c: tuple(c.execute(f"select count(*) from {t}").fetchone()[0]       # noqa: E731
+                          for t in SQLiteStore._LOG_TABLES)
+    n_batches = cnt(st._lconn())
+    assert sum(n_batches) >= 4
+    # the earlier layout: the log tables in the jobs file, no -hpalogs file yet
+    path = str(tmp_path / "j.db")
+    main = sqlite3.connect(path)
+    main.execute("attach database ? as lg", (src + "-hpalogs",))
+    for t in SQLiteStore._LOG_TABLES:
+        main.execute(f"create table main.{t} as select * from lg.{t}")
+    main.commit()
+    main.execute("detach database lg")
+    main.close()
+    # a first open moves them (copy + marker committed, then the drop) ...
+    st2 = SQLiteStore(path)
+    assert cnt(st2._lconn()) == n_batches
+    # ... and a "crash before the drop": the old tables are back in the jobs file
+    main = sqlite3.connect(path)
+    main.execute("attach database ? as lg", (path + "-hpalogs",))
+    for t in SQLiteStore._LOG_TABLES:
+        main.execute(f"create table main.{t} as select * from lg.{t}")
+    main.commit()
+    main.close()
+    st3 = SQLiteStore(path)                       # must open, no duplicates, old tables gone
+    assert cnt(st3._lconn()) == n_batches
+    assert [l.timestamp for l in st3.hpalogs("a:ns:hpa1", 10)] == want
+    tabs = {r[0] for r in st3._conn().execute("select name from sqlite_master where type='table'")}
+    assert not tabs & set(SQLiteStore._LOG_TABLES)
+
+
 def _proc_claimer(path, worker, cycles, out, go):
     st = SQLiteStore(path)
     go.wait(120)                                     # both claim concurrently

@@ -214,7 +214,7 @@ def test_gpu_async_history_save_is_off_the_cycle(tmp_path):
 def test_write_safetensors_reads_back_with_safetensors(tmp_path):
     """checkpoint.write_safetensors (plain GIL-releasing writes) produces what
     safetensors itself reads: every dtype the checkpoints use, an empty
-    tensor, the metadata; the chunked meta JSON equals json.dumps."""
+    tensor, 0-dim scalars, the metadata; the chunked meta JSON equals json.dumps."""
     import json
     import torch
     from safetensors import safe_open
@@ -223,7 +223,8 @@ def test_write_safetensors_reads_back_with_safetensors(tmp_path):
     g = torch.Generator().manual_seed(0)
     ts = {"a.values": torch.randn(37, 11, generator=g), "b": torch.randn(5, generator=g).to(torch.bfloat16),
           "c": torch.arange(9, dtype=torch.int64), "d": torch.tensor([True, False, True]),
-          "e": torch.zeros(0, 4), "f": torch.arange(7, dtype=torch.int8), "g": torch.randn(3, 2, dtype=torch.float64)}
+          "e": torch.zeros(0, 4), "f": torch.arange(7, dtype=torch.int8), "g": torch.randn(3, 2, dtype=torch.float64),
+          "h": torch.tensor(2.5), "i": torch.tensor(7, dtype=torch.int64)}         # 0-dim
     meta = {"format": "x", "meta": CK._json_chunked({"k": [[i, "a"] for i in range(10000)], "s": 1.5}, chunk=999)}
     p = tmp_path / "t.safetensors"
     CK.write_safetensors(p, ts, meta)
