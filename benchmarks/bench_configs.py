@@ -461,7 +461,7 @@ def config3e2e(args):
 
     churn = {"next": S, "new": 0, "resub": 0}
     churn_client = None
-    if kind == "mixed" and info.is_main:
+    if (kind == "mixed" or args.arrivals > 0 or args.resubmit > 0) and info.is_main:
         def _do(method, url, body):                # the service's create handler, into the shared store
             req = ApplicationHealthAnalyzeRequest.from_dict(_json.loads(body))
             jid, _ = store.create(J.build_document(req))
@@ -475,7 +475,20 @@ def config3e2e(args):
         t["now"] += poll
         if cw is not None:
             cw.set(t["now"])
-        if churn_client is not None:
+        if churn_client is not None and kind != "mixed":
+            # single-class fleet churn: --arrivals new jobs (new
+            # services) and --resubmit re-armed jobs (same id) every cycle
+            st_, _, _, a0, n_ = classes[0]
+            for _ in range(int(round(args.arrivals * n_))):
+                submit_one(churn_client, 0, churn["next"])
+                churn["next"] += 1
+                churn["new"] += 1
+            k = int(round(args.resubmit * n_))
+            base_j = a0 + (len(cyc_ms) * k) % max(1, n_)
+            for j in range(base_j, min(a0 + n_, base_j + k)):
+                submit_one(churn_client, 0, j)
+                churn["resub"] += 1
+        elif churn_client is not None:
             # mixed fleet churn, every cycle: new rolling-update canaries (0.5 %
             # of the canary class) and resubmitted HPA jobs (0.5 %: a template
             # change); the monitored class churns through its mid-run faults
@@ -739,7 +752,10 @@ def config3e2e(args):
             {"services": S, "metrics": M, "strategy": strategy, "algorithm": algo, "poll_seconds": poll,
              "classes": [{"strategy": st_, "model": al_, "jobs": n_, "metrics": len(als)}
                          for st_, al_, als, _, n_ in classes],
-             "churn": dict(new_canaries=churn["new"], hpa_resubmissions=churn["resub"]) if kind == "mixed" else None,
+             "churn": (dict(new_canaries=churn["new"], hpa_resubmissions=churn["resub"]) if kind == "mixed" else
+                       dict(arrivals_per_cycle=int(round(args.arrivals * S)), resubmissions_per_cycle=int(round(
+                           args.resubmit * S)), new_jobs=churn["new"], resubmissions=churn["resub"])
+                       if (args.arrivals or args.resubmit) else None),
              "mixed_class": args.mixed_class if kind == "mixed" and args.mixed_class >= 0 else None,
              "hpa_log_interval_s": args.hpa_log_interval if any(c[0] == "hpa" for c in classes) else None,
              "band_threshold_min": args.band_threshold if sliding_any else None,
@@ -905,6 +921,10 @@ def main():
                     "instead of the native responder")
     ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "
                     "body every N seconds in a thread while the cycles are timed (0: off)")
+    ap.add_argument("--arrivals", type=float, default=0.0, help="e2e single-class configs: fraction of --services "
+                    "submitted as NEW jobs (new services) every timed cycle")
+    ap.add_argument("--resubmit", type=float, default=0.0, help="e2e single-class configs: fraction of --services "
+                    "resubmitted (same job id, re-armed) every timed cycle")
     ap.add_argument("--cached", action="store_true", help="config 2: continuous-monitoring steady state through "
                     "the fitted-model cache")
     argv = sys.argv[1:]

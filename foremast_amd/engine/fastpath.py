@@ -212,6 +212,7 @@ class ModelArrays:
     subs: list
     lastk: torch.Tensor                        # [R] newest finite current point of each row
     inc: tuple | None = None                   # sliding groups: state of the shift-only update
+    base_rows: int = 0                         # rows carried over from the arrays of a list that then gained jobs
 
 
 @dataclass
@@ -408,6 +409,14 @@ class JobIds:
         m = self.match_in(old)
         return m[0] if m is not None and m[2] == len(self.arr) else None
 
+    def extends(self, old: "JobIds") -> int | None:
+        """len(old) when this list is ``old`` followed by new jobs (arrivals
+        appended to a laid-out list), else None."""
+        n = len(old.arr)
+        if 0 < n < len(self.arr) and np.array_equal(self.arr[:n], old.arr):
+            return n
+        return None
+
     def match_in(self, old: "JobIds"):
         """(positions in ``old``, found mask, number found) of this list's
         jobs; a position where the mask is False is arbitrary.  None when
@@ -530,8 +539,13 @@ class FastPath:
         self._pre_skip: dict = {}  # sliding group -> (cycles left to skip, current back-off) after misses
         self.prelaunch_hits = 0
         self.prelaunch_misses = 0
+        self.prelaunch_extended = 0   # early forecasts used for a list's first rows after arrivals
         self.model_slides = 0      # ModelArrays moved by a sliding step instead of rebuilt
         self.model_churns = 0      # ModelArrays restricted to a churned job list instead of rebuilt
+        self.resubmits_patched = 0  # resubmissions that kept their FastWork (unchanged plan)
+        self.arrivals_laid = 0     # new jobs appended to a laid-out list (instead of a fresh layout)
+        self.revived = 0           # re-armed jobs that took their ghost slot back
+        self.extends = 0           # per-list memos extended by appended jobs (instead of rebuilt)
         self._hist_pending = False  # a per-job fetch left history in some FastWork.hist this cycle
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
         self._keys: dict = {}     # (group, algo) -> (job ids, positions, model-cache keys)
@@ -674,9 +688,15 @@ class FastPath:
             return fast, []
         self._reused = False
         works = self.works
+        # resubmissions that changed nothing the plan reads (an HPA template
+        # toggle, a continuous monitor re-armed: HpaController.go:204-229,
+        # Barrelman.go:552-565) keep their FastWork -- its list position, row
+        # map, templates, memos and exporter series -- with the new document
+        fws = list(map(works.get, batch.ids))
+        if self._patch_resubmitted(batch, fws, now):
+            fws = list(map(works.get, batch.ids))
         # every job known at its version (the steady state of a fleet that only
         # lost jobs since the last claim): the lists through C-level passes
-        fws = list(map(works.get, batch.ids))
         if None not in fws and list(map(_version_of, fws)) == list(batch.versions):
             if len(self._gcount) == 1 and fws and fws[0].plan.sliding:
                 # one sliding group: every job is due every cycle -- on the
@@ -693,6 +713,7 @@ class FastPath:
             self.todo = todo
             self._last = (batch.ids, batch.versions, fws, todo)
             return fws, []
+        lay_prev, ghost_prev = self._lay, self.ghost     # (kept for arrivals appended to it)
         self._set_layout(None)
         fast, unknown, todo = [], [], []
         handles = getattr(batch, "handles", None)
@@ -707,11 +728,31 @@ class FastPath:
         rest = []
         reg: list[FastWork] = []
         new_fw: list[FastWork] = []
+        revived: list[FastWork] = []
         if unknown:
             docs = batch.docs(unknown)
             self._prefill_specs(docs)
+            # jobs that closed but are still laid out as ghosts: a re-armed job
+            # (continuous monitoring after Unhealthy, Barrelman.go:552-565;
+            # MonitorController.go:146-155) with the plan it had takes its
+            # ghost back -- same position, rows and memos
+            ghosts = {}
+            if lay_prev is not None:
+                L0 = lay_prev[0]
+                # the layout's jobs that left (ghosts, and jobs of this claim
+                # not known any more), by plan: a re-armed job has a new id
+                # (the job id hashes the request, stringutils.go:11-17) but
+                # the plan of the job it replaces
+                gp = np.zeros(len(L0), bool) if ghost_prev is None or len(ghost_prev) != len(L0) else ghost_prev
+                gone = [j for j, fw in enumerate(L0) if gp[j] or works.get(fw.doc.id) is not fw]
+                ghosts = {self._plan_sig(L0[j].doc): L0[j] for j in gone}
             for k, d in zip(unknown, docs):
                 old = works.get(d.id)
+                gw = ghosts.pop(self._plan_sig(d), None) if ghosts and old is None else None
+                if gw is not None and works.get(gw.doc.id) is not gw and self._revive(
+                        gw, d, batch.versions[k], None if handles is None else int(handles[k]), now):
+                    revived.append(gw)
+                    continue
                 if old is not None:              # resubmitted under the same id (dropped, unbound)
                     self._release([old])
                 p = self._make_plan(d, batch.versions[k])
@@ -730,8 +771,9 @@ class FastPath:
                 if not p.sliding:
                     reg.append(fw)
                 self._gcount_add(p.group, 1)
-                fast.append(fw)
-                todo.append(fw)
+        # claim order: the known jobs, the revived ghosts, the new jobs
+        fast += revived + new_fw
+        todo += revived + new_fw
         self.new_jobs = len(new_fw)
         if reg:
             self._register_windows(reg)
@@ -742,10 +784,120 @@ class FastPath:
         if len(todo) == len(fast):
             todo = fast
         if len(self._gcount) == 1 and fast and fast[0].plan.sliding and todo is fast and not rest:
-            self._set_layout(fast)
+            fast = todo = self._layout_arrivals(fast, len(fast) - len(new_fw), lay_prev)
         self.todo = todo
         self._last = (batch.ids, batch.versions, fast, todo) if not rest else None
         return fast, rest
+
+    # a resubmitted document that differs from the planned one only in these
+    # fields keeps its plan (they are read per cycle from the FastWork / doc)
+    _PLAN_FIELDS = ("app_name", "namespace", "strategy", "current_config", "baseline_config", "historical_config",
+                    "current_metric_store", "baseline_metric_store", "historical_metric_store", "hpa_metrics")
+
+    def _patch_resubmitted(self, batch, fws: list, now: float) -> int:
+        """Known jobs claimed at a new version whose new document plans the
+        same (same queries, stores, strategy and HPA template: a resubmission
+        re-arms the job): the FastWork takes the new document, version, end
+        time and store row in place, so the job list -- and everything kept
+        per list -- is unchanged.  Returns how many were patched."""
+        vers = batch.versions
+        cand = [k for k, fw in enumerate(fws) if fw is not None and fw.version != vers[k]]
+        if not cand:
+            return 0
+        docs = batch.docs(cand)
+        handles = getattr(batch, "handles", None)
+        patched = []
+        for k, d in zip(cand, docs):
+            fw = fws[k]
+            od = fw.doc
+            if d.id != od.id or any(getattr(d, f) != getattr(od, f) for f in self._PLAN_FIELDS):
+                continue
+            try:
+                end_ts = parse_rfc3339(d.end_time).timestamp() if d.end_time else now
+            except ValueError:
+                end_ts = now
+            if fw.wcur is not None and any(bool(self.wt.live[x]) for x in fw.wcur if x >= 0):
+                end_ts += self.wt.settle       # as _register_windows: a live window's last point settles
+            fw.doc, fw.version, fw.end_ts = d, vers[k], end_ts
+            if handles is not None:
+                fw.handle = int(handles[k])
+            fw.failed, fw.errors = "", []
+            patched.append(fw)
+        if patched:
+            self.resubmits_patched += len(patched)
+            self._patch_static_cols(patched)
+        return len(patched)
+
+    def _plan_sig(self, d: Document) -> tuple:
+        return tuple(getattr(d, f) if f != "hpa_metrics" else tuple(sorted((k, str(v)) for k, v in d.hpa_metrics.items()))
+                     for f in self._PLAN_FIELDS)
+
+    def _revive(self, fw: FastWork, d: Document, version, handle, now: float) -> bool:
+        """A ghost of the laid-out list whose job came back (re-armed under
+        its id) with the plan it had: back into ``works`` with the new
+        document; its exporter series are bound again and re-resolved (their
+        slots may have been swept while the job was closed)."""
+        od = fw.doc
+        if any(getattr(d, f) != getattr(od, f) for f in self._PLAN_FIELDS) or d.id in self.evicted:
+            return False
+        try:
+            end_ts = parse_rfc3339(d.end_time).timestamp() if d.end_time else now
+        except ValueError:
+            end_ts = now
+        fw.doc, fw.version, fw.end_ts, fw.handle = d, version, end_ts, handle
+        fw.failed, fw.errors = "", []
+        self.works[d.id] = fw
+        self._gcount_add(fw.plan.group, 1)
+        exp = self.b.exporter
+        if exp is not None:
+            exp.bind_plans([fw.plan])
+            fw.plan.export_slots = None
+            fw.plan.hpa_slots = None
+        self._patch_static_cols([fw], revived=True)
+        self.revived += 1
+        return True
+
+    def _patch_static_cols(self, fws: list, revived: bool = False) -> None:
+        """End times / store rows of patched jobs into every group memo that
+        holds them (the memo's arrays are the group arrays' own)."""
+        ser = np.fromiter(map(_serial_of, fws), np.int64, len(fws))
+        end = np.fromiter((fw.end_ts for fw in fws), np.float64, len(fws))
+        hd = [fw.handle for fw in fws]
+        for memo in self._gstat.values():
+            arr = memo[0].arr
+            pos = np.flatnonzero(np.isin(arr, ser))
+            if not len(pos):
+                continue
+            o = np.argsort(ser)
+            j = o[np.searchsorted(ser[o], arr[pos])]
+            _, ids_, handles, e, xs = memo[2]
+            e[pos] = end[j]
+            if revived:
+                ids_[pos] = [fws[j_].doc.id for j_ in j.tolist()]           # (a re-armed job's new id)
+            if handles is not None and None not in hd:
+                handles[pos] = np.asarray(hd, np.int64)[j]
+            if revived:
+                # re-resolved exporter slots; per-job extras (HPA / gauge slots) rebuilt on use
+                M = len(fws[0].plan.aliases)
+                if xs is not None:
+                    for p_, j_ in zip(pos.tolist(), j.tolist()):
+                        xs[p_ * M:(p_ + 1) * M] = self._cols_of([fws[j_]], M)[4]
+                for _, vm in memo[3].values():
+                    vm[pos] = False
+        for ga in self._garr.values():
+            if ga.end is None or ga.ident is None:
+                continue
+            pos = np.flatnonzero(np.isin(ga.ident.arr, ser))
+            if len(pos):
+                o = np.argsort(ser)
+                j = o[np.searchsorted(ser[o], ga.ident.arr[pos])]
+                ga.end[pos] = end[j]
+                if revived and ga.ids is not None:
+                    ga.ids[pos] = [fws[j_].doc.id for j_ in j.tolist()]
+                if ga.handles is not None and None not in hd:
+                    ga.handles[pos] = np.asarray(hd, np.int64)[j]
+                if revived and ga.export_slots is not None and self.b.exporter is not None:
+                    ga.export_start = self.b.exporter.contiguous_start(ga.export_slots)
 
     LAYOUT_COMPACT_EVERY = 32
     LAYOUT_GHOST_FRAC = 0.125
@@ -777,6 +929,43 @@ class FastPath:
                     return L
         self._set_layout(fws)
         return fws
+
+    def _layout_arrivals(self, fast: list, n_known: int, lay) -> list:
+        """A one-sliding-group claim with new jobs (``fast[n_known:]``): the
+        laid-out list with the arrivals APPENDED (the jobs that left stay as
+        ghosts), so every per-list memo -- template lists, row map, static
+        columns, model arrays, the early LSTM launch -- extends by the new
+        rows instead of being rebuilt.  A fresh layout when
+        there is none, it is due for compaction, a known job is not in it, or
+        the ghosts would pass LAYOUT_GHOST_FRAC."""
+        if lay is not None and self.cycle - lay[1] < self.LAYOUT_COMPACT_EVERY and n_known < len(fast):
+            L = lay[0]
+            known = fast[:n_known]
+            ix = self._jid(known).index_in(self._jid(L)) if known else np.zeros(0, np.int64)
+            if ix is not None:
+                new = fast[n_known:]
+                L2 = L + new
+                ghost = np.ones(len(L2), bool)
+                ghost[ix] = False
+                ghost[len(L):] = False
+                gj = np.flatnonzero(ghost)
+                # a new job reading a ghost's resident rows (the same series
+                # again under a new plan) would put one model key in the batch
+                # twice: lay the list out afresh instead
+                clash = len(gj) and len(np.intersect1d(np.concatenate([L2[j].rows for j in gj.tolist()]),
+                                                       np.concatenate([fw.rows for fw in new])))
+                if not clash and len(gj) <= self.LAYOUT_GHOST_FRAC * len(L2):
+                    self._lay = (L2, lay[1])
+                    if ghost.any():
+                        self.ghost = ghost
+                        self.ghost_ids = {id(L2[j]) for j in np.flatnonzero(ghost).tolist()}
+                        self.ghost_cycles += 1
+                    else:
+                        self.ghost, self.ghost_ids = None, set()
+                    self.arrivals_laid += len(new)
+                    return L2
+        self._set_layout(fast)
+        return fast
 
     def ghost_mask(self, works) -> np.ndarray | None:
         """This cycle's ghost mask of a job list (None: every job is live)."""
@@ -1045,6 +1234,12 @@ class FastPath:
         st = self.sliding
         ids = self._jid(ws)
         memo = self._tpl.get(p0.group)
+        if memo is not None and memo[0] != ids:
+            kx = ids.extends(memo[0])
+            if kx is not None:                    # arrivals appended to the laid-out list
+                ext = self._tpl_extend(memo, ws, kx, ids, M)
+                if ext is not None:
+                    memo = self._tpl[p0.group] = ext
         if memo is None or memo[0] != ids:
             # template lists and row map of this job list, reused while it is
             # unchanged (stable list objects let a staged source memoise them);
@@ -1152,6 +1347,55 @@ class FastPath:
         self._col[p0.group] = {"ids": ids, "cur": cur, "cur_t": cur_t,
                                "cur_len": cur_len, "base": base if bb else None, "base_len": base_len}
 
+    _TPL_FIELDS = ("cur_urls", "cur_stores", "base_urls", "base_stores", "hist_urls", "hist_stores")
+
+    def _tpl_extend(self, memo, ws: list, k: int, ids: "JobIds", M: int):
+        """The sliding group's template memo for ``ws`` = the memo's job list
+        + ``ws[k:]`` (arrivals): per (field, metric) the previous arrays and
+        TemplateLists extended by the new jobs' entries only; a source plans
+        an extended list from its base (TemplateList.extended).  None when the
+        new jobs do not fit the memo's mode (then the list is re-planned)."""
+        _, lists0, rows0, flags, arrs0 = memo
+        tail = ws[k:]
+        n = len(tail)
+        tarr = {}
+        for f in self._TPL_FIELDS:
+            col = [getattr(fw.plan, f) for fw in tail]
+            if any(len(c) != M for c in col):
+                return None
+            for m in range(M):
+                a = tarr[(f, m)] = np.empty(n, object)
+                a[:] = [c[m] for c in col]
+        merged, has_base = flags
+        if merged:
+            for m in range(M):
+                if not ((tarr[("cur_urls", m)] == tarr[("hist_urls", m)]).all()
+                        and (tarr[("cur_stores", m)] == tarr[("hist_stores", m)]).all()):
+                    return None
+                bu = tarr[("base_urls", m)]
+                if (bu != "").any():
+                    if not has_base or not ((bu == tarr[("hist_urls", m)]).all()
+                                            and (tarr[("base_stores", m)] == tarr[("hist_stores", m)]).all()):
+                        return None
+        lists, arrs = {}, {}
+        for key, a0 in arrs0.items():
+            t = tarr[key]
+            arrs[key] = np.concatenate([a0, t])
+            lists[key] = TemplateList.extended(lists0[key], t.tolist())
+        S = k + n
+        for (f, m), tl in lists.items():              # one store, every job queried: so is the extension
+            if f.endswith("_urls"):
+                sp = lists0[(f, m)].split
+                stl = lists[(f.replace("_urls", "_stores"), m)]
+                if sp is not None and len(sp[1]) == 1:
+                    (s0, have), = sp[1].items()
+                    if (len(have) == len(lists0[(f, m)]) and (tarr[(f.replace("_urls", "_stores"), m)] == s0).all()
+                            and (tarr[(f, m)] != "").all()):
+                        tl.split = (stl, {s0: np.arange(S)})
+        rows = np.concatenate([rows0, np.stack([fw.rows for fw in tail]).astype(np.int64)])
+        self.extends += 1
+        return (ids, lists, rows, flags, arrs)
+
     def _fetch_sliding_merged(self, ws: list[FastWork], now: float, memo) -> None:
         """Merged sliding fetch: per metric, every row's samples newer than its
         newest resident one, through now, on the step grid -- at a 60-s poll
@@ -1219,10 +1463,20 @@ class FastPath:
         # per-job state only when the job set or the window class changed (the
         # group's arrays are rebuilt from self._col every cycle regardless)
         prev = self._slide_state.get(p0.group)
-        if prev is None or prev[1] != wclass or (prev[0] != ids and ids.index_in(prev[0]) is None):
+        todo = None
+        if prev is None or prev[1] != wclass:
+            todo = ws
+        elif prev[0] != ids:
             # (a list that only lost jobs since: the survivors' state is set;
-            # the group's arrays rebuild from self._col, so not dirty)
-            for fw in ws:
+            # one that gained jobs at its end: only theirs is set; the group's
+            # arrays rebuild from self._col, so not dirty)
+            kx = ids.extends(prev[0])
+            if kx is not None:
+                todo = ws[kx:]
+            elif ids.index_in(prev[0]) is None:
+                todo = ws
+        if todo is not None:
+            for fw in todo:
                 fw.has_window = True
                 fw.dirty = False
                 fw.settled = False
@@ -1526,6 +1780,8 @@ class FastPath:
                     ix = ident.index_in(old.ident)            # jobs left the list (fleet churn)
                     if ix is not None:
                         ga.prev_models = ("churn", pm, ix)
+                    elif ident.extends(old.ident) is not None:
+                        ga.prev_models = ("extend", pm, ident.extends(old.ident))   # jobs arrived
         if xslots is not None:
             ga.export_slots = xslots
             ga.export_start = self.b.exporter.contiguous_start(xslots)
@@ -1845,6 +2101,16 @@ class FastPath:
         if memo is not None and memo[0] == ids:
             return memo[2], memo[3]
         ix = ids.index_in(memo[0]) if memo is not None else None
+        kx = ids.extends(memo[0]) if memo is not None and ix is None else None
+        if kx is not None:                       # arrivals appended: the new jobs' keys only
+            tk = [(f"{w.plan.namespace}/{w.doc.app_name}", a, b, algo) for w in works[kx:]
+                  for a, b in zip(p0.aliases, p0.base_metrics)]
+            kv = np.empty(len(works) * M, object)
+            kv[:kx * M] = memo[2]
+            kv[kx * M:] = tk
+            full = TemplateList.extended(memo[3], tk)
+            self._keys[(p0.group, algo)] = (ids, None, kv, full)
+            return kv, full
         if ix is not None:
             kv = memo[2].reshape(-1, M)[ix].reshape(-1)
         else:
@@ -1871,8 +2137,15 @@ class FastPath:
             return md
         prev = md if md is not None else ga.prev_models
         ga.prev_models = None
+        ext = None
         if isinstance(prev, tuple):
-            prev = self._model_arrays_churn(prev[1], prev[2], ga, works, store) if store.sliding else None
+            if prev[0] == "extend":
+                # arrivals: rebuilt below (the per-row arrays are array passes
+                # and one upload), with the survivors' cache keys extended,
+                # not re-derived, and the early forecast's rows a prefix
+                ext, prev = prev, None
+            else:
+                prev = self._model_arrays_churn(prev[1], prev[2], ga, works, store) if store.sliding else None
         if prev is not None and store.sliding and prev.inc is not None:
             nd = self._model_arrays_slid(prev, ga, store, stamp)
             if nd is not None:
@@ -1960,6 +2233,8 @@ class FastPath:
                                  view(kl).to(torch.int32), T, zoo.make_tables([p0.aliases[m] for m in ms], cfg, dev),
                                  keys, tl, view(kv).to(torch.int32), hr_d, hmax, len(ms)))
         md = ga.models = ModelArrays(stamp, subs, view(k_last))
+        if ext is not None:
+            md.base_rows = ext[2] * M            # the first rows are the previous arrays' rows
         if store.sliding and np.isfinite(t_last).all() and ga.cur_t.shape[0] and ga.cur_t.strides[0] == 0:
             # state for the next cycle's shift-only update (_model_arrays_slid)
             md.inc = (t_last, T, store.t0, store.ws, n, float(ga.cur_t[0, 0]), valid, lastk)
@@ -2181,7 +2456,7 @@ class FastPath:
             # fused band / reduce / compaction over it
             grp = works[0].plan.group
             lstm = b.lstm_for_jobs_of({sub.M}) if algo == "lstm" else None
-            got = self._pre_take(grp, sub, H, lstm)
+            got = self._pre_take(grp, sub, H, lstm, ga.rowmap, store)
             if got is not None:
                 fc, sig = got                       # launched during the fetch (_prelaunch)
             elif lstm is not None and lstm.reads_rows and store.buf.is_cuda:
@@ -2190,7 +2465,7 @@ class FastPath:
                 fc, sig = self._forecast(algo, LazyHist(store.buf, sub.rm, *sub.shift_lim(), sub.T), sub, H)
             fc, sig = fc.contiguous(), sig.contiguous()
             if lstm is not None and lstm.reads_rows and store.sliding:
-                self._pre_spec[grp] = (sub, H, lstm, store.ws)
+                self._pre_spec[grp] = (sub, H, lstm, store.ws, ga.rowmap)
             out = self._fused_launch(works, ga, md, store, diff, -1, None, None, 0, H=fc.shape[1], fc=fc, sig=sig)
             self.fused_steps += 1
             out["fc"] = {algo: (sub, fc)} if hpa_algo == algo else {}
@@ -2311,24 +2586,38 @@ class FastPath:
             return
         if spec is None:
             return
-        sub, H, lstm, ws0 = spec
+        sub, H, lstm, ws0, rmap = spec
         st = self.sliding
         k = st.ws - ws0
         if k < 0 or not st.buf.is_cuda:
             return
         dk = int(sub.dk) + k
         fc, sig = lstm.forecast_rows(st.buf, sub.rm, sub.shift, sub.lim, dk, sub.T, H)
-        self._pre[group] = (sub.rm, dk, sub.T, H, lstm, self.cycle, fc, sig)
+        self._pre[group] = (sub.rm, dk, sub.T, H, lstm, self.cycle, fc, sig, rmap, sub.shift, sub.lim)
 
-    def _pre_take(self, group: tuple, sub: "ModelSub", H: int, lstm):
+    def _pre_take(self, group: tuple, sub: "ModelSub", H: int, lstm, rowmap=None, store=None):
         pre = self._pre.pop(group, None)
         if pre is None:
             return None
-        rm, dk, T, H0, m0, cyc, fc, sig = pre
+        rm, dk, T, H0, m0, cyc, fc, sig, rmap, shift0, lim0 = pre
         if rm is sub.rm and dk == int(sub.dk) and T == sub.T and H0 == H and m0 is lstm and cyc == self.cycle:
             self.prelaunch_hits += 1
             self._pre_skip.pop(group, None)
             return fc, sig
+        n0 = len(rmap)
+        if (rowmap is not None and store is not None and sub.idx is None and T == sub.T and H0 == H and m0 is lstm
+                and cyc == self.cycle and len(rowmap) > n0 and np.array_equal(rowmap[:n0], rmap)):
+            # jobs arrived (appended to the laid-out list): the early forecast
+            # holds the first n0 rows if their alignment is the one the new
+            # arrays give them -- then only the new rows are forecast here
+            sh, li = sub.shift_lim()
+            if torch.equal(shift0 - dk, sh[:n0]) and torch.equal(lim0 + dk, li[:n0]):
+                fc_t, sig_t = lstm.forecast_rows(store.buf, sub.rm[n0:], sh[n0:].contiguous(), li[n0:].contiguous(),
+                                                 0, sub.T, H)
+                self.prelaunch_hits += 1
+                self.prelaunch_extended += 1
+                self._pre_skip.pop(group, None)
+                return torch.cat([fc, fc_t]), torch.cat([sig, sig_t])
         # a miss: skip the next 1, 2, 4, ... 32 cycles' early launches (a group
         # whose arrays are re-laid every cycle -- jobs resubmitted each cycle --
         # stops paying for recurrences it cannot use)

@@ -329,6 +329,9 @@ class PrometheusSource:
         ent = self._plans.get(id(templates))
         if ent is not None and ent[0] is templates:
             return ent[1]
+        got = self._extend_plan(templates)
+        if got is not None:
+            return got
         root = getattr(templates, "root", None)
         rent = self._plans.get(id(root)) if root is not None else None
         if root is not None and (rent is None or rent[0] is not root):
@@ -379,6 +382,57 @@ class PrometheusSource:
             if root is None:                            # a root list: what its subsets index
                 info = {"gid": gid, "th": hs, "apps": apps, "groups": groups, "chunks": chunks, "chunked_for": n,
                         "covered": np.ones(n, bool)}        # root positions the root's requests ask for
+        if len(self._plans) >= 32:
+            self._plans.pop(next(iter(self._plans)))
+        self._plans[id(templates)] = (templates, plan, info)
+        return plan
+
+    def _extend_plan(self, templates):
+        """Plan of ``base + new templates`` (jobs appended to a laid-out
+        list): the base's per-template columns and requests, plus the new
+        templates parsed and their apps chunked into requests of their own.
+        The result is a root (later subsets index it).  None: no usable base."""
+        base = getattr(templates, "base", None)
+        if base is None:
+            return None
+        bent = self._plans.get(id(base))
+        if bent is None or bent[0] is not base:
+            return None
+        if bent[2] is not None:
+            apps_b, groups = bent[2]["apps"], list(bent[2]["groups"])
+        else:
+            rt = getattr(base, "root", None)
+            rent = self._plans.get(id(rt)) if rt is not None else None
+            if rent is None or rent[0] is not rt or rent[2] is None:
+                return None
+            apps_b, groups = rent[2]["apps"][np.asarray(base.ix, np.int64)], list(rent[2]["groups"])
+        gid_b, th_b, _, chunks_b = bent[1]
+        tail = templates[len(base):]
+        n = len(tail)
+        gid = np.full(n, -1, np.int64)
+        apps = np.empty(n, object)
+        gmap = {g: k for k, g in enumerate(groups)}
+        for i, tpl in enumerate(tail):
+            pt = self._parse_template(tpl)
+            if pt:
+                g = gmap.get(pt[0])
+                if g is None:
+                    g = gmap[pt[0]] = len(groups)
+                    groups.append(pt[0])
+                gid[i] = g
+                apps[i] = pt[1]
+        ok = gid >= 0
+        from . import native_rt
+        hs = np.zeros(n, np.uint64)
+        if ok.any():
+            hs[ok] = native_rt.fnv1a(apps[ok].tolist())
+        # the new apps' own requests (an app already asked for by a base
+        # request is asked again: a duplicate answer is dropped by the join)
+        chunks = list(chunks_b) + self._chunks(gid, apps, groups)
+        G = np.concatenate([gid_b, gid])
+        plan = (G, np.concatenate([th_b, hs]), np.flatnonzero(G < 0), chunks)
+        info = {"gid": G, "th": plan[1], "apps": np.concatenate([apps_b, apps]), "groups": groups, "chunks": chunks,
+                "chunked_for": len(G), "covered": np.ones(len(G), bool)}
         if len(self._plans) >= 32:
             self._plans.pop(next(iter(self._plans)))
         self._plans[id(templates)] = (templates, plan, info)
@@ -745,9 +799,13 @@ class TemplateList(list):
     """The query templates of a job list.  ``root`` / ``ix``: this list is
     ``root[ix]`` (a job list that lost or reordered jobs: fleet churn), so a
     source that memoises per list (StagedSource) indexes the root's answer
-    instead of re-resolving every template."""
+    instead of re-resolving every template.  ``base``: this list is ``base``
+    followed by new templates (jobs that arrived, appended to the laid-out
+    list) -- a new root whose per-template plan is the base's plus the new
+    templates' only."""
     root = None
     ix = None
+    base = None
     split = None            # (store list, {store: positions}) memo of the brain's column fetch
 
     @classmethod
@@ -755,6 +813,13 @@ class TemplateList(list):
         out = cls(items)
         out.root = parent.root if parent.root is not None else parent
         out.ix = ix if parent.ix is None else parent.ix[ix]
+        return out
+
+    @classmethod
+    def extended(cls, parent: "TemplateList", tail: list) -> "TemplateList":
+        out = cls(parent)
+        list.extend(out, tail)
+        out.base = parent
         return out
 
 
@@ -781,6 +846,9 @@ class StagedSource:
         self._mat = np.zeros((0, 0), np.float32)
         self._n = 0
         self._lists: dict[int, tuple] = {}
+        self._keyed: dict[tuple, tuple] = {}     # (selector group, key value) -> staged (t, v, key hash)
+        self.keyed_hits = 0
+        self.gen_s = 0.0                         # time spent in the inner generator
 
     def fetch_columns(self, templates: list[str], start: float, end: float) -> "Columns":
         """Windows of many templates from the staged grid (vectorised
@@ -797,46 +865,7 @@ class StagedSource:
             return Columns.from_series(got)
         g0 = np.ceil(self.window[0] / self.step) * self.step
         G = int(np.floor((self.window[1] - g0) / self.step)) + 1
-        ent = self._lists.get(id(templates))
-        root = getattr(templates, "root", None)
-        if (ent is None or ent[0] is not templates) and root is not None:
-            rent = self._lists.pop(id(root), None)
-            if rent is None or rent[0] is not root:
-                # a root never fetched here (its first fetch was of a subset):
-                # resolve it once if every template of it is staged
-                rr = self._rows_of(root)
-                if len(rr) and (rr >= 0).all():
-                    rent = (root, rr)
-            if rent is not None and rent[0] is root:       # a subset of a staged list: index its rows
-                self._lists[id(root)] = rent                  # (kept most recently used)
-                ent = (templates, rent[1][templates.ix])
-                self._remember(templates, ent)
-        if ent is None or ent[0] is not templates:
-            miss = self._rows_of(templates) < 0
-            new = list(dict.fromkeys(t for t, m in zip(templates, miss.tolist()) if m)) if miss.any() else []
-            if new:
-                self.misses += len(new)
-                t_gen = time.perf_counter()
-                cols = inner(new, g0, g0 + (G - 1) * self.step)
-                if len(new) * G > 1e7:
-                    print(f"[staged] {len(new)} series x {G} samples in {time.perf_counter() - t_gen:.1f}s",
-                          file=sys.stderr, flush=True)
-                n0 = self._n
-                if n0 + len(new) > self._mat.shape[0] or self._mat.shape[1] != G:
-                    cap = max(n0 + len(new), 2 * self._mat.shape[0])
-                    m = np.full((cap, G), np.nan, np.float32)
-                    if n0:
-                        m[:n0] = self._mat[:n0]
-                    self._mat = m
-                for k, t in enumerate(new):
-                    a, b = cols.off[k], cols.off[k + 1]
-                    c = np.rint((cols.t[a:b] - g0) / self.step).astype(np.int64)
-                    ok = (c >= 0) & (c < G)
-                    self._mat[n0 + k, c[ok]] = cols.v[a:b][ok]
-                    self._row[t] = n0 + k
-                self._n = n0 + len(new)
-            ent = (templates, self._rows_of(templates))
-            self._remember(templates, ent)
+        ent = self._resolve(templates, inner, g0, G)
         rows = ent[1]
         c0 = max(0, int(np.ceil((start - g0) / self.step - 1e-9)))
         c1 = min(G, int(np.floor((end - g0) / self.step + 1e-9)) + 1)
@@ -849,11 +878,140 @@ class StagedSource:
         np.cumsum(lens, out=off[1:])
         return Columns(off, t[keep], v[keep], [None] * len(rows))
 
+    def _resolve(self, templates, inner, g0: float, G: int, depth: int = 0):
+        """(templates, staged row per template) of a template list, memoised
+        per list object: a subset (``root``/``ix``) indexes its root's rows, an
+        extension (``base`` + new templates) is its base's rows plus the new
+        templates' (generated if not staged yet) -- no per-template lookup of
+        the whole list under fleet churn."""
+        ent = self._lists.get(id(templates))
+        if ent is not None and ent[0] is templates:
+            self._lists.pop(id(templates))           # kept most recently used
+            self._lists[id(templates)] = ent
+            return ent
+        ent = None
+        base = getattr(templates, "base", None)
+        root = getattr(templates, "root", None)
+        if base is not None and depth < 64:
+            bent = self._resolve(base, inner, g0, G, depth + 1)
+            tail = templates[len(base):]
+            self._stage(tail, inner, g0, G)
+            ent = (templates, np.concatenate([bent[1], self._rows_of(tail)]))
+        elif root is not None and depth < 64:
+            rent = self._resolve(root, inner, g0, G, depth + 1)
+            ent = (templates, rent[1][np.asarray(templates.ix, np.int64)])
+        else:
+            self._stage(templates, inner, g0, G)
+            ent = (templates, self._rows_of(templates))
+        self._remember(templates, ent)
+        return ent
+
+    def _stage(self, templates, inner, g0: float, G: int) -> int:
+        """Generate (``inner.fetch_columns`` over the whole staging window)
+        the templates not staged yet; returns how many were."""
+        miss = self._rows_of(templates) < 0
+        new = list(dict.fromkeys(t for t, m in zip(templates, miss.tolist()) if m)) if miss.any() else []
+        if not new:
+            return 0
+        self.misses += len(new)
+        t_gen = time.perf_counter()
+        cols = inner(new, g0, g0 + (G - 1) * self.step)
+        self.gen_s += time.perf_counter() - t_gen
+        if len(new) * G > 1e7:
+            print(f"[staged] {len(new)} series x {G} samples in {time.perf_counter() - t_gen:.1f}s",
+                  file=sys.stderr, flush=True)
+        n0 = self._n
+        if n0 + len(new) > self._mat.shape[0] or self._mat.shape[1] != G:
+            cap = max(n0 + len(new), 2 * self._mat.shape[0])
+            m = np.full((cap, G), np.nan, np.float32)
+            if n0:
+                m[:n0] = self._mat[:n0]
+            self._mat = m
+        for k, t in enumerate(new):
+            a, b = cols.off[k], cols.off[k + 1]
+            c = np.rint((cols.t[a:b] - g0) / self.step).astype(np.int64)
+            ok = (c >= 0) & (c < G)
+            self._mat[n0 + k, c[ok]] = cols.v[a:b][ok]
+            self._row[t] = n0 + k
+        self._n = n0 + len(new)
+        return len(new)
+
+    def prestage(self, templates: list[str]) -> int:
+        """Stage templates ahead of the jobs that will query them (a bench
+        renders arriving jobs' series before its timed cycles, so the
+        generator never runs inside a measured brain cycle)."""
+        inner = getattr(self.inner, "fetch_columns", None)
+        if self.window is None or inner is None:
+            return 0
+        g0 = np.ceil(self.window[0] / self.step) * self.step
+        G = int(np.floor((self.window[1] - g0) / self.step)) + 1
+        return self._stage(list(templates), inner, g0, G)
+
     def fetch_keyed(self, queries: list, pool=None) -> list:
         inner = getattr(self.inner, "fetch_keyed", None)
         if inner is None:
             raise SourceError("inner source has no batched form")
-        return inner(queries, pool=pool)
+        if not self._keyed:
+            return inner(queries, pool=pool)
+        out: list = [None] * len(queries)
+        rest = []
+        for i, q in enumerate(queries):
+            got = self._keyed_answer(q)
+            if got is None:
+                rest.append(i)
+            else:
+                out[i] = got
+        if rest:
+            for i, g in zip(rest, inner([queries[i] for i in rest], pool=pool)):
+                out[i] = g
+        return out
+
+    def prestage_keyed(self, group: tuple, values: list, start: float, end: float) -> int:
+        """Render the batched (key-split) answers of ``values`` of a selector
+        group over ``[start, end]`` ahead of time: a later ``fetch_keyed``
+        whose values are all staged for its group and whose window lies in the
+        staged one is answered by slicing (the same samples: the synthetic
+        series are counter-based per timestamp).  Returns the values added."""
+        from . import native_rt
+        from .ingest import KeyedQuery
+        inner = getattr(self.inner, "fetch_keyed", None)
+        vals = [v for v in dict.fromkeys(values) if (group, v) not in self._keyed]
+        if inner is None or not vals:
+            return 0
+        t_gen = time.perf_counter()
+        g = inner([KeyedQuery(group, vals, start, end)])[0]
+        self.gen_s += time.perf_counter() - t_gen
+        hs = native_rt.fnv1a(vals)
+        pos = {int(h): k for k, h in enumerate(np.asarray(g.key).tolist())}
+        for v, h in zip(vals, hs.tolist()):
+            k = pos.get(int(h))
+            if k is None:
+                self._keyed[(group, v)] = (np.zeros(0), np.zeros(0, np.float32), int(h), start, end)
+            else:
+                a, b = int(g.off[k]), int(g.off[k + 1])
+                self._keyed[(group, v)] = (np.asarray(g.t[a:b]), np.asarray(g.v[a:b], np.float32), int(h),
+                                           start, end)
+        return len(vals)
+
+    def _keyed_answer(self, q):
+        """A batched query answered from the staged keyed rows (every value
+        staged for its group over a window covering the query's), else None.
+        The series come in the query's value order, as the generator's."""
+        from . import native_rt
+        vals = list(dict.fromkeys(q.key_values()))
+        ents = [self._keyed.get((q.group, v)) for v in vals]
+        if not vals or any(e is None or q.start < e[3] - 1e-6 or q.end > e[4] + 1e-6 for e in ents):
+            return None
+        ks, offs, ts, vs = [], [0], [], []
+        for t, v, h, _, _ in ents:
+            a, b = np.searchsorted(t, q.start - 1e-6), np.searchsorted(t, q.end + 1e-6)
+            ks.append(h)
+            ts.append(t[a:b])
+            vs.append(v[a:b])
+            offs.append(offs[-1] + b - a)
+        self.keyed_hits += 1
+        return native_rt.Keyed(np.asarray(ks, np.uint64), np.asarray(offs, np.int64), np.concatenate(ts),
+                               np.concatenate(vs).astype(np.float32, copy=False))
 
     def _remember(self, templates, ent) -> None:
         if len(self._lists) >= 64:                       # bounded: job lists change with fleet churn

@@ -71,7 +71,7 @@ def collective_device(device=None, group=None) -> torch.device:
     (``nccl``) group only moves device tensors (torch's backend capability
     table: ``nccl -> ['cuda']``), gloo moves host tensors.  ``device`` is
     the rank's GPU; without one the current HIP device is used."""
-    backend = dist.get_backend(group) if is_dist() else "gloo"
+    backend = dist.get_backend(group) if (dist.is_available() and dist.is_initialized()) else "gloo"
     if "nccl" in str(backend).lower():
         if device is not None and torch.device(device).type == "cuda":
             return torch.device(device)
@@ -93,7 +93,7 @@ def agree_all(ok: bool, tag: str = "fm/agree", timeout_s: float | None = None) -
     it the same number of times (like any collective); a rank that never
     arrives makes the others raise after ``timeout_s`` (the store's timeout by
     default) instead of hanging."""
-    if not is_dist():
+    if not (dist.is_available() and dist.is_initialized()):
         return bool(ok)
     from datetime import timedelta
     from torch.distributed import distributed_c10d as c10d

@@ -135,7 +135,7 @@ _RCCL_WORLD1 = textwrap.dedent("""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     from foremast_amd.parallel import dist as D
-    info = D.init_distributed(backend="nccl", device=dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     from foremast_amd.parallel import board as B
     res = {"backend": dist.get_backend()}
     res["agree"] = D.agree_all(True) and not D.agree_all(False)

@@ -401,3 +401,71 @@ def test_async_hpalog_writer_matches_inline_writes():
         a[0].t += 60
         b[0].t += 60
     assert getattr(a[3], "_log_writer", None) is not None and getattr(b[3], "_log_writer", None) is None
+
+
+@pytest.mark.parametrize("algo,kind", [("holt_winters", "continuous"), ("lstm", "hpa")])
+def test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, device="cpu"):
+    """a one-sliding-group fleet with churn in BOTH directions
+    every cycle for 20 cycles -- new services arrive (appended to the
+    laid-out list: the template lists, static columns, model arrays and cache
+    keys extend by the new rows), services regress and close (ghosts), and
+    jobs are resubmitted with an unchanged plan (the FastWork is patched in
+    place).  Verdicts, reasons, HPA logs and gauges equal the general path's
+    cycle by cycle."""
+    faults = {f"{kind}{j}": 4.0 for j in range(2, 60, 5)}
+    a = _brain(True, algo, faults, device)
+    b = _brain(False, algo, faults, device)
+    strat = "continuous" if kind == "continuous" else "hpa"
+    extra = ["cpu", "latency", "error5xx", "memory"] if strat == "hpa" else None
+    a[3].fast.LAYOUT_GHOST_FRAC = 0.5           # closes at the 2-sigma default: keep the layout across them
+    a[3].fast.LAYOUT_COMPACT_EVERY = 8          # ... and compact it on the way
+
+    def submit(client, j):
+        return client.start_analyzing("prod", f"{kind}{j}", None, _metrics(4), 10, strat, extra)
+    ids = [submit(a[2], j) for j in range(12)]
+    assert ids == [submit(b[2], j) for j in range(12)]
+    nxt = 12
+    app_of = {i: j for j, i in enumerate(ids)}
+    rearmed = set()
+    for cyc in range(20):
+        if cyc:
+            for _ in range(2):                                   # arrivals: new services
+                j1, j2 = submit(a[2], nxt), submit(b[2], nxt)
+                assert j1 == j2
+                ids.append(j1)
+                app_of[j1] = nxt
+                nxt += 1
+            if strat == "hpa":
+                # a resubmission of a live HPA job (same id app:ns:hpa, same plan)
+                j = app_of[ids[(cyc * 7) % len(ids)]]
+            else:
+                # a closed monitor re-armed (Barrelman.go:552-565): a new job id, the plan it had
+                closed = [app_of[i] for i in ids if a[1].get(i).status == ST.COMPLETED_UNHEALTH
+                          and app_of[i] not in rearmed]
+                j = closed[0] if closed else None
+            if j is not None:
+                rearmed.add(j)
+                j1, j2 = submit(a[2], j), submit(b[2], j)
+                assert j1 == j2
+                if j1 not in app_of:
+                    ids.append(j1)
+                    app_of[j1] = j
+        ra, rb = a[3].run_once(), b[3].run_once()
+        assert ra["claimed"] == rb["claimed"] and ra["rows"] == rb["rows"], (cyc, ra, rb)
+        _compare(a, b, ids, cyc)
+        a[0].t += 60
+        b[0].t += 60
+    f = a[3].fast
+    assert f.arrivals_laid > 0 and f.extends > 0, (f.arrivals_laid, f.extends)
+    assert (f.resubmits_patched if strat == "hpa" else f.revived) > 0, (f.resubmits_patched, f.revived)
+    if strat != "hpa":                                           # (HPA jobs stay alive)
+        assert ST.COMPLETED_UNHEALTH in {a[1].get(j).status for j in ids}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo,kind", [("holt_winters", "continuous"), ("lstm", "hpa")])
+def test_gpu_arrivals_and_departures_every_cycle_equal_general_path(algo, kind):
+    """The arrivals parity on the MI355X kernels: fused steady cycles, the
+    model cache, and (LSTM) the early forecast reused for the laid-out rows
+    with only the arrivals' rows forecast in the cycle."""
+    test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, device="cuda")
