@@ -233,6 +233,53 @@ E2E_MIXED = [("canary", "moving_average_all", "3e2e", "", 0.4),
              ("hpa", "lstm", "4e2e", "_hpa", 0.2)]
 
 
+def prestage_future(staged, classes, submit_one, js, now: float, history_days: float, ahead_s: float,
+                    only_class=None) -> int:
+    """Render the series of jobs the timed cycles will submit (indices
+    ``js`` of class ``only_class``, default the first) into the staged
+    source: their documents are built through the real create path into a
+    scratch store, and every query they will issue is staged -- sliding
+    templates over the staging window, canary history / windows as keyed
+    answers over [now - history - 1 d, now + ahead].  Returns the series
+    staged."""
+    import json as _json
+    from foremast_amd.api import jobs as J
+    from foremast_amd.api.models import ApplicationHealthAnalyzeRequest
+    from foremast_amd.api.urls import parse_config
+    from foremast_amd.controller.analyst import AnalystClient, Response
+    from foremast_amd.engine.ingest import parse_range
+    from foremast_amd.service.store import MemoryStore
+    js = list(js)
+    if not js:
+        return 0
+    scratch = MemoryStore()
+
+    def do(method, url, body):
+        req = ApplicationHealthAnalyzeRequest.from_dict(_json.loads(body))
+        jid, _ = scratch.create(J.build_document(req))
+        return Response(200, _json.dumps(J.new_response(jid, 0, "new")).encode())
+    client = AnalystClient("http://foremast-service/v1/healthcheck/", do, lambda: now)
+    c = 0 if only_class is None else only_class
+    for j in js:
+        submit_one(client, c, j)
+    tpls, keyed = [], {}
+    for d in scratch.all_docs():
+        hist = parse_config(d.historical_config)
+        if classes[c][0] != "canary":
+            tpls.extend(u for u in hist.values() if u)
+            continue
+        for url, key in [(u, "app") for u in hist.values()] + \
+                [(u, "pod") for cfg in (d.current_config, d.baseline_config) for u in parse_config(cfg).values()]:
+            spec = parse_range(url, keys=(key,)) if url else None
+            if spec is not None:
+                keyed.setdefault(spec.group, set()).update(spec.values)
+    n = staged.prestage(tpls) if tpls else 0
+    lo, hi = now - history_days * 86400.0 - 86400.0, now + ahead_s
+    for g, vals in keyed.items():
+        n += staged.prestage_keyed(g, sorted(vals), lo, hi)
+    return n
+
+
 def config3e2e(args):
     """The production brain (``Brain.run_once``) on a BASELINE fleet.
 
@@ -390,6 +437,19 @@ def config3e2e(args):
         t_hi = t["now"] + (n_cycles + 2) * poll + (150.0 if http else 0.0)
         staged = StagedSource(SyntheticSource(faults=faults, fault_after=fault_after),
                               window=(t["now"] - args.history_days * 86400 - 3600, t_hi))
+    # the jobs the timed cycles will submit (arrivals, mixed-fleet canaries):
+    # their series are rendered NOW, so the generator (the bench's stand-in
+    # for Prometheus) never runs inside a timed brain cycle
+    n_future = (args.steps + args.warmup + 2) * (
+        max(int(round(args.arrivals * S)), 0) if kind != "mixed"
+        else sum(max(1, n_ // 200) for st_, _, _, _, n_ in classes if st_ == "canary"))
+    t_pre = time.perf_counter()
+    pre_n = prestage_future(staged, classes, submit_one, range(S, S + n_future), t["now"], args.history_days,
+                            (n_cycles + 2) * poll + 3600.0, 0 if kind == "mixed" else None)
+    t_pre = time.perf_counter() - t_pre
+    if pre_n:
+        print(f"[{kind}] rank {info.rank}: pre-rendered {pre_n} series of {n_future} future jobs in {t_pre:.1f}s",
+              file=sys.stderr, flush=True)
     if http:
         from foremast_amd.engine.sources import PrometheusSource, TieredSource
         live = PrometheusSource(workers=16)
@@ -426,7 +486,7 @@ def config3e2e(args):
         cfg.lstm_window = args.lookback
     exp = BrainExporter()
     brain = Brain(store, cfg, device=dev, sources=router, clock=clock,
-                  batch_size=S + 1, worker_id=f"bench-{info.rank}", exporter=exp, history_days=args.history_days)
+                  batch_size=S + n_future + 1, worker_id=f"bench-{info.rank}", exporter=exp, history_days=args.history_days)
     # HTTP canaries: the first cycle runs 90 s after the last submission, so
     # the timed cycles sit inside the watch windows (points arriving)
     t["now"] += poll + (90.0 if http and classes[0][0] == "canary" else 0.0)
@@ -452,6 +512,8 @@ def config3e2e(args):
     req_log = []
     http_stats: list = []                   # PrometheusSource.stats deltas per cycle (attributed fetch span)
     cyc_ms: list[float] = []
+    gen_ms: list[float] = []                # the synthetic generator's time inside each cycle
+    onboard: list = []                      # (host s, jobs) onboarded per cycle
     # FOREMAST_PROFILE_CYCLES=<path>: cProfile of the timed cycles only
     _prof = None
     _tprof = [] if os.environ.get("FOREMAST_TORCH_PROFILE") else None
@@ -504,6 +566,8 @@ def config3e2e(args):
                     for j in range(base_j, min(a0 + n_, base_j + k)):
                         submit_one(churn_client, c, j)
                         churn["resub"] += 1
+        gen0 = staged.gen_s
+        ob0 = (brain.fast.onboard_s, brain.fast.onboard_jobs) if brain.fast is not None else (0.0, 0)
         n0 = (live.requests, live.bytes) if live is not None else (0, 0)
         st0 = dict(live.stats) if live is not None else None
         wt0 = brain.fast.wt.apply_s if brain.fast is not None else 0.0
@@ -531,6 +595,9 @@ def config3e2e(args):
         if len(cyc_ms) + 1 == args.warmup + args.steps:
             brain.flush_logs()             # the last timed cycle waits for the queued HPA log writes
         cyc_ms.append(1e3 * (time.perf_counter() - tc))
+        gen_ms.append(1e3 * (staged.gen_s - gen0))
+        if brain.fast is not None:
+            onboard.append((brain.fast.onboard_s - ob0[0], brain.fast.onboard_jobs - ob0[1]))
         rows.append(r.get("rows", 0))
         if live is not None:
             req_log.append((live.requests - n0[0], live.bytes - n0[1]))
@@ -692,7 +759,7 @@ def config3e2e(args):
         if cw is not None:
             cw.set(t["now"])
         t_r = time.perf_counter()
-        brain2 = Brain(store2, cfg, device=dev, sources=router, clock=clock, batch_size=S + 1,
+        brain2 = Brain(store2, cfg, device=dev, sources=router, clock=clock, batch_size=S + n_future + 1,
                        worker_id=f"bench-{info.rank}", exporter=BrainExporter(), history_days=args.history_days)
         brain2.load_checkpoint(ck)
         n_rest = brain2.load_history(ck)
@@ -794,6 +861,21 @@ def config3e2e(args):
                                    if brain.fast is not None else None),
              "fused_steady_cycles": ({"groups_fused": brain.fast.fused_steps, "declined": brain.fast.fused_declined}
                                      if brain.fast is not None else None),
+             "generator_ms_in_timed_cycles": round(sum(gen_ms[args.warmup:]), 3),
+             "onboarding": ({"jobs_per_cycle": round(sum(j for _, j in onboard[args.warmup:]) /
+                                                     max(1, len(onboard[args.warmup:])), 2),
+                             "ms_per_cycle": round(1e3 * sum(x for x, _ in onboard[args.warmup:]) /
+                                                   max(1, len(onboard[args.warmup:])), 3),
+                             "onboarding_ms_per_job": round(1e3 * sum(x for x, _ in onboard[args.warmup:]) /
+                                                            max(1, sum(j for _, j in onboard[args.warmup:])), 4)
+                             if sum(j for _, j in onboard[args.warmup:]) else None,
+                             "what": "host time of planning new jobs + fetching their 7-day history + staging it"}
+                            if onboard else None),
+             "fast_path_churn": ({"resubmits_patched": brain.fast.resubmits_patched, "revived": brain.fast.revived,
+                                  "arrivals_appended": brain.fast.arrivals_laid, "memo_extends": brain.fast.extends,
+                                  "lstm_early_launch_extended": brain.fast.prelaunch_extended,
+                                  "ghost_cycles": brain.fast.ghost_cycles} if brain.fast is not None else None),
+             "prerendered_future_series": pre_n,
              "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),
              "submit_s": round(t_sub, 3),
              "fast_jobs_first_cycle": first.get("fast_jobs"), "device": str(dev)})

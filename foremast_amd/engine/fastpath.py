@@ -38,6 +38,7 @@ import html
 import json
 import logging
 import math
+import time
 from dataclasses import dataclass, field, replace
 from datetime import datetime, timezone
 
@@ -545,6 +546,8 @@ class FastPath:
         self.resubmits_patched = 0  # resubmissions that kept their FastWork (unchanged plan)
         self.arrivals_laid = 0     # new jobs appended to a laid-out list (instead of a fresh layout)
         self.revived = 0           # re-armed jobs that took their ghost slot back
+        self.onboard_s = 0.0       # host time onboarding jobs: planning + first history fetch + staging
+        self.onboard_jobs = 0
         self.extends = 0           # per-list memos extended by appended jobs (instead of rebuilt)
         self._hist_pending = False  # a per-job fetch left history in some FastWork.hist this cycle
         self._tpl: dict = {}      # sliding group -> (job ids, template lists, row map)
@@ -729,6 +732,7 @@ class FastPath:
         reg: list[FastWork] = []
         new_fw: list[FastWork] = []
         revived: list[FastWork] = []
+        t_on = time.perf_counter()
         if unknown:
             docs = batch.docs(unknown)
             self._prefill_specs(docs)
@@ -775,6 +779,9 @@ class FastPath:
         fast += revived + new_fw
         todo += revived + new_fw
         self.new_jobs = len(new_fw)
+        if unknown:
+            self.onboard_s += time.perf_counter() - t_on
+            self.onboard_jobs += len(new_fw) + len(revived)
         if reg:
             self._register_windows(reg)
         if new_fw and self.b.exporter is not None:
@@ -1116,6 +1123,13 @@ class FastPath:
         app-keyed selectors of a batched source share ``app=~`` requests of up
         to ``fetch_batch`` apps per (selector, window).  Returns the jobs left
         for the per-job fetch."""
+        t_on = time.perf_counter()
+        try:
+            return self._fetch_static_history_(ws, now, pool)
+        finally:
+            self.onboard_s += time.perf_counter() - t_on
+
+    def _fetch_static_history_(self, ws: list[FastWork], now: float, pool=None) -> list[FastWork]:
         from .brain import _app_level
         from .ingest import KeyedQuery, keyed_split, parse_range
         from .sources import Series
@@ -1430,10 +1444,13 @@ class FastPath:
                     lens, t, v = self._columns(stores, tpls, float(lo_v), hi)
                 else:
                     # rows at another start this cycle: subsets of the planned
-                    # lists (a source indexes their plan, no re-parse)
+                    # lists (a source indexes their plan, no re-parse) -- new
+                    # rows' whole history window among them (onboarding)
+                    t_on = time.perf_counter()
                     sl = sel.tolist()
                     lens, t, v = self._columns(TemplateList.subset(stores, [stores[i] for i in sl], sel),
                                                TemplateList.subset(tpls, [tpls[i] for i in sl], sel), float(lo_v), hi)
+                    self.onboard_s += time.perf_counter() - t_on
                 if len(t):
                     wr.append(np.repeat(rows[:, m] if sel is None else rows[sel, m], lens))
                     wt.append(t)
@@ -1664,8 +1681,10 @@ class FastPath:
                     svals.append(v)
                     stl.append(t[0] if len(t) else -np.inf)
         if srows:
+            t_on = time.perf_counter()
             self.static.write_static(np.asarray(srows, np.int64), svals, np.asarray(stl, np.float64))
             self._hist_epoch += 1
+            self.onboard_s += time.perf_counter() - t_on
         if drows:
             self.sliding.write_sliding(np.asarray(drows, np.int64), dts, dvs)
         for fw in got:

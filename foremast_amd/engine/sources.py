@@ -952,7 +952,11 @@ class StagedSource:
         if inner is None:
             raise SourceError("inner source has no batched form")
         if not self._keyed:
-            return inner(queries, pool=pool)
+            t_gen = time.perf_counter()
+            try:
+                return inner(queries, pool=pool)
+            finally:
+                self.gen_s += time.perf_counter() - t_gen
         out: list = [None] * len(queries)
         rest = []
         for i, q in enumerate(queries):
@@ -962,8 +966,10 @@ class StagedSource:
             else:
                 out[i] = got
         if rest:
+            t_gen = time.perf_counter()
             for i, g in zip(rest, inner([queries[i] for i in rest], pool=pool)):
                 out[i] = g
+            self.gen_s += time.perf_counter() - t_gen
         return out
 
     def prestage_keyed(self, group: tuple, values: list, start: float, end: float) -> int:
@@ -1036,7 +1042,9 @@ class StagedSource:
         got = self.cache.get(url)
         if got is None:
             self.misses += 1
+            t_gen = time.perf_counter()
             got = self.inner.fetch(url)
+            self.gen_s += time.perf_counter() - t_gen
             if self.cache_history or sum(len(s.values) for s in got) <= 4096:
                 self.cache[url] = got
         return got
