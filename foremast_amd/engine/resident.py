@@ -102,6 +102,7 @@ class ResidentHistory:
         self._gone = None                           # (device, pinned) finite counts of retired columns
         self.bytes_in = 0
         self.max_len = 0                            # static: longest row written (view length)
+        self.dense_rows = 0                         # sliding rows whose history arrived as one grid block
 
     # ------------------------------------------------------------------ rows
     def __len__(self) -> int:
@@ -329,6 +330,41 @@ class ResidentHistory:
             return
         self.write_sliding_flat(np.repeat(np.asarray(rows, np.int64), lens), np.concatenate(times),
                                 np.concatenate(values).astype(np.float32, copy=False))
+
+    def write_sliding_dense(self, rows: np.ndarray, t: np.ndarray, V: np.ndarray) -> None:
+        """Rows with NO sample yet (new jobs' history): ``V[i, k]`` is row
+        ``rows[i]``'s sample at grid time ``t[k]`` (consecutive grid points,
+        NaN = missing).  The block goes to the device in one copy and one
+        row-scatter of a column range; ``last_t`` / ``nfin`` from array passes
+        -- no per-sample scatter (a new job's 7-day window is 10,080 samples
+        per metric)."""
+        assert self.sliding and self.t0 is not None
+        rows = np.asarray(rows, np.int64)
+        if not len(rows) or not len(t):
+            return
+        c = self.col(t)
+        if len(c) > 1 and not (np.diff(c) == 1).all():
+            ok = np.isfinite(V)
+            self.write_sliding_flat(np.repeat(rows, ok.sum(1)), np.broadcast_to(t, V.shape)[ok], V[ok])
+            return
+        a, b = max(int(c[0]), self.ws), min(int(c[-1]) + 1, self.e)
+        if b <= a:
+            return
+        V = V[:, a - int(c[0]):b - int(c[0])]
+        fin = np.isfinite(V)
+        cnt = fin.sum(1)
+        has = cnt > 0
+        last = V.shape[1] - 1 - np.argmax(fin[:, ::-1], axis=1)
+        self.nfin[rows] = cnt
+        self.last_t[rows] = np.where(has, self.t0 + (a + last) * self.step, -np.inf)
+        blk = torch.from_numpy(np.ascontiguousarray(V, np.float32))
+        idx = torch.from_numpy(rows)
+        if self.device.type == "cuda":
+            blk = blk.pin_memory().to(self.device, non_blocking=True)
+            idx = idx.to(self.device, non_blocking=True)
+        self.buf[idx, a:b] = blk
+        self.bytes_in += blk.numel() * 4
+        self.dense_rows += len(rows)
 
     def write_sliding_flat(self, r: np.ndarray, t: np.ndarray, v: np.ndarray) -> None:
         """:meth:`write_sliding` for samples already flattened (row per sample)."""

@@ -936,6 +936,23 @@ class StagedSource:
         self._n = n0 + len(new)
         return len(new)
 
+    def fetch_columns_dense(self, templates: list[str], start: float, end: float):
+        """The staged grid block of ``templates`` over [start, end]: (grid
+        times [n], values [len(templates), n], NaN = no sample) -- what
+        :meth:`fetch_columns` returns, before the missing samples are
+        squeezed out.  None outside the staging window."""
+        inner = getattr(self.inner, "fetch_columns", None)
+        if self.window is None or inner is None or not (self.window[0] <= start and end <= self.window[1]):
+            return None
+        g0 = np.ceil(self.window[0] / self.step) * self.step
+        G = int(np.floor((self.window[1] - g0) / self.step)) + 1
+        rows = self._resolve(templates, inner, g0, G)[1]
+        c0 = max(0, int(np.ceil((start - g0) / self.step - 1e-9)))
+        c1 = min(G, int(np.floor((end - g0) / self.step + 1e-9)) + 1)
+        if c1 <= c0:
+            return None
+        return g0 + self.step * np.arange(c0, c1), self._mat[rows, c0:c1]
+
     def prestage(self, templates: list[str]) -> int:
         """Stage templates ahead of the jobs that will query them (a bench
         renders arriving jobs' series before its timed cycles, so the
@@ -1095,6 +1112,10 @@ class TieredSource:
     def fetch_columns(self, templates: list[str], start: float, end: float) -> Columns:
         return self._pick(start, end).fetch_columns(templates, start, end)
 
+    def fetch_columns_dense(self, templates: list[str], start: float, end: float):
+        fd = getattr(self._pick(start, end), "fetch_columns_dense", None)
+        return fd(templates, start, end) if fd is not None else None
+
 
 class StaticSource:
     """Fixed answers by URL substring (tests, demos, and operator-provided
@@ -1213,6 +1234,16 @@ class SourceRouter:
             except (SourceError, OSError, ValueError) as e:
                 got.append(e)
         return Columns.from_series(got)
+
+    def fetch_columns_dense(self, store_type: str, templates: list[str], start: float, end: float):
+        """A source's grid block of many templates (staged / archived
+        stores), else None: the caller takes :meth:`fetch_columns`."""
+        try:
+            src = self._source(store_type)
+        except SourceError:
+            return None
+        fd = getattr(src, "fetch_columns_dense", None)
+        return fd(templates, start, end) if fd is not None else None
 
     def _source(self, store_type: str):
         kind = self.force or store_type or "prometheus"

@@ -58,13 +58,20 @@ def _cfg(algo):
     return cfg
 
 
-def _brain(resident, algo, faults, device="cpu"):
+def _brain(resident, algo, faults, device="cpu", staged=False):
     clock = Clock()
     store = MemoryStore()
     client = AnalystClient.for_app(create_app(store), clock=clock)
     exp = BrainExporter()
-    brain = Brain(store, _cfg(algo), device=device,
-                  sources=SourceRouter.synthetic_only(faults=faults, fault_after=T0 + 120),
+    if staged:
+        # column-staged series (the bench's stand-in for an archive): new
+        # rows' history arrives as dense grid blocks
+        from foremast_amd.engine.sources import StagedSource, SyntheticSource
+        src = SourceRouter(synthetic=StagedSource(SyntheticSource(faults=faults, fault_after=T0 + 120),
+                                                  window=(T0 - 8 * 86400.0, T0 + 2 * 86400.0)), force="synthetic")
+    else:
+        src = SourceRouter.synthetic_only(faults=faults, fault_after=T0 + 120)
+    brain = Brain(store, _cfg(algo), device=device, sources=src,
                   clock=clock, exporter=exp, worker_id="w0", resident_history=resident)
     return clock, store, client, brain, exp
 
@@ -403,8 +410,9 @@ def test_async_hpalog_writer_matches_inline_writes():
     assert getattr(a[3], "_log_writer", None) is not None and getattr(b[3], "_log_writer", None) is None
 
 
-@pytest.mark.parametrize("algo,kind", [("holt_winters", "continuous"), ("lstm", "hpa")])
-def test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, device="cpu"):
+@pytest.mark.parametrize("algo,kind,staged", [("holt_winters", "continuous", False), ("lstm", "hpa", False),
+                                              ("holt_winters", "continuous", True)])
+def test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, staged, device="cpu"):
     """a one-sliding-group fleet with churn in BOTH directions
     every cycle for 20 cycles -- new services arrive (appended to the
     laid-out list: the template lists, static columns, model arrays and cache
@@ -413,7 +421,7 @@ def test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, devi
     place).  Verdicts, reasons, HPA logs and gauges equal the general path's
     cycle by cycle."""
     faults = {f"{kind}{j}": 4.0 for j in range(2, 60, 5)}
-    a = _brain(True, algo, faults, device)
+    a = _brain(True, algo, faults, device, staged=staged)
     b = _brain(False, algo, faults, device)
     strat = "continuous" if kind == "continuous" else "hpa"
     extra = ["cpu", "latency", "error5xx", "memory"] if strat == "hpa" else None
@@ -458,14 +466,18 @@ def test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, devi
     f = a[3].fast
     assert f.arrivals_laid > 0 and f.extends > 0, (f.arrivals_laid, f.extends)
     assert (f.resubmits_patched if strat == "hpa" else f.revived) > 0, (f.resubmits_patched, f.revived)
+    if staged:                                                   # new rows' history written as grid blocks
+        assert f.sliding.dense_rows > 0
     if strat != "hpa":                                           # (HPA jobs stay alive)
         assert ST.COMPLETED_UNHEALTH in {a[1].get(j).status for j in ids}
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("algo,kind", [("holt_winters", "continuous"), ("lstm", "hpa")])
-def test_gpu_arrivals_and_departures_every_cycle_equal_general_path(algo, kind):
+@pytest.mark.parametrize("algo,kind,staged", [("holt_winters", "continuous", True), ("lstm", "hpa", True),
+                                              ("lstm", "hpa", False)])
+def test_gpu_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, staged):
     """The arrivals parity on the MI355X kernels: fused steady cycles, the
-    model cache, and (LSTM) the early forecast reused for the laid-out rows
-    with only the arrivals' rows forecast in the cycle."""
-    test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, device="cuda")
+    model cache, new rows' history as dense grid blocks, and (LSTM) the early
+    forecast reused for the laid-out rows with only the arrivals' rows
+    forecast in the cycle."""
+    test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, staged, device="cuda")
