@@ -82,15 +82,43 @@ def _convert(tp, v):
     return v
 
 
+def _str_or_none(v):
+    return v
+
+
+@functools.lru_cache(maxsize=None)
+def _converter(tp):
+    """The decoder of one field type, resolved once per type (``_convert``
+    re-inspected the type on every value: half of a job document's decode)."""
+    if tp is str or tp is Any:
+        return _str_or_none                     # JSON strings decode as themselves
+    origin = typing.get_origin(tp)
+    if origin is typing.Union:
+        non_none = [a for a in typing.get_args(tp) if a is not type(None)]
+        if not non_none:
+            return _str_or_none
+        inner = _converter(non_none[0])
+        return lambda v: None if v is None else inner(v)
+    if dataclasses.is_dataclass(tp):
+        return lambda v: None if v is None else (from_json(tp, v) if isinstance(v, dict) else tp())
+    if origin in (list, typing.List):
+        el = _converter(typing.get_args(tp)[0])
+        return lambda v: None if v is None else ([el(x) for x in v] if isinstance(v, list) else [])
+    if origin in (dict, typing.Dict):
+        el = _converter(typing.get_args(tp)[1])
+        return lambda v: None if v is None else ({k: el(x) for k, x in v.items()} if isinstance(v, dict) else {})
+    return lambda v: _convert(tp, v)
+
+
 @functools.lru_cache(maxsize=None)
 def _plan(cls) -> tuple:
-    """(attribute, json key, lower-cased key, type) per field — resolved once
-    per class (type-hint evaluation dominated decoding otherwise)."""
+    """(attribute, json key, lower-cased key, decoder) per field — resolved
+    once per class (type-hint evaluation dominated decoding otherwise)."""
     hints = typing.get_type_hints(cls)
     out = []
     for f in dataclasses.fields(cls):
         name = f.metadata.get("json", f.name)
-        out.append((f.name, name, name.lower(), hints[f.name]))
+        out.append((f.name, name, name.lower(), _converter(hints[f.name])))
     return tuple(out)
 
 
@@ -99,12 +127,12 @@ def from_json(cls, data: dict):
         return cls()
     kw = {}
     lower = None
-    for attr, name, lname, tp in _plan(cls):
+    for attr, name, lname, conv in _plan(cls):
         if name in data:
-            kw[attr] = _convert(tp, data[name])
+            kw[attr] = conv(data[name])
             continue
         if lower is None:   # case-insensitive fallback, built once per object
             lower = {k.lower(): v for k, v in data.items() if isinstance(k, str)}
         if lname in lower:
-            kw[attr] = _convert(tp, lower[lname])
+            kw[attr] = conv(lower[lname])
     return cls(**kw)

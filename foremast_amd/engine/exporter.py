@@ -32,6 +32,8 @@ shows how old), it never stalls rank 0's brain or scrape.
 """
 from __future__ import annotations
 
+import functools
+
 import ctypes
 import json
 import re
@@ -53,8 +55,10 @@ def sanitize(name: str) -> str:
     return n if not n[0].isdigit() else "_" + n
 
 
+@functools.lru_cache(maxsize=1 << 16)
 def _esc(v: str) -> str:
-    """Label-value escaping of the text exposition format."""
+    """Label-value escaping of the text exposition format (memoised: a job's
+    namespace and app appear in every one of its series)."""
     return v.replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
 
 

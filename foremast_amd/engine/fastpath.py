@@ -93,6 +93,8 @@ class FastPath(PlanMixin, FetchMixin, ArraysMixin, ModelsMixin, FinishMixin):
         self._col: dict = {}      # column-wise fetched windows of sliding groups (consumed by _arrays)
         self._ring = None         # merged sliding mode: host ring of the newest grid columns
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
+        self._fz: dict = {}        # group key -> the fused steady cycle's device / pinned buffers
+        self._hpa_dev: dict = {}   # group key -> HPA slot tensor + score buffers (fused HPA scoring)
         self._left: list = []      # sliding jobs released since the layout was laid (revival candidates)
         self._dense_ring: list = []  # (rows, t, v) newest columns of rows written as dense blocks this cycle
         self._slide_state: dict = {}

@@ -469,7 +469,26 @@ class FetchMixin:
             tpls, stores = lists[("hist_urls", m)], lists[("hist_stores", m)]
             since = st.last_t[rows[:, m]]
             fresh.append(rows[~np.isfinite(since), m])
-            lo = np.where(np.isfinite(since), since + step, math.ceil(hlo / step - 1e-9) * step)
+            have = np.isfinite(since)
+            lo = np.where(have, since + step, math.ceil(hlo / step - 1e-9) * step)
+            if len(lo) and not have.all() and have.any():
+                # arrivals: the new rows' whole window as one dense block when
+                # the source has one; then every row is fetched from the
+                # others' common start in one full-list call (the new rows'
+                # newest samples come again there, unchanged), no subsets
+                l_st = lo[have]
+                if l_st.min() == l_st.max():
+                    t_on = time.perf_counter()
+                    sel_f = np.flatnonzero(~have)
+                    sl = sel_f.tolist()
+                    pick = operator.itemgetter(*sl) if len(sl) > 1 else (lambda x, i=sl[0]: (x[i],))
+                    dense = self._columns_dense(TemplateList.subset(stores, list(pick(stores)), sel_f),
+                                                TemplateList.subset(tpls, list(pick(tpls)), sel_f),
+                                                float(lo[sel_f[0]]), hi)
+                    if dense is not None:
+                        self._write_fresh_dense(rows[sel_f, m], *dense)
+                        lo = np.full(len(lo), l_st[0])
+                    self.onboard_s += time.perf_counter() - t_on
             l0 = lo.min() if len(lo) else 0.0
             # every row at the same newest sample (the steady state): no sort
             starts = (l0,) if len(lo) and l0 == lo.max() else np.unique(lo)

@@ -257,11 +257,17 @@ class FinishMixin:
             # device (the fused band kernel wrote them), the hysteresis state
             # is updated in place through the slots -- one launch, one copy
             from ..ops._lib import LIB, ptr, stream_of
-            hs = getattr(ga, "_hpa_dev", None)
+            hs = self._hpa_dev.get(key)
             if hs is None or hs[0] is not sl_np:
-                hs = ga._hpa_dev = (sl_np, torch.as_tensor(sl_np, device=dev),
-                                    torch.empty((S,), dtype=torch.int32, device=dev),
-                                    torch.empty((S,), dtype=torch.int32).pin_memory())
+                old = hs
+                if old is not None and len(old[5]) >= S:           # reuse the buffers (arrivals grow S)
+                    hs = (sl_np, torch.as_tensor(sl_np, device=dev), old[4][:S], old[5][:S], old[4], old[5])
+                else:
+                    cap = S + max(S // 16, 64)
+                    bd, bh = torch.empty((cap,), dtype=torch.int32, device=dev), \
+                        torch.empty((cap,), dtype=torch.int32).pin_memory()
+                    hs = (sl_np, torch.as_tensor(sl_np, device=dev), bd[:S], bh[:S], bd, bh)
+                self._hpa_dev[key] = hs
             td = _hpa_tables(tmpl, dev)
             st = self.hpa.state
             LIB.call("fm_hpa_score_slots", ptr(last3[0]), ptr(last3[1]), ptr(last3[2]), S, M, *map(ptr, td),

@@ -428,16 +428,28 @@ class ModelsMixin:
         dev = self.b.device
         # per-row inputs that only change when the job list or the cache
         # slots do: uploaded once, kept on the arrays
-        fz = getattr(ga, "_fused", None)
-        if fz is None or fz["R"] != R or fz["n"] != n:
-            fz = {"R": R, "n": n, "slots": None, "t_new": None,
-                  "up": torch.empty((R, n), dtype=torch.float32, device=dev),
-                  "lo": torch.empty((R, n), dtype=torch.float32, device=dev),
-                  "sig": torch.empty((R,), dtype=torch.float32, device=dev),
-                  "hostv": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32, device=dev),
-                  "last3": torch.empty((3, R), dtype=torch.float32, device=dev) if p0.hpa else None,
-                  "host": torch.empty((S * 4 + R * 6 + 2,), dtype=torch.float32).pin_memory()}
-            ga._fused = fz
+        # (kept per group across cycles -- a sliding group's arrays are rebuilt
+        # every cycle -- with headroom, so arrivals grow them without a fresh
+        # device / pinned allocation per cycle)
+        fz = self._fz.get(ga.key)
+        if fz is None or fz["cap"] < R or fz["n"] != n or fz["hpa"] != bool(p0.hpa):
+            cap = R + max(R // 16, 256)
+            capS = cap // max(M, 1) + 1
+            nh = capS * 4 + cap * 6 + 2
+            fz = self._fz[ga.key] = {
+                "cap": cap, "n": n, "hpa": bool(p0.hpa), "slots": None, "t_new": None,
+                "up_": torch.empty((cap, n), dtype=torch.float32, device=dev),
+                "lo_": torch.empty((cap, n), dtype=torch.float32, device=dev),
+                "sig_": torch.empty((cap,), dtype=torch.float32, device=dev),
+                "hostv_": torch.empty((nh,), dtype=torch.float32, device=dev),
+                "last3_": torch.empty((3, cap), dtype=torch.float32, device=dev) if p0.hpa else None,
+                "host_": torch.empty((nh,), dtype=torch.float32).pin_memory()}
+        if fz.get("R") != R:
+            nv = S * 4 + R * 6 + 2
+            # ([3, R] rows R apart: a view of the first 3R floats)
+            fz.update(R=R, up=fz["up_"][:R], lo=fz["lo_"][:R], sig=fz["sig_"][:R], hostv=fz["hostv_"][:nv],
+                      host=fz["host_"][:nv],
+                      last3=fz["last3_"].view(-1)[:3 * R].view(3, R) if fz["last3_"] is not None else None)
         st = None
         if kind >= 0:
             t_new = (kmax - plan.knew).astype(np.int32)

@@ -84,8 +84,10 @@ class PlanMixin:
         for d in docs:
             urls.extend(_parse_config_cached(d.current_config).values())
             urls.extend(_parse_config_cached(d.baseline_config).values())
-        urls = list(dict.fromkeys(u for u in urls if u))
-        self._specs = dict(zip(urls, parse_ranges(urls)))
+        # a START_TIME / END_TIME template (continuous / HPA job) is never an
+        # absolute range: planning reads its metric from the query instead
+        urls = list(dict.fromkeys(u for u in urls if u and START_PLACEHOLDER not in u and END_PLACEHOLDER not in u))
+        self._specs = dict(zip(urls, parse_ranges(urls))) if urls else {}
 
     def _spec_of(self, url: str):
         from .ingest import parse_range

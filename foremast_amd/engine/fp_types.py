@@ -314,9 +314,14 @@ def _parse_config_cached(config: str) -> dict:
     return parse_config(config)
 
 
-def _label(q: str, name: str) -> str:
+@functools.lru_cache(maxsize=64)
+def _label_re(name: str):
     import re
-    m = re.search(r'(?<![\w])' + name + r'\s*=\s*"([^"]*)"', q or "")
+    return re.compile(r'(?<![\w])' + name + r'\s*=\s*"([^"]*)"')
+
+
+def _label(q: str, name: str) -> str:
+    m = _label_re(name).search(q or "")
     return m.group(1) if m else ""
 
 
