@@ -103,6 +103,7 @@ class ResidentHistory:
         self.bytes_in = 0
         self.max_len = 0                            # static: longest row written (view length)
         self.dense_rows = 0                         # sliding rows whose history arrived as one grid block
+        self._dense_pin = None                      # (pinned staging buffer, event of its last upload)
 
     # ------------------------------------------------------------------ rows
     def __len__(self) -> int:
@@ -357,11 +358,28 @@ class ResidentHistory:
         last = V.shape[1] - 1 - np.argmax(fin[:, ::-1], axis=1)
         self.nfin[rows] = cnt
         self.last_t[rows] = np.where(has, self.t0 + (a + last) * self.step, -np.inf)
-        blk = torch.from_numpy(np.ascontiguousarray(V, np.float32))
-        idx = torch.from_numpy(rows)
         if self.device.type == "cuda":
-            blk = blk.pin_memory().to(self.device, non_blocking=True)
-            idx = idx.to(self.device, non_blocking=True)
+            # one reusable pinned staging buffer (a pinned allocation per block
+            # costs more than the copy); the previous block's upload must have
+            # left it before it is refilled
+            o = (V.size + 1) // 2 * 2                # (the int64 rows start 8-byte aligned)
+            n = o + len(rows) * 2
+            st = self._dense_pin
+            if st is None or st[0].numel() < n:
+                st = self._dense_pin = (torch.empty((int(n * 1.25) + 1024,), dtype=torch.float32).pin_memory(),
+                                        torch.cuda.Event())
+            else:
+                st[1].synchronize()
+            hv = st[0][:V.size].numpy().reshape(V.shape)
+            np.copyto(hv, V, casting="unsafe")
+            hi = st[0][o:o + 2 * len(rows)].view(torch.int64).numpy()
+            hi[:] = rows
+            blk = st[0][:V.size].view(V.shape).to(self.device, non_blocking=True)
+            idx = st[0][o:o + 2 * len(rows)].view(torch.int64).to(self.device, non_blocking=True)
+            st[1].record()
+        else:
+            blk = torch.from_numpy(np.ascontiguousarray(V, np.float32))
+            idx = torch.from_numpy(rows)
         self.buf[idx, a:b] = blk
         self.bytes_in += blk.numel() * 4
         self.dense_rows += len(rows)
