@@ -444,8 +444,9 @@ def config3e2e(args):
         max(int(round(args.arrivals * S)), 0) if kind != "mixed"
         else sum(max(1, n_ // 200) for st_, _, _, _, n_ in classes if st_ == "canary"))
     t_pre = time.perf_counter()
-    pre_n = prestage_future(staged, classes, submit_one, range(S, S + n_future), t["now"], args.history_days,
-                            (n_cycles + 2) * poll + 3600.0, 0 if kind == "mixed" else None)
+    pre_n = 0 if args.no_prestage else prestage_future(
+        staged, classes, submit_one, range(S, S + n_future), t["now"], args.history_days,
+        (n_cycles + 2) * poll + 3600.0, 0 if kind == "mixed" else None)
     t_pre = time.perf_counter() - t_pre
     if pre_n:
         print(f"[{kind}] rank {info.rank}: pre-rendered {pre_n} series of {n_future} future jobs in {t_pre:.1f}s",
@@ -520,6 +521,31 @@ def config3e2e(args):
     if os.environ.get("FOREMAST_PROFILE_CYCLES"):
         import cProfile
         _prof = cProfile.Profile()
+
+    # --soak-every N: a long run's resources every N cycles
+    soak_rows: list = []
+    soak_ck = tempfile.mkdtemp(prefix="fm_soak_ck_") if args.soak_save_every else None
+
+    def soak_sample() -> dict:
+        import gc
+        import psutil
+        w = cyc_ms[-args.soak_every:]
+        dbs = {}
+        if args.store == "sqlite":
+            for suf in ("", "-wal", "-hpalogs", "-hpalogs-wal"):
+                pth = db + suf
+                dbs[suf or "jobs"] = os.path.getsize(pth) if os.path.exists(pth) else 0
+        fp = brain.fast
+        return {"cycle": len(cyc_ms), "rss_mb": round(psutil.Process().memory_info().rss / 2**20, 1),
+                "dev_alloc_mb": round(torch.cuda.memory_allocated(dev) / 2**20, 1) if dev.type == "cuda" else None,
+                "dev_reserved_mb": round(torch.cuda.memory_reserved(dev) / 2**20, 1) if dev.type == "cuda" else None,
+                "exporter_series": len(exp.table), "store_bytes": dbs,
+                "cycle_p50_ms": round(float(np.percentile(w, 50)), 3), "cycle_p99_ms": round(float(np.percentile(w, 99)), 3),
+                "fast_jobs": len(fp.works) if fp is not None else None,
+                "resident_rows": (len(fp.sliding) + len(fp.static)) if fp is not None else None,
+                "model_cache_entries": len(brain.model_cache),
+                "gc_counts": list(gc.get_count()), "gc_frozen": gc.get_freeze_count(),
+                "gc_tracked": len(gc.get_objects())}
 
     churn = {"next": S, "new": 0, "resub": 0}
     churn_client = None
@@ -609,6 +635,11 @@ def config3e2e(args):
             brain.flush_logs()             # the last timed cycle waits for the queued HPA log writes
         cyc_ms.append(1e3 * (time.perf_counter() - tc))
         gen_ms.append(1e3 * (staged.gen_s - gen0))
+        if args.soak_save_every and len(cyc_ms) % args.soak_save_every == 0:
+            brain.save_history(soak_ck, wait=False)      # the service loop's periodic async history save
+        if args.soak_every and len(cyc_ms) % args.soak_every == 0:
+            soak_rows.append(soak_sample())
+            print("[soak] " + _json.dumps(soak_rows[-1]), file=sys.stderr, flush=True)
         if brain.fast is not None:
             onboard.append((brain.fast.onboard_s - ob0[0], brain.fast.onboard_jobs - ob0[1]))
         rows.append(r.get("rows", 0))
@@ -889,6 +920,7 @@ def config3e2e(args):
                                   "lstm_early_launch_extended": brain.fast.prelaunch_extended,
                                   "ghost_cycles": brain.fast.ghost_cycles} if brain.fast is not None else None),
              "prerendered_future_series": pre_n,
+             "soak": soak_rows or None,
              "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),
              "submit_s": round(t_sub, 3),
              "fast_jobs_first_cycle": first.get("fast_jobs"), "device": str(dev)})
@@ -1016,6 +1048,12 @@ def main():
                     "instead of the native responder")
     ap.add_argument("--scrape-interval", type=float, default=0.0, help="config 3e2e: render rank 0's /metrics "
                     "body every N seconds in a thread while the cycles are timed (0: off)")
+    ap.add_argument("--soak-every", type=int, default=0, help="e2e configs: record RSS, device memory, exporter "
+                    "series, store file sizes and cycle p50/p99 every N cycles (a soak run)")
+    ap.add_argument("--soak-save-every", type=int, default=0, help="e2e configs: an asynchronous history checkpoint "
+                    "every N cycles (the service loop's cadence)")
+    ap.add_argument("--no-prestage", action="store_true", help="e2e configs: do not pre-render the arriving jobs' "
+                    "series (long soak runs: the source serves them when asked)")
     ap.add_argument("--arrivals", type=float, default=0.0, help="e2e single-class configs: fraction of --services "
                     "submitted as NEW jobs (new services) every timed cycle")
     ap.add_argument("--resubmit", type=float, default=0.0, help="e2e single-class configs: fraction of --services "

@@ -463,11 +463,35 @@ class Brain:
             # a cycle that planned a fleet leaves ~10^6 long-lived objects
             # (plans, keys, window maps): moved out of the collector's
             # generations, so a later full collection does not walk them in
-            # the middle of a steady cycle (100s of ms at a 10k-job fleet)
-            import gc
-            gc.freeze()
+            # the middle of a steady cycle (100s of ms at a 10k-job fleet).
+            # Frozen once after the first such cycle; a later one (a shard
+            # moved in, a re-plan after a restart) first thaws and collects
+            # what the earlier freeze kept (cyclic garbage of retired plans
+            # would otherwise stay forever), in a cycle that is slow anyway
+            self.gc_maintenance(refreeze=True)
         return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast) - (len(self.fast.ghost_ids) if fast and self.fast.ghost_mask(fast) is not None else 0),
                 "seconds": time.perf_counter() - t0}
+
+    GC_IDLE_EVERY_S = 600.0
+
+    def gc_maintenance(self, refreeze: bool = False, idle: bool = False) -> None:
+        """The collector's care of the frozen (permanent) generation:
+        ``refreeze`` (a big planning cycle): thaw + full collection if a
+        freeze is in place, then freeze; ``idle`` (the loop has nothing
+        claimed): the same at most every GC_IDLE_EVERY_S, so garbage of
+        jobs that closed since the last freeze is reclaimed off the cycles."""
+        import gc
+        now = time.monotonic()
+        frozen = getattr(self, "_gc_frozen_at", None)
+        if idle and (frozen is None or now - frozen < self.GC_IDLE_EVERY_S):
+            return
+        if frozen is not None:
+            gc.unfreeze()
+            gc.collect()
+            self.gc_collections = getattr(self, "gc_collections", 0) + 1
+        if refreeze or frozen is not None:
+            gc.freeze()
+            self._gc_frozen_at = now
 
     def _write_hpalogs(self, hpalogs: list) -> None:
         """HPA logs into the store: inline, or (``hpalog_async``) queued to one
@@ -685,6 +709,7 @@ class Brain:
                         hist_t = time.monotonic()
                     self._hist_pump(None)          # between cycles: the rest of a save's host copy
                     if r.get("claimed", 0) == 0:
+                        self.gc_maintenance(idle=True)      # idle tick: the frozen generation's care
                         (stop.wait(poll) if stop is not None else time.sleep(poll))
                 except Exception:
                     log.exception("brain cycle failed")

@@ -1,0 +1,35 @@
+"""The brain's care of the collector's frozen generation:
+frozen once after the first fleet-sized planning cycle; a later one, or an
+idle tick at most every GC_IDLE_EVERY_S, thaws it, runs a full collection
+(cyclic garbage of jobs that closed since) and freezes again."""
+import gc
+
+from foremast_amd.config import BrainConfig
+from foremast_amd.engine.brain import Brain
+from foremast_amd.engine.sources import SourceRouter
+from foremast_amd.service.store import MemoryStore
+
+
+class _Cyc:
+    def __init__(self):
+        self.me = self
+
+
+def test_gc_freeze_is_maintained_not_repeated():
+    b = Brain(MemoryStore(), BrainConfig(), sources=SourceRouter.synthetic_only())
+    try:
+        b.gc_maintenance(idle=True)                  # nothing frozen yet: no-op
+        assert getattr(b, "gc_collections", 0) == 0 and getattr(b, "_gc_frozen_at", None) is None
+        b.gc_maintenance(refreeze=True)              # the first big planning cycle
+        assert gc.get_freeze_count() > 0 and getattr(b, "gc_collections", 0) == 0
+        garbage = [_Cyc() for _ in range(100)]       # cycles created after the freeze ...
+        del garbage
+        b.gc_maintenance(idle=True)                  # ... an idle tick inside the interval: no collection
+        assert getattr(b, "gc_collections", 0) == 0
+        b._gc_frozen_at -= b.GC_IDLE_EVERY_S + 1     # interval passed
+        b.gc_maintenance(idle=True)
+        assert b.gc_collections == 1 and gc.get_freeze_count() > 0
+        b.gc_maintenance(refreeze=True)              # a later big planning cycle: thaw, collect, freeze
+        assert b.gc_collections == 2
+    finally:
+        gc.unfreeze()
