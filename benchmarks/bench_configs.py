@@ -637,6 +637,10 @@ def config3e2e(args):
         gen_ms.append(1e3 * (staged.gen_s - gen0))
         if args.soak_save_every and len(cyc_ms) % args.soak_save_every == 0:
             brain.save_history(soak_ck, wait=False)      # the service loop's periodic async history save
+        if args.soak_every and len(cyc_ms) % 10 == 0:          # heartbeat (a long run keeps writing)
+            print(f"[cycle] {len(cyc_ms)} {cyc_ms[-1]:.1f} ms spans "
+                  f"{ {k: round(v * 1e3, 1) for k, v in brain.spans.last.items() if v >= 5e-3} }",
+                  file=sys.stderr, flush=True)
         if args.soak_every and len(cyc_ms) % args.soak_every == 0:
             soak_rows.append(soak_sample())
             print("[soak] " + _json.dumps(soak_rows[-1]), file=sys.stderr, flush=True)

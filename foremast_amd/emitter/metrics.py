@@ -47,6 +47,7 @@ class K8sMetricsProperties:
     common_tag_name_value_pairs: str = "app:ENV.APP_NAME|info.app.name"
     initialize_for_statuses: str = "403,404,500,503"
     caller_header: str = "X-CALLER"
+    caller_default: str = "UNKNOWN"        # caller tag of a request without the header (reference default)
     enable_common_metrics_filter: bool = False
     enable_common_metrics_filter_action: bool = False
     common_metrics_whitelist: str | None = None
@@ -67,6 +68,7 @@ class K8sMetricsProperties:
         m = {"K8S_METRICS_COMMON_TAG_NAME_VALUE_PAIRS": "common_tag_name_value_pairs",
              "K8S_METRICS_INITIALIZE_FOR_STATUSES": "initialize_for_statuses",
              "K8S_METRICS_CALLER_HEADER": "caller_header",
+             "K8S_METRICS_CALLER_DEFAULT": "caller_default",
              "K8S_METRICS_COMMON_METRICS_WHITELIST": "common_metrics_whitelist",
              "K8S_METRICS_COMMON_METRICS_BLACKLIST": "common_metrics_blacklist",
              "K8S_METRICS_COMMON_METRICS_PREFIX": "common_metrics_prefix",
@@ -256,7 +258,7 @@ class K8sMetrics:
     def _key(self, method: str, uri: str, status, caller: str, exception: str) -> tuple:
         vals = dict(self.common, exception=exception, method=method, status=str(status), uri=uri)
         if self.with_caller:
-            vals["caller"] = caller or ""
+            vals["caller"] = caller or self.props.caller_default
         return tuple(vals[k] for k in self.labels)
 
     def record(self, method: str, uri: str, status: int | str, seconds: float, caller: str = "",

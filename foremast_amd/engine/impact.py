@@ -36,6 +36,12 @@ import logging
 log = logging.getLogger("foremast.brain.impact")
 
 
+# caller tag values that name no service: the emitters' value for a request
+# without the caller header ("UNKNOWN", the reference's
+# CallerWebMvcTagsProvider.java:14) and the pre-initialised error timers' "*"
+NOT_A_CALLER = frozenset({"UNKNOWN", "*"})
+
+
 def graph_from_caller_series(series: list[tuple[str, str, float]], services: list[str]) -> CallGraph:
     """``series`` = (app, caller, request_rate) triples (emitter label set);
     ``services`` fixes the global id order.  Unknown callers are ignored."""
@@ -43,7 +49,7 @@ def graph_from_caller_series(series: list[tuple[str, str, float]], services: lis
     out_rate: dict[int, float] = {}
     edges = []
     for app, caller, rate in series:
-        if not caller or caller not in idx or app not in idx or caller == app:
+        if not caller or caller in NOT_A_CALLER or caller not in idx or app not in idx or caller == app:
             continue
         u, v = idx[caller], idx[app]
         edges.append((u, v, float(rate)))
@@ -193,7 +199,7 @@ class DownstreamImpact:
         for s in ss:
             lb = s.labels or {}
             v = s.values[np.isfinite(s.values)] if len(s.values) else s.values
-            if not len(v) or not lb.get("caller") or not lb.get("app"):
+            if not len(v) or not lb.get("caller") or lb["caller"] in NOT_A_CALLER or not lb.get("app"):
                 continue
             ns = lb.get("namespace", lb.get("exported_namespace", ""))
             out.append((lb.get("cluster", ""), ns, lb["app"], lb["caller"], lb.get("caller_namespace", ns),

@@ -27,7 +27,10 @@ import java.util.Map;
  *       (403, 404, 500, 503 by default), so an error-rate rule sees 0, not no
  *       series;</li>
  *   <li>JVM memory / GC / thread and CPU binders (the rules' jvm_* and cpu
- *       series).</li>
+ *       series); Tomcat session meters through {@link ForemastMetricsListener};</li>
+ *   <li>the common-metrics gate ({@link CommonMetricsGate}: whitelist,
+ *       blacklist, prefixes, tag rules, runtime enable / disable through
+ *       {@link MetricsControlServlet}).</li>
  * </ul>
  * {@link PrometheusScrapeServlet} exposes it.  Same names and tags as the Boot 2
  * starter and foremast_amd/emitter/metrics.py.
@@ -40,9 +43,14 @@ public final class ForemastMetrics {
 
     private final PrometheusMeterRegistry registry;
     private final String callerHeader;
+    private final String callerDefault;
+    private final CommonMetricsGate gate;
 
     public ForemastMetrics(Map<String, String> settings) {
         this.registry = new PrometheusMeterRegistry(PrometheusConfig.DEFAULT);
+        // the common-metrics gate sees every meter: registered before any
+        this.gate = new CommonMetricsGate(settings);
+        registry.config().meterFilter(gate);
         List<Tag> common = new ArrayList<>();
         String app = first(System.getenv("APP_NAME"), settings.get("app"));
         if (app != null) {
@@ -50,6 +58,9 @@ public final class ForemastMetrics {
         }
         registry.config().commonTags(common);
         this.callerHeader = first(settings.get("callerHeader"), "X-CALLER");
+        // a request without the caller header: the reference's "UNKNOWN"
+        // (CallerWebMvcTagsProvider.java:14), configurable
+        this.callerDefault = first(settings.get("callerDefault"), "UNKNOWN");
         registry.config().meterFilter(new io.micrometer.core.instrument.config.MeterFilter() {
             @Override
             public io.micrometer.core.instrument.distribution.DistributionStatisticConfig configure(
@@ -99,6 +110,14 @@ public final class ForemastMetrics {
 
     public String callerHeader() {
         return callerHeader;
+    }
+
+    public String callerDefault() {
+        return callerDefault;
+    }
+
+    public CommonMetricsGate gate() {
+        return gate;
     }
 
     static String first(String a, String b) {

@@ -20,9 +20,11 @@ import java.util.Map;
  * foremast rules and the downstream-impact graph read: method, uri (the
  * handler's path pattern when Spring MVC set one, else root / NOT_FOUND /
  * REDIRECTION / UNKNOWN, never a raw path: one series per route, not per
- * id), status, outcome, exception, caller (the caller header, "*" when
- * absent).  Init parameters (web.xml / FilterRegistration): {@code app},
- * {@code callerHeader}, {@code initializeForStatuses}, {@code jvmMetrics}.
+ * id), status, outcome, exception, caller (the caller header; {@code
+ * callerDefault}, "UNKNOWN" unless set, when absent).  Init parameters
+ * (web.xml / FilterRegistration): {@code app}, {@code callerHeader},
+ * {@code callerDefault}, {@code initializeForStatuses}, {@code jvmMetrics},
+ * and the common-metrics gate's ({@link CommonMetricsGate}).
  * Async requests are recorded when they complete.
  */
 public class HttpRequestsFilter implements Filter {
@@ -78,7 +80,7 @@ public class HttpRequestsFilter implements Filter {
                 .tags("method", req.getMethod(), "uri", uri(req, status), "status", Integer.toString(status),
                       "outcome", outcome(status),
                       "exception", failure == null ? "None" : failure.getClass().getSimpleName(),
-                      "caller", caller == null || caller.trim().isEmpty() ? "*" : caller.trim())
+                      "caller", caller == null || caller.trim().isEmpty() ? metrics.callerDefault() : caller.trim())
                 .register(metrics.registry()));
     }
 

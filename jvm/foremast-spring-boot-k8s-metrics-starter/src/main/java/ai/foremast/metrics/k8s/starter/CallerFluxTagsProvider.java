@@ -8,16 +8,19 @@ import org.springframework.web.server.ServerWebExchange;
 /**
  * The reactive (WebFlux) twin of {@link CallerTagsProvider}: the default
  * {@code http.server.requests} tags of a WebFlux server plus {@code caller},
- * the caller header's value ("*" when the request carries none), so the
+ * the caller header's value ({@code k8s.metrics.caller-default}, "UNKNOWN",
+ * when the request carries none), so the
  * downstream-impact graph (foremast_amd/engine/impact.py) also sees the
  * edges of reactive services.  An empty header name turns the tag off.
  */
 public class CallerFluxTagsProvider extends DefaultWebFluxTagsProvider {
 
     private final String header;
+    private final String absent;
 
-    public CallerFluxTagsProvider(String header) {
+    public CallerFluxTagsProvider(String header, String absent) {
         this.header = header;
+        this.absent = absent == null || absent.trim().isEmpty() ? "UNKNOWN" : absent.trim();
     }
 
     @Override
@@ -27,6 +30,6 @@ public class CallerFluxTagsProvider extends DefaultWebFluxTagsProvider {
             return tags;
         }
         String caller = exchange == null ? null : exchange.getRequest().getHeaders().getFirst(header);
-        return tags.and("caller", caller == null || caller.trim().isEmpty() ? "*" : caller.trim());
+        return tags.and("caller", caller == null || caller.trim().isEmpty() ? absent : caller.trim());
     }
 }

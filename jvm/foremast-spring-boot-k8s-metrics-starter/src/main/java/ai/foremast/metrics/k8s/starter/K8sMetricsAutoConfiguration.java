@@ -145,7 +145,7 @@ public class K8sMetricsAutoConfiguration {
         @Bean
         @ConditionalOnMissingBean(org.springframework.boot.actuate.metrics.web.servlet.WebMvcTagsProvider.class)
         public CallerTagsProvider foremastCallerTags(K8sMetricsProperties props) {
-            return new CallerTagsProvider(props.getCallerHeader());
+            return new CallerTagsProvider(props.getCallerHeader(), props.getCallerDefault());
         }
 
         /** {@code GET /metrics} forwarded to the actuator's Prometheus scrape. */
@@ -177,7 +177,7 @@ public class K8sMetricsAutoConfiguration {
         @Bean
         @ConditionalOnMissingBean(org.springframework.boot.actuate.metrics.web.reactive.server.WebFluxTagsProvider.class)
         public CallerFluxTagsProvider foremastCallerFluxTags(K8sMetricsProperties props) {
-            return new CallerFluxTagsProvider(props.getCallerHeader());
+            return new CallerFluxTagsProvider(props.getCallerHeader(), props.getCallerDefault());
         }
 
         /** {@code GET /metrics} served by the actuator's Prometheus scrape (path rewrite). */

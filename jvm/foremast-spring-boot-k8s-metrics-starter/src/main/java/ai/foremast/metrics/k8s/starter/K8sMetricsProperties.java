@@ -19,6 +19,9 @@ public class K8sMetricsProperties {
     /** Header carrying the calling service; its value becomes the {@code caller} tag (empty: no tag). */
     private String callerHeader = "X-CALLER";
 
+    /** The caller tag of a request without the caller header (the reference's "UNKNOWN"). */
+    private String callerDefault = "UNKNOWN";
+
     /** Hide every meter that is not enabled explicitly, whitelisted, prefixed or tag-matched. */
     private boolean enableCommonMetricsFilter = false;
 
@@ -43,6 +46,8 @@ public class K8sMetricsProperties {
     public void setInitializeForStatuses(String v) { initializeForStatuses = v; }
     public String getCallerHeader() { return callerHeader; }
     public void setCallerHeader(String v) { callerHeader = v; }
+    public String getCallerDefault() { return callerDefault; }
+    public void setCallerDefault(String v) { callerDefault = v; }
     public boolean isEnableCommonMetricsFilter() { return enableCommonMetricsFilter; }
     public void setEnableCommonMetricsFilter(boolean v) { enableCommonMetricsFilter = v; }
     public boolean isEnableCommonMetricsFilterAction() { return enableCommonMetricsFilterAction; }

@@ -108,7 +108,7 @@ def test_demo_app_endpoints_and_metrics():
     app.queue.drain_quarter()
     assert len(app.queue.items) == n - n // 4
     text = c.get("/actuator/prometheus").text
-    assert ('http_server_requests_seconds_count{app="demo",caller="",exception="None",method="GET",status="501",'
+    assert ('http_server_requests_seconds_count{app="demo",caller="UNKNOWN",exception="None",method="GET",status="501",'
             'uri="/load"}') in text
     assert "k8s_metrics_demo_queue_size" in text
 

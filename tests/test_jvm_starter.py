@@ -72,7 +72,7 @@ def test_environment_post_processor_and_reactive_pieces_registered():
     flux = (SRC / "CallerFluxTagsProvider.java").read_text()
     mvc = (SRC / "CallerTagsProvider.java").read_text()
     for src in (flux, mvc):                         # the same caller default as the Python emitter
-        assert '"caller"' in src and '"*"' in src
+        assert '"caller"' in src and '"UNKNOWN"' in src
     auto = (SRC / "K8sMetricsAutoConfiguration.java").read_text()
     assert "CallerFluxTagsProvider" in auto and "Type.REACTIVE" in auto
 
@@ -89,3 +89,91 @@ def test_servlet_module_emits_the_starter_series():
         assert f'"{key}"' in filt
     assert '"http.server.requests"' in fm and '"http.server.requests"' in auto
     assert '"403,404,500,503"' in fm and "0.95, 0.98" in fm and "0.95, 0.98" in auto
+
+
+VECTORS = (Path(__file__).resolve().parent.parent / "jvm" / "foremast-servlet-k8s-metrics" / "src" / "test"
+           / "resources" / "gate-vectors.txt")
+_SETTING = {"enableCommonMetricsFilter": ("enable_common_metrics_filter", lambda v: v.strip().lower() == "true"),
+            "enableCommonMetricsFilterAction": ("enable_common_metrics_filter_action",
+                                                lambda v: v.strip().lower() == "true"),
+            "commonMetricsWhitelist": ("common_metrics_whitelist", str),
+            "commonMetricsBlacklist": ("common_metrics_blacklist", str),
+            "commonMetricsPrefix": ("common_metrics_prefix", str),
+            "commonMetricsTagRules": ("common_metrics_tag_rules", str)}
+
+
+def _cases():
+    cases, cur = [], None
+    for raw in VECTORS.read_text().splitlines():
+        ln = raw.strip()
+        if not ln or ln.startswith("#"):
+            continue
+        if ln.startswith("case "):
+            cur = {"name": ln[5:], "set": {}, "steps": []}
+            cases.append(cur)
+        elif ln.startswith("set "):
+            k, _, v = ln[4:].partition("=")
+            cur["set"][k.strip()] = v
+        else:
+            cur["steps"].append(ln)
+    return cases
+
+
+def test_servlet_gate_decisions_equal_python_filter():
+    """the servlet module's common-metrics gate
+    (CommonMetricsGate.java, run over gate-vectors.txt by CommonMetricsGateTest
+    under Maven) and the Python emitter's CommonMetricsFilter decide the SAME
+    table here -- whitelist, blacklist, prefixes, tag rules, the
+    management.metrics.enable.* precedence and runtime enable / disable."""
+    import pytest
+    cases = _cases()
+    assert len(cases) == 6
+    for c in cases:
+        p = EM.K8sMetricsProperties()
+        for k, v in c["set"].items():
+            if k.startswith("enable."):
+                p.enable[k[len("enable."):]] = v.strip().lower() == "true"
+            else:
+                attr, conv = _SETTING[k]
+                setattr(p, attr, conv(v))
+        if "error" in c["steps"]:
+            with pytest.raises(ValueError):
+                EM.CommonMetricsFilter(p)
+            continue
+        f = EM.CommonMetricsFilter(p)
+        for s in c["steps"]:
+            lhs, want = (x.strip() for x in s.split("->"))
+            w = lhs.split()
+            if w[0] == "check":
+                tags = dict(t.split("=", 1) for t in w[2:])
+                assert f.accept(w[1], tags) == want, (c["name"], s)
+            elif w[0] == "enable":
+                assert f.enable_metric(w[1]) == (want == "true"), (c["name"], s)
+            elif w[0] == "disable":
+                assert f.disable_metric(w[1]) == (want == "true"), (c["name"], s)
+            else:
+                raise AssertionError(f"unknown step {s}")
+    # the Java test reads the same file (classpath resource of the module)
+    jt = (VECTORS.parent.parent / "java" / "ai" / "foremast" / "metrics" / "servlet" / "CommonMetricsGateTest.java")
+    assert '"/gate-vectors.txt"' in jt.read_text()
+
+
+def test_caller_default_is_the_reference_unknown_everywhere():
+    """A request without the caller header is tagged caller="UNKNOWN" (the
+    reference's CallerWebMvcTagsProvider.java:14), configurable, in the servlet
+    module, the Boot 2 starter and the Python emitter; the impact graph never
+    takes UNKNOWN or "*" for a service."""
+    servlet = (ROOT.parent / "foremast-servlet-k8s-metrics" / "src" / "main" / "java" / "ai" / "foremast"
+               / "metrics" / "servlet")
+    assert 'first(settings.get("callerDefault"), "UNKNOWN")' in (servlet / "ForemastMetrics.java").read_text()
+    assert "metrics.callerDefault()" in (servlet / "HttpRequestsFilter.java").read_text()
+    assert EM.K8sMetricsProperties().caller_default == "UNKNOWN"
+    m = EM.K8sMetrics(EM.K8sMetricsProperties(initialize_for_statuses=""), env={"APP_NAME": "a"})
+    m.record("GET", "/x", 200, 0.01, caller="")
+    m.record("GET", "/x", 200, 0.01, caller="billing")
+    from prometheus_client import generate_latest
+    text = generate_latest(m.registry).decode()
+    assert 'caller="UNKNOWN"' in text and 'caller="billing"' in text
+    from foremast_amd.engine.impact import graph_from_caller_series
+    g = graph_from_caller_series([("a", "UNKNOWN", 1.0), ("a", "*", 1.0), ("a", "b", 1.0)], ["a", "b", "UNKNOWN", "*"])
+    assert g.col.size == 1
