@@ -390,7 +390,9 @@ def config3e2e(args):
         st_, _, al_, _, _ = classes[c]
         pods = ([[f"svc{j}-7687b9f4d7-p{k:04d}" for k in range(P)],
                  [f"svc{j}-5db89899b5-q{k:04d}" for k in range(P)]] if st_ == "canary" else None)
-        w_ = args.window if st_ == "canary" and kind != "mixed" else long_window
+        # (a soak run: canaries keep the 10-minute watch window and close on
+        # their own, so the canary class churns in both directions)
+        w_ = args.window if st_ == "canary" and (kind != "mixed" or args.soak_every) else long_window
         return client.start_analyzing("default", f"svc{j}", pods, metrics_of[c], w_, st_,
                                       al_ if st_ == "hpa" else None)
 

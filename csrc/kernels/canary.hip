@@ -1085,13 +1085,17 @@ __device__ unsigned long long g_front_t[2 * 8192];
 #define FM_FT_MARK(k) do {} while (0)
 #endif
 
-template <int NV, int K, bool PRIO = false>
-__global__ __launch_bounds__(256) void tick_front_kernel(
-    const float* __restrict__ hist, int64_t ld_h, int T, int64_t R, float* __restrict__ hs /*[R,3]*/,
-    const float* __restrict__ cur, int64_t ld_c, int n_cur, const float* __restrict__ base, int64_t ld_b,
-    int n_base, double* __restrict__ suff, int nP, int min_mw, int min_wil, int min_kru,
-    float* __restrict__ pvals, float* __restrict__ pstats, unsigned* __restrict__ queue,
-    const int* __restrict__ rowmap) {
+#define FM_FRONT_PARAMS                                                                                        \
+  const float *__restrict__ hist, int64_t ld_h, int T, int64_t R, float *__restrict__ hs /*[R,3]*/,            \
+      const float *__restrict__ cur, int64_t ld_c, int n_cur, const float *__restrict__ base, int64_t ld_b,    \
+      int n_base, double *__restrict__ suff, int nP, int min_mw, int min_wil, int min_kru,                     \
+      float *__restrict__ pvals, float *__restrict__ pstats, unsigned *__restrict__ queue,                    \
+      const int *__restrict__ rowmap
+#define FM_FRONT_ARGS hist, ld_h, T, R, hs, cur, ld_c, n_cur, base, ld_b, n_base, suff, nP, min_mw, min_wil, \
+      min_kru, pvals, pstats, queue, rowmap
+
+template <int NV, int K, bool PRIO>
+__device__ __forceinline__ void tick_front_body(FM_FRONT_PARAMS) {
   __shared__ double red[4];
   __shared__ int redi[4];
   FM_FT_MARK(0);
@@ -1195,6 +1199,28 @@ __global__ __launch_bounds__(256) void tick_front_kernel(
   FM_FT_MARK(1);
 }
 
+template <int NV, int K, bool PRIO = false>
+__global__ __launch_bounds__(256) void tick_front_kernel(FM_FRONT_PARAMS) {
+  tick_front_body<NV, K, PRIO>(FM_FRONT_ARGS);
+}
+
+// The same kernel held to 5 waves per SIMD (96 VGPRs: the rest spills): one
+// pairwise + four history workgroups per CU instead of one + three at the
+// default 111 VGPRs.  FM_FRONT_OCC=5 selects it (A/B on one box).
+template <int NV, int K, bool PRIO = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void tick_front_kernel_o5(
+    FM_FRONT_PARAMS) {
+  tick_front_body<NV, K, PRIO>(FM_FRONT_ARGS);
+}
+
+static int front_occ() {
+  static const int occ = [] {
+    const char* e = getenv("FM_FRONT_OCC");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  return occ;
+}
+
 // FM_FRONT_PRIO=1 (environment, read once): A/B of wave priorities in the
 // front kernel (tools: bench.py with and without it on one box).
 static bool front_prio() {
@@ -1226,6 +1252,9 @@ FM_API int fm_tick_front_rm(const float* hist, int64_t ld_h, int T, int64_t R, f
 #define FM_TF(NVV, KK)                                                                                             \
   if (front_prio())                                                                                                 \
     hipLaunchKernelGGL((tick_front_kernel<NVV, KK, true>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c,  \
+                       n_cur, base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap); \
+  else if (front_occ() == 5)                                                                                         \
+    hipLaunchKernelGGL((tick_front_kernel_o5<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c,     \
                        n_cur, base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap); \
   else                                                                                                               \
   hipLaunchKernelGGL((tick_front_kernel<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c, n_cur, \
