@@ -319,6 +319,10 @@ def config3e2e(args):
 
     info, dev = setup(gpus_required=args.device != "cpu")
     dev = torch.device("cpu") if args.device == "cpu" else dev
+    exchange = "mailbox" if D.is_dist() else None
+    if args.board and D.is_dist() and dev.type == "cuda":
+        from foremast_amd.parallel import board as _board
+        exchange = "board" if _board.setup(dev) is not None else "mailbox (board self-test failed)"
     kind = args.config
     strategy, algo, m_default, poll_default, names = E2E[kind]
     S, P = args.services, args.pods
@@ -926,6 +930,7 @@ def config3e2e(args):
                                   "lstm_early_launch_extended": brain.fast.prelaunch_extended,
                                   "ghost_cycles": brain.fast.ghost_cycles} if brain.fast is not None else None),
              "prerendered_future_series": pre_n,
+             "rank_exchange": exchange, "world": info.world,
              "soak": soak_rows or None,
              "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),
              "submit_s": round(t_sub, 3),
@@ -1060,6 +1065,9 @@ def main():
                     "every N cycles (the service loop's cadence)")
     ap.add_argument("--no-prestage", action="store_true", help="e2e configs: do not pre-render the arriving jobs' "
                     "series (long soak runs: the source serves them when asked)")
+    ap.add_argument("--board", action="store_true", help="e2e configs, several ranks on a GPU node: the ranks' "
+                    "gauge / verdict exchange over the device board (parallel/board.py, as `foremast brain` sets "
+                    "it up) instead of the TCPStore mailbox")
     ap.add_argument("--arrivals", type=float, default=0.0, help="e2e single-class configs: fraction of --services "
                     "submitted as NEW jobs (new services) every timed cycle")
     ap.add_argument("--resubmit", type=float, default=0.0, help="e2e single-class configs: fraction of --services "

@@ -5,6 +5,7 @@ ONE JSON line."""
 from __future__ import annotations
 
 import json
+import os
 import statistics
 import time
 from typing import Callable
@@ -17,7 +18,10 @@ from foremast_amd.parallel import dist as D
 def setup(gpus_required: bool = True):
     info = D.env_info()
     if torch.cuda.is_available():
-        dev = torch.device("cuda", info.local_rank)
+        # FOREMAST_SHARE_GPU=1: several ranks per GPU (rehearsals on a 1-GPU
+        # box, with FOREMAST_DIST_BACKEND=gloo -- RCCL wants one rank per GPU)
+        share = os.environ.get("FOREMAST_SHARE_GPU", "0") not in ("0", "")
+        dev = torch.device("cuda", info.local_rank % torch.cuda.device_count() if share else info.local_rank)
         torch.cuda.set_device(dev)
     else:
         if gpus_required:

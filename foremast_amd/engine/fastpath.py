@@ -95,8 +95,8 @@ class FastPath(PlanMixin, FetchMixin, ArraysMixin, ModelsMixin, FinishMixin):
         self._ring_top = None     # newest grid column the ring holds (older slots cleared as it advances)
         self._fz: dict = {}        # group key -> the fused steady cycle's device / pinned buffers
         self._hpa_dev: dict = {}   # group key -> HPA slot tensor + score buffers (fused HPA scoring)
-        self._left: list = []
-        self._sigs: dict = {}      # FastWork serial -> plan signature (revival lookups)      # sliding jobs released since the layout was laid (revival candidates)
+        self._left: list = []      # sliding jobs released since the layout was laid (revival candidates)
+        self._sigs: dict = {}      # FastWork serial -> plan signature (revival lookups)
         self._dense_ring: list = []  # (rows, t, v) newest columns of rows written as dense blocks this cycle
         self._slide_state: dict = {}
         self._flat_rows = None     # (row map [S, M] object, flat int64 rows, slice when they are one run)

@@ -461,7 +461,7 @@ class FetchMixin:
         step = b.step
         wins = b._windows(ws[0].doc, now)
         ids, lists, rows = memo[0], memo[1], memo[2]
-        hlo = wins["historical"][0]
+        hlo, hlo_end = wins["historical"]
         hi = math.floor(now / step + 1e-9) * step
         wr, wt, wv = [], [], []
         fresh = []                                # rows without a sample yet: empty ring rows
@@ -528,14 +528,14 @@ class FetchMixin:
             r, t, v = (np.concatenate(wr), np.concatenate(wt), np.concatenate(wv)) if wr else \
                 (np.zeros(0, np.int64), np.zeros(0), np.zeros(0, np.float32))
             st.write_sliding_flat(r, t, v)
-            self._prelaunch(p0.group)                 # the grid holds this cycle's samples
+            self._prelaunch(p0.group, rows, hlo_end)  # the grid holds this cycle's samples
             if dense:                                 # + the newest columns of rows written as blocks
                 r = np.concatenate([r] + [x[0] for x in dense])
                 t = np.concatenate([t] + [x[1] for x in dense])
                 v = np.concatenate([v] + [x[2] for x in dense])
             self._ring_write(r, t, v, fresh_rows)
         else:
-            self._prelaunch(p0.group)
+            self._prelaunch(p0.group, rows, hlo_end)
         fc = self._flat_rows
         if fc is None or fc[0] is not rows:
             flat = rows.reshape(-1).astype(np.int64)

@@ -509,7 +509,13 @@ class ModelsMixin:
                 "packed": packed_h, "stats": stats_h, "count": count_h, "anom": idx, "anom_band": band,
                 "hist_rows": ga.rowmap, "store": store, "pts": (fz["up"], fz["lo"]), "last3": fz["last3"]}
 
-    def _prelaunch(self, group: tuple) -> None:
+    def _prelaunch(self, group: tuple, rows=None, hist_end=None) -> None:
+        """The group's LSTM forecast launched as soon as the grid holds this
+        cycle's samples (during the fetch), from last cycle's arrays shifted
+        by the window's slide.  Jobs appended to the laid-out list since
+        (arrivals: ``rows`` [S, M] extends last cycle's row map) join the SAME
+        launch, their rows right-aligned like the score path will align them
+        -- one recurrence per cycle, not a second one for the new rows."""
         spec = self._pre_spec.get(group)
         self._pre.pop(group, None)
         skip = self._pre_skip.get(group)
@@ -524,8 +530,25 @@ class ModelsMixin:
         if k < 0 or not st.buf.is_cuda:
             return
         dk = int(sub.dk) + k
-        fc, sig = lstm.forecast_rows(st.buf, sub.rm, sub.shift, sub.lim, dk, sub.T, H)
-        self._pre[group] = (sub.rm, dk, sub.T, H, lstm, self.cycle, fc, sig, rmap, sub.shift, sub.lim)
+        rm, shift, lim = sub.rm, sub.shift, sub.lim
+        if rows is not None and sub.idx is None:
+            flat = rows.reshape(-1)
+            n0 = len(rmap)
+            if len(flat) > n0 and np.array_equal(flat[:n0], rmap):
+                new = flat[n0:].astype(np.int64)
+                T_n, _, end = self._alignment(new, st, hist_end)
+                if T_n <= sub.T:
+                    # raw (shift, lim) of the new rows: the kernel applies dk
+                    # to every row (effective shift - dk, lim + dk)
+                    nd = torch.from_numpy(np.concatenate([new, sub.T - end + dk, end - dk]).astype(np.int32))
+                    nd = nd.pin_memory().to(st.buf.device, non_blocking=True)
+                    nn = len(new)
+                    rm = torch.cat([sub.rm, nd[:nn]])
+                    shift = torch.cat([sub.shift, nd[nn:2 * nn]])
+                    lim = torch.cat([sub.lim, nd[2 * nn:]])
+                    rmap = flat.copy()
+        fc, sig = lstm.forecast_rows(st.buf, rm, shift, lim, dk, sub.T, H)
+        self._pre[group] = (rm, dk, sub.T, H, lstm, self.cycle, fc, sig, rmap, shift, lim)
 
     def _pre_take(self, group: tuple, sub: "ModelSub", H: int, lstm, rowmap=None, store=None):
         pre = self._pre.pop(group, None)
@@ -537,6 +560,15 @@ class ModelsMixin:
             self._pre_skip.pop(group, None)
             return fc, sig
         n0 = len(rmap)
+        if (rowmap is not None and sub.idx is None and T == sub.T and H0 == H and m0 is lstm
+                and cyc == self.cycle and len(rowmap) == n0 and np.array_equal(rowmap, rmap)):
+            # the early launch already took the arrivals in (_prelaunch)
+            sh, li = sub.shift_lim()
+            if torch.equal(shift0 - dk, sh) and torch.equal(lim0 + dk, li):
+                self.prelaunch_hits += 1
+                self.prelaunch_extended += 1
+                self._pre_skip.pop(group, None)
+                return fc, sig
         if (rowmap is not None and store is not None and sub.idx is None and T == sub.T and H0 == H and m0 is lstm
                 and cyc == self.cycle and len(rowmap) > n0 and np.array_equal(rowmap[:n0], rmap)):
             # jobs arrived (appended to the laid-out list): the early forecast
