@@ -123,6 +123,7 @@ class PlanMixin:
         fetch this cycle; a batch identical to the previous cycle's (the
         steady state of a re-examined fleet) reuses the previous lists."""
         self.cycle += 1
+        self.new_jobs = 0                # (the brain's gc care reads this: a reused batch planned nothing)
         self._wt_changed = False
         self._col.clear()
         keep_jid = self._jid_cache.get(id(self._last[2])) if self._last is not None else None

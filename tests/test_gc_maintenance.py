@@ -33,3 +33,25 @@ def test_gc_freeze_is_maintained_not_repeated():
         assert b.gc_collections == 2
     finally:
         gc.unfreeze()
+
+
+def test_steady_cycles_after_a_planning_cycle_do_not_collect(monkeypatch):
+    """Regression: a steady cycle that reuses the previous claim batch planned
+    nothing, so it must not re-run the thaw + full collection (it did when
+    the planner's job count carried over: ~0.3 s per cycle at 10k jobs)."""
+    from foremast_amd.engine import brain as brain_mod
+    from tests.test_fastpath_models import _brain, _submit
+    monkeypatch.setattr(brain_mod, "GC_FREEZE_AFTER", 3)
+    clock, store, client, b, _ = _brain(True, "holt_winters", {})
+    calls = []
+    real = b.gc_maintenance
+    monkeypatch.setattr(b, "gc_maintenance", lambda **kw: (calls.append(kw), real(**kw)))
+    try:
+        _submit(client, "continuous")
+        for _ in range(4):
+            b.run_once()
+            clock.t += 60.0
+        assert b.fast.new_jobs == 0
+        assert calls == [{"refreeze": True}]         # the planning cycle only
+    finally:
+        gc.unfreeze()
