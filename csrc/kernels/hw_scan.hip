@@ -136,7 +136,8 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
                                                            float* __restrict__ sigma, int* __restrict__ best,
                                                            int* __restrict__ nfin, float* __restrict__ sscale,
                                                            float* __restrict__ season_out, int xal, int64_t nrows,
-                                                           int ahead, int npass, long long* __restrict__ probe) {
+                                                           int ahead, int npass, long long* __restrict__ probe,
+                                                           float prune, int plap) {
   using RP = RowPad<C, EXACT>;
   // FOREMAST_HW_SCAN_DEBUG (instruction accounting with PMC, results are
   // garbage): 1 = stop after the row setup, 2 = skip the season laps
@@ -401,6 +402,16 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     __syncthreads();
   }
   long long pc1 = 0, pc2 = 0, pcs = 0;
+  // early candidate pruning (FS, one pair per wave): after lap `plap` every
+  // candidate's partial SSE is published (psse: the setup's per-wave season
+  // sums, dead by then); a pair whose two partials both exceed `prune` x the
+  // smallest partial of the candidates fitted so far stops its laps and
+  // reports SSE = inf (never selected).  The leader is never pruned, so each
+  // pass keeps at least the pass-0 winner's full fit; nfull = the finite-step
+  // count of a completed fit (sigma / nfin of the row)
+  float* psse = wsum;
+  int* nfull = reinterpret_cast<int*>(wsum + 146);
+  const bool pr_on = FS && LPP == 64 && prune > 0.f && plap > 0;
 #pragma unroll 1
   for (int pass = 0; pass < npass; ++pass) {
   const int pidx = slot + pass * SL;
@@ -441,6 +452,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   // with NaN past T so their reads stay inside the allocation.
   double ea = 0.0, eb = 0.0;
   n = 0;
+  bool pruned = false;
   if constexpr (FS) {
   // One code path for every lap: the general arithmetic (missing samples,
   // inactive steps) sits behind lap-uniform scalar branches inside the step
@@ -584,6 +596,26 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
     } else {                                  // each half reads its own last lane
       l = bperm2(P, (lane & ~(LPP - 1)) + last);
       tr = bperm2(Tt, (lane & ~(LPP - 1)) + last);
+    }
+    if (pr_on && lap + 1 == plap) {           // workgroup-uniform: every wave runs the same laps
+      const f2 a = q0 < m ? accp : zero;
+      const float pa = group_sum<LPP>(a.x), pb = group_sum<LPP>(a.y);
+      __syncthreads();                        // (psse reuses the setup's season sums)
+      if (li == 0 && pvalid) {
+        psse[ga] = pa;
+        psse[gb] = pb;
+      }
+      __syncthreads();
+      const int gk = min(G, 2 * (pass + 1) * SL);     // candidates with a partial so far
+      const float inf = __builtin_inff();
+      float mn = lane < gk && isfinite(psse[lane]) ? psse[lane] : inf;
+      mn = fminf(mn, xor_lane<1>(mn)); mn = fminf(mn, xor_lane<2>(mn)); mn = fminf(mn, xor_lane<4>(mn));
+      mn = fminf(mn, xor_lane<8>(mn)); mn = fminf(mn, xor_lane<16>(mn)); mn = fminf(mn, xor_lane<32>(mn));
+      const float lim = prune * mn;
+      if (pvalid && mn > 0.f && mn < inf && pa > lim && pb > lim) {
+        pruned = true;
+        break;
+      }
     }
   }
   l = l - tr;                                 // (P, T) -> (level, trend)
@@ -745,8 +777,13 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   }  // !FS
   if (probe != nullptr) pc2 = clock64();
   // lanes' fp64 lap sums, reduced across the lanes in fp32 (the SSE is fp32)
-  const float fa = group_sum<LPP>((float)ea), fb = group_sum<LPP>((float)eb);
+  float fa = group_sum<LPP>((float)ea), fb = group_sum<LPP>((float)eb);
   n = __builtin_amdgcn_readfirstlane(group_sum<LPP>(n));   // the same for every candidate
+  if (pruned) {
+    fa = fb = __builtin_inff();
+  } else if (pr_on && lane == 0) {
+    *nfull = n;
+  }
 
   // ---- per-candidate results
   const float tph = (float)(T % m);
@@ -810,6 +847,7 @@ __global__ __launch_bounds__(1024) void hw_scan_fit_kernel(const float* __restri
   }  // passes
   __syncthreads();
   // the winner's forecast and seasons, spread over the whole workgroup
+  if (pr_on) n = *nfull;                       // (this wave's own count may be a pruned fit's)
   {
     const float lb = lbt[0], tb = lbt[1];
     const int t0 = T % m;
@@ -906,7 +944,8 @@ long long* g_probe = nullptr;            // fm_hw_scan_set_probe: [R, 16, 8] int
 template <int C>
 int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H, float* sse,
                float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin, float* sscale,
-               float* season_out, size_t lds, int xal, int lpp, int npass, int s0, hipStream_t stream) {
+               float* season_out, size_t lds, int xal, int lpp, int npass, int s0, float prune, int plap,
+               hipStream_t stream) {
   const int GP = (G + 1) / 2;
   const int slots = lpp == 64 ? GP : (GP + 1) / 2;          // waves for one pass over the pairs
   const int waves = (slots + npass - 1) / npass;
@@ -925,7 +964,8 @@ int launch_one(const float* x, int64_t ld, int T, int64_t R, const float* cand, 
     if (lds > 65536) allow_big_lds<C, EX, FSV, LP>();                                                       \
     hipLaunchKernelGGL((hw_scan_fit_kernel<C, EX, FSV, LP>), dim3((unsigned)R), dim3(64 * waves), lds, stream, x, \
                        ld, T, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale, season_out, xal,  \
-                       R, ahead * (npass > 1 ? 2 : 1), npass | (scan_debug() << 8) | (s0 << 16), g_probe);  \
+                       R, ahead * (npass > 1 ? 2 : 1), npass | (scan_debug() << 8) | (s0 << 16), g_probe,   \
+                       prune, plap);                                                                        \
   } while (0)
   const bool ex = m % C == 0;
   if (lpp == 32) {
@@ -1010,9 +1050,15 @@ FM_API int fm_hw_scan_set_probe(void* p) {
 // overrides included, read once), else 0.
 FM_API int fm_hw_scan_supported(int T, int G, int m) { return scan_plan(T, G, m).C != 0; }
 
+//
+// ``prune`` > 0 (FS plans with one candidate pair per wave): after ``plap``
+// season laps (0: a third of the row's laps, at least 3 laps needed) a pair
+// whose two partial SSEs both exceed prune x the smallest partial so far stops
+// fitting; its candidates report SSE = inf (never selected), their state /
+// nobs are partial.  prune <= 0: the exact full grid.
 FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const float* cand, int G, int m, int H,
                           float* sse, float* state, int* nobs, float* fc, float* sigma, int* best, int* nfin,
-                          float* sscale, float* season_out, hipStream_t stream) {
+                          float* sscale, float* season_out, float prune, int plap, hipStream_t stream) {
   if (R <= 0) return 0;
   if (H < 0) return (int)hipErrorInvalidValue;
   const ScanPlan pl = scan_plan(T, G, m);
@@ -1020,10 +1066,15 @@ FM_API int fm_hw_scan_fit(const float* x, int64_t ld, int T, int64_t R, const fl
   const int C = pl.C, lpp = pl.lpp, npass = pl.npass, s0 = pl.s0;
   const size_t lds = pl.lds;
   const int xal = ((uintptr_t)x % 16 == 0) && (ld % 4 == 0);
+  if (plap <= 0) plap = (T - m) / m >= 3 ? (T - m) / m / 3 : 0;
+  if (prune <= 0.f || plap <= 0) {
+    prune = 0.f;
+    plap = 0;
+  }
 #define FM_HWS(CC)                                                                                         \
   case CC:                                                                                                 \
     return launch_one<CC>(x, ld, T, R, cand, G, m, H, sse, state, nobs, fc, sigma, best, nfin, sscale,    \
-                          season_out, lds, xal, lpp, npass, s0, stream);
+                          season_out, lds, xal, lpp, npass, s0, prune, plap, stream);
   switch (C) {
     FM_HWS(4) FM_HWS(5) FM_HWS(6) FM_HWS(8) FM_HWS(9) FM_HWS(12) FM_HWS(16) FM_HWS(18) FM_HWS(20) FM_HWS(23)
     FM_HWS(24)

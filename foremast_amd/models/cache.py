@@ -288,7 +288,7 @@ class ModelCache:
                 m = int(period_for(sub))
                 if 2 * m > T:
                     k_eff, m = 1, 1
-            fit = SM.es_fit(sub, T, k_eff, H, m, keep_state=True)
+            fit = SM.es_fit(sub, T, k_eff, H, m, keep_state=True, prune=SM.HW_SCAN_PRUNE)
             fc[idx], sig[idx] = fit.forecast, fit.sigma
             if k_eff == kind:
                 self._store([keys[i] for i in miss], kind, m, fit.model, t_last[miss], np.full(len(miss), now), dev)

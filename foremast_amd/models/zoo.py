@@ -142,7 +142,7 @@ def decide(algorithm: str, hist: torch.Tensor, T: int, cur: torch.Tensor, horizo
             m = period or _detect_period(hist, T)
             if 2 * m > T:
                 kind, m = 1, 1
-        fit = SM.es_fit(hist, T, kind, H, m)
+        fit = SM.es_fit(hist, T, kind, H, m, prune=SM.HW_SCAN_PRUNE)
         has_cur = torch.isfinite(cur).any(1).to(torch.int32)
         valid = (fit.nfin.to(cur.device) >= max(tables.min_hist, 1)).to(torch.int32) | (has_cur << 1)
         return band(fit.forecast, fit.sigma, horizon, cur, M, tables, diff, valid)
@@ -189,7 +189,7 @@ def forecast(algorithm: str, hist: torch.Tensor, T: int, H: int, period: int | N
             m = period or _detect_period(hist, T)
             if 2 * m > T:
                 kind, m = 1, 1
-        fit = SM.es_fit(hist, T, kind, H, m)
+        fit = SM.es_fit(hist, T, kind, H, m, prune=SM.HW_SCAN_PRUNE)
         return fit.forecast, fit.sigma
     if algo == "prophet":
         fit = LQ.prophet_fit(hist, T, H)

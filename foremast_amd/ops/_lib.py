@@ -43,7 +43,8 @@ _SIGS: dict[str, list] = {
                        c_u32, c_void_p],
     "fm_es_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                   c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
-    "fm_hw_scan_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int] + [c_void_p] * 10,
+    "fm_hw_scan_fit": [c_void_p, c_i64, c_int, c_i64, c_void_p, c_int, c_int, c_int] + [c_void_p] * 9
+                      + [c_float, c_int, c_void_p],
     "fm_hw_scan_supported": [c_int, c_int, c_int],
     "fm_hw_scan_set_probe": [c_void_p],
     "fm_ipc_handle_size": [],

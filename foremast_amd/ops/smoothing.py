@@ -108,8 +108,15 @@ def _hw_scan_supported_py(T: int, G: int, m: int) -> bool:
     return lds <= 160 * 1024
 
 
+# early candidate pruning of the production scan fits (zoo / model cache):
+# after a third of the season laps, a candidate pair whose partial SSEs are
+# both above HW_SCAN_PRUNE x the best partial stops (csrc/kernels/hw_scan.hip).
+# 0 disables it (the exact full grid, es_fit's own default).
+HW_SCAN_PRUNE = float(os.environ.get("FOREMAST_HW_SCAN_PRUNE", "1.25"))
+
+
 def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, grid: np.ndarray | None = None,
-           keep_state: bool = False, half_season: bool = True, method: str = "auto") -> ESFit:
+           keep_state: bool = False, half_season: bool = True, method: str = "auto", prune: float = 0.0) -> ESFit:
     """Fit SES / Holt / Holt-Winters (additive, multiplicative) by grid search
     on one-step SSE and forecast H steps past the end of the history.  With
     ``keep_state`` the best candidate's fitted state is returned as an
@@ -121,7 +128,12 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     traffic) where :func:`hw_scan_supported`; otherwise the serial grid kernels
     (csrc/kernels/smoothing.hip), whose [m][R*G] seasonal scratch is fp16
     scaled per row when ``half_season`` (half the HBM traffic that bounds
-    that fit)."""
+    that fit).
+
+    ``prune`` > 0 (scan fit only): early candidate pruning -- candidates
+    whose SSE over the first third of the laps is above ``prune`` x the best
+    one's stop there and report SSE = inf (never selected); the pick, its
+    forecast, state and sigma are those of a completed fit."""
     check(x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1, "x must be [R, T] float32")
     check(0 <= kind <= 3, f"kind must be 0..3, got {kind}")
     R = x.shape[0]
@@ -149,7 +161,7 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
     scan = kind == 2 and method != "serial" and hw_scan_supported(T, G, m)
     check(scan or method != "scan", f"the scan fit does not cover T={T}, G={G}, m={m}")
     if scan:
-        return _hw_scan_fit(x, T, R, cand, G, m, H, keep_state)
+        return _hw_scan_fit(x, T, R, cand, G, m, H, keep_state, prune)
     # fp16 only where the scratch is big enough to be HBM traffic (daily /
     # longer seasons: a handful of laps, little rounding to accumulate; at
     # m = 288 (35 laps) SSEs moved by up to 1.2 %); short seasons stay fp32
@@ -184,7 +196,7 @@ def es_fit(x: torch.Tensor, T: int | None, kind: int, H: int, m: int = 1440, gri
 
 
 def _hw_scan_fit(x: torch.Tensor, T: int, R: int, cand: torch.Tensor, G: int, m: int, H: int,
-                 keep_state: bool) -> ESFit:
+                 keep_state: bool, prune: float = 0.0) -> ESFit:
     d = x.device
     sse = torch.empty((R, G), dtype=torch.float32, device=d)
     state = torch.empty((R * G, 3), dtype=torch.float32, device=d)
@@ -196,7 +208,7 @@ def _hw_scan_fit(x: torch.Tensor, T: int, R: int, cand: torch.Tensor, G: int, m:
     sscale = torch.empty((R,), dtype=torch.float32, device=d)
     season = torch.empty((R, m), dtype=torch.float32, device=d) if keep_state else None
     LIB.call("fm_hw_scan_fit", ptr(x), x.stride(0), T, R, ptr(cand), G, m, H, ptr(sse), ptr(state), ptr(nobs),
-             ptr(fc), ptr(sig), ptr(best), ptr(nfin), ptr(sscale), ptr(season), stream_of(x))
+             ptr(fc), ptr(sig), ptr(best), ptr(nfin), ptr(sscale), ptr(season), float(prune), 0, stream_of(x))
     model = None
     if keep_state:
         b = best.long()

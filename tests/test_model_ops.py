@@ -766,6 +766,47 @@ def test_gpu_hw_scan_fit_matches_references(cuda, m):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("m", [720, 1300, 1440])
+def test_gpu_hw_scan_pruned_fit_keeps_the_oracle_pick(cuda, m):
+    """Early candidate pruning: after a third of the laps, a
+    pair whose partial SSEs are both > 1.25 x the best partial stops.  The
+    pick stays the fp64 oracle's within its SSE tolerance; candidates that
+    ran to the end report the exact fit's SSE, the pruned ones inf; the
+    winner's forecast / sigma / state and the row's finite count equal the
+    exact fit's.  Half-wave plans (m <= 768) never prune."""
+    T = 10080
+    x = _seasonal(48, T, period=m, seed=31)
+    x[:, :] *= np.geomspace(1e-2, 1e4, 48)[:, None].astype(np.float32)
+    x[3, 5000] = np.nan
+    x[4, 7000:7200] = np.nan
+    x[5, :77] = np.nan
+    x[6, :] = np.nan
+    xt = torch.from_numpy(x).to(cuda)
+    ex = SM.es_fit(xt, T, 2, 10, m, method="scan", keep_state=True)
+    pr = SM.es_fit(xt, T, 2, 10, m, method="scan", keep_state=True, prune=1.25)
+    _, _, best0, sse0 = SM.ref_es_fit(x, 2, 10, m, SM.default_grid(2))
+    s_x, s_p = ex.sse.cpu().numpy(), pr.sse.cpu().numpy()
+    cut = np.isinf(s_p) & np.isfinite(s_x)
+    if m <= 768:
+        assert not cut.any()
+    else:
+        assert cut.mean() > 0.1                       # it does prune on this data
+    keep = ~cut
+    np.testing.assert_array_equal(s_p[keep], s_x[keep])
+    bp = pr.best.cpu().numpy()
+    for r in range(48):
+        if np.isfinite(sse0[r]).any() and sse0[r].min() > 0:
+            assert sse0[r, bp[r]] <= sse0[r].min() * (1 + 2e-3), (r, bp[r], best0[r])
+    same = bp == ex.best.cpu().numpy()
+    assert same.mean() > 0.95
+    np.testing.assert_array_equal(pr.forecast.cpu().numpy()[same], ex.forecast.cpu().numpy()[same])
+    np.testing.assert_array_equal(pr.sigma.cpu().numpy()[same], ex.sigma.cpu().numpy()[same])
+    np.testing.assert_array_equal(pr.model.state.cpu().numpy()[same], ex.model.state.cpu().numpy()[same])
+    np.testing.assert_array_equal(pr.model.season.cpu().numpy()[same], ex.model.season.cpu().numpy()[same])
+    np.testing.assert_array_equal(pr.nfin.cpu().numpy(), np.isfinite(x).sum(1))
+
+
+@pytest.mark.gpu
 def test_gpu_hw_scan_long_history_big_lds(cuda):
     """14 days at 1-min resolution: the row needs > 64 KB of LDS (the launch
     raises the workgroup's dynamic LDS limit); a lap with a gap."""
@@ -791,7 +832,7 @@ def test_hw_scan_supported_mirrors_native_checks():
     for T in (400, 2880, 10080, 20160, 30000, 36000):
         for m in (24, 150, 192, 288, 1008, 1300, 1440, 1536, 1600):
             for G in (1, 27, 32, 33):
-                rc = f(None, T, T, 1, None, G, m, 10, *([None] * 10))
+                rc = f(None, T, T, 1, None, G, m, 10, *([None] * 9), 0.0, 0, None)
                 assert (rc != 1) == SM.hw_scan_supported(T, G, m), (T, m, G, rc)
 
 
