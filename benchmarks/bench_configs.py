@@ -650,6 +650,48 @@ def config3e2e(args):
         if args.soak_every and len(cyc_ms) % args.soak_every == 0:
             soak_rows.append(soak_sample())
             print("[soak] " + _json.dumps(soak_rows[-1]), file=sys.stderr, flush=True)
+            if os.environ.get("FOREMAST_SOAK_TRACEMALLOC"):
+                # where the host heap grows between samples (leak hunting)
+                import gc
+                import tracemalloc
+                if not tracemalloc.is_tracing():
+                    tracemalloc.start(4)
+                    soak_rows[-1]["tm"] = tracemalloc.take_snapshot()
+                else:
+                    from foremast_amd.api.models import Document as _Doc
+                    docs_ = [o for o in gc.get_objects() if isinstance(o, _Doc)]
+                    live_ids = set(brain.fast.works) if brain.fast is not None else set()
+                    live_docs = {id(w.doc) for w in brain.fast.works.values()} if brain.fast is not None else set()
+                    stray = [o for o in docs_ if id(o) not in live_docs]
+                    print(f"[tm] documents alive {len(docs_)}, not a live fast job {len(stray)}", file=sys.stderr,
+                          flush=True)
+                    for o in stray[-3:]:
+                        for ref in gc.get_referrers(o):
+                            if ref is docs_ or ref is stray:
+                                continue
+                            desc = type(ref).__name__
+                            if isinstance(ref, dict):
+                                owners = [type(x).__name__ for x in gc.get_referrers(ref)
+                                          if x is not docs_ and not isinstance(x, list)][:3]
+                                desc += f" (in {owners}; keys {list(ref)[:4]})"
+                            elif isinstance(ref, (list, tuple)):
+                                owners = [type(x).__name__ for x in gc.get_referrers(ref)][:4]
+                                desc += f" len {len(ref)} (in {owners})"
+                            print(f"[tm]   {o.id[:12]} {o.status} <- {desc}", file=sys.stderr, flush=True)
+                    del docs_, stray
+                    import collections
+                    cnt = collections.Counter(type(o).__name__ for o in gc.get_objects())
+                    prev_c = next((r["tc"] for r in soak_rows if "tc" in r), None)
+                    soak_rows[-1]["tc"] = cnt
+                    if prev_c is not None:
+                        grow = sorted(((cnt[k] - prev_c.get(k, 0), k) for k in cnt), reverse=True)[:8]
+                        print(f"[tm] tracked growth by type: {grow}", file=sys.stderr, flush=True)
+                    snap = tracemalloc.take_snapshot()
+                    prev = next(r["tm"] for r in soak_rows if "tm" in r)
+                    for st_ in snap.compare_to(prev, "traceback")[:12]:
+                        print(f"[tm] {st_.size_diff / 1e6:+.2f} MB {st_.count_diff:+d} "
+                              + " <- ".join(f"{f.filename.split('repo/')[-1]}:{f.lineno}" for f in st_.traceback),
+                              file=sys.stderr, flush=True)
         if brain.fast is not None:
             onboard.append((brain.fast.onboard_s - ob0[0], brain.fast.onboard_jobs - ob0[1]))
         rows.append(r.get("rows", 0))
@@ -931,7 +973,7 @@ def config3e2e(args):
                                   "ghost_cycles": brain.fast.ghost_cycles} if brain.fast is not None else None),
              "prerendered_future_series": pre_n,
              "rank_exchange": exchange, "world": info.world,
-             "soak": soak_rows or None,
+             "soak": [{k: v for k, v in r.items() if k not in ("tm", "tc")} for r in soak_rows] or None,
              "first_cycle_s (synthetic generation + fetch + stage history + first fit, untimed)": round(t_first, 3),
              "submit_s": round(t_sub, 3),
              "fast_jobs_first_cycle": first.get("fast_jobs"), "device": str(dev)})

@@ -104,6 +104,10 @@ class GaugeTable:
         self._fdead: list[int] = []              # per family: dropped lines not compacted yet
         self._sline = np.zeros(0, np.int64)      # slot -> (family << 32 | line)
         self.events: list = []                   # (slot, key | None) since the last drain (C2 publication)
+        # events are only logged once a publisher drains them (ranks > 0 of a
+        # distributed brain): rank 0 / a single rank never drains, and an
+        # undrained log kept every key ever seen alive (the soak's RSS growth)
+        self.log_events = False
         self.dropped = 0
         # key -> live owners that keep its slot number cached (fast-path jobs,
         # rank 0's map of another rank's slots): such a slot is never freed,
@@ -145,7 +149,8 @@ class GaugeTable:
                 self.vals[ns] = np.nan
                 self.expire[ns] = np.inf
                 self._add_lines(new_k, new_s)
-                self.events.extend(zip(new_s, new_k))
+                if self.log_events:
+                    self.events.extend(zip(new_s, new_k))
         return out
 
     def _add_lines(self, keys: list, slots: list) -> None:
@@ -292,7 +297,8 @@ class GaugeTable:
                 self._fdead[f] += len(sel)
             self._sline[dead] = -1
             self._free.extend(dl)
-            self.events.extend((s, None) for s in dl)
+            if self.log_events:
+                self.events.extend((s, None) for s in dl)
             self.vals[dead] = np.nan
             self.expire[dead] = np.nan
             self._nret -= len(dead)
@@ -665,8 +671,11 @@ class BrainExporter:
         t = self.table
         if not force and (t.version == self._pub_version or now - self._pub_t < self.sync_seconds):
             return False
+        first = not t.log_events
+        if first:                            # the log starts now: the first entry is a snapshot
+            t.log_events = True
         ev = t.drain_events()
-        if ev and self._logged + len(ev) > 2 * len(t) + 4096:
+        if first or (ev and self._logged + len(ev) > 2 * len(t) + 4096):
             # new epoch: the live keys as its first entry (events of the old epoch are moot)
             self._epoch += 1
             self._logged = 0

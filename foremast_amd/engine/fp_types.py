@@ -306,11 +306,13 @@ def _device_horizons(trow: torch.Tensor, t_last: torch.Tensor, step: float) -> t
 _version_of = __import__("operator").attrgetter("version")
 
 
-@functools.lru_cache(maxsize=65536)
+@functools.lru_cache(maxsize=16384)
 def _parse_config_cached(config: str) -> dict:
     """api/urls.parse_config, memoised (read-only result): a job's config
     strings are parsed by intake and again by planning, and the store /
-    history strings repeat across a fleet."""
+    history strings repeat across a fleet.  Bounded well below a fleet's
+    distinct strings: the entries that matter are a claim's new jobs (parsed
+    twice in one cycle) and the shared store strings."""
     return parse_config(config)
 
 
@@ -376,6 +378,7 @@ class JobIds:
             return c[1]
         ix = self._index_in(old)
         self._ixc = (old, ix)
+        old._forget()
         return ix
 
     def _index_in(self, old: "JobIds") -> np.ndarray | None:
@@ -406,7 +409,15 @@ class JobIds:
         cand = old._order[p]
         hit = old.arr[cand] == self.arr
         self._mc = (old, (cand, hit, int(hit.sum())))
+        old._forget()
         return self._mc[1]
+
+    def _forget(self) -> None:
+        """Drop this list's own lookups against ITS predecessor: once a newer
+        list has matched against this one they are never asked again, and
+        keeping them chained every cycle's JobIds to the previous one (the
+        soak's unbounded host growth)."""
+        self._ixc = self._mc = None
 
 
 class HpaTable:

@@ -820,6 +820,10 @@ class TemplateList(list):
         out = cls(parent)
         list.extend(out, tail)
         out.base = parent
+        # one level only: a list extended every cycle (arrivals) would chain
+        # every earlier list (each a full copy of the templates) -- the parent
+        # has been resolved by now, and one that is not resolves on its own
+        parent.base = None
         return out
 
 

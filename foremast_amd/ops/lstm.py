@@ -22,8 +22,9 @@ STACK_TILING = {256: (4, 2), 128: (2, 2), 64: (2, 2), 32: (2, 2)}   # H -> (row 
 STACK_TILING_2L = {256: (4, 202)}
 STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1),            # instantiated alternatives (lstm_stack.hip);
                           (4, 201), (2, 201), (4, 202),              # nct 201: layer-pipelined, 2 layers, 1 tile; 202: row-streamed, 2 tiles;
-                          (4, 211), (4, 212), (4, 213), (4, 214))}   # 211-213: its ablations (timing only, wrong h);
-                                                                     # 214: A one k-step ahead (correct h)
+                          (4, 211), (4, 212), (4, 213), (4, 214),    # 211-213: its ablations (timing only, wrong h);
+                          (8, 216))}                                 # 214: A one k-step ahead (correct h);
+                                                                     # 216: 16x16 tiles, 48 sequences (pack_t16)
 
 
 def stack_tiling(H: int, layers: int = 1) -> tuple[int, int]:
@@ -127,10 +128,38 @@ def pack_aug(aug: np.ndarray, H: int, RT: int) -> np.ndarray:
     return _bf16_bits(out)
 
 
+def pack_t16(aug: np.ndarray, H: int) -> np.ndarray:
+    """Augmented gate matrix [4H, K] (columns in the kernel's k-step order, K
+    a multiple of 32) -> bf16 A fragments of v_mfma_f32_16x16x32_bf16 for
+    lstm_stack2_t16_kernel: [8 waves, H/32 row tiles, K/32, 64 lanes, 8] as
+    uint16.  Row tile rt of wave w is hidden units 32 w + 4 rt + (0..3), rows
+    ordered unit-major, gate-minor (row 4u + gate), so a lane's four
+    accumulators are one unit's [i f g o]; lane l holds row l & 15, k
+    8 (l >> 4) + (0..7) of each 32-k step; rows carry their gate scale."""
+    K = aug.shape[1]
+    KS = K // 32
+    nw, rt_n = 8, H // 32
+    aug = _scaled_rows(aug, H)
+    lane = np.arange(64)
+    r, q4 = lane & 15, lane >> 4
+    out = np.zeros((nw, rt_n, KS, 64, 8), np.float32)
+    for w in range(nw):
+        for rt in range(rt_n):
+            trow = (r & 3) * H + 32 * w + 4 * rt + (r >> 2)
+            for ks in range(KS):
+                cols = 32 * ks + 8 * q4[:, None] + np.arange(8)[None, :]
+                out[w, rt, ks] = aug[trow[:, None], cols]
+    return _bf16_bits(out)
+
+
 def pack_stack(layers: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]], H: int) -> list[torch.Tensor]:
     """[(W_ih, W_hh, b_ih + b_hh)] per layer (torch.nn.LSTM conventions) ->
-    the stacked kernel's per-layer fragment buffers (uint8)."""
-    RT = stack_tiling(H)[0]
+    the stacked kernel's per-layer fragment buffers (uint8), for the tiling
+    ``stack_tiling(H, len(layers))`` picks (pack and run under the same
+    FM_LSTM_STACK_TILING)."""
+    RT, nct = stack_tiling(H, len(layers))
+    if nct == 216:
+        return _pack_stack_t16(layers, H)
     out = []
     for li, (w_ih, w_hh, b) in enumerate(layers):
         w_ih, w_hh, b = (t.detach().float().cpu().numpy() for t in (w_ih, w_hh, b))
@@ -148,6 +177,30 @@ def pack_stack(layers: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]], H:
             aug[:, H:2 * H] = w_ih
             aug[:, 2 * H] = b
         out.append(torch.from_numpy(pack_aug(aug, H, RT).view(np.uint8).copy()))
+    return out
+
+
+def _pack_stack_t16(layers, H: int) -> list[torch.Tensor]:
+    """pack_stack for the 16x16-tile kernel: layer 0 K order [x, 1 | pad to
+    32, h0_{t-1}], layer 1 [h1_{t-1}, h0_t, 1 | pad to 32]."""
+    check(len(layers) == 2 and H == 256, "the 16x16-tile kernel is the two-layer H = 256 form")
+    out = []
+    for li, (w_ih, w_hh, b) in enumerate(layers):
+        w_ih, w_hh, b = (t.detach().float().cpu().numpy() for t in (w_ih, w_hh, b))
+        I = w_ih.shape[1]
+        if li == 0:
+            check(I <= 15, "layer-0 input features must be <= 15 (x, then the bias, in one K step)")
+            aug = np.zeros((4 * H, 32 + H), np.float32)
+            aug[:, :I] = w_ih
+            aug[:, I] = b
+            aug[:, 32:] = w_hh
+        else:
+            check(I == H, "stacked layers take the previous layer's h")
+            aug = np.zeros((4 * H, 2 * H + 32), np.float32)
+            aug[:, :H] = w_hh
+            aug[:, H:2 * H] = w_ih
+            aug[:, 2 * H] = b
+        out.append(torch.from_numpy(pack_t16(aug, H).view(np.uint8).copy()))
     return out
 
 

@@ -555,7 +555,8 @@ def test_gpu_lstm_stack_matches_fp32_lstm(cuda, H, layers, I):
 @pytest.mark.gpu
 @pytest.mark.parametrize("tiling,L", [("4:1", 48), ("2:1", 48), ("4:2", 48), ("2:2", 48), ("4:1p", 48),
                                       ("2:1p", 48), ("4:2p", 48), ("4:214", 48),
-                                      ("4:1p", 1), ("4:1p", 2), ("4:2p", 1), ("4:2p", 2), ("4:2p", 3)])
+                                      ("4:1p", 1), ("4:1p", 2), ("4:2p", 1), ("4:2p", 2), ("4:2p", 3),
+                                      ("8:216", 48), ("8:216", 1), ("8:216", 2), ("8:216", 3)])
 def test_gpu_lstm_stack_tilings_agree(cuda, tiling, L, monkeypatch):
     """Every instantiated H = 256 tiling (row tiles per wave x column tiles;
     ``p``: the two-layer pipelined / row-streamed kernels, incl. their
