@@ -596,7 +596,10 @@ def config3e2e(args):
                         submit_one(churn_client, c, churn["next"])
                         churn["next"] += 1
                         churn["new"] += 1
-                elif st_ == "hpa":
+                elif st_ == "hpa" or (st_ == "continuous" and args.soak_every):
+                    # (soak: continuous monitors are re-armed round-robin as
+                    # barrelman re-arms them after a verdict, so the ones that
+                    # closed come back and the fleet stays the same size)
                     base_j = a0 + (len(cyc_ms) * k) % max(1, n_)
                     for j in range(base_j, min(a0 + n_, base_j + k)):
                         submit_one(churn_client, c, j)

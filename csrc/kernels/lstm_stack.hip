@@ -641,6 +641,210 @@ static int launch_stack2_rs(const void* xa, int64_t B, int L, const void* W0, co
   return 0;
 }
 
+// Two layers at H = 256 on 16x16 tiles: v_mfma_f32_16x16x32_bf16, BT = 48
+// sequences (three 16-column tiles) per workgroup.  The 32-column kernel
+// above needs 64 sequences per workgroup to halve the weight stream, which
+// leaves a 10k-service fleet at ceil(10000 / 64) = 157 workgroups: 99 of the
+// 256 CUs idle for the whole recurrence.  With 16-column tiles the workgroup
+// takes 48 sequences -> 209 workgroups (82 % of the CUs), 25 % less MFMA work
+// per workgroup for the same weight bytes per step.
+//
+// Layout (cdna_hip_programming.md §3, 16x16x32): lane l holds A[row l & 15][k
+// 8 (l >> 4) + j], B[k 8 (l >> 4) + j][col l & 15] and C rows 4 (l >> 4) .. +3
+// of column l & 15.  A 16-row tile is 4 hidden units x [i f g o] (row 4u + gate),
+// so a lane's four accumulators are one unit's gates of one sequence: the
+// cell stays lane-local.  Wave w owns units 32 w .. 32 w + 31 as 8 row tiles per
+// layer.  K order of the packed weights (ops/lstm.py pack_stack_t16) is the
+// order the k-steps run: layer 0 [x_t, 1 | pad] then h0_{t-1} (9 k-steps of
+// 32); layer 1 h1_{t-1}, h0_t, then [1 | pad] (17 k-steps).
+//
+// Schedule: lstm_stack2_rs_kernel's, with 16 tasks per iteration (L0 rt0..7 at
+// step s, L1 rt0..7 at step s - 1), the three cells of task T beside the
+// first k-steps of task T + 1, A fragments DA k-steps ahead, two barriers per
+// iteration (before L0 rt0 and L1 rt0).
+template <int H>
+__global__ __launch_bounds__(512) void lstm_stack2_t16_kernel(
+    const uint4* __restrict__ xa, int64_t B, int L, const uint4* __restrict__ W0, const uint4* __restrict__ W1,
+    float* __restrict__ h_out, float* __restrict__ c_out) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int NW = 8;
+  constexpr int RT = H / (4 * NW);                      // 16-row tiles per wave per layer (8)
+  constexpr int NCT = 3;
+  constexpr int KH = H / 32;                            // 32-k steps over one hidden vector
+  constexpr int KS0 = KH + 1;
+  constexpr int KS1 = 2 * KH + 1;
+  constexpr int HP = H + 8;
+  constexpr int BT = 16 * NCT;
+  constexpr int IMG = BT * HP;
+  constexpr int G0 = RT * KS0;                          // k-steps of the layer-0 tasks
+  constexpr int G = G0 + RT * KS1;                      // k-steps per iteration
+  constexpr int DA = 3;                                 // A fragments DA k-steps ahead
+  static_assert(G % (DA + 1) == 0, "A ring wraps at the iteration boundary");
+  static_assert(KS0 >= 2 * NCT && KS1 >= 4 * NCT - 3, "a task's cells fit beside the next task's k-steps");
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  unsigned short* h0b = lds;                            // [2][BT][HP]
+  unsigned short* h1b = lds + 2 * IMG;                  // [2][BT][HP]
+  const int lane = lane_id(), w = wave_id();
+  const int q4 = lane >> 4, col = lane & 15;
+  const int64_t b0 = (int64_t)blockIdx.x * BT;
+
+  for (int i = threadIdx.x; i < 4 * IMG; i += 64 * NW) lds[i] = 0;   // h_{-1} = 0
+  float c0[RT][NCT], c1[RT][NCT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) c0[rt][ct] = c1[rt][ct] = 0.f;
+  __syncthreads();
+
+  const uint4* xp[NCT];
+  bool inb[NCT];
+  int64_t bbo[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    int64_t bb = b0 + 16 * ct + col;
+    inb[ct] = bb < B;
+    bb = bb < B ? bb : B - 1;
+    bbo[ct] = bb;
+    xp[ct] = xa + (bb * L) * 2 + (q4 & 1);              // lanes q4 >= 2 hold the zero pad
+  }
+  const bool xlane = q4 < 2;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t W0w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W0 + (int64_t)wu * RT * KS0 * 64), (short)0, RT * KS0 * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t W1w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W1 + (int64_t)wu * RT * KS1 * 64), (short)0, RT * KS1 * 1024, 0x00020000);
+  const int voff = 16 * lane;
+  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
+  const uint4 onesv = make_uint4(q4 == 0 ? 0x3F80u : 0u, 0u, 0u, 0u);
+  const int lro = col * HP + 8 * q4;                    // this lane's B-fragment row (column tile 0)
+  auto lds16 = [](const unsigned short* p) { return *reinterpret_cast<const uint4*>(p); };
+
+  auto lay = [](int g) { return g >= G0 ? 1 : 0; };
+  auto tsk = [](int g) { return g < G0 ? g / KS0 : RT + (g - G0) / KS1; };
+  auto kin = [](int g) { return g < G0 ? g % KS0 : (g - G0) % KS1; };
+  auto loadA = [&](Frag& f, int g) {
+    const int rt = tsk(g) & (RT - 1), i = kin(g);
+    const u32x4 v = lay(g) ? __builtin_amdgcn_raw_buffer_load_b128(W1w, voff, (rt * KS1 + i) * 1024, 0)
+                           : __builtin_amdgcn_raw_buffer_load_b128(W0w, voff, (rt * KS0 + i) * 1024, 0);
+    f.u = make_uint4(v.x, v.y, v.z, v.w);
+  };
+
+  f32x4 acc[2][NCT];                                    // [task parity][column tile]
+  Frag ar[DA + 1];
+  // the cell of column tile ct of the finished task T: unit 32 w + 4 rt + q4 of
+  // sequence 16 ct + col; its h goes to image ``img`` (bf16), and with ``out``
+  // to h_out / c_out
+  auto cell_q = [&](int T, int ct, unsigned short* img, bool out) {
+    const int rt = T & (RT - 1);
+    const f32x4& a = acc[T & 1][ct];
+    float hv;
+    if (T >= RT) cell(a[0], a[1], a[2], a[3], c1[rt][ct], hv);
+    else cell(a[0], a[1], a[2], a[3], c0[rt][ct], hv);
+    const int u = 4 * RT * w + 4 * rt + q4;
+    img[(16 * ct + col) * HP + u] = f2bf(hv);
+    if (out && inb[ct]) {
+      h_out[bbo[ct] * H + u] = hv;
+      c_out[bbo[ct] * H + u] = c1[rt][ct] * kLstmInvK;
+    }
+  };
+
+#pragma unroll
+  for (int g = 0; g < DA; ++g) loadA(ar[g], g);
+  uint4 xn[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) xn[ct] = xlane ? xp[ct][0] : zero4;
+
+  for (int s = 0; s <= L; ++s) {
+    const int p = s & 1;
+    const unsigned short* h0r = h0b + (p ^ 1) * IMG + lro;   // h0_{s-1}
+    const unsigned short* h1r = h1b + p * IMG + lro;         // h1_{s-2}
+    unsigned short* h0w = h0b + p * IMG;                     // h0_s
+    unsigned short* h1w_old = h1b + p * IMG;                 // h1_{s-2} (L1 rt7 cells of iteration s - 1)
+    unsigned short* h1w = h1b + (p ^ 1) * IMG;               // h1_{s-1}
+    const bool l1prev = s >= 2, l1cur = s >= 1, fin = s == L;
+    uint4 xt[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      xt[ct] = xn[ct];
+      xn[ct] = xlane ? xp[ct][(s + 1 < L ? s + 1 : L - 1) * 2] : zero4;
+    }
+    // B of k-step g, column tile ct (by value: see gemm above)
+    auto bread = [&](int g, int ct) {
+      const int i = kin(g);
+      if (lay(g) == 0) {
+        const uint4 v = lds16(h0r + 16 * ct * HP + 32 * (i == 0 ? 0 : i - 1));
+        return i == 0 ? xt[ct] : v;
+      }
+      if (i < KH) return lds16(h1r + 16 * ct * HP + 32 * i);
+      const uint4 v = lds16(h0r + 16 * ct * HP + 32 * (i < 2 * KH ? i - KH : KH - 1));
+      return i == 2 * KH ? onesv : v;
+    };
+    uint4 bcur[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) bcur[ct] = xt[ct];
+    static_for<G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (g == 0 || g == G0) lds_barrier();
+      loadA(ar[(g + DA) % (DA + 1)], (g + DA) % G);
+      if constexpr (g == G0) {                                 // not prefetched across the barrier
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) bcur[ct] = bread(g, ct);
+      }
+      uint4 bnext[NCT];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) bnext[ct] = bcur[ct];
+      if constexpr (g + 1 < G && g + 1 != G0) {
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) bnext[ct] = bread(g + 1, ct);
+      }
+      constexpr int T = g < G0 ? g / KS0 : RT + (g - G0) / KS1;
+      constexpr int i = g < G0 ? g % KS0 : (g - G0) % KS1;
+      const Frag& a = ar[g % (DA + 1)];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        Frag bf;
+        bf.u = bcur[ct];
+        acc[T & 1][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, bf.v, i == 0 ? (f32x4){} : acc[T & 1][ct],
+                                                                 0, 0, 0);
+      }
+      // one cell of the previous task every 2 (layer-0 task) or 4 (layer-1
+      // task) k-steps from the second k-step on
+      constexpr int stride = g >= G0 ? 4 : 2;
+      if constexpr (i >= 1 && (i - 1) % stride == 0 && (i - 1) / stride < NCT) {
+        constexpr int q = (i - 1) / stride, Tp = (T + 2 * RT - 1) % (2 * RT);
+        if constexpr (T == 0) {
+          if (l1prev) cell_q(Tp, q, h1w_old, false);
+        } else if constexpr (Tp < RT) {
+          cell_q(Tp, q, h0w, false);
+        } else if (l1cur) {
+          cell_q(Tp, q, h1w, fin);
+        }
+      }
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) bcur[ct] = bnext[ct];
+    });
+  }
+  // L1(L-1) rt7: its cells would run in iteration L + 1
+#pragma unroll
+  for (int q = 0; q < NCT; ++q) cell_q(2 * RT - 1, q, h1b + ((L + 1) & 1) * IMG, true);
+}
+
+template <int H>
+static int launch_stack2_t16(const void* xa, int64_t B, int L, const void* W0, const void* W1, float* h_out,
+                             float* c_out, hipStream_t stream) {
+  const size_t lds = (size_t)4 * 48 * (H + 8) * sizeof(unsigned short);
+  auto k = lstm_stack2_t16_kernel<H>;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)((B + 47) / 48)), dim3(512), lds, stream, (const uint4*)xa, B, L,
+                     (const uint4*)W0, (const uint4*)W1, h_out, c_out);
+  FM_LAUNCH_CHECK();
+  return 0;
+}
+
 // Row tiles per wave / column tiles per workgroup (see ops/lstm.py
 // STACK_TILING / STACK_TILING_2L): two layers at H=256 run the row-streamed
 // BT = 64 kernel (nct = 202, RT = 4: 10k x 240 in 4.6 ms, 80k in 29.6; the
@@ -664,6 +868,10 @@ FM_API int fm_lstm_stack(const void* xa, int64_t B, int L, int H, int layers, co
   if (nct == 201 && layers == 2) {     // layer-pipelined 2-layer kernel (lstm_stack2_pipe_kernel), 1 column tile
     if (H == 256 && rt == 4) return launch_stack2_pipe<256, 4>(xa, B, L, W0, W1, h_out, c_out, stream);
     if (H == 256 && rt == 2) return launch_stack2_pipe<256, 2>(xa, B, L, W0, W1, h_out, c_out, stream);
+    return (int)hipErrorInvalidValue;
+  }
+  if (nct == 216 && layers == 2) {     // 16x16-tile 2-layer kernel (lstm_stack2_t16_kernel), 48 sequences
+    if (H == 256 && rt == 8) return launch_stack2_t16<256>(xa, B, L, W0, W1, h_out, c_out, stream);
     return (int)hipErrorInvalidValue;
   }
   if (nct == 202 && layers == 2) {     // row-tile streamed 2-layer kernel (lstm_stack2_rs_kernel), 2 column tiles

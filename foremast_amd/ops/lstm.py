@@ -24,7 +24,10 @@ STACK_TILING_ALT = {256: ((4, 2), (4, 1), (2, 2), (2, 1),            # instantia
                           (4, 201), (2, 201), (4, 202),              # nct 201: layer-pipelined, 2 layers, 1 tile; 202: row-streamed, 2 tiles;
                           (4, 211), (4, 212), (4, 213), (4, 214),    # 211-213: its ablations (timing only, wrong h);
                           (8, 216))}                                 # 214: A one k-step ahead (correct h);
-                                                                     # 216: 16x16 tiles, 48 sequences (pack_t16)
+                                                                     # 216: 16x16 tiles, 48 sequences (pack_t16):
+                                                                     # 209 workgroups instead of 157 at 10k, but
+                                                                     # 4.65 vs 4.06 ms -- every row tile re-reads B
+                                                                     # from LDS (profiles/lstm_stack_t16_ab_r6.jsonl)
 
 
 def stack_tiling(H: int, layers: int = 1) -> tuple[int, int]:
