@@ -15,6 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from benchmarks.harness import setup, time_steps  # noqa: E402
 from foremast_amd.config import BrainConfig  # noqa: E402
+from foremast_amd.api import status as ST  # noqa: E402
 from foremast_amd.parallel import dist as D  # noqa: E402
 
 
@@ -412,10 +413,18 @@ def config3e2e(args):
                         submit_one(churn_client, c, churn["next"])
                         churn["next"] += 1
                         churn["new"] += 1
-                elif st_ == "hpa" or (st_ == "continuous" and args.soak_every):
-                    # (soak: continuous monitors are re-armed round-robin as
-                    # barrelman re-arms them after a verdict, so the ones that
-                    # closed come back and the fleet stays the same size)
+                elif st_ == "continuous" and args.soak_every:
+                    # (soak: a continuous monitor that closed on a verdict is
+                    # re-armed, as barrelman re-arms it -- a new job for the
+                    # same app -- so the class keeps its size; checked
+                    # round-robin, k a cycle)
+                    base_j = a0 + (len(cyc_ms) * k) % max(1, n_)
+                    for j in range(base_j, min(a0 + n_, base_j + k)):
+                        d_ = store.get(ids[j])
+                        if d_ is not None and d_.status in ST.TERMINAL:
+                            ids[j] = submit_one(churn_client, c, j)
+                            churn["new"] += 1
+                elif st_ == "hpa":
                     base_j = a0 + (len(cyc_ms) * k) % max(1, n_)
                     for j in range(base_j, min(a0 + n_, base_j + k)):
                         submit_one(churn_client, c, j)
