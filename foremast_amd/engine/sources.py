@@ -119,6 +119,52 @@ def parse_wavefront(body: bytes | str) -> list[Series]:
     return out
 
 
+class GenMemo:
+    """A dict-like memo bounded by generations: entries go to the current
+    generation; when it holds ``cap`` entries it becomes the previous one (the
+    one before is dropped) and a lookup that hits the previous generation
+    moves the entry forward.  The working set (what a fleet's plans look up
+    again) stays, one-off keys age out -- a memo keyed by query template or
+    app name no longer grows with every job that ever arrived."""
+
+    __slots__ = ("cap", "cur", "old")
+
+    def __init__(self, cap: int = 1 << 18):
+        self.cap = int(cap)
+        self.cur: dict = {}
+        self.old: dict = {}
+
+    def get(self, k, default=None):
+        v = self.cur.get(k, _MISSING)
+        if v is not _MISSING:
+            return v
+        v = self.old.get(k, _MISSING)
+        if v is _MISSING:
+            return default
+        self[k] = v
+        return v
+
+    def __contains__(self, k) -> bool:
+        return self.get(k, _MISSING) is not _MISSING
+
+    def __getitem__(self, k):
+        v = self.get(k, _MISSING)
+        if v is _MISSING:
+            raise KeyError(k)
+        return v
+
+    def __setitem__(self, k, v) -> None:
+        if len(self.cur) >= self.cap:
+            self.old, self.cur = self.cur, {}
+        self.cur[k] = v
+
+    def __len__(self) -> int:
+        return len(self.cur) + len(self.old)
+
+
+_MISSING = object()
+
+
 def _native_ok(u) -> bool:
     """The native client speaks plain HTTP/1.1 straight to the host: a URL
     with credentials (``user:pass@host`` -> basic auth) or a host the proxy
@@ -168,9 +214,9 @@ class PrometheusSource:
         # native=False; an https store always takes the Python client
         self.native = native and client is None
         self._native: dict[str, object] = {}
-        self._tpl: dict[str, object] = {}
+        self._tpl = GenMemo()                      # template -> (selector group, app) | False
         self._plans: dict[int, tuple] = {}
-        self._relit: dict[str, str] = {}          # app -> its escaped regex literal
+        self._relit = GenMemo()                    # app -> its escaped regex literal
         self._pool = None
         self.requests = 0
         self.bytes = 0
