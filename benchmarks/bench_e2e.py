@@ -507,6 +507,29 @@ def config3e2e(args):
                                 desc += f" len {len(ref)} (in {owners})"
                             print(f"[tm]   {o.id[:12]} {o.status} <- {desc}", file=sys.stderr, flush=True)
                     del docs_, stray
+                    from foremast_amd.engine.fp_types import FastWork as _FW
+                    live_fw = {id(w) for w in brain.fast.works.values()} if brain.fast is not None else set()
+                    fws_ = [o for o in gc.get_objects() if isinstance(o, _FW) and id(o) not in live_fw]
+                    print(f"[tm] FastWork not in works: {len(fws_)}", file=sys.stderr, flush=True)
+                    for o in fws_[-3:]:
+                        for ref in gc.get_referrers(o):
+                            if ref is fws_:
+                                continue
+                            desc = type(ref).__name__
+                            if isinstance(ref, (list, tuple, dict, set)):
+                                up = []
+                                for x in gc.get_referrers(ref):
+                                    if x is fws_ or isinstance(x, type(sys._getframe())):
+                                        continue
+                                    if isinstance(x, dict):
+                                        ks = [k for k, v in x.items() if v is ref][:2]
+                                        up.append(f"dict{ks}")
+                                    else:
+                                        up.append(type(x).__name__)
+                                desc += f" len {len(ref)} <- {up[:4]}"
+                            print(f"[tm]   FastWork {o.doc.id[:10]} serial {o.serial} <- {desc}", file=sys.stderr,
+                                  flush=True)
+                    del fws_
                     import collections
                     cnt = collections.Counter(type(o).__name__ for o in gc.get_objects())
                     prev_c = next((r["tc"] for r in soak_rows if "tc" in r), None)

@@ -302,7 +302,11 @@ class WindowTable:
         self.err = np.zeros(0, bool)         # last fetch of the window failed
         self.dup = np.zeros(0, np.uint8)     # an answer carried two series of one key value (see apply)
         self.wgen = np.zeros(0, np.int64)    # bumped whenever a window id is (re)assigned or released
-        self._qcache: dict = {}              # (group, window ids) -> rendered request, checked against wgen
+        # (group, window ids) -> rendered request, checked against wgen: this
+        # round's and the previous round's only (chunks that stop coming -- a
+        # fleet's canaries turning over -- age out instead of piling up)
+        self._qcache: dict = {}
+        self._qprev: dict = {}
         self.toff = np.zeros(0)              # sample phase vs start (0 for Prometheus; nan: not seen yet)
         self.values: list = []               # key values (sorted) per window
         self.frag: list = []                 # their escaped regex alternation
@@ -529,6 +533,7 @@ class WindowTable:
         lo = self.settled[w] + self.step[w]
         hi = self._limit(w, now)
         need = lo <= hi + 1e-6
+        self._qprev, self._qcache = self._qcache, {}        # a new round of the request cache
         # the earliest time a waiting live window gains a point (skip cycles before it)
         wait = ~need & self.live[w]
         self.next_due = float((lo[wait] + self.settle).min()) if wait.any() else math.inf
@@ -557,6 +562,10 @@ class WindowTable:
                 # are rendered once
                 ck = (gi, tuple(wl))
                 c = self._qcache.get(ck)
+                if c is None:
+                    c = self._qprev.get(ck)
+                    if c is not None:
+                        self._qcache[ck] = c
                 gen = self.wgen[w[i:j]]
                 if c is None or not np.array_equal(c[3], gen):
                     alt = "|".join([frag[x] for x in wl])
@@ -566,8 +575,6 @@ class WindowTable:
                         pp = self._qpre[gi] = tuple(render_query(grp, None, mark).split(mark))
                     qfrag = self.qfrag
                     c = (alt, [values[x] for x in wl], pp[0] + "|".join([qfrag[x] for x in wl]) + pp[1], gen)
-                    if len(self._qcache) > 65536:
-                        self._qcache.clear()
                     self._qcache[ck] = c
                 q = KeyedQuery(grp, None, float(lo[i:j].min()), float(hi[i:j].max()), alt=c[0], parts=c[1],
                                qtext=c[2])
