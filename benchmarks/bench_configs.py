@@ -343,6 +343,10 @@ def main():
                     "series, store file sizes and cycle p50/p99 every N cycles (a soak run)")
     ap.add_argument("--soak-save-every", type=int, default=0, help="e2e configs: an asynchronous history checkpoint "
                     "every N cycles (the service loop's cadence)")
+    ap.add_argument("--job-retention-s", type=float, default=0.0, help="e2e configs + sqlite: delete closed jobs "
+                    "older than this (simulated seconds; the store's JOB_RETENTION_SECONDS, 0 = keep all)")
+    ap.add_argument("--hpalog-retention-s", type=float, default=0.0, help="e2e configs + sqlite: HPA-log retention "
+                    "(simulated seconds; 0 = the store default, 1 day)")
     ap.add_argument("--no-prestage", action="store_true", help="e2e configs: do not pre-render the arriving jobs' "
                     "series (long soak runs: the source serves them when asked)")
     ap.add_argument("--board", action="store_true", help="e2e configs, several ranks on a GPU node: the ranks' "

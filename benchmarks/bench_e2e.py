@@ -249,7 +249,10 @@ def config3e2e(args):
             submit(AnalystClient(f"http://127.0.0.1:{port}/v1/healthcheck/", clock=clock))
             t_sub = time.perf_counter() - t_sub
         D.barrier()
-        store = SQLiteStore(db)
+        # (soak runs: job / HPA-log retention as the shipped store applies it,
+        # JOB_RETENTION_SECONDS / HPALOG_RETENTION_SECONDS)
+        store = SQLiteStore(db, hpalog_retention_s=args.hpalog_retention_s or 86400.0,
+                            job_retention_s=args.job_retention_s)
     print(f"[{kind}] rank {info.rank}: {S} jobs submitted in {t_sub:.1f}s ({args.store})", file=sys.stderr,
           flush=True)
     if not sliding_any:
@@ -359,11 +362,22 @@ def config3e2e(args):
                 pth = db + suf
                 dbs[suf or "jobs"] = os.path.getsize(pth) if os.path.exists(pth) else 0
         fp = brain.fast
+        g = gen_ms[-args.soak_every:]
+        net = [a - b for a, b in zip(w, g)]                  # the cycle without the synthetic generator
+        ob = onboard[-args.soak_every:]
+        fs = spans.get("fetch", [])[-args.soak_every:]
         return {"cycle": len(cyc_ms), "rss_mb": round(psutil.Process().memory_info().rss / 2**20, 1),
                 "dev_alloc_mb": round(torch.cuda.memory_allocated(dev) / 2**20, 1) if dev.type == "cuda" else None,
                 "dev_reserved_mb": round(torch.cuda.memory_reserved(dev) / 2**20, 1) if dev.type == "cuda" else None,
                 "exporter_series": len(exp.table), "store_bytes": dbs,
                 "cycle_p50_ms": round(float(np.percentile(w, 50)), 3), "cycle_p99_ms": round(float(np.percentile(w, 99)), 3),
+                "cycle_minus_generator_p50_ms": round(float(np.percentile(net, 50)), 3),
+                "cycle_minus_generator_p99_ms": round(float(np.percentile(net, 99)), 3),
+                "generator_ms_mean": round(float(np.mean(g)), 3) if g else 0.0,
+                "fetch_span_p50_ms": round(float(np.percentile(fs, 50)), 3) if fs else None,
+                "onboard_ms_per_cycle": round(1e3 * sum(a for a, _ in ob) / max(1, len(ob)), 3),
+                "onboard_jobs_per_cycle": round(sum(b for _, b in ob) / max(1, len(ob)), 2),
+                "jobs_pruned": getattr(store, "jobs_pruned", None),
                 "fast_jobs": len(fp.works) if fp is not None else None,
                 "resident_rows": (len(fp.sliding) + len(fp.static)) if fp is not None else None,
                 "model_cache_entries": len(brain.model_cache),

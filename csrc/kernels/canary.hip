@@ -797,6 +797,12 @@ FM_API int fm_pairwise_tests(const float* cur, int64_t ld_c, int n_cur, const fl
 // the block to the masked per-element path.  Per element that is ~0.75 VALU
 // instructions instead of ~8, which leaves the CU's issue slots to the
 // pairwise kernel running concurrently on the side stream.
+// The row is read through a buffer resource (wave-uniform, in SGPRs) with the
+// thread's 16 B as the VGPR offset and the 4-KB step as a scalar offset: no
+// 64-bit VGPR address per load, and the range check returns zeros past the
+// row (no clamp).  109 -> 72 VGPRs for the history kernel; the front kernel
+// drops from 111 to 87 (the p-value call now bounds it): five waves per SIMD
+// instead of four, i.e. one pairwise + four history workgroups per CU.
 template <int NV>
 __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, int T, double* red, int* redi,
                                                 float& mf, float& sd, int& n) {
@@ -804,16 +810,20 @@ __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, 
   typedef float nt4 __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x;
   const int nq = (T + 3) >> 2;
-  const nt4* h = reinterpret_cast<const nt4*>(hrow);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)hrow, (short)0, nq * 16, 0x00020000);
   nt4 q[NV];
   f2 acc = {0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int qi = tid + j * 256;
-    nt4 v = __builtin_nontemporal_load(h + (qi < nq ? qi : nq - 1));   // streamed once, unpredicated
-    if (qi >= nq) {
-      v = (nt4){0.f, 0.f, 0.f, 0.f};
-    } else if (qi == nq - 1) {
+#ifdef FM_HIST_FLAT
+    // (A/B build: the round-5 flat loads, one 64-bit VGPR address each)
+    nt4 v = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(hrow) + (qi < nq ? qi : nq - 1));
+    if (qi >= nq) v = (nt4){0.f, 0.f, 0.f, 0.f};
+#else
+    nt4 v = __builtin_bit_cast(nt4, __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, j * 4096, 2 /* nt */));
+#endif
+    if (qi == nq - 1) {
       const int e0 = qi * 4;
       if (e0 + 1 >= T) v.y = 0.f;
       if (e0 + 2 >= T) v.z = 0.f;
@@ -824,7 +834,7 @@ __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, 
     acc += v.zw;
   }
   const double tot = block_sum<256>((double)acc.x + (double)acc.y, red);
-  if (isfinite(tot)) {                       // block-uniform
+  if (isfinite(tot)) {
     n = T;
     mf = (float)(tot / T);
     const f2 mm = {mf, mf};
@@ -847,30 +857,15 @@ __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, 
     sd = (float)sqrt(sst / n);
     return;
   }
-  // Rows with missing samples (Prometheus gaps, a young service's short
-  // history, the sliding store's aligned window start): masked mean /
-  // variance over the register image already loaded -- no second pass over
-  // HBM.  Only this block-uniform branch pays for the masking (per element a
-  // class test, a select and a carry-in count add).
-  if (threadIdx.x == (nq - 1) % 256) {            // the tail quad: lanes past T are padding, not zeros
-    const int j = (nq - 1) / 256, e0 = (nq - 1) * 4;
-#pragma unroll
-    for (int jj = 0; jj < NV; ++jj)
-      if (jj == j) {
-        if (e0 + 1 >= T) q[jj].y = __builtin_nanf("");
-        if (e0 + 2 >= T) q[jj].z = __builtin_nanf("");
-        if (e0 + 3 >= T) q[jj].w = __builtin_nanf("");
-      }
-  }
   f2 ms = {0.f, 0.f};
   int cnt = 0;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const bool inq = tid + j * 256 < nq;
+    const int e0 = (tid + j * 256) * 4;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float x = q[j][c];
-      const bool ok = inq && isfinite(x);
+      const bool ok = e0 + c < T && isfinite(x);
       cnt += ok ? 1 : 0;
       ms[c & 1] += ok ? x : 0.f;
     }
@@ -881,11 +876,11 @@ __device__ __forceinline__ void block_row_stats(const float* __restrict__ hrow, 
   f2 a2 = {0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const bool inq = tid + j * 256 < nq;
+    const int e0 = (tid + j * 256) * 4;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const float x = q[j][c];
-      const float d = (inq && isfinite(x)) ? x - mf : 0.f;
+      const float d = (e0 + c < T && isfinite(x)) ? x - mf : 0.f;
       a2[c & 1] += d * d;
     }
   }
@@ -1213,6 +1208,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   tick_front_body<NV, K, PRIO>(FM_FRONT_ARGS);
 }
 
+// FM_FRONT_LDS=<bytes> (environment, read once): dynamic LDS requested per
+// front-kernel workgroup, i.e. a cap on how many of them share a CU (160 KB
+// of LDS: 33 KB -> at most four).  Default 33 KB: with the buffer-load history
+// role the kernel fits five waves per SIMD, and a fifth concurrent workgroup
+// per CU measured slower (more history streams during the pairwise phase).
+static unsigned front_lds() {
+  static const unsigned b = [] {
+    const char* e = getenv("FM_FRONT_LDS");
+    return e != nullptr ? (unsigned)atoi(e) : 33u * 1024u;
+  }();
+  return b;
+}
+
 static int front_occ() {
   static const int occ = [] {
     const char* e = getenv("FM_FRONT_OCC");
@@ -1249,15 +1257,16 @@ FM_API int fm_tick_front_rm(const float* hist, int64_t ld_h, int T, int64_t R, f
   if (queue != nullptr && nH < 8) nH = 8;
   const int nq = (T + 3) / 4;
   const dim3 grid((unsigned)(nP + nH)), block(256);
+  const unsigned lds = front_lds();
 #define FM_TF(NVV, KK)                                                                                             \
   if (front_prio())                                                                                                 \
-    hipLaunchKernelGGL((tick_front_kernel<NVV, KK, true>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c,  \
+    hipLaunchKernelGGL((tick_front_kernel<NVV, KK, true>), grid, block, lds, stream, hist, ld_h, T, R, hs, cur, ld_c,  \
                        n_cur, base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap); \
   else if (front_occ() == 5)                                                                                         \
-    hipLaunchKernelGGL((tick_front_kernel_o5<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c,     \
+    hipLaunchKernelGGL((tick_front_kernel_o5<NVV, KK>), grid, block, lds, stream, hist, ld_h, T, R, hs, cur, ld_c,     \
                        n_cur, base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap); \
   else                                                                                                               \
-  hipLaunchKernelGGL((tick_front_kernel<NVV, KK>), grid, block, 0, stream, hist, ld_h, T, R, hs, cur, ld_c, n_cur, \
+  hipLaunchKernelGGL((tick_front_kernel<NVV, KK>), grid, block, lds, stream, hist, ld_h, T, R, hs, cur, ld_c, n_cur, \
                      base, ld_b, n_base, suff, nP, min_mw, min_wil, min_kru, pvals, pstats, queue, rowmap)
 #define FM_TF_K(NVV)           \
   do {                         \

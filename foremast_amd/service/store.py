@@ -24,6 +24,7 @@ import dataclasses
 import hashlib
 import json
 import math
+import os
 import sqlite3
 import threading
 import urllib.parse
@@ -463,7 +464,9 @@ from .store_es import ElasticsearchStore, _ESSession  # noqa: E402,F401
 def open_store(spec: str, elastic_url: str = "") -> JobStore:
     """``memory`` | ``sqlite:<path>`` | ``elasticsearch`` (uses ELASTIC_URL)."""
     if spec.startswith("sqlite:"):
-        return SQLiteStore(spec[len("sqlite:"):])
+        return SQLiteStore(spec[len("sqlite:"):],
+                           hpalog_retention_s=float(os.environ.get("HPALOG_RETENTION_SECONDS", 86400.0)),
+                           job_retention_s=float(os.environ.get("JOB_RETENTION_SECONDS", 0.0)))
     if spec in ("elasticsearch", "es"):
         return ElasticsearchStore(elastic_url)
     return MemoryStore()

@@ -138,9 +138,14 @@ class SQLiteStore(JobStore):
       so a job resubmitted since it was leased is never overwritten.
     """
 
-    def __init__(self, path: str, hpalog_retention_s: float = 86400.0) -> None:
+    def __init__(self, path: str, hpalog_retention_s: float = 86400.0, job_retention_s: float = 0.0) -> None:
         self.path = path
         self.hpalog_retention_s = hpalog_retention_s
+        # closed jobs older than this are deleted (0: kept forever, as the
+        # reference's Elasticsearch index keeps every job document)
+        self.job_retention_s = job_retention_s
+        self._last_job_prune = 0.0
+        self.jobs_pruned = 0
         self._local = threading.local()
         self._sessions: dict[str, _Session] = {}
         self._log_writes = 0
@@ -199,8 +204,8 @@ class SQLiteStore(JobStore):
                       "rids blob not null, score blob not null, reason blob not null, vals blob not null)")
             # per job the batches that may hold its entries: a read scans only
             # [first_bid, last_bid], a job without HPA entries none.  Entries are
-            # keyed by documents.rid: job documents are never deleted from this
-            # store (only hpalog batches age out), so a rid is never reused
+            # keyed by documents.rid: the job retention never deletes the
+            # newest row (SQLite hands out max(rid) + 1), so a rid is never reused
             c.execute("create table if not exists hpalog_jobs (rid integer primary key, first_bid integer not null, "
                       "last_bid integer not null)")
             old = {r[0] for r in main.execute("select name from sqlite_master where type='table'")} & \
@@ -482,6 +487,8 @@ class SQLiteStore(JobStore):
                               (now - max_stuck_s,) + ip)
             s.last_seq = seq
             s.last_beat = now
+        if self.job_retention_s > 0 and now - self._last_job_prune >= 60.0:
+            self.prune_jobs(now)
         ids, vers, rids = s.snapshot(limit)
 
         def resolve(pos):
@@ -494,6 +501,29 @@ class SQLiteStore(JobStore):
                 out += [_decode_row(*got[r]) for r in chunk if r in got]
             return out
         return ClaimBatch(ids, vers, resolve, handles=rids)
+
+    def prune_jobs(self, now: float) -> int:
+        """Job retention (``JOB_RETENTION_SECONDS``): delete the closed jobs
+        (terminal status) last modified before ``now - job_retention_s``, and
+        their HPA-log index rows.  Runs at most once a minute of store time
+        from the claim; the ``documents_claim`` (status, modified) index finds
+        them.  The newest document is never deleted, so rids are not reused.
+        Returns how many were deleted."""
+        self._last_job_prune = now
+        cut = now - self.job_retention_s
+        term = tuple(sorted(ST.TERMINAL))
+        with self._txn() as c:
+            rids = [r for (r,) in c.execute(
+                f"select rid from documents where status in ({','.join('?' * len(term))}) and modified < ? "
+                f"and rid < (select max(rid) from documents)", term + (cut,))]
+            if not rids:
+                return 0
+            c.execute("delete from documents where rid in (select value from json_each(?))", (json.dumps(rids),))
+        lc = self._lconn()
+        with lc:
+            lc.execute("delete from hpalog_jobs where rid in (select value from json_each(?))", (json.dumps(rids),))
+        self.jobs_pruned += len(rids)
+        return len(rids)
 
     def keep(self, worker: str, ids, now: float | None = None, handles=None) -> None:
         """Jobs that stay alive: a session's leased jobs simply stay leased."""

@@ -349,3 +349,33 @@ def test_hpalog_writes_do_not_hold_the_jobs_file(tmp_path):
     st3 = SQLiteStore(old)
     assert [l.timestamp for l in st3.hpalogs("a:ns:h", 5)] == [T0]
     assert "hpalogs" not in {r[0] for r in st3._conn().execute("select name from sqlite_master where type='table'")}
+
+
+def test_job_retention_deletes_old_closed_jobs_only(tmp_path):
+    """JOB_RETENTION_SECONDS: closed jobs last modified before now - retention
+    go (with their HPA-log index rows); open jobs, recent closed jobs and the
+    newest row stay, and the claim keeps working on what is left."""
+    st = SQLiteStore(str(tmp_path / "j.db"), job_retention_s=3600.0)
+    st.put_many(_docs(30))
+    b = st.claim_batch("w", 100, 90.0, now=T0)
+    assert len(b) == 30
+    old, recent = b.ids[:10], b.ids[10:20]
+    st.update_uniform(old, {"status": ST.COMPLETED_HEALTH, "reason": ""}, now=T0 + 10, worker="w")
+    st.update_uniform(recent, {"status": ST.COMPLETED_UNHEALTH, "reason": "x"}, now=T0 + 3000, worker="w")
+    assert st.prune_jobs(T0 + 3650) == 10
+    assert all(st.get(i) is None for i in old)
+    assert all(st.get(i) is not None for i in recent + b.ids[20:])
+    assert st.prune_jobs(T0 + 3660) == 0                 # nothing else is old enough
+    # the claim path prunes at most once a minute of store time, and still claims
+    st.put_many(_docs(5, prefix="new"))
+    got = st.claim_batch("w", 100, 90.0, now=T0 + 7000)
+    assert {i for i in got.ids if i.startswith("new")} == {d.id for d in _docs(5, prefix="new")}
+    assert all(st.get(i) is None for i in recent)           # closed at T0 + 3000: older than 1 h at T0 + 7000
+    assert st.jobs_pruned == 20
+    # retention off (the default): nothing is ever deleted
+    keep = SQLiteStore(str(tmp_path / "k.db"))
+    keep.put_many(_docs(3))
+    kb = keep.claim_batch("w", 10, 90.0, now=T0)
+    keep.update_uniform(kb.ids, {"status": ST.COMPLETED_HEALTH, "reason": ""}, now=T0, worker="w")
+    keep.claim_batch("w", 10, 90.0, now=T0 + 10 ** 7)
+    assert all(keep.get(i) is not None for i in kb.ids)
