@@ -7,6 +7,7 @@ from __future__ import annotations
 import os
 import statistics
 import sys
+import threading as _threading
 import time
 
 import numpy as np
@@ -347,10 +348,56 @@ def config3e2e(args):
     if os.environ.get("FOREMAST_PROFILE_CYCLES"):
         import cProfile
         _prof = cProfile.Profile()
+    _sprof = None
+    if os.environ.get("FOREMAST_SOAK_PROFILE"):
+        import cProfile
+        _sprof = (cProfile.Profile(), cProfile.Profile())
 
     # --soak-every N: a long run's resources every N cycles
     soak_rows: list = []
     soak_ck = tempfile.mkdtemp(prefix="fm_soak_ck_") if args.soak_save_every else None
+
+    gc_ms = [0.0, 0]                         # soak: collector time and collections since the last sample
+
+    def _gc_cb(phase, info, _t=[0.0]):
+        if phase == "start":
+            _t[0] = time.perf_counter()
+        else:
+            gc_ms[0] += 1e3 * (time.perf_counter() - _t[0])
+            gc_ms[1] += 1
+
+    if args.soak_every:
+        import gc as _gc
+        _gc.callbacks.append(_gc_cb)
+
+    def cpu_probe() -> float:
+        # a fixed host workload (fresh objects, a dict, a small numpy op): a
+        # machine-level slowdown shows here too, a brain-state one does not
+        t0 = time.perf_counter()
+        for _ in range(5):
+            d = {i: (i, str(i)) for i in range(20000)}
+            sum(v[0] for v in d.values())
+            np.sort(np.arange(50000)[::-1])
+        return 1e3 * (time.perf_counter() - t0) / 5
+
+    def _sizes() -> dict:
+        # every container attribute of the brain, its fast path, window table,
+        # resident stores and exporter table with more than 64 entries (what
+        # grows across a soak names itself here)
+        out = {}
+        fp = brain.fast
+        for tag, obj in (("brain", brain), ("fast", fp), ("wt", getattr(fp, "wt", None)),
+                         ("sliding", getattr(fp, "sliding", None)), ("static", getattr(fp, "static", None)),
+                         ("xtable", getattr(exp, "table", None) if exp is not None else None),
+                         ("cache", getattr(brain, "model_cache", None))):
+            if obj is None:
+                continue
+            for k, v in vars(obj).items():
+                if isinstance(v, (dict, list, set, tuple)) and len(v) > 64:
+                    out[f"{tag}.{k}"] = len(v)
+                elif isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] > 64:
+                    out[f"{tag}.{k}"] = int(v.shape[0])
+        return out
 
     def soak_sample() -> dict:
         import gc
@@ -366,6 +413,8 @@ def config3e2e(args):
         net = [a - b for a, b in zip(w, g)]                  # the cycle without the synthetic generator
         ob = onboard[-args.soak_every:]
         fs = spans.get("fetch", [])[-args.soak_every:]
+        gcs = (round(gc_ms[0] / max(1, len(w)), 3), gc_ms[1])
+        gc_ms[0], gc_ms[1] = 0.0, 0
         return {"cycle": len(cyc_ms), "rss_mb": round(psutil.Process().memory_info().rss / 2**20, 1),
                 "dev_alloc_mb": round(torch.cuda.memory_allocated(dev) / 2**20, 1) if dev.type == "cuda" else None,
                 "dev_reserved_mb": round(torch.cuda.memory_reserved(dev) / 2**20, 1) if dev.type == "cuda" else None,
@@ -378,6 +427,16 @@ def config3e2e(args):
                 "onboard_ms_per_cycle": round(1e3 * sum(a for a, _ in ob) / max(1, len(ob)), 3),
                 "onboard_jobs_per_cycle": round(sum(b for _, b in ob) / max(1, len(ob)), 2),
                 "jobs_pruned": getattr(store, "jobs_pruned", None),
+                "gc_ms_per_cycle": gcs[0], "gc_collections": gcs[1],
+                "container_sizes": _sizes(),
+                "cpu_probe_ms": round(cpu_probe(), 3), "threads": _threading.active_count(),
+                "span_p50_ms": {k: round(float(np.percentile(v[-args.soak_every:], 50)), 3)
+                                for k, v in spans.items() if v},
+                "http_per_cycle_ms": ({k: round(1e3 * float(np.mean([h[k] for h in http_stats[-args.soak_every:]])), 3)
+                                       for k in ("server_s", "wait_s", "parse_s", "request_s")}
+                                      | {"requests": round(float(np.mean([h["requests"] for h in
+                                                                          http_stats[-args.soak_every:]])), 1)}
+                                      if http_stats else None),
                 "fast_jobs": len(fp.works) if fp is not None else None,
                 "resident_rows": (len(fp.sliding) + len(fp.static)) if fp is not None else None,
                 "model_cache_entries": len(brain.model_cache),
@@ -477,6 +536,15 @@ def config3e2e(args):
             _tprof.append("\n".join(f"{dt:9.1f}us {n:4d} {k:28s} {st_}" for dt, n, k, st_ in rows_[:80]))
         elif _prof is not None and len(cyc_ms) >= args.warmup:
             r = _prof.runcall(brain.run_once)
+        elif _sprof is not None and (args.warmup + 100 <= len(cyc_ms) < args.warmup + 150
+                                     or len(cyc_ms) >= args.warmup + args.steps - 50):
+            # FOREMAST_SOAK_PROFILE=<prefix>: cProfile of an early and the last
+            # 50-cycle window of a soak (which functions slowed down)
+            k = 0 if len(cyc_ms) < args.warmup + 150 else 1
+            r = _sprof[k].runcall(brain.run_once)
+            if len(cyc_ms) + 1 == args.warmup + args.steps:
+                for i, pr in enumerate(_sprof):
+                    pr.dump_stats(f"{os.environ['FOREMAST_SOAK_PROFILE']}_{'early' if i == 0 else 'late'}.prof")
         else:
             r = brain.run_once()
         if len(cyc_ms) + 1 == args.warmup + args.steps:

@@ -55,3 +55,27 @@ def test_steady_cycles_after_a_planning_cycle_do_not_collect(monkeypatch):
         assert calls == [{"refreeze": True}]         # the planning cycle only
     finally:
         gc.unfreeze()
+
+
+def test_steady_cycles_freeze_their_survivors_and_collect_periodically(monkeypatch):
+    """Once frozen, each steady cycle ends with gc.freeze() (O(1)): the
+    automatic collections only walk the cycle's young objects; a thaw + full
+    collection runs when GC_FULL_EVERY_S has passed since the last freeze."""
+    from foremast_amd.engine import brain as brain_mod
+    from tests.test_fastpath_models import _brain, _submit
+    monkeypatch.setattr(brain_mod, "GC_FREEZE_AFTER", 3)
+    clock, store, client, b, _ = _brain(True, "holt_winters", {})
+    try:
+        _submit(client, "continuous")
+        b.run_once()                                   # planning cycle: the first freeze
+        clock.t += 60.0
+        assert b._gc_frozen_at is not None and getattr(b, "gc_collections", 0) == 0
+        young = gc.get_count()[0]
+        b.run_once()                                   # a steady cycle: its survivors frozen
+        clock.t += 60.0
+        assert gc.get_count()[0] <= young + 50 and getattr(b, "gc_collections", 0) == 0
+        b._gc_frozen_at -= b.GC_FULL_EVERY_S + 1       # the full-collection interval passed
+        b.run_once()
+        assert b.gc_collections == 1 and gc.get_freeze_count() > 0
+    finally:
+        gc.unfreeze()
