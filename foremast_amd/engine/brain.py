@@ -472,7 +472,7 @@ class Brain(BrainStateMixin):
             self.gc_maintenance(refreeze=True)
         elif getattr(self, "_gc_frozen_at", None) is not None:
             self._gc_cycle_end()
-        return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast) - (len(self.fast.ghost_ids) if fast and self.fast.ghost_mask(fast) is not None else 0),
+        return {"claimed": len(batch), "rows": n_rows, "outcome": outcome, "fast_jobs": len(fast) - (len(self.fast.ghost_ids) if fast else 0),
                 "seconds": time.perf_counter() - t0}
 
     GC_IDLE_EVERY_S = 600.0

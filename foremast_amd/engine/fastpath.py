@@ -133,6 +133,10 @@ class FastPath(PlanMixin, FetchMixin, ArraysMixin, ModelsMixin, FinishMixin):
         self.ghost = None          # bool [len(list)]: the list's ghosts this cycle (None: none)
         self.ghost_ids: set = set()   # id() of this cycle's ghost FastWork objects
         self.ghost_cycles = 0      # cycles that ran on a ghosted layout (instead of a re-laid list)
+        # the same per sliding group of a multi-group fleet (fp_plan._layout_groups)
+        self._glays: dict = {}     # plan group -> (job list, cycle it was laid out)
+        self._gghost: dict = {}    # plan group -> (job list, ghost mask) of this cycle
+        self._lay_fast = None      # (the laid-out claim list, its non-sliding jobs)
         from .ingest import WindowTable
         cfg = brain.cfg
         self.wt = WindowTable(cfg.metric_settle_s, cfg.fetch_batch, cfg.fetch_max_values)

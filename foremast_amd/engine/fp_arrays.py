@@ -28,7 +28,18 @@ class ArraysMixin:
             self._last_groups = g
             return g
         g: dict[tuple, list[FastWork]] = {}
-        for fw in works:
+        laid = self._glays
+        for L, _ in laid.values():
+            # a multi-group fleet's sliding group is its laid-out list itself
+            # (ghosts included and masked by ghost_mask): one width class per
+            # group, as the one-group path above
+            f0 = L[0]
+            g[f0.plan.group + (f0.wclass, False)] = L
+        lf = self._lay_fast
+        rest = lf[1] if laid and lf is not None and works is lf[0] else works   # (the laid-out part is placed)
+        for fw in rest:
+            if laid and fw.plan.sliding and fw.plan.group in laid:
+                continue
             k = fw.gkey
             if k is None or k[-2] != fw.wclass:
                 k = fw.gkey = fw.plan.group + (fw.wclass, fw.wcur is not None)

@@ -349,7 +349,7 @@ class FinishMixin:
             if self.works.get(w.doc.id) is w:
                 del self.works[w.doc.id]
                 self._gcount_add(w.plan.group, -1)
-                if w.plan.sliding and self._lay is not None:
+                if w.plan.sliding and (self._lay is not None or w.plan.group in self._glays):
                     self._left.append(w)            # a ghost of the layout from the next claim on
 
     def take_evicted(self) -> list[FastWork]:

@@ -164,15 +164,18 @@ class PlanMixin:
                     self._jid_cache[id(keep_jid[0])] = keep_jid
                 fws = todo = self._layout(fws)
             else:
+                glays_prev = self._glays
                 self._set_layout(None)
                 todo = [fw for fw in fws if not ((immutable or fw.wcur is not None) and fw.settled)]
                 if len(todo) == len(fws):
                     todo = fws
+                fws, todo = self._layout_groups(fws, todo, glays_prev)
             self._specs = {}
             self.todo = todo
             self._last = (batch.ids, batch.versions, fws, todo)
             return fws, []
         lay_prev, ghost_prev = self._lay, self.ghost     # (kept for arrivals appended to it)
+        glays_prev, gghost_prev = self._glays, self._gghost
         self._set_layout(None)
         handles = getattr(batch, "handles", None)
         # known at this version vs not, in C-level passes (a 10k-job claim
@@ -207,6 +210,10 @@ class PlanMixin:
                 # the plan of the job it replaces
                 gone = [] if ghost_prev is None or len(ghost_prev) != len(L0) else \
                     [L0[j] for j in np.flatnonzero(ghost_prev).tolist()]
+                ghosts = {self._sig_of(fw): fw for fw in gone + self._left if works.get(fw.doc.id) is not fw}
+            elif glays_prev:
+                # the same per group of a multi-group fleet (its sliding groups' layouts)
+                gone = [L_[j] for L_, msk in gghost_prev.values() for j in np.flatnonzero(msk).tolist()]
                 ghosts = {self._sig_of(fw): fw for fw in gone + self._left if works.get(fw.doc.id) is not fw}
             for k, d in zip(unknown, docs):
                 old = works.get(d.id)
@@ -250,6 +257,8 @@ class PlanMixin:
             todo = fast
         if len(self._gcount) == 1 and fast and fast[0].plan.sliding and todo is fast and not rest:
             fast = todo = self._layout_arrivals(fast, len(fast) - len(new_fw), lay_prev)
+        elif len(self._gcount) > 1 and fast:
+            fast, todo = self._layout_groups(fast, todo, glays_prev)
         self.todo = todo
         self._last = (batch.ids, batch.versions, fast, todo) if not rest else None
         return fast, rest
@@ -415,6 +424,8 @@ class PlanMixin:
     def _set_layout(self, works) -> None:
         self._lay = None if works is None else (works, self.cycle)
         self.ghost, self.ghost_ids = None, set()
+        self._glays, self._gghost = {}, {}
+        self._lay_fast = None
         if works is not None:
             self._left = []             # released jobs of the previous layout: not in this one
             self._sigs = {}
@@ -446,7 +457,70 @@ class PlanMixin:
     def ghost_mask(self, works) -> np.ndarray | None:
         """This cycle's ghost mask of a job list (None: every job is live)."""
         lay = self._lay
-        return self.ghost if (self.ghost is not None and lay is not None and works is lay[0]) else None
+        if self.ghost is not None and lay is not None and works is lay[0]:
+            return self.ghost
+        if self._gghost and works:
+            g = self._gghost.get(works[0].plan.group)
+            if g is not None and g[0] is works:
+                return g[1]
+        return None
+
+    def _layout_groups(self, fast: list, todo: list, glays_prev: dict) -> tuple[list, list]:
+        """Stable layouts for the sliding groups of a MULTI-group fleet (a
+        mixed fleet: canary table groups beside continuous / HPA sliding
+        groups), the one-group layout per group: each sliding group's list
+        keeps last cycle's order, jobs that left stay as ghosts (scored, never
+        judged), re-armed jobs took their ghost slot back in ``prepare``, new
+        jobs are appended -- so every per-list memo of the group (template
+        lists, row map, static columns, cache keys, model arrays, the early
+        LSTM launch) sees an unchanged or extended list instead of a
+        re-ordered one it must rebuild each cycle.  Re-laid afresh every
+        LAYOUT_COMPACT_EVERY cycles, when ghosts would pass
+        LAYOUT_GHOST_FRAC, or when a new job reads a ghost's rows.  Returns
+        (fast, todo): the non-sliding jobs in claim order, then the layouts."""
+        import os
+        if os.environ.get("FM_GROUP_LAYOUT", "1") == "0":
+            return fast, todo
+        sl: dict = {}
+        other_f = []
+        for fw in fast:
+            (sl.setdefault(fw.plan.group, []) if fw.plan.sliding else other_f).append(fw)
+        if not sl:
+            return fast, todo
+        other_t = [fw for fw in todo if not fw.plan.sliding] if todo is not fast else other_f
+        lays, gghost, gids = {}, {}, set()
+        for g, cur in sl.items():
+            prev = glays_prev.get(g)
+            L, laid, ghost = cur, self.cycle, None
+            if prev is not None and self.cycle - prev[1] < self.LAYOUT_COMPACT_EVERY:
+                L0 = prev[0]
+                m = self._jid(cur).match_in(self._jid(L0))
+                if m is not None:
+                    cand, hit, _ = m
+                    new = [cur[j] for j in np.flatnonzero(~hit).tolist()]
+                    L2 = L0 + new if new else L0
+                    live = np.zeros(len(L2), bool)
+                    live[cand[hit]] = True
+                    live[len(L0):] = True
+                    gm = ~live
+                    gj = np.flatnonzero(gm)
+                    clash = bool(new) and len(gj) and len(np.intersect1d(
+                        np.concatenate([L2[j].rows for j in gj.tolist()]), np.concatenate([fw.rows for fw in new])))
+                    if not clash and len(gj) <= self.LAYOUT_GHOST_FRAC * len(L2):
+                        L, laid, ghost = L2, prev[1], (gm if len(gj) else None)
+                        self.arrivals_laid += len(new)
+            lays[g] = (L, laid)
+            if ghost is not None:
+                gghost[g] = (L, ghost)
+                gids.update(id(L[j]) for j in np.flatnonzero(ghost).tolist())
+                self.ghost_cycles += 1
+        self._glays, self._gghost, self.ghost_ids = lays, gghost, gids
+        if self._left:
+            self._left = [w for w in self._left if id(w) in gids]     # revival candidates: this cycle's ghosts
+        laid_out = [fw for L, _ in lays.values() for fw in L]
+        fast2 = other_f + laid_out
+        self._lay_fast = (fast2, other_f)          # (groups() buckets only the non-sliding part)
+        return fast2, other_t + laid_out
 
     def live(self, works: list) -> list:
         """``works`` without this cycle's ghosts."""

@@ -481,3 +481,81 @@ def test_gpu_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, 
     forecast reused for the laid-out rows with only the arrivals' rows
     forecast in the cycle."""
     test_arrivals_and_departures_every_cycle_equal_general_path(algo, kind, staged, device="cuda")
+
+
+@pytest.mark.parametrize("algo,staged", [("holt_winters", False), ("mixed", True)])
+def test_multi_group_fleet_churn_every_cycle_equal_general_path(algo, staged, device="cpu"):
+    """A MULTI-group fleet (canaries in the window table beside a continuous
+    and an HPA sliding group) with churn in every group every cycle for 16
+    cycles: new continuous and HPA services arrive, continuous monitors
+    regress and close, closed ones are re-armed, HPA jobs are resubmitted,
+    and a canary arrives.  Each sliding group keeps a stable layout
+    (fp_plan._layout_groups: ghosts for jobs that left, re-armed jobs back in
+    their ghost slot, arrivals appended); verdicts, reasons, HPA logs and
+    gauges equal the general path's cycle by cycle."""
+    faults = {f"cont{j}": 4.0 for j in range(2, 40, 5)}
+    faults["canary1-7687b9f4daaaaaaaaa-p0000"] = 5.0
+    a = _brain(True, algo, faults, device, staged=staged)
+    b = _brain(False, algo, faults, device)
+    a[3].fast.LAYOUT_GHOST_FRAC = 0.5
+    a[3].fast.LAYOUT_COMPACT_EVERY = 8
+    hpa_m = ["cpu", "latency", "error5xx", "memory"]
+
+    def cont(c, j):
+        return c.start_analyzing("prod", f"cont{j}", None, _metrics(4), 10, "continuous")
+
+    def hpa(c, j):
+        return c.start_analyzing("prod", f"hpa{j}", None, _metrics(4), 10, "hpa", hpa_m)
+
+    def canary(c, j):
+        app = f"canary{j}"
+        return c.start_analyzing("default", app, [_pods(app, 2, "7687b9f4d"), _pods(app, 2, "5db89899b")],
+                                 _metrics(4), 10, "canary")
+
+    ids, app_of = [], {}
+    for kind, fn, n in (("cont", cont, 8), ("hpa", hpa, 6), ("canary", canary, 2)):
+        for j in range(n):
+            i1, i2 = fn(a[2], j), fn(b[2], j)
+            assert i1 == i2
+            ids.append(i1)
+            app_of[i1] = (kind, j)
+    nxt = {"cont": 8, "hpa": 6, "canary": 2}
+    rearmed = set()
+    for cyc in range(16):
+        if cyc:
+            for kind, fn in (("cont", cont), ("hpa", hpa)) + ((("canary", canary),) if cyc % 4 == 0 else ()):
+                j = nxt[kind]
+                i1, i2 = fn(a[2], j), fn(b[2], j)
+                assert i1 == i2
+                ids.append(i1)
+                app_of[i1] = (kind, j)
+                nxt[kind] += 1
+            # an HPA resubmission (same id, same plan) and a closed monitor re-armed
+            hj = app_of[[i for i in ids if app_of[i][0] == "hpa"][cyc % 6]][1]
+            assert hpa(a[2], hj) == hpa(b[2], hj)
+            closed = [app_of[i][1] for i in ids if app_of[i][0] == "cont"
+                      and a[1].get(i).status == ST.COMPLETED_UNHEALTH and app_of[i][1] not in rearmed]
+            if closed:
+                rearmed.add(closed[0])
+                i1, i2 = cont(a[2], closed[0]), cont(b[2], closed[0])
+                assert i1 == i2
+                if i1 not in app_of:
+                    ids.append(i1)
+                    app_of[i1] = ("cont", closed[0])
+        ra, rb = a[3].run_once(), b[3].run_once()
+        assert ra["claimed"] == rb["claimed"] and ra["rows"] == rb["rows"], (cyc, ra, rb)
+        _compare(a, b, ids, cyc)
+        a[0].t += 60
+        b[0].t += 60
+    f = a[3].fast
+    assert len(f._gcount) > 1                                   # a multi-group fleet throughout
+    assert f.arrivals_laid > 0 and f.ghost_cycles > 0, (f.arrivals_laid, f.ghost_cycles)
+    assert f.revived > 0 and f.resubmits_patched > 0, (f.revived, f.resubmits_patched)
+    assert ST.COMPLETED_UNHEALTH in {a[1].get(j).status for j in ids}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo,staged", [("holt_winters", True), ("mixed", True)])
+def test_gpu_multi_group_fleet_churn_every_cycle_equal_general_path(algo, staged):
+    """The multi-group layout parity on the MI355X kernels."""
+    test_multi_group_fleet_churn_every_cycle_equal_general_path(algo, staged, device="cuda")
