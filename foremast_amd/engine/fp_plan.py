@@ -151,12 +151,22 @@ class PlanMixin:
         # toggle, a continuous monitor re-armed: HpaController.go:204-229,
         # Barrelman.go:552-565) keep their FastWork -- its list position, row
         # map, templates, memos and exporter series -- with the new document
-        fws = list(map(works.get, batch.ids))
-        if self._patch_resubmitted(batch, fws, now):
-            fws = list(map(works.get, batch.ids))
+        # (one pass over the jobs' versions serves every test below: each pass
+        # touches every FastWork, and a long-churned fleet's objects are
+        # spread over the heap -- docs/ROUND6.md §5)
+        n_b = len(batch.ids)
+        fws = list(map(works.get, batch.ids, _NO_FW_ITER(n_b)))
+        same = np.fromiter(map(operator.eq, map(_version_of, fws), batch.versions), bool, n_b)
+        if not same.all():
+            known = np.fromiter(map(operator.is_not, fws, _NO_FW_ITER(n_b)), bool, n_b)
+            cand = np.flatnonzero(known & ~same)
+            if len(cand):
+                pk = self._patch_resubmitted(batch, fws, now, cand.tolist())
+                if pk:
+                    same[pk] = True
         # every job known at its version (the steady state of a fleet that only
         # lost jobs since the last claim): the lists through C-level passes
-        if None not in fws and list(map(_version_of, fws)) == list(batch.versions):
+        if same.all():
             if len(self._gcount) == 1 and fws and fws[0].plan.sliding:
                 # one sliding group: every job is due every cycle -- on the
                 # stable layout when the fleet only lost jobs since it was laid
@@ -166,10 +176,7 @@ class PlanMixin:
             else:
                 glays_prev = self._glays
                 self._set_layout(None)
-                todo = [fw for fw in fws if not ((immutable or fw.wcur is not None) and fw.settled)]
-                if len(todo) == len(fws):
-                    todo = fws
-                fws, todo = self._layout_groups(fws, todo, glays_prev)
+                fws, todo = self._layout_groups(fws, None, glays_prev)     # (todo: due jobs, filtered there)
             self._specs = {}
             self.todo = todo
             self._last = (batch.ids, batch.versions, fws, todo)
@@ -178,10 +185,8 @@ class PlanMixin:
         glays_prev, gghost_prev = self._glays, self._gghost
         self._set_layout(None)
         handles = getattr(batch, "handles", None)
-        # known at this version vs not, in C-level passes (a 10k-job claim
-        # with a few arrivals: no per-job Python loop)
-        fws = list(map(works.get, batch.ids, _NO_FW_ITER(len(batch.ids))))
-        same = np.fromiter(map(operator.eq, map(_version_of, fws), batch.versions), bool, len(fws))
+        # known at this version vs not (the pass above), a 10k-job claim with a
+        # few arrivals: no per-job Python loop
         unknown = np.flatnonzero(~same).tolist()
         kn = np.flatnonzero(same).tolist()
         fast = list(operator.itemgetter(*kn)(fws)) if len(kn) > 1 else [fws[k] for k in kn]
@@ -275,19 +280,19 @@ class PlanMixin:
     _PLAN_FIELDS = ("app_name", "namespace", "strategy", "current_config", "baseline_config", "historical_config",
                     "current_metric_store", "baseline_metric_store", "historical_metric_store", "hpa_metrics")
 
-    def _patch_resubmitted(self, batch, fws: list, now: float) -> int:
-        """Known jobs claimed at a new version whose new document plans the
-        same (same queries, stores, strategy and HPA template: a resubmission
-        re-arms the job): the FastWork takes the new document, version, end
-        time and store row in place, so the job list -- and everything kept
-        per list -- is unchanged.  Returns how many were patched."""
+    def _patch_resubmitted(self, batch, fws: list, now: float, cand: list) -> list:
+        """Known jobs claimed at a new version (``cand``: their claim
+        positions) whose new document plans the same (same queries, stores,
+        strategy and HPA template: a resubmission re-arms the job): the
+        FastWork takes the new document, version, end time and store row in
+        place, so the job list -- and everything kept per list -- is
+        unchanged.  Returns the claim positions patched."""
         vers = batch.versions
-        cand = [k for k, fw in enumerate(fws) if fw is not None and fw.version != vers[k]]
         if not cand:
-            return 0
+            return []
         docs = batch.docs(cand)
         handles = getattr(batch, "handles", None)
-        patched = []
+        patched, pos = [], []
         for k, d in zip(cand, docs):
             fw = fws[k]
             od = fw.doc
@@ -304,10 +309,11 @@ class PlanMixin:
                 fw.handle = int(handles[k])
             fw.failed, fw.errors = "", []
             patched.append(fw)
+            pos.append(k)
         if patched:
             self.resubmits_patched += len(patched)
             self._patch_static_cols(patched)
-        return len(patched)
+        return pos
 
     def _plan_sig(self, d: Document) -> tuple:
         return tuple(getattr(d, f) if f != "hpa_metrics" else tuple(sorted((k, str(v)) for k, v in d.hpa_metrics.items()))
@@ -479,15 +485,24 @@ class PlanMixin:
         LAYOUT_GHOST_FRAC, or when a new job reads a ghost's rows.  Returns
         (fast, todo): the non-sliding jobs in claim order, then the layouts."""
         import os
+        imm = self._immutable
+
+        def due(ws):                              # (``todo`` None: the due jobs of ``ws`` are computed here)
+            t = [fw for fw in ws if not ((imm or fw.wcur is not None) and fw.settled)]
+            return ws if len(t) == len(ws) else t
         if os.environ.get("FM_GROUP_LAYOUT", "1") == "0":
-            return fast, todo
+            return fast, (due(fast) if todo is None else todo)
         sl: dict = {}
         other_f = []
         for fw in fast:
             (sl.setdefault(fw.plan.group, []) if fw.plan.sliding else other_f).append(fw)
         if not sl:
-            return fast, todo
-        other_t = [fw for fw in todo if not fw.plan.sliding] if todo is not fast else other_f
+            return fast, (due(fast) if todo is None else todo)
+        # sliding jobs are due every cycle; only the others are filtered
+        if todo is None:
+            other_t = due(other_f)
+        else:
+            other_t = [fw for fw in todo if not fw.plan.sliding] if todo is not fast else other_f
         lays, gghost, gids = {}, {}, set()
         for g, cur in sl.items():
             prev = glays_prev.get(g)
