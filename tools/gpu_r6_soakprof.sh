@@ -12,6 +12,7 @@ for w in early late; do
   python -c "
 import pstats,sys
 s=pstats.Stats('gpurun_out/sp_$w.prof', stream=open('gpurun_out/sp_$w.txt','w'))
-s.sort_stats('tottime').print_stats(60); s.sort_stats('cumulative').print_stats(80)" || exit 1
+s.sort_stats('tottime').print_stats(60); s.sort_stats('cumulative').print_stats(80)
+s.sort_stats('cumulative').print_callees('prepare'); s.print_callees('_layout_groups'); s.print_callees('fetch_all')" || exit 1
 done
 echo done
