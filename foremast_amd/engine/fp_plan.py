@@ -21,6 +21,9 @@ class _NoFw:
 _NOFW = _NoFw()
 
 
+_lgrp_of = operator.attrgetter("lgrp")
+
+
 def _NO_FW_ITER(n: int):
     return itertools.repeat(_NOFW, n)
 
@@ -494,8 +497,8 @@ class PlanMixin:
             return fast, (due(fast) if todo is None else todo)
         sl: dict = {}
         other_f = []
-        for fw in fast:
-            (sl.setdefault(fw.plan.group, []) if fw.plan.sliding else other_f).append(fw)
+        for fw, lg in zip(fast, map(_lgrp_of, fast)):     # (one attribute per job: the layout split)
+            (other_f if lg is None else sl.setdefault(lg, [])).append(fw)
         if not sl:
             return fast, (due(fast) if todo is None else todo)
         # sliding jobs are due every cycle; only the others are filtered

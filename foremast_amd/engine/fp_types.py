@@ -86,9 +86,11 @@ class FastWork:
     wcur: np.ndarray | None = None
     wbase: np.ndarray | None = None
     serial: int = 0                            # unique per FastWork ever created (JobIds identity)
+    lgrp: tuple | None = None                  # plan group of a sliding job, else None (layout split)
 
     def __post_init__(self) -> None:
         self.serial = next(_SERIAL)
+        self.lgrp = self.plan.group if self.plan.sliding else None
 
 
 _SERIAL = __import__("itertools").count(1)
