@@ -122,6 +122,9 @@ class ModelCache:
         self._gen = 0            # bumped on every key -> slot change
         self._memo = None        # (keys list object, gen, resolved slots); keys lists are never mutated
         self._root_g = None      # (root keys list, gen, slots per root position; -2 = not looked up)
+        self._log: list = []     # (gen, key) of every key -> slot change since the memo's gen
+        self._mpos = None        # (keys list object, key -> position) of the memo list (no duplicates)
+        self.patched = 0         # lookups served by patching the memo (extended lists)
 
     def __len__(self) -> int:
         return len(self.entries)
@@ -132,6 +135,7 @@ class ModelCache:
 
     def _drop_slot(self, slab: _Slab, slot: int) -> None:
         self._gen += 1
+        self._log.append((self._gen, slab.keys[slot]))
         del self.entries[slab.keys[slot]]
         slab.keys[slot] = None
         slab.free.append(slot)
@@ -178,6 +182,11 @@ class ModelCache:
         for j, slot in zip(keep, slots):
             slab.keys[slot] = keys[j]
             self.entries[keys[j]] = base | slot
+        if self._memo is not None:                 # (the memo patches these keys' slots on its next use)
+            self._log.extend((self._gen, keys[j]) for j in keep)
+            if len(self._log) > 1 << 17:           # (no lookup for a long while: drop the memo instead)
+                self._log.clear()
+                self._memo = None
 
     # ------------------------------------------------------------------ forecast
     def es_lookup(self, keys: list, t_last: np.ndarray, step: float, now: float, T: int, kind: int) -> "EsPlan":
@@ -194,12 +203,21 @@ class ModelCache:
             # same batch object and no key -> slot change since: a steady-state
             # shard re-scoring its series skips the per-row lookups
             g = memo[2].copy()
+        elif memo is not None and (memo[0] is keys or getattr(keys, "base", None) is memo[0]) and \
+                (g := self._patched(memo, keys)) is not None:
+            # the memo's list (or that list with jobs appended: arrivals laid
+            # out at the end) after key -> slot changes (fits stored for last
+            # cycle's arrivals, evictions): the logged keys' rows re-resolved
+            # and only the appended rows looked up
+            self._memo = (keys, self._gen, g.copy())
+            self.patched += 1
         elif root is not None and rg is not None and rg[0] is root and rg[1] == self._gen and \
                 (rg[2][keys.ix] != -2).all():
             # the batch is root[ix] of an earlier one (jobs left the fleet):
             # index the lookups kept per root position
             g = rg[2][keys.ix]
             self._memo = (keys, self._gen, g.copy())
+            self._log.clear()
         else:
             g = np.fromiter((-1 if v is None else v for v in map(self.entries.get, keys)), np.int64, R)
             if len(set(keys)) != R:                # a key seen twice in one batch is fitted, not advanced twice
@@ -209,6 +227,7 @@ class ModelCache:
                         g[i] = -1
                     seen.add(key)
             self._memo = (keys, self._gen, g.copy())
+            self._log.clear()
         # lookups per root position (-2: not looked up), for later subsets
         if root is None:
             self._root_g = (keys, self._gen, g.copy())
@@ -234,6 +253,40 @@ class ModelCache:
             knew[rows] = k
             slabs.append(slab)
         return EsPlan(t_last, sid, slot, usable, knew, slabs)
+
+    def _patched(self, memo, keys) -> np.ndarray | None:
+        """The memo's lookups brought to the current generation through the
+        change log, extended by lookups of ``keys``' appended rows (None: a
+        duplicate key, or no log for the memo's generation)."""
+        mk, mgen, mg = memo[0], memo[1], memo[2]
+        if self._log and self._log[0][0] <= mgen:
+            return None                           # (the log must start after the memo's generation)
+        mp = self._mpos
+        if mp is None or mp[0] is not mk:
+            pos = {k: i for i, k in enumerate(mk)}
+            if len(pos) != len(mk):
+                return None
+            mp = (mk, pos)
+        pos = mp[1]
+        g = mg.copy()
+        for gn, k in self._log:
+            if gn > mgen:
+                i = pos.get(k)
+                if i is not None:
+                    v = self.entries.get(k)
+                    g[i] = -1 if v is None else v
+        n0 = len(mk)
+        if len(keys) > n0:
+            tail = keys[n0:]
+            if any(k in pos for k in tail) or len(set(tail)) != len(tail):
+                return None
+            g = np.concatenate([g, np.fromiter((-1 if v is None else v for v in map(self.entries.get, tail)),
+                                               np.int64, len(tail))])
+            pos = dict(pos)
+            pos.update((k, n0 + i) for i, k in enumerate(tail))
+        self._mpos = (keys, pos)
+        self._log.clear()
+        return g
 
     def es_commit(self, slab: "_Slab", sl: np.ndarray, t_last: np.ndarray, dead: np.ndarray) -> None:
         """After an update of ``slab``'s slots ``sl``: their sample time and

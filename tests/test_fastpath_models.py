@@ -317,6 +317,42 @@ def test_model_cache_subset_key_lists_match_fresh_lookups():
     assert a.hits == b.hits and a.misses == b.misses
 
 
+def test_model_cache_extended_key_lists_match_fresh_lookups():
+    """Arrivals hand the model cache a key list that is the previous list with
+    new keys appended (TemplateList.extended), after the previous cycle stored
+    fits for its own misses: the memo is patched through the change log and
+    only the appended keys are looked up -- the same slots, forecasts and
+    hit / miss counts as plain lists of the same keys, cycle after cycle, with
+    an LRU eviction on the way (capacity below the fleet)."""
+    import torch
+    from foremast_amd.engine.sources import TemplateList
+    from foremast_amd.models.cache import ModelCache
+    rng = np.random.default_rng(1)
+    R, T, H, step = 40, 300, 4, 60.0
+    t = np.arange(T + 12)
+    hist = (10 + np.sin(2 * np.pi * t / 24)[None, :] + 0.1 * rng.normal(size=(R, T + 12))).astype(np.float32)
+    keys = [(f"ns/app{i}", "cpu", "cpu", "exponential_smoothing") for i in range(R)]
+
+    def run(cache, key_list, n, k):
+        h = torch.from_numpy(np.ascontiguousarray(hist[:n, k:k + T]))
+        tl = np.full(n, 1e9 + step * (T + k))
+        return cache.es_forecast(key_list, tl, step, 1e9, h, T, 1, H, lambda sub: 24)
+
+    a, b = ModelCache(capacity=30), ModelCache(capacity=30)
+    cur = TemplateList(keys[:12])
+    n = 12
+    for k in range(8):
+        fa, sa = run(a, cur, n, k)
+        fb, sb = run(b, list(keys[:n]), n, k)
+        torch.testing.assert_close(fa, fb)
+        torch.testing.assert_close(sa, sb)
+        assert (a.hits, a.misses) == (b.hits, b.misses), k
+        n2 = n + 4                                   # four arrivals appended
+        cur = TemplateList.extended(cur, keys[n:n2])
+        n = n2
+    assert a.misses > 0 and a.hits > 0 and a.patched >= 6, a.patched
+
+
 def test_mixed_churning_fleet_fast_path_equals_general_path():
     """one brain, every strategy side by side -- canary and
     rolling-update windows (two static groups), continuous monitors of two
