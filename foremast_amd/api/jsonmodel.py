@@ -107,6 +107,12 @@ def _converter(tp):
     if origin in (dict, typing.Dict):
         el = _converter(typing.get_args(tp)[1])
         return lambda v: None if v is None else ({k: el(x) for k, x in v.items()} if isinstance(v, dict) else {})
+    if tp is float:                       # (the scalar cases of _convert, without its per-value type inspection)
+        return lambda v: float(v) if isinstance(v, (int, float)) and v.__class__ is not bool else v
+    if tp is int:
+        return lambda v: int(v) if isinstance(v, (int, float)) and v.__class__ is not bool else v
+    if origin is None and isinstance(tp, type):
+        return _str_or_none                     # bool / other scalars decode as themselves
     return lambda v: _convert(tp, v)
 
 

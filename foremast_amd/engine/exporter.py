@@ -62,6 +62,14 @@ def _esc(v: str) -> str:
     return v.replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
 
 
+@functools.lru_cache(maxsize=1 << 16)
+def _label_suffix(ns: str, app: str, cluster: str) -> bytes:
+    """The label block and separator of a sample line, encoded once per
+    (namespace, app, cluster): every series of a job shares it."""
+    return (f'{{namespace="{_esc(ns)}",app="{_esc(app)}"' + (f',cluster="{_esc(cluster)}"' if cluster else "")
+            + "} ").encode()
+
+
 def _grow(a: np.ndarray, n: int, fill) -> np.ndarray:
     if n <= len(a):
         return a
@@ -119,26 +127,37 @@ class GaugeTable:
         return len(self.index)
 
     def slots(self, keys: list[tuple[str, str, str]]) -> np.ndarray:
-        out = np.empty(len(keys), np.int64)
         idx = self.index
         with self.lock:
+            got = list(map(idx.get, keys))
             new_k, new_s = [], []
-            for i, k in enumerate(keys):
-                s = idx.get(k)
-                if s is None:
-                    if self._free:
-                        s = self._free.pop()
-                        self.keys[s] = k
-                    else:
-                        s = len(self.keys)
-                        self.keys.append(k)
-                    idx[k] = s
-                    new_k.append(k)
-                    new_s.append(s)
-                elif self._nret and self.expire[s] < np.inf:
-                    self.expire[s] = np.inf          # looked up again: live again
-                    self._nret -= 1
-                out[i] = s
+            if None in got:
+                free, kl = self._free, self.keys
+                for i in [i for i, s in enumerate(got) if s is None]:
+                    k = keys[i]
+                    s = idx.get(k)                   # (a key twice in one call)
+                    if s is None:
+                        if free:
+                            s = free.pop()
+                            kl[s] = k
+                        else:
+                            s = len(kl)
+                            kl.append(k)
+                        idx[k] = s
+                        new_k.append(k)
+                        new_s.append(s)
+                    got[i] = s
+            out = np.array(got, np.int64) if got else np.zeros(0, np.int64)
+            if self._nret and len(out):
+                # keys looked up again while retiring: live again (a new
+                # key's slot is free or fresh: nan / beyond, never finite)
+                n0 = len(self.expire)
+                old = out[out < n0]
+                ex = self.expire[old]
+                back = np.unique(old[ex < np.inf])
+                if len(back):
+                    self.expire[back] = np.inf
+                    self._nret -= len(back)
             if new_k:
                 n = len(self.keys)
                 if n > len(self.vals):
@@ -166,8 +185,8 @@ class GaugeTable:
         for name, items in fams.items():
             f = self._family(name)
             k0 = self._fn[f]
-            enc = [(f'{name}{{namespace="{_esc(k[1])}",app="{_esc(k[2])}"'
-                    + (f',cluster="{_esc(k[3])}"' if len(k) > 3 and k[3] else "") + "} ").encode() for k, _ in items]
+            nb = name.encode()
+            enc = [nb + _label_suffix(k[1], k[2], k[3] if len(k) > 3 else "") for k, _ in items]
             buf = self._fprefix[f]
             base = len(buf)
             buf += b"".join(enc)
@@ -435,6 +454,7 @@ class BrainExporter:
 
     # ---------------------------------------------------------------- writes
     @staticmethod
+    @functools.lru_cache(maxsize=1 << 14)
     def bound_names(base_metric: str) -> tuple[str, str, str]:
         b = "foremastbrain:" + sanitize(base_metric)
         return b + "_upper", b + "_lower", b + "_anomaly"
