@@ -137,6 +137,7 @@ class FastPath(PlanMixin, FetchMixin, ArraysMixin, ModelsMixin, FinishMixin):
         self._glays: dict = {}     # plan group -> (job list, cycle it was laid out)
         self._gghost: dict = {}    # plan group -> (job list, ghost mask) of this cycle
         self._lay_fast = None      # (the laid-out claim list, its non-sliding jobs)
+        self._lay_todo = None      # (the laid-out due list, its non-sliding jobs)
         from .ingest import WindowTable
         cfg = brain.cfg
         self.wt = WindowTable(cfg.metric_settle_s, cfg.fetch_batch, cfg.fetch_max_values)

@@ -29,7 +29,7 @@ class ArraysMixin:
             return g
         g: dict[tuple, list[FastWork]] = {}
         laid = self._glays
-        for L, _ in laid.values():
+        for L, *_ in laid.values():
             # a multi-group fleet's sliding group is its laid-out list itself
             # (ghosts included and masked by ghost_mask): one width class per
             # group, as the one-group path above

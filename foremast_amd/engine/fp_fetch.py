@@ -37,6 +37,11 @@ class FetchMixin:
                 slide[g0] = todo
             else:
                 rest = todo
+        elif self._glays and self._lay_todo is not None and todo is self._lay_todo[0]:
+            # a multi-group fleet's sliding groups: their laid-out lists whole
+            # (the list objects the memos and the JobIds cache know)
+            slide = {g: L for g, (L, *_) in self._glays.items()}
+            rest = list(self._lay_todo[1])
         else:
             for fw in todo:
                 (slide.setdefault(fw.plan.group, []) if fw.plan.sliding else rest).append(fw)

@@ -145,6 +145,8 @@ class PlanMixin:
             self._reused = True
             if keep_jid is not None and keep_jid[0] is fast:     # same list object: same ids
                 self._jid_cache[id(fast)] = keep_jid
+            for L_, _, lj_, _ in self._glays.values():         # (multi-group layouts: unchanged)
+                self._jid_cache[id(L_)] = (L_, lj_)
             if self.ghost is not None:
                 self.ghost_cycles += 1
             return fast, []
@@ -434,7 +436,7 @@ class PlanMixin:
         self._lay = None if works is None else (works, self.cycle)
         self.ghost, self.ghost_ids = None, set()
         self._glays, self._gghost = {}, {}
-        self._lay_fast = None
+        self._lay_fast = self._lay_todo = None
         if works is not None:
             self._left = []             # released jobs of the previous layout: not in this one
             self._sigs = {}
@@ -510,24 +512,40 @@ class PlanMixin:
         for g, cur in sl.items():
             prev = glays_prev.get(g)
             L, laid, ghost = cur, self.cycle, None
+            lj = lid = None
+            # (matching by object identity: id() reads no FastWork, and every
+            # object of cur and L0 is alive here, so the ids are unique)
+            ic = np.fromiter(map(id, cur), np.int64, len(cur))
             if prev is not None and self.cycle - prev[1] < self.LAYOUT_COMPACT_EVERY:
-                L0 = prev[0]
-                m = self._jid(cur).match_in(self._jid(L0))
-                if m is not None:
-                    cand, hit, _ = m
-                    new = [cur[j] for j in np.flatnonzero(~hit).tolist()]
-                    L2 = L0 + new if new else L0
-                    live = np.zeros(len(L2), bool)
-                    live[cand[hit]] = True
-                    live[len(L0):] = True
-                    gm = ~live
-                    gj = np.flatnonzero(gm)
-                    clash = bool(new) and len(gj) and len(np.intersect1d(
-                        np.concatenate([L2[j].rows for j in gj.tolist()]), np.concatenate([fw.rows for fw in new])))
-                    if not clash and len(gj) <= self.LAYOUT_GHOST_FRAC * len(L2):
-                        L, laid, ghost = L2, prev[1], (gm if len(gj) else None)
-                        self.arrivals_laid += len(new)
-            lays[g] = (L, laid)
+                L0, _, lj0, li0 = prev
+                o = np.argsort(li0, kind="stable")
+                p_ = np.minimum(np.searchsorted(li0[o], ic), len(li0) - 1)
+                cand = o[p_]
+                hit = li0[cand] == ic
+                nj = np.flatnonzero(~hit)
+                new = [cur[j] for j in nj.tolist()]
+                L2 = L0 + new if new else L0
+                lj = lj0 if not new else JobIds.of_arr(np.concatenate(
+                    [lj0.arr, np.fromiter(map(_serial_of, new), np.int64, len(new))]))
+                lid = li0 if not new else np.concatenate([li0, ic[nj]])
+                live = np.zeros(len(L2), bool)
+                live[cand[hit]] = True
+                live[len(L0):] = True
+                gm = ~live
+                gj = np.flatnonzero(gm)
+                clash = bool(new) and len(gj) and len(np.intersect1d(
+                    np.concatenate([L2[j].rows for j in gj.tolist()]), np.concatenate([fw.rows for fw in new])))
+                if not clash and len(gj) <= self.LAYOUT_GHOST_FRAC * len(L2):
+                    L, laid, ghost = L2, prev[1], (gm if len(gj) else None)
+                    self.arrivals_laid += len(new)
+                else:
+                    lj = lid = None
+            if lj is None:                         # laid out afresh
+                lj, lid = self._jid(L), ic
+            # the layout's JobIds carry over across cycles (extended by the
+            # arrivals' serials), so no memo check walks the list again
+            self._jid_cache[id(L)] = (L, lj)
+            lays[g] = (L, laid, lj, lid)
             if ghost is not None:
                 gghost[g] = (L, ghost)
                 gids.update(id(L[j]) for j in np.flatnonzero(ghost).tolist())
@@ -535,10 +553,12 @@ class PlanMixin:
         self._glays, self._gghost, self.ghost_ids = lays, gghost, gids
         if self._left:
             self._left = [w for w in self._left if id(w) in gids]     # revival candidates: this cycle's ghosts
-        laid_out = [fw for L, _ in lays.values() for fw in L]
+        laid_out = [fw for L, *_ in lays.values() for fw in L]
         fast2 = other_f + laid_out
+        todo2 = other_t + laid_out
         self._lay_fast = (fast2, other_f)          # (groups() buckets only the non-sliding part)
-        return fast2, other_t + laid_out
+        self._lay_todo = (todo2, other_t)          # (fetch_all takes the layouts whole)
+        return fast2, todo2
 
     def live(self, works: list) -> list:
         """``works`` without this cycle's ghosts."""

@@ -363,6 +363,13 @@ class JobIds:
         self._ixc = None          # (old, positions): the group memos all ask about the same old list
         self._mc = None           # (old, (positions, found, n found))
 
+    @classmethod
+    def of_arr(cls, arr: np.ndarray) -> "JobIds":
+        """The JobIds of a list whose serials are already known."""
+        j = cls.__new__(cls)
+        j.arr, j._order, j._ixc, j._mc = arr, None, None, None
+        return j
+
     def __len__(self) -> int:
         return len(self.arr)
 
