@@ -1089,6 +1089,63 @@ __device__ unsigned long long g_front_t[2 * 8192];
 #define FM_FRONT_ARGS hist, ld_h, T, R, hs, cur, ld_c, n_cur, base, ld_b, n_base, suff, nP, min_mw, min_wil, \
       min_kru, pvals, pstats, queue, rowmap
 
+// Control block of the front kernel's history queue (uint32 words from
+// queue[kXcdCtl]; the queue is 8 x 32 counters + this block, zeroed by the
+// host, kCtlOn set to 1 to enable the balancing): the rows the split was made
+// for, the ranges done this tick, the 9 range bounds, and per-XCD start / end
+// times (u64, 100 MHz) of this tick.
+constexpr int kXcdCtl = 256, kCtlR = 0, kCtlDone = 1, kCtlB = 2, kCtlOn = 31, kCtlT0 = 32, kCtlT1 = 48;
+constexpr int64_t kXcdMinRows = 32768;
+
+// The last workgroup of XCD range ``xcd``: its end time; the last range of
+// the tick to finish computes the next tick's bounds.
+__device__ __attribute__((noinline)) void xcd_rebalance(unsigned* ctl, int xcd, int64_t R, int64_t lo, int64_t hi) {
+  unsigned long long* t0 = reinterpret_cast<unsigned long long*>(ctl + kCtlT0);
+  unsigned long long* t1 = reinterpret_cast<unsigned long long*>(ctl + kCtlT1);
+  __hip_atomic_store(t1 + xcd, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned g = __hip_atomic_fetch_add(ctl + kCtlDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (g != 7u) return;
+  __hip_atomic_store(ctl + kCtlDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (R < 64 || R > 0x7fffffff) return;
+  const bool had = __hip_atomic_load(ctl + kCtlR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)R;
+  double b[9], rate[8], tot = 0.0;
+  for (int x = 0; x <= 8; ++x)
+    b[x] = had ? (double)__hip_atomic_load(ctl + kCtlB + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+               : (double)(R * x / 8);
+  for (int x = 0; x < 8; ++x) {
+    const unsigned long long a = __hip_atomic_load(t0 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long e = __hip_atomic_load(t1 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double rows = b[x + 1] - b[x];
+    if (!(e > a) || e - a > 100000000ull || rows < 1.0) return;   // (a range with no start this tick: keep the split)
+    rate[x] = rows / (double)(e - a);
+    tot += rate[x];
+  }
+  // a third of the way towards the split that would have ended every range
+  // together, and only when the ranges ended more than 1.5 % apart (per-tick
+  // noise is not steered by)
+  double dmin = 1e300, dmax = 0.0;
+  for (int x = 0; x < 8; ++x) {
+    const double d = (b[x + 1] - b[x]) / rate[x];
+    dmin = d < dmin ? d : dmin;
+    dmax = d > dmax ? d : dmax;
+  }
+  if (had && dmax < 1.015 * dmin) return;
+  double acc = 0.0;
+  unsigned nb[9];
+  nb[0] = 0;
+  for (int x = 0; x < 8; ++x) {
+    acc += rate[x] / tot;
+    const double tgt = x == 7 ? (double)R : acc * (double)R;
+    double v = (2.0 * b[x + 1] + tgt) / 3.0;
+    const double minv = (double)nb[x] + 1.0;           // every range keeps a row
+    const double maxv = (double)R - (double)(7 - x);
+    v = v < minv ? minv : (v > maxv ? maxv : v);
+    nb[x + 1] = x == 7 ? (unsigned)R : (unsigned)(v + 0.5);
+  }
+  for (int x = 0; x <= 8; ++x) __hip_atomic_store(ctl + kCtlB + x, nb[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(ctl + kCtlR, (unsigned)R, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NV, int K, bool PRIO>
 __device__ __forceinline__ void tick_front_body(FM_FRONT_PARAMS) {
   __shared__ double red[4];
@@ -1160,9 +1217,30 @@ __device__ __forceinline__ void tick_front_body(FM_FRONT_PARAMS) {
   const int hb = (int)blockIdx.x - nP;
   const int xcd = hb & 7;
   const int nwg = (nH >> 3) + ((nH & 7) > xcd ? 1 : 0);   // workgroups sharing this range
-  const int64_t lo = R * xcd / 8, hi = R * (xcd + 1) / 8;
+  // XCD-balanced ranges: the XCDs do not stream equally fast (per-XCD end
+  // times of the history role, tools/front_timing.py: XCDs 3-5 end 30-40 us
+  // after XCDs 0-2 at 80k rows, the same XCDs tick after tick), so the range
+  // split adapts -- the last range to finish re-divides the rows in
+  // proportion to each XCD's measured rows per microsecond for the next tick
+  // (half-way steps).  queue[256..320): control block (kXcdCtl).
+  unsigned* ctl = queue + kXcdCtl;
+  int64_t lo = R * xcd / 8, hi = R * (xcd + 1) / 8;
+  auto ld = [](const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  // (agent-scope loads: written by another XCD last tick).  Small fleets keep
+  // the even split: at the 1,250-service shard (10k rows) the per-tick
+  // durations are too short and noisy to steer by (0.078 -> 0.081 ms measured)
+  const bool bal = R >= kXcdMinRows && ld(ctl + kCtlOn) == 1u;
+  if (bal && ld(ctl + kCtlR) == (unsigned)R) {
+    lo = ld(ctl + kCtlB + xcd);
+    hi = ld(ctl + kCtlB + xcd + 1);
+  }
   unsigned* ctr = queue + xcd * 32;
-  if (threadIdx.x == 0) s_next = atomicAdd(ctr, (unsigned)kHistChunk);
+  if (threadIdx.x == 0) {
+    s_next = atomicAdd(ctr, (unsigned)kHistChunk);
+    if (bal && s_next == 0u)       // the range's first grab: its start time
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(ctl + kCtlT0) + xcd, __builtin_amdgcn_s_memrealtime(),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
   int64_t r0 = lo + (int64_t)s_next;
   while (r0 < hi) {
@@ -1189,6 +1267,7 @@ __device__ __forceinline__ void tick_front_body(FM_FRONT_PARAMS) {
     if (d == (unsigned)nwg - 1) {
       __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (bal) xcd_rebalance(ctl, xcd, R, lo, hi);
     }
   }
   FM_FT_MARK(1);

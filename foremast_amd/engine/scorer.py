@@ -17,6 +17,7 @@ HIP graph (``capture``) and replayed with zero host work per tick.
 from __future__ import annotations
 
 import dataclasses
+import os
 from dataclasses import dataclass
 
 import torch
@@ -89,9 +90,11 @@ class CanaryScorer:
         # one per row (tools/tick_breakdown.py SWEEP_FRONT)
         self.front_wgs = front_wgs or (1.0, 4.0)
         # dynamic history-row queue (8 per-XCD counters, kept zero between
-        # launches by the kernel itself)
-        self._queue = (torch.zeros(8 * 32, dtype=torch.int32, device=self.device)
+        # launches by the kernel itself) + the XCD-balance control block
+        self._queue = (torch.zeros(8 * 32 + 64, dtype=torch.int32, device=self.device)
                        if front_queue and self.device.type == "cuda" else None)
+        if self._queue is not None and os.environ.get("FM_XCD_BALANCE", "1") != "0":
+            self._queue[8 * 32 + 31] = 1      # control block: XCD-balanced history ranges (canary.hip kXcdCtl)
         self._cus = (torch.cuda.get_device_properties(self.device).multi_processor_count
                      if self.device.type == "cuda" else 0)
         rules = [self.cfg.rule_for(a) for a in aliases]

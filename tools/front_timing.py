@@ -49,6 +49,20 @@ def main() -> None:
             t0 = t[:, 0].min()
             t -= t0
             p, hh = t[:nP], t[nP:]
+            # per-XCD end of the history role (workgroups are dealt round-robin
+            # over the 8 XCDs; the history queue splits rows into 8 XCD ranges),
+            # over REPS further launches: is the late XCD always the same one?
+            xe = []
+            for _ in range(int(os.environ.get("REPS", "6"))):
+                front()
+                torch.cuda.synchronize()
+                LIB.call("fm_front_timing_read", ctypes.cast(buf, ctypes.c_void_p), 2 * n)
+                tt = np.frombuffer(buf, dtype=np.uint64).astype(np.float64).reshape(n, 2) / 100.0
+                tt -= tt[:, 0].min()
+                hx = tt[nP:]
+                xid = np.arange(nH) & 7
+                xe.append([round(float(hx[xid == x, 1].max()), 1) for x in range(8)])
+            print(json.dumps({"services": S, "wgs": wgs, "history_end_us_per_xcd": xe}), flush=True)
             print(json.dumps({
                 "services": S, "wgs": wgs, "nP": nP, "nH": nH,
                 "kernel_us": round(float(t[:, 1].max()), 1),
