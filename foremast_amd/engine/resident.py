@@ -103,7 +103,7 @@ class ResidentHistory:
         self.bytes_in = 0
         self.max_len = 0                            # static: longest row written (view length)
         self.dense_rows = 0                         # sliding rows whose history arrived as one grid block
-        self._dense_pin = None                      # (pinned staging buffer, event of its last upload)
+        self._dense_pin = None                      # [2 x (pinned staging buffer, event of its last upload), next]
 
     # ------------------------------------------------------------------ rows
     def __len__(self) -> int:
@@ -364,10 +364,19 @@ class ResidentHistory:
             # left it before it is refilled
             o = (V.size + 1) // 2 * 2                # (the int64 rows start 8-byte aligned)
             n = o + len(rows) * 2
-            st = self._dense_pin
+            # two staging buffers used in turn: a cycle's blocks (one per
+            # metric) fill one while the previous one's upload runs
+            pins = self._dense_pin
+            if pins is None:
+                pins = self._dense_pin = [None, None, 0]
+            k = pins[2]
+            pins[2] ^= 1
+            st = pins[k]
             if st is None or st[0].numel() < n:
-                st = self._dense_pin = (torch.empty((int(n * 1.25) + 1024,), dtype=torch.float32).pin_memory(),
-                                        torch.cuda.Event())
+                if st is not None:
+                    st[1].synchronize()
+                st = pins[k] = (torch.empty((int(n * 1.25) + 1024,), dtype=torch.float32).pin_memory(),
+                                torch.cuda.Event())
             else:
                 st[1].synchronize()
             hv = st[0][:V.size].numpy().reshape(V.shape)
