@@ -1129,14 +1129,20 @@ __device__ __attribute__((noinline)) void xcd_rebalance(unsigned* ctl, int xcd, 
     dmin = d < dmin ? d : dmin;
     dmax = d > dmax ? d : dmax;
   }
-  if (had && dmax < 1.015 * dmin) return;
+#ifndef FM_XCD_BAND
+#define FM_XCD_BAND 1.015
+#endif
+#ifndef FM_XCD_STEP
+#define FM_XCD_STEP 3.0
+#endif
+  if (had && dmax < FM_XCD_BAND * dmin) return;
   double acc = 0.0;
   unsigned nb[9];
   nb[0] = 0;
   for (int x = 0; x < 8; ++x) {
     acc += rate[x] / tot;
     const double tgt = x == 7 ? (double)R : acc * (double)R;
-    double v = (2.0 * b[x + 1] + tgt) / 3.0;
+    double v = ((FM_XCD_STEP - 1.0) * b[x + 1] + tgt) / FM_XCD_STEP;   // (1 / FM_XCD_STEP of the way)
     const double minv = (double)nb[x] + 1.0;           // every range keeps a row
     const double maxv = (double)R - (double)(7 - x);
     v = v < minv ? minv : (v > maxv ? maxv : v);
