@@ -1325,7 +1325,9 @@ static bool front_prio() {
 }
 
 // nP / nH: workgroups of each role (0 = one pairwise workgroup per 4 rows /
-// one history workgroup per row); queue: dynamic history rows (or nullptr).
+// one history workgroup per row); queue: dynamic history rows (or nullptr):
+// 8 x 32 + 64 zero-initialised uint32 -- the per-XCD counters and the
+// XCD-balance control block (kXcdCtl; word kXcdCtl + kCtlOn = 1 enables it).
 FM_API int fm_tick_front_rm(const float* hist, int64_t ld_h, int T, int64_t R, float* hs, const float* cur,
                             int64_t ld_c, int n_cur, const float* base, int64_t ld_b, int n_base, double* suff, int nP,
                             int nH, int min_mw, int min_wil, int min_kru, float* pvals, float* pstats,
@@ -1337,8 +1339,9 @@ FM_API int fm_tick_front_rm(const float* hist, int64_t ld_h, int T, int64_t R, f
   const int64_t pmax = (R + 3) / 4;
   if (nP <= 0 || nP > pmax) nP = (int)pmax;
   if (nH <= 0 || nH > R) nH = (int)R;
-  // queue: 8 x 32 zero-initialised uints (kept zero between launches by the
-  // kernel itself); needs at least one history workgroup per XCD range
+  // queue: 8 x 32 + 64 zero-initialised uints (the counters are kept zero
+  // between launches by the kernel itself); needs at least one history
+  // workgroup per XCD range
   if (queue != nullptr && nH < 8) nH = 8;
   const int nq = (T + 3) / 4;
   const dim3 grid((unsigned)(nP + nH)), block(256);
