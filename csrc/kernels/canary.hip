@@ -1091,11 +1091,15 @@ __device__ unsigned long long g_front_t[2 * 8192];
 
 // Control block of the front kernel's history queue (uint32 words from
 // queue[kXcdCtl]; the queue is 8 x 32 counters + this block, zeroed by the
-// host, kCtlOn set to 1 to enable the balancing): the rows the split was made
-// for, the ranges done this tick, the 9 range bounds, and per-XCD start / end
+// host, kCtlOn set to 1 to enable the balancing): a split-is-set flag, the
+// ranges done this tick, the 9 range bounds as fractions of the rows (2^-24
+// fixed point, so a split survives the row count changing with fleet churn:
+// range x is rows [R f[x] >> 24, R f[x+1] >> 24)), and per-XCD start / end
 // times (u64, 100 MHz) of this tick.
 constexpr int kXcdCtl = 256, kCtlR = 0, kCtlDone = 1, kCtlB = 2, kCtlOn = 31, kCtlT0 = 32, kCtlT1 = 48;
 constexpr int64_t kXcdMinRows = 32768;
+constexpr int kFracBits = 24;
+__device__ inline int64_t xcd_bound(int64_t R, unsigned f) { return (R * (int64_t)f) >> kFracBits; }
 
 // The last workgroup of XCD range ``xcd``: its end time; the last range of
 // the tick to finish computes the next tick's bounds.
@@ -1107,11 +1111,14 @@ __device__ __attribute__((noinline)) void xcd_rebalance(unsigned* ctl, int xcd, 
   if (g != 7u) return;
   __hip_atomic_store(ctl + kCtlDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (R < 64 || R > 0x7fffffff) return;
-  const bool had = __hip_atomic_load(ctl + kCtlR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)R;
-  double b[9], rate[8], tot = 0.0;
-  for (int x = 0; x <= 8; ++x)
-    b[x] = had ? (double)__hip_atomic_load(ctl + kCtlB + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-               : (double)(R * x / 8);
+  const bool had = __hip_atomic_load(ctl + kCtlR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  constexpr double one = (double)(1u << kFracBits);
+  double b[9], f[9], rate[8], tot = 0.0;
+  for (int x = 0; x <= 8; ++x) {   // this tick's bounds, exactly as the history role derived them
+    const unsigned fx = __hip_atomic_load(ctl + kCtlB + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b[x] = had ? (double)xcd_bound(R, fx) : (double)(R * x / 8);
+    f[x] = had ? (double)fx / one : (double)x / 8.0;
+  }
   for (int x = 0; x < 8; ++x) {
     const unsigned long long a = __hip_atomic_load(t0 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long e = __hip_atomic_load(t1 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1136,20 +1143,22 @@ __device__ __attribute__((noinline)) void xcd_rebalance(unsigned* ctl, int xcd, 
 #define FM_XCD_STEP 3.0
 #endif
   if (had && dmax < FM_XCD_BAND * dmin) return;
-  double acc = 0.0;
-  unsigned nb[9];
-  nb[0] = 0;
+  // in fraction space; every range keeps at least 1/64 of the rows (an XCD a
+  // quarter of the mean speed), so no range empties and stops being timed
+  constexpr double minf = 1.0 / 64.0;
+  double acc = 0.0, prev = 0.0;
+  unsigned nf[9];
+  nf[0] = 0;
   for (int x = 0; x < 8; ++x) {
     acc += rate[x] / tot;
-    const double tgt = x == 7 ? (double)R : acc * (double)R;
-    double v = ((FM_XCD_STEP - 1.0) * b[x + 1] + tgt) / FM_XCD_STEP;   // (1 / FM_XCD_STEP of the way)
-    const double minv = (double)nb[x] + 1.0;           // every range keeps a row
-    const double maxv = (double)R - (double)(7 - x);
+    double v = ((FM_XCD_STEP - 1.0) * f[x + 1] + acc) / FM_XCD_STEP;   // (1 / FM_XCD_STEP of the way)
+    const double minv = prev + minf, maxv = 1.0 - (double)(7 - x) * minf;
     v = v < minv ? minv : (v > maxv ? maxv : v);
-    nb[x + 1] = x == 7 ? (unsigned)R : (unsigned)(v + 0.5);
+    nf[x + 1] = x == 7 ? (1u << kFracBits) : (unsigned)(v * one + 0.5);
+    prev = (double)nf[x + 1] / one;
   }
-  for (int x = 0; x <= 8; ++x) __hip_atomic_store(ctl + kCtlB + x, nb[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(ctl + kCtlR, (unsigned)R, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  for (int x = 0; x <= 8; ++x) __hip_atomic_store(ctl + kCtlB + x, nf[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(ctl + kCtlR, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int NV, int K, bool PRIO>
@@ -1228,7 +1237,8 @@ __device__ __forceinline__ void tick_front_body(FM_FRONT_PARAMS) {
   // after XCDs 0-2 at 80k rows, the same XCDs tick after tick), so the range
   // split adapts -- the last range to finish re-divides the rows in
   // proportion to each XCD's measured rows per microsecond for the next tick
-  // (half-way steps).  queue[256..320): control block (kXcdCtl).
+  // (1/3 steps, as fractions of the rows, so the split carries over when the
+  // fleet's row count changes).  queue[256..320): control block (kXcdCtl).
   unsigned* ctl = queue + kXcdCtl;
   int64_t lo = R * xcd / 8, hi = R * (xcd + 1) / 8;
   auto ld = [](const unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -1236,9 +1246,9 @@ __device__ __forceinline__ void tick_front_body(FM_FRONT_PARAMS) {
   // the even split: at the 1,250-service shard (10k rows) the per-tick
   // durations are too short and noisy to steer by (0.078 -> 0.081 ms measured)
   const bool bal = R >= kXcdMinRows && ld(ctl + kCtlOn) == 1u;
-  if (bal && ld(ctl + kCtlR) == (unsigned)R) {
-    lo = ld(ctl + kCtlB + xcd);
-    hi = ld(ctl + kCtlB + xcd + 1);
+  if (bal && ld(ctl + kCtlR) != 0u) {
+    lo = xcd_bound(R, ld(ctl + kCtlB + xcd));
+    hi = xcd_bound(R, ld(ctl + kCtlB + xcd + 1));
   }
   unsigned* ctr = queue + xcd * 32;
   if (threadIdx.x == 0) {
