@@ -4,6 +4,7 @@ arrivals) and the moving_average_all scoring tick."""
 from __future__ import annotations
 
 import functools
+import os
 
 import numpy as np
 import torch
@@ -50,7 +51,14 @@ class ArraysMixin:
     def _scorer(self, aliases: tuple) -> CanaryScorer:
         sc = self.scorers.get(aliases)
         if sc is None:
-            sc = self.scorers[aliases] = CanaryScorer(list(aliases), self.b.cfg, device=self.b.device)
+            # XCD-balanced history ranges off in the brain: one scorer serves
+            # every group of an alias set, so a split learned on one group's
+            # launch steers the next group's, and churn moves the row count;
+            # canary e2e with 0.5 % arrivals measured 29.8-31.3 ms/cycle with it
+            # vs 26.3-28.3 without (profiles/front_xcd_fraction_ab_r6.jsonl)
+            sc = self.scorers[aliases] = CanaryScorer(
+                list(aliases), self.b.cfg, device=self.b.device,
+                xcd_balance=os.environ.get("FM_BRAIN_XCD_BALANCE", "0") == "1")
         if len(sc._out) > 8:
             sc._out.clear()
         return sc

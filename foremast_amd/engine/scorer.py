@@ -59,7 +59,8 @@ class CanaryScorer:
 
     def __init__(self, aliases: list[str], cfg: BrainConfig | None = None, device="cpu", overlap: bool = True,
                  mode: str | None = None, hist_blocks: int = 0, pw_blocks: int = 0, pw_cap_rows: int = 32,
-                 front_wgs: tuple[float, float] | None = None, front_queue: bool = True):
+                 front_wgs: tuple[float, float] | None = None, front_queue: bool = True,
+                 xcd_balance: bool | None = None):
         self.mode = mode or ("front" if overlap else "serial")
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
@@ -93,7 +94,11 @@ class CanaryScorer:
         # launches by the kernel itself) + the XCD-balance control block
         self._queue = (torch.zeros(8 * 32 + 64, dtype=torch.int32, device=self.device)
                        if front_queue and self.device.type == "cuda" else None)
-        if self._queue is not None and os.environ.get("FM_XCD_BALANCE", "1") != "0":
+        # (None = env FM_XCD_BALANCE, default on: one fleet per scorer, every
+        # tick the same rows -- bench.py, 0.542 vs 0.554 ms)
+        if xcd_balance is None:
+            xcd_balance = os.environ.get("FM_XCD_BALANCE", "1") != "0"
+        if self._queue is not None and xcd_balance:
             self._queue[8 * 32 + 31] = 1      # control block: XCD-balanced history ranges (canary.hip kXcdCtl)
         self._cus = (torch.cuda.get_device_properties(self.device).multi_processor_count
                      if self.device.type == "cuda" else 0)
