@@ -355,6 +355,29 @@ def test_gpu_front_tick_generic_shapes(cuda, M, P, T):
 
 
 @pytest.mark.gpu
+def test_gpu_front_xcd_balanced_ranges_equal_serial(cuda):
+    """32,768 rows (the balancing threshold, canary.hip kXcdMinRows): after a
+    few ticks the control block holds a split (monotone 2^-24 fractions ending
+    at 1) and the XCD-balanced history ranges still give serial's results."""
+    from foremast_amd.engine.scorer import CanaryScorer
+    aliases = ["error5xx", "latency", "traffic", "error4xx", "cpu", "memory", "tomcat_threads", "jvm_heap"]
+    T = 600
+    h, b, c = C.synth_fleet(4096, 8, T, 5, 10, 0, device=cuda, fault_rate=0.2)
+    ref = CanaryScorer(aliases, device=cuda, mode="serial").score(h, b, c, T)
+    sc = CanaryScorer(aliases, device=cuda, mode="front", xcd_balance=True)
+    for _ in range(8):
+        o = sc.score(h, b, c, T)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(o.packed, ref.packed)
+        torch.testing.assert_close(o.decide.count, ref.decide.count)
+    ctl = sc._queue[256:].cpu().numpy().view(np.uint32)
+    assert ctl[0] == 1 and ctl[31] == 1
+    f = ctl[2:11].astype(np.int64)
+    assert f[0] == 0 and f[8] == 1 << 24 and (np.diff(f) > 0).all()
+    assert not sc._queue[:256].any()          # the per-XCD counters are back to zero
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("S,M", [(1250, 8), (77, 4)])
 def test_gpu_split_tick_equals_score(cuda, S, M):
     """front_only (graph, per-slot buffers) + decide_only on another stream ==
